@@ -1,0 +1,367 @@
+"""ORACLE — test infrastructure only.  CPU fp32 restatement of the C2DSR training
+step of the reference (crystal22/C2DSR); never imported by the product path
+(``c2dsr_amd``).  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may use it, and only as the checker / the CPU baseline.
+
+Pinned against golden vectors produced by the reference itself
+(``tools/gen_fixtures.py`` → ``tests/golden/model_*.npz``; see
+``tests/test_oracle_golden.py``).  Written functionally over a flat parameter
+dict keyed by the reference's ``state_dict`` names; gradients come from torch
+autograd on CPU (plain fp32 reference, as for any floating-point kernel).
+
+Reference semantics restated (file:line in /root/reference):
+  * GCN                 models/encoders.py:36-48  (mean of [E, A·drop(E), ...], E undropped, Q12)
+  * convolve_graph      models/C2DSR.py:59-62
+  * embedding fuse      models/C2DSR.py:64-85     ((H[seq] + E[seq])·√d; F.embedding has no padding_idx, Q4)
+  * SelfAttention       models/encoders.py:7-33   (+pos_emb, dropout, TransformerEncoder, final LN eps 1e-8)
+      nn.TransformerEncoderLayer math path (n_head=1 ⇒ no fast path), causal mask +
+      INVERTED key-padding mask (seq != pad masks real tokens, Q1); a fully masked row → 0 (Q2)
+  * cal_mask / pooling  trainer.py:85-108         (cross-masked h_share pooling, Q5)
+  * bilinear + BCE      trainer.py:104-119, C2DSR.py:46-55
+  * heads + CE          trainer.py:121-154        (pad column = ignore_index, Q6; count weighting Q7; Q8)
+  * loss / AdamW        trainer.py:156-158, :21-22 (amsgrad, decoupled wd; grads accumulate, Q3)
+
+Dropout: the reference draws torch-CPU masks that no GPU RNG can reproduce, so
+parity against the reference uses p = 0.  For p > 0 the GPU kernels use a
+counter-based hash mask; :func:`keep_mask` restates that hash so the oracle
+and the HIP path drop exactly the same elements.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+MASK64 = (1 << 64) - 1
+
+
+# ----------------------------------------------------------------------------- dropout hash
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & MASK64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & MASK64
+    return x ^ (x >> 31)
+
+
+def dropout_keys(seed: int, step: int, site: int) -> tuple[int, int]:
+    x = _splitmix64((seed & MASK64) ^ _splitmix64((step * 0x100000001B3 + site) & MASK64))
+    return x & 0xFFFFFFFF, x >> 32
+
+
+def _lowbias32(h: np.ndarray) -> np.ndarray:
+    h = h.astype(np.uint32)
+    h ^= h >> np.uint32(16)
+    h *= np.uint32(0x7FEB352D)
+    h ^= h >> np.uint32(15)
+    h *= np.uint32(0x846CA68B)
+    h ^= h >> np.uint32(16)
+    return h
+
+
+def keep_mask(idx: np.ndarray, keys: tuple[int, int], p: float) -> np.ndarray:
+    """Bernoulli(1-p) keep decision for flat element indices ``idx`` (int64)."""
+    if p <= 0.0:
+        return np.ones(idx.shape, dtype=bool)
+    idx = idx.astype(np.uint64)
+    with np.errstate(over='ignore'):
+        h = _lowbias32((idx & np.uint64(0xFFFFFFFF)).astype(np.uint32) ^ np.uint32(keys[0]))
+        h = _lowbias32(h ^ (idx >> np.uint64(32)).astype(np.uint32) ^ np.uint32(keys[1]))
+    thr = min(0xFFFFFFFF, int(math.floor(p * 4294967296.0)))
+    return h >= np.uint32(thr)
+
+
+# site ids (must match c2dsr_amd/dropout.py)
+def site_gcn(table: int, layer: int) -> int:
+    return 0x100 + table * 16 + layer
+
+
+def site_enc(pass_id: int, layer: int, kind: int) -> int:
+    # kind: 0 input, 1 attn probs, 2 sa out, 3 ff mid, 4 ff out
+    return 0x1000 + pass_id * 256 + (0 if kind == 0 else 1 + layer * 8 + (kind - 1))
+
+
+class Dropper:
+    """Produces fp32 multiplicative dropout masks for a given (seed, step)."""
+
+    def __init__(self, p_gnn: float, p_attn: float, seed: int = 0, step: int = 0, row_offset: int = 0):
+        self.p_gnn, self.p_attn, self.seed, self.step = p_gnn, p_attn, seed, step
+        self.row_offset = row_offset  # global batch-row offset (data parallel)
+
+    def mask(self, shape, site: int, p: float, row_dim_prod: int | None = None) -> torch.Tensor | None:
+        if p <= 0.0:
+            return None
+        n = int(np.prod(shape))
+        base = 0
+        if row_dim_prod is not None:
+            base = self.row_offset * row_dim_prod
+        idx = np.arange(n, dtype=np.int64) + base
+        keep = keep_mask(idx, dropout_keys(self.seed, self.step, site), p)
+        return torch.from_numpy(keep.reshape(shape).astype(np.float32) / np.float32(1.0 - p))
+
+
+# ----------------------------------------------------------------------------- model pieces
+def spmm_coo(row: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n: int, h: torch.Tensor) -> torch.Tensor:
+    out = torch.zeros(n, h.shape[1], dtype=h.dtype)
+    return out.index_add(0, row, val[:, None] * h[col])
+
+
+def gcn(E, graph, n_gnn, p, dropper: Dropper, table: int):
+    """models/encoders.py:42-48."""
+    row, col, val = graph
+    hs = [E]
+    h = E
+    for k in range(n_gnn):
+        m = dropper.mask(tuple(h.shape), site_gcn(table, k), p)
+        if m is not None:
+            h = h * m
+        h = spmm_coo(row, col, val, E.shape[0], h)
+        hs.append(h)
+    return torch.stack(hs, 1).mean(1)
+
+
+def layer_norm(x, w, b, eps=1e-8):
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    return (x - mu) / torch.sqrt(var + eps) * w + b
+
+
+def attention(x, P, pre, seq, idx_pad, n_head, p, dropper, pass_id, layer):
+    """nn.MultiheadAttention → F.multi_head_attention_forward → SDPA (math), with the
+    causal float mask + inverted bool kpm merged additively (functional.py mask merge)."""
+    B, L, d = x.shape
+    dh = d // n_head
+    qkv = x @ P[pre + 'self_attn.in_proj_weight'].T + P[pre + 'self_attn.in_proj_bias']
+    q, k, v = qkv.split(d, dim=-1)
+    q = q.reshape(B, L, n_head, dh).transpose(1, 2)
+    k = k.reshape(B, L, n_head, dh).transpose(1, 2)
+    v = v.reshape(B, L, n_head, dh).transpose(1, 2)
+    causal = torch.triu(torch.ones(L, L, dtype=torch.bool), 1)
+    kpm = seq != idx_pad  # True ⇒ masked (inverted, Q1)
+    masked = causal[None, None] | kpm[:, None, None, :]
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    s = s.masked_fill(masked, float('-inf'))
+    row_ok = (~masked).any(-1, keepdim=True)
+    s = torch.where(row_ok, s, torch.zeros_like(s))
+    a = torch.softmax(s, -1) * row_ok  # fully masked rows → 0 (Q2)
+    m = dropper.mask((B, n_head, L, L), site_enc(pass_id, layer, 1), p, row_dim_prod=n_head * L * L)
+    if m is not None:
+        a = a * m
+    o = (a @ v).transpose(1, 2).reshape(B, L, d)
+    out = o @ P[pre + 'self_attn.out_proj.weight'].T + P[pre + 'self_attn.out_proj.bias']
+    m = dropper.mask((B, L, d), site_enc(pass_id, layer, 2), p, row_dim_prod=L * d)
+    return out * m if m is not None else out
+
+
+def feed_forward(x, P, pre, p, dropper, pass_id, layer):
+    B, L, d = x.shape
+    f = torch.relu(x @ P[pre + 'linear1.weight'].T + P[pre + 'linear1.bias'])
+    m = dropper.mask(tuple(f.shape), site_enc(pass_id, layer, 3), p, row_dim_prod=L * f.shape[-1])
+    if m is not None:
+        f = f * m
+    out = f @ P[pre + 'linear2.weight'].T + P[pre + 'linear2.bias']
+    m = dropper.mask((B, L, d), site_enc(pass_id, layer, 4), p, row_dim_prod=L * d)
+    return out * m if m is not None else out
+
+
+def self_attention(P, mod, seq, x, pos, cfg, dropper, pass_id):
+    """models/encoders.py:29-33 (+ TransformerEncoder / TransformerEncoderLayer)."""
+    B, L, d = x.shape
+    p = cfg['dropout_attn']
+    x = x + P[mod + '.pos_emb.weight'][pos]
+    m = dropper.mask((B, L, d), site_enc(pass_id, 0, 0), p, row_dim_prod=L * d)
+    if m is not None:
+        x = x * m
+    for l in range(cfg['n_attn']):
+        pre = f'{mod}.encoder.layers.{l}.'
+        if cfg['norm_first']:
+            x = x + attention(layer_norm(x, P[pre + 'norm1.weight'], P[pre + 'norm1.bias']), P, pre, seq,
+                              cfg['idx_pad'], cfg['n_head'], p, dropper, pass_id, l)
+            x = x + feed_forward(layer_norm(x, P[pre + 'norm2.weight'], P[pre + 'norm2.bias']), P, pre, p,
+                                 dropper, pass_id, l)
+        else:
+            x = layer_norm(x + attention(x, P, pre, seq, cfg['idx_pad'], cfg['n_head'], p, dropper, pass_id, l),
+                           P[pre + 'norm1.weight'], P[pre + 'norm1.bias'])
+            x = layer_norm(x + feed_forward(x, P, pre, p, dropper, pass_id, l),
+                           P[pre + 'norm2.weight'], P[pre + 'norm2.bias'])
+    return layer_norm(x, P[mod + '.encoder.norm.weight'], P[mod + '.encoder.norm.bias'])
+
+
+def embed_names(cfg):
+    if cfg['shared_item_embed']:
+        return 'embed_i.weight', 'embed_i.weight', 'embed_i.weight'
+    return 'embed_i.weight', 'embed_i_a.weight', 'embed_i_b.weight'
+
+
+def convolve_graph(P, graphs, cfg, dropper):
+    """models/C2DSR.py:59-62."""
+    es, ea, eb = embed_names(cfg)
+    p = cfg['dropout_gnn']
+    hs = gcn(P[es], graphs['share'], cfg['n_gnn'], p, dropper, 0)
+    ha = gcn(P[ea], graphs['specific'], cfg['n_gnn'], p, dropper, 1)
+    hb = gcn(P[eb], graphs['specific'], cfg['n_gnn'], p, dropper, 2)
+    return hs, ha, hb
+
+
+def encode(P, H, ename, mod, seq, pos, cfg, dropper, pass_id):
+    scale = cfg['d_latent'] ** 0.5
+    E = P[ename]
+    # nn.Embedding(padding_idx=pad): the pad row is read but gets no gradient from the lookup
+    e = torch.where((seq == cfg['idx_pad'])[..., None], E[seq].detach(), E[seq])
+    x = (H[seq] + e) * scale
+    return self_attention(P, mod, seq, x, pos, cfg, dropper, pass_id)
+
+
+def bilinear(x1, x2, W, b):
+    out = torch.einsum('bi,oij,bj->bo', x1, W, x2)
+    return out + b if b is not None else out
+
+
+def bce_logits(s, y):
+    return (torch.clamp(s, min=0) - s * y + torch.log1p(torch.exp(-s.abs()))).mean()
+
+
+def cross_entropy(logits, tgt, ignore):
+    valid = tgt != ignore
+    lse = torch.logsumexp(logits, -1)
+    t = torch.where(valid, tgt, torch.zeros_like(tgt))
+    picked = logits.gather(1, t[:, None])[:, 0]
+    return ((lse - picked) * valid).sum() / valid.sum()
+
+
+def train_forward(P, graphs, batch, cfg, dropper):
+    """trainer.py:91-156 (+ C2DSR.forward / forward_share).  Returns dict of tensors."""
+    (seq, seq_a, seq_b, pos, pos_a, pos_b, gt_sa, gt_sb, gt_a, gt_b, gm_a, gm_b, neg_a, neg_b) = batch
+    es, ea, eb = embed_names(cfg)
+    n_a, n_b, R = cfg['n_item_a'], cfg['n_item_b'], cfg['len_rec']
+    B = seq.shape[0]
+    out = {}
+    hs_t, ha_t, hb_t = convolve_graph(P, graphs, cfg, dropper)
+    out['hi_share'], out['hi_a'], out['hi_b'] = hs_t, ha_t, hb_t
+    h_share = encode(P, hs_t, es, 'attn_share', seq, pos, cfg, dropper, 0)
+    hx = encode(P, ha_t, ea, 'attn_a', seq_a, pos_a, cfg, dropper, 1)
+    hy = encode(P, hb_t, eb, 'attn_b', seq_b, pos_b, cfg, dropper, 2)
+    h_neg_a = encode(P, hs_t, es, 'attn_share', neg_a, pos, cfg, dropper, 3)
+    h_neg_b = encode(P, hs_t, es, 'attn_share', neg_b, pos, cfg, dropper, 4)
+    out.update(h_share=h_share, hx=hx, hy=hy, h_neg_a=h_neg_a, h_neg_b=h_neg_b)
+
+    wa = (gm_a.float() / gm_a.float().sum(-1, keepdim=True))[..., None]
+    wb = (gm_b.float() / gm_b.float().sum(-1, keepdim=True))[..., None]
+    hx_mean = (hx * wa).sum(1)
+    hy_mean = (hy * wb).sum(1)
+    Da_b = P.get('D_a.bias')
+    Db_b = P.get('D_b.bias')
+    sim_a_pos = bilinear(hx_mean, (h_share * wb).sum(1), P['D_a.weight'], Da_b)
+    sim_a_neg = bilinear(hx_mean, (h_neg_a * wa).sum(1), P['D_a.weight'], Da_b)
+    sim_b_pos = bilinear(hy_mean, (h_share * wa).sum(1), P['D_b.weight'], Db_b)
+    sim_b_neg = bilinear(hy_mean, (h_neg_b * wb).sum(1), P['D_b.weight'], Db_b)
+    out['sim_a'] = torch.stack([sim_a_pos, sim_a_neg])
+    out['sim_b'] = torch.stack([sim_b_pos, sim_b_neg])
+    one = torch.ones(B, 1)
+    zero = torch.zeros(B, 1)
+    loss_mi = bce_logits(sim_a_pos, one) + bce_logits(sim_a_neg, zero) + \
+        bce_logits(sim_b_pos, one) + bce_logits(sim_b_neg, zero)
+
+    hs_r, ha_r, hb_r = h_share[:, -R:], hx[:, -R:], hy[:, -R:]
+
+    def head(h, W, bias, hpad):
+        lg = h @ W.T + bias
+        pad = hpad @ P['classifier_pad.weight'].T + P['classifier_pad.bias']
+        return torch.cat([lg, pad], -1)
+
+    Wa, ba, Wb, bb = P['classifier_a.weight'], P['classifier_a.bias'], P['classifier_b.weight'], P['classifier_b.bias']
+    s_sa = head(hs_r, Wa, ba, hs_r).reshape(-1, n_a + 1)
+    s_sb = head(hs_r, Wb, bb, hs_r).reshape(-1, n_b + 1)
+    s_a = head(hs_r + ha_r, Wa, ba, ha_r).reshape(-1, n_a + 1)
+    s_b = head(hs_r + hb_r, Wb, bb, hb_r).reshape(-1, n_b + 1)
+    t_sa, t_sb = gt_sa[:, -R:].reshape(-1), gt_sb[:, -R:].reshape(-1)
+    t_a, t_b = gt_a[:, -R:].reshape(-1), gt_b[:, -R:].reshape(-1)
+    l_sa = cross_entropy(s_sa, t_sa, n_a)
+    l_sb = cross_entropy(s_sb, t_sb, n_b)
+    loss_share = l_sa * (t_sa != n_a).sum() / (R * B) + l_sb * (t_sb != n_b).sum() / (R * B)
+    l_a = cross_entropy(s_a, t_a, n_a)
+    l_b = cross_entropy(s_b, t_b, n_b)
+    loss_rec = loss_share + l_a + l_b
+    lam = cfg['lambda_loss']
+    loss = lam * loss_rec + (1 - lam) * loss_mi
+    out.update(loss=loss, loss_rec=loss_rec, loss_mi=loss_mi, l_sa=l_sa, l_sb=l_sb, l_a=l_a, l_b=l_b)
+    return out
+
+
+# ----------------------------------------------------------------------------- optimizer
+class AdamWAmsgrad:
+    """torch.optim.AdamW(amsgrad=True) single-tensor update (trainer.py:21-22)."""
+
+    def __init__(self, lr=1e-3, wd=5e-4, betas=(0.9, 0.999), eps=1e-8):
+        self.lr, self.wd, self.b1, self.b2, self.eps = lr, wd, betas[0], betas[1], eps
+        self.state = {}
+
+    def step(self, params: dict, grads: dict):
+        for n, g in grads.items():
+            if g is None:
+                continue
+            p = params[n]
+            st = self.state.get(n)
+            if st is None:
+                st = self.state[n] = dict(step=0, m=torch.zeros_like(p), v=torch.zeros_like(p),
+                                          vmax=torch.zeros_like(p))
+            st['step'] += 1
+            t = st['step']
+            p.mul_(1 - self.lr * self.wd)
+            st['m'].lerp_(g, 1 - self.b1)
+            st['v'].mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            bc1 = 1 - self.b1 ** t
+            bc2 = 1 - self.b2 ** t
+            torch.maximum(st['vmax'], st['v'], out=st['vmax'])
+            denom = (st['vmax'].sqrt() / math.sqrt(bc2)).add_(self.eps)
+            p.addcdiv_(st['m'], denom, value=-(self.lr / bc1))
+
+
+def trainable_names(names, cfg):
+    """Parameters that ever receive a grad (the encoder_layer template never does, Q15)."""
+    skip = {'embed_i_a.weight', 'embed_i_b.weight'} if cfg['shared_item_embed'] else set()
+    return [n for n in names if '.encoder_layer.' not in n and (n != 'D_a.bias' or cfg['d_bias'])
+            and (n != 'D_b.bias' or cfg['d_bias']) and n not in skip]
+
+
+class OracleTrainer:
+    """Step driver mirroring Trainer.run_epoch's per-batch body (trainer.py:47-53) with
+    zero_grad once (Q3)."""
+
+    def __init__(self, params: dict, graphs, cfg, seed=0, lr=1e-3, wd=5e-4):
+        self.cfg = cfg
+        self.P = {k: v.clone().float().requires_grad_(False) for k, v in params.items()}
+        self.names = trainable_names(list(self.P.keys()), cfg)
+        self.grads = {n: None for n in self.names}
+        self.graphs = graphs
+        self.opt = AdamWAmsgrad(lr=lr, wd=wd)
+        self.seed = seed
+        self.step_no = 0
+
+    def zero_grad(self):
+        self.grads = {n: None for n in self.names}
+
+    def train_batch(self, batch, row_offset=0, optimizer=True):
+        for n in self.names:
+            self.P[n].requires_grad_(True)
+        dr = Dropper(self.cfg['dropout_gnn'], self.cfg['dropout_attn'], self.seed, self.step_no, row_offset)
+        out = train_forward(self.P, self.graphs, batch, self.cfg, dr)
+        gs = torch.autograd.grad(out['loss'], [self.P[n] for n in self.names], allow_unused=True)
+        for n, g in zip(self.names, gs):
+            if g is None:
+                continue
+            self.grads[n] = g.clone() if self.grads[n] is None else self.grads[n] + g
+        for n in self.names:
+            self.P[n].requires_grad_(False)
+        if optimizer:
+            with torch.no_grad():
+                self.opt.step(self.P, self.grads)
+        self.step_no += 1
+        return {k: v.detach() for k, v in out.items()}
+
+
+def cfg_from_args(a) -> dict:
+    return dict(d_latent=a.d_latent, n_item_a=a.n_item_a, n_item_b=a.n_item_b, idx_pad=a.idx_pad,
+                len_rec=a.len_rec, lambda_loss=a.lambda_loss, n_gnn=a.n_gnn, n_attn=a.n_attn, n_head=a.n_head,
+                norm_first=a.norm_first, d_bias=a.d_bias, shared_item_embed=a.shared_item_embed,
+                dropout_gnn=a.dropout_gnn, dropout_attn=a.dropout_attn)

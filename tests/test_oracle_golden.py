@@ -1,0 +1,68 @@
+"""Pin the CPU oracle (oracle/c2dsr_oracle.py) against the reference's own outputs
+(golden vectors from tools/gen_fixtures.py).  Tolerance: 1e-4 relative (fp32)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle import c2dsr_oracle as O  # noqa: E402
+from tests import goldens as G  # noqa: E402
+
+TOL = 1e-4
+
+
+@pytest.mark.parametrize('name', list(G.CONFIGS))
+def test_oracle_two_steps_match_reference(name):
+    m = G.load(f'model_{name}.npz')
+    cfg = G.oracle_cfg(name)
+    tr = O.OracleTrainer(G.init_params(name), G.graphs_coo(name), cfg)
+    for s in range(int(m['n_steps'])):
+        b = G.batch(name, int(m[f's{s}/batch_lo']), int(m[f's{s}/batch_n']))
+        # grads are compared before the optimizer step
+        out = tr.train_batch(b, optimizer=False)
+        for k in ('hi_share', 'hi_a', 'hi_b', 'h_share', 'hx', 'hy', 'h_neg_a', 'h_neg_b', 'sim_a', 'sim_b'):
+            assert G.rel_err(out[k].numpy(), m[f's{s}/{k}']) < TOL, (s, k)
+        for k in ('loss', 'loss_rec', 'loss_mi'):
+            assert abs(float(out[k]) - float(m[f's{s}/{k}'])) <= TOL * abs(float(m[f's{s}/{k}'])), (s, k)
+        for n in tr.names:
+            key = f's{s}/grad/{n}'
+            assert key in m.files, key
+            assert G.rel_err(tr.grads[n].numpy(), m[key]) < TOL, (s, n)
+        # continue from the reference's own post-step parameters: AdamW's first steps
+        # amplify rounding noise in ~zero grads to ±lr (sign noise), see next test
+        for n in tr.names:
+            tr.P[n] = torch.from_numpy(m[f's{s}/param/{n}'].copy())
+
+
+@pytest.mark.parametrize('name', list(G.CONFIGS))
+def test_oracle_adamw_amsgrad_matches_reference(name):
+    """AdamW(amsgrad) restatement fed with the reference's own grads reproduces the
+    reference's parameters after each step (trainer.py:21-22,158)."""
+    m = G.load(f'model_{name}.npz')
+    cfg = G.oracle_cfg(name)
+    P = G.init_params(name)
+    names = O.trainable_names(list(P.keys()), cfg)
+    opt = O.AdamWAmsgrad()
+    for s in range(int(m['n_steps'])):
+        grads = {n: torch.from_numpy(m[f's{s}/grad/{n}'].copy()) for n in names}
+        opt.step(P, grads)
+        for n in names:
+            ref = m[f's{s}/param/{n}']
+            assert np.abs(P[n].numpy() - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max()), (s, n)
+
+
+def test_dropout_hash_rate_and_determinism():
+    idx = np.arange(1 << 20, dtype=np.int64)
+    k = O.dropout_keys(3407, 5, O.site_gcn(0, 0))
+    m1 = O.keep_mask(idx, k, 0.2)
+    m2 = O.keep_mask(idx, k, 0.2)
+    assert (m1 == m2).all()
+    assert abs(m1.mean() - 0.8) < 3e-3
+    k2 = O.dropout_keys(3407, 6, O.site_gcn(0, 0))
+    assert (O.keep_mask(idx, k2, 0.2) != m1).mean() > 0.2
+    # >32-bit indices use the high word
+    hi = idx + (1 << 33)
+    assert (O.keep_mask(hi, k, 0.2) != m1).mean() > 0.2

@@ -1,0 +1,315 @@
+"""Generate golden vectors from the REFERENCE implementation (runs only in the
+build container, where /root/reference exists; the GPU box never runs this).
+
+The reference is imported read-only via sys.path; nothing of its source is
+copied.  Outputs are plain arrays (npz, no pickles) under tests/golden/:
+
+  data_<cfg>.npz   processed train/val/test lists from CDSRDataset
+                   (dataloader.py:60-228, random.seed(3407) like main.py:91)
+  graph_<cfg>.npz  COO of adj_share/adj_specific (utils/graph.py:33-96)
+  model_<cfg>.npz  initial params, per-step intermediates, grads and params
+                   for two train_batch steps (trainer.py:91-160), dropout 0
+  eval_<cfg>.npz   evaluate_batch ranks after the two steps (trainer.py:162-181)
+  metrics.npz      cal_metrics / cal_score (utils/metrics.py)
+  fk_data.npz      checksums + head of the Food-Kitchen val/test processing
+
+Usage:  python tools/gen_fixtures.py   (PYTHONDONTWRITEBYTECODE=1 is set here)
+"""
+import argparse
+import hashlib
+import os
+import random
+import sys
+import tempfile
+from types import SimpleNamespace
+
+os.environ['PYTHONDONTWRITEBYTECODE'] = '1'
+sys.dont_write_bytecode = True
+
+import numpy as np
+import torch
+
+REF = '/root/reference'
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, 'tests', 'golden')
+sys.path.insert(0, REPO)
+from c2dsr_amd import synth  # noqa: E402
+
+CONFIGS = {
+    # name: (n_a, n_b, L, R, d, n_train, n_eval, model flags)
+    'base': dict(n_a=40, n_b=60, len_max=8, len_rec=4, d_latent=16, n_train=40, n_eval=12,
+                 n_gnn=1, n_attn=1, n_head=1, norm_first=False, d_bias=False, shared_item_embed=False),
+    'var': dict(n_a=40, n_b=60, len_max=8, len_rec=4, d_latent=16, n_train=40, n_eval=12,
+                n_gnn=2, n_attn=2, n_head=2, norm_first=True, d_bias=True, shared_item_embed=False),
+    'shared': dict(n_a=40, n_b=60, len_max=8, len_rec=4, d_latent=16, n_train=40, n_eval=12,
+                   n_gnn=1, n_attn=1, n_head=1, norm_first=False, d_bias=False, shared_item_embed=True),
+}
+N_NEG = 10
+BATCH = 16
+
+
+def ref_import():
+    sys.path.insert(0, REF)
+    import dataloader as ref_dl  # noqa
+    import models.C2DSR as ref_model  # noqa
+    import trainer as ref_trainer  # noqa
+    import utils.graph as ref_graph  # noqa
+    import utils.metrics as ref_metrics  # noqa
+    return ref_dl, ref_model, ref_trainer, ref_graph, ref_metrics
+
+
+def make_args(cfg, path_raw, path_data):
+    a = SimpleNamespace()
+    a.dataset = 'Synthetic'
+    a.path_raw = path_raw
+    a.path_data = path_data
+    a.use_raw = True
+    a.save_processed = False
+    a.device = torch.device('cpu')
+    a.batch_size = BATCH
+    a.batch_size_eval = 64
+    a.num_workers = 0
+    a.n_neg_sample = N_NEG
+    a.len_max = cfg['len_max']
+    a.len_rec = cfg['len_rec']
+    a.d_latent = cfg['d_latent']
+    a.n_gnn = cfg['n_gnn']
+    a.n_attn = cfg['n_attn']
+    a.n_head = cfg['n_head']
+    a.norm_first = cfg['norm_first']
+    a.d_bias = cfg['d_bias']
+    a.shared_item_embed = cfg['shared_item_embed']
+    a.dropout_gnn = 0.0
+    a.dropout_attn = 0.0
+    a.lr = 1e-3
+    a.l2 = 5e-4
+    a.lr_step = 10
+    a.lr_gamma = 0.5
+    a.lambda_loss = 0.7
+    a.n_item_a = cfg['n_a']
+    a.n_item_b = cfg['n_b']
+    a.n_item = cfg['n_a'] + cfg['n_b'] + 1
+    a.idx_pad = a.n_item - 1
+    return a
+
+
+def lists_to_arrays(rows, prefix):
+    out = {}
+    if not rows:
+        return out
+    k = len(rows[0])
+    for j in range(k):
+        col = [r[j] for r in rows]
+        out[f'{prefix}_{j}'] = np.asarray(col, dtype=np.int64)
+    return out
+
+
+def gen_config(name, cfg, ref):
+    ref_dl, ref_model, ref_trainer, ref_graph, ref_metrics = ref
+    tmp = tempfile.mkdtemp(prefix=f'c2dsr_fx_{name}_')
+    path_raw = os.path.join(tmp, 'raw')
+    path_data = os.path.join(tmp, 'data')
+    os.makedirs(path_data)
+    synth.make_dataset(path_raw, cfg['n_a'], cfg['n_b'], cfg['len_max'], cfg['n_train'], cfg['n_eval'],
+                       seed=11, ties=True, n_min=2)
+    args = make_args(cfg, path_raw, path_data)
+
+    # ---- a1: processed lists (main.py seeds random with 3407 before Trainer) ----
+    random.seed(3407)
+    torch.manual_seed(3407)
+    np.random.seed(3407)
+    ds_tr = ref_dl.CDSRDataset(args, 'train')
+    ds_va = ref_dl.CDSRDataset(args, 'val')
+    ds_te = ref_dl.CDSRDataset(args, 'test')
+    data = {}
+    data.update(lists_to_arrays(ds_tr.data, 'train'))
+    data.update(lists_to_arrays(ds_va.data, 'val'))
+    data.update(lists_to_arrays(ds_te.data, 'test'))
+    data['n_train'] = np.int64(len(ds_tr.data))
+    data['n_val'] = np.int64(len(ds_va.data))
+    data['n_test'] = np.int64(len(ds_te.data))
+    for mode in ('train', 'val', 'test'):
+        with open(os.path.join(path_raw, f'{mode}_new.txt'), encoding='utf-8') as f:
+            data[f'raw_{mode}'] = np.frombuffer(f.read().encode('utf-8'), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, f'data_{name}.npz'), **data)
+
+    # ---- a2: graphs ----
+    adj_s, adj_p = ref_graph.preprocess_graph(args, os.path.join(path_raw, 'train_new.txt'))
+    g = {}
+    for k, adj in (('share', adj_s), ('specific', adj_p)):
+        idx = adj._indices().numpy()
+        g[f'{k}_row'] = idx[0].astype(np.int64)
+        g[f'{k}_col'] = idx[1].astype(np.int64)
+        g[f'{k}_val'] = adj._values().numpy().astype(np.float32)
+    g['n'] = np.int64(args.n_item)
+    np.savez_compressed(os.path.join(OUT, f'graph_{name}.npz'), **g)
+
+    # ---- model: two train_batch steps, dropout 0, fixed batch order ----
+    torch.manual_seed(1234)
+    model = ref_model.C2DSR(args, adj_s, adj_p)
+    tr = ref_trainer.Trainer.__new__(ref_trainer.Trainer)
+    tr.model = model
+    tr.optimizer = torch.optim.AdamW(filter(lambda x: x.requires_grad, model.parameters()), lr=args.lr,
+                                     weight_decay=args.l2, amsgrad=True)
+    tr.scheduler = torch.optim.lr_scheduler.StepLR(tr.optimizer, step_size=args.lr_step, gamma=args.lr_gamma)
+    tr.device = args.device
+    tr.d_latent = args.d_latent
+    tr.n_item_a = args.n_item_a
+    tr.n_item_b = args.n_item_b
+    tr.len_rec = args.len_rec
+    tr.lambda_loss = args.lambda_loss
+    tr.label_pos = torch.ones(args.batch_size, 1)
+    tr.label_neg = torch.zeros(args.batch_size, 1)
+
+    m = {}
+    for k, v in model.state_dict().items():
+        m[f'init/{k}'] = v.detach().numpy().copy()
+    m['param_names'] = np.array([n for n, p in model.named_parameters()])
+
+    cap = {}
+
+    def hook(name):
+        def f(mod, inp, out):
+            cap.setdefault(name, []).append(out.detach().numpy().copy())
+        return f
+
+    hooks = []
+    for nm in ('gnn_share', 'gnn_a', 'gnn_b', 'attn_share', 'attn_a', 'attn_b', 'D_a', 'D_b'):
+        hooks.append(getattr(model, nm).register_forward_hook(hook(nm)))
+
+    real_step = tr.optimizer.step
+    grads_snap = {}
+
+    def step_wrapper(*a, **kw):
+        grads_snap['g'] = {n: (p.grad.detach().numpy().copy() if p.grad is not None else None)
+                           for n, p in model.named_parameters()}
+        return real_step(*a, **kw)
+
+    tr.optimizer.step = step_wrapper
+
+    tensors = [torch.LongTensor(np.stack([np.asarray(r[j]) for r in ds_tr.data])) for j in range(14)]
+    n_tr = tensors[0].shape[0]
+    batches = [tuple(t[i:i + BATCH] for t in tensors) for i in range(0, n_tr, BATCH)]
+    n_steps = min(3, len(batches))  # includes a short last batch when n_tr % BATCH != 0
+    model.train()
+    tr.optimizer.zero_grad()
+    for s in range(n_steps):
+        cap.clear()
+        model.convolve_graph()
+        loss, loss_rec, loss_mi = tr.train_batch(batches[s])
+        m[f's{s}/loss'] = np.float32(loss.item())
+        m[f's{s}/loss_rec'] = np.float32(loss_rec.item())
+        m[f's{s}/loss_mi'] = np.float32(loss_mi.item())
+        m[f's{s}/hi_share'] = cap['gnn_share'][0]
+        m[f's{s}/hi_a'] = cap['gnn_a'][0]
+        m[f's{s}/hi_b'] = cap['gnn_b'][0]
+        m[f's{s}/h_share'] = cap['attn_share'][0]
+        m[f's{s}/h_neg_a'] = cap['attn_share'][1]
+        m[f's{s}/h_neg_b'] = cap['attn_share'][2]
+        m[f's{s}/hx'] = cap['attn_a'][0]
+        m[f's{s}/hy'] = cap['attn_b'][0]
+        m[f's{s}/sim_a'] = np.stack(cap['D_a'])
+        m[f's{s}/sim_b'] = np.stack(cap['D_b'])
+        for n, gv in grads_snap['g'].items():
+            if gv is not None:
+                m[f's{s}/grad/{n}'] = gv
+        for n, p in model.named_parameters():
+            m[f's{s}/param/{n}'] = p.detach().numpy().copy()
+        m[f's{s}/batch_lo'] = np.int64(s * BATCH)
+        m[f's{s}/batch_n'] = np.int64(batches[s][0].shape[0])
+    m['n_steps'] = np.int64(n_steps)
+    for h in hooks:
+        h.remove()
+    np.savez_compressed(os.path.join(OUT, f'model_{name}.npz'), **m)
+
+    # ---- eval ranks after the steps (model.eval(), one convolve_graph) ----
+    model.eval()
+    ev = {}
+    with torch.no_grad():
+        model.convolve_graph()
+        for mode, ds in (('val', ds_va), ('test', ds_te)):
+            t = [torch.LongTensor(np.stack([np.asarray(r[j]) for r in ds.data])) for j in range(11)]
+            ra, rb = tr.evaluate_batch(tuple(t))
+            ev[f'{mode}_rank_a'] = np.asarray(ra, dtype=np.int64)
+            ev[f'{mode}_rank_b'] = np.asarray(rb, dtype=np.int64)
+            h_s, hx, hy = model(*t[:6])
+            ev[f'{mode}_h_share'] = h_s.numpy()
+            ev[f'{mode}_hx'] = hx.numpy()
+            ev[f'{mode}_hy'] = hy.numpy()
+    for n, p in model.named_parameters():
+        ev[f'param/{n}'] = p.detach().numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f'eval_{name}.npz'), **ev)
+    print(f'[{name}] train={len(ds_tr.data)} val={len(ds_va.data)} test={len(ds_te.data)} '
+          f'E_share={len(g["share_val"])} E_spec={len(g["specific_val"])} steps={n_steps}')
+
+
+def gen_metrics(ref):
+    ref_metrics = ref[4]
+    rng = np.random.default_rng(5)
+    ra = rng.integers(1, 60, size=97).tolist()
+    rb = rng.integers(1, 40, size=53).tolist()
+    out = {'ranks_a': np.asarray(ra), 'ranks_b': np.asarray(rb)}
+    for k, bm in (('fk', [0.1124, 0.0865, 0.0574, 0.0416]), ('mb', [0.0647, 0.0476, 0.0284, 0.0217])):
+        out[f'score_{k}'] = np.asarray(ref_metrics.cal_score(ra, rb, bm), dtype=np.float64)
+    out['metrics_a'] = np.asarray(ref_metrics.cal_metrics(ra), dtype=np.float64)
+    np.savez_compressed(os.path.join(OUT, 'metrics.npz'), **out)
+
+
+def gen_fk(ref):
+    """Food-Kitchen val/test processing (the only real raw files present)."""
+    ref_dl = ref[0]
+    a = SimpleNamespace(path_raw=os.path.join(REF, 'data/raw/Food-Kitchen'), path_data=tempfile.mkdtemp(),
+                        device='cpu', batch_size=128, dataset='Food-Kitchen', n_neg_sample=999, len_max=15,
+                        use_raw=True)
+    a.n_item_a = 29207
+    a.n_item_b = 34886
+    a.n_item = a.n_item_a + a.n_item_b + 1
+    a.idx_pad = a.n_item - 1
+    out = {}
+    random.seed(3407)
+    # 'train' mode on the val file = the stand-in train set
+    ds = ref_dl.CDSRDataset.__new__(ref_dl.CDSRDataset)
+    ds.__dict__.update(mode='val', path_raw=a.path_raw, device='cpu', batch_size=128, dataset=a.dataset,
+                       idx_pad=a.idx_pad, n_item_a=a.n_item_a, n_item_b=a.n_item_b, n_neg_sample=999, len_max=15)
+    tr = ds.preprocess_train()
+    arr = np.asarray(tr, dtype=np.int64)
+    out['trainlike_sha256'] = np.frombuffer(hashlib.sha256(arr.tobytes()).digest(), dtype=np.uint8)
+    out['trainlike_shape'] = np.asarray(arr.shape)
+    out['trainlike_head'] = arr[:64]
+    ev = ds.preprocess_evaluate()
+    # rows are ragged only in the [1]-lists; flatten row-wise with fixed layout
+    flat = np.concatenate([np.concatenate([np.asarray(x, dtype=np.int64) for x in r]) for r in ev])
+    out['evallike_sha256'] = np.frombuffer(hashlib.sha256(flat.tobytes()).digest(), dtype=np.uint8)
+    out['evallike_n'] = np.int64(len(ev))
+    out['evallike_head'] = np.stack([np.concatenate([np.asarray(x, dtype=np.int64) for x in r]) for r in ev[:16]])
+    # graph built on the val file as stand-in train file
+    adj_s, adj_p = ref[3].preprocess_graph(a, os.path.join(a.path_raw, 'val_new.txt'))
+    for k, adj in (('share', adj_s), ('specific', adj_p)):
+        idx = adj._indices().numpy().astype(np.int64)
+        val = adj._values().numpy().astype(np.float32)
+        out[f'{k}_nnz'] = np.int64(val.size)
+        out[f'{k}_idx_sha256'] = np.frombuffer(hashlib.sha256(idx.tobytes()).digest(), dtype=np.uint8)
+        out[f'{k}_val_sha256'] = np.frombuffer(hashlib.sha256(val.tobytes()).digest(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, 'fk_data.npz'), **out)
+    print(f'[fk] trainlike={arr.shape} eval={len(ev)} nnz={out["share_nnz"]}/{out["specific_nnz"]}')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--only', default='')
+    opt = ap.parse_args()
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(4)
+    ref = ref_import()
+    for name, cfg in CONFIGS.items():
+        if opt.only and name != opt.only:
+            continue
+        gen_config(name, cfg, ref)
+    if not opt.only:
+        gen_metrics(ref)
+        gen_fk(ref)
+
+
+if __name__ == '__main__':
+    main()
