@@ -1,0 +1,65 @@
+// K6: fused AdamW(amsgrad) over the flat parameter buffer.
+//
+// Replaces torch.optim.AdamW(lr, weight_decay=l2, amsgrad=True).step() (trainer.py:21-22,158)
+// together with the reference's "zero_grad once per epoch" accumulation (trainer.py:42, Q3):
+// the backward of a step writes a fresh gradient buffer F (all-reduced across ranks
+// under data parallelism); this kernel folds it into the epoch accumulator A (g = A + F),
+// clears F for the next step and applies the update — one pass, 48 B/param.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, float4* __restrict__ fresh,
+                                                    float4* __restrict__ accum, float4* __restrict__ m,
+                                                    float4* __restrict__ v, float4* __restrict__ vmax, long n4,
+                                                    float lr, float wd_factor, float b1, float b2, float eps,
+                                                    float step_size, float inv_bc2_sqrt) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float4 g = fresh[i];
+    if (accum) {
+      g = g + accum[i];
+      accum[i] = g;
+    }
+    fresh[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 pp = p[i], mm = m[i], vv = v[i], vx = vmax[i];
+    float* P = (float*)&pp;
+    float* G = (float*)&g;
+    float* Mm = (float*)&mm;
+    float* Vv = (float*)&vv;
+    float* Vx = (float*)&vx;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      P[k] *= wd_factor;
+      Mm[k] = Mm[k] + (1.f - b1) * (G[k] - Mm[k]);  // lerp
+      Vv[k] = Vv[k] * b2 + (1.f - b2) * G[k] * G[k];
+      Vx[k] = fmaxf(Vx[k], Vv[k]);
+      const float denom = sqrtf(Vx[k]) * inv_bc2_sqrt + eps;
+      P[k] = P[k] - step_size * (Mm[k] / denom);
+    }
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+    vmax[i] = vx;
+  }
+}
+
+}  // namespace
+
+// All buffers fp32 [n], n % 4 == 0, 16-byte aligned.  accum may be null (no epoch accumulation).
+C2_API int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,
+                       float b1, float b2, float eps, int step, void* stream) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  const double bc1 = 1.0 - pow((double)b1, (double)step);
+  const double bc2 = 1.0 - pow((double)b2, (double)step);
+  const float step_size = (float)(lr / bc1);
+  const float inv_bc2_sqrt = (float)(1.0 / sqrt(bc2));
+  const long n4 = n / 4;
+  int blocks = c2::ceil_div(n4, 256);
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  adamw_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((float4*)p, (float4*)fresh, (float4*)accum, (float4*)m,
+                                                        (float4*)v, (float4*)vmax, n4, lr, 1.f - lr * wd, b1, b2, eps,
+                                                        step_size, inv_bc2_sqrt);
+  C2_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,267 @@
+// Residual + dropout + LayerNorm (eps 1e-8) forward/backward, and the plain
+// residual/dropout element-wise ops used by the pre-norm variant.
+//
+// Replaces TransformerEncoderLayer's `norm1(x + dropout1(sa))`, `norm2(x + dropout2(ff))`
+// (post-norm, models/encoders.py:23-27 → torch transformer.py) and the final
+// `encoder.norm` (Q16: two LayerNorms back to back), plus their backward.
+// One row per group of LPR lanes, float4 per lane, the row kept in registers.
+#include "common.h"
+
+namespace {
+
+constexpr int MAXC = 4;  // float4 chunks per lane → d <= 16*LPR
+
+template <int LPR>
+__global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                         int rows, int d, c2::Drop drop, int64_t idx_base,
+                                                         const float* __restrict__ gw, const float* __restrict__ gb,
+                                                         float eps, float* __restrict__ xsave, float* __restrict__ y,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  constexpr int GROUPS = 256 / LPR;
+  const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  const long r = (long)blockIdx.x * GROUPS + g;
+  if (r >= rows) return;
+  float4 x[MAXC];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) {
+    const int c = (lane + q * LPR) * 4;
+    if (c < d) {
+      float4 v = c2::f4(0.f);
+      if (a) v = *(const float4*)(a + r * d + c);
+      if (b) {
+        float4 u = *(const float4*)(b + r * d + c);
+        if (drop.active()) {
+          const uint64_t bi = (uint64_t)(idx_base + r) * d + c;
+          u = u * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+        }
+        v = v + u;
+      }
+      x[q] = v;
+      if (xsave) *(float4*)(xsave + r * d + c) = v;
+      s += v.x + v.y + v.z + v.w;
+    }
+  }
+  const float mean = c2::group_sum<LPR>(s) / d;
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) {
+    const int c = (lane + q * LPR) * 4;
+    if (c < d) {
+      const float4 t = x[q] + c2::f4(-mean);
+      ss += t.x * t.x + t.y * t.y + t.z * t.z + t.w * t.w;
+    }
+  }
+  const float var = c2::group_sum<LPR>(ss) / d;
+  const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) {
+    const int c = (lane + q * LPR) * 4;
+    if (c < d) {
+      const float4 w4 = *(const float4*)(gw + c), b4 = *(const float4*)(gb + c);
+      float4 o;
+      o.x = (x[q].x - mean) * rstd * w4.x + b4.x;
+      o.y = (x[q].y - mean) * rstd * w4.y + b4.y;
+      o.z = (x[q].z - mean) * rstd * w4.z + b4.z;
+      o.w = (x[q].w - mean) * rstd * w4.w + b4.w;
+      *(float4*)(y + r * d + c) = o;
+    }
+  }
+  if (lane == 0) {
+    mean_out[r] = mean;
+    rstd_out[r] = rstd;
+  }
+}
+
+// backward; grid-stride over rows with a fixed grid so dgamma/dbeta partials are per block.
+template <int LPR>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const float* __restrict__ gw,
+                                                     const float* __restrict__ dy, int rows, int d,
+                                                     float* __restrict__ dx, int dx_accumulate,
+                                                     float* __restrict__ db_out, c2::Drop drop, int64_t idx_base,
+                                                     float* __restrict__ part) {
+  constexpr int GROUPS = 256 / LPR;
+  const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  float4 pg[MAXC], pb[MAXC];
+#pragma unroll
+  for (int q = 0; q < MAXC; ++q) pg[q] = pb[q] = c2::f4(0.f);
+  for (long r = (long)blockIdx.x * GROUPS + g; r < rows; r += (long)gridDim.x * GROUPS) {
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float4 xh[MAXC], gg[MAXC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXC; ++q) {
+      const int c = (lane + q * LPR) * 4;
+      if (c < d) {
+        const float4 xv = *(const float4*)(x + r * d + c);
+        const float4 dv = *(const float4*)(dy + r * d + c);
+        const float4 w4 = *(const float4*)(gw + c);
+        xh[q] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
+        gg[q] = dv * w4;
+        s1 += gg[q].x + gg[q].y + gg[q].z + gg[q].w;
+        s2 += gg[q].x * xh[q].x + gg[q].y * xh[q].y + gg[q].z * xh[q].z + gg[q].w * xh[q].w;
+        pg[q] = pg[q] + dv * xh[q];
+        pb[q] = pb[q] + dv;
+      }
+    }
+    const float m1 = c2::group_sum<LPR>(s1) / d, m2 = c2::group_sum<LPR>(s2) / d;
+#pragma unroll
+    for (int q = 0; q < MAXC; ++q) {
+      const int c = (lane + q * LPR) * 4;
+      if (c < d) {
+        float4 o;
+        o.x = rstd * (gg[q].x - m1 - xh[q].x * m2);
+        o.y = rstd * (gg[q].y - m1 - xh[q].y * m2);
+        o.z = rstd * (gg[q].z - m1 - xh[q].z * m2);
+        o.w = rstd * (gg[q].w - m1 - xh[q].w * m2);
+        if (dx) {
+          float4 prev = dx_accumulate ? *(const float4*)(dx + r * d + c) : c2::f4(0.f);
+          *(float4*)(dx + r * d + c) = prev + o;
+        }
+        if (db_out) {
+          if (drop.active()) {
+            const uint64_t bi = (uint64_t)(idx_base + r) * d + c;
+            o = o * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+          }
+          *(float4*)(db_out + r * d + c) = o;
+        }
+      }
+    }
+  }
+  // block reduce of the per-group partials → part[block][2][d]
+  __shared__ float red[256 * 4];
+  for (int q = 0; q < MAXC; ++q) {
+    if (q * LPR * 4 >= d) break;  // uniform within a block
+    const int c = (lane + q * LPR) * 4;
+    for (int which = 0; which < 2; ++which) {
+      const float4 v = which ? pb[q] : pg[q];
+      // each group writes its float4; then groups are summed by the first group
+      __syncthreads();
+      *(float4*)(&red[threadIdx.x * 4]) = v;
+      __syncthreads();
+      if (g == 0 && c < d) {
+        float4 t = c2::f4(0.f);
+        for (int gg2 = 0; gg2 < GROUPS; ++gg2) t = t + *(const float4*)(&red[(gg2 * LPR + lane) * 4]);
+        *(float4*)(part + ((long)blockIdx.x * 2 + which) * d + c) = t;
+      }
+    }
+  }
+}
+
+__global__ void reduce_parts_kernel(const float* __restrict__ part, int nblk, int d, float* __restrict__ dgw,
+                                    float* __restrict__ dgb) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * d) return;
+  const int which = c / d, cc = c % d;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[((long)b * 2 + which) * d + cc];
+  float* o = which ? dgb : dgw;
+  if (o) o[cc] += s;
+}
+
+__global__ void add_drop_kernel(const float* __restrict__ a, const float* __restrict__ b, long n4, int d,
+                                c2::Drop drop, int64_t idx_base, float* __restrict__ y) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 u = ((const float4*)b)[i];
+  if (drop.active()) {
+    const uint64_t bi = (uint64_t)idx_base * d + (uint64_t)i * 4;
+    u = u * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+  }
+  if (a) u = u + ((const float4*)a)[i];
+  ((float4*)y)[i] = u;
+}
+
+// dx = (y > 0) ? dy * scale : 0   — backward of drop(relu(.)) given its output y
+__global__ void relu_drop_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y, long n, float scale,
+                                     float* __restrict__ dx) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dx[i] = y[i] > 0.f ? dy[i] * scale : 0.f;
+}
+
+int lpr_for(int d) {
+  // one float4 per lane up to d = 256, then up to MAXC float4 per lane (d <= 1024)
+  int l = 4;
+  while (l < d / 4 && l < 64) l *= 2;
+  return l;
+}
+
+constexpr int LN_BWD_BLOCKS = 512;
+
+}  // namespace
+
+C2_API size_t c2dsr_ln_bwd_workspace(int d) { return (size_t)LN_BWD_BLOCKS * 2 * d * 4; }
+
+// y = LN(a + drop(b)) * w + bias; a or b may be null.  xsave (LN input) optional.
+C2_API int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
+                            int64_t idx_base, const float* w, const float* bias, float eps, float* xsave, float* y,
+                            float* mean, float* rstd, void* stream) {
+  if (d % 4 || d > 1024) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  hipStream_t s = (hipStream_t)stream;
+  const int lpr = lpr_for(d);
+  dim3 grid(c2::ceil_div(rows, 256 / lpr));
+#define C2_LN(L) add_ln_fwd_kernel<L><<<grid, 256, 0, s>>>(a, b, rows, d, dr, idx_base, w, bias, eps, xsave, y, mean, rstd)
+  switch (lpr) {
+    case 64: C2_LN(64); break;
+    case 32: C2_LN(32); break;
+    case 16: C2_LN(16); break;
+    case 8: C2_LN(8); break;
+    default: C2_LN(4); break;
+  }
+#undef C2_LN
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// dx (+)= LN backward; db_out = dx ⊙ dropout mask (grad of the dropped residual branch);
+// dgw/dgb += Σ_rows (accumulated; may be null).
+C2_API int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, const float* w, const float* dy, int rows,
+                        int d, float* dx, int dx_accumulate, float* db_out, uint32_t k0, uint32_t k1, float p,
+                        int64_t idx_base, float* dgw, float* dgb, void* workspace, void* stream) {
+  if (d % 4 || d > 1024) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  hipStream_t s = (hipStream_t)stream;
+  const int lpr = lpr_for(d);
+  const int groups = 256 / lpr;
+  int nblk = c2::ceil_div(rows, groups);
+  if (nblk > LN_BWD_BLOCKS) nblk = LN_BWD_BLOCKS;
+  float* part = (float*)workspace;
+#define C2_LNB(L) \
+  ln_bwd_kernel<L><<<nblk, 256, 0, s>>>(x, mean, rstd, w, dy, rows, d, dx, dx_accumulate, db_out, dr, idx_base, part)
+  switch (lpr) {
+    case 64: C2_LNB(64); break;
+    case 32: C2_LNB(32); break;
+    case 16: C2_LNB(16); break;
+    case 8: C2_LNB(8); break;
+    default: C2_LNB(4); break;
+  }
+#undef C2_LNB
+  if (dgw || dgb) reduce_parts_kernel<<<c2::ceil_div(2 * d, 256), 256, 0, s>>>(part, nblk, d, dgw, dgb);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// y = (a ? a : 0) + drop(b)      (element-wise, n multiple of 4; row index = flat/d)
+C2_API int c2dsr_add_dropout(const float* a, const float* b, long n, int d, uint32_t k0, uint32_t k1, float p,
+                             int64_t idx_base, float* y, void* stream) {
+  if (n % 4 || d % 4) return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  const long n4 = n / 4;
+  add_drop_kernel<<<c2::ceil_div(n4, 256), 256, 0, (hipStream_t)stream>>>(a, b, n4, d, dr, idx_base, y);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+C2_API int c2dsr_relu_drop_bwd(const float* dy, const float* y, long n, float p, float* dx, void* stream) {
+  if (n == 0) return 0;
+  const float scale = p > 0.f ? (float)(1.0 / (1.0 - (double)p)) : 1.f;
+  relu_drop_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dy, y, n, scale, dx);
+  C2_CHECK_LAUNCH();
+  return 0;
+}

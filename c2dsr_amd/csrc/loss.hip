@@ -1,0 +1,348 @@
+// Loss head of Trainer.train_batch: masked mean pooling, bilinear infomax
+// discriminators + BCE, classifier heads with a pad column + cross-entropy with
+// ignore_index, and the scalar loss combination — forward and backward.
+//
+// Replaces trainer.py:85-156 (cal_mask, pooling, D_a/D_b, BCE-with-logits,
+// torch.cat of the pad column, F.cross_entropy(ignore_index=n), count weighting).
+#include "common.h"
+
+namespace {
+
+// out[b,c] = Σ_l h[b,l,c] * gm[b,l] / Σ_l gm[b,l]      (trainer.py:85-89,101-108)
+__global__ void pool_fwd_kernel(const float* __restrict__ h, const int64_t* __restrict__ gm, int B, int L, int d,
+                                float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * d) return;
+  const int b = (int)(i / d), c = (int)(i % d);
+  float S = 0.f;
+  for (int l = 0; l < L; ++l) S += (float)gm[(long)b * L + l];
+  float acc = 0.f;
+  for (int l = 0; l < L; ++l) {
+    const float w = (float)gm[(long)b * L + l] / S;
+    acc += h[((long)b * L + l) * d + c] * w;
+  }
+  out[i] = acc;
+}
+
+// dh[b,l,c] += dout[b,c] * gm[b,l] / Σ gm[b,:]
+__global__ void pool_bwd_kernel(const float* __restrict__ dout, const int64_t* __restrict__ gm, int B, int L, int d,
+                                float* __restrict__ dh) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * L * d) return;
+  const int c = (int)(i % d);
+  const long bl = i / d;
+  const int b = (int)(bl / L);
+  float S = 0.f;
+  for (int l = 0; l < L; ++l) S += (float)gm[(long)b * L + l];
+  const float w = (float)gm[bl] / S;
+  dh[i] += dout[(long)b * d + c] * w;
+}
+
+// out[r*ldo] = Σ_c x[r*ldx + c] * y[r*ldy + c] + (bias ? bias[0] : 0); one wave per row
+__global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ x, long ldx, const float* __restrict__ y,
+                                                     long ldy, int M, int d, const float* __restrict__ bias,
+                                                     float* __restrict__ out, long ldo) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= M) return;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) s += x[r * ldx + c] * y[r * ldy + c];
+  s = c2::wave_sum(s);
+  if (lane == 0) out[r * ldo] = s + (bias ? bias[0] : 0.f);
+}
+
+// s: [4][B] = sim_a_pos, sim_a_neg, sim_b_pos, sim_b_neg (labels 1,0,1,0).
+// loss_mi = Σ_k Σ_b BCE(s_k, y_k) / Bn;  ds[k][b] = (σ(s) - y)/Bn  (Bn = global batch; = B on one device)
+__global__ __launch_bounds__(1024) void mi_loss_kernel(const float* __restrict__ s, int B, float Bn,
+                                                       float* __restrict__ loss_mi, float* __restrict__ ds) {
+  __shared__ float red[1024];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x = s[k * B + b];
+      const float y = (k & 1) ? 0.f : 1.f;
+      acc[k] += fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
+      const float sig = 1.f / (1.f + __expf(-x));
+      ds[k * B + b] = (sig - y) / Bn;
+    }
+  }
+  float tot = 0.f;
+  for (int k = 0; k < 4; ++k) {
+    red[threadIdx.x] = acc[k];
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    tot += red[0] / Bn;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *loss_mi = tot;
+}
+
+// Hcat = [hs_r ; hs_r + hx_r], Hpad = [hs_r ; hx_r] (rows (b, L-R+k)), tcat = [t_share_r ; t_spec_r]
+__global__ void rec_gather_kernel(const float* __restrict__ hs, const float* __restrict__ hx, int B, int L, int d,
+                                  int R, float* __restrict__ Hcat, float* __restrict__ Hpad) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long BR = (long)B * R;
+  if (i >= BR * d) return;
+  const long r = i / d;
+  const int c = (int)(i % d);
+  const long b = r / R, l = L - R + r % R;
+  const float a = hs[(b * L + l) * d + c], x = hx[(b * L + l) * d + c];
+  Hcat[r * d + c] = a;
+  Hcat[(BR + r) * d + c] = a + x;
+  Hpad[r * d + c] = a;
+  Hpad[(BR + r) * d + c] = x;
+}
+
+__global__ void rec_targets_kernel(const int64_t* __restrict__ ts, const int64_t* __restrict__ tx, int B, int L, int R,
+                                   int64_t* __restrict__ tcat) {
+  const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long BR = (long)B * R;
+  if (r >= BR) return;
+  const long b = r / R, l = L - R + r % R;
+  tcat[r] = ts[b * L + l];
+  tcat[BR + r] = tx[b * L + l];
+}
+
+// dhs[b,l] += dHcat[r] + dHcat[BR+r] + dHpad[r];  dhx[b,l] += dHcat[BR+r] + dHpad[BR+r]
+__global__ void rec_scatter_kernel(const float* __restrict__ dHcat, const float* __restrict__ dHpad, int B, int L,
+                                   int d, int R, float* __restrict__ dhs, float* __restrict__ dhx) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long BR = (long)B * R;
+  if (i >= BR * d) return;
+  const long r = i / d;
+  const int c = (int)(i % d);
+  const long b = r / R, l = L - R + r % R;
+  const float g1 = dHcat[r * d + c], g2 = dHcat[(BR + r) * d + c];
+  dhs[(b * L + l) * d + c] += g1 + g2 + dHpad[r * d + c];
+  dhx[(b * L + l) * d + c] += g2 + dHpad[(BR + r) * d + c];
+}
+
+// Per-row CE: lse over ncol logits, loss_row = valid ? lse - logit[t] : 0.  One wave per row.
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ lg, long ld, int M, int ncol,
+                                                     const int64_t* __restrict__ tgt, int ignore,
+                                                     float* __restrict__ lse_out, float* __restrict__ loss_row) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= M) return;
+  const float* row = lg + r * ld;
+  float m = -INFINITY, s = 0.f;
+  for (int c = lane; c < ncol; c += 64) {
+    const float v = row[c];
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+    } else {
+      s += __expf(v - m);
+    }
+  }
+  // combine (m, s) across the wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    const float mm = fmaxf(m, m2);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mm)) + (m2 == -INFINITY ? 0.f : s2 * __expf(m2 - mm));
+    m = mm;
+  }
+  if (lane == 0) {
+    const float lse = m + logf(s);
+    lse_out[r] = lse;
+    const long t = tgt[r];
+    loss_row[r] = (t != ignore) ? lse - row[t] : 0.f;
+  }
+}
+
+// dl[r,c] = (exp(l - lse) - [c==t]) * w_r,  w_r = valid ? gscale*lam*coef[r >= split] : 0.  In place allowed.
+__global__ __launch_bounds__(256) void ce_bwd_kernel(float* __restrict__ lg, long ld, int M, int ncol,
+                                                     const int64_t* __restrict__ tgt, int ignore,
+                                                     const float* __restrict__ lse, const float* __restrict__ coef,
+                                                     int split, const float* __restrict__ gscale, float lam) {
+  const int ncb = (ncol + 255) / 256;
+  const long r = blockIdx.x / ncb;
+  const int c = (int)(blockIdx.x % ncb) * 256 + threadIdx.x;
+  if (r >= M || c >= ncol) return;
+  const long t = tgt[r];
+  const float w = (t != ignore) ? gscale[0] * lam * coef[r >= split ? 1 : 0] : 0.f;
+  float* p = lg + r * ld + c;
+  const float e = __expf(*p - lse[r]);
+  *p = (e - (c == t ? 1.f : 0.f)) * w;
+}
+
+// out[r, :] += a[r*sa] * v[:]
+__global__ void outer_add_kernel(const float* __restrict__ a, long sa, const float* __restrict__ v, int M, int d,
+                                 float* __restrict__ out, long ldo) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * d) return;
+  const long r = i / d;
+  const int c = (int)(i % d);
+  out[r * ldo + c] += a[r * sa] * v[c];
+}
+
+// Per-head partial sums (trainer.py:143-152) of this rank's rows: vec[0..3] = Σ loss over
+// valid rows of (share_a, spec_a, share_b, spec_b), vec[4..7] = their valid counts.
+// rowsA/rowsB: per-row CE of the [share ; specific] stacks (2*BR rows each).
+__global__ __launch_bounds__(1024) void loss_partials_kernel(const float* __restrict__ rowsA,
+                                                             const int64_t* __restrict__ tA, int n_a,
+                                                             const float* __restrict__ rowsB,
+                                                             const int64_t* __restrict__ tB, int n_b, int BR,
+                                                             float* __restrict__ vec) {
+  __shared__ float red[1024];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = threadIdx.x; r < 2 * BR; r += blockDim.x) {
+    const int h = r >= BR ? 1 : 0;
+    if (tA[r] != n_a) {
+      acc[h] += rowsA[r];
+      acc[4 + h] += 1.f;
+    }
+    if (tB[r] != n_b) {
+      acc[2 + h] += rowsB[r];
+      acc[6 + h] += 1.f;
+    }
+  }
+  for (int k = 0; k < 8; ++k) {
+    red[threadIdx.x] = acc[k];
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) vec[k] = red[0];
+    __syncthreads();
+  }
+}
+
+// scalar combination (trainer.py:143-156) from the (globally reduced) vec[0..8]
+// (vec[8] = loss_mi).  out3 = (loss, loss_rec, loss_mi); coefA/coefB = per-row
+// gradient weights (share, specific) of the two stacks.
+__global__ void finalize_kernel(const float* __restrict__ vec, float RB, float lam, float* __restrict__ out3,
+                                float* __restrict__ coefA, float* __restrict__ coefB) {
+  if (threadIdx.x != 0) return;
+  const float ce_sa = vec[0] / vec[4], ce_a = vec[1] / vec[5];
+  const float ce_sb = vec[2] / vec[6], ce_b = vec[3] / vec[7];
+  const float loss_share = ce_sa * vec[4] / RB + ce_sb * vec[6] / RB;
+  const float loss_rec = loss_share + ce_a + ce_b;
+  const float lmi = vec[8];
+  out3[0] = lam * loss_rec + (1.f - lam) * lmi;
+  out3[1] = loss_rec;
+  out3[2] = lmi;
+  coefA[0] = 1.f / RB;
+  coefA[1] = 1.f / vec[5];
+  coefB[0] = 1.f / RB;
+  coefB[1] = 1.f / vec[7];
+}
+
+// ds[k][b] *= gscale * (1 - lam)
+__global__ void scale_ds_kernel(float* __restrict__ ds, int n, const float* __restrict__ gscale, float f) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ds[i] *= gscale[0] * f;
+}
+
+// out[i] = x[i] * s[i / d] (row scale; dx1 = ds ⊙ u)
+__global__ void rowscale_kernel(const float* __restrict__ x, const float* __restrict__ s, long n, int d,
+                                float* __restrict__ out, int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = x[i] * s[i / d];
+  out[i] = accumulate ? out[i] + v : v;
+}
+
+}  // namespace
+
+C2_API int c2dsr_pool_fwd(const float* h, const int64_t* gm, int B, int L, int d, float* out, void* stream) {
+  const long n = (long)B * d;
+  if (n == 0) return 0;
+  pool_fwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(h, gm, B, L, d, out);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_pool_bwd(const float* dout, const int64_t* gm, int B, int L, int d, float* dh, void* stream) {
+  const long n = (long)B * L * d;
+  if (n == 0) return 0;
+  pool_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dout, gm, B, L, d, dh);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int d, const float* bias,
+                        float* out, long ldo, void* stream) {
+  if (M == 0) return 0;
+  rowdot_kernel<<<c2::ceil_div(M, 4), 256, 0, (hipStream_t)stream>>>(x, ldx, y, ldy, M, d, bias, out, ldo);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_mi_loss(const float* s, int B, int B_norm, float* loss_mi, float* ds, void* stream) {
+  mi_loss_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(s, B, (float)B_norm, loss_mi, ds);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_rec_gather(const float* hs, const float* hx, int B, int L, int d, int R, float* Hcat, float* Hpad,
+                            void* stream) {
+  const long n = (long)B * R * d;
+  if (n == 0) return 0;
+  rec_gather_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(hs, hx, B, L, d, R, Hcat, Hpad);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_rec_targets(const int64_t* ts, const int64_t* tx, int B, int L, int R, int64_t* tcat, void* stream) {
+  const long n = (long)B * R;
+  if (n == 0) return 0;
+  rec_targets_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(ts, tx, B, L, R, tcat);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs, float* dhx,
+                             void* stream) {
+  const long n = (long)B * R * d;
+  if (n == 0) return 0;
+  rec_scatter_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dHcat, dHpad, B, L, d, R, dhs, dhx);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_ce_fwd(const float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, float* lse,
+                        float* loss_row, void* stream) {
+  if (M == 0) return 0;
+  ce_fwd_kernel<<<c2::ceil_div(M, 4), 256, 0, (hipStream_t)stream>>>(logits, ld, M, ncol, tgt, ignore, lse, loss_row);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_ce_bwd(float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, const float* lse,
+                        const float* coef, int split, const float* gscale, float lam, void* stream) {
+  if (M == 0) return 0;
+  dim3 grid((unsigned)((long)c2::ceil_div(ncol, 256) * M));
+  ce_bwd_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(logits, ld, M, ncol, tgt, ignore, lse, coef, split, gscale, lam);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_outer_add(const float* a, long sa, const float* v, int M, int d, float* out, long ldo, void* stream) {
+  const long n = (long)M * d;
+  if (n == 0) return 0;
+  outer_add_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(a, sa, v, M, d, out, ldo);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, const float* rowsB, const int64_t* tB,
+                               int n_b, int BR, float* vec, void* stream) {
+  loss_partials_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(rowsA, tA, n_a, rowsB, tB, n_b, BR, vec);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_loss_finalize(const float* vec, int BR_global, float lam, float* out3, float* coefA, float* coefB,
+                               void* stream) {
+  finalize_kernel<<<1, 64, 0, (hipStream_t)stream>>>(vec, (float)BR_global, lam, out3, coefA, coefB);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_scale_ds(float* ds, int n, const float* gscale, float f, void* stream) {
+  if (n == 0) return 0;
+  scale_ds_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(ds, n, gscale, f);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_rowscale(const float* x, const float* s, long n, int d, float* out, int accumulate, void* stream) {
+  if (n == 0) return 0;
+  rowscale_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(x, s, n, d, out, accumulate);
+  C2_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,129 @@
+"""Item-transition graphs (a2): the operand of the GCN SpMM.
+
+Mirrors utils/graph.py:33-109 of the reference (``preprocess_graph`` / ``normalize`` /
+``make_graph``), built straight into CSR (and the CSR of Aᵀ for the backward)
+instead of a torch sparse COO:
+
+* each raw line ``user \\t id \\t item|ts|...`` is stable-sorted by timestamp (:36-47);
+* ``adj_share`` gets an edge pre→d for every consecutive pair, ``adj_specific``
+  an edge src→d between consecutive same-domain items (A: d < n_a, else B) (:54-81).
+  The reference's de-dup dictionary is never filled (Q11), so repeated
+  transitions are all kept and summed: edge weight = transition count;
+* rows are normalised D⁻¹A with 1/deg computed in float32 by np.power(rowsum, -1)
+  and zero-degree rows left 0 (:10-17, :86-92), value = fl32(r_inv[i] * count).
+"""
+from __future__ import annotations
+
+import codecs
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+
+def read_sequences(filename: str) -> list[list[int]]:
+    """dataloader.py:39-58 / utils/graph.py:36-47: items of each line, stable-sorted by timestamp."""
+    out = []
+    with codecs.open(filename, 'r', encoding='utf-8') as f:
+        for line in f:
+            fields = line.strip().split('\t')[2:]
+            pairs = []
+            for w in fields:
+                parts = w.split('|')
+                pairs.append((int(parts[0]), int(parts[1])))
+            pairs.sort(key=lambda e: e[1])
+            out.append([p[0] for p in pairs])
+    return out
+
+
+def transition_edges(seqs: list[list[int]], n_item_a: int) -> tuple[np.ndarray, np.ndarray]:
+    """(share_edges [E,2], specific_edges [E',2]) in the reference's emission order."""
+    share, spec = [], []
+    for seq in seqs:
+        src = tgt = pre = -1
+        for d in seq:
+            if d < n_item_a:
+                if src != -1:
+                    spec.append((src, d))
+                src = d
+            else:
+                if tgt != -1:
+                    spec.append((tgt, d))
+                tgt = d
+            if pre != -1:
+                share.append((pre, d))
+            pre = d
+    return np.asarray(share, dtype=np.int64).reshape(-1, 2), np.asarray(spec, dtype=np.int64).reshape(-1, 2)
+
+
+@dataclass
+class CSRGraph:
+    n: int
+    rowptr: np.ndarray  # int32 [n+1]
+    col: np.ndarray     # int32 [nnz]
+    val: np.ndarray     # float32 [nnz]
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.size)
+
+    def transpose(self) -> 'CSRGraph':
+        rows = np.repeat(np.arange(self.n, dtype=np.int64), np.diff(self.rowptr))
+        order = np.lexsort((rows, self.col))
+        col_t = rows[order].astype(np.int32)
+        val_t = self.val[order]
+        cnt = np.bincount(self.col, minlength=self.n)
+        rowptr = np.zeros(self.n + 1, dtype=np.int64)
+        np.cumsum(cnt, out=rowptr[1:])
+        return CSRGraph(self.n, rowptr.astype(np.int32), col_t, val_t)
+
+    def coo(self):
+        rows = np.repeat(np.arange(self.n, dtype=np.int64), np.diff(self.rowptr))
+        return rows, self.col.astype(np.int64), self.val
+
+
+def normalized_csr(edges: np.ndarray, n: int) -> CSRGraph:
+    """Count-weighted, row-normalised adjacency (utils/graph.py:10-17,86-92)."""
+    if edges.size == 0:
+        return CSRGraph(n, np.zeros(n + 1, np.int32), np.zeros(0, np.int32), np.zeros(0, np.float32))
+    key = edges[:, 0] * n + edges[:, 1]
+    uk, cnt = np.unique(key, return_counts=True)  # sorted by (row, col)
+    row = uk // n
+    col = uk % n
+    deg = np.bincount(edges[:, 0], minlength=n).astype(np.float32)  # exact integer row sums
+    with np.errstate(divide='ignore'):
+        r_inv = np.power(deg, np.float32(-1)).astype(np.float32)
+    r_inv[np.isinf(r_inv)] = np.float32(0.0)
+    val = (r_inv[row] * cnt.astype(np.float32)).astype(np.float32)
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(row, minlength=n), out=rowptr[1:])
+    return CSRGraph(n, rowptr.astype(np.int32), col.astype(np.int32), val)
+
+
+def preprocess_graph(seqs_or_file, n_item_a: int, n_item: int) -> tuple[CSRGraph, CSRGraph]:
+    seqs = read_sequences(seqs_or_file) if isinstance(seqs_or_file, str) else seqs_or_file
+    e_share, e_spec = transition_edges(seqs, n_item_a)
+    return normalized_csr(e_share, n_item), normalized_csr(e_spec, n_item)
+
+
+class DeviceGraph:
+    """CSR of A and of Aᵀ resident on the device (buffers owned by the model)."""
+
+    def __init__(self, g: CSRGraph, device):
+        self.n = g.n
+        self.nnz = g.nnz
+        t = g.transpose()
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+        self.rowptr, self.col, self.val = to(g.rowptr), to(g.col), to(g.val)
+        self.rowptr_t, self.col_t, self.val_t = to(t.rowptr), to(t.col), to(t.val)
+        self.host = g
+
+    def to_torch_sparse(self):
+        r, c, v = self.host.coo()
+        return torch.sparse_coo_tensor(np.vstack([r, c]), v, (self.n, self.n))
+
+
+def make_graph(args, filename: str):
+    """utils/graph.py:99-109 (always from the raw file; no pickles)."""
+    g_share, g_spec = preprocess_graph(filename, args.n_item_a, args.n_item)
+    return g_share, g_spec

@@ -1,0 +1,161 @@
+"""Fused loss head of ``Trainer.train_batch`` (trainer.py:85-156) as one autograd node.
+
+forward:  masked-mean pooling (cal_mask, :85-108) → bilinear discriminators D_a/D_b
+          (:104-108) → 4× BCE-with-logits (:113-119) → last-R slices and the four
+          classifier heads with the pad column (:122-140) → 4× cross-entropy with
+          ignore_index = pad column (:143-152) → count-weighted share loss, loss_rec,
+          loss = λ·rec + (1-λ)·mi (:147-156).
+backward: all gradients of the five encoder outputs; parameter gradients are
+          accumulated directly into the parameters' ``.grad`` buffers.
+
+The two heads that share a classifier matrix (share_a + specific_a, share_b +
+specific_b) are stacked into one [2·B·R, d] GEMM each.  The logits are
+materialised ([2BR, n+1] fp32, the pad column written by a row-dot); the
+backward turns them into dlogits in place.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+
+from ._lib import lib, stream
+from .ops import FP32, _grad_target, gemm
+
+
+class LossMeta:
+    def __init__(self, *, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, n_a, n_b, R, lam, Wa, ba, Wb, bb, wpad,
+                 bpad, Da_w, Da_b, Db_w, Db_b, precision=FP32, B_global=None, allreduce=None):
+        self.__dict__.update(locals())
+        del self.__dict__['self']
+
+
+class LossHeadFn(Function):
+    @staticmethod
+    def forward(ctx, h_share, hx, hy, h_neg_a, h_neg_b, m: LossMeta):
+        B, L, d = h_share.shape
+        R = m.R
+        BR = B * R
+        dev = h_share.device
+        s = stream()
+        f32 = dict(device=dev, dtype=torch.float32)
+        # ---- pooling (6 vectors) ----
+        Phx = torch.empty(B, d, **f32)
+        Phy = torch.empty(B, d, **f32)
+        X2a = torch.empty(2 * B, d, **f32)  # [h_share·wb ; h_neg_a·wa]
+        X2b = torch.empty(2 * B, d, **f32)  # [h_share·wa ; h_neg_b·wb]
+        lib('c2dsr_pool_fwd', hx, m.gm_a, B, L, d, Phx, s)
+        lib('c2dsr_pool_fwd', hy, m.gm_b, B, L, d, Phy, s)
+        lib('c2dsr_pool_fwd', h_share, m.gm_b, B, L, d, X2a, s)
+        lib('c2dsr_pool_fwd', h_neg_a, m.gm_a, B, L, d, X2a[B:], s)
+        lib('c2dsr_pool_fwd', h_share, m.gm_a, B, L, d, X2b, s)
+        lib('c2dsr_pool_fwd', h_neg_b, m.gm_b, B, L, d, X2b[B:], s)
+        # ---- bilinear: s = x1ᵀ W x2 (+b)  via  U = X2·Wᵀ, s = rowdot(x1, U) ----
+        Ua = torch.empty(2 * B, d, **f32)
+        Ub = torch.empty(2 * B, d, **f32)
+        gemm(X2a, m.Da_w, Ua, M=2 * B, N=d, K=d, transB=1, precision=FP32)
+        gemm(X2b, m.Db_w, Ub, M=2 * B, N=d, K=d, transB=1, precision=FP32)
+        S = torch.empty(4, B, **f32)
+        lib('c2dsr_rowdot', Phx, d, Ua, d, B, d, m.Da_b, S[0], 1, s)
+        lib('c2dsr_rowdot', Phx, d, Ua[B:], d, B, d, m.Da_b, S[1], 1, s)
+        lib('c2dsr_rowdot', Phy, d, Ub, d, B, d, m.Db_b, S[2], 1, s)
+        lib('c2dsr_rowdot', Phy, d, Ub[B:], d, B, d, m.Db_b, S[3], 1, s)
+        vec = torch.empty(9, **f32)  # [CE sums ×4, counts ×4, loss_mi]
+        Bg = m.B_global if m.B_global is not None else B
+        dS = torch.empty(4, B, **f32)
+        lib('c2dsr_mi_loss', S, B, Bg, vec[8:], dS, s)
+        # ---- classifier heads ----
+        heads = []
+        for (hdom, W, bias, t_share, t_spec, n) in ((hx, m.Wa, m.ba, m.gt_share_a, m.gt_a, m.n_a),
+                                                   (hy, m.Wb, m.bb, m.gt_share_b, m.gt_b, m.n_b)):
+            Hcat = torch.empty(2 * BR, d, **f32)
+            Hpad = torch.empty(2 * BR, d, **f32)
+            lib('c2dsr_rec_gather', h_share, hdom, B, L, d, R, Hcat, Hpad, s)
+            tcat = torch.empty(2 * BR, device=dev, dtype=torch.int64)
+            lib('c2dsr_rec_targets', t_share, t_spec, B, L, R, tcat, s)
+            ld = n + 1
+            logits = torch.empty(2 * BR, ld, **f32)
+            gemm(Hcat, W, logits, M=2 * BR, N=n, K=d, transB=1, ldc=ld, bias=bias, precision=m.precision)
+            lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, 2 * BR, d, m.bpad, logits[:, n:], ld, s)
+            lse = torch.empty(2 * BR, **f32)
+            rows = torch.empty(2 * BR, **f32)
+            lib('c2dsr_ce_fwd', logits, ld, 2 * BR, ld, tcat, n, lse, rows, s)
+            heads.append((Hcat, Hpad, tcat, logits, lse, rows, W, bias, n))
+        out3 = torch.empty(3, **f32)
+        coefA = torch.empty(2, **f32)
+        coefB = torch.empty(2, **f32)
+        (_, _, tA, _, _, rA, _, _, _), (_, _, tB, _, _, rB, _, _, _) = heads
+        lib('c2dsr_loss_partials', rA, tA, m.n_a, rB, tB, m.n_b, BR, vec, s)
+        if m.allreduce is not None:  # data parallel: global counts / sums (exact normalisation)
+            m.allreduce(vec)
+        lib('c2dsr_loss_finalize', vec, Bg * R, float(m.lam), out3, coefA, coefB, s)
+        ctx.m, ctx.heads, ctx.coefs = m, heads, (coefA, coefB)
+        ctx.mi = (Phx, Phy, X2a, X2b, Ua, Ub, dS)
+        ctx.shape = (B, L, d)
+        loss, loss_rec, loss_mi_o = out3[0], out3[1], out3[2]
+        ctx.mark_non_differentiable(loss_rec, loss_mi_o)
+        return loss, loss_rec, loss_mi_o
+
+    @staticmethod
+    def backward(ctx, gloss, _g1, _g2):
+        m = ctx.m
+        B, L, d = ctx.shape
+        R = m.R
+        BR = B * R
+        dev = gloss.device
+        s = stream()
+        f32 = dict(device=dev, dtype=torch.float32)
+        gscale = gloss.contiguous().reshape(1)
+        dh_share = torch.zeros(B, L, d, **f32)
+        dhx = torch.zeros(B, L, d, **f32)
+        dhy = torch.zeros(B, L, d, **f32)
+        dh_na = torch.zeros(B, L, d, **f32)
+        dh_nb = torch.zeros(B, L, d, **f32)
+        # ---- classifier heads ----
+        gwpad, gbpad = _grad_target(m.wpad), _grad_target(m.bpad)
+        for (Hcat, Hpad, tcat, logits, lse, rows, W, bias, n), coef, hdom_grad in zip(ctx.heads, ctx.coefs,
+                                                                                      (dhx, dhy)):
+            ld = n + 1
+            lib('c2dsr_ce_bwd', logits, ld, 2 * BR, ld, tcat, n, lse, coef, BR, gscale, float(m.lam), s)
+            dHcat = torch.empty(2 * BR, d, **f32)
+            gemm(logits, W, dHcat, M=2 * BR, N=d, K=n, lda=ld, precision=m.precision)
+            dHpad = torch.zeros(2 * BR, d, **f32)
+            lib('c2dsr_outer_add', logits[:, n:], ld, m.wpad, 2 * BR, d, dHpad, d, s)
+            gW = _grad_target(W)
+            if gW is not None:
+                gemm(logits, Hcat, gW, M=n, N=d, K=2 * BR, transA=1, lda=ld, beta=1.0, precision=m.precision)
+            gb = _grad_target(bias)
+            if gb is not None:
+                lib('c2dsr_colsum', logits, 2 * BR, n, ld, 1.0, 1.0, gb, s)
+            if gwpad is not None:
+                gemm(logits[:, n:], Hpad, gwpad, M=1, N=d, K=2 * BR, transA=1, lda=ld, beta=1.0, precision=FP32)
+            if gbpad is not None:
+                lib('c2dsr_colsum', logits[:, n:], 2 * BR, 1, ld, 1.0, 1.0, gbpad, s)
+            lib('c2dsr_rec_scatter', dHcat, dHpad, B, L, d, R, dh_share, hdom_grad, s)
+        # ---- discriminators ----
+        Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi
+        lib('c2dsr_scale_ds', dS, 4 * B, gscale, float(1.0 - m.lam), s)
+        dP = {}
+        for (x1, X2, U, Wd, bd, k) in ((Phx, X2a, Ua, m.Da_w, m.Da_b, 0), (Phy, X2b, Ub, m.Db_w, m.Db_b, 2)):
+            dx1 = torch.empty(B, d, **f32)
+            lib('c2dsr_rowscale', U, dS[k], B * d, d, dx1, 0, s)
+            lib('c2dsr_rowscale', U[B:], dS[k + 1], B * d, d, dx1, 1, s)
+            dU = torch.empty(2 * B, d, **f32)
+            lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
+            lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
+            dX2 = torch.empty(2 * B, d, **f32)
+            gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
+            gWd = _grad_target(Wd)
+            if gWd is not None:
+                gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
+            gbd = _grad_target(bd)
+            if gbd is not None:
+                lib('c2dsr_colsum', dS[k], 2 * B, 1, 1, 1.0, 1.0, gbd, s)
+            dP[k] = (dx1, dX2)
+        (dPhx, dX2a), (dPhy, dX2b) = dP[0], dP[2]
+        lib('c2dsr_pool_bwd', dPhx, m.gm_a, B, L, d, dhx, s)
+        lib('c2dsr_pool_bwd', dPhy, m.gm_b, B, L, d, dhy, s)
+        lib('c2dsr_pool_bwd', dX2a, m.gm_b, B, L, d, dh_share, s)
+        lib('c2dsr_pool_bwd', dX2a[B:], m.gm_a, B, L, d, dh_na, s)
+        lib('c2dsr_pool_bwd', dX2b, m.gm_a, B, L, d, dh_share, s)
+        lib('c2dsr_pool_bwd', dX2b[B:], m.gm_b, B, L, d, dh_nb, s)
+        return dh_share, dhx, dhy, dh_na, dh_nb, None

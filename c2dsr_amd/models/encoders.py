@@ -1,0 +1,168 @@
+"""Drop-in ``models.encoders``: ``GCN`` and ``SelfAttention`` (models/encoders.py:7-48)
+with the reference's constructor/forward signatures and parameter names, computed
+by the gfx950 kernels (c2dsr_amd/ops.py).
+
+Parameter containers (nn.Embedding / nn.Linear / nn.LayerNorm) are used only to
+hold and initialise weights with the reference's names, order and init schemes
+(so ``state_dict`` is interchangeable); their forward is never called.
+"""
+from __future__ import annotations
+
+import copy
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import dropout as DK
+from .. import ops
+
+
+class MultiheadAttentionParams(nn.Module):
+    """Weights of nn.MultiheadAttention(d, n_head): in_proj_weight/bias, out_proj.
+    Init order as torch: out_proj Linear init, then xavier_uniform_(in_proj_weight),
+    zero in_proj_bias and out_proj.bias."""
+
+    def __init__(self, d, n_head):
+        super().__init__()
+        self.num_heads = n_head
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
+        self.in_proj_bias = nn.Parameter(torch.empty(3 * d))
+        self.out_proj = nn.Linear(d, d)
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.in_proj_bias)
+        nn.init.zeros_(self.out_proj.bias)
+
+
+class EncoderLayerParams(nn.Module):
+    """Weights of nn.TransformerEncoderLayer(d, n_head, dim_feedforward=d) (encoders.py:23-25)."""
+
+    def __init__(self, d, n_head, d_ff):
+        super().__init__()
+        self.self_attn = MultiheadAttentionParams(d, n_head)
+        self.linear1 = nn.Linear(d, d_ff)
+        self.linear2 = nn.Linear(d_ff, d)
+        self.norm1 = nn.LayerNorm(d, eps=1e-8)
+        self.norm2 = nn.LayerNorm(d, eps=1e-8)
+
+
+class EncoderParams(nn.Module):
+    """nn.TransformerEncoder(layer, n_attn, LayerNorm) parameter layout: deep copies of the layer."""
+
+    def __init__(self, layer, n_attn, d):
+        super().__init__()
+        self.layers = nn.ModuleList([copy.deepcopy(layer) for _ in range(n_attn)])
+        self.norm = nn.LayerNorm(d, eps=1e-8)
+
+
+class StepState:
+    """Per-training-step dropout bookkeeping shared by the model's modules."""
+
+    def __init__(self, seed=0):
+        self.seed = seed
+        self.step = 0
+        self.row_offset = 0   # global batch-row offset of this rank (data parallel)
+        self.next_share_pass = DK.PASS_NEG0
+
+    def keys(self, site):
+        return DK.keys(self.seed, self.step, site)
+
+
+class SelfAttention(nn.Module):
+    """models/encoders.py:7-33: pos-emb add + dropout + post/pre-norm TransformerEncoder
+    (n_attn layers, FFN width d, ReLU, eps 1e-8) + final LayerNorm, with the causal
+    mask and the inverted key-padding mask (seq != pad ⇒ masked, Q1)."""
+
+    def __init__(self, args):
+        super().__init__()
+        self.idx_pad = args.idx_pad
+        self.len_max = args.len_max
+        self.d = args.d_latent
+        self.n_head = args.n_head
+        self.n_attn = args.n_attn
+        self.norm_first = args.norm_first
+        self.p = args.dropout_attn
+        attn_mask = torch.triu(torch.full((args.len_max, args.len_max), float('-inf')), diagonal=1)
+        self.register_buffer('attn_mask', attn_mask)
+        self.pos_emb = nn.Embedding(args.len_max, args.d_latent)
+        self.encoder_layer = EncoderLayerParams(args.d_latent, args.n_head, args.d_latent)
+        self.encoder = EncoderParams(self.encoder_layer, args.n_attn, args.d_latent)
+        self.precision = ops.FP32
+        self.state = StepState()
+
+    # ---- dropout plumbing ----
+    def _drop(self, pass_id, layer, kind):
+        p = self.p if self.training else 0.0
+        if p <= 0.0:
+            return 0.0, (0, 0)
+        return p, self.state.keys(DK.site_enc(pass_id, layer, kind))
+
+    def encode(self, x, seq, pass_id):
+        """The TransformerEncoder stack on an already embedded + dropped [B, L, d] input."""
+        B, L, d = x.shape
+        rb_rows = self.state.row_offset * L
+        for li, lay in enumerate(self.encoder.layers):
+            at = lay.self_attn
+            p_at, k_at = self._drop(pass_id, li, DK.K_ATTN)
+            p_sa, k_sa = self._drop(pass_id, li, DK.K_SA)
+            p_fm, k_fm = self._drop(pass_id, li, DK.K_FF_MID)
+            p_fo, k_fo = self._drop(pass_id, li, DK.K_FF_OUT)
+
+            def sa_block(inp):
+                qkv = ops.linear(inp, at.in_proj_weight, at.in_proj_bias, self.precision)
+                o = ops.AttnFn.apply(qkv, seq, self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset)
+                return ops.linear(o, at.out_proj.weight, at.out_proj.bias, self.precision)
+
+            def ff_block(inp):
+                f = ops.linear(inp, lay.linear1.weight, lay.linear1.bias, self.precision,
+                               relu_drop=(k_fm, p_fm, rb_rows))
+                return ops.linear(f, lay.linear2.weight, lay.linear2.bias, self.precision)
+
+            if self.norm_first:
+                y = ops.AddLNFn.apply(x, None, lay.norm1.weight, lay.norm1.bias, 0.0, (0, 0), 0, lay.norm1.eps)
+                x = ops.AddDropFn.apply(x, sa_block(y), p_sa, k_sa, rb_rows)
+                y = ops.AddLNFn.apply(x, None, lay.norm2.weight, lay.norm2.bias, 0.0, (0, 0), 0, lay.norm2.eps)
+                x = ops.AddDropFn.apply(x, ff_block(y), p_fo, k_fo, rb_rows)
+            else:
+                x = ops.AddLNFn.apply(x, sa_block(x), lay.norm1.weight, lay.norm1.bias, p_sa, k_sa, rb_rows,
+                                      lay.norm1.eps)
+                x = ops.AddLNFn.apply(x, ff_block(x), lay.norm2.weight, lay.norm2.bias, p_fo, k_fo, rb_rows,
+                                      lay.norm2.eps)
+        nm = self.encoder.norm
+        return ops.AddLNFn.apply(x, None, nm.weight, nm.bias, 0.0, (0, 0), 0, nm.eps)
+
+    def forward(self, seq, seq_enc, pos, pass_id=None):
+        """encoders.py:29-33 on a caller-provided seq_enc (the fused path is ``forward_items``)."""
+        if pass_id is None:
+            pass_id = DK.PASS_SHARE
+        p, k = self._drop(pass_id, 0, DK.K_INPUT)
+        x = ops.PosDropFn.apply(seq_enc.contiguous(), self.pos_emb.weight, pos, p, k, self.state.row_offset)
+        return self.encode(x, seq, pass_id)
+
+    def forward_items(self, seq, pos, H, tok, E, sink, pass_id):
+        """Fused C2DSR.py:65-71 + encoders.py:29-33: gather (H[seq]+E[seq])·√d + P[pos], dropout, encoder."""
+        p, k = self._drop(pass_id, 0, DK.K_INPUT)
+        x = ops.EmbedFn.apply(tok, E, self.pos_emb.weight, seq, pos, H, math.sqrt(self.d), p, k,
+                              self.state.row_offset, sink, self.idx_pad)
+        return self.encode(x, seq, pass_id)
+
+
+class GCN(nn.Module):
+    """models/encoders.py:36-48: mean of [E, A·drop(E), ...] over n_gnn propagation rounds."""
+
+    def __init__(self, args):
+        super().__init__()
+        self.dropout_gnn = args.dropout_gnn
+        self.n_gnn = args.n_gnn
+        self.state = StepState()
+        self.table = 0
+        self.pad_row = args.idx_pad
+
+    def forward(self, h, adj, sink=None):
+        """h: [N, d] table, adj: c2dsr_amd.graph.DeviceGraph.  Returns (H, token)."""
+        p = self.dropout_gnn if self.training else 0.0
+        keys = [self.state.keys(DK.site_gcn(self.table, k)) if p > 0 else (0, 0) for k in range(self.n_gnn)]
+        if sink is None:
+            sink = ops.GradSink(h.shape[0], h.shape[1], h.device)
+        H, tok = ops.GCNFn.apply(h, adj, self.n_gnn, p, keys, self.pad_row, sink)
+        return H, tok, sink

@@ -1,0 +1,356 @@
+"""torch.autograd bindings of the HIP kernels (every op here launches our own
+gfx950 kernels through the C ABI; torch only allocates memory and orders streams).
+
+Gradients of the model's own (flattened) parameters are written straight into
+their ``.grad`` buffers by the kernels (accumulating, like AccumulateGrad would),
+so autograd never materialises a second copy of a table-sized gradient.
+"""
+from __future__ import annotations
+
+import torch
+from torch.autograd import Function
+
+from ._lib import lib, stream, require_device
+
+FP32, BF16 = 0, 1
+
+
+def _grad_target(param):
+    """The buffer a kernel may accumulate a parameter's gradient into, or None."""
+    if param is None or not param.requires_grad:
+        return None
+    g = param.grad
+    if g is None:
+        param.grad = torch.zeros_like(param)
+        g = param.grad
+    return g
+
+
+# ----------------------------------------------------------------------------- GEMM helpers
+def gemm(A, B, C, *, M, N, K, transA=0, transB=0, lda=None, ldb=None, ldc=None, alpha=1.0, beta=0.0, bias=None,
+         relu_drop=None, precision=FP32, split_k=0):
+    """C = alpha·op(A)·op(B) + beta·C + bias (see include/c2dsr.h:c2dsr_gemm)."""
+    if lda is None:
+        lda = M if transA else K
+    if ldb is None:
+        ldb = K if transB else N
+    if ldc is None:
+        ldc = N
+    k0 = k1 = 0
+    p = 0.0
+    row_base = 0
+    epi = 0
+    if relu_drop is not None:
+        epi = 1
+        (k0, k1), p, row_base = relu_drop
+    lib('c2dsr_gemm', transA, transB, M, N, K, A, lda, B, ldb, C, ldc, float(alpha), float(beta), bias, epi, k0, k1,
+        float(p), int(row_base), precision, split_k, stream())
+    return C
+
+
+class LinearFn(Function):
+    """y = x·Wᵀ + b  [optionally drop(relu(.))]  — nn.Linear / TransformerEncoderLayer linear1, linear2,
+    in_proj, out_proj (models/encoders.py:23-27 → torch transformer.py)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, precision, relu_drop):
+        require_device(x)
+        N, K = W.shape
+        M = x.numel() // K
+        y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
+        gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)
+        ctx.save_for_backward(x, W, y if relu_drop is not None else None)
+        ctx.b = b
+        ctx.precision = precision
+        ctx.relu_p = relu_drop[1] if relu_drop is not None else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, y = ctx.saved_tensors
+        N, K = W.shape
+        M = x.numel() // K
+        dy = dy.contiguous()
+        if ctx.relu_p is not None:
+            d2 = torch.empty_like(dy)
+            lib('c2dsr_relu_drop_bwd', dy, y, dy.numel(), float(ctx.relu_p), d2, stream())
+            dy = d2
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
+        gW = _grad_target(W)
+        if gW is not None:
+            gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
+        gb = _grad_target(ctx.b)
+        if gb is not None:
+            lib('c2dsr_colsum', dy, M, N, N, 1.0, 1.0, gb, stream())
+        return dx, None, None, None, None
+
+
+def linear(x, W, b, precision=FP32, relu_drop=None):
+    return LinearFn.apply(x.contiguous(), W, b, precision, relu_drop)
+
+
+# ----------------------------------------------------------------------------- GCN (K1)
+class GradSink:
+    """Dense gradient w.r.t. one GCN output table H, filled by every embedding lookup of H
+    (deterministic segment sums) and consumed once by the GCN backward."""
+
+    def __init__(self, n, d, device):
+        self.n, self.d, self.device = n, d, device
+        self.G = None
+
+    def buf(self):
+        if self.G is None:
+            self.G = torch.zeros(self.n, self.d, device=self.device, dtype=torch.float32)
+        return self.G
+
+
+class GCNFn(Function):
+    """H = mean(E, A·drop(E), A·drop(A·drop(E)), ...)  (models/encoders.py:42-48).
+    Outputs (H, token): H is non-differentiable; the scalar token carries the
+    dependency of every lookup of H back to this node."""
+
+    @staticmethod
+    def forward(ctx, E, graph, n_gnn, p, keys, pad_row, sink):
+        require_device(E)
+        N, d = E.shape
+        out = torch.empty_like(E)
+        s = stream()
+        inv = 1.0 / (n_gnn + 1)
+        if n_gnn == 0:  # H = E
+            lib('c2dsr_gcn_spmm', graph.rowptr, graph.col, graph.val, N, d, E, 0, 0, 0.0, 0, 0.0, E, 1.0, 0.0, -1,
+                0.0, out, None, s)
+        h_prev = E
+        for k in range(n_gnn):
+            last = k == n_gnn - 1
+            h_k = None if last else torch.empty_like(E)
+            k0, k1 = keys[k]
+            lib('c2dsr_gcn_spmm', graph.rowptr, graph.col, graph.val, N, d, h_prev, k0, k1, float(p), 0, inv,
+                E if k == 0 else None, inv, 0.0, -1, 0.0 if k == 0 else 1.0, out, h_k, s)
+            h_prev = h_k
+        ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
+        ctx.E = E
+        ctx.mark_non_differentiable(out)
+        tok = E.new_zeros(())
+        return out, tok
+
+    @staticmethod
+    def backward(ctx, _gH, _gtok):
+        G = ctx.sink.G
+        E = ctx.E
+        if G is None:
+            return (None,) * 7
+        N, d = E.shape
+        g = ctx.graph
+        n = ctx.n_gnn
+        inv = 1.0 / (n + 1)
+        s = stream()
+        direct = E.grad is not None
+        gE = E.grad if direct else torch.zeros_like(E)
+        if n == 0:
+            # H = E: gE += G (all rows) ... + direct lookup (rows != pad)
+            lib('c2dsr_gcn_spmm', g.rowptr_t, g.col_t, g.val_t, N, d, G, 0, 0, 0.0, 1, 0.0, G, 1.0, 1.0,
+                ctx.pad_row, 1.0, gE, None, s)
+        else:
+            X, alpha = G, inv
+            for k in range(n, 1, -1):  # T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k
+                T = torch.empty_like(E)
+                k0, k1 = ctx.keys[k - 1]
+                lib('c2dsr_gcn_spmm', g.rowptr_t, g.col_t, g.val_t, N, d, X, k0, k1, float(ctx.p), 1, alpha, G, inv,
+                    0.0, -1, 0.0, T, None, s)
+                X, alpha = T, 1.0
+            k0, k1 = ctx.keys[0]
+            lib('c2dsr_gcn_spmm', g.rowptr_t, g.col_t, g.val_t, N, d, X, k0, k1, float(ctx.p), 1, alpha, G, inv, 1.0,
+                ctx.pad_row, 1.0, gE, None, s)
+        ctx.sink.G = None
+        return (None if direct else gE), None, None, None, None, None, None
+
+
+# ----------------------------------------------------------------------------- embedding fuse (K2)
+class EmbedFn(Function):
+    """x = drop((H[seq] + E[seq])·√d + P[pos])  (models/C2DSR.py:65-71 + encoders.py:30-31)."""
+
+    @staticmethod
+    def forward(ctx, tok, E, P, seq, pos, H, scale, p, keys, row_base, sink, pad_row):
+        require_device(E)
+        B, L = seq.shape
+        d = E.shape[1]
+        x = torch.empty(B, L, d, device=E.device, dtype=torch.float32)
+        lib('c2dsr_embed_fwd', seq, pos, B * L, d, H, E, None, P, float(scale), keys[0], keys[1], float(p),
+            int(row_base) * L, x, stream())
+        ctx.save_for_backward(seq, pos)
+        ctx.scale, ctx.p, ctx.keys, ctx.row_base, ctx.sink, ctx.n_items = scale, p, keys, row_base, sink, E.shape[0]
+        ctx.P = P
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        seq, pos = ctx.saved_tensors
+        B, L = seq.shape
+        gx = gx.contiguous()
+        d = gx.shape[-1]
+        n = B * L
+        G = ctx.sink.buf() if ctx.sink is not None else None
+        gP = _grad_target(ctx.P)
+        gP_ret = None
+        if gP is None and ctx.needs_input_grad[2]:
+            gP_ret = torch.zeros_like(ctx.P)
+            gP = gP_ret
+        ws_bytes = lib.raw('c2dsr_embed_bwd_workspace')(n, d)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
+        lib('c2dsr_embed_bwd', seq, pos, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.row_base) * L,
+            float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes, stream())
+        tok_grad = torch.zeros((), device=gx.device)
+        return tok_grad, None, gP_ret, None, None, None, None, None, None, None, None, None
+
+
+class PosDropFn(Function):
+    """x = drop(seq_enc + P[pos])  — SelfAttention.forward on a caller-provided seq_enc (encoders.py:30-31)."""
+
+    @staticmethod
+    def forward(ctx, xin, P, pos, p, keys, row_base):
+        B, L, d = xin.shape
+        x = torch.empty_like(xin)
+        lib('c2dsr_embed_fwd', pos, pos, B * L, d, None, None, xin, P, 1.0, keys[0], keys[1], float(p),
+            int(row_base) * L, x, stream())
+        ctx.save_for_backward(pos)
+        ctx.p, ctx.keys, ctx.row_base, ctx.P = p, keys, row_base, P
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        (pos,) = ctx.saved_tensors
+        B, L = pos.shape
+        gx = gx.contiguous()
+        d = gx.shape[-1]
+        n = B * L
+        gP = _grad_target(ctx.P)
+        gP_ret = None
+        if gP is None and ctx.needs_input_grad[1]:
+            gP_ret = torch.zeros_like(ctx.P)
+            gP = gP_ret
+        gxin = torch.empty_like(gx)
+        ws_bytes = lib.raw('c2dsr_embed_bwd_workspace')(n, d)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
+        lib('c2dsr_embed_bwd', pos, pos, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.row_base) * L,
+            1.0, None, 0, gP, ctx.P.shape[0], gxin, ws, ws_bytes, stream())
+        return gxin, gP_ret, None, None, None, None
+
+
+# ----------------------------------------------------------------------------- attention
+class AttnFn(Function):
+    """SDPA core with causal + inverted key-padding mask (Q1, Q2)."""
+
+    @staticmethod
+    def forward(ctx, qkv, seq, pad, n_head, p, keys, b_base):
+        B, L, d3 = qkv.shape
+        d = d3 // 3
+        out = torch.empty(B, L, d, device=qkv.device, dtype=torch.float32)
+        P = torch.empty(B, n_head, L, L, device=qkv.device, dtype=torch.float32)
+        lib('c2dsr_attn_fwd', qkv, seq, int(pad), B, L, d, n_head, keys[0], keys[1], float(p), int(b_base), out, P,
+            stream())
+        ctx.save_for_backward(qkv, seq, P)
+        ctx.pad, ctx.n_head, ctx.p, ctx.keys, ctx.b_base = pad, n_head, p, keys, b_base
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, seq, P = ctx.saved_tensors
+        B, L, d3 = qkv.shape
+        d = d3 // 3
+        dqkv = torch.empty_like(qkv)
+        lib('c2dsr_attn_bwd', qkv, seq, int(ctx.pad), B, L, d, ctx.n_head, ctx.keys[0], ctx.keys[1], float(ctx.p),
+            int(ctx.b_base), P, dout.contiguous(), dqkv, stream())
+        return dqkv, None, None, None, None, None, None
+
+
+# ----------------------------------------------------------------------------- residual / layernorm
+class AddLNFn(Function):
+    """y = LayerNorm(a + drop(b))  (b may be None: plain LayerNorm of a); eps 1e-8."""
+
+    @staticmethod
+    def forward(ctx, a, b, w, bias, p, keys, row_base, eps):
+        d = a.shape[-1]
+        rows = a.numel() // d
+        y = torch.empty_like(a)
+        xsave = torch.empty_like(a) if b is not None else None
+        mean = torch.empty(rows, device=a.device)
+        rstd = torch.empty(rows, device=a.device)
+        lib('c2dsr_add_ln_fwd', a, b, rows, d, keys[0], keys[1], float(p), int(row_base), w, bias, float(eps), xsave, y,
+            mean, rstd, stream())
+        ctx.save_for_backward(xsave if b is not None else a, mean, rstd)
+        ctx.w, ctx.bias, ctx.p, ctx.keys, ctx.row_base, ctx.has_b = w, bias, p, keys, row_base, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd = ctx.saved_tensors
+        d = x.shape[-1]
+        rows = x.numel() // d
+        dy = dy.contiguous()
+        da = torch.empty_like(x)
+        db = torch.empty_like(x) if ctx.has_b else None
+        gw, gb = _grad_target(ctx.w), _grad_target(ctx.bias)
+        ws = torch.empty(lib.raw('c2dsr_ln_bwd_workspace')(d), dtype=torch.uint8, device=x.device)
+        lib('c2dsr_ln_bwd', x, mean, rstd, ctx.w, dy, rows, d, da, 0, db, ctx.keys[0], ctx.keys[1], float(ctx.p),
+            int(ctx.row_base), gw, gb, ws, stream())
+        return da, db, None, None, None, None, None, None
+
+
+class AddDropFn(Function):
+    """y = a + drop(b)  (pre-norm residual)."""
+
+    @staticmethod
+    def forward(ctx, a, b, p, keys, row_base):
+        d = a.shape[-1]
+        y = torch.empty_like(a)
+        lib('c2dsr_add_dropout', a, b.contiguous(), a.numel(), d, keys[0], keys[1], float(p), int(row_base), y,
+            stream())
+        ctx.p, ctx.keys, ctx.row_base = p, keys, row_base
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        db = torch.empty_like(dy)
+        lib('c2dsr_add_dropout', None, dy, dy.numel(), dy.shape[-1], ctx.keys[0], ctx.keys[1], float(ctx.p),
+            int(ctx.row_base), db, stream())
+        return dy, db, None, None, None
+
+
+# ----------------------------------------------------------------------------- bilinear (D_a / D_b)
+class BilinearFn(Function):
+    """nn.Bilinear(d, d, 1): s = x1ᵀ W x2 (+b)  (models/C2DSR.py:46-55 used at trainer.py:104-108)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, W, b):
+        B, d = x1.shape
+        U = torch.empty(B, d, device=x1.device, dtype=torch.float32)
+        gemm(x2, W, U, M=B, N=d, K=d, transB=1)
+        out = torch.empty(B, 1, device=x1.device, dtype=torch.float32)
+        lib('c2dsr_rowdot', x1, d, U, d, B, d, b, out, 1, stream())
+        ctx.save_for_backward(x1, x2, U)
+        ctx.W, ctx.b = W, b
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x1, x2, U = ctx.saved_tensors
+        B, d = x1.shape
+        ds = dout.contiguous().reshape(B)
+        s = stream()
+        dx1 = torch.empty_like(x1)
+        lib('c2dsr_rowscale', U, ds, B * d, d, dx1, 0, s)
+        dU = torch.empty_like(x1)
+        lib('c2dsr_rowscale', x1, ds, B * d, d, dU, 0, s)
+        dx2 = torch.empty_like(x2)
+        gemm(dU, ctx.W, dx2, M=B, N=d, K=d)
+        gW = _grad_target(ctx.W)
+        if gW is not None:
+            gemm(dU, x2, gW, M=d, N=d, K=B, transA=1, beta=1.0)
+        gb = _grad_target(ctx.b)
+        if gb is not None:
+            lib('c2dsr_colsum', ds, B, 1, 1, 1.0, 1.0, gb, s)
+        return dx1, dx2, None, None

@@ -1,0 +1,118 @@
+/* C2DSR MI355X (gfx950) kernel library — C ABI.
+ *
+ * Drop-in boundary for the C2DSR per-step training path.  The
+ * reference (crystal22/C2DSR) is pure PyTorch: its "operator interface" is the
+ * ATen calls made from models/C2DSR.py, models/encoders.py and trainer.py.  Each
+ * entry point below replaces the ATen work of one reference site (cited per
+ * function); the host-side mirror of the reference's module API
+ * (c2dsr_amd/models/C2DSR.py, c2dsr_amd/models/encoders.py, c2dsr_amd/trainer.py)
+ * binds them through ctypes (c2dsr_amd/_lib.py).  See INTEGRATION.md.
+ *
+ * Conventions: plain device pointers (fp32 unless stated, int64 index tensors as
+ * the reference's LongTensors), row-major, sizes as ints; `stream` is a
+ * hipStream_t passed as void*.  Every function is asynchronous on `stream` and
+ * returns 0 or a hipError_t code (hipErrorInvalidValue = 1 for bad shapes).
+ * Dropout (where a `p` appears) uses the stateless counter hash
+ * keep(idx) = lowbias32(lowbias32(lo(idx)^k0) ^ hi(idx) ^ k1) >= floor(p·2^32),
+ * scale 1/(1-p); (k0,k1) come from (seed, step, site) — see c2dsr_amd/dropout.py.
+ */
+#ifndef C2DSR_H
+#define C2DSR_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* K1 GCN propagation, CSR SpMM with fused dropout / mean.
+ * Replaces models/encoders.py:42-48 (F.dropout, torch.spmm, torch.stack(...).mean) as
+ * called by models/C2DSR.py:59-62, and its backward (CSR of Aᵀ, mask_on_output=1).
+ *   Y[i] = alpha·Σ_e val[e]·(Mask⊙X)[col[e]] + (beta + (i!=pad_row ? delta : 0))·Z[i] + gamma·Y[i]
+ *   Y2[i] = Σ_e val[e]·(Mask⊙X)[col[e]]   (optional) */
+int c2dsr_gcn_spmm(const int* rowptr, const int* col, const float* val, int n_rows, int d, const float* X,
+                   uint32_t k0, uint32_t k1, float p, int mask_on_output, float alpha, const float* Z, float beta,
+                   float delta, int pad_row, float gamma, float* Y, float* Y2, void* stream);
+
+/* K2 embedding fuse.  Replaces models/C2DSR.py:65-71,81-82 + models/encoders.py:30-31:
+ *   X[r] = drop((H[seq[r]] + E[seq[r]])·scale + P[pos[r]])      (Xin == NULL)
+ *   X[r] = drop(Xin[r] + P[pos[r]])                              (Xin != NULL: SelfAttention.forward)
+ * dropout index (idx_base + r)·d + c. */
+int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H, const float* E,
+                    const float* Xin, const float* P, float scale, uint32_t k0, uint32_t k1, float p,
+                    int64_t idx_base, float* X, void* stream);
+size_t c2dsr_embed_bwd_workspace(int n_rows, int d);
+/* Deterministic (radix-sort + ordered segment sum) backward of the above
+ * (replaces embedding_dense_backward):  G[seq[r]] += scale·drop(gX[r]);
+ * gP[pos[r]] += drop(gX[r]);  gXin[r] = drop(gX[r]).  Null outputs are skipped. */
+int c2dsr_embed_bwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* gX, uint32_t k0,
+                    uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items, float* gP, int n_pos,
+                    float* gXin, void* workspace, size_t ws_bytes, void* stream);
+
+/* Dense GEMM on the matrix cores (nn.Linear / nn.Bilinear / classifier addmm and their
+ * backward; models/encoders.py:33, trainer.py:104-108,131-140):
+ *   C = alpha·op(A)·op(B) + beta·C + bias;  epilogue 1: C = drop(relu(C)), index (row_base+row)·N+col.
+ * precision 0: exact fp32 MFMA (v_mfma_f32_32x32x2_f32); 1: bf16 operands, fp32 accumulate.
+ * split_k 0 = automatic. */
+int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
+               float* C, int ldc, float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1,
+               float p, int64_t row_base, int precision, int split_k, void* stream);
+/* out[n] = beta·out[n] + alpha·Σ_m X[m·ldx + n]   (bias gradients) */
+int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* stream);
+
+/* Attention core (SDPA math path with causal + inverted key-padding mask, Q1/Q2;
+ * models/encoders.py:14,33).  qkv [B,L,3d], out [B,L,d], Psave [B,H,L,L]; L <= 128. */
+int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,
+                   uint32_t k1, float p, int64_t b_base, float* out, float* Psave, void* stream);
+int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,
+                   uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout, float* dqkv,
+                   void* stream);
+
+/* Residual + dropout + LayerNorm (TransformerEncoderLayer norm1/norm2, encoder.norm; eps 1e-8). */
+int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
+                     int64_t idx_base, const float* w, const float* bias, float eps, float* xsave, float* y,
+                     float* mean, float* rstd, void* stream);
+size_t c2dsr_ln_bwd_workspace(int d);
+int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, const float* w, const float* dy, int rows,
+                 int d, float* dx, int dx_accumulate, float* db_out, uint32_t k0, uint32_t k1, float p,
+                 int64_t idx_base, float* dgw, float* dgb, void* workspace, void* stream);
+int c2dsr_add_dropout(const float* a, const float* b, long n, int d, uint32_t k0, uint32_t k1, float p,
+                      int64_t idx_base, float* y, void* stream);
+/* backward of drop(relu(.)) from its output: dx = (y > 0) ? dy/(1-p) : 0 */
+int c2dsr_relu_drop_bwd(const float* dy, const float* y, long n, float p, float* dx, void* stream);
+
+/* Loss head (trainer.py:85-156). */
+int c2dsr_pool_fwd(const float* h, const int64_t* gm, int B, int L, int d, float* out, void* stream);
+int c2dsr_pool_bwd(const float* dout, const int64_t* gm, int B, int L, int d, float* dh, void* stream);
+int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int d, const float* bias, float* out,
+                 long ldo, void* stream);
+/* loss_mi = Σ_k Σ_b BCE(s_k[b], y_k)/B_norm, ds = (σ(s)-y)/B_norm; s = [sim_a_pos; sim_a_neg; sim_b_pos; sim_b_neg] */
+int c2dsr_mi_loss(const float* s, int B, int B_norm, float* loss_mi, float* ds, void* stream);
+int c2dsr_rec_gather(const float* hs, const float* hx, int B, int L, int d, int R, float* Hcat, float* Hpad,
+                     void* stream);
+int c2dsr_rec_targets(const int64_t* ts, const int64_t* tx, int B, int L, int R, int64_t* tcat, void* stream);
+int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs, float* dhx,
+                      void* stream);
+int c2dsr_ce_fwd(const float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, float* lse,
+                 float* loss_row, void* stream);
+int c2dsr_ce_bwd(float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, const float* lse,
+                 const float* coef, int split, const float* gscale, float lam, void* stream);
+int c2dsr_outer_add(const float* a, long sa, const float* v, int M, int d, float* out, long ldo, void* stream);
+/* vec[0..7] = per-head CE sums and valid counts of this rank's rows (all-reduced under DP) */
+int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, const float* rowsB, const int64_t* tB, int n_b,
+                        int BR, float* vec, void* stream);
+/* out3 = (loss, loss_rec, loss_mi) from vec[0..8]; coefA/B = per-row grad weights */
+int c2dsr_loss_finalize(const float* vec, int BR_global, float lam, float* out3, float* coefA, float* coefB,
+                        void* stream);
+int c2dsr_scale_ds(float* ds, int n, const float* gscale, float f, void* stream);
+int c2dsr_rowscale(const float* x, const float* s, long n, int d, float* out, int accumulate, void* stream);
+
+/* K6 AdamW(amsgrad) over flat buffers, folding the fresh grad into the epoch accumulator
+ * (trainer.py:21-22,42,158). */
+int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,
+                float b1, float b2, float eps, int step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* C2DSR_H */

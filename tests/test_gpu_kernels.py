@@ -1,0 +1,235 @@
+"""Per-kernel numerics on the MI355X: each HIP kernel (through the C ABI) against a
+plain torch-fp32 CPU computation of the same op.  fp32-MFMA paths: rel 1e-5 (of
+max |ref|); bf16-MFMA paths: rel 2e-2; integer/index work: bit-exact."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _lib():
+    from c2dsr_amd._lib import lib
+    assert torch.cuda.is_available()
+    lib.load()
+    yield
+
+
+@pytest.mark.parametrize('ta,tb', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('prec,tol', [(0, 1e-5), (1, 2e-2)])
+@pytest.mark.parametrize('M,N,K', [(300, 200, 96), (128, 128, 32), (37, 53, 19), (256, 768, 256), (64, 40, 5000)])
+def test_gemm(ta, tb, prec, tol, M, N, K):
+    from c2dsr_amd.ops import gemm
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K + ta * 2 + tb)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) if tb else torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = 0.5 * ((A.T if ta else A) @ (B.T if tb else B)) + 2.0 * C0 + bias
+    C = C0.to(DEV)
+    gemm(A.to(DEV), B.to(DEV), C, M=M, N=N, K=K, transA=ta, transB=tb, alpha=0.5, beta=2.0, bias=bias.to(DEV),
+         precision=prec, split_k=1)
+    torch.cuda.synchronize()
+    assert rel(C, ref) < tol
+    # split-K path (no bias)
+    ref2 = (A.T if ta else A) @ (B.T if tb else B) + C0
+    C = C0.to(DEV)
+    gemm(A.to(DEV), B.to(DEV), C, M=M, N=N, K=K, transA=ta, transB=tb, beta=1.0, precision=prec, split_k=0)
+    assert rel(C, ref2) < tol
+
+
+def test_gemm_relu_dropout_epilogue():
+    from c2dsr_amd.ops import gemm
+    from oracle.c2dsr_oracle import keep_mask
+    M, N, K, p = 200, 64, 48, 0.3
+    A, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
+    keys = (123456, 987654)
+    C = torch.empty(M, N, device=DEV)
+    gemm(A.to(DEV), W.to(DEV), C, M=M, N=N, K=K, transB=1, bias=b.to(DEV), relu_drop=(keys, p, 1000), precision=0)
+    idx = (np.arange(M)[:, None] + 1000) * N + np.arange(N)[None, :]
+    mk = torch.from_numpy(keep_mask(idx, keys, p).astype(np.float32)) / (1 - p)
+    ref = torch.relu(A @ W.T + b) * mk
+    assert rel(C, ref) < 1e-5
+
+
+@pytest.mark.parametrize('d,n_gnn,p', [(16, 1, 0.0), (64, 1, 0.25), (256, 2, 0.2), (12, 1, 0.0)])
+def test_gcn_fwd_bwd_vs_oracle(d, n_gnn, p):
+    from c2dsr_amd import ops
+    from c2dsr_amd.graph import DeviceGraph, normalized_csr
+    from oracle import c2dsr_oracle as O
+    rng = np.random.default_rng(d + n_gnn)
+    N = 700
+    edges = rng.integers(0, N - 1, size=(5000, 2))
+    edges = np.concatenate([edges, edges[:300]])  # duplicates (counts > 1)
+    g = normalized_csr(edges, N)
+    dg = DeviceGraph(g, DEV)
+    E = torch.randn(N, d)
+    seed, step = 3407, 5
+    keys = [O.dropout_keys(seed, step, O.site_gcn(1, k)) for k in range(n_gnn)]
+    Ed = E.to(DEV).requires_grad_(True)
+    sink = ops.GradSink(N, d, DEV)
+    H, tok = ops.GCNFn.apply(Ed, dg, n_gnn, p, keys, N - 1, sink)
+    dr = O.Dropper(p, 0.0, seed, step)
+    r, c, v = g.coo()
+    graph = (torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v))
+    Er = E.clone().requires_grad_(True)
+    Hr = O.gcn(Er, graph, n_gnn, p, dr, 1)
+    assert rel(H, Hr) < 1e-5
+    # backward: inject a dense grad of H through the sink + direct-lookup term on non-pad rows
+    G = torch.randn(N, d)
+    sink.buf().copy_(G.to(DEV))
+    tok.backward()
+    ref = torch.autograd.grad(Hr, Er, G)[0] + G * (torch.arange(N) != N - 1)[:, None]
+    assert rel(Ed.grad, ref) < 1e-5
+
+
+@pytest.mark.parametrize('d,n_items,n_rows,p', [(64, 50, 3000, 0.0), (256, 40000, 20000, 0.2), (16, 7, 513, 0.1)])
+def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
+    from c2dsr_amd._lib import lib, stream
+    from oracle.c2dsr_oracle import keep_mask
+    rng = np.random.default_rng(d)
+    L = 10
+    B = n_rows // L
+    n_rows = B * L
+    # heavy duplication incl. a dominant "pad" id
+    seq = rng.integers(0, n_items, size=n_rows)
+    seq[rng.random(n_rows) < 0.4] = n_items - 1
+    pos = rng.integers(0, L, size=n_rows)
+    H, E, P = torch.randn(n_items, d), torch.randn(n_items, d), torch.randn(L, d)
+    keys = (11, 22)
+    scale = math.sqrt(d)
+    X = torch.empty(n_rows, d, device=DEV)
+    sd, pd = torch.from_numpy(seq).to(DEV), torch.from_numpy(pos).to(DEV)
+    lib('c2dsr_embed_fwd', sd, pd, n_rows, d, H.to(DEV), E.to(DEV), None, P.to(DEV), scale, keys[0], keys[1], p, 77,
+        X, stream())
+    idx = (np.arange(n_rows)[:, None] + 77) * d + np.arange(d)[None, :]
+    mk = torch.from_numpy(keep_mask(idx, keys, p).astype(np.float32)) / (1 - p)
+    ref = ((H[seq] + E[seq]) * scale + P[pos]) * mk
+    assert rel(X, ref) < 1e-6
+    gX = torch.randn(n_rows, d)
+    outs = []
+    for _ in range(2):
+        G = torch.zeros(n_items, d, device=DEV)
+        gP = torch.zeros(L, d, device=DEV)
+        ws_b = lib.raw('c2dsr_embed_bwd_workspace')(n_rows, d)
+        ws = torch.empty(ws_b, dtype=torch.uint8, device=DEV)
+        lib('c2dsr_embed_bwd', sd, pd, n_rows, d, gX.to(DEV), keys[0], keys[1], p, 77, scale, G, n_items, gP, L, None,
+            ws, ws_b, stream())
+        outs.append((G.cpu(), gP.cpu()))
+    g = gX * mk
+    Gr = torch.zeros(n_items, d, dtype=torch.float64).index_add_(0, torch.from_numpy(seq), (g * scale).double())
+    Pr = torch.zeros(L, d, dtype=torch.float64).index_add_(0, torch.from_numpy(pos), g.double())
+    assert rel(outs[0][0], Gr) < 1e-5 and rel(outs[0][1], Pr) < 1e-5
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])  # bitwise reproducible
+
+
+@pytest.mark.parametrize('L,d,H,p', [(8, 16, 1, 0.0), (8, 16, 2, 0.0), (50, 256, 1, 0.2), (30, 64, 2, 0.1),
+                                     (100, 128, 1, 0.0), (128, 64, 4, 0.0)])
+def test_attention_vs_oracle(L, d, H, p):
+    from c2dsr_amd import ops
+    from oracle import c2dsr_oracle as O
+    torch.manual_seed(L + d)
+    B = 24
+    pad = 999
+    lens = torch.randint(1, L, (B,))
+    seq = torch.randint(0, 900, (B, L))
+    for b in range(B):  # left padding; position 0 always pad, plus random interior pads
+        seq[b, :L - lens[b]] = pad
+    seq[torch.rand(B, L) < 0.3] = pad
+    seq[:, 0] = pad
+    qkv = torch.randn(B, L, 3 * d)
+    W = torch.eye(3 * d, d)  # identity in_proj so oracle attention sees qkv directly
+    seed, step = 5, 9
+    dr = O.Dropper(0.0, p, seed, step)
+    keys = O.dropout_keys(seed, step, O.site_enc(2, 0, 1))
+    qd = qkv.to(DEV).requires_grad_(True)
+    out = ops.AttnFn.apply(qd, seq.to(DEV), pad, H, p, keys, 0)
+    # oracle: attention() applies in_proj; feed x with W_in = [I;I;I]-like split by using qkv as-is
+    Pm = {'l.self_attn.in_proj_weight': torch.zeros(3 * d, d), 'l.self_attn.in_proj_bias': torch.zeros(3 * d),
+          'l.self_attn.out_proj.weight': torch.eye(d), 'l.self_attn.out_proj.bias': torch.zeros(d)}
+    del W
+
+    class _Q:  # monkey-patched input projection: return qkv directly
+        pass
+    qr = qkv.clone().requires_grad_(True)
+    # reproduce O.attention on given q,k,v
+    dh = d // H
+    q, k, v = qr.split(d, -1)
+    q = q.reshape(B, L, H, dh).transpose(1, 2)
+    k = k.reshape(B, L, H, dh).transpose(1, 2)
+    v = v.reshape(B, L, H, dh).transpose(1, 2)
+    causal = torch.triu(torch.ones(L, L, dtype=torch.bool), 1)
+    masked = causal[None, None] | (seq != pad)[:, None, None, :]
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    s = s.masked_fill(masked, float('-inf'))
+    ok = (~masked).any(-1, keepdim=True)
+    a = torch.softmax(torch.where(ok, s, torch.zeros_like(s)), -1) * ok
+    m = dr.mask((B, H, L, L), O.site_enc(2, 0, 1), p, row_dim_prod=H * L * L)
+    if m is not None:
+        a = a * m
+    ref = (a @ v).transpose(1, 2).reshape(B, L, d)
+    assert rel(out, ref) < 1e-5
+    go = torch.randn(B, L, d)
+    out.backward(go.to(DEV))
+    ref.backward(go)
+    assert rel(qd.grad, qr.grad) < 1e-5
+    _ = Pm
+
+
+@pytest.mark.parametrize('d', [16, 64, 256, 512])
+@pytest.mark.parametrize('p', [0.0, 0.2])
+def test_add_layernorm_fwd_bwd(d, p):
+    from c2dsr_amd import ops
+    from oracle.c2dsr_oracle import keep_mask
+    rows = 777
+    a, b = torch.randn(rows, d), torch.randn(rows, d)
+    w, bias = torch.randn(d), torch.randn(d)
+    keys = (5, 6)
+    ad, bd = a.to(DEV).requires_grad_(True), b.to(DEV).requires_grad_(True)
+    wd = w.to(DEV).requires_grad_(True)
+    bsd = bias.to(DEV).requires_grad_(True)
+    y = ops.AddLNFn.apply(ad, bd, wd, bsd, p, keys, 10, 1e-8)
+    idx = (np.arange(rows)[:, None] + 10) * d + np.arange(d)[None, :]
+    mk = torch.from_numpy(keep_mask(idx, keys, p).astype(np.float32)) / (1 - p)
+    ar, br, wr, bbr = [t.clone().requires_grad_(True) for t in (a, b, w, bias)]
+    x = ar + br * mk
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    ref = (x - mu) / torch.sqrt(var + 1e-8) * wr + bbr
+    assert rel(y, ref) < 1e-5
+    gy = torch.randn(rows, d)
+    y.backward(gy.to(DEV))
+    ref.backward(gy)
+    for got, want in ((ad.grad, ar.grad), (bd.grad, br.grad), (wd.grad, wr.grad), (bsd.grad, bbr.grad)):
+        assert rel(got, want) < 2e-5
+
+
+def test_adamw_kernel_vs_oracle():
+    from c2dsr_amd._lib import lib, stream
+    from oracle.c2dsr_oracle import AdamWAmsgrad
+    n = 10_000
+    p = torch.randn(n)
+    opt = AdamWAmsgrad(lr=1e-3, wd=5e-4)
+    P = {'w': p.clone()}
+    bufs = [p.clone().to(DEV)] + [torch.zeros(n, device=DEV) for _ in range(5)]
+    pd, fresh, accum, m, v, vmax = bufs
+    acc_ref = torch.zeros(n)
+    for step in range(1, 4):
+        g = torch.randn(n)
+        acc_ref += g
+        fresh.copy_(g.to(DEV))
+        lib('c2dsr_adamw', pd, fresh, accum, m, v, vmax, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, step, stream())
+        opt.step(P, {'w': acc_ref.clone()})
+        assert rel(pd, P['w']) < 1e-6
+        assert float(fresh.abs().max()) == 0.0
+        assert rel(accum, acc_ref) < 1e-7

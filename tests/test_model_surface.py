@@ -1,0 +1,44 @@
+"""CPU checks of the drop-in module surface: parameter names, shapes and the
+initialisation (same torch RNG draws as the reference, so equal state_dicts for
+the same seed), the C-ABI library exports, and the header-derived binding."""
+import torch
+
+from tests import goldens as G
+from tests.test_gpu_parity import golden_graphs, make_args
+
+
+def test_init_matches_reference_state_dict():
+    from c2dsr_amd.models.C2DSR import C2DSR
+    for name in G.CONFIGS:
+        args = make_args(G.CONFIGS[name])
+        args.device = torch.device('cpu')
+        gs, gp = golden_graphs(name)
+        torch.manual_seed(1234)  # tools/gen_fixtures.py seeds the reference model with 1234
+        model = C2DSR(args, gs, gp)
+        ref = G.init_params(name)
+        sd = model.state_dict()
+        assert set(ref) <= set(sd), set(ref) - set(sd)
+        for k, v in ref.items():
+            assert torch.equal(sd[k], v), (name, k)
+
+
+def test_library_exports_every_declared_symbol():
+    import ctypes
+    from c2dsr_amd._lib import LIB_PATH, parse_header
+    lib = ctypes.CDLL(LIB_PATH)
+    sigs = parse_header()
+    assert len(sigs) >= 25
+    for name in sigs:
+        assert hasattr(lib, name), name
+
+
+def test_trainable_parameters_exclude_template_layer():
+    from c2dsr_amd.models.C2DSR import C2DSR
+    args = make_args(G.CONFIGS['base'])
+    args.device = torch.device('cpu')
+    gs, gp = golden_graphs('base')
+    model = C2DSR(args, gs, gp)
+    names = [n for n, _ in model.trainable_named_parameters()]
+    assert not any('.encoder_layer.' in n for n in names)
+    m = G.load('model_base.npz')
+    assert set(names) == {k[len('s0/grad/'):] for k in m.files if k.startswith('s0/grad/')}
