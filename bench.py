@@ -1,0 +1,250 @@
+"""Training-throughput benchmark of the MI355X C2DSR path (BASELINE.json metric:
+"train sequences/sec at d=256, seq_len=50, |items|~100k; 1/2/4/8 GPU").
+
+A step = convolve_graph() + train_batch() (HIP forward, fused loss head, backward,
+RCCL gradient all-reduce when N>1, fused AdamW-amsgrad) over one batch of synthetic
+two-domain sequences already resident in HBM.  Workload (N=1 line): Movie-Book item
+counts (36,845 + 63,937; BASELINE configs[2]), d=256, L=50, B=2048 per GPU, R=10,
+dropout 0.2, bf16 MFMA compute / fp32 storage.  Weak scaling: every rank trains its
+own batch of B, `value` = total sequences/s over all ranks.
+
+Launch:  python bench.py [--gpus N --steps K --warmup W]
+         N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import random
+import sys
+import time
+from types import SimpleNamespace
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (n_a, n_b, d, L, B)
+    'mb': dict(n_a=36845, n_b=63937, d=256, L=50, B=2048, label='Movie-Book sizes (synthetic)'),
+    'fk': dict(n_a=29207, n_b=34886, d=256, L=50, B=1024, label='Food-Kitchen sizes (synthetic)'),
+    'ee': dict(n_a=8367, n_b=11404, d=256, L=50, B=512, label='Entertainment-Education sizes (synthetic)'),
+    'tiny': dict(n_a=2000, n_b=3000, d=64, L=20, B=256, label='tiny smoke workload'),
+}
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    if int(os.environ.get('RANK', '0')) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def make_workload(cfg, n_seqs, seed=1):
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import synth
+    seqs = synth.make_sequences(n_seqs, cfg['n_a'], cfg['n_b'], cfg['L'], seed=seed, n_min=6)
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, cfg['n_a'], cfg['n_b'], cfg['L']))
+    gs, gp = GR.preprocess_graph(seqs, cfg['n_a'], cfg['n_a'] + cfg['n_b'] + 1)
+    return rows, gs, gp
+
+
+def make_args(cfg, device, precision, dropout=0.2):
+    n = cfg['n_a'] + cfg['n_b'] + 1
+    return SimpleNamespace(d_latent=cfg['d'], n_item=n, n_item_a=cfg['n_a'], n_item_b=cfg['n_b'], idx_pad=n - 1,
+                           shared_item_embed=False, d_bias=False, n_gnn=1, dropout_gnn=dropout, n_attn=1, n_head=1,
+                           dropout_attn=dropout, norm_first=False, len_max=cfg['L'], len_rec=10, lambda_loss=0.7,
+                           lr=1e-3, l2=5e-4, lr_step=10, lr_gamma=0.5, batch_size=cfg['B'], device=device,
+                           precision=precision, seed=3407)
+
+
+class KernelTimer:
+    """HIP-event timing of the classifier-head GEMMs (the dominant MFMA kernels), recorded on
+    the stream they are launched on, inside the timed region."""
+
+    def __init__(self):
+        self.events = []
+        self.flops = []
+        self.active = False
+
+    def install(self):
+        from c2dsr_amd import losshead, ops
+        orig = ops.gemm
+        timer = self
+
+        def timed_gemm(A, B, C, *, M, N, K, **kw):
+            big = timer.active and M * N * K >= (1 << 33)
+            if big:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            out = orig(A, B, C, M=M, N=N, K=K, **kw)
+            if big:
+                e1.record()
+                timer.events.append((e0, e1))
+                timer.flops.append(2.0 * M * N * K)
+            return out
+
+        losshead.gemm = timed_gemm
+
+    def summary(self):
+        if not self.events:
+            return None
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in self.events]
+        tot_ms = sum(ms)
+        tot_fl = sum(self.flops)
+        return dict(launches=len(ms), avg_ms=tot_ms / len(ms), tflops=tot_fl / (tot_ms * 1e-3) / 1e12,
+                    flop_per_launch=tot_fl / len(ms))
+
+
+def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
+    """The oracle (CPU fp32 restatement, oracle/c2dsr_oracle.py) on a bounded sample of the same
+    workload: same item tables, d, L; a small batch for a few steps."""
+    sys.path.insert(0, ROOT)
+    from oracle import c2dsr_oracle as O
+    from c2dsr_amd.models.C2DSR import C2DSR
+    threads = os.cpu_count() or 1
+    threads = min(threads, 16)
+    torch.set_num_threads(threads)
+    args = make_args(cfg, torch.device('cpu'), 'fp32')
+    torch.manual_seed(0)
+    model = C2DSR(args, gs, gp)
+    params = {n: p.detach().clone() for n, p in model.named_parameters()}
+    graphs = {}
+    for k, g in (('share', gs), ('specific', gp)):
+        r, c, v = g.coo()
+        graphs[k] = (torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v))
+    ocfg = O.cfg_from_args(args)
+    tr = O.OracleTrainer(params, graphs, ocfg, seed=3407)
+    Bs = 64
+    done = 0
+    t0 = None
+    steps = 0
+    while True:
+        lo = (steps * Bs) % max(1, rows[0].shape[0] - Bs)
+        b = tuple(torch.from_numpy(r[lo:lo + Bs].copy()) for r in rows)
+        if steps == 1:
+            t0 = time.time()  # first step is warm-up
+        tr.train_batch(b)
+        steps += 1
+        if steps > 1:
+            done += Bs
+            if time.time() - t0 > budget_s or steps >= 6:
+                break
+    el = time.time() - t0
+    return dict(value=round(done / el, 3), unit='train sequences/sec', cores=threads, kind='port',
+                sample=f'oracle (torch-CPU fp32 restatement) train step, {cfg["label"]}, d={cfg["d"]}, '
+                       f'L={cfg["L"]}, batch {Bs}, {steps - 1} timed steps, dropout 0.2')
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', default='mb', choices=list(CONFIGS))
+    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--batch', type=int, default=0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-budget', type=float, default=20.0)
+    opt = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+    cfg = dict(CONFIGS[opt.config])
+    if opt.batch:
+        cfg['B'] = opt.batch
+    B = cfg['B']
+    n_batches = opt.steps + opt.warmup
+    t_prep = time.time()
+    # enough distinct sequences for every step's batch (>= 20*B per the survey's generator spec)
+    rows, gs, gp = make_workload(cfg, max(20 * B, n_batches * B * 13 // 10) if opt.config != 'tiny' else 4 * B,
+                                 seed=1)
+    n_rows = rows[0].shape[0]
+    log(f'[bench] {cfg["label"]}: {n_rows} train sequences, graph nnz {gs.nnz}/{gp.nnz}, '
+        f'prep {time.time() - t_prep:.1f}s')
+
+    from c2dsr_amd.trainer import Trainer
+    args = make_args(cfg, device, opt.precision)
+    torch.manual_seed(3407)
+    tr = Trainer(args, None, data=(None, None, None), graphs=(gs, gp))
+    tr.dp_split = False  # weak scaling: each rank its own batch
+    batches = []
+    for i in range(n_batches):
+        lo = ((i * world + rank) * B) % max(1, n_rows - B)
+        batches.append(tuple(torch.from_numpy(r[lo:lo + B].copy()).to(device) for r in rows))
+    timer = KernelTimer()
+    timer.install()
+    tr.model.train()
+    tr.optimizer.zero_grad()
+
+    def step(b):
+        tr.model.convolve_graph()
+        return tr.train_batch(b, global_rows=B * world)
+
+    for i in range(opt.warmup):
+        step(batches[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    timer.active = True
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for i in range(opt.steps):
+        last = step(batches[opt.warmup + i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    timer.active = False
+    if world > 1:
+        t = torch.tensor([el], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    loss = float(last[0])
+    ks = timer.summary()
+    ms = el / opt.steps * 1e3
+    value = B * world * opt.steps / el
+    if rank == 0:
+        peak = PEAK_BF16_TFLOPS if opt.precision == 'bf16' else PEAK_FP32_TFLOPS
+        roof = None
+        if ks is not None:
+            roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
+                        frac=round(ks['tflops'] / peak, 4), traffic=None,
+                        kernel='c2dsr gemm_kernel (classifier-head logits / dH / dW, K5)',
+                        avg_launch_ms=round(ks['avg_ms'], 4), flop_per_launch=ks['flop_per_launch'],
+                        launches=ks['launches'])
+        cpu = None
+        if world == 1 and not opt.no_cpu_baseline:
+            cpu = cpu_baseline(cfg, rows, gs, gp, opt.cpu_budget)
+        out = {'metric': 'train sequences/sec at d=256, seq_len=50, |items|~100k',
+               'value': round(value, 2), 'unit': 'train sequences/sec', 'n_gpus': world, 'steps': opt.steps,
+               'warmup': opt.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+               'vs_baseline': None, 'dtype': opt.precision, 'data': 'synthetic (Zipf two-domain sequences)',
+               'config': {'workload': f'{opt.config}: {cfg["label"]}', 'n_item_a': cfg['n_a'], 'n_item_b': cfg['n_b'],
+                          'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B, 'global_batch': B * world,
+                          'len_rec': 10, 'dropout': 0.2, 'parallelism': f'dp{world}'},
+               'loss': round(loss, 5) if math.isfinite(loss) else None,
+               'roofline': roof, 'cpu_baseline': cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -166,13 +166,13 @@ def test_train_step_with_dropout_matches_oracle(norm_first, n_head, n_gnn):
         with torch.no_grad():
             orc.opt.step(orc.P, orc.grads)
         for n, p in tr.model.named_parameters():
-            if n in orc.P:
+            if n in orc.names:
                 g = orc.grads[n]
                 sig = g.abs() > 1e-3 * g.abs().max()
                 assert rel(p.detach().cpu()[sig], orc.P[n][sig]) < TOL, (s, n)
         with torch.no_grad():  # re-sync (sign noise of ~zero grads)
             for n, p in tr.model.named_parameters():
-                if n in orc.P:
+                if n in orc.names:
                     p.copy_(orc.P[n].to(DEV))
         orc.step_no = tr.model.state.step + 1
 
