@@ -215,33 +215,52 @@ __global__ __launch_bounds__(256) void seg_reduce_a(const uint32_t* __restrict__
   }
 }
 
-// pass B: runs that start in chunk c and continue: sum tail[c] + head[c+1] + ... in order.
+// pass B: runs that start in chunk c and continue: out[key] += tail[c] + head[c+1] + ... .
+// One block per chunk; the run's partials are dealt round-robin to the block's lane
+// groups and the group sums are added in group order (fixed order → deterministic).
 template <int LPR>
 __global__ __launch_bounds__(256) void seg_reduce_b(const uint32_t* __restrict__ K, int n, int d,
                                                     float* __restrict__ out, const float* __restrict__ part_head,
                                                     const float* __restrict__ part_tail, int skip_key) {
   constexpr int GROUPS = 256 / LPR;
+  __shared__ int s_np;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [GROUPS][d]
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
-  const long chunk = (long)blockIdx.x * GROUPS + g;
+  const long chunk = blockIdx.x;
   const long start = chunk * SEG_CH;
-  if (start >= n) return;
   const long end = min((long)n, start + SEG_CH);
   const uint32_t key = K[end - 1];
   const bool continues = end < n && K[end] == key;
   const bool whole_cont = K[start] == key && start > 0 && K[start - 1] == key;
-  if (!continues || whole_cont || (int)key == skip_key) return;
-  for (int c = lane * 4; c < d; c += LPR * 4) {
-    float4 acc = *(const float4*)(part_tail + chunk * d + c);
+  if (!continues || whole_cont || (int)key == skip_key) return;  // uniform over the block
+  if (threadIdx.x == 0) {
     long k = chunk + 1;
     while (true) {
-      acc = acc + *(const float4*)(part_head + k * d + c);
       const long ek = min((long)n, (k + 1) * SEG_CH);
       if (!(ek < n && K[ek] == key)) break;
       ++k;
     }
-    float4* o = (float4*)(out + (long)key * d + c);
-    *o = *o + acc;
+    s_np = (int)(k - chunk + 1);  // tail of c + heads of c+1..k
+  }
+  __syncthreads();
+  const int np = s_np;
+  for (int c = lane * 4; c < d; c += LPR * 4) {
+    float4 acc = c2::f4(0.f);
+    for (int q = g; q < np; q += GROUPS) {
+      const float* src = q == 0 ? part_tail + chunk * d : part_head + (chunk + q) * d;
+      acc = acc + *(const float4*)(src + c);
+    }
+    *(float4*)(red + g * d + c) = acc;
+  }
+  __syncthreads();
+  if (g == 0) {
+    for (int c = lane * 4; c < d; c += LPR * 4) {
+      float4 t = *(const float4*)(red + c);
+      for (int q = 1; q < GROUPS; ++q) t = t + *(const float4*)(red + q * d + c);
+      float4* o = (float4*)(out + (long)key * d + c);
+      *o = *o + t;
+    }
   }
 }
 
@@ -321,7 +340,7 @@ void seg_launch(const SortWs& w, int n, const RowSrc& src, float* out, int skip_
   const int nchunks = c2::ceil_div(n, SEG_CH);
   dim3 grid(c2::ceil_div(nchunks, GROUPS));
   seg_reduce_a<LPR><<<grid, 256, 0, s>>>(w.k0, w.v0, n, src, out, w.ph, w.pt, skip_key);
-  seg_reduce_b<LPR><<<grid, 256, 0, s>>>(w.k0, n, src.d, out, w.ph, w.pt, skip_key);
+  seg_reduce_b<LPR><<<nchunks, 256, (size_t)GROUPS * src.d * 4, s>>>(w.k0, n, src.d, out, w.ph, w.pt, skip_key);
 }
 
 void seg_dispatch(const SortWs& w, int n, const RowSrc& src, float* out, int skip_key, hipStream_t s) {

@@ -3,38 +3,68 @@
 // Replaces models/encoders.py:42-48 (F.dropout + torch.spmm + stack/mean) as called
 // by models/C2DSR.py:59-62, and its autograd backward.
 //
-//   Y[i] = alpha * Σ_e val[e] * (Min ⊙ X)[col[e]]   (mask on the gathered row:  forward)
-//   Y[i] = alpha * Mout_i ⊙ Σ_e val[e] * X[col[e]]  (mask on the output row: backward, A^T CSR)
-//        + (beta + (i != pad_row ? delta : 0)) * Z[i] + gamma * Y[i]
-//   Y2[i] = Σ_e ...   (raw propagation, optional: next GCN layer's input)
+//   P[i]  = Σ_e val[e] * (Min ⊙ X)[col[e]]          (mask on the gathered row:  forward)
+//   P[i]  = Mout_i ⊙ Σ_e val[e] * X[col[e]]          (mask on the output row:    backward, CSR of Aᵀ)
+//   Y[i]  = alpha * P[i] + (beta + (i != pad_row ? delta : 0)) * Z[i] + gamma * Y[i]
+//   Y2[i] = P[i]   (optional: the next GCN layer's input)
 //
-// Layout: one row of d fp32 per "row group" of LPR lanes, each lane a float4
-// column slice (d <= 4*LPR per pass, looped for larger d).  Rows are dealt to
-// row groups in order; the gather of neighbour rows is the HBM/Infinity-cache
-// bound part (bytes per row: (2 + nnz_i) * d * 4 + 8 nnz_i).
+// Load balance: item popularity is Zipf-like, so a few rows hold a large share of
+// the edges.  The host splits every row into pieces of at most SPLIT edges (a
+// static "work" list built once per graph, c2dsr_amd/graph.py); a piece of an
+// unsplit row runs the full epilogue, pieces of split rows write raw partial sums
+// to a scratch slab that a second pass adds up in piece order (deterministic).
+// One work item per group of LPR lanes, float4 per lane (d <= 4*LPR per pass).
 #include "common.h"
 
 namespace {
 
+struct Epi {
+  float alpha;
+  const float* Z;
+  float beta, delta;
+  int pad_row;
+  float gamma;
+  float* Y;
+  float* Y2;
+  c2::Drop drop;
+};
+
+template <bool MASK_OUT>
+__device__ __forceinline__ void epilogue(float4 acc, long row, int c, int d, const Epi& ep) {
+  if (MASK_OUT && ep.drop.active()) {
+    const uint64_t b = (uint64_t)row * d + c;
+    acc = acc * make_float4(ep.drop.mul(b), ep.drop.mul(b + 1), ep.drop.mul(b + 2), ep.drop.mul(b + 3));
+  }
+  if (ep.Y2) *(float4*)(ep.Y2 + row * d + c) = acc;
+  float4 y = ep.alpha * acc;
+  if (ep.Z) {
+    const float zc = ep.beta + (row != ep.pad_row ? ep.delta : 0.f);
+    y = c2::fma4(zc, *(const float4*)(ep.Z + row * d + c), y);
+  }
+  if (ep.gamma != 0.f) y = c2::fma4(ep.gamma, *(const float4*)(ep.Y + row * d + c), y);
+  *(float4*)(ep.Y + row * d + c) = y;
+}
+
+// work[w] = {row, e_begin, e_end, slot}; slot < 0: whole row (epilogue), else partial slab index.
 template <int LPR, bool MASK_OUT>
-__global__ __launch_bounds__(256) void spmm_kernel(const int* __restrict__ rowptr, const int* __restrict__ col,
-                                                   const float* __restrict__ val, int n_rows, int d,
-                                                   const float* __restrict__ X, c2::Drop drop, float alpha,
-                                                   const float* __restrict__ Z, float beta, float delta,
-                                                   int pad_row, float gamma, float* __restrict__ Y,
-                                                   float* __restrict__ Y2) {
+__global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work, int n_work,
+                                                   const int* __restrict__ col, const float* __restrict__ val, int d,
+                                                   const float* __restrict__ X, Epi ep, float* __restrict__ part) {
   constexpr int GROUPS = 256 / LPR;
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
-  const long row = (long)blockIdx.x * GROUPS + g;
-  if (row >= n_rows) return;
-  const int e0 = rowptr[row], e1 = rowptr[row + 1];
+  const long w = (long)blockIdx.x * GROUPS + g;
+  if (w >= n_work) return;
+  const int4 wk = work[w];
+  const long row = wk.x;
+  const int e0 = wk.y, e1 = wk.z, slot = wk.w;
+  const c2::Drop& drop = ep.drop;
   for (int c = lane * 4; c < d; c += LPR * 4) {
     float4 acc = c2::f4(0.f);
     int e = e0;
     for (; e + 3 < e1; e += 4) {
-      int j0 = col[e], j1 = col[e + 1], j2 = col[e + 2], j3 = col[e + 3];
-      float v0 = val[e], v1 = val[e + 1], v2 = val[e + 2], v3 = val[e + 3];
+      const int j0 = col[e], j1 = col[e + 1], j2 = col[e + 2], j3 = col[e + 3];
+      const float v0 = val[e], v1 = val[e + 1], v2 = val[e + 2], v3 = val[e + 3];
       float4 x0 = *(const float4*)(X + (long)j0 * d + c);
       float4 x1 = *(const float4*)(X + (long)j1 * d + c);
       float4 x2 = *(const float4*)(X + (long)j2 * d + c);
@@ -53,7 +83,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int* __restrict__ rowpt
       acc = c2::fma4(v3, x3, acc);
     }
     for (; e < e1; ++e) {
-      int j = col[e];
+      const int j = col[e];
       float4 x = *(const float4*)(X + (long)j * d + c);
       if (!MASK_OUT && drop.active()) {
         const uint64_t b = (uint64_t)j * d + c;
@@ -61,48 +91,63 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int* __restrict__ rowpt
       }
       acc = c2::fma4(val[e], x, acc);
     }
-    if (MASK_OUT && drop.active()) {
-      const uint64_t b = (uint64_t)row * d + c;
-      acc = acc * make_float4(drop.mul(b), drop.mul(b + 1), drop.mul(b + 2), drop.mul(b + 3));
-    }
-    if (Y2) *(float4*)(Y2 + row * d + c) = acc;
-    float4 y = alpha * acc;
-    if (Z) {
-      const float zc = beta + (row != pad_row ? delta : 0.f);
-      y = c2::fma4(zc, *(const float4*)(Z + row * d + c), y);
-    }
-    if (gamma != 0.f) y = c2::fma4(gamma, *(const float4*)(Y + row * d + c), y);
-    *(float4*)(Y + row * d + c) = y;
+    if (slot >= 0)
+      *(float4*)(part + (long)slot * d + c) = acc;
+    else
+      epilogue<MASK_OUT>(acc, row, c, d, ep);
   }
 }
 
-template <bool MASK_OUT>
-int launch_spmm(const int* rowptr, const int* col, const float* val, int n_rows, int d, const float* X, c2::Drop dr,
-                float alpha, const float* Z, float beta, float delta, int pad_row, float gamma, float* Y, float* Y2,
-                hipStream_t s) {
-  if (d % 4) return (int)hipErrorInvalidValue;
-  int lpr = d / 4 >= 64 ? 64 : (d / 4 >= 32 ? 32 : (d / 4 >= 16 ? 16 : (d / 4 >= 8 ? 8 : 4)));
-  int groups = 256 / lpr;
-  dim3 grid(c2::ceil_div(n_rows, groups));
-  switch (lpr) {
-    case 64: spmm_kernel<64, MASK_OUT><<<grid, 256, 0, s>>>(rowptr, col, val, n_rows, d, X, dr, alpha, Z, beta, delta, pad_row, gamma, Y, Y2); break;
-    case 32: spmm_kernel<32, MASK_OUT><<<grid, 256, 0, s>>>(rowptr, col, val, n_rows, d, X, dr, alpha, Z, beta, delta, pad_row, gamma, Y, Y2); break;
-    case 16: spmm_kernel<16, MASK_OUT><<<grid, 256, 0, s>>>(rowptr, col, val, n_rows, d, X, dr, alpha, Z, beta, delta, pad_row, gamma, Y, Y2); break;
-    case 8: spmm_kernel<8, MASK_OUT><<<grid, 256, 0, s>>>(rowptr, col, val, n_rows, d, X, dr, alpha, Z, beta, delta, pad_row, gamma, Y, Y2); break;
-    default: spmm_kernel<4, MASK_OUT><<<grid, 256, 0, s>>>(rowptr, col, val, n_rows, d, X, dr, alpha, Z, beta, delta, pad_row, gamma, Y, Y2); break;
+// split[s] = {row, slot_begin, slot_end}: sum the row's pieces in order, then the epilogue.
+template <int LPR, bool MASK_OUT>
+__global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ split, int n_split, int d, Epi ep,
+                                                      const float* __restrict__ part) {
+  constexpr int GROUPS = 256 / LPR;
+  const int g = threadIdx.x / LPR;
+  const int lane = threadIdx.x % LPR;
+  const long s = (long)blockIdx.x * GROUPS + g;
+  if (s >= n_split) return;
+  const int4 sp = split[s];
+  for (int c = lane * 4; c < d; c += LPR * 4) {
+    float4 acc = c2::f4(0.f);
+    for (int k = sp.y; k < sp.z; ++k) acc = acc + *(const float4*)(part + (long)k * d + c);
+    epilogue<MASK_OUT>(acc, sp.x, c, d, ep);
   }
+}
+
+int lpr_for(int d) { return d / 4 >= 64 ? 64 : (d / 4 >= 32 ? 32 : (d / 4 >= 16 ? 16 : (d / 4 >= 8 ? 8 : 4))); }
+
+template <bool MASK_OUT>
+int launch(const int4* work, int n_work, const int4* split, int n_split, const int* col, const float* val, int d,
+           const float* X, const Epi& ep, float* part, hipStream_t s) {
+  const int lpr = lpr_for(d);
+  const int groups = 256 / lpr;
+#define C2_SPMM(L)                                                                                              \
+  spmm_kernel<L, MASK_OUT><<<c2::ceil_div(n_work, groups), 256, 0, s>>>(work, n_work, col, val, d, X, ep, part); \
+  if (n_split > 0) combine_kernel<L, MASK_OUT><<<c2::ceil_div(n_split, groups), 256, 0, s>>>(split, n_split, d, ep, part);
+  switch (lpr) {
+    case 64: C2_SPMM(64) break;
+    case 32: C2_SPMM(32) break;
+    case 16: C2_SPMM(16) break;
+    case 8: C2_SPMM(8) break;
+    default: C2_SPMM(4) break;
+  }
+#undef C2_SPMM
   C2_CHECK_LAUNCH();
   return 0;
 }
 
 }  // namespace
 
-C2_API int c2dsr_gcn_spmm(const int* rowptr, const int* col, const float* val, int n_rows, int d, const float* X,
-                          uint32_t k0, uint32_t k1, float p, int mask_on_output, float alpha, const float* Z,
-                          float beta, float delta, int pad_row, float gamma, float* Y, float* Y2, void* stream) {
-  c2::Drop dr = c2::make_drop(k0, k1, p);
+C2_API int c2dsr_gcn_spmm(const int* work, int n_work, const int* split, int n_split, float* part, const int* col,
+                          const float* val, int d, const float* X, uint32_t k0, uint32_t k1, float p,
+                          int mask_on_output, float alpha, const float* Z, float beta, float delta, int pad_row,
+                          float gamma, float* Y, float* Y2, void* stream) {
+  if (d % 4) return (int)hipErrorInvalidValue;
+  if (n_work == 0) return 0;
+  Epi ep{alpha, Z, beta, delta, pad_row, gamma, Y, Y2, c2::make_drop(k0, k1, p)};
   hipStream_t s = (hipStream_t)stream;
   if (mask_on_output)
-    return launch_spmm<true>(rowptr, col, val, n_rows, d, X, dr, alpha, Z, beta, delta, pad_row, gamma, Y, Y2, s);
-  return launch_spmm<false>(rowptr, col, val, n_rows, d, X, dr, alpha, Z, beta, delta, pad_row, gamma, Y, Y2, s);
+    return launch<true>((const int4*)work, n_work, (const int4*)split, n_split, col, val, d, X, ep, part, s);
+  return launch<false>((const int4*)work, n_work, (const int4*)split, n_split, col, val, d, X, ep, part, s);
 }

@@ -211,21 +211,35 @@ __global__ void scale_kernel(float* __restrict__ C, int M, int N, int ldc, float
   C[(long)r * ldc + c] = beta == 0.f ? 0.f : beta * C[(long)r * ldc + c];
 }
 
-// colsum: out[n] = beta*out[n] + alpha * Σ_m X[m*ldx + n]  (bias gradients)
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, int M, int N, int ldx, float alpha,
-                                                     float beta, float* __restrict__ out) {
-  __shared__ float part[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < N)
-    for (int m = w; m < M; m += 4) s += X[(long)m * ldx + c];
-  part[w][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (w == 0 && c < N) {
-    float t = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
-    out[c] = (beta == 0.f ? 0.f : beta * out[c]) + alpha * t;
+// colsum: out[n] = beta*out[n] + alpha * Σ_m X[m*ldx + n]  (bias gradients).
+// Stage 1: chunks of CS_ROWS rows x 256 columns per block, one column per thread
+// (coalesced row reads) → part[chunk][n]; stage 2 sums the chunks in order.
+constexpr int CS_ROWS = 128;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ X, int M, int N, long ldx,
+                                                          float* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int chunk = blockIdx.y;
+  if (c >= N) return;
+  const int r0 = chunk * CS_ROWS, r1 = min(M, r0 + CS_ROWS);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int r = r0;
+  for (; r + 3 < r1; r += 4) {
+    s0 += X[(long)r * ldx + c];
+    s1 += X[(long)(r + 1) * ldx + c];
+    s2 += X[(long)(r + 2) * ldx + c];
+    s3 += X[(long)(r + 3) * ldx + c];
   }
+  for (; r < r1; ++r) s0 += X[(long)r * ldx + c];
+  part[(long)chunk * N + c] = (s0 + s1) + (s2 + s3);
+}
+
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
+                                                           float alpha, float beta, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float t = 0.f;
+  for (int k = 0; k < chunks; ++k) t += part[(long)k * N + c];
+  out[c] = (beta == 0.f ? 0.f : beta * out[c]) + alpha * t;
 }
 
 template <bool BF16, bool TA, bool TB>
@@ -297,9 +311,21 @@ C2_API int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* 
   return 0;
 }
 
-C2_API int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* stream) {
+C2_API size_t c2dsr_colsum_workspace(int M, int N) {
+  return (size_t)c2::ceil_div(M, CS_ROWS) * (size_t)N * 4 + 256;
+}
+
+C2_API int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* workspace,
+                        void* stream) {
   if (N <= 0) return 0;
-  colsum_kernel<<<c2::ceil_div(N, 64), 256, 0, (hipStream_t)stream>>>(X, M, N, ldx, alpha, beta, out);
+  hipStream_t s = (hipStream_t)stream;
+  const int chunks = c2::ceil_div(M, CS_ROWS);
+  float* part = (float*)workspace;
+  if (chunks > 0) {
+    dim3 g1(c2::ceil_div(N, 256), chunks);
+    colsum_part_kernel<<<g1, 256, 0, s>>>(X, M, N, ldx, part);
+  }
+  colsum_final_kernel<<<c2::ceil_div(N, 256), 256, 0, s>>>(part, chunks, N, alpha, beta, out);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -149,15 +149,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
-__global__ void reduce_parts_kernel(const float* __restrict__ part, int nblk, int d, float* __restrict__ dgw,
-                                    float* __restrict__ dgb) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * d) return;
-  const int which = c / d, cc = c % d;
+// dgw/dgb += Σ_blocks part: 64 columns x 16 block-groups per workgroup, fixed-order combine
+__global__ __launch_bounds__(1024) void reduce_parts_kernel(const float* __restrict__ part, int nblk, int d,
+                                                            float* __restrict__ dgw, float* __restrict__ dgb) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[((long)b * 2 + which) * d + cc];
-  float* o = which ? dgb : dgw;
-  if (o) o[cc] += s;
+  if (c < 2 * d) {
+    const int which = c / d, cc = c % d;
+    for (int b = q; b < nblk; b += 16) s += part[((long)b * 2 + which) * d + cc];
+  }
+  red[q][cl] = s;
+  __syncthreads();
+  if (q == 0 && c < 2 * d) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    const int which = c / d, cc = c % d;
+    float* o = which ? dgb : dgw;
+    if (o) o[cc] += t;
+  }
 }
 
 __global__ void add_drop_kernel(const float* __restrict__ a, const float* __restrict__ b, long n4, int d,
@@ -241,7 +252,7 @@ C2_API int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, co
     default: C2_LNB(4); break;
   }
 #undef C2_LNB
-  if (dgw || dgb) reduce_parts_kernel<<<c2::ceil_div(2 * d, 256), 256, 0, s>>>(part, nblk, d, dgw, dgb);
+  if (dgw || dgb) reduce_parts_kernel<<<c2::ceil_div(2 * d, 64), 1024, 0, s>>>(part, nblk, d, dgw, dgb);
   C2_CHECK_LAUNCH();
   return 0;
 }

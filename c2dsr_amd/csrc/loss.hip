@@ -8,34 +8,39 @@
 
 namespace {
 
-// out[b,c] = Σ_l h[b,l,c] * gm[b,l] / Σ_l gm[b,l]      (trainer.py:85-89,101-108)
-__global__ void pool_fwd_kernel(const float* __restrict__ h, const int64_t* __restrict__ gm, int B, int L, int d,
+// w[b,l] = gm[b,l] / Σ_l gm[b,l]   (Trainer.cal_mask, trainer.py:85-89)
+__global__ void pool_weights_kernel(const int64_t* __restrict__ gm, int B, int L, float* __restrict__ w) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float S = 0.f;
+  for (int l = 0; l < L; ++l) S += (float)gm[(long)b * L + l];
+  for (int l = 0; l < L; ++l) w[(long)b * L + l] = (float)gm[(long)b * L + l] / S;
+}
+
+// out[b,c] = Σ_l h[b,l,c] * w[b,l]      (trainer.py:101-108)
+__global__ void pool_fwd_kernel(const float* __restrict__ h, const float* __restrict__ w, int B, int L, int d,
                                 float* __restrict__ out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)B * d) return;
   const int b = (int)(i / d), c = (int)(i % d);
-  float S = 0.f;
-  for (int l = 0; l < L; ++l) S += (float)gm[(long)b * L + l];
   float acc = 0.f;
-  for (int l = 0; l < L; ++l) {
-    const float w = (float)gm[(long)b * L + l] / S;
-    acc += h[((long)b * L + l) * d + c] * w;
-  }
+  for (int l = 0; l < L; ++l) acc += h[((long)b * L + l) * d + c] * w[(long)b * L + l];
   out[i] = acc;
 }
 
-// dh[b,l,c] += dout[b,c] * gm[b,l] / Σ gm[b,:]
-__global__ void pool_bwd_kernel(const float* __restrict__ dout, const int64_t* __restrict__ gm, int B, int L, int d,
+// dh[b,l,c] += dout[b,c] * w[b,l]   (float4 per thread)
+__global__ void pool_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ w, int B, int L, int d,
                                 float* __restrict__ dh) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)B * L * d) return;
-  const int c = (int)(i % d);
-  const long bl = i / d;
-  const int b = (int)(bl / L);
-  float S = 0.f;
-  for (int l = 0; l < L; ++l) S += (float)gm[(long)b * L + l];
-  const float w = (float)gm[bl] / S;
-  dh[i] += dout[(long)b * d + c] * w;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
+  if (i >= (long)B * L * d / 4) return;
+  const long e = i * 4;
+  const int c = (int)(e % d);
+  const long bl = e / d;
+  const long b = bl / L;
+  const float wt = w[bl];
+  const float4 g = *(const float4*)(dout + b * d + c);
+  float4* o = (float4*)(dh + e);
+  *o = c2::fma4(wt, g, *o);
 }
 
 // out[r*ldo] = Σ_c x[r*ldx + c] * y[r*ldy + c] + (bias ? bias[0] : 0); one wave per row
@@ -251,17 +256,23 @@ __global__ void rowscale_kernel(const float* __restrict__ x, const float* __rest
 
 }  // namespace
 
-C2_API int c2dsr_pool_fwd(const float* h, const int64_t* gm, int B, int L, int d, float* out, void* stream) {
-  const long n = (long)B * d;
-  if (n == 0) return 0;
-  pool_fwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(h, gm, B, L, d, out);
+C2_API int c2dsr_pool_weights(const int64_t* gm, int B, int L, float* w, void* stream) {
+  if (B == 0) return 0;
+  pool_weights_kernel<<<c2::ceil_div(B, 256), 256, 0, (hipStream_t)stream>>>(gm, B, L, w);
   C2_CHECK_LAUNCH();
   return 0;
 }
-C2_API int c2dsr_pool_bwd(const float* dout, const int64_t* gm, int B, int L, int d, float* dh, void* stream) {
-  const long n = (long)B * L * d;
+C2_API int c2dsr_pool_fwd(const float* h, const float* w, int B, int L, int d, float* out, void* stream) {
+  const long n = (long)B * d;
   if (n == 0) return 0;
-  pool_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dout, gm, B, L, d, dh);
+  pool_fwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(h, w, B, L, d, out);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_pool_bwd(const float* dout, const float* w, int B, int L, int d, float* dh, void* stream) {
+  const long n = (long)B * L * d / 4;
+  if (n == 0 || d % 4) return n == 0 ? 0 : (int)hipErrorInvalidValue;
+  pool_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dout, w, B, L, d, dh);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -106,8 +106,34 @@ def preprocess_graph(seqs_or_file, n_item_a: int, n_item: int) -> tuple[CSRGraph
     return normalized_csr(e_share, n_item), normalized_csr(e_spec, n_item)
 
 
+SPLIT = 64  # max edges per SpMM work item (Zipf-popular items are cut into pieces)
+
+
+def work_plan(g: CSRGraph, split: int = SPLIT):
+    """Static load-balancing plan of the SpMM kernel (include/c2dsr.h:c2dsr_gcn_spmm):
+    work [n_work, 4] = (row, e_begin, e_end, slot), split [n_split, 4] = (row, slot_b, slot_e, 0)."""
+    deg = np.diff(g.rowptr.astype(np.int64))
+    pieces = np.maximum(1, (deg + split - 1) // split)
+    n_work = int(pieces.sum())
+    row = np.repeat(np.arange(g.n, dtype=np.int64), pieces)
+    first = np.repeat(np.cumsum(pieces) - pieces, pieces)
+    k = np.arange(n_work, dtype=np.int64) - first  # piece index within its row
+    eb = g.rowptr[row].astype(np.int64) + k * split
+    ee = np.minimum(eb + split, g.rowptr[row + 1].astype(np.int64))
+    is_split = pieces[row] > 1
+    slot = np.full(n_work, -1, dtype=np.int64)
+    slot[is_split] = np.arange(int(is_split.sum()))
+    work = np.stack([row, eb, ee, slot], 1).astype(np.int32)
+    srows = np.nonzero(pieces > 1)[0]
+    sp = pieces[srows]
+    sb = np.cumsum(sp) - sp
+    split_arr = np.stack([srows, sb, sb + sp, np.zeros_like(srows)], 1).astype(np.int32)
+    return work, split_arr, int(is_split.sum())
+
+
 class DeviceGraph:
-    """CSR of A and of Aᵀ resident on the device (buffers owned by the model)."""
+    """CSR of A and of Aᵀ resident on the device (buffers owned by the model), with the
+    SpMM work plans of both."""
 
     def __init__(self, g: CSRGraph, device):
         self.n = g.n
@@ -116,7 +142,17 @@ class DeviceGraph:
         to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
         self.rowptr, self.col, self.val = to(g.rowptr), to(g.col), to(g.val)
         self.rowptr_t, self.col_t, self.val_t = to(t.rowptr), to(t.col), to(t.val)
+        w, s, nslot = work_plan(g)
+        wt, st, nslot_t = work_plan(t)
+        self.work, self.split, self.n_work, self.n_split, self.n_slots = to(w), to(s), len(w), len(s), nslot
+        self.work_t, self.split_t, self.n_work_t, self.n_split_t, self.n_slots_t = (to(wt), to(st), len(wt), len(st),
+                                                                                    nslot_t)
         self.host = g
+
+    def plan(self, transposed: bool):
+        if transposed:
+            return self.work_t, self.n_work_t, self.split_t, self.n_split_t, self.n_slots_t, self.col_t, self.val_t
+        return self.work, self.n_work, self.split, self.n_split, self.n_slots, self.col, self.val
 
     def to_torch_sparse(self):
         r, c, v = self.host.coo()

@@ -19,7 +19,7 @@ import torch
 from torch.autograd import Function
 
 from ._lib import lib, stream
-from .ops import FP32, _grad_target, gemm
+from .ops import FP32, _grad_target, colsum, gemm
 
 
 class LossMeta:
@@ -39,16 +39,20 @@ class LossHeadFn(Function):
         s = stream()
         f32 = dict(device=dev, dtype=torch.float32)
         # ---- pooling (6 vectors) ----
+        wa = torch.empty(B, L, **f32)
+        wb = torch.empty(B, L, **f32)
+        lib('c2dsr_pool_weights', m.gm_a, B, L, wa, s)
+        lib('c2dsr_pool_weights', m.gm_b, B, L, wb, s)
         Phx = torch.empty(B, d, **f32)
         Phy = torch.empty(B, d, **f32)
         X2a = torch.empty(2 * B, d, **f32)  # [h_share·wb ; h_neg_a·wa]
         X2b = torch.empty(2 * B, d, **f32)  # [h_share·wa ; h_neg_b·wb]
-        lib('c2dsr_pool_fwd', hx, m.gm_a, B, L, d, Phx, s)
-        lib('c2dsr_pool_fwd', hy, m.gm_b, B, L, d, Phy, s)
-        lib('c2dsr_pool_fwd', h_share, m.gm_b, B, L, d, X2a, s)
-        lib('c2dsr_pool_fwd', h_neg_a, m.gm_a, B, L, d, X2a[B:], s)
-        lib('c2dsr_pool_fwd', h_share, m.gm_a, B, L, d, X2b, s)
-        lib('c2dsr_pool_fwd', h_neg_b, m.gm_b, B, L, d, X2b[B:], s)
+        lib('c2dsr_pool_fwd', hx, wa, B, L, d, Phx, s)
+        lib('c2dsr_pool_fwd', hy, wb, B, L, d, Phy, s)
+        lib('c2dsr_pool_fwd', h_share, wb, B, L, d, X2a, s)
+        lib('c2dsr_pool_fwd', h_neg_a, wa, B, L, d, X2a[B:], s)
+        lib('c2dsr_pool_fwd', h_share, wa, B, L, d, X2b, s)
+        lib('c2dsr_pool_fwd', h_neg_b, wb, B, L, d, X2b[B:], s)
         # ---- bilinear: s = x1ᵀ W x2 (+b)  via  U = X2·Wᵀ, s = rowdot(x1, U) ----
         Ua = torch.empty(2 * B, d, **f32)
         Ub = torch.empty(2 * B, d, **f32)
@@ -90,6 +94,7 @@ class LossHeadFn(Function):
         lib('c2dsr_loss_finalize', vec, Bg * R, float(m.lam), out3, coefA, coefB, s)
         ctx.m, ctx.heads, ctx.coefs = m, heads, (coefA, coefB)
         ctx.mi = (Phx, Phy, X2a, X2b, Ua, Ub, dS)
+        ctx.w = (wa, wb)
         ctx.shape = (B, L, d)
         loss, loss_rec, loss_mi_o = out3[0], out3[1], out3[2]
         ctx.mark_non_differentiable(loss_rec, loss_mi_o)
@@ -125,11 +130,11 @@ class LossHeadFn(Function):
                 gemm(logits, Hcat, gW, M=n, N=d, K=2 * BR, transA=1, lda=ld, beta=1.0, precision=m.precision)
             gb = _grad_target(bias)
             if gb is not None:
-                lib('c2dsr_colsum', logits, 2 * BR, n, ld, 1.0, 1.0, gb, s)
+                colsum(logits, 2 * BR, n, ld, gb)
             if gwpad is not None:
                 gemm(logits[:, n:], Hpad, gwpad, M=1, N=d, K=2 * BR, transA=1, lda=ld, beta=1.0, precision=FP32)
             if gbpad is not None:
-                lib('c2dsr_colsum', logits[:, n:], 2 * BR, 1, ld, 1.0, 1.0, gbpad, s)
+                colsum(logits[:, n:], 2 * BR, 1, ld, gbpad)
             lib('c2dsr_rec_scatter', dHcat, dHpad, B, L, d, R, dh_share, hdom_grad, s)
         # ---- discriminators ----
         Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi
@@ -149,13 +154,14 @@ class LossHeadFn(Function):
                 gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
             gbd = _grad_target(bd)
             if gbd is not None:
-                lib('c2dsr_colsum', dS[k], 2 * B, 1, 1, 1.0, 1.0, gbd, s)
+                colsum(dS[k], 2 * B, 1, 1, gbd)
             dP[k] = (dx1, dX2)
         (dPhx, dX2a), (dPhy, dX2b) = dP[0], dP[2]
-        lib('c2dsr_pool_bwd', dPhx, m.gm_a, B, L, d, dhx, s)
-        lib('c2dsr_pool_bwd', dPhy, m.gm_b, B, L, d, dhy, s)
-        lib('c2dsr_pool_bwd', dX2a, m.gm_b, B, L, d, dh_share, s)
-        lib('c2dsr_pool_bwd', dX2a[B:], m.gm_a, B, L, d, dh_na, s)
-        lib('c2dsr_pool_bwd', dX2b, m.gm_a, B, L, d, dh_share, s)
-        lib('c2dsr_pool_bwd', dX2b[B:], m.gm_b, B, L, d, dh_nb, s)
+        wa, wb = ctx.w
+        lib('c2dsr_pool_bwd', dPhx, wa, B, L, d, dhx, s)
+        lib('c2dsr_pool_bwd', dPhy, wb, B, L, d, dhy, s)
+        lib('c2dsr_pool_bwd', dX2a, wb, B, L, d, dh_share, s)
+        lib('c2dsr_pool_bwd', dX2a[B:], wa, B, L, d, dh_na, s)
+        lib('c2dsr_pool_bwd', dX2b, wa, B, L, d, dh_share, s)
+        lib('c2dsr_pool_bwd', dX2b[B:], wb, B, L, d, dh_nb, s)
         return dh_share, dhx, dhy, dh_na, dh_nb, None

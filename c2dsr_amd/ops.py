@@ -48,6 +48,12 @@ def gemm(A, B, C, *, M, N, K, transA=0, transB=0, lda=None, ldb=None, ldc=None, 
     return C
 
 
+def colsum(X, M, N, ldx, out, alpha=1.0, beta=1.0):
+    """out[n] = beta·out[n] + alpha·Σ_m X[m·ldx + n]"""
+    ws = torch.empty(lib.raw('c2dsr_colsum_workspace')(M, N), dtype=torch.uint8, device=out.device)
+    lib('c2dsr_colsum', X, M, N, ldx, float(alpha), float(beta), out, ws, stream())
+
+
 class LinearFn(Function):
     """y = x·Wᵀ + b  [optionally drop(relu(.))]  — nn.Linear / TransformerEncoderLayer linear1, linear2,
     in_proj, out_proj (models/encoders.py:23-27 → torch transformer.py)."""
@@ -84,7 +90,7 @@ class LinearFn(Function):
             gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
         gb = _grad_target(ctx.b)
         if gb is not None:
-            lib('c2dsr_colsum', dy, M, N, N, 1.0, 1.0, gb, stream())
+            colsum(dy, M, N, N, gb)
         return dx, None, None, None, None
 
 
@@ -107,6 +113,15 @@ class GradSink:
         return self.G
 
 
+def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, pad_row, gamma, Y, Y2=None):
+    """Y = alpha·P + (beta + [i != pad]·delta)·Z + gamma·Y with P = A·drop(X) (or drop(Aᵀ·X)); see c2dsr_gcn_spmm."""
+    work, n_work, split, n_split, n_slots, col, val = graph.plan(transposed)
+    d = X.shape[1]
+    part = torch.empty(max(n_slots, 1), d, device=X.device, dtype=torch.float32)
+    lib('c2dsr_gcn_spmm', work, n_work, split, n_split, part, col, val, d, X, keys[0], keys[1], float(p),
+        int(mask_on_output), float(alpha), Z, float(beta), float(delta), int(pad_row), float(gamma), Y, Y2, stream())
+
+
 class GCNFn(Function):
     """H = mean(E, A·drop(E), A·drop(A·drop(E)), ...)  (models/encoders.py:42-48).
     Outputs (H, token): H is non-differentiable; the scalar token carries the
@@ -115,20 +130,15 @@ class GCNFn(Function):
     @staticmethod
     def forward(ctx, E, graph, n_gnn, p, keys, pad_row, sink):
         require_device(E)
-        N, d = E.shape
         out = torch.empty_like(E)
-        s = stream()
         inv = 1.0 / (n_gnn + 1)
         if n_gnn == 0:  # H = E
-            lib('c2dsr_gcn_spmm', graph.rowptr, graph.col, graph.val, N, d, E, 0, 0, 0.0, 0, 0.0, E, 1.0, 0.0, -1,
-                0.0, out, None, s)
+            spmm(graph, False, E, (0, 0), 0.0, 0, 0.0, E, 1.0, 0.0, -1, 0.0, out)
         h_prev = E
         for k in range(n_gnn):
-            last = k == n_gnn - 1
-            h_k = None if last else torch.empty_like(E)
-            k0, k1 = keys[k]
-            lib('c2dsr_gcn_spmm', graph.rowptr, graph.col, graph.val, N, d, h_prev, k0, k1, float(p), 0, inv,
-                E if k == 0 else None, inv, 0.0, -1, 0.0 if k == 0 else 1.0, out, h_k, s)
+            h_k = None if k == n_gnn - 1 else torch.empty_like(E)
+            spmm(graph, False, h_prev, keys[k], p, 0, inv, E if k == 0 else None, inv, 0.0, -1,
+                 0.0 if k == 0 else 1.0, out, h_k)
             h_prev = h_k
         ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
         ctx.E = E
@@ -142,28 +152,20 @@ class GCNFn(Function):
         E = ctx.E
         if G is None:
             return (None,) * 7
-        N, d = E.shape
         g = ctx.graph
         n = ctx.n_gnn
         inv = 1.0 / (n + 1)
-        s = stream()
         direct = E.grad is not None
         gE = E.grad if direct else torch.zeros_like(E)
-        if n == 0:
-            # H = E: gE += G (all rows) ... + direct lookup (rows != pad)
-            lib('c2dsr_gcn_spmm', g.rowptr_t, g.col_t, g.val_t, N, d, G, 0, 0, 0.0, 1, 0.0, G, 1.0, 1.0,
-                ctx.pad_row, 1.0, gE, None, s)
+        if n == 0:  # H = E: gE += G (all rows) + direct lookup (rows != pad)
+            spmm(g, True, G, (0, 0), 0.0, 1, 0.0, G, 1.0, 1.0, ctx.pad_row, 1.0, gE)
         else:
             X, alpha = G, inv
             for k in range(n, 1, -1):  # T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k
                 T = torch.empty_like(E)
-                k0, k1 = ctx.keys[k - 1]
-                lib('c2dsr_gcn_spmm', g.rowptr_t, g.col_t, g.val_t, N, d, X, k0, k1, float(ctx.p), 1, alpha, G, inv,
-                    0.0, -1, 0.0, T, None, s)
+                spmm(g, True, X, ctx.keys[k - 1], ctx.p, 1, alpha, G, inv, 0.0, -1, 0.0, T)
                 X, alpha = T, 1.0
-            k0, k1 = ctx.keys[0]
-            lib('c2dsr_gcn_spmm', g.rowptr_t, g.col_t, g.val_t, N, d, X, k0, k1, float(ctx.p), 1, alpha, G, inv, 1.0,
-                ctx.pad_row, 1.0, gE, None, s)
+            spmm(g, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 1.0, ctx.pad_row, 1.0, gE)
         ctx.sink.G = None
         return (None if direct else gE), None, None, None, None, None, None
 
@@ -352,5 +354,5 @@ class BilinearFn(Function):
             gemm(dU, x2, gW, M=d, N=d, K=B, transA=1, beta=1.0)
         gb = _grad_target(ctx.b)
         if gb is not None:
-            lib('c2dsr_colsum', ds, B, 1, 1, 1.0, 1.0, gb, s)
+            colsum(ds, B, 1, 1, gb)
         return dx1, dx2, None, None

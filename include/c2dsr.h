@@ -28,11 +28,14 @@ extern "C" {
 /* K1 GCN propagation, CSR SpMM with fused dropout / mean.
  * Replaces models/encoders.py:42-48 (F.dropout, torch.spmm, torch.stack(...).mean) as
  * called by models/C2DSR.py:59-62, and its backward (CSR of Aᵀ, mask_on_output=1).
- *   Y[i] = alpha·Σ_e val[e]·(Mask⊙X)[col[e]] + (beta + (i!=pad_row ? delta : 0))·Z[i] + gamma·Y[i]
- *   Y2[i] = Σ_e val[e]·(Mask⊙X)[col[e]]   (optional) */
-int c2dsr_gcn_spmm(const int* rowptr, const int* col, const float* val, int n_rows, int d, const float* X,
-                   uint32_t k0, uint32_t k1, float p, int mask_on_output, float alpha, const float* Z, float beta,
-                   float delta, int pad_row, float gamma, float* Y, float* Y2, void* stream);
+ *   P[i] = Σ_e val[e]·(Mask⊙X)[col[e]];  Y[i] = alpha·P[i] + (beta + (i!=pad_row ? delta : 0))·Z[i] + gamma·Y[i];
+ *   Y2[i] = P[i] (optional).
+ * work: int32 [n_work][4] = {row, e_begin, e_end, slot} (slot -1: whole row); split: int32
+ * [n_split][4] = {row, slot_begin, slot_end, 0} for rows cut into pieces; part: fp32 [n_slots][d]. */
+int c2dsr_gcn_spmm(const int* work, int n_work, const int* split, int n_split, float* part, const int* col,
+                   const float* val, int d, const float* X, uint32_t k0, uint32_t k1, float p, int mask_on_output,
+                   float alpha, const float* Z, float beta, float delta, int pad_row, float gamma, float* Y, float* Y2,
+                   void* stream);
 
 /* K2 embedding fuse.  Replaces models/C2DSR.py:65-71,81-82 + models/encoders.py:30-31:
  *   X[r] = drop((H[seq[r]] + E[seq[r]])·scale + P[pos[r]])      (Xin == NULL)
@@ -57,8 +60,10 @@ int c2dsr_embed_bwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, c
 int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
                float* C, int ldc, float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1,
                float p, int64_t row_base, int precision, int split_k, void* stream);
-/* out[n] = beta·out[n] + alpha·Σ_m X[m·ldx + n]   (bias gradients) */
-int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* stream);
+/* out[n] = beta·out[n] + alpha·Σ_m X[m·ldx + n]   (bias gradients; deterministic 2-stage) */
+size_t c2dsr_colsum_workspace(int M, int N);
+int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* workspace,
+                 void* stream);
 
 /* Attention core (SDPA math path with causal + inverted key-padding mask, Q1/Q2;
  * models/encoders.py:14,33).  qkv [B,L,3d], out [B,L,d], Psave [B,H,L,L]; L <= 128. */
@@ -82,8 +87,10 @@ int c2dsr_add_dropout(const float* a, const float* b, long n, int d, uint32_t k0
 int c2dsr_relu_drop_bwd(const float* dy, const float* y, long n, float p, float* dx, void* stream);
 
 /* Loss head (trainer.py:85-156). */
-int c2dsr_pool_fwd(const float* h, const int64_t* gm, int B, int L, int d, float* out, void* stream);
-int c2dsr_pool_bwd(const float* dout, const int64_t* gm, int B, int L, int d, float* dh, void* stream);
+/* w[b,l] = gm[b,l]/Σ_l gm[b,l] (cal_mask); out[b] = Σ_l h[b,l]·w[b,l]; dh[b,l] += dout[b]·w[b,l] */
+int c2dsr_pool_weights(const int64_t* gm, int B, int L, float* w, void* stream);
+int c2dsr_pool_fwd(const float* h, const float* w, int B, int L, int d, float* out, void* stream);
+int c2dsr_pool_bwd(const float* dout, const float* w, int B, int L, int d, float* dh, void* stream);
 int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int d, const float* bias, float* out,
                  long ldo, void* stream);
 /* loss_mi = Σ_k Σ_b BCE(s_k[b], y_k)/B_norm, ds = (σ(s)-y)/B_norm; s = [sim_a_pos; sim_a_neg; sim_b_pos; sim_b_neg] */

@@ -70,7 +70,9 @@ def test_gcn_fwd_bwd_vs_oracle(d, n_gnn, p):
     rng = np.random.default_rng(d + n_gnn)
     N = 700
     edges = rng.integers(0, N - 1, size=(5000, 2))
-    edges = np.concatenate([edges, edges[:300]])  # duplicates (counts > 1)
+    hub_out = np.stack([np.full(900, 3), rng.integers(0, N - 1, 900)], 1)  # row 3: 900 edges (split rows)
+    hub_in = np.stack([rng.integers(0, N - 1, 700), np.full(700, 5)], 1)   # col 5: a hub in Aᵀ
+    edges = np.concatenate([edges, edges[:300], hub_out, hub_in])  # duplicates (counts > 1)
     g = normalized_csr(edges, N)
     dg = DeviceGraph(g, DEV)
     E = torch.randn(N, d)
