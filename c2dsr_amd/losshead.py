@@ -19,7 +19,13 @@ import torch
 from torch.autograd import Function
 
 from ._lib import lib, stream
-from .ops import FP32, _grad_target, colsum, gemm
+from .ops import BF16, FP32, _grad_target, colsum, gemm
+
+
+def split_count(rows, tile, target_wgs=1024):
+    """number of work splits so that (row tiles × splits) ≈ target_wgs workgroups"""
+    tiles = max(1, -(-rows // tile))
+    return max(1, min(16, -(-target_wgs // tiles)))
 
 
 class LossMeta:
@@ -68,6 +74,8 @@ class LossHeadFn(Function):
         dS = torch.empty(4, B, **f32)
         lib('c2dsr_mi_loss', S, B, Bg, vec[8:], dS, s)
         # ---- classifier heads ----
+        fused = m.precision == BF16 and bool(lib.raw('c2dsr_ce_supported')(d))
+        ctx.fused = fused
         heads = []
         for (hdom, W, bias, t_share, t_spec, n) in ((hx, m.Wa, m.ba, m.gt_share_a, m.gt_a, m.n_a),
                                                    (hy, m.Wb, m.bb, m.gt_share_b, m.gt_b, m.n_b)):
@@ -76,14 +84,29 @@ class LossHeadFn(Function):
             lib('c2dsr_rec_gather', h_share, hdom, B, L, d, R, Hcat, Hpad, s)
             tcat = torch.empty(2 * BR, device=dev, dtype=torch.int64)
             lib('c2dsr_rec_targets', t_share, t_spec, B, L, R, tcat, s)
-            ld = n + 1
-            logits = torch.empty(2 * BR, ld, **f32)
-            gemm(Hcat, W, logits, M=2 * BR, N=n, K=d, transB=1, ldc=ld, bias=bias, precision=m.precision)
-            lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, 2 * BR, d, m.bpad, logits[:, n:], ld, s)
             lse = torch.empty(2 * BR, **f32)
             rows = torch.empty(2 * BR, **f32)
-            lib('c2dsr_ce_fwd', logits, ld, 2 * BR, ld, tcat, n, lse, rows, s)
-            heads.append((Hcat, Hpad, tcat, logits, lse, rows, W, bias, n))
+            if fused:
+                Hb = torch.empty(2 * BR, d, device=dev, dtype=torch.bfloat16)
+                Wb = torch.empty(n, d, device=dev, dtype=torch.bfloat16)
+                lib('c2dsr_f32_to_bf16', Hcat, Hcat.numel(), Hb, s)
+                lib('c2dsr_f32_to_bf16', W, W.numel(), Wb, s)
+                padlogit = torch.empty(2 * BR, **f32)
+                lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, 2 * BR, d, m.bpad, padlogit, 1, s)
+                ns = split_count(2 * BR, 256)
+                pm = torch.empty(ns, 2 * BR, **f32)
+                ps = torch.empty(ns, 2 * BR, **f32)
+                lse2 = torch.empty(2 * BR, **f32)
+                lib('c2dsr_ce_fused_fwd', Hb, Wb, bias, 2 * BR, n, d, ns, pm, ps, padlogit, tcat, Hcat, W, lse, lse2,
+                    rows, s)
+                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padlogit, lse2), lse, rows, W, bias, n))
+            else:
+                ld = n + 1
+                logits = torch.empty(2 * BR, ld, **f32)
+                gemm(Hcat, W, logits, M=2 * BR, N=n, K=d, transB=1, ldc=ld, bias=bias, precision=m.precision)
+                lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, 2 * BR, d, m.bpad, logits[:, n:], ld, s)
+                lib('c2dsr_ce_fwd', logits, ld, 2 * BR, ld, tcat, n, lse, rows, s)
+                heads.append((Hcat, Hpad, tcat, logits, lse, rows, W, bias, n))
         out3 = torch.empty(3, **f32)
         coefA = torch.empty(2, **f32)
         coefB = torch.empty(2, **f32)
@@ -119,22 +142,39 @@ class LossHeadFn(Function):
         gwpad, gbpad = _grad_target(m.wpad), _grad_target(m.bpad)
         for (Hcat, Hpad, tcat, logits, lse, rows, W, bias, n), coef, hdom_grad in zip(ctx.heads, ctx.coefs,
                                                                                       (dhx, dhy)):
-            ld = n + 1
-            lib('c2dsr_ce_bwd', logits, ld, 2 * BR, ld, tcat, n, lse, coef, BR, gscale, float(m.lam), s)
-            dHcat = torch.empty(2 * BR, d, **f32)
-            gemm(logits, W, dHcat, M=2 * BR, N=d, K=n, lda=ld, precision=m.precision)
-            dHpad = torch.zeros(2 * BR, d, **f32)
-            lib('c2dsr_outer_add', logits[:, n:], ld, m.wpad, 2 * BR, d, dHpad, d, s)
-            gW = _grad_target(W)
-            if gW is not None:
-                gemm(logits, Hcat, gW, M=n, N=d, K=2 * BR, transA=1, lda=ld, beta=1.0, precision=m.precision)
-            gb = _grad_target(bias)
-            if gb is not None:
-                colsum(logits, 2 * BR, n, ld, gb)
+            M2 = 2 * BR
+            dHcat = torch.empty(M2, d, **f32)
+            dHpad = torch.zeros(M2, d, **f32)
+            gW, gb = _grad_target(W), _grad_target(bias)
+            if ctx.fused:
+                Hb, Wb, padlogit, lse2 = logits
+                rw = torch.empty(M2, **f32)
+                dpad = torch.empty(M2, **f32)
+                lib('c2dsr_ce_row_weights', tcat, M2, n, coef, BR, gscale, float(m.lam), padlogit, lse, rw, dpad, s)
+                ns = split_count(M2, 128)
+                dHp = torch.empty(ns, M2, d, **f32)
+                lib('c2dsr_ce_fused_dh', Hb, Wb, bias, M2, n, d, ns, lse2, tcat, rw, dHp, dHcat, s)
+                del dHp
+                nr = split_count(n, 128)
+                dWp = torch.empty(nr, n, d, **f32)
+                dbp = torch.empty(nr, n, **f32)
+                lib('c2dsr_ce_fused_dw', Hb, Wb, bias, M2, n, d, nr, lse2, tcat, rw, dWp, dbp, gW, gb, s)
+                del dWp, dbp
+                pad_col, pad_ld = dpad, 1
+            else:
+                ld = n + 1
+                lib('c2dsr_ce_bwd', logits, ld, M2, ld, tcat, n, lse, coef, BR, gscale, float(m.lam), s)
+                gemm(logits, W, dHcat, M=M2, N=d, K=n, lda=ld, precision=m.precision)
+                if gW is not None:
+                    gemm(logits, Hcat, gW, M=n, N=d, K=M2, transA=1, lda=ld, beta=1.0, precision=m.precision)
+                if gb is not None:
+                    colsum(logits, M2, n, ld, gb)
+                pad_col, pad_ld = logits[:, n:], ld
+            lib('c2dsr_outer_add', pad_col, pad_ld, m.wpad, M2, d, dHpad, d, s)
             if gwpad is not None:
-                gemm(logits[:, n:], Hpad, gwpad, M=1, N=d, K=2 * BR, transA=1, lda=ld, beta=1.0, precision=FP32)
+                gemm(pad_col, Hpad, gwpad, M=1, N=d, K=M2, transA=1, lda=pad_ld, beta=1.0, precision=FP32)
             if gbpad is not None:
-                colsum(logits[:, n:], 2 * BR, 1, ld, gbpad)
+                colsum(pad_col, M2, 1, pad_ld, gbpad)
             lib('c2dsr_rec_scatter', dHcat, dHpad, B, L, d, R, dh_share, hdom_grad, s)
         # ---- discriminators ----
         Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi

@@ -114,6 +114,27 @@ int c2dsr_loss_finalize(const float* vec, int BR_global, float lam, float* out3,
 int c2dsr_scale_ds(float* ds, int n, const float* gscale, float f, void* stream);
 int c2dsr_rowscale(const float* x, const float* s, long n, int d, float* out, int accumulate, void* stream);
 
+/* K5 fused classifier head + cross-entropy (bf16 MFMA, logits never materialised; trainer.py:131-154).
+ * Hb [M][D], Wb [n][D] bf16 (D = 128 or 256); bias [n] fp32.  Forward: lse, lse2 = lse·log2e and
+ * loss_row over the n items + the pad column (padlogit), target logit from fp32 H/W. */
+int c2dsr_ce_supported(int D);
+int c2dsr_f32_to_bf16(const float* x, long n, void* y, void* stream);
+int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_split,
+                       float* part_m, float* part_s, const float* padlogit, const int64_t* tgt, const float* H,
+                       const float* W, float* lse, float* lse2, float* loss_row, void* stream);
+/* rw[r] = valid ? gscale·lam·coef[r >= split] : 0;  dpad[r] = exp(padlogit - lse)·rw */
+int c2dsr_ce_row_weights(const int64_t* tgt, int M, int ignore, const float* coef, int split, const float* gscale,
+                         float lam, const float* padlogit, const float* lse, float* rw, float* dpad, void* stream);
+/* dH[r] = Σ_c P'[r][c]·W[c], P' = (softmax - onehot)·rw  (dHp: [n_split][M][D] scratch) */
+int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_split,
+                      const float* lse2, const int64_t* tgt, const float* rw, float* dHp, float* dH, void* stream);
+/* gW[c] += Σ_r P'[r][c]·H[r];  gb[c] += Σ_r P'[r][c]  (dWp: [n_rsplit][n][D], dbp: [n_rsplit][n] scratch) */
+int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_rsplit,
+                      const float* lse2, const int64_t* tgt, const float* rw, float* dWp, float* dbp, float* gW,
+                      float* gb, void* stream);
+/* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */
+int c2dsr_selftest_tr(int rr0, int kb0, short* out, void* stream);
+
 /* K6 AdamW(amsgrad) over flat buffers, folding the fresh grad into the epoch accumulator
  * (trainer.py:21-22,42,158). */
 int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,

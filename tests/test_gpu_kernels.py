@@ -227,3 +227,73 @@ def test_adamw_kernel_vs_oracle():
         assert rel(pd, P['w']) < 1e-6
         assert float(fresh.abs().max()) == 0.0
         assert rel(accum, acc_ref) < 1e-7
+
+
+def test_transposed_lds_fragment_addressing():
+    """ds_read_b64_tr_b16 + swizzled image: the fragment layout the fused CE kernels rely on."""
+    from c2dsr_amd._lib import lib, stream
+    for rr0, kb0 in ((0, 0), (16, 32), (32, 128), (48, 224)):
+        out = torch.zeros(1024, dtype=torch.int16, device=DEV)
+        lib('c2dsr_selftest_tr', rr0, kb0, out, stream())
+        got = out.cpu().numpy().astype(np.int64)
+        for lane in range(64):
+            h = lane >> 5
+            for j in range(8):
+                row = rr0 + 8 * (j >> 2) + 4 * h + (j & 3)
+                assert got[lane * 8 + j] == row * 256 + kb0 + (lane & 31), (rr0, kb0, lane, j)
+                rrow = rr0 + (lane & 31)
+                assert got[512 + lane * 8 + j] == rrow * 256 + kb0 + 8 * h + j, ('row', rr0, kb0, lane, j)
+
+
+def _bf16(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+@pytest.mark.parametrize('M,n,D', [(300, 700, 256), (1000, 2100, 128), (64, 65, 256)])
+def test_fused_linear_ce_vs_reference(M, n, D):
+    """K5 fused head (bf16 MFMA) vs a float64 CPU computation of the same op on the same bf16-rounded
+    operands: lse rel 2e-5; gradients (P' rounded to bf16 for the 2nd product) rel 1e-2 of max."""
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(M + n)
+    H = _bf16(torch.randn(M, D, generator=g) * 0.5)
+    W = _bf16(torch.randn(n, D, generator=g) * 0.5)
+    b = torch.randn(n, generator=g) * 0.1
+    pl = torch.randn(M, generator=g)
+    t = torch.randint(0, n + 1, (M,), generator=g)
+    t[:5] = n  # ignored rows
+    BR = M // 2
+    coef = torch.tensor([0.37, 1.9])
+    gs = torch.tensor([1.0])
+    lam = 0.7
+    s = stream()
+    d = lambda x: x.to(DEV)  # noqa: E731
+    Hb, Wb = d(H.to(torch.bfloat16)), d(W.to(torch.bfloat16))
+    ns, nr = 3, 2
+    pm, ps = torch.empty(ns, M, device=DEV), torch.empty(ns, M, device=DEV)
+    lse, lse2, rows = (torch.empty(M, device=DEV) for _ in range(3))
+    lib('c2dsr_ce_fused_fwd', Hb, Wb, d(b), M, n, D, ns, pm, ps, d(pl), d(t), d(H), d(W), lse, lse2, rows, s)
+    # reference
+    lg = torch.cat([H.double() @ W.double().T + b.double(), pl.double()[:, None]], 1)
+    lse_r = torch.logsumexp(lg, 1)
+    valid = t != n
+    rows_r = torch.where(valid, lse_r - lg.gather(1, t[:, None])[:, 0], torch.zeros(M, dtype=torch.float64))
+    assert rel(lse, lse_r) < 2e-5
+    assert rel(rows, rows_r) < 1e-4
+    rw, dpad = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    lib('c2dsr_ce_row_weights', d(t), M, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, dpad, s)
+    w_r = torch.where(valid, lam * coef[(torch.arange(M) >= BR).long()].double(), torch.zeros(M, dtype=torch.float64))
+    P = torch.softmax(lg, 1)
+    oh = torch.zeros_like(P)
+    oh[torch.arange(M), t] = 1.0
+    dl = (P - oh) * w_r[:, None]
+    assert rel(rw, w_r) < 1e-6 and rel(dpad, dl[:, n]) < 1e-4
+    dH = torch.empty(M, D, device=DEV)
+    dHp = torch.empty(ns, M, D, device=DEV)
+    lib('c2dsr_ce_fused_dh', Hb, Wb, d(b), M, n, D, ns, lse2, d(t), rw, dHp, dH, s)
+    assert rel(dH, dl[:, :n] @ W.double()) < 1e-2
+    gW = torch.ones(n, D, device=DEV)
+    gb = torch.ones(n, device=DEV)
+    dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
+    lib('c2dsr_ce_fused_dw', Hb, Wb, d(b), M, n, D, nr, lse2, d(t), rw, dWp, dbp, gW, gb, s)
+    assert rel(gW - 1, dl[:, :n].T @ H.double()) < 1e-2
+    assert rel(gb - 1, dl[:, :n].sum(0)) < 1e-2
