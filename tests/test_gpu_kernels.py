@@ -242,7 +242,8 @@ def test_transposed_lds_fragment_addressing():
                 row = rr0 + 8 * (j >> 2) + 4 * h + (j & 3)
                 assert got[lane * 8 + j] == row * 256 + kb0 + (lane & 31), (rr0, kb0, lane, j)
                 rrow = rr0 + (lane & 31)
-                assert got[512 + lane * 8 + j] == rrow * 256 + kb0 + 8 * h + j, ('row', rr0, kb0, lane, j)
+                if rr0 + 31 < 64:
+                    assert got[512 + lane * 8 + j] == rrow * 256 + kb0 + 8 * h + j, ('row', rr0, kb0, lane, j)
 
 
 def _bf16(t):
