@@ -67,41 +67,41 @@ def make_args(cfg, device, precision, dropout=0.2):
 
 
 class KernelTimer:
-    """HIP-event timing of the classifier-head GEMMs (the dominant MFMA kernels), recorded on
-    the stream they are launched on, inside the timed region."""
+    """HIP-event timing (on the stream the kernel is launched on, inside the timed region) of the
+    dominant kernel: the fused classifier-head dW kernel (K5, c2dsr_ce_fused_dw) in bf16 mode, the
+    materialised-logits GEMMs otherwise.  Algorithmic FLOPs per launch = 2·M·n·d (the dW product;
+    the recomputed logits tile is overhead and not credited)."""
 
-    def __init__(self):
-        self.events = []
-        self.flops = []
-        self.active = False
+    def __init__(self, precision):
+        from c2dsr_amd._lib import lib
+        self.lib = lib
+        self.name = 'c2dsr_ce_fused_dw' if precision == 'bf16' else 'c2dsr_gemm'
 
-    def install(self):
-        from c2dsr_amd import losshead, ops
-        orig = ops.gemm
-        timer = self
+    def start(self):
+        self.lib.timed.clear()
+        self.lib.time_names.add(self.name)
 
-        def timed_gemm(A, B, C, *, M, N, K, **kw):
-            big = timer.active and M * N * K >= (1 << 33)
-            if big:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-            out = orig(A, B, C, M=M, N=N, K=K, **kw)
-            if big:
-                e1.record()
-                timer.events.append((e0, e1))
-                timer.flops.append(2.0 * M * N * K)
-            return out
-
-        losshead.gemm = timed_gemm
+    def stop(self):
+        self.lib.time_names.discard(self.name)
 
     def summary(self):
-        if not self.events:
-            return None
+        recs = self.lib.timed.get(self.name, [])
         torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) for a, b in self.events]
-        tot_ms = sum(ms)
-        tot_fl = sum(self.flops)
+        ms, fl = [], []
+        for e0, e1, a in recs:
+            if self.name == 'c2dsr_ce_fused_dw':
+                M, n, D = a[3], a[4], a[5]
+                f = 2.0 * M * n * D
+            else:
+                M, N, K = a[2], a[3], a[4]
+                f = 2.0 * M * N * K
+                if f < 1e11:  # only the classifier-head GEMMs
+                    continue
+            ms.append(e0.elapsed_time(e1))
+            fl.append(f)
+        if not ms:
+            return None
+        tot_ms, tot_fl = sum(ms), sum(fl)
         return dict(launches=len(ms), avg_ms=tot_ms / len(ms), tflops=tot_fl / (tot_ms * 1e-3) / 1e12,
                     flop_per_launch=tot_fl / len(ms))
 
@@ -187,8 +187,7 @@ def main():
     for i in range(n_batches):
         lo = ((i * world + rank) * B) % max(1, n_rows - B)
         batches.append(tuple(torch.from_numpy(r[lo:lo + B].copy()).to(device) for r in rows))
-    timer = KernelTimer()
-    timer.install()
+    timer = KernelTimer(opt.precision)
     tr.model.train()
     tr.optimizer.zero_grad()
 
@@ -201,7 +200,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.active = True
+    timer.start()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = None
@@ -211,12 +210,12 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    timer.active = False
+    timer.stop()
     if world > 1:
         t = torch.tensor([el], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
-    loss = float(last[0])
+    loss = float(last[0].detach())
     ks = timer.summary()
     ms = el / opt.steps * 1e3
     value = B * world * opt.steps / el
@@ -226,7 +225,8 @@ def main():
         if ks is not None:
             roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
                         frac=round(ks['tflops'] / peak, 4), traffic=None,
-                        kernel='c2dsr gemm_kernel (classifier-head logits / dH / dW, K5)',
+                        kernel=('ce_dw_kernel<256> (K5 fused classifier-head dW/db, bf16 MFMA)'
+                                if opt.precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
                         avg_launch_ms=round(ks['avg_ms'], 4), flop_per_launch=ks['flop_per_launch'],
                         launches=ks['launches'])
         cpu = None

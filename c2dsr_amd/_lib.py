@@ -59,6 +59,8 @@ class _Lib:
     def __init__(self):
         self._lib = None
         self._sigs = None
+        self.time_names = set()  # entry points bracketed by HIP events (bench.py roofline)
+        self.timed = {}
 
     def load(self):
         if self._lib is not None:
@@ -87,7 +89,14 @@ class _Lib:
                 conv.append(a.data_ptr())
             else:
                 conv.append(a)
-        rc = getattr(lib, name)(*conv)
+        if name in self.time_names:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = getattr(lib, name)(*conv)
+            e1.record()
+            self.timed.setdefault(name, []).append((e0, e1, conv))
+        else:
+            rc = getattr(lib, name)(*conv)
         if rc != 0:
             raise HipLibError(f'{name} failed with hipError {rc}')
         return rc

@@ -597,7 +597,7 @@ C2_API int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias, 
   return 0;
 }
 
-// gW [n][D] += Σ_r P'[r][c] H[r];  gb [n] += Σ_r P'[r][c].  dWp [n_rsplit][n][D], dbp [n_rsplit][n] scratch.
+// dWp[s][c] = Σ_{r in split s} P'[r][c] H[r];  dbp[s][c] = Σ_r P'[r][c]  (combine with c2dsr_sum_parts).
 C2_API int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_rsplit,
                              const float* lse2, const int64_t* tgt, const float* rw, float* dWp, float* dbp,
                              float* gW, float* gb, void* stream) {
@@ -607,9 +607,15 @@ C2_API int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias, 
   dim3 grid(c2::ceil_div(n, 128), n_rsplit);
   int e = launch_d(D, 2, grid, s, (const bf16*)Hb, (const bf16*)Wb, bias, M, n, per, dWp, dbp, lse2, tgt, rw);
   if (e) return e;
-  const long tot = (long)n * D;
-  if (gW) sum_parts_kernel<<<c2::ceil_div(tot, 256), 256, 0, s>>>(dWp, n_rsplit, tot, 1.f, gW);
-  if (gb) sum_parts_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(dbp, n_rsplit, n, 1.f, gb);
+  (void)gW;
+  (void)gb;
+  return 0;
+}
+
+// out[i] = beta*out[i] + Σ_s part[s][i]  (fixed order) — combines the split partials
+C2_API int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream) {
+  if (n == 0) return 0;
+  sum_parts_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(part, nparts, n, beta, out);
   C2_CHECK_LAUNCH();
   return 0;
 }

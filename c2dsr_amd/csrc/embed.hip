@@ -219,10 +219,10 @@ __global__ __launch_bounds__(256) void seg_reduce_a(const uint32_t* __restrict__
 // One block per chunk; the run's partials are dealt round-robin to the block's lane
 // groups and the group sums are added in group order (fixed order → deterministic).
 template <int LPR>
-__global__ __launch_bounds__(256) void seg_reduce_b(const uint32_t* __restrict__ K, int n, int d,
-                                                    float* __restrict__ out, const float* __restrict__ part_head,
-                                                    const float* __restrict__ part_tail, int skip_key) {
-  constexpr int GROUPS = 256 / LPR;
+__global__ __launch_bounds__(1024) void seg_reduce_b(const uint32_t* __restrict__ K, int n, int d,
+                                                     float* __restrict__ out, const float* __restrict__ part_head,
+                                                     const float* __restrict__ part_tail, int skip_key) {
+  constexpr int GROUPS = 1024 / LPR;
   __shared__ int s_np;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [GROUPS][d]
   const int g = threadIdx.x / LPR;
@@ -246,12 +246,18 @@ __global__ __launch_bounds__(256) void seg_reduce_b(const uint32_t* __restrict__
   __syncthreads();
   const int np = s_np;
   for (int c = lane * 4; c < d; c += LPR * 4) {
-    float4 acc = c2::f4(0.f);
-    for (int q = g; q < np; q += GROUPS) {
-      const float* src = q == 0 ? part_tail + chunk * d : part_head + (chunk + q) * d;
-      acc = acc + *(const float4*)(src + c);
+    float4 a0 = c2::f4(0.f), a1 = c2::f4(0.f);
+    int q = g;
+    for (; q + GROUPS < np; q += 2 * GROUPS) {
+      const float* s0 = q == 0 ? part_tail + chunk * d : part_head + (chunk + q) * d;
+      a0 = a0 + *(const float4*)(s0 + c);
+      a1 = a1 + *(const float4*)(part_head + (chunk + q + GROUPS) * d + c);
     }
-    *(float4*)(red + g * d + c) = acc;
+    if (q < np) {
+      const float* s0 = q == 0 ? part_tail + chunk * d : part_head + (chunk + q) * d;
+      a0 = a0 + *(const float4*)(s0 + c);
+    }
+    *(float4*)(red + g * d + c) = a0 + a1;
   }
   __syncthreads();
   if (g == 0) {
@@ -340,7 +346,7 @@ void seg_launch(const SortWs& w, int n, const RowSrc& src, float* out, int skip_
   const int nchunks = c2::ceil_div(n, SEG_CH);
   dim3 grid(c2::ceil_div(nchunks, GROUPS));
   seg_reduce_a<LPR><<<grid, 256, 0, s>>>(w.k0, w.v0, n, src, out, w.ph, w.pt, skip_key);
-  seg_reduce_b<LPR><<<nchunks, 256, (size_t)GROUPS * src.d * 4, s>>>(w.k0, n, src.d, out, w.ph, w.pt, skip_key);
+  seg_reduce_b<LPR><<<nchunks, 1024, (size_t)(1024 / LPR) * src.d * 4, s>>>(w.k0, n, src.d, out, w.ph, w.pt, skip_key);
 }
 
 void seg_dispatch(const SortWs& w, int n, const RowSrc& src, float* out, int skip_key, hipStream_t s) {

@@ -216,11 +216,11 @@ __global__ void scale_kernel(float* __restrict__ C, int M, int N, int ldc, float
 // (coalesced row reads) → part[chunk][n]; stage 2 sums the chunks in order.
 constexpr int CS_ROWS = 128;
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ X, int M, int N, long ldx,
-                                                          float* __restrict__ part) {
+                                                          int rows, float* __restrict__ part) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   const int chunk = blockIdx.y;
   if (c >= N) return;
-  const int r0 = chunk * CS_ROWS, r1 = min(M, r0 + CS_ROWS);
+  const int r0 = chunk * rows, r1 = min(M, r0 + rows);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int r = r0;
   for (; r + 3 < r1; r += 4) {
@@ -311,19 +311,23 @@ C2_API int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* 
   return 0;
 }
 
+// rows per stage-1 chunk: at least CS_ROWS, and few enough chunks (<= 64) for a short stage 2
+inline int cs_rows(int M) { return c2::ceil_div(c2::ceil_div(M, 64), CS_ROWS) * CS_ROWS; }
+
 C2_API size_t c2dsr_colsum_workspace(int M, int N) {
-  return (size_t)c2::ceil_div(M, CS_ROWS) * (size_t)N * 4 + 256;
+  return (size_t)c2::ceil_div(M, cs_rows(M)) * (size_t)N * 4 + 256;
 }
 
 C2_API int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* workspace,
                         void* stream) {
   if (N <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int chunks = c2::ceil_div(M, CS_ROWS);
+  const int rows = cs_rows(M);
+  const int chunks = c2::ceil_div(M, rows);
   float* part = (float*)workspace;
   if (chunks > 0) {
     dim3 g1(c2::ceil_div(N, 256), chunks);
-    colsum_part_kernel<<<g1, 256, 0, s>>>(X, M, N, ldx, part);
+    colsum_part_kernel<<<g1, 256, 0, s>>>(X, M, N, ldx, rows, part);
   }
   colsum_final_kernel<<<c2::ceil_div(N, 256), 256, 0, s>>>(part, chunks, N, alpha, beta, out);
   C2_CHECK_LAUNCH();

@@ -159,6 +159,10 @@ class LossHeadFn(Function):
                 dWp = torch.empty(nr, n, d, **f32)
                 dbp = torch.empty(nr, n, **f32)
                 lib('c2dsr_ce_fused_dw', Hb, Wb, bias, M2, n, d, nr, lse2, tcat, rw, dWp, dbp, gW, gb, s)
+                if gW is not None:
+                    lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
+                if gb is not None:
+                    lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
                 del dWp, dbp
                 pad_col, pad_ld = dpad, 1
             else:

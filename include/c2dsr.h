@@ -128,10 +128,13 @@ int c2dsr_ce_row_weights(const int64_t* tgt, int M, int ignore, const float* coe
 /* dH[r] = Σ_c P'[r][c]·W[c], P' = (softmax - onehot)·rw  (dHp: [n_split][M][D] scratch) */
 int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_split,
                       const float* lse2, const int64_t* tgt, const float* rw, float* dHp, float* dH, void* stream);
-/* gW[c] += Σ_r P'[r][c]·H[r];  gb[c] += Σ_r P'[r][c]  (dWp: [n_rsplit][n][D], dbp: [n_rsplit][n] scratch) */
+/* dWp[s][c] = Σ_{r∈split s} P'[r][c]·H[r];  dbp[s][c] = Σ_r P'[r][c]  (gW/gb unused: combine the
+ * [n_rsplit][n][D] / [n_rsplit][n] partials with c2dsr_sum_parts) */
 int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_rsplit,
                       const float* lse2, const int64_t* tgt, const float* rw, float* dWp, float* dbp, float* gW,
                       float* gb, void* stream);
+/* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
+int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */
 int c2dsr_selftest_tr(int rr0, int kb0, short* out, void* stream);
 

@@ -296,5 +296,7 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     gb = torch.ones(n, device=DEV)
     dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
     lib('c2dsr_ce_fused_dw', Hb, Wb, d(b), M, n, D, nr, lse2, d(t), rw, dWp, dbp, gW, gb, s)
+    lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
+    lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     assert rel(gW - 1, dl[:, :n].T @ H.double()) < 1e-2
     assert rel(gb - 1, dl[:, :n].sum(0)) < 1e-2
