@@ -1,146 +1,214 @@
-// Self-attention core for the sequence encoder: S = QKᵀ/√dh + mask, P = softmax(S),
-// O = dropout(P)·V, one workgroup per (sequence, head), everything for a
-// sequence staged in LDS (L <= 128).
+// Self-attention core of the sequence encoder on the matrix cores (exact fp32:
+// v_mfma_f32_32x32x2_f32), one workgroup (4 waves) per (sequence, head), the sequence
+// padded to LP = 32/64/128 rows and the head dim streamed through LDS in chunks.
+//
+//   S = Q·Kᵀ/√dh + mask,  P = softmax(S),  O = drop(P)·V           (forward)
+//   dPd = dO·Vᵀ, dS = P ⊙ (dP - Σ_j P·dP), dQ = dS·K/√dh, dK = dSᵀ·Q/√dh, dV = Pdᵀ·dO
 //
 // Replaces F.multi_head_attention_forward → scaled_dot_product_attention (math path)
-// as reached from models/encoders.py:33 with attn_mask = causal (encoders.py:14) and
-// key_padding_mask = (seq != pad) (encoders.py:33) merged additively — i.e. query i
-// attends only to keys j <= i that ARE padding (Q1); a row with no admissible key
-// yields 0 (Q2).  Keys that are masked for every query are skipped outright.
+// reached from models/encoders.py:33 with attn_mask = causal (encoders.py:14) and
+// key_padding_mask = (seq != pad) merged additively — query i attends only to keys
+// j <= i that ARE padding (Q1); a row with no admissible key yields 0 (Q2).  The
+// attention FLOPs are small (L <= 128), so the exact-fp32 MFMA keeps both precision
+// modes bit-identical here while staying far off the critical path.
 #include "common.h"
 
 namespace {
 
-// head-dim chunk staged in LDS for the QKᵀ-type products (smaller at L=128 to fit 160 KB)
-template <int LMAX>
-struct Ch {
-  static constexpr int V = LMAX >= 128 ? 16 : 32;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int creg(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+
+// KC: head-dim chunk for the Q·Kᵀ-type products; CC: output-column chunk for the P·V-type
+// products (smaller at LP = 128 so the backward's two score tiles + staging fit 160 KB).
+template <int LP>
+struct Smem {
+  static constexpr int KC = LP >= 128 ? 16 : 32;
+  static constexpr int CC = LP >= 128 ? 32 : 128;
+  static constexpr int SLD = LP + 1;
+  static constexpr int XLD = KC + 1;
+  static constexpr int VLD = CC + 1;
+  static constexpr int STAGE = 2 * LP * XLD > LP * VLD ? 2 * LP * XLD : LP * VLD;
 };
 
-// per-thread ownership of (i,j) pairs of an L x L tile: pair = t + 256*u
-template <int LMAX>
-struct Pairs {
-  static constexpr int U = (LMAX * LMAX + 255) / 256;
-};
-
-// dot[i][j] = Σ_c X[i][c]·Y[j][c] over the head dim for admissible pairs, staged in CH-wide chunks.
-template <int LMAX>
-__device__ __forceinline__ void pair_dots(const float* __restrict__ Xg, long xs, const float* __restrict__ Yg, long ys,
-                                          int L, int dh, const unsigned char* __restrict__ keyok, float* Xl, float* Yl,
-                                          float (&acc)[Pairs<LMAX>::U]) {
-  constexpr int CH = Ch<LMAX>::V;
-  const int t = threadIdx.x;
+// acc (32x32 tile (ti, tj) of X·Yᵀ over the head dim, X/Y rows = sequence positions) —
+// each wave owns tiles w, w+4, ... of the (LP/32)^2 grid.  X, Y: global rows of stride xs/ys.
+template <int LP>
+__device__ void xyT(const float* __restrict__ X, long xs, const float* __restrict__ Y, long ys, int L, int dh,
+                    float* Xs, float* Ys, f32x16 (&acc)[(LP / 32) * (LP / 32) / 4 > 0 ? (LP / 32) * (LP / 32) / 4 : 1]) {
+  constexpr int NT = LP / 32;
+  constexpr int XLD = Smem<LP>::XLD;
+  constexpr int KC = Smem<LP>::KC;
+  constexpr int PER = (NT * NT + 3) / 4;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
 #pragma unroll
-  for (int u = 0; u < Pairs<LMAX>::U; ++u) acc[u] = 0.f;
-  for (int c0 = 0; c0 < dh; c0 += CH) {
+  for (int u = 0; u < PER; ++u)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[u][i] = 0.f;
+  for (int k0 = 0; k0 < dh; k0 += KC) {
     __syncthreads();
-    for (int e = t; e < L * CH; e += 256) {
-      const int i = e / CH, c = e % CH;
-      Xl[i * (CH + 1) + c] = (c0 + c < dh) ? Xg[i * xs + c0 + c] : 0.f;
-      Yl[i * (CH + 1) + c] = (c0 + c < dh) ? Yg[i * ys + c0 + c] : 0.f;
+    for (int e = t; e < LP * KC; e += 256) {
+      const int i = e / KC, c = e % KC;
+      const bool ok = i < L && k0 + c < dh;
+      Xs[i * XLD + c] = ok ? X[i * xs + k0 + c] : 0.f;
+      Ys[i * XLD + c] = ok ? Y[i * ys + k0 + c] : 0.f;
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < Pairs<LMAX>::U; ++u) {
-      const int pr = t + 256 * u;
-      const int i = pr / LMAX, j = pr % LMAX;
-      if (i < L && j <= i && keyok[j]) {
-        float s = acc[u];
-#pragma unroll 8
-        for (int c = 0; c < CH; ++c) s = fmaf(Xl[i * (CH + 1) + c], Yl[j * (CH + 1) + c], s);
-        acc[u] = s;
+    for (int u = 0; u < PER; ++u) {
+      const int tile = w + 4 * u;
+      if (tile >= NT * NT) break;
+      const int ti = tile / NT, tj = tile % NT;
+      if (tj > ti) continue;  // causal: j > i never admissible
+#pragma unroll 4
+      for (int ks = 0; ks < KC / 2; ++ks) {
+        const float a = Xs[(ti * 32 + (lane & 31)) * XLD + ks * 2 + (lane >> 5)];
+        const float b = Ys[(tj * 32 + (lane & 31)) * XLD + ks * 2 + (lane >> 5)];
+        acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[u], 0, 0, 0);
       }
     }
   }
-  __syncthreads();
 }
 
-template <int LMAX>
+// out[i][c] (+)= scale * Σ_j A[i][j] * Y[j][c] for i < L, c < dh.  A in LDS ([LP][SLD], or
+// transposed: A[i][j] = As[j][i]); Y global rows (stride ys).  Each wave: 32 output columns of
+// a CC-wide chunk, all LP rows.
+template <int LP, bool TRANS_A>
+__device__ void pv(const float* As, const float* __restrict__ Y, long ys, int L, int dh, float* Vs,
+                   float* __restrict__ out, long os, float scale, int jmax) {
+  constexpr int NT = LP / 32;
+  constexpr int SLD = Smem<LP>::SLD;
+  constexpr int VLD = Smem<LP>::VLD;
+  constexpr int CC = Smem<LP>::CC;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  for (int c0 = 0; c0 < dh; c0 += CC) {
+    __syncthreads();
+    for (int e = t; e < LP * CC; e += 256) {
+      const int j = e / CC, c = e % CC;
+      Vs[j * VLD + c] = (j < L && c0 + c < dh) ? Y[j * ys + c0 + c] : 0.f;
+    }
+    __syncthreads();
+    const int cw = w * 32;
+    if (cw < CC && c0 + cw < dh) {
+      f32x16 acc[NT];
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[ti][i] = 0.f;
+      for (int ks = 0; ks < jmax / 2; ++ks) {
+        const int j = ks * 2 + (lane >> 5);
+        const float b = Vs[j * VLD + cw + (lane & 31)];
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti) {
+          const int i = ti * 32 + (lane & 31);
+          const float a = TRANS_A ? As[j * SLD + i] : As[i * SLD + j];
+          acc[ti] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[ti], 0, 0, 0);
+        }
+      }
+      const int c = c0 + cw + (lane & 31);
+      if (c < dh) {
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int i = ti * 32 + creg(r, lane);
+            if (i < L) out[i * os + c] = scale * acc[ti][r];
+          }
+      }
+    }
+  }
+}
+
+template <int LP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ seq,
                                                        int64_t pad, int L, int d, int H, c2::Drop drop,
                                                        int64_t b_base, float* __restrict__ out,
                                                        float* __restrict__ Psave) {
+  constexpr int NT = LP / 32;
+  constexpr int SLD = Smem<LP>::SLD;
+  constexpr int XLD = Smem<LP>::XLD;
+  constexpr int PER = (NT * NT + 3) / 4;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
-  constexpr int CH = Ch<LMAX>::V;
   const int dh = d / H;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Ps = sm;                         // [LMAX][LMAX+1]
-  float* Xl = Ps + LMAX * (LMAX + 1);     // [LMAX][CH+1]
-  float* Yl = Xl + LMAX * (CH + 1);       // [LMAX][CH+1]
-  __shared__ unsigned char keyok[LMAX];
-  for (int j = t; j < LMAX; j += 256) keyok[j] = (j < L) && (seq[(long)b * L + j] == pad);
-  __syncthreads();
-  const long rs = 3l * d;  // row stride of qkv
+  float* Ss = sm;                      // [LP][SLD]  scores → dropped probabilities
+  float* Xs = Ss + LP * SLD;           // [LP][XLD]
+  float* Ys = Xs + LP * XLD;           // [LP][XLD]
+  float* Vs = Xs;                      // the P·V staging reuses the X/Y staging area (Smem::STAGE)
+  __shared__ unsigned char keyok[LP];
+  for (int j = t; j < LP; j += 256) keyok[j] = (j < L) && (seq[(long)b * L + j] == pad);
+  const long rs = 3l * d;
   const float* Q = qkv + (long)b * L * rs + h * dh;
   const float* K = Q + d;
   const float* V = Q + 2 * d;
-  float acc[Pairs<LMAX>::U];
-  pair_dots<LMAX>(Q, rs, K, rs, L, dh, keyok, Xl, Yl, acc);
+  f32x16 acc[PER];
+  xyT<LP>(Q, rs, K, rs, L, dh, Xs, Ys, acc);
   const float sc = 1.0f / sqrtf((float)dh);
+  __syncthreads();
 #pragma unroll
-  for (int u = 0; u < Pairs<LMAX>::U; ++u) {
-    const int pr = t + 256 * u;
-    const int i = pr / LMAX, j = pr % LMAX;
-    if (i < L && j < L) Ps[i * (LMAX + 1) + j] = (j <= i && keyok[j]) ? acc[u] * sc : -INFINITY;
+  for (int u = 0; u < PER; ++u) {
+    const int tile = w + 4 * u;
+    if (tile >= NT * NT) break;
+    const int ti = tile / NT, tj = tile % NT;
+    const int j = tj * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = ti * 32 + creg(r, lane);
+      Ss[i * SLD + j] = (j <= i && keyok[j]) ? acc[u][r] * sc : -INFINITY;
+    }
   }
   __syncthreads();
-  // softmax per row: wave w rows w, w+4, ...
-  const int w = t >> 6, lane = t & 63;
-  for (int i = w; i < L; i += 4) {
+  for (int i = w; i < LP; i += 4) {
+    if (i >= L) {
+      for (int j = lane; j < LP; j += 64) Ss[i * SLD + j] = 0.f;
+      continue;
+    }
     float m = -INFINITY;
-    for (int j = lane; j < L; j += 64) m = fmaxf(m, Ps[i * (LMAX + 1) + j]);
+    for (int j = lane; j < L; j += 64) m = fmaxf(m, Ss[i * SLD + j]);
     m = c2::wave_max(m);
     float s = 0.f;
     for (int j = lane; j < L; j += 64) {
-      const float e = (m == -INFINITY) ? 0.f : __expf(Ps[i * (LMAX + 1) + j] - m);
-      Ps[i * (LMAX + 1) + j] = e;
+      const float e = (m == -INFINITY) ? 0.f : __expf(Ss[i * SLD + j] - m);
+      Ss[i * SLD + j] = e;
       s += e;
     }
     s = c2::wave_sum(s);
     const float inv = s > 0.f ? 1.0f / s : 0.f;
     const uint64_t rowidx = ((uint64_t)((b_base + b) * H + h) * L + i) * L;
-    for (int j = lane; j < L; j += 64) {
-      const float pv = Ps[i * (LMAX + 1) + j] * inv;
-      Psave[((long)blockIdx.x * L + i) * L + j] = pv;
-      Ps[i * (LMAX + 1) + j] = pv * drop.mul(rowidx + j);
+    for (int j = lane; j < LP; j += 64) {
+      if (j < L) {
+        const float pv_ = Ss[i * SLD + j] * inv;
+        Psave[((long)blockIdx.x * L + i) * L + j] = pv_;
+        Ss[i * SLD + j] = pv_ * drop.mul(rowidx + j);
+      } else {
+        Ss[i * SLD + j] = 0.f;
+      }
     }
   }
-  __syncthreads();
-  // O[i][c] = Σ_{j<=i, key j admissible} Pd[i][j] V[j][c]; thread owns column c
-  for (int c = t; c < dh; c += 256) {
-    float o[LMAX];
-#pragma unroll
-    for (int i = 0; i < LMAX; ++i) o[i] = 0.f;
-    for (int j = 0; j < L; ++j) {
-      if (!keyok[j]) continue;
-      const float v = V[(long)j * rs + c];
-#pragma unroll
-      for (int i = 0; i < LMAX; ++i)
-        if (i >= j && i < L) o[i] = fmaf(Ps[i * (LMAX + 1) + j], v, o[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < LMAX; ++i)
-      if (i < L) out[((long)b * L + i) * d + h * dh + c] = o[i];
-  }
+  pv<LP, false>(Ss, V, rs, L, dh, Vs, out + (long)b * L * d + h * dh, d, 1.0f, LP);
 }
 
-template <int LMAX>
+template <int LP>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ seq,
                                                        int64_t pad, int L, int d, int H, c2::Drop drop,
                                                        int64_t b_base, const float* __restrict__ Psave,
                                                        const float* __restrict__ dout, float* __restrict__ dqkv) {
+  constexpr int NT = LP / 32;
+  constexpr int SLD = Smem<LP>::SLD;
+  constexpr int XLD = Smem<LP>::XLD;
+  constexpr int PER = (NT * NT + 3) / 4;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
-  constexpr int CH = Ch<LMAX>::V;
   const int dh = d / H;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Pd = sm;                          // dropped probabilities [LMAX][LMAX+1]
-  float* dS = Pd + LMAX * (LMAX + 1);      // [LMAX][LMAX+1]
-  float* Xl = dS + LMAX * (LMAX + 1);
-  float* Yl = Xl + LMAX * (CH + 1);
-  __shared__ unsigned char keyok[LMAX];
-  for (int j = t; j < LMAX; j += 256) keyok[j] = (j < L) && (seq[(long)b * L + j] == pad);
+  float* Pd = sm;                      // dropped probabilities [LP][SLD]
+  float* dS = Pd + LP * SLD;           // dP → dS [LP][SLD]
+  float* Xs = dS + LP * SLD;
+  float* Ys = Xs + LP * XLD;
+  float* Vs = Xs;
+  __shared__ unsigned char keyok[LP];
+  for (int j = t; j < LP; j += 256) keyok[j] = (j < L) && (seq[(long)b * L + j] == pad);
   const long rs = 3l * d;
   const float* Q = qkv + (long)b * L * rs + h * dh;
   const float* K = Q + d;
@@ -149,105 +217,75 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__
   float* dQ = dqkv + (long)b * L * rs + h * dh;
   float* dK = dQ + d;
   float* dV = dQ + 2 * d;
-  __syncthreads();
-  // dPd[i][j] = dO_i · V_j
-  float acc[Pairs<LMAX>::U];
-  pair_dots<LMAX>(dO, d, V, rs, L, dh, keyok, Xl, Yl, acc);
   const float* Pg = Psave + (long)blockIdx.x * L * L;
+  f32x16 acc[PER];
+  xyT<LP>(dO, d, V, rs, L, dh, Xs, Ys, acc);  // dPd = dO·Vᵀ
+  __syncthreads();
+  // dP = dPd ⊙ mask/(1-p); Pd = P ⊙ mask/(1-p)
 #pragma unroll
-  for (int u = 0; u < Pairs<LMAX>::U; ++u) {
-    const int pr = t + 256 * u;
-    const int i = pr / LMAX, j = pr % LMAX;
-    if (i < L && j < L) {
-      const uint64_t idx = ((uint64_t)((b_base + b) * H + h) * L + i) * L + j;
-      const float mk = drop.mul(idx);
-      const float p = Pg[(long)i * L + j];
-      Pd[i * (LMAX + 1) + j] = p * mk;
-      dS[i * (LMAX + 1) + j] = acc[u] * mk;  // dP (grad w.r.t. the softmax output)
+  for (int u = 0; u < PER; ++u) {
+    const int tile = w + 4 * u;
+    if (tile >= NT * NT) break;
+    const int ti = tile / NT, tj = tile % NT;
+    const int j = tj * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = ti * 32 + creg(r, lane);
+      float p = 0.f, dp = 0.f;
+      if (i < L && j < L) {
+        const float mk = drop.mul(((uint64_t)((b_base + b) * H + h) * L + i) * L + j);
+        p = Pg[(long)i * L + j];
+        dp = (j <= i) ? acc[u][r] * mk : 0.f;
+        p *= mk;
+      }
+      Pd[i * SLD + j] = p;
+      dS[i * SLD + j] = dp;
     }
   }
   __syncthreads();
-  // dS = P ⊙ (dP - Σ_j P·dP)
-  const int w = t >> 6, lane = t & 63;
-  for (int i = w; i < L; i += 4) {
+  for (int i = w; i < LP; i += 4) {
+    if (i >= L) {
+      for (int j = lane; j < LP; j += 64) dS[i * SLD + j] = 0.f;
+      continue;
+    }
     float s = 0.f;
-    for (int j = lane; j < L; j += 64) s += Pg[(long)i * L + j] * dS[i * (LMAX + 1) + j];
+    for (int j = lane; j < L; j += 64) s += Pg[(long)i * L + j] * dS[i * SLD + j];
     s = c2::wave_sum(s);
-    for (int j = lane; j < L; j += 64) {
-      const float p = Pg[(long)i * L + j];
-      dS[i * (LMAX + 1) + j] = p * (dS[i * (LMAX + 1) + j] - s);
-    }
+    for (int j = lane; j < LP; j += 64) dS[i * SLD + j] = j < L ? Pg[(long)i * L + j] * (dS[i * SLD + j] - s) : 0.f;
   }
-  __syncthreads();
   const float sc = 1.0f / sqrtf((float)dh);
-  for (int c = t; c < dh; c += 256) {
-    float a[LMAX];
-    // dV[j] = Σ_{i>=j} Pd[i][j] dO[i]   and   dK[j] = sc Σ_{i>=j} dS[i][j] Q[i]
-#pragma unroll
-    for (int j = 0; j < LMAX; ++j) a[j] = 0.f;
-    for (int i = 0; i < L; ++i) {
-      const float go = dO[(long)i * d + c];
-#pragma unroll
-      for (int j = 0; j < LMAX; ++j)
-        if (j <= i) a[j] = fmaf(Pd[i * (LMAX + 1) + j], go, a[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < LMAX; ++j)
-      if (j < L) dV[(long)j * rs + c] = a[j];
-#pragma unroll
-    for (int j = 0; j < LMAX; ++j) a[j] = 0.f;
-    for (int i = 0; i < L; ++i) {
-      const float q = Q[(long)i * rs + c];
-#pragma unroll
-      for (int j = 0; j < LMAX; ++j)
-        if (j <= i) a[j] = fmaf(dS[i * (LMAX + 1) + j], q, a[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < LMAX; ++j)
-      if (j < L) dK[(long)j * rs + c] = a[j] * sc;
-    // dQ[i] = sc Σ_{j<=i} dS[i][j] K[j]
-#pragma unroll
-    for (int i = 0; i < LMAX; ++i) a[i] = 0.f;
-    for (int j = 0; j < L; ++j) {
-      if (!keyok[j]) continue;
-      const float k = K[(long)j * rs + c];
-#pragma unroll
-      for (int i = 0; i < LMAX; ++i)
-        if (i >= j && i < L) a[i] = fmaf(dS[i * (LMAX + 1) + j], k, a[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < LMAX; ++i)
-      if (i < L) dQ[(long)i * rs + c] = a[i] * sc;
-  }
+  pv<LP, false>(dS, K, rs, L, dh, Vs, dQ, rs, sc, LP);  // dQ = dS·K/√dh
+  pv<LP, true>(dS, Q, rs, L, dh, Vs, dK, rs, sc, LP);   // dK = dSᵀ·Q/√dh
+  pv<LP, true>(Pd, dO, d, L, dh, Vs, dV, rs, 1.0f, LP);  // dV = Pdᵀ·dO
 }
 
-template <int LMAX>
-size_t fwd_smem() { return sizeof(float) * (LMAX * (LMAX + 1) + 2 * LMAX * (Ch<LMAX>::V + 1)); }
-template <int LMAX>
-size_t bwd_smem() { return sizeof(float) * (2 * LMAX * (LMAX + 1) + 2 * LMAX * (Ch<LMAX>::V + 1)); }
+template <int LP>
+size_t fwd_smem() { return sizeof(float) * ((size_t)LP * Smem<LP>::SLD + Smem<LP>::STAGE); }
+template <int LP>
+size_t bwd_smem() { return sizeof(float) * ((size_t)2 * LP * Smem<LP>::SLD + Smem<LP>::STAGE); }
 
-template <int LMAX>
+template <int LP>
 void launch_fwd(dim3 grid, hipStream_t s, const float* qkv, const int64_t* seq, int64_t pad, int L, int d, int H,
                 c2::Drop dr, int64_t b_base, float* out, float* Psave) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<LMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)fwd_smem<LMAX>());
+    (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<LP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)fwd_smem<LP>());
     attr = true;
   }
-  attn_fwd_kernel<LMAX><<<grid, 256, fwd_smem<LMAX>(), s>>>(qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
+  attn_fwd_kernel<LP><<<grid, 256, fwd_smem<LP>(), s>>>(qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
 }
 
-template <int LMAX>
+template <int LP>
 void launch_bwd(dim3 grid, hipStream_t s, const float* qkv, const int64_t* seq, int64_t pad, int L, int d, int H,
                 c2::Drop dr, int64_t b_base, const float* Psave, const float* dout, float* dqkv) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<LMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)bwd_smem<LMAX>());
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<LP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bwd_smem<LP>());
     attr = true;
   }
-  attn_bwd_kernel<LMAX><<<grid, 256, bwd_smem<LMAX>(), s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
+  attn_bwd_kernel<LP><<<grid, 256, bwd_smem<LP>(), s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
 }
 
 }  // namespace
@@ -262,9 +300,7 @@ C2_API int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
-  if (L <= 16)
-    launch_fwd<16>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
-  else if (L <= 32)
+  if (L <= 32)
     launch_fwd<32>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
   else if (L <= 64)
     launch_fwd<64>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
@@ -282,9 +318,7 @@ C2_API int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
-  if (L <= 16)
-    launch_bwd<16>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
-  else if (L <= 32)
+  if (L <= 32)
     launch_bwd<32>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
   else if (L <= 64)
     launch_bwd<64>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
