@@ -76,76 +76,111 @@ __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
   return r;
 }
 
-// Register-staged tile loader: rows g0..g0+TILE-1 of a row-major bf16 [rows][D] matrix
+typedef __attribute__((address_space(3))) char lds_char;
+
+// One LDS-DMA wave-instruction: each lane copies `bytes` (4 or 16) from its global address to
+// LDS[m0 + lane*bytes].  Issued from inline asm so the compiler's wait-count pass does not
+// conservatively drain it before every later LDS read (it cannot prove the prefetch buffer
+// disjoint from the one being read); the kernels wait for it by hand (dma_wait) before the
+// barrier that publishes the buffer.  m0 is written here and nowhere else in these kernels.
+__device__ __forceinline__ void dma16(const void* g, char* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(g) : "memory");
+}
+__device__ __forceinline__ void dma4(const void* g, void* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(g) : "memory");
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// vmcnt(0) the compiler can see (its wait-count state then knows the register operands
+// loaded before the tile loop have landed, and emits no waits for them inside the loop)
+// pin a register operand here: its load must be issued (and have landed) before this point
+__device__ __forceinline__ void pin(bf16x8& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(int& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void vm_drain() {
+  __builtin_amdgcn_sched_barrier(0);  // keep the preceding loads above the wait
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS-DMA tile loader: rows g0..g0+TILE-1 of a row-major bf16 [nrows][D] matrix into the
+// swizzled image, no staging registers.  One wave-instruction fills 1 KiB = 4 image rows of
+// one half-tile; lane l writes physical chunk l&15 of row l>>4, so its SOURCE is the logical
+// chunk (l&15) ^ swizzle(row).  Rows past the end are clamped to the last row (finite data;
+// callers zero their contribution).
 template <int D>
-struct TileLoad {
-  static constexpr int CHUNKS = TILE * D / 8;  // 16-byte chunks per tile
-  static constexpr int PER = CHUNKS / 256;
-  uint4 v[PER];
-  __device__ __forceinline__ void load(const bf16* __restrict__ X, long nrows, long g0) {
+__device__ __forceinline__ void dma_tile(const bf16* __restrict__ X, long nrows, long g0, char* img) {
+  constexpr int GROUPS = TILE / 4;             // 4-row groups per half-tile
+  constexpr int INSTR = GROUPS * (D / 128);    // wave-instructions per tile
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int q = threadIdx.x + 256 * i;
-      const int row = q / (D / 8), ch = q % (D / 8);
-      const long gr = g0 + row;
-      v[i] = gr < nrows ? *(const uint4*)(X + gr * D + ch * 8) : make_uint4(0, 0, 0, 0);
-    }
+  for (int q = w; q < INSTR; q += 4) {
+    const int half = q / GROUPS, rg = q % GROUPS;
+    const int row = rg * 4 + (lane >> 4);
+    const int lch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    long gr = g0 + row;
+    gr = gr < nrows ? gr : nrows - 1;
+    dma16(X + gr * D + half * 128 + lch * 8, img + half * (TILE * 256) + rg * 1024);
   }
-  __device__ __forceinline__ void store(char* img) const {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int q = threadIdx.x + 256 * i;
-      const int row = q / (D / 8), ch = q % (D / 8);
-      *(uint4*)(img + (ch >> 4) * (TILE * 256) + swz(row, ch & 15)) = v[i];
-    }
-  }
-};
+}
+
+// 64 consecutive 4-byte values (a padded per-row / per-column constant array) → LDS, by wave `wv`
+__device__ __forceinline__ void dma_vec64(const void* __restrict__ src, void* dst, int wv) {
+  if ((threadIdx.x >> 6) == wv) dma4((const char*)src + 4 * (threadIdx.x & 63), dst);
+}
 
 __device__ __forceinline__ int creg(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
+// raw v_exp_f32 (2^x; no denormal range handling — results below 2^-126 flush to 0)
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // ---------------------------------------------------------------- forward: partial LSE
 // grid (ceil(M/256), n_split); 4 waves x 64 rows.  part_m/part_s [n_split][M]: log2-domain
-// running max and sum of 2^(s·log2e) over the split's columns.
+// running max and sum of 2^(s·log2e) over the split's columns.  bias2 = bias·log2e padded
+// with -inf to a multiple of TILE.
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_lse_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
-                                                        const float* __restrict__ bias, int M, int n,
+                                                        const float* __restrict__ bias2, int M, int n,
                                                         int cols_per_split, float* __restrict__ part_m,
                                                         float* __restrict__ part_s) {
   constexpr int KS = D / 16;
   __shared__ __attribute__((aligned(16))) char img[2][TILE * D * 2];
-  __shared__ float b2s[2][TILE];
+  __shared__ __attribute__((aligned(16))) float b2s[2][TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rbase = blockIdx.x * 256 + w * 64;
   const int c_beg = blockIdx.y * cols_per_split;
   const int c_end = min(n, c_beg + cols_per_split);
+  const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
+  if (ntiles > 0) {
+    dma_tile<D>(Wb, n, c_beg, img[0]);
+    dma_vec64(bias2 + c_beg, b2s[0], 0);
+  }
   bf16x8 hf[2][KS];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
-    const int r = rbase + rb * 32 + (lane & 31);
+    const int r = min(M - 1, rbase + rb * 32 + (lane & 31));
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (r < M)
-        hf[rb][ks] = *(const bf16x8*)(Hb + (long)r * D + ks * 16 + 8 * (lane >> 5));
-      else
-        for (int j = 0; j < 8; ++j) hf[rb][ks][j] = (bf16)0.f;
-    }
+    for (int ks = 0; ks < KS; ++ks) hf[rb][ks] = *(const bf16x8*)(Hb + (long)r * D + ks * 16 + 8 * (lane >> 5));
   }
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) pin(hf[rb][ks]);
   float mrun[2] = {-INFINITY, -INFINITY}, srun[2] = {0.f, 0.f};
-  const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
-  TileLoad<D> ld;
-  if (ntiles > 0) {
-    ld.load(Wb, n, c_beg);
-    ld.store(img[0]);
-    if (threadIdx.x < TILE) {
-      const int c = c_beg + threadIdx.x;
-      b2s[0][threadIdx.x] = c < n ? bias[c] * LOG2E : -INFINITY;
-    }
-  }
+  vm_drain();
+  dma_wait();
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
+    const char* cimg = img[t & 1];
+    const float* cb2s = b2s[t & 1];
+    char* nimg = img[(t & 1) ^ 1];
+    float* nb2s = b2s[(t & 1) ^ 1];
     const int c0 = c_beg + t * TILE;
-    if (t + 1 < ntiles) ld.load(Wb, n, c0 + TILE);
+    if (t + 1 < ntiles) {
+      dma_tile<D>(Wb, n, c0 + TILE, nimg);
+      dma_vec64(bias2 + c0 + TILE, nb2s, 1);
+    }
     f32x16 acc[2][2];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
@@ -153,17 +188,28 @@ __global__ __launch_bounds__(256, 1) void ce_lse_kernel(const bf16* __restrict__
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[cb][rb][i] = 0.f;
+    bf16x8 fa[2], fb[2];
+    fa[0] = row_frag(cimg, 0, 0, lane);
+    fa[1] = row_frag(cimg, 32, 0, lane);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+        fb[0] = row_frag(cimg, 0, (ks + 1) * 16, lane);
+        fb[1] = row_frag(cimg, 32, (ks + 1) * 16, lane);
+      }
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const bf16x8 a = row_frag(img[cur], cb * 32, ks * 16, lane);
+      for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
-          acc[cb][rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, hf[rb][ks], acc[cb][rb], 0, 0, 0);
-      }
+          acc[cb][rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cb], hf[rb][ks], acc[cb][rb], 0, 0, 0);
+      fa[0] = fb[0];
+      fa[1] = fb[1];
     }
-    // online log2-sum-exp2 per lane row (lanes l and l^32 share a row, different columns)
+    float4 b4[2][4];  // bias·log2e of this lane's 32 columns (4 runs of 4)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) b4[cb][j4] = *(const float4*)&cb2s[cb * 32 + 8 * j4 + 4 * (lane >> 5)];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       float tmax = -INFINITY;
@@ -171,36 +217,28 @@ __global__ __launch_bounds__(256, 1) void ce_lse_kernel(const bf16* __restrict__
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float v = fmaf(acc[cb][rb][i], LOG2E, b2s[cur][cb * 32 + creg(i, lane)]);
+          const float v = fmaf(acc[cb][rb][i], LOG2E, ((const float*)&b4[cb][i >> 2])[i & 3]);
           acc[cb][rb][i] = v;
           tmax = fmaxf(tmax, v);
         }
       const float mnew = fmaxf(mrun[rb], tmax);
-      float s = (mrun[rb] == -INFINITY) ? 0.f : srun[rb] * exp2f(mrun[rb] - mnew);
-      if (mnew != -INFINITY) {
+      float s = (mrun[rb] == -INFINITY) ? 0.f : srun[rb] * ex2(mrun[rb] - mnew);
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
+      for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) s += exp2f(acc[cb][rb][i] - mnew);
-      }
+        for (int i = 0; i < 16; ++i) s += ex2(acc[cb][rb][i] - mnew);
       mrun[rb] = mnew;
       srun[rb] = s;
     }
-    if (t + 1 < ntiles) {
-      ld.store(img[cur ^ 1]);
-      if (threadIdx.x < TILE) {
-        const int c = c0 + TILE + threadIdx.x;
-        b2s[cur ^ 1][threadIdx.x] = c < n ? bias[c] * LOG2E : -INFINITY;
-      }
-    }
+    dma_wait();
     __syncthreads();
   }
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
     const float m2 = __shfl_xor(mrun[rb], 32, 64), s2 = __shfl_xor(srun[rb], 32, 64);
     const float mm = fmaxf(mrun[rb], m2);
-    const float s = (mrun[rb] == -INFINITY ? 0.f : srun[rb] * exp2f(mrun[rb] - mm)) +
-                    (m2 == -INFINITY ? 0.f : s2 * exp2f(m2 - mm));
+    const float s = (mrun[rb] == -INFINITY ? 0.f : srun[rb] * ex2(mrun[rb] - mm)) +
+                    (m2 == -INFINITY ? 0.f : s2 * ex2(m2 - mm));
     const int r = rbase + rb * 32 + (lane & 31);
     if (lane < 32 && r < M) {
       part_m[(long)blockIdx.y * M + r] = mm;
@@ -246,92 +284,107 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
 
 // ---------------------------------------------------------------- backward: dH
 // grid (ceil(M/128), n_split); 4 waves x 32 rows; sweeps the split's columns.
-// dHp [n_split][M][D] (fp32 partials, combined by ce_sum_parts_kernel).
+// dHp [n_split][M][D] (fp32 partials, combined by c2dsr_sum_parts).
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
-                                                       const float* __restrict__ bias, int M, int n,
+                                                       const float* __restrict__ bias2, int M, int n,
                                                        int cols_per_split, const float* __restrict__ lse2,
-                                                       const int64_t* __restrict__ tgt,
+                                                       const int* __restrict__ tgt32,
                                                        const float* __restrict__ roww, float* __restrict__ dHp) {
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
   __shared__ __attribute__((aligned(16))) char img[2][TILE * D * 2];
-  __shared__ float b2s[2][TILE];
+  __shared__ __attribute__((aligned(16))) float b2s[2][TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x * 128 + w * 32 + (lane & 31);
+  const int rc = min(r, M - 1);
   const int c_beg = blockIdx.y * cols_per_split;
   const int c_end = min(n, c_beg + cols_per_split);
+  const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
+  if (ntiles > 0) {
+    dma_tile<D>(Wb, n, c_beg, img[0]);
+    dma_vec64(bias2 + c_beg, b2s[0], 0);
+  }
   bf16x8 hf[KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (r < M)
-      hf[ks] = *(const bf16x8*)(Hb + (long)r * D + ks * 16 + 8 * (lane >> 5));
-    else
-      for (int j = 0; j < 8; ++j) hf[ks][j] = (bf16)0.f;
-  }
-  const float lr = r < M ? lse2[r] : 0.f;
-  const float rw = r < M ? roww[r] : 0.f;
-  const long tr = r < M ? tgt[r] : -1;
+  for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
+  float lr = lse2[rc];
+  float rw = r < M ? roww[rc] : 0.f;
+  int tr = tgt32[rc];
+  pin(lr);
+  pin(rw);
+  pin(tr);
   f32x16 dacc[KB];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dacc[kb][i] = 0.f;
-  const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
-  TileLoad<D> ld;
-  if (ntiles > 0) {
-    ld.load(Wb, n, c_beg);
-    ld.store(img[0]);
-    if (threadIdx.x < TILE) {
-      const int c = c_beg + threadIdx.x;
-      b2s[0][threadIdx.x] = c < n ? bias[c] * LOG2E : -INFINITY;
-    }
-  }
+  vm_drain();
+  dma_wait();
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
+    const char* cimg = img[t & 1];
+    const float* cb2s = b2s[t & 1];
+    char* nimg = img[(t & 1) ^ 1];
+    float* nb2s = b2s[(t & 1) ^ 1];
     const int c0 = c_beg + t * TILE;
-    if (t + 1 < ntiles) ld.load(Wb, n, c0 + TILE);
+    if (t + 1 < ntiles) {
+      dma_tile<D>(Wb, n, c0 + TILE, nimg);
+      dma_vec64(bias2 + c0 + TILE, nb2s, 1);
+    }
     f32x16 s[2];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[cb][i] = 0.f;
+    bf16x8 fa[2], fb[2];
+    fa[0] = row_frag(cimg, 0, 0, lane);
+    fa[1] = row_frag(cimg, 32, 0, lane);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-        s[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(img[cur], cb * 32, ks * 16, lane), hf[ks], s[cb], 0,
-                                                        0, 0);
-    // P'ᵀ[c][r] = (2^(s·log2e + b2 - lse2) - [c == t]) * w_r
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+        fb[0] = row_frag(cimg, 0, (ks + 1) * 16, lane);
+        fb[1] = row_frag(cimg, 32, (ks + 1) * 16, lane);
+      }
+      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], hf[ks], s[0], 0, 0, 0);
+      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], hf[ks], s[1], 0, 0, 0);
+      fa[0] = fb[0];
+      fa[1] = fb[1];
+    }
+    // P'ᵀ[c][r] = (2^(s·log2e + b2 - lse2) - [c == t]) * w_r   (b2 = -inf past n → 0)
     bf16x8 x[2][2];
+    const int tl = tr - c0;  // target column relative to this tile (may be out of range)
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int cl = cb * 32 + creg(i, lane);
-        const float e = exp2f(fmaf(s[cb][i], LOG2E, b2s[cur][cl]) - lr);
-        s[cb][i] = (e - ((long)(c0 + cl) == tr ? 1.f : 0.f)) * rw;
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int cl0 = cb * 32 + 8 * j4 + 4 * (lane >> 5);
+        const float4 b4 = *(const float4*)&cb2s[cl0];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * j4 + e;
+          const float ev = ex2(fmaf(s[cb][i], LOG2E, ((const float*)&b4)[e]) - lr);
+          s[cb][i] = (ev - (cl0 + e == tl ? 1.f : 0.f)) * rw;
+        }
       }
       x[cb][0] = acc_frag(s[cb], 0);
       x[cb][1] = acc_frag(s[cb], 1);
     }
-    // dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r]
+    // dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r]   (A = transposed reads of the W image)
+    bf16x8 ta = tr_frag(cimg, 0, 0, lane), tb;
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-          dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(img[cur], cb * 32 + 16 * st, kb * 32, lane),
-                                                             x[cb][st], dacc[kb], 0, 0, 0);
-    if (t + 1 < ntiles) {
-      ld.store(img[cur ^ 1]);
-      if (threadIdx.x < TILE) {
-        const int c = c0 + TILE + threadIdx.x;
-        b2s[cur ^ 1][threadIdx.x] = c < n ? bias[c] * LOG2E : -INFINITY;
+    for (int q = 0; q < KB * 4; ++q) {
+      const int kb = q >> 2, cb = (q >> 1) & 1, st = q & 1;
+      if (q + 1 < KB * 4) {
+        const int q1 = q + 1;
+        tb = tr_frag(cimg, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, lane);
       }
+      dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta, x[cb][st], dacc[kb], 0, 0, 0);
+      ta = tb;
     }
+    dma_wait();
     __syncthreads();
   }
   if (r < M) {
@@ -345,97 +398,115 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
 
 // ---------------------------------------------------------------- backward: dW, db
 // grid (ceil(n/128), n_rsplit); 4 waves x 32 columns; sweeps the split's rows.
+// Per-row constants are padded to a multiple of TILE rows (lse2 0, roww 0, tgt32 -1).
 // dWp [n_rsplit][n][D], dbp [n_rsplit][n] fp32 partials.
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
-                                                       const float* __restrict__ bias, int M, int n,
+                                                       const float* __restrict__ bias2, int M, int n,
                                                        int rows_per_split, const float* __restrict__ lse2,
-                                                       const int64_t* __restrict__ tgt,
+                                                       const int* __restrict__ tgt32,
                                                        const float* __restrict__ roww, float* __restrict__ dWp,
                                                        float* __restrict__ dbp) {
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
   __shared__ __attribute__((aligned(16))) char img[2][TILE * D * 2];
-  __shared__ float rl[2][TILE], rwv[2][TILE];
-  __shared__ long rt[2][TILE];
+  __shared__ __attribute__((aligned(16))) float rl[2][TILE];
+  __shared__ __attribute__((aligned(16))) float rwv[2][TILE];
+  __shared__ __attribute__((aligned(16))) int rt[2][TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 128 + w * 32 + (lane & 31);
   const int r_beg = blockIdx.y * rows_per_split;
   const int r_end = min(M, r_beg + rows_per_split);
+  const int ntiles = r_end > r_beg ? (r_end - r_beg + TILE - 1) / TILE : 0;
+  auto issue = [&](int r0, char* img, float* rl, float* rwv, int* rt) {
+    dma_tile<D>(Hb, M, r0, img);
+    dma_vec64(lse2 + r0, rl, 0);
+    dma_vec64(roww + r0, rwv, 1);
+    dma_vec64(tgt32 + r0, rt, 2);
+  };
+  if (ntiles > 0) issue(r_beg, img[0], rl[0], rwv[0], rt[0]);
   bf16x8 wf[KS];
+  const int cc = min(c, n - 1);
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    if (c < n)
-      wf[ks] = *(const bf16x8*)(Wb + (long)c * D + ks * 16 + 8 * (lane >> 5));
-    else
-      for (int j = 0; j < 8; ++j) wf[ks][j] = (bf16)0.f;
-  }
-  const float b2 = c < n ? bias[c] * LOG2E : 0.f;
+  for (int ks = 0; ks < KS; ++ks) wf[ks] = *(const bf16x8*)(Wb + (long)cc * D + ks * 16 + 8 * (lane >> 5));
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) pin(wf[ks]);
+  float b2 = bias2[c];  // -inf past n: those columns contribute 0
+  pin(b2);
   f32x16 dacc[KB];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dacc[kb][i] = 0.f;
   float db = 0.f;
-  const int ntiles = r_end > r_beg ? (r_end - r_beg + TILE - 1) / TILE : 0;
-  TileLoad<D> ld;
-  auto rowinfo = [&](int buf, int r0) {
-    if (threadIdx.x < TILE) {
-      const int r = r0 + threadIdx.x;
-      const bool ok = r < r_end;
-      rl[buf][threadIdx.x] = ok ? lse2[r] : 0.f;
-      rwv[buf][threadIdx.x] = ok ? roww[r] : 0.f;
-      rt[buf][threadIdx.x] = ok ? tgt[r] : -1;
-    }
-  };
-  if (ntiles > 0) {
-    ld.load(Hb, r_end, r_beg);
-    ld.store(img[0]);
-    rowinfo(0, r_beg);
-  }
+  vm_drain();
+  dma_wait();
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
+    const int cu = t & 1, nx = cu ^ 1;
+    const char* cimg = img[cu];
+    const float* crl = rl[cu];
+    const float* crwv = rwv[cu];
+    const int* crt = rt[cu];
+    char* nimg = img[nx];
+    float* nrl = rl[nx];
+    float* nrwv = rwv[nx];
+    int* nrt = rt[nx];
     const int r0 = r_beg + t * TILE;
-    if (t + 1 < ntiles) ld.load(Hb, r_end, r0 + TILE);
+    if (t + 1 < ntiles) issue(r0 + TILE, nimg, nrl, nrwv, nrt);
     f32x16 s[2];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int i = 0; i < 16; ++i) s[rb][i] = 0.f;
+    bf16x8 fa[2], fb[2];
+    fa[0] = row_frag(cimg, 0, 0, lane);
+    fa[1] = row_frag(cimg, 32, 0, lane);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-        s[rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(img[cur], rb * 32, ks * 16, lane), wf[ks], s[rb], 0,
-                                                        0, 0);
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+        fb[0] = row_frag(cimg, 0, (ks + 1) * 16, lane);
+        fb[1] = row_frag(cimg, 32, (ks + 1) * 16, lane);
+      }
+      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], wf[ks], s[0], 0, 0, 0);
+      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], wf[ks], s[1], 0, 0, 0);
+      fa[0] = fb[0];
+      fa[1] = fb[1];
+    }
     bf16x8 x[2][2];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int rl_ = rb * 32 + creg(i, lane);
-        const float e = exp2f(fmaf(s[rb][i], LOG2E, b2) - rl[cur][rl_]);
-        const float v = c < n ? (e - ((long)c == rt[cur][rl_] ? 1.f : 0.f)) * rwv[cur][rl_] : 0.f;
-        s[rb][i] = v;
-        db += v;
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int r4 = rb * 32 + 8 * j4 + 4 * (lane >> 5);
+        const float4 L4 = *(const float4*)&crl[r4];
+        const float4 W4 = *(const float4*)&crwv[r4];
+        const int4 T4 = *(const int4*)&crt[r4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * j4 + e;
+          const float ev = ex2(fmaf(s[rb][i], LOG2E, b2) - ((const float*)&L4)[e]);
+          const float v = (ev - (c == ((const int*)&T4)[e] ? 1.f : 0.f)) * ((const float*)&W4)[e];
+          s[rb][i] = v;
+          db += v;
+        }
       }
       x[rb][0] = acc_frag(s[rb], 0);
       x[rb][1] = acc_frag(s[rb], 1);
     }
-    // dWᵀ[k][c] += Σ_r H[r][k] P'[r][c]
+    // dWᵀ[k][c] += Σ_r H[r][k] P'[r][c]   (A = transposed reads of the H image)
+    bf16x8 ta = tr_frag(cimg, 0, 0, lane), tb;
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-          dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(img[cur], rb * 32 + 16 * st, kb * 32, lane),
-                                                             x[rb][st], dacc[kb], 0, 0, 0);
-    if (t + 1 < ntiles) {
-      ld.store(img[cur ^ 1]);
-      rowinfo(cur ^ 1, r0 + TILE);
+    for (int q = 0; q < KB * 4; ++q) {
+      const int kb = q >> 2, rb = (q >> 1) & 1, st = q & 1;
+      if (q + 1 < KB * 4) {
+        const int q1 = q + 1;
+        tb = tr_frag(cimg, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, lane);
+      }
+      dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta, x[rb][st], dacc[kb], 0, 0, 0);
+      ta = tb;
     }
+    dma_wait();
     __syncthreads();
   }
   db += __shfl_xor(db, 32, 64);
@@ -473,20 +544,32 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, long n, bf16* __
   }
 }
 
-// rw[r] = valid ? gscale * lam * coef[r >= split] : 0
-__global__ void ce_roww_kernel(const int64_t* __restrict__ tgt, int M, int ignore, const float* __restrict__ coef,
-                               int split, const float* __restrict__ gscale, float lam, float* __restrict__ rw) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= M) return;
-  rw[r] = tgt[r] != ignore ? gscale[0] * lam * coef[r >= split ? 1 : 0] : 0.f;
+// bias2[c] = bias[c]·log2e for c < n, -inf up to n_pad
+__global__ void bias2_kernel(const float* __restrict__ bias, int n, int n_pad, float* __restrict__ b2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n_pad) b2[c] = c < n ? bias[c] * LOG2E : -INFINITY;
 }
 
-// dpad[r] = exp(pl[r] - lse[r]) * rw[r]  (pad column of the softmax; its target is ignored)
-__global__ void ce_padgrad_kernel(const float* __restrict__ pl, const float* __restrict__ lse,
-                                  const float* __restrict__ rw, int M, float* __restrict__ dpad) {
+// per row r < M_pad: rw = valid ? gscale*lam*coef[r >= split] : 0; t32 = target (-1 past M);
+// lse2 padded with 0; dpad = exp(pl - lse)·rw (the pad column of the softmax; its target is ignored)
+__global__ void ce_roww_kernel(const int64_t* __restrict__ tgt, int M, int M_pad, int ignore,
+                               const float* __restrict__ coef, int split, const float* __restrict__ gscale,
+                               float lam, const float* __restrict__ pl, const float* __restrict__ lse,
+                               float* __restrict__ rw, int* __restrict__ t32, float* __restrict__ lse2,
+                               float* __restrict__ dpad) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= M) return;
-  dpad[r] = expf(pl[r] - lse[r]) * rw[r];
+  if (r >= M_pad) return;
+  if (r >= M) {
+    rw[r] = 0.f;
+    t32[r] = -1;
+    lse2[r] = 0.f;
+    return;
+  }
+  const long t = tgt[r];
+  const float w = t != ignore ? gscale[0] * lam * coef[r >= split ? 1 : 0] : 0.f;
+  rw[r] = w;
+  t32[r] = (int)t;
+  dpad[r] = expf(pl[r] - lse[r]) * w;
 }
 
 // self-test of the transposed fragment addressing: image row = rr, col = k holds rr*256+k (int16)
@@ -515,26 +598,6 @@ __global__ void selftest_tr_kernel(int rr0, int kb0, short* __restrict__ out) {
   for (int j = 0; j < 8; ++j) out[512 + lane * 8 + j] = rs[j];
 }
 
-template <int D>
-void launch_all(int which, dim3 grid, hipStream_t s, const bf16* Hb, const bf16* Wb, const float* bias, int M, int n,
-                int per, float* a0, float* a1, const float* lse2, const int64_t* tgt, const float* rw) {
-  if (which == 0) ce_lse_kernel<D><<<grid, 256, 0, s>>>(Hb, Wb, bias, M, n, per, a0, a1);
-  if (which == 1) ce_dh_kernel<D><<<grid, 256, 0, s>>>(Hb, Wb, bias, M, n, per, lse2, tgt, rw, a0);
-  if (which == 2) ce_dw_kernel<D><<<grid, 256, 0, s>>>(Hb, Wb, bias, M, n, per, lse2, tgt, rw, a0, a1);
-}
-
-int launch_d(int D, int which, dim3 grid, hipStream_t s, const bf16* Hb, const bf16* Wb, const float* bias, int M,
-             int n, int per, float* a0, float* a1, const float* lse2, const int64_t* tgt, const float* rw) {
-  if (D == 128)
-    launch_all<128>(which, grid, s, Hb, Wb, bias, M, n, per, a0, a1, lse2, tgt, rw);
-  else if (D == 256)
-    launch_all<256>(which, grid, s, Hb, Wb, bias, M, n, per, a0, a1, lse2, tgt, rw);
-  else
-    return (int)hipErrorInvalidValue;
-  C2_CHECK_LAUNCH();
-  return 0;
-}
-
 int per_split(int total, int nsplit, int gran) {
   int tiles = c2::ceil_div(total, gran);
   return c2::ceil_div(tiles, nsplit) * gran;
@@ -551,64 +614,79 @@ C2_API int c2dsr_f32_to_bf16(const float* x, long n, void* y, void* stream) {
   return 0;
 }
 
-// forward: part_m/part_s [n_split][M] → (with pad logits, targets, fp32 H/W for the target logit)
-// lse, lse2 (= lse·log2e), loss_row [M].
-C2_API int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_split,
+C2_API int c2dsr_ce_bias2(const float* bias, int n, int n_pad, float* bias2, void* stream) {
+  bias2_kernel<<<c2::ceil_div(n_pad, 256), 256, 0, (hipStream_t)stream>>>(bias, n, n_pad, bias2);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// forward: part_m/part_s [n_split][M] → (with pad logits, targets, fp32 H/W/bias for the target
+// logit) lse, lse2 (= lse·log2e), loss_row [M].
+C2_API int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
                               float* part_m, float* part_s, const float* padlogit, const int64_t* tgt,
-                              const float* H, const float* W, float* lse, float* lse2, float* loss_row,
-                              void* stream) {
+                              const float* H, const float* W, const float* bias, float* lse, float* lse2,
+                              float* loss_row, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (M == 0) return 0;
   const int per = per_split(n, n_split, TILE);
   dim3 grid(c2::ceil_div(M, 256), n_split);
-  int e = launch_d(D, 0, grid, s, (const bf16*)Hb, (const bf16*)Wb, bias, M, n, per, part_m, part_s, nullptr, nullptr,
-                   nullptr);
-  if (e) return e;
+  if (D == 128)
+    ce_lse_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s);
+  else if (D == 256)
+    ce_lse_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s);
+  else
+    return (int)hipErrorInvalidValue;
   ce_rows_kernel<<<c2::ceil_div(M, 4), 256, 0, s>>>(part_m, part_s, n_split, M, padlogit, tgt, n, H, W, bias, D, lse,
                                                     lse2, loss_row);
   C2_CHECK_LAUNCH();
   return 0;
 }
 
-C2_API int c2dsr_ce_row_weights(const int64_t* tgt, int M, int ignore, const float* coef, int split,
+C2_API int c2dsr_ce_row_weights(const int64_t* tgt, int M, int M_pad, int ignore, const float* coef, int split,
                                 const float* gscale, float lam, const float* padlogit, const float* lse, float* rw,
-                                float* dpad, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  if (M == 0) return 0;
-  ce_roww_kernel<<<c2::ceil_div(M, 256), 256, 0, s>>>(tgt, M, ignore, coef, split, gscale, lam, rw);
-  ce_padgrad_kernel<<<c2::ceil_div(M, 256), 256, 0, s>>>(padlogit, lse, rw, M, dpad);
+                                int* t32, float* lse2, float* dpad, void* stream) {
+  if (M_pad == 0) return 0;
+  ce_roww_kernel<<<c2::ceil_div(M_pad, 256), 256, 0, (hipStream_t)stream>>>(tgt, M, M_pad, ignore, coef, split,
+                                                                             gscale, lam, padlogit, lse, rw, t32,
+                                                                             lse2, dpad);
   C2_CHECK_LAUNCH();
   return 0;
 }
 
-// dH = Σ_c P'[r][c] W[c]  → dH [M][D] (overwritten); dHp: [n_split][M][D] scratch
-C2_API int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_split,
-                             const float* lse2, const int64_t* tgt, const float* rw, float* dHp, float* dH,
-                             void* stream) {
+// dHp[s][r] = Σ_{c in split s} P'[r][c] W[c]  (combine with c2dsr_sum_parts)
+C2_API int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
+                             const float* lse2, const int* t32, const float* rw, float* dHp, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (M == 0) return 0;
   const int per = per_split(n, n_split, TILE);
   dim3 grid(c2::ceil_div(M, 128), n_split);
-  int e = launch_d(D, 1, grid, s, (const bf16*)Hb, (const bf16*)Wb, bias, M, n, per, dHp, nullptr, lse2, tgt, rw);
-  if (e) return e;
-  const long tot = (long)M * D;
-  sum_parts_kernel<<<c2::ceil_div(tot, 256), 256, 0, s>>>(dHp, n_split, tot, 0.f, dH);
+  if (D == 128)
+    ce_dh_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dHp);
+  else if (D == 256)
+    ce_dh_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dHp);
+  else
+    return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
   return 0;
 }
 
-// dWp[s][c] = Σ_{r in split s} P'[r][c] H[r];  dbp[s][c] = Σ_r P'[r][c]  (combine with c2dsr_sum_parts).
-C2_API int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_rsplit,
-                             const float* lse2, const int64_t* tgt, const float* rw, float* dWp, float* dbp,
-                             float* gW, float* gb, void* stream) {
+// dWp[s][c] = Σ_{r in split s} P'[r][c] H[r];  dbp[s][c] = Σ_r P'[r][c]  (combine with c2dsr_sum_parts)
+C2_API int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
+                             const float* lse2, const int* t32, const float* rw, float* dWp, float* dbp,
+                             void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return 0;
   const int per = per_split(M, n_rsplit, TILE);
   dim3 grid(c2::ceil_div(n, 128), n_rsplit);
-  int e = launch_d(D, 2, grid, s, (const bf16*)Hb, (const bf16*)Wb, bias, M, n, per, dWp, dbp, lse2, tgt, rw);
-  if (e) return e;
-  (void)gW;
-  (void)gb;
+  if (D == 128)
+    ce_dw_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dWp,
+                                           dbp);
+  else if (D == 256)
+    ce_dw_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dWp,
+                                           dbp);
+  else
+    return (int)hipErrorInvalidValue;
+  C2_CHECK_LAUNCH();
   return 0;
 }
 

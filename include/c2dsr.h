@@ -115,24 +115,26 @@ int c2dsr_scale_ds(float* ds, int n, const float* gscale, float f, void* stream)
 int c2dsr_rowscale(const float* x, const float* s, long n, int d, float* out, int accumulate, void* stream);
 
 /* K5 fused classifier head + cross-entropy (bf16 MFMA, logits never materialised; trainer.py:131-154).
- * Hb [M][D], Wb [n][D] bf16 (D = 128 or 256); bias [n] fp32.  Forward: lse, lse2 = lse·log2e and
- * loss_row over the n items + the pad column (padlogit), target logit from fp32 H/W. */
+ * Hb [M][D], Wb [n][D] bf16 (D = 128 or 256); bias2 = bias·log2e padded with -inf to n_pad (multiple of
+ * 128, c2dsr_ce_bias2).  Forward: lse, lse2 = lse·log2e, loss_row over the n items + the pad column
+ * (padlogit); the target logit is taken from fp32 H/W/bias. */
 int c2dsr_ce_supported(int D);
 int c2dsr_f32_to_bf16(const float* x, long n, void* y, void* stream);
-int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_split,
+int c2dsr_ce_bias2(const float* bias, int n, int n_pad, float* bias2, void* stream);
+int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
                        float* part_m, float* part_s, const float* padlogit, const int64_t* tgt, const float* H,
-                       const float* W, float* lse, float* lse2, float* loss_row, void* stream);
-/* rw[r] = valid ? gscale·lam·coef[r >= split] : 0;  dpad[r] = exp(padlogit - lse)·rw */
-int c2dsr_ce_row_weights(const int64_t* tgt, int M, int ignore, const float* coef, int split, const float* gscale,
-                         float lam, const float* padlogit, const float* lse, float* rw, float* dpad, void* stream);
-/* dH[r] = Σ_c P'[r][c]·W[c], P' = (softmax - onehot)·rw  (dHp: [n_split][M][D] scratch) */
-int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_split,
-                      const float* lse2, const int64_t* tgt, const float* rw, float* dHp, float* dH, void* stream);
-/* dWp[s][c] = Σ_{r∈split s} P'[r][c]·H[r];  dbp[s][c] = Σ_r P'[r][c]  (gW/gb unused: combine the
- * [n_rsplit][n][D] / [n_rsplit][n] partials with c2dsr_sum_parts) */
-int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias, int M, int n, int D, int n_rsplit,
-                      const float* lse2, const int64_t* tgt, const float* rw, float* dWp, float* dbp, float* gW,
-                      float* gb, void* stream);
+                       const float* W, const float* bias, float* lse, float* lse2, float* loss_row, void* stream);
+/* per row r < M_pad (multiple of 64): rw = valid ? gscale·lam·coef[r >= split] : 0, t32 = target (-1 pad),
+ * lse2 pads = 0, dpad = exp(padlogit - lse)·rw */
+int c2dsr_ce_row_weights(const int64_t* tgt, int M, int M_pad, int ignore, const float* coef, int split,
+                         const float* gscale, float lam, const float* padlogit, const float* lse, float* rw, int* t32,
+                         float* lse2, float* dpad, void* stream);
+/* dHp[s][r] = Σ_{c∈split s} P'[r][c]·W[c], P' = (softmax - onehot)·rw  ([n_split][M][D]; c2dsr_sum_parts) */
+int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
+                      const float* lse2, const int* t32, const float* rw, float* dHp, void* stream);
+/* dWp[s][c] = Σ_{r∈split s} P'[r][c]·H[r];  dbp[s][c] = Σ_r P'[r][c]  ([n_rsplit][n][D], [n_rsplit][n]) */
+int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
+                      const float* lse2, const int* t32, const float* rw, float* dWp, float* dbp, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
 int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */
