@@ -87,19 +87,24 @@ class LossHeadFn(Function):
             lse = torch.empty(2 * BR, **f32)
             rows = torch.empty(2 * BR, **f32)
             if fused:
-                Hb = torch.empty(2 * BR, d, device=dev, dtype=torch.bfloat16)
+                M2 = 2 * BR
+                M_pad = -(-M2 // 64) * 64
+                n_pad = -(-n // 128) * 128
+                Hb = torch.empty(M2, d, device=dev, dtype=torch.bfloat16)
                 Wb = torch.empty(n, d, device=dev, dtype=torch.bfloat16)
                 lib('c2dsr_f32_to_bf16', Hcat, Hcat.numel(), Hb, s)
                 lib('c2dsr_f32_to_bf16', W, W.numel(), Wb, s)
-                padlogit = torch.empty(2 * BR, **f32)
-                lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, 2 * BR, d, m.bpad, padlogit, 1, s)
-                ns = split_count(2 * BR, 256)
-                pm = torch.empty(ns, 2 * BR, **f32)
-                ps = torch.empty(ns, 2 * BR, **f32)
-                lse2 = torch.empty(2 * BR, **f32)
-                lib('c2dsr_ce_fused_fwd', Hb, Wb, bias, 2 * BR, n, d, ns, pm, ps, padlogit, tcat, Hcat, W, lse, lse2,
-                    rows, s)
-                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padlogit, lse2), lse, rows, W, bias, n))
+                bias2 = torch.empty(n_pad, **f32)
+                lib('c2dsr_ce_bias2', bias, n, n_pad, bias2, s)
+                padlogit = torch.empty(M2, **f32)
+                lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, M2, d, m.bpad, padlogit, 1, s)
+                ns = split_count(M2, 256)
+                pm = torch.empty(ns, M2, **f32)
+                ps = torch.empty(ns, M2, **f32)
+                lse2 = torch.empty(M_pad, **f32)
+                lib('c2dsr_ce_fused_fwd', Hb, Wb, bias2, M2, n, d, ns, pm, ps, padlogit, tcat, Hcat, W, bias, lse,
+                    lse2, rows, s)
+                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padlogit, lse2, bias2), lse, rows, W, bias, n))
             else:
                 ld = n + 1
                 logits = torch.empty(2 * BR, ld, **f32)
@@ -147,18 +152,22 @@ class LossHeadFn(Function):
             dHpad = torch.zeros(M2, d, **f32)
             gW, gb = _grad_target(W), _grad_target(bias)
             if ctx.fused:
-                Hb, Wb, padlogit, lse2 = logits
-                rw = torch.empty(M2, **f32)
+                Hb, Wb, padlogit, lse2, bias2 = logits
+                M_pad = lse2.shape[0]
+                rw = torch.empty(M_pad, **f32)
+                t32 = torch.empty(M_pad, device=dev, dtype=torch.int32)
                 dpad = torch.empty(M2, **f32)
-                lib('c2dsr_ce_row_weights', tcat, M2, n, coef, BR, gscale, float(m.lam), padlogit, lse, rw, dpad, s)
+                lib('c2dsr_ce_row_weights', tcat, M2, M_pad, n, coef, BR, gscale, float(m.lam), padlogit, lse, rw, t32,
+                    lse2, dpad, s)
                 ns = split_count(M2, 128)
                 dHp = torch.empty(ns, M2, d, **f32)
-                lib('c2dsr_ce_fused_dh', Hb, Wb, bias, M2, n, d, ns, lse2, tcat, rw, dHp, dHcat, s)
+                lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M2, n, d, ns, lse2, t32, rw, dHp, s)
+                lib('c2dsr_sum_parts', dHp, ns, M2 * d, 0.0, dHcat, s)
                 del dHp
                 nr = split_count(n, 128)
                 dWp = torch.empty(nr, n, d, **f32)
                 dbp = torch.empty(nr, n, **f32)
-                lib('c2dsr_ce_fused_dw', Hb, Wb, bias, M2, n, d, nr, lse2, tcat, rw, dWp, dbp, gW, gb, s)
+                lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M2, n, d, nr, lse2, t32, rw, dWp, dbp, s)
                 if gW is not None:
                     lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
                 if gb is not None:

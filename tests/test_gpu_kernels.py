@@ -270,9 +270,14 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     d = lambda x: x.to(DEV)  # noqa: E731
     Hb, Wb = d(H.to(torch.bfloat16)), d(W.to(torch.bfloat16))
     ns, nr = 3, 2
+    M_pad = -(-M // 64) * 64
+    n_pad = -(-n // 128) * 128
+    bias2 = torch.empty(n_pad, device=DEV)
+    lib('c2dsr_ce_bias2', d(b), n, n_pad, bias2, s)
     pm, ps = torch.empty(ns, M, device=DEV), torch.empty(ns, M, device=DEV)
-    lse, lse2, rows = (torch.empty(M, device=DEV) for _ in range(3))
-    lib('c2dsr_ce_fused_fwd', Hb, Wb, d(b), M, n, D, ns, pm, ps, d(pl), d(t), d(H), d(W), lse, lse2, rows, s)
+    lse, rows = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    lse2 = torch.empty(M_pad, device=DEV)
+    lib('c2dsr_ce_fused_fwd', Hb, Wb, bias2, M, n, D, ns, pm, ps, d(pl), d(t), d(H), d(W), d(b), lse, lse2, rows, s)
     # reference
     lg = torch.cat([H.double() @ W.double().T + b.double(), pl.double()[:, None]], 1)
     lse_r = torch.logsumexp(lg, 1)
@@ -280,22 +285,24 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     rows_r = torch.where(valid, lse_r - lg.gather(1, t[:, None])[:, 0], torch.zeros(M, dtype=torch.float64))
     assert rel(lse, lse_r) < 2e-5
     assert rel(rows, rows_r) < 1e-4
-    rw, dpad = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
-    lib('c2dsr_ce_row_weights', d(t), M, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, dpad, s)
+    rw, dpad = torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)
+    t32 = torch.empty(M_pad, device=DEV, dtype=torch.int32)
+    lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, t32, lse2, dpad, s)
     w_r = torch.where(valid, lam * coef[(torch.arange(M) >= BR).long()].double(), torch.zeros(M, dtype=torch.float64))
     P = torch.softmax(lg, 1)
     oh = torch.zeros_like(P)
     oh[torch.arange(M), t] = 1.0
     dl = (P - oh) * w_r[:, None]
-    assert rel(rw, w_r) < 1e-6 and rel(dpad, dl[:, n]) < 1e-4
+    assert rel(rw[:M], w_r) < 1e-6 and rel(dpad, dl[:, n]) < 1e-4
     dH = torch.empty(M, D, device=DEV)
     dHp = torch.empty(ns, M, D, device=DEV)
-    lib('c2dsr_ce_fused_dh', Hb, Wb, d(b), M, n, D, ns, lse2, d(t), rw, dHp, dH, s)
+    lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M, n, D, ns, lse2, t32, rw, dHp, s)
+    lib('c2dsr_sum_parts', dHp, ns, M * D, 0.0, dH, s)
     assert rel(dH, dl[:, :n] @ W.double()) < 1e-2
     gW = torch.ones(n, D, device=DEV)
     gb = torch.ones(n, device=DEV)
     dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
-    lib('c2dsr_ce_fused_dw', Hb, Wb, d(b), M, n, D, nr, lse2, d(t), rw, dWp, dbp, gW, gb, s)
+    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M, n, D, nr, lse2, t32, rw, dWp, dbp, s)
     lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     assert rel(gW - 1, dl[:, :n].T @ H.double()) < 1e-2
