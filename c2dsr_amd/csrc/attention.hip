@@ -259,6 +259,258 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__
   pv<LP, true>(Pd, dO, d, L, dh, Vs, dV, rs, 1.0f, LP);  // dV = Pdᵀ·dO
 }
 
+// ---------------------------------------------------------------------------------------
+// Register-streamed variant (LP = 32/64, dh % 4 == 0): no LDS staging of Q/K/V/dO at all.
+//  * score tiles (Q·Kᵀ, dO·Vᵀ): each wave owns one causal 32x32 tile (LP = 64: 3 tiles on
+//    waves 0-2) or a quarter of the head dim of the single tile (LP = 32, partials summed
+//    in LDS in a fixed order).  Operands come straight from HBM as float4 per lane: lane
+//    (r, hi) holds row r, columns 8c + 4hi .. +3, and MFMA step (c, e) consumes element e of
+//    both operands — any k-permutation works as long as A and B share it.  Chunks of 8
+//    c-steps are double-buffered in registers.
+//  * P·V-type products: each wave owns 32-column tiles of the output; the B operand
+//    (V / K / Q / dO rows, 128 contiguous bytes per half-wave) is preloaded for every k-step
+//    before the MFMA chain; A (probabilities / dS) is read from LDS.
+//  * key range: every column j >= jmax (one past the last padding key) is masked for every
+//    query, so the k-loops of the P·V and dS·K products stop at jmax (exact: those P are 0).
+// ---------------------------------------------------------------------------------------
+template <int LP>
+struct Fast {
+  static constexpr int NT = LP / 32;
+  static constexpr int T = NT * (NT + 1) / 2;  // causal tiles
+  static constexpr int KS = 4 / T;             // head-dim split per tile
+  static constexpr int SLD = LP + 1;
+};
+
+__device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
+  // causal tiles in order (0,0), (1,0), (1,1)
+  ti = t == 0 ? 0 : 1;
+  tj = t == 2 ? 1 : 0;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p, bool ok) {
+  return ok ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Raw (unscaled, unmasked) X·Yᵀ tiles into S[LP][SLD]; tiles never computed are left untouched.
+// part: LDS scratch of 4*1024 floats (used only when KS > 1).
+template <int LP>
+__device__ void scores_fast(const float* __restrict__ X, long xs, const float* __restrict__ Y, long ys, int L, int dh,
+                            int jmax, float* S, float* part) {
+  using F = Fast<LP>;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, r = lane & 31, hi = lane >> 5;
+  const int tile = w / F::KS, kp = w % F::KS;
+  int ti = 0, tj = 0;
+  tile_of(tile, ti, tj);
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  const bool active = tile < F::T && tj * 32 < jmax;
+  if (active) {
+    const int CS = (dh + 7) >> 3;  // c-steps of 8 columns
+    const int cb = kp * CS / F::KS, ce = (kp + 1) * CS / F::KS;
+    const int xr = ti * 32 + r, yr = tj * 32 + r;
+    const bool xok = xr < L, yok = yr < jmax;
+    const float* xp = X + (long)xr * xs + 4 * hi;
+    const float* yp = Y + (long)yr * ys + 4 * hi;
+    float4 xa[8], ya[8], xb[8], yb[8];
+    auto load = [&](float4 (&xv)[8], float4 (&yv)[8], int c0) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int col = 8 * (c0 + c) + 4 * hi;
+        const bool cok = c0 + c < ce && col < dh;
+        xv[c] = ld4(xp + 8 * (c0 + c), xok && cok);
+        yv[c] = ld4(yp + 8 * (c0 + c), yok && cok);
+      }
+    };
+    auto mma = [&](const float4 (&xv)[8], const float4 (&yv)[8]) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[c].x, yv[c].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[c].y, yv[c].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[c].z, yv[c].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[c].w, yv[c].w, acc, 0, 0, 0);
+      }
+    };
+    load(xa, ya, cb);
+    for (int c0 = cb; c0 < ce; c0 += 16) {
+      if (c0 + 8 < ce) load(xb, yb, c0 + 8);
+      mma(xa, ya);
+      if (c0 + 8 >= ce) break;
+      if (c0 + 16 < ce) load(xa, ya, c0 + 16);
+      mma(xb, yb);
+    }
+  }
+  if constexpr (F::KS == 1) {
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) S[(ti * 32 + creg(q, lane)) * F::SLD + tj * 32 + r] = acc[q];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) part[w * 1024 + q * 64 + lane] = acc[q];
+    __syncthreads();
+    for (int e = t; e < 1024; e += 256) {
+      const int q = e >> 6, ln = e & 63;
+      const float v = (part[e] + part[1024 + e]) + (part[2048 + e] + part[3072 + e]);
+      S[creg(q, ln) * F::SLD + (ln & 31)] = v;
+      (void)q;
+    }
+  }
+}
+
+// out[i][c] = scale * Σ_{k < kend} A[i][k] * Y[k][c]  for i < rows, c < dh (all of them written).
+// A in LDS: A[i][k] = As[i*SLD + k], or As[k*SLD + i] when TRANS.  Y: global rows of stride ys.
+template <int LP, bool TRANS>
+__device__ void pv_fast(const float* As, const float* __restrict__ Y, long ys, int rows, int dh, int kend,
+                        float* __restrict__ out, long os, float scale) {
+  using F = Fast<LP>;
+  constexpr int KMAX = LP / 2;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, r = lane & 31, hi = lane >> 5;
+  const int CT = (dh + 31) >> 5;
+  const int ksteps = (kend + 1) >> 1;
+  for (int ct = w; ct < CT; ct += 4) {
+    const int c = ct * 32 + r;
+    const bool cok = c < dh;
+    float bv[KMAX];
+#pragma unroll
+    for (int ks = 0; ks < KMAX; ++ks) {
+      const int k = 2 * ks + hi;
+      bv[ks] = (ks < ksteps && k < kend && cok) ? Y[(long)k * ys + c] : 0.f;
+    }
+    f32x16 acc[F::NT];
+#pragma unroll
+    for (int ti = 0; ti < F::NT; ++ti)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[ti][i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KMAX; ++ks) {
+      if (ks < ksteps) {
+        const int k = 2 * ks + hi;
+#pragma unroll
+        for (int ti = 0; ti < F::NT; ++ti) {
+          const int i = ti * 32 + r;
+          const float a = TRANS ? As[k * F::SLD + i] : As[i * F::SLD + k];
+          acc[ti] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv[ks], acc[ti], 0, 0, 0);
+        }
+      }
+    }
+    if (cok) {
+#pragma unroll
+      for (int ti = 0; ti < F::NT; ++ti)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = ti * 32 + creg(q, lane);
+          if (i < rows) out[(long)i * os + c] = scale * acc[ti][q];
+        }
+    }
+  }
+}
+
+// padding keys of sequence b: keyok[j], and jmax = 1 + last padding position (0 if none)
+template <int LP>
+__device__ int key_setup(const int64_t* __restrict__ seq, int64_t pad, int b, int L, unsigned char* keyok) {
+  const int t = threadIdx.x;
+  __shared__ int jm;
+  if (t == 0) jm = 0;
+  __syncthreads();
+  if (t < LP) {
+    const bool ok = t < L && seq[(long)b * L + t] == pad;
+    keyok[t] = ok;
+    if (ok) atomicMax(&jm, t + 1);
+  }
+  __syncthreads();
+  return jm;
+}
+
+template <int LP>
+__global__ __launch_bounds__(256, 2) void attn_fwd_fast(const float* __restrict__ qkv,
+                                                        const int64_t* __restrict__ seq, int64_t pad, int L, int d,
+                                                        int H, c2::Drop drop, int64_t b_base,
+                                                        float* __restrict__ out, float* __restrict__ Psave) {
+  using F = Fast<LP>;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int dh = d / H;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  __shared__ float Ss[LP * F::SLD];
+  __shared__ float part[F::KS > 1 ? 4 * 1024 : 1];
+  __shared__ unsigned char keyok[LP];
+  const int jmax = key_setup<LP>(seq, pad, b, L, keyok);
+  const long rs = 3l * d;
+  const float* Q = qkv + (long)b * L * rs + h * dh;
+  const float* K = Q + d;
+  const float* V = Q + 2 * d;
+  scores_fast<LP>(Q, rs, K, rs, L, dh, jmax, Ss, part);
+  __syncthreads();
+  const float sc = 1.0f / sqrtf((float)dh);
+  for (int i = w; i < LP; i += 4) {
+    const int j = lane;
+    const bool adm = i < L && j < LP && j <= i && j < jmax && keyok[j];
+    const float sv = adm ? Ss[i * F::SLD + j] * sc : -INFINITY;
+    const float m = c2::wave_max(sv);
+    const float e = (adm && m != -INFINITY) ? __expf(sv - m) : 0.f;
+    const float s = c2::wave_sum(e);
+    const float pv_ = s > 0.f ? e * (1.0f / s) : 0.f;
+    if (i < L && j < L) {
+      Psave[((long)blockIdx.x * L + i) * L + j] = pv_;
+      const uint64_t idx = ((uint64_t)((b_base + b) * H + h) * L + i) * L + j;
+      if (j < LP) Ss[i * F::SLD + j] = pv_ * drop.mul(idx);
+    } else if (j < LP) {
+      Ss[i * F::SLD + j] = 0.f;
+    }
+  }
+  __syncthreads();
+  pv_fast<LP, false>(Ss, V, rs, L, dh, jmax, out + (long)b * L * d + h * dh, d, 1.0f);
+}
+
+template <int LP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_fast(const float* __restrict__ qkv,
+                                                        const int64_t* __restrict__ seq, int64_t pad, int L, int d,
+                                                        int H, c2::Drop drop, int64_t b_base,
+                                                        const float* __restrict__ Psave,
+                                                        const float* __restrict__ dout, float* __restrict__ dqkv) {
+  using F = Fast<LP>;
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int dh = d / H;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  __shared__ float Pd[LP * F::SLD];
+  __shared__ float dS[LP * F::SLD];
+  __shared__ float part[F::KS > 1 ? 4 * 1024 : 1];
+  __shared__ unsigned char keyok[LP];
+  const int jmax = key_setup<LP>(seq, pad, b, L, keyok);
+  const long rs = 3l * d;
+  const float* Q = qkv + (long)b * L * rs + h * dh;
+  const float* K = Q + d;
+  const float* V = Q + 2 * d;
+  const float* dO = dout + (long)b * L * d + h * dh;
+  float* dQ = dqkv + (long)b * L * rs + h * dh;
+  float* dK = dQ + d;
+  float* dV = dQ + 2 * d;
+  const float* Pg = Psave + (long)blockIdx.x * L * L;
+  scores_fast<LP>(dO, d, V, rs, L, dh, jmax, dS, part);  // dPd = dO·Vᵀ (admissible tiles)
+  __syncthreads();
+  // dP = dPd ⊙ mask/(1-p); Pd = P ⊙ mask/(1-p); dS = P ⊙ (dP - Σ_j P·dP)
+  for (int i = w; i < LP; i += 4) {
+    const int j = lane;
+    float p = 0.f, dp = 0.f, pd = 0.f;
+    if (i < L && j < L) {
+      p = Pg[(long)i * L + j];
+      const float mk = drop.mul(((uint64_t)((b_base + b) * H + h) * L + i) * L + j);
+      pd = p * mk;
+      if (j <= i && j < jmax && keyok[j]) dp = dS[i * F::SLD + j] * mk;
+    }
+    const float s = c2::wave_sum(p * dp);
+    if (j < LP) {
+      Pd[i * F::SLD + j] = pd;
+      dS[i * F::SLD + j] = p * (dp - s);
+    }
+  }
+  __syncthreads();
+  const float sc = 1.0f / sqrtf((float)dh);
+  pv_fast<LP, false>(dS, K, rs, L, dh, jmax, dQ, rs, sc);  // dQ = dS·K/√dh
+  pv_fast<LP, true>(dS, Q, rs, L, dh, L, dK, rs, sc);      // dK = dSᵀ·Q/√dh
+  pv_fast<LP, true>(Pd, dO, d, L, dh, L, dV, rs, 1.0f);    // dV = Pdᵀ·dO
+}
+
 template <int LP>
 size_t fwd_smem() { return sizeof(float) * ((size_t)LP * Smem<LP>::SLD + Smem<LP>::STAGE); }
 template <int LP>
@@ -300,7 +552,12 @@ C2_API int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
-  if (L <= 32)
+  const bool fast = (d / H) % 4 == 0 && d % 4 == 0;
+  if (fast && L <= 32)
+    attn_fwd_fast<32><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
+  else if (fast && L <= 64)
+    attn_fwd_fast<64><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
+  else if (L <= 32)
     launch_fwd<32>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
   else if (L <= 64)
     launch_fwd<64>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
@@ -318,7 +575,12 @@ C2_API int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
-  if (L <= 32)
+  const bool fast = (d / H) % 4 == 0 && d % 4 == 0;
+  if (fast && L <= 32)
+    attn_bwd_fast<32><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
+  else if (fast && L <= 64)
+    attn_bwd_fast<64><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
+  else if (L <= 32)
     launch_bwd<32>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
   else if (L <= 64)
     launch_bwd<64>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);

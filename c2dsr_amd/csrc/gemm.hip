@@ -212,34 +212,46 @@ __global__ void scale_kernel(float* __restrict__ C, int M, int N, int ldc, float
 }
 
 // colsum: out[n] = beta*out[n] + alpha * Σ_m X[m*ldx + n]  (bias gradients).
-// Stage 1: chunks of CS_ROWS rows x 256 columns per block, one column per thread
-// (coalesced row reads) → part[chunk][n]; stage 2 sums the chunks in order.
-constexpr int CS_ROWS = 128;
+// Stage 1: a 64-column x CS_ROWS-row block per workgroup (4 waves interleaved over rows,
+// each wave reading 256 contiguous bytes per row) → part[chunk][n]; stage 2: 16 wave groups
+// per 64 columns sum the chunks, combined in a fixed order (deterministic).
+constexpr int CS_ROWS = 256;
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ X, int M, int N, long ldx,
-                                                          int rows, float* __restrict__ part) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+                                                          float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   const int chunk = blockIdx.y;
-  if (c >= N) return;
-  const int r0 = chunk * rows, r1 = min(M, r0 + rows);
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int r = r0;
-  for (; r + 3 < r1; r += 4) {
-    s0 += X[(long)r * ldx + c];
-    s1 += X[(long)(r + 1) * ldx + c];
-    s2 += X[(long)(r + 2) * ldx + c];
-    s3 += X[(long)(r + 3) * ldx + c];
+  const int r0 = chunk * CS_ROWS, r1 = min(M, r0 + CS_ROWS);
+  float s0 = 0.f, s1 = 0.f;
+  if (c < N) {
+    int r = r0 + q;
+    for (; r + 4 < r1; r += 8) {
+      s0 += X[(long)r * ldx + c];
+      s1 += X[(long)(r + 4) * ldx + c];
+    }
+    if (r < r1) s0 += X[(long)r * ldx + c];
   }
-  for (; r < r1; ++r) s0 += X[(long)r * ldx + c];
-  part[(long)chunk * N + c] = (s0 + s1) + (s2 + s3);
+  red[q][cl] = s0 + s1;
+  __syncthreads();
+  if (q == 0 && c < N) part[(long)chunk * N + c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
-                                                           float alpha, float beta, float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restrict__ part, int chunks, int N,
+                                                            float alpha, float beta, float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float t = 0.f;
-  for (int k = 0; k < chunks; ++k) t += part[(long)k * N + c];
-  out[c] = (beta == 0.f ? 0.f : beta * out[c]) + alpha * t;
+  if (c < N)
+    for (int k = q; k < chunks; k += 16) t += part[(long)k * N + c];
+  red[q][cl] = t;
+  __syncthreads();
+  if (q == 0 && c < N) {
+    float s = 0.f;
+    for (int k = 0; k < 16; ++k) s += red[k][cl];
+    out[c] = (beta == 0.f ? 0.f : beta * out[c]) + alpha * s;
+  }
 }
 
 template <bool BF16, bool TA, bool TB>
@@ -311,25 +323,19 @@ C2_API int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* 
   return 0;
 }
 
-// rows per stage-1 chunk: at least CS_ROWS, and few enough chunks (<= 64) for a short stage 2
-inline int cs_rows(int M) { return c2::ceil_div(c2::ceil_div(M, 64), CS_ROWS) * CS_ROWS; }
-
-C2_API size_t c2dsr_colsum_workspace(int M, int N) {
-  return (size_t)c2::ceil_div(M, cs_rows(M)) * (size_t)N * 4 + 256;
-}
+C2_API size_t c2dsr_colsum_workspace(int M, int N) { return (size_t)c2::ceil_div(M, CS_ROWS) * (size_t)N * 4 + 256; }
 
 C2_API int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* workspace,
                         void* stream) {
   if (N <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int rows = cs_rows(M);
-  const int chunks = c2::ceil_div(M, rows);
+  const int chunks = c2::ceil_div(M, CS_ROWS);
   float* part = (float*)workspace;
   if (chunks > 0) {
-    dim3 g1(c2::ceil_div(N, 256), chunks);
-    colsum_part_kernel<<<g1, 256, 0, s>>>(X, M, N, ldx, rows, part);
+    dim3 g1(c2::ceil_div(N, 64), chunks);
+    colsum_part_kernel<<<g1, 256, 0, s>>>(X, M, N, ldx, part);
   }
-  colsum_final_kernel<<<c2::ceil_div(N, 256), 256, 0, s>>>(part, chunks, N, alpha, beta, out);
+  colsum_final_kernel<<<c2::ceil_div(N, 64), 1024, 0, s>>>(part, chunks, N, alpha, beta, out);
   C2_CHECK_LAUNCH();
   return 0;
 }
