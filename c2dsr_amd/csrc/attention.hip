@@ -34,7 +34,7 @@ struct Smem {
 // acc (32x32 tile (ti, tj) of X·Yᵀ over the head dim, X/Y rows = sequence positions) —
 // each wave owns tiles w, w+4, ... of the (LP/32)^2 grid.  X, Y: global rows of stride xs/ys.
 template <int LP>
-__device__ void xyT(const float* __restrict__ X, long xs, const float* __restrict__ Y, long ys, int L, int dh,
+__device__ __forceinline__ void xyT(const float* __restrict__ X, long xs, const float* __restrict__ Y, long ys, int L, int dh,
                     float* Xs, float* Ys, f32x16 (&acc)[(LP / 32) * (LP / 32) / 4 > 0 ? (LP / 32) * (LP / 32) / 4 : 1]) {
   constexpr int NT = LP / 32;
   constexpr int XLD = Smem<LP>::XLD;
@@ -74,7 +74,7 @@ __device__ void xyT(const float* __restrict__ X, long xs, const float* __restric
 // transposed: A[i][j] = As[j][i]); Y global rows (stride ys).  Each wave: 32 output columns of
 // a CC-wide chunk, all LP rows.
 template <int LP, bool TRANS_A>
-__device__ void pv(const float* As, const float* __restrict__ Y, long ys, int L, int dh, float* Vs,
+__device__ __forceinline__ void pv(const float* As, const float* __restrict__ Y, long ys, int L, int dh, float* Vs,
                    float* __restrict__ out, long os, float scale, int jmax) {
   constexpr int NT = LP / 32;
   constexpr int SLD = Smem<LP>::SLD;
@@ -287,14 +287,19 @@ __device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
   tj = t == 2 ? 1 : 0;
 }
 
-__device__ __forceinline__ float4 ld4(const float* p, bool ok) {
-  return ok ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+// buffer descriptor over rows [0, rows) of a row-major fp32 matrix (row stride `stride` floats)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base, int rows, long stride) {
+  const int bytes = __builtin_amdgcn_readfirstlane(rows * (int)stride * 4);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 ld_b128(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
 // Raw (unscaled, unmasked) X·Yᵀ tiles into S[LP][SLD]; tiles never computed are left untouched.
 // part: LDS scratch of 4*1024 floats (used only when KS > 1).
 template <int LP>
-__device__ void scores_fast(const float* __restrict__ X, long xs, const float* __restrict__ Y, long ys, int L, int dh,
+__device__ __forceinline__ void scores_fast(const float* __restrict__ X, long xs, const float* __restrict__ Y, long ys, int L, int dh,
                             int jmax, float* S, float* part) {
   using F = Fast<LP>;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63, r = lane & 31, hi = lane >> 5;
@@ -308,18 +313,21 @@ __device__ void scores_fast(const float* __restrict__ X, long xs, const float* _
   if (active) {
     const int CS = (dh + 7) >> 3;  // c-steps of 8 columns
     const int cb = kp * CS / F::KS, ce = (kp + 1) * CS / F::KS;
-    const int xr = ti * 32 + r, yr = tj * 32 + r;
-    const bool xok = xr < L, yok = yr < jmax;
-    const float* xp = X + (long)xr * xs + 4 * hi;
-    const float* yp = Y + (long)yr * ys + 4 * hi;
+    // buffer loads: rows past L (X) or jmax (Y) fall outside the descriptor and read 0
+    const auto xsrc = rows_rsrc(X, L, xs);
+    const auto ysrc = rows_rsrc(Y, jmax, ys);
+    const int xo = ((ti * 32 + r) * (int)xs + 4 * hi) * 4;
+    const int yo = ((tj * 32 + r) * (int)ys + 4 * hi) * 4;
+    const int cmax = (dh - 4 * hi - 4) >> 3;  // last c-step whose columns are inside the head
     float4 xa[8], ya[8], xb[8], yb[8];
     auto load = [&](float4 (&xv)[8], float4 (&yv)[8], int c0) {
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const int col = 8 * (c0 + c) + 4 * hi;
-        const bool cok = c0 + c < ce && col < dh;
-        xv[c] = ld4(xp + 8 * (c0 + c), xok && cok);
-        yv[c] = ld4(yp + 8 * (c0 + c), yok && cok);
+        const bool cok = c0 + c < ce && c0 + c <= cmax;
+        const float4 xv_ = ld_b128(xsrc, xo + 32 * c, 32 * c0);
+        const float4 yv_ = ld_b128(ysrc, yo + 32 * c, 32 * c0);
+        xv[c] = cok ? xv_ : make_float4(0.f, 0.f, 0.f, 0.f);
+        yv[c] = cok ? yv_ : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     };
     auto mma = [&](const float4 (&xv)[8], const float4 (&yv)[8]) {
@@ -361,7 +369,7 @@ __device__ void scores_fast(const float* __restrict__ X, long xs, const float* _
 // out[i][c] = scale * Σ_{k < kend} A[i][k] * Y[k][c]  for i < rows, c < dh (all of them written).
 // A in LDS: A[i][k] = As[i*SLD + k], or As[k*SLD + i] when TRANS.  Y: global rows of stride ys.
 template <int LP, bool TRANS>
-__device__ void pv_fast(const float* As, const float* __restrict__ Y, long ys, int rows, int dh, int kend,
+__device__ __forceinline__ void pv_fast(const float* As, const float* __restrict__ Y, long ys, int rows, int dh, int kend,
                         float* __restrict__ out, long os, float scale) {
   using F = Fast<LP>;
   constexpr int KMAX = LP / 2;
@@ -372,10 +380,12 @@ __device__ void pv_fast(const float* As, const float* __restrict__ Y, long ys, i
     const int c = ct * 32 + r;
     const bool cok = c < dh;
     float bv[KMAX];
+    const auto ysrc = rows_rsrc(Y, kend, ys);  // rows >= kend read 0
+    const int yo = (hi * (int)ys + c) * 4;
 #pragma unroll
     for (int ks = 0; ks < KMAX; ++ks) {
-      const int k = 2 * ks + hi;
-      bv[ks] = (ks < ksteps && k < kend && cok) ? Y[(long)k * ys + c] : 0.f;
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ysrc, yo, 8 * ks * (int)ys, 0));
+      bv[ks] = cok ? v : 0.f;
     }
     f32x16 acc[F::NT];
 #pragma unroll
@@ -408,7 +418,7 @@ __device__ void pv_fast(const float* As, const float* __restrict__ Y, long ys, i
 
 // padding keys of sequence b: keyok[j], and jmax = 1 + last padding position (0 if none)
 template <int LP>
-__device__ int key_setup(const int64_t* __restrict__ seq, int64_t pad, int b, int L, unsigned char* keyok) {
+__device__ __forceinline__ int key_setup(const int64_t* __restrict__ seq, int64_t pad, int b, int L, unsigned char* keyok) {
   const int t = threadIdx.x;
   __shared__ int jm;
   if (t == 0) jm = 0;
