@@ -23,6 +23,21 @@ from .models.C2DSR import C2DSR
 from .optim import FlatAdamW
 
 
+def dp_rows(B_full, rank, world, dp_split=True, global_rows=None):
+    """Rows of a batch this rank trains and where they sit in the global batch.
+
+    dp_split: rank r takes rows [r·⌈B/p⌉, (r+1)·⌈B/p⌉) of the SAME global batch (p ranks reproduce the
+    single-device step); otherwise every rank trains its own batch of B rows (weak scaling), placed at
+    global rows [r·B, (r+1)·B).  Returns (lo, hi, row_offset, B_global); row_offset feeds the dropout
+    index so every rank drops exactly what one device would."""
+    if world > 1 and dp_split:
+        per = (B_full + world - 1) // world
+        lo, hi = min(B_full, rank * per), min(B_full, (rank + 1) * per)
+        return lo, hi, lo, B_full
+    B_global = global_rows if global_rows is not None else B_full * world
+    return 0, B_full, rank * B_full if world > 1 else 0, B_global
+
+
 def dp_info():
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         return dist.get_rank(), dist.get_world_size()
@@ -95,13 +110,6 @@ class Trainer(object):
         w = m / m.sum(-1, keepdim=True)
         return w.unsqueeze(-1).repeat(1, 1, self.d_latent)
 
-    def _local(self, t):
-        if self.world == 1 or not self.dp_split:
-            return t
-        B = t.shape[0]
-        per = (B + self.world - 1) // self.world
-        return t[self.rank * per:min(B, (self.rank + 1) * per)]
-
     def loss_meta(self, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global):
         m = self.model
         allreduce = None
@@ -118,16 +126,9 @@ class Trainer(object):
         """trainer.py:91-160.  ``batch``: 14 int64 [B, L] tensors (host or device).  Under data
         parallelism each rank trains its slice of the global batch (or, with ``dp_split=False``, its
         own batch; ``global_rows`` then gives the global batch size)."""
-        B_full = batch[0].shape[0]
-        if self.world > 1 and self.dp_split:
-            per = (B_full + self.world - 1) // self.world
-            row_offset = self.rank * per
-            B_global = B_full
-        else:
-            row_offset = self.rank * B_full if self.world > 1 else 0
-            B_global = global_rows if global_rows is not None else B_full * self.world
+        lo, hi, row_offset, B_global = dp_rows(batch[0].shape[0], self.rank, self.world, self.dp_split, global_rows)
         (seq_share, seq_a, seq_b, pos, pos_a, pos_b, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, neg_a,
-         neg_b) = [self._local(x).to(self.device, non_blocking=True) for x in batch]
+         neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
         m = self.model
         m.state.row_offset = row_offset
         h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)

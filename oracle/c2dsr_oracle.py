@@ -217,20 +217,33 @@ def bilinear(x1, x2, W, b):
     return out + b if b is not None else out
 
 
-def bce_logits(s, y):
-    return (torch.clamp(s, min=0) - s * y + torch.log1p(torch.exp(-s.abs()))).mean()
+def bce_logits(s, y, denom=None):
+    v = torch.clamp(s, min=0) - s * y + torch.log1p(torch.exp(-s.abs()))
+    return v.mean() if denom is None else v.sum() / denom
 
 
-def cross_entropy(logits, tgt, ignore):
+def cross_entropy(logits, tgt, ignore, denom=None):
     valid = tgt != ignore
     lse = torch.logsumexp(logits, -1)
     t = torch.where(valid, tgt, torch.zeros_like(tgt))
     picked = logits.gather(1, t[:, None])[:, 0]
-    return ((lse - picked) * valid).sum() / valid.sum()
+    return ((lse - picked) * valid).sum() / (valid.sum() if denom is None else denom)
 
 
-def train_forward(P, graphs, batch, cfg, dropper):
-    """trainer.py:91-156 (+ C2DSR.forward / forward_share).  Returns dict of tensors."""
+def loss_counts(batch, cfg):
+    """Local counts the loss normalises by: B and the valid targets of the four heads (trainer.py:131-154)."""
+    gt_sa, gt_sb, gt_a, gt_b = batch[6], batch[7], batch[8], batch[9]
+    n_a, n_b, R = cfg['n_item_a'], cfg['n_item_b'], cfg['len_rec']
+    return torch.tensor([gt_sa.shape[0], (gt_sa[:, -R:] != n_a).sum(), (gt_sb[:, -R:] != n_b).sum(),
+                         (gt_a[:, -R:] != n_a).sum(), (gt_b[:, -R:] != n_b).sum()], dtype=torch.float64)
+
+
+def train_forward(P, graphs, batch, cfg, dropper, counts=None):
+    """trainer.py:91-156 (+ C2DSR.forward / forward_share).  Returns dict of tensors.
+
+    ``counts`` (data parallelism): the GLOBAL [B, #valid_sa, #valid_sb, #valid_a,
+    #valid_b] of the whole batch this rank holds a slice of.  Every mean then divides the local sum by
+    the global count, so the per-rank losses (and gradients) sum over ranks to the single-device ones."""
     (seq, seq_a, seq_b, pos, pos_a, pos_b, gt_sa, gt_sb, gt_a, gt_b, gm_a, gm_b, neg_a, neg_b) = batch
     es, ea, eb = embed_names(cfg)
     n_a, n_b, R = cfg['n_item_a'], cfg['n_item_b'], cfg['len_rec']
@@ -259,8 +272,9 @@ def train_forward(P, graphs, batch, cfg, dropper):
     out['sim_b'] = torch.stack([sim_b_pos, sim_b_neg])
     one = torch.ones(B, 1)
     zero = torch.zeros(B, 1)
-    loss_mi = bce_logits(sim_a_pos, one) + bce_logits(sim_a_neg, zero) + \
-        bce_logits(sim_b_pos, one) + bce_logits(sim_b_neg, zero)
+    cB = None if counts is None else float(counts[0])
+    loss_mi = bce_logits(sim_a_pos, one, cB) + bce_logits(sim_a_neg, zero, cB) + \
+        bce_logits(sim_b_pos, one, cB) + bce_logits(sim_b_neg, zero, cB)
 
     hs_r, ha_r, hb_r = h_share[:, -R:], hx[:, -R:], hy[:, -R:]
 
@@ -276,11 +290,19 @@ def train_forward(P, graphs, batch, cfg, dropper):
     s_b = head(hs_r + hb_r, Wb, bb, hb_r).reshape(-1, n_b + 1)
     t_sa, t_sb = gt_sa[:, -R:].reshape(-1), gt_sb[:, -R:].reshape(-1)
     t_a, t_b = gt_a[:, -R:].reshape(-1), gt_b[:, -R:].reshape(-1)
-    l_sa = cross_entropy(s_sa, t_sa, n_a)
-    l_sb = cross_entropy(s_sb, t_sb, n_b)
-    loss_share = l_sa * (t_sa != n_a).sum() / (R * B) + l_sb * (t_sb != n_b).sum() / (R * B)
-    l_a = cross_entropy(s_a, t_a, n_a)
-    l_b = cross_entropy(s_b, t_b, n_b)
+    if counts is None:
+        l_sa = cross_entropy(s_sa, t_sa, n_a)
+        l_sb = cross_entropy(s_sb, t_sb, n_b)
+        loss_share = l_sa * (t_sa != n_a).sum() / (R * B) + l_sb * (t_sb != n_b).sum() / (R * B)
+        l_a = cross_entropy(s_a, t_a, n_a)
+        l_b = cross_entropy(s_b, t_b, n_b)
+    else:
+        c = [float(x) for x in counts]
+        l_sa = cross_entropy(s_sa, t_sa, n_a, c[1])
+        l_sb = cross_entropy(s_sb, t_sb, n_b, c[2])
+        loss_share = l_sa * c[1] / (R * c[0]) + l_sb * c[2] / (R * c[0])
+        l_a = cross_entropy(s_a, t_a, n_a, c[3])
+        l_b = cross_entropy(s_b, t_b, n_b, c[4])
     loss_rec = loss_share + l_a + l_b
     lam = cfg['lambda_loss']
     loss = lam * loss_rec + (1 - lam) * loss_mi
@@ -341,11 +363,11 @@ class OracleTrainer:
     def zero_grad(self):
         self.grads = {n: None for n in self.names}
 
-    def train_batch(self, batch, row_offset=0, optimizer=True):
+    def train_batch(self, batch, row_offset=0, optimizer=True, counts=None):
         for n in self.names:
             self.P[n].requires_grad_(True)
         dr = Dropper(self.cfg['dropout_gnn'], self.cfg['dropout_attn'], self.seed, self.step_no, row_offset)
-        out = train_forward(self.P, self.graphs, batch, self.cfg, dr)
+        out = train_forward(self.P, self.graphs, batch, self.cfg, dr, counts)
         gs = torch.autograd.grad(out['loss'], [self.P[n] for n in self.names], allow_unused=True)
         for n, g in zip(self.names, gs):
             if g is None:
