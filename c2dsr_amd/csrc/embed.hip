@@ -150,7 +150,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
 }
 
 // ------------------------------------------------------------------ segment reduce
-constexpr int SEG_CH = 64;
+constexpr int SEG_CH = 32;
 
 struct RowSrc {
   const float* gX;
@@ -169,49 +169,69 @@ struct RowSrc {
 };
 
 // pass A: every chunk of SEG_CH sorted entries sums its runs; whole runs go straight to
-// out[key] (+=), runs cut by a chunk edge go to head/tail partial slots.
+// out[key] (+=), runs cut by a chunk edge go to head/tail partial slots.  The block stages
+// its keys and row ids in LDS first (no dependent global loads in the run walk); each
+// lane group streams its chunk's rows four at a time.
 template <int LPR>
 __global__ __launch_bounds__(256) void seg_reduce_a(const uint32_t* __restrict__ K, const uint32_t* __restrict__ V,
                                                     int n, RowSrc src, float* __restrict__ out,
                                                     float* __restrict__ part_head, float* __restrict__ part_tail,
                                                     int skip_key) {
   constexpr int GROUPS = 256 / LPR;
+  constexpr int ENT = GROUPS * SEG_CH;
+  __shared__ uint32_t sk[ENT + 2];  // sk[e + 1] = K[b0 + e]; sk[0], sk[ENT + 1]: the neighbours
+  __shared__ uint32_t sv[ENT];
+  const long b0 = (long)blockIdx.x * ENT;
+  for (int e = threadIdx.x; e < ENT + 2; e += 256) {
+    const long gi = b0 - 1 + e;
+    sk[e] = (gi >= 0 && gi < n) ? K[gi] : 0xffffffffu;
+  }
+  for (int e = threadIdx.x; e < ENT; e += 256) {
+    const long gi = b0 + e;
+    sv[e] = gi < n ? V[gi] : 0u;
+  }
+  __syncthreads();
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
   const long chunk = (long)blockIdx.x * GROUPS + g;
   const long start = chunk * SEG_CH;
   if (start >= n) return;
-  const long end = min((long)n, start + SEG_CH);
+  const int cnt = (int)min((long)SEG_CH, n - start);
+  const int o = g * SEG_CH;
+  const bool cont_head = start > 0 && sk[o] == sk[o + 1];
+  const bool cont_tail = start + cnt < n && sk[o + cnt + 1] == sk[o + cnt];
   const int d = src.d;
-  const bool cont_head = start > 0 && K[start - 1] == K[start];
-  long i = start;
-  while (i < end) {
-    const uint32_t key = K[i];
-    long j = i;
-    while (j < end && K[j] == key) ++j;
-    const bool is_head = (i == start) && cont_head;
-    const bool is_tail = (j == end) && (end < n) && (K[end] == key);
-    float* dst;
-    bool accumulate = false;
-    if (!is_head && !is_tail) {
-      if ((int)key == skip_key) {
-        i = j;
-        continue;
+  for (int c = lane * 4; c < d; c += LPR * 4) {
+    float4 acc = c2::f4(0.f);
+    int rs = 0;  // first entry of the current run
+    auto flush = [&](int q) {
+      const uint32_t key = sk[o + q + 1];
+      const bool head = rs == 0 && cont_head;
+      const bool tail = q == cnt - 1 && cont_tail;
+      if (head) {
+        *(float4*)(part_head + chunk * d + c) = acc;
+      } else if (tail) {
+        *(float4*)(part_tail + chunk * d + c) = acc;
+      } else if ((int)key != skip_key) {
+        float4* dst = (float4*)(out + (long)key * d + c);
+        *dst = *dst + acc;
       }
-      dst = out + (long)key * d;
-      accumulate = true;
-    } else if (is_head) {
-      dst = part_head + chunk * d;
-    } else {
-      dst = part_tail + chunk * d;
+      acc = c2::f4(0.f);
+      rs = q + 1;
+    };
+    for (int q0 = 0; q0 < cnt; q0 += 4) {
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = q0 + u < cnt ? src.load(sv[o + q0 + u], c) : c2::f4(0.f);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u;
+        if (q < cnt) {
+          acc = acc + x[u];
+          if (q == cnt - 1 || sk[o + q + 2] != sk[o + q + 1]) flush(q);
+        }
+      }
     }
-    for (int c = lane * 4; c < d; c += LPR * 4) {
-      float4 acc = c2::f4(0.f);
-      for (long q = i; q < j; ++q) acc = acc + src.load(V[q], c);
-      if (accumulate) acc = acc + *(const float4*)(dst + c);
-      *(float4*)(dst + c) = acc;
-    }
-    i = j;
   }
 }
 
@@ -234,16 +254,21 @@ __global__ __launch_bounds__(1024) void seg_reduce_b(const uint32_t* __restrict_
   const bool continues = end < n && K[end] == key;
   const bool whole_cont = K[start] == key && start > 0 && K[start - 1] == key;
   if (!continues || whole_cont || (int)key == skip_key) return;  // uniform over the block
-  if (threadIdx.x == 0) {
-    long k = chunk + 1;
-    while (true) {
-      const long ek = min((long)n, (k + 1) * SEG_CH);
-      if (!(ek < n && K[ek] == key)) break;
-      ++k;
-    }
-    s_np = (int)(k - chunk + 1);  // tail of c + heads of c+1..k
-  }
+  // last chunk k >= chunk+1 the run reaches: the first k whose end does not continue it.
+  // Searched 1024 chunks at a time by the whole block (a hub / padding run spans hundreds).
+  if (threadIdx.x == 0) s_np = 0x7fffffff;
   __syncthreads();
+  const long nchunks = (n + SEG_CH - 1) / SEG_CH;
+  for (long base = chunk + 1; base < nchunks; base += 1024) {
+    const long k = base + threadIdx.x;
+    if (k < nchunks) {
+      const long ek = min((long)n, (k + 1) * SEG_CH);
+      if (!(ek < n && K[ek] == key)) atomicMin(&s_np, (int)(k - chunk + 1));  // tail of c + heads of c+1..k
+    }
+    __syncthreads();
+    if (s_np != 0x7fffffff) break;
+    __syncthreads();
+  }
   const int np = s_np;
   for (int c = lane * 4; c < d; c += LPR * 4) {
     float4 a0 = c2::f4(0.f), a1 = c2::f4(0.f);
@@ -344,7 +369,7 @@ template <int LPR>
 void seg_launch(const SortWs& w, int n, const RowSrc& src, float* out, int skip_key, hipStream_t s) {
   constexpr int GROUPS = 256 / LPR;
   const int nchunks = c2::ceil_div(n, SEG_CH);
-  dim3 grid(c2::ceil_div(nchunks, GROUPS));
+  dim3 grid(c2::ceil_div(nchunks, GROUPS));  // GROUPS chunks (GROUPS*SEG_CH entries) per block
   seg_reduce_a<LPR><<<grid, 256, 0, s>>>(w.k0, w.v0, n, src, out, w.ph, w.pt, skip_key);
   seg_reduce_b<LPR><<<nchunks, 1024, (size_t)(1024 / LPR) * src.d * 4, s>>>(w.k0, n, src.d, out, w.ph, w.pt, skip_key);
 }

@@ -1,0 +1,122 @@
+// MFMA operand images in LDS shared by the gfx950 kernels (fused CE, row GEMMs):
+// XOR-swizzled bf16 tiles read row-wise (ds_read_b128) and transposed
+// (ds_read_b64_tr_b16), LDS-DMA loaders with hand-placed waits, register pinning.
+#pragma once
+#include "common.h"
+
+namespace c2img {
+
+typedef __bf16 bf16;
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr int TILE = 64;  // rows of the swept operand per LDS tile
+
+// ---------------------------------------------------------------- LDS image
+// A [TILE][D] bf16 tile is stored as D/128 half-tiles of [TILE][128] bf16 (256-byte
+// rows); 16-byte chunk `ch` of row `row` sits at swz(row, ch).
+__device__ __forceinline__ int swz(int row, int ch) {
+  return row * 256 + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+// byte offset of element (row, k) (k multiple of 8 for a 16-byte read)
+__device__ __forceinline__ int img_off(int row, int k) { return (k >> 7) * (TILE * 256) + swz(row, (k & 127) >> 3) + 2 * (k & 7); }
+
+// A-operand fragment for v_mfma_f32_32x32x16_bf16 whose rows are TILE rows r0..r0+31 and
+// whose k-slice is k0..k0+15 (k0 multiple of 16): lane (i = l&31, h = l>>5) gets (row r0+i, k0+8h..+7).
+__device__ __forceinline__ bf16x8 row_frag(const char* img, int r0, int k0, int lane) {
+  const int row = r0 + (lane & 31), k = k0 + 8 * (lane >> 5);
+  return *(const bf16x8*)(img + img_off(row, k));
+}
+
+// Transposed fragment: the MFMA operand whose row index is the image's k (kb0..kb0+31 ↔ lane&31)
+// and whose reduction index runs over image rows in the permuted order of an accumulator
+// fed back as B: element j of lane half h ↔ image row rr0 + 8*(j>>2) + 4*h + (j&3).
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int rr0, int kb0, int lane) {
+  const int g = lane >> 4, h = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
+  const int kcol = kb0 + 16 * (g & 1);  // this 16-lane group's 16 image columns
+  const int row = rr0 + 4 * h + q;
+  const int ch = ((kcol & 127) >> 3) + (p >> 1);
+  const int base = (kcol >> 7) * (TILE * 256);
+  const char* a0 = img + base + swz(row, ch) + 8 * (p & 1);
+  const char* a1 = img + base + swz(row + 8, ch) + 8 * (p & 1);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// accumulator registers 8s..8s+7 → bf16 B operand of k-step s
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)a[8 * s + j];
+  return r;
+}
+
+typedef __attribute__((address_space(3))) char lds_char;
+
+// One LDS-DMA wave-instruction: each lane copies `bytes` (4 or 16) from its global address to
+// LDS[m0 + lane*bytes].  Issued from inline asm so the compiler's wait-count pass does not
+// conservatively drain it before every later LDS read (it cannot prove the prefetch buffer
+// disjoint from the one being read); the kernels wait for it by hand (dma_wait) before the
+// barrier that publishes the buffer.  m0 is written here and nowhere else in these kernels.
+__device__ __forceinline__ void dma16(const void* g, char* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(g) : "memory");
+}
+__device__ __forceinline__ void dma4(const void* g, void* lds) {
+  const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(g) : "memory");
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// vmcnt(0) the compiler can see (its wait-count state then knows the register operands
+// loaded before the tile loop have landed, and emits no waits for them inside the loop)
+// pin a register operand here: its load must be issued (and have landed) before this point
+__device__ __forceinline__ void pin(bf16x8& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(int& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void vm_drain() {
+  __builtin_amdgcn_sched_barrier(0);  // keep the preceding loads above the wait
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS-DMA tile loader: rows g0..g0+TILE-1 of a row-major bf16 [nrows][D] matrix into the
+// swizzled image, no staging registers.  One wave-instruction fills 1 KiB = 4 image rows of
+// one half-tile; lane l writes physical chunk l&15 of row l>>4, so its SOURCE is the logical
+// chunk (l&15) ^ swizzle(row).  Rows past the end are clamped to the last row (finite data;
+// callers zero their contribution).
+template <int D>
+__device__ __forceinline__ void dma_tile(const bf16* __restrict__ X, long nrows, long g0, char* img) {
+  constexpr int GROUPS = TILE / 4;             // 4-row groups per half-tile
+  constexpr int INSTR = GROUPS * (D / 128);    // wave-instructions per tile
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = w; q < INSTR; q += 4) {
+    const int half = q / GROUPS, rg = q % GROUPS;
+    const int row = rg * 4 + (lane >> 4);
+    const int lch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    long gr = g0 + row;
+    gr = gr < nrows ? gr : nrows - 1;
+    dma16(X + gr * D + half * 128 + lch * 8, img + half * (TILE * 256) + rg * 1024);
+  }
+}
+
+// 64 consecutive 4-byte values (a padded per-row / per-column constant array) → LDS, by wave `wv`
+__device__ __forceinline__ void dma_vec64(const void* __restrict__ src, void* dst, int wv) {
+  if ((threadIdx.x >> 6) == wv) dma4((const char*)src + 4 * (threadIdx.x & 63), dst);
+}
+
+__device__ __forceinline__ int creg(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
+
+// raw v_exp_f32 (2^x; no denormal range handling — results below 2^-126 flush to 0)
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+}  // namespace c2img

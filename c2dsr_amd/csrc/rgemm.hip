@@ -1,0 +1,258 @@
+// Row-streaming GEMMs for the sequence-encoder projections at d = 256 (bf16 MFMA, fp32
+// accumulate, fp32 activations in HBM):
+//
+//   rg:  C[M, N] = alpha·A[M, K]·B[N, K]ᵀ + beta·C + bias  (+ relu·dropout epilogue)
+//        forward  y = x·Wᵀ   (B = W in bf16)          K = d_in
+//        backward dx = dy·W  (B = Wᵀ in bf16)         K = d_out
+//   wg:  dW[N, D] += Σ_t dY[t, N]ᵀ·X[t, D]            (split over t, fixed-order combine)
+//
+// Replaces the nn.Linear addmm / mm calls of TransformerEncoderLayer (in_proj, out_proj,
+// linear1, linear2; models/encoders.py:23-27 → torch/nn/modules/transformer.py) at the
+// shapes where M = B·L ≫ N, K.  These are HBM-bound (every activation byte is read once
+// per product), so the design streams the long operand straight into MFMA registers:
+//  * rg: persistent and B-stationary: each wave holds its B columns (all K, bf16) in
+//    registers for the whole launch, so B never moves again (an LDS-tiled version was bound
+//    by the LDS fill rate of re-loaded B tiles); A streams through a double-buffered LDS
+//    image with row-contiguous loads two chunks ahead.
+//  * wg: both operands are t-major; 64-row stages of dY and X are converted to bf16 into
+//    two images and read TRANSPOSED (ds_read_b64_tr_b16), the t permutation being common
+//    to both operands.
+#include "img.h"
+
+namespace {
+using namespace c2img;
+
+struct Epi2 {
+  float alpha, beta;
+  const float* bias;
+  int relu;
+  c2::Drop drop;
+  int64_t row_base;
+};
+
+__device__ __forceinline__ bf16x8 cvt8(float4 a, float4 b) {
+  bf16x8 r;
+  r[0] = (bf16)a.x; r[1] = (bf16)a.y; r[2] = (bf16)a.z; r[3] = (bf16)a.w;
+  r[4] = (bf16)b.x; r[5] = (bf16)b.y; r[6] = (bf16)b.z; r[7] = (bf16)b.w;
+  return r;
+}
+
+// LDS image of a 32-row A chunk [32][256] bf16: two half-tiles of [32][128] (256-byte rows,
+// XOR-swizzled 16-byte chunks as in img.h: conflict-free row fragments).
+__device__ __forceinline__ int aoff(int row, int k) { return (k >> 7) * (32 * 256) + swz(row, (k & 127) >> 3) + 2 * (k & 7); }
+
+// buffer descriptor over [base, base + bytes); every input made provably wave-uniform
+// (readfirstlane) so the buffer ops need no waterfall loop (cdna_hip_programming.md T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_bytes(const void* base, long bytes) {
+  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL));
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
+}
+
+// B-stationary, persistent.  Each wave keeps CT 32-column tiles of B (all K, bf16) in registers
+// for the whole launch; the workgroup (4 waves = 128·CT columns) walks 32-row tiles of A in
+// 256-wide k-chunks: 256 threads load a [32][256] fp32 chunk with row-contiguous float4 buffer
+// loads two chunks ahead, convert it to bf16 into a double-buffered LDS image, and every wave
+// multiplies the image's row fragments with its B registers.  The loop body is branch-free
+// (rows past M read 0 / are not stored through the buffer descriptors; the last tile is
+// repeated to fill a pair) so the compiler's wait counts stay exact and the prefetch lives.
+// Block b runs on XCD b % 8; the G column groups of an XCD walk the same rows in the same
+// order, so the G passes over A share its L2.
+template <int KCH, int CT, bool EPI>
+__global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
+                                                 const bf16* __restrict__ B, long ldb, float* __restrict__ C,
+                                                 long ldc, Epi2 ep, int G) {
+  __shared__ __attribute__((aligned(16))) char aimg[2][32 * 256 * 2];
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nslots = gridDim.x >> 3;
+  const int nwalk = nslots / G;
+  const int g = slot % G, walker = slot / G;
+  if (walker >= nwalk) return;  // uniform
+  const int RT = (M + 31) >> 5;
+  const int rt0 = xcd + 8 * walker, rts = 8 * nwalk;
+  const int ntile = rt0 < RT ? (RT - 1 - rt0) / rts + 1 : 0;
+  if (ntile == 0) return;  // uniform
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ncol0 = g * (128 * CT) + w * (32 * CT);  // this wave's first column
+  // ---- B fragments → registers (once): lane (j = l&31, kh) holds B[col j][16ks + 8kh .. +7]
+  bf16x8 bq[CT][KCH * 16];
+  float bcol[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = min(ncol0 + ct * 32 + (lane & 31), N - 1);
+#pragma unroll
+    for (int ks = 0; ks < KCH * 16; ++ks) bq[ct][ks] = *(const bf16x8*)(B + (long)col * ldb + ks * 16 + 8 * (lane >> 5));
+    bcol[ct] = ep.bias ? ep.bias[col] : 0.f;
+  }
+  // land every loop-invariant register operand here, where the compiler sees the wait
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+#pragma unroll
+    for (int ks = 0; ks < KCH * 16; ++ks) pin(bq[ct][ks]);
+    pin(bcol[ct]);
+  }
+  vm_drain();
+  const auto asrc = rsrc_bytes(A, (long)M * lda * 4);  // rows >= M read 0
+  const auto csrc = rsrc_bytes(C, (long)M * ldc * 4);  // stores to rows >= M are dropped
+  // chunk c = (tile c / KCH (clamped to the last), k-chunk c % KCH); thread t loads float4
+  // t + 256u, u < 8: row (t >> 6) + 4u, columns 4·lane .. +3
+  const int ldab = (int)lda * 4;
+  const int lrow = threadIdx.x >> 6;
+#define RG_LOAD(c, P)                                                                                          \
+  {                                                                                                            \
+    const int tile_ = min((c) / KCH, ntile - 1), kc_ = (c) % KCH;                                              \
+    const int vo_ = ((rt0 + tile_ * rts) * 32 + lrow) * ldab + (kc_ * 256 + 4 * lane) * 4;                     \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) P[u] =                                                       \
+        __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc, vo_ + u * 4 * ldab, 0, 0));     \
+  }
+#define RG_STAGE(P, im)                                                                                        \
+  {                                                                                                            \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                            \
+      bf16x4 v_;                                                                                               \
+      v_[0] = (bf16)P[u].x; v_[1] = (bf16)P[u].y; v_[2] = (bf16)P[u].z; v_[3] = (bf16)P[u].w;                  \
+      *(bf16x4*)((im) + aoff(lrow + 4 * u, 4 * lane)) = v_;                                                   \
+    }                                                                                                          \
+  }
+  f32x16 acc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
+  // step c (k-chunk KC, compile-time): R (free) is refilled with chunk c+2; S holds chunk c+1,
+  // staged after the multiply.  Written out per chunk so R/S alternate without copies.
+#define RG_STEP(c, KC, R, S)                                                                                   \
+  {                                                                                                            \
+    RG_LOAD((c) + 2, R)                                                                                        \
+    const char* im_ = aimg[(c) & 1];                                                                           \
+    _Pragma("unroll") for (int ks = 0; ks < 16; ++ks) {                                                        \
+      const bf16x8 af_ = *(const bf16x8*)(im_ + aoff(lane & 31, ks * 16 + 8 * (lane >> 5)));                   \
+      _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) acc[ct] =                                              \
+          __builtin_amdgcn_mfma_f32_32x32x16_bf16(af_, bq[ct][(KC) * 16 + ks], acc[ct], 0, 0, 0);              \
+    }                                                                                                          \
+    if constexpr ((KC) == KCH - 1) epilogue(min((c) / KCH, ntile - 1));                                       \
+    RG_STAGE(S, aimg[((c) + 1) & 1])                                                                           \
+    __syncthreads();                                                                                           \
+  }
+  const auto epilogue = [&](int tile) {
+    const int r0 = (rt0 + tile * rts) * 32;
+    // lane holds C[r0 + creg(r)][ncol0 + 32ct + (lane&31)]
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int col = ncol0 + 32 * ct + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = r0 + creg(r, lane);
+        float v = fmaf(ep.alpha, acc[ct][r], bcol[ct]);
+        if constexpr (EPI) {
+          const uint64_t idx = (uint64_t)(ep.row_base + rr) * N + col;
+          uint32_t h = c2::lowbias32((uint32_t)idx ^ ep.drop.k0);
+          h = c2::lowbias32(h ^ (uint32_t)(idx >> 32) ^ ep.drop.k1);
+          v = fmaxf(v, 0.f) * (h >= ep.drop.thr ? ep.drop.scale : 0.f);
+        }
+        const int off = col < N ? (rr * (int)ldc + col) * 4 : 0x7fffffff;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), csrc, off, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
+    }
+  };
+  float4 Pa[8], Pb[8];
+  RG_LOAD(0, Pa)
+  RG_LOAD(1, Pb)
+  RG_STAGE(Pa, aimg[0])
+  __syncthreads();
+  const int npair = (ntile + 1) >> 1;
+  for (int i = 0; i < npair; ++i) {
+    const int c0 = i * 2 * KCH;
+    if constexpr (KCH == 1) {
+      RG_STEP(c0, 0, Pa, Pb)
+      RG_STEP(c0 + 1, 0, Pb, Pa)
+    } else if constexpr (KCH == 2) {
+      RG_STEP(c0, 0, Pa, Pb)
+      RG_STEP(c0 + 1, 1, Pb, Pa)
+      RG_STEP(c0 + 2, 0, Pa, Pb)
+      RG_STEP(c0 + 3, 1, Pb, Pa)
+    } else {
+      RG_STEP(c0, 0, Pa, Pb)
+      RG_STEP(c0 + 1, 1, Pb, Pa)
+      RG_STEP(c0 + 2, 2, Pa, Pb)
+      RG_STEP(c0 + 3, 0, Pb, Pa)
+      RG_STEP(c0 + 4, 1, Pa, Pb)
+      RG_STEP(c0 + 5, 2, Pb, Pa)
+    }
+  }
+#undef RG_STEP
+#undef RG_STAGE
+#undef RG_LOAD
+}
+
+// fp32 [R][Cc] (row stride lds) → bf16, optionally transposed (out [Cc][R])
+__global__ void to_bf16_kernel(const float* __restrict__ x, int R, int Cc, long ldx, int trans, bf16* __restrict__ y) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)R * Cc) return;
+  const int r = (int)(i / Cc), c = (int)(i % Cc);
+  const bf16 v = (bf16)x[(long)r * ldx + c];
+  if (trans)
+    y[(long)c * R + r] = v;
+  else
+    y[i] = v;
+}
+
+}  // namespace
+
+// 1 when c2dsr_rgemm takes (M, N, K): K ∈ {256, 512, 768} (the encoder projections at d = 256)
+C2_API int c2dsr_rgemm_supported(int M, int N, int K) { return M > 0 && N > 0 && (K == 256 || K == 512 || K == 768); }
+
+// C[M,N] = alpha·A[M,K]·B[N,K]ᵀ + bias[N]  (beta must be 0; epilogue 1: relu then dropout(p), index
+// (row_base+row)·N + col).  A fp32 (row stride lda, 16-byte aligned rows), B bf16 [N][ldb].
+C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                       float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                       int64_t row_base, void* stream) {
+  if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
+  Epi2 ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base};
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int CT = K == 256 ? 2 : 1;
+  const int G = c2::ceil_div(N, 128 * CT);
+  // persistent grid: exactly the workgroups that are resident at once (occupancy of the variant)
+  static int per_cu[6] = {0, 0, 0, 0, 0, 0};
+  auto launch = [&](void (*kern)(int, int, int, const float*, long, const bf16*, long, float*, long, Epi2, int),
+                    int slot) -> int {
+    if (!per_cu[slot]) {
+      int n = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kern, 256, 0);
+      per_cu[slot] = n > 0 ? n : 1;
+    }
+    const int blocks = (ncu * per_cu[slot] / 8) * 8;
+    if (blocks / 8 < G) return (int)hipErrorInvalidValue;
+    kern<<<blocks, 256, 0, s>>>(M, N, K, A, lda, (const bf16*)B, ldb, C, ldc, ep, G);
+    return 0;
+  };
+  int rc;
+  const bool e = epilogue == 1;
+  if (K == 256)
+    rc = e ? launch(rg_kernel<1, 2, true>, 0) : launch(rg_kernel<1, 2, false>, 1);
+  else if (K == 512)
+    rc = e ? launch(rg_kernel<2, 1, true>, 2) : launch(rg_kernel<2, 1, false>, 3);
+  else
+    rc = e ? launch(rg_kernel<3, 1, true>, 4) : launch(rg_kernel<3, 1, false>, 5);
+  if (rc) return rc;
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// y = bf16(x) for x fp32 [R][Cc] (row stride ldx); trans: y is [Cc][R]
+C2_API int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream) {
+  const long n = (long)R * Cc;
+  if (n == 0) return 0;
+  to_bf16_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(x, R, Cc, ldx, trans, (bf16*)y);
+  C2_CHECK_LAUNCH();
+  return 0;
+}

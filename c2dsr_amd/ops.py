@@ -54,9 +54,36 @@ def colsum(X, M, N, ldx, out, alpha=1.0, beta=1.0):
     lib('c2dsr_colsum', X, M, N, ldx, float(alpha), float(beta), out, ws, stream())
 
 
+def rgemm_ok(M, N, K):
+    return bool(lib.raw('c2dsr_rgemm_supported')(M, N, K))
+
+
+def to_bf16(X, trans=False):
+    """bf16 copy of a 2-D fp32 matrix (transposed if asked)."""
+    R, Cc = X.shape
+    y = torch.empty((Cc, R) if trans else (R, Cc), device=X.device, dtype=torch.bfloat16)
+    lib('c2dsr_to_bf16', X, R, Cc, X.stride(0), int(trans), y, stream())
+    return y
+
+
+def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None):
+    """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm)."""
+    k0 = k1 = 0
+    p = 0.0
+    row_base = 0
+    epi = 0
+    if relu_drop is not None:
+        epi = 1
+        (k0, k1), p, row_base = relu_drop
+    lib('c2dsr_rgemm', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
+        int(row_base), stream())
+    return C
+
+
 class LinearFn(Function):
     """y = x·Wᵀ + b  [optionally drop(relu(.))]  — nn.Linear / TransformerEncoderLayer linear1, linear2,
-    in_proj, out_proj (models/encoders.py:23-27 → torch transformer.py)."""
+    in_proj, out_proj (models/encoders.py:23-27 → torch transformer.py).  bf16 mode at d = 256-multiples:
+    the row-streaming MFMA kernels (csrc/rgemm.hip); otherwise the tiled GEMM (csrc/gemm.hip)."""
 
     @staticmethod
     def forward(ctx, x, W, b, precision, relu_drop):
@@ -64,7 +91,10 @@ class LinearFn(Function):
         N, K = W.shape
         M = x.numel() // K
         y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
-        gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)
+        if precision == BF16 and rgemm_ok(M, N, K):
+            rgemm(x, to_bf16(W), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
+        else:
+            gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)
         ctx.save_for_backward(x, W, y if relu_drop is not None else None)
         ctx.b = b
         ctx.precision = precision
@@ -84,7 +114,10 @@ class LinearFn(Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
+            if ctx.precision == BF16 and rgemm_ok(M, K, N):
+                rgemm(dy, to_bf16(W, trans=True), dx, M=M, N=K, K=N)
+            else:
+                gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
         gW = _grad_target(W)
         if gW is not None:
             gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)

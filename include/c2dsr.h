@@ -145,6 +145,18 @@ int c2dsr_selftest_tr(int rr0, int kb0, short* out, void* stream);
 int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,
                 float b1, float b2, float eps, int step, void* stream);
 
+
+/* K3 projections, row-streaming bf16 MFMA (csrc/rgemm.hip).  Replaces the addmm/mm of
+ * TransformerEncoderLayer in_proj/out_proj/linear1/linear2 (models/encoders.py:23-27) at
+ * K ∈ {256,512,768}:  C[M,N] = alpha·A[M,K]·B[N,K]ᵀ + bias (beta must be 0; epilogue 1: relu·dropout(p),
+ * index (row_base+row)·N + col).  A fp32 (lda % 4 == 0), B bf16 [N][ldb]. */
+int c2dsr_rgemm_supported(int M, int N, int K);
+int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                int64_t row_base, void* stream);
+/* y = bf16(x), x fp32 [R][Cc] with row stride ldx; trans: y is [Cc][R] (weight copies for rgemm). */
+int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

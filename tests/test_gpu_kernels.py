@@ -307,3 +307,40 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     assert rel(gW - 1, dl[:, :n].T @ H.double()) < 1e-2
     assert rel(gb - 1, dl[:, :n].sum(0)) < 1e-2
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize('M,N,K', [(1000, 768, 256), (300, 256, 768), (129, 256, 256), (77, 320, 512)])
+def test_rgemm_vs_bf16_rounded_fp32(M, N, K):
+    """Row-streaming projection GEMM: exact products of bf16-rounded operands, fp32 sums."""
+    from c2dsr_amd.ops import rgemm, rgemm_ok, to_bf16
+    assert rgemm_ok(M, N, K)
+    g = torch.Generator().manual_seed(M + N + K)
+    A, W, C0, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(M, N, generator=g), \
+        torch.randn(N, generator=g)
+    C = C0.to(DEV)
+    rgemm(A.to(DEV), to_bf16(W.to(DEV)), C, M=M, N=N, K=K, alpha=0.5, beta=2.0, bias=b.to(DEV))
+    ref = 0.5 * (_bf(A).double() @ _bf(W).double().T) + 2.0 * C0.double() + b.double()
+    assert rel(C, ref) < 2e-6
+    # transposed weight copy (the dx = dy·W product)
+    Wt = torch.randn(K, N, generator=g)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), to_bf16(Wt.to(DEV), trans=True), C, M=M, N=N, K=K)
+    assert rel(C, _bf(A).double() @ _bf(Wt).double()) < 2e-6
+
+
+def test_rgemm_relu_dropout_epilogue():
+    from c2dsr_amd.ops import rgemm, to_bf16
+    from oracle.c2dsr_oracle import keep_mask
+    M, N, K, p = 333, 256, 256, 0.3
+    A, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
+    keys = (123456, 987654)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), to_bf16(W.to(DEV)), C, M=M, N=N, K=K, bias=b.to(DEV), relu_drop=(keys, p, 1000))
+    idx = (np.arange(M)[:, None] + 1000) * N + np.arange(N)[None, :]
+    mk = torch.from_numpy(keep_mask(idx, keys, p).astype(np.float32)).double() / (1 - p)
+    ref = torch.relu(_bf(A).double() @ _bf(W).double().T + b.double()) * mk
+    assert rel(C, ref) < 2e-6
