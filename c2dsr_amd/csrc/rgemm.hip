@@ -187,6 +187,147 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
 #undef RG_LOAD
 }
 
+// ---------------------------------------------------------------------------------------------
+// wg: dW[N, 256] partials = Σ_{t in split} dY[t, N]ᵀ·X[t, 256], both operands t-major (fp32).
+// Workgroup = 4 waves = a 128-row slice of N × all 256 columns (wave: 64 × 128, 2×4 MFMA tiles);
+// 32-row chunks of dY (32×128) and X (32×256) are converted to bf16 into LDS images and both
+// operands are read TRANSPOSED (ds_read_b64_tr_b16): the reduction runs over the image rows (t)
+// in the same permuted order for A and B.  Loads run two chunks ahead in registers, the loop
+// body is branch-free (rows past T read 0 through the buffer descriptors).
+// part[split][N][256] (fixed-order combine: c2dsr_sum_parts).
+
+// transposed fragment from a [32][ncols] image (half-tiles of [32][128], stride 8 KB)
+__device__ __forceinline__ bf16x8 tr32(const char* img, int rr0, int kb0, int lane) {
+  const int g = lane >> 4, h = lane >> 5, q = (lane & 15) >> 2, p = lane & 3;
+  const int kcol = kb0 + 16 * (g & 1);
+  const int row = rr0 + 4 * h + q;
+  const int ch = ((kcol & 127) >> 3) + (p >> 1);
+  const int base = (kcol >> 7) * (32 * 256);
+  const char* a0 = img + base + swz(row, ch) + 8 * (p & 1);
+  const char* a1 = img + base + swz(row + 8, ch) + 8 * (p & 1);
+  bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
+  bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a1);
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __restrict__ dY, long ldy,
+                                                 const float* __restrict__ X, long ldx, float* __restrict__ part,
+                                                 int NTL, int rows_per_split) {
+  __shared__ __attribute__((aligned(16))) char yimg[2][32 * 128 * 2];
+  __shared__ __attribute__((aligned(16))) char ximg[2][32 * 256 * 2];
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nslots = gridDim.x >> 3;
+  const int per_x = nslots / NTL;  // splits per XCD
+  const int nt = slot % NTL, sl = slot / NTL;
+  if (sl >= per_x) return;  // uniform
+  const int split = xcd + 8 * sl;
+  const int t_beg = split * rows_per_split;
+  const int t_end = min(T, t_beg + rows_per_split);
+  const int nchunk = t_end > t_beg ? (t_end - t_beg + 31) >> 5 : 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int n_base = nt * 128;
+  const auto ysrc = rsrc_bytes(dY, (long)t_end * ldy * 4);  // rows past the split's end read 0
+  const auto xsrc = rsrc_bytes(X, (long)t_end * ldx * 4);
+  const int lrow = threadIdx.x >> 6;  // 0..3
+  const int ldyb = (int)ldy * 4, ldxb = (int)ldx * 4;
+  // chunk c: thread t loads dY rows lrow + 4u (u < 8) → 1 float4 (cols 4·(lane&31) of the 128) per
+  // half-wave pair... simpler: dY chunk 32×128 floats = 1024 float4 = 4 per thread, X 2048 = 8 per thread
+#define WG_LOAD(c, PY, PX)                                                                                    \
+  {                                                                                                           \
+    const int t0_ = t_beg + min(c, nchunk - 1) * 32;                                                          \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
+      const int q_ = threadIdx.x + 256 * u; /* 0..1023: row q_>>5, float4 q_&31 */                           \
+      PY[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(                              \
+                                             ysrc, (t0_ + (q_ >> 5)) * ldyb + (n_base + 4 * (q_ & 31)) * 4, 0, 0)); \
+    }                                                                                                         \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                           \
+      PX[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(                              \
+                                             xsrc, (t0_ + lrow + 4 * u) * ldxb + 16 * lane, 0, 0));           \
+    }                                                                                                         \
+  }
+#define WG_PUT(im, row, col, v4)                                                                              \
+  {                                                                                                           \
+    bf16x4 b_;                                                                                                \
+    b_[0] = (bf16)(v4).x; b_[1] = (bf16)(v4).y; b_[2] = (bf16)(v4).z; b_[3] = (bf16)(v4).w;                   \
+    *(bf16x4*)((im) + ((col) >> 7) * (32 * 256) + swz(row, ((col) & 127) >> 3) + 2 * ((col) & 7)) = b_;       \
+  }
+#define WG_STAGE(PY, PX, b)                                                                                   \
+  {                                                                                                           \
+    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
+      const int q_ = threadIdx.x + 256 * u;                                                                   \
+      WG_PUT(yimg[b], q_ >> 5, 4 * (q_ & 31), PY[u])                                                          \
+    }                                                                                                         \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) WG_PUT(ximg[b], lrow + 4 * u, 4 * lane, PX[u])              \
+  }
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
+  const int wn = (w >> 1) * 64, wi = (w & 1) * 128;  // this wave's 64 n-rows and 128 i-columns
+#define WG_STEP(c, RY, RX, SY, SX)                                                                            \
+  {                                                                                                           \
+    WG_LOAD((c) + 2, RY, RX)                                                                                  \
+    const char* yi_ = yimg[(c) & 1];                                                                          \
+    const char* xi_ = ximg[(c) & 1];                                                                          \
+    _Pragma("unroll") for (int kst = 0; kst < 2; ++kst) {                                                     \
+      bf16x8 fa_[2], fb_[4];                                                                                  \
+      _Pragma("unroll") for (int a = 0; a < 2; ++a) fa_[a] = tr32(yi_, 16 * kst, wn + 32 * a, lane);          \
+      _Pragma("unroll") for (int b = 0; b < 4; ++b) fb_[b] = tr32(xi_, 16 * kst, wi + 32 * b, lane);          \
+      _Pragma("unroll") for (int a = 0; a < 2; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) acc[a][b] = \
+          __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_[a], fb_[b], acc[a][b], 0, 0, 0);                        \
+    }                                                                                                         \
+    WG_STAGE(SY, SX, ((c) + 1) & 1)                                                                           \
+    __syncthreads();                                                                                          \
+  }
+  if (nchunk > 0) {
+    float4 Ya[4], Xa[8], Yb[4], Xb[8];
+    WG_LOAD(0, Ya, Xa)
+    WG_LOAD(1, Yb, Xb)
+    WG_STAGE(Ya, Xa, 0)
+    __syncthreads();
+    for (int c = 0; c < nchunk; c += 2) {
+      WG_STEP(c, Ya, Xa, Yb, Xb)
+      if (c + 1 >= nchunk) break;
+      WG_STEP(c + 1, Yb, Xb, Ya, Xa)
+    }
+  }
+#undef WG_STEP
+#undef WG_STAGE
+#undef WG_PUT
+#undef WG_LOAD
+  // D[n][i]: lane holds (row n = wn + 32a + creg(r), col i = wi + 32b + (lane&31))
+  float* out = part + (long)split * N * 256;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = n_base + wn + 32 * a + creg(r, lane);
+        if (n < N) out[(long)n * 256 + wi + 32 * b + (lane & 31)] = acc[a][b][r];
+      }
+}
+
+// out[i] = beta·out[i] + Σ_s part[s][i]  (fixed order, float4)
+__global__ void sum_parts_kernel2(const float* __restrict__ part, int nparts, long n, float beta,
+                                  float* __restrict__ out) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < nparts; ++s) {
+    const float4 v = *(const float4*)(part + (long)s * n + i);
+    t = make_float4(t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w);
+  }
+  float4 o = beta == 0.f ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(out + i);
+  *(float4*)(out + i) = make_float4(beta * o.x + t.x, beta * o.y + t.y, beta * o.z + t.z, beta * o.w + t.w);
+}
+
 // fp32 [R][Cc] (row stride lds) → bf16, optionally transposed (out [Cc][R])
 __global__ void to_bf16_kernel(const float* __restrict__ x, int R, int Cc, long ldx, int trans, bf16* __restrict__ y) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -202,7 +343,9 @@ __global__ void to_bf16_kernel(const float* __restrict__ x, int R, int Cc, long 
 }  // namespace
 
 // 1 when c2dsr_rgemm takes (M, N, K): K ∈ {256, 512, 768} (the encoder projections at d = 256)
-C2_API int c2dsr_rgemm_supported(int M, int N, int K) { return M > 0 && N > 0 && (K == 256 || K == 512 || K == 768); }
+C2_API int c2dsr_rgemm_supported(int M, int N, int K) {
+  return M > 0 && N > 0 && (K == 256 || K == 512 || K == 768) && (long)M * K * 4 < (1L << 31) && (long)M * N * 4 < (1L << 31);
+}
 
 // C[M,N] = alpha·A[M,K]·B[N,K]ᵀ + bias[N]  (beta must be 0; epilogue 1: relu then dropout(p), index
 // (row_base+row)·N + col).  A fp32 (row stride lda, 16-byte aligned rows), B bf16 [N][ldb].
@@ -244,6 +387,37 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
   else
     rc = e ? launch(rg_kernel<3, 1, true>, 4) : launch(rg_kernel<3, 1, false>, 5);
   if (rc) return rc;
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// dW[N][256] (+)= Σ_t dY[t][N]ᵀ·X[t][256] (N % 128 == 0): split over t into `splits` partial
+// slices part[splits][N][256] (c2dsr_wgemm_workspace bytes), combined in a fixed order into dW
+// with beta (0 or 1).
+static int wg_splits(int N) {
+  int dev = 0, ncu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  if (ncu <= 0) ncu = 256;
+  const int NTL = N / 128;
+  return (ncu / 8 / NTL) * 8;  // per XCD: ncu/8 slots / NTL n-tiles
+}
+C2_API int c2dsr_wgemm_supported(int T, int N, int D) {
+  return T > 0 && D == 256 && N % 128 == 0 && N <= 32 * 128 && (long)T * N * 4 < (1L << 31) && (long)T * D * 4 < (1L << 31);
+}
+C2_API size_t c2dsr_wgemm_workspace(int N) { return (size_t)wg_splits(N) * N * 256 * 4; }
+C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
+                       void* part, void* stream) {
+  if (!c2dsr_wgemm_supported(T, N, D) || ldy % 4 || ldx % 4) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int NTL = N / 128;
+  const int splits = wg_splits(N);
+  if (splits < 8) return (int)hipErrorInvalidValue;
+  const int rows = c2::ceil_div(c2::ceil_div(T, splits), 32) * 32;
+  const int blocks = splits * NTL;  // = 8 XCDs x (splits/8) x NTL
+  wg_kernel<<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, NTL, rows);
+  const long n = (long)N * 256;
+  sum_parts_kernel2<<<c2::ceil_div(n / 4, 256), 256, 0, s>>>((const float*)part, splits, n, beta, dW);
   C2_CHECK_LAUNCH();
   return 0;
 }

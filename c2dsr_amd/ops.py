@@ -80,6 +80,16 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None):
     return C
 
 
+def wgemm_ok(T, N, D):
+    return bool(lib.raw('c2dsr_wgemm_supported')(T, N, D))
+
+
+def wgemm(dY, X, dW, *, T, N, D, beta=1.0):
+    """dW[N, D] = beta·dW + dYᵀ·X over T rows (c2dsr_wgemm, deterministic split-t partials)."""
+    ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
+    lib('c2dsr_wgemm', T, N, D, dY, N, X, D, float(beta), dW, ws, stream())
+
+
 class LinearFn(Function):
     """y = x·Wᵀ + b  [optionally drop(relu(.))]  — nn.Linear / TransformerEncoderLayer linear1, linear2,
     in_proj, out_proj (models/encoders.py:23-27 → torch transformer.py).  bf16 mode at d = 256-multiples:
@@ -120,7 +130,10 @@ class LinearFn(Function):
                 gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
         gW = _grad_target(W)
         if gW is not None:
-            gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
+            if ctx.precision == BF16 and wgemm_ok(M, N, K):
+                wgemm(dy, x, gW, T=M, N=N, D=K)
+            else:
+                gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
         gb = _grad_target(ctx.b)
         if gb is not None:
             colsum(dy, M, N, N, gb)

@@ -322,8 +322,8 @@ def test_rgemm_vs_bf16_rounded_fp32(M, N, K):
     A, W, C0, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(M, N, generator=g), \
         torch.randn(N, generator=g)
     C = C0.to(DEV)
-    rgemm(A.to(DEV), to_bf16(W.to(DEV)), C, M=M, N=N, K=K, alpha=0.5, beta=2.0, bias=b.to(DEV))
-    ref = 0.5 * (_bf(A).double() @ _bf(W).double().T) + 2.0 * C0.double() + b.double()
+    rgemm(A.to(DEV), to_bf16(W.to(DEV)), C, M=M, N=N, K=K, alpha=0.5, bias=b.to(DEV))
+    ref = 0.5 * (_bf(A).double() @ _bf(W).double().T) + b.double()
     assert rel(C, ref) < 2e-6
     # transposed weight copy (the dx = dy·W product)
     Wt = torch.randn(K, N, generator=g)
@@ -344,3 +344,24 @@ def test_rgemm_relu_dropout_epilogue():
     mk = torch.from_numpy(keep_mask(idx, keys, p).astype(np.float32)).double() / (1 - p)
     ref = torch.relu(_bf(A).double() @ _bf(W).double().T + b.double()) * mk
     assert rel(C, ref) < 2e-6
+
+
+@pytest.mark.parametrize('T,N', [(1000, 256), (4097, 768), (31, 128)])
+def test_wgemm_vs_bf16_rounded_fp32(T, N):
+    """Projection weight gradient: dW = beta·dW + dYᵀ·X (bf16-rounded operands, fp32 sums)."""
+    from c2dsr_amd.ops import wgemm, wgemm_ok
+    D = 256
+    assert wgemm_ok(T, N, D)
+    g = torch.Generator().manual_seed(T + N)
+    dY, X, W0 = torch.randn(T, N, generator=g), torch.randn(T, D, generator=g), torch.randn(N, D, generator=g)
+    dW = W0.to(DEV)
+    wgemm(dY.to(DEV), X.to(DEV), dW, T=T, N=N, D=D, beta=1.0)
+    ref = W0.double() + _bf(dY).double().T @ _bf(X).double()
+    assert rel(dW, ref) < 1e-5
+    dW = torch.full((N, D), 7.0, device=DEV)
+    wgemm(dY.to(DEV), X.to(DEV), dW, T=T, N=N, D=D, beta=0.0)
+    assert rel(dW, _bf(dY).double().T @ _bf(X).double()) < 1e-5
+    # deterministic: same bits on a re-run
+    dW2 = torch.full((N, D), 7.0, device=DEV)
+    wgemm(dY.to(DEV), X.to(DEV), dW2, T=T, N=N, D=D, beta=0.0)
+    assert torch.equal(dW, dW2)
