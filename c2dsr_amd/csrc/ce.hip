@@ -29,54 +29,47 @@ using namespace c2img;
 // running max and sum of 2^(s·log2e) over the split's columns.  bias2 = bias·log2e padded
 // with -inf to a multiple of TILE.
 template <int D>
-__global__ __launch_bounds__(256, 1) void ce_lse_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
+__global__ __launch_bounds__(512, 1) void ce_lse_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
                                                         const float* __restrict__ bias2, int M, int n,
                                                         int cols_per_split, float* __restrict__ part_m,
                                                         float* __restrict__ part_s) {
+  // 8 waves x 32 rows: two waves per SIMD, so one wave's exp/max epilogue runs in the other's
+  // MFMA shadow (a single wave per SIMD serialised them)
   constexpr int KS = D / 16;
   __shared__ __attribute__((aligned(16))) char img[2][TILE * D * 2];
   __shared__ __attribute__((aligned(16))) float b2s[2][TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int rbase = blockIdx.x * 256 + w * 64;
+  const int r = blockIdx.x * 256 + w * 32 + (lane & 31);
   const int c_beg = blockIdx.y * cols_per_split;
   const int c_end = min(n, c_beg + cols_per_split);
   const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
   if (ntiles > 0) {
-    dma_tile<D>(Wb, n, c_beg, img[0]);
+    dma_tile<D, 8>(Wb, n, c_beg, img[0]);
     dma_vec64(bias2 + c_beg, b2s[0], 0);
   }
-  bf16x8 hf[2][KS];
+  bf16x8 hf[KS];
+  const int rc = min(M - 1, r);
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    const int r = min(M - 1, rbase + rb * 32 + (lane & 31));
+  for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) hf[rb][ks] = *(const bf16x8*)(Hb + (long)r * D + ks * 16 + 8 * (lane >> 5));
-  }
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) pin(hf[rb][ks]);
-  float mrun[2] = {-INFINITY, -INFINITY}, srun[2] = {0.f, 0.f};
+  for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
+  float mrun = -INFINITY, srun = 0.f;
   vm_drain();
   dma_wait();
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
     const char* cimg = img[t & 1];
     const float* cb2s = b2s[t & 1];
-    char* nimg = img[(t & 1) ^ 1];
-    float* nb2s = b2s[(t & 1) ^ 1];
     const int c0 = c_beg + t * TILE;
     if (t + 1 < ntiles) {
-      dma_tile<D>(Wb, n, c0 + TILE, nimg);
-      dma_vec64(bias2 + c0 + TILE, nb2s, 1);
+      dma_tile<D, 8>(Wb, n, c0 + TILE, img[(t & 1) ^ 1]);
+      dma_vec64(bias2 + c0 + TILE, b2s[(t & 1) ^ 1], 1);
     }
-    f32x16 acc[2][2];
+    f32x16 acc[2];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[cb][rb][i] = 0.f;
+      for (int i = 0; i < 16; ++i) acc[cb][i] = 0.f;
     bf16x8 fa[2], fb[2];
     fa[0] = row_frag(cimg, 0, 0, lane);
     fa[1] = row_frag(cimg, 32, 0, lane);
@@ -86,11 +79,8 @@ __global__ __launch_bounds__(256, 1) void ce_lse_kernel(const bf16* __restrict__
         fb[0] = row_frag(cimg, 0, (ks + 1) * 16, lane);
         fb[1] = row_frag(cimg, 32, (ks + 1) * 16, lane);
       }
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-          acc[cb][rb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cb], hf[rb][ks], acc[cb][rb], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], hf[ks], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], hf[ks], acc[1], 0, 0, 0);
       fa[0] = fb[0];
       fa[1] = fb[1];
     }
@@ -99,40 +89,32 @@ __global__ __launch_bounds__(256, 1) void ce_lse_kernel(const bf16* __restrict__
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int j4 = 0; j4 < 4; ++j4) b4[cb][j4] = *(const float4*)&cb2s[cb * 32 + 8 * j4 + 4 * (lane >> 5)];
+    float tmax = -INFINITY;
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      float tmax = -INFINITY;
+    for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
+      for (int i = 0; i < 16; ++i) {
+        const float v = fmaf(acc[cb][i], LOG2E, ((const float*)&b4[cb][i >> 2])[i & 3]);
+        acc[cb][i] = v;
+        tmax = fmaxf(tmax, v);
+      }
+    const float mnew = fmaxf(mrun, tmax);
+    float sm = (mrun == -INFINITY) ? 0.f : srun * ex2(mrun - mnew);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float v = fmaf(acc[cb][rb][i], LOG2E, ((const float*)&b4[cb][i >> 2])[i & 3]);
-          acc[cb][rb][i] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      const float mnew = fmaxf(mrun[rb], tmax);
-      float s = (mrun[rb] == -INFINITY) ? 0.f : srun[rb] * ex2(mrun[rb] - mnew);
+    for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s += ex2(acc[cb][rb][i] - mnew);
-      mrun[rb] = mnew;
-      srun[rb] = s;
-    }
+      for (int i = 0; i < 16; ++i) sm += ex2(acc[cb][i] - mnew);
+    mrun = mnew;
+    srun = sm;
     dma_wait();
     __syncthreads();
   }
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    const float m2 = __shfl_xor(mrun[rb], 32, 64), s2 = __shfl_xor(srun[rb], 32, 64);
-    const float mm = fmaxf(mrun[rb], m2);
-    const float s = (mrun[rb] == -INFINITY ? 0.f : srun[rb] * ex2(mrun[rb] - mm)) +
-                    (m2 == -INFINITY ? 0.f : s2 * ex2(m2 - mm));
-    const int r = rbase + rb * 32 + (lane & 31);
-    if (lane < 32 && r < M) {
-      part_m[(long)blockIdx.y * M + r] = mm;
-      part_s[(long)blockIdx.y * M + r] = s;
-    }
+  const float m2 = __shfl_xor(mrun, 32, 64), s2 = __shfl_xor(srun, 32, 64);
+  const float mm = fmaxf(mrun, m2);
+  const float sm = (mrun == -INFINITY ? 0.f : srun * ex2(mrun - mm)) + (m2 == -INFINITY ? 0.f : s2 * ex2(m2 - mm));
+  if (lane < 32 && r < M) {
+    part_m[(long)blockIdx.y * M + r] = mm;
+    part_s[(long)blockIdx.y * M + r] = sm;
   }
 }
 
@@ -520,9 +502,9 @@ C2_API int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2
   const int per = per_split(n, n_split, TILE);
   dim3 grid(c2::ceil_div(M, 256), n_split);
   if (D == 128)
-    ce_lse_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s);
+    ce_lse_kernel<128><<<grid, 512, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s);
   else if (D == 256)
-    ce_lse_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s);
+    ce_lse_kernel<256><<<grid, 512, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s);
   else
     return (int)hipErrorInvalidValue;
   ce_rows_kernel<<<c2::ceil_div(M, 4), 256, 0, s>>>(part_m, part_s, n_split, M, padlogit, tgt, n, H, W, bias, D, lse,

@@ -93,13 +93,13 @@ __device__ __forceinline__ void vm_drain() {
 // one half-tile; lane l writes physical chunk l&15 of row l>>4, so its SOURCE is the logical
 // chunk (l&15) ^ swizzle(row).  Rows past the end are clamped to the last row (finite data;
 // callers zero their contribution).
-template <int D>
+template <int D, int NW = 4>
 __device__ __forceinline__ void dma_tile(const bf16* __restrict__ X, long nrows, long g0, char* img) {
   constexpr int GROUPS = TILE / 4;             // 4-row groups per half-tile
   constexpr int INSTR = GROUPS * (D / 128);    // wave-instructions per tile
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int q = w; q < INSTR; q += 4) {
+  for (int q = w; q < INSTR; q += NW) {
     const int half = q / GROUPS, rg = q % GROUPS;
     const int row = rg * 4 + (lane >> 4);
     const int lch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));

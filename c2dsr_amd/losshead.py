@@ -22,10 +22,29 @@ from ._lib import lib, stream
 from .ops import BF16, FP32, _grad_target, colsum, gemm
 
 
-def split_count(rows, tile, target_wgs=1024):
-    """number of work splits so that (row tiles × splits) ≈ target_wgs workgroups"""
+_NCU = None
+
+
+def _ncu():
+    global _NCU
+    if _NCU is None:
+        _NCU = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
+            if torch.cuda.is_available() else 256
+    return _NCU
+
+
+def split_count(rows, tile, max_split=16, per_cu=1):
+    """Work splits for a (row tiles × splits) grid of one-workgroup-per-CU kernels: the count that
+    minimises the launch's makespan ⌈tiles·s / slots⌉ / s (whole rounds of workgroups; a partial
+    last round leaves CUs idle), the smaller count on ties (fewer partial slices to combine)."""
     tiles = max(1, -(-rows // tile))
-    return max(1, min(16, -(-target_wgs // tiles)))
+    slots = _ncu() * per_cu
+    best, best_t = 1, None
+    for s in range(1, max_split + 1):
+        t = -(-tiles * s // slots) / s
+        if best_t is None or t < best_t - 1e-12:
+            best, best_t = s, t
+    return best
 
 
 class LossMeta:
