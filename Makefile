@@ -4,7 +4,7 @@ ARCH ?= gfx950
 SRC := $(wildcard c2dsr_amd/csrc/*.hip)
 OBJ := $(patsubst c2dsr_amd/csrc/%.hip,build/%.o,$(SRC))
 HDR := $(wildcard c2dsr_amd/csrc/*.h) include/c2dsr.h
-FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Iinclude -Wno-unused-result
+FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++20 -Iinclude -Wno-unused-result
 
 all: c2dsr_amd/libc2dsr_hip.so
 

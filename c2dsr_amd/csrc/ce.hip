@@ -19,6 +19,11 @@
 // prefetch.  Work is split over column (lse, dH) or row (dW) ranges for occupancy and
 // the partials are combined in a fixed order (deterministic).
 #include "img.h"
+#ifndef C2_DT
+#define C2_DT 3
+#endif
+
+#include <utility>
 
 namespace {
 
@@ -154,7 +159,12 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------- backward: dH
-// grid (ceil(M/128), n_split); 4 waves x 32 rows; sweeps the split's columns.
+// grid (ceil(M/128), n_split); 4 waves x 32 rows, one wave per SIMD (512 registers); sweeps the
+// split's columns 64 at a time.  Every LDS fragment read is an asm ds_read at a precomputed
+// per-lane offset + immediate (no address VALU in the loop), issued DEPTH MFMAs ahead of its
+// consumer with a counted lgkmcnt wait; the dHᵀ accumulators live in AGPRs for the whole sweep;
+// W tiles arrive by saddr LDS-DMA (scalar tile base, per-lane offsets computed once).
+// Wb must hold ⌈n/64⌉·64 rows (zero padding past n); bias2 is -inf past n.
 // dHp [n_split][M][D] (fp32 partials, combined by c2dsr_sum_parts).
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
@@ -164,7 +174,12 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
                                                        const float* __restrict__ roww, float* __restrict__ dHp) {
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
-  __shared__ __attribute__((aligned(16))) char img[2][TILE * D * 2];
+  constexpr int NQ = KB * 4;
+  constexpr int DEPTH = 3;    // S-phase row fragments ahead
+  constexpr int DT = C2_DT;   // dH-phase transposed fragments ahead
+  constexpr int IMG = TILE * D * 2;            // bytes per image
+  constexpr int NDMA = (TILE / 4) * (D / 128) / 4;  // DMA wave-instructions per wave per tile
+  __shared__ __attribute__((aligned(16))) char img[2][IMG];
   __shared__ __attribute__((aligned(16))) float b2s[2][TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x * 128 + w * 32 + (lane & 31);
@@ -172,18 +187,42 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
   const int c_beg = blockIdx.y * cols_per_split;
   const int c_end = min(n, c_beg + cols_per_split);
   const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
-  if (ntiles > 0) {
-    dma_tile<D>(Wb, n, c_beg, img[0]);
-    dma_vec64(bias2 + c_beg, b2s[0], 0);
+  // ---- per-lane constants
+  ImgOffsets o = img_offsets(lane);
+  const int ib = (int)lds_addr(img[0]);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) o.roff[c] += ib;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    o.troff[v][0] += ib;
+    o.troff[v][1] += ib;
   }
+  unsigned dvoff[NDMA], ddst[NDMA];
+#pragma unroll
+  for (int i = 0; i < NDMA; ++i) {
+    const int q = w + 4 * i;
+    constexpr int GROUPS = TILE / 4;
+    const int half = q / GROUPS, rg = q % GROUPS;
+    const int row = rg * 4 + (lane >> 4);
+    const int lch = (lane & 15) ^ swz_f(row);
+    dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
+    ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
+  }
+  auto dma = [&](int c0, int buf) {
+    const bf16* base = Wb + (long)c0 * D;
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
+    dma_vec64(bias2 + c0, b2s[buf], 0);
+  };
   bf16x8 hf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
   float lr = lse2[rc];
   float rw = r < M ? roww[rc] : 0.f;
   int tr = tgt32[rc];
+  if (ntiles > 0) dma(c_beg, 0);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
   pin(lr);
   pin(rw);
   pin(tr);
@@ -195,38 +234,45 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
   vm_drain();
   dma_wait();
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const char* cimg = img[t & 1];
-    const float* cb2s = b2s[t & 1];
-    char* nimg = img[(t & 1) ^ 1];
-    float* nb2s = b2s[(t & 1) ^ 1];
+  const int c_last = c_beg + (ntiles - 1) * TILE;
+
+  // one column tile: S, softmax-gradient epilogue, dHᵀ update.  The image of tile t is buffer
+  // t & 1; `o` holds the offsets into it (swapped to the other buffer after every tile).
+  auto tile = [&](int t) {
+    constexpr int BOFF = 0;
+    const int buf = t & 1;
     const int c0 = c_beg + t * TILE;
-    if (t + 1 < ntiles) {
-      dma_tile<D>(Wb, n, c0 + TILE, nimg);
-      dma_vec64(bias2 + c0 + TILE, nb2s, 1);
-    }
-    f32x16 s[2];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[cb][i] = 0.f;
-    bf16x8 fa[2], fb[2];
-    fa[0] = row_frag(cimg, 0, 0, lane);
-    fa[1] = row_frag(cimg, 32, 0, lane);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 1 < KS) {
-        fb[0] = row_frag(cimg, 0, (ks + 1) * 16, lane);
-        fb[1] = row_frag(cimg, 32, (ks + 1) * 16, lane);
-      }
-      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], hf[ks], s[0], 0, 0, 0);
-      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], hf[ks], s[1], 0, 0, 0);
-      fa[0] = fb[0];
-      fa[1] = fb[1];
-    }
-    // P'ᵀ[c][r] = (2^(s·log2e + b2 - lse2) - [c == t]) * w_r   (b2 = -inf past n → 0)
+    dma(min(c0 + TILE, c_last), buf ^ 1);  // the last tile re-loads itself: no branch here
+    const float* cb2s = b2s[buf];
+    // ---- S = W_tile · Hᵀ  (2 column blocks x 16 k-steps), fragments DEPTH k-steps ahead
+    f32x16 sa[2];
+    bf16x8 fa[DEPTH + 1][2];
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      ((row_frag_o<TILE, 0, P, BOFF>(fa[P][0], o), row_frag_o<TILE, 32, P, BOFF>(fa[P][1], o)), ...);
+    }(std::make_integer_sequence<int, DEPTH>{});
+    [&]<int... K>(std::integer_sequence<int, K...>) {
+      (
+          [&] {
+            constexpr int ks = K;
+            if constexpr (ks + DEPTH < KS) {
+              row_frag_o<TILE, 0, ks + DEPTH, BOFF>(fa[(ks + DEPTH) % (DEPTH + 1)][0], o);
+              row_frag_o<TILE, 32, ks + DEPTH, BOFF>(fa[(ks + DEPTH) % (DEPTH + 1)][1], o);
+            }
+            constexpr int ahead = (KS - 1 - ks) < DEPTH ? (KS - 1 - ks) : DEPTH;
+            lds_wait2<2 * ahead>(fa[ks % (DEPTH + 1)][0], fa[ks % (DEPTH + 1)][1]);
+            if constexpr (ks == 0) {
+              sa[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
+              sa[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
+            } else {
+              sa[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DEPTH + 1)][0], hf[ks], sa[0], 0, 0, 0);
+              sa[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DEPTH + 1)][1], hf[ks], sa[1], 0, 0, 0);
+            }
+          }(),
+          ...);
+    }(std::make_integer_sequence<int, KS>{});
+    // ---- P'ᵀ[c][r] = (2^(s·log2e + b2 - lse2) - [c == t]) * w_r   (b2 = -inf past n → 0)
     bf16x8 x[2][2];
-    const int tl = tr - c0;  // target column relative to this tile (may be out of range)
+    const int tl = tr - c0;
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
@@ -236,28 +282,49 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * j4 + e;
-          const float ev = ex2(fmaf(s[cb][i], LOG2E, ((const float*)&b4)[e]) - lr);
-          s[cb][i] = (ev - (cl0 + e == tl ? 1.f : 0.f)) * rw;
+          const float ev = ex2(fmaf(sa[cb][i], LOG2E, ((const float*)&b4)[e]) - lr);
+          sa[cb][i] = (ev - (cl0 + e == tl ? 1.f : 0.f)) * rw;
         }
       }
-      x[cb][0] = acc_frag(s[cb], 0);
-      x[cb][1] = acc_frag(s[cb], 1);
+      x[cb][0] = acc_frag(sa[cb], 0);
+      x[cb][1] = acc_frag(sa[cb], 1);
     }
-    // dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r]   (A = transposed reads of the W image)
-    bf16x8 ta = tr_frag(cimg, 0, 0, lane), tb;
-#pragma unroll
-    for (int q = 0; q < KB * 4; ++q) {
-      const int kb = q >> 2, cb = (q >> 1) & 1, st = q & 1;
-      if (q + 1 < KB * 4) {
-        const int q1 = q + 1;
-        tb = tr_frag(cimg, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, lane);
-      }
-      dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta, x[cb][st], dacc[kb], 0, 0, 0);
-      ta = tb;
-    }
+    // ---- dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r], q = (kb, cb, st); transposed fragments DEPTH ahead
+    bf16x8 tf[DT + 1];
+    [&]<int... P>(std::integer_sequence<int, P...>) {
+      (tr_frag_o<TILE, ((P >> 1) & 1) * 32 + 16 * (P & 1), (P >> 2) * 32, BOFF>(tf[P], o), ...);
+    }(std::make_integer_sequence<int, DT>{});
+    asm volatile("" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[1][0]), "+v"(x[1][1]));
+    mfma_operand_fence();  // the x fragments were just written by VALU
+    [&]<int... Q>(std::integer_sequence<int, Q...>) {
+      (
+          [&] {
+            constexpr int q = Q;
+            if constexpr (q + DT < NQ) {
+              constexpr int q1 = q + DT;
+              tr_frag_o<TILE, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, BOFF>(tf[q1 % (DT + 1)], o);
+            }
+            constexpr int ahead = (NQ - 1 - q) < DT ? (NQ - 1 - q) : DT;
+            lds_wait<2 * ahead>(tf[q % (DT + 1)]);
+            mfma_agpr(dacc[q >> 2], tf[q % (DT + 1)], x[(q >> 1) & 1][q & 1]);
+          }(),
+          ...);
+    }(std::make_integer_sequence<int, NQ>{});
     dma_wait();
     __syncthreads();
+  };
+  for (int t = 0; t < ntiles; ++t) {
+    tile(t);
+    const int sh = (t & 1) ? -IMG : IMG;  // next tile's buffer
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o.roff[c] += sh;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      o.troff[v][0] += sh;
+      o.troff[v][1] += sh;
+    }
   }
+  mfma_drain();
   if (r < M) {
     float* out = dHp + ((long)blockIdx.y * M + r) * D;
 #pragma unroll

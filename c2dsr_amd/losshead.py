@@ -108,9 +108,12 @@ class LossHeadFn(Function):
             if fused:
                 M2 = 2 * BR
                 M_pad = -(-M2 // 64) * 64
-                n_pad = -(-n // 128) * 128
+                n_pad = -(-n // 128) * 128 + 64  # + a 64-value tail: tiles near n DMA 64 constants
                 Hb = torch.empty(M2, d, device=dev, dtype=torch.bfloat16)
-                Wb = torch.empty(n, d, device=dev, dtype=torch.bfloat16)
+                n64 = -(-n // 64) * 64  # whole 64-row W tiles for the LDS-DMA (zero rows past n)
+                Wb = torch.empty(n64, d, device=dev, dtype=torch.bfloat16)
+                if n64 > n:
+                    Wb[n:].zero_()
                 lib('c2dsr_f32_to_bf16', Hcat, Hcat.numel(), Hb, s)
                 lib('c2dsr_f32_to_bf16', W, W.numel(), Wb, s)
                 bias2 = torch.empty(n_pad, **f32)

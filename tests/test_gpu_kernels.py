@@ -268,10 +268,13 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     lam = 0.7
     s = stream()
     d = lambda x: x.to(DEV)  # noqa: E731
-    Hb, Wb = d(H.to(torch.bfloat16)), d(W.to(torch.bfloat16))
+    Hb = d(H.to(torch.bfloat16))
+    n64 = -(-n // 64) * 64  # the fused kernels read whole 64-row W tiles: zero rows past n
+    Wb = torch.zeros(n64, D, dtype=torch.bfloat16, device=DEV)
+    Wb[:n] = d(W.to(torch.bfloat16))
     ns, nr = 3, 2
     M_pad = -(-M // 64) * 64
-    n_pad = -(-n // 128) * 128
+    n_pad = -(-n // 128) * 128 + 64
     bias2 = torch.empty(n_pad, device=DEV)
     lib('c2dsr_ce_bias2', d(b), n, n_pad, bias2, s)
     pm, ps = torch.empty(ns, M, device=DEV), torch.empty(ns, M, device=DEV)
