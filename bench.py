@@ -67,43 +67,50 @@ def make_args(cfg, device, precision, dropout=0.2):
 
 
 class KernelTimer:
-    """HIP-event timing (on the stream the kernel is launched on, inside the timed region) of the
-    dominant kernel: the fused classifier-head dW kernel (K5, c2dsr_ce_fused_dw) in bf16 mode, the
-    materialised-logits GEMMs otherwise.  Algorithmic FLOPs per launch = 2·M·n·d (the dW product;
-    the recomputed logits tile is overhead and not credited)."""
+    """HIP-event timing (on the stream the kernels are launched on, inside the timed region) of the
+    dominant op, K5 — the fused classifier head + cross-entropy — in bf16 mode: its three kernels
+    c2dsr_ce_fused_fwd (online log-sum-exp), c2dsr_ce_fused_dh, c2dsr_ce_fused_dw.  Credited FLOPs
+    (SURVEY.md §8(d)): 2·M·n·d per launch of each (forward logits, dH, dW products); the logits tiles
+    the two backward kernels recompute are overhead and not credited.  fp32 mode: the materialised
+    logits GEMMs (c2dsr_gemm calls of > 1e11 FLOP)."""
+
+    NAMES_BF16 = ('c2dsr_ce_fused_fwd', 'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
 
     def __init__(self, precision):
         from c2dsr_amd._lib import lib
         self.lib = lib
-        self.name = 'c2dsr_ce_fused_dw' if precision == 'bf16' else 'c2dsr_gemm'
+        self.names = self.NAMES_BF16 if precision == 'bf16' else ('c2dsr_gemm',)
 
     def start(self):
         self.lib.timed.clear()
-        self.lib.time_names.add(self.name)
+        self.lib.time_names.update(self.names)
 
     def stop(self):
-        self.lib.time_names.discard(self.name)
+        self.lib.time_names.difference_update(self.names)
 
     def summary(self):
-        recs = self.lib.timed.get(self.name, [])
         torch.cuda.synchronize()
-        ms, fl = [], []
-        for e0, e1, a in recs:
-            if self.name == 'c2dsr_ce_fused_dw':
-                M, n, D = a[3], a[4], a[5]
-                f = 2.0 * M * n * D
-            else:
-                M, N, K = a[2], a[3], a[4]
-                f = 2.0 * M * N * K
-                if f < 1e11:  # only the classifier-head GEMMs
-                    continue
-            ms.append(e0.elapsed_time(e1))
-            fl.append(f)
-        if not ms:
+        per = {}
+        ms_all, fl_all = 0.0, 0.0
+        for name in self.names:
+            ms, fl = [], []
+            for e0, e1, a in self.lib.timed.get(name, []):
+                if name == 'c2dsr_gemm':
+                    f = 2.0 * a[2] * a[3] * a[4]
+                    if f < 1e11:  # only the classifier-head GEMMs
+                        continue
+                else:  # (Hb, Wb, bias2, M, n, D, ...)
+                    f = 2.0 * a[3] * a[4] * a[5]
+                ms.append(e0.elapsed_time(e1))
+                fl.append(f)
+            if ms:
+                per[name] = dict(launches=len(ms), avg_ms=round(sum(ms) / len(ms), 4),
+                                 tflops=round(sum(fl) / (sum(ms) * 1e-3) / 1e12, 1))
+                ms_all += sum(ms)
+                fl_all += sum(fl)
+        if not per:
             return None
-        tot_ms, tot_fl = sum(ms), sum(fl)
-        return dict(launches=len(ms), avg_ms=tot_ms / len(ms), tflops=tot_fl / (tot_ms * 1e-3) / 1e12,
-                    flop_per_launch=tot_fl / len(ms))
+        return dict(tflops=fl_all / (ms_all * 1e-3) / 1e12, ms=ms_all, per_kernel=per)
 
 
 def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
@@ -225,10 +232,10 @@ def main():
         if ks is not None:
             roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
                         frac=round(ks['tflops'] / peak, 4), traffic=None,
-                        kernel=('ce_dw_kernel<256> (K5 fused classifier-head dW/db, bf16 MFMA)'
+                        kernel=('K5 fused classifier head + CE: ce_lse_kernel + ce_dh_kernel + ce_dw_kernel '
+                                '(bf16 MFMA); credited 2·M·n·d per launch each'
                                 if opt.precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
-                        avg_launch_ms=round(ks['avg_ms'], 4), flop_per_launch=ks['flop_per_launch'],
-                        launches=ks['launches'])
+                        ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'])
         cpu = None
         if world == 1 and not opt.no_cpu_baseline:
             cpu = cpu_baseline(cfg, rows, gs, gp, opt.cpu_budget)

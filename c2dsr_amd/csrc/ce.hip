@@ -19,9 +19,6 @@
 // prefetch.  Work is split over column (lse, dH) or row (dW) ranges for occupancy and
 // the partials are combined in a fixed order (deterministic).
 #include "img.h"
-#ifndef C2_DT
-#define C2_DT 3
-#endif
 
 #include <utility>
 
@@ -160,12 +157,24 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
 
 // ---------------------------------------------------------------- backward: dH
 // grid (ceil(M/128), n_split); 4 waves x 32 rows, one wave per SIMD (512 registers); sweeps the
-// split's columns 64 at a time.  Every LDS fragment read is an asm ds_read at a precomputed
-// per-lane offset + immediate (no address VALU in the loop), issued DEPTH MFMAs ahead of its
-// consumer with a counted lgkmcnt wait; the dHᵀ accumulators live in AGPRs for the whole sweep;
-// W tiles arrive by saddr LDS-DMA (scalar tile base, per-lane offsets computed once).
-// Wb must hold ⌈n/64⌉·64 rows (zero padding past n); bias2 is -inf past n.
-// dHp [n_split][M][D] (fp32 partials, combined by c2dsr_sum_parts).
+// split's columns 64 at a time, software-pipelined over three W images:
+//   step t:  [ S(t+1) = W_{t+1}·Hᵀ on the matrix cores  ∥  epilogue of S(t) on the VALU ]
+//            dHᵀ += W_tᵀ·P'ᵀ(t);  tile t+3 lands while tile t+2 waits
+// The epilogue is P'ᵀ[c][r] = 2^(s·log2e + b2[c] + cr[r]) with cr = log2(w_r) - lse2_r (the row
+// weight folded into the exponent; w = 0 → -inf → 0); the one-hot part of (softmax - onehot)
+// is the exact per-row correction -w_r·W[t_r] applied by c2dsr_ce_dh_combine.  Every LDS fragment
+// read is an asm ds_read at a precomputed per-lane offset, issued ahead of its MFMA with a counted
+// wait; all MFMAs are asm (fixed order), the dHᵀ accumulators live in AGPRs; a sched_barrier
+// between chunks keeps each epilogue slice in its MFMA gap.
+// Wb holds ⌈n/64⌉·64 rows (zero padding past n); bias2 is -inf past n.
+// dHp [n_split][M][D] fp32 partials.
+__device__ __forceinline__ void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b));
+}
+
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
                                                        const float* __restrict__ bias2, int M, int n,
@@ -175,156 +184,184 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
   constexpr int NQ = KB * 4;
-  constexpr int DEPTH = 3;    // S-phase row fragments ahead
-  constexpr int DT = C2_DT;   // dH-phase transposed fragments ahead
-  constexpr int IMG = TILE * D * 2;            // bytes per image
+  constexpr int DS = 3;                          // S-phase row fragments ahead
+  constexpr int DT = 3;                          // dH-phase transposed fragments ahead
+  constexpr int EPK = 16 / KS;                   // epilogue elements per S k-step (per column block)
+  constexpr int IMG = TILE * D * 2;              // bytes per image
   constexpr int NDMA = (TILE / 4) * (D / 128) / 4;  // DMA wave-instructions per wave per tile
-  __shared__ __attribute__((aligned(16))) char img[2][IMG];
-  __shared__ __attribute__((aligned(16))) float b2s[2][TILE];
+  __shared__ __attribute__((aligned(16))) char img[3][IMG];
+  __shared__ __attribute__((aligned(16))) float b2s[3][TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x * 128 + w * 32 + (lane & 31);
   const int rc = min(r, M - 1);
   const int c_beg = blockIdx.y * cols_per_split;
   const int c_end = min(n, c_beg + cols_per_split);
   const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
-  // ---- per-lane constants
-  ImgOffsets o = img_offsets(lane);
-  const int ib = (int)lds_addr(img[0]);
-#pragma unroll
-  for (int c = 0; c < 8; ++c) o.roff[c] += ib;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    o.troff[v][0] += ib;
-    o.troff[v][1] += ib;
-  }
-  unsigned dvoff[NDMA], ddst[NDMA];
-#pragma unroll
-  for (int i = 0; i < NDMA; ++i) {
-    const int q = w + 4 * i;
-    constexpr int GROUPS = TILE / 4;
-    const int half = q / GROUPS, rg = q % GROUPS;
-    const int row = rg * 4 + (lane >> 4);
-    const int lch = (lane & 15) ^ swz_f(row);
-    dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
-    ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
-  }
-  auto dma = [&](int c0, int buf) {
-    const bf16* base = Wb + (long)c0 * D;
-#pragma unroll
-    for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
-    dma_vec64(bias2 + c0, b2s[buf], 0);
-  };
-  bf16x8 hf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
-  float lr = lse2[rc];
-  float rw = r < M ? roww[rc] : 0.f;
-  int tr = tgt32[rc];
-  if (ntiles > 0) dma(c_beg, 0);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
-  pin(lr);
-  pin(rw);
-  pin(tr);
   f32x16 dacc[KB];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dacc[kb][i] = 0.f;
-  vm_drain();
-  dma_wait();
-  __syncthreads();
-  const int c_last = c_beg + (ntiles - 1) * TILE;
-
-  // one column tile: S, softmax-gradient epilogue, dHᵀ update.  The image of tile t is buffer
-  // t & 1; `o` holds the offsets into it (swapped to the other buffer after every tile).
-  auto tile = [&](int t) {
-    constexpr int BOFF = 0;
-    const int buf = t & 1;
-    const int c0 = c_beg + t * TILE;
-    dma(min(c0 + TILE, c_last), buf ^ 1);  // the last tile re-loads itself: no branch here
-    const float* cb2s = b2s[buf];
-    // ---- S = W_tile · Hᵀ  (2 column blocks x 16 k-steps), fragments DEPTH k-steps ahead
-    f32x16 sa[2];
-    bf16x8 fa[DEPTH + 1][2];
-    [&]<int... P>(std::integer_sequence<int, P...>) {
-      ((row_frag_o<TILE, 0, P, BOFF>(fa[P][0], o), row_frag_o<TILE, 32, P, BOFF>(fa[P][1], o)), ...);
-    }(std::make_integer_sequence<int, DEPTH>{});
-    [&]<int... K>(std::integer_sequence<int, K...>) {
-      (
-          [&] {
-            constexpr int ks = K;
-            if constexpr (ks + DEPTH < KS) {
-              row_frag_o<TILE, 0, ks + DEPTH, BOFF>(fa[(ks + DEPTH) % (DEPTH + 1)][0], o);
-              row_frag_o<TILE, 32, ks + DEPTH, BOFF>(fa[(ks + DEPTH) % (DEPTH + 1)][1], o);
-            }
-            constexpr int ahead = (KS - 1 - ks) < DEPTH ? (KS - 1 - ks) : DEPTH;
-            lds_wait2<2 * ahead>(fa[ks % (DEPTH + 1)][0], fa[ks % (DEPTH + 1)][1]);
-            if constexpr (ks == 0) {
-              sa[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
-              sa[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
-            } else {
-              sa[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DEPTH + 1)][0], hf[ks], sa[0], 0, 0, 0);
-              sa[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DEPTH + 1)][1], hf[ks], sa[1], 0, 0, 0);
-            }
-          }(),
-          ...);
-    }(std::make_integer_sequence<int, KS>{});
-    // ---- P'ᵀ[c][r] = (2^(s·log2e + b2 - lse2) - [c == t]) * w_r   (b2 = -inf past n → 0)
-    bf16x8 x[2][2];
-    const int tl = tr - c0;
+  if (ntiles > 0) {
+    const int c_last = c_beg + (ntiles - 1) * TILE;
+    // ---- per-lane constants
+    const ImgOffsets o0 = img_offsets(lane);
+    const int ib = (int)lds_addr(img[0]);
+    unsigned dvoff[NDMA], ddst[NDMA];
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-#pragma unroll
-      for (int j4 = 0; j4 < 4; ++j4) {
-        const int cl0 = cb * 32 + 8 * j4 + 4 * (lane >> 5);
-        const float4 b4 = *(const float4*)&cb2s[cl0];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * j4 + e;
-          const float ev = ex2(fmaf(sa[cb][i], LOG2E, ((const float*)&b4)[e]) - lr);
-          sa[cb][i] = (ev - (cl0 + e == tl ? 1.f : 0.f)) * rw;
-        }
-      }
-      x[cb][0] = acc_frag(sa[cb], 0);
-      x[cb][1] = acc_frag(sa[cb], 1);
+    for (int i = 0; i < NDMA; ++i) {
+      const int q = w + 4 * i;
+      constexpr int GROUPS = TILE / 4;
+      const int half = q / GROUPS, rg = q % GROUPS;
+      const int row = rg * 4 + (lane >> 4);
+      const int lch = (lane & 15) ^ swz_f(row);
+      dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
+      ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
     }
-    // ---- dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r], q = (kb, cb, st); transposed fragments DEPTH ahead
-    bf16x8 tf[DT + 1];
-    [&]<int... P>(std::integer_sequence<int, P...>) {
-      (tr_frag_o<TILE, ((P >> 1) & 1) * 32 + 16 * (P & 1), (P >> 2) * 32, BOFF>(tf[P], o), ...);
-    }(std::make_integer_sequence<int, DT>{});
-    asm volatile("" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[1][0]), "+v"(x[1][1]));
-    mfma_operand_fence();  // the x fragments were just written by VALU
-    [&]<int... Q>(std::integer_sequence<int, Q...>) {
-      (
-          [&] {
-            constexpr int q = Q;
-            if constexpr (q + DT < NQ) {
-              constexpr int q1 = q + DT;
-              tr_frag_o<TILE, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, BOFF>(tf[q1 % (DT + 1)], o);
-            }
-            constexpr int ahead = (NQ - 1 - q) < DT ? (NQ - 1 - q) : DT;
-            lds_wait<2 * ahead>(tf[q % (DT + 1)]);
-            mfma_agpr(dacc[q >> 2], tf[q % (DT + 1)], x[(q >> 1) & 1][q & 1]);
-          }(),
-          ...);
-    }(std::make_integer_sequence<int, NQ>{});
+    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % 3
+      const int c0 = min(c_beg + tt * TILE, c_last);
+      const int buf = tt % 3;
+      const bf16* base = Wb + (long)c0 * D;
+#pragma unroll
+      for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
+      dma_vec64(bias2 + c0, b2s[buf], 0);
+    };
+    bf16x8 hf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
+    const float rw = r < M ? roww[rc] : 0.f;
+    float cr = rw > 0.f ? __log2f(rw) - lse2[rc] : -INFINITY;
+    dma(0);
+    dma(1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
+    pin(cr);
+    vm_drain();
     dma_wait();
     __syncthreads();
-  };
-  for (int t = 0; t < ntiles; ++t) {
-    tile(t);
-    const int sh = (t & 1) ? -IMG : IMG;  // next tile's buffer
+
+    // offsets into buffer b of the 16 per-lane fragment bases
+    auto offs = [&](int b, int (&ro)[8], int (&to)[4][2]) {
+      const int add = ib + b * IMG;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) o.roff[c] += sh;
+      for (int c = 0; c < 8; ++c) ro[c] = o0.roff[c] + add;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      o.troff[v][0] += sh;
-      o.troff[v][1] += sh;
+      for (int v = 0; v < 4; ++v) {
+        to[v][0] = o0.troff[v][0] + add;
+        to[v][1] = o0.troff[v][1] + add;
+      }
+    };
+    // ---- S(0) (not overlapped)
+    f32x16 sc[2];
+    {
+      int ro[8], to[4][2];
+      offs(0, ro, to);
+      ImgOffsets oS;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) oS.roff[c] = ro[c];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 f0 = *(const bf16x8*)(img[0] + o0.roff[ks & 7] + (ks >> 3) * TILE * 256);
+        const bf16x8 f1 = *(const bf16x8*)(img[0] + o0.roff[ks & 7] + (ks >> 3) * TILE * 256 + 32 * 256);
+        if (ks == 0) {
+          sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, hf[0], f32x16{}, 0, 0, 0);
+          sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, hf[0], f32x16{}, 0, 0, 0);
+        } else {
+          sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, hf[ks], sc[0], 0, 0, 0);
+          sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, hf[ks], sc[1], 0, 0, 0);
+        }
+      }
+    }
+    for (int t = 0; t < ntiles; ++t) {
+      const int bh = t % 3, bs = (t + 1) % 3;
+      dma(t + 2);  // into the buffer tile t-1 used (every wave passed the barrier after its dH)
+      ImgOffsets oS, oH;
+      {
+        int ro[8], to[4][2];
+        offs(bs, ro, to);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) oS.roff[c] = ro[c];
+        offs(bh, ro, to);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          oH.troff[v][0] = to[v][0];
+          oH.troff[v][1] = to[v][1];
+        }
+      }
+      const float* cb2s = b2s[bh];
+      float4 b4[2][4];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) b4[cb][j4] = *(const float4*)&cb2s[cb * 32 + 8 * j4 + 4 * (lane >> 5)];
+      // ---- S(t+1) ∥ epilogue(t): k-step ks runs 2 MFMAs, issues the reads DS steps ahead, and
+      // computes EPK elements of each column block of S(t)
+      f32x16 sn[2];
+      bf16x8 fa[DS + 2][2];  // ring one longer than the lookahead: a slot is rewritten two MFMAs after its read
+      bf16x8 x[2][2];
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((fa[P][0] = row_frag_c<TILE, 0, P, 0>(oS), fa[P][1] = row_frag_c<TILE, 32, P, 0>(oS)), ...);
+      }(std::make_integer_sequence<int, DS>{});
+      __builtin_amdgcn_sched_barrier(0);
+      [&]<int... K>(std::integer_sequence<int, K...>) {
+        (
+            [&] {
+              constexpr int ks = K;
+              if constexpr (ks + DS < KS) {
+                fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
+                fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
+              }
+              if constexpr (ks == 0) {
+                sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
+                sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
+              } else {
+                sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][0], hf[ks], sn[0], 0, 0, 0);
+                sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][1], hf[ks], sn[1], 0, 0, 0);
+              }
+              // epilogue slice: elements [ks·EPK, ks·EPK + EPK) of both column blocks
+#pragma unroll
+              for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int e = 0; e < EPK; ++e) {
+                  const int i = ks * EPK + e;
+                  sc[cb][i] = ex2(fmaf(sc[cb][i], LOG2E, ((const float*)&b4[cb][i >> 2])[i & 3]) + cr);
+                }
+              if constexpr ((ks * EPK + EPK) % 8 == 0) {
+                constexpr int st = (ks * EPK) / 8;
+                x[0][st] = acc_frag(sc[0], st);
+                x[1][st] = acc_frag(sc[1], st);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, KS>{});
+      // ---- dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r], q = (kb, cb, st)
+      bf16x8 tf[DT + 2];
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((tf[P] = tr_frag_c<TILE, ((P >> 1) & 1) * 32 + 16 * (P & 1), (P >> 2) * 32, 0>(oH)), ...);
+      }(std::make_integer_sequence<int, DT>{});
+      __builtin_amdgcn_sched_barrier(0);
+      [&]<int... Q>(std::integer_sequence<int, Q...>) {
+        (
+            [&] {
+              constexpr int q = Q;
+              if constexpr (q + DT < NQ) {
+                constexpr int q1 = q + DT;
+                tf[q1 % (DT + 2)] = tr_frag_c<TILE, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, 0>(oH);
+              }
+              dacc[q >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[(q >> 1) & 1][q & 1],
+                                                                   dacc[q >> 2], 0, 0, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, NQ>{});
+      // S(t+1) becomes the next step's S(t): its MFMAs have long retired (the dH chain ran since)
+      sc[0] = sn[0];
+      sc[1] = sn[1];
+      dma_wait();
+      __syncthreads();
     }
   }
-  mfma_drain();
   if (r < M) {
     float* out = dHp + ((long)blockIdx.y * M + r) * D;
 #pragma unroll
@@ -332,6 +369,20 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int i = 0; i < 16; ++i) out[kb * 32 + creg(i, lane)] = dacc[kb][i];
   }
+}
+
+// dH[r] = Σ_s dHp[s][r] - (0 <= t_r < n ? w_r·W[t_r] : 0)   (the one-hot part of P'; fixed order)
+__global__ void ce_dh_combine_kernel(const float* __restrict__ dHp, int ns, int M, int D,
+                                     const int* __restrict__ t32, const float* __restrict__ rw,
+                                     const float* __restrict__ W, int n, float* __restrict__ dH) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= (long)M * D) return;
+  const int r = (int)(i / D), k = (int)(i % D);
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < ns; ++s) t = c2::operator+(t, *(const float4*)(dHp + (long)s * M * D + i));
+  const int tg = t32[r];
+  if (tg >= 0 && tg < n) t = c2::fma4(-rw[r], *(const float4*)(W + (long)tg * D + k), t);
+  *(float4*)(dH + i) = t;
 }
 
 // ---------------------------------------------------------------- backward: dW, db
@@ -624,6 +675,17 @@ C2_API int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2,
                                            dbp);
   else
     return (int)hipErrorInvalidValue;
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// dH = Σ_s dHp[s] - w_r·W[t_r]  (the one-hot part of P' for rows with an item target)
+C2_API int c2dsr_ce_dh_combine(const float* dHp, int ns, int M, int D, const int* t32, const float* rw, const float* W,
+                               int n, float* dH, void* stream) {
+  if (M == 0) return 0;
+  if (D % 4) return (int)hipErrorInvalidValue;
+  ce_dh_combine_kernel<<<c2::ceil_div((long)M * D / 4, 256), 256, 0, (hipStream_t)stream>>>(dHp, ns, M, D, t32, rw, W,
+                                                                                            n, dH);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -162,6 +162,21 @@ __device__ __forceinline__ void mfma_agpr(f32x16& acc, const bf16x8& a, const bf
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 __device__ __forceinline__ void mfma_operand_fence() { asm volatile("s_nop 1" ::: "memory"); }
+// the same, preceded (inside the statement) by `s_waitcnt lgkmcnt(N)` for asm-read operands: a
+// separate wait statement that names the operand makes hipcc see a fresh VGPR write and pad the
+// MFMA with s_nop (17-43 cycles each between MFMAs)
+template <int N>
+__device__ __forceinline__ void mfma_agpr_w(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%3)\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b), "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void mfma_v_w(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%3)\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b), "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void mfma_v0_w(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%3)\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(acc) : "v"(a), "v"(b), "n"(N));
+}
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 3" ::: "memory"); }
 
 // ---------------------------------------------------------------- precomputed-offset image access
@@ -211,6 +226,31 @@ __device__ __forceinline__ void tr_frag_o(bf16x8& v, const ImgOffsets& o) {
   v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
   v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
 }
+// Compiler-visible LDS fragment loads at a per-lane offset (an LDS byte address) + IMM: hipcc
+// counts them (exact lgkmcnt waits, no hazard pads); keep them DEPTH steps ahead with
+// __builtin_amdgcn_sched_barrier(0) between steps so the scheduler cannot sink them to their use.
+typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
+template <int IMM>
+__device__ __forceinline__ bf16x8 lds_ld128(int off) {
+  return *(const lds_bf16x8*)(size_t)(unsigned)(off + IMM);
+}
+template <int TR, int R0, int KS, int BUF>
+__device__ __forceinline__ bf16x8 row_frag_c(const ImgOffsets& o) {
+  return lds_ld128<BUF + (KS >> 3) * TR * 256 + R0 * 256>(o.roff[KS & 7]);
+}
+template <int TR, int RR0, int KB0, int BUF>
+__device__ __forceinline__ bf16x8 tr_frag_c(const ImgOffsets& o) {
+  constexpr int IMM = BUF + RR0 * 256 + (KB0 >> 7) * TR * 256;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4*)(size_t)(unsigned)(o.troff[(KB0 & 127) / 32][0] + IMM));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_bf16x4*)(size_t)(unsigned)(o.troff[(KB0 & 127) / 32][1] + IMM));
+  bf16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
 // LDS-DMA with a scalar global base and a per-lane 32-bit byte offset (saddr form)
 __device__ __forceinline__ void dma16_s(const void* sbase, unsigned voff, unsigned lds_dst) {
   asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2 offset:0"

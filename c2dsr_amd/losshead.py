@@ -184,7 +184,7 @@ class LossHeadFn(Function):
                 ns = split_count(M2, 128)
                 dHp = torch.empty(ns, M2, d, **f32)
                 lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M2, n, d, ns, lse2, t32, rw, dHp, s)
-                lib('c2dsr_sum_parts', dHp, ns, M2 * d, 0.0, dHcat, s)
+                lib('c2dsr_ce_dh_combine', dHp, ns, M2, d, t32, rw, W, n, dHcat, s)
                 del dHp
                 nr = split_count(n, 128)
                 dWp = torch.empty(nr, n, d, **f32)

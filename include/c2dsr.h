@@ -129,11 +129,15 @@ int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2, int M
 int c2dsr_ce_row_weights(const int64_t* tgt, int M, int M_pad, int ignore, const float* coef, int split,
                          const float* gscale, float lam, const float* padlogit, const float* lse, float* rw, int* t32,
                          float* lse2, float* dpad, void* stream);
-/* dHp[s][r] = Σ_{c∈split s} P'[r][c]·W[c], P' = (softmax - onehot)·rw  ([n_split][M][D]; c2dsr_sum_parts).
- * Wb holds ⌈n/64⌉·64 rows (zero rows past n); bias2 holds n_pad + 64 values (-inf past n). */
+/* dHp[s][r] = Σ_{c∈split s} softmax[r][c]·rw_r·W[c]  ([n_split][M][D]; the one-hot part and the split
+ * sum are applied by c2dsr_ce_dh_combine).  Wb holds ⌈n/64⌉·64 rows (zero rows past n); bias2 holds
+ * n_pad + 64 values (-inf past n). */
 int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
                       const float* lse2, const int* t32, const float* rw, float* dHp, void* stream);
 /* dWp[s][c] = Σ_{r∈split s} P'[r][c]·H[r];  dbp[s][c] = Σ_r P'[r][c]  ([n_rsplit][n][D], [n_rsplit][n]) */
+/* dH[r] = Σ_s dHp[s][r] - (0 <= t32[r] < n ? rw[r]·W[t32[r]] : 0)  (W fp32 [n][D]; fixed order) */
+int c2dsr_ce_dh_combine(const float* dHp, int ns, int M, int D, const int* t32, const float* rw, const float* W, int n,
+                        float* dH, void* stream);
 int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
                       const float* lse2, const int* t32, const float* rw, float* dWp, float* dbp, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
