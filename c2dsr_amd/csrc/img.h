@@ -230,9 +230,12 @@ __device__ __forceinline__ void tr_frag_o(bf16x8& v, const ImgOffsets& o) {
 // counts them (exact lgkmcnt waits, no hazard pads); keep them DEPTH steps ahead with
 // __builtin_amdgcn_sched_barrier(0) between steps so the scheduler cannot sink them to their use.
 typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
+// An LDS byte address with a provably clear sign bit: only then does the backend fold a
+// constant into the ds_read offset field instead of materialising one address per read.
+__device__ __forceinline__ unsigned lds_base(int off) { return (unsigned)off & 0x3ffffu; }
 template <int IMM>
 __device__ __forceinline__ bf16x8 lds_ld128(int off) {
-  return *(const lds_bf16x8*)(size_t)(unsigned)(off + IMM);
+  return *(const lds_bf16x8*)(size_t)(lds_base(off) + IMM);
 }
 template <int TR, int R0, int KS, int BUF>
 __device__ __forceinline__ bf16x8 row_frag_c(const ImgOffsets& o) {
@@ -242,9 +245,9 @@ template <int TR, int RR0, int KB0, int BUF>
 __device__ __forceinline__ bf16x8 tr_frag_c(const ImgOffsets& o) {
   constexpr int IMM = BUF + RR0 * 256 + (KB0 >> 7) * TR * 256;
   const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-      (lds_bf16x4*)(size_t)(unsigned)(o.troff[(KB0 & 127) / 32][0] + IMM));
+      (lds_bf16x4*)(size_t)(lds_base(o.troff[(KB0 & 127) / 32][0]) + IMM));
   const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-      (lds_bf16x4*)(size_t)(unsigned)(o.troff[(KB0 & 127) / 32][1] + IMM));
+      (lds_bf16x4*)(size_t)(lds_base(o.troff[(KB0 & 127) / 32][1]) + IMM));
   bf16x8 v;
   v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
   v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
