@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
 //   step t:  [ S(t+1) = W_{t+1}·Hᵀ on the matrix cores  ∥  epilogue of S(t) on the VALU ]
 //            dHᵀ += W_tᵀ·P'ᵀ(t);  tile t+3 lands while tile t+2 waits
 // The epilogue is P'ᵀ[c][r] = 2^(s·log2e + b2[c] + cr[r]) with cr = log2(w_r) - lse2_r (the row
-// weight folded into the exponent; w = 0 → -inf → 0); the one-hot part of (softmax - onehot)
+// weight folded into the exponent; w = 0 → -inf → 0; from c2dsr_ce_row_weights); the one-hot part of (softmax - onehot)
 // is the exact per-row correction -w_r·W[t_r] applied by c2dsr_ce_dh_combine.  Every LDS fragment
 // read is an asm ds_read at a precomputed per-lane offset, issued ahead of its MFMA with a counted
 // wait; all MFMAs are asm (fixed order), the dHᵀ accumulators live in AGPRs; a sched_barrier
@@ -178,9 +178,8 @@ __device__ __forceinline__ void mfma_v0(f32x16& acc, const bf16x8& a, const bf16
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
                                                        const float* __restrict__ bias2, int M, int n,
-                                                       int cols_per_split, const float* __restrict__ lse2,
-                                                       const int* __restrict__ tgt32,
-                                                       const float* __restrict__ roww, float* __restrict__ dHp) {
+                                                       int cols_per_split, const float* __restrict__ crow,
+                                                       float* __restrict__ dHp) {
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
   constexpr int NQ = KB * 4;
@@ -229,8 +228,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
     bf16x8 hf[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
-    const float rw = r < M ? roww[rc] : 0.f;
-    float cr = rw > 0.f ? __log2f(rw) - lse2[rc] : -INFINITY;
+    float cr = r < M ? crow[rc] : -INFINITY;
     dma(0);
     dma(1);
 #pragma unroll
@@ -288,12 +286,13 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
           oH.troff[v][1] = to[v][1];
         }
       }
-      const float* cb2s = b2s[bh];
-      float4 b4[2][4];
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int j4 = 0; j4 < 4; ++j4) b4[cb][j4] = *(const float4*)&cb2s[cb * 32 + 8 * j4 + 4 * (lane >> 5)];
+      f32x4 b4[2][4];
+      {
+        const int bo = (int)lds_addr(b2s[0]) + 16 * (lane >> 5) + bh * (TILE * 4);
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+          ((b4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(bo)), ...);
+        }(std::make_integer_sequence<int, 8>{});
+      }
       // ---- S(t+1) ∥ epilogue(t): k-step ks runs 2 MFMAs, issues the reads DS steps ahead, and
       // computes EPK elements of each column block of S(t)
       f32x16 sn[2];
@@ -386,117 +385,205 @@ __global__ void ce_dh_combine_kernel(const float* __restrict__ dHp, int ns, int 
 }
 
 // ---------------------------------------------------------------- backward: dW, db
-// grid (ceil(n/128), n_rsplit); 4 waves x 32 columns; sweeps the split's rows.
-// Per-row constants are padded to a multiple of TILE rows (lse2 0, roww 0, tgt32 -1).
-// dWp [n_rsplit][n][D], dbp [n_rsplit][n] fp32 partials.
+// grid (ceil(n/128), n_rsplit); 4 waves x 32 columns, one wave per SIMD; sweeps the split's rows
+// 64 at a time over three H images — the dH kernel with the roles of H and W exchanged:
+//   step t:  [ S(t+1) = H_{t+1}·W_cᵀ on the matrix cores  ∥  epilogue of S(t), first 24 of 32 ]
+//            [ dWᵀ += H_tᵀ·P'(t)                          ∥  epilogue of S(t), last 8        ]
+// P'[r][c] = 2^(s·log2e + cr_r + b2_c) - [t_r = c]·w_r with cr = log2(w_r) - lse2_r (c2dsr_ce_row_weights);
+// db[c] = Σ_r P'[r][c].  The dWᵀ MFMAs run column-block-major (x[0][0] first), so the last
+// epilogue slice overlaps the first 24 of them.
+// Hb holds ⌈M/64⌉·64 rows (zero padding past M); crow / roww / tgt32 are padded likewise
+// (-inf / 0 / -1).  dWp [n_rsplit][n][D], dbp [n_rsplit][n] fp32 partials.
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
                                                        const float* __restrict__ bias2, int M, int n,
-                                                       int rows_per_split, const float* __restrict__ lse2,
+                                                       int rows_per_split, const float* __restrict__ crow,
                                                        const int* __restrict__ tgt32,
                                                        const float* __restrict__ roww, float* __restrict__ dWp,
                                                        float* __restrict__ dbp) {
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
-  __shared__ __attribute__((aligned(16))) char img[2][TILE * D * 2];
-  __shared__ __attribute__((aligned(16))) float rl[2][TILE];
-  __shared__ __attribute__((aligned(16))) float rwv[2][TILE];
-  __shared__ __attribute__((aligned(16))) int rt[2][TILE];
+  constexpr int NQ = KB * 4;
+  constexpr int DS = 3;
+  constexpr int DT = 3;
+  constexpr int IMG = TILE * D * 2;
+  constexpr int NDMA = (TILE / 4) * (D / 128) / 4;
+  static_assert(KS >= 8, "the epilogue schedule assumes at least 8 S k-steps");
+  __shared__ __attribute__((aligned(16))) char img[3][IMG];
+  __shared__ __attribute__((aligned(16))) float rv[3][3][TILE];  // [buffer][crow, roww, tgt32][row]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 128 + w * 32 + (lane & 31);
+  const int cc = min(c, n - 1);
   const int r_beg = blockIdx.y * rows_per_split;
   const int r_end = min(M, r_beg + rows_per_split);
   const int ntiles = r_end > r_beg ? (r_end - r_beg + TILE - 1) / TILE : 0;
-  auto issue = [&](int r0, char* img, float* rl, float* rwv, int* rt) {
-    dma_tile<D>(Hb, M, r0, img);
-    dma_vec64(lse2 + r0, rl, 0);
-    dma_vec64(roww + r0, rwv, 1);
-    dma_vec64(tgt32 + r0, rt, 2);
-  };
-  if (ntiles > 0) issue(r_beg, img[0], rl[0], rwv[0], rt[0]);
-  bf16x8 wf[KS];
-  const int cc = min(c, n - 1);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) wf[ks] = *(const bf16x8*)(Wb + (long)cc * D + ks * 16 + 8 * (lane >> 5));
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) pin(wf[ks]);
-  float b2 = bias2[c];  // -inf past n: those columns contribute 0
-  pin(b2);
   f32x16 dacc[KB];
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dacc[kb][i] = 0.f;
   float db = 0.f;
-  vm_drain();
-  dma_wait();
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int cu = t & 1, nx = cu ^ 1;
-    const char* cimg = img[cu];
-    const float* crl = rl[cu];
-    const float* crwv = rwv[cu];
-    const int* crt = rt[cu];
-    char* nimg = img[nx];
-    float* nrl = rl[nx];
-    float* nrwv = rwv[nx];
-    int* nrt = rt[nx];
-    const int r0 = r_beg + t * TILE;
-    if (t + 1 < ntiles) issue(r0 + TILE, nimg, nrl, nrwv, nrt);
-    f32x16 s[2];
+  if (ntiles > 0) {
+    const int r_last = r_beg + (ntiles - 1) * TILE;
+    const ImgOffsets o0 = img_offsets(lane);
+    const int ib = (int)lds_addr(img[0]);
+    const int rvb = (int)lds_addr(rv[0][0]) + 16 * (lane >> 5);
+    unsigned dvoff[NDMA], ddst[NDMA];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s[rb][i] = 0.f;
-    bf16x8 fa[2], fb[2];
-    fa[0] = row_frag(cimg, 0, 0, lane);
-    fa[1] = row_frag(cimg, 32, 0, lane);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 1 < KS) {
-        fb[0] = row_frag(cimg, 0, (ks + 1) * 16, lane);
-        fb[1] = row_frag(cimg, 32, (ks + 1) * 16, lane);
-      }
-      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], wf[ks], s[0], 0, 0, 0);
-      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], wf[ks], s[1], 0, 0, 0);
-      fa[0] = fb[0];
-      fa[1] = fb[1];
+    for (int i = 0; i < NDMA; ++i) {
+      const int q = w + 4 * i;
+      constexpr int GROUPS = TILE / 4;
+      const int half = q / GROUPS, rg = q % GROUPS;
+      const int row = rg * 4 + (lane >> 4);
+      const int lch = (lane & 15) ^ swz_f(row);
+      dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
+      ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
     }
-    bf16x8 x[2][2];
+    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % 3
+      const int r0 = min(r_beg + tt * TILE, r_last);
+      const int buf = tt % 3;
+      const bf16* base = Hb + (long)r0 * D;
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
+      for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
+      dma_vec64(crow + r0, rv[buf][0], 1);
+      dma_vec64(roww + r0, rv[buf][1], 2);
+      dma_vec64(tgt32 + r0, rv[buf][2], 3);
+    };
+    bf16x8 wf[KS];
 #pragma unroll
-      for (int j4 = 0; j4 < 4; ++j4) {
-        const int r4 = rb * 32 + 8 * j4 + 4 * (lane >> 5);
-        const float4 L4 = *(const float4*)&crl[r4];
-        const float4 W4 = *(const float4*)&crwv[r4];
-        const int4 T4 = *(const int4*)&crt[r4];
+    for (int ks = 0; ks < KS; ++ks) wf[ks] = *(const bf16x8*)(Wb + (long)cc * D + ks * 16 + 8 * (lane >> 5));
+    float b2 = bias2[c];  // -inf past n: those columns contribute 0
+    dma(0);
+    dma(1);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * j4 + e;
-          const float ev = ex2(fmaf(s[rb][i], LOG2E, b2) - ((const float*)&L4)[e]);
-          const float v = (ev - (c == ((const int*)&T4)[e] ? 1.f : 0.f)) * ((const float*)&W4)[e];
-          s[rb][i] = v;
-          db += v;
-        }
-      }
-      x[rb][0] = acc_frag(s[rb], 0);
-      x[rb][1] = acc_frag(s[rb], 1);
-    }
-    // dWᵀ[k][c] += Σ_r H[r][k] P'[r][c]   (A = transposed reads of the H image)
-    bf16x8 ta = tr_frag(cimg, 0, 0, lane), tb;
-#pragma unroll
-    for (int q = 0; q < KB * 4; ++q) {
-      const int kb = q >> 2, rb = (q >> 1) & 1, st = q & 1;
-      if (q + 1 < KB * 4) {
-        const int q1 = q + 1;
-        tb = tr_frag(cimg, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, lane);
-      }
-      dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ta, x[rb][st], dacc[kb], 0, 0, 0);
-      ta = tb;
-    }
+    for (int ks = 0; ks < KS; ++ks) pin(wf[ks]);
+    pin(b2);
+    vm_drain();
     dma_wait();
     __syncthreads();
+    auto offs = [&](int b, int (&ro)[8], int (&to)[4][2]) {
+      const int add = ib + b * IMG;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ro[k] = o0.roff[k] + add;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        to[v][0] = o0.troff[v][0] + add;
+        to[v][1] = o0.troff[v][1] + add;
+      }
+    };
+    // ---- S(0) (not overlapped)
+    f32x16 sc[2];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 f0 = *(const bf16x8*)(img[0] + o0.roff[ks & 7] + (ks >> 3) * TILE * 256);
+      const bf16x8 f1 = *(const bf16x8*)(img[0] + o0.roff[ks & 7] + (ks >> 3) * TILE * 256 + 32 * 256);
+      if (ks == 0) {
+        sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, wf[0], f32x16{}, 0, 0, 0);
+        sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, wf[0], f32x16{}, 0, 0, 0);
+      } else {
+        sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, wf[ks], sc[0], 0, 0, 0);
+        sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, wf[ks], sc[1], 0, 0, 0);
+      }
+    }
+    for (int t = 0; t < ntiles; ++t) {
+      const int bh = t % 3, bs = (t + 1) % 3;
+      dma(t + 2);
+      ImgOffsets oS, oH;
+      {
+        int ro[8], to[4][2];
+        offs(bs, ro, to);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) oS.roff[k] = ro[k];
+        offs(bh, ro, to);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          oH.troff[v][0] = to[v][0];
+          oH.troff[v][1] = to[v][1];
+        }
+      }
+      // per-row constants of this lane's 32 rows: element i of column block cb is row cb·32 + creg(i)
+      f32x4 cr4[2][4], w4[2][4];
+      i32x4 t4[2][4];
+      {
+        const int rvo = rvb + bh * (3 * TILE * 4);  // row r4 = cb·32 + 8·j4 + 4·(lane >> 5) of vector k
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+          ((cr4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(rvo),
+            w4[J >> 2][J & 3] = lds_ld<f32x4, TILE * 4 + 128 * (J >> 2) + 32 * (J & 3)>(rvo),
+            t4[J >> 2][J & 3] = lds_ld<i32x4, 2 * TILE * 4 + 128 * (J >> 2) + 32 * (J & 3)>(rvo)),
+           ...);
+        }(std::make_integer_sequence<int, 8>{});
+      }
+      bf16x8 x[2][2];
+#define C2_DW_EPI(cb, i)                                                                                    \
+  {                                                                                                         \
+    const float ev = ex2(fmaf(sc[cb][i], LOG2E, ((const float*)&cr4[cb][(i) >> 2])[(i) & 3]) + b2);         \
+    const float v = ev - (((const int*)&t4[cb][(i) >> 2])[(i) & 3] == c ? ((const float*)&w4[cb][(i) >> 2])[(i) & 3] : 0.f); \
+    sc[cb][i] = v;                                                                                          \
+    db += v;                                                                                                \
+  }
+// the 32 epilogue elements in the order the dWᵀ MFMAs need them (e → block e/16, element e%16) are
+// spread over U = 2·KS + 2·KB issue units: two per S k-step (2 MFMAs), one per dWᵀ step q < 2·KB;
+// x[cb][st] is packed right after its last element, before its first use at q = (2cb + st)·KB
+#define C2_DW_EPI_UNITS(u0, u1)                                                   \
+  {                                                                               \
+    constexpr int U = 2 * KS + 2 * KB;                                            \
+    constexpr int e0 = (32 * (u0) + U - 1) / U, e1 = (32 * (u1) + U - 1) / U;     \
+    _Pragma("unroll") for (int e = e0; e < e1; ++e) C2_DW_EPI(e >> 4, e & 15)     \
+    _Pragma("unroll") for (int cs = 0; cs < 4; ++cs) if (8 * cs + 7 >= e0 && 8 * cs + 7 < e1) \
+      x[cs >> 1][cs & 1] = acc_frag(sc[cs >> 1], cs & 1);                         \
+  }
+      // ---- S(t+1) ∥ epilogue(t)
+      f32x16 sn[2];
+      bf16x8 fa[DS + 2][2];
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((fa[P][0] = row_frag_c<TILE, 0, P, 0>(oS), fa[P][1] = row_frag_c<TILE, 32, P, 0>(oS)), ...);
+      }(std::make_integer_sequence<int, DS>{});
+      __builtin_amdgcn_sched_barrier(0);
+      [&]<int... K>(std::integer_sequence<int, K...>) {
+        (
+            [&] {
+              constexpr int ks = K;
+              if constexpr (ks + DS < KS) {
+                fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
+                fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
+              }
+              if constexpr (ks == 0) {
+                sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], wf[0], f32x16{}, 0, 0, 0);
+                sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], wf[0], f32x16{}, 0, 0, 0);
+              } else {
+                sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][0], wf[ks], sn[0], 0, 0, 0);
+                sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][1], wf[ks], sn[1], 0, 0, 0);
+              }
+              C2_DW_EPI_UNITS(2 * ks, 2 * ks + 2)
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, KS>{});
+      // ---- dWᵀ[k][c] += Σ_r H[r][k] P'[r][c], q = (cb, st, kb): x[cb][st] is used from q = 16cb + 8st on
+      bf16x8 tf[DT + 2];
+#define C2_DW_TF(q1) tr_frag_c<TILE, (((q1) / KB) >> 1) * 32 + 16 * (((q1) / KB) & 1), ((q1) % KB) * 32, 0>(oH)
+      [&]<int... P>(std::integer_sequence<int, P...>) { ((tf[P] = C2_DW_TF(P)), ...); }(std::make_integer_sequence<int, DT>{});
+      __builtin_amdgcn_sched_barrier(0);
+      [&]<int... Q>(std::integer_sequence<int, Q...>) {
+        (
+            [&] {
+              constexpr int q = Q;
+              constexpr int cs = q / KB, kb = q % KB;
+              if constexpr (q + DT < NQ) tf[(q + DT) % (DT + 2)] = C2_DW_TF(q + DT);
+              dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[cs >> 1][cs & 1], dacc[kb], 0, 0, 0);
+              if constexpr (q < 2 * KB) C2_DW_EPI_UNITS(2 * KS + q, 2 * KS + q + 1)
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, NQ>{});
+#undef C2_DW_TF
+#undef C2_DW_EPI_UNITS
+#undef C2_DW_EPI
+      sc[0] = sn[0];
+      sc[1] = sn[1];
+      dma_wait();
+      __syncthreads();
+    }
   }
   db += __shfl_xor(db, 32, 64);
   if (c < n) {
@@ -540,24 +627,25 @@ __global__ void bias2_kernel(const float* __restrict__ bias, int n, int n_pad, f
 }
 
 // per row r < M_pad: rw = valid ? gscale*lam*coef[r >= split] : 0; t32 = target (-1 past M);
-// lse2 padded with 0; dpad = exp(pl - lse)·rw (the pad column of the softmax; its target is ignored)
+// crow = log2(rw) - lse2 (-inf where rw = 0 and past M); dpad = exp(pl - lse)·rw (the pad column of the softmax; its target is ignored)
 __global__ void ce_roww_kernel(const int64_t* __restrict__ tgt, int M, int M_pad, int ignore,
                                const float* __restrict__ coef, int split, const float* __restrict__ gscale,
                                float lam, const float* __restrict__ pl, const float* __restrict__ lse,
-                               float* __restrict__ rw, int* __restrict__ t32, float* __restrict__ lse2,
-                               float* __restrict__ dpad) {
+                               float* __restrict__ rw, int* __restrict__ t32, const float* __restrict__ lse2,
+                               float* __restrict__ crow, float* __restrict__ dpad) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= M_pad) return;
   if (r >= M) {
     rw[r] = 0.f;
     t32[r] = -1;
-    lse2[r] = 0.f;
+    crow[r] = -INFINITY;
     return;
   }
   const long t = tgt[r];
   const float w = t != ignore ? gscale[0] * lam * coef[r >= split ? 1 : 0] : 0.f;
   rw[r] = w;
   t32[r] = (int)t;
+  crow[r] = w > 0.f ? __log2f(w) - lse2[r] : -INFINITY;
   dpad[r] = expf(pl[r] - lse[r]) * w;
 }
 
@@ -633,26 +721,26 @@ C2_API int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2
 
 C2_API int c2dsr_ce_row_weights(const int64_t* tgt, int M, int M_pad, int ignore, const float* coef, int split,
                                 const float* gscale, float lam, const float* padlogit, const float* lse, float* rw,
-                                int* t32, float* lse2, float* dpad, void* stream) {
+                                int* t32, const float* lse2, float* crow, float* dpad, void* stream) {
   if (M_pad == 0) return 0;
   ce_roww_kernel<<<c2::ceil_div(M_pad, 256), 256, 0, (hipStream_t)stream>>>(tgt, M, M_pad, ignore, coef, split,
                                                                              gscale, lam, padlogit, lse, rw, t32,
-                                                                             lse2, dpad);
+                                                                             lse2, crow, dpad);
   C2_CHECK_LAUNCH();
   return 0;
 }
 
 // dHp[s][r] = Σ_{c in split s} P'[r][c] W[c]  (combine with c2dsr_sum_parts)
 C2_API int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
-                             const float* lse2, const int* t32, const float* rw, float* dHp, void* stream) {
+                             const float* crow, float* dHp, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (M == 0) return 0;
   const int per = per_split(n, n_split, TILE);
   dim3 grid(c2::ceil_div(M, 128), n_split);
   if (D == 128)
-    ce_dh_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dHp);
+    ce_dh_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, dHp);
   else if (D == 256)
-    ce_dh_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dHp);
+    ce_dh_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, dHp);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
@@ -661,17 +749,17 @@ C2_API int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2,
 
 // dWp[s][c] = Σ_{r in split s} P'[r][c] H[r];  dbp[s][c] = Σ_r P'[r][c]  (combine with c2dsr_sum_parts)
 C2_API int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
-                             const float* lse2, const int* t32, const float* rw, float* dWp, float* dbp,
+                             const float* crow, const int* t32, const float* rw, float* dWp, float* dbp,
                              void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return 0;
   const int per = per_split(M, n_rsplit, TILE);
   dim3 grid(c2::ceil_div(n, 128), n_rsplit);
   if (D == 128)
-    ce_dw_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dWp,
+    ce_dw_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, t32, rw, dWp,
                                            dbp);
   else if (D == 256)
-    ce_dw_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, lse2, t32, rw, dWp,
+    ce_dw_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, t32, rw, dWp,
                                            dbp);
   else
     return (int)hipErrorInvalidValue;

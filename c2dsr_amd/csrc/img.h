@@ -11,6 +11,8 @@ typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
@@ -233,6 +235,12 @@ typedef __attribute__((address_space(3))) bf16x8 lds_bf16x8;
 // An LDS byte address with a provably clear sign bit: only then does the backend fold a
 // constant into the ds_read offset field instead of materialising one address per read.
 __device__ __forceinline__ unsigned lds_base(int off) { return (unsigned)off & 0x3ffffu; }
+// typed LDS load at a sign-bit-clear byte address + IMM (the constant folds into the offset field)
+template <typename T, int IMM>
+__device__ __forceinline__ T lds_ld(int off) {
+  typedef __attribute__((address_space(3))) T lds_T;
+  return *(const lds_T*)(size_t)(lds_base(off) + IMM);
+}
 template <int IMM>
 __device__ __forceinline__ bf16x8 lds_ld128(int off) {
   return *(const lds_bf16x8*)(size_t)(lds_base(off) + IMM);

@@ -109,7 +109,9 @@ class LossHeadFn(Function):
                 M2 = 2 * BR
                 M_pad = -(-M2 // 64) * 64
                 n_pad = -(-n // 128) * 128 + 64  # + a 64-value tail: tiles near n DMA 64 constants
-                Hb = torch.empty(M2, d, device=dev, dtype=torch.bfloat16)
+                Hb = torch.empty(M_pad, d, device=dev, dtype=torch.bfloat16)  # whole 64-row H tiles (dW sweep)
+                if M_pad > M2:
+                    Hb[M2:].zero_()
                 n64 = -(-n // 64) * 64  # whole 64-row W tiles for the LDS-DMA (zero rows past n)
                 Wb = torch.empty(n64, d, device=dev, dtype=torch.bfloat16)
                 if n64 > n:
@@ -179,17 +181,18 @@ class LossHeadFn(Function):
                 rw = torch.empty(M_pad, **f32)
                 t32 = torch.empty(M_pad, device=dev, dtype=torch.int32)
                 dpad = torch.empty(M2, **f32)
+                crow = torch.empty(M_pad, **f32)
                 lib('c2dsr_ce_row_weights', tcat, M2, M_pad, n, coef, BR, gscale, float(m.lam), padlogit, lse, rw, t32,
-                    lse2, dpad, s)
+                    lse2, crow, dpad, s)
                 ns = split_count(M2, 128)
                 dHp = torch.empty(ns, M2, d, **f32)
-                lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M2, n, d, ns, lse2, t32, rw, dHp, s)
+                lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M2, n, d, ns, crow, dHp, s)
                 lib('c2dsr_ce_dh_combine', dHp, ns, M2, d, t32, rw, W, n, dHcat, s)
                 del dHp
                 nr = split_count(n, 128)
                 dWp = torch.empty(nr, n, d, **f32)
                 dbp = torch.empty(nr, n, **f32)
-                lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M2, n, d, nr, lse2, t32, rw, dWp, dbp, s)
+                lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M2, n, d, nr, crow, t32, rw, dWp, dbp, s)
                 if gW is not None:
                     lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
                 if gb is not None:

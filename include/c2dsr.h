@@ -125,21 +125,22 @@ int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2, int M
                        float* part_m, float* part_s, const float* padlogit, const int64_t* tgt, const float* H,
                        const float* W, const float* bias, float* lse, float* lse2, float* loss_row, void* stream);
 /* per row r < M_pad (multiple of 64): rw = valid ? gscale·lam·coef[r >= split] : 0, t32 = target (-1 pad),
- * lse2 pads = 0, dpad = exp(padlogit - lse)·rw */
+ * crow = log2(rw) - lse2 (-inf where rw = 0 and past M), dpad = exp(padlogit - lse)·rw */
 int c2dsr_ce_row_weights(const int64_t* tgt, int M, int M_pad, int ignore, const float* coef, int split,
                          const float* gscale, float lam, const float* padlogit, const float* lse, float* rw, int* t32,
-                         float* lse2, float* dpad, void* stream);
+                         const float* lse2, float* crow, float* dpad, void* stream);
 /* dHp[s][r] = Σ_{c∈split s} softmax[r][c]·rw_r·W[c]  ([n_split][M][D]; the one-hot part and the split
  * sum are applied by c2dsr_ce_dh_combine).  Wb holds ⌈n/64⌉·64 rows (zero rows past n); bias2 holds
- * n_pad + 64 values (-inf past n). */
+ * n_pad + 64 values (-inf past n); crow from c2dsr_ce_row_weights. */
 int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
-                      const float* lse2, const int* t32, const float* rw, float* dHp, void* stream);
-/* dWp[s][c] = Σ_{r∈split s} P'[r][c]·H[r];  dbp[s][c] = Σ_r P'[r][c]  ([n_rsplit][n][D], [n_rsplit][n]) */
+                      const float* crow, float* dHp, void* stream);
+/* dWp[s][c] = Σ_{r∈split s} P'[r][c]·H[r];  dbp[s][c] = Σ_r P'[r][c]  ([n_rsplit][n][D], [n_rsplit][n]).
+ * Hb holds ⌈M/64⌉·64 rows (zero rows past M); crow / t32 / rw as written by c2dsr_ce_row_weights. */
 /* dH[r] = Σ_s dHp[s][r] - (0 <= t32[r] < n ? rw[r]·W[t32[r]] : 0)  (W fp32 [n][D]; fixed order) */
 int c2dsr_ce_dh_combine(const float* dHp, int ns, int M, int D, const int* t32, const float* rw, const float* W, int n,
                         float* dH, void* stream);
 int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
-                      const float* lse2, const int* t32, const float* rw, float* dWp, float* dbp, void* stream);
+                      const float* crow, const int* t32, const float* rw, float* dWp, float* dbp, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
 int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */

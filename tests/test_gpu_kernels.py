@@ -268,12 +268,13 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     lam = 0.7
     s = stream()
     d = lambda x: x.to(DEV)  # noqa: E731
-    Hb = d(H.to(torch.bfloat16))
+    M_pad = -(-M // 64) * 64
+    Hb = torch.zeros(M_pad, D, dtype=torch.bfloat16, device=DEV)  # whole 64-row H tiles: zero rows past M
+    Hb[:M] = d(H.to(torch.bfloat16))
     n64 = -(-n // 64) * 64  # the fused kernels read whole 64-row W tiles: zero rows past n
     Wb = torch.zeros(n64, D, dtype=torch.bfloat16, device=DEV)
     Wb[:n] = d(W.to(torch.bfloat16))
     ns, nr = 3, 2
-    M_pad = -(-M // 64) * 64
     n_pad = -(-n // 128) * 128 + 64
     bias2 = torch.empty(n_pad, device=DEV)
     lib('c2dsr_ce_bias2', d(b), n, n_pad, bias2, s)
@@ -290,7 +291,8 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     assert rel(rows, rows_r) < 1e-4
     rw, dpad = torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)
     t32 = torch.empty(M_pad, device=DEV, dtype=torch.int32)
-    lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, t32, lse2, dpad, s)
+    crow = torch.empty(M_pad, device=DEV)
+    lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, t32, lse2, crow, dpad, s)
     w_r = torch.where(valid, lam * coef[(torch.arange(M) >= BR).long()].double(), torch.zeros(M, dtype=torch.float64))
     P = torch.softmax(lg, 1)
     oh = torch.zeros_like(P)
@@ -299,13 +301,13 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     assert rel(rw[:M], w_r) < 1e-6 and rel(dpad, dl[:, n]) < 1e-4
     dH = torch.empty(M, D, device=DEV)
     dHp = torch.empty(ns, M, D, device=DEV)
-    lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M, n, D, ns, lse2, t32, rw, dHp, s)
+    lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M, n, D, ns, crow, dHp, s)
     lib('c2dsr_ce_dh_combine', dHp, ns, M, D, t32, rw, d(W), n, dH, s)
     assert rel(dH, dl[:, :n] @ W.double()) < 1e-2
     gW = torch.ones(n, D, device=DEV)
     gb = torch.ones(n, device=DEV)
     dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
-    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M, n, D, nr, lse2, t32, rw, dWp, dbp, s)
+    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M, n, D, nr, crow, t32, rw, dWp, dbp, s)
     lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     assert rel(gW - 1, dl[:, :n].T @ H.double()) < 1e-2
