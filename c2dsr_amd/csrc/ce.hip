@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
   constexpr int IMG = TILE * D * 2;              // bytes per image
   constexpr int NDMA = (TILE / 4) * (D / 128) / 4;  // DMA wave-instructions per wave per tile
   __shared__ __attribute__((aligned(16))) char img[3][IMG];
-  __shared__ __attribute__((aligned(16))) float b2s[3][TILE];
+  __shared__ __attribute__((aligned(16))) float b2s[3][4][TILE];  // [buffer][wave] (each wave its own copy)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x * 128 + w * 32 + (lane & 31);
   const int rc = min(r, M - 1);
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
       const bf16* base = Wb + (long)c0 * D;
 #pragma unroll
       for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
-      dma_vec64(bias2 + c0, b2s[buf], 0);
+      dma4(bias2 + c0 + lane, b2s[buf][w]);
     };
     bf16x8 hf[KS];
 #pragma unroll
@@ -272,7 +272,12 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
     }
     for (int t = 0; t < ntiles; ++t) {
       const int bh = t % 3, bs = (t + 1) % 3;
-      dma(t + 2);  // into the buffer tile t-1 used (every wave passed the barrier after its dH)
+      // tile t+2 → the buffer tile t-1 used (every wave passed the barrier after its dH); its pieces
+      // are issued one per odd S k-step below, so no MFMA gap carries more than one
+      const int cn = min(c_beg + (t + 2) * TILE, c_last);
+      const bf16* nsrc = Wb + (long)cn * D;
+      const unsigned nbuf = ((t + 2) % 3) * IMG;
+      dma4(bias2 + cn + lane, b2s[(t + 2) % 3][w]);
       ImgOffsets oS, oH;
       {
         int ro[8], to[4][2];
@@ -288,7 +293,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
       }
       f32x4 b4[2][4];
       {
-        const int bo = (int)lds_addr(b2s[0]) + 16 * (lane >> 5) + bh * (TILE * 4);
+        const int bo = (int)lds_addr(b2s[bh][w]) + 16 * (lane >> 5);
         [&]<int... J>(std::integer_sequence<int, J...>) {
           ((b4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(bo)), ...);
         }(std::make_integer_sequence<int, 8>{});
@@ -310,6 +315,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
                 fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
                 fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
               }
+              if constexpr (ks % 2 == 1 && ks / 2 < NDMA) dma16_s<ks == 1>(nsrc, dvoff[ks / 2], ddst[ks / 2] + nbuf);
               if constexpr (ks == 0) {
                 sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
                 sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
@@ -410,7 +416,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
   constexpr int NDMA = (TILE / 4) * (D / 128) / 4;
   static_assert(KS >= 8, "the epilogue schedule assumes at least 8 S k-steps");
   __shared__ __attribute__((aligned(16))) char img[3][IMG];
-  __shared__ __attribute__((aligned(16))) float rv[3][3][TILE];  // [buffer][crow, roww, tgt32][row]
+  __shared__ __attribute__((aligned(16))) float rv[3][4][3][TILE];  // [buffer][wave][crow, roww, tgt32][row]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 128 + w * 32 + (lane & 31);
   const int cc = min(c, n - 1);
@@ -427,7 +433,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
     const int r_last = r_beg + (ntiles - 1) * TILE;
     const ImgOffsets o0 = img_offsets(lane);
     const int ib = (int)lds_addr(img[0]);
-    const int rvb = (int)lds_addr(rv[0][0]) + 16 * (lane >> 5);
+    const int rvb = (int)lds_addr(rv[0][w]) + 16 * (lane >> 5);
     unsigned dvoff[NDMA], ddst[NDMA];
 #pragma unroll
     for (int i = 0; i < NDMA; ++i) {
@@ -439,15 +445,18 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
       dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
       ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
     }
+    auto dma_rows = [&](int r0, int buf) {  // each wave its own copy of the tile's row constants
+      dma4(crow + r0 + lane, rv[buf][w][0]);
+      dma4(roww + r0 + lane, rv[buf][w][1]);
+      dma4(tgt32 + r0 + lane, rv[buf][w][2]);
+    };
     auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % 3
       const int r0 = min(r_beg + tt * TILE, r_last);
       const int buf = tt % 3;
       const bf16* base = Hb + (long)r0 * D;
 #pragma unroll
       for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
-      dma_vec64(crow + r0, rv[buf][0], 1);
-      dma_vec64(roww + r0, rv[buf][1], 2);
-      dma_vec64(tgt32 + r0, rv[buf][2], 3);
+      dma_rows(r0, buf);
     };
     bf16x8 wf[KS];
 #pragma unroll
@@ -487,7 +496,10 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
     }
     for (int t = 0; t < ntiles; ++t) {
       const int bh = t % 3, bs = (t + 1) % 3;
-      dma(t + 2);
+      const int rn = min(r_beg + (t + 2) * TILE, r_last);  // tile t+2: pieces in the odd S k-steps
+      const bf16* nsrc = Hb + (long)rn * D;
+      const unsigned nbuf = ((t + 2) % 3) * IMG;
+      dma_rows(rn, (t + 2) % 3);
       ImgOffsets oS, oH;
       {
         int ro[8], to[4][2];
@@ -505,7 +517,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
       f32x4 cr4[2][4], w4[2][4];
       i32x4 t4[2][4];
       {
-        const int rvo = rvb + bh * (3 * TILE * 4);  // row r4 = cb·32 + 8·j4 + 4·(lane >> 5) of vector k
+        const int rvo = rvb + bh * (4 * 3 * TILE * 4);  // row r4 = cb·32 + 8·j4 + 4·(lane >> 5) of vector k
         [&]<int... J>(std::integer_sequence<int, J...>) {
           ((cr4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(rvo),
             w4[J >> 2][J & 3] = lds_ld<f32x4, TILE * 4 + 128 * (J >> 2) + 32 * (J & 3)>(rvo),
@@ -547,6 +559,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
                 fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
                 fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
               }
+              if constexpr (ks % 2 == 1 && ks / 2 < NDMA) dma16_s<ks == 1>(nsrc, dvoff[ks / 2], ddst[ks / 2] + nbuf);
               if constexpr (ks == 0) {
                 sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], wf[0], f32x16{}, 0, 0, 0);
                 sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], wf[0], f32x16{}, 0, 0, 0);

@@ -74,11 +74,11 @@ typedef __attribute__((address_space(3))) char lds_char;
 // barrier that publishes the buffer.  m0 is written here and nowhere else in these kernels.
 __device__ __forceinline__ void dma16(const void* g, char* lds) {
   const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_char*)lds);
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(g) : "memory");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m), "v"(g) : "memory");
 }
 __device__ __forceinline__ void dma4(const void* g, void* lds) {
   const unsigned m = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_char*)lds);
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(g) : "memory");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(g) : "memory");
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // vmcnt(0) the compiler can see (its wait-count state then knows the register operands
@@ -262,10 +262,18 @@ __device__ __forceinline__ bf16x8 tr_frag_c(const ImgOffsets& o) {
   return v;
 }
 
-// LDS-DMA with a scalar global base and a per-lane 32-bit byte offset (saddr form)
+// LDS-DMA with a scalar global base and a per-lane 32-bit byte offset (saddr form).  The M0 write →
+// LDS-DMA pair needs one wait state (s_nop 0).  hipcc may produce sbase with v_readfirstlane (a VALU
+// SGPR write, 5 wait states before a VMEM reads it): the first piece after sbase changes opens
+// with s_nop 4 (FRESH), later pieces of the same base are far enough behind it.
+template <bool FRESH = true>
 __device__ __forceinline__ void dma16_s(const void* sbase, unsigned voff, unsigned lds_dst) {
-  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2 offset:0"
-               ::"s"(lds_dst), "v"(voff), "s"(sbase) : "memory");
+  if constexpr (FRESH)
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:0"
+                 ::"s"(lds_dst), "v"(voff), "s"(sbase) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 offset:0"
+                 ::"s"(lds_dst), "v"(voff), "s"(sbase) : "memory");
 }
 
 // 64 consecutive 4-byte values (a padded per-row / per-column constant array) → LDS, by wave `wv`
