@@ -188,8 +188,9 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
   constexpr int EPK = 16 / KS;                   // epilogue elements per S k-step (per column block)
   constexpr int IMG = TILE * D * 2;              // bytes per image
   constexpr int NDMA = (TILE / 4) * (D / 128) / 4;  // DMA wave-instructions per wave per tile
-  __shared__ __attribute__((aligned(16))) char img[3][IMG];
-  __shared__ __attribute__((aligned(16))) float b2s[3][4][TILE];  // [buffer][wave] (each wave its own copy)
+  constexpr int NB = 4;                              // W images: S(t+1), dH(t), tile t+2 landed, t+3 landing
+  __shared__ __attribute__((aligned(16))) char img[NB][IMG];
+  __shared__ __attribute__((aligned(16))) float b2s[NB][4][TILE];  // [buffer][wave] (each wave its own copy)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x * 128 + w * 32 + (lane & 31);
   const int rc = min(r, M - 1);
@@ -217,9 +218,9 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
       dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
       ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
     }
-    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % 3
+    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % NB
       const int c0 = min(c_beg + tt * TILE, c_last);
-      const int buf = tt % 3;
+      const int buf = tt % NB;
       const bf16* base = Wb + (long)c0 * D;
 #pragma unroll
       for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
@@ -231,6 +232,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
     float cr = r < M ? crow[rc] : -INFINITY;
     dma(0);
     dma(1);
+    dma(2);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
     pin(cr);
@@ -271,13 +273,14 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
       }
     }
     for (int t = 0; t < ntiles; ++t) {
-      const int bh = t % 3, bs = (t + 1) % 3;
-      // tile t+2 → the buffer tile t-1 used (every wave passed the barrier after its dH); its pieces
-      // are issued one per odd S k-step below, so no MFMA gap carries more than one
-      const int cn = min(c_beg + (t + 2) * TILE, c_last);
+      const int bh = t % NB, bs = (t + 1) % NB;
+      // tile t+3 → the buffer tile t-1 used (every wave passed the barrier after its dH); its pieces
+      // are issued in the dH phase (MFMA-bound, issue slots to spare), one per four dH steps, and
+      // land during the next step
+      const int cn = min(c_beg + (t + 3) * TILE, c_last);
       const bf16* nsrc = Wb + (long)cn * D;
-      const unsigned nbuf = ((t + 2) % 3) * IMG;
-      dma4(bias2 + cn + lane, b2s[(t + 2) % 3][w]);
+      const unsigned nbuf = ((t + 3) % NB) * IMG;
+      dma4(bias2 + cn + lane, b2s[(t + 3) % NB][w]);
       ImgOffsets oS, oH;
       {
         int ro[8], to[4][2];
@@ -315,7 +318,6 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
                 fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
                 fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
               }
-              if constexpr (ks % 2 == 1 && ks / 2 < NDMA) dma16_s<ks == 1>(nsrc, dvoff[ks / 2], ddst[ks / 2] + nbuf);
               if constexpr (ks == 0) {
                 sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
                 sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
@@ -356,6 +358,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
               }
               dacc[q >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[(q >> 1) & 1][q & 1],
                                                                    dacc[q >> 2], 0, 0, 0);
+              if constexpr (q % 4 == 1 && q / 4 < NDMA) dma16_s<q == 1>(nsrc, dvoff[q / 4], ddst[q / 4] + nbuf);
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
       // S(t+1) becomes the next step's S(t): its MFMAs have long retired (the dH chain ran since)
       sc[0] = sn[0];
       sc[1] = sn[1];
-      dma_wait();
+      dma_wait_keep<NDMA + 1>();  // tile t+2 has landed; tile t+3 may still be in flight
       __syncthreads();
     }
   }

@@ -81,6 +81,9 @@ __device__ __forceinline__ void dma4(const void* g, void* lds) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(m), "v"(g) : "memory");
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// wait until at most N vector-memory operations (the newest N; vmcnt retires in order) are outstanding
+template <int N>
+__device__ __forceinline__ void dma_wait_keep() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 // vmcnt(0) the compiler can see (its wait-count state then knows the register operands
 // loaded before the tile loop have landed, and emits no waits for them inside the loop)
 // pin a register operand here: its load must be issued (and have landed) before this point
