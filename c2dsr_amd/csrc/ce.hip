@@ -417,9 +417,10 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
   constexpr int DT = 3;
   constexpr int IMG = TILE * D * 2;
   constexpr int NDMA = (TILE / 4) * (D / 128) / 4;
+  constexpr int NB = 4;  // H images: S(t+1), dW(t), tile t+2 landed, t+3 landing
   static_assert(KS >= 8, "the epilogue schedule assumes at least 8 S k-steps");
-  __shared__ __attribute__((aligned(16))) char img[3][IMG];
-  __shared__ __attribute__((aligned(16))) float rv[3][4][3][TILE];  // [buffer][wave][crow, roww, tgt32][row]
+  __shared__ __attribute__((aligned(16))) char img[NB][IMG];
+  __shared__ __attribute__((aligned(16))) float rv[NB][4][3][TILE];  // [buffer][wave][crow, roww, tgt32][row]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 128 + w * 32 + (lane & 31);
   const int cc = min(c, n - 1);
@@ -453,9 +454,9 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
       dma4(roww + r0 + lane, rv[buf][w][1]);
       dma4(tgt32 + r0 + lane, rv[buf][w][2]);
     };
-    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % 3
+    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % NB
       const int r0 = min(r_beg + tt * TILE, r_last);
-      const int buf = tt % 3;
+      const int buf = tt % NB;
       const bf16* base = Hb + (long)r0 * D;
 #pragma unroll
       for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
@@ -467,6 +468,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
     float b2 = bias2[c];  // -inf past n: those columns contribute 0
     dma(0);
     dma(1);
+    dma(2);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) pin(wf[ks]);
     pin(b2);
@@ -498,11 +500,11 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
       }
     }
     for (int t = 0; t < ntiles; ++t) {
-      const int bh = t % 3, bs = (t + 1) % 3;
-      const int rn = min(r_beg + (t + 2) * TILE, r_last);  // tile t+2: pieces in the odd S k-steps
+      const int bh = t % NB, bs = (t + 1) % NB;
+      const int rn = min(r_beg + (t + 3) * TILE, r_last);  // tile t+3: pieces in the dWᵀ phase
       const bf16* nsrc = Hb + (long)rn * D;
-      const unsigned nbuf = ((t + 2) % 3) * IMG;
-      dma_rows(rn, (t + 2) % 3);
+      const unsigned nbuf = ((t + 3) % NB) * IMG;
+      dma_rows(rn, (t + 3) % NB);
       ImgOffsets oS, oH;
       {
         int ro[8], to[4][2];
@@ -520,7 +522,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
       f32x4 cr4[2][4], w4[2][4];
       i32x4 t4[2][4];
       {
-        const int rvo = rvb + bh * (4 * 3 * TILE * 4);  // row r4 = cb·32 + 8·j4 + 4·(lane >> 5) of vector k
+        const int rvo = rvb + bh * (4 * 3 * TILE * 4);  // [NB][4][3][TILE]  // row r4 = cb·32 + 8·j4 + 4·(lane >> 5) of vector k
         [&]<int... J>(std::integer_sequence<int, J...>) {
           ((cr4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(rvo),
             w4[J >> 2][J & 3] = lds_ld<f32x4, TILE * 4 + 128 * (J >> 2) + 32 * (J & 3)>(rvo),
@@ -562,7 +564,6 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
                 fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
                 fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
               }
-              if constexpr (ks % 2 == 1 && ks / 2 < NDMA) dma16_s<ks == 1>(nsrc, dvoff[ks / 2], ddst[ks / 2] + nbuf);
               if constexpr (ks == 0) {
                 sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], wf[0], f32x16{}, 0, 0, 0);
                 sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], wf[0], f32x16{}, 0, 0, 0);
@@ -588,6 +589,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
               if constexpr (q + DT < NQ) tf[(q + DT) % (DT + 2)] = C2_DW_TF(q + DT);
               dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[cs >> 1][cs & 1], dacc[kb], 0, 0, 0);
               if constexpr (q < 2 * KB) C2_DW_EPI_UNITS(2 * KS + q, 2 * KS + q + 1)
+              if constexpr (q % 4 == 3 && q / 4 < NDMA) dma16_s<q == 3>(nsrc, dvoff[q / 4], ddst[q / 4] + nbuf);
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
 #undef C2_DW_EPI
       sc[0] = sn[0];
       sc[1] = sn[1];
-      dma_wait();
+      dma_wait_keep<NDMA + 3>();  // tile t+2 has landed; tile t+3 (pieces + 3 row vectors) may be in flight
       __syncthreads();
     }
   }
