@@ -27,89 +27,133 @@ namespace {
 using namespace c2img;
 
 // ---------------------------------------------------------------- forward: partial LSE
-// grid (ceil(M/256), n_split); 4 waves x 64 rows.  part_m/part_s [n_split][M]: log2-domain
-// running max and sum of 2^(s·log2e) over the split's columns.  bias2 = bias·log2e padded
-// with -inf to a multiple of TILE.
+// grid (ceil(M/256), n_split); 8 waves x 32 rows, two waves per SIMD (one wave's exp/max
+// epilogue runs in the other's MFMA shadow).  part_m/part_s [n_split][M]: log2-domain running
+// max and sum of 2^(s·log2e) over the split's columns.  bias2 = bias·log2e, -inf past n.
+// W tiles stream through three LDS images: tile t+2's pieces (four per wave, saddr LDS-DMA)
+// are issued between the k-steps of tile t and land during tile t+1.  Wb holds ⌈n/64⌉·64
+// rows (zero padding past n).
 template <int D>
 __global__ __launch_bounds__(512, 1) void ce_lse_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
                                                         const float* __restrict__ bias2, int M, int n,
                                                         int cols_per_split, float* __restrict__ part_m,
                                                         float* __restrict__ part_s) {
-  // 8 waves x 32 rows: two waves per SIMD, so one wave's exp/max epilogue runs in the other's
-  // MFMA shadow (a single wave per SIMD serialised them)
   constexpr int KS = D / 16;
-  __shared__ __attribute__((aligned(16))) char img[2][TILE * D * 2];
-  __shared__ __attribute__((aligned(16))) float b2s[2][TILE];
+  constexpr int NW = 8;
+  constexpr int NB = 3;
+  constexpr int DS = 3;
+  constexpr int IMG = TILE * D * 2;
+  constexpr int NDMA = (TILE / 4) * (D / 128) / NW;  // pieces per wave per tile
+  static_assert(NDMA >= 1 && (KS / NDMA) >= 1, "tile / wave split");
+  __shared__ __attribute__((aligned(16))) char img[NB][IMG];
+  __shared__ __attribute__((aligned(16))) float b2s[NB][NW][TILE];  // [buffer][wave]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x * 256 + w * 32 + (lane & 31);
   const int c_beg = blockIdx.y * cols_per_split;
   const int c_end = min(n, c_beg + cols_per_split);
   const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
-  if (ntiles > 0) {
-    dma_tile<D, 8>(Wb, n, c_beg, img[0]);
-    dma_vec64(bias2 + c_beg, b2s[0], 0);
-  }
-  bf16x8 hf[KS];
-  const int rc = min(M - 1, r);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
   float mrun = -INFINITY, srun = 0.f;
-  vm_drain();
-  dma_wait();
-  __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const char* cimg = img[t & 1];
-    const float* cb2s = b2s[t & 1];
-    const int c0 = c_beg + t * TILE;
-    if (t + 1 < ntiles) {
-      dma_tile<D, 8>(Wb, n, c0 + TILE, img[(t & 1) ^ 1]);
-      dma_vec64(bias2 + c0 + TILE, b2s[(t & 1) ^ 1], 1);
+  if (ntiles > 0) {
+    const int c_last = c_beg + (ntiles - 1) * TILE;
+    const ImgOffsets o0 = img_offsets(lane);
+    const int ib = (int)lds_addr(img[0]);
+    const int bb = (int)lds_addr(b2s[0][w]) + 16 * (lane >> 5);
+    unsigned dvoff[NDMA], ddst[NDMA];
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int q = w + NW * i;
+      constexpr int GROUPS = TILE / 4;
+      const int half = q / GROUPS, rg = q % GROUPS;
+      const int row = rg * 4 + (lane >> 4);
+      const int lch = (lane & 15) ^ swz_f(row);
+      dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
+      ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
     }
-    f32x16 acc[2];
+    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % NB
+      const int c0 = min(c_beg + tt * TILE, c_last);
+      const int buf = tt % NB;
+      const bf16* base = Wb + (long)c0 * D;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+      for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
+      dma4(bias2 + c0 + lane, b2s[buf][w]);
+    };
+    bf16x8 hf[KS];
+    const int rc = min(M - 1, r);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[cb][i] = 0.f;
-    bf16x8 fa[2], fb[2];
-    fa[0] = row_frag(cimg, 0, 0, lane);
-    fa[1] = row_frag(cimg, 32, 0, lane);
+    for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
+    dma(0);
+    dma(1);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 1 < KS) {
-        fb[0] = row_frag(cimg, 0, (ks + 1) * 16, lane);
-        fb[1] = row_frag(cimg, 32, (ks + 1) * 16, lane);
-      }
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], hf[ks], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], hf[ks], acc[1], 0, 0, 0);
-      fa[0] = fb[0];
-      fa[1] = fb[1];
-    }
-    float4 b4[2][4];  // bias·log2e of this lane's 32 columns (4 runs of 4)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int j4 = 0; j4 < 4; ++j4) b4[cb][j4] = *(const float4*)&cb2s[cb * 32 + 8 * j4 + 4 * (lane >> 5)];
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float v = fmaf(acc[cb][i], LOG2E, ((const float*)&b4[cb][i >> 2])[i & 3]);
-        acc[cb][i] = v;
-        tmax = fmaxf(tmax, v);
-      }
-    const float mnew = fmaxf(mrun, tmax);
-    float sm = (mrun == -INFINITY) ? 0.f : srun * ex2(mrun - mnew);
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sm += ex2(acc[cb][i] - mnew);
-    mrun = mnew;
-    srun = sm;
+    for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
+    vm_drain();
     dma_wait();
     __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+      const int bc = t % NB;
+      const int cn = min(c_beg + (t + 2) * TILE, c_last);
+      const bf16* nsrc = Wb + (long)cn * D;
+      const unsigned nbuf = ((t + 2) % NB) * IMG;
+      dma4(bias2 + cn + lane, b2s[(t + 2) % NB][w]);
+      ImgOffsets oS;
+      {
+        const int add = ib + bc * IMG;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) oS.roff[k] = o0.roff[k] + add;
+      }
+      f32x16 acc[2];
+      bf16x8 fa[DS + 2][2];
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((fa[P][0] = row_frag_c<TILE, 0, P, 0>(oS), fa[P][1] = row_frag_c<TILE, 32, P, 0>(oS)), ...);
+      }(std::make_integer_sequence<int, DS>{});
+      __builtin_amdgcn_sched_barrier(0);
+      [&]<int... K>(std::integer_sequence<int, K...>) {
+        (
+            [&] {
+              constexpr int ks = K;
+              if constexpr (ks + DS < KS) {
+                fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
+                fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
+              }
+              if constexpr (ks % (KS / NDMA) == 1 % (KS / NDMA) && ks / (KS / NDMA) < NDMA)
+                dma16_s<ks / (KS / NDMA) == 0>(nsrc, dvoff[ks / (KS / NDMA)], ddst[ks / (KS / NDMA)] + nbuf);
+              if constexpr (ks == 0) {
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
+              } else {
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][0], hf[ks], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][1], hf[ks], acc[1], 0, 0, 0);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, KS>{});
+      f32x4 b4[2][4];  // bias·log2e of this lane's 32 columns (4 runs of 4)
+      {
+        const int bo = bb + bc * (NW * TILE * 4);
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+          ((b4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(bo)), ...);
+        }(std::make_integer_sequence<int, 8>{});
+      }
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float v = fmaf(acc[cb][i], LOG2E, b4[cb][i >> 2][i & 3]);
+          acc[cb][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      const float mnew = fmaxf(mrun, tmax);
+      float sm = (mrun == -INFINITY) ? 0.f : srun * ex2(mrun - mnew);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sm += ex2(acc[cb][i] - mnew);
+      mrun = mnew;
+      srun = sm;
+      dma_wait_keep<NDMA + 1>();  // tile t+1 has landed; tile t+2 may still be in flight
+      __syncthreads();
+    }
   }
   const float m2 = __shfl_xor(mrun, 32, 64), s2 = __shfl_xor(srun, 32, 64);
   const float mm = fmaxf(mrun, m2);
@@ -398,17 +442,15 @@ __global__ void ce_dh_combine_kernel(const float* __restrict__ dHp, int ns, int 
 // 64 at a time over three H images — the dH kernel with the roles of H and W exchanged:
 //   step t:  [ S(t+1) = H_{t+1}·W_cᵀ on the matrix cores  ∥  epilogue of S(t), first 24 of 32 ]
 //            [ dWᵀ += H_tᵀ·P'(t)                          ∥  epilogue of S(t), last 8        ]
-// P'[r][c] = 2^(s·log2e + cr_r + b2_c) - [t_r = c]·w_r with cr = log2(w_r) - lse2_r (c2dsr_ce_row_weights);
-// db[c] = Σ_r P'[r][c].  The dWᵀ MFMAs run column-block-major (x[0][0] first), so the last
+// P'[r][c] = 2^(s·log2e + cr_r + b2_c) with cr = log2(w_r) - lse2_r (c2dsr_ce_row_weights), db[c] = Σ_r P'[r][c];
+// the one-hot part of (softmax - onehot)·w is applied afterwards by c2dsr_ce_onehot_dw.  The dWᵀ MFMAs run column-block-major (x[0][0] first), so the last
 // epilogue slice overlaps the first 24 of them.
-// Hb holds ⌈M/64⌉·64 rows (zero padding past M); crow / roww / tgt32 are padded likewise
-// (-inf / 0 / -1).  dWp [n_rsplit][n][D], dbp [n_rsplit][n] fp32 partials.
+// Hb holds ⌈M/64⌉·64 rows (zero padding past M); crow is padded likewise with -inf.  dWp [n_rsplit][n][D], dbp [n_rsplit][n] fp32 partials.
 template <int D>
 __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
                                                        const float* __restrict__ bias2, int M, int n,
                                                        int rows_per_split, const float* __restrict__ crow,
-                                                       const int* __restrict__ tgt32,
-                                                       const float* __restrict__ roww, float* __restrict__ dWp,
+                                                       float* __restrict__ dWp,
                                                        float* __restrict__ dbp) {
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
@@ -420,7 +462,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
   constexpr int NB = 4;  // H images: S(t+1), dW(t), tile t+2 landed, t+3 landing
   static_assert(KS >= 8, "the epilogue schedule assumes at least 8 S k-steps");
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
-  __shared__ __attribute__((aligned(16))) float rv[NB][4][3][TILE];  // [buffer][wave][crow, roww, tgt32][row]
+  __shared__ __attribute__((aligned(16))) float rv[NB][4][TILE];  // [buffer][wave][row] crow
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 128 + w * 32 + (lane & 31);
   const int cc = min(c, n - 1);
@@ -449,11 +491,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
       dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
       ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
     }
-    auto dma_rows = [&](int r0, int buf) {  // each wave its own copy of the tile's row constants
-      dma4(crow + r0 + lane, rv[buf][w][0]);
-      dma4(roww + r0 + lane, rv[buf][w][1]);
-      dma4(tgt32 + r0 + lane, rv[buf][w][2]);
-    };
+    auto dma_rows = [&](int r0, int buf) { dma4(crow + r0 + lane, rv[buf][w]); };  // each wave its own copy
     auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % NB
       const int r0 = min(r_beg + tt * TILE, r_last);
       const int buf = tt % NB;
@@ -519,24 +557,19 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
         }
       }
       // per-row constants of this lane's 32 rows: element i of column block cb is row cb·32 + creg(i)
-      f32x4 cr4[2][4], w4[2][4];
-      i32x4 t4[2][4];
+      f32x4 cr4[2][4];
       {
-        const int rvo = rvb + bh * (4 * 3 * TILE * 4);  // [NB][4][3][TILE]  // row r4 = cb·32 + 8·j4 + 4·(lane >> 5) of vector k
+        const int rvo = rvb + bh * (4 * TILE * 4);  // [NB][4][TILE]; row r4 = cb·32 + 8·j4 + 4·(lane >> 5)
         [&]<int... J>(std::integer_sequence<int, J...>) {
-          ((cr4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(rvo),
-            w4[J >> 2][J & 3] = lds_ld<f32x4, TILE * 4 + 128 * (J >> 2) + 32 * (J & 3)>(rvo),
-            t4[J >> 2][J & 3] = lds_ld<i32x4, 2 * TILE * 4 + 128 * (J >> 2) + 32 * (J & 3)>(rvo)),
-           ...);
+          ((cr4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(rvo)), ...);
         }(std::make_integer_sequence<int, 8>{});
       }
       bf16x8 x[2][2];
 #define C2_DW_EPI(cb, i)                                                                                    \
   {                                                                                                         \
     const float ev = ex2(fmaf(sc[cb][i], LOG2E, ((const float*)&cr4[cb][(i) >> 2])[(i) & 3]) + b2);         \
-    const float v = ev - (((const int*)&t4[cb][(i) >> 2])[(i) & 3] == c ? ((const float*)&w4[cb][(i) >> 2])[(i) & 3] : 0.f); \
-    sc[cb][i] = v;                                                                                          \
-    db += v;                                                                                                \
+    sc[cb][i] = ev;                                                                                         \
+    db += ev;                                                                                               \
   }
 // the 32 epilogue elements in the order the dWᵀ MFMAs need them (e → block e/16, element e%16) are
 // spread over U = 2·KS + 2·KB issue units: two per S k-step (2 MFMAs), one per dWᵀ step q < 2·KB;
@@ -599,7 +632,7 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
 #undef C2_DW_EPI
       sc[0] = sn[0];
       sc[1] = sn[1];
-      dma_wait_keep<NDMA + 3>();  // tile t+2 has landed; tile t+3 (pieces + 3 row vectors) may be in flight
+      dma_wait_keep<NDMA + 1>();  // tile t+2 has landed; tile t+3 (pieces + row vector) may be in flight
       __syncthreads();
     }
   }
@@ -765,19 +798,19 @@ C2_API int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2,
   return 0;
 }
 
-// dWp[s][c] = Σ_{r in split s} P'[r][c] H[r];  dbp[s][c] = Σ_r P'[r][c]  (combine with c2dsr_sum_parts)
+// dWp[s][c] = Σ_{r in split s} P'[r][c] H[r];  dbp[s][c] = Σ_r P'[r][c]  (softmax part; combine with
+// c2dsr_sum_parts, then c2dsr_ce_onehot_dw)
 C2_API int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
-                             const float* crow, const int* t32, const float* rw, float* dWp, float* dbp,
-                             void* stream) {
+                             const float* crow, float* dWp, float* dbp, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return 0;
   const int per = per_split(M, n_rsplit, TILE);
   dim3 grid(c2::ceil_div(n, 128), n_rsplit);
   if (D == 128)
-    ce_dw_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, t32, rw, dWp,
+    ce_dw_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, dWp,
                                            dbp);
   else if (D == 256)
-    ce_dw_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, t32, rw, dWp,
+    ce_dw_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, crow, dWp,
                                            dbp);
   else
     return (int)hipErrorInvalidValue;

@@ -158,13 +158,15 @@ struct RowSrc {
   c2::Drop drop;
   int64_t idx_base;
   float scale;
+  const float* rs;  // optional per-row multiplier
   __device__ __forceinline__ float4 load(uint32_t r, int c) const {
+    if (!gX) return make_float4(c == 0 ? (rs ? scale * rs[r] : scale) : 0.f, 0.f, 0.f, 0.f);  // the row (1, 0, …)
     float4 v = *(const float4*)(gX + (long)r * d + c);
     if (drop.active()) {
       const uint64_t b = (uint64_t)(idx_base + r) * d + c;
       v = v * make_float4(drop.mul(b), drop.mul(b + 1), drop.mul(b + 2), drop.mul(b + 3));
     }
-    return scale * v;
+    return (rs ? scale * rs[r] : scale) * v;
   }
 };
 
@@ -307,6 +309,12 @@ __global__ void drop_scale_kernel(const float* __restrict__ gX, long n4, int d, 
   ((float4*)out)[i] = v;
 }
 
+// out[c] += T[c][0] for c < n  (T [n][4], the d = 4 segment sums of the (w_r, 0, 0, 0) rows)
+__global__ void col0_add_kernel(const float* __restrict__ T, int n, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n) out[c] += T[4 * (long)c];
+}
+
 int lpr_for(int d) { return d / 4 >= 64 ? 64 : (d / 4 >= 32 ? 32 : (d / 4 >= 16 ? 16 : (d / 4 >= 8 ? 8 : 4))); }
 
 struct SortWs {
@@ -431,18 +439,52 @@ C2_API int c2dsr_embed_bwd(const int64_t* seq, const int64_t* pos, int n_rows, i
   if (G) {
     int e = radix_sort(seq, n_rows, n_items, w, s);
     if (e) return e;
-    RowSrc src{gX, d, dr, idx_base, scale};
+    RowSrc src{gX, d, dr, idx_base, scale, nullptr};
     seg_dispatch(w, n_rows, src, G, -1, s);
   }
   if (gP) {
     int e = radix_sort(pos, n_rows, n_pos, w, s);
     if (e) return e;
-    RowSrc src{gX, d, dr, idx_base, 1.0f};
+    RowSrc src{gX, d, dr, idx_base, 1.0f, nullptr};
     seg_dispatch(w, n_rows, src, gP, -1, s);
   }
   if (gXin) {
     long n4 = (long)n_rows * d / 4;
     drop_scale_kernel<<<c2::ceil_div(n4, 256), 256, 0, s>>>(gX, n4, d, dr, idx_base, gXin);
+  }
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+C2_API size_t c2dsr_ce_onehot_workspace(int M, int n, int D) {
+  return ws_layout(M, D, nullptr, nullptr) + (((size_t)n * 16 + 255) & ~size_t(255));
+}
+
+// The one-hot part of the classifier-head gradient (trainer.py:131-154 via F.cross_entropy):
+//   gW[t_r] -= rw_r·H[r],  gb[t_r] -= rw_r   for rows with 0 <= t_r < n (t_r = n is ignore_index)
+// Rows are radix-sorted by target and each target's run is reduced in row order (deterministic);
+// the bias part runs the same segment reduction over the rows (rw_r, 0, 0, 0).
+C2_API int c2dsr_ce_onehot_dw(const int64_t* tgt, int M, int n, const float* H, int D, const float* rw, float* gW,
+                              float* gb, void* workspace, size_t ws_bytes, void* stream) {
+  if (D % 4) return (int)hipErrorInvalidValue;
+  if (M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  SortWs w;
+  const size_t sort_bytes = ws_layout(M, D, &w, (char*)workspace);
+  if (ws_bytes < c2dsr_ce_onehot_workspace(M, n, D)) return (int)hipErrorInvalidValue;
+  int e = radix_sort(tgt, M, n + 1, w, s);
+  if (e) return e;
+  const c2::Drop nodrop = c2::make_drop(0, 0, 0.f);
+  if (gW) {
+    RowSrc src{H, D, nodrop, 0, -1.f, rw};
+    seg_dispatch(w, M, src, gW, n, s);
+  }
+  if (gb) {
+    float* T = (float*)((char*)workspace + sort_bytes);
+    hipMemsetAsync(T, 0, (size_t)n * 16, s);
+    RowSrc src{nullptr, 4, nodrop, 0, -1.f, rw};
+    seg_dispatch(w, M, src, T, n, s);
+    col0_add_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(T, n, gb);
   }
   C2_CHECK_LAUNCH();
   return 0;

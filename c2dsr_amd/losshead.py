@@ -192,12 +192,16 @@ class LossHeadFn(Function):
                 nr = split_count(n, 128)
                 dWp = torch.empty(nr, n, d, **f32)
                 dbp = torch.empty(nr, n, **f32)
-                lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M2, n, d, nr, crow, t32, rw, dWp, dbp, s)
+                lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M2, n, d, nr, crow, dWp, dbp, s)
                 if gW is not None:
                     lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
                 if gb is not None:
                     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
                 del dWp, dbp
+                if gW is not None or gb is not None:
+                    wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M2, n, d))
+                    ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+                    lib('c2dsr_ce_onehot_dw', tcat, M2, n, Hcat, d, rw, gW, gb, ws, wsb, s)
                 pad_col, pad_ld = dpad, 1
             else:
                 ld = n + 1

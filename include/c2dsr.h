@@ -134,13 +134,20 @@ int c2dsr_ce_row_weights(const int64_t* tgt, int M, int M_pad, int ignore, const
  * n_pad + 64 values (-inf past n); crow from c2dsr_ce_row_weights. */
 int c2dsr_ce_fused_dh(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
                       const float* crow, float* dHp, void* stream);
-/* dWp[s][c] = Σ_{r∈split s} P'[r][c]·H[r];  dbp[s][c] = Σ_r P'[r][c]  ([n_rsplit][n][D], [n_rsplit][n]).
- * Hb holds ⌈M/64⌉·64 rows (zero rows past M); crow / t32 / rw as written by c2dsr_ce_row_weights. */
+/* dWp[s][c] = Σ_{r∈split s} E[r][c]·H[r];  dbp[s][c] = Σ_r E[r][c]  ([n_rsplit][n][D], [n_rsplit][n]) with
+ * E = softmax·rw, the softmax part of P' (the one-hot part: c2dsr_ce_onehot_dw).  Hb holds ⌈M/64⌉·64 rows
+ * (zero rows past M); crow as written by c2dsr_ce_row_weights. */
 /* dH[r] = Σ_s dHp[s][r] - (0 <= t32[r] < n ? rw[r]·W[t32[r]] : 0)  (W fp32 [n][D]; fixed order) */
 int c2dsr_ce_dh_combine(const float* dHp, int ns, int M, int D, const int* t32, const float* rw, const float* W, int n,
                         float* dH, void* stream);
 int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
-                      const float* crow, const int* t32, const float* rw, float* dWp, float* dbp, void* stream);
+                      const float* crow, float* dWp, float* dbp, void* stream);
+/* one-hot part of the head's weight/bias gradient: gW[t_r] -= rw_r·H[r], gb[t_r] -= rw_r for 0 <= t_r < n
+ * (t_r = n is the ignored pad target); rows radix-sorted by target, each run summed in row order
+ * (deterministic).  H fp32 [M][D]; gW / gb may be null. */
+size_t c2dsr_ce_onehot_workspace(int M, int n, int D);
+int c2dsr_ce_onehot_dw(const int64_t* tgt, int M, int n, const float* H, int D, const float* rw, float* gW, float* gb,
+                       void* workspace, size_t ws_bytes, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
 int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */

@@ -307,9 +307,12 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     gW = torch.ones(n, D, device=DEV)
     gb = torch.ones(n, device=DEV)
     dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
-    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M, n, D, nr, crow, t32, rw, dWp, dbp, s)
+    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M, n, D, nr, crow, dWp, dbp, s)
     lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
+    wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M, n, D))
+    ws = torch.empty(wsb, device=DEV, dtype=torch.uint8)
+    lib('c2dsr_ce_onehot_dw', d(t), M, n, d(H), D, rw, gW, gb, ws, wsb, s)
     assert rel(gW - 1, dl[:, :n].T @ H.double()) < 1e-2
     assert rel(gb - 1, dl[:, :n].sum(0)) < 1e-2
 
