@@ -113,6 +113,20 @@ class KernelTimer:
         return dict(tflops=fl_all / (ms_all * 1e-3) / 1e12, ms=ms_all, per_kernel=per)
 
 
+def k5_traffic(precision):
+    """HBM bytes per K5 launch triple (lse + dH + dW kernels, both heads averaged) from the separate
+    rocprofv3 FETCH_SIZE (x2, the gfx950 correction) / WRITE_SIZE passes of tools/round_profile.sh,
+    summarised by tools/pmc_traffic.py into profiles/k5_traffic.json.  PMC counters cannot be read
+    from inside this process, so the committed measurement of the same code is reported (null if
+    absent or for another precision)."""
+    path = os.path.join(ROOT, 'profiles', 'k5_traffic.json')
+    if precision != 'bf16' or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    return t.get('bytes_per_launch_triple'), t.get('source')
+
+
 def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
     """The oracle (CPU fp32 restatement, oracle/c2dsr_oracle.py) on a bounded sample of the same
     workload: same item tables, d, L; a small batch for a few steps."""
@@ -230,8 +244,9 @@ def main():
         peak = PEAK_BF16_TFLOPS if opt.precision == 'bf16' else PEAK_FP32_TFLOPS
         roof = None
         if ks is not None:
+            traffic, tsrc = k5_traffic(opt.precision)
             roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
-                        frac=round(ks['tflops'] / peak, 4), traffic=None,
+                        frac=round(ks['tflops'] / peak, 4), traffic=traffic, traffic_source=tsrc,
                         kernel=('K5 fused classifier head + CE: ce_lse_kernel + ce_dh_kernel + ce_dw_kernel '
                                 '(bf16 MFMA); credited 2·M·n·d per launch each'
                                 if opt.precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),

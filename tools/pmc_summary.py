@@ -45,7 +45,10 @@ for t, k in rows[:top]:
     wc = avg(s.get('SQ_WAVE_CYCLES', [])) or 1.0
     bc = avg(s.get('SQ_BUSY_CYCLES', [])) or 1.0
     mf = avg(s.get('SQ_VALU_MFMA_BUSY_CYCLES', []))
+    # MFMA busy fraction over the 1024 SIMDs: cycles from GRBM_GUI_ACTIVE (summed over the 8 XCDs)
+    # when collected, else the launch duration at 2.1 GHz
+    cyc = avg(s.get('GRBM_GUI_ACTIVE', [])) / 8 or us * 2.1e3
     print(f'{k:48} {n:4d} {us:9.1f} {f:8.1f} {w:8.1f} {(f + w) * 1e3 / us:7.0f} '
-          f'{100 * mf / (bc * 4 * 256 / 4) if bc else 0:6.1f} {100 * avg(s.get("SQ_WAIT_ANY", [])) / wc:6.1f} '
+          f'{100 * mf / (1024 * cyc):6.1f} {100 * avg(s.get("SQ_WAIT_ANY", [])) / wc:6.1f} '
           f'{100 * avg(s.get("SQ_WAIT_INST_ANY", [])) / wc:6.1f} {100 * avg(s.get("SQ_WAIT_INST_LDS", [])) / wc:5.1f} '
           f'{avg(s.get("SQ_INSTS_VALU", [])):8.0f}')
