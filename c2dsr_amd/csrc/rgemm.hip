@@ -215,7 +215,8 @@ __device__ __forceinline__ bf16x8 tr32(const char* img, int rr0, int kb0, int la
 
 __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __restrict__ dY, long ldy,
                                                  const float* __restrict__ X, long ldx, float* __restrict__ part,
-                                                 int NTL, int rows_per_split) {
+                                                 float* __restrict__ part_b, int NTL, int rows_per_split) {
+  __shared__ __attribute__((aligned(16))) float4 red_b[8][32];
   __shared__ __attribute__((aligned(16))) char yimg[2][32 * 128 * 2];
   __shared__ __attribute__((aligned(16))) char ximg[2][32 * 256 * 2];
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -254,14 +255,23 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __re
     b_[0] = (bf16)(v4).x; b_[1] = (bf16)(v4).y; b_[2] = (bf16)(v4).z; b_[3] = (bf16)(v4).w;                   \
     *(bf16x4*)((im) + ((col) >> 7) * (32 * 256) + swz(row, ((col) & 127) >> 3) + 2 * ((col) & 7)) = b_;       \
   }
-#define WG_STAGE(PY, PX, b)                                                                                   \
+// staging chunk cc also adds its dY rows into the column sums (the bias gradient): this thread
+// always holds columns n_base + 4·(tid & 31) of rows (tid >> 5) + 8u; clamped re-loads past the
+// last chunk are weighted 0
+#define WG_STAGE(PY, PX, b, cc)                                                                               \
   {                                                                                                           \
+    const float on_ = (cc) < nchunk ? 1.f : 0.f;                                                              \
     _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
       const int q_ = threadIdx.x + 256 * u;                                                                   \
       WG_PUT(yimg[b], q_ >> 5, 4 * (q_ & 31), PY[u])                                                          \
+      csum.x = fmaf(on_, PY[u].x, csum.x);                                                                    \
+      csum.y = fmaf(on_, PY[u].y, csum.y);                                                                    \
+      csum.z = fmaf(on_, PY[u].z, csum.z);                                                                    \
+      csum.w = fmaf(on_, PY[u].w, csum.w);                                                                    \
     }                                                                                                         \
     _Pragma("unroll") for (int u = 0; u < 8; ++u) WG_PUT(ximg[b], lrow + 4 * u, 4 * lane, PX[u])              \
   }
+  float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
   f32x16 acc[2][4];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -282,14 +292,14 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __re
       _Pragma("unroll") for (int a = 0; a < 2; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) acc[a][b] = \
           __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_[a], fb_[b], acc[a][b], 0, 0, 0);                        \
     }                                                                                                         \
-    WG_STAGE(SY, SX, ((c) + 1) & 1)                                                                           \
+    WG_STAGE(SY, SX, ((c) + 1) & 1, (c) + 1)                                                                  \
     __syncthreads();                                                                                          \
   }
   if (nchunk > 0) {
     float4 Ya[4], Xa[8], Yb[4], Xb[8];
     WG_LOAD(0, Ya, Xa)
     WG_LOAD(1, Yb, Xb)
-    WG_STAGE(Ya, Xa, 0)
+    WG_STAGE(Ya, Xa, 0, 0)
     __syncthreads();
     for (int c = 0; c < nchunk; c += 2) {
       WG_STEP(c, Ya, Xa, Yb, Xb)
@@ -301,6 +311,19 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __re
 #undef WG_STAGE
 #undef WG_PUT
 #undef WG_LOAD
+  // column sums: the 8 threads of a column group (tid >> 5 = 0..7) combined in a fixed order
+  if (part_b) {
+    red_b[threadIdx.x >> 5][threadIdx.x & 31] = csum;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      float4 t = red_b[0][threadIdx.x];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) t = make_float4(t.x + red_b[j][threadIdx.x].x, t.y + red_b[j][threadIdx.x].y,
+                                                  t.z + red_b[j][threadIdx.x].z, t.w + red_b[j][threadIdx.x].w);
+      const int n0 = n_base + 4 * threadIdx.x;
+      if (n0 < N) *(float4*)(part_b + (long)split * N + n0) = t;
+    }
+  }
   // D[n][i]: lane holds (row n = wn + 32a + creg(r), col i = wi + 32b + (lane&31))
   float* out = part + (long)split * N * 256;
 #pragma unroll
@@ -314,16 +337,27 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __re
       }
 }
 
-// out[i] = beta·out[i] + Σ_s part[s][i]  (fixed order, float4)
+// out[i] = beta·out[i] + Σ_s part[s][i]  (fixed order, float4): 8 lanes per float4 output, lane j
+// summing the splits s ≡ j (mod 8), then a fixed xor tree over the 8 lanes
 __global__ void sum_parts_kernel2(const float* __restrict__ part, int nparts, long n, float beta,
                                   float* __restrict__ out) {
-  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i >= n) return;
+  const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long i = (g >> 3) * 4;
+  const int j = (int)(g & 7);
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = 0; s < nparts; ++s) {
-    const float4 v = *(const float4*)(part + (long)s * n + i);
-    t = make_float4(t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w);
+  if (i < n)
+    for (int s = j; s < nparts; s += 8) {
+      const float4 v = *(const float4*)(part + (long)s * n + i);
+      t = make_float4(t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w);
+    }
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    t.x += __shfl_xor(t.x, m, 64);
+    t.y += __shfl_xor(t.y, m, 64);
+    t.z += __shfl_xor(t.z, m, 64);
+    t.w += __shfl_xor(t.w, m, 64);
   }
+  if (i >= n || j) return;
   float4 o = beta == 0.f ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(out + i);
   *(float4*)(out + i) = make_float4(beta * o.x + t.x, beta * o.y + t.y, beta * o.z + t.z, beta * o.w + t.w);
 }
@@ -391,9 +425,10 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
   return 0;
 }
 
-// dW[N][256] (+)= Σ_t dY[t][N]ᵀ·X[t][256] (N % 128 == 0): split over t into `splits` partial
-// slices part[splits][N][256] (c2dsr_wgemm_workspace bytes), combined in a fixed order into dW
-// with beta (0 or 1).
+// dW[N][256] (+)= Σ_t dY[t][N]ᵀ·X[t][256] (N % 128 == 0) and, when db is given, db[N] (+)= Σ_t dY[t][N]
+// (the bias gradient, from the same dY chunks): split over t into `splits` partial slices
+// part[splits][N][256] + [splits][N] (c2dsr_wgemm_workspace bytes), combined in a fixed order with
+// beta (0 or 1).
 static int wg_splits(int N) {
   int dev = 0, ncu = 0;
   (void)hipGetDevice(&dev);
@@ -405,9 +440,9 @@ static int wg_splits(int N) {
 C2_API int c2dsr_wgemm_supported(int T, int N, int D) {
   return T > 0 && D == 256 && N % 128 == 0 && N <= 32 * 128 && (long)T * N * 4 < (1L << 31) && (long)T * D * 4 < (1L << 31);
 }
-C2_API size_t c2dsr_wgemm_workspace(int N) { return (size_t)wg_splits(N) * N * 256 * 4; }
+C2_API size_t c2dsr_wgemm_workspace(int N) { return (size_t)wg_splits(N) * N * 257 * 4; }
 C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
-                       void* part, void* stream) {
+                       float* db, void* part, void* stream) {
   if (!c2dsr_wgemm_supported(T, N, D) || ldy % 4 || ldx % 4) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int NTL = N / 128;
@@ -415,9 +450,11 @@ C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const floa
   if (splits < 8) return (int)hipErrorInvalidValue;
   const int rows = c2::ceil_div(c2::ceil_div(T, splits), 32) * 32;
   const int blocks = splits * NTL;  // = 8 XCDs x (splits/8) x NTL
-  wg_kernel<<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, NTL, rows);
   const long n = (long)N * 256;
-  sum_parts_kernel2<<<c2::ceil_div(n / 4, 256), 256, 0, s>>>((const float*)part, splits, n, beta, dW);
+  float* part_b = db ? (float*)part + (long)splits * n : nullptr;
+  wg_kernel<<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, part_b, NTL, rows);
+  sum_parts_kernel2<<<c2::ceil_div(n / 4 * 8, 256), 256, 0, s>>>((const float*)part, splits, n, beta, dW);
+  if (db) sum_parts_kernel2<<<c2::ceil_div((long)N / 4 * 8, 256), 256, 0, s>>>(part_b, splits, N, beta, db);
   C2_CHECK_LAUNCH();
   return 0;
 }

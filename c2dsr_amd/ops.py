@@ -84,10 +84,11 @@ def wgemm_ok(T, N, D):
     return bool(lib.raw('c2dsr_wgemm_supported')(T, N, D))
 
 
-def wgemm(dY, X, dW, *, T, N, D, beta=1.0):
-    """dW[N, D] = beta·dW + dYᵀ·X over T rows (c2dsr_wgemm, deterministic split-t partials)."""
+def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None):
+    """dW[N, D] = beta·dW + dYᵀ·X over T rows and (db given) db[N] = beta·db + Σ_t dY[t]
+    (c2dsr_wgemm, deterministic split-t partials)."""
     ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
-    lib('c2dsr_wgemm', T, N, D, dY, N, X, D, float(beta), dW, ws, stream())
+    lib('c2dsr_wgemm', T, N, D, dY, N, X, D, float(beta), dW, db, ws, stream())
 
 
 class LinearFn(Function):
@@ -129,12 +130,12 @@ class LinearFn(Function):
             else:
                 gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
         gW = _grad_target(W)
-        if gW is not None:
-            if ctx.precision == BF16 and wgemm_ok(M, N, K):
-                wgemm(dy, x, gW, T=M, N=N, D=K)
-            else:
-                gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
         gb = _grad_target(ctx.b)
+        if gW is not None and ctx.precision == BF16 and wgemm_ok(M, N, K):
+            wgemm(dy, x, gW, T=M, N=N, D=K, db=gb)  # bias gradient from the same dY chunks
+            gb = None
+        elif gW is not None:
+            gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
         if gb is not None:
             colsum(dy, M, N, N, gb)
         return dx, None, None, None, None

@@ -167,14 +167,15 @@ int c2dsr_rgemm_supported(int M, int N, int K);
 int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                 float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                 int64_t row_base, void* stream);
-/* K3 projection weight gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
- * (the mm of the linear backward, N % 128 == 0), bf16 MFMA with transposed LDS reads, split over
- * t into partials part[splits][N][256] (workspace bytes from c2dsr_wgemm_workspace) combined in
- * a fixed order (deterministic).  beta ∈ {0, 1}. */
+/* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
+ * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
+ * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS
+ * reads, split over t into partials (workspace bytes from c2dsr_wgemm_workspace) combined in a fixed
+ * order (deterministic).  beta ∈ {0, 1}. */
 int c2dsr_wgemm_supported(int T, int N, int D);
 size_t c2dsr_wgemm_workspace(int N);
 int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
-                void* part, void* stream);
+                float* db, void* part, void* stream);
 /* y = bf16(x), x fp32 [R][Cc] with row stride ldx; trans: y is [Cc][R] (weight copies for rgemm). */
 int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream);
 

@@ -367,8 +367,13 @@ def test_wgemm_vs_bf16_rounded_fp32(T, N):
     ref = W0.double() + _bf(dY).double().T @ _bf(X).double()
     assert rel(dW, ref) < 1e-5
     dW = torch.full((N, D), 7.0, device=DEV)
-    wgemm(dY.to(DEV), X.to(DEV), dW, T=T, N=N, D=D, beta=0.0)
+    db = torch.full((N,), 3.0, device=DEV)
+    wgemm(dY.to(DEV), X.to(DEV), dW, T=T, N=N, D=D, beta=0.0, db=db)
     assert rel(dW, _bf(dY).double().T @ _bf(X).double()) < 1e-5
+    assert rel(db, dY.double().sum(0)) < 1e-6  # fp32 column sums of the unrounded dY
+    db1 = torch.ones(N, device=DEV)
+    wgemm(dY.to(DEV), X.to(DEV), torch.zeros(N, D, device=DEV), T=T, N=N, D=D, beta=1.0, db=db1)
+    assert rel(db1, 1.0 + dY.double().sum(0)) < 1e-6
     # deterministic: same bits on a re-run
     dW2 = torch.full((N, D), 7.0, device=DEV)
     wgemm(dY.to(DEV), X.to(DEV), dW2, T=T, N=N, D=D, beta=0.0)
