@@ -63,6 +63,7 @@ class StepState:
         self.step = 0
         self.row_offset = 0   # global batch-row offset of this rank (data parallel)
         self.next_share_pass = DK.PASS_NEG0
+        self.grad_hook = None  # c2dsr_amd.dp.GradBuckets while a data-parallel backward runs
 
     def keys(self, site):
         return DK.keys(self.seed, self.step, site)
@@ -163,6 +164,6 @@ class GCN(nn.Module):
         p = self.dropout_gnn if self.training else 0.0
         keys = [self.state.keys(DK.site_gcn(self.table, k)) if p > 0 else (0, 0) for k in range(self.n_gnn)]
         if sink is None:
-            sink = ops.GradSink(h.shape[0], h.shape[1], h.device)
+            sink = ops.GradSink(h.shape[0], h.shape[1], h.device, self.state)
         H, tok = ops.GCNFn.apply(h, adj, self.n_gnn, p, keys, self.pad_row, sink)
         return H, tok, sink

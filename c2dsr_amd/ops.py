@@ -11,6 +11,7 @@ import torch
 from torch.autograd import Function
 
 from ._lib import lib, stream, require_device
+from .dp import notify_lookup, notify_table
 
 FP32, BF16 = 0, 1
 
@@ -150,9 +151,10 @@ class GradSink:
     """Dense gradient w.r.t. one GCN output table H, filled by every embedding lookup of H
     (deterministic segment sums) and consumed once by the GCN backward."""
 
-    def __init__(self, n, d, device):
+    def __init__(self, n, d, device, state=None):
         self.n, self.d, self.device = n, d, device
         self.G = None
+        self.state = state  # StepState: carries the data-parallel bucket hook (c2dsr_amd/dp.py)
 
     def buf(self):
         if self.G is None:
@@ -198,6 +200,7 @@ class GCNFn(Function):
         G = ctx.sink.G
         E = ctx.E
         if G is None:
+            notify_table(ctx.sink.state, E)
             return (None,) * 7
         g = ctx.graph
         n = ctx.n_gnn
@@ -214,6 +217,8 @@ class GCNFn(Function):
                 X, alpha = T, 1.0
             spmm(g, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 1.0, ctx.pad_row, 1.0, gE)
         ctx.sink.G = None
+        if direct:
+            notify_table(ctx.sink.state, E)  # E.grad final: its all-reduce runs under the next GCN backward
         return (None if direct else gE), None, None, None, None, None, None
 
 
@@ -251,6 +256,8 @@ class EmbedFn(Function):
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
         lib('c2dsr_embed_bwd', seq, pos, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.row_base) * L,
             float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes, stream())
+        if ctx.sink is not None:
+            notify_lookup(ctx.sink.state)
         tok_grad = torch.zeros((), device=gx.device)
         return tok_grad, None, gP_ret, None, None, None, None, None, None, None, None, None
 
@@ -403,3 +410,33 @@ class BilinearFn(Function):
         if gb is not None:
             colsum(ds, B, 1, 1, gb)
         return dx1, dx2, None, None
+
+
+# ----------------------------------------------------------------------------- evaluation (§8 f1)
+def eval_rank(h_share, h_a, h_b, idx_last_a, idx_last_b, xory, gt, neg, Wa, ba, Wb, bb):
+    """rank[i] = 1 + #(s(neg) > s(gt)) with s = classifier_dom(h_share[i,-1] + h_dom[i, idx_last_dom[i]])
+    (trainer.py:162-181), all rows at once (csrc/eval.hip).  Returns int32 [B] on the device."""
+    require_device(h_share)
+    B, L, d = h_share.shape
+    for t in (h_a, h_b):
+        if t.shape != h_share.shape:
+            raise ValueError('h_share / hx / hy shapes differ')
+    n_neg = neg.shape[1] if neg.dim() == 2 else 0
+    ints = [x.reshape(-1).contiguous().long() for x in (idx_last_a, idx_last_b, xory, gt)]
+    for x in ints:
+        if x.numel() != B:
+            raise ValueError('idx_last / xory / gt must hold one entry per row')
+    neg = neg.contiguous().long()
+    rank = torch.empty(B, dtype=torch.int32, device=h_share.device)
+    lib('c2dsr_eval_rank', h_share.contiguous(), h_a.contiguous(), h_b.contiguous(), B, L, d, *ints, neg, n_neg,
+        Wa.contiguous(), ba.contiguous(), Wa.shape[0], Wb.contiguous(), bb.contiguous(), Wb.shape[0], rank, stream())
+    return rank
+
+
+def rank_metrics(rank, xory, dom, sums):
+    """sums[0..7] += (hr5, hr20, mrr5, mrr20, ndcg5, ndcg20, count, n_bad) of the rows of domain ``dom``
+    (utils/metrics.py:4-19, fp64 on the device)."""
+    require_device(rank)
+    xory = xory.reshape(-1).contiguous().long()
+    lib('c2dsr_rank_metrics', rank, xory, rank.numel(), int(dom), sums, stream())
+    return sums

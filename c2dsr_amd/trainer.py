@@ -17,8 +17,11 @@ import torch
 import torch.distributed as dist
 
 from .dataloader import get_dataloader
+from . import ops
+from .dp import GradBuckets
 from .graph import make_graph
 from .losshead import LossHeadFn, LossMeta
+from .metrics import RankMetrics
 from .models.C2DSR import C2DSR
 from .optim import FlatAdamW
 
@@ -85,24 +88,14 @@ class Trainer(object):
         if self.noter is not None:
             self.noter.log_train(acc[0], acc[1], acc[2], time.time() - t0)
         self.model.eval()
-        ra, rb = [], []
         with torch.no_grad():
             self.model.convolve_graph()
-            for batch in self.valloader:
-                a, b = self.evaluate_batch(batch)
-                ra += a
-                rb += b
-        return ra, rb
+            return self._evaluate(self.valloader)
 
     def run_test(self):
         self.model.eval()
-        ra, rb = [], []
         with torch.no_grad():
-            for batch in self.testloader:
-                a, b = self.evaluate_batch(batch)
-                ra += a
-                rb += b
-        return ra, rb
+            return self._evaluate(self.testloader)
 
     def cal_mask(self, gt_mask):
         """trainer.py:85-89 (API compatibility; the fused loss head computes the weights itself)."""
@@ -136,34 +129,65 @@ class Trainer(object):
         h_neg_b = m.forward_share(neg_b, pos)
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
         loss, loss_rec, loss_mi = LossHeadFn.apply(h_share, hx, hy, h_neg_a, h_neg_b, meta)
-        loss.backward()
         if self.world > 1:
-            dist.all_reduce(m.flat.fresh)
+            # bucketed all-reduce of the fresh gradient, each bucket issued as soon as the backward
+            # has made it final (c2dsr_amd/dp.py): dense params under the GCN backwards, each item
+            # table under the next table's GCN backward
+            tables = [m.embed_i.weight, m.embed_i_a.weight, m.embed_i_b.weight]
+            m.state.grad_hook = GradBuckets(m.flat, tables, n_lookups=5)
+            try:
+                loss.backward()
+            finally:
+                hook, m.state.grad_hook = m.state.grad_hook, None
+            hook.finish()
+        else:
+            loss.backward()
         self.optimizer.step()
         return loss, loss_rec, loss_mi
 
     # ------------------------------------------------------------------ evaluation
-    def evaluate_batch(self, batch):
-        """trainer.py:162-181: rank of the ground truth among its sampled negatives
-        (ties not counted: rank = #(neg > gt) + 1), per domain of the last item."""
+    def eval_ranks(self, batch):
+        """Device ranks of one evaluation batch (trainer.py:162-181 on csrc/eval.hip): returns
+        (rank int32 [B], xory int64 [B]); row i belongs to domain a iff xory[i] == 0."""
         (seq_share, seq_a, seq_b, pos, pos_a, pos_b, idx_last_a, idx_last_b, xory_last, gt_last,
          list_neg) = [x.to(self.device) for x in batch]
         h_share, hx, hy = self.model(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
-        B, L, d = h_share.shape
-        rows = torch.arange(B, device=self.device)
-        flag = xory_last[:, 0]
-        h_last = h_share[:, -1]
-        rank_a, rank_b = [], []
-        for dom, hdom, il, clf in ((0, hx, idx_last_a[:, 0], self.model.classifier_a),
-                                   (1, hy, idx_last_b[:, 0], self.model.classifier_b)):
-            sel = (flag == dom).nonzero().flatten()
-            if sel.numel() == 0:
-                continue
-            q = h_last[sel] + hdom[rows[sel], il[sel]]
-            scores = clf(q)
-            gt = scores.gather(1, gt_last[sel])
-            neg = scores.gather(1, list_neg[sel])
-            r = ((neg > gt).sum(1) + 1).tolist()
-            (rank_a if dom == 0 else rank_b).extend(r)
-        # keep the reference's output order (rows in batch order within each domain)
-        return rank_a, rank_b
+        m = self.model
+        rank = ops.eval_rank(h_share, hx, hy, idx_last_a, idx_last_b, xory_last, gt_last, list_neg,
+                             m.classifier_a.weight, m.classifier_a.bias, m.classifier_b.weight, m.classifier_b.bias)
+        return rank, xory_last.reshape(-1)
+
+    @staticmethod
+    def _split(ranks, flags):
+        r = torch.cat(ranks).tolist() if ranks else []
+        f = torch.cat(flags).tolist() if flags else []
+        if any(x < 1 for x in r):
+            raise IndexError('evaluation index out of range (idx_last / gt / negative item)')
+        ra = [x for x, fl in zip(r, f) if fl == 0]
+        rb = [x for x, fl in zip(r, f) if fl != 0]
+        return ra, rb
+
+    def evaluate_batch(self, batch):
+        """trainer.py:162-181: rank of the ground truth among its sampled negatives (ties not counted:
+        rank = #(neg > gt) + 1), split by the domain of the last item, rows in batch order."""
+        rank, flag = self.eval_ranks(batch)
+        return self._split([rank], [flag])
+
+    def _evaluate(self, loader):
+        ranks, flags = [], []
+        for batch in loader:
+            rank, flag = self.eval_ranks(batch)
+            ranks.append(rank)
+            flags.append(flag)
+        return self._split(ranks, flags)  # one host sync per evaluation pass
+
+    def evaluate_metrics(self, loader):
+        """Metrics of a whole evaluation pass on the device (cal_metrics per domain, one host sync):
+        returns a metrics.RankMetrics (``.values()``, ``.score(benchmark)``)."""
+        acc = RankMetrics(self.device)
+        self.model.eval()
+        with torch.no_grad():
+            for batch in loader:
+                rank, flag = self.eval_ranks(batch)
+                acc.add(rank, flag)
+        return acc

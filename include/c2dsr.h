@@ -179,6 +179,21 @@ int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, i
 /* y = bf16(x), x fp32 [R][Cc] with row stride ldx; trans: y is [Cc][R] (weight copies for rgemm). */
 int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream);
 
+/* Evaluation (csrc/eval.hip).  Replaces trainer.py:162-181 (evaluate_batch):
+ * per row i, dom = (xory[i] == 0 ? a : b), q = h_share[i,L-1] + h_dom[i, idx_last_dom[i]],
+ * s(j) = q·W_dom[j] + b_dom[j] over the candidates gt[i] and neg[i, 0..n_neg), and
+ * rank[i] = 1 + #{k : s(neg[i,k]) > s(gt[i])} (ties not counted).  h_* [B,L,d]; idx_last_*, xory, gt
+ * int64 [B] (the reference's [B,1] tensors); neg int64 [B][n_neg]; rank int32 [B], -1 for an index out
+ * of range (the reference raises IndexError; the host binding raises). */
+int c2dsr_eval_rank(const float* h_share, const float* h_a, const float* h_b, int B, int L, int d,
+                    const int64_t* idx_last_a, const int64_t* idx_last_b, const int64_t* xory, const int64_t* gt,
+                    const int64_t* neg, int n_neg, const float* Wa, const float* ba, int n_a, const float* Wb,
+                    const float* bb, int n_b, int* rank, void* stream);
+/* utils/metrics.py:4-19 (cal_metrics) as device sums: sums[0..7] += (hr5, hr20, mrr5, mrr20, ndcg5, ndcg20,
+ * count, n_bad) over the rows with (xory == 0) == (dom == 0); fp64, fixed reduction order.  The metrics
+ * are sums[k]/count; accumulating over all batches of an evaluation costs one host sync per epoch. */
+int c2dsr_rank_metrics(const int* rank, const int64_t* xory, int B, int dom, double* sums, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,6 +20,8 @@ Reference semantics restated (file:line in /root/reference):
   * bilinear + BCE      trainer.py:104-119, C2DSR.py:46-55
   * heads + CE          trainer.py:121-154        (pad column = ignore_index, Q6; count weighting Q7; Q8)
   * loss / AdamW        trainer.py:156-158, :21-22 (amsgrad, decoupled wd; grads accumulate, Q3)
+  * evaluate_batch      trainer.py:162-181        (rank vs sampled negatives, ties not counted)
+  * cal_metrics/score   utils/metrics.py:4-31     (HR/MRR/NDCG@{5,20}, improvement over benchmark)
 
 Dropout: the reference draws torch-CPU masks that no GPU RNG can reproduce, so
 parity against the reference uses p = 0.  For p > 0 the GPU kernels use a
@@ -387,3 +389,53 @@ def cfg_from_args(a) -> dict:
                 len_rec=a.len_rec, lambda_loss=a.lambda_loss, n_gnn=a.n_gnn, n_attn=a.n_attn, n_head=a.n_head,
                 norm_first=a.norm_first, d_bias=a.d_bias, shared_item_embed=a.shared_item_embed,
                 dropout_gnn=a.dropout_gnn, dropout_attn=a.dropout_attn)
+
+
+# ----------------------------------------------------------------------------- evaluation (§8 f1)
+def evaluate_batch(P, graphs, batch, cfg):
+    """trainer.py:162-181 (model.eval(): no dropout; convolve_graph first as in run_epoch:64).
+    Returns (rank_a, rank_b) lists, rows in batch order within each domain."""
+    (seq, seq_a, seq_b, pos, pos_a, pos_b, il_a, il_b, xory, gt, neg) = batch
+    es, ea, eb = embed_names(cfg)
+    cfg0 = dict(cfg, dropout_gnn=0.0, dropout_attn=0.0)
+    dr = Dropper(0.0, 0.0)
+    with torch.no_grad():
+        hs_t, ha_t, hb_t = convolve_graph(P, graphs, cfg0, dr)
+        h_share = encode(P, hs_t, es, 'attn_share', seq, pos, cfg0, dr, 0)
+        hx = encode(P, ha_t, ea, 'attn_a', seq_a, pos_a, cfg0, dr, 1)
+        hy = encode(P, hb_t, eb, 'attn_b', seq_b, pos_b, cfg0, dr, 2)
+        ra, rb = [], []
+        for i in range(seq.shape[0]):
+            if int(xory[i]) == 0:
+                q = h_share[i, -1] + hx[i, int(il_a[i])]
+                s = P['classifier_a.weight'] @ q + P['classifier_a.bias']
+                ra.append(int((s[neg[i]] > s[gt[i]]).sum()) + 1)
+            else:
+                q = h_share[i, -1] + hy[i, int(il_b[i])]
+                s = P['classifier_b.weight'] @ q + P['classifier_b.bias']
+                rb.append(int((s[neg[i]] > s[gt[i]]).sum()) + 1)
+    return ra, rb
+
+
+def cal_metrics(ranks):
+    """utils/metrics.py:4-19."""
+    N = len(ranks)
+    v = [0.0] * 6
+    for r in ranks:
+        if r <= 20:
+            v[1] += 1
+            v[3] += 1 / r
+            v[5] += 1 / np.log2(r + 1)
+            if r <= 5:
+                v[0] += 1
+                v[2] += 1 / r
+                v[4] += 1 / np.log2(r + 1)
+    return [x / N for x in v]
+
+
+def cal_score(ranks_a, ranks_b, benchmark):
+    """utils/metrics.py:22-31."""
+    res = cal_metrics(ranks_a) + cal_metrics(ranks_b)
+    sel = [res[0], res[4], res[6], res[10]]
+    imp = np.array([x / y - 1 for x, y in zip(sel, benchmark)])
+    return [float(np.mean(imp))] + res

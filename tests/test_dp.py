@@ -69,3 +69,74 @@ def test_dp_world2_equals_single_device(tmp_path, cfg_name, p):
     assert got.shape == ref.shape
     assert np.abs(got - ref).max() <= 1e-5 * max(1.0, np.abs(ref).max())
     np.testing.assert_allclose(loss, [float(out['loss']), float(out['loss_rec']), float(out['loss_mi'])], rtol=1e-5)
+
+
+# ----------------------------------------------------------------------------- bucketed all-reduce (dp.py)
+def _toy_store(shared):
+    from c2dsr_amd.flat import FlatStore
+    torch.manual_seed(0)
+    e = torch.nn.Parameter(torch.randn(7, 5))
+    ea = e if shared else torch.nn.Parameter(torch.randn(7, 5))
+    eb = e if shared else torch.nn.Parameter(torch.randn(7, 5))
+    pos = torch.nn.Parameter(torch.randn(3, 5))
+    w = torch.nn.Parameter(torch.randn(6, 5))
+    b = torch.nn.Parameter(torch.randn(6))
+    named = [('embed_i.weight', e), ('embed_i_a.weight', ea), ('embed_i_b.weight', eb), ('pos', pos), ('w', w),
+             ('b', b)]
+    return FlatStore(named, torch.device('cpu')), (e, ea, eb)
+
+
+class _Done:
+    def wait(self):
+        pass
+
+
+@pytest.mark.parametrize('shared', [False, True])
+def test_grad_buckets_cover_once(shared):
+    from c2dsr_amd.dp import GradBuckets
+    flat, tables = _toy_store(shared)
+    seen = []
+    gb = GradBuckets(flat, list(tables), n_lookups=5, allreduce=lambda t: seen.append(t) or _Done())
+    for _ in range(4):
+        gb.lookup_done()
+    assert gb.issued == []
+    gb.lookup_done()  # dense bucket final after the 5th lookup backward
+    t_end = max(hi for _, hi in gb.table_range.values())
+    assert len(gb.issued) >= 1 and all(lo >= t_end for lo, _ in gb.issued)
+    for t in reversed(tables):  # GCN backwards run b, a, share
+        gb.table_done(t)
+    gb.finish()
+    mark = torch.zeros(flat.numel, dtype=torch.int32)
+    for lo, hi in gb.issued:
+        mark[lo:hi] += 1
+    for _, p, o, n in flat.entries:
+        assert bool((mark[o:o + n] == 1).all())
+
+
+def _bucket_worker(rank, world, port, out_dir):
+    from c2dsr_amd.dp import GradBuckets
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    flat, tables = _toy_store(False)
+    g = torch.Generator().manual_seed(100 + rank)
+    flat.fresh.copy_(torch.randn(flat.numel, generator=g))
+    full = flat.fresh.clone()
+    dist.all_reduce(full)
+    gb = GradBuckets(flat, list(tables), n_lookups=2)
+    gb.lookup_done()
+    gb.table_done(tables[2])  # a table may become final before the dense bucket
+    gb.lookup_done()
+    gb.table_done(tables[1])
+    gb.table_done(tables[0])
+    gb.finish()
+    err = 0.0
+    for _, p, o, n in flat.entries:
+        err = max(err, float((flat.fresh[o:o + n] - full[o:o + n]).abs().max()))
+    if rank == 0:
+        np.save(os.path.join(out_dir, 'err.npy'), np.array([err]))
+    dist.destroy_process_group()
+
+
+def test_grad_buckets_world2_equal_full_allreduce(tmp_path):
+    mp.spawn(_bucket_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert float(np.load(tmp_path / 'err.npy')[0]) == 0.0

@@ -66,3 +66,30 @@ def test_dropout_hash_rate_and_determinism():
     # >32-bit indices use the high word
     hi = idx + (1 << 33)
     assert (O.keep_mask(hi, k, 0.2) != m1).mean() > 0.2
+
+
+def _eval_batch(name, mode):
+    d = G.load(f'data_{name}.npz')
+    return tuple(torch.from_numpy(np.ascontiguousarray(d[f'{mode}_{j}'])) for j in range(11))
+
+
+def eval_params(name):
+    e = G.load(f'eval_{name}.npz')
+    return {k[len('param/'):]: torch.from_numpy(e[k].copy()) for k in e.files if k.startswith('param/')}
+
+
+@pytest.mark.parametrize('name', list(G.CONFIGS))
+def test_oracle_eval_ranks_match_reference(name):
+    e = G.load(f'eval_{name}.npz')
+    for mode in ('val', 'test'):
+        ra, rb = O.evaluate_batch(eval_params(name), G.graphs_coo(name), _eval_batch(name, mode), G.oracle_cfg(name))
+        assert ra == e[f'{mode}_rank_a'].tolist(), (mode, 'a')
+        assert rb == e[f'{mode}_rank_b'].tolist(), (mode, 'b')
+
+
+def test_oracle_metrics_match_reference():
+    m = G.load('metrics.npz')
+    ra, rb = m['ranks_a'].tolist(), m['ranks_b'].tolist()
+    np.testing.assert_allclose(O.cal_metrics(ra), m['metrics_a'], rtol=1e-14)
+    np.testing.assert_allclose(O.cal_score(ra, rb, [0.1124, 0.0865, 0.0574, 0.0416]), m['score_fk'], rtol=1e-14)
+    np.testing.assert_allclose(O.cal_score(ra, rb, [0.0647, 0.0476, 0.0284, 0.0217]), m['score_mb'], rtol=1e-14)
