@@ -113,6 +113,79 @@ class KernelTimer:
         return dict(tflops=fl_all / (ms_all * 1e-3) / 1e12, ms=ms_all, per_kernel=per)
 
 
+class HbmTimer:
+    """HIP-event timing of the HBM-bound K1 (c2dsr_gcn_spmm) and K2 (c2dsr_embed_fwd / _bwd) launches
+    inside the timed region, with ALGORITHMIC bytes per launch:
+
+    * K1 SpMM launch over a graph of N rows and E edges, row width d (fp32):
+      4·d·E (neighbour rows gathered) + 8·E (col + val) + 4·(N+1) (row pointers)
+      + 4·d·N·(1 [write Y] + [Z read: self / gradient term] + [Y read: accumulate, gamma != 0] + [Y2 write])
+      — fwd (n_gnn=1) = 4d(2N+E)+8E+4(N+1), bwd = 4d(3N+E)+8E+4(N+1), the survey's formulas;
+    * K2 forward, per looked-up row: 16 (seq + pos int64) + 4·d·(#tables read) + 4·d (write);
+      the L-row position table is cache-resident and not credited;
+    * K2 backward, per row: 16 + 4·d (read dX) [+ 4·d if dXin is written]; plus 8·d per DISTINCT item
+      of the batch (read-modify-write of its gradient row, ``uniq`` from the host copy of the batch).
+      Sort passes and pad-row segments are overhead, not credited."""
+
+    NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_bwd')
+
+    def __init__(self, n_rows_table, nnz_by_col_ptr, uniq_by_seq_ptr):
+        from c2dsr_amd._lib import lib
+        self.lib = lib
+        self.N = n_rows_table
+        self.nnz = nnz_by_col_ptr
+        self.uniq = uniq_by_seq_ptr
+
+    def start(self):
+        for n in self.NAMES:
+            self.lib.timed.pop(n, None)
+        self.lib.time_names.update(self.NAMES)
+
+    def stop(self):
+        self.lib.time_names.difference_update(self.NAMES)
+
+    def launch_bytes(self, name, a):
+        if name == 'c2dsr_gcn_spmm':
+            d, E, N = a[7], self.nnz[a[5]], self.N
+            rows = 1 + (a[14] is not None) + (a[18] != 0.0) + (a[20] is not None)
+            return 4 * d * E + 8 * E + 4 * (N + 1) + 4 * d * N * rows
+        if name == 'c2dsr_embed_fwd':
+            n, d = a[2], a[3]
+            reads = (a[4] is not None) + (a[5] is not None) + (a[6] is not None)
+            return n * (16 + 4 * d * reads + 4 * d)
+        n, d = a[2], a[3]  # c2dsr_embed_bwd
+        return n * (16 + 4 * d + (4 * d if a[14] is not None else 0)) + 8 * d * self.uniq.get(a[0], 0)
+
+    def summary(self, steps):
+        torch.cuda.synchronize()
+        per, tb, tms = {}, 0.0, 0.0
+        for name in self.NAMES:
+            rec = self.lib.timed.get(name, [])
+            if not rec:
+                continue
+            ms = sum(e0.elapsed_time(e1) for e0, e1, _ in rec)
+            by = sum(self.launch_bytes(name, a) for _, _, a in rec)
+            per[name] = dict(launches=len(rec), avg_ms=round(ms / len(rec), 4), gbs=round(by / (ms * 1e-3) / 1e9, 1),
+                             bytes_per_launch=int(by / len(rec)))
+            tb += by
+            tms += ms
+        if not per:
+            return None
+        ach = tb / (tms * 1e-3) / 1e9
+        return dict(bound='hbm', achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit='GB/s', frac=round(ach / PEAK_HBM_GBS, 4),
+                    traffic=None, kernel='K1 c2dsr_gcn_spmm (fwd+bwd) + K2 c2dsr_embed_fwd/bwd; algorithmic bytes '
+                    '(bench.py HbmTimer)', ms_per_step=round(tms / steps, 4), per_kernel=per)
+
+
+def uniq_counts(batches):
+    """data_ptr of every device index tensor of the batches -> number of distinct items in it."""
+    out = {}
+    for b in batches:
+        for j in (0, 1, 2, 12, 13):  # seq_share, seq_a, seq_b, neg_a, neg_b
+            out[b[j].data_ptr()] = int(torch.unique(b[j]).numel())
+    return out
+
+
 def k5_traffic(precision):
     """HBM bytes per K5 launch triple (lse + dH + dW kernels, both heads averaged) from the separate
     rocprofv3 FETCH_SIZE (x2, the gfx950 correction) / WRITE_SIZE passes of tools/round_profile.sh,
@@ -167,16 +240,114 @@ def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
                        f'L={cfg["L"]}, batch {Bs}, {steps - 1} timed steps, dropout 0.2')
 
 
+def run_c5(opt, world, rank, device):
+    """BASELINE configs[4] / SURVEY.md §8(d) C5 as a kernel roofline run: synthetic two-domain
+    10M + 10M items, d=512, L=100, B=8192 global (8192/N per GPU, weak per-GPU work at N=8: 1024),
+    graph from 2M sequences.  A full replicated model is infeasible (164 GB of fp32 parameters before
+    optimizer state, ~13 TB of logits), so a step is the HBM-bound part of the training step on the
+    shared table: K1 GCN forward (A·drop(E), mean) + the five K2 embedding gathers (share, a, b, neg_a,
+    neg_b index sets) forward + their deterministic backward + the K1 GCN backward through Aᵀ into
+    E.grad, all on the product's autograd functions (ops.GCNFn / ops.EmbedFn).  Value = algorithmic
+    GB/s of those kernels (HbmTimer); each rank works on its own batch (no exchange)."""
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import ops, synth
+    from c2dsr_amd import dropout as DK
+    from c2dsr_amd.models.encoders import GCN, StepState
+    n_a = n_b = 10_000_000
+    d, L = 512, 100
+    N = n_a + n_b + 1
+    B = opt.batch or 1024  # 8192 global over the 8 GPUs of the node
+    t0 = time.time()
+    items, off = synth.make_flat_sequences(opt.c5_seqs, n_a, n_b, L, seed=1)
+    seq_id = np.repeat(np.arange(off.size - 1, dtype=np.int64), np.diff(off))
+    same = seq_id[1:] == seq_id[:-1]
+    share = np.stack([items[:-1][same], items[1:][same]], 1)
+    del seq_id, same
+    g = GR.normalized_csr(share, N)
+    del share
+    log(f'[c5] {off.size - 1} sequences, {items.size} interactions, share graph nnz {g.nnz}, '
+        f'prep {time.time() - t0:.1f}s')
+    first = rank * B  # this rank's batch rows
+    seqs = [items[off[i]:off[i + 1]].tolist() for i in range(first * 2, first * 2 + 2 * B)]
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, n_a, n_b, L))  # drops sequences without targets
+    assert rows[0].shape[0] >= B, rows[0].shape
+    del items, off
+    dg = GR.DeviceGraph(g, device)
+    b = [torch.from_numpy(r[:B].copy()).to(device) for r in rows]
+    passes = [(b[0], b[3]), (b[1], b[4]), (b[2], b[5]), (b[12], b[3]), (b[13], b[3])]
+    torch.manual_seed(0)
+    E = torch.nn.Parameter(torch.empty(N, d, device=device).normal_(0.0, 0.1))
+    E.grad = torch.zeros_like(E)
+    P = torch.nn.Parameter(torch.empty(L, d, device=device).normal_(0.0, 0.1))
+    P.grad = torch.zeros_like(P)
+    gx = torch.empty(B, L, d, device=device).normal_(0.0, 1e-3)
+    args = SimpleNamespace(dropout_gnn=0.2, n_gnn=1, idx_pad=N - 1)
+    state = StepState(seed=3407)
+    gcn = GCN(args)
+    gcn.state = state
+    p = 0.2
+
+    def step():
+        state.step += 1
+        H, tok, sink = gcn(E, dg)
+        xs = []
+        for k, (seq, pos) in enumerate(passes):
+            keys = state.keys(DK.site_enc(k, 0, DK.K_INPUT))
+            xs.append(ops.EmbedFn.apply(tok, E, P, seq, pos, H, math.sqrt(d), p, keys, rank * B, sink, N - 1))
+        torch.autograd.backward(xs, [gx] * len(xs))
+
+    nnz = {}
+    for t in (False, True):
+        col = dg.plan(t)[5]
+        nnz[col.data_ptr()] = col.numel()
+    uniq = {seq.data_ptr(): int(torch.unique(seq).numel()) for seq, _ in passes}
+    ht = HbmTimer(N, nnz, uniq)
+    for _ in range(opt.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ht.start()
+    t0 = time.perf_counter()
+    for _ in range(opt.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ht.stop()
+    if world > 1:
+        t = torch.tensor([el], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    roof = ht.summary(opt.steps)
+    if rank == 0:
+        out = {'metric': 'C5 HBM roofline: K1 GCN SpMM + K2 embedding gather (fwd+bwd), algorithmic GB/s',
+               'value': round(roof['achieved'] * world, 1), 'unit': 'GB/s (all ranks)', 'n_gpus': world,
+               'steps': opt.steps, 'warmup': opt.warmup, 'ms_per_step': round(el / opt.steps * 1e3, 3),
+               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+               'data': 'synthetic (Zipf two-domain sequences, vectorised generator)',
+               'config': {'workload': 'c5: synthetic 10M+10M items, d=512, L=100 (BASELINE configs[4])',
+                          'n_item': N, 'd': d, 'seq_len': L, 'batch_per_gpu': B, 'global_batch': B * world,
+                          'graph_sequences': opt.c5_seqs, 'graph_nnz': g.nnz, 'dropout': p,
+                          'parallelism': f'dp{world}'},
+               'roofline': roof, 'cpu_baseline': None}
+        print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', default='mb', choices=list(CONFIGS))
+    ap.add_argument('--config', default='mb', choices=list(CONFIGS) + ['c5'])
     ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--batch', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
+    ap.add_argument('--c5-seqs', type=int, default=2_000_000)
     opt = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -186,6 +357,11 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     device = torch.device('cuda', local)
+    if opt.config == 'c5':
+        run_c5(opt, world, rank, device)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     cfg = dict(CONFIGS[opt.config])
     if opt.batch:
         cfg['B'] = opt.batch
@@ -209,6 +385,13 @@ def main():
         lo = ((i * world + rank) * B) % max(1, n_rows - B)
         batches.append(tuple(torch.from_numpy(r[lo:lo + B].copy()).to(device) for r in rows))
     timer = KernelTimer(opt.precision)
+    dgs = tr.model.graphs()
+    nnz = {}
+    for g in dgs:
+        for t in (False, True):
+            col = g.plan(t)[5]
+            nnz[col.data_ptr()] = col.numel()
+    htimer = HbmTimer(tr.model.n_item, nnz, uniq_counts(batches))
     tr.model.train()
     tr.optimizer.zero_grad()
 
@@ -222,6 +405,7 @@ def main():
     if world > 1:
         dist.barrier()
     timer.start()
+    htimer.start()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = None
@@ -232,12 +416,14 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     timer.stop()
+    htimer.stop()
     if world > 1:
         t = torch.tensor([el], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     loss = float(last[0].detach())
     ks = timer.summary()
+    hb = htimer.summary(opt.steps)
     ms = el / opt.steps * 1e3
     value = B * world * opt.steps / el
     if rank == 0:
@@ -262,7 +448,7 @@ def main():
                           'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B, 'global_batch': B * world,
                           'len_rec': 10, 'dropout': 0.2, 'parallelism': f'dp{world}'},
                'loss': round(loss, 5) if math.isfinite(loss) else None,
-               'roofline': roof, 'cpu_baseline': cpu}
+               'roofline': roof, 'roofline_hbm': hb, 'cpu_baseline': cpu}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -199,7 +199,7 @@ int lpr_for(int d) {
   return l;
 }
 
-constexpr int LN_BWD_BLOCKS = 512;
+constexpr int LN_BWD_BLOCKS = 2048;  // 8 waves per SIMD at d=256 (grid-stride over rows)
 
 }  // namespace
 

@@ -80,3 +80,49 @@ def make_dataset(path: str, n_a: int, n_b: int, len_max: int, n_train: int, n_ev
     for k, (mode, n) in enumerate((('train', n_train), ('val', n_eval), ('test', n_eval))):
         seqs = make_sequences(n, n_a, n_b, len_max, seed=seed + 101 * k, n_min=n_min)
         write_raw(path, mode, seqs, seed=seed + 7 + k, ties=ties)
+
+
+def make_flat_sequences(n_users: int, n_a: int, n_b: int, len_max: int, *, seed: int = 1, s: float = 1.2,
+                        n_min: int = 6, p_a: float = 0.5) -> tuple[np.ndarray, np.ndarray]:
+    """Vectorised generator for the large synthetic configs (10M+10M items,
+    ~2M sequences): same distribution as :func:`make_sequences` (Zipf(s) popularity per domain over
+    a random permutation of the ids, domain ~ Bernoulli(p_a), length ~ U[n_min, L]) returned flat:
+    (items int64 [Σn], offsets int64 [n_users+1])."""
+    rng = np.random.default_rng(seed)
+    n_min = max(2, min(n_min, len_max))
+    lens = rng.integers(n_min, len_max + 1, size=n_users)
+    off = np.zeros(n_users + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    tot = int(off[-1])
+    dom = rng.random(tot) < p_a
+    out = np.empty(tot, dtype=np.int64)
+    for is_a, n, base in ((True, n_a, 0), (False, n_b, n_a)):
+        cdf = np.cumsum(zipf_probs(n, s))
+        cdf /= cdf[-1]
+        sel = dom if is_a else ~dom
+        k = int(sel.sum())
+        rank = np.minimum(np.searchsorted(cdf, rng.random(k), side='right'), n - 1)
+        perm = rng.permutation(n)
+        out[sel] = perm[rank] + base
+    return out, off
+
+
+def transition_edges_flat(items: np.ndarray, off: np.ndarray, n_item_a: int) -> tuple[np.ndarray, np.ndarray]:
+    """graph.transition_edges on flat sequences (vectorised; same edge multiset and emission order):
+    share = consecutive pairs within a sequence, specific = consecutive same-domain pairs."""
+    seq_id = np.repeat(np.arange(off.size - 1, dtype=np.int64), np.diff(off))
+    same = seq_id[1:] == seq_id[:-1]
+    share = np.stack([items[:-1][same], items[1:][same]], 1)
+    is_a = items < n_item_a
+    # per domain: consecutive items of that domain within one sequence, interleaved back into the
+    # reference's emission order (position of the later item)
+    pos = np.arange(items.size, dtype=np.int64)
+    parts = []
+    for m in (is_a, ~is_a):
+        it, sid, ps = items[m], seq_id[m], pos[m]
+        ok = sid[1:] == sid[:-1]
+        parts.append((ps[1:][ok], it[:-1][ok], it[1:][ok]))
+    ps = np.concatenate([p[0] for p in parts])
+    order = np.argsort(ps, kind='stable')
+    spec = np.stack([np.concatenate([p[1] for p in parts])[order], np.concatenate([p[2] for p in parts])[order]], 1)
+    return share.reshape(-1, 2), spec.reshape(-1, 2)

@@ -24,3 +24,18 @@ def test_work_plan_covers_every_edge_once():
     for row, sb, se, _ in split:
         pieces = work[work[:, 0] == row]
         assert (pieces[:, 3] == np.arange(sb, se)).all()
+
+
+def test_flat_generator_edges_match_reference_rules():
+    """The vectorised C5 generator's edges equal graph.transition_edges (the reference's rules) on
+    the same sequences."""
+    import numpy as np
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import synth
+    items, off = synth.make_flat_sequences(500, 300, 400, 30, seed=4)
+    assert off[-1] == items.size and items.min() >= 0 and items.max() < 700
+    seqs = [items[off[i]:off[i + 1]].tolist() for i in range(500)]
+    sh_ref, sp_ref = GR.transition_edges(seqs, 300)
+    sh, sp = synth.transition_edges_flat(items, off, 300)
+    np.testing.assert_array_equal(sh, sh_ref)
+    np.testing.assert_array_equal(sp, sp_ref)
