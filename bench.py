@@ -127,7 +127,7 @@ class HbmTimer:
       of the batch (read-modify-write of its gradient row, ``uniq`` from the host copy of the batch).
       Sort passes and pad-row segments are overhead, not credited."""
 
-    NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_bwd')
+    NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_bwd', 'c2dsr_embed_bwd_planned')
 
     def __init__(self, n_rows_table, nnz_by_col_ptr, uniq_by_seq_ptr):
         from c2dsr_amd._lib import lib
@@ -137,12 +137,16 @@ class HbmTimer:
         self.uniq = uniq_by_seq_ptr
 
     def start(self):
+        from c2dsr_amd import ops
         for n in self.NAMES:
             self.lib.timed.pop(n, None)
         self.lib.time_names.update(self.NAMES)
+        # a planned backward's first argument is the seq plan: resolve it to the index tensor at launch
+        self.lib.time_meta['c2dsr_embed_bwd_planned'] = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0]), 0)
 
     def stop(self):
         self.lib.time_names.difference_update(self.NAMES)
+        self.lib.time_meta.pop('c2dsr_embed_bwd_planned', None)
 
     def launch_bytes(self, name, a):
         if name == 'c2dsr_gcn_spmm':
@@ -153,7 +157,9 @@ class HbmTimer:
             n, d = a[2], a[3]
             reads = (a[4] is not None) + (a[5] is not None) + (a[6] is not None)
             return n * (16 + 4 * d * reads + 4 * d)
-        n, d = a[2], a[3]  # c2dsr_embed_bwd
+        n, d = a[2], a[3]
+        if name == 'c2dsr_embed_bwd_planned':  # (seq_plan, pos_plan, n, d, gX, .., G, n_items, gP, n_pos, gXin, ..)
+            return n * (16 + 4 * d + (4 * d if a[14] is not None else 0)) + 8 * d * a[-1]
         return n * (16 + 4 * d + (4 * d if a[14] is not None else 0)) + 8 * d * self.uniq.get(a[0], 0)
 
     def summary(self, steps):

@@ -55,12 +55,16 @@ class HipLibError(RuntimeError):
     pass
 
 
+DEBUG_SYNC = os.environ.get('C2DSR_DEBUG_SYNC', '0') == '1'
+
+
 class _Lib:
     def __init__(self):
         self._lib = None
         self._sigs = None
         self.time_names = set()  # entry points bracketed by HIP events (bench.py roofline)
         self.timed = {}
+        self.time_meta = {}  # name -> fn(args) evaluated at launch; its value is appended to the record
 
     def load(self):
         if self._lib is not None:
@@ -94,7 +98,19 @@ class _Lib:
             e0.record()
             rc = getattr(lib, name)(*conv)
             e1.record()
-            self.timed.setdefault(name, []).append((e0, e1, conv))
+            meta = self.time_meta.get(name)
+            rec = conv + [meta(conv)] if meta is not None else conv
+            self.timed.setdefault(name, []).append((e0, e1, rec))
+        elif DEBUG_SYNC:  # C2DSR_DEBUG_SYNC=1: attribute an asynchronous device fault to its entry point
+            try:
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001
+                raise HipLibError(f'device fault before {name} (after the previous entry point)') from e
+            rc = getattr(lib, name)(*conv)
+            try:
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001
+                raise HipLibError(f'device fault in {name} (args {conv})') from e
         else:
             rc = getattr(lib, name)(*conv)
         if rc != 0:

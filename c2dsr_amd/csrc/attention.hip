@@ -287,9 +287,11 @@ __device__ __forceinline__ void tile_of(int t, int& ti, int& tj) {
   tj = t == 2 ? 1 : 0;
 }
 
-// buffer descriptor over rows [0, rows) of a row-major fp32 matrix (row stride `stride` floats)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base, int rows, long stride) {
-  const int bytes = __builtin_amdgcn_readfirstlane(rows * (int)stride * 4);
+// buffer descriptor over rows [0, rows) x columns [0, width) of a row-major fp32 matrix (row stride
+// `stride` floats): the range ends with the last row's `width` columns, so a load past the head of
+// the last row (the end of qkv for the last sequence) reads 0 instead of running off the buffer.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* base, int rows, long stride, int width) {
+  const int bytes = __builtin_amdgcn_readfirstlane(rows > 0 ? ((rows - 1) * (int)stride + width) * 4 : 0);
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
 }
 __device__ __forceinline__ float4 ld_b128(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
@@ -314,8 +316,8 @@ __device__ __forceinline__ void scores_fast(const float* __restrict__ X, long xs
     const int CS = (dh + 7) >> 3;  // c-steps of 8 columns
     const int cb = kp * CS / F::KS, ce = (kp + 1) * CS / F::KS;
     // buffer loads: rows past L (X) or jmax (Y) fall outside the descriptor and read 0
-    const auto xsrc = rows_rsrc(X, L, xs);
-    const auto ysrc = rows_rsrc(Y, jmax, ys);
+    const auto xsrc = rows_rsrc(X, L, xs, dh);
+    const auto ysrc = rows_rsrc(Y, jmax, ys, dh);
     const int xo = ((ti * 32 + r) * (int)xs + 4 * hi) * 4;
     const int yo = ((tj * 32 + r) * (int)ys + 4 * hi) * 4;
     const int cmax = (dh - 4 * hi - 4) >> 3;  // last c-step whose columns are inside the head
@@ -324,8 +326,10 @@ __device__ __forceinline__ void scores_fast(const float* __restrict__ X, long xs
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         const bool cok = c0 + c < ce && c0 + c <= cmax;
-        const float4 xv_ = ld_b128(xsrc, xo + 32 * c, 32 * c0);
-        const float4 yv_ = ld_b128(ysrc, yo + 32 * c, 32 * c0);
+        // the whole offset in voffset: the descriptor's range check does not cover soffset, so a
+        // scalar part could carry a load of the last sequence past the end of the buffer
+        const float4 xv_ = ld_b128(xsrc, xo + 32 * (c0 + c), 0);
+        const float4 yv_ = ld_b128(ysrc, yo + 32 * (c0 + c), 0);
         xv[c] = cok ? xv_ : make_float4(0.f, 0.f, 0.f, 0.f);
         yv[c] = cok ? yv_ : make_float4(0.f, 0.f, 0.f, 0.f);
       }
@@ -380,11 +384,11 @@ __device__ __forceinline__ void pv_fast(const float* As, const float* __restrict
     const int c = ct * 32 + r;
     const bool cok = c < dh;
     float bv[KMAX];
-    const auto ysrc = rows_rsrc(Y, kend, ys);  // rows >= kend read 0
+    const auto ysrc = rows_rsrc(Y, kend, ys, dh);  // rows >= kend read 0
     const int yo = (hi * (int)ys + c) * 4;
 #pragma unroll
     for (int ks = 0; ks < KMAX; ++ks) {
-      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ysrc, yo, 8 * ks * (int)ys, 0));
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ysrc, yo + 8 * ks * (int)ys, 0, 0));
       bv[ks] = cok ? v : 0.f;
     }
     f32x16 acc[F::NT];

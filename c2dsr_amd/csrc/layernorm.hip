@@ -11,7 +11,8 @@ namespace {
 
 constexpr int MAXC = 4;  // float4 chunks per lane → d <= 16*LPR
 
-template <int LPR>
+// NC = float4 chunks per lane (a compile-time count, so the row lives in exactly NC float4s)
+template <int LPR, int NC>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                          int rows, int d, c2::Drop drop, int64_t idx_base,
                                                          const float* __restrict__ gw, const float* __restrict__ gb,
@@ -21,11 +22,12 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
   const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
   const long r = (long)blockIdx.x * GROUPS + g;
   if (r >= rows) return;
-  float4 x[MAXC];
+  float4 x[NC];
   float s = 0.f;
 #pragma unroll
-  for (int q = 0; q < MAXC; ++q) {
+  for (int q = 0; q < NC; ++q) {
     const int c = (lane + q * LPR) * 4;
+    x[q] = c2::f4(0.f);
     if (c < d) {
       float4 v = c2::f4(0.f);
       if (a) v = *(const float4*)(a + r * d + c);
@@ -45,7 +47,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
   const float mean = c2::group_sum<LPR>(s) / d;
   float ss = 0.f;
 #pragma unroll
-  for (int q = 0; q < MAXC; ++q) {
+  for (int q = 0; q < NC; ++q) {
     const int c = (lane + q * LPR) * 4;
     if (c < d) {
       const float4 t = x[q] + c2::f4(-mean);
@@ -55,7 +57,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
   const float var = c2::group_sum<LPR>(ss) / d;
   const float rstd = 1.0f / sqrtf(var + eps);
 #pragma unroll
-  for (int q = 0; q < MAXC; ++q) {
+  for (int q = 0; q < NC; ++q) {
     const int c = (lane + q * LPR) * 4;
     if (c < d) {
       const float4 w4 = *(const float4*)(gw + c), b4 = *(const float4*)(gb + c);
@@ -74,7 +76,8 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
 }
 
 // backward; grid-stride over rows with a fixed grid so dgamma/dbeta partials are per block.
-template <int LPR>
+// Each lane group works on RB rows per step (all their loads issued before the reductions).
+template <int LPR, int NC>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const float* __restrict__ gw,
                                                      const float* __restrict__ dy, int rows, int d,
@@ -82,57 +85,78 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
                                                      float* __restrict__ db_out, c2::Drop drop, int64_t idx_base,
                                                      float* __restrict__ part) {
   constexpr int GROUPS = 256 / LPR;
+  constexpr int RB = 2;
   const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
-  float4 pg[MAXC], pb[MAXC];
+  float4 pg[NC], pb[NC], w4[NC];
 #pragma unroll
-  for (int q = 0; q < MAXC; ++q) pg[q] = pb[q] = c2::f4(0.f);
-  for (long r = (long)blockIdx.x * GROUPS + g; r < rows; r += (long)gridDim.x * GROUPS) {
-    const float mean = mean_in[r], rstd = rstd_in[r];
-    float4 xh[MAXC], gg[MAXC];
-    float s1 = 0.f, s2 = 0.f;
+  for (int q = 0; q < NC; ++q) {
+    pg[q] = pb[q] = c2::f4(0.f);
+    const int c = (lane + q * LPR) * 4;
+    w4[q] = c < d ? *(const float4*)(gw + c) : c2::f4(0.f);
+  }
+  const long stride = (long)gridDim.x * GROUPS;
+  for (long r0 = (long)blockIdx.x * GROUPS + g; r0 < rows; r0 += RB * stride) {
+    float4 xv[RB][NC], dv[RB][NC];
+    float mean[RB], rstd[RB];
 #pragma unroll
-    for (int q = 0; q < MAXC; ++q) {
-      const int c = (lane + q * LPR) * 4;
-      if (c < d) {
-        const float4 xv = *(const float4*)(x + r * d + c);
-        const float4 dv = *(const float4*)(dy + r * d + c);
-        const float4 w4 = *(const float4*)(gw + c);
-        xh[q] = make_float4((xv.x - mean) * rstd, (xv.y - mean) * rstd, (xv.z - mean) * rstd, (xv.w - mean) * rstd);
-        gg[q] = dv * w4;
-        s1 += gg[q].x + gg[q].y + gg[q].z + gg[q].w;
-        s2 += gg[q].x * xh[q].x + gg[q].y * xh[q].y + gg[q].z * xh[q].z + gg[q].w * xh[q].w;
-        pg[q] = pg[q] + dv * xh[q];
-        pb[q] = pb[q] + dv;
+    for (int k = 0; k < RB; ++k) {
+      const long r = r0 + k * stride;
+      const bool ok = r < rows;
+      mean[k] = ok ? mean_in[r] : 0.f;
+      rstd[k] = ok ? rstd_in[r] : 0.f;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int c = (lane + q * LPR) * 4;
+        const bool in = ok && c < d;
+        xv[k][q] = in ? *(const float4*)(x + r * d + c) : c2::f4(0.f);
+        dv[k][q] = in ? *(const float4*)(dy + r * d + c) : c2::f4(0.f);
       }
     }
-    const float m1 = c2::group_sum<LPR>(s1) / d, m2 = c2::group_sum<LPR>(s2) / d;
 #pragma unroll
-    for (int q = 0; q < MAXC; ++q) {
-      const int c = (lane + q * LPR) * 4;
-      if (c < d) {
-        float4 o;
-        o.x = rstd * (gg[q].x - m1 - xh[q].x * m2);
-        o.y = rstd * (gg[q].y - m1 - xh[q].y * m2);
-        o.z = rstd * (gg[q].z - m1 - xh[q].z * m2);
-        o.w = rstd * (gg[q].w - m1 - xh[q].w * m2);
-        if (dx) {
-          float4 prev = dx_accumulate ? *(const float4*)(dx + r * d + c) : c2::f4(0.f);
-          *(float4*)(dx + r * d + c) = prev + o;
-        }
-        if (db_out) {
-          if (drop.active()) {
-            const uint64_t bi = (uint64_t)(idx_base + r) * d + c;
-            o = o * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+    for (int k = 0; k < RB; ++k) {
+      const long r = r0 + k * stride;
+      if (r >= rows) break;  // uniform over the group
+      float4 xh[NC], gg[NC];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        xh[q] = make_float4((xv[k][q].x - mean[k]) * rstd[k], (xv[k][q].y - mean[k]) * rstd[k],
+                            (xv[k][q].z - mean[k]) * rstd[k], (xv[k][q].w - mean[k]) * rstd[k]);
+        gg[q] = dv[k][q] * w4[q];
+        s1 += gg[q].x + gg[q].y + gg[q].z + gg[q].w;
+        s2 += gg[q].x * xh[q].x + gg[q].y * xh[q].y + gg[q].z * xh[q].z + gg[q].w * xh[q].w;
+        pg[q] = pg[q] + dv[k][q] * xh[q];
+        pb[q] = pb[q] + dv[k][q];
+      }
+      const float m1 = c2::group_sum<LPR>(s1) / d, m2 = c2::group_sum<LPR>(s2) / d;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int c = (lane + q * LPR) * 4;
+        if (c < d) {
+          float4 o;
+          o.x = rstd[k] * (gg[q].x - m1 - xh[q].x * m2);
+          o.y = rstd[k] * (gg[q].y - m1 - xh[q].y * m2);
+          o.z = rstd[k] * (gg[q].z - m1 - xh[q].z * m2);
+          o.w = rstd[k] * (gg[q].w - m1 - xh[q].w * m2);
+          if (dx) {
+            float4 prev = dx_accumulate ? *(const float4*)(dx + r * d + c) : c2::f4(0.f);
+            *(float4*)(dx + r * d + c) = prev + o;
           }
-          *(float4*)(db_out + r * d + c) = o;
+          if (db_out) {
+            if (drop.active()) {
+              const uint64_t bi = (uint64_t)(idx_base + r) * d + c;
+              o = o * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+            }
+            *(float4*)(db_out + r * d + c) = o;
+          }
         }
       }
     }
   }
   // block reduce of the per-group partials → part[block][2][d]
   __shared__ float red[256 * 4];
-  for (int q = 0; q < MAXC; ++q) {
-    if (q * LPR * 4 >= d) break;  // uniform within a block
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
     const int c = (lane + q * LPR) * 4;
     for (int which = 0; which < 2; ++which) {
       const float4 v = which ? pb[q] : pg[q];
@@ -158,7 +182,22 @@ __global__ __launch_bounds__(1024) void reduce_parts_kernel(const float* __restr
   float s = 0.f;
   if (c < 2 * d) {
     const int which = c / d, cc = c % d;
-    for (int b = q; b < nblk; b += 16) s += part[((long)b * 2 + which) * d + cc];
+    const float* pp = part + (long)which * d + cc;
+    const long st = 2l * d;
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f, s5 = 0.f, s6 = 0.f, s7 = 0.f;
+    int b = q;
+    for (; b + 7 * 16 < nblk; b += 8 * 16) {  // eight independent loads in flight per lane
+      s += pp[b * st];
+      s1 += pp[(b + 16) * st];
+      s2 += pp[(b + 32) * st];
+      s3 += pp[(b + 48) * st];
+      s4 += pp[(b + 64) * st];
+      s5 += pp[(b + 80) * st];
+      s6 += pp[(b + 96) * st];
+      s7 += pp[(b + 112) * st];
+    }
+    for (; b < nblk; b += 16) s += pp[b * st];
+    s = ((s + s1) + (s2 + s3)) + ((s4 + s5) + (s6 + s7));
   }
   red[q][cl] = s;
   __syncthreads();
@@ -215,14 +254,22 @@ C2_API int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uin
   hipStream_t s = (hipStream_t)stream;
   const int lpr = lpr_for(d);
   dim3 grid(c2::ceil_div(rows, 256 / lpr));
-#define C2_LN(L) add_ln_fwd_kernel<L><<<grid, 256, 0, s>>>(a, b, rows, d, dr, idx_base, w, bias, eps, xsave, y, mean, rstd)
-  switch (lpr) {
-    case 64: C2_LN(64); break;
-    case 32: C2_LN(32); break;
-    case 16: C2_LN(16); break;
-    case 8: C2_LN(8); break;
-    default: C2_LN(4); break;
+#define C2_LN(L, NC) add_ln_fwd_kernel<L, NC><<<grid, 256, 0, s>>>(a, b, rows, d, dr, idx_base, w, bias, eps, xsave, y, mean, rstd)
+#define C2_LNC(L)                                   \
+  switch (c2::ceil_div(d, 4 * L)) {                 \
+    case 1: C2_LN(L, 1); break;                     \
+    case 2: C2_LN(L, 2); break;                     \
+    case 3: C2_LN(L, 3); break;                     \
+    default: C2_LN(L, 4); break;                    \
   }
+  switch (lpr) {
+    case 64: C2_LNC(64); break;
+    case 32: C2_LNC(32); break;
+    case 16: C2_LNC(16); break;
+    case 8: C2_LNC(8); break;
+    default: C2_LNC(4); break;
+  }
+#undef C2_LNC
 #undef C2_LN
   C2_CHECK_LAUNCH();
   return 0;
@@ -242,15 +289,23 @@ C2_API int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, co
   int nblk = c2::ceil_div(rows, groups);
   if (nblk > LN_BWD_BLOCKS) nblk = LN_BWD_BLOCKS;
   float* part = (float*)workspace;
-#define C2_LNB(L) \
-  ln_bwd_kernel<L><<<nblk, 256, 0, s>>>(x, mean, rstd, w, dy, rows, d, dx, dx_accumulate, db_out, dr, idx_base, part)
-  switch (lpr) {
-    case 64: C2_LNB(64); break;
-    case 32: C2_LNB(32); break;
-    case 16: C2_LNB(16); break;
-    case 8: C2_LNB(8); break;
-    default: C2_LNB(4); break;
+#define C2_LNB(L, NC) \
+  ln_bwd_kernel<L, NC><<<nblk, 256, 0, s>>>(x, mean, rstd, w, dy, rows, d, dx, dx_accumulate, db_out, dr, idx_base, part)
+#define C2_LNBC(L)                                  \
+  switch (c2::ceil_div(d, 4 * L)) {                 \
+    case 1: C2_LNB(L, 1); break;                    \
+    case 2: C2_LNB(L, 2); break;                    \
+    case 3: C2_LNB(L, 3); break;                    \
+    default: C2_LNB(L, 4); break;                   \
   }
+  switch (lpr) {
+    case 64: C2_LNBC(64); break;
+    case 32: C2_LNBC(32); break;
+    case 16: C2_LNBC(16); break;
+    case 8: C2_LNBC(8); break;
+    default: C2_LNBC(4); break;
+  }
+#undef C2_LNBC
 #undef C2_LNB
   if (dgw || dgb) reduce_parts_kernel<<<c2::ceil_div(2 * d, 64), 1024, 0, s>>>(part, nblk, d, dgw, dgb);
   C2_CHECK_LAUNCH();

@@ -19,7 +19,7 @@ import torch
 from torch.autograd import Function
 
 from ._lib import lib, stream
-from .ops import BF16, FP32, _grad_target, colsum, gemm
+from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm
 
 
 _NCU = None
@@ -128,7 +128,9 @@ class LossHeadFn(Function):
                 lse2 = torch.empty(M_pad, **f32)
                 lib('c2dsr_ce_fused_fwd', Hb, Wb, bias2, M2, n, d, ns, pm, ps, padlogit, tcat, Hcat, W, bias, lse,
                     lse2, rows, s)
-                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padlogit, lse2, bias2), lse, rows, W, bias, n))
+                # target sort for the one-hot part of dW/db, on the side stream under the rest of the step
+                tplan = IndexPlan(tcat, n + 1) if any(ctx.needs_input_grad[:5]) and W.requires_grad else None
+                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padlogit, lse2, bias2, tplan), lse, rows, W, bias, n))
             else:
                 ld = n + 1
                 logits = torch.empty(2 * BR, ld, **f32)
@@ -176,7 +178,7 @@ class LossHeadFn(Function):
             dHpad = torch.zeros(M2, d, **f32)
             gW, gb = _grad_target(W), _grad_target(bias)
             if ctx.fused:
-                Hb, Wb, padlogit, lse2, bias2 = logits
+                Hb, Wb, padlogit, lse2, bias2, tplan = logits
                 M_pad = lse2.shape[0]
                 rw = torch.empty(M_pad, **f32)
                 t32 = torch.empty(M_pad, device=dev, dtype=torch.int32)
@@ -198,7 +200,11 @@ class LossHeadFn(Function):
                 if gb is not None:
                     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
                 del dWp, dbp
-                if gW is not None or gb is not None:
+                if (gW is not None or gb is not None) and tplan is not None:
+                    wsb = int(lib.raw('c2dsr_ce_onehot_planned_workspace')(M2, n, d))
+                    ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+                    lib('c2dsr_ce_onehot_dw_planned', tplan.get(), M2, n, Hcat, d, rw, gW, gb, ws, wsb, s)
+                elif gW is not None or gb is not None:
                     wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M2, n, d))
                     ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
                     lib('c2dsr_ce_onehot_dw', tcat, M2, n, Hcat, d, rw, gW, gb, ws, wsb, s)

@@ -64,6 +64,7 @@ class StepState:
         self.row_offset = 0   # global batch-row offset of this rank (data parallel)
         self.next_share_pass = DK.PASS_NEG0
         self.grad_hook = None  # c2dsr_amd.dp.GradBuckets while a data-parallel backward runs
+        self.plans = {}  # (step, data_ptr, numel, n_keys) -> ops.IndexPlan (sorted on the side stream)
 
     def keys(self, site):
         return DK.keys(self.seed, self.step, site)

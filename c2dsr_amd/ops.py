@@ -10,7 +10,7 @@ from __future__ import annotations
 import torch
 from torch.autograd import Function
 
-from ._lib import lib, stream, require_device
+from ._lib import HipLibError, lib, stream, require_device
 from .dp import notify_lookup, notify_table
 
 FP32, BF16 = 0, 1
@@ -222,6 +222,108 @@ class GCNFn(Function):
         return (None if direct else gE), None, None, None, None, None, None
 
 
+# ----------------------------------------------------------------------------- index plans
+_side_streams = {}
+_PLAN_SIDE = __import__('os').environ.get('C2DSR_PLAN_SIDE', '1') == '1'
+PLAN_SRC = {}  # plan buffer data_ptr -> data_ptr of the index tensor it sorts (roofline accounting)
+
+
+def side_stream(device):
+    """The stream the index plans are sorted on (one per device), concurrent with the forward."""
+    key = torch.device(device).index
+    if key not in _side_streams:
+        _side_streams[key] = torch.cuda.Stream(device=device)
+    return _side_streams[key]
+
+
+class IndexPlan:
+    """c2dsr_index_plan of one index tensor (stable radix sort into (key, row) order), launched on the
+    side stream as soon as the forward sees the indices, so the sort runs under the forward kernels;
+    ``get()`` orders the current stream after it and returns the plan buffer."""
+
+    def __init__(self, idx, n_keys):
+        n = idx.numel()
+        nb = int(lib.raw('c2dsr_index_plan_bytes')(n))
+        self.buf = torch.empty(nb, dtype=torch.uint8, device=idx.device)
+        PLAN_SRC[self.buf.data_ptr()] = idx.data_ptr()
+        side = side_stream(idx.device) if _PLAN_SIDE else torch.cuda.current_stream(idx.device)
+        side.wait_stream(torch.cuda.current_stream(idx.device))  # idx and buf are ready
+        lib('c2dsr_index_plan', idx, n, int(n_keys), self.buf, nb, side.cuda_stream)
+        if _CHECK_PLANS:
+            self.idx, self.n_keys = idx, int(n_keys)
+        self.buf.record_stream(side)
+        self.ev = torch.cuda.Event()
+        self.ev.record(side)
+
+    def get(self):
+        torch.cuda.current_stream(self.buf.device).wait_event(self.ev)
+        if _CHECK_PLANS:
+            _check_plan(self.buf, self.idx, self.n_keys)
+        return self.buf
+
+
+_CHECK_PLANS = __import__('os').environ.get('C2DSR_CHECK_PLANS', '0') == '1'
+_CHECK_ERR = __import__('os').environ.get('C2DSR_CHECK_ERR', '0') == '1'  # error word only (no sync before use)
+
+
+def _check_err(ws, off, name):
+    err = int(ws[off:off + 4].view(torch.int32).item())
+    if err:
+        raise HipLibError(f'{name}: inconsistent plan skipped on the device (error word {err:#x})')
+
+
+def _check_plan(buf, idx, n_keys, seg_ch=32):
+    """Debug (C2DSR_CHECK_PLANS=1): the plan against a host restatement (keys, rows, piece descriptors,
+    splits) before any kernel consumes it."""
+    import numpy as np
+    torch.cuda.synchronize()
+    b = buf.cpu().numpy()
+    x = idx.reshape(-1).cpu().numpy().astype(np.int64)
+    n = x.size
+    a = lambda v: (v + 255) // 256 * 256  # noqa: E731
+    if n and (x.min() < 0 or x.max() >= n_keys):
+        raise HipLibError(f'index plan: keys outside [0, {n_keys}): {x.min()}..{x.max()}')
+    order = np.argsort(x, kind='stable')
+    K = x[order]
+    o_v = a(4 * n); o_st = o_v + a(4 * n); o_sp = o_st + a(4 * (n + 2)); o_ct = o_sp + a(16 * (n // seg_ch + 1))
+    o_ds = o_ct + a(16)
+    cnt = b[o_ct:o_ct + 16].view(np.int32)
+    starts = [i for i in range(n) if i == 0 or i % seg_ch == 0 or K[i] != K[i - 1]]
+    errs = []
+    if not np.array_equal(b[:4 * n].view(np.uint32), K.astype(np.uint32)):
+        errs.append('keys')
+    if not np.array_equal(b[o_v:o_v + 4 * n].view(np.uint32), order.astype(np.uint32)):
+        errs.append('rows')
+    if int(cnt[0]) != len(starts):
+        errs.append(f'pieces {int(cnt[0])} != {len(starts)}')
+    else:
+        ends = starts[1:] + [n]
+        ref = []
+        for s_, e_ in zip(starts, ends):
+            hd = s_ % seg_ch == 0 and s_ > 0 and K[s_ - 1] == K[s_]
+            tl = e_ % seg_ch == 0 and e_ < n and K[e_] == K[s_]
+            ref.append((s_, e_, K[s_], 1 if hd else (2 if tl else 0)))
+        got = b[o_ds:o_ds + 16 * len(ref)].view(np.int32).reshape(-1, 4)
+        if not np.array_equal(got, np.array(ref, dtype=np.int32).reshape(-1, 4)):
+            errs.append('desc')
+    if errs:
+        raise HipLibError(f'index plan mismatch (n={n}, n_keys={n_keys}): {errs}')
+
+
+def index_plan(state, idx, n_keys):
+    """Plan of ``idx`` cached per training step on the StepState (pos tensors are shared by passes)."""
+    cache = getattr(state, 'plans', None) if state is not None else None
+    if cache is None:
+        return IndexPlan(idx, n_keys)
+    key = (state.step, idx.data_ptr(), idx.numel(), int(n_keys))
+    pl = cache.get(key)
+    if pl is None:
+        if cache and next(iter(cache))[0] != state.step:
+            cache.clear()
+        pl = cache[key] = IndexPlan(idx, n_keys)
+    return pl
+
+
 # ----------------------------------------------------------------------------- embedding fuse (K2)
 class EmbedFn(Function):
     """x = drop((H[seq] + E[seq])·√d + P[pos])  (models/C2DSR.py:65-71 + encoders.py:30-31)."""
@@ -237,6 +339,11 @@ class EmbedFn(Function):
         ctx.save_for_backward(seq, pos)
         ctx.scale, ctx.p, ctx.keys, ctx.row_base, ctx.sink, ctx.n_items = scale, p, keys, row_base, sink, E.shape[0]
         ctx.P = P
+        ctx.plans = None
+        if any(ctx.needs_input_grad[:3]) and (P.requires_grad or sink is not None):  # forward runs under no_grad
+            state = sink.state if sink is not None else None
+            ctx.plans = (index_plan(state, seq, E.shape[0]) if sink is not None else None,
+                         index_plan(state, pos, P.shape[0]) if P.requires_grad else None)
         return x
 
     @staticmethod
@@ -252,10 +359,22 @@ class EmbedFn(Function):
         if gP is None and ctx.needs_input_grad[2]:
             gP_ret = torch.zeros_like(ctx.P)
             gP = gP_ret
-        ws_bytes = lib.raw('c2dsr_embed_bwd_workspace')(n, d)
-        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
-        lib('c2dsr_embed_bwd', seq, pos, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.row_base) * L,
-            float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes, stream())
+        if ctx.plans is not None and (G is None or ctx.plans[0] is not None) and (gP is None or ctx.plans[1] is not None):
+            sp = ctx.plans[0].get() if G is not None else None
+            pp = ctx.plans[1].get() if gP is not None else None
+            ws_bytes = lib.raw('c2dsr_embed_bwd_planned_workspace')(n, d)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
+            lib('c2dsr_embed_bwd_planned', sp, pp, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p),
+                int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes,
+                stream())
+            if _CHECK_PLANS or _CHECK_ERR:
+                _check_err(ws, int(lib.raw('c2dsr_seg_err_offset')(n, d)), 'c2dsr_embed_bwd_planned')
+        else:
+            ws_bytes = lib.raw('c2dsr_embed_bwd_workspace')(n, d)
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
+            lib('c2dsr_embed_bwd', seq, pos, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.row_base) * L,
+                float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes, stream())
+        ctx.plans = None
         if ctx.sink is not None:
             notify_lookup(ctx.sink.state)
         tok_grad = torch.zeros((), device=gx.device)

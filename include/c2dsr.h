@@ -45,6 +45,20 @@ int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, c
                     const float* Xin, const float* P, float scale, uint32_t k0, uint32_t k1, float p,
                     int64_t idx_base, float* X, void* stream);
 size_t c2dsr_embed_bwd_workspace(int n_rows, int d);
+/* Sort plan of an index array (stable LSD radix sort; depends on the indices only, so it is built
+ * on a side stream under the forward pass): plan = [keys u32 n | rows u32 n | scratch], keys
+ * ascending, rows ascending within equal keys.  Replaces the sort inside embedding_dense_backward
+ * (the deterministic path of F.embedding's backward, models/C2DSR.py:65). */
+size_t c2dsr_index_plan_bytes(int n);
+int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, size_t plan_bytes, void* stream);
+/* c2dsr_embed_bwd on prebuilt plans of seq / pos (seq_plan needed iff G, pos_plan iff gP).  A plan
+ * whose pieces fall outside [0, n_rows) entries or [0, n_items) / [0, n_pos) rows is not followed:
+ * the int at workspace + c2dsr_seg_err_offset(n_rows, d) is then nonzero (debug check). */
+size_t c2dsr_embed_bwd_planned_workspace(int n_rows, int d);
+size_t c2dsr_seg_err_offset(int n_rows, int d);
+int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
+                            uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items,
+                            float* gP, int n_pos, float* gXin, void* workspace, size_t ws_bytes, void* stream);
 /* Deterministic (radix-sort + ordered segment sum) backward of the above
  * (replaces embedding_dense_backward):  G[seq[r]] += scale·drop(gX[r]);
  * gP[pos[r]] += drop(gX[r]);  gXin[r] = drop(gX[r]).  Null outputs are skipped. */
@@ -146,6 +160,10 @@ int c2dsr_ce_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M,
  * (t_r = n is the ignored pad target); rows radix-sorted by target, each run summed in row order
  * (deterministic).  H fp32 [M][D]; gW / gb may be null. */
 size_t c2dsr_ce_onehot_workspace(int M, int n, int D);
+/* the same on a prebuilt target plan (c2dsr_index_plan of tgt, n_keys = n + 1) */
+size_t c2dsr_ce_onehot_planned_workspace(int M, int n, int D);
+int c2dsr_ce_onehot_dw_planned(const void* plan, int M, int n, const float* H, int D, const float* rw, float* gW,
+                               float* gb, void* workspace, size_t ws_bytes, void* stream);
 int c2dsr_ce_onehot_dw(const int64_t* tgt, int M, int n, const float* H, int D, const float* rw, float* gW, float* gb,
                        void* workspace, size_t ws_bytes, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */

@@ -133,6 +133,33 @@ def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
     Pr = torch.zeros(L, d, dtype=torch.float64).index_add_(0, torch.from_numpy(pos), g.double())
     assert rel(outs[0][0], Gr) < 1e-5 and rel(outs[0][1], Pr) < 1e-5
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])  # bitwise reproducible
+    # prebuilt sort plans (side-stream path of ops.EmbedFn): same segment sums, bit for bit
+    from c2dsr_amd.ops import IndexPlan
+    sp, pp = IndexPlan(sd, n_items), IndexPlan(pd, L)
+    G = torch.full((n_items, d), 0.0, device=DEV)
+    gP = torch.zeros(L, d, device=DEV)
+    gXin = torch.empty(n_rows, d, device=DEV)
+    ws_b = lib.raw('c2dsr_embed_bwd_planned_workspace')(n_rows, d)
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=DEV)
+    lib('c2dsr_embed_bwd_planned', sp.get(), pp.get(), n_rows, d, gX.to(DEV), keys[0], keys[1], p, 77, scale, G,
+        n_items, gP, L, gXin, ws, ws_b, stream())
+    off = lib.raw('c2dsr_seg_err_offset')(n_rows, d)
+    assert int(ws[off:off + 4].view(torch.int32).item()) == 0
+    # a plan of other indices (keys past the output rows) is skipped and flagged, never followed
+    bad = IndexPlan(torch.full((n_rows,), n_items + 5, dtype=torch.int64, device=DEV), n_items + 6)
+    G2 = torch.zeros(n_items, d, device=DEV)
+    lib('c2dsr_embed_bwd_planned', bad.get(), None, n_rows, d, gX.to(DEV), keys[0], keys[1], p, 77, scale, G2,
+        n_items, None, L, None, ws, ws_b, stream())
+    assert int(ws[off:off + 4].view(torch.int32).item()) != 0 and float(G2.abs().sum()) == 0.0
+    assert torch.equal(G.cpu(), outs[0][0]) and torch.equal(gP.cpu(), outs[0][1])
+    assert rel(gXin, gX * mk) < 1e-6
+    # the plan itself: keys ascending, rows ascending within a key (stable)
+    pl = sp.get().cpu()
+    nb = (n_rows * 4 + 255) // 256 * 256
+    kk = pl[:n_rows * 4].view(torch.int32).numpy()
+    vv = pl[nb:nb + n_rows * 4].view(torch.int32).numpy()
+    order = np.lexsort((np.arange(n_rows), seq))
+    assert np.array_equal(kk, seq[order]) and np.array_equal(vv, order)
 
 
 @pytest.mark.parametrize('L,d,H,p', [(8, 16, 1, 0.0), (8, 16, 2, 0.0), (50, 256, 1, 0.2), (30, 64, 2, 0.1),
@@ -312,9 +339,17 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M, n, D))
     ws = torch.empty(wsb, device=DEV, dtype=torch.uint8)
+    gW0, gb0 = gW.clone(), gb.clone()
     lib('c2dsr_ce_onehot_dw', d(t), M, n, d(H), D, rw, gW, gb, ws, wsb, s)
     assert rel(gW - 1, dl[:, :n].T @ H.double()) < 1e-2
     assert rel(gb - 1, dl[:, :n].sum(0)) < 1e-2
+    # the same on a prebuilt target plan: bit for bit
+    from c2dsr_amd.ops import IndexPlan
+    tp = IndexPlan(d(t), n + 1)
+    wsb = int(lib.raw('c2dsr_ce_onehot_planned_workspace')(M, n, D))
+    ws = torch.empty(wsb, device=DEV, dtype=torch.uint8)
+    lib('c2dsr_ce_onehot_dw_planned', tp.get(), M, n, d(H), D, rw, gW0, gb0, ws, wsb, s)
+    assert torch.equal(gW0, gW) and torch.equal(gb0, gb)
 
 
 def _bf(x):
