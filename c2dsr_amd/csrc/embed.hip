@@ -151,90 +151,65 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
   }
 }
 
-// ------------------------------------------------------------------ sort plan → work lists
-// The sorted entries are cut into pieces: a piece starts at every run start (key change) and at
-// every SEG_CH boundary, so a piece is a run, or the part of a long run inside one chunk.  One
-// lane group sums one piece: a whole run goes to out[key] (+=), a cut run leaves its piece in the
-// chunk's head/tail slot.  A "split" is a run that continues past the end of its first chunk:
-// out[key] += tail[c] + head[c+1] + ... + head[last], summed in chunk order (deterministic).
-// Building the lists depends on the indices only (part of the plan, off the critical path).
+// ------------------------------------------------------------------ sort plan → split lists
+// The sorted entries are cut into chunks of SEG_CH; one lane group walks one chunk (pass A).  A
+// run wholly inside a chunk goes to out[key] (+=); a run cut by a chunk edge leaves its pieces in
+// the chunks' head/tail slots.  A "split" is a run that continues past the end of its first
+// chunk: out[key] += tail[c] + head[c+1] + ... + head[last], summed in chunk order (pass B).  The
+// split list depends on the indices only, so it is part of the plan (off the critical path).
 constexpr int SEG_CH = 32;
 constexpr int PL_T = 256;         // plan kernels: threads per block
 constexpr int PL_E = 4;           // entries per thread
 constexpr int PL_B = PL_T * PL_E;  // entries per block
 
-__device__ __forceinline__ bool piece_start(const uint32_t* K, int i) {
-  return i == 0 || (i % SEG_CH) == 0 || K[i] != K[i - 1];
-}
 __device__ __forceinline__ bool split_start(const uint32_t* K, int n, int i) {
   if (!(i == 0 || K[i] != K[i - 1])) return false;
   const int ce = (i / SEG_CH + 1) * SEG_CH;
   return ce < n && K[ce] == K[i];
 }
 
-// per block: number of pieces and splits among its PL_B entries → cnt[2·b], cnt[2·b+1]
+// per block: number of splits starting among its PL_B entries → cnt[b]
 __global__ __launch_bounds__(PL_T) void plan_count_kernel(const uint32_t* __restrict__ K, int n,
                                                           uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t red[2][PL_T / 64];
-  uint32_t p = 0, q = 0;
+  __shared__ uint32_t red[PL_T / 64];
+  uint32_t q = 0;
   for (int j = 0; j < PL_E; ++j) {
     const int i = blockIdx.x * PL_B + j * PL_T + threadIdx.x;
-    if (i < n) {
-      p += piece_start(K, i);
-      q += split_start(K, n, i);
-    }
+    if (i < n) q += split_start(K, n, i);
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    p += __shfl_xor(p, o, 64);
-    q += __shfl_xor(q, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = p;
-    red[1][threadIdx.x >> 6] = q;
-  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
   __syncthreads();
-  if (threadIdx.x < 2) {
+  if (threadIdx.x == 0) {
     uint32_t t = 0;
-    for (int w = 0; w < PL_T / 64; ++w) t += red[threadIdx.x][w];
-    cnt[2 * blockIdx.x + threadIdx.x] = t;
+    for (int w = 0; w < PL_T / 64; ++w) t += red[w];
+    cnt[blockIdx.x] = t;
   }
 }
 
-// exclusive scan of the block counts (single workgroup); totals → counts[0..1], starts[total] = n
-__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ cnt, int nb, int n,
-                                                         int* __restrict__ counts, int* __restrict__ starts) {
-  __shared__ uint32_t part[2][1024];
+// exclusive scan of the block counts (single workgroup); total → counts[1]
+__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ cnt, int nb, int* __restrict__ counts) {
+  __shared__ uint32_t part[1024];
   const int t = threadIdx.x;
   const int per = (nb + 1023) / 1024;
   const int lo = min(nb, t * per), hi = min(nb, lo + per);
-  uint32_t s0 = 0, s1 = 0;
-  for (int i = lo; i < hi; ++i) {
-    s0 += cnt[2 * i];
-    s1 += cnt[2 * i + 1];
-  }
-  part[0][t] = s0;
-  part[1][t] = s1;
+  uint32_t s0 = 0;
+  for (int i = lo; i < hi; ++i) s0 += cnt[i];
+  part[t] = s0;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t v0 = t >= o ? part[0][t - o] : 0, v1 = t >= o ? part[1][t - o] : 0;
+    const uint32_t v0 = t >= o ? part[t - o] : 0;
     __syncthreads();
-    part[0][t] += v0;
-    part[1][t] += v1;
+    part[t] += v0;
     __syncthreads();
   }
-  uint32_t r0 = part[0][t] - s0, r1 = part[1][t] - s1;
+  uint32_t r0 = part[t] - s0;
   for (int i = lo; i < hi; ++i) {
-    const uint32_t c0 = cnt[2 * i], c1 = cnt[2 * i + 1];
-    cnt[2 * i] = r0;
-    cnt[2 * i + 1] = r1;
+    const uint32_t c0 = cnt[i];
+    cnt[i] = r0;
     r0 += c0;
-    r1 += c1;
   }
-  if (t == 1023) {
-    counts[0] = (int)part[0][1023];
-    counts[1] = (int)part[1][1023];
-    starts[part[0][1023]] = n;
-  }
+  if (t == 1023) counts[1] = (int)part[1023];
 }
 
 // exclusive block-wide prefix of one u32 per thread (PL_T threads)
@@ -253,27 +228,21 @@ __device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t* red) {
   return base + inc - v;
 }
 
-// writes starts[piece] = first entry, splits[j] = {key, first chunk, chunks spanned, 0}
+// writes splits[j] = {key, first chunk, chunks spanned, 0} in entry order
 __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restrict__ K, int n,
-                                                         const uint32_t* __restrict__ cnt, int* __restrict__ starts,
-                                                         int4* __restrict__ splits) {
+                                                         const uint32_t* __restrict__ cnt, int4* __restrict__ splits) {
   __shared__ uint32_t red[PL_T / 64];
   // thread t owns entries [base + t·PL_E, base + (t+1)·PL_E): contiguous, so the order is kept
   const int i0 = blockIdx.x * PL_B + threadIdx.x * PL_E;
-  uint32_t fp = 0, fs = 0;
+  uint32_t fs = 0;
   for (int j = 0; j < PL_E; ++j) {
     const int i = i0 + j;
-    if (i < n) {
-      fp |= (uint32_t)piece_start(K, i) << j;
-      fs |= (uint32_t)split_start(K, n, i) << j;
-    }
+    if (i < n) fs |= (uint32_t)split_start(K, n, i) << j;
   }
-  uint32_t op = cnt[2 * blockIdx.x] + block_prefix(__popc(fp), red);
-  uint32_t os = cnt[2 * blockIdx.x + 1] + block_prefix(__popc(fs), red);
+  uint32_t os = cnt[blockIdx.x] + block_prefix(__popc(fs), red);
   for (int j = 0; j < PL_E; ++j) {
-    const int i = i0 + j;
-    if (fp >> j & 1) starts[op++] = i;
     if (fs >> j & 1) {
+      const int i = i0 + j;
       const uint32_t key = K[i];
       int lo = i, hi = n;  // first entry with a larger key (keys are sorted)
       while (lo < hi) {
@@ -286,23 +255,9 @@ __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restr
   }
 }
 
-// desc[w] = {first entry, end, key, kind}: kind 0 = whole run (out[key] +=), 1 = head slot of chunk
-// first/SEG_CH, 2 = tail slot of chunk (end-1)/SEG_CH — everything pass A needs in one load.
-__global__ __launch_bounds__(256) void plan_desc_kernel(const uint32_t* __restrict__ K, int n,
-                                                        const int* __restrict__ starts, const int* __restrict__ counts,
-                                                        int4* __restrict__ desc) {
-  const int np = counts[0];
-  for (int w = blockIdx.x * 256 + threadIdx.x; w < np; w += gridDim.x * 256) {
-    const int s = starts[w], e = starts[w + 1];
-    const uint32_t key = K[s];
-    const bool head = (s % SEG_CH) == 0 && s > 0 && K[s - 1] == key;
-    const bool tail = (e % SEG_CH) == 0 && e < n && K[e] == key;
-    desc[w] = make_int4(s, e, (int)key, head ? 1 : (tail ? 2 : 0));
-  }
-}
-
 // ------------------------------------------------------------------ segment sums
-constexpr int SEG_U = 8;  // rows in flight per lane group
+constexpr int SEG_U = 8;   // rows in flight per lane group
+constexpr int SUBP = 128;  // pieces per level-1 block of a split
 
 struct RowSrc {
   const float* gX;
@@ -322,105 +277,245 @@ struct RowSrc {
   }
 };
 
-// pass A: one lane group per piece (grid-stride over the device-side piece count).  The chain per
-// piece is descriptor → row ids → rows (+ the old out row, loaded alongside) → store; rows SEG_U at
-// a time, summed in entry order.
-// A plan that does not describe n entries over n_out output rows (a plan of other indices, or
-// one read before it was complete) is never followed: the offending pieces are skipped and err
-// is set (checked by the host in debug runs), so it cannot turn into a stray access.
+// One segment-sum job: out[key] += Σ src rows of every run of a plan.  Several jobs over plans
+// of the same row width share one launch of each pass (the embedding backward's item and
+// position sums).
+struct SegJob {
+  const uint32_t *K, *V;       // plan: sorted keys, their rows
+  const int4* splits;          // plan: runs that cross a chunk end
+  const int2* subs;            // plan: (split, first piece) of every SUBP-piece sub-range
+  const int* suboff;           // plan: first sub of every split
+  const int* counts;           // plan: [pieces, splits, subs]
+  int* err;                    // plan: error word (debug)
+  int n, n_out, skip_key, nblocks;
+  RowSrc src;
+  float *out, *ph, *pt, *slot2;
+};
+
+// pass A: one lane group per chunk of SEG_CH sorted entries.  The block stages its keys and row
+// ids in LDS (one coalesced load; no dependent index loads in the walk).  Rows are loaded
+// SEG_U at a time and summed in entry order; a run that closes inside the chunk leaves its sum in
+// the slot of its last row, and the read-modify-writes of out[] for all runs closing in the batch
+// are issued together (all loads, then all stores), so short runs do not serialise.  The chunk's
+// first run goes to its head slot when it continues the previous chunk, the last run to the tail
+// slot when it continues into the next (pass B adds those up).  Keys outside [0, n_out) are never
+// followed (err is set; checked by the host in debug runs).
 template <int LPR>
-__global__ __launch_bounds__(256) void seg_piece_kernel(const uint32_t* __restrict__ V, const int4* __restrict__ desc,
-                                                        const int* __restrict__ counts, int n, int n_out, RowSrc src,
-                                                        float* __restrict__ out, float* __restrict__ part_head,
-                                                        float* __restrict__ part_tail, int skip_key,
-                                                        int* __restrict__ err) {
+__global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
   constexpr int GROUPS = 256 / LPR;
-  const int lane = threadIdx.x % LPR;
-  int npieces = counts[0];
-  if (npieces < 0 || npieces > n) {
-    if (threadIdx.x == 0) atomicOr(err, 1);
-    return;
+  constexpr int ENT = GROUPS * SEG_CH;
+  __shared__ uint32_t sk[ENT + 2];  // sk[e + 1] = K[b0 + e]; sk[0], sk[ENT + 1]: the neighbours
+  __shared__ uint32_t sv[ENT];
+  const bool second = (int)blockIdx.x >= j0.nblocks;
+  const SegJob& J = second ? j1 : j0;
+  const int blk = second ? (int)blockIdx.x - j0.nblocks : (int)blockIdx.x;
+  const int n = J.n;
+  const long b0 = (long)blk * ENT;
+  for (int e = threadIdx.x; e < ENT + 2; e += 256) {
+    const long gi = b0 - 1 + e;
+    sk[e] = (gi >= 0 && gi < n) ? J.K[gi] : 0xffffffffu;
   }
+  for (int e = threadIdx.x; e < ENT; e += 256) {
+    const long gi = b0 + e;
+    sv[e] = gi < n ? min(J.V[gi], (uint32_t)(n - 1)) : 0u;
+  }
+  __syncthreads();
+  const int g = threadIdx.x / LPR;
+  const int lane = threadIdx.x % LPR;
+  const long chunk = (long)blk * GROUPS + g;
+  const long start = chunk * SEG_CH;
+  if (start >= n) return;
+  const int cnt = (int)min((long)SEG_CH, n - start);
+  const int o = g * SEG_CH;
+  const bool cont_head = start > 0 && sk[o] == sk[o + 1];
+  const bool cont_tail = start + cnt < n && sk[o + cnt + 1] == sk[o + cnt];
+  const RowSrc& src = J.src;
   const int d = src.d;
-  for (int w = blockIdx.x * GROUPS + threadIdx.x / LPR; w < npieces; w += gridDim.x * GROUPS) {
-    const int4 ds = desc[w];
-    const int s = ds.x, e = ds.y, key = ds.z, kind = ds.w;
-    if (s < 0 || e > n || e <= s || e - s > SEG_CH || key < 0 || key >= n_out) {
-      if (lane == 0) atomicOr(err, 2);
-      continue;
-    }
-    if (key == skip_key) continue;
-    float* dst = kind == 1 ? part_head + (long)(s / SEG_CH) * d
-                           : (kind == 2 ? part_tail + (long)((e - 1) / SEG_CH) * d : out + (long)key * d);
-    for (int c = lane * 4; c < d; c += LPR * 4) {
-      float4 acc = kind == 0 ? *(const float4*)(dst + c) : c2::f4(0.f);
-      for (int q0 = s; q0 < e; q0 += SEG_U) {
-        uint32_t r[SEG_U];
+  for (int c = lane * 4; c < d; c += LPR * 4) {
+    float4 acc = c2::f4(0.f);
+    bool first = true;  // the next run to close is the chunk's first
+    for (int h0 = 0; h0 < cnt; h0 += SEG_U) {
+      float4 x[SEG_U];
 #pragma unroll
-        for (int u = 0; u < SEG_U; ++u) r[u] = q0 + u < e ? min(V[q0 + u], (uint32_t)(n - 1)) : 0u;
-        float4 x[SEG_U];
+      for (int u = 0; u < SEG_U; ++u) x[u] = h0 + u < cnt ? src.load(sv[o + h0 + u], c) : c2::f4(0.f);
+      int kind[SEG_U];  // 0: nothing closes at u, 1: out[key] +=, 2: head slot, 3: tail slot, 4: bad key
 #pragma unroll
-        for (int u = 0; u < SEG_U; ++u) x[u] = q0 + u < e ? src.load(r[u], c) : c2::f4(0.f);
-        float4 t = x[0];
-#pragma unroll
-        for (int u = 1; u < SEG_U; ++u) t = t + x[u];
-        acc = acc + t;
+      for (int u = 0; u < SEG_U; ++u) {
+        const int q = h0 + u;
+        kind[u] = 0;
+        if (q < cnt) {
+          acc = acc + x[u];
+          if (q == cnt - 1 || sk[o + q + 2] != sk[o + q + 1]) {
+            const uint32_t key = sk[o + q + 1];
+            if (first && cont_head)
+              kind[u] = 2;
+            else if (q == cnt - 1 && cont_tail)
+              kind[u] = 3;
+            else if (key >= (uint32_t)J.n_out)
+              kind[u] = 4;
+            else if ((int)key != J.skip_key)
+              kind[u] = 1;
+            x[u] = acc;  // the run's sum, in the slot of its last row
+            acc = c2::f4(0.f);
+            first = false;
+          }
+        }
       }
-      *(float4*)(dst + c) = acc;
+      float4 prev[SEG_U];
+#pragma unroll
+      for (int u = 0; u < SEG_U; ++u)
+        prev[u] = kind[u] == 1 ? *(const float4*)(J.out + (long)sk[o + h0 + u + 1] * d + c) : c2::f4(0.f);
+#pragma unroll
+      for (int u = 0; u < SEG_U; ++u) {
+        if (kind[u] == 1)
+          *(float4*)(J.out + (long)sk[o + h0 + u + 1] * d + c) = prev[u] + x[u];
+        else if (kind[u] == 2)
+          *(float4*)(J.ph + chunk * d + c) = x[u];
+        else if (kind[u] == 3)
+          *(float4*)(J.pt + chunk * d + c) = x[u];
+        else if (kind[u] == 4 && lane == 0)
+          atomicOr(J.err, 2);
+      }
     }
   }
 }
 
-// pass B: one block per split (grid-stride): out[key] += tail[c] + head[c+1..c+np-1]; the pieces are
-// dealt round-robin to the block's lane groups (four loads in flight per group), the group sums are
-// added in group order.
+// the job of a pass-B block (blockIdx.y), field by field (uniform selects; no struct copy)
+struct SplitView {
+  const int4* splits;
+  const int2* subs;
+  const int* suboff;
+  const int* counts;
+  int* err;
+  int n, n_out, skip_key, d;
+  float* out;
+  const float *ph, *pt;
+  float* slot2;
+  __device__ __forceinline__ SplitView(const SegJob& j0, const SegJob& j1, bool y)
+      : splits(y ? j1.splits : j0.splits), subs(y ? j1.subs : j0.subs), suboff(y ? j1.suboff : j0.suboff),
+        counts(y ? j1.counts : j0.counts), err(y ? j1.err : j0.err), n(y ? j1.n : j0.n),
+        n_out(y ? j1.n_out : j0.n_out), skip_key(y ? j1.skip_key : j0.skip_key), d(y ? j1.src.d : j0.src.d),
+        out(y ? j1.out : j0.out), ph(y ? j1.ph : j0.ph), pt(y ? j1.pt : j0.pt), slot2(y ? j1.slot2 : j0.slot2) {}
+  __device__ __forceinline__ int nchunks() const { return (n + SEG_CH - 1) / SEG_CH; }
+  __device__ __forceinline__ int max_sub() const { return nchunks() + 2 + n / (SEG_CH * SUBP); }
+};
+
+// pass B, level 1: one block per sub-range of SUBP pieces of a split (grid-stride over the plan's
+// sub list, blockIdx.y = job): the pieces (tail of the split's first chunk, heads of the following
+// ones) are dealt round-robin to the block's lane groups (eight loads in flight each), the group
+// sums added in group order → slot2[sub].  Level 2: one lane group per split adds its level-1
+// sums in sub order to out[key].  Fixed orders → deterministic; a padding run of thousands of
+// pieces is spread over many blocks.
 template <int LPR>
-__global__ __launch_bounds__(1024) void seg_split_kernel(const int4* __restrict__ splits,
-                                                         const int* __restrict__ counts, int nchunks, int n_out,
-                                                         int d, float* __restrict__ out,
-                                                         const float* __restrict__ part_head,
-                                                         const float* __restrict__ part_tail, int skip_key,
-                                                         int* __restrict__ err) {
+__global__ __launch_bounds__(1024) void seg_split1_kernel(SegJob j0, SegJob j1) {
   constexpr int GROUPS = 1024 / LPR;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [GROUPS][d]
+  const SplitView J(j0, j1, blockIdx.y != 0);
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
-  const int nsplit = counts[1];
-  if (nsplit < 0 || nsplit > nchunks) {
-    if (threadIdx.x == 0) atomicOr(err, 4);
+  const int d = J.d, nchunks = J.nchunks();
+  const int nsub = J.counts[2], nsplit = J.counts[1];
+  if (nsub < 0 || nsub > J.max_sub() || nsplit < 0 || nsplit > nchunks) {
+    if (threadIdx.x == 0) atomicOr(J.err, 4);
     return;
   }
-  for (int j = blockIdx.x; j < nsplit; j += gridDim.x) {
-    const int4 sp = splits[j];
-    const int key = sp.x, chunk = sp.y, np = sp.z;
-    if (key < 0 || key >= n_out || chunk < 0 || np < 2 || chunk + np > nchunks) {  // uniform over the block
-      if (threadIdx.x == 0) atomicOr(err, 8);
+  for (int j = blockIdx.x; j < nsub; j += gridDim.x) {
+    const int2 sb = J.subs[j];  // (split, first piece of this sub-range)
+    const int si = min(max(sb.x, 0), max(nsplit - 1, 0));
+    const int4 sp = J.splits[si];
+    const int chunk = sp.y, np = sp.z;
+    const int q_lo = sb.y, q_hi = min(np, sb.y + SUBP);
+    if (sb.x != si || chunk < 0 || np < 2 || chunk + np > nchunks || q_lo < 0 || q_lo >= q_hi) {  // uniform
+      if (threadIdx.x == 0) atomicOr(J.err, 8);
       continue;
     }
-    if (key == skip_key) continue;  // uniform over the block
-    auto slot = [&](int q) -> const float* {
-      return q == 0 ? part_tail + (long)chunk * d : part_head + (long)(chunk + q) * d;
-    };
+    const float* tail0 = J.pt + (long)chunk * d;
+    const float* head0 = J.ph + (long)chunk * d;
     for (int c = lane * 4; c < d; c += LPR * 4) {
       float4 a[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) a[u] = c2::f4(0.f);
-      int q = g;
-      for (; q + 7 * GROUPS < np; q += 8 * GROUPS) {
+      int q = q_lo + g;
+      for (; q + 7 * GROUPS < q_hi; q += 8 * GROUPS) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a[u] = a[u] + *(const float4*)(slot(q + u * GROUPS) + c);
+        for (int u = 0; u < 8; ++u) {
+          const int qq = q + u * GROUPS;
+          a[u] = a[u] + *(const float4*)((qq == 0 ? tail0 : head0 + (long)qq * d) + c);
+        }
       }
-      for (; q < np; q += GROUPS) a[0] = a[0] + *(const float4*)(slot(q) + c);
+      for (; q < q_hi; q += GROUPS) a[0] = a[0] + *(const float4*)((q == 0 ? tail0 : head0 + (long)q * d) + c);
       *(float4*)(red + g * d + c) = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
     __syncthreads();
     for (int c = threadIdx.x * 4; c < d; c += 1024 * 4) {
       float4 t = *(const float4*)(red + c);
       for (int q = 1; q < GROUPS; ++q) t = t + *(const float4*)(red + q * d + c);
-      float4* o = (float4*)(out + (long)key * d + c);
-      *o = *o + t;
+      *(float4*)(J.slot2 + (long)j * d + c) = t;
     }
     __syncthreads();
+  }
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void seg_split2_kernel(SegJob j0, SegJob j1) {
+  constexpr int GROUPS = 256 / LPR;
+  const SplitView J(j0, j1, blockIdx.y != 0);
+  const int lane = threadIdx.x % LPR;
+  const int d = J.d, nchunks = J.nchunks();
+  const int nsplit = J.counts[1], nsub = J.counts[2];
+  if (nsplit < 0 || nsplit > nchunks || nsub < 0 || nsub > J.max_sub()) {
+    if (threadIdx.x == 0) atomicOr(J.err, 4);
+    return;
+  }
+  for (int j = blockIdx.x * GROUPS + threadIdx.x / LPR; j < nsplit; j += gridDim.x * GROUPS) {
+    const int key = J.splits[j].x;
+    const int b0 = J.suboff[j], b1 = J.suboff[j + 1];
+    if (key < 0 || key >= J.n_out || b0 < 0 || b1 <= b0 || b1 > nsub) {
+      if (lane == 0) atomicOr(J.err, 8);
+      continue;
+    }
+    if (key == J.skip_key) continue;
+    float* o = J.out + (long)key * d;
+    for (int c = lane * 4; c < d; c += LPR * 4) {
+      float4 t = *(const float4*)(o + c);
+      for (int k = b0; k < b1; ++k) t = t + *(const float4*)(J.slot2 + (long)k * d + c);
+      *(float4*)(o + c) = t;
+    }
+  }
+}
+
+// plan: sub-ranges of every split.  One workgroup: per-thread runs of splits, block scan of their
+// sub counts → suboff[nsplit + 1], subs[total] = (split, first piece), counts[2] = total; the
+// error word starts at 0.
+__global__ __launch_bounds__(1024) void plan_subs_kernel(const int4* __restrict__ splits, int* __restrict__ counts,
+                                                         int* __restrict__ suboff, int2* __restrict__ subs,
+                                                         int* __restrict__ err) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int ns = counts[1];
+  const int per = (ns + 1023) / 1024;
+  const int lo = min(ns, t * per), hi = min(ns, lo + per);
+  int sum = 0;
+  for (int i = lo; i < hi; ++i) sum += (splits[i].z + SUBP - 1) / SUBP;
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int i = lo; i < hi; ++i) {
+    suboff[i] = run;
+    const int k = (splits[i].z + SUBP - 1) / SUBP;
+    for (int y = 0; y < k; ++y) subs[run + y] = make_int2(i, y * SUBP);
+    run += k;
+  }
+  if (t == 1023) {
+    suboff[ns] = part[1023];
+    counts[2] = part[1023];
+    *err = 0;
   }
 }
 
@@ -446,17 +541,21 @@ int lpr_for(int d) { return d / 4 >= 64 ? 64 : (d / 4 >= 32 ? 32 : (d / 4 >= 16 
 
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
 
-// A plan: keys[n] (sorted ids) | vals[n] (their rows) | starts[n+2] | splits[n/SEG_CH+1] int4 |
-// counts[4] | desc[n] int4 | scratch (second LSD buffers, digit histograms, plan block counts).
+// A plan: keys[n] (sorted ids) | rows[n] | splits[n/SEG_CH+1] int4 | counts[4] = (-, splits, subs,
+// error word) | suboff[n/SEG_CH+2] | subs[max_subs] int2 | scratch (second
+// LSD buffers, digit histograms, plan block counts).
 struct Plan {
   uint32_t *k0, *v0;
-  int* starts;
   int4* splits;
   int* counts;
-  int4* desc;
+  int* suboff;
+  int2* subs;
   uint32_t *k1, *v1, *hist, *bcnt;
   int nblocks;
 };
+
+// sub-ranges of SUBP pieces over all splits: at most one per split plus one per SUBP chunks
+int max_subs(int n) { return n / SEG_CH + 2 + n / (SEG_CH * SUBP) + 1; }
 
 size_t plan_layout(int n, Plan* p, char* base) {
   const int nblocks = c2::ceil_div(n, RS_TILE);
@@ -469,16 +568,16 @@ size_t plan_layout(int n, Plan* p, char* base) {
   };
   char* k0 = take((size_t)n * 4);
   char* v0 = take((size_t)n * 4);
-  char* st = take((size_t)(n + 2) * 4);
   char* sp = take((size_t)(n / SEG_CH + 1) * 16);
   char* ct = take(16);
-  char* ds = take((size_t)n * 16);
+  char* so = take((size_t)(n / SEG_CH + 2) * 4);
+  char* sb = take((size_t)max_subs(n) * 8);
   char* k1 = take((size_t)n * 4);
   char* v1 = take((size_t)n * 4);
   char* hist = take((size_t)256 * nblocks * 4);
-  char* bc = take((size_t)2 * pb * 4);
+  char* bc = take((size_t)pb * 4);
   if (p)
-    *p = Plan{(uint32_t*)k0, (uint32_t*)v0, (int*)st, (int4*)sp, (int*)ct, (int4*)ds,
+    *p = Plan{(uint32_t*)k0, (uint32_t*)v0, (int4*)sp, (int*)ct, (int*)so, (int2*)sb,
               (uint32_t*)k1, (uint32_t*)v1, (uint32_t*)hist, (uint32_t*)bc, nblocks};
   return off;
 }
@@ -491,7 +590,8 @@ Plan plan_view(const void* base, int n) {
 
 // head/tail partial slots of the segment sums, then the error word
 size_t seg_slot_bytes(int n, int d) { return align256((size_t)c2::ceil_div(n, SEG_CH) * d * 4); }
-size_t seg_ws_bytes(int n, int d) { return 2 * seg_slot_bytes(n, d) + 256; }
+size_t seg_slot2_bytes(int n, int d) { return align256((size_t)max_subs(n) * d * 4); }
+size_t seg_ws_bytes(int n, int d) { return 2 * seg_slot_bytes(n, d) + seg_slot2_bytes(n, d); }
 
 // sort idx[0..n) (values < n_keys) → k0/v0 sorted (key, original row), stable; then the work lists
 int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t s) {
@@ -512,9 +612,9 @@ int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t
   }
   const int pb = c2::ceil_div(n, PL_B);
   plan_count_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt);
-  plan_scan_kernel<<<1, 1024, 0, s>>>(w.bcnt, pb, n, w.counts, w.starts);
-  plan_emit_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt, w.starts, w.splits);
-  plan_desc_kernel<<<std::min(c2::ceil_div(n, 256), 1024), 256, 0, s>>>(w.k0, n, w.starts, w.counts, w.desc);
+  plan_scan_kernel<<<1, 1024, 0, s>>>(w.bcnt, pb, w.counts);
+  plan_emit_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt, w.splits);
+  plan_subs_kernel<<<1, 1024, 0, s>>>(w.splits, w.counts, w.suboff, w.subs, w.counts + 3);
   C2_CHECK_LAUNCH();
   return 0;
 }
@@ -531,33 +631,52 @@ int num_cus() {
 }
 
 template <int LPR>
-void seg_launch(const Plan& p, int n, int n_out, const RowSrc& src, float* out, float* ph, float* pt, int skip_key,
-                int* err, hipStream_t s) {
+void seg_launch(SegJob j0, SegJob j1, int njobs, hipStream_t s) {
   constexpr int GROUPS = 256 / LPR;
-  // pieces <= n; 8 blocks (32 waves) per CU, grid-stride over the device-side count
-  const int grid = std::max(1, std::min(c2::ceil_div(n, GROUPS), 8 * num_cus()));
-  seg_piece_kernel<LPR><<<grid, 256, 0, s>>>(p.v0, p.desc, p.counts, n, n_out, src, out, ph, pt, skip_key, err);
-  if (n > SEG_CH) {
-    const int nchunks = c2::ceil_div(n, SEG_CH);
-    const int gs = std::max(1, std::min(n / SEG_CH, num_cus()));
-    seg_split_kernel<LPR><<<gs, 1024, (size_t)(1024 / LPR) * src.d * 4, s>>>(p.splits, p.counts, nchunks, n_out,
-                                                                             src.d, out, ph, pt, skip_key, err);
+  j0.nblocks = c2::ceil_div(c2::ceil_div(j0.n, SEG_CH), GROUPS);  // one lane group per chunk
+  j1.nblocks = njobs > 1 ? c2::ceil_div(c2::ceil_div(j1.n, SEG_CH), GROUPS) : 0;
+  seg_chunk_kernel<LPR><<<j0.nblocks + j1.nblocks, 256, 0, s>>>(j0, j1);
+  const int nmax = std::max(j0.n, njobs > 1 ? j1.n : 0);
+  if (nmax > SEG_CH) {
+    dim3 g1(std::max(1, std::min(max_subs(nmax), 2 * num_cus())), njobs);
+    seg_split1_kernel<LPR><<<g1, 1024, (size_t)(1024 / LPR) * j0.src.d * 4, s>>>(j0, j1);
+    dim3 g2(std::max(1, std::min(c2::ceil_div(c2::ceil_div(nmax, SEG_CH), GROUPS), 2 * num_cus())), njobs);
+    seg_split2_kernel<LPR><<<g2, 256, 0, s>>>(j0, j1);
   }
 }
 
-// out[key] += Σ src rows of each run of the plan (keys < n_out), partial slots and the error word
-// carved from ws
-void seg_dispatch(const Plan& p, int n, int n_out, const RowSrc& src, float* out, char* ws, int skip_key,
-                  hipStream_t s) {
-  float* ph = (float*)ws;
-  float* pt = (float*)(ws + seg_slot_bytes(n, src.d));
-  int* err = (int*)(ws + 2 * seg_slot_bytes(n, src.d));
-  switch (lpr_for(src.d)) {
-    case 64: seg_launch<64>(p, n, n_out, src, out, ph, pt, skip_key, err, s); break;
-    case 32: seg_launch<32>(p, n, n_out, src, out, ph, pt, skip_key, err, s); break;
-    case 16: seg_launch<16>(p, n, n_out, src, out, ph, pt, skip_key, err, s); break;
-    case 8: seg_launch<8>(p, n, n_out, src, out, ph, pt, skip_key, err, s); break;
-    default: seg_launch<4>(p, n, n_out, src, out, ph, pt, skip_key, err, s); break;
+// out[key] += Σ src rows of each run of the plan (keys < n_out); partial slots from ws
+SegJob seg_job(const Plan& p, int n, int n_out, const RowSrc& src, float* out, char* ws, int skip_key) {
+  SegJob j;
+  j.K = p.k0;
+  j.V = p.v0;
+  j.splits = p.splits;
+  j.subs = p.subs;
+  j.suboff = p.suboff;
+  j.counts = p.counts;
+  j.err = p.counts + 3;
+  j.n = n;
+  j.n_out = n_out;
+  j.skip_key = skip_key;
+  j.nblocks = 0;
+  j.src = src;
+  j.out = out;
+  j.ph = (float*)ws;
+  j.pt = (float*)(ws + seg_slot_bytes(n, src.d));
+  j.slot2 = (float*)(ws + 2 * seg_slot_bytes(n, src.d));
+  return j;
+}
+
+// one or two jobs of the same row width in one launch per pass
+void seg_dispatch(const SegJob& j0, const SegJob* j1, hipStream_t s) {
+  const SegJob& b = j1 ? *j1 : j0;
+  const int nj = j1 ? 2 : 1;
+  switch (lpr_for(j0.src.d)) {
+    case 64: seg_launch<64>(j0, b, nj, s); break;
+    case 32: seg_launch<32>(j0, b, nj, s); break;
+    case 16: seg_launch<16>(j0, b, nj, s); break;
+    case 8: seg_launch<8>(j0, b, nj, s); break;
+    default: seg_launch<4>(j0, b, nj, s); break;
   }
 }
 
@@ -603,30 +722,42 @@ C2_API int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, s
   return build_plan(idx, n, n_keys, p, (hipStream_t)stream);
 }
 
-C2_API size_t c2dsr_embed_bwd_planned_workspace(int n_rows, int d) { return seg_ws_bytes(n_rows, d); }
+// two segment-sum jobs (items, positions) run side by side: two slot regions
+C2_API size_t c2dsr_embed_bwd_planned_workspace(int n_rows, int d) { return 2 * seg_ws_bytes(n_rows, d); }
+
+// offset of a plan's device error word (nonzero once a segment sum met an inconsistent plan)
+C2_API size_t c2dsr_plan_err_offset(int n) {
+  Plan p;
+  char* const base = reinterpret_cast<char*>(uintptr_t{4096});  // any non-null base: offsets only
+  plan_layout(n, &p, base);
+  return (size_t)(reinterpret_cast<char*>(p.counts + 3) - base);
+}
 
 // gX: grad w.r.t. the dropout output X [n_rows, d]; seq_plan / pos_plan from c2dsr_index_plan.
 //   G[seq[r]]  += scale * drop(gX[r])            (G dense [n_items, d]; skipped if G null)
 //   gP[pos[r]] += drop(gX[r])                     (gP dense [n_pos, d]; skipped if null)
 //   gXin[r]     = drop(gX[r])                     (optional, for the non-gather mode)
-C2_API size_t c2dsr_seg_err_offset(int n_rows, int d) { return 2 * seg_slot_bytes(n_rows, d); }
-
+// The item and position sums share one launch of each pass.
 C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
                                    uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G,
                                    int n_items, float* gP, int n_pos, float* gXin, void* workspace, size_t ws_bytes,
                                    void* stream) {
   if (d % 4) return (int)hipErrorInvalidValue;
   if (n_rows == 0) return 0;
-  if (ws_bytes < seg_ws_bytes(n_rows, d) || (G && !seq_plan) || (gP && !pos_plan)) return (int)hipErrorInvalidValue;
+  if (ws_bytes < c2dsr_embed_bwd_planned_workspace(n_rows, d) || (G && !seq_plan) || (gP && !pos_plan))
+    return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   c2::Drop dr = c2::make_drop(k0, k1, p);
-  hipMemsetAsync((char*)workspace + c2dsr_seg_err_offset(n_rows, d), 0, 4, s);
+  char* ws = (char*)workspace;
+  SegJob jobs[2];
+  int nj = 0;
   if (G)
-    seg_dispatch(plan_view(seq_plan, n_rows), n_rows, n_items, RowSrc{gX, d, dr, idx_base, scale, nullptr}, G,
-                 (char*)workspace, -1, s);
+    jobs[nj++] = seg_job(plan_view(seq_plan, n_rows), n_rows, n_items, RowSrc{gX, d, dr, idx_base, scale, nullptr}, G,
+                         ws, -1);
   if (gP)
-    seg_dispatch(plan_view(pos_plan, n_rows), n_rows, n_pos, RowSrc{gX, d, dr, idx_base, 1.0f, nullptr}, gP,
-                 (char*)workspace, -1, s);
+    jobs[nj++] = seg_job(plan_view(pos_plan, n_rows), n_rows, n_pos, RowSrc{gX, d, dr, idx_base, 1.0f, nullptr}, gP,
+                         ws + seg_ws_bytes(n_rows, d), -1);
+  if (nj) seg_dispatch(jobs[0], nj > 1 ? &jobs[1] : nullptr, s);
   if (gXin) {
     long n4 = (long)n_rows * d / 4;
     drop_scale_kernel<<<c2::ceil_div(n4, 256), 256, 0, s>>>(gX, n4, d, dr, idx_base, gXin);
@@ -636,36 +767,25 @@ C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, i
 }
 
 C2_API size_t c2dsr_embed_bwd_workspace(int n_rows, int d) {
-  return align256(plan_layout(n_rows, nullptr, nullptr)) + seg_ws_bytes(n_rows, d);
+  return 2 * align256(plan_layout(n_rows, nullptr, nullptr)) + c2dsr_embed_bwd_planned_workspace(n_rows, d);
 }
 
-// unplanned form: sorts inside (one plan buffer reused for seq, then pos)
+// unplanned form: both plans built inside, then the planned backward
 C2_API int c2dsr_embed_bwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* gX, uint32_t k0,
                            uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items, float* gP,
                            int n_pos, float* gXin, void* workspace, size_t ws_bytes, void* stream) {
   if (d % 4) return (int)hipErrorInvalidValue;
   if (n_rows == 0) return 0;
   if (ws_bytes < c2dsr_embed_bwd_workspace(n_rows, d)) return (int)hipErrorInvalidValue;
-  char* plan = (char*)workspace;
   const size_t pb = align256(plan_layout(n_rows, nullptr, nullptr));
-  char* seg = plan + pb;
-  const size_t sb = seg_ws_bytes(n_rows, d);
+  char* sp = (char*)workspace;
+  char* pp = sp + pb;
+  char* seg = pp + pb;
   int e;
-  if (G) {
-    if ((e = c2dsr_index_plan(seq, n_rows, n_items, plan, pb, stream))) return e;
-    if ((e = c2dsr_embed_bwd_planned(plan, nullptr, n_rows, d, gX, k0, k1, p, idx_base, scale, G, n_items, nullptr,
-                                     0, nullptr, seg, sb, stream)))
-      return e;
-  }
-  if (gP) {
-    if ((e = c2dsr_index_plan(pos, n_rows, n_pos, plan, pb, stream))) return e;
-    if ((e = c2dsr_embed_bwd_planned(nullptr, plan, n_rows, d, gX, k0, k1, p, idx_base, 1.0f, nullptr, 0, gP, n_pos,
-                                     nullptr, seg, sb, stream)))
-      return e;
-  }
-  if (gXin) return c2dsr_embed_bwd_planned(nullptr, nullptr, n_rows, d, gX, k0, k1, p, idx_base, 1.0f, nullptr, 0,
-                                           nullptr, 0, gXin, seg, sb, stream);
-  return 0;
+  if (G && (e = c2dsr_index_plan(seq, n_rows, n_items, sp, pb, stream))) return e;
+  if (gP && (e = c2dsr_index_plan(pos, n_rows, n_pos, pp, pb, stream))) return e;
+  return c2dsr_embed_bwd_planned(G ? sp : nullptr, gP ? pp : nullptr, n_rows, d, gX, k0, k1, p, idx_base, scale, G,
+                                 n_items, gP, n_pos, gXin, seg, c2dsr_embed_bwd_planned_workspace(n_rows, d), stream);
 }
 
 C2_API size_t c2dsr_ce_onehot_planned_workspace(int M, int n, int D) {
@@ -686,12 +806,15 @@ C2_API int c2dsr_ce_onehot_dw_planned(const void* plan, int M, int n, const floa
   char* seg = (char*)workspace;
   const Plan p = plan_view(plan, M);
   const c2::Drop nodrop = c2::make_drop(0, 0, 0.f);
-  hipMemsetAsync(seg + c2dsr_seg_err_offset(M, D), 0, 4, s);
-  if (gW) seg_dispatch(p, M, n + 1, RowSrc{H, D, nodrop, 0, -1.f, rw}, gW, seg, n, s);
+  if (gW) {
+    const SegJob j = seg_job(p, M, n + 1, RowSrc{H, D, nodrop, 0, -1.f, rw}, gW, seg, n);
+    seg_dispatch(j, nullptr, s);
+  }
   if (gb) {
     float* T = (float*)(seg + seg_ws_bytes(M, D));
     hipMemsetAsync(T, 0, (size_t)n * 16, s);
-    seg_dispatch(p, M, n + 1, RowSrc{nullptr, 4, nodrop, 0, -1.f, rw}, T, seg, n, s);
+    const SegJob j = seg_job(p, M, n + 1, RowSrc{nullptr, 4, nodrop, 0, -1.f, rw}, T, seg, n);
+    seg_dispatch(j, nullptr, s);
     col0_add_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(T, n, gb);
   }
   C2_CHECK_LAUNCH();

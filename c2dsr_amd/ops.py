@@ -273,8 +273,8 @@ def _check_err(ws, off, name):
 
 
 def _check_plan(buf, idx, n_keys, seg_ch=32):
-    """Debug (C2DSR_CHECK_PLANS=1): the plan against a host restatement (keys, rows, piece descriptors,
-    splits) before any kernel consumes it."""
+    """Debug (C2DSR_CHECK_PLANS=1): the plan against a host restatement (sorted keys, rows, split list)
+    before any kernel consumes it."""
     import numpy as np
     torch.cuda.synchronize()
     b = buf.cpu().numpy()
@@ -285,27 +285,28 @@ def _check_plan(buf, idx, n_keys, seg_ch=32):
         raise HipLibError(f'index plan: keys outside [0, {n_keys}): {x.min()}..{x.max()}')
     order = np.argsort(x, kind='stable')
     K = x[order]
-    o_v = a(4 * n); o_st = o_v + a(4 * n); o_sp = o_st + a(4 * (n + 2)); o_ct = o_sp + a(16 * (n // seg_ch + 1))
-    o_ds = o_ct + a(16)
+    o_v = a(4 * n)
+    o_sp = o_v + a(4 * n)
+    o_ct = o_sp + a(16 * (n // seg_ch + 1))
     cnt = b[o_ct:o_ct + 16].view(np.int32)
-    starts = [i for i in range(n) if i == 0 or i % seg_ch == 0 or K[i] != K[i - 1]]
     errs = []
     if not np.array_equal(b[:4 * n].view(np.uint32), K.astype(np.uint32)):
         errs.append('keys')
     if not np.array_equal(b[o_v:o_v + 4 * n].view(np.uint32), order.astype(np.uint32)):
         errs.append('rows')
-    if int(cnt[0]) != len(starts):
-        errs.append(f'pieces {int(cnt[0])} != {len(starts)}')
-    else:
-        ends = starts[1:] + [n]
-        ref = []
-        for s_, e_ in zip(starts, ends):
-            hd = s_ % seg_ch == 0 and s_ > 0 and K[s_ - 1] == K[s_]
-            tl = e_ % seg_ch == 0 and e_ < n and K[e_] == K[s_]
-            ref.append((s_, e_, K[s_], 1 if hd else (2 if tl else 0)))
-        got = b[o_ds:o_ds + 16 * len(ref)].view(np.int32).reshape(-1, 4)
+    ref = []
+    for i in range(n):
+        if i == 0 or K[i] != K[i - 1]:
+            ce = (i // seg_ch + 1) * seg_ch
+            if ce < n and K[ce] == K[i]:
+                end = int(np.searchsorted(K, K[i], side='right'))
+                ref.append((K[i], i // seg_ch, (end - 1) // seg_ch - i // seg_ch + 1, 0))
+    if int(cnt[1]) != len(ref):
+        errs.append(f'splits {int(cnt[1])} != {len(ref)}')
+    elif ref:
+        got = b[o_sp:o_sp + 16 * len(ref)].view(np.int32).reshape(-1, 4)
         if not np.array_equal(got, np.array(ref, dtype=np.int32).reshape(-1, 4)):
-            errs.append('desc')
+            errs.append('split list')
     if errs:
         raise HipLibError(f'index plan mismatch (n={n}, n_keys={n_keys}): {errs}')
 
@@ -368,7 +369,10 @@ class EmbedFn(Function):
                 int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes,
                 stream())
             if _CHECK_PLANS or _CHECK_ERR:
-                _check_err(ws, int(lib.raw('c2dsr_seg_err_offset')(n, d)), 'c2dsr_embed_bwd_planned')
+                off = int(lib.raw('c2dsr_plan_err_offset')(n))
+                for pl in (sp, pp):
+                    if pl is not None:
+                        _check_err(pl, off, 'c2dsr_embed_bwd_planned')
         else:
             ws_bytes = lib.raw('c2dsr_embed_bwd_workspace')(n, d)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)

@@ -51,11 +51,12 @@ size_t c2dsr_embed_bwd_workspace(int n_rows, int d);
  * (the deterministic path of F.embedding's backward, models/C2DSR.py:65). */
 size_t c2dsr_index_plan_bytes(int n);
 int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, size_t plan_bytes, void* stream);
-/* c2dsr_embed_bwd on prebuilt plans of seq / pos (seq_plan needed iff G, pos_plan iff gP).  A plan
- * whose pieces fall outside [0, n_rows) entries or [0, n_items) / [0, n_pos) rows is not followed:
- * the int at workspace + c2dsr_seg_err_offset(n_rows, d) is then nonzero (debug check). */
+/* c2dsr_embed_bwd on prebuilt plans of seq / pos (seq_plan needed iff G, pos_plan iff gP); the item
+ * and position sums share one launch of each pass.  A plan whose keys fall outside [0, n_items) /
+ * [0, n_pos) or whose split lists are inconsistent is not followed: the int at
+ * plan + c2dsr_plan_err_offset(n_rows) is then nonzero (debug check). */
 size_t c2dsr_embed_bwd_planned_workspace(int n_rows, int d);
-size_t c2dsr_seg_err_offset(int n_rows, int d);
+size_t c2dsr_plan_err_offset(int n);
 int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
                             uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items,
                             float* gP, int n_pos, float* gXin, void* workspace, size_t ws_bytes, void* stream);

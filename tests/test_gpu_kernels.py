@@ -143,14 +143,14 @@ def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
     ws = torch.empty(ws_b, dtype=torch.uint8, device=DEV)
     lib('c2dsr_embed_bwd_planned', sp.get(), pp.get(), n_rows, d, gX.to(DEV), keys[0], keys[1], p, 77, scale, G,
         n_items, gP, L, gXin, ws, ws_b, stream())
-    off = lib.raw('c2dsr_seg_err_offset')(n_rows, d)
-    assert int(ws[off:off + 4].view(torch.int32).item()) == 0
+    off = lib.raw('c2dsr_plan_err_offset')(n_rows)
+    assert int(sp.get()[off:off + 4].view(torch.int32).item()) == 0
     # a plan of other indices (keys past the output rows) is skipped and flagged, never followed
     bad = IndexPlan(torch.full((n_rows,), n_items + 5, dtype=torch.int64, device=DEV), n_items + 6)
     G2 = torch.zeros(n_items, d, device=DEV)
     lib('c2dsr_embed_bwd_planned', bad.get(), None, n_rows, d, gX.to(DEV), keys[0], keys[1], p, 77, scale, G2,
         n_items, None, L, None, ws, ws_b, stream())
-    assert int(ws[off:off + 4].view(torch.int32).item()) != 0 and float(G2.abs().sum()) == 0.0
+    assert int(bad.get()[off:off + 4].view(torch.int32).item()) != 0 and float(G2.abs().sum()) == 0.0
     assert torch.equal(G.cpu(), outs[0][0]) and torch.equal(gP.cpu(), outs[0][1])
     assert rel(gXin, gX * mk) < 1e-6
     # the plan itself: keys ascending, rows ascending within a key (stable)
