@@ -359,9 +359,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    ndev = torch.cuda.device_count()
+    if world > 1 and ndev < world:
+        # rehearsal on a smaller box (e.g. two ranks on one GPU): RCCL cannot put two ranks on one
+        # device, so the collectives go through gloo; the 8-GPU node uses RCCL
+        local = local % max(ndev, 1)
     if world > 1:
+        backend = os.environ.get('C2DSR_DIST_BACKEND') or ('nccl' if ndev >= world else 'gloo')
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device('cuda', local)
     if opt.config == 'c5':
         run_c5(opt, world, rank, device)
