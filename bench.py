@@ -206,6 +206,18 @@ def k5_traffic(precision):
     return t.get('bytes_per_launch_triple'), t.get('source')
 
 
+def hbm_traffic():
+    """K1 + K2 HBM bytes per step (all their launches) from the same PMC passes (profiles/hbm_traffic.json,
+    tools/pmc_traffic.py): measured DRAM traffic below the algorithmic bytes means the MALL / L2 served
+    part of the gathers (re-read table rows)."""
+    path = os.path.join(ROOT, 'profiles', 'hbm_traffic.json')
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    return t.get('bytes_per_step'), t.get('source')
+
+
 def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
     """The oracle (CPU fp32 restatement, oracle/c2dsr_oracle.py) on a bounded sample of the same
     workload: same item tables, d, L; a small batch for a few steps."""
@@ -452,6 +464,9 @@ def main():
                                 '(bf16 MFMA); credited 2·M·n·d per launch each'
                                 if opt.precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
                         ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'])
+        if hb is not None and opt.config == 'mb' and opt.precision == 'bf16':
+            hb['traffic'], hb['traffic_source'] = hbm_traffic()
+            hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
         cpu = None
         if world == 1 and not opt.no_cpu_baseline:
             cpu = cpu_baseline(cfg, rows, gs, gp, opt.cpu_budget)

@@ -1,5 +1,7 @@
 """K5 HBM traffic per launch from the FETCH_SIZE / WRITE_SIZE passes of tools/round_profile.sh:
 FETCH_SIZE (KB) doubled per the gfx950 correction (MI355X_MICROARCH.md §HBM), WRITE_SIZE (KB) as is.
+Also the K1 + K2 kernels (GCN SpMM, embedding gather / segment sums) per step → hbm_traffic.json next to
+the K5 file (the PMC run is bench.py --steps 2 --warmup 1: 3 steps).
 usage: python tools/pmc_traffic.py gpurun_out/TAG [profiles/k5_traffic.json]"""
 import csv
 import json
@@ -11,16 +13,19 @@ from collections import defaultdict
 pre = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else None
 K5 = ('ce_lse_kernel', 'ce_dh_kernel', 'ce_dw_kernel')
+K12 = ('spmm_kernel', 'combine_kernel', 'embed_fwd_kernel', 'seg_chunk_kernel', 'seg_split1_kernel',
+       'seg_split2_kernel')
+PMC_STEPS = 3
 
 
-def per_kernel(path, counter):
+def per_kernel(path, counter, names=K5):
     vals = defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r['Counter_Name'] != counter:
             continue
         name = re.sub(r'\(anonymous namespace\)::', '', r['Kernel_Name'])
-        for k in K5:
-            if k in name:
+        for k in names:
+            if re.search(r'\b' + k + r'\b', name):
                 vals[k].append(float(r['Counter_Value']) * 1e3)  # KB -> B
     return vals
 
@@ -40,3 +45,20 @@ if out:
     json.dump(dict(bytes_per_launch_triple=tot, per_kernel=rows,
                    source=f'rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE passes, {pre.split("/")[-1]}, rev {rev}'),
               open(out, 'w'), indent=1)
+
+fe2 = per_kernel(f'{pre}_fetch/run_counter_collection.csv', 'FETCH_SIZE', K12)
+wr2 = per_kernel(f'{pre}_write/run_counter_collection.csv', 'WRITE_SIZE', K12)
+rows2 = {}
+for k in K12:
+    f = 2 * sum(fe2[k]) / PMC_STEPS
+    w = sum(wr2[k]) / PMC_STEPS
+    rows2[k] = dict(launches_per_step=len(fe2[k]) / PMC_STEPS, fetch_bytes=round(f), write_bytes=round(w),
+                    bytes=round(f + w))
+    print(f'{k:18} per step: fetch {f / 1e6:9.1f} MB  write {w / 1e6:8.1f} MB')
+tot2 = sum(r['bytes'] for r in rows2.values())
+print(f'K1+K2 per step: {tot2 / 1e6:.1f} MB')
+if out:
+    import os
+    json.dump(dict(bytes_per_step=tot2, per_kernel=rows2,
+                   source=f'rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE passes, {pre.split("/")[-1]}, rev {rev}'),
+              open(os.path.join(os.path.dirname(out), 'hbm_traffic.json'), 'w'), indent=1)
