@@ -28,7 +28,14 @@ struct Epi2 {
   int relu;
   c2::Drop drop;
   int64_t row_base;
+  const float* aux;  // AUX epilogues: [M][ldc] fp32 read at the output positions
+  float aux_scale;
 };
+
+// epilogues that read a second [M, N] tensor at the output positions (prefetched one tile ahead):
+//   AUX_ACC:  C = alpha·A·Bᵀ + bias + aux             (aux may be C itself: C += A·Bᵀ)
+//   AUX_MASK: C = aux > 0 ? (alpha·A·Bᵀ + bias)·s : 0  (backward of drop(relu(.)) given its output aux)
+enum { AUX_NONE = 0, AUX_ACC = 1, AUX_MASK = 2 };
 
 __device__ __forceinline__ bf16x8 cvt8(float4 a, float4 b) {
   bf16x8 r;
@@ -59,9 +66,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_bytes(const void* base, l
 // repeated to fill a pair) so the compiler's wait counts stay exact and the prefetch lives.
 // Block b runs on XCD b % 8; the G column groups of an XCD walk the same rows in the same
 // order, so the G passes over A share its L2.
-template <int KCH, int CT, bool EPI>
+template <int KCH, int CT, bool EPI, int AUX = AUX_NONE>
 __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
-                                                 const bf16* __restrict__ B, long ldb, float* __restrict__ C,
+                                                 const bf16* __restrict__ B, long ldb, float* C,
                                                  long ldc, Epi2 ep, int G) {
   __shared__ __attribute__((aligned(16))) char aimg[2][32 * 256 * 2];
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -95,6 +102,24 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
   vm_drain();
   const auto asrc = rsrc_bytes(A, (long)M * lda * 4);  // rows >= M read 0
   const auto csrc = rsrc_bytes(C, (long)M * ldc * 4);  // stores to rows >= M are dropped
+  const auto xsrc = rsrc_bytes(AUX != AUX_NONE ? ep.aux : C, (long)M * ldc * 4);  // rows >= M read 0
+  // aux values of this wave's outputs for the current tile, loaded one tile ahead
+  float xa[AUX != AUX_NONE ? CT : 1][16];
+  const auto aux_load = [&](int tile) {
+    if constexpr (AUX != AUX_NONE) {
+      const int r0 = (rt0 + tile * rts) * 32;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int col = ncol0 + 32 * ct + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int off = col < N ? ((r0 + creg(r, lane)) * (int)ldc + col) * 4 : 0x7fffffff;
+          xa[ct][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xsrc, off, 0, 0));
+        }
+      }
+    }
+  };
+  aux_load(0);
   // chunk c = (tile c / KCH (clamped to the last), k-chunk c % KCH); thread t loads float4
   // t + 256u, u < 8: row (t >> 6) + 4u, columns 4·lane .. +3
   const int ldab = (int)lda * 4;
@@ -130,11 +155,13 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) acc[ct] =                                              \
           __builtin_amdgcn_mfma_f32_32x32x16_bf16(af_, bq[ct][(KC) * 16 + ks], acc[ct], 0, 0, 0);              \
     }                                                                                                          \
-    if constexpr ((KC) == KCH - 1) epilogue(min((c) / KCH, ntile - 1));                                       \
+    if constexpr ((KC) == KCH - 1) epilogue(min((c) / KCH, ntile - 1), (c) / KCH < ntile);                    \
     RG_STAGE(S, aimg[((c) + 1) & 1])                                                                           \
     __syncthreads();                                                                                           \
   }
-  const auto epilogue = [&](int tile) {
+  // live = false: the repeated last tile of an odd count (its stores are dropped, so an in-place
+  // AUX_ACC never adds twice)
+  const auto epilogue = [&](int tile, bool live) {
     const int r0 = (rt0 + tile * rts) * 32;
     // lane holds C[r0 + creg(r)][ncol0 + 32ct + (lane&31)]
 #pragma unroll
@@ -150,12 +177,15 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
           h = c2::lowbias32(h ^ (uint32_t)(idx >> 32) ^ ep.drop.k1);
           v = fmaxf(v, 0.f) * (h >= ep.drop.thr ? ep.drop.scale : 0.f);
         }
-        const int off = col < N ? (rr * (int)ldc + col) * 4 : 0x7fffffff;
+        if constexpr (AUX == AUX_ACC) v += xa[ct][r];
+        if constexpr (AUX == AUX_MASK) v = xa[ct][r] > 0.f ? v * ep.aux_scale : 0.f;
+        const int off = (col < N && live) ? (rr * (int)ldc + col) * 4 : 0x7fffffff;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), csrc, off, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
     }
+    aux_load(min(tile + 1, ntile - 1));  // the next tile's aux values, in flight under its MFMAs
   };
   float4 Pa[8], Pb[8];
   RG_LOAD(0, Pa)
@@ -383,11 +413,26 @@ C2_API int c2dsr_rgemm_supported(int M, int N, int K) {
 
 // C[M,N] = alpha·A[M,K]·B[N,K]ᵀ + bias[N]  (beta must be 0; epilogue 1: relu then dropout(p), index
 // (row_base+row)·N + col).  A fp32 (row stride lda, 16-byte aligned rows), B bf16 [N][ldb].
+C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                           float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                           int64_t row_base, int aux_mode, const float* aux, float aux_scale, void* stream);
+
 C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                        float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                        int64_t row_base, void* stream) {
+  return c2dsr_rgemm_aux(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, 0,
+                         nullptr, 0.f, stream);
+}
+
+// ... with an aux epilogue: aux_mode 1: C = alpha·A·Bᵀ + bias + aux (aux == C: accumulate in
+// place); 2: C = aux > 0 ? (alpha·A·Bᵀ + bias)·aux_scale : 0 (aux [M][ldc]).
+C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                           float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                           int64_t row_base, int aux_mode, const float* aux, float aux_scale, void* stream) {
   if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
-  Epi2 ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base};
+  if (aux_mode < 0 || aux_mode > 2 || (aux_mode && (!aux || epilogue))) return (int)hipErrorInvalidValue;
+  Epi2 ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base, aux,
+          aux_scale};
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -399,7 +444,7 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
   const int CT = K == 256 ? 2 : 1;
   const int G = c2::ceil_div(N, 128 * CT);
   // persistent grid: exactly the workgroups that are resident at once (occupancy of the variant)
-  static int per_cu[6] = {0, 0, 0, 0, 0, 0};
+  static int per_cu[12] = {0};
   auto launch = [&](void (*kern)(int, int, int, const float*, long, const bf16*, long, float*, long, Epi2, int),
                     int slot) -> int {
     if (!per_cu[slot]) {
@@ -414,7 +459,21 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
   };
   int rc;
   const bool e = epilogue == 1;
-  if (K == 256)
+  if (aux_mode == AUX_ACC) {
+    if (K == 256)
+      rc = launch(rg_kernel<1, 2, false, AUX_ACC>, 6);
+    else if (K == 512)
+      rc = launch(rg_kernel<2, 1, false, AUX_ACC>, 7);
+    else
+      rc = launch(rg_kernel<3, 1, false, AUX_ACC>, 8);
+  } else if (aux_mode == AUX_MASK) {
+    if (K == 256)
+      rc = launch(rg_kernel<1, 2, false, AUX_MASK>, 9);
+    else if (K == 512)
+      rc = launch(rg_kernel<2, 1, false, AUX_MASK>, 10);
+    else
+      rc = launch(rg_kernel<3, 1, false, AUX_MASK>, 11);
+  } else if (K == 256)
     rc = e ? launch(rg_kernel<1, 2, true>, 0) : launch(rg_kernel<1, 2, false>, 1);
   else if (K == 512)
     rc = e ? launch(rg_kernel<2, 1, true>, 2) : launch(rg_kernel<2, 1, false>, 3);

@@ -110,15 +110,16 @@ class SelfAttention(nn.Module):
             p_fm, k_fm = self._drop(pass_id, li, DK.K_FF_MID)
             p_fo, k_fo = self._drop(pass_id, li, DK.K_FF_OUT)
 
-            def sa_block(inp):
-                qkv = ops.linear(inp, at.in_proj_weight, at.in_proj_bias, self.precision)
+            def sa_block(inp, res=None):
+                qkv = ops.linear(inp, at.in_proj_weight, at.in_proj_bias, self.precision, res=res)
                 o = ops.AttnFn.apply(qkv, seq, self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset)
                 return ops.linear(o, at.out_proj.weight, at.out_proj.bias, self.precision)
 
-            def ff_block(inp):
+            def ff_block(inp, res=None):
+                ff = ops.FFLink(p_fm)
                 f = ops.linear(inp, lay.linear1.weight, lay.linear1.bias, self.precision,
-                               relu_drop=(k_fm, p_fm, rb_rows))
-                return ops.linear(f, lay.linear2.weight, lay.linear2.bias, self.precision)
+                               relu_drop=(k_fm, p_fm, rb_rows), res=res, ff=ff, ff_role='in')
+                return ops.linear(f, lay.linear2.weight, lay.linear2.bias, self.precision, ff=ff, ff_role='out')
 
             if self.norm_first:
                 y = ops.AddLNFn.apply(x, None, lay.norm1.weight, lay.norm1.bias, 0.0, (0, 0), 0, lay.norm1.eps)
@@ -126,10 +127,14 @@ class SelfAttention(nn.Module):
                 y = ops.AddLNFn.apply(x, None, lay.norm2.weight, lay.norm2.bias, 0.0, (0, 0), 0, lay.norm2.eps)
                 x = ops.AddDropFn.apply(x, ff_block(y), p_fo, k_fo, rb_rows)
             else:
-                x = ops.AddLNFn.apply(x, sa_block(x), lay.norm1.weight, lay.norm1.bias, p_sa, k_sa, rb_rows,
-                                      lay.norm1.eps)
-                x = ops.AddLNFn.apply(x, ff_block(x), lay.norm2.weight, lay.norm2.bias, p_fo, k_fo, rb_rows,
-                                      lay.norm2.eps)
+                # x feeds the block's first projection and the LN residual: the LN backward parks its
+                # gradient in the link and the projection's dX accumulates onto it (ops.ResidualLink)
+                r1 = ops.ResidualLink()
+                x = ops.AddLNFn.apply(x, sa_block(x, r1), lay.norm1.weight, lay.norm1.bias, p_sa, k_sa, rb_rows,
+                                      lay.norm1.eps, r1)
+                r2 = ops.ResidualLink()
+                x = ops.AddLNFn.apply(x, ff_block(x, r2), lay.norm2.weight, lay.norm2.bias, p_fo, k_fo, rb_rows,
+                                      lay.norm2.eps, r2)
         nm = self.encoder.norm
         return ops.AddLNFn.apply(x, None, nm.weight, nm.bias, 0.0, (0, 0), 0, nm.eps)
 

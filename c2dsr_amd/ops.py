@@ -67,8 +67,12 @@ def to_bf16(X, trans=False):
     return y
 
 
-def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None):
-    """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm)."""
+AUX_ACC, AUX_MASK = 1, 2
+
+
+def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, aux_mode=0, aux=None, aux_scale=0.0):
+    """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm); aux_mode
+    AUX_ACC: C += aux (aux may be C itself), AUX_MASK: C = aux > 0 ? C·aux_scale : 0 (c2dsr_rgemm_aux)."""
     k0 = k1 = 0
     p = 0.0
     row_base = 0
@@ -76,8 +80,12 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None):
     if relu_drop is not None:
         epi = 1
         (k0, k1), p, row_base = relu_drop
-    lib('c2dsr_rgemm', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
-        int(row_base), stream())
+    if aux_mode:
+        lib('c2dsr_rgemm_aux', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
+            int(row_base), int(aux_mode), aux, float(aux_scale), stream())
+    else:
+        lib('c2dsr_rgemm', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
+            int(row_base), stream())
     return C
 
 
@@ -92,13 +100,35 @@ def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None):
     lib('c2dsr_wgemm', T, N, D, dY, N, X, D, float(beta), dW, db, ws, stream())
 
 
+class ResidualLink:
+    """Joins the two consumers of a post-norm encoder layer's input x — the layer's first projection and
+    the residual branch of its LayerNorm (models/encoders.py:23-27 → transformer.py: x = norm(x + block(x))).
+    The LayerNorm backward parks its gradient w.r.t. x here instead of returning it; the projection's dX
+    product then accumulates onto it in its epilogue, so autograd never adds the two in a separate pass."""
+
+    def __init__(self):
+        self.grad = None
+
+
+class FFLink:
+    """Joins linear1 (drop(relu(.)) epilogue) and linear2 of a feed-forward block: when linear2's dX
+    product applied the drop(relu) backward in its epilogue (mask = linear2's input > 0), linear1
+    receives an already-masked gradient."""
+
+    def __init__(self, p):
+        self.p = p
+        self.premasked = False
+
+
 class LinearFn(Function):
     """y = x·Wᵀ + b  [optionally drop(relu(.))]  — nn.Linear / TransformerEncoderLayer linear1, linear2,
     in_proj, out_proj (models/encoders.py:23-27 → torch transformer.py).  bf16 mode at d = 256-multiples:
-    the row-streaming MFMA kernels (csrc/rgemm.hip); otherwise the tiled GEMM (csrc/gemm.hip)."""
+    the row-streaming MFMA kernels (csrc/rgemm.hip); otherwise the tiled GEMM (csrc/gemm.hip).
+    res: ResidualLink (this projection reads the layer input; its dX accumulates onto the parked LN
+    gradient).  ff: FFLink — role 'in' for linear1 (the relu-drop producer), 'out' for linear2."""
 
     @staticmethod
-    def forward(ctx, x, W, b, precision, relu_drop):
+    def forward(ctx, x, W, b, precision, relu_drop, res=None, ff=None, ff_role=None):
         require_device(x)
         N, K = W.shape
         M = x.numel() // K
@@ -111,6 +141,7 @@ class LinearFn(Function):
         ctx.b = b
         ctx.precision = precision
         ctx.relu_p = relu_drop[1] if relu_drop is not None else None
+        ctx.res, ctx.ff, ctx.ff_role = res, ff, ff_role
         return y
 
     @staticmethod
@@ -119,16 +150,32 @@ class LinearFn(Function):
         N, K = W.shape
         M = x.numel() // K
         dy = dy.contiguous()
-        if ctx.relu_p is not None:
+        if ctx.relu_p is not None and not (ctx.ff is not None and ctx.ff.premasked):
             d2 = torch.empty_like(dy)
             lib('c2dsr_relu_drop_bwd', dy, y, dy.numel(), float(ctx.relu_p), d2, stream())
             dy = d2
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            if ctx.precision == BF16 and rgemm_ok(M, K, N):
+            fused = ctx.precision == BF16 and rgemm_ok(M, K, N)
+            park = ctx.res.grad if ctx.res is not None else None
+            if ctx.res is not None:
+                ctx.res.grad = None
+            if fused and park is not None:  # dx = parked LN gradient + dy·W, in place
+                dx = park
+                rgemm(dy, to_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
+            elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here
+                dx = torch.empty_like(x)
+                rgemm(dy, to_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x,
+                      aux_scale=1.0 / (1.0 - ctx.ff.p))
+                ctx.ff.premasked = True
+            elif fused:
+                dx = torch.empty_like(x)
                 rgemm(dy, to_bf16(W, trans=True), dx, M=M, N=K, K=N)
+            elif park is not None:
+                dx = park
+                gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0, precision=ctx.precision)
             else:
+                dx = torch.empty_like(x)
                 gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
         gW = _grad_target(W)
         gb = _grad_target(ctx.b)
@@ -139,11 +186,11 @@ class LinearFn(Function):
             gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
         if gb is not None:
             colsum(dy, M, N, N, gb)
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
-def linear(x, W, b, precision=FP32, relu_drop=None):
-    return LinearFn.apply(x.contiguous(), W, b, precision, relu_drop)
+def linear(x, W, b, precision=FP32, relu_drop=None, res=None, ff=None, ff_role=None):
+    return LinearFn.apply(x.contiguous(), W, b, precision, relu_drop, res, ff, ff_role)
 
 
 # ----------------------------------------------------------------------------- GCN (K1)
@@ -450,7 +497,7 @@ class AddLNFn(Function):
     """y = LayerNorm(a + drop(b))  (b may be None: plain LayerNorm of a); eps 1e-8."""
 
     @staticmethod
-    def forward(ctx, a, b, w, bias, p, keys, row_base, eps):
+    def forward(ctx, a, b, w, bias, p, keys, row_base, eps, res=None):
         d = a.shape[-1]
         rows = a.numel() // d
         y = torch.empty_like(a)
@@ -461,6 +508,7 @@ class AddLNFn(Function):
             mean, rstd, stream())
         ctx.save_for_backward(xsave if b is not None else a, mean, rstd)
         ctx.w, ctx.bias, ctx.p, ctx.keys, ctx.row_base, ctx.has_b = w, bias, p, keys, row_base, b is not None
+        ctx.res = res
         return y
 
     @staticmethod
@@ -475,7 +523,10 @@ class AddLNFn(Function):
         ws = torch.empty(lib.raw('c2dsr_ln_bwd_workspace')(d), dtype=torch.uint8, device=x.device)
         lib('c2dsr_ln_bwd', x, mean, rstd, ctx.w, dy, rows, d, da, 0, db, ctx.keys[0], ctx.keys[1], float(ctx.p),
             int(ctx.row_base), gw, gb, ws, stream())
-        return da, db, None, None, None, None, None, None
+        if ctx.res is not None:  # parked for the layer's first projection (ResidualLink)
+            ctx.res.grad = da
+            da = None
+        return da, db, None, None, None, None, None, None, None
 
 
 class AddDropFn(Function):

@@ -186,6 +186,15 @@ int c2dsr_rgemm_supported(int M, int N, int K);
 int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                 float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                 int64_t row_base, void* stream);
+/* c2dsr_rgemm with an epilogue reading aux [M][ldc] at the output positions (prefetched a tile ahead):
+ *   aux_mode 1: C = alpha·A·Bᵀ + bias + aux   (aux == C accumulates in place: the residual-gradient sum
+ *               of a post-norm encoder layer, which autograd would otherwise add in a separate pass)
+ *   aux_mode 2: C = aux > 0 ? (alpha·A·Bᵀ + bias)·aux_scale : 0   (dX of linear2 masked by the
+ *               backward of drop(relu(.)) of linear1, given its output aux; models/encoders.py:23-27)
+ * epilogue must be 0 and beta 0 with an aux mode. */
+int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                    float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                    int64_t row_base, int aux_mode, const float* aux, float aux_scale, void* stream);
 /* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
  * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
  * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS

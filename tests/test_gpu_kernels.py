@@ -413,3 +413,24 @@ def test_wgemm_vs_bf16_rounded_fp32(T, N):
     dW2 = torch.full((N, D), 7.0, device=DEV)
     wgemm(dY.to(DEV), X.to(DEV), dW2, T=T, N=N, D=D, beta=0.0)
     assert torch.equal(dW, dW2)
+
+
+@pytest.mark.parametrize('K', [256, 768])
+def test_rgemm_aux_epilogues(K):
+    """c2dsr_rgemm_aux: in-place accumulate (the residual-gradient sum) and the drop(relu) backward mask,
+    against bf16-rounded fp32 products; odd row-tile counts exercise the repeated last tile."""
+    from c2dsr_amd.ops import AUX_ACC, AUX_MASK, rgemm, to_bf16
+    g = torch.Generator().manual_seed(K)
+    M, N = 32 * 37 + 5, 256
+    A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+    Wb = to_bf16(W.to(DEV))
+    prod = _bf(A).double() @ _bf(W).double().T
+    C0 = torch.randn(M, N, generator=g)
+    C = C0.to(DEV)
+    rgemm(A.to(DEV), Wb, C, M=M, N=N, K=K, aux_mode=AUX_ACC, aux=C)
+    assert rel(C, prod + C0.double()) < 2e-6
+    src = torch.randn(M, N, generator=g)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), Wb, C, M=M, N=N, K=K, aux_mode=AUX_MASK, aux=src.to(DEV), aux_scale=1.25)
+    want = torch.where(src.double() > 0, prod * 1.25, torch.zeros_like(prod))
+    assert rel(C, want) < 2e-6
