@@ -17,7 +17,7 @@ import re
 import torch  # noqa: F401  (load torch's HIP runtime first: same soname libamdhip64.so.7)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libc2dsr_hip.so')
+LIB_PATH = os.environ.get('C2DSR_LIB') or os.path.join(_HERE, 'libc2dsr_hip.so')
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'c2dsr.h')
 
 _CTYPES = {

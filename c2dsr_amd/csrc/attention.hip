@@ -13,6 +13,8 @@
 // modes bit-identical here while staying far off the critical path.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -525,6 +527,192 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fast(const float* __restrict_
   pv_fast<LP, true>(Pd, dO, d, L, dh, L, dV, rs, 1.0f);    // dV = Pdᵀ·dO
 }
 
+// ---------------------------------------------------------------------------------------
+// Wave-per-sequence forward (L <= 64, dh % 32 == 0): no LDS, no barriers.  The score tiles are
+// computed TRANSPOSED, Sᵀ = K·Qᵀ, so the lane of a query holds its whole row of scores in
+// registers (keys j = 32tj + creg(r, lane)): the softmax is in-register plus one lane^32 exchange.
+// P·V then takes the probabilities straight from those registers as the MFMA A operand: step r of
+// a key tile consumes register r, i.e. key (r&3) + 8(r>>2) + 4·(lane>>5) — a permutation of the
+// reduction index that the B operand (V rows, one float per lane, loaded in the same permuted
+// order) shares, so the sum is exact.  Output tiles come out lane = column: coalesced stores.
+// Keys past the last padding key are inadmissible for every query (Q1), so only jmax rows of K/V
+// are read (buffer descriptors zero the rest).
+// softmax of one query tile of transposed scores held by lane = query (tiles a: keys 0..31 and, when
+// TWO, b: keys 32..63) → probabilities to prow (all L keys of each row; 0 past the tiles) and the
+// dropped probabilities back into a / b.  Masks: key admissible (pad bit of kb), causal j <= i, i < L.
+template <bool TWO>
+__device__ __forceinline__ void wave_softmax(f32x16& a, f32x16& b, int ti, int L, uint64_t kb, float sc,
+                                             const c2::Drop& drop, uint64_t pbase, float* __restrict__ prow0) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hi = lane >> 5;
+  const int i = 32 * ti + r;
+  const bool row = i < L;
+  // admissible keys of this lane's 16 (or 32) registers as bit masks
+  uint32_t m0 = 0, m1 = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int j = creg(q, lane);
+    m0 |= (uint32_t)(row && j <= i && ((kb >> j) & 1)) << q;
+    if constexpr (TWO) m1 |= (uint32_t)(row && 32 + j <= i && ((kb >> (32 + j)) & 1)) << q;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    if ((m0 >> q) & 1) m = fmaxf(m, a[q] * sc);
+    if constexpr (TWO) if ((m1 >> q) & 1) m = fmaxf(m, b[q] * sc);
+  }
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    a[q] = ((m0 >> q) & 1) ? __expf(a[q] * sc - m) : 0.f;
+    sum += a[q];
+    if constexpr (TWO) {
+      b[q] = ((m1 >> q) & 1) ? __expf(b[q] * sc - m) : 0.f;
+      sum += b[q];
+    }
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+  float* prow = prow0 + (long)i * L;
+  const uint64_t rb = pbase + (uint64_t)i * L;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int j = creg(q, lane);
+    const float p0 = a[q] * inv;
+    if (row && j < L) prow[j] = p0;
+    a[q] = p0 * drop.mul(rb + j);
+    if constexpr (TWO) {
+      const float p1 = b[q] * inv;
+      if (row && 32 + j < L) prow[32 + j] = p1;
+      b[q] = p1 * drop.mul(rb + 32 + j);
+    }
+  }
+  if (row)  // probabilities of the keys past the computed tiles are 0
+    for (int j = (TWO ? 64 : 32) + hi; j < L; j += 2) prow[j] = 0.f;
+}
+
+template <int TJ, int TI>
+__device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const float* __restrict__ K,
+                                              const float* __restrict__ V, long rs, int L, int dh, int jmax,
+                                              uint64_t kb, const c2::Drop& drop, uint64_t pbase,
+                                              float* __restrict__ o_row0, long os, float* __restrict__ prow0) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hi = lane >> 5;
+  // tiles (tj, ti): 0 = (0,0), 1 = (0,1), 2 = (1,1)
+  f32x16 t0, t1, t2;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) t0[q] = t1[q] = t2[q] = 0.f;
+  {
+    const auto qsrc = rows_rsrc(Q, L, rs, dh);
+    const auto ksrc = rows_rsrc(K, jmax, rs, dh);
+    const int q0o = (r * (int)rs + 4 * hi) * 4, q1o = ((32 + r) * (int)rs + 4 * hi) * 4;
+    const int k0o = q0o, k1o = q1o;
+    const int CS = dh >> 3;
+    constexpr int SU = 2;  // c-steps per register buffer, two buffers in flight
+    float4 ba[SU][4], bb[SU][4];  // [c-step][k0, k1, q0, q1]
+    auto load = [&](float4 (&kq)[SU][4], int c0) {
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int co = 32 * (c0 + u);  // past the head: outside the descriptors → 0
+        kq[u][0] = ld_b128(ksrc, k0o + co, 0);
+        kq[u][1] = TJ > 1 ? ld_b128(ksrc, k1o + co, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        kq[u][2] = ld_b128(qsrc, q0o + co, 0);
+        kq[u][3] = TI > 1 ? ld_b128(qsrc, q1o + co, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    };
+    auto mma = [&](const float4 (&kq)[SU][4]) {
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const float ka[4] = {kq[u][0].x, kq[u][0].y, kq[u][0].z, kq[u][0].w};
+        const float kc[4] = {kq[u][1].x, kq[u][1].y, kq[u][1].z, kq[u][1].w};
+        const float qa[4] = {kq[u][2].x, kq[u][2].y, kq[u][2].z, kq[u][2].w};
+        const float qc[4] = {kq[u][3].x, kq[u][3].y, kq[u][3].z, kq[u][3].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qa[e], t0, 0, 0, 0);
+          if constexpr (TI > 1) t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qc[e], t1, 0, 0, 0);
+          if constexpr (TI > 1 && TJ > 1) t2 = __builtin_amdgcn_mfma_f32_32x32x2f32(kc[e], qc[e], t2, 0, 0, 0);
+        }
+      }
+    };
+    load(ba, 0);
+#pragma unroll 1
+    for (int c0 = 0; c0 < CS; c0 += 2 * SU) {
+      if (c0 + SU < CS) load(bb, c0 + SU);
+      mma(ba);
+      if (c0 + SU >= CS) break;
+      if (c0 + 2 * SU < CS) load(ba, c0 + 2 * SU);
+      mma(bb);
+    }
+  }
+  const float sc = 1.0f / sqrtf((float)dh);
+  wave_softmax<false>(t0, t0, 0, L, kb, sc, drop, pbase, prow0);
+  if constexpr (TI > 1) wave_softmax<(TJ > 1)>(t1, t2, 1, L, kb, sc, drop, pbase, prow0);
+  // O = Pd·V per 32-column tile of the head (two waves per SIMD hide each other's V loads)
+  const auto vsrc = rows_rsrc(V, jmax, rs, dh);
+  auto vload = [&](float (&v)[2][16], int ct) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int key = (q & 3) + 8 * (q >> 2) + 4 * hi;  // the key of register q (lane half hi)
+      v[0][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrc, (key * (int)rs + 32 * ct + r) * 4, 0, 0));
+      v[1][q] = TJ > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                             vsrc, ((32 + key) * (int)rs + 32 * ct + r) * 4, 0, 0))
+                       : 0.f;
+    }
+  };
+  auto otile = [&](const float (&v)[2][16], int ct) {
+    f32x16 o0, o1;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) o0[q] = o1[q] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(t0[q], v[0][q], o0, 0, 0, 0);
+      if constexpr (TI > 1) {
+        o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(t1[q], v[0][q], o1, 0, 0, 0);
+        if constexpr (TJ > 1) o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(t2[q], v[1][q], o1, 0, 0, 0);
+      }
+    }
+    const int c = 32 * ct + r;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i0 = creg(q, lane), i1 = 32 + i0;
+      if (i0 < L) o_row0[(long)i0 * os + c] = o0[q];
+      if (TI > 1 && i1 < L) o_row0[(long)i1 * os + c] = o1[q];
+    }
+  };
+  const int CT = dh >> 5;
+#pragma unroll 1
+  for (int ct = 0; ct < CT; ++ct) {
+    float va[2][16];
+    vload(va, ct);
+    otile(va, ct);
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_wave(const float* __restrict__ qkv, const int64_t* __restrict__ seq,
+                                                     int64_t pad, int B, int L, int d, int H, c2::Drop drop,
+                                                     int64_t b_base, float* __restrict__ out,
+                                                     float* __restrict__ Psave) {
+  const int lane = threadIdx.x & 63;
+  const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bh >= B * H) return;  // uniform over the wave
+  const int b = bh / H, h = bh % H, dh = d / H;
+  const bool ok = lane < L && seq[(long)b * L + lane] == pad;
+  const uint64_t kb = __ballot(ok);
+  const int jmax = kb ? 64 - __clzll((long long)kb) : 0;
+  const long rs = 3l * d;
+  const float* Q = qkv + (long)b * L * rs + h * dh;
+  const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
+  float* orow = out + (long)b * L * d + h * dh;
+  float* prow = Psave + (long)bh * L * L;
+  const int TJ = jmax > 32 ? 2 : 1, TI = L > 32 ? 2 : 1;
+  if (TI == 1)
+    fwd_wave_body<1, 1>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
+  else if (TJ == 1)
+    fwd_wave_body<1, 2>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
+  else
+    fwd_wave_body<2, 2>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
+}
+
 template <int LP>
 size_t fwd_smem() { return sizeof(float) * ((size_t)LP * Smem<LP>::SLD + Smem<LP>::STAGE); }
 template <int LP>
@@ -567,7 +755,9 @@ C2_API int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
   const bool fast = (d / H) % 4 == 0 && d % 4 == 0;
-  if (fast && L <= 32)
+  if (L <= 64 && (d / H) % 32 == 0 && !getenv("C2DSR_ATTN_TILED"))
+    attn_fwd_wave<<<c2::ceil_div((long)B * H, 4), 256, 0, s>>>(qkv, seq, pad, B, L, d, H, dr, b_base, out, Psave);
+  else if (fast && L <= 32)
     attn_fwd_fast<32><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
   else if (fast && L <= 64)
     attn_fwd_fast<64><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
