@@ -713,6 +713,238 @@ __global__ __launch_bounds__(256) void attn_fwd_wave(const float* __restrict__ q
     fwd_wave_body<2, 2>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
 }
 
+// ---------------------------------------------------------------------------------------
+// Wave-per-sequence backward (L <= 64, dh % 32 == 0), the forward's transposed layout:
+//   dPᵀ = V·dOᵀ (lane = query i, registers = keys j), P reloaded in the same layout;
+//   dP⊙mask, Pd = P⊙mask, dS = P⊙(dPm − Σ_j P·dPm) in registers (+ one lane^32 exchange);
+//   dQ = dS·K/√dh straight from the registers (key permutation as in the forward);
+//   dV = Pdᵀ·dO and dK = dSᵀ·Q/√dh need keys in lanes: Pd and dS go through a per-wave LDS
+//   transpose ([64][65] floats) and are read back with lane = key, register r = query
+//   (r&3) + 8(r>>2) + 4·(lane>>5) — the same permutation trick over the query index.
+// Rows of dK / dV past the last padding key are written as zeros (those keys are inadmissible).
+// order this wave's LDS writes before its later reads (and reads before later writes)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void zero16(f32x16& a) {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) a[q] = 0.f;
+}
+
+// acc (+)= A·B over one 32-key (or 32-query) tile: A from registers / LDS (per step r), B one float per
+// lane per step from a buffer descriptor at rows rowof(r) (relative), column c.
+template <int TJ, int TI>
+__device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const float* __restrict__ K,
+                                              const float* __restrict__ V, const float* __restrict__ dO,
+                                              long rs, long ds, int L, int dh, int jmax, uint64_t kb,
+                                              const c2::Drop& drop, uint64_t pbase, const float* __restrict__ prow0,
+                                              float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV,
+                                              float* T) {
+  const int lane = threadIdx.x & 63, r = lane & 31, hi = lane >> 5;
+  // ---- dPᵀ tiles (tj, ti): 0 = (0,0), 1 = (0,1), 2 = (1,1)
+  f32x16 g0, g1, g2;
+  zero16(g0); zero16(g1); zero16(g2);
+  {
+    const auto vsrc = rows_rsrc(V, jmax, rs, dh);
+    const auto osrc = rows_rsrc(dO, L, ds, dh);
+    const int v0o = (r * (int)rs + 4 * hi) * 4, v1o = ((32 + r) * (int)rs + 4 * hi) * 4;
+    const int o0o = (r * (int)ds + 4 * hi) * 4, o1o = ((32 + r) * (int)ds + 4 * hi) * 4;
+    const int CS = dh >> 3;
+#pragma unroll 1
+    for (int c0 = 0; c0 < CS; c0 += 2) {
+      float4 kq[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int co = 32 * (c0 + u);
+        kq[u][0] = ld_b128(vsrc, v0o + co, 0);
+        kq[u][1] = TJ > 1 ? ld_b128(vsrc, v1o + co, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        kq[u][2] = ld_b128(osrc, o0o + co, 0);
+        kq[u][3] = TI > 1 ? ld_b128(osrc, o1o + co, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float ka[4] = {kq[u][0].x, kq[u][0].y, kq[u][0].z, kq[u][0].w};
+        const float kc[4] = {kq[u][1].x, kq[u][1].y, kq[u][1].z, kq[u][1].w};
+        const float qa[4] = {kq[u][2].x, kq[u][2].y, kq[u][2].z, kq[u][2].w};
+        const float qc[4] = {kq[u][3].x, kq[u][3].y, kq[u][3].z, kq[u][3].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          g0 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qa[e], g0, 0, 0, 0);
+          if constexpr (TI > 1) g1 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qc[e], g1, 0, 0, 0);
+          if constexpr (TI > 1 && TJ > 1) g2 = __builtin_amdgcn_mfma_f32_32x32x2f32(kc[e], qc[e], g2, 0, 0, 0);
+        }
+      }
+    }
+  }
+  // ---- softmax gradient per query (lane): P reloaded, dS into g*, Pd into p*
+  f32x16 p0, p1, p2;
+  auto sgrad = [&](f32x16& g_a, f32x16& g_b, f32x16& p_a, f32x16& p_b, bool two, int ti) {
+    const int i = 32 * ti + r;
+    const bool row = i < L;
+    const float* prow = prow0 + (long)i * L;
+    const uint64_t rb = pbase + (uint64_t)i * L;
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j0 = creg(q, lane), j1 = 32 + j0;
+      const float pa = row && j0 < L ? prow[j0] : 0.f;
+      const float pb = two && row && j1 < L ? prow[j1] : 0.f;
+      const float ma = drop.mul(rb + j0), mb = two ? drop.mul(rb + j1) : 0.f;
+      const bool ada = row && j0 <= i && ((kb >> j0) & 1), adb = two && row && j1 <= i && ((kb >> j1) & 1);
+      g_a[q] = ada ? g_a[q] * ma : 0.f;
+      g_b[q] = adb ? g_b[q] * mb : 0.f;
+      acc += pa * g_a[q] + pb * g_b[q];
+      p_a[q] = pa;
+      p_b[q] = pb;
+      // keep the masks for Pd: stash them in the dPm slots' partner after the row sum
+      (void)ma;
+      (void)mb;
+    }
+    acc += __shfl_xor(acc, 32, 64);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j0 = creg(q, lane), j1 = 32 + j0;
+      g_a[q] = p_a[q] * (g_a[q] - acc);
+      g_b[q] = two ? p_b[q] * (g_b[q] - acc) : 0.f;
+      p_a[q] = p_a[q] * drop.mul(rb + j0);
+      p_b[q] = two ? p_b[q] * drop.mul(rb + j1) : 0.f;
+    }
+  };
+  {
+    f32x16 zg, zp;
+    zero16(zg); zero16(zp);
+    zero16(p1); zero16(p2);
+    sgrad(g0, zg, p0, zp, false, 0);
+    if constexpr (TI > 1) sgrad(g1, g2, p1, p2, TJ > 1, 1);
+  }
+  const float sc = 1.0f / sqrtf((float)dh);
+  const int CT = dh >> 5;
+  // ---- dQ = dS·K/√dh (lane = column, rows = queries)
+  {
+    const auto ksrc = rows_rsrc(K, jmax, rs, dh);
+#pragma unroll 1
+    for (int ct = 0; ct < CT; ++ct) {
+      float k0v[16], k1v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int key = (q & 3) + 8 * (q >> 2) + 4 * hi;
+        k0v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrc, (key * (int)rs + 32 * ct + r) * 4, 0, 0));
+        k1v[q] = TJ > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                              ksrc, ((32 + key) * (int)rs + 32 * ct + r) * 4, 0, 0))
+                        : 0.f;
+      }
+      f32x16 o0, o1;
+      zero16(o0); zero16(o1);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(g0[q], k0v[q], o0, 0, 0, 0);
+        if constexpr (TI > 1) {
+          o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(g1[q], k0v[q], o1, 0, 0, 0);
+          if constexpr (TJ > 1) o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(g2[q], k1v[q], o1, 0, 0, 0);
+        }
+      }
+      const int c = 32 * ct + r;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i0 = creg(q, lane), i1 = 32 + i0;
+        if (i0 < L) dQ[(long)i0 * rs + c] = sc * o0[q];
+        if (TI > 1 && i1 < L) dQ[(long)i1 * rs + c] = sc * o1[q];
+      }
+    }
+  }
+  // ---- dV = Pdᵀ·dO, dK = dSᵀ·Q/√dh: transpose through this wave's LDS tile T[i][j] (stride 65)
+  constexpr int TLD = 65;
+  auto put = [&](const f32x16& a, const f32x16& b, bool two, int ti) {
+    const int i = 32 * ti + r;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j0 = creg(q, lane);
+      T[i * TLD + j0] = a[q];
+      if (two) T[i * TLD + 32 + j0] = b[q];
+    }
+  };
+  auto keys_out = [&](const float* __restrict__ Src, long ss, int nrows, float scale, float* __restrict__ Dst) {
+    const auto src = rows_rsrc(Src, nrows, ss, dh);
+#pragma unroll 1
+    for (int ct = 0; ct < CT; ++ct) {
+      float b0v[16], b1v[16];  // Src rows (queries) of register q: (q&3) + 8(q>>2) + 4hi (+32)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int qi = (q & 3) + 8 * (q >> 2) + 4 * hi;
+        b0v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(src, (qi * (int)ss + 32 * ct + r) * 4, 0, 0));
+        b1v[q] = TI > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                              src, ((32 + qi) * (int)ss + 32 * ct + r) * 4, 0, 0))
+                        : 0.f;
+      }
+      const int c = 32 * ct + r;
+#pragma unroll
+      for (int tj = 0; tj < TJ; ++tj) {
+        f32x16 o;
+        zero16(o);
+#pragma unroll
+        for (int ti = tj; ti < TI; ++ti) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int qi = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * hi;
+            const float a = T[qi * TLD + 32 * tj + r];
+            o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, ti ? b1v[q] : b0v[q], o, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int j = 32 * tj + creg(q, lane);
+          if (j < L) Dst[(long)j * rs + c] = scale * o[q];
+        }
+      }
+      for (int j = 32 * TJ + hi; j < L; j += 2) Dst[(long)j * rs + c] = 0.f;  // keys past the tiles
+    }
+  };
+  // T starts as garbage: every entry the products read ([0, 32·TI) x [0, 32·TJ)) is written first
+  put(p0, p0, false, 0);
+  if constexpr (TI > 1) put(p1, p2, TJ > 1, 1);
+  if constexpr (TJ > 1) {  // tile (tj = 1, ti = 0) is above the diagonal: zero
+#pragma unroll
+    for (int q = 0; q < 16; ++q) T[r * TLD + 32 + creg(q, lane)] = 0.f;
+  }
+  wave_lds_sync();
+  keys_out(dO, ds, L, 1.0f, dV);
+  wave_lds_sync();
+  put(g0, g0, false, 0);
+  if constexpr (TI > 1) put(g1, g2, TJ > 1, 1);
+  wave_lds_sync();
+  keys_out(Q, rs, L, sc, dK);
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ qkv, const int64_t* __restrict__ seq,
+                                                     int64_t pad, int B, int L, int d, int H, c2::Drop drop,
+                                                     int64_t b_base, const float* __restrict__ Psave,
+                                                     const float* __restrict__ dout, float* __restrict__ dqkv) {
+  __shared__ float tbuf[4][64 * 65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int bh = blockIdx.x * 4 + w;
+  if (bh >= B * H) return;  // uniform over the wave (no block-level barriers below)
+  const int b = bh / H, h = bh % H, dh = d / H;
+  const bool ok = lane < L && seq[(long)b * L + lane] == pad;
+  const uint64_t kb = __ballot(ok);
+  const int jmax = kb ? 64 - __clzll((long long)kb) : 0;
+  const long rs = 3l * d;
+  const float* Q = qkv + (long)b * L * rs + h * dh;
+  const float* dO = dout + (long)b * L * d + h * dh;
+  float* dQ = dqkv + (long)b * L * rs + h * dh;
+  const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
+  const float* prow = Psave + (long)bh * L * L;
+  const int TJ = jmax > 32 ? 2 : 1, TI = L > 32 ? 2 : 1;
+  if (TI == 1)
+    bwd_wave_body<1, 1>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+  else if (TJ == 1)
+    bwd_wave_body<1, 2>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+  else
+    bwd_wave_body<2, 2>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+}
+
 template <int LP>
 size_t fwd_smem() { return sizeof(float) * ((size_t)LP * Smem<LP>::SLD + Smem<LP>::STAGE); }
 template <int LP>
@@ -780,7 +1012,10 @@ C2_API int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
   const bool fast = (d / H) % 4 == 0 && d % 4 == 0;
-  if (fast && L <= 32)
+  if (L <= 64 && (d / H) % 32 == 0 && !getenv("C2DSR_ATTN_TILED"))
+    attn_bwd_wave<<<c2::ceil_div((long)B * H, 4), 256, 0, s>>>(qkv, seq, pad, B, L, d, H, dr, b_base, Psave, dout,
+                                                               dqkv);
+  else if (fast && L <= 32)
     attn_bwd_fast<32><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
   else if (fast && L <= 64)
     attn_bwd_fast<64><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
