@@ -67,6 +67,37 @@ def to_bf16(X, trans=False):
     return y
 
 
+# bf16 images of the projection weights, made once per weight update: the three sequence-encoder
+# passes through one SelfAttention share weights, and every forward / backward product re-used to
+# convert them.  Valid while neither the fused optimizer (WEIGHTS.epoch, bumped per step) nor a torch
+# in-place op (W._version) has written the weight since.
+class _WeightImages:
+    def __init__(self):
+        self.epoch = 0
+        self.cache = {}
+
+    def bump(self):
+        self.epoch += 1
+        self.cache.clear()
+
+    def get(self, W, trans):
+        key = (W.data_ptr(), tuple(W.shape), bool(trans))
+        tag = (self.epoch, W._version)
+        hit = self.cache.get(key)
+        if hit is not None and hit[0] == tag:
+            return hit[1]
+        y = to_bf16(W, trans)
+        self.cache[key] = (tag, y)
+        return y
+
+
+WEIGHTS = _WeightImages()
+
+
+def weight_bf16(W, trans=False):
+    return WEIGHTS.get(W.detach(), trans)
+
+
 AUX_ACC, AUX_MASK = 1, 2
 
 
@@ -134,7 +165,7 @@ class LinearFn(Function):
         M = x.numel() // K
         y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
         if precision == BF16 and rgemm_ok(M, N, K):
-            rgemm(x, to_bf16(W), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
+            rgemm(x, weight_bf16(W), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
         else:
             gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)
         ctx.save_for_backward(x, W, y if relu_drop is not None else None)
@@ -162,15 +193,15 @@ class LinearFn(Function):
                 ctx.res.grad = None
             if fused and park is not None:  # dx = parked LN gradient + dy·W, in place
                 dx = park
-                rgemm(dy, to_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
+                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
             elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here
                 dx = torch.empty_like(x)
-                rgemm(dy, to_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x,
+                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x,
                       aux_scale=1.0 / (1.0 - ctx.ff.p))
                 ctx.ff.premasked = True
             elif fused:
                 dx = torch.empty_like(x)
-                rgemm(dy, to_bf16(W, trans=True), dx, M=M, N=K, K=N)
+                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N)
             elif park is not None:
                 dx = park
                 gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0, precision=ctx.precision)

@@ -37,4 +37,6 @@ class FlatAdamW(torch.optim.Optimizer):
         f = self.flat
         lib('c2dsr_adamw', f.param, f.fresh, f.accum if self.accumulate else None, self.m, self.v, self.vmax, f.numel,
             float(g['lr']), float(g['weight_decay']), float(b1), float(b2), float(g['eps']), self.n_steps, stream())
+        from .ops import WEIGHTS
+        WEIGHTS.bump()  # the weights' bf16 images are stale now
         return None
