@@ -43,6 +43,68 @@ __global__ void pool_bwd_kernel(const float* __restrict__ dout, const float* __r
   *o = c2::fma4(wt, g, *o);
 }
 
+// out1[b] = Σ_l h[b,l]·w1[b,l]  (and out2[b] = Σ_l h[b,l]·w2[b,l] when w2 is given: one read of h for
+// both poolings of h_share).  One block per b: the four waves take rows l ≡ w (mod 4), float4 per
+// lane (d <= 256 per pass over c), rows whose weights are all 0 (padding / non-target positions) are
+// not read; the wave partials are added in wave order (deterministic).
+__global__ __launch_bounds__(256) void pool2_fwd_kernel(const float* __restrict__ h, const float* __restrict__ w1,
+                                                        const float* __restrict__ w2, int B, int L, int d,
+                                                        float* __restrict__ out1, float* __restrict__ out2) {
+  __shared__ float4 red[2][4][64];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float* hb = h + (long)b * L * d;
+  const float* wa = w1 + (long)b * L;
+  const float* wb = w2 ? w2 + (long)b * L : nullptr;
+  for (int c0 = 0; c0 < d; c0 += 256) {
+    const int c = c0 + lane * 4;
+    const bool cin = c < d;
+    float4 a1 = c2::f4(0.f), a2 = c2::f4(0.f);
+    for (int l0 = w; l0 < L; l0 += 16) {
+      float x1[4], x2[4];
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int l = l0 + 4 * u;
+        x1[u] = l < L ? wa[l] : 0.f;
+        x2[u] = (wb && l < L) ? wb[l] : 0.f;
+        v[u] = (cin && (x1[u] != 0.f || x2[u] != 0.f)) ? *(const float4*)(hb + (long)l * d + c) : c2::f4(0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a1 = c2::fma4(x1[u], v[u], a1);
+        a2 = c2::fma4(x2[u], v[u], a2);
+      }
+    }
+    red[0][w][lane] = a1;
+    red[1][w][lane] = a2;
+    __syncthreads();
+    if (w < 2 && cin && (w == 0 || out2)) {
+      float4 t = red[w][0][lane];
+      for (int k = 1; k < 4; ++k) t = t + red[w][k][lane];
+      *(float4*)((w ? out2 : out1) + (long)b * d + c) = t;
+    }
+    __syncthreads();
+  }
+}
+
+// dh[b,l] = (accumulate ? dh[b,l] : 0) + d1[b]·w1[b,l] (+ d2[b]·w2[b,l])   (float4 per thread)
+__global__ void pool2_bwd_kernel(const float* __restrict__ d1, const float* __restrict__ w1,
+                                 const float* __restrict__ d2, const float* __restrict__ w2, int B, int L, int d,
+                                 int accumulate, float* __restrict__ dh) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
+  if (i >= (long)B * L * d / 4) return;
+  const long e = i * 4;
+  const int c = (int)(e % d);
+  const long bl = e / d;
+  const long b = bl / L;
+  const float x1 = w1[bl], x2 = d2 ? w2[bl] : 0.f;
+  float4 o = accumulate ? *(const float4*)(dh + e) : c2::f4(0.f);
+  if (x1 != 0.f) o = c2::fma4(x1, *(const float4*)(d1 + b * d + c), o);
+  if (x2 != 0.f) o = c2::fma4(x2, *(const float4*)(d2 + b * d + c), o);
+  *(float4*)(dh + e) = o;
+}
+
 // out[r*ldo] = Σ_c x[r*ldx + c] * y[r*ldy + c] + (bias ? bias[0] : 0); one wave per row
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ x, long ldx, const float* __restrict__ y,
                                                      long ldy, int M, int d, const float* __restrict__ bias,
@@ -273,6 +335,22 @@ C2_API int c2dsr_pool_bwd(const float* dout, const float* w, int B, int L, int d
   const long n = (long)B * L * d / 4;
   if (n == 0 || d % 4) return n == 0 ? 0 : (int)hipErrorInvalidValue;
   pool_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dout, w, B, L, d, dh);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_pool2_fwd(const float* h, const float* w1, const float* w2, int B, int L, int d, float* out1,
+                           float* out2, void* stream) {
+  if (B == 0) return 0;
+  if (d % 4 || (w2 && !out2)) return (int)hipErrorInvalidValue;
+  pool2_fwd_kernel<<<B, 256, 0, (hipStream_t)stream>>>(h, w1, w2, B, L, d, out1, out2);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, const float* w2, int B, int L, int d,
+                           int accumulate, float* dh, void* stream) {
+  const long n = (long)B * L * d / 4;
+  if (n == 0 || d % 4) return n == 0 ? 0 : (int)hipErrorInvalidValue;
+  pool2_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(d1, w1, d2, w2, B, L, d, accumulate, dh);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -72,12 +72,11 @@ class LossHeadFn(Function):
         Phy = torch.empty(B, d, **f32)
         X2a = torch.empty(2 * B, d, **f32)  # [h_share·wb ; h_neg_a·wa]
         X2b = torch.empty(2 * B, d, **f32)  # [h_share·wa ; h_neg_b·wb]
-        lib('c2dsr_pool_fwd', hx, wa, B, L, d, Phx, s)
-        lib('c2dsr_pool_fwd', hy, wb, B, L, d, Phy, s)
-        lib('c2dsr_pool_fwd', h_share, wb, B, L, d, X2a, s)
-        lib('c2dsr_pool_fwd', h_neg_a, wa, B, L, d, X2a[B:], s)
-        lib('c2dsr_pool_fwd', h_share, wa, B, L, d, X2b, s)
-        lib('c2dsr_pool_fwd', h_neg_b, wb, B, L, d, X2b[B:], s)
+        lib('c2dsr_pool2_fwd', hx, wa, None, B, L, d, Phx, None, s)
+        lib('c2dsr_pool2_fwd', hy, wb, None, B, L, d, Phy, None, s)
+        lib('c2dsr_pool2_fwd', h_share, wb, wa, B, L, d, X2a, X2b, s)  # both poolings of h_share (Q5), one read
+        lib('c2dsr_pool2_fwd', h_neg_a, wa, None, B, L, d, X2a[B:], None, s)
+        lib('c2dsr_pool2_fwd', h_neg_b, wb, None, B, L, d, X2b[B:], None, s)
         # ---- bilinear: s = x1ᵀ W x2 (+b)  via  U = X2·Wᵀ, s = rowdot(x1, U) ----
         Ua = torch.empty(2 * B, d, **f32)
         Ub = torch.empty(2 * B, d, **f32)
@@ -164,11 +163,40 @@ class LossHeadFn(Function):
         s = stream()
         f32 = dict(device=dev, dtype=torch.float32)
         gscale = gloss.contiguous().reshape(1)
-        dh_share = torch.zeros(B, L, d, **f32)
-        dhx = torch.zeros(B, L, d, **f32)
-        dhy = torch.zeros(B, L, d, **f32)
-        dh_na = torch.zeros(B, L, d, **f32)
-        dh_nb = torch.zeros(B, L, d, **f32)
+        # ---- discriminators ----
+        Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi
+        lib('c2dsr_scale_ds', dS, 4 * B, gscale, float(1.0 - m.lam), s)
+        dP = {}
+        for (x1, X2, U, Wd, bd, k) in ((Phx, X2a, Ua, m.Da_w, m.Da_b, 0), (Phy, X2b, Ub, m.Db_w, m.Db_b, 2)):
+            dx1 = torch.empty(B, d, **f32)
+            lib('c2dsr_rowscale', U, dS[k], B * d, d, dx1, 0, s)
+            lib('c2dsr_rowscale', U[B:], dS[k + 1], B * d, d, dx1, 1, s)
+            dU = torch.empty(2 * B, d, **f32)
+            lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
+            lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
+            dX2 = torch.empty(2 * B, d, **f32)
+            gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
+            gWd = _grad_target(Wd)
+            if gWd is not None:
+                gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
+            gbd = _grad_target(bd)
+            if gbd is not None:
+                colsum(dS[k], 2 * B, 1, 1, gbd)
+            dP[k] = (dx1, dX2)
+        (dPhx, dX2a), (dPhy, dX2b) = dP[0], dP[2]
+        wa, wb = ctx.w
+        # the pooling backward WRITES the five encoder-output gradients (no zero fill); the classifier
+        # heads below add their last-R-position parts
+        dh_share = torch.empty(B, L, d, **f32)
+        dhx = torch.empty(B, L, d, **f32)
+        dhy = torch.empty(B, L, d, **f32)
+        dh_na = torch.empty(B, L, d, **f32)
+        dh_nb = torch.empty(B, L, d, **f32)
+        lib('c2dsr_pool2_bwd', dPhx, wa, None, None, B, L, d, 0, dhx, s)
+        lib('c2dsr_pool2_bwd', dPhy, wb, None, None, B, L, d, 0, dhy, s)
+        lib('c2dsr_pool2_bwd', dX2a, wb, dX2b, wa, B, L, d, 0, dh_share, s)
+        lib('c2dsr_pool2_bwd', dX2a[B:], wa, None, None, B, L, d, 0, dh_na, s)
+        lib('c2dsr_pool2_bwd', dX2b[B:], wb, None, None, B, L, d, 0, dh_nb, s)
         # ---- classifier heads ----
         gwpad, gbpad = _grad_target(m.wpad), _grad_target(m.bpad)
         for (Hcat, Hpad, tcat, logits, lse, rows, W, bias, n), coef, hdom_grad in zip(ctx.heads, ctx.coefs,
@@ -224,32 +252,4 @@ class LossHeadFn(Function):
             if gbpad is not None:
                 colsum(pad_col, M2, 1, pad_ld, gbpad)
             lib('c2dsr_rec_scatter', dHcat, dHpad, B, L, d, R, dh_share, hdom_grad, s)
-        # ---- discriminators ----
-        Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi
-        lib('c2dsr_scale_ds', dS, 4 * B, gscale, float(1.0 - m.lam), s)
-        dP = {}
-        for (x1, X2, U, Wd, bd, k) in ((Phx, X2a, Ua, m.Da_w, m.Da_b, 0), (Phy, X2b, Ub, m.Db_w, m.Db_b, 2)):
-            dx1 = torch.empty(B, d, **f32)
-            lib('c2dsr_rowscale', U, dS[k], B * d, d, dx1, 0, s)
-            lib('c2dsr_rowscale', U[B:], dS[k + 1], B * d, d, dx1, 1, s)
-            dU = torch.empty(2 * B, d, **f32)
-            lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
-            lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
-            dX2 = torch.empty(2 * B, d, **f32)
-            gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
-            gWd = _grad_target(Wd)
-            if gWd is not None:
-                gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
-            gbd = _grad_target(bd)
-            if gbd is not None:
-                colsum(dS[k], 2 * B, 1, 1, gbd)
-            dP[k] = (dx1, dX2)
-        (dPhx, dX2a), (dPhy, dX2b) = dP[0], dP[2]
-        wa, wb = ctx.w
-        lib('c2dsr_pool_bwd', dPhx, wa, B, L, d, dhx, s)
-        lib('c2dsr_pool_bwd', dPhy, wb, B, L, d, dhy, s)
-        lib('c2dsr_pool_bwd', dX2a, wb, B, L, d, dh_share, s)
-        lib('c2dsr_pool_bwd', dX2a[B:], wa, B, L, d, dh_na, s)
-        lib('c2dsr_pool_bwd', dX2b, wa, B, L, d, dh_share, s)
-        lib('c2dsr_pool_bwd', dX2b[B:], wb, B, L, d, dh_nb, s)
         return dh_share, dhx, dhy, dh_na, dh_nb, None

@@ -106,6 +106,13 @@ int c2dsr_relu_drop_bwd(const float* dy, const float* y, long n, float p, float*
 int c2dsr_pool_weights(const int64_t* gm, int B, int L, float* w, void* stream);
 int c2dsr_pool_fwd(const float* h, const float* w, int B, int L, int d, float* out, void* stream);
 int c2dsr_pool_bwd(const float* dout, const float* w, int B, int L, int d, float* dh, void* stream);
+/* two poolings of one h in one read (rows with zero weights skipped): out1[b] = Σ_l h[b,l]·w1[b,l],
+ * out2[b] = Σ_l h[b,l]·w2[b,l] (w2 may be null); and the backward in write or accumulate mode:
+ * dh[b,l] = (accumulate ? dh[b,l] : 0) + d1[b]·w1[b,l] + d2[b]·w2[b,l] (d2 may be null). */
+int c2dsr_pool2_fwd(const float* h, const float* w1, const float* w2, int B, int L, int d, float* out1, float* out2,
+                    void* stream);
+int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, const float* w2, int B, int L, int d,
+                    int accumulate, float* dh, void* stream);
 int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int d, const float* bias, float* out,
                  long ldo, void* stream);
 /* loss_mi = Σ_k Σ_b BCE(s_k[b], y_k)/B_norm, ds = (σ(s)-y)/B_norm; s = [sim_a_pos; sim_a_neg; sim_b_pos; sim_b_neg] */
