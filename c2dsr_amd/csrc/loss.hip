@@ -105,6 +105,90 @@ __global__ void pool2_bwd_kernel(const float* __restrict__ d1, const float* __re
   *(float4*)(dh + e) = o;
 }
 
+// Valid-row compaction of a classifier head's targets (rows with t == ignore contribute nothing to the
+// loss or to any gradient, trainer.py:131-154 / F.cross_entropy(ignore_index)): one workgroup,
+// contiguous per-thread ranges, stable.  idx[k] = k-th valid row, inv[r] = its compact index or -1,
+// tc[k] = t[idx[k]], counts = (valid rows in [0, split), valid rows in [split, M)).
+__global__ __launch_bounds__(1024) void compact_valid_kernel(const int64_t* __restrict__ t, int M, int split,
+                                                             int ignore, int* __restrict__ idx, int* __restrict__ inv,
+                                                             int64_t* __restrict__ tc, int* __restrict__ counts) {
+  __shared__ int part[1024];
+  __shared__ int part_lo[1024];
+  const int th = threadIdx.x;
+  const int per = (M + 1023) / 1024;
+  const int lo = min(M, th * per), hi = min(M, lo + per);
+  int c = 0, clo = 0;
+  for (int r = lo; r < hi; ++r) {
+    const bool v = t[r] != ignore;
+    c += v;
+    clo += v && r < split;
+  }
+  part[th] = c;
+  part_lo[th] = clo;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int a = th >= o ? part[th - o] : 0, b = th >= o ? part_lo[th - o] : 0;
+    __syncthreads();
+    part[th] += a;
+    part_lo[th] += b;
+    __syncthreads();
+  }
+  int k = part[th] - c;
+  for (int r = lo; r < hi; ++r) {
+    const int64_t tr = t[r];
+    if (tr != ignore) {
+      idx[k] = r;
+      inv[r] = k;
+      tc[k] = tr;
+      ++k;
+    } else {
+      inv[r] = -1;
+    }
+  }
+  if (th == 1023) {
+    counts[0] = part_lo[1023];
+    counts[1] = part[1023] - part_lo[1023];
+  }
+}
+
+// dst[k][c] = src[idx[k]·ld + c]   (k < n, c < d; float4 when d % 4 == 0 and ld % 4 == 0)
+__global__ void gather_rows_kernel(const float* __restrict__ src, long ld, const int* __restrict__ idx, int n, int d,
+                                   float* __restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d % 4 == 0 && ld % 4 == 0) {
+    const int d4 = d / 4;
+    if (i >= (long)n * d4) return;
+    const long k = i / d4;
+    const int c = (int)(i % d4) * 4;
+    *(float4*)(dst + k * d + c) = *(const float4*)(src + (long)idx[k] * ld + c);
+  } else {
+    if (i >= (long)n * d) return;
+    const long k = i / d;
+    const int c = (int)(i % d);
+    dst[k * d + c] = src[(long)idx[k] * ld + c];
+  }
+}
+
+// dst[r][c] = inv[r] >= 0 ? src[inv[r]·d + c] : 0   (r < M)
+__global__ void expand_rows_kernel(const float* __restrict__ src, const int* __restrict__ inv, int M, int d,
+                                   float* __restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d % 4 == 0) {
+    const int d4 = d / 4;
+    if (i >= (long)M * d4) return;
+    const long r = i / d4;
+    const int c = (int)(i % d4) * 4;
+    const int k = inv[r];
+    *(float4*)(dst + r * d + c) = k >= 0 ? *(const float4*)(src + (long)k * d + c) : c2::f4(0.f);
+  } else {
+    if (i >= (long)M * d) return;
+    const long r = i / d;
+    const int c = (int)(i % d);
+    const int k = inv[r];
+    dst[r * d + c] = k >= 0 ? src[(long)k * d + c] : 0.f;
+  }
+}
+
 // out[r*ldo] = Σ_c x[r*ldx + c] * y[r*ldy + c] + (bias ? bias[0] : 0); one wave per row
 __global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ x, long ldx, const float* __restrict__ y,
                                                      long ldy, int M, int d, const float* __restrict__ bias,
@@ -351,6 +435,27 @@ C2_API int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, co
   const long n = (long)B * L * d / 4;
   if (n == 0 || d % 4) return n == 0 ? 0 : (int)hipErrorInvalidValue;
   pool2_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(d1, w1, d2, w2, B, L, d, accumulate, dh);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, int* idx, int* inv, int64_t* tc,
+                               int* counts, void* stream) {
+  if (M <= 0) return M == 0 ? 0 : (int)hipErrorInvalidValue;
+  compact_valid_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(t, M, split, ignore, idx, inv, tc, counts);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_gather_rows(const float* src, long ld, const int* idx, int n, int d, float* dst, void* stream) {
+  if (n <= 0 || d <= 0) return 0;
+  const long work = (d % 4 == 0 && ld % 4 == 0) ? (long)n * d / 4 : (long)n * d;
+  gather_rows_kernel<<<c2::ceil_div(work, 256), 256, 0, (hipStream_t)stream>>>(src, ld, idx, n, d, dst);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_expand_rows(const float* src, const int* inv, int M, int d, float* dst, void* stream) {
+  if (M <= 0 || d <= 0) return 0;
+  const long work = d % 4 == 0 ? (long)M * d / 4 : (long)M * d;
+  expand_rows_kernel<<<c2::ceil_div(work, 256), 256, 0, (hipStream_t)stream>>>(src, inv, M, d, dst);
   C2_CHECK_LAUNCH();
   return 0;
 }

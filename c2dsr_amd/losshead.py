@@ -95,47 +95,75 @@ class LossHeadFn(Function):
         fused = m.precision == BF16 and bool(lib.raw('c2dsr_ce_supported')(d))
         ctx.fused = fused
         heads = []
-        for (hdom, W, bias, t_share, t_spec, n) in ((hx, m.Wa, m.ba, m.gt_share_a, m.gt_a, m.n_a),
-                                                   (hy, m.Wb, m.bb, m.gt_share_b, m.gt_b, m.n_b)):
-            Hcat = torch.empty(2 * BR, d, **f32)
-            Hpad = torch.empty(2 * BR, d, **f32)
+        specs = ((hx, m.Wa, m.ba, m.gt_share_a, m.gt_a, m.n_a), (hy, m.Wb, m.bb, m.gt_share_b, m.gt_b, m.n_b))
+        M2 = 2 * BR
+        pre = []
+        for (hdom, W, bias, t_share, t_spec, n) in specs:
+            Hcat = torch.empty(M2, d, **f32)
+            Hpad = torch.empty(M2, d, **f32)
             lib('c2dsr_rec_gather', h_share, hdom, B, L, d, R, Hcat, Hpad, s)
-            tcat = torch.empty(2 * BR, device=dev, dtype=torch.int64)
+            tcat = torch.empty(M2, device=dev, dtype=torch.int64)
             lib('c2dsr_rec_targets', t_share, t_spec, B, L, R, tcat, s)
-            lse = torch.empty(2 * BR, **f32)
-            rows = torch.empty(2 * BR, **f32)
+            comp = None
             if fused:
-                M2 = 2 * BR
-                M_pad = -(-M2 // 64) * 64
+                # rows whose target is the ignore index contribute nothing to the loss or any gradient
+                # (trainer.py:131-154): the fused CE runs on the valid rows only (stable compaction)
+                idx = torch.empty(M2, device=dev, dtype=torch.int32)
+                inv = torch.empty(M2, device=dev, dtype=torch.int32)
+                tc = torch.empty(M2, device=dev, dtype=torch.int64)
+                cnt = torch.empty(2, device=dev, dtype=torch.int32)
+                lib('c2dsr_compact_valid', tcat, M2, BR, n, idx, inv, tc, cnt, s)
+                comp = (idx, inv, tc, cnt)
+            pre.append((Hcat, Hpad, tcat, comp))
+        if fused:  # one host read of both heads' valid-row counts (sizes the compact launches)
+            counts = torch.cat([c[3][3] for c in pre]).tolist()
+        for k, ((hdom, W, bias, t_share, t_spec, n), (Hcat, Hpad, tcat, comp)) in enumerate(zip(specs, pre)):
+            lse = torch.empty(M2, **f32)
+            rows = torch.empty(M2, **f32)
+            if fused:
+                idx, inv, tc, _ = comp
+                Mv0, Mv1 = counts[2 * k], counts[2 * k + 1]
+                Mv = Mv0 + Mv1
+                M_pad = max(64, -(-Mv // 64) * 64)
                 n_pad = -(-n // 128) * 128 + 64  # + a 64-value tail: tiles near n DMA 64 constants
+                Hc = torch.empty(Mv, d, **f32)
+                lib('c2dsr_gather_rows', Hcat, d, idx, Mv, d, Hc, s)
                 Hb = torch.empty(M_pad, d, device=dev, dtype=torch.bfloat16)  # whole 64-row H tiles (dW sweep)
-                if M_pad > M2:
-                    Hb[M2:].zero_()
+                if M_pad > Mv:
+                    Hb[Mv:].zero_()
                 n64 = -(-n // 64) * 64  # whole 64-row W tiles for the LDS-DMA (zero rows past n)
                 Wb = torch.empty(n64, d, device=dev, dtype=torch.bfloat16)
                 if n64 > n:
                     Wb[n:].zero_()
-                lib('c2dsr_f32_to_bf16', Hcat, Hcat.numel(), Hb, s)
+                if Mv:
+                    lib('c2dsr_f32_to_bf16', Hc, Hc.numel(), Hb, s)
                 lib('c2dsr_f32_to_bf16', W, W.numel(), Wb, s)
                 bias2 = torch.empty(n_pad, **f32)
                 lib('c2dsr_ce_bias2', bias, n, n_pad, bias2, s)
                 padlogit = torch.empty(M2, **f32)
                 lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, M2, d, m.bpad, padlogit, 1, s)
-                ns = split_count(M2, 256)
-                pm = torch.empty(ns, M2, **f32)
-                ps = torch.empty(ns, M2, **f32)
+                padc = torch.empty(max(Mv, 1), **f32)
+                lib('c2dsr_gather_rows', padlogit, 1, idx, Mv, 1, padc, s)
+                lse_c = torch.empty(max(Mv, 1), **f32)
+                rows_c = torch.empty(max(Mv, 1), **f32)
                 lse2 = torch.empty(M_pad, **f32)
-                lib('c2dsr_ce_fused_fwd', Hb, Wb, bias2, M2, n, d, ns, pm, ps, padlogit, tcat, Hcat, W, bias, lse,
-                    lse2, rows, s)
+                if Mv:
+                    ns = split_count(Mv, 256)
+                    pm = torch.empty(ns, Mv, **f32)
+                    ps = torch.empty(ns, Mv, **f32)
+                    lib('c2dsr_ce_fused_fwd', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, padc, tc, Hc, W, bias, lse_c,
+                        lse2, rows_c, s)
+                lib('c2dsr_expand_rows', rows_c, inv, M2, 1, rows, s)  # per-row losses, 0 on ignored rows
                 # target sort for the one-hot part of dW/db, on the side stream under the rest of the step
-                tplan = IndexPlan(tcat, n + 1) if any(ctx.needs_input_grad[:5]) and W.requires_grad else None
-                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padlogit, lse2, bias2, tplan), lse, rows, W, bias, n))
+                tplan = IndexPlan(tc[:Mv], n + 1) if Mv and any(ctx.needs_input_grad[:5]) and W.requires_grad else None
+                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padc, lse2, bias2, tplan, Hc, tc, inv, Mv, Mv0, lse_c), lse,
+                              rows, W, bias, n))
             else:
                 ld = n + 1
-                logits = torch.empty(2 * BR, ld, **f32)
-                gemm(Hcat, W, logits, M=2 * BR, N=n, K=d, transB=1, ldc=ld, bias=bias, precision=m.precision)
-                lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, 2 * BR, d, m.bpad, logits[:, n:], ld, s)
-                lib('c2dsr_ce_fwd', logits, ld, 2 * BR, ld, tcat, n, lse, rows, s)
+                logits = torch.empty(M2, ld, **f32)
+                gemm(Hcat, W, logits, M=M2, N=n, K=d, transB=1, ldc=ld, bias=bias, precision=m.precision)
+                lib('c2dsr_rowdot', Hpad, d, m.wpad, 0, M2, d, m.bpad, logits[:, n:], ld, s)
+                lib('c2dsr_ce_fwd', logits, ld, M2, ld, tcat, n, lse, rows, s)
                 heads.append((Hcat, Hpad, tcat, logits, lse, rows, W, bias, n))
         out3 = torch.empty(3, **f32)
         coefA = torch.empty(2, **f32)
@@ -206,36 +234,42 @@ class LossHeadFn(Function):
             dHpad = torch.zeros(M2, d, **f32)
             gW, gb = _grad_target(W), _grad_target(bias)
             if ctx.fused:
-                Hb, Wb, padlogit, lse2, bias2, tplan = logits
+                Hb, Wb, padc, lse2, bias2, tplan, Hc, tc, inv, Mv, Mv0, lse_c = logits
                 M_pad = lse2.shape[0]
                 rw = torch.empty(M_pad, **f32)
                 t32 = torch.empty(M_pad, device=dev, dtype=torch.int32)
-                dpad = torch.empty(M2, **f32)
+                dpad_c = torch.empty(max(Mv, 1), **f32)
                 crow = torch.empty(M_pad, **f32)
-                lib('c2dsr_ce_row_weights', tcat, M2, M_pad, n, coef, BR, gscale, float(m.lam), padlogit, lse, rw, t32,
-                    lse2, crow, dpad, s)
-                ns = split_count(M2, 128)
-                dHp = torch.empty(ns, M2, d, **f32)
-                lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M2, n, d, ns, crow, dHp, s)
-                lib('c2dsr_ce_dh_combine', dHp, ns, M2, d, t32, rw, W, n, dHcat, s)
-                del dHp
-                nr = split_count(n, 128)
-                dWp = torch.empty(nr, n, d, **f32)
-                dbp = torch.empty(nr, n, **f32)
-                lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M2, n, d, nr, crow, dWp, dbp, s)
-                if gW is not None:
-                    lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
-                if gb is not None:
-                    lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
-                del dWp, dbp
-                if (gW is not None or gb is not None) and tplan is not None:
-                    wsb = int(lib.raw('c2dsr_ce_onehot_planned_workspace')(M2, n, d))
-                    ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
-                    lib('c2dsr_ce_onehot_dw_planned', tplan.get(), M2, n, Hcat, d, rw, gW, gb, ws, wsb, s)
-                elif gW is not None or gb is not None:
-                    wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M2, n, d))
-                    ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
-                    lib('c2dsr_ce_onehot_dw', tcat, M2, n, Hcat, d, rw, gW, gb, ws, wsb, s)
+                dHc = torch.empty(max(Mv, 1), d, **f32)
+                if Mv:
+                    # compact rows keep their order: the first Mv0 are the shared-sequence rows (coef[0])
+                    lib('c2dsr_ce_row_weights', tc, Mv, M_pad, n, coef, Mv0, gscale, float(m.lam), padc, lse_c, rw,
+                        t32, lse2, crow, dpad_c, s)
+                    ns = split_count(Mv, 128)
+                    dHp = torch.empty(ns, Mv, d, **f32)
+                    lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, Mv, n, d, ns, crow, dHp, s)
+                    lib('c2dsr_ce_dh_combine', dHp, ns, Mv, d, t32, rw, W, n, dHc, s)
+                    del dHp
+                    nr = split_count(n, 128)
+                    dWp = torch.empty(nr, n, d, **f32)
+                    dbp = torch.empty(nr, n, **f32)
+                    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)
+                    if gW is not None:
+                        lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
+                    if gb is not None:
+                        lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
+                    del dWp, dbp
+                    if (gW is not None or gb is not None) and tplan is not None:
+                        wsb = int(lib.raw('c2dsr_ce_onehot_planned_workspace')(Mv, n, d))
+                        ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+                        lib('c2dsr_ce_onehot_dw_planned', tplan.get(), Mv, n, Hc, d, rw, gW, gb, ws, wsb, s)
+                    elif gW is not None or gb is not None:
+                        wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(Mv, n, d))
+                        ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+                        lib('c2dsr_ce_onehot_dw', tc, Mv, n, Hc, d, rw, gW, gb, ws, wsb, s)
+                lib('c2dsr_expand_rows', dHc, inv, M2, d, dHcat, s)  # 0 on ignored rows
+                dpad = torch.empty(M2, **f32)
+                lib('c2dsr_expand_rows', dpad_c, inv, M2, 1, dpad, s)
                 pad_col, pad_ld = dpad, 1
             else:
                 ld = n + 1

@@ -113,6 +113,15 @@ int c2dsr_pool2_fwd(const float* h, const float* w1, const float* w2, int B, int
                     void* stream);
 int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, const float* w2, int B, int L, int d,
                     int accumulate, float* dh, void* stream);
+/* Valid-row compaction of a classifier head's targets (trainer.py:131-154: rows whose target is the
+ * ignore_index contribute nothing to the loss or any gradient, so the fused CE runs on the valid
+ * rows only).  Stable: idx[k] = k-th row with t != ignore, inv[r] = compact index or -1, tc[k] =
+ * t[idx[k]], counts[0..1] = valid rows in [0, split) and [split, M).  One workgroup. */
+int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, int* idx, int* inv, int64_t* tc, int* counts,
+                        void* stream);
+/* dst[k][:] = src[idx[k]·ld + :] (k < n);  dst[r][:] = inv[r] >= 0 ? src[inv[r]][:] : 0 (r < M) */
+int c2dsr_gather_rows(const float* src, long ld, const int* idx, int n, int d, float* dst, void* stream);
+int c2dsr_expand_rows(const float* src, const int* inv, int M, int d, float* dst, void* stream);
 int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int d, const float* bias, float* out,
                  long ldo, void* stream);
 /* loss_mi = Σ_k Σ_b BCE(s_k[b], y_k)/B_norm, ds = (σ(s)-y)/B_norm; s = [sim_a_pos; sim_a_neg; sim_b_pos; sim_b_neg] */
