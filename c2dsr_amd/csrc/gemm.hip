@@ -44,6 +44,7 @@ struct Epi {
   int relu;
   c2::Drop drop;
   int64_t row_base;
+  const int* rowmap;  // dropout row index = row_base + (rowmap ? rowmap[row] : row)
 };
 
 // Operand tile loader: fills S[r][k] (r over BM or BN rows, k over BK) from a global
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(int M, int N, int K, cons
           v += bcol;
           if (ep.relu) {
             v = fmaxf(v, 0.f);
-            v *= ep.drop.mul((uint64_t)(ep.row_base + row) * N + col);
+            v *= ep.drop.mul((uint64_t)(ep.row_base + (ep.rowmap ? ep.rowmap[row] : row)) * N + col);
           }
           *cp = v;
         }
@@ -281,12 +282,13 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // epilogue 1 = relu then dropout(p) with index (row_base+row)*N + col.
 C2_API int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
                       float* C, int ldc, float alpha, float beta, const float* bias, int epilogue, uint32_t k0,
-                      uint32_t k1, float p, int64_t row_base, int precision, int split_k, void* stream) {
+                      uint32_t k1, float p, int64_t row_base, const int* rowmap, int precision, int split_k,
+                      void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0) {
     // C = beta*C + bias
-    Epi ep{0.f, beta, bias, 0, c2::make_drop(0, 0, 0.f), 0};
+    Epi ep{0.f, beta, bias, 0, c2::make_drop(0, 0, 0.f), 0, nullptr};
     (void)ep;
     scale_kernel<<<c2::ceil_div((long)M * N, 256), 256, 0, s>>>(C, M, N, ldc, beta);
     if (bias) return (int)hipErrorInvalidValue;
@@ -308,7 +310,7 @@ C2_API int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* 
   const bool a_ok = al16(A) && lda % 4 == 0 && (transA ? M % 4 == 0 : K % 4 == 0);
   const bool b_ok = al16(B) && ldb % 4 == 0 && (transB ? K % 4 == 0 : N % 4 == 0);
   const bool vec = a_ok && b_ok;
-  Epi ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base};
+  Epi ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base, rowmap};
   int atomic = 0;
   if (splits > 1) {
     if (beta != 1.f) scale_kernel<<<c2::ceil_div((long)M * N, 256), 256, 0, s>>>(C, M, N, ldc, beta);

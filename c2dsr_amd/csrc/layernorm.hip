@@ -15,6 +15,7 @@ constexpr int MAXC = 4;  // float4 chunks per lane → d <= 16*LPR
 template <int LPR, int NC>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                          int rows, int d, c2::Drop drop, int64_t idx_base,
+                                                         const int* __restrict__ rowmap,
                                                          const float* __restrict__ gw, const float* __restrict__ gb,
                                                          float eps, float* __restrict__ xsave, float* __restrict__ y,
                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out) {
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
       if (b) {
         float4 u = *(const float4*)(b + r * d + c);
         if (drop.active()) {
-          const uint64_t bi = (uint64_t)(idx_base + r) * d + c;
+          const uint64_t bi = (uint64_t)(idx_base + (rowmap ? rowmap[r] : r)) * d + c;
           u = u * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
         }
         v = v + u;
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
                                                      const float* __restrict__ dy, int rows, int d,
                                                      float* __restrict__ dx, int dx_accumulate,
                                                      float* __restrict__ db_out, c2::Drop drop, int64_t idx_base,
-                                                     float* __restrict__ part) {
+                                                     const int* __restrict__ rowmap, float* __restrict__ part) {
   constexpr int GROUPS = 256 / LPR;
   constexpr int RB = 2;
   const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
           }
           if (db_out) {
             if (drop.active()) {
-              const uint64_t bi = (uint64_t)(idx_base + r) * d + c;
+              const uint64_t bi = (uint64_t)(idx_base + (rowmap ? rowmap[r] : r)) * d + c;
               o = o * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
             }
             *(float4*)(db_out + r * d + c) = o;
@@ -246,15 +247,15 @@ C2_API size_t c2dsr_ln_bwd_workspace(int d) { return (size_t)LN_BWD_BLOCKS * 2 *
 
 // y = LN(a + drop(b)) * w + bias; a or b may be null.  xsave (LN input) optional.
 C2_API int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
-                            int64_t idx_base, const float* w, const float* bias, float eps, float* xsave, float* y,
-                            float* mean, float* rstd, void* stream) {
+                            int64_t idx_base, const int* rowmap, const float* w, const float* bias, float eps,
+                            float* xsave, float* y, float* mean, float* rstd, void* stream) {
   if (d % 4 || d > 1024) return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
   const int lpr = lpr_for(d);
   dim3 grid(c2::ceil_div(rows, 256 / lpr));
-#define C2_LN(L, NC) add_ln_fwd_kernel<L, NC><<<grid, 256, 0, s>>>(a, b, rows, d, dr, idx_base, w, bias, eps, xsave, y, mean, rstd)
+#define C2_LN(L, NC) add_ln_fwd_kernel<L, NC><<<grid, 256, 0, s>>>(a, b, rows, d, dr, idx_base, rowmap, w, bias, eps, xsave, y, mean, rstd)
 #define C2_LNC(L)                                   \
   switch (c2::ceil_div(d, 4 * L)) {                 \
     case 1: C2_LN(L, 1); break;                     \
@@ -279,7 +280,7 @@ C2_API int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uin
 // dgw/dgb += Σ_rows (accumulated; may be null).
 C2_API int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, const float* w, const float* dy, int rows,
                         int d, float* dx, int dx_accumulate, float* db_out, uint32_t k0, uint32_t k1, float p,
-                        int64_t idx_base, float* dgw, float* dgb, void* workspace, void* stream) {
+                        int64_t idx_base, const int* rowmap, float* dgw, float* dgb, void* workspace, void* stream) {
   if (d % 4 || d > 1024) return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
   c2::Drop dr = c2::make_drop(k0, k1, p);
@@ -290,7 +291,7 @@ C2_API int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, co
   if (nblk > LN_BWD_BLOCKS) nblk = LN_BWD_BLOCKS;
   float* part = (float*)workspace;
 #define C2_LNB(L, NC) \
-  ln_bwd_kernel<L, NC><<<nblk, 256, 0, s>>>(x, mean, rstd, w, dy, rows, d, dx, dx_accumulate, db_out, dr, idx_base, part)
+  ln_bwd_kernel<L, NC><<<nblk, 256, 0, s>>>(x, mean, rstd, w, dy, rows, d, dx, dx_accumulate, db_out, dr, idx_base, rowmap, part)
 #define C2_LNBC(L)                                  \
   switch (c2::ceil_div(d, 4 * L)) {                 \
     case 1: C2_LNB(L, 1); break;                    \

@@ -105,50 +105,147 @@ __global__ void pool2_bwd_kernel(const float* __restrict__ d1, const float* __re
   *(float4*)(dh + e) = o;
 }
 
-// Valid-row compaction of a classifier head's targets (rows with t == ignore contribute nothing to the
-// loss or to any gradient, trainer.py:131-154 / F.cross_entropy(ignore_index)): one workgroup,
-// contiguous per-thread ranges, stable.  idx[k] = k-th valid row, inv[r] = its compact index or -1,
-// tc[k] = t[idx[k]], counts = (valid rows in [0, split), valid rows in [split, M)).
-__global__ __launch_bounds__(1024) void compact_valid_kernel(const int64_t* __restrict__ t, int M, int split,
-                                                             int ignore, int* __restrict__ idx, int* __restrict__ inv,
-                                                             int64_t* __restrict__ tc, int* __restrict__ counts) {
-  __shared__ int part[1024];
-  __shared__ int part_lo[1024];
-  const int th = threadIdx.x;
-  const int per = (M + 1023) / 1024;
-  const int lo = min(M, th * per), hi = min(M, lo + per);
-  int c = 0, clo = 0;
-  for (int r = lo; r < hi; ++r) {
-    const bool v = t[r] != ignore;
-    c += v;
-    clo += v && r < split;
+// Stable multi-set row compaction over M rows, two launches: block b covers rows [b·1024, (b+1)·1024)
+// in four rounds of 256 (one row per lane, coalesced reads); membership of every set comes from one
+// Op::mask(r) bit per set; a row's compact index is (rows of the set in earlier blocks) + (earlier
+// waves and rounds of its block) + (lower lanes of its ballot).  The count pass writes per-block set
+// sizes bc[b·NS + s]; the emit pass sums the earlier blocks' sizes and calls Op::put / Op::totals.
+constexpr int CMP_TILE = 1024;
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+template <class Op>
+__global__ __launch_bounds__(256) void cmp_count_kernel(Op op, int M, int* __restrict__ bc) {
+  constexpr int NS = Op::NS;
+  __shared__ int wc[NS][4];
+  const int th = threadIdx.x, w = th >> 6, ln = th & 63;
+  int c[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) c[q] = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = blockIdx.x * CMP_TILE + j * 256 + th;
+    const uint32_t m = r < M ? op.mask(r) : 0u;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) c[q] += (int)__popcll(__ballot((m >> q) & 1u));
   }
-  part[th] = c;
-  part_lo[th] = clo;
+  if (ln == 0)
+#pragma unroll
+    for (int q = 0; q < NS; ++q) wc[q][w] = c[q];
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int a = th >= o ? part[th - o] : 0, b = th >= o ? part_lo[th - o] : 0;
+  if (th < NS) bc[blockIdx.x * NS + th] = wc[th][0] + wc[th][1] + wc[th][2] + wc[th][3];
+}
+
+template <class Op>
+__global__ __launch_bounds__(256) void cmp_emit_kernel(Op op, int M, const int* __restrict__ bc) {
+  constexpr int NS = Op::NS;
+  __shared__ int wc[NS][4];
+  const int th = threadIdx.x, w = th >> 6, ln = th & 63;
+  int base[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) base[q] = 0;
+  for (int b = th; b < (int)blockIdx.x; b += 256)
+#pragma unroll
+    for (int q = 0; q < NS; ++q) base[q] += bc[b * NS + q];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) base[q] = wave_sum_i(base[q]);
+  if (ln == 0)
+#pragma unroll
+    for (int q = 0; q < NS; ++q) wc[q][w] = base[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NS; ++q) base[q] = wc[q][0] + wc[q][1] + wc[q][2] + wc[q][3];
+  const uint64_t below = (1ull << ln) - 1ull;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = blockIdx.x * CMP_TILE + j * 256 + th;
+    const uint32_t m = r < M ? op.mask(r) : 0u;
+    uint64_t bal[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) bal[q] = __ballot((m >> q) & 1u);
+    __syncthreads();  // wc free (previous round / the base reduction read it)
+    if (ln == 0)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) wc[q][w] = (int)__popcll(bal[q]);
     __syncthreads();
-    part[th] += a;
-    part_lo[th] += b;
-    __syncthreads();
-  }
-  int k = part[th] - c;
-  for (int r = lo; r < hi; ++r) {
-    const int64_t tr = t[r];
-    if (tr != ignore) {
-      idx[k] = r;
-      inv[r] = k;
-      tc[k] = tr;
-      ++k;
-    } else {
-      inv[r] = -1;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      int pre = base[q];
+      for (int v = 0; v < w; ++v) pre += wc[q][v];
+      if (r < M) op.put(q, r, (m >> q) & 1u, pre + (int)__popcll(bal[q] & below));
+      base[q] += wc[q][0] + wc[q][1] + wc[q][2] + wc[q][3];
     }
   }
-  if (th == 1023) {
-    counts[0] = part_lo[1023];
-    counts[1] = part[1023] - part_lo[1023];
+  if (blockIdx.x == gridDim.x - 1 && th == 0) op.totals(base);
+}
+
+// Valid-row compaction of a classifier head's targets (rows with t == ignore contribute nothing to the
+// loss or to any gradient, trainer.py:131-154 / F.cross_entropy(ignore_index)).  Set 0 = valid rows
+// (emitted: idx[k], inv[r], tc[k] = t[idx[k]]), set 1 = valid rows below split (counted only);
+// counts = (valid rows in [0, split), valid rows in [split, M)).
+struct ValidOp {
+  static constexpr int NS = 2;
+  const int64_t* t;
+  int split;
+  int64_t ignore;
+  int *idx, *inv;
+  int64_t* tc;
+  int* counts;
+  __device__ uint32_t mask(int r) const {
+    const uint32_t v = t[r] != ignore;
+    return v | ((v && r < split) ? 2u : 0u);
   }
+  __device__ void put(int q, int r, uint32_t in, int k) const {
+    if (q != 0) return;
+    if (in) {
+      idx[k] = r;
+      tc[k] = t[r];
+    }
+    inv[r] = in ? k : -1;
+  }
+  __device__ void totals(const int* tot) const {
+    counts[0] = tot[1];
+    counts[1] = tot[0] - tot[1];
+  }
+};
+
+// Rows of the encoder passes the loss reads: set q uses the 3-bit code (bits >> 3q) & 7 — 1 / 2 =
+// positions with gm_a / gm_b nonzero (the pass's pooling weights), 4 = the last R positions of each
+// sequence (classifier heads).  idx / inv of set q at offset q·M; count[q] = set size.
+struct NeedOp {
+  static constexpr int NS = 8;
+  const int64_t *gm_a, *gm_b;
+  int L, R, n_sets, bits;
+  int *idx, *inv, *count;
+  long M;
+  __device__ uint32_t mask(int r) const {
+    const uint32_t a = gm_a[r] != 0, b = gm_b[r] != 0, tail = r % L >= L - R;
+    const uint32_t have = a | (b << 1) | (tail << 2);
+    uint32_t m = 0;
+    for (int q = 0; q < n_sets; ++q) m |= ((bits >> (3 * q)) & 7u & have) ? (1u << q) : 0u;
+    return m;
+  }
+  __device__ void put(int q, int r, uint32_t in, int k) const {
+    if (q >= n_sets) return;
+    if (in) idx[q * M + k] = r;
+    inv[q * M + r] = in ? k : -1;
+  }
+  __device__ void totals(const int* tot) const {
+    for (int q = 0; q < n_sets; ++q) count[q] = tot[q];
+  }
+};
+
+template <class Op>
+int compact_rows(const Op& op, int M, int* ws, hipStream_t s) {
+  const int nblk = c2::ceil_div(M, CMP_TILE);
+  cmp_count_kernel<Op><<<nblk, 256, 0, s>>>(op, M, ws);
+  cmp_emit_kernel<Op><<<nblk, 256, 0, s>>>(op, M, ws);
+  C2_CHECK_LAUNCH();
+  return 0;
 }
 
 // dst[k][c] = src[idx[k]·ld + c]   (k < n, c < d; float4 when d % 4 == 0 and ld % 4 == 0)
@@ -438,12 +535,23 @@ C2_API int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, co
   C2_CHECK_LAUNCH();
   return 0;
 }
+C2_API size_t c2dsr_compact_workspace(int M, int n_sets) {
+  return (size_t)c2::ceil_div(M, CMP_TILE) * (size_t)(n_sets < 2 ? 2 : 8) * sizeof(int);
+}
 C2_API int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, int* idx, int* inv, int64_t* tc,
-                               int* counts, void* stream) {
-  if (M <= 0) return M == 0 ? 0 : (int)hipErrorInvalidValue;
-  compact_valid_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(t, M, split, ignore, idx, inv, tc, counts);
-  C2_CHECK_LAUNCH();
-  return 0;
+                               int* counts, int* ws, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (M < 0) return (int)hipErrorInvalidValue;
+  if (M == 0) return (int)hipMemsetAsync(counts, 0, 2 * sizeof(int), s);
+  return compact_rows(ValidOp{t, split, ignore, idx, inv, tc, counts}, M, ws, s);
+}
+C2_API int c2dsr_need_rows(const int64_t* gm_a, const int64_t* gm_b, int B, int L, int R, int n_sets, int bits,
+                           int* idx, int* inv, int* count, int* ws, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (B < 0 || L <= 0 || n_sets < 1 || n_sets > 8) return (int)hipErrorInvalidValue;
+  if (B == 0) return (int)hipMemsetAsync(count, 0, n_sets * sizeof(int), s);
+  const int M = B * L;
+  return compact_rows(NeedOp{gm_a, gm_b, L, R, n_sets, bits, idx, inv, count, (long)M}, M, ws, s);
 }
 C2_API int c2dsr_gather_rows(const float* src, long ld, const int* idx, int n, int d, float* dst, void* stream) {
   if (n <= 0 || d <= 0) return 0;

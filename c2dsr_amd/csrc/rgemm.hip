@@ -30,6 +30,7 @@ struct Epi2 {
   int64_t row_base;
   const float* aux;  // AUX epilogues: [M][ldc] fp32 read at the output positions
   float aux_scale;
+  const int* rowmap;  // dropout row index = row_base + (rowmap ? rowmap[row] : row)
 };
 
 // epilogues that read a second [M, N] tensor at the output positions (prefetched one tile ahead):
@@ -172,7 +173,8 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
         const int rr = r0 + creg(r, lane);
         float v = fmaf(ep.alpha, acc[ct][r], bcol[ct]);
         if constexpr (EPI) {
-          const uint64_t idx = (uint64_t)(ep.row_base + rr) * N + col;
+          const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
+          const uint64_t idx = (uint64_t)(ep.row_base + rg_) * N + col;
           uint32_t h = c2::lowbias32((uint32_t)idx ^ ep.drop.k0);
           h = c2::lowbias32(h ^ (uint32_t)(idx >> 32) ^ ep.drop.k1);
           v = fmaxf(v, 0.f) * (h >= ep.drop.thr ? ep.drop.scale : 0.f);
@@ -415,12 +417,13 @@ C2_API int c2dsr_rgemm_supported(int M, int N, int K) {
 // (row_base+row)·N + col).  A fp32 (row stride lda, 16-byte aligned rows), B bf16 [N][ldb].
 C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                            float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                           int64_t row_base, int aux_mode, const float* aux, float aux_scale, void* stream);
+                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, float aux_scale,
+                           void* stream);
 
 C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                        float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                       int64_t row_base, void* stream) {
-  return c2dsr_rgemm_aux(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, 0,
+                       int64_t row_base, const int* rowmap, void* stream) {
+  return c2dsr_rgemm_aux(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, rowmap, 0,
                          nullptr, 0.f, stream);
 }
 
@@ -428,11 +431,12 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
 // place); 2: C = aux > 0 ? (alpha·A·Bᵀ + bias)·aux_scale : 0 (aux [M][ldc]).
 C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                            float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                           int64_t row_base, int aux_mode, const float* aux, float aux_scale, void* stream) {
+                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, float aux_scale,
+                           void* stream) {
   if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
   if (aux_mode < 0 || aux_mode > 2 || (aux_mode && (!aux || epilogue))) return (int)hipErrorInvalidValue;
   Epi2 ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base, aux,
-          aux_scale};
+          aux_scale, rowmap};
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;

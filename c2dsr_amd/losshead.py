@@ -112,7 +112,9 @@ class LossHeadFn(Function):
                 inv = torch.empty(M2, device=dev, dtype=torch.int32)
                 tc = torch.empty(M2, device=dev, dtype=torch.int64)
                 cnt = torch.empty(2, device=dev, dtype=torch.int32)
-                lib('c2dsr_compact_valid', tcat, M2, BR, n, idx, inv, tc, cnt, s)
+                cws = torch.empty(lib.raw('c2dsr_compact_workspace')(M2, 1) // 4 + 1, device=dev,
+                                  dtype=torch.int32)
+                lib('c2dsr_compact_valid', tcat, M2, BR, n, idx, inv, tc, cnt, cws, s)
                 comp = (idx, inv, tc, cnt)
             pre.append((Hcat, Hpad, tcat, comp))
         if fused:  # one host read of both heads' valid-row counts (sizes the compact launches)

@@ -65,6 +65,7 @@ class StepState:
         self.next_share_pass = DK.PASS_NEG0
         self.grad_hook = None  # c2dsr_amd.dp.GradBuckets while a data-parallel backward runs
         self.plans = {}  # (step, data_ptr, numel, n_keys) -> ops.IndexPlan (sorted on the side stream)
+        self.need = {}   # pass_id -> ops.RowSet: rows of the pass the loss reads (set by Trainer.train_batch)
 
     def keys(self, site):
         return DK.keys(self.seed, self.step, site)
@@ -103,6 +104,8 @@ class SelfAttention(nn.Module):
         """The TransformerEncoder stack on an already embedded + dropped [B, L, d] input."""
         B, L, d = x.shape
         rb_rows = self.state.row_offset * L
+        rs = self.state.need.get(pass_id) if self.training and not self.norm_first else None
+        n_layers = len(self.encoder.layers)
         for li, lay in enumerate(self.encoder.layers):
             at = lay.self_attn
             p_at, k_at = self._drop(pass_id, li, DK.K_ATTN)
@@ -121,6 +124,29 @@ class SelfAttention(nn.Module):
                                relu_drop=(k_fm, p_fm, rb_rows), res=res, ff=ff, ff_role='in')
                 return ops.linear(f, lay.linear2.weight, lay.linear2.bias, self.precision, ff=ff, ff_role='out')
 
+            if rs is not None and li == n_layers - 1:
+                # Last layer, post-norm: everything after the attention is row-wise, and the loss reads only
+                # the rows of `rs` (pooled positions, last R positions) — the rest of the layer and the final
+                # LayerNorm run on those rows (dropout indices through the row map, so the masks are the
+                # full-size run's); the output is expanded back with zeros elsewhere.
+                r1 = ops.ResidualLink(inv=rs.inv)
+                qkv = ops.linear(x, at.in_proj_weight, at.in_proj_bias, self.precision, res=r1)
+                o = ops.AttnFn.apply(qkv, seq, self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset)
+                oc = ops.GatherRowsFn.apply(o.reshape(B * L, d), rs)
+                sa = ops.linear(oc, at.out_proj.weight, at.out_proj.bias, self.precision)
+                xc = ops.gather_rows_nograd(x.reshape(B * L, d), rs)
+                x1 = ops.AddLNFn.apply(xc, sa, lay.norm1.weight, lay.norm1.bias, p_sa, k_sa, rb_rows, lay.norm1.eps,
+                                       r1, rs.idx)
+                r2 = ops.ResidualLink()
+                ff = ops.FFLink(p_fm)
+                f = ops.linear(x1, lay.linear1.weight, lay.linear1.bias, self.precision,
+                               relu_drop=(k_fm, p_fm, rb_rows, rs.idx), res=r2, ff=ff, ff_role='in')
+                f2 = ops.linear(f, lay.linear2.weight, lay.linear2.bias, self.precision, ff=ff, ff_role='out')
+                x2 = ops.AddLNFn.apply(x1, f2, lay.norm2.weight, lay.norm2.bias, p_fo, k_fo, rb_rows, lay.norm2.eps,
+                                       r2, rs.idx)
+                nm = self.encoder.norm
+                outc = ops.AddLNFn.apply(x2, None, nm.weight, nm.bias, 0.0, (0, 0), 0, nm.eps)
+                return ops.ExpandRowsFn.apply(outc, rs, (B, L, d))
             if self.norm_first:
                 y = ops.AddLNFn.apply(x, None, lay.norm1.weight, lay.norm1.bias, 0.0, (0, 0), 0, lay.norm1.eps)
                 x = ops.AddDropFn.apply(x, sa_block(y), p_sa, k_sa, rb_rows)

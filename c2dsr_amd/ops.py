@@ -29,7 +29,7 @@ def _grad_target(param):
 
 # ----------------------------------------------------------------------------- GEMM helpers
 def gemm(A, B, C, *, M, N, K, transA=0, transB=0, lda=None, ldb=None, ldc=None, alpha=1.0, beta=0.0, bias=None,
-         relu_drop=None, precision=FP32, split_k=0):
+         relu_drop=None, precision=FP32, split_k=0, rowmap=None):
     """C = alpha·op(A)·op(B) + beta·C + bias (see include/c2dsr.h:c2dsr_gemm)."""
     if lda is None:
         lda = M if transA else K
@@ -43,9 +43,11 @@ def gemm(A, B, C, *, M, N, K, transA=0, transB=0, lda=None, ldb=None, ldc=None, 
     epi = 0
     if relu_drop is not None:
         epi = 1
-        (k0, k1), p, row_base = relu_drop
+        (k0, k1), p, row_base = relu_drop[:3]
+        if len(relu_drop) > 3:
+            rowmap = relu_drop[3]
     lib('c2dsr_gemm', transA, transB, M, N, K, A, lda, B, ldb, C, ldc, float(alpha), float(beta), bias, epi, k0, k1,
-        float(p), int(row_base), precision, split_k, stream())
+        float(p), int(row_base), rowmap, precision, split_k, stream())
     return C
 
 
@@ -101,7 +103,8 @@ def weight_bf16(W, trans=False):
 AUX_ACC, AUX_MASK = 1, 2
 
 
-def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, aux_mode=0, aux=None, aux_scale=0.0):
+def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, aux_mode=0, aux=None, aux_scale=0.0,
+          rowmap=None):
     """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm); aux_mode
     AUX_ACC: C += aux (aux may be C itself), AUX_MASK: C = aux > 0 ? C·aux_scale : 0 (c2dsr_rgemm_aux)."""
     k0 = k1 = 0
@@ -110,13 +113,15 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
     epi = 0
     if relu_drop is not None:
         epi = 1
-        (k0, k1), p, row_base = relu_drop
+        (k0, k1), p, row_base = relu_drop[:3]
+        if len(relu_drop) > 3:
+            rowmap = relu_drop[3]
     if aux_mode:
         lib('c2dsr_rgemm_aux', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
-            int(row_base), int(aux_mode), aux, float(aux_scale), stream())
+            int(row_base), rowmap, int(aux_mode), aux, float(aux_scale), stream())
     else:
         lib('c2dsr_rgemm', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
-            int(row_base), stream())
+            int(row_base), rowmap, stream())
     return C
 
 
@@ -137,8 +142,9 @@ class ResidualLink:
     The LayerNorm backward parks its gradient w.r.t. x here instead of returning it; the projection's dX
     product then accumulates onto it in its epilogue, so autograd never adds the two in a separate pass."""
 
-    def __init__(self):
+    def __init__(self, inv=None):
         self.grad = None
+        self.inv = inv  # the LN ran on a row subset: its parked gradient is compact, expanded here (RowSet.inv)
 
 
 class FFLink:
@@ -191,6 +197,10 @@ class LinearFn(Function):
             park = ctx.res.grad if ctx.res is not None else None
             if ctx.res is not None:
                 ctx.res.grad = None
+                if park is not None and ctx.res.inv is not None:  # compact rows → full, zeros elsewhere
+                    full = torch.empty_like(x)
+                    lib('c2dsr_expand_rows', park, ctx.res.inv, M, K, full, stream())
+                    park = full
             if fused and park is not None:  # dx = parked LN gradient + dy·W, in place
                 dx = park
                 rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
@@ -222,6 +232,61 @@ class LinearFn(Function):
 
 def linear(x, W, b, precision=FP32, relu_drop=None, res=None, ff=None, ff_role=None):
     return LinearFn.apply(x.contiguous(), W, b, precision, relu_drop, res, ff, ff_role)
+
+
+# ----------------------------------------------------------------------------- row subsets
+class RowSet:
+    """The rows of one encoder pass the loss reads (c2dsr_need_rows): idx [n] (ascending), inv [M] (compact
+    index or -1).  The last encoder layer runs its row-wise part on these rows only."""
+
+    def __init__(self, idx, inv, n, M):
+        self.idx, self.inv, self.n, self.M = idx, inv, int(n), int(M)
+
+
+class GatherRowsFn(Function):
+    """[M, d] → [n, d] rows of a RowSet; backward scatters into zeros."""
+
+    @staticmethod
+    def forward(ctx, x, rs):
+        d = x.shape[-1]
+        out = torch.empty(rs.n, d, device=x.device, dtype=x.dtype)
+        lib('c2dsr_gather_rows', x, d, rs.idx, rs.n, d, out, stream())
+        ctx.rs, ctx.shape = rs, x.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        rs = ctx.rs
+        full = torch.empty(ctx.shape, device=g.device, dtype=g.dtype)
+        lib('c2dsr_expand_rows', g.contiguous(), rs.inv, rs.M, g.shape[-1], full, stream())
+        return full, None
+
+
+class ExpandRowsFn(Function):
+    """[n, d] rows of a RowSet → [*shape] with zeros elsewhere; backward gathers."""
+
+    @staticmethod
+    def forward(ctx, xc, rs, shape):
+        d = xc.shape[-1]
+        out = torch.empty(shape, device=xc.device, dtype=xc.dtype)
+        lib('c2dsr_expand_rows', xc, rs.inv, rs.M, d, out, stream())
+        ctx.rs = rs
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        rs = ctx.rs
+        d = g.shape[-1]
+        out = torch.empty(rs.n, d, device=g.device, dtype=g.dtype)
+        lib('c2dsr_gather_rows', g.contiguous(), d, rs.idx, rs.n, d, out, stream())
+        return out, None, None
+
+
+def gather_rows_nograd(x, rs):
+    d = x.shape[-1]
+    out = torch.empty(rs.n, d, device=x.device, dtype=x.dtype)
+    lib('c2dsr_gather_rows', x.detach(), d, rs.idx, rs.n, d, out, stream())
+    return out
 
 
 # ----------------------------------------------------------------------------- GCN (K1)
@@ -528,18 +593,19 @@ class AddLNFn(Function):
     """y = LayerNorm(a + drop(b))  (b may be None: plain LayerNorm of a); eps 1e-8."""
 
     @staticmethod
-    def forward(ctx, a, b, w, bias, p, keys, row_base, eps, res=None):
+    def forward(ctx, a, b, w, bias, p, keys, row_base, eps, res=None, rowmap=None):
         d = a.shape[-1]
         rows = a.numel() // d
         y = torch.empty_like(a)
         xsave = torch.empty_like(a) if b is not None else None
         mean = torch.empty(rows, device=a.device)
         rstd = torch.empty(rows, device=a.device)
-        lib('c2dsr_add_ln_fwd', a, b, rows, d, keys[0], keys[1], float(p), int(row_base), w, bias, float(eps), xsave, y,
-            mean, rstd, stream())
+        lib('c2dsr_add_ln_fwd', a, b, rows, d, keys[0], keys[1], float(p), int(row_base), rowmap, w, bias, float(eps),
+            xsave, y, mean, rstd, stream())
         ctx.save_for_backward(xsave if b is not None else a, mean, rstd)
         ctx.w, ctx.bias, ctx.p, ctx.keys, ctx.row_base, ctx.has_b = w, bias, p, keys, row_base, b is not None
         ctx.res = res
+        ctx.rowmap = rowmap
         return y
 
     @staticmethod
@@ -553,11 +619,11 @@ class AddLNFn(Function):
         gw, gb = _grad_target(ctx.w), _grad_target(ctx.bias)
         ws = torch.empty(lib.raw('c2dsr_ln_bwd_workspace')(d), dtype=torch.uint8, device=x.device)
         lib('c2dsr_ln_bwd', x, mean, rstd, ctx.w, dy, rows, d, da, 0, db, ctx.keys[0], ctx.keys[1], float(ctx.p),
-            int(ctx.row_base), gw, gb, ws, stream())
+            int(ctx.row_base), ctx.rowmap, gw, gb, ws, stream())
         if ctx.res is not None:  # parked for the layer's first projection (ResidualLink)
             ctx.res.grad = da
             da = None
-        return da, db, None, None, None, None, None, None, None
+        return da, db, None, None, None, None, None, None, None, None
 
 
 class AddDropFn(Function):

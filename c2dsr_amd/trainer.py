@@ -10,6 +10,7 @@ the reference (zero_grad only at the start of run_epoch, Q3).
 """
 from __future__ import annotations
 
+import os
 import time
 from os.path import join
 
@@ -17,7 +18,9 @@ import torch
 import torch.distributed as dist
 
 from .dataloader import get_dataloader
+from . import dropout as DK
 from . import ops
+from ._lib import lib, stream
 from .dp import GradBuckets
 from .graph import make_graph
 from .losshead import LossHeadFn, LossMeta
@@ -70,6 +73,7 @@ class Trainer(object):
         self.n_item_a = args.n_item_a
         self.n_item_b = args.n_item_b
         self.len_rec = args.len_rec
+        self.compact_rows = os.environ.get('C2DSR_ROW_COMPACT', '1') == '1'
         self.lambda_loss = args.lambda_loss
         self.rank, self.world = dp_info()
         self.dp_split = True  # slice each global batch across data-parallel ranks
@@ -115,6 +119,29 @@ class Trainer(object):
                         Da_w=m.D_a.weight, Da_b=m.D_a.bias, Db_w=m.D_b.weight, Db_b=m.D_b.bias,
                         precision=m.precision, B_global=B_global, allreduce=allreduce)
 
+    # encoder passes → which rows the loss reads: bit 1 / 2 = pooled with the a / b weights
+    # (trainer.py:101-108, Q5), bit 4 = the last R positions (classifier heads, trainer.py:122-146)
+    PASS_ROWS = ((DK.PASS_SHARE, 1 | 2 | 4), (DK.PASS_A, 1 | 4), (DK.PASS_B, 2 | 4), (DK.PASS_NEG0, 1),
+                 (DK.PASS_NEG0 + 1, 2))
+
+    def rows_read(self, gm_a, gm_b):
+        """RowSets of the five encoder passes (c2dsr_need_rows; one host read of the five counts), so the
+        last encoder layer runs its row-wise part only where the loss looks."""
+        if not self.compact_rows or not self.model.training or self.model.attn_share.norm_first:
+            return {}
+        B, L = gm_a.shape
+        M = B * L
+        n = len(self.PASS_ROWS)
+        dev = gm_a.device
+        idx = torch.empty(n, M, device=dev, dtype=torch.int32)
+        inv = torch.empty(n, M, device=dev, dtype=torch.int32)
+        cnt = torch.empty(n, device=dev, dtype=torch.int32)
+        ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, device=dev, dtype=torch.int32)
+        code = sum(bits << (3 * q) for q, (_, bits) in enumerate(self.PASS_ROWS))
+        lib('c2dsr_need_rows', gm_a, gm_b, B, L, self.len_rec, n, code, idx, inv, cnt, ws, stream())
+        counts = cnt.tolist()
+        return {pid: ops.RowSet(idx[q], inv[q], counts[q], M) for q, (pid, _) in enumerate(self.PASS_ROWS)}
+
     def train_batch(self, batch, *, global_rows=None):
         """trainer.py:91-160.  ``batch``: 14 int64 [B, L] tensors (host or device).  Under data
         parallelism each rank trains its slice of the global batch (or, with ``dp_split=False``, its
@@ -124,9 +151,13 @@ class Trainer(object):
          neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
         m = self.model
         m.state.row_offset = row_offset
-        h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
-        h_neg_a = m.forward_share(neg_a, pos)
-        h_neg_b = m.forward_share(neg_b, pos)
+        m.state.need = self.rows_read(gm_a, gm_b)
+        try:
+            h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
+            h_neg_a = m.forward_share(neg_a, pos)
+            h_neg_b = m.forward_share(neg_b, pos)
+        finally:
+            m.state.need = {}
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
         loss, loss_rec, loss_mi = LossHeadFn.apply(h_share, hx, hy, h_neg_a, h_neg_b, meta)
         if self.world > 1:

@@ -74,7 +74,7 @@ int c2dsr_embed_bwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, c
  * split_k 0 = automatic. */
 int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
                float* C, int ldc, float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1,
-               float p, int64_t row_base, int precision, int split_k, void* stream);
+               float p, int64_t row_base, const int* rowmap, int precision, int split_k, void* stream);
 /* out[n] = beta·out[n] + alpha·Σ_m X[m·ldx + n]   (bias gradients; deterministic 2-stage) */
 size_t c2dsr_colsum_workspace(int M, int N);
 int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* workspace,
@@ -90,12 +90,12 @@ int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int
 
 /* Residual + dropout + LayerNorm (TransformerEncoderLayer norm1/norm2, encoder.norm; eps 1e-8). */
 int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
-                     int64_t idx_base, const float* w, const float* bias, float eps, float* xsave, float* y,
+                     int64_t idx_base, const int* rowmap, const float* w, const float* bias, float eps, float* xsave, float* y,
                      float* mean, float* rstd, void* stream);
 size_t c2dsr_ln_bwd_workspace(int d);
 int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, const float* w, const float* dy, int rows,
                  int d, float* dx, int dx_accumulate, float* db_out, uint32_t k0, uint32_t k1, float p,
-                 int64_t idx_base, float* dgw, float* dgb, void* workspace, void* stream);
+                 int64_t idx_base, const int* rowmap, float* dgw, float* dgb, void* workspace, void* stream);
 int c2dsr_add_dropout(const float* a, const float* b, long n, int d, uint32_t k0, uint32_t k1, float p,
                       int64_t idx_base, float* y, void* stream);
 /* backward of drop(relu(.)) from its output: dx = (y > 0) ? dy/(1-p) : 0 */
@@ -113,12 +113,21 @@ int c2dsr_pool2_fwd(const float* h, const float* w1, const float* w2, int B, int
                     void* stream);
 int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, const float* w2, int B, int L, int d,
                     int accumulate, float* dh, void* stream);
-/* Valid-row compaction of a classifier head's targets (trainer.py:131-154: rows whose target is the
+/* Stable row compaction, two launches over 1024-row tiles; ws = c2dsr_compact_workspace(M, n_sets) bytes
+ * of device scratch (per-tile set sizes).
+ * Valid-row compaction of a classifier head's targets (trainer.py:131-154: rows whose target is the
  * ignore_index contribute nothing to the loss or any gradient, so the fused CE runs on the valid
- * rows only).  Stable: idx[k] = k-th row with t != ignore, inv[r] = compact index or -1, tc[k] =
- * t[idx[k]], counts[0..1] = valid rows in [0, split) and [split, M).  One workgroup. */
+ * rows only): idx[k] = k-th row with t != ignore, inv[r] = compact index or -1, tc[k] = t[idx[k]],
+ * counts[0..1] = valid rows in [0, split) and [split, M). */
+size_t c2dsr_compact_workspace(int M, int n_sets);
 int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, int* idx, int* inv, int64_t* tc, int* counts,
-                        void* stream);
+                        int* ws, void* stream);
+/* Rows of the encoder passes the loss reads (trainer.py:101-154), n_sets <= 8 at once: set q's code is
+ * (bits >> 3q) & 7 — 1 / 2 = positions with gm_a / gm_b nonzero (the pass's pooling weights), 4 = the
+ * last R positions (classifier heads).  idx / inv of set q at offset q·B·L: idx[k] = k-th needed row,
+ * inv[r] = compact index or -1; count[q] = set size. */
+int c2dsr_need_rows(const int64_t* gm_a, const int64_t* gm_b, int B, int L, int R, int n_sets, int bits, int* idx,
+                    int* inv, int* count, int* ws, void* stream);
 /* dst[k][:] = src[idx[k]·ld + :] (k < n);  dst[r][:] = inv[r] >= 0 ? src[inv[r]][:] : 0 (r < M) */
 int c2dsr_gather_rows(const float* src, long ld, const int* idx, int n, int d, float* dst, void* stream);
 int c2dsr_expand_rows(const float* src, const int* inv, int M, int d, float* dst, void* stream);
@@ -201,7 +210,10 @@ int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float*
 int c2dsr_rgemm_supported(int M, int N, int K);
 int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                 float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                int64_t row_base, void* stream);
+                int64_t row_base, const int* rowmap, void* stream);
+/* rowmap (GEMM epilogue 1, add_ln_fwd, ln_bwd; may be null): dropout row index = base + rowmap[row]
+ * instead of base + row, so a kernel run on a compacted subset of rows drops exactly the elements the
+ * full-size run would (the last encoder layer runs on the rows the loss reads). */
 /* c2dsr_rgemm with an epilogue reading aux [M][ldc] at the output positions (prefetched a tile ahead):
  *   aux_mode 1: C = alpha·A·Bᵀ + bias + aux   (aux == C accumulates in place: the residual-gradient sum
  *               of a post-norm encoder layer, which autograd would otherwise add in a separate pass)
@@ -210,7 +222,7 @@ int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int
  * epilogue must be 0 and beta 0 with an aux mode. */
 int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                     float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                    int64_t row_base, int aux_mode, const float* aux, float aux_scale, void* stream);
+                    int64_t row_base, const int* rowmap, int aux_mode, const float* aux, float aux_scale, void* stream);
 /* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
  * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
  * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS

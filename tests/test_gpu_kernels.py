@@ -434,3 +434,56 @@ def test_rgemm_aux_epilogues(K):
     rgemm(A.to(DEV), Wb, C, M=M, N=N, K=K, aux_mode=AUX_MASK, aux=src.to(DEV), aux_scale=1.25)
     want = torch.where(src.double() > 0, prod * 1.25, torch.zeros_like(prod))
     assert rel(C, want) < 2e-6
+
+
+@pytest.mark.parametrize('B,L,R', [(1, 7, 3), (37, 50, 10), (300, 50, 10), (2048, 50, 10)])
+def test_need_rows_compaction(B, L, R):
+    """c2dsr_need_rows: five sets in one pass (stable, across 1024-row tiles) vs numpy."""
+    from c2dsr_amd._lib import lib, stream
+    g = np.random.default_rng(B)
+    gm_a = (g.random((B, L)) < 0.3).astype(np.int64)
+    gm_b = (g.random((B, L)) < 0.2).astype(np.int64)
+    codes = (7, 5, 6, 1, 2)
+    M, n = B * L, len(codes)
+    idx = torch.full((n, M), -7, device=DEV, dtype=torch.int32)
+    inv = torch.empty(n, M, device=DEV, dtype=torch.int32)
+    cnt = torch.empty(n, device=DEV, dtype=torch.int32)
+    ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, device=DEV, dtype=torch.int32)
+    bits = sum(c << (3 * q) for q, c in enumerate(codes))
+    lib('c2dsr_need_rows', torch.from_numpy(gm_a).to(DEV), torch.from_numpy(gm_b).to(DEV), B, L, R, n, bits, idx,
+        inv, cnt, ws, stream())
+    tail = np.broadcast_to(np.arange(L) >= L - R, (B, L)).reshape(-1)
+    a, b = gm_a.reshape(-1) != 0, gm_b.reshape(-1) != 0
+    for q, c in enumerate(codes):
+        need = (a if c & 1 else False) | (b if c & 2 else False) | (tail if c & 4 else False)
+        want = np.nonzero(need)[0]
+        assert int(cnt[q]) == len(want)
+        assert np.array_equal(idx[q, :len(want)].cpu().numpy(), want)
+        winv = np.full(M, -1)
+        winv[want] = np.arange(len(want))
+        assert np.array_equal(inv[q].cpu().numpy(), winv)
+
+
+@pytest.mark.parametrize('M', [1, 1000, 1024, 40960])
+def test_compact_valid_targets(M):
+    from c2dsr_amd._lib import lib, stream
+    g = np.random.default_rng(M)
+    ignore = 99
+    t = g.integers(0, 100, M)
+    t[g.random(M) < 0.4] = ignore
+    split = M // 2
+    tt = torch.from_numpy(t).to(DEV)
+    idx = torch.empty(M, device=DEV, dtype=torch.int32)
+    inv = torch.empty(M, device=DEV, dtype=torch.int32)
+    tc = torch.empty(M, device=DEV, dtype=torch.int64)
+    cnt = torch.empty(2, device=DEV, dtype=torch.int32)
+    ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, 1) // 4 + 1, device=DEV, dtype=torch.int32)
+    lib('c2dsr_compact_valid', tt, M, split, ignore, idx, inv, tc, cnt, ws, stream())
+    want = np.nonzero(t != ignore)[0]
+    n = len(want)
+    assert cnt.tolist() == [int((want < split).sum()), int((want >= split).sum())]
+    assert np.array_equal(idx[:n].cpu().numpy(), want)
+    assert np.array_equal(tc[:n].cpu().numpy(), t[want])
+    winv = np.full(M, -1)
+    winv[want] = np.arange(n)
+    assert np.array_equal(inv.cpu().numpy(), winv)
