@@ -31,12 +31,15 @@ struct Epi2 {
   const float* aux;  // AUX epilogues: [M][ldc] fp32 read at the output positions
   float aux_scale;
   const int* rowmap;  // dropout row index = row_base + (rowmap ? rowmap[row] : row)
+  const int* auxmap;  // AUX_ACC_MAP: aux row of output row r = auxmap[r] (< 0: none, aux reads 0)
 };
 
 // epilogues that read a second [M, N] tensor at the output positions (prefetched one tile ahead):
 //   AUX_ACC:  C = alpha·A·Bᵀ + bias + aux             (aux may be C itself: C += A·Bᵀ)
 //   AUX_MASK: C = aux > 0 ? (alpha·A·Bᵀ + bias)·s : 0  (backward of drop(relu(.)) given its output aux)
-enum { AUX_NONE = 0, AUX_ACC = 1, AUX_MASK = 2 };
+//   AUX_ACC_MAP: C = alpha·A·Bᵀ + bias + aux[auxmap[r]]  (aux holds a compacted subset of the rows; the
+//                map of the tile after next is loaded with the aux values of the next one)
+enum { AUX_NONE = 0, AUX_ACC = 1, AUX_MASK = 2, AUX_ACC_MAP = 3 };
 
 __device__ __forceinline__ bf16x8 cvt8(float4 a, float4 b) {
   bf16x8 r;
@@ -106,6 +109,17 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
   const auto xsrc = rsrc_bytes(AUX != AUX_NONE ? ep.aux : C, (long)M * ldc * 4);  // rows >= M read 0
   // aux values of this wave's outputs for the current tile, loaded one tile ahead
   float xa[AUX != AUX_NONE ? CT : 1][16];
+  int xm[AUX == AUX_ACC_MAP ? 16 : 1];  // AUX_ACC_MAP: aux rows of the tile aux_load reads next
+  const auto map_load = [&](int tile) {
+    if constexpr (AUX == AUX_ACC_MAP) {
+      const int r0 = (rt0 + tile * rts) * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = r0 + creg(r, lane);
+        xm[r] = rr < M ? ep.auxmap[rr] : -1;
+      }
+    }
+  };
   const auto aux_load = [&](int tile) {
     if constexpr (AUX != AUX_NONE) {
       const int r0 = (rt0 + tile * rts) * 32;
@@ -114,12 +128,18 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
         const int col = ncol0 + 32 * ct + (lane & 31);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int off = col < N ? ((r0 + creg(r, lane)) * (int)ldc + col) * 4 : 0x7fffffff;
+          int off;
+          if constexpr (AUX == AUX_ACC_MAP)
+            off = (col < N && xm[r] >= 0) ? (xm[r] * (int)ldc + col) * 4 : 0x7fffffff;
+          else
+            off = col < N ? ((r0 + creg(r, lane)) * (int)ldc + col) * 4 : 0x7fffffff;
           xa[ct][r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xsrc, off, 0, 0));
         }
       }
+      map_load(min(tile + 1, ntile - 1));
     }
   };
+  map_load(0);
   aux_load(0);
   // chunk c = (tile c / KCH (clamped to the last), k-chunk c % KCH); thread t loads float4
   // t + 256u, u < 8: row (t >> 6) + 4u, columns 4·lane .. +3
@@ -179,7 +199,7 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
           h = c2::lowbias32(h ^ (uint32_t)(idx >> 32) ^ ep.drop.k1);
           v = fmaxf(v, 0.f) * (h >= ep.drop.thr ? ep.drop.scale : 0.f);
         }
-        if constexpr (AUX == AUX_ACC) v += xa[ct][r];
+        if constexpr (AUX == AUX_ACC || AUX == AUX_ACC_MAP) v += xa[ct][r];
         if constexpr (AUX == AUX_MASK) v = xa[ct][r] > 0.f ? v * ep.aux_scale : 0.f;
         const int off = (col < N && live) ? (rr * (int)ldc + col) * 4 : 0x7fffffff;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, v), csrc, off, 0, 0);
@@ -417,26 +437,29 @@ C2_API int c2dsr_rgemm_supported(int M, int N, int K) {
 // (row_base+row)·N + col).  A fp32 (row stride lda, 16-byte aligned rows), B bf16 [N][ldb].
 C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                            float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, float aux_scale,
-                           void* stream);
+                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
+                           float aux_scale, void* stream);
 
 C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                        float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                        int64_t row_base, const int* rowmap, void* stream) {
   return c2dsr_rgemm_aux(M, N, K, A, lda, B, ldb, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, rowmap, 0,
-                         nullptr, 0.f, stream);
+                         nullptr, nullptr, 0.f, stream);
 }
 
 // ... with an aux epilogue: aux_mode 1: C = alpha·A·Bᵀ + bias + aux (aux == C: accumulate in
-// place); 2: C = aux > 0 ? (alpha·A·Bᵀ + bias)·aux_scale : 0 (aux [M][ldc]).
+// place); 2: C = aux > 0 ? (alpha·A·Bᵀ + bias)·aux_scale : 0 (aux [M][ldc]); 3: C = alpha·A·Bᵀ + bias
+// + aux[auxmap[r]] (auxmap [M], entries < 0 add nothing; aux holds the mapped rows only).
 C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                            float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, float aux_scale,
-                           void* stream) {
+                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
+                           float aux_scale, void* stream) {
   if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
-  if (aux_mode < 0 || aux_mode > 2 || (aux_mode && (!aux || epilogue))) return (int)hipErrorInvalidValue;
+  if (aux_mode < 0 || aux_mode > 3 || (aux_mode && (!aux || epilogue))) return (int)hipErrorInvalidValue;
+  if ((aux_mode == AUX_ACC_MAP) != (auxmap != nullptr) || (aux_mode == AUX_ACC_MAP && aux == C))
+    return (int)hipErrorInvalidValue;
   Epi2 ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base, aux,
-          aux_scale, rowmap};
+          aux_scale, rowmap, auxmap};
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -448,7 +471,7 @@ C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const v
   const int CT = K == 256 ? 2 : 1;
   const int G = c2::ceil_div(N, 128 * CT);
   // persistent grid: exactly the workgroups that are resident at once (occupancy of the variant)
-  static int per_cu[12] = {0};
+  static int per_cu[15] = {0};
   auto launch = [&](void (*kern)(int, int, int, const float*, long, const bf16*, long, float*, long, Epi2, int),
                     int slot) -> int {
     if (!per_cu[slot]) {
@@ -470,6 +493,13 @@ C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const v
       rc = launch(rg_kernel<2, 1, false, AUX_ACC>, 7);
     else
       rc = launch(rg_kernel<3, 1, false, AUX_ACC>, 8);
+  } else if (aux_mode == AUX_ACC_MAP) {
+    if (K == 256)
+      rc = launch(rg_kernel<1, 2, false, AUX_ACC_MAP>, 12);
+    else if (K == 512)
+      rc = launch(rg_kernel<2, 1, false, AUX_ACC_MAP>, 13);
+    else
+      rc = launch(rg_kernel<3, 1, false, AUX_ACC_MAP>, 14);
   } else if (aux_mode == AUX_MASK) {
     if (K == 256)
       rc = launch(rg_kernel<1, 2, false, AUX_MASK>, 9);

@@ -100,11 +100,11 @@ def weight_bf16(W, trans=False):
     return WEIGHTS.get(W.detach(), trans)
 
 
-AUX_ACC, AUX_MASK = 1, 2
+AUX_ACC, AUX_MASK, AUX_ACC_MAP = 1, 2, 3
 
 
 def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, aux_mode=0, aux=None, aux_scale=0.0,
-          rowmap=None):
+          rowmap=None, auxmap=None):
     """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm); aux_mode
     AUX_ACC: C += aux (aux may be C itself), AUX_MASK: C = aux > 0 ? C·aux_scale : 0 (c2dsr_rgemm_aux)."""
     k0 = k1 = 0
@@ -118,7 +118,7 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
             rowmap = relu_drop[3]
     if aux_mode:
         lib('c2dsr_rgemm_aux', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
-            int(row_base), rowmap, int(aux_mode), aux, float(aux_scale), stream())
+            int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
     else:
         lib('c2dsr_rgemm', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
             int(row_base), rowmap, stream())
@@ -197,11 +197,16 @@ class LinearFn(Function):
             park = ctx.res.grad if ctx.res is not None else None
             if ctx.res is not None:
                 ctx.res.grad = None
-                if park is not None and ctx.res.inv is not None:  # compact rows → full, zeros elsewhere
-                    full = torch.empty_like(x)
-                    lib('c2dsr_expand_rows', park, ctx.res.inv, M, K, full, stream())
-                    park = full
-            if fused and park is not None:  # dx = parked LN gradient + dy·W, in place
+            sub = park is not None and ctx.res.inv is not None  # parked gradient of a row subset
+            if sub and not fused:  # compact rows → full, zeros elsewhere
+                full = torch.empty_like(x)
+                lib('c2dsr_expand_rows', park, ctx.res.inv, M, K, full, stream())
+                park, sub = full, False
+            if sub:  # dx = dy·W + the parked rows, read through the row map
+                dx = torch.empty_like(x)
+                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park,
+                      auxmap=ctx.res.inv)
+            elif fused and park is not None:  # dx = parked LN gradient + dy·W, in place
                 dx = park
                 rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
             elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here

@@ -219,10 +219,13 @@ int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void* B, int
  *               of a post-norm encoder layer, which autograd would otherwise add in a separate pass)
  *   aux_mode 2: C = aux > 0 ? (alpha·A·Bᵀ + bias)·aux_scale : 0   (dX of linear2 masked by the
  *               backward of drop(relu(.)) of linear1, given its output aux; models/encoders.py:23-27)
- * epilogue must be 0 and beta 0 with an aux mode. */
+ *   aux_mode 3: C = alpha·A·Bᵀ + bias + (auxmap[r] >= 0 ? aux[auxmap[r]] : 0)   (auxmap [M]; aux holds a
+ *               compacted subset of the rows — the LayerNorm gradient of the last layer's row subset)
+ * epilogue must be 0 and beta 0 with an aux mode; auxmap non-null exactly for mode 3 (aux != C). */
 int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
                     float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                    int64_t row_base, const int* rowmap, int aux_mode, const float* aux, float aux_scale, void* stream);
+                    int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
+                    float aux_scale, void* stream);
 /* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
  * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
  * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS

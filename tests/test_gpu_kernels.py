@@ -419,7 +419,7 @@ def test_wgemm_vs_bf16_rounded_fp32(T, N):
 def test_rgemm_aux_epilogues(K):
     """c2dsr_rgemm_aux: in-place accumulate (the residual-gradient sum) and the drop(relu) backward mask,
     against bf16-rounded fp32 products; odd row-tile counts exercise the repeated last tile."""
-    from c2dsr_amd.ops import AUX_ACC, AUX_MASK, rgemm, to_bf16
+    from c2dsr_amd.ops import AUX_ACC, AUX_ACC_MAP, AUX_MASK, rgemm, to_bf16
     g = torch.Generator().manual_seed(K)
     M, N = 32 * 37 + 5, 256
     A, W = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
@@ -434,6 +434,16 @@ def test_rgemm_aux_epilogues(K):
     rgemm(A.to(DEV), Wb, C, M=M, N=N, K=K, aux_mode=AUX_MASK, aux=src.to(DEV), aux_scale=1.25)
     want = torch.where(src.double() > 0, prod * 1.25, torch.zeros_like(prod))
     assert rel(C, want) < 2e-6
+    # AUX_ACC_MAP: aux holds a compacted subset of the rows, read through the row map
+    keep = torch.nonzero(torch.rand(M, generator=g) < 0.6).reshape(-1)
+    inv = torch.full((M,), -1, dtype=torch.int32)
+    inv[keep] = torch.arange(keep.numel(), dtype=torch.int32)
+    park = torch.randn(keep.numel(), N, generator=g)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), Wb, C, M=M, N=N, K=K, aux_mode=AUX_ACC_MAP, aux=park.to(DEV), auxmap=inv.to(DEV))
+    full = torch.zeros(M, N, dtype=torch.float64)
+    full[keep] = park.double()
+    assert rel(C, prod + full) < 2e-6
 
 
 @pytest.mark.parametrize('B,L,R', [(1, 7, 3), (37, 50, 10), (300, 50, 10), (2048, 50, 10)])
