@@ -49,7 +49,7 @@ def split_count(rows, tile, max_split=16, per_cu=1):
 
 class LossMeta:
     def __init__(self, *, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, n_a, n_b, R, lam, Wa, ba, Wb, bb, wpad,
-                 bpad, Da_w, Da_b, Db_w, Db_b, precision=FP32, B_global=None, allreduce=None):
+                 bpad, Da_w, Da_b, Db_w, Db_b, precision=FP32, B_global=None, allreduce=None, ce_pre=None):
         self.__dict__.update(locals())
         del self.__dict__['self']
 
@@ -98,13 +98,19 @@ class LossHeadFn(Function):
         specs = ((hx, m.Wa, m.ba, m.gt_share_a, m.gt_a, m.n_a), (hy, m.Wb, m.bb, m.gt_share_b, m.gt_b, m.n_b))
         M2 = 2 * BR
         pre = []
-        for (hdom, W, bias, t_share, t_spec, n) in specs:
+        pre_given = fused and m.ce_pre is not None  # targets + compaction enqueued by Trainer.prepare
+        for k, (hdom, W, bias, t_share, t_spec, n) in enumerate(specs):
             Hcat = torch.empty(M2, d, **f32)
             Hpad = torch.empty(M2, d, **f32)
             lib('c2dsr_rec_gather', h_share, hdom, B, L, d, R, Hcat, Hpad, s)
+            comp = None
+            if pre_given:
+                tcat, idx, inv, tc, (hc, slot) = m.ce_pre[k]
+                comp = (idx, inv, tc, (hc, slot))
+                pre.append((Hcat, Hpad, tcat, comp))
+                continue
             tcat = torch.empty(M2, device=dev, dtype=torch.int64)
             lib('c2dsr_rec_targets', t_share, t_spec, B, L, R, tcat, s)
-            comp = None
             if fused:
                 # rows whose target is the ignore index contribute nothing to the loss or any gradient
                 # (trainer.py:131-154): the fused CE runs on the valid rows only (stable compaction)
@@ -117,7 +123,9 @@ class LossHeadFn(Function):
                 lib('c2dsr_compact_valid', tcat, M2, BR, n, idx, inv, tc, cnt, cws, s)
                 comp = (idx, inv, tc, cnt)
             pre.append((Hcat, Hpad, tcat, comp))
-        if fused:  # one host read of both heads' valid-row counts (sizes the compact launches)
+        if pre_given:  # deferred host read (ops.HostCounts), long since landed
+            counts = [c[3][3][0][c[3][3][1] + j] for c in pre for j in (0, 1)]
+        elif fused:  # one host read of both heads' valid-row counts (sizes the compact launches)
             counts = torch.cat([c[3][3] for c in pre]).tolist()
         for k, ((hdom, W, bias, t_share, t_spec, n), (Hcat, Hpad, tcat, comp)) in enumerate(zip(specs, pre)):
             lse = torch.empty(M2, **f32)

@@ -240,12 +240,40 @@ def linear(x, W, b, precision=FP32, relu_drop=None, res=None, ff=None, ff_role=N
 
 
 # ----------------------------------------------------------------------------- row subsets
+class HostCounts:
+    """Small device int32 counts copied to pinned host memory behind the work that produces them, read
+    on first use: the host blocks only if the device has not got that far yet, so the stream never
+    drains the way an immediate ``.tolist()`` would make it."""
+
+    def __init__(self, dev_counts):
+        self.host = torch.empty(dev_counts.numel(), dtype=torch.int32, pin_memory=True)
+        self.host.copy_(dev_counts, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        self.vals = None
+
+    def __getitem__(self, i):
+        if self.vals is None:
+            self.ev.synchronize()
+            self.vals = self.host.tolist()
+        return self.vals[i]
+
+
 class RowSet:
     """The rows of one encoder pass the loss reads (c2dsr_need_rows): idx [n] (ascending), inv [M] (compact
-    index or -1).  The last encoder layer runs its row-wise part on these rows only."""
+    index or -1).  The last encoder layer runs its row-wise part on these rows only.  ``n`` may be given
+    as (HostCounts, slot), read when first needed."""
 
     def __init__(self, idx, inv, n, M):
-        self.idx, self.inv, self.n, self.M = idx, inv, int(n), int(M)
+        self.idx, self.inv, self.M = idx, inv, int(M)
+        self._n = n
+
+    @property
+    def n(self):
+        if isinstance(self._n, tuple):
+            hc, q = self._n
+            self._n = int(hc[q])
+        return int(self._n)
 
 
 class GatherRowsFn(Function):

@@ -124,23 +124,59 @@ class Trainer(object):
     PASS_ROWS = ((DK.PASS_SHARE, 1 | 2 | 4), (DK.PASS_A, 1 | 4), (DK.PASS_B, 2 | 4), (DK.PASS_NEG0, 1),
                  (DK.PASS_NEG0 + 1, 2))
 
-    def rows_read(self, gm_a, gm_b):
-        """RowSets of the five encoder passes (c2dsr_need_rows; one host read of the five counts), so the
-        last encoder layer runs its row-wise part only where the loss looks."""
-        if not self.compact_rows or not self.model.training or self.model.attn_share.norm_first:
-            return {}
+    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b):
+        """Index work the step sizes its launches by, enqueued ahead of the forward with one deferred host
+        read of all its counts (ops.HostCounts; nothing waits until the first count is needed):
+          * RowSets of the five encoder passes (c2dsr_need_rows), so the last encoder layer runs its
+            row-wise part only where the loss looks;
+          * per classifier head, the stacked [share; specific] targets of the last R positions
+            (c2dsr_rec_targets) and their valid-row compaction (c2dsr_compact_valid) for the fused CE.
+        Returns (need: {pass_id: RowSet}, ce_pre: [(tcat, idx, inv, tc, (HostCounts, slot)), ...] or None)."""
+        m = self.model
         B, L = gm_a.shape
-        M = B * L
-        n = len(self.PASS_ROWS)
+        M, R = B * L, self.len_rec
         dev = gm_a.device
-        idx = torch.empty(n, M, device=dev, dtype=torch.int32)
-        inv = torch.empty(n, M, device=dev, dtype=torch.int32)
-        cnt = torch.empty(n, device=dev, dtype=torch.int32)
-        ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, device=dev, dtype=torch.int32)
-        code = sum(bits << (3 * q) for q, (_, bits) in enumerate(self.PASS_ROWS))
-        lib('c2dsr_need_rows', gm_a, gm_b, B, L, self.len_rec, n, code, idx, inv, cnt, ws, stream())
-        counts = cnt.tolist()
-        return {pid: ops.RowSet(idx[q], inv[q], counts[q], M) for q, (pid, _) in enumerate(self.PASS_ROWS)}
+        s = stream()
+        i32 = dict(device=dev, dtype=torch.int32)
+        counts = []
+        need_sets = None
+        if self.compact_rows and m.training and not m.attn_share.norm_first:
+            n = len(self.PASS_ROWS)
+            idx = torch.empty(n, M, **i32)
+            inv = torch.empty(n, M, **i32)
+            cnt = torch.empty(n, **i32)
+            ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, **i32)
+            code = sum(bits << (3 * q) for q, (_, bits) in enumerate(self.PASS_ROWS))
+            lib('c2dsr_need_rows', gm_a, gm_b, B, L, R, n, code, idx, inv, cnt, ws, s)
+            need_sets = (idx, inv)
+            counts.append(cnt)
+        ce = None
+        if m.precision == ops.BF16 and bool(lib.raw('c2dsr_ce_supported')(self.d_latent)):
+            M2 = 2 * B * R
+            ce = []
+            for ts, tx, n_items in ((gt_share_a, gt_a, self.n_item_a), (gt_share_b, gt_b, self.n_item_b)):
+                tcat = torch.empty(M2, device=dev, dtype=torch.int64)
+                lib('c2dsr_rec_targets', ts, tx, B, L, R, tcat, s)
+                idx_c = torch.empty(M2, **i32)
+                inv_c = torch.empty(M2, **i32)
+                tc = torch.empty(M2, device=dev, dtype=torch.int64)
+                cnt = torch.empty(2, **i32)
+                ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M2, 1) // 4 + 1, **i32)
+                lib('c2dsr_compact_valid', tcat, M2, B * R, n_items, idx_c, inv_c, tc, cnt, ws, s)
+                ce.append((tcat, idx_c, inv_c, tc))
+                counts.append(cnt)
+        if not counts:
+            return {}, None
+        hc = ops.HostCounts(torch.cat(counts))
+        need = {}
+        if need_sets is not None:
+            idx, inv = need_sets
+            need = {pid: ops.RowSet(idx[q], inv[q], (hc, q), M) for q, (pid, _) in enumerate(self.PASS_ROWS)}
+        ce_pre = None
+        if ce is not None:
+            base = len(self.PASS_ROWS) if need_sets is not None else 0
+            ce_pre = [c + ((hc, base + 2 * k),) for k, c in enumerate(ce)]
+        return need, ce_pre
 
     def train_batch(self, batch, *, global_rows=None):
         """trainer.py:91-160.  ``batch``: 14 int64 [B, L] tensors (host or device).  Under data
@@ -151,7 +187,7 @@ class Trainer(object):
          neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
         m = self.model
         m.state.row_offset = row_offset
-        m.state.need = self.rows_read(gm_a, gm_b)
+        m.state.need, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b)
         try:
             h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
             h_neg_a = m.forward_share(neg_a, pos)
@@ -159,6 +195,7 @@ class Trainer(object):
         finally:
             m.state.need = {}
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
+        meta.ce_pre = ce_pre
         loss, loss_rec, loss_mi = LossHeadFn.apply(h_share, hx, hy, h_neg_a, h_neg_b, meta)
         if self.world > 1:
             # bucketed all-reduce of the fresh gradient, each bucket issued as soon as the backward
