@@ -47,13 +47,13 @@ __global__ void pool_bwd_kernel(const float* __restrict__ dout, const float* __r
 // both poolings of h_share).  One block per b: the four waves take rows l ≡ w (mod 4), float4 per
 // lane (d <= 256 per pass over c), rows whose weights are all 0 (padding / non-target positions) are
 // not read; the wave partials are added in wave order (deterministic).
-__global__ __launch_bounds__(256) void pool2_fwd_kernel(const float* __restrict__ h, const float* __restrict__ w1,
+__global__ __launch_bounds__(256) void pool2_fwd_kernel(const float* __restrict__ h, const int* __restrict__ hmap,
+                                                        const float* __restrict__ w1,
                                                         const float* __restrict__ w2, int B, int L, int d,
                                                         float* __restrict__ out1, float* __restrict__ out2) {
   __shared__ float4 red[2][4][64];
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const float* hb = h + (long)b * L * d;
   const float* wa = w1 + (long)b * L;
   const float* wb = w2 ? w2 + (long)b * L : nullptr;
   for (int c0 = 0; c0 < d; c0 += 256) {
@@ -68,7 +68,9 @@ __global__ __launch_bounds__(256) void pool2_fwd_kernel(const float* __restrict_
         const int l = l0 + 4 * u;
         x1[u] = l < L ? wa[l] : 0.f;
         x2[u] = (wb && l < L) ? wb[l] : 0.f;
-        v[u] = (cin && (x1[u] != 0.f || x2[u] != 0.f)) ? *(const float4*)(hb + (long)l * d + c) : c2::f4(0.f);
+        const long bl = (long)b * L + l;
+        v[u] = (cin && (x1[u] != 0.f || x2[u] != 0.f)) ? *(const float4*)(h + (hmap ? hmap[bl] : bl) * d + c)
+                                                        : c2::f4(0.f);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -88,15 +90,17 @@ __global__ __launch_bounds__(256) void pool2_fwd_kernel(const float* __restrict_
   }
 }
 
-// dh[b,l] = (accumulate ? dh[b,l] : 0) + d1[b]·w1[b,l] (+ d2[b]·w2[b,l])   (float4 per thread)
+// dh[k] = (accumulate ? dh[k] : 0) + d1[b]·w1[b,l] (+ d2[b]·w2[b,l]) for the row k of (b, l): k = b·L + l, or,
+// with a compact dh, bl = idx[k] over its n_rows rows   (float4 per thread)
 __global__ void pool2_bwd_kernel(const float* __restrict__ d1, const float* __restrict__ w1,
-                                 const float* __restrict__ d2, const float* __restrict__ w2, int B, int L, int d,
-                                 int accumulate, float* __restrict__ dh) {
+                                 const float* __restrict__ d2, const float* __restrict__ w2, int L, int d,
+                                 long rows, const int* __restrict__ idx, int accumulate, float* __restrict__ dh) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
-  if (i >= (long)B * L * d / 4) return;
+  if (i >= rows * d / 4) return;
   const long e = i * 4;
   const int c = (int)(e % d);
-  const long bl = e / d;
+  const long k = e / d;
+  const long bl = idx ? idx[k] : k;
   const long b = bl / L;
   const float x1 = w1[bl], x2 = d2 ? w2[bl] : 0.f;
   float4 o = accumulate ? *(const float4*)(dh + e) : c2::f4(0.f);
@@ -330,7 +334,9 @@ __global__ __launch_bounds__(1024) void mi_loss_kernel(const float* __restrict__
 }
 
 // Hcat = [hs_r ; hs_r + hx_r], Hpad = [hs_r ; hx_r] (rows (b, L-R+k)), tcat = [t_share_r ; t_spec_r]
-__global__ void rec_gather_kernel(const float* __restrict__ hs, const float* __restrict__ hx, int B, int L, int d,
+// (row maps: a [B·L] → compact row index of hs / hx when they hold a row subset, else null)
+__global__ void rec_gather_kernel(const float* __restrict__ hs, const int* __restrict__ hs_map,
+                                  const float* __restrict__ hx, const int* __restrict__ hx_map, int B, int L, int d,
                                   int R, float* __restrict__ Hcat, float* __restrict__ Hpad) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long BR = (long)B * R;
@@ -338,7 +344,8 @@ __global__ void rec_gather_kernel(const float* __restrict__ hs, const float* __r
   const long r = i / d;
   const int c = (int)(i % d);
   const long b = r / R, l = L - R + r % R;
-  const float a = hs[(b * L + l) * d + c], x = hx[(b * L + l) * d + c];
+  const long bl = b * L + l;
+  const float a = hs[(hs_map ? hs_map[bl] : bl) * d + c], x = hx[(hx_map ? hx_map[bl] : bl) * d + c];
   Hcat[r * d + c] = a;
   Hcat[(BR + r) * d + c] = a + x;
   Hpad[r * d + c] = a;
@@ -357,16 +364,18 @@ __global__ void rec_targets_kernel(const int64_t* __restrict__ ts, const int64_t
 
 // dhs[b,l] += dHcat[r] + dHcat[BR+r] + dHpad[r];  dhx[b,l] += dHcat[BR+r] + dHpad[BR+r]
 __global__ void rec_scatter_kernel(const float* __restrict__ dHcat, const float* __restrict__ dHpad, int B, int L,
-                                   int d, int R, float* __restrict__ dhs, float* __restrict__ dhx) {
+                                   int d, int R, float* __restrict__ dhs, const int* __restrict__ dhs_map,
+                                   float* __restrict__ dhx, const int* __restrict__ dhx_map) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long BR = (long)B * R;
   if (i >= BR * d) return;
   const long r = i / d;
   const int c = (int)(i % d);
   const long b = r / R, l = L - R + r % R;
+  const long bl = b * L + l;
   const float g1 = dHcat[r * d + c], g2 = dHcat[(BR + r) * d + c];
-  dhs[(b * L + l) * d + c] += g1 + g2 + dHpad[r * d + c];
-  dhx[(b * L + l) * d + c] += g2 + dHpad[(BR + r) * d + c];
+  dhs[(dhs_map ? dhs_map[bl] : bl) * d + c] += g1 + g2 + dHpad[r * d + c];
+  dhx[(dhx_map ? dhx_map[bl] : bl) * d + c] += g2 + dHpad[(BR + r) * d + c];
 }
 
 // Per-row CE: lse over ncol logits, loss_row = valid ? lse - logit[t] : 0.  One wave per row.
@@ -519,19 +528,21 @@ C2_API int c2dsr_pool_bwd(const float* dout, const float* w, int B, int L, int d
   C2_CHECK_LAUNCH();
   return 0;
 }
-C2_API int c2dsr_pool2_fwd(const float* h, const float* w1, const float* w2, int B, int L, int d, float* out1,
-                           float* out2, void* stream) {
+C2_API int c2dsr_pool2_fwd(const float* h, const int* hmap, const float* w1, const float* w2, int B, int L, int d,
+                           float* out1, float* out2, void* stream) {
   if (B == 0) return 0;
   if (d % 4 || (w2 && !out2)) return (int)hipErrorInvalidValue;
-  pool2_fwd_kernel<<<B, 256, 0, (hipStream_t)stream>>>(h, w1, w2, B, L, d, out1, out2);
+  pool2_fwd_kernel<<<B, 256, 0, (hipStream_t)stream>>>(h, hmap, w1, w2, B, L, d, out1, out2);
   C2_CHECK_LAUNCH();
   return 0;
 }
 C2_API int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, const float* w2, int B, int L, int d,
-                           int accumulate, float* dh, void* stream) {
-  const long n = (long)B * L * d / 4;
+                           const int* idx, int n_rows, int accumulate, float* dh, void* stream) {
+  const long rows = idx ? (long)n_rows : (long)B * L;
+  const long n = rows * d / 4;
   if (n == 0 || d % 4) return n == 0 ? 0 : (int)hipErrorInvalidValue;
-  pool2_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(d1, w1, d2, w2, B, L, d, accumulate, dh);
+  pool2_bwd_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(d1, w1, d2, w2, L, d, rows, idx, accumulate,
+                                                                          dh);
   C2_CHECK_LAUNCH();
   return 0;
 }
@@ -579,11 +590,12 @@ C2_API int c2dsr_mi_loss(const float* s, int B, int B_norm, float* loss_mi, floa
   C2_CHECK_LAUNCH();
   return 0;
 }
-C2_API int c2dsr_rec_gather(const float* hs, const float* hx, int B, int L, int d, int R, float* Hcat, float* Hpad,
-                            void* stream) {
+C2_API int c2dsr_rec_gather(const float* hs, const int* hs_map, const float* hx, const int* hx_map, int B, int L, int d,
+                            int R, float* Hcat, float* Hpad, void* stream) {
   const long n = (long)B * R * d;
   if (n == 0) return 0;
-  rec_gather_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(hs, hx, B, L, d, R, Hcat, Hpad);
+  rec_gather_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(hs, hs_map, hx, hx_map, B, L, d, R, Hcat,
+                                                                           Hpad);
   C2_CHECK_LAUNCH();
   return 0;
 }
@@ -594,11 +606,12 @@ C2_API int c2dsr_rec_targets(const int64_t* ts, const int64_t* tx, int B, int L,
   C2_CHECK_LAUNCH();
   return 0;
 }
-C2_API int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs, float* dhx,
-                             void* stream) {
+C2_API int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs,
+                             const int* dhs_map, float* dhx, const int* dhx_map, void* stream) {
   const long n = (long)B * R * d;
   if (n == 0) return 0;
-  rec_scatter_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dHcat, dHpad, B, L, d, R, dhs, dhx);
+  rec_scatter_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dHcat, dHpad, B, L, d, R, dhs, dhs_map, dhx,
+                                                                            dhx_map);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -49,7 +49,8 @@ def split_count(rows, tile, max_split=16, per_cu=1):
 
 class LossMeta:
     def __init__(self, *, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, n_a, n_b, R, lam, Wa, ba, Wb, bb, wpad,
-                 bpad, Da_w, Da_b, Db_w, Db_b, precision=FP32, B_global=None, allreduce=None, ce_pre=None):
+                 bpad, Da_w, Da_b, Db_w, Db_b, precision=FP32, B_global=None, allreduce=None, ce_pre=None,
+                 row_sets=None):
         self.__dict__.update(locals())
         del self.__dict__['self']
 
@@ -57,7 +58,8 @@ class LossMeta:
 class LossHeadFn(Function):
     @staticmethod
     def forward(ctx, h_share, hx, hy, h_neg_a, h_neg_b, m: LossMeta):
-        B, L, d = h_share.shape
+        B, L = m.gm_a.shape  # (encoder outputs may hold a row subset: [n, d])
+        d = h_share.shape[-1]
         R = m.R
         BR = B * R
         dev = h_share.device
@@ -72,11 +74,15 @@ class LossHeadFn(Function):
         Phy = torch.empty(B, d, **f32)
         X2a = torch.empty(2 * B, d, **f32)  # [h_share·wb ; h_neg_a·wa]
         X2b = torch.empty(2 * B, d, **f32)  # [h_share·wa ; h_neg_b·wb]
-        lib('c2dsr_pool2_fwd', hx, wa, None, B, L, d, Phx, None, s)
-        lib('c2dsr_pool2_fwd', hy, wb, None, B, L, d, Phy, None, s)
-        lib('c2dsr_pool2_fwd', h_share, wb, wa, B, L, d, X2a, X2b, s)  # both poolings of h_share (Q5), one read
-        lib('c2dsr_pool2_fwd', h_neg_a, wa, None, B, L, d, X2a[B:], None, s)
-        lib('c2dsr_pool2_fwd', h_neg_b, wb, None, B, L, d, X2b[B:], None, s)
+        # encoder outputs may hold only the rows the loss reads (row_sets: share, a, b, neg_a, neg_b; the
+        # last encoder layer ran on them): read through their inverse maps
+        rsets = tuple(m.row_sets) if m.row_sets is not None else (None,) * 5
+        mp = [r.inv if r is not None else None for r in rsets]
+        lib('c2dsr_pool2_fwd', hx, mp[1], wa, None, B, L, d, Phx, None, s)
+        lib('c2dsr_pool2_fwd', hy, mp[2], wb, None, B, L, d, Phy, None, s)
+        lib('c2dsr_pool2_fwd', h_share, mp[0], wb, wa, B, L, d, X2a, X2b, s)  # both poolings of h_share (Q5)
+        lib('c2dsr_pool2_fwd', h_neg_a, mp[3], wa, None, B, L, d, X2a[B:], None, s)
+        lib('c2dsr_pool2_fwd', h_neg_b, mp[4], wb, None, B, L, d, X2b[B:], None, s)
         # ---- bilinear: s = x1ᵀ W x2 (+b)  via  U = X2·Wᵀ, s = rowdot(x1, U) ----
         Ua = torch.empty(2 * B, d, **f32)
         Ub = torch.empty(2 * B, d, **f32)
@@ -102,7 +108,7 @@ class LossHeadFn(Function):
         for k, (hdom, W, bias, t_share, t_spec, n) in enumerate(specs):
             Hcat = torch.empty(M2, d, **f32)
             Hpad = torch.empty(M2, d, **f32)
-            lib('c2dsr_rec_gather', h_share, hdom, B, L, d, R, Hcat, Hpad, s)
+            lib('c2dsr_rec_gather', h_share, mp[0], hdom, mp[1 + k], B, L, d, R, Hcat, Hpad, s)
             comp = None
             if pre_given:
                 tcat, idx, inv, tc, (hc, slot) = m.ce_pre[k]
@@ -187,6 +193,8 @@ class LossHeadFn(Function):
         ctx.mi = (Phx, Phy, X2a, X2b, Ua, Ub, dS)
         ctx.w = (wa, wb)
         ctx.shape = (B, L, d)
+        ctx.rsets = rsets
+        ctx.hshapes = [t.shape for t in (h_share, hx, hy, h_neg_a, h_neg_b)]
         loss, loss_rec, loss_mi_o = out3[0], out3[1], out3[2]
         ctx.mark_non_differentiable(loss_rec, loss_mi_o)
         return loss, loss_rec, loss_mi_o
@@ -225,20 +233,20 @@ class LossHeadFn(Function):
         wa, wb = ctx.w
         # the pooling backward WRITES the five encoder-output gradients (no zero fill); the classifier
         # heads below add their last-R-position parts
-        dh_share = torch.empty(B, L, d, **f32)
-        dhx = torch.empty(B, L, d, **f32)
-        dhy = torch.empty(B, L, d, **f32)
-        dh_na = torch.empty(B, L, d, **f32)
-        dh_nb = torch.empty(B, L, d, **f32)
-        lib('c2dsr_pool2_bwd', dPhx, wa, None, None, B, L, d, 0, dhx, s)
-        lib('c2dsr_pool2_bwd', dPhy, wb, None, None, B, L, d, 0, dhy, s)
-        lib('c2dsr_pool2_bwd', dX2a, wb, dX2b, wa, B, L, d, 0, dh_share, s)
-        lib('c2dsr_pool2_bwd', dX2a[B:], wa, None, None, B, L, d, 0, dh_na, s)
-        lib('c2dsr_pool2_bwd', dX2b[B:], wb, None, None, B, L, d, 0, dh_nb, s)
+        # (row-subset outputs get row-subset gradients: pooling writes their rows, heads add through the maps)
+        dh_share, dhx, dhy, dh_na, dh_nb = [torch.empty(sh, **f32) for sh in ctx.hshapes]
+        rsets = ctx.rsets
+        sub = [(r.idx, r.n) if r is not None else (None, 0) for r in rsets]
+        mp = [r.inv if r is not None else None for r in rsets]
+        lib('c2dsr_pool2_bwd', dPhx, wa, None, None, B, L, d, *sub[1], 0, dhx, s)
+        lib('c2dsr_pool2_bwd', dPhy, wb, None, None, B, L, d, *sub[2], 0, dhy, s)
+        lib('c2dsr_pool2_bwd', dX2a, wb, dX2b, wa, B, L, d, *sub[0], 0, dh_share, s)
+        lib('c2dsr_pool2_bwd', dX2a[B:], wa, None, None, B, L, d, *sub[3], 0, dh_na, s)
+        lib('c2dsr_pool2_bwd', dX2b[B:], wb, None, None, B, L, d, *sub[4], 0, dh_nb, s)
         # ---- classifier heads ----
         gwpad, gbpad = _grad_target(m.wpad), _grad_target(m.bpad)
-        for (Hcat, Hpad, tcat, logits, lse, rows, W, bias, n), coef, hdom_grad in zip(ctx.heads, ctx.coefs,
-                                                                                      (dhx, dhy)):
+        for k, ((Hcat, Hpad, tcat, logits, lse, rows, W, bias, n), coef, hdom_grad) in enumerate(
+                zip(ctx.heads, ctx.coefs, (dhx, dhy))):
             M2 = 2 * BR
             dHcat = torch.empty(M2, d, **f32)
             dHpad = torch.zeros(M2, d, **f32)
@@ -295,5 +303,5 @@ class LossHeadFn(Function):
                 gemm(pad_col, Hpad, gwpad, M=1, N=d, K=M2, transA=1, lda=pad_ld, beta=1.0, precision=FP32)
             if gbpad is not None:
                 colsum(pad_col, M2, 1, pad_ld, gbpad)
-            lib('c2dsr_rec_scatter', dHcat, dHpad, B, L, d, R, dh_share, hdom_grad, s)
+            lib('c2dsr_rec_scatter', dHcat, dHpad, B, L, d, R, dh_share, mp[0], hdom_grad, mp[1 + k], s)
         return dh_share, dhx, dhy, dh_na, dh_nb, None

@@ -66,6 +66,7 @@ class StepState:
         self.grad_hook = None  # c2dsr_amd.dp.GradBuckets while a data-parallel backward runs
         self.plans = {}  # (step, data_ptr, numel, n_keys) -> ops.IndexPlan (sorted on the side stream)
         self.need = {}   # pass_id -> ops.RowSet: rows of the pass the loss reads (set by Trainer.train_batch)
+        self.compact_out = False  # encoder outputs of such passes stay [n, d] (the loss reads them through rs.inv)
 
     def keys(self, site):
         return DK.keys(self.seed, self.step, site)
@@ -128,7 +129,7 @@ class SelfAttention(nn.Module):
                 # Last layer, post-norm: everything after the attention is row-wise, and the loss reads only
                 # the rows of `rs` (pooled positions, last R positions) — the rest of the layer and the final
                 # LayerNorm run on those rows (dropout indices through the row map, so the masks are the
-                # full-size run's); the output is expanded back with zeros elsewhere.
+                # full-size run's).
                 r1 = ops.ResidualLink(inv=rs.inv)
                 qkv = ops.linear(x, at.in_proj_weight, at.in_proj_bias, self.precision, res=r1)
                 o = ops.AttnFn.apply(qkv, seq, self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset)
@@ -146,7 +147,8 @@ class SelfAttention(nn.Module):
                                        r2, rs.idx)
                 nm = self.encoder.norm
                 outc = ops.AddLNFn.apply(x2, None, nm.weight, nm.bias, 0.0, (0, 0), 0, nm.eps)
-                return ops.ExpandRowsFn.apply(outc, rs, (B, L, d))
+                # [n, d]: the loss head reads it through rs.inv (Trainer.train_batch passes the row sets)
+                return outc if self.state.compact_out else ops.ExpandRowsFn.apply(outc, rs, (B, L, d))
             if self.norm_first:
                 y = ops.AddLNFn.apply(x, None, lay.norm1.weight, lay.norm1.bias, 0.0, (0, 0), 0, lay.norm1.eps)
                 x = ops.AddDropFn.apply(x, sa_block(y), p_sa, k_sa, rb_rows)

@@ -187,15 +187,18 @@ class Trainer(object):
          neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
         m = self.model
         m.state.row_offset = row_offset
-        m.state.need, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b)
+        need, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b)
+        m.state.need, m.state.compact_out = need, bool(need)
         try:
             h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
             h_neg_a = m.forward_share(neg_a, pos)
             h_neg_b = m.forward_share(neg_b, pos)
         finally:
-            m.state.need = {}
+            m.state.need, m.state.compact_out = {}, False
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
         meta.ce_pre = ce_pre
+        if need:  # the five encoder outputs hold only these rows
+            meta.row_sets = tuple(need[pid] for pid, _ in self.PASS_ROWS)
         loss, loss_rec, loss_mi = LossHeadFn.apply(h_share, hx, hy, h_neg_a, h_neg_b, meta)
         if self.world > 1:
             # bucketed all-reduce of the fresh gradient, each bucket issued as soon as the backward

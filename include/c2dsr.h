@@ -108,11 +108,14 @@ int c2dsr_pool_fwd(const float* h, const float* w, int B, int L, int d, float* o
 int c2dsr_pool_bwd(const float* dout, const float* w, int B, int L, int d, float* dh, void* stream);
 /* two poolings of one h in one read (rows with zero weights skipped): out1[b] = Σ_l h[b,l]·w1[b,l],
  * out2[b] = Σ_l h[b,l]·w2[b,l] (w2 may be null); and the backward in write or accumulate mode:
- * dh[b,l] = (accumulate ? dh[b,l] : 0) + d1[b]·w1[b,l] + d2[b]·w2[b,l] (d2 may be null). */
-int c2dsr_pool2_fwd(const float* h, const float* w1, const float* w2, int B, int L, int d, float* out1, float* out2,
-                    void* stream);
+ * dh[b,l] = (accumulate ? dh[b,l] : 0) + d1[b]·w1[b,l] + d2[b]·w2[b,l] (d2 may be null).
+ * Row subsets (an encoder pass whose last layer ran on the rows the loss reads): h row (b,l) is
+ * h[hmap[b·L+l]] (hmap null: identity; every row with a nonzero weight must be mapped); the backward
+ * writes the n_rows rows of a compact dh, row k being (b,l) = idx[k] (idx null: all B·L rows). */
+int c2dsr_pool2_fwd(const float* h, const int* hmap, const float* w1, const float* w2, int B, int L, int d,
+                    float* out1, float* out2, void* stream);
 int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, const float* w2, int B, int L, int d,
-                    int accumulate, float* dh, void* stream);
+                    const int* idx, int n_rows, int accumulate, float* dh, void* stream);
 /* Stable row compaction, two launches over 1024-row tiles; ws = c2dsr_compact_workspace(M, n_sets) bytes
  * of device scratch (per-tile set sizes).
  * Valid-row compaction of a classifier head's targets (trainer.py:131-154: rows whose target is the
@@ -135,11 +138,11 @@ int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int 
                  long ldo, void* stream);
 /* loss_mi = Σ_k Σ_b BCE(s_k[b], y_k)/B_norm, ds = (σ(s)-y)/B_norm; s = [sim_a_pos; sim_a_neg; sim_b_pos; sim_b_neg] */
 int c2dsr_mi_loss(const float* s, int B, int B_norm, float* loss_mi, float* ds, void* stream);
-int c2dsr_rec_gather(const float* hs, const float* hx, int B, int L, int d, int R, float* Hcat, float* Hpad,
-                     void* stream);
+int c2dsr_rec_gather(const float* hs, const int* hs_map, const float* hx, const int* hx_map, int B, int L, int d,
+                     int R, float* Hcat, float* Hpad, void* stream);
 int c2dsr_rec_targets(const int64_t* ts, const int64_t* tx, int B, int L, int R, int64_t* tcat, void* stream);
-int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs, float* dhx,
-                      void* stream);
+int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs,
+                      const int* dhs_map, float* dhx, const int* dhx_map, void* stream);
 int c2dsr_ce_fwd(const float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, float* lse,
                  float* loss_row, void* stream);
 int c2dsr_ce_bwd(float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, const float* lse,
