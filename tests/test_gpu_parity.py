@@ -143,15 +143,15 @@ def test_train_steps_match_reference(name, compact):
                     p.copy_(ref.to(DEV))
 
 
-@pytest.mark.parametrize('norm_first,n_head,n_gnn', [(False, 1, 1), (True, 2, 2)])
-def test_train_step_with_dropout_matches_oracle(norm_first, n_head, n_gnn):
+@pytest.mark.parametrize('norm_first,n_head,n_gnn,n_attn', [(False, 1, 1, 1), (True, 2, 2, 1), (False, 2, 1, 2)])
+def test_train_step_with_dropout_matches_oracle(norm_first, n_head, n_gnn, n_attn):
     """Larger synthetic case, dropout 0.2 everywhere: HIP step vs oracle with the same hash masks."""
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
     from c2dsr_amd import synth
     from oracle import c2dsr_oracle as O
     import random
-    c = dict(n_a=300, n_b=400, len_max=20, len_rec=5, d_latent=64, n_gnn=n_gnn, n_attn=1, n_head=n_head,
+    c = dict(n_a=300, n_b=400, len_max=20, len_rec=5, d_latent=64, n_gnn=n_gnn, n_attn=n_attn, n_head=n_head,
              norm_first=norm_first, d_bias=True, shared_item_embed=False)
     seqs = synth.make_sequences(200, c['n_a'], c['n_b'], c['len_max'], seed=3, n_min=4)
     random.seed(3407)
@@ -166,7 +166,7 @@ def test_train_step_with_dropout_matches_oracle(norm_first, n_head, n_gnn):
         r, cc, v = g.coo()
         graphs[k] = (torch.from_numpy(r), torch.from_numpy(cc), torch.from_numpy(v))
     ocfg = dict(d_latent=64, n_item_a=c['n_a'], n_item_b=c['n_b'], idx_pad=c['n_a'] + c['n_b'], len_rec=5,
-                lambda_loss=0.7, n_gnn=n_gnn, n_attn=1, n_head=n_head, norm_first=norm_first, d_bias=True,
+                lambda_loss=0.7, n_gnn=n_gnn, n_attn=n_attn, n_head=n_head, norm_first=norm_first, d_bias=True,
                 shared_item_embed=False, dropout_gnn=0.2, dropout_attn=0.2)
     orc = O.OracleTrainer(params, graphs, ocfg, seed=77)
     orc.step_no = 1  # the model's first convolve_graph opens step 1
