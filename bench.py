@@ -200,10 +200,10 @@ def k5_traffic(precision):
     absent or for another precision)."""
     path = os.path.join(ROOT, 'profiles', 'k5_traffic.json')
     if precision != 'bf16' or not os.path.exists(path):
-        return None, None
+        return None, None, None
     with open(path) as f:
         t = json.load(f)
-    return t.get('bytes_per_launch_triple'), t.get('source')
+    return t.get('bytes_per_launch_triple'), t.get('source'), t.get('mfma_busy')
 
 
 def hbm_traffic():
@@ -457,13 +457,15 @@ def main():
         peak = PEAK_BF16_TFLOPS if opt.precision == 'bf16' else PEAK_FP32_TFLOPS
         roof = None
         if ks is not None:
-            traffic, tsrc = k5_traffic(opt.precision)
+            traffic, tsrc, busy = k5_traffic(opt.precision)
             roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
                         frac=round(ks['tflops'] / peak, 4), traffic=traffic, traffic_source=tsrc,
                         kernel=('K5 fused classifier head + CE: ce_lse_kernel + ce_dh_kernel + ce_dw_kernel '
                                 '(bf16 MFMA); credited 2·M·n·d per launch each'
                                 if opt.precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
-                        ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'])
+                        ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'],
+                        mfma_busy=busy, mfma_busy_note='SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles of the K5 launches '
+                        '(same PMC run as traffic; counts the recomputed logits tiles that frac does not credit)')
         if hb is not None and opt.config == 'mb' and opt.precision == 'bf16':
             hb['traffic'], hb['traffic_source'] = hbm_traffic()
             hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'

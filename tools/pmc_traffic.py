@@ -40,9 +40,26 @@ for k in K5:
     print(f'{k:16} launches {len(fe[k]):3d}  fetch {f / 1e6:9.1f} MB  write {w / 1e6:8.1f} MB')
 tot = sum(r['bytes'] for r in rows.values())
 print(f'K5 launch triple: {tot / 1e6:.1f} MB')
+# MFMA-busy fraction of the K5 kernels from the SQ pass (SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs'
+# cycles, GRBM_GUI_ACTIVE summed over the 8 XCDs), summed over their launches
+mfma_busy = None
+try:
+    busy, cyc = 0.0, 0.0
+    for r in csv.DictReader(open(f'{pre}_sq/run_counter_collection.csv')):
+        name = re.sub(r'\(anonymous namespace\)::', '', r['Kernel_Name'])
+        if not any(re.search(r'\b' + k + r'\b', name) for k in K5):
+            continue
+        if r['Counter_Name'] == 'SQ_VALU_MFMA_BUSY_CYCLES':
+            busy += float(r['Counter_Value'])
+        elif r['Counter_Name'] == 'GRBM_GUI_ACTIVE':
+            cyc += 1024 * float(r['Counter_Value']) / 8
+    mfma_busy = round(busy / cyc, 4) if cyc else None
+    print(f'K5 MFMA busy: {mfma_busy}')
+except FileNotFoundError:
+    pass
 if out:
     rev = subprocess.run(['git', 'rev-parse', '--short', 'HEAD'], capture_output=True, text=True).stdout.strip()
-    json.dump(dict(bytes_per_launch_triple=tot, per_kernel=rows,
+    json.dump(dict(bytes_per_launch_triple=tot, per_kernel=rows, mfma_busy=mfma_busy,
                    source=f'rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE passes, {pre.split("/")[-1]}, rev {rev}'),
               open(out, 'w'), indent=1)
 
