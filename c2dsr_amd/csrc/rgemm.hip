@@ -390,10 +390,10 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __re
 }
 
 // out[i] = beta·out[i] + Σ_s part[s][i]  (fixed order, float4): 8 lanes per float4 output, lane j
-// summing the splits s ≡ j (mod 8), then a fixed xor tree over the 8 lanes
-__global__ void sum_parts_kernel2(const float* __restrict__ part, int nparts, long n, float beta,
-                                  float* __restrict__ out) {
-  const long g = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// summing the splits s ≡ j (mod 8), then a fixed xor tree over the 8 lanes.  blk: this range's block.
+__device__ __forceinline__ void sum_parts_body(const float* __restrict__ part, int nparts, long n, float beta,
+                                               float* __restrict__ out, long blk) {
+  const long g = blk * blockDim.x + threadIdx.x;
   const long i = (g >> 3) * 4;
   const int j = (int)(g & 7);
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -412,6 +412,17 @@ __global__ void sum_parts_kernel2(const float* __restrict__ part, int nparts, lo
   if (i >= n || j) return;
   float4 o = beta == 0.f ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(out + i);
   *(float4*)(out + i) = make_float4(beta * o.x + t.x, beta * o.y + t.y, beta * o.z + t.z, beta * o.w + t.w);
+}
+
+// the weight and bias partial sums of one wgemm in one launch: blocks [0, blocks_a) sum range a, the rest
+// range b (each block entirely in one range)
+__global__ void sum_parts_kernel2(const float* __restrict__ part_a, long n_a, float* __restrict__ out_a,
+                                  const float* __restrict__ part_b, long n_b, float* __restrict__ out_b,
+                                  int nparts, float beta, long blocks_a) {
+  if ((long)blockIdx.x < blocks_a)
+    sum_parts_body(part_a, nparts, n_a, beta, out_a, blockIdx.x);
+  else
+    sum_parts_body(part_b, nparts, n_b, beta, out_b, blockIdx.x - blocks_a);
 }
 
 // fp32 [R][Cc] (row stride lds) → bf16, optionally transposed (out [Cc][R])
@@ -546,8 +557,9 @@ C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const floa
   const long n = (long)N * 256;
   float* part_b = db ? (float*)part + (long)splits * n : nullptr;
   wg_kernel<<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, part_b, NTL, rows);
-  sum_parts_kernel2<<<c2::ceil_div(n / 4 * 8, 256), 256, 0, s>>>((const float*)part, splits, n, beta, dW);
-  if (db) sum_parts_kernel2<<<c2::ceil_div((long)N / 4 * 8, 256), 256, 0, s>>>(part_b, splits, N, beta, db);
+  const long blocks_a = c2::ceil_div(n / 4 * 8, 256), blocks_b = db ? c2::ceil_div((long)N / 4 * 8, 256) : 0;
+  sum_parts_kernel2<<<blocks_a + blocks_b, 256, 0, s>>>((const float*)part, n, dW, part_b, N, db, splits, beta,
+                                                        blocks_a);
   C2_CHECK_LAUNCH();
   return 0;
 }
