@@ -362,8 +362,11 @@ __global__ void rec_targets_kernel(const int64_t* __restrict__ ts, const int64_t
   tcat[BR + r] = tx[b * L + l];
 }
 
-// dhs[b,l] += dHcat[r] + dHcat[BR+r] + dHpad[r];  dhx[b,l] += dHcat[BR+r] + dHpad[BR+r]
-__global__ void rec_scatter_kernel(const float* __restrict__ dHcat, const float* __restrict__ dHpad, int B, int L,
+// dhs[b,l] += dHcat[r] + dHcat[BR+r] + pad[r]·wpad;  dhx[b,l] += dHcat[BR+r] + pad[BR+r]·wpad
+// (pad = the pad column of dlogits, stride pad_ld: the classifier_pad input gradient is its outer product
+// with wpad, folded in here instead of being materialised)
+__global__ void rec_scatter_kernel(const float* __restrict__ dHcat, const float* __restrict__ pad, long pad_ld,
+                                   const float* __restrict__ wpad, int B, int L,
                                    int d, int R, float* __restrict__ dhs, const int* __restrict__ dhs_map,
                                    float* __restrict__ dhx, const int* __restrict__ dhx_map) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -373,9 +376,9 @@ __global__ void rec_scatter_kernel(const float* __restrict__ dHcat, const float*
   const int c = (int)(i % d);
   const long b = r / R, l = L - R + r % R;
   const long bl = b * L + l;
-  const float g1 = dHcat[r * d + c], g2 = dHcat[(BR + r) * d + c];
-  dhs[(dhs_map ? dhs_map[bl] : bl) * d + c] += g1 + g2 + dHpad[r * d + c];
-  dhx[(dhx_map ? dhx_map[bl] : bl) * d + c] += g2 + dHpad[(BR + r) * d + c];
+  const float g1 = dHcat[r * d + c], g2 = dHcat[(BR + r) * d + c], wp = wpad[c];
+  dhs[(dhs_map ? dhs_map[bl] : bl) * d + c] += g1 + g2 + pad[r * pad_ld] * wp;
+  dhx[(dhx_map ? dhx_map[bl] : bl) * d + c] += g2 + pad[(BR + r) * pad_ld] * wp;
 }
 
 // Per-row CE: lse over ncol logits, loss_row = valid ? lse - logit[t] : 0.  One wave per row.
@@ -606,12 +609,12 @@ C2_API int c2dsr_rec_targets(const int64_t* ts, const int64_t* tx, int B, int L,
   C2_CHECK_LAUNCH();
   return 0;
 }
-C2_API int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs,
-                             const int* dhs_map, float* dhx, const int* dhx_map, void* stream) {
+C2_API int c2dsr_rec_scatter(const float* dHcat, const float* pad, long pad_ld, const float* wpad, int B, int L, int d,
+                             int R, float* dhs, const int* dhs_map, float* dhx, const int* dhx_map, void* stream) {
   const long n = (long)B * R * d;
   if (n == 0) return 0;
-  rec_scatter_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dHcat, dHpad, B, L, d, R, dhs, dhs_map, dhx,
-                                                                            dhx_map);
+  rec_scatter_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(dHcat, pad, pad_ld, wpad, B, L, d, R, dhs,
+                                                                            dhs_map, dhx, dhx_map);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -249,7 +249,6 @@ class LossHeadFn(Function):
                 zip(ctx.heads, ctx.coefs, (dhx, dhy))):
             M2 = 2 * BR
             dHcat = torch.empty(M2, d, **f32)
-            dHpad = torch.zeros(M2, d, **f32)
             gW, gb = _grad_target(W), _grad_target(bias)
             if ctx.fused:
                 Hb, Wb, padc, lse2, bias2, tplan, Hc, tc, inv, Mv, Mv0, lse_c = logits
@@ -298,10 +297,11 @@ class LossHeadFn(Function):
                 if gb is not None:
                     colsum(logits, M2, n, ld, gb)
                 pad_col, pad_ld = logits[:, n:], ld
-            lib('c2dsr_outer_add', pad_col, pad_ld, m.wpad, M2, d, dHpad, d, s)
             if gwpad is not None:
                 gemm(pad_col, Hpad, gwpad, M=1, N=d, K=M2, transA=1, lda=pad_ld, beta=1.0, precision=FP32)
             if gbpad is not None:
                 colsum(pad_col, M2, 1, pad_ld, gbpad)
-            lib('c2dsr_rec_scatter', dHcat, dHpad, B, L, d, R, dh_share, mp[0], hdom_grad, mp[1 + k], s)
+            # classifier_pad's input gradient (pad column ⊗ wpad) is folded into the scatter
+            lib('c2dsr_rec_scatter', dHcat, pad_col, pad_ld, m.wpad, B, L, d, R, dh_share, mp[0], hdom_grad, mp[1 + k],
+                s)
         return dh_share, dhx, dhy, dh_na, dh_nb, None

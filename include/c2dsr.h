@@ -141,8 +141,11 @@ int c2dsr_mi_loss(const float* s, int B, int B_norm, float* loss_mi, float* ds, 
 int c2dsr_rec_gather(const float* hs, const int* hs_map, const float* hx, const int* hx_map, int B, int L, int d,
                      int R, float* Hcat, float* Hpad, void* stream);
 int c2dsr_rec_targets(const int64_t* ts, const int64_t* tx, int B, int L, int R, int64_t* tcat, void* stream);
-int c2dsr_rec_scatter(const float* dHcat, const float* dHpad, int B, int L, int d, int R, float* dhs,
-                      const int* dhs_map, float* dhx, const int* dhx_map, void* stream);
+/* dhs[b,l] += dHcat[r] + dHcat[BR+r] + pad[r·pad_ld]·wpad;  dhx[b,l] += dHcat[BR+r] + pad[(BR+r)·pad_ld]·wpad
+ * for the last R positions (r = b·R + l - (L-R)); pad = the pad column of the stacked dlogits (classifier_pad,
+ * trainer.py:136-140), its input gradient folded in; maps as for c2dsr_rec_gather */
+int c2dsr_rec_scatter(const float* dHcat, const float* pad, long pad_ld, const float* wpad, int B, int L, int d, int R,
+                      float* dhs, const int* dhs_map, float* dhx, const int* dhx_map, void* stream);
 int c2dsr_ce_fwd(const float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, float* lse,
                  float* loss_row, void* stream);
 int c2dsr_ce_bwd(float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, const float* lse,
