@@ -538,8 +538,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fast(const float* __restrict_
 // Keys past the last padding key are inadmissible for every query (Q1), so only jmax rows of K/V
 // are read (buffer descriptors zero the rest).
 // softmax of one query tile of transposed scores held by lane = query (tiles a: keys 0..31 and, when
-// TWO, b: keys 32..63) → probabilities to prow (all L keys of each row; 0 past the tiles) and the
-// dropped probabilities back into a / b.  Masks: key admissible (pad bit of kb), causal j <= i, i < L.
+// TWO, b: keys 32..63) → probabilities to the wave's save area in REGISTER layout (tile t of query tile
+// ti at pw[(2·ti + t)·1024 + 64·q + lane]: every store instruction writes 256 contiguous bytes, and the
+// backward reloads them in the same layout) and the dropped probabilities back into a / b.
+// Masks: key admissible (pad bit of kb), causal j <= i, i < L (masked entries are stored as 0).
+constexpr int WAVE_PSAVE = 4096;  // floats of probability save per (sequence, head) on the wave path
+
 template <bool TWO>
 __device__ __forceinline__ void wave_softmax(f32x16& a, f32x16& b, int ti, int L, uint64_t kb, float sc,
                                              const c2::Drop& drop, uint64_t pbase, float* __restrict__ prow0) {
@@ -573,22 +577,21 @@ __device__ __forceinline__ void wave_softmax(f32x16& a, f32x16& b, int ti, int L
   }
   sum += __shfl_xor(sum, 32, 64);
   const float inv = sum > 0.f ? 1.0f / sum : 0.f;
-  float* prow = prow0 + (long)i * L;
+  float* pw = prow0 + 2 * ti * 1024 + lane;
   const uint64_t rb = pbase + (uint64_t)i * L;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int j = creg(q, lane);
     const float p0 = a[q] * inv;
-    if (row && j < L) prow[j] = p0;
+    pw[64 * q] = p0;
     a[q] = p0 * drop.mul(rb + j);
     if constexpr (TWO) {
       const float p1 = b[q] * inv;
-      if (row && 32 + j < L) prow[32 + j] = p1;
+      pw[1024 + 64 * q] = p1;
       b[q] = p1 * drop.mul(rb + 32 + j);
     }
   }
-  if (row)  // probabilities of the keys past the computed tiles are 0
-    for (int j = (TWO ? 64 : 32) + hi; j < L; j += 2) prow[j] = 0.f;
+  (void)hi;
 }
 
 template <int TJ, int TI>
@@ -703,7 +706,7 @@ __global__ __launch_bounds__(256) void attn_fwd_wave(const float* __restrict__ q
   const float* Q = qkv + (long)b * L * rs + h * dh;
   const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
   float* orow = out + (long)b * L * d + h * dh;
-  float* prow = Psave + (long)bh * L * L;
+  float* prow = Psave + (long)bh * WAVE_PSAVE;
   const int TJ = jmax > 32 ? 2 : 1, TI = L > 32 ? 2 : 1;
   if (TI == 1)
     fwd_wave_body<1, 1>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
@@ -784,14 +787,14 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
   auto sgrad = [&](f32x16& g_a, f32x16& g_b, f32x16& p_a, f32x16& p_b, bool two, int ti) {
     const int i = 32 * ti + r;
     const bool row = i < L;
-    const float* prow = prow0 + (long)i * L;
+    const float* pw = prow0 + 2 * ti * 1024 + lane;  // the forward's register-layout save (wave_softmax)
     const uint64_t rb = pbase + (uint64_t)i * L;
     float acc = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int j0 = creg(q, lane), j1 = 32 + j0;
-      const float pa = row && j0 < L ? prow[j0] : 0.f;
-      const float pb = two && row && j1 < L ? prow[j1] : 0.f;
+      const float pa = row ? pw[64 * q] : 0.f;
+      const float pb = two && row ? pw[1024 + 64 * q] : 0.f;
       const float ma = drop.mul(rb + j0), mb = two ? drop.mul(rb + j1) : 0.f;
       const bool ada = row && j0 <= i && ((kb >> j0) & 1), adb = two && row && j1 <= i && ((kb >> j1) & 1);
       g_a[q] = ada ? g_a[q] * ma : 0.f;
@@ -935,7 +938,7 @@ __global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ q
   const float* dO = dout + (long)b * L * d + h * dh;
   float* dQ = dqkv + (long)b * L * rs + h * dh;
   const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
-  const float* prow = Psave + (long)bh * L * L;
+  const float* prow = Psave + (long)bh * WAVE_PSAVE;
   const int TJ = jmax > 32 ? 2 : 1, TI = L > 32 ? 2 : 1;
   if (TI == 1)
     bwd_wave_body<1, 1>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
@@ -974,10 +977,20 @@ void launch_bwd(dim3 grid, hipStream_t s, const float* qkv, const int64_t* seq, 
   attn_bwd_kernel<LP><<<grid, 256, bwd_smem<LP>(), s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
 }
 
+bool wave_path(int L, int d, int H) { return L <= 64 && (d / H) % 32 == 0 && !getenv("C2DSR_ATTN_TILED"); }
+
 }  // namespace
 
+// floats of Psave c2dsr_attn_fwd / _bwd need: B·H·L·L on the tiled paths, B·H·4096 on the wave path
+// (probabilities kept in the kernels' register layout)
+C2_API size_t c2dsr_attn_psave_floats(int B, int L, int d, int H) {
+  if (H <= 0 || d % H) return 0;
+  return (size_t)B * H * (wave_path(L, d, H) ? WAVE_PSAVE : (size_t)L * L);
+}
+
 // qkv [B, L, 3d] (q | k | v per row, heads contiguous inside each), out [B, L, d],
-// Psave [B, H, L, L] softmax probabilities (pre-dropout).  Dropout index:
+// Psave c2dsr_attn_psave_floats(B, L, d, H) floats: softmax probabilities (pre-dropout), [B, H, L, L]
+// on the tiled paths, the wave kernels' register layout on the wave path.  Dropout index:
 // (((b_base + b)*H + h)*L + i)*L + j.
 C2_API int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,
                           uint32_t k1, float p, int64_t b_base, float* out, float* Psave, void* stream) {
@@ -987,7 +1000,7 @@ C2_API int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
   const bool fast = (d / H) % 4 == 0 && d % 4 == 0;
-  if (L <= 64 && (d / H) % 32 == 0 && !getenv("C2DSR_ATTN_TILED"))
+  if (wave_path(L, d, H))
     attn_fwd_wave<<<c2::ceil_div((long)B * H, 4), 256, 0, s>>>(qkv, seq, pad, B, L, d, H, dr, b_base, out, Psave);
   else if (fast && L <= 32)
     attn_fwd_fast<32><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, out, Psave);
@@ -1012,7 +1025,7 @@ C2_API int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int
   hipStream_t s = (hipStream_t)stream;
   dim3 grid(B * H);
   const bool fast = (d / H) % 4 == 0 && d % 4 == 0;
-  if (L <= 64 && (d / H) % 32 == 0 && !getenv("C2DSR_ATTN_TILED"))
+  if (wave_path(L, d, H))
     attn_bwd_wave<<<c2::ceil_div((long)B * H, 4), 256, 0, s>>>(qkv, seq, pad, B, L, d, H, dr, b_base, Psave, dout,
                                                                dqkv);
   else if (fast && L <= 32)

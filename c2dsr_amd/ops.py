@@ -603,7 +603,8 @@ class AttnFn(Function):
         B, L, d3 = qkv.shape
         d = d3 // 3
         out = torch.empty(B, L, d, device=qkv.device, dtype=torch.float32)
-        P = torch.empty(B, n_head, L, L, device=qkv.device, dtype=torch.float32)
+        P = torch.empty(int(lib.raw('c2dsr_attn_psave_floats')(B, L, d, n_head)), device=qkv.device,
+                        dtype=torch.float32)  # the kernels' own layout
         lib('c2dsr_attn_fwd', qkv, seq, int(pad), B, L, d, n_head, keys[0], keys[1], float(p), int(b_base), out, P,
             stream())
         ctx.save_for_backward(qkv, seq, P)

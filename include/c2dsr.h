@@ -81,7 +81,10 @@ int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta,
                  void* stream);
 
 /* Attention core (SDPA math path with causal + inverted key-padding mask, Q1/Q2;
- * models/encoders.py:14,33).  qkv [B,L,3d], out [B,L,d], Psave [B,H,L,L]; L <= 128. */
+ * models/encoders.py:14,33).  qkv [B,L,3d], out [B,L,d], Psave c2dsr_attn_psave_floats(B, L, d, H) floats
+ * (the saved probabilities: [B,H,L,L] on the tiled paths, the wave kernels' register layout on the
+ * wave path, L <= 64 and d/H % 32 == 0); L <= 128. */
+size_t c2dsr_attn_psave_floats(int B, int L, int d, int H);
 int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,
                    uint32_t k1, float p, int64_t b_base, float* out, float* Psave, void* stream);
 int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,

@@ -35,7 +35,7 @@ def main():
     sd = torch.from_numpy(seq).to(dev)
     qkv = torch.randn(B, L, 3 * d, device=dev)
     out = torch.empty(B, L, d, device=dev)
-    P = torch.empty(B, H, L, L, device=dev)
+    P = torch.empty(int(lib.raw("c2dsr_attn_psave_floats")(B, L, d, H)), device=dev)  # the kernels' layout
     dout = torch.randn(B, L, d, device=dev)
     dqkv = torch.empty_like(qkv)
     s = stream()
