@@ -17,7 +17,9 @@ namespace {
 //   rank = 1 + #{k : s(neg[i,k]) > s(gt[i])}             (trainer.py:173,180; ties not counted)
 // Every candidate is scored by the same lane mapping and reduction tree, so an item that
 // appears as both target and negative gets bit-identical scores (as in the reference's
-// single GEMV).  Bad indices (outside [0,L) / [0,n_dom)) give rank = -1 (the host raises).
+// single GEMV).  Negative indices wrap as torch indexing does (hx[i, -1] is position L-1,
+// scores[-k] is item n_dom-k); indices outside [-L,L) / [-n_dom,n_dom) give rank = -1 (the
+// host raises IndexError, as the reference would).
 template <int G, bool VEC>
 __global__ __launch_bounds__(256) void eval_rank_kernel(
     const float* __restrict__ hs, const float* __restrict__ ha, const float* __restrict__ hb, int L, int d,
@@ -33,7 +35,8 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(
   const int i = blockIdx.x;
   const int tid = threadIdx.x;
   const bool da = xory[i] == 0;
-  const int64_t il = da ? il_a[i] : il_b[i];
+  int64_t il = da ? il_a[i] : il_b[i];
+  if (il < 0) il += L;
   const float* hdom = da ? ha : hb;
   const float* W = da ? Wa : Wb;
   const float* bias = da ? ba : bb;
@@ -55,7 +58,8 @@ __global__ __launch_bounds__(256) void eval_rank_kernel(
   const int grp = tid / G;
   constexpr int NG = 256 / G;
   for (int j = grp; j < n_cand; j += NG) {
-    const int64_t item = j == 0 ? gt[i] : neg[(long)i * n_neg + (j - 1)];
+    int64_t item = j == 0 ? gt[i] : neg[(long)i * n_neg + (j - 1)];
+    if (item < 0) item += n_dom;
     float acc = 0.f;
     if (item >= 0 && item < n_dom) {
       const float* w = W + item * (long)d;

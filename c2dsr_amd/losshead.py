@@ -304,4 +304,7 @@ class LossHeadFn(Function):
             # classifier_pad's input gradient (pad column ⊗ wpad) is folded into the scatter
             lib('c2dsr_rec_scatter', dHcat, pad_col, pad_ld, m.wpad, B, L, d, R, dh_share, mp[0], hdom_grad, mp[1 + k],
                 s)
+        # the saved buffers (bf16 images, logits / lse, plans) are released with the backward even if a
+        # caller keeps the graph alive (e.g. an undetached loss accumulator)
+        ctx.m = ctx.heads = ctx.mi = ctx.w = ctx.rsets = ctx.coefs = None
         return dh_share, dhx, dhy, dh_na, dh_nb, None

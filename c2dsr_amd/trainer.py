@@ -87,7 +87,7 @@ class Trainer(object):
         for batch in self.trainloader:
             self.model.convolve_graph()
             loss, loss_rec, loss_mi = self.train_batch(batch)
-            acc += torch.stack([loss, loss_rec, loss_mi]) * batch[0].shape[0]  # one sync per epoch (f4)
+            acc += torch.stack([loss.detach(), loss_rec, loss_mi]) * batch[0].shape[0]  # one sync per epoch (f4)
         acc = (acc / max(self.n_tr, 1)).tolist()
         if self.noter is not None:
             self.noter.log_train(acc[0], acc[1], acc[2], time.time() - t0)

@@ -260,6 +260,18 @@ def train_forward(P, graphs, batch, cfg, dropper, counts=None):
     h_neg_b = encode(P, hs_t, es, 'attn_share', neg_b, pos, cfg, dropper, 4)
     out.update(h_share=h_share, hx=hx, hy=hy, h_neg_a=h_neg_a, h_neg_b=h_neg_b)
 
+    out.update(loss_head(P, h_share, hx, hy, h_neg_a, h_neg_b, batch, cfg, counts))
+    return out
+
+
+def loss_head(P, h_share, hx, hy, h_neg_a, h_neg_b, batch, cfg, counts=None):
+    """trainer.py:101-156: pooling (cal_mask), the bilinear discriminators + BCE and the four classifier
+    heads + CE, from the five encoder outputs.  Device-agnostic (tests also run it on cuda tensors as the
+    fp32 checker of the full-size bf16 head)."""
+    (seq, _, _, _, _, _, gt_sa, gt_sb, gt_a, gt_b, gm_a, gm_b, _, _) = batch
+    n_a, n_b, R = cfg['n_item_a'], cfg['n_item_b'], cfg['len_rec']
+    B = seq.shape[0]
+    out = {}
     wa = (gm_a.float() / gm_a.float().sum(-1, keepdim=True))[..., None]
     wb = (gm_b.float() / gm_b.float().sum(-1, keepdim=True))[..., None]
     hx_mean = (hx * wa).sum(1)
@@ -272,8 +284,8 @@ def train_forward(P, graphs, batch, cfg, dropper, counts=None):
     sim_b_neg = bilinear(hy_mean, (h_neg_b * wb).sum(1), P['D_b.weight'], Db_b)
     out['sim_a'] = torch.stack([sim_a_pos, sim_a_neg])
     out['sim_b'] = torch.stack([sim_b_pos, sim_b_neg])
-    one = torch.ones(B, 1)
-    zero = torch.zeros(B, 1)
+    one = torch.ones(B, 1, device=hx.device)
+    zero = torch.zeros(B, 1, device=hx.device)
     cB = None if counts is None else float(counts[0])
     loss_mi = bce_logits(sim_a_pos, one, cB) + bce_logits(sim_a_neg, zero, cB) + \
         bce_logits(sim_b_pos, one, cB) + bce_logits(sim_b_neg, zero, cB)

@@ -69,10 +69,13 @@ def test_eval_rank_kernel_large(d, n_neg, L):
     ba, bb = torch.randn(n_a, generator=g), torch.randn(n_b, generator=g)
     xory = torch.randint(0, 2, (B, 1), generator=g)
     il_a, il_b = torch.randint(0, L, (B, 1), generator=g), torch.randint(0, L, (B, 1), generator=g)
+    # no prior item in the domain: the reference reads hx[i, -1] (Python wrap to L-1)
+    il_a[::5], il_b[::7], il_b[1::11] = -1, -1, -L
     n_dom = torch.where(xory[:, 0] == 0, n_a, n_b)
     gt = (torch.rand(B, 1, generator=g) * n_dom[:, None]).long()
     neg = (torch.rand(B, n_neg, generator=g) * n_dom[:, None]).long()
     neg[::3, 0] = gt[::3, 0]
+    neg[1::13, 1] = -1  # torch indexing wraps a negative item id too (scores[-1])
     got = ops.eval_rank(*(t.to(DEV) for t in (hs, ha, hb, il_a, il_b, xory, gt, neg, Wa, ba, Wb, bb))).cpu()
     for i in range(B):
         dom_a = int(xory[i]) == 0
@@ -80,10 +83,11 @@ def test_eval_rank_kernel_large(d, n_neg, L):
         W, b = (Wa, ba) if dom_a else (Wb, bb)
         s = W.double() @ q + b.double()
         sg = s[gt[i, 0]]
-        sn = s[neg[i]]
+        sn = s[neg[i]]  # wraps negative ids like the reference's scores_a[list_neg[i]]
         band = 1e-5 * float(s.abs().max())
         lo = 1 + int((sn > sg + band).sum())
-        hi = 1 + int(((sn > sg - band) & (neg[i] != gt[i, 0])).sum())
+        same = (neg[i] % len(s)) == (gt[i, 0] % len(s))
+        hi = 1 + int(((sn > sg - band) & ~same).sum())
         assert lo <= int(got[i]) <= hi, (i, int(got[i]), lo, hi)
 
 

@@ -162,13 +162,23 @@ def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
     assert np.array_equal(kk, seq[order]) and np.array_equal(vv, order)
 
 
-@pytest.mark.parametrize('L,d,H,p', [(8, 16, 1, 0.0), (8, 16, 2, 0.0), (50, 256, 1, 0.2), (30, 64, 2, 0.1),
-                                     (100, 128, 1, 0.0), (128, 64, 4, 0.0)])
-def test_attention_vs_oracle(L, d, H, p):
+def _tail_of_segment(t):
+    """A device copy of ``t`` whose storage ENDS where its own hipMalloc segment ends (the caching allocator
+    gives requests >= 10 MB, rounded to 2 MB, a segment of their own): a kernel reading past the tensor's
+    last element leaves the allocation (regression guard for the round-1 attention fault)."""
+    torch.cuda.empty_cache()
+    seg = 2 << 20
+    nbytes = max(12 << 20, -(-t.numel() * 4 // seg) * seg)
+    buf = torch.empty(nbytes // 4, device=DEV, dtype=torch.float32)
+    out = buf[buf.numel() - t.numel():].view(t.shape)
+    out.copy_(t.to(DEV))
+    return out
+
+
+def _attention_case(B, L, d, H, p, tail=False):
     from c2dsr_amd import ops
     from oracle import c2dsr_oracle as O
-    torch.manual_seed(L + d)
-    B = 24
+    torch.manual_seed(L + d + B)
     pad = 999
     lens = torch.randint(1, L, (B,))
     seq = torch.randint(0, 900, (B, L))
@@ -180,11 +190,10 @@ def test_attention_vs_oracle(L, d, H, p):
     seed, step = 5, 9
     dr = O.Dropper(0.0, p, seed, step)
     keys = O.dropout_keys(seed, step, O.site_enc(2, 0, 1))
-    qd = qkv.to(DEV).requires_grad_(True)
+    qd = (_tail_of_segment(qkv) if tail else qkv.to(DEV)).requires_grad_(True)
     out = ops.AttnFn.apply(qd, seq.to(DEV), pad, H, p, keys, 0)
     # the oracle's attention math (oracle/c2dsr_oracle.py:attention) on the given q, k, v
     qr = qkv.clone().requires_grad_(True)
-    # reproduce O.attention on given q,k,v
     dh = d // H
     q, k, v = qr.split(d, -1)
     q = q.reshape(B, L, H, dh).transpose(1, 2)
@@ -202,9 +211,25 @@ def test_attention_vs_oracle(L, d, H, p):
     ref = (a @ v).transpose(1, 2).reshape(B, L, d)
     assert rel(out, ref) < 1e-5
     go = torch.randn(B, L, d)
-    out.backward(go.to(DEV))
+    out.backward(_tail_of_segment(go) if tail else go.to(DEV))
     ref.backward(go)
+    torch.cuda.synchronize()
     assert rel(qd.grad, qr.grad) < 1e-5
+
+
+@pytest.mark.parametrize('L,d,H,p', [(8, 16, 1, 0.0), (8, 16, 2, 0.0), (50, 256, 1, 0.2), (30, 64, 2, 0.1),
+                                     (100, 128, 1, 0.0), (128, 64, 4, 0.0)])
+def test_attention_vs_oracle(L, d, H, p):
+    _attention_case(24, L, d, H, p)
+
+
+# wave path: L <= 64 and d/H % 32 == 0; tiled otherwise.  Short / odd last batches with qkv (and dout)
+# ending exactly at the end of their allocation: the round-1 fault was a wave-path buffer descriptor
+# reaching past the last sequence (test_train_steps_match_reference[shared], B 8, L 8, d 16).
+@pytest.mark.parametrize('B,L,d,H,p', [(8, 8, 16, 1, 0.0), (13, 50, 256, 1, 0.2), (7, 8, 64, 2, 0.0),
+                                       (5, 100, 128, 1, 0.1), (1, 50, 256, 1, 0.0), (3, 64, 32, 1, 0.0)])
+def test_attention_short_batch_at_allocation_end(B, L, d, H, p):
+    _attention_case(B, L, d, H, p, tail=True)
 
 
 @pytest.mark.parametrize('d', [16, 64, 256, 512])

@@ -143,21 +143,21 @@ def test_train_steps_match_reference(name, compact):
                     p.copy_(ref.to(DEV))
 
 
-@pytest.mark.parametrize('norm_first,n_head,n_gnn,n_attn', [(False, 1, 1, 1), (True, 2, 2, 1), (False, 2, 1, 2)])
-def test_train_step_with_dropout_matches_oracle(norm_first, n_head, n_gnn, n_attn):
-    """Larger synthetic case, dropout 0.2 everywhere: HIP step vs oracle with the same hash masks."""
+def _oracle_case(c, *, B, n_users, dropout=0.2, precision='fp32', seed=77):
+    """Synthetic raw sequences → (HIP trainer, OracleTrainer with the same params, graphs and hash masks,
+    int64 batch rows)."""
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
     from c2dsr_amd import synth
     from oracle import c2dsr_oracle as O
     import random
-    c = dict(n_a=300, n_b=400, len_max=20, len_rec=5, d_latent=64, n_gnn=n_gnn, n_attn=n_attn, n_head=n_head,
-             norm_first=norm_first, d_bias=True, shared_item_embed=False)
-    seqs = synth.make_sequences(200, c['n_a'], c['n_b'], c['len_max'], seed=3, n_min=4)
+    seqs = synth.make_sequences(n_users, c['n_a'], c['n_b'], c['len_max'], seed=3, n_min=4)
     random.seed(3407)
     rows = DL.to_arrays(DL.preprocess_train(seqs, c['n_a'], c['n_b'], c['len_max']))
+    assert rows[0].shape[0] >= 2 * B
     gs, gp = GR.preprocess_graph(seqs, c['n_a'], c['n_a'] + c['n_b'] + 1)
-    args = make_args(c, dropout=0.2, seed=77)
+    args = make_args(c, dropout=dropout, precision=precision, seed=seed)
+    args.batch_size = B
     torch.manual_seed(0)
     tr = build_trainer(args, gs, gp)
     params = {n: p.detach().cpu().clone() for n, p in tr.model.named_parameters()}
@@ -165,37 +165,177 @@ def test_train_step_with_dropout_matches_oracle(norm_first, n_head, n_gnn, n_att
     for k, g in (('share', gs), ('specific', gp)):
         r, cc, v = g.coo()
         graphs[k] = (torch.from_numpy(r), torch.from_numpy(cc), torch.from_numpy(v))
-    ocfg = dict(d_latent=64, n_item_a=c['n_a'], n_item_b=c['n_b'], idx_pad=c['n_a'] + c['n_b'], len_rec=5,
-                lambda_loss=0.7, n_gnn=n_gnn, n_attn=n_attn, n_head=n_head, norm_first=norm_first, d_bias=True,
-                shared_item_embed=False, dropout_gnn=0.2, dropout_attn=0.2)
-    orc = O.OracleTrainer(params, graphs, ocfg, seed=77)
+    ocfg = dict(d_latent=c['d_latent'], n_item_a=c['n_a'], n_item_b=c['n_b'], idx_pad=c['n_a'] + c['n_b'],
+                len_rec=c['len_rec'], lambda_loss=0.7, n_gnn=c['n_gnn'], n_attn=c['n_attn'], n_head=c['n_head'],
+                norm_first=c['norm_first'], d_bias=c['d_bias'], shared_item_embed=c['shared_item_embed'],
+                dropout_gnn=dropout, dropout_attn=dropout)
+    orc = O.OracleTrainer(params, graphs, ocfg, seed=seed)
     orc.step_no = 1  # the model's first convolve_graph opens step 1
+    return tr, orc, rows
+
+
+def _steps_vs_oracle(tr, orc, rows, B, n_steps, tol_out, tol_grad, tol_param, on_step=None):
+    """Train n_steps on the HIP path and the oracle side by side (grads accumulate, Q3); compare the hi
+    tables, the encoder outputs on the rows the loss reads, the three losses, every parameter gradient
+    (max-abs error relative to the oracle's max-abs) and the post-step parameters."""
     tr.model.train()
     tr.optimizer.zero_grad()
-    B = 48
-    for s in range(2):
+    worst = {}
+    for s in range(n_steps):
         b = tuple(torch.from_numpy(r[s * B:(s + 1) * B].copy()) for r in rows)
         box = capture(tr)
         tr.model.convolve_graph()
         loss, loss_rec, loss_mi = tr.train_batch(b)
         out = orc.train_batch(b, optimizer=False)
-        for k in ('hi_share', 'h_share', 'hx', 'hy'):
-            assert rel(*read_rows(box, k, box[k], out[k])) < TOL, (s, k)
-        assert abs(float(loss) - float(out['loss'])) < TOL * abs(float(out['loss']))
+        torch.cuda.synchronize()
+        if on_step is not None:
+            on_step(s, box)
+        for k in ('hi_share', 'hi_a', 'hi_b', 'h_share', 'hx', 'hy'):
+            if k in out:
+                e = rel(*read_rows(box, k, box[k], out[k]))
+                worst[k] = max(worst.get(k, 0.0), e)
+                assert e < tol_out, (s, k, e)
+        for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
+            if k in out:
+                e = abs(float(v.detach()) - float(out[k])) / abs(float(out[k]))
+                worst[k] = max(worst.get(k, 0.0), e)
+                assert e < tol_out, (s, k, float(v), float(out[k]))
         for n in orc.names:
-            assert rel(box['grads'][n], orc.grads[n]) < 5 * TOL, (s, n)
+            e = rel(box['grads'][n], orc.grads[n])
+            worst['grad/' + n] = max(worst.get('grad/' + n, 0.0), e)
+            assert e < tol_grad, (s, n, e)
         with torch.no_grad():
             orc.opt.step(orc.P, orc.grads)
         for n, p in tr.model.named_parameters():
             if n in orc.names:
+                # AdamW's early updates are ≈ lr·sign(g): compare where the gradient's sign is beyond
+                # the gradient tolerance
                 g = orc.grads[n]
-                sig = g.abs() > 1e-3 * g.abs().max()
-                assert rel(p.detach().cpu()[sig], orc.P[n][sig]) < TOL, (s, n)
+                sig = g.abs() > 2 * tol_grad * g.abs().max()
+                e = rel(p.detach().cpu()[sig], orc.P[n][sig])
+                assert e < tol_param, (s, n, e)
         with torch.no_grad():  # re-sync (sign noise of ~zero grads)
             for n, p in tr.model.named_parameters():
                 if n in orc.names:
                     p.copy_(orc.P[n].to(DEV))
         orc.step_no = tr.model.state.step + 1
+    return worst
+
+
+@pytest.mark.parametrize('norm_first,n_head,n_gnn,n_attn', [(False, 1, 1, 1), (True, 2, 2, 1), (False, 2, 1, 2)])
+def test_train_step_with_dropout_matches_oracle(norm_first, n_head, n_gnn, n_attn):
+    """Larger synthetic case, dropout 0.2 everywhere: HIP step vs oracle with the same hash masks."""
+    c = dict(n_a=300, n_b=400, len_max=20, len_rec=5, d_latent=64, n_gnn=n_gnn, n_attn=n_attn, n_head=n_head,
+             norm_first=norm_first, d_bias=True, shared_item_embed=False)
+    tr, orc, rows = _oracle_case(c, B=48, n_users=200)
+    _steps_vs_oracle(tr, orc, rows, 48, 2, TOL, 5 * TOL, TOL)
+
+
+# The benchmarked configuration's shape (d=256, L=50, R=10; BASELINE configs[1..3]) at item counts the
+# oracle finishes in seconds.  At d=256 every bf16-mode kernel the bench runs is dispatched: the fused
+# linear+CE (c2dsr_ce_supported), its valid-row compaction and the one-hot planned dW, the
+# register-streamed projection GEMM with its aux epilogues (ResidualLink, drop(relu) backward, mapped aux
+# on the row-subset last layer), the weight-gradient GEMM, the wave attention.
+C256 = dict(n_a=3000, n_b=4000, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
+            norm_first=False, d_bias=False, shared_item_embed=False)
+# bf16 tolerance (documented, DESIGN.md §4): bf16 operands carry 8 significand bits (rel. rounding 2^-9);
+# products accumulate in fp32.  Outputs/losses within 2e-2 relative, gradients within 5e-2 of the
+# gradient's max-abs (the error of a dot product over K bf16-rounded terms grows like sqrt(K)·2^-9 of
+# its magnitude), post-step parameters within 2e-2 where |g| exceeds 2·5e-2 of its max (AdamW's first
+# steps move every parameter by ≈ lr·sign(g), so entries with a noise-level gradient may move either way).
+BF16_OUT, BF16_GRAD, BF16_PARAM = 2e-2, 5e-2, 2e-2
+
+
+@pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
+def test_bf16_step_d256_matches_oracle(compact):
+    """The benchmarked path (bf16 mode, d=256) over two steps with dropout 0.2 vs the fp32 oracle: every
+    parameter gradient, the encoder outputs, the losses and the post-step parameters (VERDICT r01 #1)."""
+    from c2dsr_amd._lib import lib
+    assert bool(lib.raw('c2dsr_ce_supported')(256))
+    tr, orc, rows = _oracle_case(C256, B=96, n_users=260, precision='bf16')
+    tr.compact_rows = compact
+    seen = {}
+
+    def on_step(s, box):
+        seen[s] = {pid: int(v.numel()) for pid, v in box.get('need', {}).items()}
+
+    worst = _steps_vs_oracle(tr, orc, rows, 96, 2, BF16_OUT, BF16_GRAD, BF16_PARAM, on_step)
+    print('bf16 d=256 worst relative errors:', {k: f'{v:.2e}' for k, v in sorted(worst.items(), key=lambda x: -x[1])[:8]})
+    assert bool(seen[0]) == compact  # the row-subset last layer ran (or not)
+
+
+def test_fp32_step_d256_matches_oracle():
+    """Same shape in the fp32 parity mode at the north_star tolerance (1e-4; gradients 5e-4)."""
+    tr, orc, rows = _oracle_case(C256, B=96, n_users=260, precision='fp32')
+    _steps_vs_oracle(tr, orc, rows, 96, 2, TOL, 5 * TOL, TOL)
+
+
+@pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
+def test_bf16_full_size_mb_loss_head_vs_fp32(compact):
+    """Full-size property check of the benchmarked step (BASELINE configs[2] item counts 36,845 / 63,937,
+    d=256, L=50, B=2048, R=10, dropout 0.2, bf16): the loss is finite, and the fused bf16 classifier heads
+    + CE and the discriminators agree with the fp32 materialised loss head (the oracle's loss_head, run with
+    torch on the device) evaluated on the HIP encoder outputs of the same step — the losses and the
+    classifier / discriminator gradients (VERDICT r01 #1)."""
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import synth
+    from c2dsr_amd import dropout as DK
+    from oracle import c2dsr_oracle as O
+    import random
+    c = dict(n_a=36845, n_b=63937, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
+             norm_first=False, d_bias=False, shared_item_embed=False)
+    B = 2048
+    seqs = synth.make_sequences(2 * B, c['n_a'], c['n_b'], c['len_max'], seed=1, n_min=6)
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, c['n_a'], c['n_b'], c['len_max']))
+    gs, gp = GR.preprocess_graph(seqs, c['n_a'], c['n_a'] + c['n_b'] + 1)
+    args = make_args(c, dropout=0.2, precision='bf16', seed=3407)
+    args.batch_size = B
+    torch.manual_seed(0)
+    tr = build_trainer(args, gs, gp)
+    tr.compact_rows = compact
+    P = {n: p.detach().clone() for n, p in tr.model.named_parameters()}
+    tr.model.train()
+    tr.optimizer.zero_grad()
+    b = tuple(torch.from_numpy(r[:B].copy()) for r in rows)
+    box = capture(tr)
+    tr.model.convolve_graph()
+    loss, loss_rec, loss_mi = tr.train_batch(b)
+    torch.cuda.synchronize()
+    assert all(math.isfinite(float(v.detach())) for v in (loss, loss_rec, loss_mi))
+    assert bool(box['need']) == compact
+
+    L, d = c['len_max'], c['d_latent']
+
+    def full(key, got):
+        # a row-subset output holds only the rows the loss reads; the others do not enter the loss
+        pid = {'h_share': DK.PASS_SHARE, 'hx': DK.PASS_A, 'hy': DK.PASS_B, 'neg0': DK.PASS_NEG0,
+               'neg1': DK.PASS_NEG0 + 1}[key]
+        idx = box['need'].get(pid)
+        if idx is None:
+            return got.reshape(B, L, d).float()
+        out = torch.zeros(B * L, d, device=DEV)
+        out[idx.to(DEV)] = got.reshape(-1, d)
+        return out.reshape(B, L, d)
+
+    hs = [full(k, v).requires_grad_(False) for k, v in (('h_share', box['h_share']), ('hx', box['hx']),
+                                                         ('hy', box['hy']), ('neg0', box['neg'][0]),
+                                                         ('neg1', box['neg'][1]))]
+    names = ['classifier_a.weight', 'classifier_a.bias', 'classifier_b.weight', 'classifier_b.bias',
+             'classifier_pad.weight', 'classifier_pad.bias', 'D_a.weight', 'D_b.weight']
+    for n in names:
+        P[n].requires_grad_(True)
+    cfg = dict(n_item_a=c['n_a'], n_item_b=c['n_b'], len_rec=c['len_rec'], lambda_loss=0.7)
+    bd = tuple(x.to(DEV) for x in b)
+    out = O.loss_head(P, *hs, bd, cfg)
+    grads = torch.autograd.grad(out['loss'], [P[n] for n in names])
+    for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
+        e = abs(float(v.detach()) - float(out[k])) / abs(float(out[k]))
+        assert e < 2e-3, (k, float(v), float(out[k]), e)
+    for n, g in zip(names, grads):
+        e = rel(box['grads'][n], g)
+        assert e < BF16_GRAD, (n, e)
 
 
 def test_bf16_step_close_to_fp32():
