@@ -220,7 +220,8 @@ def hbm_traffic():
 
 def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
     """The oracle (CPU fp32 restatement, oracle/c2dsr_oracle.py) on a bounded sample of the same
-    workload: same item tables, d, L; a small batch for a few steps."""
+    workload at the configuration's own batch: same item tables, d, L,
+    B; one untimed warm-up step, then timed steps until ``budget_s`` is spent (at least one)."""
     sys.path.insert(0, ROOT)
     from oracle import c2dsr_oracle as O
     from c2dsr_amd.models.C2DSR import C2DSR
@@ -231,31 +232,32 @@ def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
     torch.manual_seed(0)
     model = C2DSR(args, gs, gp)
     params = {n: p.detach().clone() for n, p in model.named_parameters()}
+    del model
     graphs = {}
     for k, g in (('share', gs), ('specific', gp)):
         r, c, v = g.coo()
         graphs[k] = (torch.from_numpy(r), torch.from_numpy(c), torch.from_numpy(v))
     ocfg = O.cfg_from_args(args)
     tr = O.OracleTrainer(params, graphs, ocfg, seed=3407)
-    Bs = 64
-    done = 0
-    t0 = None
-    steps = 0
+    Bs = cfg['B']
+    n_rows = rows[0].shape[0]
+    steps, done, el = 0, 0, 0.0
     while True:
-        lo = (steps * Bs) % max(1, rows[0].shape[0] - Bs)
+        lo = (steps * Bs) % max(1, n_rows - Bs)
         b = tuple(torch.from_numpy(r[lo:lo + Bs].copy()) for r in rows)
-        if steps == 1:
-            t0 = time.time()  # first step is warm-up
+        t0 = time.time()
         tr.train_batch(b)
-        steps += 1
-        if steps > 1:
+        if steps > 0:  # the first step is the warm-up
+            el += time.time() - t0
             done += Bs
-            if time.time() - t0 > budget_s or steps >= 6:
+            log(f'[bench] cpu baseline step {steps}: {time.time() - t0:.1f}s')
+            if el > budget_s:
                 break
-    el = time.time() - t0
+        steps += 1
     return dict(value=round(done / el, 3), unit='train sequences/sec', cores=threads, kind='port',
                 sample=f'oracle (torch-CPU fp32 restatement) train step, {cfg["label"]}, d={cfg["d"]}, '
-                       f'L={cfg["L"]}, batch {Bs}, {steps - 1} timed steps, dropout 0.2')
+                       f'L={cfg["L"]}, batch {Bs} (the GPU line\'s batch), 1 warm-up + {done // Bs} timed steps, '
+                       'dropout 0.2')
 
 
 def run_c5(opt, world, rank, device):
@@ -366,6 +368,11 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--c5-seqs', type=int, default=2_000_000)
+    ap.add_argument('--no-extra', dest='extra', action='store_false',
+                    help='skip the extra lines (MB fp32 mode, FK bf16) of the default N=1 run')
+    ap.add_argument('--dp-split', action='store_true',
+                    help='strong scaling: every rank trains its slice of the same global batch (BASELINE '
+                         'configs[3], e.g. --config ee --batch 4096)')
     opt = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -392,26 +399,68 @@ def main():
     cfg = dict(CONFIGS[opt.config])
     if opt.batch:
         cfg['B'] = opt.batch
-    B = cfg['B']
-    n_batches = opt.steps + opt.warmup
-    t_prep = time.time()
-    # enough distinct sequences for every step's batch (>= 20*B per the survey's generator spec)
-    rows, gs, gp = make_workload(cfg, max(20 * B, n_batches * B * 13 // 10) if opt.config != 'tiny' else 4 * B,
-                                 seed=1)
-    n_rows = rows[0].shape[0]
-    log(f'[bench] {cfg["label"]}: {n_rows} train sequences, graph nnz {gs.nnz}/{gp.nnz}, '
-        f'prep {time.time() - t_prep:.1f}s')
+    wl = workload(cfg, opt.config)
+    res = run_train(opt, cfg, opt.config, opt.precision, wl, world, rank, device)
+    if rank == 0:
+        extra = {}
+        if world == 1 and opt.extra and opt.config == 'mb' and not opt.batch:
+            # driver-visible lines of the other single-GPU configurations: the fp32 parity
+            # mode on the same workload, and BASELINE configs[1] (Food-Kitchen sizes, B=1024, bf16)
+            extra['mb_fp32'] = brief(run_train(opt, cfg, 'mb', 'fp32', wl, world, rank, device))
+            torch.cuda.empty_cache()
+            fk = dict(CONFIGS['fk'])
+            wfk = workload(fk, 'fk')
+            extra['fk_bf16'] = brief(run_train(opt, fk, 'fk', 'bf16', wfk, world, rank, device))
+            del wfk
+        cpu = None
+        if world == 1 and not opt.no_cpu_baseline:
+            cpu = cpu_baseline(cfg, *wl, opt.cpu_budget)
+        res['cpu_baseline'] = cpu
+        if extra:
+            res['extra_lines'] = extra
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
+
+def workload(cfg, name):
+    """The synthetic workload of a configuration, pinned: 20·B sequences (≥ 20·B_global)
+    from the fixed generator seed, and the graphs built from them — independent of --steps / --warmup."""
+    t_prep = time.time()
+    rows, gs, gp = make_workload(cfg, 20 * cfg['B'] if name != 'tiny' else 4 * cfg['B'], seed=1)
+    log(f'[bench] {cfg["label"]}: {rows[0].shape[0]} train sequences, graph nnz {gs.nnz}/{gp.nnz}, '
+        f'prep {time.time() - t_prep:.1f}s')
+    return rows, gs, gp
+
+
+def brief(r):
+    keep = ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'loss')
+    out = {k: r[k] for k in keep}
+    for k in ('roofline', 'roofline_hbm'):
+        if r.get(k):
+            out[k] = {kk: r[k][kk] for kk in ('bound', 'achieved', 'peak', 'unit', 'frac', 'ms_per_step')}
+    return out
+
+
+def run_train(opt, cfg, name, precision, wl, world, rank, device):
+    """W untimed + K timed training steps of one configuration; returns the bench line (rank 0)."""
+    rows, gs, gp = wl
+    B = cfg['B']
+    n_rows = rows[0].shape[0]
+    n_batches = opt.steps + opt.warmup
     from c2dsr_amd.trainer import Trainer
-    args = make_args(cfg, device, opt.precision)
+    args = make_args(cfg, device, precision)
     torch.manual_seed(3407)
     tr = Trainer(args, None, data=(None, None, None), graphs=(gs, gp))
-    tr.dp_split = False  # weak scaling: each rank its own batch
+    tr.dp_split = opt.dp_split
+    B_local = B if not opt.dp_split else -(-B // world)
     batches = []
     for i in range(n_batches):
-        lo = ((i * world + rank) * B) % max(1, n_rows - B)
+        # weak scaling: rank r trains batch (i·world + r); dp_split: all ranks slice the same global batch
+        j = i * world + rank if not opt.dp_split else i
+        lo = (j * B) % max(1, n_rows - B)
         batches.append(tuple(torch.from_numpy(r[lo:lo + B].copy()).to(device) for r in rows))
-    timer = KernelTimer(opt.precision)
+    timer = KernelTimer(precision)
     dgs = tr.model.graphs()
     nnz = {}
     for g in dgs:
@@ -421,10 +470,11 @@ def main():
     htimer = HbmTimer(tr.model.n_item, nnz, uniq_counts(batches))
     tr.model.train()
     tr.optimizer.zero_grad()
+    B_global = B * world if not opt.dp_split else B
 
     def step(b):
         tr.model.convolve_graph()
-        return tr.train_batch(b, global_rows=B * world)
+        return tr.train_batch(b, global_rows=B_global)
 
     for i in range(opt.warmup):
         step(batches[i])
@@ -452,38 +502,34 @@ def main():
     ks = timer.summary()
     hb = htimer.summary(opt.steps)
     ms = el / opt.steps * 1e3
-    value = B * world * opt.steps / el
-    if rank == 0:
-        peak = PEAK_BF16_TFLOPS if opt.precision == 'bf16' else PEAK_FP32_TFLOPS
-        roof = None
-        if ks is not None:
-            traffic, tsrc, busy = k5_traffic(opt.precision)
-            roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
-                        frac=round(ks['tflops'] / peak, 4), traffic=traffic, traffic_source=tsrc,
-                        kernel=('K5 fused classifier head + CE: ce_lse_kernel + ce_dh_kernel + ce_dw_kernel '
-                                '(bf16 MFMA); credited 2·M·n·d per launch each'
-                                if opt.precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
-                        ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'],
-                        mfma_busy=busy, mfma_busy_note='SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles of the K5 launches '
-                        '(same PMC run as traffic; counts the recomputed logits tiles that frac does not credit)')
-        if hb is not None and opt.config == 'mb' and opt.precision == 'bf16':
-            hb['traffic'], hb['traffic_source'] = hbm_traffic()
-            hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
-        cpu = None
-        if world == 1 and not opt.no_cpu_baseline:
-            cpu = cpu_baseline(cfg, rows, gs, gp, opt.cpu_budget)
-        out = {'metric': 'train sequences/sec at d=256, seq_len=50, |items|~100k',
-               'value': round(value, 2), 'unit': 'train sequences/sec', 'n_gpus': world, 'steps': opt.steps,
-               'warmup': opt.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
-               'vs_baseline': None, 'dtype': opt.precision, 'data': 'synthetic (Zipf two-domain sequences)',
-               'config': {'workload': f'{opt.config}: {cfg["label"]}', 'n_item_a': cfg['n_a'], 'n_item_b': cfg['n_b'],
-                          'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B, 'global_batch': B * world,
-                          'len_rec': 10, 'dropout': 0.2, 'parallelism': f'dp{world}'},
-               'loss': round(loss, 5) if math.isfinite(loss) else None,
-               'roofline': roof, 'roofline_hbm': hb, 'cpu_baseline': cpu}
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    value = B_global * opt.steps / el
+    del tr, batches
+    peak = PEAK_BF16_TFLOPS if precision == 'bf16' else PEAK_FP32_TFLOPS
+    roof = None
+    if ks is not None:
+        traffic, tsrc, busy = k5_traffic(precision) if name == 'mb' else (None, None, None)
+        roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
+                    frac=round(ks['tflops'] / peak, 4), traffic=traffic, traffic_source=tsrc,
+                    kernel=('K5 fused classifier head + CE: ce_lse_kernel + ce_dh_kernel + ce_dw_kernel '
+                            '(bf16 MFMA); credited 2·M·n·d per launch each'
+                            if precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
+                    ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'],
+                    mfma_busy=busy, mfma_busy_note='SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles of the K5 launches '
+                    '(same PMC run as traffic; counts the recomputed logits tiles that frac does not credit)')
+    if hb is not None and name == 'mb' and precision == 'bf16':
+        hb['traffic'], hb['traffic_source'] = hbm_traffic()
+        hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
+    par = f'dp{world}' + ('-split' if opt.dp_split and world > 1 else '')
+    return {'metric': 'train sequences/sec at d=256, seq_len=50, |items|~100k',
+            'value': round(value, 2), 'unit': 'train sequences/sec', 'n_gpus': world, 'steps': opt.steps,
+            'warmup': opt.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
+            'scaling': 'strong' if opt.dp_split and world > 1 else 'weak',
+            'vs_baseline': None, 'dtype': precision, 'data': 'synthetic (Zipf two-domain sequences)',
+            'config': {'workload': f'{name}: {cfg["label"]}', 'n_item_a': cfg['n_a'], 'n_item_b': cfg['n_b'],
+                       'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B_local, 'global_batch': B_global,
+                       'train_sequences': int(n_rows), 'len_rec': 10, 'dropout': 0.2, 'parallelism': par},
+            'loss': round(loss, 5) if math.isfinite(loss) else None,
+            'roofline': roof, 'roofline_hbm': hb}
 
 
 if __name__ == '__main__':
