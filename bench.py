@@ -68,13 +68,16 @@ def make_args(cfg, device, precision, dropout=0.2):
 
 class KernelTimer:
     """HIP-event timing (on the stream the kernels are launched on, inside the timed region) of the
-    dominant op, K5 — the fused classifier head + cross-entropy — in bf16 mode: its three kernels
-    c2dsr_ce_fused_fwd (online log-sum-exp), c2dsr_ce_fused_dh, c2dsr_ce_fused_dw.  Credited FLOPs
-    (SURVEY.md §8(d)): 2·M·n·d per launch of each (forward logits, dH, dW products); the logits tiles
-    the two backward kernels recompute are overhead and not credited.  fp32 mode: the materialised
+    dominant op, K5 — the fused classifier head + cross-entropy — in bf16 mode: c2dsr_ce_fused_fwd_u
+    (online log-sum-exp AND the softmax·W part of dH in one sweep) and c2dsr_ce_fused_dw (the older
+    split c2dsr_ce_fused_fwd / _dh pair when selected).  Credited FLOPs: 2·M·n·d per
+    product — forward logits, dH, dW (fwd_u carries two) — the logits tile the dW kernel recomputes is
+    overhead and not credited.  fp32 mode: the materialised
     logits GEMMs (c2dsr_gemm calls of > 1e11 FLOP)."""
 
-    NAMES_BF16 = ('c2dsr_ce_fused_fwd', 'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
+    NAMES_BF16 = ('c2dsr_ce_fused_fwd_u', 'c2dsr_ce_fused_fwd', 'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
+    # credited products per launch: fwd_u = the lse logits + the softmax·W part of dH (online, one sweep)
+    CREDIT = {'c2dsr_ce_fused_fwd_u': 2}
 
     def __init__(self, precision):
         from c2dsr_amd._lib import lib
@@ -100,7 +103,7 @@ class KernelTimer:
                     if f < 1e11:  # only the classifier-head GEMMs
                         continue
                 else:  # (Hb, Wb, bias2, M, n, D, ...)
-                    f = 2.0 * a[3] * a[4] * a[5]
+                    f = 2.0 * a[3] * a[4] * a[5] * self.CREDIT.get(name, 1)
                 ms.append(e0.elapsed_time(e1))
                 fl.append(f)
             if ms:
@@ -510,8 +513,8 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device):
         traffic, tsrc, busy = k5_traffic(precision) if name == 'mb' else (None, None, None)
         roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
                     frac=round(ks['tflops'] / peak, 4), traffic=traffic, traffic_source=tsrc,
-                    kernel=('K5 fused classifier head + CE: ce_lse_kernel + ce_dh_kernel + ce_dw_kernel '
-                            '(bf16 MFMA); credited 2·M·n·d per launch each'
+                    kernel=('K5 fused classifier head + CE: ce_fwdu_kernel (lse + dH, online) + ce_dw_kernel '
+                            '(bf16 MFMA); credited 2·M·n·d per product (fwd_u 2, dw 1)'
                             if precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
                     ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'],
                     mfma_busy=busy, mfma_busy_note='SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles of the K5 launches '

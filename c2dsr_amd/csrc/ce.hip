@@ -423,6 +423,279 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- forward with dH: online LSE + U
+// The forward of the training step already has the only thing the input gradient needs besides lse:
+//   dH_r = rw_r · (Σ_c softmax_rc·W_c − W_{t_r}),   softmax_rc = 2^(s_rc·log2e + b2_c − lse2_r)
+// so it is accumulated here, flash-attention style (W is both the "keys" and the "values"), and the
+// backward has no dH sweep at all: 4·M·n·D MFMA flops for lse + dH instead of 2 + 4 in two kernels.
+// Same block shape and software pipeline as ce_dh_kernel (grid (ceil(M/128), n_split), 4 waves × 32
+// rows, one wave per SIMD, four W images):
+//   step t:  [ S(t+1) = W_{t+1}·Hᵀ ∥ epilogue of S(t): p = 2^(v − m), z += p, pack ]
+//            [ Uᵀ += W_tᵀ·Pᵀ(t)   ∥ DMA of tile t+3 ∥ v = S(t+1)·log2e + b2 and its row max ]
+// m is the row's running max (log2 domain), raised LAZILY: only when a tile's max exceeds it by more
+// than TAU does the wave rescale its accumulators (p ≤ 2^TAU otherwise; m never exceeds the true max,
+// so no term underflows against a stale m).  Each lane holds one row r (the Sᵀ / Uᵀ column), its two
+// half-waves different columns c / different k: the row max is combined across lane^32.
+// Outputs per split s: part_m[s][r] = m, part_s[s][r] = Σ_c 2^(v_rc − m), Up[s][r][:] = Σ_c 2^(v_rc − m)·W_c
+// (combined by ce_rows_kernel and ce_dh_from_u_kernel).
+template <int D>
+__global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict__ Hb, const bf16* __restrict__ Wb,
+                                                         const float* __restrict__ bias2, int M, int n,
+                                                         int cols_per_split, float* __restrict__ part_m,
+                                                         float* __restrict__ part_s, float* __restrict__ Up) {
+  constexpr int KS = D / 16;
+  constexpr int KB = D / 32;
+  constexpr int NQ = KB * 4;
+  constexpr int DS = 3;
+  constexpr int DT = 3;
+  constexpr int EPK = 16 / KS;
+  constexpr int MPK = 32 / NQ;                       // max-prep elements per U step
+  constexpr int IMG = TILE * D * 2;
+  constexpr int NDMA = (TILE / 4) * (D / 128) / 4;
+  constexpr int NB = 4;
+  constexpr float TAU = 8.f;
+  __shared__ __attribute__((aligned(16))) char img[NB][IMG];
+  __shared__ __attribute__((aligned(16))) float b2s[NB][4][TILE];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = blockIdx.x * 128 + w * 32 + (lane & 31);
+  const int rc = min(r, M - 1);
+  const int c_beg = blockIdx.y * cols_per_split;
+  const int c_end = min(n, c_beg + cols_per_split);
+  const int ntiles = c_end > c_beg ? (c_end - c_beg + TILE - 1) / TILE : 0;
+  f32x16 dacc[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dacc[kb][i] = 0.f;
+  float mrow = -INFINITY, zrow = 0.f;
+  if (ntiles > 0) {
+    const int c_last = c_beg + (ntiles - 1) * TILE;
+    const ImgOffsets o0 = img_offsets(lane);
+    const int ib = (int)lds_addr(img[0]);
+    unsigned dvoff[NDMA], ddst[NDMA];
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int q = w + 4 * i;
+      constexpr int GROUPS = TILE / 4;
+      const int half = q / GROUPS, rg = q % GROUPS;
+      const int row = rg * 4 + (lane >> 4);
+      const int lch = (lane & 15) ^ swz_f(row);
+      dvoff[i] = (unsigned)((row * D + half * 128 + lch * 8) * 2);
+      ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (TILE * 256) + rg * 1024));
+    }
+    auto dma = [&](int tt) {
+      const int c0 = min(c_beg + tt * TILE, c_last);
+      const int buf = tt % NB;
+      const bf16* base = Wb + (long)c0 * D;
+#pragma unroll
+      for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
+      dma4(bias2 + c0 + lane, b2s[buf][w]);
+    };
+    bf16x8 hf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) hf[ks] = *(const bf16x8*)(Hb + (long)rc * D + ks * 16 + 8 * (lane >> 5));
+    dma(0);
+    dma(1);
+    dma(2);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) pin(hf[ks]);
+    vm_drain();
+    dma_wait();
+    __syncthreads();
+    auto offs = [&](int b, int (&ro)[8], int (&to)[4][2]) {
+      const int add = ib + b * IMG;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) ro[c] = o0.roff[c] + add;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        to[v][0] = o0.troff[v][0] + add;
+        to[v][1] = o0.troff[v][1] + add;
+      }
+    };
+    // bias·log2e of this lane's 32 columns of tile buffer b (4 runs of 4 per column block)
+    auto bias4 = [&](int b, f32x4 (&b4)[2][4]) {
+      const int bo = (int)lds_addr(b2s[b][w]) + 16 * (lane >> 5);
+      [&]<int... J>(std::integer_sequence<int, J...>) {
+        ((b4[J >> 2][J & 3] = lds_ld<f32x4, 128 * (J >> 2) + 32 * (J & 3)>(bo)), ...);
+      }(std::make_integer_sequence<int, 8>{});
+    };
+    // ---- S(0) and its max (not overlapped)
+    f32x16 sc[2];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 f0 = *(const bf16x8*)(img[0] + o0.roff[ks & 7] + (ks >> 3) * TILE * 256);
+      const bf16x8 f1 = *(const bf16x8*)(img[0] + o0.roff[ks & 7] + (ks >> 3) * TILE * 256 + 32 * 256);
+      if (ks == 0) {
+        sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, hf[0], f32x16{}, 0, 0, 0);
+        sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, hf[0], f32x16{}, 0, 0, 0);
+      } else {
+        sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, hf[ks], sc[0], 0, 0, 0);
+        sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, hf[ks], sc[1], 0, 0, 0);
+      }
+    }
+    float mnext;
+    {
+      f32x4 b4[2][4];
+      bias4(0, b4);
+      float tm = -INFINITY;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          sc[cb][i] = fmaf(sc[cb][i], LOG2E, ((const float*)&b4[cb][i >> 2])[i & 3]);
+          tm = fmaxf(tm, sc[cb][i]);
+        }
+      mnext = fmaxf(tm, __shfl_xor(tm, 32, 64));
+    }
+    for (int t = 0; t < ntiles; ++t) {
+      const int bh = t % NB, bs = (t + 1) % NB;
+      const int cn = min(c_beg + (t + 3) * TILE, c_last);
+      const bf16* nsrc = Wb + (long)cn * D;
+      const unsigned nbuf = ((t + 3) % NB) * IMG;
+      dma4(bias2 + cn + lane, b2s[(t + 3) % NB][w]);
+      // lazy rescale: the row's max moved up by more than TAU (always on the first tile)
+      {
+        const bool need = mnext > mrow + TAU;
+        if (__builtin_amdgcn_ballot_w64(need)) {
+          const float f = need ? ex2(mrow - mnext) : 1.f;  // mrow = -inf → 0
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) dacc[kb][i] *= f;
+          zrow *= f;
+          mrow = need ? mnext : mrow;
+        }
+      }
+      const float msub = mrow == -INFINITY ? 0.f : mrow;  // all of S(t) is -inf then: p = 0
+      ImgOffsets oS, oH;
+      {
+        int ro[8], to[4][2];
+        offs(bs, ro, to);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) oS.roff[c] = ro[c];
+        offs(bh, ro, to);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          oH.troff[v][0] = to[v][0];
+          oH.troff[v][1] = to[v][1];
+        }
+      }
+      // ---- S(t+1) ∥ epilogue(t)
+      f32x16 sn[2];
+      bf16x8 fa[DS + 2][2];
+      bf16x8 x[2][2];
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((fa[P][0] = row_frag_c<TILE, 0, P, 0>(oS), fa[P][1] = row_frag_c<TILE, 32, P, 0>(oS)), ...);
+      }(std::make_integer_sequence<int, DS>{});
+      __builtin_amdgcn_sched_barrier(0);
+      [&]<int... K>(std::integer_sequence<int, K...>) {
+        (
+            [&] {
+              constexpr int ks = K;
+              if constexpr (ks + DS < KS) {
+                fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
+                fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
+              }
+              if constexpr (ks == 0) {
+                sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
+                sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
+              } else {
+                sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][0], hf[ks], sn[0], 0, 0, 0);
+                sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks % (DS + 2)][1], hf[ks], sn[1], 0, 0, 0);
+              }
+#pragma unroll
+              for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+                for (int e = 0; e < EPK; ++e) {
+                  const int i = ks * EPK + e;
+                  const float pv = ex2(sc[cb][i] - msub);
+                  sc[cb][i] = pv;
+                  zrow += pv;
+                }
+              if constexpr ((ks * EPK + EPK) % 8 == 0) {
+                constexpr int st = (ks * EPK) / 8;
+                x[0][st] = acc_frag(sc[0], st);
+                x[1][st] = acc_frag(sc[1], st);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, KS>{});
+      // ---- Uᵀ[k][r] += Σ_c W[c][k] Pᵀ[c][r]  ∥  v = S(t+1)·log2e + b2 and its max
+      f32x4 b4n[2][4];
+      bias4(bs, b4n);
+      float tm = -INFINITY;
+      bf16x8 tf[DT + 2];
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((tf[P] = tr_frag_c<TILE, ((P >> 1) & 1) * 32 + 16 * (P & 1), (P >> 2) * 32, 0>(oH)), ...);
+      }(std::make_integer_sequence<int, DT>{});
+      __builtin_amdgcn_sched_barrier(0);
+      [&]<int... Q>(std::integer_sequence<int, Q...>) {
+        (
+            [&] {
+              constexpr int q = Q;
+              if constexpr (q + DT < NQ) {
+                constexpr int q1 = q + DT;
+                tf[q1 % (DT + 2)] = tr_frag_c<TILE, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, 0>(oH);
+              }
+              dacc[q >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[(q >> 1) & 1][q & 1],
+                                                                   dacc[q >> 2], 0, 0, 0);
+              if constexpr (q % 4 == 1 && q / 4 < NDMA) dma16_s<q == 1>(nsrc, dvoff[q / 4], ddst[q / 4] + nbuf);
+#pragma unroll
+              for (int e = 0; e < MPK; ++e) {
+                const int el = q * MPK + e;
+                const int cb = el >> 4, i = el & 15;
+                const float v = fmaf(sn[cb][i], LOG2E, ((const float*)&b4n[cb][i >> 2])[i & 3]);
+                sn[cb][i] = v;
+                tm = fmaxf(tm, v);
+              }
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, NQ>{});
+      mnext = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      sc[0] = sn[0];
+      sc[1] = sn[1];
+      dma_wait_keep<NDMA + 1>();
+      __syncthreads();
+    }
+  }
+  const float ztot = zrow + __shfl_xor(zrow, 32, 64);
+  if (r < M) {
+    if (lane < 32) {
+      part_m[(long)blockIdx.y * M + r] = mrow;
+      part_s[(long)blockIdx.y * M + r] = ztot;
+    }
+    float* out = Up + ((long)blockIdx.y * M + r) * D;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) out[kb * 32 + creg(i, lane)] = dacc[kb][i];
+  }
+}
+
+// dH[r] = rw_r · (Σ_s 2^(pm[s][r] − lse2_r)·Up[s][r] − W[t_r])   (t_r outside [0, n): no one-hot term;
+// fixed split order)
+__global__ void ce_dh_from_u_kernel(const float* __restrict__ Up, const float* __restrict__ pm, int ns, int M, int D,
+                                    const float* __restrict__ lse2, const int* __restrict__ t32,
+                                    const float* __restrict__ rw, const float* __restrict__ W, int n,
+                                    float* __restrict__ dH) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= (long)M * D) return;
+  const int r = (int)(i / D), k = (int)(i % D);
+  const float l2 = lse2[r];
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < ns; ++s) {
+    const float m = pm[(long)s * M + r];
+    if (m == -INFINITY) continue;
+    t = c2::fma4(exp2f(m - l2), *(const float4*)(Up + ((long)s * M) * D + i), t);
+  }
+  const float w = rw[r];
+  const int tg = t32[r];
+  if (tg >= 0 && tg < n) t = c2::fma4(-1.f, *(const float4*)(W + (long)tg * D + k), t);
+  *(float4*)(dH + i) = make_float4(t.x * w, t.y * w, t.z * w, t.w * w);
+}
+
 // dH[r] = Σ_s dHp[s][r] - (0 <= t_r < n ? w_r·W[t_r] : 0)   (the one-hot part of P'; fixed order)
 __global__ void ce_dh_combine_kernel(const float* __restrict__ dHp, int ns, int M, int D,
                                      const int* __restrict__ t32, const float* __restrict__ rw,
@@ -766,6 +1039,38 @@ C2_API int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2
     return (int)hipErrorInvalidValue;
   ce_rows_kernel<<<c2::ceil_div(M, 4), 256, 0, s>>>(part_m, part_s, n_split, M, padlogit, tgt, n, H, W, bias, D, lse,
                                                     lse2, loss_row);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// forward + the softmax part of dH: part_m/part_s [n_split][M] (log2-domain max, sum) and Up [n_split][M][D]
+// → (with pad logits, targets, fp32 H/W/bias for the target logit) lse, lse2, loss_row [M]
+C2_API int c2dsr_ce_fused_fwd_u(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D,
+                                int n_split, float* part_m, float* part_s, float* Up, const float* padlogit,
+                                const int64_t* tgt, const float* H, const float* W, const float* bias, float* lse,
+                                float* lse2, float* loss_row, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (M == 0) return 0;
+  const int per = per_split(n, n_split, TILE);
+  dim3 grid(c2::ceil_div(M, 128), n_split);
+  if (D == 128)
+    ce_fwdu_kernel<128><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s, Up);
+  else if (D == 256)
+    ce_fwdu_kernel<256><<<grid, 256, 0, s>>>((const bf16*)Hb, (const bf16*)Wb, bias2, M, n, per, part_m, part_s, Up);
+  else
+    return (int)hipErrorInvalidValue;
+  ce_rows_kernel<<<c2::ceil_div(M, 4), 256, 0, s>>>(part_m, part_s, n_split, M, padlogit, tgt, n, H, W, bias, D, lse,
+                                                    lse2, loss_row);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+C2_API int c2dsr_ce_dh_from_u(const float* Up, const float* part_m, int ns, int M, int D, const float* lse2,
+                              const int* t32, const float* rw, const float* W, int n, float* dH, void* stream) {
+  if (M == 0) return 0;
+  if (D % 4) return (int)hipErrorInvalidValue;
+  ce_dh_from_u_kernel<<<c2::ceil_div((long)M * D / 4, 256), 256, 0, (hipStream_t)stream>>>(Up, part_m, ns, M, D, lse2,
+                                                                                          t32, rw, W, n, dH);
   C2_CHECK_LAUNCH();
   return 0;
 }

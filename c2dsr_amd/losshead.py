@@ -163,7 +163,18 @@ class LossHeadFn(Function):
                 lse_c = torch.empty(max(Mv, 1), **f32)
                 rows_c = torch.empty(max(Mv, 1), **f32)
                 lse2 = torch.empty(M_pad, **f32)
-                if Mv:
+                u = None
+                if Mv and any(ctx.needs_input_grad[:5]):
+                    # forward + the softmax part of the input gradient in one sweep (online lse, flash
+                    # style): the backward runs no dH sweep
+                    ns = split_count(Mv, 128)
+                    pm = torch.empty(ns, Mv, **f32)
+                    ps = torch.empty(ns, Mv, **f32)
+                    Up = torch.empty(ns, Mv, d, **f32)
+                    lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tc, Hc, W, bias,
+                        lse_c, lse2, rows_c, s)
+                    u = (Up, pm, ns)
+                elif Mv:
                     ns = split_count(Mv, 256)
                     pm = torch.empty(ns, Mv, **f32)
                     ps = torch.empty(ns, Mv, **f32)
@@ -172,7 +183,7 @@ class LossHeadFn(Function):
                 lib('c2dsr_expand_rows', rows_c, inv, M2, 1, rows, s)  # per-row losses, 0 on ignored rows
                 # target sort for the one-hot part of dW/db, on the side stream under the rest of the step
                 tplan = IndexPlan(tc[:Mv], n + 1) if Mv and any(ctx.needs_input_grad[:5]) and W.requires_grad else None
-                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padc, lse2, bias2, tplan, Hc, tc, inv, Mv, Mv0, lse_c), lse,
+                heads.append((Hcat, Hpad, tcat, (Hb, Wb, padc, lse2, bias2, tplan, Hc, tc, inv, Mv, Mv0, lse_c, u), lse,
                               rows, W, bias, n))
             else:
                 ld = n + 1
@@ -251,7 +262,7 @@ class LossHeadFn(Function):
             dHcat = torch.empty(M2, d, **f32)
             gW, gb = _grad_target(W), _grad_target(bias)
             if ctx.fused:
-                Hb, Wb, padc, lse2, bias2, tplan, Hc, tc, inv, Mv, Mv0, lse_c = logits
+                Hb, Wb, padc, lse2, bias2, tplan, Hc, tc, inv, Mv, Mv0, lse_c, u = logits
                 M_pad = lse2.shape[0]
                 rw = torch.empty(M_pad, **f32)
                 t32 = torch.empty(M_pad, device=dev, dtype=torch.int32)
@@ -262,11 +273,15 @@ class LossHeadFn(Function):
                     # compact rows keep their order: the first Mv0 are the shared-sequence rows (coef[0])
                     lib('c2dsr_ce_row_weights', tc, Mv, M_pad, n, coef, Mv0, gscale, float(m.lam), padc, lse_c, rw,
                         t32, lse2, crow, dpad_c, s)
-                    ns = split_count(Mv, 128)
-                    dHp = torch.empty(ns, Mv, d, **f32)
-                    lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, Mv, n, d, ns, crow, dHp, s)
-                    lib('c2dsr_ce_dh_combine', dHp, ns, Mv, d, t32, rw, W, n, dHc, s)
-                    del dHp
+                    if u is not None:  # dH = rw·(softmax·W − W[t]) from the forward's online partials
+                        Up, pm, nsu = u
+                        lib('c2dsr_ce_dh_from_u', Up, pm, nsu, Mv, d, lse2, t32, rw, W, n, dHc, s)
+                    else:
+                        ns = split_count(Mv, 128)
+                        dHp = torch.empty(ns, Mv, d, **f32)
+                        lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, Mv, n, d, ns, crow, dHp, s)
+                        lib('c2dsr_ce_dh_combine', dHp, ns, Mv, d, t32, rw, W, n, dHc, s)
+                        del dHp
                     nr = split_count(n, 128)
                     dWp = torch.empty(nr, n, d, **f32)
                     dbp = torch.empty(nr, n, **f32)

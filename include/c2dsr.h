@@ -173,6 +173,16 @@ int c2dsr_ce_bias2(const float* bias, int n, int n_pad, float* bias2, void* stre
 int c2dsr_ce_fused_fwd(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
                        float* part_m, float* part_s, const float* padlogit, const int64_t* tgt, const float* H,
                        const float* W, const float* bias, float* lse, float* lse2, float* loss_row, void* stream);
+/* The same forward plus the softmax part of the input gradient, accumulated online (flash style):
+ * part_m/part_s [n_split][M] and Up [n_split][M][D] (Up[s][r] = Σ_{c∈s} 2^(v_rc − part_m[s][r])·W_c, v the
+ * log2-domain logit); the backward then needs no dH sweep (c2dsr_ce_dh_from_u). */
+int c2dsr_ce_fused_fwd_u(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
+                         float* part_m, float* part_s, float* Up, const float* padlogit, const int64_t* tgt,
+                         const float* H, const float* W, const float* bias, float* lse, float* lse2, float* loss_row,
+                         void* stream);
+/* dH[r] = rw[r]·(Σ_s 2^(part_m[s][r] − lse2[r])·Up[s][r] − (0 <= t32[r] < n ? W[t32[r]] : 0))  (fixed order) */
+int c2dsr_ce_dh_from_u(const float* Up, const float* part_m, int ns, int M, int D, const float* lse2, const int* t32,
+                       const float* rw, const float* W, int n, float* dH, void* stream);
 /* per row r < M_pad (multiple of 64): rw = valid ? gscale·lam·coef[r >= split] : 0, t32 = target (-1 pad),
  * crow = log2(rw) - lse2 (-inf where rw = 0 and past M), dpad = exp(padlogit - lse)·rw */
 int c2dsr_ce_row_weights(const int64_t* tgt, int M, int M_pad, int ignore, const float* coef, int split,

@@ -356,6 +356,18 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, M, n, D, ns, crow, dHp, s)
     lib('c2dsr_ce_dh_combine', dHp, ns, M, D, t32, rw, d(W), n, dH, s)
     assert rel(dH, dl[:, :n] @ W.double()) < 1e-2
+    # forward with the softmax part of dH accumulated online (lazy max rescale), then dH from its partials
+    pm2, ps2 = torch.empty(ns, M, device=DEV), torch.empty(ns, M, device=DEV)
+    Up = torch.empty(ns, M, D, device=DEV)
+    lse_u, rows_u = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    lse2_u = torch.empty(M_pad, device=DEV)
+    lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, M, n, D, ns, pm2, ps2, Up, d(pl), d(t), d(H), d(W), d(b), lse_u,
+        lse2_u, rows_u, s)
+    assert rel(lse_u, lse_r) < 2e-5
+    assert rel(rows_u, rows_r) < 1e-4
+    dHu = torch.empty(M, D, device=DEV)
+    lib('c2dsr_ce_dh_from_u', Up, pm2, ns, M, D, lse2_u, t32, rw, d(W), n, dHu, s)
+    assert rel(dHu, dl[:, :n] @ W.double()) < 1e-2
     gW = torch.ones(n, D, device=DEV)
     gb = torch.ones(n, device=DEV)
     dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
@@ -375,6 +387,60 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     ws = torch.empty(wsb, device=DEV, dtype=torch.uint8)
     lib('c2dsr_ce_onehot_dw_planned', tp.get(), M, n, d(H), D, rw, gW0, gb0, ws, wsb, s)
     assert torch.equal(gW0, gW) and torch.equal(gb0, gb)
+
+
+@pytest.mark.parametrize('M,n,D,ns', [(200, 1500, 256, 2), (333, 3000, 128, 5), (130, 900, 256, 1)])
+def test_fused_ce_online_rescale(M, n, D, ns):
+    """c2dsr_ce_fused_fwd_u when the row max keeps rising across column tiles (bias ramp of 60 nats and
+    a column-dependent scale: the lazy rescale fires many times, at different tiles for different rows
+    of one wave) and when it falls (reversed ramp on half of the rows via their H sign): lse vs float64,
+    dH = rw·(softmax·W − W[t]) vs float64."""
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(M * 7 + n)
+    H = _bf16(torch.randn(M, D, generator=g) * 0.3)
+    H[1::2, :8] = _bf16(-H[1::2, :8].abs() - 1.0)
+    H[0::2, :8] = _bf16(H[0::2, :8].abs() + 1.0)
+    W = torch.randn(n, D, generator=g) * 0.2
+    W[:, :8] = torch.linspace(-2.0, 2.0, n)[:, None]  # a score ramp rising for even rows, falling for odd rows
+    W = _bf16(W)
+    b = torch.linspace(0.0, 60.0, n) * (torch.rand(n, generator=g) > 0.5)
+    pl = torch.randn(M, generator=g)
+    t = torch.randint(0, n, (M,), generator=g)
+    s = stream()
+    d = lambda x: x.to(DEV)  # noqa: E731
+    M_pad = -(-M // 64) * 64
+    Hb = torch.zeros(M_pad, D, dtype=torch.bfloat16, device=DEV)
+    Hb[:M] = d(H.to(torch.bfloat16))
+    n64 = -(-n // 64) * 64
+    Wb = torch.zeros(n64, D, dtype=torch.bfloat16, device=DEV)
+    Wb[:n] = d(W.to(torch.bfloat16))
+    n_pad = -(-n // 128) * 128 + 64
+    bias2 = torch.empty(n_pad, device=DEV)
+    lib('c2dsr_ce_bias2', d(b), n, n_pad, bias2, s)
+    pm, ps = torch.empty(ns, M, device=DEV), torch.empty(ns, M, device=DEV)
+    Up = torch.empty(ns, M, D, device=DEV)
+    lse, rows = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    lse2 = torch.empty(M_pad, device=DEV)
+    lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, M, n, D, ns, pm, ps, Up, d(pl), d(t), d(H), d(W), d(b), lse, lse2,
+        rows, s)
+    lg = torch.cat([H.double() @ W.double().T + b.double(), pl.double()[:, None]], 1)
+    lse_r = torch.logsumexp(lg, 1)
+    assert rel(lse, lse_r) < 2e-5
+    coef, gs, lam = torch.tensor([0.5, 1.5]), torch.tensor([1.0]), 0.7
+    rw, dpad = torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)
+    t32 = torch.empty(M_pad, device=DEV, dtype=torch.int32)
+    crow = torch.empty(M_pad, device=DEV)
+    lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), M // 2, d(gs), lam, d(pl), lse, rw, t32, lse2, crow,
+        dpad, s)
+    dH = torch.empty(M, D, device=DEV)
+    lib('c2dsr_ce_dh_from_u', Up, pm, ns, M, D, lse2, t32, rw, d(W), n, dH, s)
+    w_r = lam * coef[(torch.arange(M) >= M // 2).long()].double()
+    P = torch.softmax(lg, 1)
+    oh = torch.zeros_like(P)
+    oh[torch.arange(M), t] = 1.0
+    ref = ((P - oh) * w_r[:, None])[:, :n] @ W.double()
+    assert rel(dH, ref) < 1e-2
+    assert torch.isfinite(Up).all()
 
 
 def _bf(x):
