@@ -196,7 +196,7 @@ def uniq_counts(batches):
 
 
 def k5_traffic(precision):
-    """HBM bytes per K5 launch triple (lse + dH + dW kernels, both heads averaged) from the separate
+    """HBM bytes per K5 launch set of one head (fwd_u + rows + dW kernels, both heads averaged) from the separate
     rocprofv3 FETCH_SIZE (x2, the gfx950 correction) / WRITE_SIZE passes of tools/round_profile.sh,
     summarised by tools/pmc_traffic.py into profiles/k5_traffic.json.  PMC counters cannot be read
     from inside this process, so the committed measurement of the same code is reported (null if

@@ -16,6 +16,7 @@ come from ``range(n_b - n_a)`` (Q14).
 """
 from __future__ import annotations
 
+import os
 import random
 from os.path import join
 
@@ -23,6 +24,7 @@ import numpy as np
 import torch
 from torch.utils.data import DataLoader, Dataset
 
+from . import processed
 from .graph import read_sequences
 
 TRAIN_FIELDS = ('seq_share', 'seq_a', 'seq_b', 'pos', 'pos_a', 'pos_b', 'gt_share_a', 'gt_share_b', 'gt_a',
@@ -163,16 +165,29 @@ def to_arrays(rows) -> list[np.ndarray]:
 
 
 class CDSRDataset(Dataset):
-    """dataloader.py:9-37,230-234 (always from the raw files; nothing is pickled)."""
+    """dataloader.py:9-37,230-234.  ``args.use_raw`` (main.py:24) selects the source as in the reference:
+    raw ``{mode}_new.txt`` under ``path_raw`` (processed here, then saved to ``path_data/{mode}.pkl`` like
+    dataloader.py:26-29), else the processed ``path_data/{mode}.pkl`` (dataloader.py:32-34), read with a
+    restricted unpickler that accepts only lists, tuples and ints (``processed.load_lists``).  ``args``
+    without a ``use_raw`` attribute (tests, benchmarks) read the raw files and write nothing."""
 
     def __init__(self, args, mode):
         self.mode = mode
-        fn = join(args.path_raw, mode + '_new.txt')
-        seqs = read_sequences(fn)
-        if mode == 'train':
-            self.data = preprocess_train(seqs, args.n_item_a, args.n_item_b, args.len_max)
+        use_raw = getattr(args, 'use_raw', None)
+        if use_raw is False:
+            self.data = processed.load_lists(join(args.path_data, mode + '.pkl'))
         else:
-            self.data = preprocess_evaluate(seqs, args.n_item_a, args.n_item_b, args.len_max, args.n_neg_sample)
+            fn = join(args.path_raw, mode + '_new.txt')
+            if not os.path.exists(fn):
+                raise FileNotFoundError(f'raw {mode} file {fn} is missing (use_raw reads path_raw/{mode}_new.txt)')
+            seqs = read_sequences(fn)
+            if mode == 'train':
+                self.data = preprocess_train(seqs, args.n_item_a, args.n_item_b, args.len_max)
+            else:
+                self.data = preprocess_evaluate(seqs, args.n_item_a, args.n_item_b, args.len_max,
+                                                args.n_neg_sample)
+            if use_raw:
+                processed.save_lists(join(args.path_data, mode + '.pkl'), self.data)
         self.length = len(self.data)
 
     def __len__(self):
@@ -188,9 +203,11 @@ def count_item(path):
 
 
 def get_dataloader(args):
-    """dataloader.py:245-259: sets n_item_a/b, n_item, idx_pad on args."""
-    args.n_item_a = count_item(join(args.path_raw, 'items_a.txt'))
-    args.n_item_b = count_item(join(args.path_raw, 'items_b.txt'))
+    """dataloader.py:245-259: sets n_item_a/b, n_item, idx_pad on args (item counts from ``path_raw`` with
+    ``use_raw``, else from ``path_data``, like dataloader.py:247)."""
+    p = args.path_data if getattr(args, 'use_raw', None) is False else args.path_raw
+    args.n_item_a = count_item(join(p, 'items_a.txt'))
+    args.n_item_b = count_item(join(p, 'items_b.txt'))
     args.n_item = args.n_item_a + args.n_item_b + 1
     args.idx_pad = args.n_item - 1
     nw = getattr(args, 'num_workers', 0)

@@ -15,6 +15,7 @@ instead of a torch sparse COO:
 from __future__ import annotations
 
 import codecs
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -160,6 +161,18 @@ class DeviceGraph:
 
 
 def make_graph(args, filename: str):
-    """utils/graph.py:99-109 (always from the raw file; no pickles)."""
+    """utils/graph.py:99-109.  With ``args.use_raw`` (or no such attribute) the graphs are built from the
+    raw train file (and saved to ``path_data/graph.pkl`` when ``args.save_processed``); with
+    ``use_raw=False`` they are read from that file (processed.load_graph: no code runs from it)."""
+    from . import processed
+    use_raw = getattr(args, 'use_raw', None)
+    if use_raw is False:
+        a_s, a_p = processed.load_graph(os.path.join(args.path_data, 'graph.pkl'))
+        from .models.C2DSR import _as_csr
+        return _as_csr(a_s, args.n_item), _as_csr(a_p, args.n_item)
+    if not os.path.exists(filename):
+        raise FileNotFoundError(f'raw train file {filename} is missing (the graph is built from it)')
     g_share, g_spec = preprocess_graph(filename, args.n_item_a, args.n_item)
+    if use_raw and getattr(args, 'save_processed', False):
+        processed.save_graph(os.path.join(args.path_data, 'graph.pkl'), g_share, g_spec)
     return g_share, g_spec

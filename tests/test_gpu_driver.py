@@ -1,0 +1,137 @@
+"""a10 / x1: main.py's epoch loop (main.py:88-148) through the drop-in Trainer(args, noter) on the GPU,
+against the reference's own trajectory (tests/golden/traj_<cfg>.npz, tools/gen_fixtures.py --traj):
+seeded like main.py:90-95, Trainer → get_dataloader → make_graph → C2DSR, then per epoch run_epoch
+(shuffled DataLoader, convolve_graph per batch, gradients accumulated over the epoch, Q3), the StepLR
+step, run_test — per-epoch train losses, the batch order, the val/test ranks and cal_score.
+
+Both the raw path (use_raw, processing the raw files) and the processed path (use_raw=False, reading
+the reference-written pickles) are driven.  Dropout 0 (the reference's CPU masks cannot be
+reproduced on a GPU); fp32 mode, where the step matches the reference within 1e-4."""
+import os
+import random
+import shutil
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from tests import goldens as G
+
+pytestmark = pytest.mark.gpu
+BENCH_FK = [0.1124, 0.0865, 0.0574, 0.0416]
+
+
+class Noter:
+    def __init__(self):
+        self.train = []
+
+    def log_train(self, *a):
+        self.train.append(a[:3])
+
+
+def _args(name, path_raw, path_data, use_raw):
+    c = G.CONFIGS[name]
+    return SimpleNamespace(
+        dataset='Synthetic', path_raw=str(path_raw), path_data=str(path_data), use_raw=use_raw, save_processed=False,
+        device=torch.device('cuda:0'), batch_size=G.BATCH, batch_size_eval=64, num_workers=0, n_neg_sample=G.N_NEG,
+        len_max=c['len_max'], len_rec=c['len_rec'], d_latent=c['d_latent'], n_gnn=c['n_gnn'], n_attn=c['n_attn'],
+        n_head=c['n_head'], norm_first=c['norm_first'], d_bias=c['d_bias'], shared_item_embed=c['shared_item_embed'],
+        dropout_gnn=0.0, dropout_attn=0.0, lr=1e-3, l2=5e-4, lr_step=10, lr_gamma=0.5, lambda_loss=0.7)
+
+
+def _raw_dir(tmp_path, name):
+    d = G.load(f'data_{name}.npz')
+    raw = tmp_path / 'raw'
+    raw.mkdir()
+    for mode in ('train', 'val', 'test'):
+        (raw / f'{mode}_new.txt').write_bytes(d[f'raw_{mode}'].tobytes())
+    for f in ('items_a.txt', 'items_b.txt'):
+        shutil.copy(os.path.join(G.GOLDEN, f'processed_{name}', f), raw / f)
+    return raw
+
+
+class _Rec:
+    """Records the shuffled batch order; the iteration itself is the DataLoader's."""
+
+    def __init__(self, loader, order):
+        self.loader, self.order, self.dataset = loader, order, loader.dataset
+
+    def __iter__(self):
+        for b in self.loader:
+            self.order.append(b[0].numpy().copy())
+            yield b
+
+
+def _drive(args):
+    from c2dsr_amd.trainer import Trainer
+    from oracle.c2dsr_oracle import cal_score  # utils/metrics.py:22-31, which main.py keeps
+    random.seed(3407)  # main.py:90-95
+    torch.manual_seed(3407)
+    torch.cuda.manual_seed_all(3407)
+    np.random.seed(3407)
+    noter = Noter()
+    tr = Trainer(args, noter)
+    sched = torch.optim.lr_scheduler.StepLR(tr.optimizer, step_size=args.lr_step, gamma=args.lr_gamma)  # main.py:99
+    loader = tr.trainloader
+    out = []
+    for _ in range(int(G.load('traj_base.npz')['n_epoch'])):
+        order = []
+        tr.trainloader = _Rec(loader, order)
+        va, vb = tr.run_epoch()
+        sched.step()
+        ta, tb = tr.run_test()
+        out.append(dict(order=np.concatenate(order), loss=np.asarray(noter.train[-1]), val_a=va, val_b=vb,
+                        test_a=ta, test_b=tb, val_score=np.asarray(cal_score(va, vb, BENCH_FK)),
+                        test_score=np.asarray(cal_score(ta, tb, BENCH_FK))))
+    return tr, out
+
+
+def _check(name, tr, out):
+    ref = G.load(f'traj_{name}.npz')
+    for e, got in enumerate(out):
+        np.testing.assert_array_equal(got['order'], ref[f'e{e}/order_seq_share'], err_msg=f'epoch {e} batch order')
+        np.testing.assert_allclose(got['loss'], ref[f'e{e}/loss'], rtol=1e-4, err_msg=f'epoch {e} losses')
+        for k in ('val_a', 'val_b', 'test_a', 'test_b'):
+            np.testing.assert_array_equal(np.asarray(got[k]), ref[f'e{e}/{k}'], err_msg=f'epoch {e} {k}')
+        np.testing.assert_allclose(got['val_score'], ref[f'e{e}/val_score'], rtol=1e-9)
+        np.testing.assert_allclose(got['test_score'], ref[f'e{e}/test_score'], rtol=1e-9)
+    for n, p in tr.model.named_parameters():
+        r = ref[f'final/{n}']
+        assert G.rel_err(p.detach().cpu().numpy(), r) < 1e-3, n
+    # the device-side metric accumulation (one host sync per pass) gives the same test score
+    last = len(out) - 1
+    np.testing.assert_allclose(tr.evaluate_metrics(tr.testloader).score(BENCH_FK), ref[f'e{last}/test_score'],
+                               rtol=1e-9)
+
+
+@pytest.mark.parametrize('name', ['base', 'var'])
+def test_epoch_trajectory_raw_path(tmp_path, name):
+    raw = _raw_dir(tmp_path, name)
+    tr, out = _drive(_args(name, raw, tmp_path / 'data', True))
+    _check(name, tr, out)
+
+
+def test_epoch_trajectory_processed_path(tmp_path):
+    """use_raw=False (main.py's default): the reference-written {train,val,test}.pkl / graph.pkl."""
+    tr, out = _drive(_args('base', tmp_path / 'no_raw', os.path.join(G.GOLDEN, 'processed_base'), False))
+    _check('base', tr, out)
+
+
+def test_run_epoch_memory_flat(tmp_path):
+    """f4: no per-step host sync and no graph kept alive across steps (the epoch loss
+    accumulator once held every step's autograd graph).  Allocated memory after each of several
+    epochs stays the same."""
+    raw = _raw_dir(tmp_path, 'base')
+    from c2dsr_amd.trainer import Trainer
+    random.seed(3407)
+    torch.manual_seed(3407)
+    args = _args('base', raw, tmp_path / 'data', True)
+    tr = Trainer(args, Noter())
+    tr.run_epoch()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    for _ in range(3):
+        tr.run_epoch()
+        torch.cuda.synchronize()
+        assert torch.cuda.memory_allocated() <= base, (torch.cuda.memory_allocated(), base)

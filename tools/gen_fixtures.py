@@ -12,6 +12,12 @@ copied.  Outputs are plain arrays (npz, no pickles) under tests/golden/:
   eval_<cfg>.npz   evaluate_batch ranks after the two steps (trainer.py:162-181)
   metrics.npz      cal_metrics / cal_score (utils/metrics.py)
   fk_data.npz      checksums + head of the Food-Kitchen val/test processing
+  traj_<cfg>.npz   main.py's epoch loop driven through the reference Trainer(args, noter) for
+                   N_EPOCH epochs (seeded like main.py:90-95, dropout 0, num_workers 0): per-epoch
+                   train losses, the shuffled batch order, val/test ranks and cal_score
+  processed_<cfg>/ the {train,val,test}.pkl + graph.pkl the reference writes with --use_raw
+                   --save_processed (dataloader.py:26-29, utils/graph.py:101-103) and the item lists,
+                   for the use_raw=False read path (c2dsr_amd/processed.py)
 
 Usage:  python tools/gen_fixtures.py   (PYTHONDONTWRITEBYTECODE=1 is set here)
 """
@@ -244,6 +250,80 @@ def gen_config(name, cfg, ref):
           f'E_share={len(g["share_val"])} E_spec={len(g["specific_val"])} steps={n_steps}')
 
 
+N_EPOCH = 3
+
+
+class _Noter:
+    def __init__(self):
+        self.train = []
+
+    def log_train(self, *a):
+        self.train.append(a[:3])
+
+    def __getattr__(self, name):
+        return lambda *a, **k: None
+
+
+def gen_trajectory(name, cfg, ref):
+    """main.py:88-148 through the reference's own Trainer (trainer.py:13-83), dropout 0."""
+    import shutil
+    ref_dl, ref_model, ref_trainer, ref_graph, ref_metrics = ref
+    tmp = tempfile.mkdtemp(prefix=f'c2dsr_traj_{name}_')
+    path_raw = os.path.join(tmp, 'raw')
+    path_data = os.path.join(tmp, 'data')
+    os.makedirs(path_data)
+    synth.make_dataset(path_raw, cfg['n_a'], cfg['n_b'], cfg['len_max'], cfg['n_train'], cfg['n_eval'],
+                       seed=11, ties=True, n_min=2)
+    args = make_args(cfg, path_raw, path_data)
+    args.save_processed = True
+    bench = [0.1124, 0.0865, 0.0574, 0.0416]
+    random.seed(3407)
+    torch.manual_seed(3407)
+    np.random.seed(3407)
+    noter = _Noter()
+    tr = ref_trainer.Trainer(args, noter)
+    sched = torch.optim.lr_scheduler.StepLR(tr.optimizer, step_size=args.lr_step, gamma=args.lr_gamma)
+    out = {'n_epoch': np.int64(N_EPOCH)}
+    for k, v in tr.model.state_dict().items():
+        out[f'init/{k}'] = v.detach().numpy().copy()
+    loader = tr.trainloader
+
+    class _Rec:  # records the shuffled batch order; iteration itself is the DataLoader's
+        def __init__(self, order):
+            self.order = order
+            self.dataset = loader.dataset
+
+        def __iter__(self):
+            for b in loader:
+                self.order.append(b[0].numpy().copy())
+                yield b
+
+    for e in range(N_EPOCH):
+        order = []
+        tr.trainloader = _Rec(order)
+        va, vb = tr.run_epoch()
+        sched.step()
+        ta, tb = tr.run_test()
+        out[f'e{e}/order_seq_share'] = np.concatenate(order)
+        out[f'e{e}/loss'] = np.asarray(noter.train[-1], dtype=np.float64)
+        out[f'e{e}/val_a'] = np.asarray(va, dtype=np.int64)
+        out[f'e{e}/val_b'] = np.asarray(vb, dtype=np.int64)
+        out[f'e{e}/test_a'] = np.asarray(ta, dtype=np.int64)
+        out[f'e{e}/test_b'] = np.asarray(tb, dtype=np.int64)
+        out[f'e{e}/val_score'] = np.asarray(ref_metrics.cal_score(va, vb, bench), dtype=np.float64)
+        out[f'e{e}/test_score'] = np.asarray(ref_metrics.cal_score(ta, tb, bench), dtype=np.float64)
+    for n, p in tr.model.named_parameters():
+        out[f'final/{n}'] = p.detach().numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f'traj_{name}.npz'), **out)
+    dst = os.path.join(OUT, f'processed_{name}')
+    os.makedirs(dst, exist_ok=True)
+    for f in ('train.pkl', 'val.pkl', 'test.pkl', 'graph.pkl'):
+        shutil.copy(os.path.join(path_data, f), os.path.join(dst, f))
+    for f in ('items_a.txt', 'items_b.txt'):
+        shutil.copy(os.path.join(path_raw, f), os.path.join(dst, f))
+    print(f'[traj {name}] epochs={N_EPOCH} losses={[tuple(out[f"e{e}/loss"]) for e in range(N_EPOCH)]}')
+
+
 def gen_metrics(ref):
     ref_metrics = ref[4]
     rng = np.random.default_rng(5)
@@ -298,10 +378,15 @@ def gen_fk(ref):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--only', default='')
+    ap.add_argument('--traj', action='store_true', help='only the epoch trajectories')
     opt = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
     ref = ref_import()
+    if opt.traj:
+        for name in ('base', 'var'):
+            gen_trajectory(name, CONFIGS[name], ref)
+        return
     for name, cfg in CONFIGS.items():
         if opt.only and name != opt.only:
             continue

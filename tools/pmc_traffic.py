@@ -12,7 +12,8 @@ from collections import defaultdict
 
 pre = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else None
-K5 = ('ce_lse_kernel', 'ce_dh_kernel', 'ce_dw_kernel')
+# the kernels the two timed K5 entry points launch per head (c2dsr_ce_fused_fwd_u: fwdu + rows; _dw: dw)
+K5 = ('ce_fwdu_kernel', 'ce_rows_kernel', 'ce_dw_kernel')
 K12 = ('spmm_kernel', 'combine_kernel', 'embed_fwd_kernel', 'seg_chunk_kernel', 'seg_split1_kernel',
        'seg_split2_kernel')
 PMC_STEPS = 3
@@ -39,7 +40,7 @@ for k in K5:
     rows[k] = dict(launches=len(fe[k]), fetch_bytes=round(f), write_bytes=round(w), bytes=round(f + w))
     print(f'{k:16} launches {len(fe[k]):3d}  fetch {f / 1e6:9.1f} MB  write {w / 1e6:8.1f} MB')
 tot = sum(r['bytes'] for r in rows.values())
-print(f'K5 launch triple: {tot / 1e6:.1f} MB')
+print(f'K5 per head (fwd_u + rows + dw launches): {tot / 1e6:.1f} MB')
 # MFMA-busy fraction of the K5 kernels from the SQ pass (SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs'
 # cycles, GRBM_GUI_ACTIVE summed over the 8 XCDs), summed over their launches
 mfma_busy = None
