@@ -24,7 +24,7 @@ import numpy as np
 import torch
 from torch.utils.data import DataLoader, Dataset
 
-from . import processed
+from . import prep, processed
 from .graph import read_sequences
 
 TRAIN_FIELDS = ('seq_share', 'seq_a', 'seq_b', 'pos', 'pos_a', 'pos_b', 'gt_share_a', 'gt_share_b', 'gt_a',
@@ -164,37 +164,60 @@ def to_arrays(rows) -> list[np.ndarray]:
     return [np.asarray([r[j] for r in rows], dtype=np.int64) for j in range(len(rows[0]))]
 
 
+def native_prep() -> bool:
+    """The native pipeline (c2dsr_amd/prep.py) processes raw files unless C2DSR_PREP=python."""
+    return os.environ.get('C2DSR_PREP', 'native') != 'python' and prep.available()
+
+
 class CDSRDataset(Dataset):
     """dataloader.py:9-37,230-234.  ``args.use_raw`` (main.py:24) selects the source as in the reference:
     raw ``{mode}_new.txt`` under ``path_raw`` (processed here, then saved to ``path_data/{mode}.pkl`` like
     dataloader.py:26-29), else the processed ``path_data/{mode}.pkl`` (dataloader.py:32-34), read with a
     restricted unpickler that accepts only lists, tuples and ints (``processed.load_lists``).  ``args``
-    without a ``use_raw`` attribute (tests, benchmarks) read the raw files and write nothing."""
+    without a ``use_raw`` attribute (tests, benchmarks) read the raw files and write nothing.
+
+    Raw files are processed by the native pipeline (libc2dsr_prep.so, bit-exact, same draws from
+    Python's ``random``) or, with C2DSR_PREP=python, by the Python restatement above.  The rows are held
+    as one int64 array per field (``fields``); ``data`` gives the reference's list-of-lists form."""
 
     def __init__(self, args, mode):
         self.mode = mode
         use_raw = getattr(args, 'use_raw', None)
         if use_raw is False:
-            self.data = processed.load_lists(join(args.path_data, mode + '.pkl'))
+            self.fields = to_arrays(processed.load_lists(join(args.path_data, mode + '.pkl')))
         else:
             fn = join(args.path_raw, mode + '_new.txt')
             if not os.path.exists(fn):
                 raise FileNotFoundError(f'raw {mode} file {fn} is missing (use_raw reads path_raw/{mode}_new.txt)')
-            seqs = read_sequences(fn)
+            self.fields = self._process(fn, args, mode)
+        self.length = len(self.fields[0]) if self.fields else 0
+        if use_raw:
+            processed.save_lists(join(args.path_data, mode + '.pkl'), self.data)
+
+    @staticmethod
+    def _process(fn, args, mode):
+        if native_prep():
+            rf = prep.RawFile(fn)
             if mode == 'train':
-                self.data = preprocess_train(seqs, args.n_item_a, args.n_item_b, args.len_max)
-            else:
-                self.data = preprocess_evaluate(seqs, args.n_item_a, args.n_item_b, args.len_max,
-                                                args.n_neg_sample)
-            if use_raw:
-                processed.save_lists(join(args.path_data, mode + '.pkl'), self.data)
-        self.length = len(self.data)
+                rows = rf.train_rows(args.n_item_a, args.n_item_b, args.len_max)
+                return [rows[:, j] for j in range(rows.shape[1])]
+            seqs, last, neg = rf.eval_rows(args.n_item_a, args.n_item_b, args.len_max, args.n_neg_sample)
+            return [seqs[:, j] for j in range(6)] + [last[:, j:j + 1] for j in range(4)] + [neg]
+        seqs = read_sequences(fn)
+        if mode == 'train':
+            return to_arrays(preprocess_train(seqs, args.n_item_a, args.n_item_b, args.len_max))
+        return to_arrays(preprocess_evaluate(seqs, args.n_item_a, args.n_item_b, args.len_max, args.n_neg_sample))
+
+    @property
+    def data(self):
+        """The reference's form: one list of per-field lists per sequence."""
+        return [[f[i].tolist() for f in self.fields] for i in range(self.length)]
 
     def __len__(self):
         return self.length
 
     def __getitem__(self, index):
-        return tuple(torch.LongTensor(x) for x in self.data[index])
+        return tuple(torch.from_numpy(f[index]) for f in self.fields)
 
 
 def count_item(path):

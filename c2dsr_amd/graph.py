@@ -102,6 +102,12 @@ def normalized_csr(edges: np.ndarray, n: int) -> CSRGraph:
 
 
 def preprocess_graph(seqs_or_file, n_item_a: int, n_item: int) -> tuple[CSRGraph, CSRGraph]:
+    """A raw file is parsed and walked by the native pipeline (c2dsr_amd/prep.py) unless
+    C2DSR_PREP=python; a list of sequences by :func:`transition_edges`."""
+    from . import prep
+    if isinstance(seqs_or_file, str) and os.environ.get('C2DSR_PREP', 'native') != 'python' and prep.available():
+        e_share, e_spec = prep.RawFile(seqs_or_file).edges(n_item_a)
+        return normalized_csr(e_share, n_item), normalized_csr(e_spec, n_item)
     seqs = read_sequences(seqs_or_file) if isinstance(seqs_or_file, str) else seqs_or_file
     e_share, e_spec = transition_edges(seqs, n_item_a)
     return normalized_csr(e_share, n_item), normalized_csr(e_spec, n_item)
