@@ -57,13 +57,13 @@ def make_workload(cfg, n_seqs, seed=1):
     return rows, gs, gp
 
 
-def make_args(cfg, device, precision, dropout=0.2):
+def make_args(cfg, device, precision, dropout=0.2, zero1=False):
     n = cfg['n_a'] + cfg['n_b'] + 1
     return SimpleNamespace(d_latent=cfg['d'], n_item=n, n_item_a=cfg['n_a'], n_item_b=cfg['n_b'], idx_pad=n - 1,
                            shared_item_embed=False, d_bias=False, n_gnn=1, dropout_gnn=dropout, n_attn=1, n_head=1,
                            dropout_attn=dropout, norm_first=False, len_max=cfg['L'], len_rec=10, lambda_loss=0.7,
                            lr=1e-3, l2=5e-4, lr_step=10, lr_gamma=0.5, batch_size=cfg['B'], device=device,
-                           precision=precision, seed=3407)
+                           precision=precision, seed=3407, zero1=zero1)
 
 
 class KernelTimer:
@@ -373,6 +373,8 @@ def main():
     ap.add_argument('--c5-seqs', type=int, default=2_000_000)
     ap.add_argument('--no-extra', dest='extra', action='store_false',
                     help='skip the extra lines (MB fp32 mode, FK bf16) of the default N=1 run')
+    ap.add_argument('--zero1', action='store_true',
+                    help='N>1: ZeRO-1 (reduce-scatter, 1/p AdamW, all-gather; c2dsr_amd/dp.py) for the main line')
     ap.add_argument('--dp-split', action='store_true',
                     help='strong scaling: every rank trains its slice of the same global batch (BASELINE '
                          'configs[3], e.g. --config ee --batch 4096)')
@@ -404,8 +406,24 @@ def main():
         cfg['B'] = opt.batch
     wl = workload(cfg, opt.config)
     res = run_train(opt, cfg, opt.config, opt.precision, wl, world, rank, device)
+    extra = {}
+    if world > 1 and opt.extra:
+        # the other exchange of the N>1 path: ZeRO-1 if the main line replicated AdamW,
+        # else the replicated all-reduce — same workload, same ranks
+        torch.cuda.empty_cache()
+        alt = not opt.zero1
+        r2 = run_train(opt, cfg, opt.config, opt.precision, wl, world, rank, device, zero1=alt)
+        if rank == 0:
+            extra['dp_zero1' if alt else 'dp_allreduce'] = brief(r2)
+        if opt.config == 'mb' and not opt.batch:
+            # BASELINE configs[3] (C4): Entertainment-Education sizes, B=4096 global split over the ranks
+            # (strong scaling), the same exchange as the main line
+            torch.cuda.empty_cache()
+            ee = dict(CONFIGS['ee'], B=4096)
+            r3 = run_train(opt, ee, 'ee', opt.precision, workload(ee, 'ee'), world, rank, device, dp_split=True)
+            if rank == 0:
+                extra['ee_c4_split'] = brief(r3)
     if rank == 0:
-        extra = {}
         if world == 1 and opt.extra and opt.config == 'mb' and not opt.batch:
             # driver-visible lines of the other single-GPU configurations: the fp32 parity
             # mode on the same workload, and BASELINE configs[1] (Food-Kitchen sizes, B=1024, bf16)
@@ -437,7 +455,7 @@ def workload(cfg, name):
 
 
 def brief(r):
-    keep = ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'loss')
+    keep = ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'loss', 'n_gpus')
     out = {k: r[k] for k in keep}
     for k in ('roofline', 'roofline_hbm'):
         if r.get(k):
@@ -445,22 +463,24 @@ def brief(r):
     return out
 
 
-def run_train(opt, cfg, name, precision, wl, world, rank, device):
+def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp_split=None):
     """W untimed + K timed training steps of one configuration; returns the bench line (rank 0)."""
     rows, gs, gp = wl
     B = cfg['B']
     n_rows = rows[0].shape[0]
     n_batches = opt.steps + opt.warmup
     from c2dsr_amd.trainer import Trainer
-    args = make_args(cfg, device, precision)
+    zero1 = opt.zero1 if zero1 is None else zero1
+    dp_split = opt.dp_split if dp_split is None else dp_split
+    args = make_args(cfg, device, precision, zero1=zero1 and world > 1)
     torch.manual_seed(3407)
     tr = Trainer(args, None, data=(None, None, None), graphs=(gs, gp))
-    tr.dp_split = opt.dp_split
-    B_local = B if not opt.dp_split else -(-B // world)
+    tr.dp_split = dp_split
+    B_local = B if not dp_split else -(-B // world)
     batches = []
     for i in range(n_batches):
         # weak scaling: rank r trains batch (i·world + r); dp_split: all ranks slice the same global batch
-        j = i * world + rank if not opt.dp_split else i
+        j = i * world + rank if not dp_split else i
         lo = (j * B) % max(1, n_rows - B)
         batches.append(tuple(torch.from_numpy(r[lo:lo + B].copy()).to(device) for r in rows))
     timer = KernelTimer(precision)
@@ -473,7 +493,7 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device):
     htimer = HbmTimer(tr.model.n_item, nnz, uniq_counts(batches))
     tr.model.train()
     tr.optimizer.zero_grad()
-    B_global = B * world if not opt.dp_split else B
+    B_global = B * world if not dp_split else B
 
     def step(b):
         tr.model.convolve_graph()
@@ -522,11 +542,11 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device):
     if hb is not None and name == 'mb' and precision == 'bf16':
         hb['traffic'], hb['traffic_source'] = hbm_traffic()
         hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
-    par = f'dp{world}' + ('-split' if opt.dp_split and world > 1 else '')
+    par = f'dp{world}' + ('-split' if dp_split and world > 1 else '') + ('-zero1' if zero1 and world > 1 else '')
     return {'metric': 'train sequences/sec at d=256, seq_len=50, |items|~100k',
             'value': round(value, 2), 'unit': 'train sequences/sec', 'n_gpus': world, 'steps': opt.steps,
             'warmup': opt.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
-            'scaling': 'strong' if opt.dp_split and world > 1 else 'weak',
+            'scaling': 'strong' if dp_split and world > 1 else 'weak',
             'vs_baseline': None, 'dtype': precision, 'data': 'synthetic (Zipf two-domain sequences)',
             'config': {'workload': f'{name}: {cfg["label"]}', 'n_item_a': cfg['n_a'], 'n_item_b': cfg['n_b'],
                        'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B_local, 'global_batch': B_global,

@@ -454,11 +454,11 @@ __global__ __launch_bounds__(1024) void loss_partials_kernel(const float* __rest
   for (int r = threadIdx.x; r < 2 * BR; r += blockDim.x) {
     const int h = r >= BR ? 1 : 0;
     if (tA[r] != n_a) {
-      acc[h] += rowsA[r];
+      if (rowsA) acc[h] += rowsA[r];
       acc[4 + h] += 1.f;
     }
     if (tB[r] != n_b) {
-      acc[2 + h] += rowsB[r];
+      if (rowsB) acc[2 + h] += rowsB[r];
       acc[6 + h] += 1.f;
     }
   }
@@ -476,22 +476,24 @@ __global__ __launch_bounds__(1024) void loss_partials_kernel(const float* __rest
 
 // scalar combination (trainer.py:143-156) from the (globally reduced) vec[0..8]
 // (vec[8] = loss_mi).  out3 = (loss, loss_rec, loss_mi); coefA/coefB = per-row
-// gradient weights (share, specific) of the two stacks.
-__global__ void finalize_kernel(const float* __restrict__ vec, float RB, float lam, float* __restrict__ out3,
-                                float* __restrict__ coefA, float* __restrict__ coefB) {
+// gradient weights (share, specific) of the two stacks.  cnt (nullable): the valid-target counts
+// (cnt[4..7]) when they were reduced separately, ahead of the forward (data parallel).
+__global__ void finalize_kernel(const float* __restrict__ vec, const float* __restrict__ cnt, float RB, float lam,
+                                float* __restrict__ out3, float* __restrict__ coefA, float* __restrict__ coefB) {
   if (threadIdx.x != 0) return;
-  const float ce_sa = vec[0] / vec[4], ce_a = vec[1] / vec[5];
-  const float ce_sb = vec[2] / vec[6], ce_b = vec[3] / vec[7];
-  const float loss_share = ce_sa * vec[4] / RB + ce_sb * vec[6] / RB;
+  const float* c = cnt ? cnt : vec;
+  const float ce_sa = vec[0] / c[4], ce_a = vec[1] / c[5];
+  const float ce_sb = vec[2] / c[6], ce_b = vec[3] / c[7];
+  const float loss_share = ce_sa * c[4] / RB + ce_sb * c[6] / RB;
   const float loss_rec = loss_share + ce_a + ce_b;
   const float lmi = vec[8];
   out3[0] = lam * loss_rec + (1.f - lam) * lmi;
   out3[1] = loss_rec;
   out3[2] = lmi;
   coefA[0] = 1.f / RB;
-  coefA[1] = 1.f / vec[5];
+  coefA[1] = 1.f / c[5];
   coefB[0] = 1.f / RB;
-  coefB[1] = 1.f / vec[7];
+  coefB[1] = 1.f / c[7];
 }
 
 // ds[k][b] *= gscale * (1 - lam)
@@ -646,9 +648,9 @@ C2_API int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, c
   C2_CHECK_LAUNCH();
   return 0;
 }
-C2_API int c2dsr_loss_finalize(const float* vec, int BR_global, float lam, float* out3, float* coefA, float* coefB,
-                               void* stream) {
-  finalize_kernel<<<1, 64, 0, (hipStream_t)stream>>>(vec, (float)BR_global, lam, out3, coefA, coefB);
+C2_API int c2dsr_loss_finalize(const float* vec, const float* cnt, int BR_global, float lam, float* out3, float* coefA,
+                               float* coefB, void* stream) {
+  finalize_kernel<<<1, 64, 0, (hipStream_t)stream>>>(vec, cnt, (float)BR_global, lam, out3, coefA, coefB);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -1,78 +1,209 @@
-"""Bucketed data-parallel gradient all-reduce, overlapped with the backward.
+"""Data-parallel gradient exchange, overlapped with the backward.
 
-The step has one real exchange: the sum all-reduce of this step's flat gradient
-(``FlatStore.fresh``).  Instead of one collective after ``loss.backward()``, the flat
-buffer is cut into buckets that become final at known points of the backward, and each
-bucket's all-reduce is issued (``async_op=True``: RCCL on its own stream, ordered after
-the kernels already enqueued) the moment it is final, so the collectives run under the
-remaining backward kernels:
+The step has one real exchange: the sum over ranks of this step's flat gradient
+(``FlatStore.fresh``).  ``CommPlan`` cuts the flat store, once, into *reduction ranges* that become
+final at known points of the backward; ``DPComm`` issues each range's collective (``async_op=True``:
+RCCL on its own stream, ordered after the kernels already enqueued) the moment it is final, so the
+collectives run under the remaining backward kernels:
 
-* the **dense** bucket (every parameter that is not an item table: pos_emb, encoder,
-  classifier heads, D_a/D_b) is final once the last embedding-lookup backward
-  (``EmbedFn.backward``, the tail of every encoder pass) has run — the loss head and
-  every encoder backward precede it by data dependence.  It is issued then, under the
-  three GCN backwards;
-* each **item table** bucket (``embed_i``, ``embed_i_a``, ``embed_i_b``; one bucket when
-  ``shared_item_embed``) is final after the last GCN backward that reads that table
-  (``GCNFn.backward`` writes ``E.grad`` last), and is issued then, under the next table's
-  GCN backward.
+* the **dense** ranges (every parameter that is not an item table: pos_emb, encoder, classifier heads,
+  D_a/D_b) are final once the last embedding-lookup backward (``EmbedFn.backward``, the tail of every
+  encoder pass) has run — the loss head and every encoder backward precede it by data dependence —
+  and are issued then, under the three GCN backwards;
+* each **item table** (``embed_i``, ``embed_i_a``, ``embed_i_b``; one table when ``shared_item_embed``)
+  is final after the last GCN backward that reads it.  That backward's last SpMM runs in row chunks
+  (``GCNFn.backward`` asks ``row_cuts``) and each chunk's collective is issued as soon as the chunk is
+  written, under the chunks after it and the next table's backward — so only the last chunk of the
+  last table is exposed, not the whole table.
 
-Reference behaviour replaced: the single-process ``loss.backward(); optimizer.step()``
-of trainer.py:156-158 — with these sums the rank-local step equals the single-device
-step (global-count loss normalisation, losshead.LossMeta).
+Two modes:
+  ``allreduce``  every rank ends with the summed gradient in ``fresh`` and runs the (replicated) AdamW
+                 over all of it (c2dsr_amd/optim.py);
+  ``zero1``      ZeRO-1: each range is reduce-scattered, rank r receiving the sum of its 1/p part of the
+                 range into ``Zero1.gshard``; AdamW updates only the owned parts (optimizer state and the
+                 epoch accumulation are 1/p-sized), then each range's parameters are all-gathered
+                 (``Zero1.gather``).  Same bytes on the wire as the all-reduce (reduce-scatter +
+                 all-gather), 1/p of the optimizer's HBM traffic and state.
+
+Every range's length is a multiple of 4·world elements (FlatStore aligns every parameter slice to
+4·world), so the reduce-scatter splits it into equal float4-aligned parts.
+
+Reference behaviour replaced: the single-process ``loss.backward(); optimizer.step()`` of
+trainer.py:156-158 — with these sums the rank-local step equals the single-device step (global-count
+loss normalisation, losshead.LossMeta).
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
 
+TABLE_CHUNKS = 4  # row chunks of the last GCN backward of each table (collectives issued per chunk)
+ROW_ALIGN = 8     # chunk boundaries at multiples of 8 rows
 
-class GradBuckets:
-    """Issues the per-bucket all-reduces of ``flat.fresh`` as the backward makes them final.
 
-    tables: the item-table parameters (possibly the same one several times); gcn_uses[i]
-    is how many GCN backwards will write tables[i]'s gradient this step; n_lookups the
-    number of embedding-lookup passes whose backward must run before the dense bucket is
-    final.  ``allreduce(t)`` must return a work handle with ``.wait()`` (default:
-    ``dist.all_reduce(t, async_op=True)``)."""
+class CommPlan:
+    """Static partition of ``flat`` into reduction ranges.
 
-    def __init__(self, flat, tables, n_lookups, allreduce=None):
-        self.flat = flat
-        self.allreduce = allreduce or (lambda t: dist.all_reduce(t, async_op=True))
-        ptr2slice = {p.data_ptr(): (o, n) for _, p, o, n in flat.entries}
-        self.table_left = {}
-        self.table_range = {}
+    tables: item-table parameters (possibly the same one several times: shared_item_embed).
+    Attributes: ``dense`` [(lo, hi)], ``table_chunks`` {table ptr: [(r0, r1, lo, hi)]} (rows r0..r1 of the
+    table ↔ flat range lo..hi; the last chunk also covers the slice's alignment padding), ``ranges`` every
+    range in a fixed order (dense first, then the tables' chunks), ``index`` {(lo, hi): position}."""
+
+    def __init__(self, flat, tables, world: int, chunks: int = TABLE_CHUNKS):
+        self.world = world
+        align = 4 * world
+        ptr2 = {p.data_ptr(): (o, n, p) for _, p, o, n in flat.entries}
+        self.table_chunks = {}
+        cuts = []
         for t in tables:
             k = t.data_ptr()
-            if k not in ptr2slice:
+            if k in self.table_chunks:
+                continue
+            if k not in ptr2:
                 raise KeyError('table parameter is not in the flat store')
-            self.table_left[k] = self.table_left.get(k, 0) + 1
-            o, n = ptr2slice[k]
-            self.table_range[k] = (o, o + n)
-        # dense bucket = complement of the table ranges, merged into contiguous pieces
-        cuts = sorted(self.table_range.values())
+            o, n, p = ptr2[k]
+            N, d = p.shape
+            hi = o + flat.padded(n)
+            if (o % align) or (hi % align):
+                raise ValueError('flat store is not aligned for this world size')
+            rows = sorted({min(N, (N * c // chunks) // ROW_ALIGN * ROW_ALIGN) for c in range(chunks)} | {N})
+            if (ROW_ALIGN * d) % align:
+                rows = [0, N]  # chunk boundaries would not be aligned: one chunk
+            ch = []
+            for a, b in zip(rows[:-1], rows[1:]):
+                if b > a:
+                    ch.append((a, b, o + a * d, hi if b == N else o + b * d))
+            self.table_chunks[k] = ch
+            cuts.append((o, hi))
         dense, lo = [], 0
-        for a, b in cuts:
+        for a, b in sorted(cuts):
             if a > lo:
                 dense.append((lo, a))
-            lo = max(lo, (b + 3) // 4 * 4)
+            lo = max(lo, b)
         if lo < flat.numel:
             dense.append((lo, flat.numel))
         self.dense = dense
+        self.ranges = list(dense) + [(lo, hi) for ch in self.table_chunks.values() for _, _, lo, hi in ch]
+        self.index = {r: i for i, r in enumerate(self.ranges)}
+        pos = 0
+        for lo, hi in sorted(self.ranges):  # every element in exactly one range
+            if lo != pos or (hi - lo) % align:
+                raise RuntimeError(f'reduction ranges do not tile the flat store at {pos}..{lo}')
+            pos = hi
+        if pos != flat.numel:
+            raise RuntimeError('reduction ranges do not cover the flat store')
+
+
+def _gloo_cuda(t):
+    return t.is_cuda and dist.get_backend() == 'gloo'
+
+
+def reduce_scatter(out, inp):
+    """Sum of ``inp`` over ranks, this rank's 1/world part into ``out`` (async handle).  gloo (CPU
+    rehearsal of several ranks on one device) has no device reduce-scatter: all-reduce a copy instead."""
+    if _gloo_cuda(inp):
+        tmp = inp.clone()
+        dist.all_reduce(tmp)
+        r, n = dist.get_rank(), out.numel()
+        out.copy_(tmp[r * n:(r + 1) * n])
+        return _Done()
+    return dist.reduce_scatter_tensor(out, inp, async_op=True)
+
+
+def all_gather(out, inp):
+    """Every rank's ``inp`` (its part of ``out``, possibly a view of it) into ``out`` (async handle)."""
+    if _gloo_cuda(inp):
+        parts = [torch.empty_like(inp) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, inp.clone())
+        out.copy_(torch.cat(parts))
+        return _Done()
+    return dist.all_gather_into_tensor(out, inp, async_op=True)
+
+
+class _Done:
+    def wait(self):
+        pass
+
+
+class Zero1:
+    """ZeRO-1 ownership: rank r owns the r-th 1/world part of every reduction range.  The owned parts,
+    concatenated in ``plan.ranges`` order, form this rank's shard (``shard_numel`` elements); the
+    optimizer keeps its state and the epoch accumulation only for the shard."""
+
+    def __init__(self, flat, plan: CommPlan, rank: int, world: int, gather=None):
+        self.flat, self.plan, self.rank, self.world = flat, plan, rank, world
+        self.parts = []  # (range lo, range hi, own lo, own hi, shard offset)
+        off = 0
+        for lo, hi in plan.ranges:
+            c = (hi - lo) // world
+            self.parts.append((lo, hi, lo + rank * c, lo + (rank + 1) * c, off))
+            off += c
+        self.shard_numel = off
+        self.gshard = torch.zeros(off, device=flat.device, dtype=torch.float32)
+        self._gather = gather or all_gather
+
+    def part_of(self, rng):
+        return self.parts[self.plan.index[rng]]
+
+    def gather(self):
+        """All-gather every range's updated parameters (owned part → all ranks); returns the handles."""
+        p = self.flat.param
+        return [self._gather(p[lo:hi], p[olo:ohi]) for lo, hi, olo, ohi, _ in self.parts]
+
+
+class DPComm:
+    """Issues the collectives of one backward as the backward makes each range final.
+
+    n_lookups: the embedding-lookup passes whose backward must run before the dense ranges are final;
+    gcn_uses: {table ptr: GCN backwards that read it this step}.  ``reduce(rng)`` launches one range's
+    collective and returns a handle with ``.wait()`` (defaults: all-reduce of ``fresh[lo:hi]``, or with
+    ``zero`` a reduce-scatter into the owned part of ``zero.gshard``)."""
+
+    def __init__(self, flat, plan: CommPlan, n_lookups, tables, zero: Zero1 | None = None, reduce=None):
+        self.flat, self.plan, self.zero = flat, plan, zero
+        if reduce is None:
+            if zero is None:
+                reduce = lambda lo, hi: dist.all_reduce(flat.fresh[lo:hi], async_op=True)  # noqa: E731
+            else:
+                def reduce(lo, hi):
+                    _, _, olo, ohi, off = zero.part_of((lo, hi))
+                    return reduce_scatter(zero.gshard[off:off + ohi - olo], flat.fresh[lo:hi])
+        self.reduce = reduce
         self.lookups_left = n_lookups
+        self.table_left = {}
+        for t in tables:
+            k = t.data_ptr()
+            self.table_left[k] = self.table_left.get(k, 0) + 1
+        self.done = [False] * len(plan.ranges)
         self.works = []
         self.issued = []  # (lo, hi) in issue order (tests)
 
     def _issue(self, lo, hi):
-        if hi > lo:
-            self.works.append(self.allreduce(self.flat.fresh[lo:hi]))
+        i = self.plan.index[(lo, hi)]
+        if not self.done[i]:
+            self.done[i] = True
+            self.works.append(self.reduce(lo, hi))
             self.issued.append((lo, hi))
 
     def lookup_done(self):
         """One embedding-lookup backward finished (EmbedFn.backward / PosDropFn.backward)."""
         self.lookups_left -= 1
         if self.lookups_left == 0:
-            for lo, hi in self.dense:
+            for lo, hi in self.plan.dense:
+                self._issue(lo, hi)
+
+    def row_cuts(self, table):
+        """Row chunks [(r0, r1)] for the GCN backward about to write ``table``'s gradient if it is that
+        table's last one this step (its collectives then go per chunk), else None."""
+        k = table.data_ptr()
+        if self.table_left.get(k) != 1:
+            return None
+        return [(r0, r1) for r0, r1, _, _ in self.plan.table_chunks[k]]
+
+    def table_rows_done(self, table, r0, r1):
+        """Rows r0..r1 of ``table``'s gradient are final (a chunk of its last GCN backward)."""
+        for a, b, lo, hi in self.plan.table_chunks[table.data_ptr()]:
+            if r0 <= a and b <= r1:
                 self._issue(lo, hi)
 
     def table_done(self, table):
@@ -82,26 +213,14 @@ class GradBuckets:
             return
         self.table_left[k] -= 1
         if self.table_left[k] == 0:
-            self._issue(*self.table_range[k])
+            for _, _, lo, hi in self.plan.table_chunks[k]:
+                self._issue(lo, hi)
 
     def finish(self):
-        """Issue whatever was not triggered (e.g. a backward that skipped a pass), then make the
-        current stream wait for every collective."""
-        if self.lookups_left > 0:
-            self.lookups_left = 1
-            self.lookup_done()
-        for k, left in self.table_left.items():
-            if left > 0:
-                self.table_left[k] = 0
-                self._issue(*self.table_range[k])
-        covered = sorted(self.issued)
-        pos = 0
-        for lo, hi in covered:  # every element reduced exactly once
-            if lo != pos:
-                raise RuntimeError(f'gradient bucket gap at {pos}..{lo}')
-            pos = (hi + 3) // 4 * 4
-        if pos < self.flat.numel:
-            raise RuntimeError('gradient buckets do not cover the flat store')
+        """Issue whatever was not triggered (e.g. a backward that skipped a pass), then make the current
+        stream wait for every collective."""
+        for lo, hi in self.plan.ranges:
+            self._issue(lo, hi)
         for w in self.works:
             w.wait()
         self.works = []
@@ -117,3 +236,14 @@ def notify_table(state, table):
     h = getattr(state, 'grad_hook', None)
     if h is not None:
         h.table_done(table)
+
+
+def row_cuts(state, table):
+    h = getattr(state, 'grad_hook', None)
+    return None if h is None else h.row_cuts(table)
+
+
+def notify_rows(state, table, r0, r1):
+    h = getattr(state, 'grad_hook', None)
+    if h is not None:
+        h.table_rows_done(table, r0, r1)

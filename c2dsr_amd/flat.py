@@ -13,7 +13,11 @@ import torch
 
 
 class FlatStore:
-    def __init__(self, params: list[tuple[str, torch.nn.Parameter]], device):
+    """``align``: every slice starts at a multiple of ``align`` floats (4 = 16 B; data parallel uses 4·world
+    so the reduction ranges of c2dsr_amd/dp.py split into equal float4-aligned parts per rank)."""
+
+    def __init__(self, params: list[tuple[str, torch.nn.Parameter]], device, align: int = 4):
+        self.align = align
         seen = {}
         entries = []
         off = 0
@@ -23,7 +27,7 @@ class FlatStore:
             seen[id(p)] = name
             n = p.numel()
             entries.append((name, p, off, n))
-            off += (n + 3) // 4 * 4
+            off += self.padded(n)
         self.numel = off
         self.device = device
         self.param = torch.zeros(off, device=device, dtype=torch.float32)
@@ -35,6 +39,9 @@ class FlatStore:
             self.param[o:o + n].copy_(p.detach().reshape(-1).to(device))
             p.data = self.param[o:o + n].view(p.shape)
             p.grad = self.fresh[o:o + n].view(p.shape)
+
+    def padded(self, n: int) -> int:
+        return (n + self.align - 1) // self.align * self.align
 
     def params(self):
         return [p for _, p, _, _ in self.entries]

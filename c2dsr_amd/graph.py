@@ -155,6 +155,14 @@ class DeviceGraph:
         self.work_t, self.split_t, self.n_work_t, self.n_split_t, self.n_slots_t = (to(wt), to(st), len(wt), len(st),
                                                                                     nslot_t)
         self.host = g
+        self._row_keys = {False: (w[:, 0], s[:, 0]), True: (wt[:, 0], st[:, 0])}  # host copies, sorted by row
+
+    def row_slice(self, transposed: bool, r0: int, r1: int):
+        """(w0, w1, s0, s1): the work items and split combines of output rows r0..r1."""
+        wr, sr = self._row_keys[transposed]
+        w0, w1 = np.searchsorted(wr, [r0, r1])
+        s0, s1 = np.searchsorted(sr, [r0, r1])
+        return int(w0), int(w1), int(s0), int(s1)
 
     def plan(self, transposed: bool):
         if transposed:

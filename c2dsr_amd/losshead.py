@@ -50,9 +50,23 @@ def split_count(rows, tile, max_split=16, per_cu=1):
 class LossMeta:
     def __init__(self, *, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, n_a, n_b, R, lam, Wa, ba, Wb, bb, wpad,
                  bpad, Da_w, Da_b, Db_w, Db_b, precision=FP32, B_global=None, allreduce=None, ce_pre=None,
-                 row_sets=None):
+                 row_sets=None, counts=None, reduce_async=None):
+        """counts: (cnt [8] fp32, handle) — valid-target counts all-reduced ahead of the forward (data
+        parallel); reduce_async(t) starts an all-reduce of t and returns its handle."""
         self.__dict__.update(locals())
         del self.__dict__['self']
+        self.pending = None
+
+    def finish_values(self):
+        """Data parallel: wait for the loss values' sums and recompute (loss, loss_rec, loss_mi) from them
+        (the backward already ran on the gradient weights, which depend on the counts only)."""
+        if self.pending is None:
+            return
+        work, vec, cnt, BR_global, out3 = self.pending
+        self.pending = None
+        work.wait()
+        scratch = torch.empty(4, device=vec.device, dtype=torch.float32)
+        lib('c2dsr_loss_finalize', vec, cnt, BR_global, float(self.lam), out3, scratch[:2], scratch[2:], stream())
 
 
 class LossHeadFn(Function):
@@ -197,9 +211,17 @@ class LossHeadFn(Function):
         coefB = torch.empty(2, **f32)
         (_, _, tA, _, _, rA, _, _, _), (_, _, tB, _, _, rB, _, _, _) = heads
         lib('c2dsr_loss_partials', rA, tA, m.n_a, rB, tB, m.n_b, BR, vec, s)
-        if m.allreduce is not None:  # data parallel: global counts / sums (exact normalisation)
+        cnt = None
+        if m.counts is not None:
+            # data parallel: the global valid-target counts (the only global values the gradient needs)
+            # were all-reduced ahead of the forward (Trainer.prepare); the loss values' sums are reduced
+            # asynchronously and finalized after the backward (LossMeta.finish_values)
+            cnt, work = m.counts
+            work.wait()
+            m.pending = (m.reduce_async(vec), vec, cnt, Bg * R, out3)
+        elif m.allreduce is not None:  # data parallel without pre-reduced counts: reduce everything now
             m.allreduce(vec)
-        lib('c2dsr_loss_finalize', vec, Bg * R, float(m.lam), out3, coefA, coefB, s)
+        lib('c2dsr_loss_finalize', vec, cnt, Bg * R, float(m.lam), out3, coefA, coefB, s)
         ctx.m, ctx.heads, ctx.coefs = m, heads, (coefA, coefB)
         ctx.mi = (Phx, Phy, X2a, X2b, Ua, Ub, dS)
         ctx.w = (wa, wb)

@@ -63,7 +63,7 @@ class StepState:
         self.step = 0
         self.row_offset = 0   # global batch-row offset of this rank (data parallel)
         self.next_share_pass = DK.PASS_NEG0
-        self.grad_hook = None  # c2dsr_amd.dp.GradBuckets while a data-parallel backward runs
+        self.grad_hook = None  # c2dsr_amd.dp.DPComm while a data-parallel backward runs
         self.plans = {}  # (step, data_ptr, numel, n_keys) -> ops.IndexPlan (sorted on the side stream)
         self.need = {}   # pass_id -> ops.RowSet: rows of the pass the loss reads (set by Trainer.train_batch)
         self.compact_out = False  # encoder outputs of such passes stay [n, d] (the loss reads them through rs.inv)

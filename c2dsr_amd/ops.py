@@ -11,7 +11,7 @@ import torch
 from torch.autograd import Function
 
 from ._lib import HipLibError, lib, stream, require_device
-from .dp import notify_lookup, notify_table
+from .dp import notify_lookup, notify_rows, notify_table, row_cuts
 
 FP32, BF16 = 0, 1
 
@@ -338,13 +338,21 @@ class GradSink:
         return self.G
 
 
-def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, pad_row, gamma, Y, Y2=None):
-    """Y = alpha·P + (beta + [i != pad]·delta)·Z + gamma·Y with P = A·drop(X) (or drop(Aᵀ·X)); see c2dsr_gcn_spmm."""
+def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, pad_row, gamma, Y, Y2=None,
+         rows=None, part=None):
+    """Y = alpha·P + (beta + [i != pad]·delta)·Z + gamma·Y with P = A·drop(X) (or drop(Aᵀ·X)); see c2dsr_gcn_spmm.
+    ``rows`` = (r0, r1): only output rows r0..r1 (the work items / split combines of those rows: the plan
+    is sorted by row and a split row's pieces share its row, so a row range is a contiguous slice of both)."""
     work, n_work, split, n_split, n_slots, col, val = graph.plan(transposed)
     d = X.shape[1]
-    part = torch.empty(max(n_slots, 1), d, device=X.device, dtype=torch.float32)
+    if part is None:
+        part = torch.empty(max(n_slots, 1), d, device=X.device, dtype=torch.float32)
+    if rows is not None:
+        w0, w1, s0, s1 = graph.row_slice(transposed, *rows)
+        work, n_work, split, n_split = work[w0:w1], w1 - w0, split[s0:s1], s1 - s0
     lib('c2dsr_gcn_spmm', work, n_work, split, n_split, part, col, val, d, X, keys[0], keys[1], float(p),
         int(mask_on_output), float(alpha), Z, float(beta), float(delta), int(pad_row), float(gamma), Y, Y2, stream())
+    return part
 
 
 class GCNFn(Function):
@@ -391,7 +399,15 @@ class GCNFn(Function):
                 T = torch.empty_like(E)
                 spmm(g, True, X, ctx.keys[k - 1], ctx.p, 1, alpha, G, inv, 0.0, -1, 0.0, T)
                 X, alpha = T, 1.0
-            spmm(g, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 1.0, ctx.pad_row, 1.0, gE)
+            cuts = row_cuts(ctx.sink.state, E) if direct else None
+            if cuts is None:
+                spmm(g, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 1.0, ctx.pad_row, 1.0, gE)
+            else:  # this table's gradient is final chunk by chunk: its collectives start per chunk (dp.py)
+                part = None
+                for r0, r1 in cuts:
+                    part = spmm(g, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 1.0, ctx.pad_row, 1.0, gE,
+                                rows=(r0, r1), part=part)
+                    notify_rows(ctx.sink.state, E, r0, r1)
         ctx.sink.G = None
         if direct:
             notify_table(ctx.sink.state, E)  # E.grad final: its all-reduce runs under the next GCN backward

@@ -12,21 +12,29 @@ from .flat import FlatStore
 
 
 class FlatAdamW(torch.optim.Optimizer):
-    def __init__(self, flat: FlatStore, lr=1e-3, weight_decay=5e-4, betas=(0.9, 0.999), eps=1e-8, amsgrad=True):
+    """``zero``: a c2dsr_amd.dp.Zero1 — ZeRO-1: the summed gradient of this rank's parts
+    arrives reduce-scattered in ``zero.gshard``; m / v / vmax and the epoch accumulation are kept for the
+    shard only, the kernel runs once per owned part, and the updated parts are all-gathered."""
+
+    def __init__(self, flat: FlatStore, lr=1e-3, weight_decay=5e-4, betas=(0.9, 0.999), eps=1e-8, amsgrad=True,
+                 zero=None):
         if not amsgrad:
             raise ValueError('the C2DSR path uses amsgrad=True (trainer.py:21-22)')
         super().__init__(flat.params(), dict(lr=lr, weight_decay=weight_decay, betas=betas, eps=eps, amsgrad=True))
         self.flat = flat
+        self.zero = zero
         dev = flat.device
-        self.m = torch.zeros(flat.numel, device=dev)
-        self.v = torch.zeros(flat.numel, device=dev)
-        self.vmax = torch.zeros(flat.numel, device=dev)
+        n = flat.numel if zero is None else zero.shard_numel
+        self.m = torch.zeros(n, device=dev)
+        self.v = torch.zeros(n, device=dev)
+        self.vmax = torch.zeros(n, device=dev)
+        self.accum = flat.accum if zero is None else torch.zeros(n, device=dev)
         self.n_steps = 0
         self.accumulate = True  # grads accumulate until zero_grad (Q3)
 
     def zero_grad(self, set_to_none: bool = True):
         """Reference semantics: clears the epoch accumulation (grads would be None)."""
-        self.flat.accum.zero_()
+        self.accum.zero_()
         self.flat.fresh.zero_()
 
     @torch.no_grad()
@@ -35,8 +43,19 @@ class FlatAdamW(torch.optim.Optimizer):
         self.n_steps += 1
         b1, b2 = g['betas']
         f = self.flat
-        lib('c2dsr_adamw', f.param, f.fresh, f.accum if self.accumulate else None, self.m, self.v, self.vmax, f.numel,
-            float(g['lr']), float(g['weight_decay']), float(b1), float(b2), float(g['eps']), self.n_steps, stream())
+        hyper = (float(g['lr']), float(g['weight_decay']), float(b1), float(b2), float(g['eps']), self.n_steps)
+        if self.zero is None:
+            lib('c2dsr_adamw', f.param, f.fresh, self.accum if self.accumulate else None, self.m, self.v, self.vmax,
+                f.numel, *hyper, stream())
+        else:
+            z = self.zero
+            for _, _, olo, ohi, off in z.parts:
+                n, sl = ohi - olo, slice(off, off + ohi - olo)
+                lib('c2dsr_adamw', f.param[olo:ohi], z.gshard[sl], self.accum[sl] if self.accumulate else None,
+                    self.m[sl], self.v[sl], self.vmax[sl], n, *hyper, stream())
+            f.fresh.zero_()  # the next backward accumulates into it
+            for w in z.gather():
+                w.wait()
         from .ops import WEIGHTS
         WEIGHTS.bump()  # the weights' bf16 images are stale now
         return None

@@ -21,7 +21,7 @@ from .dataloader import get_dataloader
 from . import dropout as DK
 from . import ops
 from ._lib import lib, stream
-from .dp import GradBuckets
+from .dp import CommPlan, DPComm, Zero1
 from .graph import make_graph
 from .losshead import LossHeadFn, LossMeta
 from .metrics import RankMetrics
@@ -61,8 +61,16 @@ class Trainer(object):
             graphs = make_graph(args, join(args.path_raw, 'train_new.txt'))
         self.adj_share, self.adj_specific = graphs
         self.model = C2DSR(args, self.adj_share, self.adj_specific).to(args.device)
-        self.model.flatten()
-        self.optimizer = FlatAdamW(self.model.flat, lr=args.lr, weight_decay=args.l2)
+        self.rank, self.world = dp_info()
+        self.model.flatten(align=4 * self.world)
+        self.comm_plan, self.zero = None, None
+        if self.world > 1:
+            m = self.model
+            self.comm_plan = CommPlan(m.flat, [m.embed_i.weight, m.embed_i_a.weight, m.embed_i_b.weight], self.world)
+            # ZeRO-1: args.zero1 or C2DSR_ZERO1=1
+            if getattr(args, 'zero1', False) or os.environ.get('C2DSR_ZERO1', '0') == '1':
+                self.zero = Zero1(m.flat, self.comm_plan, self.rank, self.world)
+        self.optimizer = FlatAdamW(self.model.flat, lr=args.lr, weight_decay=args.l2, zero=self.zero)
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=args.lr_step, gamma=args.lr_gamma)
         self.noter = noter
         self.n_tr = len(self.trainloader.dataset) if self.trainloader is not None else 0
@@ -75,7 +83,6 @@ class Trainer(object):
         self.len_rec = args.len_rec
         self.compact_rows = os.environ.get('C2DSR_ROW_COMPACT', '1') == '1'
         self.lambda_loss = args.lambda_loss
-        self.rank, self.world = dp_info()
         self.dp_split = True  # slice each global batch across data-parallel ranks
 
     # ------------------------------------------------------------------ training
@@ -165,6 +172,17 @@ class Trainer(object):
                 lib('c2dsr_compact_valid', tcat, M2, B * R, n_items, idx_c, inv_c, tc, cnt, ws, s)
                 ce.append((tcat, idx_c, inv_c, tc))
                 counts.append(cnt)
+        if self.world > 1:
+            # the global valid-target counts — all the gradient's normalisation needs (trainer.py:143-156,
+            # SURVEY.md §8(e)) — reduced ahead of the forward, overlapped with it
+            tg = [c[0] for c in ce] if ce is not None else []
+            for ts, tx in ((gt_share_a, gt_a), (gt_share_b, gt_b))[len(tg):]:
+                t = torch.empty(2 * B * R, device=dev, dtype=torch.int64)
+                lib('c2dsr_rec_targets', ts, tx, B, L, R, t, s)
+                tg.append(t)
+            cvec = torch.empty(9, device=dev, dtype=torch.float32)
+            lib('c2dsr_loss_partials', None, tg[0], self.n_item_a, None, tg[1], self.n_item_b, B * R, cvec, s)
+            self.dp_counts = (cvec, dist.all_reduce(cvec, async_op=True))
         if not counts:
             return {}, None
         hc = ops.HostCounts(torch.cat(counts))
@@ -187,6 +205,7 @@ class Trainer(object):
          neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
         m = self.model
         m.state.row_offset = row_offset
+        self.dp_counts = None
         need, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b)
         m.state.need, m.state.compact_out = need, bool(need)
         try:
@@ -197,20 +216,24 @@ class Trainer(object):
             m.state.need, m.state.compact_out = {}, False
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
         meta.ce_pre = ce_pre
+        if self.dp_counts is not None:
+            meta.counts = self.dp_counts
+            meta.reduce_async = lambda t: dist.all_reduce(t, async_op=True)  # noqa: E731
         if need:  # the five encoder outputs hold only these rows
             meta.row_sets = tuple(need[pid] for pid, _ in self.PASS_ROWS)
         loss, loss_rec, loss_mi = LossHeadFn.apply(h_share, hx, hy, h_neg_a, h_neg_b, meta)
         if self.world > 1:
-            # bucketed all-reduce of the fresh gradient, each bucket issued as soon as the backward
-            # has made it final (c2dsr_amd/dp.py): dense params under the GCN backwards, each item
-            # table under the next table's GCN backward
+            # the fresh gradient's collectives, each range issued as soon as the backward has made it final
+            # (c2dsr_amd/dp.py): dense params under the GCN backwards, each item table per row chunk of its
+            # last GCN backward; all-reduce, or reduce-scatter with ZeRO-1
             tables = [m.embed_i.weight, m.embed_i_a.weight, m.embed_i_b.weight]
-            m.state.grad_hook = GradBuckets(m.flat, tables, n_lookups=5)
+            m.state.grad_hook = DPComm(m.flat, self.comm_plan, 5, tables, zero=self.zero)
             try:
                 loss.backward()
             finally:
                 hook, m.state.grad_hook = m.state.grad_hook, None
             hook.finish()
+            meta.finish_values()
         else:
             loss.backward()
         self.optimizer.step()

@@ -154,12 +154,14 @@ int c2dsr_ce_fwd(const float* logits, long ld, int M, int ncol, const int64_t* t
 int c2dsr_ce_bwd(float* logits, long ld, int M, int ncol, const int64_t* tgt, int ignore, const float* lse,
                  const float* coef, int split, const float* gscale, float lam, void* stream);
 int c2dsr_outer_add(const float* a, long sa, const float* v, int M, int d, float* out, long ldo, void* stream);
-/* vec[0..7] = per-head CE sums and valid counts of this rank's rows (all-reduced under DP) */
+/* vec[0..7] = per-head CE sums and valid counts of this rank's rows (all-reduced under DP); rowsA/rowsB
+ * may be NULL (counts only: data parallel reduces the counts ahead of the forward) */
 int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, const float* rowsB, const int64_t* tB, int n_b,
                         int BR, float* vec, void* stream);
-/* out3 = (loss, loss_rec, loss_mi) from vec[0..8]; coefA/B = per-row grad weights */
-int c2dsr_loss_finalize(const float* vec, int BR_global, float lam, float* out3, float* coefA, float* coefB,
-                        void* stream);
+/* out3 = (loss, loss_rec, loss_mi) from vec[0..8]; coefA/B = per-row grad weights; cnt (nullable) supplies
+ * the valid counts cnt[4..7] instead of vec[4..7] */
+int c2dsr_loss_finalize(const float* vec, const float* cnt, int BR_global, float lam, float* out3, float* coefA,
+                        float* coefB, void* stream);
 int c2dsr_scale_ds(float* ds, int n, const float* gscale, float f, void* stream);
 int c2dsr_rowscale(const float* x, const float* s, long n, int d, float* out, int accumulate, void* stream);
 

@@ -71,19 +71,19 @@ def test_dp_world2_equals_single_device(tmp_path, cfg_name, p):
     np.testing.assert_allclose(loss, [float(out['loss']), float(out['loss_rec']), float(out['loss_mi'])], rtol=1e-5)
 
 
-# ----------------------------------------------------------------------------- bucketed all-reduce (dp.py)
-def _toy_store(shared):
+# ----------------------------------------------------------------------------- gradient exchange (dp.py)
+def _toy_store(shared, world=2, N=37, d=8):
     from c2dsr_amd.flat import FlatStore
     torch.manual_seed(0)
-    e = torch.nn.Parameter(torch.randn(7, 5))
-    ea = e if shared else torch.nn.Parameter(torch.randn(7, 5))
-    eb = e if shared else torch.nn.Parameter(torch.randn(7, 5))
-    pos = torch.nn.Parameter(torch.randn(3, 5))
-    w = torch.nn.Parameter(torch.randn(6, 5))
+    e = torch.nn.Parameter(torch.randn(N, d))
+    ea = e if shared else torch.nn.Parameter(torch.randn(N, d))
+    eb = e if shared else torch.nn.Parameter(torch.randn(N, d))
+    pos = torch.nn.Parameter(torch.randn(3, d))
+    w = torch.nn.Parameter(torch.randn(6, d))
     b = torch.nn.Parameter(torch.randn(6))
-    named = [('embed_i.weight', e), ('embed_i_a.weight', ea), ('embed_i_b.weight', eb), ('pos', pos), ('w', w),
+    named = [('pos', pos), ('embed_i.weight', e), ('embed_i_a.weight', ea), ('w', w), ('embed_i_b.weight', eb),
              ('b', b)]
-    return FlatStore(named, torch.device('cpu')), (e, ea, eb)
+    return FlatStore(named, torch.device('cpu'), align=4 * world), (e, ea, eb)
 
 
 class _Done:
@@ -91,52 +91,133 @@ class _Done:
         pass
 
 
+@pytest.mark.parametrize('world', [1, 2, 3, 4, 8])
 @pytest.mark.parametrize('shared', [False, True])
-def test_grad_buckets_cover_once(shared):
-    from c2dsr_amd.dp import GradBuckets
-    flat, tables = _toy_store(shared)
-    seen = []
-    gb = GradBuckets(flat, list(tables), n_lookups=5, allreduce=lambda t: seen.append(t) or _Done())
-    for _ in range(4):
-        gb.lookup_done()
-    assert gb.issued == []
-    gb.lookup_done()  # dense bucket final after the 5th lookup backward
-    t_end = max(hi for _, hi in gb.table_range.values())
-    assert len(gb.issued) >= 1 and all(lo >= t_end for lo, _ in gb.issued)
-    for t in reversed(tables):  # GCN backwards run b, a, share
-        gb.table_done(t)
-    gb.finish()
+def test_comm_plan_tiles_flat_store(world, shared):
+    from c2dsr_amd.dp import CommPlan, Zero1
+    flat, tables = _toy_store(shared, world)
+    plan = CommPlan(flat, list(tables), world)
     mark = torch.zeros(flat.numel, dtype=torch.int32)
-    for lo, hi in gb.issued:
+    for lo, hi in plan.ranges:
+        assert (hi - lo) % (4 * world) == 0 and lo % 4 == 0
         mark[lo:hi] += 1
-    for _, p, o, n in flat.entries:
-        assert bool((mark[o:o + n] == 1).all())
+    assert bool((mark == 1).all())
+    for ch in plan.table_chunks.values():  # row chunks are consecutive and cover the table
+        assert ch[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ch, ch[1:]))
+    own = torch.zeros(flat.numel, dtype=torch.int32)
+    for r in range(world):  # the ranks' ZeRO-1 parts partition every range
+        z = Zero1(flat, plan, r, world, gather=lambda o, i: _Done())
+        for lo, hi, olo, ohi, off in z.parts:
+            assert lo <= olo < ohi <= hi and (ohi - olo) * world == hi - lo
+            own[olo:ohi] += 1
+        assert z.shard_numel * world == flat.numel
+    assert bool((own == 1).all())
+
+
+@pytest.mark.parametrize('shared', [False, True])
+def test_dpcomm_issue_points(shared):
+    """Dense ranges after the last lookup backward; a table's chunks as its last GCN backward writes
+    them (earlier GCN backwards of a shared table issue nothing); finish() covers the rest once."""
+    from c2dsr_amd.dp import CommPlan, DPComm
+    flat, tables = _toy_store(shared)
+    plan = CommPlan(flat, list(tables), 2)
+    seen = []
+    dc = DPComm(flat, plan, 5, list(tables), reduce=lambda lo, hi: seen.append((lo, hi)) or _Done())
+    for _ in range(4):
+        dc.lookup_done()
+    assert dc.issued == []
+    dc.lookup_done()
+    assert dc.issued == plan.dense
+    for k, t in enumerate(reversed(tables)):  # GCN backwards run b, a, share
+        cuts = dc.row_cuts(t)
+        last = not shared or k == 2
+        assert (cuts is not None) == last
+        n0 = len(dc.issued)
+        if cuts:
+            for r0, r1 in cuts:
+                dc.table_rows_done(t, r0, r1)
+                assert len(dc.issued) > n0
+                n0 = len(dc.issued)
+        dc.table_done(t)
+    dc.finish()
+    assert sorted(dc.issued) == sorted(plan.ranges) and len(seen) == len(plan.ranges)
+
+
+def _zero_worker(rank, world, port, shared, out_dir):
+    """Two AdamW steps with epoch accumulation: replicated (all-reduce + update of everything) vs ZeRO-1
+    (reduce-scatter per range + update of the owned parts + all-gather).  Gradients are small integers so
+    every summation order is exact: the parameters must be bit-equal on every rank."""
+    from c2dsr_amd.dp import CommPlan, DPComm, Zero1
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    flat, tables = _toy_store(shared, world)
+    plan = CommPlan(flat, list(tables), world)
+    zero = Zero1(flat, plan, rank, world)
+    ref_p = flat.param.clone()
+    ref_acc = torch.zeros(flat.numel)
+    ref_opt, z_opt = O.AdamWAmsgrad(), O.AdamWAmsgrad()
+    z_acc = torch.zeros(zero.shard_numel)
+    g = torch.Generator().manual_seed(100 + rank)
+    for step in range(2):
+        fresh = torch.randint(-8, 9, (flat.numel,), generator=g).float()
+        full = fresh.clone()
+        dist.all_reduce(full)
+        ref_acc += full
+        ref_opt.step({'all': ref_p}, {'all': ref_acc.clone()})
+        flat.fresh.copy_(fresh)
+        dc = DPComm(flat, plan, 1, list(tables), zero=zero)
+        for t in reversed(tables):
+            for r0, r1 in dc.row_cuts(t) or []:
+                dc.table_rows_done(t, r0, r1)
+            dc.table_done(t)
+        dc.lookup_done()
+        dc.finish()
+        for k, (lo, hi, olo, ohi, off) in enumerate(zero.parts):
+            sl = slice(off, off + ohi - olo)
+            assert torch.equal(zero.gshard[sl], full[olo:ohi])
+            z_acc[sl] += zero.gshard[sl]
+            z_opt.step({k: flat.param[olo:ohi]}, {k: z_acc[sl].clone()})
+        for w in zero.gather():
+            w.wait()
+        if not torch.equal(flat.param, ref_p):
+            raise AssertionError(f'rank {rank} step {step}: ZeRO-1 params differ by '
+                                 f'{float((flat.param - ref_p).abs().max())}')
+    if rank == 0:
+        np.save(os.path.join(out_dir, 'ok.npy'), np.array([1]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,shared', [(2, False), (4, False), (4, True)])
+def test_zero1_equals_replicated_allreduce(tmp_path, world, shared):
+    mp.spawn(_zero_worker, args=(world, _free_port(), shared, str(tmp_path)), nprocs=world, join=True)
+    assert (tmp_path / 'ok.npy').exists()
 
 
 def _bucket_worker(rank, world, port, out_dir):
-    from c2dsr_amd.dp import GradBuckets
+    from c2dsr_amd.dp import CommPlan, DPComm
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    flat, tables = _toy_store(False)
+    flat, tables = _toy_store(False, world)
     g = torch.Generator().manual_seed(100 + rank)
     flat.fresh.copy_(torch.randn(flat.numel, generator=g))
     full = flat.fresh.clone()
     dist.all_reduce(full)
-    gb = GradBuckets(flat, list(tables), n_lookups=2)
-    gb.lookup_done()
-    gb.table_done(tables[2])  # a table may become final before the dense bucket
-    gb.lookup_done()
-    gb.table_done(tables[1])
-    gb.table_done(tables[0])
-    gb.finish()
-    err = 0.0
-    for _, p, o, n in flat.entries:
-        err = max(err, float((flat.fresh[o:o + n] - full[o:o + n]).abs().max()))
+    dc = DPComm(flat, CommPlan(flat, list(tables), world), 2, list(tables))
+    dc.lookup_done()
+    dc.table_done(tables[2])  # a table may become final before the dense ranges
+    dc.lookup_done()
+    for r0, r1 in dc.row_cuts(tables[1]):
+        dc.table_rows_done(tables[1], r0, r1)
+    dc.table_done(tables[1])
+    dc.table_done(tables[0])
+    dc.finish()
+    err = float((flat.fresh - full).abs().max())
     if rank == 0:
         np.save(os.path.join(out_dir, 'err.npy'), np.array([err]))
     dist.destroy_process_group()
 
 
-def test_grad_buckets_world2_equal_full_allreduce(tmp_path):
+def test_allreduce_ranges_world2_equal_full_allreduce(tmp_path):
     mp.spawn(_bucket_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert float(np.load(tmp_path / 'err.npy')[0]) == 0.0

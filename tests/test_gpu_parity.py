@@ -394,3 +394,50 @@ def test_dp_world2_bucketed_allreduce_matches_reference(tmp_path, name):
     assert names
     for n in names:
         assert rel(got[f'g/{n}'], m[f's0/grad/{n}']) < TOL, n
+
+
+def _zero_gpu_worker(rank, world, port, name, zero, out_dir):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), C2DSR_ZERO1='1' if zero else '0')
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        gs, gp = golden_graphs(name)
+        tr = build_trainer(make_args(G.CONFIGS[name]), gs, gp, G.init_params(name))
+        assert (tr.zero is not None) == zero
+        tr.model.train()
+        tr.optimizer.zero_grad()
+        m = G.load(f'model_{name}.npz')
+        for s in range(int(m['n_steps'])):
+            tr.model.convolve_graph()
+            tr.train_batch(G.batch(name, int(m[f's{s}/batch_lo']), int(m[f's{s}/batch_n'])))
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, f'p{rank}_{int(zero)}.npz'),
+                 **{n: p.detach().cpu().numpy() for n, p in tr.model.named_parameters()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('name', ['base', 'shared'])
+def test_zero1_world2_equals_replicated_and_reference(tmp_path, name):
+    """ZeRO-1 (reduce-scatter per reduction range, AdamW on the owned halves, all-gather)
+    vs the replicated all-reduce path, two ranks on cuda:0 over all of the golden steps: the parameters
+    are bit-equal (two-term sums are order-free) on both ranks, and match the reference's."""
+    import socket
+    import torch.multiprocessing as mp
+    for zero in (False, True):
+        with socket.socket() as s:
+            s.bind(('127.0.0.1', 0))
+            port = s.getsockname()[1]
+        mp.spawn(_zero_gpu_worker, args=(2, port, name, zero, str(tmp_path)), nprocs=2, join=True)
+    ref = np.load(tmp_path / 'p0_0.npz')
+    m = G.load(f'model_{name}.npz')
+    last = int(m['n_steps']) - 1
+    for f in ('p1_0.npz', 'p0_1.npz', 'p1_1.npz'):
+        got = np.load(tmp_path / f)
+        for n in ref.files:
+            np.testing.assert_array_equal(got[n], ref[n], err_msg=f'{f} {n}')
+    for n in ref.files:
+        k = f's{last}/param/{n}'
+        if k in m.files:
+            assert rel(ref[n], m[k]) < 1e-3, n
