@@ -22,6 +22,23 @@
 
 #include <utility>
 
+// tuning knobs (measured with tools/ce_micro.py; the defaults are the shipped configuration)
+#ifndef CE_FWDU_DS
+#define CE_FWDU_DS 3
+#endif
+#ifndef CE_FWDU_DT
+#define CE_FWDU_DT 3
+#endif
+#ifndef CE_FWDU_KBFAST
+#define CE_FWDU_KBFAST 0
+#endif
+#ifndef CE_DW_DS
+#define CE_DW_DS 3
+#endif
+#ifndef CE_DW_DT
+#define CE_DW_DT 3
+#endif
+
 namespace {
 
 using namespace c2img;
@@ -388,8 +405,17 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
       }(std::make_integer_sequence<int, KS>{});
       // ---- dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r], q = (kb, cb, st)
       bf16x8 tf[DT + 2];
+      // U step q: output k-block U_KB(q), column quarter U_J(q) (16 columns: block U_J >> 1, half U_J & 1);
+      // CE_FWDU_KBFAST cycles the 8 accumulators fastest (no back-to-back MFMAs on one accumulator)
+#if CE_FWDU_KBFAST
+#define U_KB(q) ((q) % KB)
+#define U_J(q) ((q) / KB)
+#else
+#define U_KB(q) ((q) >> 2)
+#define U_J(q) ((q) & 3)
+#endif
       [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((tf[P] = tr_frag_c<TILE, ((P >> 1) & 1) * 32 + 16 * (P & 1), (P >> 2) * 32, 0>(oH)), ...);
+        ((tf[P] = tr_frag_c<TILE, U_J(P) * 16, U_KB(P) * 32, 0>(oH)), ...);
       }(std::make_integer_sequence<int, DT>{});
       __builtin_amdgcn_sched_barrier(0);
       [&]<int... Q>(std::integer_sequence<int, Q...>) {
@@ -398,10 +424,10 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
               constexpr int q = Q;
               if constexpr (q + DT < NQ) {
                 constexpr int q1 = q + DT;
-                tf[q1 % (DT + 2)] = tr_frag_c<TILE, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, 0>(oH);
+                tf[q1 % (DT + 2)] = tr_frag_c<TILE, U_J(q1) * 16, U_KB(q1) * 32, 0>(oH);
               }
-              dacc[q >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[(q >> 1) & 1][q & 1],
-                                                                   dacc[q >> 2], 0, 0, 0);
+              dacc[U_KB(q)] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[U_J(q) >> 1][U_J(q) & 1],
+                                                                     dacc[U_KB(q)], 0, 0, 0);
               if constexpr (q % 4 == 1 && q / 4 < NDMA) dma16_s<q == 1>(nsrc, dvoff[q / 4], ddst[q / 4] + nbuf);
               __builtin_amdgcn_sched_barrier(0);
             }(),
@@ -446,8 +472,8 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
   constexpr int NQ = KB * 4;
-  constexpr int DS = 3;
-  constexpr int DT = 3;
+  constexpr int DS = CE_FWDU_DS;  // LDS fragment prefetch depth, S phase
+  constexpr int DT = CE_FWDU_DT;  // LDS fragment prefetch depth, U phase
   constexpr int EPK = 16 / KS;
   constexpr int MPK = 32 / NQ;                       // max-prep elements per U step
   constexpr int IMG = TILE * D * 2;
@@ -626,8 +652,17 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
       bias4(bs, b4n);
       float tm = -INFINITY;
       bf16x8 tf[DT + 2];
+      // U step q: output k-block U_KB(q), column quarter U_J(q) (16 columns: block U_J >> 1, half U_J & 1);
+      // CE_FWDU_KBFAST cycles the 8 accumulators fastest (no back-to-back MFMAs on one accumulator)
+#if CE_FWDU_KBFAST
+#define U_KB(q) ((q) % KB)
+#define U_J(q) ((q) / KB)
+#else
+#define U_KB(q) ((q) >> 2)
+#define U_J(q) ((q) & 3)
+#endif
       [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((tf[P] = tr_frag_c<TILE, ((P >> 1) & 1) * 32 + 16 * (P & 1), (P >> 2) * 32, 0>(oH)), ...);
+        ((tf[P] = tr_frag_c<TILE, U_J(P) * 16, U_KB(P) * 32, 0>(oH)), ...);
       }(std::make_integer_sequence<int, DT>{});
       __builtin_amdgcn_sched_barrier(0);
       [&]<int... Q>(std::integer_sequence<int, Q...>) {
@@ -636,10 +671,10 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
               constexpr int q = Q;
               if constexpr (q + DT < NQ) {
                 constexpr int q1 = q + DT;
-                tf[q1 % (DT + 2)] = tr_frag_c<TILE, ((q1 >> 1) & 1) * 32 + 16 * (q1 & 1), (q1 >> 2) * 32, 0>(oH);
+                tf[q1 % (DT + 2)] = tr_frag_c<TILE, U_J(q1) * 16, U_KB(q1) * 32, 0>(oH);
               }
-              dacc[q >> 2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[(q >> 1) & 1][q & 1],
-                                                                   dacc[q >> 2], 0, 0, 0);
+              dacc[U_KB(q)] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[U_J(q) >> 1][U_J(q) & 1],
+                                                                     dacc[U_KB(q)], 0, 0, 0);
               if constexpr (q % 4 == 1 && q / 4 < NDMA) dma16_s<q == 1>(nsrc, dvoff[q / 4], ddst[q / 4] + nbuf);
 #pragma unroll
               for (int e = 0; e < MPK; ++e) {
@@ -653,6 +688,8 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
             }(),
             ...);
       }(std::make_integer_sequence<int, NQ>{});
+#undef U_KB
+#undef U_J
       mnext = fmaxf(tm, __shfl_xor(tm, 32, 64));
       sc[0] = sn[0];
       sc[1] = sn[1];
@@ -728,8 +765,8 @@ __global__ __launch_bounds__(256, 1) void ce_dw_kernel(const bf16* __restrict__ 
   constexpr int KS = D / 16;
   constexpr int KB = D / 32;
   constexpr int NQ = KB * 4;
-  constexpr int DS = 3;
-  constexpr int DT = 3;
+  constexpr int DS = CE_DW_DS;
+  constexpr int DT = CE_DW_DT;
   constexpr int IMG = TILE * D * 2;
   constexpr int NDMA = (TILE / 4) * (D / 128) / 4;
   constexpr int NB = 4;  // H images: S(t+1), dW(t), tile t+2 landed, t+3 landing

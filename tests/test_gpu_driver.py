@@ -96,14 +96,20 @@ def _check(name, tr, out):
             np.testing.assert_array_equal(np.asarray(got[k]), ref[f'e{e}/{k}'], err_msg=f'epoch {e} {k}')
         np.testing.assert_allclose(got['val_score'], ref[f'e{e}/val_score'], rtol=1e-9)
         np.testing.assert_allclose(got['test_score'], ref[f'e{e}/test_score'], rtol=1e-9)
-    # final parameters after n_epoch·⌈n_train/B⌉ AdamW(amsgrad) steps: Adam's normalised update moves an
-    # element by ~lr whatever its gradient's size, so an element whose gradient is at rounding level can
-    # step either way; bound the drift in units of lr and require it to be rare
-    n_steps = len(out) * len(ref['e0/order_seq_share']) // G.BATCH + len(out)
+    # final parameters after n_epoch·⌈n_train/B⌉ AdamW(amsgrad) steps.  Adam's normalised update moves an
+    # element by ~lr whatever its gradient's size, so an element whose gradient is at rounding level steps
+    # either way in the two implementations.  The query and key projections are such a case here: with the
+    # inverted key-padding mask (Q1) every query attends only to PAD keys, which share one embedding and
+    # position, so all of a row's scores are equal and dL/dQ, dL/dK are exactly 0 up to rounding — their
+    # rows (in_proj[:2d]) are held only to the drift bound; every other parameter must agree closely.
+    n_steps = len(out) * (len(ref['e0/order_seq_share']) + G.BATCH - 1) // G.BATCH
+    d_lat = G.CONFIGS[name]['d_latent']
     for n, p in tr.model.named_parameters():
         d = np.abs(p.detach().cpu().numpy().astype(np.float64) - ref[f'final/{n}'])
         assert d.max() <= n_steps * 1e-3, (n, d.max())
-        assert (d > 1e-5).mean() < 0.02, (n, (d > 1e-5).mean())
+        if 'self_attn.in_proj_' in n:
+            d = d[2 * d_lat:]
+        assert (d > 2e-5).mean() < 0.01, (n, (d > 2e-5).mean(), d.max())
     # the device-side metric accumulation (one host sync per pass) gives the same test score
     last = len(out) - 1
     np.testing.assert_allclose(tr.evaluate_metrics(tr.testloader).score(BENCH_FK), ref[f'e{last}/test_score'],
