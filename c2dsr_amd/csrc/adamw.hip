@@ -4,11 +4,14 @@
 // together with the reference's "zero_grad once per epoch" accumulation (trainer.py:42, Q3):
 // the backward of a step writes a fresh gradient buffer F (all-reduced across ranks
 // under data parallelism); this kernel folds it into the epoch accumulator A (g = A + F),
-// clears F for the next step and applies the update — one pass, 48 B/param.
+// clears F for the next step and applies the update — one pass, 48 B/param.  On one device the
+// backward accumulates straight into A (fresh == accum: KEEP), and the pass reads g = A only:
+// 36 B/param.
 #include "common.h"
 
 namespace {
 
+template <bool KEEP>
 __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, float4* __restrict__ fresh,
                                                     float4* __restrict__ accum, float4* __restrict__ m,
                                                     float4* __restrict__ v, float4* __restrict__ vmax, long n4,
@@ -16,11 +19,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, floa
                                                     float step_size, float inv_bc2_sqrt) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 g = fresh[i];
-    if (accum) {
-      g = g + accum[i];
-      accum[i] = g;
+    if constexpr (!KEEP) {
+      if (accum) {
+        g = g + accum[i];
+        accum[i] = g;
+      }
+      fresh[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    fresh[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 pp = p[i], mm = m[i], vv = v[i], vx = vmax[i];
     float* P = (float*)&pp;
     float* G = (float*)&g;
@@ -45,7 +50,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, floa
 
 }  // namespace
 
-// All buffers fp32 [n], n % 4 == 0, 16-byte aligned.  accum may be null (no epoch accumulation).
+// All buffers fp32 [n], n % 4 == 0, 16-byte aligned.  accum may be null (no epoch accumulation);
+// accum == fresh: the gradient buffer is the epoch accumulation itself (read only).
 C2_API int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,
                        float b1, float b2, float eps, int step, void* stream) {
   if (n % 4) return (int)hipErrorInvalidValue;
@@ -57,9 +63,14 @@ C2_API int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v,
   const long n4 = n / 4;
   int blocks = c2::ceil_div(n4, 256);
   if (blocks > 256 * 16) blocks = 256 * 16;
-  adamw_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((float4*)p, (float4*)fresh, (float4*)accum, (float4*)m,
-                                                        (float4*)v, (float4*)vmax, n4, lr, 1.f - lr * wd, b1, b2, eps,
-                                                        step_size, inv_bc2_sqrt);
+  if (accum && accum == fresh)
+    adamw_kernel<true><<<blocks, 256, 0, (hipStream_t)stream>>>((float4*)p, (float4*)fresh, nullptr, (float4*)m,
+                                                                (float4*)v, (float4*)vmax, n4, lr, 1.f - lr * wd, b1,
+                                                                b2, eps, step_size, inv_bc2_sqrt);
+  else
+    adamw_kernel<false><<<blocks, 256, 0, (hipStream_t)stream>>>((float4*)p, (float4*)fresh, (float4*)accum,
+                                                                 (float4*)m, (float4*)v, (float4*)vmax, n4, lr,
+                                                                 1.f - lr * wd, b1, b2, eps, step_size, inv_bc2_sqrt);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -16,8 +16,11 @@ class FlatStore:
     """``align``: every slice starts at a multiple of ``align`` floats (4 = 16 B; data parallel uses 4·world
     so the reduction ranges of c2dsr_amd/dp.py split into equal float4-aligned parts per rank)."""
 
-    def __init__(self, params: list[tuple[str, torch.nn.Parameter]], device, align: int = 4):
+    def __init__(self, params: list[tuple[str, torch.nn.Parameter]], device, align: int = 4, direct: bool = False):
+        """``direct``: no separate per-step buffer — ``fresh`` IS the epoch accumulation ``accum`` (one
+        device: nothing is reduced, the backward accumulates into it and AdamW only reads it)."""
         self.align = align
+        self.direct = direct
         seen = {}
         entries = []
         off = 0
@@ -31,8 +34,8 @@ class FlatStore:
         self.numel = off
         self.device = device
         self.param = torch.zeros(off, device=device, dtype=torch.float32)
-        self.fresh = torch.zeros(off, device=device, dtype=torch.float32)
         self.accum = torch.zeros(off, device=device, dtype=torch.float32)
+        self.fresh = self.accum if direct else torch.zeros(off, device=device, dtype=torch.float32)
         self.entries = entries
         self.names = [e[0] for e in entries]
         for name, p, o, n in entries:
@@ -61,5 +64,7 @@ class FlatStore:
         """Accumulated gradient (epoch accumulator + this step's) of one parameter."""
         for nm, p, o, n in self.entries:
             if nm == name:
+                if self.direct:
+                    return self.accum[o:o + n].view(p.shape)
                 return (self.accum[o:o + n] + self.fresh[o:o + n]).view(p.shape)
         raise KeyError(name)

@@ -119,12 +119,12 @@ class C2DSR(nn.Module):
         """Parameters that receive gradients (the unused encoder_layer template never does, Q15)."""
         return [(n, p) for n, p in self.named_parameters() if '.encoder_layer.' not in n and p.requires_grad]
 
-    def flatten(self, align: int = 4):
+    def flatten(self, align: int = 4, direct: bool = False):
         """Move every trainable parameter (and its .grad) into the flat HBM store (slices aligned to
         ``align`` floats; data parallel passes 4·world, c2dsr_amd/dp.py)."""
         from ..flat import FlatStore
         dev = self.embed_i.weight.device
-        self.flat = FlatStore(self.trainable_named_parameters(), dev, align)
+        self.flat = FlatStore(self.trainable_named_parameters(), dev, align, direct)
         return self.flat
 
     def graphs(self):

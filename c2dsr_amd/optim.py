@@ -45,6 +45,8 @@ class FlatAdamW(torch.optim.Optimizer):
         f = self.flat
         hyper = (float(g['lr']), float(g['weight_decay']), float(b1), float(b2), float(g['eps']), self.n_steps)
         if self.zero is None:
+            # direct store (one device): fresh is accum — read only, 36 B/param; without epoch accumulation
+            # the same buffer is this step's gradient and is cleared
             lib('c2dsr_adamw', f.param, f.fresh, self.accum if self.accumulate else None, self.m, self.v, self.vmax,
                 f.numel, *hyper, stream())
         else:

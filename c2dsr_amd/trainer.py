@@ -62,7 +62,8 @@ class Trainer(object):
         self.adj_share, self.adj_specific = graphs
         self.model = C2DSR(args, self.adj_share, self.adj_specific).to(args.device)
         self.rank, self.world = dp_info()
-        self.model.flatten(align=4 * self.world)
+        # one device: the backward accumulates straight into the epoch accumulation (no per-step buffer)
+        self.model.flatten(align=4 * self.world, direct=self.world == 1)
         self.comm_plan, self.zero = None, None
         if self.world > 1:
             m = self.model

@@ -219,7 +219,8 @@ int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* ou
 int c2dsr_selftest_tr(int rr0, int kb0, short* out, void* stream);
 
 /* K6 AdamW(amsgrad) over flat buffers, folding the fresh grad into the epoch accumulator
- * (trainer.py:21-22,42,158). */
+ * (trainer.py:21-22,42,158); accum == fresh: the backward accumulated into the epoch accumulator
+ * directly (one device) and it is only read. */
 int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,
                 float b1, float b2, float eps, int step, void* stream);
 

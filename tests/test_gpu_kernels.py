@@ -281,6 +281,28 @@ def test_adamw_kernel_vs_oracle():
         assert rel(accum, acc_ref) < 1e-7
 
 
+def test_adamw_direct_accumulation_vs_oracle():
+    """One device: the backward accumulates into the epoch accumulator itself (fresh == accum, FlatStore
+    direct); the kernel only reads it (36 B/param) and the update equals the oracle's."""
+    from c2dsr_amd._lib import lib, stream
+    from oracle.c2dsr_oracle import AdamWAmsgrad
+    n = 10_000
+    p = torch.randn(n)
+    opt = AdamWAmsgrad(lr=1e-3, wd=5e-4)
+    P = {'w': p.clone()}
+    pd = p.clone().to(DEV)
+    acc, m, v, vmax = (torch.zeros(n, device=DEV) for _ in range(4))
+    acc_ref = torch.zeros(n)
+    for step in range(1, 4):
+        g = torch.randn(n)
+        acc_ref += g
+        acc += g.to(DEV)
+        lib('c2dsr_adamw', pd, acc, acc, m, v, vmax, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, step, stream())
+        opt.step(P, {'w': acc_ref.clone()})
+        assert rel(pd, P['w']) < 1e-6
+        assert rel(acc, acc_ref) < 1e-6  # read only
+
+
 def test_transposed_lds_fragment_addressing():
     """ds_read_b64_tr_b16 + swizzled image: the fragment layout the fused CE kernels rely on."""
     from c2dsr_amd._lib import lib, stream
