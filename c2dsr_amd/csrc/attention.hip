@@ -13,6 +13,8 @@
 // modes bit-identical here while staying far off the critical path.
 #include "common.h"
 
+typedef __bf16 bf16;
+
 #include <cstdlib>
 
 namespace {
@@ -739,12 +741,14 @@ __device__ __forceinline__ void zero16(f32x16& a) {
 
 // acc (+)= A·B over one 32-key (or 32-query) tile: A from registers / LDS (per step r), B one float per
 // lane per step from a buffer descriptor at rows rowof(r) (relative), column c.
-template <int TJ, int TI>
+// OT: element type of dqkv (float, or bf16 when its only consumers — the in_proj backward GEMMs — read
+// it as a bf16 MFMA operand anyway: c2dsr_attn_bwd_b16)
+template <int TJ, int TI, typename OT>
 __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const float* __restrict__ K,
                                               const float* __restrict__ V, const float* __restrict__ dO,
                                               long rs, long ds, int L, int dh, int jmax, uint64_t kb,
                                               const c2::Drop& drop, uint64_t pbase, const float* __restrict__ prow0,
-                                              float* __restrict__ dQ, float* __restrict__ dK, float* __restrict__ dV,
+                                              OT* __restrict__ dQ, OT* __restrict__ dK, OT* __restrict__ dV,
                                               float* T) {
   const int lane = threadIdx.x & 63, r = lane & 31, hi = lane >> 5;
   // ---- dPᵀ tiles (tj, ti): 0 = (0,0), 1 = (0,1), 2 = (1,1)
@@ -853,8 +857,8 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i0 = creg(q, lane), i1 = 32 + i0;
-        if (i0 < L) dQ[(long)i0 * rs + c] = sc * o0[q];
-        if (TI > 1 && i1 < L) dQ[(long)i1 * rs + c] = sc * o1[q];
+        if (i0 < L) dQ[(long)i0 * rs + c] = (OT)(sc * o0[q]);
+        if (TI > 1 && i1 < L) dQ[(long)i1 * rs + c] = (OT)(sc * o1[q]);
       }
     }
   }
@@ -869,7 +873,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
       if (two) T[i * TLD + 32 + j0] = b[q];
     }
   };
-  auto keys_out = [&](const float* __restrict__ Src, long ss, int nrows, float scale, float* __restrict__ Dst) {
+  auto keys_out = [&](const float* __restrict__ Src, long ss, int nrows, float scale, OT* __restrict__ Dst) {
     const auto src = rows_rsrc(Src, nrows, ss, dh);
 #pragma unroll 1
     for (int ct = 0; ct < CT; ++ct) {
@@ -899,10 +903,10 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int j = 32 * tj + creg(q, lane);
-          if (j < L) Dst[(long)j * rs + c] = scale * o[q];
+          if (j < L) Dst[(long)j * rs + c] = (OT)(scale * o[q]);
         }
       }
-      for (int j = 32 * TJ + hi; j < L; j += 2) Dst[(long)j * rs + c] = 0.f;  // keys past the tiles
+      for (int j = 32 * TJ + hi; j < L; j += 2) Dst[(long)j * rs + c] = (OT)0.f;  // keys past the tiles
     }
   };
   // T starts as garbage: every entry the products read ([0, 32·TI) x [0, 32·TJ)) is written first
@@ -921,10 +925,11 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
   keys_out(Q, rs, L, sc, dK);
 }
 
+template <typename OT>
 __global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ qkv, const int64_t* __restrict__ seq,
                                                      int64_t pad, int B, int L, int d, int H, c2::Drop drop,
                                                      int64_t b_base, const float* __restrict__ Psave,
-                                                     const float* __restrict__ dout, float* __restrict__ dqkv) {
+                                                     const float* __restrict__ dout, OT* __restrict__ dqkv) {
   __shared__ float tbuf[4][64 * 65];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int bh = blockIdx.x * 4 + w;
@@ -936,16 +941,16 @@ __global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ q
   const long rs = 3l * d;
   const float* Q = qkv + (long)b * L * rs + h * dh;
   const float* dO = dout + (long)b * L * d + h * dh;
-  float* dQ = dqkv + (long)b * L * rs + h * dh;
+  OT* dQ = dqkv + (long)b * L * rs + h * dh;
   const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
   const float* prow = Psave + (long)bh * WAVE_PSAVE;
   const int TJ = jmax > 32 ? 2 : 1, TI = L > 32 ? 2 : 1;
   if (TI == 1)
-    bwd_wave_body<1, 1>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+    bwd_wave_body<1, 1, OT>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
   else if (TJ == 1)
-    bwd_wave_body<1, 2>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+    bwd_wave_body<1, 2, OT>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
   else
-    bwd_wave_body<2, 2>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+    bwd_wave_body<2, 2, OT>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
 }
 
 template <int LP>
@@ -1026,8 +1031,8 @@ C2_API int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int
   dim3 grid(B * H);
   const bool fast = (d / H) % 4 == 0 && d % 4 == 0;
   if (wave_path(L, d, H))
-    attn_bwd_wave<<<c2::ceil_div((long)B * H, 4), 256, 0, s>>>(qkv, seq, pad, B, L, d, H, dr, b_base, Psave, dout,
-                                                               dqkv);
+    attn_bwd_wave<float><<<c2::ceil_div((long)B * H, 4), 256, 0, s>>>(qkv, seq, pad, B, L, d, H, dr, b_base, Psave,
+                                                                      dout, dqkv);
   else if (fast && L <= 32)
     attn_bwd_fast<32><<<grid, 256, 0, s>>>(qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
   else if (fast && L <= 64)
@@ -1038,6 +1043,23 @@ C2_API int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int
     launch_bwd<64>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
   else
     launch_bwd<128>(grid, s, qkv, seq, pad, L, d, H, dr, b_base, Psave, dout, dqkv);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// 1 when c2dsr_attn_bwd_b16 takes the shape (the wave kernels: L <= 64, d/H a multiple of 32)
+C2_API int c2dsr_attn_bwd_b16_supported(int L, int d, int H) { return H > 0 && d % H == 0 && wave_path(L, d, H); }
+
+// c2dsr_attn_bwd with dqkv written in bf16 (its consumers, the in_proj backward GEMMs c2dsr_rgemm_aux_b16a /
+// c2dsr_wgemm_b16y, use it as a bf16 MFMA operand: the same values they would round it to)
+C2_API int c2dsr_attn_bwd_b16(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H,
+                              uint32_t k0, uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout,
+                              void* dqkv, void* stream) {
+  if (!c2dsr_attn_bwd_b16_supported(L, d, H)) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  attn_bwd_wave<bf16><<<c2::ceil_div((long)B * H, 4), 256, 0, (hipStream_t)stream>>>(
+      qkv, seq, pad, B, L, d, H, dr, b_base, Psave, dout, (bf16*)dqkv);
   C2_CHECK_LAUNCH();
   return 0;
 }

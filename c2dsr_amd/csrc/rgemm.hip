@@ -70,8 +70,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_bytes(const void* base, l
 // repeated to fill a pair) so the compiler's wait counts stay exact and the prefetch lives.
 // Block b runs on XCD b % 8; the G column groups of an XCD walk the same rows in the same
 // order, so the G passes over A share its L2.
-template <int KCH, int CT, bool EPI, int AUX = AUX_NONE>
-__global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const float* __restrict__ A, long lda,
+// AB16: A is bf16 in HBM (the attention backward's dqkv, c2dsr_rgemm_aux_b16a): the same [32][256] chunk
+// lands as 8-byte loads and is staged without conversion — half the bytes of the fp32 stream, identical
+// products (the fp32 path rounds A to bf16 the same way, RNE).
+template <int KCH, int CT, bool EPI, int AUX = AUX_NONE, bool AB16 = false>
+__global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void* __restrict__ A, long lda,
                                                  const bf16* __restrict__ B, long ldb, float* C,
                                                  long ldc, Epi2 ep, int G) {
   __shared__ __attribute__((aligned(16))) char aimg[2][32 * 256 * 2];
@@ -104,7 +107,8 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
     pin(bcol[ct]);
   }
   vm_drain();
-  const auto asrc = rsrc_bytes(A, (long)M * lda * 4);  // rows >= M read 0
+  constexpr int AEB = AB16 ? 2 : 4;  // bytes per A element
+  const auto asrc = rsrc_bytes(A, (long)M * lda * AEB);  // rows >= M read 0
   const auto csrc = rsrc_bytes(C, (long)M * ldc * 4);  // stores to rows >= M are dropped
   const auto xsrc = rsrc_bytes(AUX != AUX_NONE ? ep.aux : C, (long)M * ldc * 4);  // rows >= M read 0
   // aux values of this wave's outputs for the current tile, loaded one tile ahead
@@ -143,20 +147,31 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const floa
   aux_load(0);
   // chunk c = (tile c / KCH (clamped to the last), k-chunk c % KCH); thread t loads float4
   // t + 256u, u < 8: row (t >> 6) + 4u, columns 4·lane .. +3
-  const int ldab = (int)lda * 4;
+  const int ldab = (int)lda * AEB;
   const int lrow = threadIdx.x >> 6;
+  // AB16: P[u].xy carry the 4 bf16 values (8 bytes) of the same row / columns
 #define RG_LOAD(c, P)                                                                                          \
   {                                                                                                            \
     const int tile_ = min((c) / KCH, ntile - 1), kc_ = (c) % KCH;                                              \
-    const int vo_ = ((rt0 + tile_ * rts) * 32 + lrow) * ldab + (kc_ * 256 + 4 * lane) * 4;                     \
-    _Pragma("unroll") for (int u = 0; u < 8; ++u) P[u] =                                                       \
-        __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc, vo_ + u * 4 * ldab, 0, 0));     \
+    const int vo_ = ((rt0 + tile_ * rts) * 32 + lrow) * ldab + (kc_ * 256 + 4 * lane) * AEB;                   \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                            \
+      if constexpr (AB16) {                                                                                    \
+        const auto h_ = __builtin_amdgcn_raw_buffer_load_b64(asrc, vo_ + u * 4 * ldab, 0, 0);                  \
+        P[u] = make_float4(__builtin_bit_cast(float, h_[0]), __builtin_bit_cast(float, h_[1]), 0.f, 0.f);      \
+      } else {                                                                                                 \
+        P[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc, vo_ + u * 4 * ldab, 0, 0)); \
+      }                                                                                                        \
+    }                                                                                                          \
   }
 #define RG_STAGE(P, im)                                                                                        \
   {                                                                                                            \
     _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                            \
       bf16x4 v_;                                                                                               \
-      v_[0] = (bf16)P[u].x; v_[1] = (bf16)P[u].y; v_[2] = (bf16)P[u].z; v_[3] = (bf16)P[u].w;                  \
+      if constexpr (AB16) {                                                                                    \
+        v_ = __builtin_bit_cast(bf16x4, make_float2(P[u].x, P[u].y));                                          \
+      } else {                                                                                                 \
+        v_[0] = (bf16)P[u].x; v_[1] = (bf16)P[u].y; v_[2] = (bf16)P[u].z; v_[3] = (bf16)P[u].w;                \
+      }                                                                                                        \
       *(bf16x4*)((im) + aoff(lrow + 4 * u, 4 * lane)) = v_;                                                   \
     }                                                                                                          \
   }
@@ -265,7 +280,10 @@ __device__ __forceinline__ bf16x8 tr32(const char* img, int rr0, int kb0, int la
   return r;
 }
 
-__global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __restrict__ dY, long ldy,
+// YB16: dY is bf16 in HBM (the attention backward's dqkv): 8-byte loads, no conversion; the bias
+// column sums add the same bf16 values.
+template <bool YB16>
+__global__ __launch_bounds__(256) void wg_kernel(int T, int N, const void* __restrict__ dY, long ldy,
                                                  const float* __restrict__ X, long ldx, float* __restrict__ part,
                                                  float* __restrict__ part_b, int NTL, int rows_per_split) {
   __shared__ __attribute__((aligned(16))) float4 red_b[8][32];
@@ -282,10 +300,11 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __re
   const int nchunk = t_end > t_beg ? (t_end - t_beg + 31) >> 5 : 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n_base = nt * 128;
-  const auto ysrc = rsrc_bytes(dY, (long)t_end * ldy * 4);  // rows past the split's end read 0
+  constexpr int YEB = YB16 ? 2 : 4;
+  const auto ysrc = rsrc_bytes(dY, (long)t_end * ldy * YEB);  // rows past the split's end read 0
   const auto xsrc = rsrc_bytes(X, (long)t_end * ldx * 4);
   const int lrow = threadIdx.x >> 6;  // 0..3
-  const int ldyb = (int)ldy * 4, ldxb = (int)ldx * 4;
+  const int ldyb = (int)ldy * YEB, ldxb = (int)ldx * 4;
   // chunk c: thread t loads dY rows lrow + 4u (u < 8) → 1 float4 (cols 4·(lane&31) of the 128) per
   // half-wave pair... simpler: dY chunk 32×128 floats = 1024 float4 = 4 per thread, X 2048 = 8 per thread
 #define WG_LOAD(c, PY, PX)                                                                                    \
@@ -293,8 +312,14 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const float* __re
     const int t0_ = t_beg + min(c, nchunk - 1) * 32;                                                          \
     _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
       const int q_ = threadIdx.x + 256 * u; /* 0..1023: row q_>>5, float4 q_&31 */                           \
-      PY[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(                              \
-                                             ysrc, (t0_ + (q_ >> 5)) * ldyb + (n_base + 4 * (q_ & 31)) * 4, 0, 0)); \
+      const int yo_ = (t0_ + (q_ >> 5)) * ldyb + (n_base + 4 * (q_ & 31)) * YEB;                              \
+      if constexpr (YB16) {                                                                                   \
+        const auto h_ = __builtin_amdgcn_raw_buffer_load_b64(ysrc, yo_, 0, 0);                                \
+        const bf16x4 b_ = __builtin_bit_cast(bf16x4, h_);                                                     \
+        PY[u] = make_float4((float)b_[0], (float)b_[1], (float)b_[2], (float)b_[3]);                          \
+      } else {                                                                                                \
+        PY[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ysrc, yo_, 0, 0));           \
+      }                                                                                                       \
     }                                                                                                         \
     _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                           \
       PX[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(                              \
@@ -461,11 +486,12 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
 // ... with an aux epilogue: aux_mode 1: C = alpha·A·Bᵀ + bias + aux (aux == C: accumulate in
 // place); 2: C = aux > 0 ? (alpha·A·Bᵀ + bias)·aux_scale : 0 (aux [M][ldc]); 3: C = alpha·A·Bᵀ + bias
 // + aux[auxmap[r]] (auxmap [M], entries < 0 add nothing; aux holds the mapped rows only).
-C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
-                           float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
-                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
-                           float aux_scale, void* stream) {
+static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, const void* B, int ldb, float* C,
+                      int ldc, float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1,
+                      float p, int64_t row_base, const int* rowmap, int aux_mode, const float* aux,
+                      const int* auxmap, float aux_scale, void* stream) {
   if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
+  if (ab16 && (K != 768 || epilogue || aux_mode == AUX_MASK)) return (int)hipErrorInvalidValue;
   if (aux_mode < 0 || aux_mode > 3 || (aux_mode && (!aux || epilogue))) return (int)hipErrorInvalidValue;
   if ((aux_mode == AUX_ACC_MAP) != (auxmap != nullptr) || (aux_mode == AUX_ACC_MAP && aux == C))
     return (int)hipErrorInvalidValue;
@@ -482,8 +508,8 @@ C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const v
   const int CT = K == 256 ? 2 : 1;
   const int G = c2::ceil_div(N, 128 * CT);
   // persistent grid: exactly the workgroups that are resident at once (occupancy of the variant)
-  static int per_cu[15] = {0};
-  auto launch = [&](void (*kern)(int, int, int, const float*, long, const bf16*, long, float*, long, Epi2, int),
+  static int per_cu[18] = {0};
+  auto launch = [&](void (*kern)(int, int, int, const void*, long, const bf16*, long, float*, long, Epi2, int),
                     int slot) -> int {
     if (!per_cu[slot]) {
       int n = 0;
@@ -497,7 +523,14 @@ C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const v
   };
   int rc;
   const bool e = epilogue == 1;
-  if (aux_mode == AUX_ACC) {
+  if (ab16) {  // K = 768: the in_proj backward over the attention's bf16 dqkv
+    if (aux_mode == AUX_ACC)
+      rc = launch(rg_kernel<3, 1, false, AUX_ACC, true>, 15);
+    else if (aux_mode == AUX_ACC_MAP)
+      rc = launch(rg_kernel<3, 1, false, AUX_ACC_MAP, true>, 16);
+    else
+      rc = launch(rg_kernel<3, 1, false, AUX_NONE, true>, 17);
+  } else if (aux_mode == AUX_ACC) {
     if (K == 256)
       rc = launch(rg_kernel<1, 2, false, AUX_ACC>, 6);
     else if (K == 512)
@@ -529,6 +562,22 @@ C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const v
   return 0;
 }
 
+C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                           float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
+                           float aux_scale, void* stream) {
+  return rgemm_impl(M, N, K, A, false, lda, B, ldb, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, rowmap,
+                    aux_mode, aux, auxmap, aux_scale, stream);
+}
+
+// the same with A bf16 (K = 768, no epilogue, aux modes 0 / 1 / 3)
+C2_API int c2dsr_rgemm_aux_b16a(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
+                                float alpha, float beta, const float* bias, int aux_mode, const float* aux,
+                                const int* auxmap, void* stream) {
+  return rgemm_impl(M, N, K, A, true, lda, B, ldb, C, ldc, alpha, beta, bias, 0, 0, 0, 0.f, 0, nullptr, aux_mode, aux,
+                    auxmap, 0.f, stream);
+}
+
 // dW[N][256] (+)= Σ_t dY[t][N]ᵀ·X[t][256] (N % 128 == 0) and, when db is given, db[N] (+)= Σ_t dY[t][N]
 // (the bias gradient, from the same dY chunks): split over t into `splits` partial slices
 // part[splits][N][256] + [splits][N] (c2dsr_wgemm_workspace bytes), combined in a fixed order with
@@ -545,8 +594,8 @@ C2_API int c2dsr_wgemm_supported(int T, int N, int D) {
   return T > 0 && D == 256 && N % 128 == 0 && N <= 32 * 128 && (long)T * N * 4 < (1L << 31) && (long)T * D * 4 < (1L << 31);
 }
 C2_API size_t c2dsr_wgemm_workspace(int N) { return (size_t)wg_splits(N) * N * 257 * 4; }
-C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
-                       float* db, void* part, void* stream) {
+static int wgemm_impl(int T, int N, int D, const void* dY, bool yb16, int ldy, const float* X, int ldx, float beta,
+                      float* dW, float* db, void* part, void* stream) {
   if (!c2dsr_wgemm_supported(T, N, D) || ldy % 4 || ldx % 4) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int NTL = N / 128;
@@ -556,12 +605,25 @@ C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const floa
   const int blocks = splits * NTL;  // = 8 XCDs x (splits/8) x NTL
   const long n = (long)N * 256;
   float* part_b = db ? (float*)part + (long)splits * n : nullptr;
-  wg_kernel<<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, part_b, NTL, rows);
+  if (yb16)
+    wg_kernel<true><<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, part_b, NTL, rows);
+  else
+    wg_kernel<false><<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, part_b, NTL, rows);
   const long blocks_a = c2::ceil_div(n / 4 * 8, 256), blocks_b = db ? c2::ceil_div((long)N / 4 * 8, 256) : 0;
   sum_parts_kernel2<<<blocks_a + blocks_b, 256, 0, s>>>((const float*)part, n, dW, part_b, N, db, splits, beta,
                                                         blocks_a);
   C2_CHECK_LAUNCH();
   return 0;
+}
+
+C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
+                       float* db, void* part, void* stream) {
+  return wgemm_impl(T, N, D, dY, false, ldy, X, ldx, beta, dW, db, part, stream);
+}
+// dY bf16
+C2_API int c2dsr_wgemm_b16y(int T, int N, int D, const void* dY, int ldy, const float* X, int ldx, float beta,
+                            float* dW, float* db, void* part, void* stream) {
+  return wgemm_impl(T, N, D, dY, true, ldy, X, ldx, beta, dW, db, part, stream);
 }
 
 // y = bf16(x) for x fp32 [R][Cc] (row stride ldx); trans: y is [Cc][R]

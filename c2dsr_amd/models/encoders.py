@@ -115,8 +115,8 @@ class SelfAttention(nn.Module):
             p_fo, k_fo = self._drop(pass_id, li, DK.K_FF_OUT)
 
             def sa_block(inp, res=None):
-                qkv = ops.linear(inp, at.in_proj_weight, at.in_proj_bias, self.precision, res=res)
-                o = ops.AttnFn.apply(qkv, seq, self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset)
+                o = ops.QKVAttnFn.apply(inp.contiguous(), at.in_proj_weight, at.in_proj_bias, seq, self.idx_pad,
+                                        self.n_head, p_at, k_at, self.state.row_offset, self.precision, res)
                 return ops.linear(o, at.out_proj.weight, at.out_proj.bias, self.precision)
 
             def ff_block(inp, res=None):
@@ -131,8 +131,8 @@ class SelfAttention(nn.Module):
                 # LayerNorm run on those rows (dropout indices through the row map, so the masks are the
                 # full-size run's).
                 r1 = ops.ResidualLink(inv=rs.inv)
-                qkv = ops.linear(x, at.in_proj_weight, at.in_proj_bias, self.precision, res=r1)
-                o = ops.AttnFn.apply(qkv, seq, self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset)
+                o = ops.QKVAttnFn.apply(x.contiguous(), at.in_proj_weight, at.in_proj_bias, seq, self.idx_pad,
+                                        self.n_head, p_at, k_at, self.state.row_offset, self.precision, r1)
                 oc = ops.GatherRowsFn.apply(o.reshape(B * L, d), rs)
                 sa = ops.linear(oc, at.out_proj.weight, at.out_proj.bias, self.precision)
                 xc = ops.gather_rows_nograd(x.reshape(B * L, d), rs)

@@ -116,7 +116,12 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
         (k0, k1), p, row_base = relu_drop[:3]
         if len(relu_drop) > 3:
             rowmap = relu_drop[3]
-    if aux_mode:
+    if A.dtype == torch.bfloat16:  # the attention backward's bf16 dqkv (in_proj dX; c2dsr_rgemm_aux_b16a)
+        if epi or aux_mode == AUX_MASK:
+            raise HipLibError('rgemm: bf16 A supports no epilogue / mask mode')
+        lib('c2dsr_rgemm_aux_b16a', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, int(aux_mode), aux,
+            auxmap, stream())
+    elif aux_mode:
         lib('c2dsr_rgemm_aux', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
             int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
     else:
@@ -133,7 +138,8 @@ def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None):
     """dW[N, D] = beta·dW + dYᵀ·X over T rows and (db given) db[N] = beta·db + Σ_t dY[t]
     (c2dsr_wgemm, deterministic split-t partials)."""
     ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
-    lib('c2dsr_wgemm', T, N, D, dY, N, X, D, float(beta), dW, db, ws, stream())
+    name = 'c2dsr_wgemm_b16y' if dY.dtype == torch.bfloat16 else 'c2dsr_wgemm'
+    lib(name, T, N, D, dY, N, X, D, float(beta), dW, db, ws, stream())
 
 
 class ResidualLink:
@@ -184,55 +190,65 @@ class LinearFn(Function):
     @staticmethod
     def backward(ctx, dy):
         x, W, y = ctx.saved_tensors
-        N, K = W.shape
-        M = x.numel() // K
-        dy = dy.contiguous()
-        if ctx.relu_p is not None and not (ctx.ff is not None and ctx.ff.premasked):
-            d2 = torch.empty_like(dy)
-            lib('c2dsr_relu_drop_bwd', dy, y, dy.numel(), float(ctx.relu_p), d2, stream())
-            dy = d2
-        dx = None
-        if ctx.needs_input_grad[0]:
-            fused = ctx.precision == BF16 and rgemm_ok(M, K, N)
-            park = ctx.res.grad if ctx.res is not None else None
-            if ctx.res is not None:
-                ctx.res.grad = None
-            sub = park is not None and ctx.res.inv is not None  # parked gradient of a row subset
-            if sub and not fused:  # compact rows → full, zeros elsewhere
-                full = torch.empty_like(x)
-                lib('c2dsr_expand_rows', park, ctx.res.inv, M, K, full, stream())
-                park, sub = full, False
-            if sub:  # dx = dy·W + the parked rows, read through the row map
-                dx = torch.empty_like(x)
-                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park,
-                      auxmap=ctx.res.inv)
-            elif fused and park is not None:  # dx = parked LN gradient + dy·W, in place
-                dx = park
-                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
-            elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here
-                dx = torch.empty_like(x)
-                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x,
-                      aux_scale=1.0 / (1.0 - ctx.ff.p))
-                ctx.ff.premasked = True
-            elif fused:
-                dx = torch.empty_like(x)
-                rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N)
-            elif park is not None:
-                dx = park
-                gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0, precision=ctx.precision)
-            else:
-                dx = torch.empty_like(x)
-                gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
-        gW = _grad_target(W)
-        gb = _grad_target(ctx.b)
-        if gW is not None and ctx.precision == BF16 and wgemm_ok(M, N, K):
-            wgemm(dy, x, gW, T=M, N=N, D=K, db=gb)  # bias gradient from the same dY chunks
-            gb = None
-        elif gW is not None:
-            gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
-        if gb is not None:
-            colsum(dy, M, N, N, gb)
+        dx = linear_backward(ctx, x, W, y, dy, ctx.needs_input_grad[0])
         return dx, None, None, None, None, None, None, None
+
+
+def linear_backward(ctx, x, W, y, dy, need_dx):
+    """The backward of y = x·Wᵀ + b [drop(relu)] (LinearFn.backward; QKVAttnFn's in_proj part).  ctx carries
+    b, precision, relu_p, res, ff, ff_role.  dy may be bf16 (the attention's dqkv): then the fused bf16-mode
+    kernels are taken, which read it without conversion."""
+    N, K = W.shape
+    M = x.numel() // K
+    dy = dy.contiguous()
+    if ctx.relu_p is not None and not (ctx.ff is not None and ctx.ff.premasked):
+        d2 = torch.empty_like(dy)
+        lib('c2dsr_relu_drop_bwd', dy, y, dy.numel(), float(ctx.relu_p), d2, stream())
+        dy = d2
+    dx = None
+    if need_dx:
+        fused = ctx.precision == BF16 and rgemm_ok(M, K, N)
+        park = ctx.res.grad if ctx.res is not None else None
+        if ctx.res is not None:
+            ctx.res.grad = None
+        sub = park is not None and ctx.res.inv is not None  # parked gradient of a row subset
+        if sub and not fused:  # compact rows → full, zeros elsewhere
+            full = torch.empty_like(x)
+            lib('c2dsr_expand_rows', park, ctx.res.inv, M, K, full, stream())
+            park, sub = full, False
+        if sub:  # dx = dy·W + the parked rows, read through the row map
+            dx = torch.empty_like(x)
+            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park,
+                  auxmap=ctx.res.inv)
+        elif fused and park is not None:  # dx = parked LN gradient + dy·W, in place
+            dx = park
+            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
+        elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here
+            dx = torch.empty_like(x)
+            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x,
+                  aux_scale=1.0 / (1.0 - ctx.ff.p))
+            ctx.ff.premasked = True
+        elif fused:
+            dx = torch.empty_like(x)
+            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N)
+        elif park is not None:
+            dx = park
+            gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0, precision=ctx.precision)
+        else:
+            dx = torch.empty_like(x)
+            gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
+    gW = _grad_target(W)
+    gb = _grad_target(ctx.b)
+    if gW is not None and ctx.precision == BF16 and wgemm_ok(M, N, K):
+        wgemm(dy, x, gW, T=M, N=N, D=K, db=gb)  # bias gradient from the same dY chunks
+        gb = None
+    elif gW is not None:
+        gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
+    if gb is not None:
+        colsum(dy, M, N, N, gb)
+    return dx
+
+
 
 
 def linear(x, W, b, precision=FP32, relu_drop=None, res=None, ff=None, ff_role=None):
@@ -636,6 +652,59 @@ class AttnFn(Function):
         lib('c2dsr_attn_bwd', qkv, seq, int(ctx.pad), B, L, d, ctx.n_head, ctx.keys[0], ctx.keys[1], float(ctx.p),
             int(ctx.b_base), P, dout.contiguous(), dqkv, stream())
         return dqkv, None, None, None, None, None, None
+
+
+class QKVAttnFn(Function):
+    """qkv = x·W_inᵀ + b_in, then the attention core (models/encoders.py:33 → MultiheadAttention: in_proj and
+    SDPA) as one autograd node, so that in bf16 mode the attention backward can hand dqkv to the in_proj
+    backward GEMMs in bf16 (c2dsr_attn_bwd_b16 → c2dsr_rgemm_aux_b16a / c2dsr_wgemm_b16y): their only
+    consumers read it as a bf16 MFMA operand, so the values are the ones they would round to, at half the
+    bytes.  Otherwise identical to LinearFn followed by AttnFn.  res: the ResidualLink of the layer input."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, seq, pad, n_head, p, keys, b_base, precision, res=None):
+        require_device(x)
+        N, K = W.shape
+        M = x.numel() // K
+        qkv = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
+        if precision == BF16 and rgemm_ok(M, N, K):
+            rgemm(x, weight_bf16(W), qkv, M=M, N=N, K=K, bias=b)
+        else:
+            gemm(x, W, qkv, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
+        B, L, d3 = qkv.shape
+        d = d3 // 3
+        out = torch.empty(B, L, d, device=x.device, dtype=torch.float32)
+        P = torch.empty(int(lib.raw('c2dsr_attn_psave_floats')(B, L, d, n_head)), device=x.device,
+                        dtype=torch.float32)
+        lib('c2dsr_attn_fwd', qkv, seq, int(pad), B, L, d, n_head, keys[0], keys[1], float(p), int(b_base), out, P,
+            stream())
+        ctx.save_for_backward(x, W, qkv, seq, P)
+        ctx.pad, ctx.n_head, ctx.p, ctx.keys, ctx.b_base = pad, n_head, p, keys, b_base
+        ctx.b, ctx.precision, ctx.relu_p, ctx.res, ctx.ff, ctx.ff_role = b, precision, None, res, None, None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, W, qkv, seq, P = ctx.saved_tensors
+        B, L, d3 = qkv.shape
+        d = d3 // 3
+        M = B * L
+        s = stream()
+        b16 = (ctx.precision == BF16 and _B16_DQKV and bool(lib.raw('c2dsr_attn_bwd_b16_supported')(L, d, ctx.n_head))
+               and rgemm_ok(M, d, d3) and wgemm_ok(M, d3, d))
+        args = (qkv, seq, int(ctx.pad), B, L, d, ctx.n_head, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.b_base), P,
+                dout.contiguous())
+        if b16:
+            dqkv = torch.empty(qkv.shape, device=qkv.device, dtype=torch.bfloat16)
+            lib('c2dsr_attn_bwd_b16', *args, dqkv, s)
+        else:
+            dqkv = torch.empty_like(qkv)
+            lib('c2dsr_attn_bwd', *args, dqkv, s)
+        dx = linear_backward(ctx, x, W, None, dqkv, ctx.needs_input_grad[0])
+        return (dx,) + (None,) * 10
+
+
+_B16_DQKV = __import__('os').environ.get('C2DSR_B16_DQKV', '1') == '1'
 
 
 # ----------------------------------------------------------------------------- residual / layernorm

@@ -90,6 +90,13 @@ int c2dsr_attn_fwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int
 int c2dsr_attn_bwd(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,
                    uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout, float* dqkv,
                    void* stream);
+/* The same backward writing dqkv in bf16 (wave kernels only: c2dsr_attn_bwd_b16_supported).  In bf16 mode
+ * the only consumers of dqkv are the in_proj backward GEMMs, which use it as a bf16 MFMA operand anyway
+ * (c2dsr_rgemm_aux_b16a, c2dsr_wgemm_b16y): half the bytes written and read back. */
+int c2dsr_attn_bwd_b16_supported(int L, int d, int H);
+int c2dsr_attn_bwd_b16(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,
+                       uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout, void* dqkv,
+                       void* stream);
 
 /* Residual + dropout + LayerNorm (TransformerEncoderLayer norm1/norm2, encoder.norm; eps 1e-8). */
 int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
@@ -248,6 +255,11 @@ int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B,
                     float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                     int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
                     float aux_scale, void* stream);
+/* c2dsr_rgemm_aux with A in bf16 (K = 768: the in_proj dX over the attention's bf16 dqkv; no epilogue,
+ * aux modes 0 / 1 / 3) — the products equal the fp32-A call's, which rounds A to bf16 the same way. */
+int c2dsr_rgemm_aux_b16a(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
+                         float alpha, float beta, const float* bias, int aux_mode, const float* aux, const int* auxmap,
+                         void* stream);
 /* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
  * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
  * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS
@@ -257,6 +269,9 @@ int c2dsr_wgemm_supported(int T, int N, int D);
 size_t c2dsr_wgemm_workspace(int N);
 int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
                 float* db, void* part, void* stream);
+/* ... with dY in bf16 (the bias sums add the bf16 values) */
+int c2dsr_wgemm_b16y(int T, int N, int D, const void* dY, int ldy, const float* X, int ldx, float beta, float* dW,
+                     float* db, void* part, void* stream);
 /* y = bf16(x), x fp32 [R][Cc] with row stride ldx; trans: y is [Cc][R] (weight copies for rgemm). */
 int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream);
 

@@ -610,3 +610,77 @@ def test_compact_valid_targets(M):
     winv = np.full(M, -1)
     winv[want] = np.arange(n)
     assert np.array_equal(inv.cpu().numpy(), winv)
+
+
+# ----------------------------------------------------------------------------- bf16 dqkv hand-off
+@pytest.mark.parametrize('B,L,d,H,p', [(13, 50, 256, 1, 0.2), (6, 64, 64, 2, 0.0), (4, 8, 32, 1, 0.1)])
+def test_attention_bwd_b16_is_the_rounded_fp32_dqkv(B, L, d, H, p):
+    """c2dsr_attn_bwd_b16 writes exactly bf16(RNE) of what c2dsr_attn_bwd writes in fp32."""
+    from c2dsr_amd._lib import lib, stream
+    torch.manual_seed(B + L + d)
+    pad = 999
+    seq = torch.randint(0, 900, (B, L))
+    for b in range(B):
+        seq[b, :L - int(torch.randint(1, L, (1,)))] = pad
+    seq[:, 0] = pad
+    sd = seq.to(DEV)
+    qkv = torch.randn(B, L, 3 * d, device=DEV)
+    dout = torch.randn(B, L, d, device=DEV)
+    P = torch.empty(int(lib.raw('c2dsr_attn_psave_floats')(B, L, d, H)), device=DEV)
+    out = torch.empty(B, L, d, device=DEV)
+    s = stream()
+    assert bool(lib.raw('c2dsr_attn_bwd_b16_supported')(L, d, H))
+    lib('c2dsr_attn_fwd', qkv, sd, pad, B, L, d, H, 11, 22, p, 3, out, P, s)
+    g32 = torch.empty_like(qkv)
+    lib('c2dsr_attn_bwd', qkv, sd, pad, B, L, d, H, 11, 22, p, 3, P, dout, g32, s)
+    g16 = torch.empty(qkv.shape, device=DEV, dtype=torch.bfloat16)
+    lib('c2dsr_attn_bwd_b16', qkv, sd, pad, B, L, d, H, 11, 22, p, 3, P, dout, g16, s)
+    torch.cuda.synchronize()
+    assert torch.equal(g16, g32.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize('aux', [0, 1, 3])
+def test_rgemm_b16a_equals_fp32_path(aux):
+    """The in_proj dX over a bf16 dqkv equals the fp32-A call on the same (bf16-valued) operand, bit for bit,
+    in every aux mode the backward uses (none, in-place residual sum, mapped row-subset sum)."""
+    from c2dsr_amd.ops import AUX_ACC, AUX_ACC_MAP, rgemm, to_bf16
+    M, N, K = 1037, 256, 768
+    g = torch.Generator().manual_seed(aux)
+    A16 = torch.randn(M, K, generator=g).to(DEV).to(torch.bfloat16)
+    Wb = to_bf16(torch.randn(K, N, generator=g).to(DEV), trans=True)
+    kw = {}
+    if aux == 1:
+        base = torch.randn(M, N, generator=g).to(DEV)
+    elif aux == 3:
+        n_sub = 300
+        auxmap = torch.full((M,), -1, dtype=torch.int32)
+        auxmap[torch.randperm(M, generator=g)[:n_sub]] = torch.arange(n_sub, dtype=torch.int32)
+        park = torch.randn(n_sub, N, generator=g).to(DEV)
+        kw = dict(aux_mode=AUX_ACC_MAP, aux=park, auxmap=auxmap.to(DEV))
+    outs = []
+    for A in (A16, A16.float()):
+        if aux == 1:
+            C = base.clone()
+            rgemm(A, Wb, C, M=M, N=N, K=K, aux_mode=AUX_ACC, aux=C)
+        else:
+            C = torch.empty(M, N, device=DEV)
+            rgemm(A, Wb, C, M=M, N=N, K=K, **kw)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_wgemm_b16y_equals_fp32_path():
+    from c2dsr_amd.ops import wgemm
+    T, N, D = 4097, 768, 256
+    g = torch.Generator().manual_seed(7)
+    dY16 = torch.randn(T, N, generator=g).to(DEV).to(torch.bfloat16)
+    X = torch.randn(T, D, generator=g).to(DEV)
+    res = []
+    for dY in (dY16, dY16.float()):
+        dW = torch.full((N, D), 0.5, device=DEV)
+        db = torch.full((N,), 0.25, device=DEV)
+        wgemm(dY, X, dW, T=T, N=N, D=D, beta=1.0, db=db)
+        res.append((dW, db))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])

