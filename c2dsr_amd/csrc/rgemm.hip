@@ -21,6 +21,7 @@
 
 namespace {
 using namespace c2img;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct Epi2 {
   float alpha, beta;
@@ -156,8 +157,9 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
     const int vo_ = ((rt0 + tile_ * rts) * 32 + lrow) * ldab + (kc_ * 256 + 4 * lane) * AEB;                   \
     _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                            \
       if constexpr (AB16) {                                                                                    \
-        const auto h_ = __builtin_amdgcn_raw_buffer_load_b64(asrc, vo_ + u * 4 * ldab, 0, 0);                  \
-        P[u] = make_float4(__builtin_bit_cast(float, h_[0]), __builtin_bit_cast(float, h_[1]), 0.f, 0.f);      \
+        const f32x2 h_ = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(asrc, vo_ + u * 4 * ldab, 0, 0)); \
+        P[u].x = h_[0];                                                                                        \
+        P[u].y = h_[1];                                                                                        \
       } else {                                                                                                 \
         P[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc, vo_ + u * 4 * ldab, 0, 0)); \
       }                                                                                                        \
@@ -168,7 +170,10 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
     _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                            \
       bf16x4 v_;                                                                                               \
       if constexpr (AB16) {                                                                                    \
-        v_ = __builtin_bit_cast(bf16x4, make_float2(P[u].x, P[u].y));                                          \
+        f32x2 g_;                                                                                              \
+        g_[0] = P[u].x;                                                                                        \
+        g_[1] = P[u].y;                                                                                        \
+        v_ = __builtin_bit_cast(bf16x4, g_);                                                                   \
       } else {                                                                                                 \
         v_[0] = (bf16)P[u].x; v_[1] = (bf16)P[u].y; v_[2] = (bf16)P[u].z; v_[3] = (bf16)P[u].w;                \
       }                                                                                                        \

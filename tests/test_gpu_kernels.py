@@ -667,7 +667,11 @@ def test_rgemm_b16a_equals_fp32_path(aux):
             rgemm(A, Wb, C, M=M, N=N, K=K, **kw)
         outs.append(C)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    dif = (outs[0] - outs[1]).abs()
+    bad = torch.nonzero(dif > 0)
+    assert torch.equal(outs[0], outs[1]), (f'{bad.shape[0]} differ, max {float(dif.max())}, rows '
+                                           f'{bad[:, 0].unique()[:20].tolist()}, cols {bad[:, 1].unique()[:20].tolist()}, '
+                                           f'ref scale {float(outs[1].abs().max())}')
 
 
 def test_wgemm_b16y_equals_fp32_path():
