@@ -55,6 +55,9 @@
 #ifndef CE_X_NOMAX
 #define CE_X_NOMAX 0
 #endif
+#ifndef CE_X_NOLDS
+#define CE_X_NOLDS 0
+#endif
 #ifndef CE_X_TAU
 #define CE_X_TAU 8.f
 #endif
@@ -688,10 +691,17 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
         (
             [&] {
               constexpr int ks = K;
+#if !CE_X_NOLDS
               if constexpr (ks + DS < KS) {
                 fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
                 fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
               }
+#else
+              if constexpr (ks + DS < KS) {
+                fa[(ks + DS) % (DS + 2)][0] = fa[0][0];
+                fa[(ks + DS) % (DS + 2)][1] = fa[0][1];
+              }
+#endif
               if constexpr (ks == 0) {
                 sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
                 sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);

@@ -105,7 +105,7 @@ struct TileLoader {
 template <bool BF16, bool TA, bool TB, bool VEC>
 __global__ __launch_bounds__(THREADS) void gemm_kernel(int M, int N, int K, const float* __restrict__ A, int lda,
                                                        const float* __restrict__ B, int ldb, float* __restrict__ C,
-                                                       int ldc, Epi ep, int k_per_split, int atomic) {
+                                                       int ldc, Epi ep, int k_per_split, int partial) {
   typedef typename Lds<BF16>::T T;
   constexpr int LD = Lds<BF16>::LD;
   __shared__ __attribute__((aligned(16))) T As[BM * LD];
@@ -183,16 +183,16 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(int M, int N, int K, cons
     for (int j = 0; j < 2; ++j) {
       const int col = n0 + wn * 64 + j * 32 + (lane & 31);
       if (col >= N) continue;
-      const float bcol = (ep.bias && !atomic) ? ep.bias[col] : 0.f;
+      const float bcol = (ep.bias && !partial) ? ep.bias[col] : 0.f;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int row = m0 + wm * 64 + i * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
         if (row >= M) continue;
-        float* cp = C + (long)row * ldc + col;
         float v = ep.alpha * acc[i][j][reg];
-        if (atomic) {
-          atomicAdd(cp, v);
+        if (partial) {  // split-K: this split's partial slab [M][N] (summed in split order afterwards)
+          C[(long)blockIdx.z * M * N + (long)row * N + col] = v;
         } else {
+          float* cp = C + (long)row * ldc + col;
           if (ep.beta != 0.f) v = fmaf(ep.beta, *cp, v);
           v += bcol;
           if (ep.relu) {
@@ -203,6 +203,38 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(int M, int N, int K, cons
         }
       }
     }
+}
+
+// C[r][c] = beta·C[r][c] + Σ_s part[s][r][c], s in order (deterministic split-K combine)
+__global__ void splitk_sum_kernel(const float* __restrict__ part, int splits, int M, int N, float beta,
+                                  float* __restrict__ C, int ldc) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * N) return;
+  const int r = (int)(i / N), c = (int)(i % N);
+  float t = 0.f;
+  for (int s = 0; s < splits; ++s) t += part[(long)s * M * N + i];
+  float* cp = C + (long)r * ldc + c;
+  *cp = beta == 0.f ? t : fmaf(beta, *cp, t);
+}
+
+// split-K partial slabs: one scratch buffer per device, grown on demand (never inside a captured graph)
+float* splitk_scratch(size_t floats) {
+  static float* buf[64] = {nullptr};
+  static size_t cap[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (cap[dev] < floats) {
+    if (buf[dev]) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(buf[dev]);
+    }
+    buf[dev] = nullptr;
+    cap[dev] = 0;
+    if (hipMalloc((void**)&buf[dev], floats * sizeof(float)) != hipSuccess) return nullptr;
+    cap[dev] = floats;
+  }
+  return buf[dev];
 }
 
 __global__ void scale_kernel(float* __restrict__ C, int M, int N, int ldc, float beta) {
@@ -257,20 +289,20 @@ __global__ __launch_bounds__(1024) void colsum_final_kernel(const float* __restr
 
 template <bool BF16, bool TA, bool TB>
 void launch_t(dim3 grid, hipStream_t s, bool vec, int M, int N, int K, const float* A, int lda, const float* B, int ldb,
-              float* C, int ldc, Epi ep, int kps, int atomic) {
+              float* C, int ldc, Epi ep, int kps, int partial) {
   if (vec)
-    gemm_kernel<BF16, TA, TB, true><<<grid, THREADS, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
+    gemm_kernel<BF16, TA, TB, true><<<grid, THREADS, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, ep, kps, partial);
   else
-    gemm_kernel<BF16, TA, TB, false><<<grid, THREADS, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
+    gemm_kernel<BF16, TA, TB, false><<<grid, THREADS, 0, s>>>(M, N, K, A, lda, B, ldb, C, ldc, ep, kps, partial);
 }
 
 template <bool BF16>
 void launch_p(int ta, int tb, dim3 grid, hipStream_t s, bool vec, int M, int N, int K, const float* A, int lda,
-              const float* B, int ldb, float* C, int ldc, Epi ep, int kps, int atomic) {
-  if (!ta && !tb) launch_t<BF16, false, false>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
-  if (!ta && tb) launch_t<BF16, false, true>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
-  if (ta && !tb) launch_t<BF16, true, false>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
-  if (ta && tb) launch_t<BF16, true, true>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
+              const float* B, int ldb, float* C, int ldc, Epi ep, int kps, int partial) {
+  if (!ta && !tb) launch_t<BF16, false, false>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, partial);
+  if (!ta && tb) launch_t<BF16, false, true>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, partial);
+  if (ta && !tb) launch_t<BF16, true, false>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, partial);
+  if (ta && tb) launch_t<BF16, true, true>(grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, partial);
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -311,16 +343,22 @@ C2_API int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* 
   const bool b_ok = al16(B) && ldb % 4 == 0 && (transB ? K % 4 == 0 : N % 4 == 0);
   const bool vec = a_ok && b_ok;
   Epi ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base, rowmap};
-  int atomic = 0;
+  // split-K: each split writes its partial product to a slab, summed in split order afterwards
+  // (deterministic: no float atomics)
+  int partial = 0;
+  float* out = C;
   if (splits > 1) {
-    if (beta != 1.f) scale_kernel<<<c2::ceil_div((long)M * N, 256), 256, 0, s>>>(C, M, N, ldc, beta);
-    atomic = 1;
+    out = splitk_scratch((size_t)splits * M * N);
+    if (!out) return (int)hipErrorOutOfMemory;
+    partial = 1;
   }
   dim3 grid(c2::ceil_div(N, BN), c2::ceil_div(M, BM), splits);
   if (precision == 1)
-    launch_p<true>(transA, transB, grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
+    launch_p<true>(transA, transB, grid, s, vec, M, N, K, A, lda, B, ldb, out, ldc, ep, kps, partial);
   else
-    launch_p<false>(transA, transB, grid, s, vec, M, N, K, A, lda, B, ldb, C, ldc, ep, kps, atomic);
+    launch_p<false>(transA, transB, grid, s, vec, M, N, K, A, lda, B, ldb, out, ldc, ep, kps, partial);
+  if (partial)
+    splitk_sum_kernel<<<c2::ceil_div((long)M * N, 256), 256, 0, s>>>(out, splits, M, N, beta, C, ldc);
   C2_CHECK_LAUNCH();
   return 0;
 }

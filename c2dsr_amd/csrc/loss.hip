@@ -9,12 +9,19 @@
 namespace {
 
 // w[b,l] = gm[b,l] / Σ_l gm[b,l]   (Trainer.cal_mask, trainer.py:85-89)
-__global__ void pool_weights_kernel(const int64_t* __restrict__ gm, int B, int L, float* __restrict__ w) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+// one wave per sequence: lane l holds positions l, l + 64, ...; the mask counts are small integers, so the
+// fp32 sum is exact in any order
+__global__ __launch_bounds__(256) void pool_weights_kernel(const int64_t* __restrict__ gm, int B, int L,
+                                                           float* __restrict__ w) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;  // uniform over the wave
+  const int64_t* g = gm + (long)b * L;
   float S = 0.f;
-  for (int l = 0; l < L; ++l) S += (float)gm[(long)b * L + l];
-  for (int l = 0; l < L; ++l) w[(long)b * L + l] = (float)gm[(long)b * L + l] / S;
+  for (int l = lane; l < L; l += 64) S += (float)g[l];
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) S += __shfl_xor(S, m, 64);
+  for (int l = lane; l < L; l += 64) w[(long)b * L + l] = (float)g[l] / S;
 }
 
 // out[b,c] = Σ_l h[b,l,c] * w[b,l]      (trainer.py:101-108)
@@ -515,7 +522,7 @@ __global__ void rowscale_kernel(const float* __restrict__ x, const float* __rest
 
 C2_API int c2dsr_pool_weights(const int64_t* gm, int B, int L, float* w, void* stream) {
   if (B == 0) return 0;
-  pool_weights_kernel<<<c2::ceil_div(B, 256), 256, 0, (hipStream_t)stream>>>(gm, B, L, w);
+  pool_weights_kernel<<<c2::ceil_div(B, 4), 256, 0, (hipStream_t)stream>>>(gm, B, L, w);
   C2_CHECK_LAUNCH();
   return 0;
 }

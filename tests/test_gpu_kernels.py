@@ -688,3 +688,20 @@ def test_wgemm_b16y_equals_fp32_path():
         res.append((dW, db))
     torch.cuda.synchronize()
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_gemm_split_k_deterministic():
+    """Split-K (the bilinear weight gradient: M = N = d, K = B) sums its partial slabs in split order: the
+    same bits on every run, no float atomics."""
+    from c2dsr_amd.ops import gemm
+    M, N, K = 256, 256, 4096
+    g = torch.Generator().manual_seed(3)
+    A, B, C0 = torch.randn(K, M, generator=g), torch.randn(K, N, generator=g), torch.randn(M, N, generator=g)
+    outs = []
+    for _ in range(3):
+        C = C0.to(DEV)
+        gemm(A.to(DEV), B.to(DEV), C, M=M, N=N, K=K, transA=1, beta=1.0, split_k=0)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert rel(outs[0], C0.double() + A.double().T @ B.double()) < 1e-5
