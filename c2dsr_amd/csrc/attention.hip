@@ -15,6 +15,22 @@
 
 typedef __bf16 bf16;
 
+// experiment switch (wrong results; timing only): ATTN_X_NOMFMA replaces the wave kernels' fp32 MFMAs by
+// one FMA into the accumulator, to measure how much of their time the matrix products take
+#ifndef ATTN_X_NOMFMA
+#define ATTN_X_NOMFMA 0
+#endif
+#if ATTN_X_NOMFMA
+template <typename V>
+__device__ __forceinline__ V wmfma_fake(float a, float b, V c) {
+  c[0] = fmaf(a, b, c[0]);
+  return c;
+}
+#define WMFMA(a, b, c, x, y, z) wmfma_fake((a), (b), (c))
+#else
+#define WMFMA(a, b, c, x, y, z) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), (x), (y), (z))
+#endif
+
 #include <cstdlib>
 
 namespace {
@@ -633,9 +649,9 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const
         const float qc[4] = {kq[u][3].x, kq[u][3].y, kq[u][3].z, kq[u][3].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          t0 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qa[e], t0, 0, 0, 0);
-          if constexpr (TI > 1) t1 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qc[e], t1, 0, 0, 0);
-          if constexpr (TI > 1 && TJ > 1) t2 = __builtin_amdgcn_mfma_f32_32x32x2f32(kc[e], qc[e], t2, 0, 0, 0);
+          t0 = WMFMA(ka[e], qa[e], t0, 0, 0, 0);
+          if constexpr (TI > 1) t1 = WMFMA(ka[e], qc[e], t1, 0, 0, 0);
+          if constexpr (TI > 1 && TJ > 1) t2 = WMFMA(kc[e], qc[e], t2, 0, 0, 0);
         }
       }
     };
@@ -670,10 +686,10 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const
     for (int q = 0; q < 16; ++q) o0[q] = o1[q] = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(t0[q], v[0][q], o0, 0, 0, 0);
+      o0 = WMFMA(t0[q], v[0][q], o0, 0, 0, 0);
       if constexpr (TI > 1) {
-        o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(t1[q], v[0][q], o1, 0, 0, 0);
-        if constexpr (TJ > 1) o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(t2[q], v[1][q], o1, 0, 0, 0);
+        o1 = WMFMA(t1[q], v[0][q], o1, 0, 0, 0);
+        if constexpr (TJ > 1) o1 = WMFMA(t2[q], v[1][q], o1, 0, 0, 0);
       }
     }
     const int c = 32 * ct + r;
@@ -779,9 +795,9 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
         const float qc[4] = {kq[u][3].x, kq[u][3].y, kq[u][3].z, kq[u][3].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          g0 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qa[e], g0, 0, 0, 0);
-          if constexpr (TI > 1) g1 = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[e], qc[e], g1, 0, 0, 0);
-          if constexpr (TI > 1 && TJ > 1) g2 = __builtin_amdgcn_mfma_f32_32x32x2f32(kc[e], qc[e], g2, 0, 0, 0);
+          g0 = WMFMA(ka[e], qa[e], g0, 0, 0, 0);
+          if constexpr (TI > 1) g1 = WMFMA(ka[e], qc[e], g1, 0, 0, 0);
+          if constexpr (TI > 1 && TJ > 1) g2 = WMFMA(kc[e], qc[e], g2, 0, 0, 0);
         }
       }
     }
@@ -847,10 +863,10 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
       zero16(o0); zero16(o1);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(g0[q], k0v[q], o0, 0, 0, 0);
+        o0 = WMFMA(g0[q], k0v[q], o0, 0, 0, 0);
         if constexpr (TI > 1) {
-          o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(g1[q], k0v[q], o1, 0, 0, 0);
-          if constexpr (TJ > 1) o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(g2[q], k1v[q], o1, 0, 0, 0);
+          o1 = WMFMA(g1[q], k0v[q], o1, 0, 0, 0);
+          if constexpr (TJ > 1) o1 = WMFMA(g2[q], k1v[q], o1, 0, 0, 0);
         }
       }
       const int c = 32 * ct + r;
@@ -897,7 +913,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
           for (int q = 0; q < 16; ++q) {
             const int qi = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * hi;
             const float a = T[qi * TLD + 32 * tj + r];
-            o = __builtin_amdgcn_mfma_f32_32x32x2f32(a, ti ? b1v[q] : b0v[q], o, 0, 0, 0);
+            o = WMFMA(a, ti ? b1v[q] : b0v[q], o, 0, 0, 0);
           }
         }
 #pragma unroll
