@@ -95,10 +95,9 @@ class _Lib:
                 conv.append(a)
         if name in self.time_names:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            st = _LAUNCH[-1] if _LAUNCH else None  # the stream the kernels go to
-            e0.record(st)
+            e0.record()
             rc = getattr(lib, name)(*conv)
-            e1.record(st)
+            e1.record()
             meta = self.time_meta.get(name)
             rec = conv + [meta(conv)] if meta is not None else conv
             self.timed.setdefault(name, []).append((e0, e1, rec))
@@ -125,30 +124,8 @@ class _Lib:
 lib = _Lib()
 
 
-_LAUNCH = []  # stack of torch streams the kernels are launched on instead of the current one (launch_on)
-
-
 def stream() -> int:
-    if _LAUNCH:
-        return _LAUNCH[-1].cuda_stream
     return torch.cuda.current_stream().cuda_stream
-
-
-class launch_on:
-    """Launch the library's kernels on ``s`` while torch's current stream (allocations, autograd) stays
-    what it is; the caller orders ``s`` against the current stream with events and calls
-    ``Tensor.record_stream(s)`` on what the kernels touch."""
-
-    def __init__(self, s):
-        self.s = s
-
-    def __enter__(self):
-        _LAUNCH.append(self.s)
-        return self.s
-
-    def __exit__(self, *exc):
-        _LAUNCH.pop()
-        return False
 
 
 def require_device(t: torch.Tensor):

@@ -21,7 +21,6 @@ class FlatStore:
         device: nothing is reduced, the backward accumulates into it and AdamW only reads it)."""
         self.align = align
         self.direct = direct
-        self.tables_ready = None  # event after the optimizer updated the item tables (optim.FlatAdamW)
         seen = {}
         entries = []
         off = 0

@@ -12,9 +12,6 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-import contextlib
-
-from .. import _lib
 from .. import dropout as DK
 from .. import ops
 from ..graph import CSRGraph, DeviceGraph
@@ -142,26 +139,13 @@ class C2DSR(nn.Module):
 
     # ------------------------------------------------------------------ reference API
     def convolve_graph(self):
-        """C2DSR.py:59-62.  Right after an optimizer step the three propagations only need the updated item
-        tables: they run on a side stream from the optimizer's `tables_ready` event, under the rest of the
-        parameter update still running on the current stream, which waits for them before going on."""
+        """C2DSR.py:59-62."""
         if self.training:
             self.new_step()
         g_share, g_spec = self.graphs()
-        ev = getattr(self.flat, 'tables_ready', None) if hasattr(self, 'flat') else None
-        side = None
-        if ev is not None:
-            self.flat.tables_ready = None
-            side = ops.side_stream(self.embed_i.weight.device, 'gcn')
-            side.wait_event(ev)
-        with (_lib.launch_on(side) if side is not None else contextlib.nullcontext()):
-            hs, ts, ss = self.gnn_share(self.embed_i.weight, g_share)
-            ha, ta, sa = self.gnn_a(self.embed_i_a.weight, g_spec)
-            hb, tb, sb = self.gnn_b(self.embed_i_b.weight, g_spec)
-        if side is not None:
-            done = torch.cuda.Event()
-            done.record(side)
-            torch.cuda.current_stream(self.embed_i.weight.device).wait_event(done)
+        hs, ts, ss = self.gnn_share(self.embed_i.weight, g_share)
+        ha, ta, sa = self.gnn_a(self.embed_i_a.weight, g_spec)
+        hb, tb, sb = self.gnn_b(self.embed_i_b.weight, g_spec)
         self.hi_share, self.hi_a, self.hi_b = hs, ha, hb
         self._tok, self._sink = (ts, ta, tb), (ss, sa, sb)
 

@@ -10,7 +10,7 @@ from __future__ import annotations
 import torch
 from torch.autograd import Function
 
-from ._lib import _LAUNCH, HipLibError, lib, stream, require_device
+from ._lib import HipLibError, lib, stream, require_device
 from .dp import notify_lookup, notify_rows, notify_table, row_cuts
 
 FP32, BF16 = 0, 1
@@ -363,8 +363,6 @@ def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, p
     d = X.shape[1]
     if part is None:
         part = torch.empty(max(n_slots, 1), d, device=X.device, dtype=torch.float32)
-        if _LAUNCH:  # kernels on a side stream (C2DSR.convolve_graph): keep the scratch until it is done
-            part.record_stream(_LAUNCH[-1])
     if rows is not None:
         w0, w1, s0, s1 = graph.row_slice(transposed, *rows)
         work, n_work, split, n_split = work[w0:w1], w1 - w0, split[s0:s1], s1 - s0
@@ -382,16 +380,12 @@ class GCNFn(Function):
     def forward(ctx, E, graph, n_gnn, p, keys, pad_row, sink):
         require_device(E)
         out = torch.empty_like(E)
-        if _LAUNCH:
-            out.record_stream(_LAUNCH[-1])
         inv = 1.0 / (n_gnn + 1)
         if n_gnn == 0:  # H = E
             spmm(graph, False, E, (0, 0), 0.0, 0, 0.0, E, 1.0, 0.0, -1, 0.0, out)
         h_prev = E
         for k in range(n_gnn):
             h_k = None if k == n_gnn - 1 else torch.empty_like(E)
-            if h_k is not None and _LAUNCH:
-                h_k.record_stream(_LAUNCH[-1])
             spmm(graph, False, h_prev, keys[k], p, 0, inv, E if k == 0 else None, inv, 0.0, -1,
                  0.0 if k == 0 else 1.0, out, h_k)
             h_prev = h_k
@@ -442,10 +436,9 @@ _PLAN_SIDE = __import__('os').environ.get('C2DSR_PLAN_SIDE', '1') == '1'
 PLAN_SRC = {}  # plan buffer data_ptr -> data_ptr of the index tensor it sorts (roofline accounting)
 
 
-def side_stream(device, role='plans'):
-    """A side stream per (device, role): 'plans' — the index plans, sorted concurrently with the forward;
-    'gcn' — the GCN forward right after an optimizer step, under the rest of the parameter update."""
-    key = (torch.device(device).index, role)
+def side_stream(device):
+    """The stream the index plans are sorted on (one per device), concurrent with the forward."""
+    key = torch.device(device).index
     if key not in _side_streams:
         _side_streams[key] = torch.cuda.Stream(device=device)
     return _side_streams[key]

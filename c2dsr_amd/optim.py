@@ -31,23 +31,6 @@ class FlatAdamW(torch.optim.Optimizer):
         self.accum = flat.accum if zero is None else torch.zeros(n, device=dev)
         self.n_steps = 0
         self.accumulate = True  # grads accumulate until zero_grad (Q3)
-        # item-table slices updated first (the next step's GCN forward reads only them: it runs on a side
-        # stream after `flat.tables_ready` while the rest of the update finishes; C2DSR.convolve_graph)
-        self.first_ranges = None
-
-    def set_first(self, tables):
-        """Update these parameters' slices (the item tables) first and mark them with an event."""
-        f = self.flat
-        ptr = {p.data_ptr(): (o, f.padded(n)) for _, p, o, n in f.entries}
-        rs = sorted({ptr[t.data_ptr()] for t in tables})
-        rest, lo = [], 0
-        for o, n in rs:
-            if o > lo:
-                rest.append((lo, o - lo))
-            lo = o + n
-        if lo < f.numel:
-            rest.append((lo, f.numel - lo))
-        self.first_ranges = (rs, rest)
 
     def zero_grad(self, set_to_none: bool = True):
         """Reference semantics: clears the epoch accumulation (grads would be None)."""
@@ -61,22 +44,7 @@ class FlatAdamW(torch.optim.Optimizer):
         b1, b2 = g['betas']
         f = self.flat
         hyper = (float(g['lr']), float(g['weight_decay']), float(b1), float(b2), float(g['eps']), self.n_steps)
-        if self.zero is None and self.first_ranges is not None:
-            # tables, event, then the rest (same kernel over slices: elementwise, so the same values)
-            acc = self.accumulate
-            first, rest = self.first_ranges
-            for o, n in first:
-                sl = slice(o, o + n)
-                lib('c2dsr_adamw', f.param[sl], f.fresh[sl], self.accum[sl] if acc else None, self.m[sl], self.v[sl],
-                    self.vmax[sl], n, *hyper, stream())
-            ev = torch.cuda.Event()
-            ev.record()
-            f.tables_ready = ev
-            for o, n in rest:
-                sl = slice(o, o + n)
-                lib('c2dsr_adamw', f.param[sl], f.fresh[sl], self.accum[sl] if acc else None, self.m[sl], self.v[sl],
-                    self.vmax[sl], n, *hyper, stream())
-        elif self.zero is None:
+        if self.zero is None:
             # direct store (one device): fresh is accum — read only, 36 B/param; without epoch accumulation
             # the same buffer is this step's gradient and is cleared
             lib('c2dsr_adamw', f.param, f.fresh, self.accum if self.accumulate else None, self.m, self.v, self.vmax,

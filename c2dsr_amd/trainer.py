@@ -72,9 +72,6 @@ class Trainer(object):
             if getattr(args, 'zero1', False) or os.environ.get('C2DSR_ZERO1', '0') == '1':
                 self.zero = Zero1(m.flat, self.comm_plan, self.rank, self.world)
         self.optimizer = FlatAdamW(self.model.flat, lr=args.lr, weight_decay=args.l2, zero=self.zero)
-        if self.zero is None and os.environ.get('C2DSR_GCN_OVERLAP', '1') == '1':
-            m = self.model  # the next convolve_graph needs only the tables: they are updated first
-            self.optimizer.set_first([m.embed_i.weight, m.embed_i_a.weight, m.embed_i_b.weight])
         self.scheduler = torch.optim.lr_scheduler.StepLR(self.optimizer, step_size=args.lr_step, gamma=args.lr_gamma)
         self.noter = noter
         self.n_tr = len(self.trainloader.dataset) if self.trainloader is not None else 0
