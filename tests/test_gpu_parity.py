@@ -270,22 +270,28 @@ def test_fp32_step_d256_matches_oracle():
     _steps_vs_oracle(tr, orc, rows, 96, 2, TOL, 5 * TOL, TOL)
 
 
+# BASELINE configs[2] (C3, the headline: Movie-Book item counts, B=2048) and configs[1] (C2: Food-Kitchen
+# item counts, B=1024), both d=256, L=50, R=10, bf16
+FULL = {'C3_mb': (36845, 63937, 2048), 'C2_fk': (29207, 34886, 1024)}
+
+
+@pytest.mark.parametrize('cfg', ['C3_mb', 'C2_fk'])
 @pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
-def test_bf16_full_size_mb_loss_head_vs_fp32(compact):
-    """Full-size property check of the benchmarked step (BASELINE configs[2] item counts 36,845 / 63,937,
-    d=256, L=50, B=2048, R=10, dropout 0.2, bf16): the loss is finite, and the fused bf16 classifier heads
-    + CE and the discriminators agree with the fp32 materialised loss head (the oracle's loss_head, run with
-    torch on the device) evaluated on the HIP encoder outputs of the same step — the losses and the
-    classifier / discriminator gradients (VERDICT r01 #1)."""
+def test_bf16_full_size_loss_head_vs_fp32(compact, cfg):
+    """Full-size property check of the benchmarked step at the BASELINE configs' item counts and batch
+    (d=256, L=50, R=10, dropout 0.2, bf16): the loss is finite, and the fused bf16 classifier heads + CE and
+    the discriminators agree with the fp32 materialised loss head (the oracle's loss_head, run with torch on
+    the device) evaluated on the HIP encoder outputs of the same step — the losses and the classifier /
+    discriminator gradients (VERDICT r01 #1)."""
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
     from c2dsr_amd import synth
     from c2dsr_amd import dropout as DK
     from oracle import c2dsr_oracle as O
     import random
-    c = dict(n_a=36845, n_b=63937, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
+    n_a, n_b, B = FULL[cfg]
+    c = dict(n_a=n_a, n_b=n_b, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
              norm_first=False, d_bias=False, shared_item_embed=False)
-    B = 2048
     seqs = synth.make_sequences(2 * B, c['n_a'], c['n_b'], c['len_max'], seed=1, n_min=6)
     random.seed(3407)
     rows = DL.to_arrays(DL.preprocess_train(seqs, c['n_a'], c['n_b'], c['len_max']))
@@ -336,6 +342,16 @@ def test_bf16_full_size_mb_loss_head_vs_fp32(compact):
     for n, g in zip(names, grads):
         e = rel(box['grads'][n], g)
         assert e < BF16_GRAD, (n, e)
+
+
+def test_c1_food_kitchen_shape_fp32_vs_oracle():
+    """BASELINE configs[0] (C1) shape: Food-Kitchen item counts (29,207 / 34,886), d=64, L=15, R=10, B=128,
+    fp32 mode, dropout 0.2 (hash masks) — two steps vs the oracle at the north_star tolerance (1e-4; the
+    reference's own CPU run of C1 is main.py on the FK files, which do not travel to the GPU box)."""
+    c1 = dict(n_a=29207, n_b=34886, len_max=15, len_rec=10, d_latent=64, n_gnn=1, n_attn=1, n_head=1,
+              norm_first=False, d_bias=False, shared_item_embed=False)
+    tr, orc, rows = _oracle_case(c1, B=128, n_users=400, precision='fp32')
+    _steps_vs_oracle(tr, orc, rows, 128, 2, TOL, 5 * TOL, TOL)
 
 
 def test_bf16_step_close_to_fp32():
@@ -445,3 +461,71 @@ def test_zero1_world2_equals_replicated_and_reference(tmp_path, name):
             if 'self_attn.in_proj_' in n:  # Q/K rows: the gradient is rounding noise (Q1; test_gpu_driver.py)
                 got, want = got[2 * d:], want[2 * d:]
             assert rel(got, want) < 1e-3, n
+
+
+C4 = dict(n_a=8367, n_b=11404, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
+          norm_first=False, d_bias=False, shared_item_embed=False)
+
+
+def _c4_case(precision):
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import synth
+    import random
+    c = C4
+    seqs = synth.make_sequences(600, c['n_a'], c['n_b'], c['len_max'], seed=5, n_min=6)
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, c['n_a'], c['n_b'], c['len_max']))
+    gs, gp = GR.preprocess_graph(seqs, c['n_a'], c['n_a'] + c['n_b'] + 1)
+    args = make_args(c, dropout=0.2, precision=precision, seed=11)
+    args.batch_size = 256
+    torch.manual_seed(0)
+    tr = build_trainer(args, gs, gp)
+    return tr, tuple(torch.from_numpy(r[:256].copy()) for r in rows)
+
+
+def _c4_worker(rank, world, port, precision, out_dir):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        tr, b = _c4_case(precision)
+        assert tr.world == world and tr.dp_split
+        tr.model.train()
+        tr.optimizer.zero_grad()
+        box = capture(tr)
+        tr.model.convolve_graph()
+        loss, _, _ = tr.train_batch(b)
+        torch.cuda.synchronize()
+        if rank == 0:
+            np.savez(os.path.join(out_dir, 'c4.npz'), loss=float(loss),
+                     **{f'g/{n}': v.numpy() for n, v in box['grads'].items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_c4_ee_shape_dp_split_world2_equals_single_device(tmp_path, precision):
+    """BASELINE configs[3] (C4) shape: Entertainment-Education item counts, d=256, L=50, one global batch
+    split over two data-parallel ranks (dp_split, rows [r·B/2, (r+1)·B/2), global-count normalisation, the
+    gradient exchange of c2dsr_amd/dp.py; two ranks on cuda:0 over gloo) against the same global batch on
+    one device: the loss and every gradient agree to the summation-order level."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    mp.spawn(_c4_worker, args=(2, port, precision, str(tmp_path)), nprocs=2, join=True)
+    got = np.load(tmp_path / 'c4.npz')
+    tr, b = _c4_case(precision)
+    tr.model.train()
+    tr.optimizer.zero_grad()
+    box = capture(tr)
+    tr.model.convolve_graph()
+    loss, _, _ = tr.train_batch(b)
+    torch.cuda.synchronize()
+    assert abs(float(got['loss']) - float(loss)) <= 1e-5 * abs(float(loss))
+    tol = 1e-4 if precision == 'fp32' else 2e-3
+    for n, g in box['grads'].items():
+        assert rel(got[f'g/{n}'], g) < tol, n
