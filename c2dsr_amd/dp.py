@@ -6,10 +6,12 @@ final at known points of the backward; ``DPComm`` issues each range's collective
 RCCL on its own stream, ordered after the kernels already enqueued) the moment it is final, so the
 collectives run under the remaining backward kernels:
 
-* the **dense** ranges (every parameter that is not an item table: pos_emb, encoder, classifier heads,
-  D_a/D_b) are final once the last embedding-lookup backward (``EmbedFn.backward``, the tail of every
-  encoder pass) has run — the loss head and every encoder backward precede it by data dependence —
-  and are issued then, under the three GCN backwards;
+* the **head** range (classifier_a/b/pad, D_a/D_b: ≈26 M of the MB config's 106 M parameters) is final
+  when the loss head's backward returns (nothing else reads those parameters) and is issued then, under
+  the five encoder backwards;
+* the **dense** ranges (pos_emb and the encoders) are final once the last embedding-lookup backward
+  (``EmbedFn.backward``, the tail of every encoder pass) has run and are issued then, under the three
+  GCN backwards;
 * each **item table** (``embed_i``, ``embed_i_a``, ``embed_i_b``; one table when ``shared_item_embed``)
   is final after the last GCN backward that reads it.  That backward's last SpMM runs in row chunks
   (``GCNFn.backward`` asks ``row_cuts``) and each chunk's collective is issued as soon as the chunk is
@@ -49,7 +51,9 @@ class CommPlan:
     table ↔ flat range lo..hi; the last chunk also covers the slice's alignment padding), ``ranges`` every
     range in a fixed order (dense first, then the tables' chunks), ``index`` {(lo, hi): position}."""
 
-    def __init__(self, flat, tables, world: int, chunks: int = TABLE_CHUNKS):
+    def __init__(self, flat, tables, world: int, chunks: int = TABLE_CHUNKS, head=()):
+        """head: parameters whose gradient is final when the loss head's backward returns (their slices,
+        merged where contiguous, become ``head`` ranges issued then)."""
         self.world = world
         align = 4 * world
         ptr2 = {p.data_ptr(): (o, n, p) for _, p, o, n in flat.entries}
@@ -75,15 +79,25 @@ class CommPlan:
                     ch.append((a, b, o + a * d, hi if b == N else o + b * d))
             self.table_chunks[k] = ch
             cuts.append((o, hi))
+        tab = sorted(cuts)
+        hs = sorted({(ptr2[p.data_ptr()][0], ptr2[p.data_ptr()][0] + flat.padded(ptr2[p.data_ptr()][1]))
+                     for p in head if p.data_ptr() in ptr2 and p.data_ptr() not in self.table_chunks})
+        self.head = []
+        for a, b in hs:  # merge contiguous head slices
+            if self.head and self.head[-1][1] == a:
+                self.head[-1] = (self.head[-1][0], b)
+            else:
+                self.head.append((a, b))
         dense, lo = [], 0
-        for a, b in sorted(cuts):
+        for a, b in sorted(tab + self.head):
             if a > lo:
                 dense.append((lo, a))
             lo = max(lo, b)
         if lo < flat.numel:
             dense.append((lo, flat.numel))
         self.dense = dense
-        self.ranges = list(dense) + [(lo, hi) for ch in self.table_chunks.values() for _, _, lo, hi in ch]
+        self.ranges = list(self.head) + list(dense) + [(lo, hi) for ch in self.table_chunks.values()
+                                                       for _, _, lo, hi in ch]
         self.index = {r: i for i, r in enumerate(self.ranges)}
         pos = 0
         for lo, hi in sorted(self.ranges):  # every element in exactly one range
@@ -184,6 +198,11 @@ class DPComm:
             self.done[i] = True
             self.works.append(self.reduce(lo, hi))
             self.issued.append((lo, hi))
+
+    def head_done(self):
+        """The loss head's backward returned: the classifier / discriminator gradients are final."""
+        for lo, hi in self.plan.head:
+            self._issue(lo, hi)
 
     def lookup_done(self):
         """One embedding-lookup backward finished (EmbedFn.backward / PosDropFn.backward)."""

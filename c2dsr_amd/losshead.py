@@ -56,6 +56,7 @@ class LossMeta:
         self.__dict__.update(locals())
         del self.__dict__['self']
         self.pending = None
+        self.on_head_grads = None  # data parallel: called when the backward has written the head gradients
 
     def finish_values(self):
         """Data parallel: wait for the loss values' sums and recompute (loss, loss_rec, loss_mi) from them
@@ -343,5 +344,8 @@ class LossHeadFn(Function):
                 s)
         # the saved buffers (bf16 images, logits / lse, plans) are released with the backward even if a
         # caller keeps the graph alive (e.g. an undetached loss accumulator)
+        if m.on_head_grads is not None:  # the classifier / discriminator gradients are final: their
+            m.on_head_grads()                # collectives run under the encoder backwards (dp.py)
+            m.on_head_grads = None
         ctx.m = ctx.heads = ctx.mi = ctx.w = ctx.rsets = ctx.coefs = None
         return dh_share, dhx, dhy, dh_na, dh_nb, None

@@ -67,7 +67,12 @@ class Trainer(object):
         self.comm_plan, self.zero = None, None
         if self.world > 1:
             m = self.model
-            self.comm_plan = CommPlan(m.flat, [m.embed_i.weight, m.embed_i_a.weight, m.embed_i_b.weight], self.world)
+            head = [m.classifier_a.weight, m.classifier_a.bias, m.classifier_b.weight, m.classifier_b.bias,
+                    m.classifier_pad.weight, m.classifier_pad.bias, m.D_a.weight, m.D_b.weight]
+            if m.D_a.bias is not None:
+                head += [m.D_a.bias, m.D_b.bias]
+            self.comm_plan = CommPlan(m.flat, [m.embed_i.weight, m.embed_i_a.weight, m.embed_i_b.weight], self.world,
+                                      head=head)
             # ZeRO-1: args.zero1 or C2DSR_ZERO1=1
             if getattr(args, 'zero1', False) or os.environ.get('C2DSR_ZERO1', '0') == '1':
                 self.zero = Zero1(m.flat, self.comm_plan, self.rank, self.world)
@@ -229,6 +234,7 @@ class Trainer(object):
             # last GCN backward; all-reduce, or reduce-scatter with ZeRO-1
             tables = [m.embed_i.weight, m.embed_i_a.weight, m.embed_i_b.weight]
             m.state.grad_hook = DPComm(m.flat, self.comm_plan, 5, tables, zero=self.zero)
+            meta.on_head_grads = m.state.grad_hook.head_done  # issued as the loss head's backward returns
             try:
                 loss.backward()
             finally:

@@ -72,7 +72,7 @@ def test_dp_world2_equals_single_device(tmp_path, cfg_name, p):
 
 
 # ----------------------------------------------------------------------------- gradient exchange (dp.py)
-def _toy_store(shared, world=2, N=37, d=8):
+def _toy_store(shared, world=2, N=37, d=8, with_head=False):
     from c2dsr_amd.flat import FlatStore
     torch.manual_seed(0)
     e = torch.nn.Parameter(torch.randn(N, d))
@@ -81,9 +81,12 @@ def _toy_store(shared, world=2, N=37, d=8):
     pos = torch.nn.Parameter(torch.randn(3, d))
     w = torch.nn.Parameter(torch.randn(6, d))
     b = torch.nn.Parameter(torch.randn(6))
+    ca = torch.nn.Parameter(torch.randn(11, d))
+    cb = torch.nn.Parameter(torch.randn(11))
     named = [('pos', pos), ('embed_i.weight', e), ('embed_i_a.weight', ea), ('w', w), ('embed_i_b.weight', eb),
-             ('b', b)]
-    return FlatStore(named, torch.device('cpu'), align=4 * world), (e, ea, eb)
+             ('b', b), ('classifier_a.weight', ca), ('classifier_a.bias', cb)]
+    st = FlatStore(named, torch.device('cpu'), align=4 * world)
+    return (st, (e, ea, eb), (ca, cb)) if with_head else (st, (e, ea, eb))
 
 
 class _Done:
@@ -112,6 +115,24 @@ def test_comm_plan_tiles_flat_store(world, shared):
             own[olo:ohi] += 1
         assert z.shard_numel * world == flat.numel
     assert bool((own == 1).all())
+
+
+def test_head_ranges_issue_first():
+    """The classifier / discriminator range goes out when the loss head's backward returns, before the
+    encoder (dense) ranges and the tables; all ranges still tile the store exactly once."""
+    from c2dsr_amd.dp import CommPlan, DPComm
+    flat, tables, head = _toy_store(False, with_head=True)
+    plan = CommPlan(flat, list(tables), 2, head=list(head))
+    assert len(plan.head) == 1  # contiguous slices merged
+    dc = DPComm(flat, plan, 1, list(tables), reduce=lambda lo, hi: _Done())
+    dc.head_done()
+    assert dc.issued == plan.head
+    dc.lookup_done()
+    assert dc.issued == plan.head + plan.dense
+    for t in tables:
+        dc.table_done(t)
+    dc.finish()
+    assert sorted(dc.issued) == sorted(plan.ranges)
 
 
 @pytest.mark.parametrize('shared', [False, True])
