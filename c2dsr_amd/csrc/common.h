@@ -16,9 +16,12 @@ namespace c2 {
 
 constexpr int WAVE = 64;
 
-// Counter-based dropout hash (restated in oracle/c2dsr_oracle.py:keep_mask).
-// keep(idx) = lowbias32(lowbias32(lo(idx) ^ k0) ^ hi(idx) ^ k1) >= thr,
-// thr = floor(p * 2^32).  Stateless, so fwd and bwd regenerate the same mask.
+// Counter-based dropout hash (restated in oracle/c2dsr_oracle.py:keep_mask).  One 32-bit hash per PAIR of
+// elements, a 16-bit half for each:
+//   h(q)     = lowbias32(lowbias32(lo(q) ^ k0) ^ hi(q) ^ k1),   q = idx >> 1
+//   keep(idx) = ((h(q) >> (16 · (idx & 1))) & 0xffff) >= thr,   thr = floor(p · 2^16)
+// (p resolved to 2^-16; torch's own Bernoulli draws are float-resolution too).  Stateless, so fwd and bwd
+// regenerate the same mask; a float4 of consecutive elements costs two hashes (mul4).
 __device__ __forceinline__ uint32_t lowbias32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x7feb352dU;
@@ -28,15 +31,26 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t h) {
   return h;
 }
 
+__device__ __forceinline__ uint32_t pair_hash(uint64_t q, uint32_t k0, uint32_t k1) {
+  const uint32_t h = lowbias32((uint32_t)q ^ k0);
+  return lowbias32(h ^ (uint32_t)(q >> 32) ^ k1);
+}
+
 struct Drop {
-  uint32_t k0, k1, thr;
-  float scale;  // 1/(1-p); thr == 0 means "no dropout"
+  uint32_t k0, k1, thr;  // thr: 16-bit threshold (1..65535) or 0 = "no dropout"
+  float scale;           // 1/(1-p)
   __device__ __forceinline__ bool active() const { return thr != 0; }
   __device__ __forceinline__ float mul(uint64_t idx) const {
     if (thr == 0) return 1.0f;
-    uint32_t h = lowbias32((uint32_t)idx ^ k0);
-    h = lowbias32(h ^ (uint32_t)(idx >> 32) ^ k1);
-    return h >= thr ? scale : 0.0f;
+    const uint32_t h = pair_hash(idx >> 1, k0, k1);
+    return ((h >> (16 * (uint32_t)(idx & 1))) & 0xffffu) >= thr ? scale : 0.0f;
+  }
+  // the multipliers of elements idx .. idx+3 (idx a multiple of 2): two hashes
+  __device__ __forceinline__ float4 mul4(uint64_t idx) const {
+    if (thr == 0) return make_float4(1.f, 1.f, 1.f, 1.f);
+    const uint32_t h0 = pair_hash(idx >> 1, k0, k1), h1 = pair_hash((idx >> 1) + 1, k0, k1);
+    return make_float4((h0 & 0xffffu) >= thr ? scale : 0.f, (h0 >> 16) >= thr ? scale : 0.f,
+                       (h1 & 0xffffu) >= thr ? scale : 0.f, (h1 >> 16) >= thr ? scale : 0.f);
   }
 };
 
@@ -48,8 +62,8 @@ inline Drop make_drop(uint32_t k0, uint32_t k1, float p) {
     d.thr = 0;
     d.scale = 1.0f;
   } else {
-    double t = (double)p * 4294967296.0;
-    d.thr = t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+    double t = (double)p * 65536.0;
+    d.thr = t >= 65535.0 ? 0xffffu : (uint32_t)t;
     if (d.thr == 0) d.thr = 1;  // p so small it rounds to 0: still "active" but keeps ~all
     d.scale = (float)(1.0 / (1.0 - (double)p));
   }

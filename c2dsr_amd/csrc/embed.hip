@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
     float4 x = a + *(const float4*)(P + p * d + c);
     if (drop.active()) {
       const uint64_t b = (uint64_t)(idx_base + r) * d + c;
-      x = x * make_float4(drop.mul(b), drop.mul(b + 1), drop.mul(b + 2), drop.mul(b + 3));
+      x = x * drop.mul4(b);
     }
     *(float4*)(X + r * d + c) = x;
   }
@@ -271,7 +271,7 @@ struct RowSrc {
     float4 v = *(const float4*)(gX + (long)r * d + c);
     if (drop.active()) {
       const uint64_t b = (uint64_t)(idx_base + r) * d + c;
-      v = v * make_float4(drop.mul(b), drop.mul(b + 1), drop.mul(b + 2), drop.mul(b + 3));
+      v = v * drop.mul4(b);
     }
     return (rs ? scale * rs[r] : scale) * v;
   }
@@ -526,7 +526,7 @@ __global__ void drop_scale_kernel(const float* __restrict__ gX, long n4, int d, 
   float4 v = ((const float4*)gX)[i];
   if (drop.active()) {
     const uint64_t b = (uint64_t)idx_base * d + (uint64_t)i * 4;
-    v = v * make_float4(drop.mul(b), drop.mul(b + 1), drop.mul(b + 2), drop.mul(b + 3));
+    v = v * drop.mul4(b);
   }
   ((float4*)out)[i] = v;
 }

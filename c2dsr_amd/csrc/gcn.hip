@@ -33,7 +33,7 @@ template <bool MASK_OUT>
 __device__ __forceinline__ void epilogue(float4 acc, long row, int c, int d, const Epi& ep) {
   if (MASK_OUT && ep.drop.active()) {
     const uint64_t b = (uint64_t)row * d + c;
-    acc = acc * make_float4(ep.drop.mul(b), ep.drop.mul(b + 1), ep.drop.mul(b + 2), ep.drop.mul(b + 3));
+    acc = acc * ep.drop.mul4(b);
   }
   if (ep.Y2) *(float4*)(ep.Y2 + row * d + c) = acc;
   float4 y = ep.alpha * acc;
@@ -72,10 +72,10 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work
       if (!MASK_OUT && drop.active()) {
         const uint64_t b0 = (uint64_t)j0 * d + c, b1 = (uint64_t)j1 * d + c;
         const uint64_t b2 = (uint64_t)j2 * d + c, b3 = (uint64_t)j3 * d + c;
-        x0 = x0 * make_float4(drop.mul(b0), drop.mul(b0 + 1), drop.mul(b0 + 2), drop.mul(b0 + 3));
-        x1 = x1 * make_float4(drop.mul(b1), drop.mul(b1 + 1), drop.mul(b1 + 2), drop.mul(b1 + 3));
-        x2 = x2 * make_float4(drop.mul(b2), drop.mul(b2 + 1), drop.mul(b2 + 2), drop.mul(b2 + 3));
-        x3 = x3 * make_float4(drop.mul(b3), drop.mul(b3 + 1), drop.mul(b3 + 2), drop.mul(b3 + 3));
+        x0 = x0 * drop.mul4(b0);
+        x1 = x1 * drop.mul4(b1);
+        x2 = x2 * drop.mul4(b2);
+        x3 = x3 * drop.mul4(b3);
       }
       acc = c2::fma4(v0, x0, acc);
       acc = c2::fma4(v1, x1, acc);
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work
       float4 x = *(const float4*)(X + (long)j * d + c);
       if (!MASK_OUT && drop.active()) {
         const uint64_t b = (uint64_t)j * d + c;
-        x = x * make_float4(drop.mul(b), drop.mul(b + 1), drop.mul(b + 2), drop.mul(b + 3));
+        x = x * drop.mul4(b);
       }
       acc = c2::fma4(val[e], x, acc);
     }

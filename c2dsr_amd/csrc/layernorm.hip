@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
         float4 u = *(const float4*)(b + r * d + c);
         if (drop.active()) {
           const uint64_t bi = (uint64_t)(idx_base + (rowmap ? rowmap[r] : r)) * d + c;
-          u = u * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+          u = u * drop.mul4(bi);
         }
         v = v + u;
       }
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
           if (db_out) {
             if (drop.active()) {
               const uint64_t bi = (uint64_t)(idx_base + (rowmap ? rowmap[r] : r)) * d + c;
-              o = o * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+              o = o * drop.mul4(bi);
             }
             *(float4*)(db_out + r * d + c) = o;
           }
@@ -218,7 +218,7 @@ __global__ void add_drop_kernel(const float* __restrict__ a, const float* __rest
   float4 u = ((const float4*)b)[i];
   if (drop.active()) {
     const uint64_t bi = (uint64_t)idx_base * d + (uint64_t)i * 4;
-    u = u * make_float4(drop.mul(bi), drop.mul(bi + 1), drop.mul(bi + 2), drop.mul(bi + 3));
+    u = u * drop.mul4(bi);
   }
   if (a) u = u + ((const float4*)a)[i];
   ((float4*)y)[i] = u;

@@ -215,9 +215,7 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
         if constexpr (EPI) {
           const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
           const uint64_t idx = (uint64_t)(ep.row_base + rg_) * N + col;
-          uint32_t h = c2::lowbias32((uint32_t)idx ^ ep.drop.k0);
-          h = c2::lowbias32(h ^ (uint32_t)(idx >> 32) ^ ep.drop.k1);
-          v = fmaxf(v, 0.f) * (h >= ep.drop.thr ? ep.drop.scale : 0.f);
+          v = fmaxf(v, 0.f) * ep.drop.mul(idx);
         }
         if constexpr (AUX == AUX_ACC || AUX == AUX_ACC_MAP) v += xa[ct][r];
         if constexpr (AUX == AUX_MASK) v = xa[ct][r] > 0.f ? v * ep.aux_scale : 0.f;

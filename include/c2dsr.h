@@ -13,8 +13,9 @@
  * hipStream_t passed as void*.  Every function is asynchronous on `stream` and
  * returns 0 or a hipError_t code (hipErrorInvalidValue = 1 for bad shapes).
  * Dropout (where a `p` appears) uses the stateless counter hash
- * keep(idx) = lowbias32(lowbias32(lo(idx)^k0) ^ hi(idx) ^ k1) >= floor(p·2^32),
- * scale 1/(1-p); (k0,k1) come from (seed, step, site) — see c2dsr_amd/dropout.py.
+ * h(q) = lowbias32(lowbias32(lo(q)^k0) ^ hi(q) ^ k1) for the element pair q = idx >> 1 and
+ * keep(idx) = ((h(q) >> 16·(idx & 1)) & 0xffff) >= floor(p·2^16), scale 1/(1-p); (k0,k1) come from
+ * (seed, step, site) — see c2dsr_amd/dropout.py.
  */
 #ifndef C2DSR_H
 #define C2DSR_H

@@ -62,15 +62,18 @@ def _lowbias32(h: np.ndarray) -> np.ndarray:
 
 
 def keep_mask(idx: np.ndarray, keys: tuple[int, int], p: float) -> np.ndarray:
-    """Bernoulli(1-p) keep decision for flat element indices ``idx`` (int64)."""
+    """Bernoulli(1-p) keep decision for flat element indices ``idx`` (int64): one 32-bit hash per pair of
+    elements q = idx >> 1, a 16-bit half per element, threshold floor(p·2^16) (c2dsr_amd/csrc/common.h)."""
     if p <= 0.0:
         return np.ones(idx.shape, dtype=bool)
     idx = idx.astype(np.uint64)
+    q = idx >> np.uint64(1)
     with np.errstate(over='ignore'):
-        h = _lowbias32((idx & np.uint64(0xFFFFFFFF)).astype(np.uint32) ^ np.uint32(keys[0]))
-        h = _lowbias32(h ^ (idx >> np.uint64(32)).astype(np.uint32) ^ np.uint32(keys[1]))
-    thr = min(0xFFFFFFFF, int(math.floor(p * 4294967296.0)))
-    return h >= np.uint32(thr)
+        h = _lowbias32((q & np.uint64(0xFFFFFFFF)).astype(np.uint32) ^ np.uint32(keys[0]))
+        h = _lowbias32(h ^ (q >> np.uint64(32)).astype(np.uint32) ^ np.uint32(keys[1]))
+    half = (h >> (np.uint32(16) * (idx & np.uint64(1)).astype(np.uint32))) & np.uint32(0xFFFF)
+    thr = max(1, min(0xFFFF, int(math.floor(p * 65536.0))))
+    return half >= np.uint32(thr)
 
 
 # site ids (must match c2dsr_amd/dropout.py)
