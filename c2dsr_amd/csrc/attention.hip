@@ -559,22 +559,52 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_fast(const float* __restrict_
 // TWO, b: keys 32..63) → probabilities to the wave's save area in REGISTER layout (tile t of query tile
 // ti at pw[(2·ti + t)·1024 + 64·q + lane]: every store instruction writes 256 contiguous bytes, and the
 // backward reloads them in the same layout) and the dropped probabilities back into a / b.
-// Masks: key admissible (pad bit of kb), causal j <= i, i < L (masked entries are stored as 0).
+// Masks: see WMask (masked entries are stored as 0).
 constexpr int WAVE_PSAVE = 4096;  // floats of probability save per (sequence, head) on the wave path
 
-template <bool TWO>
-__device__ __forceinline__ void wave_softmax(f32x16& a, f32x16& b, int ti, int L, uint64_t kb, float sc,
+// Which (query, key) pairs of one wave's sequence are admissible, and where they sit in the dropout index.
+// Full layout (ROWS = false): query i and key j are sequence positions; admissible iff i < L, j <= i and
+// position j is padding (bit j of kb, Q1).  Row-subset layout (ROWS = true, c2dsr_attn_fwd_rows): queries
+// are the rows of the pass the loss reads and keys the padding rows, both compact in position order, so
+// the keys admissible to a query are a prefix of the key list: j < cq (cq = padding positions <= the
+// query's position); query / key positions (qp per lane, key j's held by lane j in kposv) give the
+// full-layout dropout index, so both layouts drop the same entries.
+struct WMask {
+  uint64_t kb;  // full: padding positions of the sequence
+  int L;        // positions per sequence (dropout index stride; full: query rows)
+  int qp[2];    // ROWS: positions of this lane's queries 32t + (lane & 31), t = 0, 1
+  int cq[2];    // ROWS: admissible key prefix of those queries (0 past the last query)
+  int kposv;    // ROWS: lane j holds the position of key j
+};
+
+template <bool ROWS>
+__device__ __forceinline__ bool wm_adm(const WMask& mk, int t, int j) {
+  if constexpr (ROWS) return j < mk.cq[t];
+  const int i = 32 * t + (threadIdx.x & 31);
+  return i < mk.L && j <= i && ((mk.kb >> j) & 1);
+}
+template <bool ROWS>
+__device__ __forceinline__ int wm_kpos(const WMask& mk, int j) {
+  if constexpr (ROWS) return __shfl(mk.kposv, j, 64);
+  return j;
+}
+template <bool ROWS>
+__device__ __forceinline__ int wm_qpos(const WMask& mk, int t) {
+  if constexpr (ROWS) return mk.qp[t];
+  return 32 * t + (threadIdx.x & 31);
+}
+
+template <bool TWO, bool ROWS>
+__device__ __forceinline__ void wave_softmax(f32x16& a, f32x16& b, int ti, const WMask& mk, float sc,
                                              const c2::Drop& drop, uint64_t pbase, float* __restrict__ prow0) {
-  const int lane = threadIdx.x & 63, r = lane & 31, hi = lane >> 5;
-  const int i = 32 * ti + r;
-  const bool row = i < L;
+  const int lane = threadIdx.x & 63;
   // admissible keys of this lane's 16 (or 32) registers as bit masks
   uint32_t m0 = 0, m1 = 0;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int j = creg(q, lane);
-    m0 |= (uint32_t)(row && j <= i && ((kb >> j) & 1)) << q;
-    if constexpr (TWO) m1 |= (uint32_t)(row && 32 + j <= i && ((kb >> (32 + j)) & 1)) << q;
+    m0 |= (uint32_t)wm_adm<ROWS>(mk, ti, j) << q;
+    if constexpr (TWO) m1 |= (uint32_t)wm_adm<ROWS>(mk, ti, 32 + j) << q;
   }
   float m = -INFINITY;
 #pragma unroll
@@ -596,37 +626,39 @@ __device__ __forceinline__ void wave_softmax(f32x16& a, f32x16& b, int ti, int L
   sum += __shfl_xor(sum, 32, 64);
   const float inv = sum > 0.f ? 1.0f / sum : 0.f;
   float* pw = prow0 + 2 * ti * 1024 + lane;
-  const uint64_t rb = pbase + (uint64_t)i * L;
+  const uint64_t rb = pbase + (uint64_t)wm_qpos<ROWS>(mk, ti) * mk.L;
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int j = creg(q, lane);
     const float p0 = a[q] * inv;
     pw[64 * q] = p0;
-    a[q] = p0 * drop.mul(rb + j);
+    a[q] = p0 * drop.mul(rb + wm_kpos<ROWS>(mk, j));
     if constexpr (TWO) {
       const float p1 = b[q] * inv;
       pw[1024 + 64 * q] = p1;
-      b[q] = p1 * drop.mul(rb + 32 + j);
+      b[q] = p1 * drop.mul(rb + wm_kpos<ROWS>(mk, 32 + j));
     }
   }
-  (void)hi;
 }
 
-template <int TJ, int TI>
-__device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const float* __restrict__ K,
-                                              const float* __restrict__ V, long rs, int L, int dh, int jmax,
-                                              uint64_t kb, const c2::Drop& drop, uint64_t pbase,
+// Q rows of stride qs (nq of them), K / V rows of stride ks (nk), O rows of stride os.  Score tiles (tj, ti):
+// t0 = (0,0), t1 = (0,1), t2 = (1,1) and, in the row-subset layout only, t3 = (1,0) (in the full layout
+// it lies above the causal diagonal; compact queries can see keys of higher index).
+template <int TJ, int TI, bool ROWS>
+__device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, long qs, const float* __restrict__ K,
+                                              const float* __restrict__ V, long ks, int nq, int dh, int nk,
+                                              const WMask& mk, const c2::Drop& drop, uint64_t pbase,
                                               float* __restrict__ o_row0, long os, float* __restrict__ prow0) {
+  constexpr bool T3 = ROWS && TJ > 1;
   const int lane = threadIdx.x & 63, r = lane & 31, hi = lane >> 5;
-  // tiles (tj, ti): 0 = (0,0), 1 = (0,1), 2 = (1,1)
-  f32x16 t0, t1, t2;
+  f32x16 t0, t1, t2, t3;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) t0[q] = t1[q] = t2[q] = 0.f;
+  for (int q = 0; q < 16; ++q) t0[q] = t1[q] = t2[q] = t3[q] = 0.f;
   {
-    const auto qsrc = rows_rsrc(Q, L, rs, dh);
-    const auto ksrc = rows_rsrc(K, jmax, rs, dh);
-    const int q0o = (r * (int)rs + 4 * hi) * 4, q1o = ((32 + r) * (int)rs + 4 * hi) * 4;
-    const int k0o = q0o, k1o = q1o;
+    const auto qsrc = rows_rsrc(Q, nq, qs, dh);
+    const auto ksrc = rows_rsrc(K, nk, ks, dh);
+    const int q0o = (r * (int)qs + 4 * hi) * 4, q1o = ((32 + r) * (int)qs + 4 * hi) * 4;
+    const int k0o = (r * (int)ks + 4 * hi) * 4, k1o = ((32 + r) * (int)ks + 4 * hi) * 4;
     const int CS = dh >> 3;
     constexpr int SU = 2;  // c-steps per register buffer, two buffers in flight
     float4 ba[SU][4], bb[SU][4];  // [c-step][k0, k1, q0, q1]
@@ -650,6 +682,7 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           t0 = WMFMA(ka[e], qa[e], t0, 0, 0, 0);
+          if constexpr (T3) t3 = WMFMA(kc[e], qa[e], t3, 0, 0, 0);
           if constexpr (TI > 1) t1 = WMFMA(ka[e], qc[e], t1, 0, 0, 0);
           if constexpr (TI > 1 && TJ > 1) t2 = WMFMA(kc[e], qc[e], t2, 0, 0, 0);
         }
@@ -666,17 +699,17 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const
     }
   }
   const float sc = 1.0f / sqrtf((float)dh);
-  wave_softmax<false>(t0, t0, 0, L, kb, sc, drop, pbase, prow0);
-  if constexpr (TI > 1) wave_softmax<(TJ > 1)>(t1, t2, 1, L, kb, sc, drop, pbase, prow0);
+  wave_softmax<T3, ROWS>(t0, t3, 0, mk, sc, drop, pbase, prow0);
+  if constexpr (TI > 1) wave_softmax<(TJ > 1), ROWS>(t1, t2, 1, mk, sc, drop, pbase, prow0);
   // O = Pd·V per 32-column tile of the head (two waves per SIMD hide each other's V loads)
-  const auto vsrc = rows_rsrc(V, jmax, rs, dh);
+  const auto vsrc = rows_rsrc(V, nk, ks, dh);
   auto vload = [&](float (&v)[2][16], int ct) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int key = (q & 3) + 8 * (q >> 2) + 4 * hi;  // the key of register q (lane half hi)
-      v[0][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrc, (key * (int)rs + 32 * ct + r) * 4, 0, 0));
+      v[0][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrc, (key * (int)ks + 32 * ct + r) * 4, 0, 0));
       v[1][q] = TJ > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                             vsrc, ((32 + key) * (int)rs + 32 * ct + r) * 4, 0, 0))
+                             vsrc, ((32 + key) * (int)ks + 32 * ct + r) * 4, 0, 0))
                        : 0.f;
     }
   };
@@ -687,6 +720,7 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       o0 = WMFMA(t0[q], v[0][q], o0, 0, 0, 0);
+      if constexpr (T3) o0 = WMFMA(t3[q], v[1][q], o0, 0, 0, 0);
       if constexpr (TI > 1) {
         o1 = WMFMA(t1[q], v[0][q], o1, 0, 0, 0);
         if constexpr (TJ > 1) o1 = WMFMA(t2[q], v[1][q], o1, 0, 0, 0);
@@ -696,8 +730,8 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int i0 = creg(q, lane), i1 = 32 + i0;
-      if (i0 < L) o_row0[(long)i0 * os + c] = o0[q];
-      if (TI > 1 && i1 < L) o_row0[(long)i1 * os + c] = o1[q];
+      if (i0 < nq) o_row0[(long)i0 * os + c] = o0[q];
+      if (TI > 1 && i1 < nq) o_row0[(long)i1 * os + c] = o1[q];
     }
   };
   const int CT = dh >> 5;
@@ -709,17 +743,26 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, const
   }
 }
 
+// the wave's sequence in the full layout: padding bits and key extent (one past the last padding key)
+__device__ __forceinline__ WMask full_mask(const int64_t* __restrict__ seq, int64_t pad, int b, int L, int& jmax) {
+  const int lane = threadIdx.x & 63;
+  const bool ok = lane < L && seq[(long)b * L + lane] == pad;
+  WMask mk;
+  mk.kb = __ballot(ok);
+  mk.L = L;
+  jmax = mk.kb ? 64 - __clzll((long long)mk.kb) : 0;
+  return mk;
+}
+
 __global__ __launch_bounds__(256) void attn_fwd_wave(const float* __restrict__ qkv, const int64_t* __restrict__ seq,
                                                      int64_t pad, int B, int L, int d, int H, c2::Drop drop,
                                                      int64_t b_base, float* __restrict__ out,
                                                      float* __restrict__ Psave) {
-  const int lane = threadIdx.x & 63;
   const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bh >= B * H) return;  // uniform over the wave
   const int b = bh / H, h = bh % H, dh = d / H;
-  const bool ok = lane < L && seq[(long)b * L + lane] == pad;
-  const uint64_t kb = __ballot(ok);
-  const int jmax = kb ? 64 - __clzll((long long)kb) : 0;
+  int jmax;
+  const WMask mk = full_mask(seq, pad, b, L, jmax);
   const long rs = 3l * d;
   const float* Q = qkv + (long)b * L * rs + h * dh;
   const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
@@ -727,11 +770,69 @@ __global__ __launch_bounds__(256) void attn_fwd_wave(const float* __restrict__ q
   float* prow = Psave + (long)bh * WAVE_PSAVE;
   const int TJ = jmax > 32 ? 2 : 1, TI = L > 32 ? 2 : 1;
   if (TI == 1)
-    fwd_wave_body<1, 1>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
+    fwd_wave_body<1, 1, false>(Q, rs, Q + d, Q + 2 * d, rs, L, dh, jmax, mk, drop, pbase, orow, d, prow);
   else if (TJ == 1)
-    fwd_wave_body<1, 2>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
+    fwd_wave_body<1, 2, false>(Q, rs, Q + d, Q + 2 * d, rs, L, dh, jmax, mk, drop, pbase, orow, d, prow);
   else
-    fwd_wave_body<2, 2>(Q, Q + d, Q + 2 * d, rs, L, dh, jmax, kb, drop, pbase, orow, d, prow);
+    fwd_wave_body<2, 2, false>(Q, rs, Q + d, Q + 2 * d, rs, L, dh, jmax, mk, drop, pbase, orow, d, prow);
+}
+
+// the wave's sequence in the row-subset layout: compact query rows [q0, q0 + nq) and key rows [k0, k0 + nk)
+// (q_off / k_off per sequence; q_idx / k_idx hold global rows b·L + position)
+__device__ __forceinline__ WMask rows_mask(const int64_t* __restrict__ seq, int64_t pad, int b, int L,
+                                           const int* __restrict__ q_idx, const int* __restrict__ q_off,
+                                           const int* __restrict__ k_idx, const int* __restrict__ k_off, int& q0,
+                                           int& nq, int& k0, int& nk) {
+  const int lane = threadIdx.x & 63;
+  q0 = __builtin_amdgcn_readfirstlane(q_off[b]);
+  nq = __builtin_amdgcn_readfirstlane(q_off[b + 1]) - q0;
+  k0 = __builtin_amdgcn_readfirstlane(k_off[b]);
+  nk = __builtin_amdgcn_readfirstlane(k_off[b + 1]) - k0;
+  nq = min(max(nq, 0), L);
+  nk = min(max(nk, 0), L);
+  const bool ok = lane < L && seq[(long)b * L + lane] == pad;
+  const uint64_t kb = __ballot(ok);
+  WMask mk;
+  mk.kb = kb;
+  mk.L = L;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int i = 32 * t + (lane & 31);
+    const int qp = i < nq ? q_idx[q0 + i] - b * L : 0;
+    const uint64_t upto = qp >= 63 ? ~0ull : ((2ull << qp) - 1ull);  // positions 0..qp
+    mk.qp[t] = qp;
+    mk.cq[t] = i < nq ? min((int)__popcll(kb & upto), nk) : 0;
+  }
+  mk.kposv = lane < nk ? k_idx[k0 + lane] - b * L : 0;
+  return mk;
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_rows(const float* __restrict__ q, const float* __restrict__ kv,
+                                                     const int64_t* __restrict__ seq, int64_t pad,
+                                                     const int* __restrict__ q_idx, const int* __restrict__ q_off,
+                                                     const int* __restrict__ k_idx, const int* __restrict__ k_off,
+                                                     int B, int L, int d, int H, c2::Drop drop, int64_t b_base,
+                                                     float* __restrict__ out, float* __restrict__ Psave) {
+  const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bh >= B * H) return;  // uniform over the wave
+  const int b = bh / H, h = bh % H, dh = d / H;
+  int q0, nq, k0, nk;
+  const WMask mk = rows_mask(seq, pad, b, L, q_idx, q_off, k_idx, k_off, q0, nq, k0, nk);
+  if (nq == 0) return;  // uniform
+  const float* Q = q + (long)q0 * d + h * dh;
+  const float* K = kv + (long)k0 * 2 * d + h * dh;
+  const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
+  float* orow = out + (long)q0 * d + h * dh;
+  float* prow = Psave + (long)bh * WAVE_PSAVE;
+  const int TJ = nk > 32 ? 2 : 1, TI = nq > 32 ? 2 : 1;
+  if (TI == 1 && TJ == 1)
+    fwd_wave_body<1, 1, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
+  else if (TI == 1)
+    fwd_wave_body<2, 1, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
+  else if (TJ == 1)
+    fwd_wave_body<1, 2, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
+  else
+    fwd_wave_body<2, 2, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -755,25 +856,26 @@ __device__ __forceinline__ void zero16(f32x16& a) {
   for (int q = 0; q < 16; ++q) a[q] = 0.f;
 }
 
-// acc (+)= A·B over one 32-key (or 32-query) tile: A from registers / LDS (per step r), B one float per
-// lane per step from a buffer descriptor at rows rowof(r) (relative), column c.
-// OT: element type of dqkv (float, or bf16 when its only consumers — the in_proj backward GEMMs — read
-// it as a bf16 MFMA operand anyway: c2dsr_attn_bwd_b16)
-template <int TJ, int TI, typename OT>
-__device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const float* __restrict__ K,
-                                              const float* __restrict__ V, const float* __restrict__ dO,
-                                              long rs, long ds, int L, int dh, int jmax, uint64_t kb,
+// OT: element type of dQ / dK / dV (float, or bf16 when their only consumers — the in_proj backward GEMMs —
+// read them as a bf16 MFMA operand anyway: c2dsr_attn_bwd_b16).  Strides: Q qs, K / V ks, dO ds, dQ dqs,
+// dK / dV dks; nkw: key rows of dK / dV to write (rows past the key tiles get zeros).  Tiles as in
+// fwd_wave_body (g3 = (1,0) in the row-subset layout only).
+template <int TJ, int TI, typename OT, bool ROWS>
+__device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long qs, const float* __restrict__ K,
+                                              const float* __restrict__ V, long ks, const float* __restrict__ dO,
+                                              long ds, int nq, int dh, int nk, const WMask& mk,
                                               const c2::Drop& drop, uint64_t pbase, const float* __restrict__ prow0,
-                                              OT* __restrict__ dQ, OT* __restrict__ dK, OT* __restrict__ dV,
-                                              float* T) {
+                                              OT* __restrict__ dQ, long dqs, OT* __restrict__ dK,
+                                              OT* __restrict__ dV, long dks, int nkw, float* T) {
+  constexpr bool T3 = ROWS && TJ > 1;
   const int lane = threadIdx.x & 63, r = lane & 31, hi = lane >> 5;
-  // ---- dPᵀ tiles (tj, ti): 0 = (0,0), 1 = (0,1), 2 = (1,1)
-  f32x16 g0, g1, g2;
-  zero16(g0); zero16(g1); zero16(g2);
+  // ---- dPᵀ tiles (tj, ti): 0 = (0,0), 1 = (0,1), 2 = (1,1), 3 = (1,0)
+  f32x16 g0, g1, g2, g3;
+  zero16(g0); zero16(g1); zero16(g2); zero16(g3);
   {
-    const auto vsrc = rows_rsrc(V, jmax, rs, dh);
-    const auto osrc = rows_rsrc(dO, L, ds, dh);
-    const int v0o = (r * (int)rs + 4 * hi) * 4, v1o = ((32 + r) * (int)rs + 4 * hi) * 4;
+    const auto vsrc = rows_rsrc(V, nk, ks, dh);
+    const auto osrc = rows_rsrc(dO, nq, ds, dh);
+    const int v0o = (r * (int)ks + 4 * hi) * 4, v1o = ((32 + r) * (int)ks + 4 * hi) * 4;
     const int o0o = (r * (int)ds + 4 * hi) * 4, o1o = ((32 + r) * (int)ds + 4 * hi) * 4;
     const int CS = dh >> 3;
 #pragma unroll 1
@@ -796,6 +898,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           g0 = WMFMA(ka[e], qa[e], g0, 0, 0, 0);
+          if constexpr (T3) g3 = WMFMA(kc[e], qa[e], g3, 0, 0, 0);
           if constexpr (TI > 1) g1 = WMFMA(ka[e], qc[e], g1, 0, 0, 0);
           if constexpr (TI > 1 && TJ > 1) g2 = WMFMA(kc[e], qc[e], g2, 0, 0, 0);
         }
@@ -803,28 +906,25 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
     }
   }
   // ---- softmax gradient per query (lane): P reloaded, dS into g*, Pd into p*
-  f32x16 p0, p1, p2;
+  f32x16 p0, p1, p2, p3;
   auto sgrad = [&](f32x16& g_a, f32x16& g_b, f32x16& p_a, f32x16& p_b, bool two, int ti) {
-    const int i = 32 * ti + r;
-    const bool row = i < L;
+    // rows past the queries were saved as 0 (every register of a computed tile is stored)
+    const bool row = ROWS || 32 * ti + r < mk.L;
     const float* pw = prow0 + 2 * ti * 1024 + lane;  // the forward's register-layout save (wave_softmax)
-    const uint64_t rb = pbase + (uint64_t)i * L;
+    const uint64_t rb = pbase + (uint64_t)wm_qpos<ROWS>(mk, ti) * mk.L;
     float acc = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int j0 = creg(q, lane), j1 = 32 + j0;
       const float pa = row ? pw[64 * q] : 0.f;
       const float pb = two && row ? pw[1024 + 64 * q] : 0.f;
-      const float ma = drop.mul(rb + j0), mb = two ? drop.mul(rb + j1) : 0.f;
-      const bool ada = row && j0 <= i && ((kb >> j0) & 1), adb = two && row && j1 <= i && ((kb >> j1) & 1);
+      const float ma = drop.mul(rb + wm_kpos<ROWS>(mk, j0)), mb = two ? drop.mul(rb + wm_kpos<ROWS>(mk, j1)) : 0.f;
+      const bool ada = wm_adm<ROWS>(mk, ti, j0), adb = two && wm_adm<ROWS>(mk, ti, j1);
       g_a[q] = ada ? g_a[q] * ma : 0.f;
       g_b[q] = adb ? g_b[q] * mb : 0.f;
       acc += pa * g_a[q] + pb * g_b[q];
       p_a[q] = pa;
       p_b[q] = pb;
-      // keep the masks for Pd: stash them in the dPm slots' partner after the row sum
-      (void)ma;
-      (void)mb;
     }
     acc += __shfl_xor(acc, 32, 64);
 #pragma unroll
@@ -832,31 +932,34 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
       const int j0 = creg(q, lane), j1 = 32 + j0;
       g_a[q] = p_a[q] * (g_a[q] - acc);
       g_b[q] = two ? p_b[q] * (g_b[q] - acc) : 0.f;
-      p_a[q] = p_a[q] * drop.mul(rb + j0);
-      p_b[q] = two ? p_b[q] * drop.mul(rb + j1) : 0.f;
+      p_a[q] = p_a[q] * drop.mul(rb + wm_kpos<ROWS>(mk, j0));
+      p_b[q] = two ? p_b[q] * drop.mul(rb + wm_kpos<ROWS>(mk, j1)) : 0.f;
     }
   };
   {
     f32x16 zg, zp;
     zero16(zg); zero16(zp);
-    zero16(p1); zero16(p2);
-    sgrad(g0, zg, p0, zp, false, 0);
+    zero16(p1); zero16(p2); zero16(p3);
+    if constexpr (T3)
+      sgrad(g0, g3, p0, p3, true, 0);
+    else
+      sgrad(g0, zg, p0, zp, false, 0);
     if constexpr (TI > 1) sgrad(g1, g2, p1, p2, TJ > 1, 1);
   }
   const float sc = 1.0f / sqrtf((float)dh);
   const int CT = dh >> 5;
   // ---- dQ = dS·K/√dh (lane = column, rows = queries)
   {
-    const auto ksrc = rows_rsrc(K, jmax, rs, dh);
+    const auto ksrc = rows_rsrc(K, nk, ks, dh);
 #pragma unroll 1
     for (int ct = 0; ct < CT; ++ct) {
       float k0v[16], k1v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int key = (q & 3) + 8 * (q >> 2) + 4 * hi;
-        k0v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrc, (key * (int)rs + 32 * ct + r) * 4, 0, 0));
+        k0v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrc, (key * (int)ks + 32 * ct + r) * 4, 0, 0));
         k1v[q] = TJ > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                              ksrc, ((32 + key) * (int)rs + 32 * ct + r) * 4, 0, 0))
+                              ksrc, ((32 + key) * (int)ks + 32 * ct + r) * 4, 0, 0))
                         : 0.f;
       }
       f32x16 o0, o1;
@@ -864,6 +967,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         o0 = WMFMA(g0[q], k0v[q], o0, 0, 0, 0);
+        if constexpr (T3) o0 = WMFMA(g3[q], k1v[q], o0, 0, 0, 0);
         if constexpr (TI > 1) {
           o1 = WMFMA(g1[q], k0v[q], o1, 0, 0, 0);
           if constexpr (TJ > 1) o1 = WMFMA(g2[q], k1v[q], o1, 0, 0, 0);
@@ -873,8 +977,8 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i0 = creg(q, lane), i1 = 32 + i0;
-        if (i0 < L) dQ[(long)i0 * rs + c] = (OT)(sc * o0[q]);
-        if (TI > 1 && i1 < L) dQ[(long)i1 * rs + c] = (OT)(sc * o1[q]);
+        if (i0 < nq) dQ[(long)i0 * dqs + c] = (OT)(sc * o0[q]);
+        if (TI > 1 && i1 < nq) dQ[(long)i1 * dqs + c] = (OT)(sc * o1[q]);
       }
     }
   }
@@ -889,8 +993,8 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
       if (two) T[i * TLD + 32 + j0] = b[q];
     }
   };
-  auto keys_out = [&](const float* __restrict__ Src, long ss, int nrows, float scale, OT* __restrict__ Dst) {
-    const auto src = rows_rsrc(Src, nrows, ss, dh);
+  auto keys_out = [&](const float* __restrict__ Src, long ss, float scale, OT* __restrict__ Dst) {
+    const auto src = rows_rsrc(Src, nq, ss, dh);
 #pragma unroll 1
     for (int ct = 0; ct < CT; ++ct) {
       float b0v[16], b1v[16];  // Src rows (queries) of register q: (q&3) + 8(q>>2) + 4hi (+32)
@@ -908,7 +1012,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
         f32x16 o;
         zero16(o);
 #pragma unroll
-        for (int ti = tj; ti < TI; ++ti) {
+        for (int ti = ROWS ? 0 : tj; ti < TI; ++ti) {
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int qi = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * hi;
@@ -919,26 +1023,26 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, const
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int j = 32 * tj + creg(q, lane);
-          if (j < L) Dst[(long)j * rs + c] = (OT)(scale * o[q]);
+          if (j < nkw) Dst[(long)j * dks + c] = (OT)(scale * o[q]);
         }
       }
-      for (int j = 32 * TJ + hi; j < L; j += 2) Dst[(long)j * rs + c] = (OT)0.f;  // keys past the tiles
+      for (int j = 32 * TJ + hi; j < nkw; j += 2) Dst[(long)j * dks + c] = (OT)0.f;  // keys past the tiles
     }
   };
   // T starts as garbage: every entry the products read ([0, 32·TI) x [0, 32·TJ)) is written first
-  put(p0, p0, false, 0);
+  put(p0, p3, T3, 0);
   if constexpr (TI > 1) put(p1, p2, TJ > 1, 1);
-  if constexpr (TJ > 1) {  // tile (tj = 1, ti = 0) is above the diagonal: zero
+  if constexpr (!ROWS && TJ > 1) {  // full layout: tile (tj = 1, ti = 0) is above the diagonal: zero
 #pragma unroll
     for (int q = 0; q < 16; ++q) T[r * TLD + 32 + creg(q, lane)] = 0.f;
   }
   wave_lds_sync();
-  keys_out(dO, ds, L, 1.0f, dV);
+  keys_out(dO, ds, 1.0f, dV);
   wave_lds_sync();
-  put(g0, g0, false, 0);
+  put(g0, g3, T3, 0);
   if constexpr (TI > 1) put(g1, g2, TJ > 1, 1);
   wave_lds_sync();
-  keys_out(Q, rs, L, sc, dK);
+  keys_out(Q, qs, sc, dK);
 }
 
 template <typename OT>
@@ -947,13 +1051,12 @@ __global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ q
                                                      int64_t b_base, const float* __restrict__ Psave,
                                                      const float* __restrict__ dout, OT* __restrict__ dqkv) {
   __shared__ float tbuf[4][64 * 65];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6;
   const int bh = blockIdx.x * 4 + w;
   if (bh >= B * H) return;  // uniform over the wave (no block-level barriers below)
   const int b = bh / H, h = bh % H, dh = d / H;
-  const bool ok = lane < L && seq[(long)b * L + lane] == pad;
-  const uint64_t kb = __ballot(ok);
-  const int jmax = kb ? 64 - __clzll((long long)kb) : 0;
+  int jmax;
+  const WMask mk = full_mask(seq, pad, b, L, jmax);
   const long rs = 3l * d;
   const float* Q = qkv + (long)b * L * rs + h * dh;
   const float* dO = dout + (long)b * L * d + h * dh;
@@ -961,12 +1064,61 @@ __global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ q
   const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
   const float* prow = Psave + (long)bh * WAVE_PSAVE;
   const int TJ = jmax > 32 ? 2 : 1, TI = L > 32 ? 2 : 1;
+#define BWD_FULL(TJ_, TI_)                                                                                     \
+  bwd_wave_body<TJ_, TI_, OT, false>(Q, rs, Q + d, Q + 2 * d, rs, dO, d, L, dh, jmax, mk, drop, pbase, prow, dQ, rs, \
+                                     dQ + d, dQ + 2 * d, rs, L, tbuf[w])
   if (TI == 1)
-    bwd_wave_body<1, 1, OT>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+    BWD_FULL(1, 1);
   else if (TJ == 1)
-    bwd_wave_body<1, 2, OT>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+    BWD_FULL(1, 2);
   else
-    bwd_wave_body<2, 2, OT>(Q, Q + d, Q + 2 * d, dO, rs, d, L, dh, jmax, kb, drop, pbase, prow, dQ, dQ + d, dQ + 2 * d, tbuf[w]);
+    BWD_FULL(2, 2);
+#undef BWD_FULL
+}
+
+template <typename OT>
+__global__ __launch_bounds__(256) void attn_bwd_rows(const float* __restrict__ q, const float* __restrict__ kv,
+                                                     const int64_t* __restrict__ seq, int64_t pad,
+                                                     const int* __restrict__ q_idx, const int* __restrict__ q_off,
+                                                     const int* __restrict__ k_idx, const int* __restrict__ k_off,
+                                                     int B, int L, int d, int H, c2::Drop drop, int64_t b_base,
+                                                     const float* __restrict__ Psave, const float* __restrict__ dout,
+                                                     OT* __restrict__ dq, OT* __restrict__ dkv) {
+  __shared__ float tbuf[4][64 * 65];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bh = blockIdx.x * 4 + w;
+  if (bh >= B * H) return;  // uniform over the wave (no block-level barriers below)
+  const int b = bh / H, h = bh % H, dh = d / H;
+  int q0, nq, k0, nk;
+  const WMask mk = rows_mask(seq, pad, b, L, q_idx, q_off, k_idx, k_off, q0, nq, k0, nk);
+  OT* dK = dkv + (long)k0 * 2 * d + h * dh;
+  if (nq == 0) {  // no query of this sequence is read: its keys get no gradient
+    for (int e = lane; e < nk * dh; e += 64) {
+      const int j = e / dh, c = e % dh;
+      dK[(long)j * 2 * d + c] = (OT)0.f;
+      dK[(long)j * 2 * d + d + c] = (OT)0.f;
+    }
+    return;
+  }
+  const float* Q = q + (long)q0 * d + h * dh;
+  const float* K = kv + (long)k0 * 2 * d + h * dh;
+  const float* dO = dout + (long)q0 * d + h * dh;
+  OT* dQ = dq + (long)q0 * d + h * dh;
+  const uint64_t pbase = (uint64_t)((b_base + b) * H + h) * L * L;
+  const float* prow = Psave + (long)bh * WAVE_PSAVE;
+  const int TJ = nk > 32 ? 2 : 1, TI = nq > 32 ? 2 : 1;
+#define BWD_ROWS(TJ_, TI_)                                                                                     \
+  bwd_wave_body<TJ_, TI_, OT, true>(Q, d, K, K + d, 2l * d, dO, d, nq, dh, nk, mk, drop, pbase, prow, dQ, d, dK,  \
+                                    dK + d, 2l * d, nk, tbuf[w])
+  if (TI == 1 && TJ == 1)
+    BWD_ROWS(1, 1);
+  else if (TI == 1)
+    BWD_ROWS(2, 1);
+  else if (TJ == 1)
+    BWD_ROWS(1, 2);
+  else
+    BWD_ROWS(2, 2);
+#undef BWD_ROWS
 }
 
 template <int LP>
@@ -1076,6 +1228,48 @@ C2_API int c2dsr_attn_bwd_b16(const float* qkv, const int64_t* seq, int64_t pad,
   c2::Drop dr = c2::make_drop(k0, k1, p);
   attn_bwd_wave<bf16><<<c2::ceil_div((long)B * H, 4), 256, 0, (hipStream_t)stream>>>(
       qkv, seq, pad, B, L, d, H, dr, b_base, Psave, dout, (bf16*)dqkv);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Row-subset attention (the last post-norm encoder layer of a training pass, whose output the loss reads
+// only at the rows of a RowSet): queries are those rows, keys the padding rows (the only admissible ones,
+// Q1), both compact in position order per sequence — q [nq_total, d] (row q_off[b] + i = query i of
+// sequence b, global row q_idx[...]), kv [nk_total, 2d] (K | V, row k_off[b] + j), out [nq_total, d].
+// Same masks, dropout indices and Psave layout (B·H·4096 floats) as c2dsr_attn_fwd's wave path; the
+// outputs at the query rows equal the full-layout ones up to the order of the key sums.
+C2_API int c2dsr_attn_rows_supported(int L, int d, int H) { return c2dsr_attn_bwd_b16_supported(L, d, H); }
+
+C2_API int c2dsr_attn_fwd_rows(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
+                               const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H,
+                               uint32_t k0, uint32_t k1, float p, int64_t b_base, float* out, float* Psave,
+                               void* stream) {
+  if (!c2dsr_attn_rows_supported(L, d, H)) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  attn_fwd_rows<<<c2::ceil_div((long)B * H, 4), 256, 0, (hipStream_t)stream>>>(
+      q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, c2::make_drop(k0, k1, p), b_base, out, Psave);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// dq [nq_total, d], dkv [nk_total, 2d]: fp32 (out_bf16 = 0) or bf16 (1; their consumers, the in_proj
+// backward GEMMs, read them as a bf16 MFMA operand)
+C2_API int c2dsr_attn_bwd_rows(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
+                               const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H,
+                               uint32_t k0, uint32_t k1, float p, int64_t b_base, const float* Psave,
+                               const float* dout, void* dq, void* dkv, int out_bf16, void* stream) {
+  if (!c2dsr_attn_rows_supported(L, d, H)) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  const c2::Drop dr = c2::make_drop(k0, k1, p);
+  const dim3 grid(c2::ceil_div((long)B * H, 4));
+  hipStream_t s = (hipStream_t)stream;
+  if (out_bf16)
+    attn_bwd_rows<bf16><<<grid, 256, 0, s>>>(q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, dr, b_base,
+                                             Psave, dout, (bf16*)dq, (bf16*)dkv);
+  else
+    attn_bwd_rows<float><<<grid, 256, 0, s>>>(q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, dr, b_base,
+                                              Psave, dout, (float*)dq, (float*)dkv);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -231,7 +231,7 @@ struct NeedOp {
   static constexpr int NS = 8;
   const int64_t *gm_a, *gm_b;
   int L, R, n_sets, bits;
-  int *idx, *inv, *count;
+  int *idx, *inv, *count, *off;  // off (may be null): [n_sets][B + 1] first compact row of each sequence
   long M;
   __device__ uint32_t mask(int r) const {
     const uint32_t a = gm_a[r] != 0, b = gm_b[r] != 0, tail = r % L >= L - R;
@@ -244,9 +244,41 @@ struct NeedOp {
     if (q >= n_sets) return;
     if (in) idx[q * M + k] = r;
     inv[q * M + r] = in ? k : -1;
+    if (off && r % L == 0) off[q * (M / L + 1) + r / L] = k;
   }
   __device__ void totals(const int* tot) const {
-    for (int q = 0; q < n_sets; ++q) count[q] = tot[q];
+    for (int q = 0; q < n_sets; ++q) {
+      count[q] = tot[q];
+      if (off) off[q * (M / L + 1) + M / L] = tot[q];
+    }
+  }
+};
+
+// Padding rows of up to 8 encoder passes (the only admissible attention keys, Q1): set q = rows with
+// seqs[q·M + r] == pad; idx / inv / count / off as NeedOp.
+struct PadOp {
+  static constexpr int NS = 8;
+  const int64_t* seqs;
+  int64_t pad;
+  int L, n_sets;
+  int *idx, *inv, *count, *off;
+  long M;
+  __device__ uint32_t mask(int r) const {
+    uint32_t m = 0;
+    for (int q = 0; q < n_sets; ++q) m |= (seqs[q * M + r] == pad) ? (1u << q) : 0u;
+    return m;
+  }
+  __device__ void put(int q, int r, uint32_t in, int k) const {
+    if (q >= n_sets) return;
+    if (in) idx[q * M + k] = r;
+    inv[q * M + r] = in ? k : -1;
+    if (r % L == 0) off[q * (M / L + 1) + r / L] = k;
+  }
+  __device__ void totals(const int* tot) const {
+    for (int q = 0; q < n_sets; ++q) {
+      count[q] = tot[q];
+      off[q * (M / L + 1) + M / L] = tot[q];
+    }
   }
 };
 
@@ -275,6 +307,21 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, long ld, const
     const int c = (int)(i % d);
     dst[k * d + c] = src[(long)idx[k] * ld + c];
   }
+}
+
+// dst[r][c] = (ia >= 0 ? a[ia·d + c] : 0) + (ib >= 0 ? b[ib·d + c] : 0), ia = inv_a[r], ib = inv_b[r]
+__global__ void combine_rows_kernel(const float* __restrict__ a, const int* __restrict__ inv_a,
+                                    const float* __restrict__ b, const int* __restrict__ inv_b, int M, int d4,
+                                    float* __restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)M * d4) return;
+  const long r = i / d4;
+  const int c = (int)(i % d4) * 4;
+  const int ia = inv_a[r], ib = inv_b[r];
+  const long d = 4l * d4;
+  const float4 x = ia >= 0 ? *(const float4*)(a + ia * d + c) : c2::f4(0.f);
+  const float4 y = ib >= 0 ? *(const float4*)(b + ib * d + c) : c2::f4(0.f);
+  *(float4*)(dst + r * d + c) = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
 }
 
 // dst[r][c] = inv[r] >= 0 ? src[inv[r]·d + c] : 0   (r < M)
@@ -569,12 +616,35 @@ C2_API int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, i
   return compact_rows(ValidOp{t, split, ignore, idx, inv, tc, counts}, M, ws, s);
 }
 C2_API int c2dsr_need_rows(const int64_t* gm_a, const int64_t* gm_b, int B, int L, int R, int n_sets, int bits,
-                           int* idx, int* inv, int* count, int* ws, void* stream) {
+                           int* idx, int* inv, int* count, int* off, int* ws, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (B < 0 || L <= 0 || n_sets < 1 || n_sets > 8) return (int)hipErrorInvalidValue;
-  if (B == 0) return (int)hipMemsetAsync(count, 0, n_sets * sizeof(int), s);
+  if (B == 0) {
+    if (off) (void)hipMemsetAsync(off, 0, n_sets * sizeof(int), s);
+    return (int)hipMemsetAsync(count, 0, n_sets * sizeof(int), s);
+  }
   const int M = B * L;
-  return compact_rows(NeedOp{gm_a, gm_b, L, R, n_sets, bits, idx, inv, count, (long)M}, M, ws, s);
+  return compact_rows(NeedOp{gm_a, gm_b, L, R, n_sets, bits, idx, inv, count, off, (long)M}, M, ws, s);
+}
+C2_API int c2dsr_pad_rows(const int64_t* seqs, int64_t pad, int B, int L, int n_sets, int* idx, int* inv, int* count,
+                          int* off, int* ws, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (B < 0 || L <= 0 || n_sets < 1 || n_sets > 8 || !off) return (int)hipErrorInvalidValue;
+  if (B == 0) {
+    (void)hipMemsetAsync(off, 0, n_sets * sizeof(int), s);
+    return (int)hipMemsetAsync(count, 0, n_sets * sizeof(int), s);
+  }
+  const int M = B * L;
+  return compact_rows(PadOp{seqs, pad, L, n_sets, idx, inv, count, off, (long)M}, M, ws, s);
+}
+C2_API int c2dsr_combine_rows(const float* a, const int* inv_a, const float* b, const int* inv_b, int M, int d,
+                              float* dst, void* stream) {
+  if (M <= 0) return 0;
+  if (d <= 0 || d % 4) return (int)hipErrorInvalidValue;
+  const long work = (long)M * d / 4;
+  combine_rows_kernel<<<c2::ceil_div(work, 256), 256, 0, (hipStream_t)stream>>>(a, inv_a, b, inv_b, M, d / 4, dst);
+  C2_CHECK_LAUNCH();
+  return 0;
 }
 C2_API int c2dsr_gather_rows(const float* src, long ld, const int* idx, int n, int d, float* dst, void* stream) {
   if (n <= 0 || d <= 0) return 0;

@@ -494,7 +494,9 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
                       float p, int64_t row_base, const int* rowmap, int aux_mode, const float* aux,
                       const int* auxmap, float aux_scale, void* stream) {
   if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
-  if (ab16 && (K != 768 || epilogue || aux_mode == AUX_MASK)) return (int)hipErrorInvalidValue;
+  if (ab16 && (epilogue || aux_mode == AUX_MASK || (K != 768 && aux_mode == AUX_ACC_MAP) ||
+               (K == 512 && aux_mode != AUX_NONE)))
+    return (int)hipErrorInvalidValue;
   if (aux_mode < 0 || aux_mode > 3 || (aux_mode && (!aux || epilogue))) return (int)hipErrorInvalidValue;
   if ((aux_mode == AUX_ACC_MAP) != (auxmap != nullptr) || (aux_mode == AUX_ACC_MAP && aux == C))
     return (int)hipErrorInvalidValue;
@@ -511,7 +513,7 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
   const int CT = K == 256 ? 2 : 1;
   const int G = c2::ceil_div(N, 128 * CT);
   // persistent grid: exactly the workgroups that are resident at once (occupancy of the variant)
-  static int per_cu[18] = {0};
+  static int per_cu[21] = {0};
   auto launch = [&](void (*kern)(int, int, int, const void*, long, const bf16*, long, float*, long, Epi2, int),
                     int slot) -> int {
     if (!per_cu[slot]) {
@@ -526,7 +528,12 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
   };
   int rc;
   const bool e = epilogue == 1;
-  if (ab16) {  // K = 768: the in_proj backward over the attention's bf16 dqkv
+  if (ab16 && K == 256) {  // the row-subset attention's bf16 dq (+ the parked LN gradient)
+    rc = aux_mode == AUX_ACC ? launch(rg_kernel<1, 2, false, AUX_ACC, true>, 18)
+                             : launch(rg_kernel<1, 2, false, AUX_NONE, true>, 19);
+  } else if (ab16 && K == 512) {  // ... and its bf16 dkv
+    rc = launch(rg_kernel<2, 1, false, AUX_NONE, true>, 20);
+  } else if (ab16) {  // K = 768: the in_proj backward over the attention's bf16 dqkv
     if (aux_mode == AUX_ACC)
       rc = launch(rg_kernel<3, 1, false, AUX_ACC, true>, 15);
     else if (aux_mode == AUX_ACC_MAP)

@@ -66,6 +66,7 @@ class StepState:
         self.grad_hook = None  # c2dsr_amd.dp.DPComm while a data-parallel backward runs
         self.plans = {}  # (step, data_ptr, numel, n_keys) -> ops.IndexPlan (sorted on the side stream)
         self.need = {}   # pass_id -> ops.RowSet: rows of the pass the loss reads (set by Trainer.train_batch)
+        self.pad_rows = {}  # pass_id -> ops.RowSet: its padding rows, the attention's keys (idem)
         self.compact_out = False  # encoder outputs of such passes stay [n, d] (the loss reads them through rs.inv)
 
     def keys(self, site):
@@ -131,11 +132,18 @@ class SelfAttention(nn.Module):
                 # LayerNorm run on those rows (dropout indices through the row map, so the masks are the
                 # full-size run's).
                 r1 = ops.ResidualLink(inv=rs.inv)
-                o = ops.QKVAttnFn.apply(x.contiguous(), at.in_proj_weight, at.in_proj_bias, seq, self.idx_pad,
-                                        self.n_head, p_at, k_at, self.state.row_offset, self.precision, r1)
-                oc = ops.GatherRowsFn.apply(o.reshape(B * L, d), rs)
-                sa = ops.linear(oc, at.out_proj.weight, at.out_proj.bias, self.precision)
                 xc = ops.gather_rows_nograd(x.reshape(B * L, d), rs)
+                ks = self.state.pad_rows.get(pass_id)
+                if ks is not None and ops.attn_rows_ok(L, d, self.n_head):
+                    # Q only at these rows, K / V only at the padding rows (the only admissible keys, Q1)
+                    oc = ops.RowsQKVAttnFn.apply(x.contiguous(), xc, at.in_proj_weight, at.in_proj_bias, seq,
+                                                 self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset,
+                                                 self.precision, rs, ks, r1)
+                else:
+                    o = ops.QKVAttnFn.apply(x.contiguous(), at.in_proj_weight, at.in_proj_bias, seq, self.idx_pad,
+                                            self.n_head, p_at, k_at, self.state.row_offset, self.precision, r1)
+                    oc = ops.GatherRowsFn.apply(o.reshape(B * L, d), rs)
+                sa = ops.linear(oc, at.out_proj.weight, at.out_proj.bias, self.precision)
                 x1 = ops.AddLNFn.apply(xc, sa, lay.norm1.weight, lay.norm1.bias, p_sa, k_sa, rb_rows, lay.norm1.eps,
                                        r1, rs.idx)
                 r2 = ops.ResidualLink()

@@ -276,12 +276,13 @@ class HostCounts:
 
 
 class RowSet:
-    """The rows of one encoder pass the loss reads (c2dsr_need_rows): idx [n] (ascending), inv [M] (compact
-    index or -1).  The last encoder layer runs its row-wise part on these rows only.  ``n`` may be given
-    as (HostCounts, slot), read when first needed."""
+    """The rows of one encoder pass the loss reads (c2dsr_need_rows) — or its padding rows, the attention's
+    keys (c2dsr_pad_rows): idx [n] (ascending), inv [M] (compact index or -1).  The last encoder layer runs
+    its row-wise part on these rows only.  ``n`` may be given as (HostCounts, slot), read when first needed."""
 
-    def __init__(self, idx, inv, n, M):
+    def __init__(self, idx, inv, n, M, off=None):
         self.idx, self.inv, self.M = idx, inv, int(M)
+        self.off = off  # [B + 1] compact index of each sequence's first row (c2dsr_need_rows / c2dsr_pad_rows)
         self._n = n
 
     @property
@@ -705,6 +706,108 @@ class QKVAttnFn(Function):
 
 
 _B16_DQKV = __import__('os').environ.get('C2DSR_B16_DQKV', '1') == '1'
+
+
+def attn_rows_ok(L, d, n_head):
+    return bool(lib.raw('c2dsr_attn_rows_supported')(L, d, n_head))
+
+
+def _proj(x, W, b, y, precision):
+    """y = x·Wᵀ + b (x fp32 [M, K], W a row range of a projection weight)."""
+    N, K = W.shape
+    M = x.shape[0]
+    if M == 0:
+        return y
+    if precision == BF16 and rgemm_ok(M, N, K):
+        rgemm(x, weight_bf16(W), y, M=M, N=N, K=K, bias=b)
+    else:
+        gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
+    return y
+
+
+def _proj_backward(x, W, dy, dx, acc, gW, gb, precision):
+    """dx (+)= dy·W  (acc: dx holds a gradient to add to) and gW += dyᵀ·x, gb += Σ dy for y = x·Wᵀ + b over a
+    row range of the weight; dy fp32 or bf16 (then every product takes the bf16-operand kernels)."""
+    N, K = W.shape
+    M = x.shape[0]
+    if M == 0:
+        return
+    if precision == BF16 and rgemm_ok(M, K, N):
+        rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC if acc else 0,
+              aux=dx if acc else None)
+    else:
+        gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0 if acc else 0.0, precision=precision)
+    if gW is not None and precision == BF16 and wgemm_ok(M, N, K):
+        wgemm(dy, x, gW, T=M, N=N, D=K, db=gb)
+    else:
+        if gW is not None:
+            gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=precision)
+        if gb is not None:
+            colsum(dy, M, N, N, gb)
+
+
+class RowsQKVAttnFn(Function):
+    """The in_proj + attention core of the LAST post-norm encoder layer of a training pass, on the rows that
+    matter only (models/encoders.py:33 → MultiheadAttention; everything after the attention is row-wise and
+    the loss reads the rows of ``rs``): Q is projected for the query rows rs (from xc = x[rs], the rows the
+    layer's residual reads too), K / V for the padding rows ks — the only keys any query may attend to (Q1) —
+    and the attention runs on those compact rows (c2dsr_attn_fwd_rows).  Returns the [n_q, d] attention
+    output of the rs rows, equal to the full layer's at those rows up to the order of the key sums.
+    Backward: dq, dkv (bf16 in bf16 mode, as QKVAttnFn) → dx = dq·Wq (+ the parked LN gradient of the rs rows,
+    ResidualLink) on the query rows + dkv·Wkv on the key rows, combined into the [B, L, d] input gradient
+    (rows in neither set get 0: nothing downstream reads them)."""
+
+    @staticmethod
+    def forward(ctx, x, xc, W, b, seq, pad, n_head, p, keys, b_base, precision, rs, ks, res=None):
+        require_device(x)
+        B, L, d = x.shape
+        if not attn_rows_ok(L, d, n_head) or rs.off is None or ks.off is None:
+            raise HipLibError('RowsQKVAttnFn: unsupported shape or row sets without per-sequence offsets')
+        nq, nk = rs.n, ks.n
+        xk = torch.empty(nk, d, device=x.device, dtype=torch.float32)
+        if nk:
+            lib('c2dsr_gather_rows', x.detach(), d, ks.idx, nk, d, xk, stream())
+        q = _proj(xc, W[:d], b[:d], torch.empty(nq, d, device=x.device, dtype=torch.float32), precision)
+        kv = _proj(xk, W[d:], b[d:], torch.empty(nk, 2 * d, device=x.device, dtype=torch.float32), precision)
+        out = torch.empty(nq, d, device=x.device, dtype=torch.float32)
+        P = torch.empty(int(lib.raw('c2dsr_attn_psave_floats')(B, L, d, n_head)), device=x.device,
+                        dtype=torch.float32)
+        lib('c2dsr_attn_fwd_rows', q, kv, seq, int(pad), rs.idx, rs.off, ks.idx, ks.off, B, L, d, n_head, keys[0],
+            keys[1], float(p), int(b_base), out, P, stream())
+        ctx.save_for_backward(xc, xk, W, q, kv, seq, P)
+        ctx.b, ctx.pad, ctx.n_head, ctx.p, ctx.keys, ctx.b_base = b, pad, n_head, p, keys, b_base
+        ctx.precision, ctx.rs, ctx.ks, ctx.res, ctx.shape = precision, rs, ks, res, (B, L, d)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xc, xk, W, q, kv, seq, P = ctx.saved_tensors
+        B, L, d = ctx.shape
+        rs, ks = ctx.rs, ctx.ks
+        nq, nk = q.shape[0], kv.shape[0]
+        s = stream()
+        b16 = (ctx.precision == BF16 and _B16_DQKV and rgemm_ok(max(nq, 1), d, d) and rgemm_ok(max(nk, 1), d, 2 * d)
+               and wgemm_ok(max(nq, 1), d, d) and wgemm_ok(max(nk, 1), 2 * d, d))
+        gt = torch.bfloat16 if b16 else torch.float32
+        dq = torch.empty(nq, d, device=q.device, dtype=gt)
+        dkv = torch.empty(nk, 2 * d, device=q.device, dtype=gt)
+        lib('c2dsr_attn_bwd_rows', q, kv, seq, int(ctx.pad), rs.idx, rs.off, ks.idx, ks.off, B, L, d, ctx.n_head,
+            ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.b_base), P, dout.contiguous(), dq, dkv, int(b16), s)
+        park = None
+        if ctx.res is not None:
+            park, ctx.res.grad = ctx.res.grad, None
+        gW, gb = _grad_target(W), _grad_target(ctx.b)
+        dxq = park if park is not None else torch.empty(nq, d, device=q.device, dtype=torch.float32)
+        _proj_backward(xc, W[:d], dq, dxq, park is not None, None if gW is None else gW[:d],
+                       None if gb is None else gb[:d], ctx.precision)
+        dxk = torch.empty(nk, d, device=q.device, dtype=torch.float32)
+        _proj_backward(xk, W[d:], dkv, dxk, False, None if gW is None else gW[d:], None if gb is None else gb[d:],
+                       ctx.precision)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(B, L, d, device=q.device, dtype=torch.float32)
+            lib('c2dsr_combine_rows', dxq, rs.inv, dxk, ks.inv, B * L, d, dx, s)
+        return (dx,) + (None,) * 13
 
 
 # ----------------------------------------------------------------------------- residual / layernorm

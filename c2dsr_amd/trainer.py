@@ -88,6 +88,8 @@ class Trainer(object):
         self.n_item_b = args.n_item_b
         self.len_rec = args.len_rec
         self.compact_rows = os.environ.get('C2DSR_ROW_COMPACT', '1') == '1'
+        # last-layer attention on the read rows / padding keys only (ops.RowsQKVAttnFn)
+        self.rows_attn = os.environ.get('C2DSR_ROWS_ATTN', '1') == '1'
         self.lambda_loss = args.lambda_loss
         self.dp_split = True  # slice each global batch across data-parallel ranks
 
@@ -137,14 +139,16 @@ class Trainer(object):
     PASS_ROWS = ((DK.PASS_SHARE, 1 | 2 | 4), (DK.PASS_A, 1 | 4), (DK.PASS_B, 2 | 4), (DK.PASS_NEG0, 1),
                  (DK.PASS_NEG0 + 1, 2))
 
-    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b):
+    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b, seqs=None):
         """Index work the step sizes its launches by, enqueued ahead of the forward with one deferred host
         read of all its counts (ops.HostCounts; nothing waits until the first count is needed):
           * RowSets of the five encoder passes (c2dsr_need_rows), so the last encoder layer runs its
-            row-wise part only where the loss looks;
+            row-wise part only where the loss looks, and (seqs: the passes' sequences in PASS_ROWS order)
+            their padding rows (c2dsr_pad_rows), the only keys its attention can use;
           * per classifier head, the stacked [share; specific] targets of the last R positions
             (c2dsr_rec_targets) and their valid-row compaction (c2dsr_compact_valid) for the fused CE.
-        Returns (need: {pass_id: RowSet}, ce_pre: [(tcat, idx, inv, tc, (HostCounts, slot)), ...] or None)."""
+        Returns (need: {pass_id: RowSet}, pads: {pass_id: RowSet},
+                 ce_pre: [(tcat, idx, inv, tc, (HostCounts, slot)), ...] or None)."""
         m = self.model
         B, L = gm_a.shape
         M, R = B * L, self.len_rec
@@ -152,17 +156,26 @@ class Trainer(object):
         s = stream()
         i32 = dict(device=dev, dtype=torch.int32)
         counts = []
-        need_sets = None
+        need_sets = pad_sets = None
         if self.compact_rows and m.training and not m.attn_share.norm_first:
             n = len(self.PASS_ROWS)
             idx = torch.empty(n, M, **i32)
             inv = torch.empty(n, M, **i32)
             cnt = torch.empty(n, **i32)
+            off = torch.empty(n, B + 1, **i32)
             ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, **i32)
             code = sum(bits << (3 * q) for q, (_, bits) in enumerate(self.PASS_ROWS))
-            lib('c2dsr_need_rows', gm_a, gm_b, B, L, R, n, code, idx, inv, cnt, ws, s)
-            need_sets = (idx, inv)
+            lib('c2dsr_need_rows', gm_a, gm_b, B, L, R, n, code, idx, inv, cnt, off, ws, s)
+            need_sets = (idx, inv, off)
             counts.append(cnt)
+            if seqs is not None and self.rows_attn and ops.attn_rows_ok(L, self.d_latent, m.attn_share.n_head):
+                sq = torch.stack([x.reshape(M) for x in seqs])
+                pidx, pinv = torch.empty(n, M, **i32), torch.empty(n, M, **i32)
+                pcnt, poff = torch.empty(n, **i32), torch.empty(n, B + 1, **i32)
+                pws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, **i32)
+                lib('c2dsr_pad_rows', sq, int(m.attn_share.idx_pad), B, L, n, pidx, pinv, pcnt, poff, pws, s)
+                pad_sets = (pidx, pinv, poff)
+                counts.append(pcnt)
         ce = None
         if m.precision == ops.BF16 and bool(lib.raw('c2dsr_ce_supported')(self.d_latent)):
             M2 = 2 * B * R
@@ -190,17 +203,20 @@ class Trainer(object):
             lib('c2dsr_loss_partials', None, tg[0], self.n_item_a, None, tg[1], self.n_item_b, B * R, cvec, s)
             self.dp_counts = (cvec, dist.all_reduce(cvec, async_op=True))
         if not counts:
-            return {}, None
+            return {}, {}, None
         hc = ops.HostCounts(torch.cat(counts))
-        need = {}
-        if need_sets is not None:
-            idx, inv = need_sets
-            need = {pid: ops.RowSet(idx[q], inv[q], (hc, q), M) for q, (pid, _) in enumerate(self.PASS_ROWS)}
+        need, pads = {}, {}
+        base = 0
+        for sets, out in ((need_sets, need), (pad_sets, pads)):
+            if sets is not None:
+                idx, inv, off = sets
+                out.update({pid: ops.RowSet(idx[q], inv[q], (hc, base + q), M, off[q])
+                            for q, (pid, _) in enumerate(self.PASS_ROWS)})
+                base += len(self.PASS_ROWS)
         ce_pre = None
         if ce is not None:
-            base = len(self.PASS_ROWS) if need_sets is not None else 0
             ce_pre = [c + ((hc, base + 2 * k),) for k, c in enumerate(ce)]
-        return need, ce_pre
+        return need, pads, ce_pre
 
     def train_batch(self, batch, *, global_rows=None):
         """trainer.py:91-160.  ``batch``: 14 int64 [B, L] tensors (host or device).  Under data
@@ -212,14 +228,15 @@ class Trainer(object):
         m = self.model
         m.state.row_offset = row_offset
         self.dp_counts = None
-        need, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b)
-        m.state.need, m.state.compact_out = need, bool(need)
+        need, pads, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b,
+                                          (seq_share, seq_a, seq_b, neg_a, neg_b))
+        m.state.need, m.state.pad_rows, m.state.compact_out = need, pads, bool(need)
         try:
             h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
             h_neg_a = m.forward_share(neg_a, pos)
             h_neg_b = m.forward_share(neg_b, pos)
         finally:
-            m.state.need, m.state.compact_out = {}, False
+            m.state.need, m.state.pad_rows, m.state.compact_out = {}, {}, False
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
         meta.ce_pre = ce_pre
         if self.dp_counts is not None:

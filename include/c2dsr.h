@@ -98,6 +98,20 @@ int c2dsr_attn_bwd_b16_supported(int L, int d, int H);
 int c2dsr_attn_bwd_b16(const float* qkv, const int64_t* seq, int64_t pad, int B, int L, int d, int H, uint32_t k0,
                        uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout, void* dqkv,
                        void* stream);
+/* Row-subset attention (the last post-norm encoder layer of a training pass; wave kernels only,
+ * c2dsr_attn_rows_supported): queries = the rows the loss reads, keys = the padding rows, compact per
+ * sequence in position order.  q [nq, d] (row q_off[b] + i: query i of sequence b, global row
+ * q_idx[q_off[b] + i] = b·L + position), kv [nk, 2d] (K | V; k_idx / k_off likewise), out [nq, d],
+ * Psave B·H·4096 floats; masks and dropout indices as c2dsr_attn_fwd at those positions.  Backward:
+ * dq [nq, d], dkv [nk, 2d], fp32 or (out_bf16) bf16. */
+int c2dsr_attn_rows_supported(int L, int d, int H);
+int c2dsr_attn_fwd_rows(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
+                        const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H, uint32_t k0,
+                        uint32_t k1, float p, int64_t b_base, float* out, float* Psave, void* stream);
+int c2dsr_attn_bwd_rows(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
+                        const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H, uint32_t k0,
+                        uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout, void* dq,
+                        void* dkv, int out_bf16, void* stream);
 
 /* Residual + dropout + LayerNorm (TransformerEncoderLayer norm1/norm2, encoder.norm; eps 1e-8). */
 int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
@@ -139,9 +153,18 @@ int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, int* idx
 /* Rows of the encoder passes the loss reads (trainer.py:101-154), n_sets <= 8 at once: set q's code is
  * (bits >> 3q) & 7 — 1 / 2 = positions with gm_a / gm_b nonzero (the pass's pooling weights), 4 = the
  * last R positions (classifier heads).  idx / inv of set q at offset q·B·L: idx[k] = k-th needed row,
- * inv[r] = compact index or -1; count[q] = set size. */
+ * inv[r] = compact index or -1; count[q] = set size; off (may be null) [n_sets][B+1]: off[q][b] = compact
+ * index of sequence b's first row (off[q][B] = count[q]). */
 int c2dsr_need_rows(const int64_t* gm_a, const int64_t* gm_b, int B, int L, int R, int n_sets, int bits, int* idx,
-                    int* inv, int* count, int* ws, void* stream);
+                    int* inv, int* count, int* off, int* ws, void* stream);
+/* Padding rows of n_sets <= 8 encoder passes (the attention's only admissible keys, Q1): set q = rows r of
+ * seqs [n_sets][B·L] with seqs[q][r] == pad; idx / inv / count / off (required) as c2dsr_need_rows. */
+int c2dsr_pad_rows(const int64_t* seqs, int64_t pad, int B, int L, int n_sets, int* idx, int* inv, int* count,
+                   int* off, int* ws, void* stream);
+/* dst[r] = (inv_a[r] >= 0 ? a[inv_a[r]] : 0) + (inv_b[r] >= 0 ? b[inv_b[r]] : 0), rows of d floats (d % 4 == 0):
+ * the input gradient of the row-subset attention layer (query rows + key rows) */
+int c2dsr_combine_rows(const float* a, const int* inv_a, const float* b, const int* inv_b, int M, int d, float* dst,
+                       void* stream);
 /* dst[k][:] = src[idx[k]·ld + :] (k < n);  dst[r][:] = inv[r] >= 0 ? src[inv[r]][:] : 0 (r < M) */
 int c2dsr_gather_rows(const float* src, long ld, const int* idx, int n, int d, float* dst, void* stream);
 int c2dsr_expand_rows(const float* src, const int* inv, int M, int d, float* dst, void* stream);
@@ -256,8 +279,9 @@ int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B,
                     float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                     int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
                     float aux_scale, void* stream);
-/* c2dsr_rgemm_aux with A in bf16 (K = 768: the in_proj dX over the attention's bf16 dqkv; no epilogue,
- * aux modes 0 / 1 / 3) — the products equal the fp32-A call's, which rounds A to bf16 the same way. */
+/* c2dsr_rgemm_aux with A in bf16 (the in_proj dX over the attention's bf16 gradient; no epilogue): K = 768
+ * (dqkv; aux modes 0 / 1 / 3), K = 256 (the row-subset layer's dq; aux modes 0 / 1), K = 512 (its dkv;
+ * aux mode 0) — the products equal the fp32-A call's, which rounds A to bf16 the same way. */
 int c2dsr_rgemm_aux_b16a(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
                          float alpha, float beta, const float* bias, int aux_mode, const float* aux, const int* auxmap,
                          void* stream);

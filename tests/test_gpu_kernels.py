@@ -571,20 +571,68 @@ def test_need_rows_compaction(B, L, R):
     idx = torch.full((n, M), -7, device=DEV, dtype=torch.int32)
     inv = torch.empty(n, M, device=DEV, dtype=torch.int32)
     cnt = torch.empty(n, device=DEV, dtype=torch.int32)
+    off = torch.empty(n, B + 1, device=DEV, dtype=torch.int32)
     ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, device=DEV, dtype=torch.int32)
     bits = sum(c << (3 * q) for q, c in enumerate(codes))
     lib('c2dsr_need_rows', torch.from_numpy(gm_a).to(DEV), torch.from_numpy(gm_b).to(DEV), B, L, R, n, bits, idx,
-        inv, cnt, ws, stream())
+        inv, cnt, off, ws, stream())
     tail = np.broadcast_to(np.arange(L) >= L - R, (B, L)).reshape(-1)
     a, b = gm_a.reshape(-1) != 0, gm_b.reshape(-1) != 0
     for q, c in enumerate(codes):
         need = (a if c & 1 else False) | (b if c & 2 else False) | (tail if c & 4 else False)
-        want = np.nonzero(need)[0]
-        assert int(cnt[q]) == len(want)
-        assert np.array_equal(idx[q, :len(want)].cpu().numpy(), want)
-        winv = np.full(M, -1)
-        winv[want] = np.arange(len(want))
-        assert np.array_equal(inv[q].cpu().numpy(), winv)
+        _check_row_set(need, idx[q], inv[q], cnt[q], off[q], B, L)
+
+
+def _check_row_set(need, idx, inv, cnt, off, B, L):
+    M = B * L
+    want = np.nonzero(need)[0]
+    assert int(cnt) == len(want)
+    assert np.array_equal(idx[:len(want)].cpu().numpy(), want)
+    winv = np.full(M, -1)
+    winv[want] = np.arange(len(want))
+    assert np.array_equal(inv.cpu().numpy(), winv)
+    woff = np.concatenate([[0], np.cumsum(need.reshape(B, L).sum(1))])
+    assert np.array_equal(off.cpu().numpy(), woff)
+
+
+@pytest.mark.parametrize('B,L', [(1, 7), (37, 50), (2048, 50)])
+def test_pad_rows_compaction(B, L):
+    """c2dsr_pad_rows: padding rows of five sequences at once, with per-sequence offsets."""
+    from c2dsr_amd._lib import lib, stream
+    g = np.random.default_rng(B + 1)
+    pad = 77
+    seqs = g.integers(0, 70, (5, B, L))
+    seqs[g.random((5, B, L)) < 0.45] = pad
+    seqs[0, :, :L // 2] = pad  # left padding
+    seqs[1, 0] = pad           # an all-padding sequence
+    seqs[2, -1] = 3            # one without padding
+    M, n = B * L, 5
+    idx = torch.full((n, M), -7, device=DEV, dtype=torch.int32)
+    inv = torch.empty(n, M, device=DEV, dtype=torch.int32)
+    cnt = torch.empty(n, device=DEV, dtype=torch.int32)
+    off = torch.empty(n, B + 1, device=DEV, dtype=torch.int32)
+    ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, device=DEV, dtype=torch.int32)
+    lib('c2dsr_pad_rows', torch.from_numpy(seqs).to(DEV), pad, B, L, n, idx, inv, cnt, off, ws, stream())
+    for q in range(n):
+        _check_row_set(seqs[q].reshape(-1) == pad, idx[q], inv[q], cnt[q], off[q], B, L)
+
+
+def test_combine_rows():
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(5)
+    M, d = 3001, 256
+    ma, mb = torch.rand(M, generator=g) < 0.4, torch.rand(M, generator=g) < 0.6
+    inv_a = torch.full((M,), -1, dtype=torch.int32)
+    inv_a[ma] = torch.arange(int(ma.sum()), dtype=torch.int32)
+    inv_b = torch.full((M,), -1, dtype=torch.int32)
+    inv_b[mb] = torch.arange(int(mb.sum()), dtype=torch.int32)
+    a, b = torch.randn(int(ma.sum()), d, generator=g), torch.randn(int(mb.sum()), d, generator=g)
+    out = torch.empty(M, d, device=DEV)
+    lib('c2dsr_combine_rows', a.to(DEV), inv_a.to(DEV), b.to(DEV), inv_b.to(DEV), M, d, out, stream())
+    want = torch.zeros(M, d)
+    want[ma] += a
+    want[mb] += b
+    assert torch.equal(out.cpu(), want)
 
 
 @pytest.mark.parametrize('M', [1, 1000, 1024, 40960])
@@ -705,3 +753,103 @@ def test_gemm_split_k_deterministic():
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
     assert rel(outs[0], C0.double() + A.double().T @ B.double()) < 1e-5
+
+
+# ----------------------------------------------------------------------------- row-subset attention
+def _rows_case(B, L, seed, q_frac):
+    """Sequences with padding anywhere (left-padded, scattered, none, all) and a query-row subset."""
+    g = np.random.default_rng(seed)
+    pad = 999
+    seq = g.integers(0, 900, (B, L))
+    for b in range(B):
+        kind = b % 4
+        if kind == 0:
+            seq[b, :g.integers(0, L + 1)] = pad
+        elif kind == 1:
+            seq[b, g.random(L) < 0.5] = pad
+        elif kind == 2 and b % 8 == 2:
+            seq[b, :] = pad
+        # kind 3 / the rest: no padding
+    need = g.random((B, L)) < q_frac
+    need[:, -3:] = True
+    need[B // 2] = False  # a sequence with no query row
+    return pad, seq, need
+
+
+def _row_set(mask):
+    from c2dsr_amd.ops import RowSet
+    B, L = mask.shape
+    flat = mask.reshape(-1)
+    idx = np.nonzero(flat)[0].astype(np.int32)
+    inv = np.full(B * L, -1, np.int32)
+    inv[idx] = np.arange(len(idx), dtype=np.int32)
+    off = np.concatenate([[0], np.cumsum(mask.sum(1))]).astype(np.int32)
+    t = lambda a: torch.from_numpy(a).to(DEV)  # noqa: E731
+    return RowSet(t(idx), t(inv), len(idx), B * L, t(off)), idx
+
+
+@pytest.mark.parametrize('B,L,d,H,p,q_frac', [(64, 50, 256, 1, 0.2, 0.4), (40, 64, 256, 2, 0.0, 0.9),
+                                              (24, 32, 64, 2, 0.3, 0.5), (9, 64, 32, 1, 0.1, 0.2)])
+def test_attention_rows_equals_full_layout(B, L, d, H, p, q_frac):
+    """c2dsr_attn_fwd_rows / _bwd_rows (queries = a row subset, keys = the padding rows, compact) against the
+    full-layout wave kernels on the same q / k / v: the output and dq at the query rows, dk / dv at the
+    padding rows (the full layout's other rows of dk / dv are 0 when dout is 0 off the query rows)."""
+    from c2dsr_amd._lib import lib, stream
+    pad, seq, need = _rows_case(B, L, B * L + d, q_frac)
+    rs, qi = _row_set(need)
+    ks, ki = _row_set(seq == pad)
+    torch.manual_seed(B)
+    qkv = torch.randn(B * L, 3 * d, device=DEV)
+    dout_c = torch.randn(len(qi), d, device=DEV)
+    dout = torch.zeros(B * L, d, device=DEV)
+    dout[torch.from_numpy(qi).long().to(DEV)] = dout_c
+    sd = torch.from_numpy(seq).to(DEV)
+    s = stream()
+    nP = int(lib.raw('c2dsr_attn_psave_floats')(B, L, d, H))
+    P, Pr = torch.empty(nP, device=DEV), torch.empty(nP, device=DEV)
+    out = torch.empty(B * L, d, device=DEV)
+    lib('c2dsr_attn_fwd', qkv, sd, pad, B, L, d, H, 5, 6, p, 2, out, P, s)
+    g = torch.empty_like(qkv)
+    lib('c2dsr_attn_bwd', qkv, sd, pad, B, L, d, H, 5, 6, p, 2, P, dout, g, s)
+    qL, kL = torch.from_numpy(qi).long().to(DEV), torch.from_numpy(ki).long().to(DEV)
+    q = qkv[qL, :d].contiguous()
+    kv = qkv[kL, d:].contiguous()
+    out_r = torch.empty(len(qi), d, device=DEV)
+    lib('c2dsr_attn_fwd_rows', q, kv, sd, pad, rs.idx, rs.off, ks.idx, ks.off, B, L, d, H, 5, 6, p, 2, out_r, Pr, s)
+    dq = torch.full((len(qi), d), 7.0, device=DEV)
+    dkv = torch.full((len(ki), 2 * d), 7.0, device=DEV)
+    lib('c2dsr_attn_bwd_rows', q, kv, sd, pad, rs.idx, rs.off, ks.idx, ks.off, B, L, d, H, 5, 6, p, 2, Pr, dout_c,
+        dq, dkv, 0, s)
+    dq16 = torch.empty(len(qi), d, device=DEV, dtype=torch.bfloat16)
+    dkv16 = torch.empty(len(ki), 2 * d, device=DEV, dtype=torch.bfloat16)
+    lib('c2dsr_attn_bwd_rows', q, kv, sd, pad, rs.idx, rs.off, ks.idx, ks.off, B, L, d, H, 5, 6, p, 2, Pr, dout_c,
+        dq16, dkv16, 1, s)
+    torch.cuda.synchronize()
+    assert rel(out_r, out[qL]) < 2e-6
+    assert rel(dq, g[qL, :d]) < 2e-6
+    assert rel(dkv, g[kL, d:]) < 2e-6
+    assert torch.equal(dq16, dq.to(torch.bfloat16)) and torch.equal(dkv16, dkv.to(torch.bfloat16))
+    # rows with no admissible key (no padding at or before them) are exactly 0 in both
+    assert torch.equal(out_r[out[qL].abs().amax(1) == 0], torch.zeros_like(out_r[out[qL].abs().amax(1) == 0]))
+
+
+@pytest.mark.parametrize('K,aux', [(256, 0), (256, 1), (512, 0)])
+def test_rgemm_b16a_row_subset_shapes(K, aux):
+    """bf16-A dX products of the row-subset layer (dq: K = 256 with the parked LN gradient, dkv: K = 512) equal
+    the fp32-A call bit for bit."""
+    from c2dsr_amd.ops import AUX_ACC, rgemm, to_bf16
+    M, N = 2113, 256
+    g = torch.Generator().manual_seed(K + aux)
+    A16 = torch.randn(M, K, generator=g).to(DEV).to(torch.bfloat16)
+    Wb = to_bf16(torch.randn(K, N, generator=g).to(DEV), trans=True)
+    base = torch.randn(M, N, generator=g).to(DEV)
+    outs = []
+    for A in (A16, A16.float()):
+        C = base.clone()
+        if aux:
+            rgemm(A, Wb, C, M=M, N=N, K=K, aux_mode=AUX_ACC, aux=C)
+        else:
+            rgemm(A, Wb, C, M=M, N=N, K=K)
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
