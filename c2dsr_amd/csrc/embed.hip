@@ -266,9 +266,20 @@ struct RowSrc {
   int64_t idx_base;
   float scale;
   const float* rs;  // optional per-row multiplier
+  // optional: row r is the sum of two compact sources, gX[map1[r]] + gX2[map2[r]] (entries < 0: absent) —
+  // the row-subset attention layer's input gradient (query rows + key rows, ops.RowsQKVAttnFn)
+  const int *map1, *map2;
+  const float* gX2;
   __device__ __forceinline__ float4 load(uint32_t r, int c) const {
     if (!gX) return make_float4(c == 0 ? (rs ? scale * rs[r] : scale) : 0.f, 0.f, 0.f, 0.f);  // the row (1, 0, …)
-    float4 v = *(const float4*)(gX + (long)r * d + c);
+    float4 v;
+    if (map1) {
+      const int a = map1[r], b = map2[r];
+      v = a >= 0 ? *(const float4*)(gX + (long)a * d + c) : c2::f4(0.f);
+      if (b >= 0) v = v + *(const float4*)(gX2 + (long)b * d + c);
+    } else {
+      v = *(const float4*)(gX + (long)r * d + c);
+    }
     if (drop.active()) {
       const uint64_t b = (uint64_t)(idx_base + r) * d + c;
       v = v * drop.mul4(b);
@@ -595,10 +606,12 @@ size_t seg_ws_bytes(int n, int d) { return 2 * seg_slot_bytes(n, d) + seg_slot2_
 
 // sort idx[0..n) (values < n_keys) → k0/v0 sorted (key, original row), stable; then the work lists
 int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t s) {
-  prep_keys_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(idx, n, w.k0, w.v0);
   int bits = 1;
   while ((1l << bits) < (long)n_keys) ++bits;
-  uint32_t *ki = w.k0, *vi = w.v0, *ko = w.k1, *vo = w.v1;
+  // the passes alternate between the two buffer pairs: start in the pair the last pass does not write
+  const bool odd = ((bits + 7) / 8) & 1;
+  uint32_t *ki = odd ? w.k1 : w.k0, *vi = odd ? w.v1 : w.v0, *ko = odd ? w.k0 : w.k1, *vo = odd ? w.v0 : w.v1;
+  prep_keys_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(idx, n, ki, vi);
   for (int shift = 0; shift < bits; shift += 8) {
     rs_hist_kernel<<<w.nblocks, RS_THREADS, 0, s>>>(ki, n, shift, w.nblocks, w.hist);
     rs_scan_kernel<<<1, 1024, 0, s>>>(w.hist, 256 * w.nblocks);
@@ -606,7 +619,7 @@ int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t
     uint32_t* t = ki; ki = ko; ko = t;
     t = vi; vi = vo; vo = t;
   }
-  if (ki != w.k0) {  // odd number of passes: copy back
+  if (ki != w.k0) {  // (not taken: the start pair makes the last pass land in k0 / v0)
     hipMemcpyAsync(w.k0, ki, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
     hipMemcpyAsync(w.v0, vi, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
   }
@@ -738,10 +751,10 @@ C2_API size_t c2dsr_plan_err_offset(int n) {
 //   gP[pos[r]] += drop(gX[r])                     (gP dense [n_pos, d]; skipped if null)
 //   gXin[r]     = drop(gX[r])                     (optional, for the non-gather mode)
 // The item and position sums share one launch of each pass.
-C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
-                                   uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G,
-                                   int n_items, float* gP, int n_pos, float* gXin, void* workspace, size_t ws_bytes,
-                                   void* stream) {
+static int embed_bwd_planned_impl(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
+                                  const int* map1, const float* gX2, const int* map2, uint32_t k0, uint32_t k1,
+                                  float p, int64_t idx_base, float scale, float* G, int n_items, float* gP, int n_pos,
+                                  float* gXin, void* workspace, size_t ws_bytes, void* stream) {
   if (d % 4) return (int)hipErrorInvalidValue;
   if (n_rows == 0) return 0;
   if (ws_bytes < c2dsr_embed_bwd_planned_workspace(n_rows, d) || (G && !seq_plan) || (gP && !pos_plan))
@@ -752,10 +765,11 @@ C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, i
   SegJob jobs[2];
   int nj = 0;
   if (G)
-    jobs[nj++] = seg_job(plan_view(seq_plan, n_rows), n_rows, n_items, RowSrc{gX, d, dr, idx_base, scale, nullptr}, G,
-                         ws, -1);
+    jobs[nj++] = seg_job(plan_view(seq_plan, n_rows), n_rows, n_items,
+                         RowSrc{gX, d, dr, idx_base, scale, nullptr, map1, map2, gX2}, G, ws, -1);
   if (gP)
-    jobs[nj++] = seg_job(plan_view(pos_plan, n_rows), n_rows, n_pos, RowSrc{gX, d, dr, idx_base, 1.0f, nullptr}, gP,
+    jobs[nj++] = seg_job(plan_view(pos_plan, n_rows), n_rows, n_pos,
+                         RowSrc{gX, d, dr, idx_base, 1.0f, nullptr, map1, map2, gX2}, gP,
                          ws + seg_ws_bytes(n_rows, d), -1);
   if (nj) seg_dispatch(jobs[0], nj > 1 ? &jobs[1] : nullptr, s);
   if (gXin) {
@@ -764,6 +778,26 @@ C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, i
   }
   C2_CHECK_LAUNCH();
   return 0;
+}
+
+C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
+                                   uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G,
+                                   int n_items, float* gP, int n_pos, float* gXin, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+  return embed_bwd_planned_impl(seq_plan, pos_plan, n_rows, d, gX, nullptr, nullptr, nullptr, k0, k1, p, idx_base,
+                                scale, G, n_items, gP, n_pos, gXin, workspace, ws_bytes, stream);
+}
+
+// the same with gX given as two compact row sources: row r = (inv_a[r] >= 0 ? gXa[inv_a[r]] : 0)
+// + (inv_b[r] >= 0 ? gXb[inv_b[r]] : 0)
+C2_API int c2dsr_embed_bwd_planned_rows(const void* seq_plan, const void* pos_plan, int n_rows, int d,
+                                        const float* gXa, const int* inv_a, const float* gXb, const int* inv_b,
+                                        uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G,
+                                        int n_items, float* gP, int n_pos, void* workspace, size_t ws_bytes,
+                                        void* stream) {
+  if (!gXa || !inv_a || !gXb || !inv_b) return (int)hipErrorInvalidValue;
+  return embed_bwd_planned_impl(seq_plan, pos_plan, n_rows, d, gXa, inv_a, gXb, inv_b, k0, k1, p, idx_base, scale,
+                                G, n_items, gP, n_pos, nullptr, workspace, ws_bytes, stream);
 }
 
 C2_API size_t c2dsr_embed_bwd_workspace(int n_rows, int d) {

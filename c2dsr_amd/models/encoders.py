@@ -102,8 +102,9 @@ class SelfAttention(nn.Module):
             return 0.0, (0, 0)
         return p, self.state.keys(DK.site_enc(pass_id, layer, kind))
 
-    def encode(self, x, seq, pass_id):
-        """The TransformerEncoder stack on an already embedded + dropped [B, L, d] input."""
+    def encode(self, x, seq, pass_id, link=None):
+        """The TransformerEncoder stack on an already embedded + dropped [B, L, d] input.  link: the
+        ops.RowsGrad of the embedding that produced x (its input gradient may then stay in compact parts)."""
         B, L, d = x.shape
         rb_rows = self.state.row_offset * L
         rs = self.state.need.get(pass_id) if self.training and not self.norm_first else None
@@ -138,7 +139,7 @@ class SelfAttention(nn.Module):
                     # Q only at these rows, K / V only at the padding rows (the only admissible keys, Q1)
                     oc = ops.RowsQKVAttnFn.apply(x.contiguous(), xc, at.in_proj_weight, at.in_proj_bias, seq,
                                                  self.idx_pad, self.n_head, p_at, k_at, self.state.row_offset,
-                                                 self.precision, rs, ks, r1)
+                                                 self.precision, rs, ks, r1, link if li == 0 else None)
                 else:
                     o = ops.QKVAttnFn.apply(x.contiguous(), at.in_proj_weight, at.in_proj_bias, seq, self.idx_pad,
                                             self.n_head, p_at, k_at, self.state.row_offset, self.precision, r1)
@@ -185,9 +186,10 @@ class SelfAttention(nn.Module):
     def forward_items(self, seq, pos, H, tok, E, sink, pass_id):
         """Fused C2DSR.py:65-71 + encoders.py:29-33: gather (H[seq]+E[seq])·√d + P[pos], dropout, encoder."""
         p, k = self._drop(pass_id, 0, DK.K_INPUT)
+        link = ops.RowsGrad() if self.training else None
         x = ops.EmbedFn.apply(tok, E, self.pos_emb.weight, seq, pos, H, math.sqrt(self.d), p, k,
-                              self.state.row_offset, sink, self.idx_pad)
-        return self.encode(x, seq, pass_id)
+                              self.state.row_offset, sink, self.idx_pad, link)
+        return self.encode(x, seq, pass_id, link)
 
 
 class GCN(nn.Module):

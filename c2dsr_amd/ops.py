@@ -393,7 +393,8 @@ class GCNFn(Function):
         ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
         ctx.E = E
         ctx.mark_non_differentiable(out)
-        tok = E.new_zeros(())
+        ctx.set_materialize_grads(False)  # H gets no gradient: no [n, d] zeros for it
+        tok = torch.empty((), device=E.device)  # value never read (the dependency is all it carries)
         return out, tok
 
     @staticmethod
@@ -539,7 +540,7 @@ class EmbedFn(Function):
     """x = drop((H[seq] + E[seq])·√d + P[pos])  (models/C2DSR.py:65-71 + encoders.py:30-31)."""
 
     @staticmethod
-    def forward(ctx, tok, E, P, seq, pos, H, scale, p, keys, row_base, sink, pad_row):
+    def forward(ctx, tok, E, P, seq, pos, H, scale, p, keys, row_base, sink, pad_row, link=None):
         require_device(E)
         B, L = seq.shape
         d = E.shape[1]
@@ -549,6 +550,7 @@ class EmbedFn(Function):
         ctx.save_for_backward(seq, pos)
         ctx.scale, ctx.p, ctx.keys, ctx.row_base, ctx.sink, ctx.n_items = scale, p, keys, row_base, sink, E.shape[0]
         ctx.P = P
+        ctx.link = link
         ctx.plans = None
         if any(ctx.needs_input_grad[:3]) and (P.requires_grad or sink is not None):  # forward runs under no_grad
             state = sink.state if sink is not None else None
@@ -560,23 +562,35 @@ class EmbedFn(Function):
     def backward(ctx, gx):
         seq, pos = ctx.saved_tensors
         B, L = seq.shape
-        gx = gx.contiguous()
         d = gx.shape[-1]
         n = B * L
+        parts = ctx.link.take() if ctx.link is not None else None  # gx is a placeholder then (RowsGrad)
         G = ctx.sink.buf() if ctx.sink is not None else None
         gP = _grad_target(ctx.P)
         gP_ret = None
         if gP is None and ctx.needs_input_grad[2]:
             gP_ret = torch.zeros_like(ctx.P)
             gP = gP_ret
-        if ctx.plans is not None and (G is None or ctx.plans[0] is not None) and (gP is None or ctx.plans[1] is not None):
+        planned = (ctx.plans is not None and (G is None or ctx.plans[0] is not None)
+                   and (gP is None or ctx.plans[1] is not None))
+        if parts is not None and not planned:
+            gx = torch.empty(B, L, d, device=gP.device if gP is not None else G.device, dtype=torch.float32)
+            lib('c2dsr_combine_rows', *parts, n, d, gx, stream())
+            parts = None
+        gx = gx.contiguous() if parts is None else None
+        if planned:
             sp = ctx.plans[0].get() if G is not None else None
             pp = ctx.plans[1].get() if gP is not None else None
             ws_bytes = lib.raw('c2dsr_embed_bwd_planned_workspace')(n, d)
-            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
-            lib('c2dsr_embed_bwd_planned', sp, pp, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p),
-                int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes,
-                stream())
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=(G if G is not None else gP).device)
+            if parts is not None:  # the two compact row sources, read through their maps
+                lib('c2dsr_embed_bwd_planned_rows', sp, pp, n, d, *parts, ctx.keys[0], ctx.keys[1], float(ctx.p),
+                    int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], ws, ws_bytes,
+                    stream())
+            else:
+                lib('c2dsr_embed_bwd_planned', sp, pp, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p),
+                    int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes,
+                    stream())
             if _CHECK_PLANS or _CHECK_ERR:
                 off = int(lib.raw('c2dsr_plan_err_offset')(n))
                 for pl in (sp, pp):
@@ -590,8 +604,24 @@ class EmbedFn(Function):
         ctx.plans = None
         if ctx.sink is not None:
             notify_lookup(ctx.sink.state)
-        tok_grad = torch.zeros((), device=gx.device)
-        return tok_grad, None, gP_ret, None, None, None, None, None, None, None, None, None
+        tok_grad = torch.empty((), device=seq.device)  # value never read (GCNFn.backward reads the sink)
+        return tok_grad, None, gP_ret, None, None, None, None, None, None, None, None, None, None
+
+
+class RowsGrad:
+    """Hands the row-subset attention layer's input gradient to the embedding backward as its two compact
+    parts (query rows, key rows; RowsQKVAttnFn) when that layer reads the embedding output directly (one
+    encoder layer): the embedding's segment sums read the parts through their row maps
+    (c2dsr_embed_bwd_planned_rows) and the [B, L, d] gradient is never written.  Autograd carries a
+    zero-stride placeholder of the right shape between the two nodes; the link is the only consumer path,
+    so nothing else reads the placeholder."""
+
+    def __init__(self):
+        self.parts = None
+
+    def take(self):
+        parts, self.parts = self.parts, None
+        return parts
 
 
 class PosDropFn(Function):
@@ -758,7 +788,7 @@ class RowsQKVAttnFn(Function):
     (rows in neither set get 0: nothing downstream reads them)."""
 
     @staticmethod
-    def forward(ctx, x, xc, W, b, seq, pad, n_head, p, keys, b_base, precision, rs, ks, res=None):
+    def forward(ctx, x, xc, W, b, seq, pad, n_head, p, keys, b_base, precision, rs, ks, res=None, link=None):
         require_device(x)
         B, L, d = x.shape
         if not attn_rows_ok(L, d, n_head) or rs.off is None or ks.off is None:
@@ -776,7 +806,7 @@ class RowsQKVAttnFn(Function):
             keys[1], float(p), int(b_base), out, P, stream())
         ctx.save_for_backward(xc, xk, W, q, kv, seq, P)
         ctx.b, ctx.pad, ctx.n_head, ctx.p, ctx.keys, ctx.b_base = b, pad, n_head, p, keys, b_base
-        ctx.precision, ctx.rs, ctx.ks, ctx.res, ctx.shape = precision, rs, ks, res, (B, L, d)
+        ctx.precision, ctx.rs, ctx.ks, ctx.res, ctx.shape, ctx.link = precision, rs, ks, res, (B, L, d), link
         return out
 
     @staticmethod
@@ -804,10 +834,13 @@ class RowsQKVAttnFn(Function):
         _proj_backward(xk, W[d:], dkv, dxk, False, None if gW is None else gW[d:], None if gb is None else gb[d:],
                        ctx.precision)
         dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and ctx.link is not None:  # the embedding backward reads the parts (RowsGrad)
+            ctx.link.parts = (dxq, rs.inv, dxk, ks.inv)
+            dx = torch.empty(1, 1, 1, device=q.device).expand(B, L, d)
+        elif ctx.needs_input_grad[0]:
             dx = torch.empty(B, L, d, device=q.device, dtype=torch.float32)
             lib('c2dsr_combine_rows', dxq, rs.inv, dxk, ks.inv, B * L, d, dx, s)
-        return (dx,) + (None,) * 13
+        return (dx,) + (None,) * 14
 
 
 # ----------------------------------------------------------------------------- residual / layernorm

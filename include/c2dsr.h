@@ -61,6 +61,13 @@ size_t c2dsr_plan_err_offset(int n);
 int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
                             uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items,
                             float* gP, int n_pos, float* gXin, void* workspace, size_t ws_bytes, void* stream);
+/* The same with gX given as two compact row sources (the row-subset attention layer's input gradient: query
+ * rows + key rows, never combined into a full [n_rows, d] tensor): row r of gX = (inv_a[r] >= 0 ?
+ * gXa[inv_a[r]] : 0) + (inv_b[r] >= 0 ? gXb[inv_b[r]] : 0). */
+int c2dsr_embed_bwd_planned_rows(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gXa,
+                                 const int* inv_a, const float* gXb, const int* inv_b, uint32_t k0, uint32_t k1,
+                                 float p, int64_t idx_base, float scale, float* G, int n_items, float* gP, int n_pos,
+                                 void* workspace, size_t ws_bytes, void* stream);
 /* Deterministic (radix-sort + ordered segment sum) backward of the above
  * (replaces embedding_dense_backward):  G[seq[r]] += scale·drop(gX[r]);
  * gP[pos[r]] += drop(gX[r]);  gXin[r] = drop(gX[r]).  Null outputs are skipped. */
