@@ -43,8 +43,32 @@ def main():
     g = lambda: lib('c2dsr_attn_bwd', qkv, sd, pad, B, L, d, H, 1, 2, 0.2, 0, P, dout, dqkv, s)  # noqa: E731
     tf = timeit(f)
     tb = timeit(g)
-    print(f'attn fwd {tf:.1f} us, bwd {tb:.1f} us ({os.environ.get("C2DSR_ATTN_TILED") and "tiled" or "default"})',
-          flush=True)
+    # row-subset layout (the last layer of a training pass): queries = last R positions + ~30% of the rest,
+    # keys = the padding rows
+    need = rng.random((B, L)) < 0.3
+    need[:, -10:] = True
+
+    def rowset(mask):
+        flat = mask.reshape(-1)
+        idx = np.nonzero(flat)[0].astype(np.int32)
+        off = np.concatenate([[0], np.cumsum(mask.sum(1))]).astype(np.int32)
+        return torch.from_numpy(idx).to(dev), torch.from_numpy(off).to(dev), len(idx)
+    qi, qo, nq = rowset(need)
+    ki, ko, nk = rowset(seq == pad)
+    q = torch.randn(nq, d, device=dev)
+    kv = torch.randn(nk, 2 * d, device=dev)
+    o_r = torch.empty(nq, d, device=dev)
+    do_r = torch.randn(nq, d, device=dev)
+    dq = torch.empty(nq, d, device=dev, dtype=torch.bfloat16)
+    dkv = torch.empty(nk, 2 * d, device=dev, dtype=torch.bfloat16)
+    fr = lambda: lib('c2dsr_attn_fwd_rows', q, kv, sd, pad, qi, qo, ki, ko, B, L, d, H, 1, 2, 0.2, 0, o_r, P, s)  # noqa
+    gr = lambda: lib('c2dsr_attn_bwd_rows', q, kv, sd, pad, qi, qo, ki, ko, B, L, d, H, 1, 2, 0.2, 0, P, do_r,  # noqa
+                     dq, dkv, 1, s)
+    tfr = timeit(fr)
+    tbr = timeit(gr)
+    print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: attn fwd {tf:.1f} us, bwd {tb:.1f} us; '
+          f'rows (nq {nq / B:.1f}, nk {nk / B:.1f} per seq) fwd {tfr:.1f} us, bwd {tbr:.1f} us; '
+          f'checksum {float(o_r.double().sum()):.6e} {float(dkv.double().sum()):.6e}', flush=True)
 
 
 if __name__ == '__main__':

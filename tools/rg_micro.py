@@ -1,0 +1,41 @@
+"""Micro-benchmark of the K3 row-streaming projection GEMM (c2dsr_rgemm) at the encoder's shapes: time vs M
+for K = 256 (N = 256, 512) and the achieved HBM rate of its A read + C write (HIP events).
+usage: python tools/rg_micro.py"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from c2dsr_amd.ops import rgemm, to_bf16  # noqa: E402
+
+
+def timeit(fn, reps=30):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+def main():
+    dev = torch.device('cuda')
+    K = 256
+    for N in (256, 512):
+        Wb = to_bf16(torch.randn(N, K, device=dev))
+        for M in (8192, 20000, 38000, 57000, 102400):
+            A = torch.randn(M, K, device=dev)
+            C = torch.empty(M, N, device=dev)
+            t = timeit(lambda: rgemm(A, Wb, C, M=M, N=N, K=K))
+            gb = 4.0 * M * (K + N) / t / 1e3
+            print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: N {N} M {M:6d}: {t:6.1f} us '
+                  f'{gb:6.0f} GB/s', flush=True)
+
+
+if __name__ == '__main__':
+    main()
