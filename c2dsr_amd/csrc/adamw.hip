@@ -9,7 +9,31 @@
 // 36 B/param.
 #include "common.h"
 
+// ADAMW_NT: non-temporal (streaming) loads and stores — every byte is touched once per step
+#ifndef ADAMW_NT
+#define ADAMW_NT 1
+#endif
+
 namespace {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_s(const float4* p) {
+#if ADAMW_NT
+  const f32x4v v = __builtin_nontemporal_load((const f32x4v*)p);
+  return make_float4(v[0], v[1], v[2], v[3]);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_s(float4* p, float4 v) {
+#if ADAMW_NT
+  f32x4v x;
+  x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  __builtin_nontemporal_store(x, (f32x4v*)p);
+#else
+  *p = v;
+#endif
+}
 
 template <bool KEEP>
 __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, float4* __restrict__ fresh,
@@ -18,15 +42,15 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, floa
                                                     float lr, float wd_factor, float b1, float b2, float eps,
                                                     float step_size, float inv_bc2_sqrt) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float4 g = fresh[i];
+    float4 g = ld_s(fresh + i);
     if constexpr (!KEEP) {
       if (accum) {
-        g = g + accum[i];
-        accum[i] = g;
+        g = g + ld_s(accum + i);
+        st_s(accum + i, g);
       }
-      fresh[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      st_s(fresh + i, make_float4(0.f, 0.f, 0.f, 0.f));
     }
-    float4 pp = p[i], mm = m[i], vv = v[i], vx = vmax[i];
+    float4 pp = ld_s(p + i), mm = ld_s(m + i), vv = ld_s(v + i), vx = ld_s(vmax + i);
     float* P = (float*)&pp;
     float* G = (float*)&g;
     float* Mm = (float*)&mm;
@@ -41,10 +65,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, floa
       const float denom = sqrtf(Vx[k]) * inv_bc2_sqrt + eps;
       P[k] = P[k] - step_size * (Mm[k] / denom);
     }
-    p[i] = pp;
-    m[i] = mm;
-    v[i] = vv;
-    vmax[i] = vx;
+    st_s(p + i, pp);
+    st_s(m + i, mm);
+    st_s(v + i, vv);
+    st_s(vmax + i, vx);
   }
 }
 

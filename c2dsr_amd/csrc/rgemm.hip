@@ -637,6 +637,62 @@ C2_API int c2dsr_wgemm_b16y(int T, int N, int D, const void* dY, int ldy, const 
 }
 
 // y = bf16(x) for x fp32 [R][Cc] (row stride ldx); trans: y is [Cc][R]
+namespace {
+constexpr int MULTI_MAX = 64;
+struct MultiBf16 {
+  const float* x[MULTI_MAX];
+  bf16* y[MULTI_MAX];
+  int R[MULTI_MAX], C[MULTI_MAX], ld[MULTI_MAX], tr[MULTI_MAX];
+  int bstart[MULTI_MAX + 1];  // first block of each matrix (256 elements per block)
+  int count;
+};
+// every matrix of the list in one launch: block b converts 256 elements of the matrix whose block range holds
+// it (block-uniform lookup: scalar reads of the argument block)
+__global__ __launch_bounds__(256) void to_bf16_multi_kernel(MultiBf16 m) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = m.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (m.bstart[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const long e = (long)(b - m.bstart[lo]) * 256 + threadIdx.x;
+  const int Cc = m.C[lo], R = m.R[lo];
+  if (e >= (long)R * Cc) return;
+  const int r = (int)(e / Cc), c = (int)(e % Cc);
+  const bf16 v = (bf16)m.x[lo][(long)r * m.ld[lo] + c];
+  if (m.tr[lo])
+    m.y[lo][(long)c * R + r] = v;
+  else
+    m.y[lo][e] = v;
+}
+}  // namespace
+
+// c2dsr_to_bf16 over a list of matrices in one launch: desc = HOST array of count (<= 64) records of six
+// int64 (x, y, R, Cc, ldx, trans) with the meaning of c2dsr_to_bf16's arguments
+C2_API int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream) {
+  if (count < 0 || count > MULTI_MAX) return (int)hipErrorInvalidValue;
+  if (count == 0) return 0;
+  MultiBf16 m;
+  m.count = count;
+  m.bstart[0] = 0;
+  for (int k = 0; k < count; ++k) {
+    const int64_t* d = desc + 6 * k;
+    m.x[k] = (const float*)(intptr_t)d[0];
+    m.y[k] = (bf16*)(intptr_t)d[1];
+    m.R[k] = (int)d[2];
+    m.C[k] = (int)d[3];
+    m.ld[k] = (int)d[4];
+    m.tr[k] = (int)d[5];
+    if (m.R[k] < 0 || m.C[k] < 0 || (long)m.R[k] * m.C[k] > (1l << 30)) return (int)hipErrorInvalidValue;
+    m.bstart[k + 1] = m.bstart[k] + (int)c2::ceil_div((long)m.R[k] * m.C[k], 256);
+  }
+  if (m.bstart[count] == 0) return 0;
+  for (int k = count + 1; k <= MULTI_MAX; ++k) m.bstart[k] = m.bstart[count];
+  to_bf16_multi_kernel<<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
 C2_API int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream) {
   const long n = (long)R * Cc;
   if (n == 0) return 0;

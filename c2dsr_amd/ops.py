@@ -7,6 +7,7 @@ so autograd never materialises a second copy of a table-sized gradient.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 from torch.autograd import Function
 
@@ -73,23 +74,43 @@ def to_bf16(X, trans=False):
 # passes through one SelfAttention share weights, and every forward / backward product re-used to
 # convert them.  Valid while neither the fused optimizer (WEIGHTS.epoch, bumped per step) nor a torch
 # in-place op (W._version) has written the weight since.
+# After a bump, the first request converts every image used in the previous epoch in ONE launch
+# (c2dsr_to_bf16_multi, rewriting the previous images in place) instead of one small launch per image.
 class _WeightImages:
     def __init__(self):
         self.epoch = 0
-        self.cache = {}
+        self.cache = {}  # key -> (tag, image)
+        self.known = {}  # key -> (W, image) of the previous epoch: refreshed together on the next request
 
     def bump(self):
         self.epoch += 1
+        self.known = {k: (v[2], v[1]) for k, v in self.cache.items()}  # the images used this epoch
         self.cache.clear()
+
+    def _refresh_known(self):
+        recs, done = [], []
+        for key, (W, y) in self.known.items():
+            R, Cc = W.shape
+            recs += [W.data_ptr(), y.data_ptr(), R, Cc, W.stride(0), int(key[2])]
+            done.append((key, W, y))
+        self.known = {}
+        for i in range(0, len(done), 64):
+            chunk = done[i:i + 64]
+            desc = np.asarray(recs[6 * i:6 * (i + len(chunk))], dtype=np.int64)
+            lib('c2dsr_to_bf16_multi', desc.ctypes.data, len(chunk), stream())
+        for key, W, y in done:
+            self.cache[key] = ((self.epoch, W._version), y, W)
 
     def get(self, W, trans):
         key = (W.data_ptr(), tuple(W.shape), bool(trans))
         tag = (self.epoch, W._version)
+        if key not in self.cache and key in self.known:
+            self._refresh_known()
         hit = self.cache.get(key)
         if hit is not None and hit[0] == tag:
             return hit[1]
         y = to_bf16(W, trans)
-        self.cache[key] = (tag, y)
+        self.cache[key] = (tag, y, W)
         return y
 
 

@@ -306,6 +306,9 @@ int c2dsr_wgemm_b16y(int T, int N, int D, const void* dY, int ldy, const float* 
                      float* db, void* part, void* stream);
 /* y = bf16(x), x fp32 [R][Cc] with row stride ldx; trans: y is [Cc][R] (weight copies for rgemm). */
 int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream);
+/* c2dsr_to_bf16 over up to 64 matrices in one launch (the projection weights' bf16 images after an optimizer
+ * step): desc = HOST array of count records of six int64 (x, y, R, Cc, ldx, trans) */
+int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream);
 
 /* Evaluation (csrc/eval.hip).  Replaces trainer.py:162-181 (evaluate_batch):
  * per row i, dom = (xory[i] == 0 ? a : b), q = h_share[i,L-1] + h_dom[i, idx_last_dom[i]],

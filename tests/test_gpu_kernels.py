@@ -872,3 +872,26 @@ def test_rgemm_b16a_row_subset_shapes(K, aux):
         outs.append(C)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+def test_to_bf16_multi_equals_single():
+    """The batched weight-image conversion (one launch per optimizer step) writes exactly what c2dsr_to_bf16
+    writes per matrix (plain and transposed, a strided source, an empty matrix)."""
+    from c2dsr_amd._lib import lib, stream
+    from c2dsr_amd.ops import to_bf16
+    g = torch.Generator().manual_seed(1)
+    big = torch.randn(300, 520, generator=g).to(DEV)
+    mats = [(torch.randn(256, 256, generator=g).to(DEV), 0), (torch.randn(512, 256, generator=g).to(DEV), 1),
+            (big[:, :300], 1), (big[10:, 8:], 0), (torch.empty(0, 256, device=DEV), 0), (torch.randn(3, 5, generator=g).to(DEV), 1)]
+    outs, recs = [], []
+    for X, tr in mats:
+        R, C = X.shape
+        y = torch.empty((C, R) if tr else (R, C), device=DEV, dtype=torch.bfloat16)
+        outs.append(y)
+        recs += [X.data_ptr(), y.data_ptr(), R, C, X.stride(0), tr]
+    desc = np.asarray(recs, dtype=np.int64)
+    lib('c2dsr_to_bf16_multi', desc.ctypes.data, len(mats), stream())
+    torch.cuda.synchronize()
+    for (X, tr), y in zip(mats, outs):
+        if X.numel():
+            assert torch.equal(y, to_bf16(X, bool(tr)))
