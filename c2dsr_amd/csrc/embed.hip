@@ -270,11 +270,11 @@ struct RowSrc {
   // the row-subset attention layer's input gradient (query rows + key rows, ops.RowsQKVAttnFn)
   const int *map1, *map2;
   const float* gX2;
-  __device__ __forceinline__ float4 load(uint32_t r, int c) const {
+  // a, b: map1[r], map2[r] when the maps are set (the caller stages them), else unused
+  __device__ __forceinline__ float4 load(uint32_t r, int c, int a = -1, int b = -1) const {
     if (!gX) return make_float4(c == 0 ? (rs ? scale * rs[r] : scale) : 0.f, 0.f, 0.f, 0.f);  // the row (1, 0, …)
     float4 v;
     if (map1) {
-      const int a = map1[r], b = map2[r];
       v = a >= 0 ? *(const float4*)(gX + (long)a * d + c) : c2::f4(0.f);
       if (b >= 0) v = v + *(const float4*)(gX2 + (long)b * d + c);
     } else {
@@ -317,6 +317,8 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
   constexpr int ENT = GROUPS * SEG_CH;
   __shared__ uint32_t sk[ENT + 2];  // sk[e + 1] = K[b0 + e]; sk[0], sk[ENT + 1]: the neighbours
   __shared__ uint32_t sv[ENT];
+  constexpr bool CANMAP = LPR >= 16;  // two-source rows only at d >= 64 (c2dsr_embed_bwd_planned_rows checks)
+  __shared__ int sm[2][CANMAP ? ENT : 1];  // two-source rows: map1 / map2 of each staged row (RowSrc::map1)
   const bool second = (int)blockIdx.x >= j0.nblocks;
   const SegJob& J = second ? j1 : j0;
   const int blk = second ? (int)blockIdx.x - j0.nblocks : (int)blockIdx.x;
@@ -326,9 +328,15 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
     const long gi = b0 - 1 + e;
     sk[e] = (gi >= 0 && gi < n) ? J.K[gi] : 0xffffffffu;
   }
+  const bool mapped = CANMAP && J.src.map1 != nullptr;
   for (int e = threadIdx.x; e < ENT; e += 256) {
     const long gi = b0 + e;
-    sv[e] = gi < n ? min(J.V[gi], (uint32_t)(n - 1)) : 0u;
+    const uint32_t rv = gi < n ? min(J.V[gi], (uint32_t)(n - 1)) : 0u;
+    sv[e] = rv;
+    if (mapped) {
+      sm[0][e] = J.src.map1[rv];
+      sm[1][e] = J.src.map2[rv];
+    }
   }
   __syncthreads();
   const int g = threadIdx.x / LPR;
@@ -348,7 +356,10 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
     for (int h0 = 0; h0 < cnt; h0 += SEG_U) {
       float4 x[SEG_U];
 #pragma unroll
-      for (int u = 0; u < SEG_U; ++u) x[u] = h0 + u < cnt ? src.load(sv[o + h0 + u], c) : c2::f4(0.f);
+      for (int u = 0; u < SEG_U; ++u) {
+        const int e = o + h0 + u;
+        x[u] = h0 + u < cnt ? (mapped ? src.load(sv[e], c, sm[0][e], sm[1][e]) : src.load(sv[e], c)) : c2::f4(0.f);
+      }
       int kind[SEG_U];  // 0: nothing closes at u, 1: out[key] +=, 2: head slot, 3: tail slot, 4: bad key
 #pragma unroll
       for (int u = 0; u < SEG_U; ++u) {
@@ -795,7 +806,7 @@ C2_API int c2dsr_embed_bwd_planned_rows(const void* seq_plan, const void* pos_pl
                                         uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G,
                                         int n_items, float* gP, int n_pos, void* workspace, size_t ws_bytes,
                                         void* stream) {
-  if (!gXa || !inv_a || !gXb || !inv_b) return (int)hipErrorInvalidValue;
+  if (!gXa || !inv_a || !gXb || !inv_b || d < 64) return (int)hipErrorInvalidValue;
   return embed_bwd_planned_impl(seq_plan, pos_plan, n_rows, d, gXa, inv_a, gXb, inv_b, k0, k1, p, idx_base, scale,
                                 G, n_items, gP, n_pos, nullptr, workspace, ws_bytes, stream);
 }
