@@ -810,7 +810,10 @@ __device__ __forceinline__ WMask rows_mask(const int64_t* __restrict__ seq, int6
 #ifndef ATTN_ROWS_OCC
 #define ATTN_ROWS_OCC 2
 #endif
-__global__ __launch_bounds__(256, ATTN_ROWS_OCC) void attn_fwd_rows(const float* __restrict__ q, const float* __restrict__ kv,
+#ifndef ATTN_ROWS_OCC_F
+#define ATTN_ROWS_OCC_F ATTN_ROWS_OCC
+#endif
+__global__ __launch_bounds__(256, ATTN_ROWS_OCC_F) void attn_fwd_rows(const float* __restrict__ q, const float* __restrict__ kv,
                                                      const int64_t* __restrict__ seq, int64_t pad,
                                                      const int* __restrict__ q_idx, const int* __restrict__ q_off,
                                                      const int* __restrict__ k_idx, const int* __restrict__ k_off,

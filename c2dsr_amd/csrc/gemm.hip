@@ -212,7 +212,16 @@ __global__ void splitk_sum_kernel(const float* __restrict__ part, int splits, in
   if (i >= (long)M * N) return;
   const int r = (int)(i / N), c = (int)(i % N);
   float t = 0.f;
-  for (int s = 0; s < splits; ++s) t += part[(long)s * M * N + i];
+  const long sl = (long)M * N;
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {  // eight slabs' loads in flight, added in split order
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(s + u) * sl + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t += v[u];
+  }
+  for (; s < splits; ++s) t += part[s * sl + i];
   float* cp = C + (long)r * ldc + c;
   *cp = beta == 0.f ? t : fmaf(beta, *cp, t);
 }
@@ -249,8 +258,10 @@ __global__ void scale_kernel(float* __restrict__ C, int M, int N, int ldc, float
 // each wave reading 256 contiguous bytes per row) → part[chunk][n]; stage 2: 16 wave groups
 // per 64 columns sum the chunks, combined in a fixed order (deterministic).
 constexpr int CS_ROWS = 256;
+// w (may be null): per-row weights w[r·ldw] (c2dsr_wcolsum)
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ X, int M, int N, long ldx,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, const float* __restrict__ w = nullptr,
+                                                          long ldw = 0) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -259,11 +270,19 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
   float s0 = 0.f, s1 = 0.f;
   if (c < N) {
     int r = r0 + q;
-    for (; r + 4 < r1; r += 8) {
-      s0 += X[(long)r * ldx + c];
-      s1 += X[(long)(r + 4) * ldx + c];
+    if (w) {
+      for (; r + 4 < r1; r += 8) {
+        s0 = fmaf(w[(long)r * ldw], X[(long)r * ldx + c], s0);
+        s1 = fmaf(w[(long)(r + 4) * ldw], X[(long)(r + 4) * ldx + c], s1);
+      }
+      if (r < r1) s0 = fmaf(w[(long)r * ldw], X[(long)r * ldx + c], s0);
+    } else {
+      for (; r + 4 < r1; r += 8) {
+        s0 += X[(long)r * ldx + c];
+        s1 += X[(long)(r + 4) * ldx + c];
+      }
+      if (r < r1) s0 += X[(long)r * ldx + c];
     }
-    if (r < r1) s0 += X[(long)r * ldx + c];
   }
   red[q][cl] = s0 + s1;
   __syncthreads();
@@ -365,15 +384,24 @@ C2_API int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* 
 
 C2_API size_t c2dsr_colsum_workspace(int M, int N) { return (size_t)c2::ceil_div(M, CS_ROWS) * (size_t)N * 4 + 256; }
 
+C2_API int c2dsr_wcolsum(const float* X, int M, int N, int ldx, const float* w, long ldw, float alpha, float beta,
+                         float* out, void* workspace, void* stream);
 C2_API int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* workspace,
                         void* stream) {
+  return c2dsr_wcolsum(X, M, N, ldx, nullptr, 0, alpha, beta, out, workspace, stream);
+}
+
+// out[n] = beta·out[n] + alpha·Σ_m w[m·ldw]·X[m·ldx + n]  (w null: 1) — the classifier_pad weight gradient
+// (a 1 × d product over the 2·B·R stacked rows), without a split-K GEMM
+C2_API int c2dsr_wcolsum(const float* X, int M, int N, int ldx, const float* w, long ldw, float alpha, float beta,
+                         float* out, void* workspace, void* stream) {
   if (N <= 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int chunks = c2::ceil_div(M, CS_ROWS);
   float* part = (float*)workspace;
   if (chunks > 0) {
     dim3 g1(c2::ceil_div(N, 64), chunks);
-    colsum_part_kernel<<<g1, 256, 0, s>>>(X, M, N, ldx, part);
+    colsum_part_kernel<<<g1, 256, 0, s>>>(X, M, N, ldx, part, w, ldw);
   }
   colsum_final_kernel<<<c2::ceil_div(N, 64), 1024, 0, s>>>(part, chunks, N, alpha, beta, out);
   C2_CHECK_LAUNCH();

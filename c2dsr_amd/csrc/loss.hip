@@ -503,28 +503,49 @@ __global__ __launch_bounds__(1024) void loss_partials_kernel(const float* __rest
                                                              const float* __restrict__ rowsB,
                                                              const int64_t* __restrict__ tB, int n_b, int BR,
                                                              float* __restrict__ vec) {
-  __shared__ float red[1024];
+  constexpr int U = 8;  // rows in flight per thread (independent loads, one latency per batch)
+  __shared__ float red[8][16];
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = threadIdx.x; r < 2 * BR; r += blockDim.x) {
-    const int h = r >= BR ? 1 : 0;
-    if (tA[r] != n_a) {
-      if (rowsA) acc[h] += rowsA[r];
-      acc[4 + h] += 1.f;
+  const int M = 2 * BR;
+  for (int r0 = threadIdx.x; r0 < M; r0 += blockDim.x * U) {
+    int64_t ta[U], tb[U];
+    float ra[U], rb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = r0 + u * (int)blockDim.x;
+      const bool ok = r < M;
+      ta[u] = ok ? tA[r] : (int64_t)n_a;
+      tb[u] = ok ? tB[r] : (int64_t)n_b;
+      ra[u] = ok && rowsA ? rowsA[r] : 0.f;
+      rb[u] = ok && rowsB ? rowsB[r] : 0.f;
     }
-    if (tB[r] != n_b) {
-      if (rowsB) acc[2 + h] += rowsB[r];
-      acc[6 + h] += 1.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int h = r0 + u * (int)blockDim.x >= BR ? 1 : 0;
+      if (ta[u] != n_a) {
+        acc[h] += ra[u];
+        acc[4 + h] += 1.f;
+      }
+      if (tb[u] != n_b) {
+        acc[2 + h] += rb[u];
+        acc[6 + h] += 1.f;
+      }
     }
   }
+  // fixed-order reduction: wave tree, then the 16 wave sums in wave order
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
   for (int k = 0; k < 8; ++k) {
-    red[threadIdx.x] = acc[k];
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) vec[k] = red[0];
-    __syncthreads();
+    float v = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[k][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    float t = 0.f;
+    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) t += red[threadIdx.x][q];
+    vec[threadIdx.x] = t;
   }
 }
 

@@ -336,8 +336,9 @@ class LossHeadFn(Function):
                 if gb is not None:
                     colsum(logits, M2, n, ld, gb)
                 pad_col, pad_ld = logits[:, n:], ld
-            if gwpad is not None:
-                gemm(pad_col, Hpad, gwpad, M=1, N=d, K=M2, transA=1, lda=pad_ld, beta=1.0, precision=FP32)
+            if gwpad is not None:  # gwpad[0, :] += Σ_r pad_col[r]·Hpad[r, :]
+                ws = torch.empty(lib.raw('c2dsr_colsum_workspace')(M2, d), dtype=torch.uint8, device=dev)
+                lib('c2dsr_wcolsum', Hpad, M2, d, d, pad_col, pad_ld, 1.0, 1.0, gwpad, ws, s)
             if gbpad is not None:
                 colsum(pad_col, M2, 1, pad_ld, gbpad)
             # classifier_pad's input gradient (pad column ⊗ wpad) is folded into the scatter

@@ -87,6 +87,9 @@ int c2dsr_gemm(int transA, int transB, int M, int N, int K, const float* A, int 
 size_t c2dsr_colsum_workspace(int M, int N);
 int c2dsr_colsum(const float* X, int M, int N, int ldx, float alpha, float beta, float* out, void* workspace,
                  void* stream);
+/* out[n] = beta·out[n] + alpha·Σ_m w[m·ldw]·X[m·ldx + n]  (w null: 1; workspace: c2dsr_colsum_workspace) */
+int c2dsr_wcolsum(const float* X, int M, int N, int ldx, const float* w, long ldw, float alpha, float beta, float* out,
+                  void* workspace, void* stream);
 
 /* Attention core (SDPA math path with causal + inverted key-padding mask, Q1/Q2;
  * models/encoders.py:14,33).  qkv [B,L,3d], out [B,L,d], Psave c2dsr_attn_psave_floats(B, L, d, H) floats

@@ -901,3 +901,43 @@ def test_to_bf16_multi_equals_single():
     for (X, tr), y in zip(mats, outs):
         if X.numel():
             assert torch.equal(y, to_bf16(X, bool(tr)))
+
+
+@pytest.mark.parametrize('M,N,strided', [(40960, 256, True), (1000, 37, False), (3, 256, True)])
+def test_weighted_colsum(M, N, strided):
+    """c2dsr_wcolsum (the classifier_pad weight gradient: Σ_r w_r·H[r, :], w a strided column) and plain
+    c2dsr_colsum against float64, and bitwise reproducible."""
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(M + N)
+    X = torch.randn(M, N, generator=g)
+    wfull = torch.randn(M, 5, generator=g)
+    w, ldw = (wfull[:, 3], 5) if strided else (wfull[:, 0].contiguous(), 1)
+    out0 = torch.randn(N, generator=g)
+    ws = torch.empty(lib.raw('c2dsr_colsum_workspace')(M, N), dtype=torch.uint8, device=DEV)
+    Xd, wd = X.to(DEV), wfull.to(DEV)
+    wptr = wd[:, 3] if strided else wd[:, 0].contiguous()
+    res = []
+    for _ in range(2):
+        out = out0.to(DEV)
+        lib('c2dsr_wcolsum', Xd, M, N, N, wptr, ldw, 0.5, 1.0, out, ws, stream())
+        res.append(out)
+    plain = out0.to(DEV)
+    lib('c2dsr_colsum', Xd, M, N, N, 1.0, 0.0, plain, ws, stream())
+    torch.cuda.synchronize()
+    ref = out0.double() + 0.5 * (w.double()[:, None] * X.double()).sum(0)
+    assert rel(res[0], ref) < 1e-5 and torch.equal(res[0], res[1])
+    assert rel(plain, X.double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize('n,nparts', [(16 * 1024 * 256, 3), (1001, 2), (64000, 1)])
+def test_sum_parts(n, nparts):
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(n)
+    part = torch.randn(nparts, n, generator=g)
+    out0 = torch.randn(n, generator=g)
+    out = out0.to(DEV)
+    lib('c2dsr_sum_parts', part.to(DEV), nparts, n, 1.0, out, stream())
+    t = torch.zeros(n)
+    for s_ in range(nparts):  # the kernel's order: the parts summed in split order, then added to beta·out
+        t += part[s_]
+    assert torch.equal(out.cpu(), out0 + t)
