@@ -110,7 +110,15 @@ __global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ s
   const int4 sp = split[s];
   for (int c = lane * 4; c < d; c += LPR * 4) {
     float4 acc = c2::f4(0.f);
-    for (int k = sp.y; k < sp.z; ++k) acc = acc + *(const float4*)(part + (long)k * d + c);
+    int k = sp.y;
+    for (; k + 8 <= sp.z; k += 8) {  // eight pieces' loads in flight, added in piece order
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *(const float4*)(part + (long)(k + u) * d + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = acc + v[u];
+    }
+    for (; k < sp.z; ++k) acc = acc + *(const float4*)(part + (long)k * d + c);
     epilogue<MASK_OUT>(acc, sp.x, c, d, ep);
   }
 }

@@ -498,41 +498,27 @@ __global__ void outer_add_kernel(const float* __restrict__ a, long sa, const flo
 // Per-head partial sums (trainer.py:143-152) of this rank's rows: vec[0..3] = Σ loss over
 // valid rows of (share_a, spec_a, share_b, spec_b), vec[4..7] = their valid counts.
 // rowsA/rowsB: per-row CE of the [share ; specific] stacks (2*BR rows each).
-__global__ __launch_bounds__(1024) void loss_partials_kernel(const float* __restrict__ rowsA,
-                                                             const int64_t* __restrict__ tA, int n_a,
-                                                             const float* __restrict__ rowsB,
-                                                             const int64_t* __restrict__ tB, int n_b, int BR,
-                                                             float* __restrict__ vec) {
-  constexpr int U = 8;  // rows in flight per thread (independent loads, one latency per batch)
-  __shared__ float red[8][16];
+// stage 1: one row per thread, block partials part[blk][8] (wave trees, then wave order); stage 2: one wave
+// adds the block partials in block order → vec[0..8).  Fixed orders: deterministic.
+__global__ __launch_bounds__(256) void loss_partials_kernel(const float* __restrict__ rowsA,
+                                                            const int64_t* __restrict__ tA, int n_a,
+                                                            const float* __restrict__ rowsB,
+                                                            const int64_t* __restrict__ tB, int n_b, int BR,
+                                                            float* __restrict__ part) {
+  __shared__ float red[8][4];
+  const int r = blockIdx.x * 256 + threadIdx.x;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int M = 2 * BR;
-  for (int r0 = threadIdx.x; r0 < M; r0 += blockDim.x * U) {
-    int64_t ta[U], tb[U];
-    float ra[U], rb[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int r = r0 + u * (int)blockDim.x;
-      const bool ok = r < M;
-      ta[u] = ok ? tA[r] : (int64_t)n_a;
-      tb[u] = ok ? tB[r] : (int64_t)n_b;
-      ra[u] = ok && rowsA ? rowsA[r] : 0.f;
-      rb[u] = ok && rowsB ? rowsB[r] : 0.f;
+  if (r < 2 * BR) {
+    const int h = r >= BR ? 1 : 0;
+    if (tA[r] != n_a) {
+      acc[h] = rowsA ? rowsA[r] : 0.f;
+      acc[4 + h] = 1.f;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int h = r0 + u * (int)blockDim.x >= BR ? 1 : 0;
-      if (ta[u] != n_a) {
-        acc[h] += ra[u];
-        acc[4 + h] += 1.f;
-      }
-      if (tb[u] != n_b) {
-        acc[2 + h] += rb[u];
-        acc[6 + h] += 1.f;
-      }
+    if (tB[r] != n_b) {
+      acc[2 + h] = rowsB ? rowsB[r] : 0.f;
+      acc[6 + h] = 1.f;
     }
   }
-  // fixed-order reduction: wave tree, then the 16 wave sums in wave order
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -542,11 +528,39 @@ __global__ __launch_bounds__(1024) void loss_partials_kernel(const float* __rest
     if (lane == 0) red[k][w] = v;
   }
   __syncthreads();
-  if (threadIdx.x < 8) {
-    float t = 0.f;
-    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) t += red[threadIdx.x][q];
-    vec[threadIdx.x] = t;
+  if (threadIdx.x < 8)
+    part[blockIdx.x * 8 + threadIdx.x] = (red[threadIdx.x][0] + red[threadIdx.x][1]) +
+                                         (red[threadIdx.x][2] + red[threadIdx.x][3]);
+}
+
+__global__ __launch_bounds__(64) void loss_partials_final_kernel(const float* __restrict__ part, int nblk,
+                                                                 float* __restrict__ vec) {
+  const int k = threadIdx.x & 7, g = threadIdx.x >> 3;  // 8 lane groups stride over the blocks
+  float t = 0.f;
+  for (int b = g; b < nblk; b += 8) t += part[b * 8 + k];
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) t += __shfl_xor(t, o, 64);
+  if (threadIdx.x < 8) vec[k] = t;
+}
+
+// per-device scratch for the stage-1 partials (grown on demand, never freed)
+float* partials_scratch(size_t floats) {
+  static float* buf[64] = {nullptr};
+  static size_t cap[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (cap[dev] < floats) {
+    if (buf[dev]) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(buf[dev]);
+    }
+    buf[dev] = nullptr;
+    cap[dev] = 0;
+    if (hipMalloc((void**)&buf[dev], floats * sizeof(float)) != hipSuccess) return nullptr;
+    cap[dev] = floats;
   }
+  return buf[dev];
 }
 
 // scalar combination (trainer.py:143-156) from the (globally reduced) vec[0..8]
@@ -742,7 +756,12 @@ C2_API int c2dsr_outer_add(const float* a, long sa, const float* v, int M, int d
 }
 C2_API int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, const float* rowsB, const int64_t* tB,
                                int n_b, int BR, float* vec, void* stream) {
-  loss_partials_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(rowsA, tA, n_a, rowsB, tB, n_b, BR, vec);
+  const int nblk = c2::ceil_div(2 * BR, 256);
+  if (nblk == 0) return (int)hipMemsetAsync(vec, 0, 8 * sizeof(float), (hipStream_t)stream);
+  float* part = partials_scratch((size_t)nblk * 8);
+  if (!part) return (int)hipErrorOutOfMemory;
+  loss_partials_kernel<<<nblk, 256, 0, (hipStream_t)stream>>>(rowsA, tA, n_a, rowsB, tB, n_b, BR, part);
+  loss_partials_final_kernel<<<1, 64, 0, (hipStream_t)stream>>>(part, nblk, vec);
   C2_CHECK_LAUNCH();
   return 0;
 }
