@@ -208,14 +208,36 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int col = ncol0 + 32 * ct + (lane & 31);
+      // dropout: lanes l and l^1 hold the same rows at columns 2m, 2m+1 — one element pair, one hash (N even):
+      // each lane hashes 8 of the 16 rows (even lane rows 0-7, odd lane 8-15) and takes the partner's 8
+      uint32_t hown[EPI ? 8 : 1], hpar[EPI ? 8 : 1];
+      const bool pairs = EPI && ep.drop.active() && (N & 1) == 0;
+      if constexpr (EPI) {
+        if (pairs) {
+          const int par = lane & 1;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int rr = r0 + creg(j + 8 * par, lane);
+            const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
+            hown[j] = c2::pair_hash(((uint64_t)(ep.row_base + rg_) * N + (col & ~1)) >> 1, ep.drop.k0, ep.drop.k1);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hpar[j] = __shfl_xor(hown[j], 1, 64);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rr = r0 + creg(r, lane);
         float v = fmaf(ep.alpha, acc[ct][r], bcol[ct]);
         if constexpr (EPI) {
-          const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
-          const uint64_t idx = (uint64_t)(ep.row_base + rg_) * N + col;
-          v = fmaxf(v, 0.f) * ep.drop.mul(idx);
+          if (pairs) {
+            const uint32_t h = ((r >> 3) == (lane & 1)) ? hown[r & 7] : hpar[r & 7];
+            v = ((h >> (16 * (col & 1))) & 0xffffu) >= ep.drop.thr ? fmaxf(v, 0.f) * ep.drop.scale : 0.f;
+          } else {
+            const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
+            const uint64_t idx = (uint64_t)(ep.row_base + rg_) * N + col;
+            v = fmaxf(v, 0.f) * ep.drop.mul(idx);
+          }
         }
         if constexpr (AUX == AUX_ACC || AUX == AUX_ACC_MAP) v += xa[ct][r];
         if constexpr (AUX == AUX_MASK) v = xa[ct][r] > 0.f ? v * ep.aux_scale : 0.f;

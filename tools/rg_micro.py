@@ -23,6 +23,23 @@ def timeit(fn, reps=30):
     return e0.elapsed_time(e1) / reps * 1e3
 
 
+def epilogue_costs():
+    """The drop(relu) epilogue (linear1) with and without a row map, against the plain product."""
+    dev = torch.device('cuda')
+    K = N = 256
+    M = 57000
+    Wb = to_bf16(torch.randn(N, K, device=dev))
+    A = torch.randn(M, K, device=dev)
+    C = torch.empty(M, N, device=dev)
+    rowmap = torch.sort(torch.randperm(102400, device=dev)[:M])[0].to(torch.int32)
+    lib_ = os.path.basename(os.environ.get("C2DSR_LIB", "default"))
+    for name, kw in (('plain', {}), ('relu_drop', dict(relu_drop=((1, 2), 0.2, 0))),
+                     ('relu_drop+map', dict(relu_drop=((1, 2), 0.2, 0, rowmap))),
+                     ('relu p=0', dict(relu_drop=((1, 2), 0.0, 0)))):
+        t = timeit(lambda: rgemm(A, Wb, C, M=M, N=N, K=K, **kw))
+        print(f'{lib_}: epilogue {name:14s} M {M}: {t:6.1f} us', flush=True)
+
+
 def main():
     dev = torch.device('cuda')
     K = 256
@@ -38,4 +55,7 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == 'epi':
+        epilogue_costs()
+    else:
+        main()
