@@ -211,6 +211,216 @@ __global__ __launch_bounds__(1024) void reduce_parts_kernel(const float* __restr
   }
 }
 
+// ---- Two LayerNorms back to back (the last post-norm layer's norm2 and the encoder's final norm, Q16):
+//   x = a + drop(b),  x2 = LN2(x)·w2 + b2,  y = LNF(x2)·wF + bF
+// in one pass; x2 is never stored (the backward recomputes it from x and LN2's statistics).
+template <int LPR, int NC>
+__global__ __launch_bounds__(256) void add_ln2_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                          int rows, int d, c2::Drop drop, int64_t idx_base,
+                                                          const int* __restrict__ rowmap, const float* __restrict__ w2,
+                                                          const float* __restrict__ b2, float eps2,
+                                                          const float* __restrict__ wF, const float* __restrict__ bF,
+                                                          float epsF, float* __restrict__ xsave, float* __restrict__ y,
+                                                          float* __restrict__ st) {
+  constexpr int GROUPS = 256 / LPR;
+  const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  const long r = (long)blockIdx.x * GROUPS + g;
+  if (r >= rows) return;
+  float4 x[NC];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = (lane + q * LPR) * 4;
+    x[q] = c2::f4(0.f);
+    if (c < d) {
+      float4 u = *(const float4*)(b + r * d + c);
+      if (drop.active()) u = u * drop.mul4((uint64_t)(idx_base + (rowmap ? rowmap[r] : r)) * d + c);
+      const float4 v = *(const float4*)(a + r * d + c) + u;
+      x[q] = v;
+      *(float4*)(xsave + r * d + c) = v;
+      s += v.x + v.y + v.z + v.w;
+    }
+  }
+  float mean[2], rstd[2];
+  const float* ws[2] = {w2, wF};
+  const float* bs[2] = {b2, bF};
+  const float eps[2] = {eps2, epsF};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (k) {
+      s = 0.f;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int c = (lane + q * LPR) * 4;
+        if (c < d) s += x[q].x + x[q].y + x[q].z + x[q].w;
+      }
+    }
+    mean[k] = c2::group_sum<LPR>(s) / d;
+    float ss = 0.f;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = (lane + q * LPR) * 4;
+      if (c < d) {
+        const float4 t = x[q] + c2::f4(-mean[k]);
+        ss += t.x * t.x + t.y * t.y + t.z * t.z + t.w * t.w;
+      }
+    }
+    rstd[k] = 1.0f / sqrtf(c2::group_sum<LPR>(ss) / d + eps[k]);
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = (lane + q * LPR) * 4;
+      if (c < d) {
+        const float4 w4 = *(const float4*)(ws[k] + c), b4 = *(const float4*)(bs[k] + c);
+        float4 o;
+        o.x = (x[q].x - mean[k]) * rstd[k] * w4.x + b4.x;
+        o.y = (x[q].y - mean[k]) * rstd[k] * w4.y + b4.y;
+        o.z = (x[q].z - mean[k]) * rstd[k] * w4.z + b4.z;
+        o.w = (x[q].w - mean[k]) * rstd[k] * w4.w + b4.w;
+        x[q] = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = (lane + q * LPR) * 4;
+    if (c < d) *(float4*)(y + r * d + c) = x[q];
+  }
+  if (lane == 0) {
+    st[r] = mean[0];
+    st[rows + r] = rstd[0];
+    st[2l * rows + r] = mean[1];
+    st[3l * rows + r] = rstd[1];
+  }
+}
+
+// backward of add_ln2_fwd: dxF → dx2 (final norm) → dx (norm2) in registers; dx = the residual gradient,
+// db_out = dx ⊙ drop mask; the four weight/bias gradients as per-block partials part[blk][4][d]
+// (norm2 weight, norm2 bias, final weight, final bias).  x2 is recomputed from x and LN2's statistics.
+template <int LPR, int NC>
+__global__ __launch_bounds__(256) void ln2_bwd_kernel(const float* __restrict__ x, const float* __restrict__ st,
+                                                      const float* __restrict__ w2, const float* __restrict__ b2,
+                                                      const float* __restrict__ wF, const float* __restrict__ dy,
+                                                      int rows, int d, float* __restrict__ dx,
+                                                      float* __restrict__ db_out, c2::Drop drop, int64_t idx_base,
+                                                      const int* __restrict__ rowmap, float* __restrict__ part) {
+  constexpr int GROUPS = 256 / LPR;
+  const int g = threadIdx.x / LPR, lane = threadIdx.x % LPR;
+  float4 p2w[NC], p2b[NC], pFw[NC], pFb[NC], w24[NC], b24[NC], wF4[NC];
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    p2w[q] = p2b[q] = pFw[q] = pFb[q] = c2::f4(0.f);
+    const int c = (lane + q * LPR) * 4;
+    w24[q] = c < d ? *(const float4*)(w2 + c) : c2::f4(0.f);
+    b24[q] = c < d ? *(const float4*)(b2 + c) : c2::f4(0.f);
+    wF4[q] = c < d ? *(const float4*)(wF + c) : c2::f4(0.f);
+  }
+  const long stride = (long)gridDim.x * GROUPS;
+  for (long r = (long)blockIdx.x * GROUPS + g; r < rows; r += stride) {
+    const float m2 = st[r], r2 = st[rows + r], mF = st[2l * rows + r], rF = st[3l * rows + r];
+    float4 xh2[NC], xhF[NC], gv[NC], dv[NC];
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = (lane + q * LPR) * 4;
+      const bool in = c < d;
+      const float4 xv = in ? *(const float4*)(x + r * d + c) : c2::f4(0.f);
+      dv[q] = in ? *(const float4*)(dy + r * d + c) : c2::f4(0.f);
+      xh2[q] = make_float4((xv.x - m2) * r2, (xv.y - m2) * r2, (xv.z - m2) * r2, (xv.w - m2) * r2);
+      // x2 exactly as the forward computed it: (x - m2)·r2·w2 + b2
+      const float4 x2 = make_float4((xv.x - m2) * r2 * w24[q].x + b24[q].x, (xv.y - m2) * r2 * w24[q].y + b24[q].y,
+                                    (xv.z - m2) * r2 * w24[q].z + b24[q].z, (xv.w - m2) * r2 * w24[q].w + b24[q].w);
+      xhF[q] = make_float4((x2.x - mF) * rF, (x2.y - mF) * rF, (x2.z - mF) * rF, (x2.w - mF) * rF);
+    }
+    // final norm: dx2 = rF·(g − mean(g) − x̂F·mean(g·x̂F)),  g = dy·wF
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      gv[q] = dv[q] * wF4[q];
+      s1 += gv[q].x + gv[q].y + gv[q].z + gv[q].w;
+      s2 += gv[q].x * xhF[q].x + gv[q].y * xhF[q].y + gv[q].z * xhF[q].z + gv[q].w * xhF[q].w;
+      pFw[q] = pFw[q] + dv[q] * xhF[q];
+      pFb[q] = pFb[q] + dv[q];
+    }
+    float a1 = c2::group_sum<LPR>(s1) / d, a2 = c2::group_sum<LPR>(s2) / d;
+#pragma unroll
+    for (int q = 0; q < NC; ++q)
+      dv[q] = make_float4(rF * (gv[q].x - a1 - xhF[q].x * a2), rF * (gv[q].y - a1 - xhF[q].y * a2),
+                          rF * (gv[q].z - a1 - xhF[q].z * a2), rF * (gv[q].w - a1 - xhF[q].w * a2));
+    // norm2 with dy2 = dx2
+    s1 = s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      gv[q] = dv[q] * w24[q];
+      s1 += gv[q].x + gv[q].y + gv[q].z + gv[q].w;
+      s2 += gv[q].x * xh2[q].x + gv[q].y * xh2[q].y + gv[q].z * xh2[q].z + gv[q].w * xh2[q].w;
+      p2w[q] = p2w[q] + dv[q] * xh2[q];
+      p2b[q] = p2b[q] + dv[q];
+    }
+    a1 = c2::group_sum<LPR>(s1) / d;
+    a2 = c2::group_sum<LPR>(s2) / d;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const int c = (lane + q * LPR) * 4;
+      if (c < d) {
+        float4 o = make_float4(r2 * (gv[q].x - a1 - xh2[q].x * a2), r2 * (gv[q].y - a1 - xh2[q].y * a2),
+                               r2 * (gv[q].z - a1 - xh2[q].z * a2), r2 * (gv[q].w - a1 - xh2[q].w * a2));
+        *(float4*)(dx + r * d + c) = o;
+        if (drop.active()) o = o * drop.mul4((uint64_t)(idx_base + (rowmap ? rowmap[r] : r)) * d + c);
+        *(float4*)(db_out + r * d + c) = o;
+      }
+    }
+  }
+  // block reduce of the per-group partials → part[block][4][d]
+  __shared__ float red[256 * 4];
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const int c = (lane + q * LPR) * 4;
+    for (int which = 0; which < 4; ++which) {
+      const float4 v = which == 0 ? p2w[q] : which == 1 ? p2b[q] : which == 2 ? pFw[q] : pFb[q];
+      __syncthreads();
+      *(float4*)(&red[threadIdx.x * 4]) = v;
+      __syncthreads();
+      if (g == 0 && c < d) {
+        float4 t = c2::f4(0.f);
+        for (int gg2 = 0; gg2 < GROUPS; ++gg2) t = t + *(const float4*)(&red[(gg2 * LPR + lane) * 4]);
+        *(float4*)(part + ((long)blockIdx.x * 4 + which) * d + c) = t;
+      }
+    }
+  }
+}
+
+// out_k[c] += Σ_blocks part[blk][k][c] for k < 4 (null outputs skipped): as reduce_parts_kernel over 4 sets
+__global__ __launch_bounds__(1024) void reduce_parts4_kernel(const float* __restrict__ part, int nblk, int d,
+                                                             float* __restrict__ o0, float* __restrict__ o1,
+                                                             float* __restrict__ o2, float* __restrict__ o3) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < 4 * d) {
+    const float* pp = part + c;
+    const long st = 4l * d;
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int b = q;
+    for (; b + 3 * 16 < nblk; b += 4 * 16) {
+      s += pp[b * st];
+      s1 += pp[(b + 16) * st];
+      s2 += pp[(b + 32) * st];
+      s3 += pp[(b + 48) * st];
+    }
+    for (; b < nblk; b += 16) s += pp[b * st];
+    s = (s + s1) + (s2 + s3);
+  }
+  red[q][cl] = s;
+  __syncthreads();
+  if (q == 0 && c < 4 * d) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    const int which = c / d, cc = c % d;
+    float* o = which == 0 ? o0 : which == 1 ? o1 : which == 2 ? o2 : o3;
+    if (o) o[cc] += t;
+  }
+}
+
 __global__ void add_drop_kernel(const float* __restrict__ a, const float* __restrict__ b, long n4, int d,
                                 c2::Drop drop, int64_t idx_base, float* __restrict__ y) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -309,6 +519,79 @@ C2_API int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, co
 #undef C2_LNBC
 #undef C2_LNB
   if (dgw || dgb) reduce_parts_kernel<<<c2::ceil_div(2 * d, 64), 1024, 0, s>>>(part, nblk, d, dgw, dgb);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+// y = LNF(LN2(a + drop(b))·w2 + b2)·wF + bF (post-norm norm2 + the encoder's final norm); xsave = a + drop(b);
+// st [4][rows] = (mean2, rstd2, meanF, rstdF)
+C2_API int c2dsr_add_ln2_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
+                             int64_t idx_base, const int* rowmap, const float* w2, const float* b2, float eps2,
+                             const float* wF, const float* bF, float epsF, float* xsave, float* y, float* st,
+                             void* stream) {
+  if (d % 4 || d > 1024 || !a || !b) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  hipStream_t s = (hipStream_t)stream;
+  const int lpr = lpr_for(d);
+  dim3 grid(c2::ceil_div(rows, 256 / lpr));
+#define C2_LN(L, NC) add_ln2_fwd_kernel<L, NC><<<grid, 256, 0, s>>>(a, b, rows, d, dr, idx_base, rowmap, w2, b2, eps2, wF, bF, epsF, xsave, y, st)
+#define C2_LNC(L)                                   \
+  switch (c2::ceil_div(d, 4 * L)) {                 \
+    case 1: C2_LN(L, 1); break;                     \
+    case 2: C2_LN(L, 2); break;                     \
+    case 3: C2_LN(L, 3); break;                     \
+    default: C2_LN(L, 4); break;                    \
+  }
+  switch (lpr) {
+    case 64: C2_LNC(64); break;
+    case 32: C2_LNC(32); break;
+    case 16: C2_LNC(16); break;
+    case 8: C2_LNC(8); break;
+    default: C2_LNC(4); break;
+  }
+#undef C2_LNC
+#undef C2_LN
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+C2_API size_t c2dsr_ln2_bwd_workspace(int d) { return (size_t)LN_BWD_BLOCKS * 4 * d * 4; }
+
+// backward of c2dsr_add_ln2_fwd: dx = the gradient w.r.t. a, db_out = dx ⊙ drop mask (w.r.t. b); the four
+// LayerNorm parameter gradients accumulated (null ones skipped)
+C2_API int c2dsr_ln2_bwd(const float* xsave, const float* st, const float* w2, const float* b2, const float* wF,
+                         const float* dy, int rows, int d, float* dx, float* db_out, uint32_t k0, uint32_t k1, float p,
+                         int64_t idx_base, const int* rowmap, float* dgw2, float* dgb2, float* dgwF, float* dgbF,
+                         void* workspace, void* stream) {
+  if (d % 4 || d > 1024 || !dx || !db_out) return (int)hipErrorInvalidValue;
+  if (rows == 0) return 0;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  hipStream_t s = (hipStream_t)stream;
+  const int lpr = lpr_for(d);
+  int nblk = c2::ceil_div(rows, 256 / lpr);
+  if (nblk > LN_BWD_BLOCKS) nblk = LN_BWD_BLOCKS;
+  float* part = (float*)workspace;
+#define C2_LNB(L, NC) \
+  ln2_bwd_kernel<L, NC><<<nblk, 256, 0, s>>>(xsave, st, w2, b2, wF, dy, rows, d, dx, db_out, dr, idx_base, rowmap, part)
+#define C2_LNBC(L)                                  \
+  switch (c2::ceil_div(d, 4 * L)) {                 \
+    case 1: C2_LNB(L, 1); break;                    \
+    case 2: C2_LNB(L, 2); break;                    \
+    case 3: C2_LNB(L, 3); break;                    \
+    default: C2_LNB(L, 4); break;                   \
+  }
+  switch (lpr) {
+    case 64: C2_LNBC(64); break;
+    case 32: C2_LNBC(32); break;
+    case 16: C2_LNBC(16); break;
+    case 8: C2_LNBC(8); break;
+    default: C2_LNBC(4); break;
+  }
+#undef C2_LNBC
+#undef C2_LNB
+  if (dgw2 || dgb2 || dgwF || dgbF)
+    reduce_parts4_kernel<<<c2::ceil_div(4 * d, 64), 1024, 0, s>>>(part, nblk, d, dgw2, dgb2, dgwF, dgbF);
   C2_CHECK_LAUNCH();
   return 0;
 }

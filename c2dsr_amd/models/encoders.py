@@ -152,10 +152,10 @@ class SelfAttention(nn.Module):
                 f = ops.linear(x1, lay.linear1.weight, lay.linear1.bias, self.precision,
                                relu_drop=(k_fm, p_fm, rb_rows, rs.idx), res=r2, ff=ff, ff_role='in')
                 f2 = ops.linear(f, lay.linear2.weight, lay.linear2.bias, self.precision, ff=ff, ff_role='out')
-                x2 = ops.AddLNFn.apply(x1, f2, lay.norm2.weight, lay.norm2.bias, p_fo, k_fo, rb_rows, lay.norm2.eps,
-                                       r2, rs.idx)
                 nm = self.encoder.norm
-                outc = ops.AddLNFn.apply(x2, None, nm.weight, nm.bias, 0.0, (0, 0), 0, nm.eps)
+                # norm2 and the final norm in one pass each way (the row between them is never stored)
+                outc = ops.AddLN2Fn.apply(x1, f2, lay.norm2.weight, lay.norm2.bias, nm.weight, nm.bias, p_fo, k_fo,
+                                          rb_rows, lay.norm2.eps, nm.eps, r2, rs.idx)
                 # [n, d]: the loss head reads it through rs.inv (Trainer.train_batch passes the row sets)
                 return outc if self.state.compact_out else ops.ExpandRowsFn.apply(outc, rs, (B, L, d))
             if self.norm_first:

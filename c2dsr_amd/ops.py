@@ -902,6 +902,43 @@ class AddLNFn(Function):
         return da, db, None, None, None, None, None, None, None, None
 
 
+class AddLN2Fn(Function):
+    """y = LN_F(LN_2(a + drop(b))·w2 + b2)·wF + bF — the last post-norm layer's norm2 and the encoder's final
+    norm (models/encoders.py:23-27 → transformer.py, Q16) in one pass each way (c2dsr_add_ln2_fwd / _ln2_bwd):
+    the intermediate row is neither written nor re-read.  res: the ResidualLink of a (its gradient is parked
+    there for linear1's dX product); rowmap: dropout rows of a row subset (as AddLNFn)."""
+
+    @staticmethod
+    def forward(ctx, a, b, w2, b2, wF, bF, p, keys, row_base, eps2, epsF, res=None, rowmap=None):
+        d = a.shape[-1]
+        rows = a.numel() // d
+        y = torch.empty_like(a)
+        xsave = torch.empty_like(a)
+        st = torch.empty(4, rows, device=a.device)
+        lib('c2dsr_add_ln2_fwd', a, b.contiguous(), rows, d, keys[0], keys[1], float(p), int(row_base), rowmap, w2,
+            b2, float(eps2), wF, bF, float(epsF), xsave, y, st, stream())
+        ctx.save_for_backward(xsave, st)
+        ctx.ws, ctx.p, ctx.keys, ctx.row_base, ctx.res, ctx.rowmap = (w2, b2, wF, bF), p, keys, row_base, res, rowmap
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xsave, st = ctx.saved_tensors
+        d = xsave.shape[-1]
+        rows = xsave.numel() // d
+        w2, b2, wF, bF = ctx.ws
+        da = torch.empty_like(xsave)
+        db = torch.empty_like(xsave)
+        ws = torch.empty(lib.raw('c2dsr_ln2_bwd_workspace')(d), dtype=torch.uint8, device=xsave.device)
+        lib('c2dsr_ln2_bwd', xsave, st, w2, b2, wF, dy.contiguous(), rows, d, da, db, ctx.keys[0], ctx.keys[1],
+            float(ctx.p), int(ctx.row_base), ctx.rowmap, _grad_target(w2), _grad_target(b2), _grad_target(wF),
+            _grad_target(bF), ws, stream())
+        if ctx.res is not None:  # parked for linear1's dX product (ResidualLink)
+            ctx.res.grad = da
+            da = None
+        return (da, db) + (None,) * 11
+
+
 class AddDropFn(Function):
     """y = a + drop(b)  (pre-norm residual)."""
 

@@ -133,6 +133,18 @@ int c2dsr_ln_bwd(const float* x, const float* mean, const float* rstd, const flo
                  int64_t idx_base, const int* rowmap, float* dgw, float* dgb, void* workspace, void* stream);
 int c2dsr_add_dropout(const float* a, const float* b, long n, int d, uint32_t k0, uint32_t k1, float p,
                       int64_t idx_base, float* y, void* stream);
+/* Two LayerNorms back to back (the last post-norm layer's norm2 and the encoder's final norm, Q16) in one pass:
+ * y = LNF(LN2(a + drop(b))·w2 + b2)·wF + bF; xsave = a + drop(b); st [4][rows] = mean2, rstd2, meanF, rstdF.
+ * The backward recomputes LN2's output from xsave and st: dx = ∂/∂a, db_out = dx ⊙ drop mask, and the four
+ * parameter gradients accumulated (workspace c2dsr_ln2_bwd_workspace(d) bytes). */
+int c2dsr_add_ln2_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,
+                      int64_t idx_base, const int* rowmap, const float* w2, const float* b2, float eps2,
+                      const float* wF, const float* bF, float epsF, float* xsave, float* y, float* st, void* stream);
+size_t c2dsr_ln2_bwd_workspace(int d);
+int c2dsr_ln2_bwd(const float* xsave, const float* st, const float* w2, const float* b2, const float* wF,
+                  const float* dy, int rows, int d, float* dx, float* db_out, uint32_t k0, uint32_t k1, float p,
+                  int64_t idx_base, const int* rowmap, float* dgw2, float* dgb2, float* dgwF, float* dgbF,
+                  void* workspace, void* stream);
 /* backward of drop(relu(.)) from its output: dx = (y > 0) ? dy/(1-p) : 0 */
 int c2dsr_relu_drop_bwd(const float* dy, const float* y, long n, float p, float* dx, void* stream);
 

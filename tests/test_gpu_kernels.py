@@ -941,3 +941,44 @@ def test_sum_parts(n, nparts):
     for s_ in range(nparts):  # the kernel's order: the parts summed in split order, then added to beta·out
         t += part[s_]
     assert torch.equal(out.cpu(), out0 + t)
+
+
+@pytest.mark.parametrize('rows,d,p,mapped', [(3001, 256, 0.2, True), (517, 64, 0.0, False), (64, 512, 0.1, False)])
+def test_add_ln2_equals_two_layernorms(rows, d, p, mapped):
+    """c2dsr_add_ln2_fwd / _ln2_bwd (norm2 + the encoder's final norm in one pass) against the two
+    c2dsr_add_ln_fwd / c2dsr_ln_bwd calls they replace: outputs, input gradients and all four parameter
+    gradients."""
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(rows + d)
+    t = lambda *sh: torch.randn(*sh, generator=g).to(DEV)  # noqa: E731
+    a, b, dy = t(rows, d), t(rows, d), t(rows, d)
+    w2, b2, wF, bF = t(d) * 0.5 + 1, t(d) * 0.1, t(d) * 0.5 + 1, t(d) * 0.1
+    keys, base = (7, 9), 11
+    rowmap = torch.sort(torch.randperm(4 * rows, generator=g)[:rows])[0].to(torch.int32).to(DEV) if mapped else None
+    s = stream()
+    f32 = dict(device=DEV, dtype=torch.float32)
+    # reference: two calls
+    xs, x2, m2, r2 = (torch.empty(rows, d, **f32), torch.empty(rows, d, **f32), torch.empty(rows, **f32),
+                      torch.empty(rows, **f32))
+    lib('c2dsr_add_ln_fwd', a, b, rows, d, keys[0], keys[1], p, base, rowmap, w2, b2, 1e-8, xs, x2, m2, r2, s)
+    y, mF, rF = torch.empty(rows, d, **f32), torch.empty(rows, **f32), torch.empty(rows, **f32)
+    lib('c2dsr_add_ln_fwd', x2, None, rows, d, 0, 0, 0.0, 0, None, wF, bF, 1e-8, None, y, mF, rF, s)
+    ws = torch.empty(lib.raw('c2dsr_ln_bwd_workspace')(d), dtype=torch.uint8, device=DEV)
+    gr = [torch.zeros(d, **f32) for _ in range(4)]
+    dx2 = torch.empty(rows, d, **f32)
+    lib('c2dsr_ln_bwd', x2, mF, rF, wF, dy, rows, d, dx2, 0, None, 0, 0, 0.0, 0, None, gr[2], gr[3], ws, s)
+    da, db = torch.empty(rows, d, **f32), torch.empty(rows, d, **f32)
+    lib('c2dsr_ln_bwd', xs, m2, r2, w2, dx2, rows, d, da, 0, db, keys[0], keys[1], p, base, rowmap, gr[0], gr[1], ws,
+        s)
+    # fused
+    xs2, y2, st = torch.empty(rows, d, **f32), torch.empty(rows, d, **f32), torch.empty(4, rows, **f32)
+    lib('c2dsr_add_ln2_fwd', a, b, rows, d, keys[0], keys[1], p, base, rowmap, w2, b2, 1e-8, wF, bF, 1e-8, xs2, y2,
+        st, s)
+    ws2 = torch.empty(lib.raw('c2dsr_ln2_bwd_workspace')(d), dtype=torch.uint8, device=DEV)
+    gf = [torch.zeros(d, **f32) for _ in range(4)]
+    da2, db2 = torch.empty(rows, d, **f32), torch.empty(rows, d, **f32)
+    lib('c2dsr_ln2_bwd', xs2, st, w2, b2, wF, dy, rows, d, da2, db2, keys[0], keys[1], p, base, rowmap, *gf, ws2, s)
+    torch.cuda.synchronize()
+    assert torch.equal(xs2, xs)
+    for u, v in [(y2, y), (da2, da), (db2, db)] + list(zip(gf, gr)):
+        assert rel(u, v) < 1e-6
