@@ -208,37 +208,51 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
       const int col = ncol0 + 32 * ct + (lane & 31);
-      // dropout: lanes l and l^1 hold the same rows at columns 2m, 2m+1 — one element pair, one hash (N even):
-      // each lane hashes 8 of the 16 rows (even lane rows 0-7, odd lane 8-15) and takes the partner's 8
-      uint32_t hown[EPI ? 8 : 1], hpar[EPI ? 8 : 1];
-      const bool pairs = EPI && ep.drop.active() && (N & 1) == 0;
+      // drop(relu) multipliers of this column tile's 16 registers, in one of three kernel-uniform modes:
+      // no dropout; pairs — lanes l and l^1 hold the same rows at columns 2m, 2m+1, one element pair, one
+      // hash (N even): each lane hashes 8 of the 16 rows (even lane rows 0-7, odd lane 8-15) and takes the
+      // partner's 8; per element (N odd)
+      float dm[EPI ? 16 : 1];
       if constexpr (EPI) {
-        if (pairs) {
-          const int par = lane & 1;
+        if (!ep.drop.active()) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int rr = r0 + creg(j + 8 * par, lane);
-            const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
-            hown[j] = c2::pair_hash(((uint64_t)(ep.row_base + rg_) * N + (col & ~1)) >> 1, ep.drop.k0, ep.drop.k1);
+          for (int r = 0; r < 16; ++r) dm[r] = 1.f;
+        } else if ((N & 1) == 0) {
+          const int par = lane & 1;
+          uint32_t hown[8], hpar[8];
+          int rows_[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rows_[j] = r0 + creg(j + 8 * par, lane);
+          if (ep.rowmap) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rows_[j] = ep.rowmap[min(rows_[j], M - 1)];
           }
 #pragma unroll
+          for (int j = 0; j < 8; ++j)
+            hown[j] = c2::pair_hash(((uint64_t)(ep.row_base + rows_[j]) * N + (col & ~1)) >> 1, ep.drop.k0,
+                                    ep.drop.k1);
+#pragma unroll
           for (int j = 0; j < 8; ++j) hpar[j] = __shfl_xor(hown[j], 1, 64);
+          const uint32_t sh = 16 * (col & 1);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t h = ((r >> 3) == par) ? hown[r & 7] : hpar[r & 7];
+            dm[r] = ((h >> sh) & 0xffffu) >= ep.drop.thr ? ep.drop.scale : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rr = r0 + creg(r, lane);
+            const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
+            dm[r] = ep.drop.mul((uint64_t)(ep.row_base + rg_) * N + col);
+          }
         }
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int rr = r0 + creg(r, lane);
         float v = fmaf(ep.alpha, acc[ct][r], bcol[ct]);
-        if constexpr (EPI) {
-          if (pairs) {
-            const uint32_t h = ((r >> 3) == (lane & 1)) ? hown[r & 7] : hpar[r & 7];
-            v = ((h >> (16 * (col & 1))) & 0xffffu) >= ep.drop.thr ? fmaxf(v, 0.f) * ep.drop.scale : 0.f;
-          } else {
-            const int rg_ = ep.rowmap ? ep.rowmap[min(rr, M - 1)] : rr;
-            const uint64_t idx = (uint64_t)(ep.row_base + rg_) * N + col;
-            v = fmaxf(v, 0.f) * ep.drop.mul(idx);
-          }
-        }
+        if constexpr (EPI) v = fmaxf(v, 0.f) * dm[r];
         if constexpr (AUX == AUX_ACC || AUX == AUX_ACC_MAP) v += xa[ct][r];
         if constexpr (AUX == AUX_MASK) v = xa[ct][r] > 0.f ? v * ep.aux_scale : 0.f;
         const int off = (col < N && live) ? (rr * (int)ldc + col) * 4 : 0x7fffffff;
