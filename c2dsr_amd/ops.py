@@ -83,9 +83,13 @@ class _WeightImages:
         self.known = {}  # key -> (W, image) of the previous epoch: refreshed together on the next request
 
     def bump(self):
+        """After an optimizer step: re-convert every image used this epoch now, behind the update on the stream
+        (the host does it while the GPU runs the optimizer, not at the first projection of the next forward)."""
         self.epoch += 1
         self.known = {k: (v[2], v[1]) for k, v in self.cache.items()}  # the images used this epoch
         self.cache.clear()
+        if self.known:
+            self._refresh_known()
 
     def _refresh_known(self):
         recs, done = [], []

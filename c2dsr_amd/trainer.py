@@ -230,6 +230,12 @@ class Trainer(object):
         self.dp_counts = None
         need, pads, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b,
                                           (seq_share, seq_a, seq_b, neg_a, neg_b))
+        if m.training:
+            # the embedding backward's sort plans of every pass, enqueued on the side stream now (while the GCN
+            # forward runs) rather than from inside each pass's forward
+            for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b), (neg_a, pos), (neg_b, pos)):
+                ops.index_plan(m.state, sq, m.n_item)
+                ops.index_plan(m.state, ps, m.attn_share.len_max)
         m.state.need, m.state.pad_rows, m.state.compact_out = need, pads, bool(need)
         try:
             h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
