@@ -128,9 +128,12 @@ class HbmTimer:
       the L-row position table is cache-resident and not credited;
     * K2 backward, per row: 16 + 4·d (read dX) [+ 4·d if dXin is written]; plus 8·d per DISTINCT item
       of the batch (read-modify-write of its gradient row, ``uniq`` from the host copy of the batch).
+      With dX in two compact parts (c2dsr_embed_bwd_planned_rows): per row 16 + 8 (indices, two maps), plus
+      4·d per row of each part (n_q + n_k rows read), plus the 8·d per distinct item.
       Sort passes and pad-row segments are overhead, not credited."""
 
-    NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_bwd', 'c2dsr_embed_bwd_planned')
+    NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_bwd', 'c2dsr_embed_bwd_planned',
+             'c2dsr_embed_bwd_planned_rows')
 
     def __init__(self, n_rows_table, nnz_by_col_ptr, uniq_by_seq_ptr):
         from c2dsr_amd._lib import lib
@@ -146,10 +149,13 @@ class HbmTimer:
         self.lib.time_names.update(self.NAMES)
         # a planned backward's first argument is the seq plan: resolve it to the index tensor at launch
         self.lib.time_meta['c2dsr_embed_bwd_planned'] = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0]), 0)
+        self.lib.time_meta['c2dsr_embed_bwd_planned_rows'] = lambda a: (
+            self.uniq.get(ops.PLAN_SRC.get(a[0]), 0), ops.ROW_COUNT.get(a[4], 0) + ops.ROW_COUNT.get(a[6], 0))
 
     def stop(self):
         self.lib.time_names.difference_update(self.NAMES)
         self.lib.time_meta.pop('c2dsr_embed_bwd_planned', None)
+        self.lib.time_meta.pop('c2dsr_embed_bwd_planned_rows', None)
 
     def launch_bytes(self, name, a):
         if name == 'c2dsr_gcn_spmm':
@@ -161,6 +167,9 @@ class HbmTimer:
             reads = (a[4] is not None) + (a[5] is not None) + (a[6] is not None)
             return n * (16 + 4 * d * reads + 4 * d)
         n, d = a[2], a[3]
+        if name == 'c2dsr_embed_bwd_planned_rows':  # (.., n, d, gXa, inv_a, gXb, inv_b, ..) + (uniq, rows of parts)
+            uniq, part_rows = a[-1]
+            return n * (16 + 8) + 4 * d * part_rows + 8 * d * uniq
         if name == 'c2dsr_embed_bwd_planned':  # (seq_plan, pos_plan, n, d, gX, .., G, n_items, gP, n_pos, gXin, ..)
             return n * (16 + 4 * d + (4 * d if a[14] is not None else 0)) + 8 * d * a[-1]
         return n * (16 + 4 * d + (4 * d if a[14] is not None else 0)) + 8 * d * self.uniq.get(a[0], 0)

@@ -256,7 +256,16 @@ __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restr
 }
 
 // ------------------------------------------------------------------ segment sums
-constexpr int SEG_U = 8;   // rows in flight per lane group
+// rows in flight per lane group: 4 (occupancy over batch depth — the embedding backward at the bench shapes:
+// 8 → 87 µs, 4 → 68 µs, 16 → 133 µs per pass); SEG_PIPE 1 = the next batch's rows loaded under this batch's
+// read-modify-writes (measured no better at 4)
+#ifndef SEG_U_CFG
+#define SEG_U_CFG 4
+#endif
+constexpr int SEG_U = SEG_U_CFG;  // rows in flight per lane group
+#ifndef SEG_PIPE
+#define SEG_PIPE 0
+#endif
 constexpr int SUBP = 128;  // pieces per level-1 block of a split
 
 struct RowSrc {
@@ -353,13 +362,14 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
   for (int c = lane * 4; c < d; c += LPR * 4) {
     float4 acc = c2::f4(0.f);
     bool first = true;  // the next run to close is the chunk's first
-    for (int h0 = 0; h0 < cnt; h0 += SEG_U) {
-      float4 x[SEG_U];
+    auto load = [&](float4 (&x)[SEG_U], int h0) {
 #pragma unroll
       for (int u = 0; u < SEG_U; ++u) {
         const int e = o + h0 + u;
         x[u] = h0 + u < cnt ? (mapped ? src.load(sv[e], c, sm[0][e], sm[1][e]) : src.load(sv[e], c)) : c2::f4(0.f);
       }
+    };
+    auto process = [&](float4 (&x)[SEG_U], int h0) {
       int kind[SEG_U];  // 0: nothing closes at u, 1: out[key] +=, 2: head slot, 3: tail slot, 4: bad key
 #pragma unroll
       for (int u = 0; u < SEG_U; ++u) {
@@ -398,7 +408,26 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
         else if (kind[u] == 4 && lane == 0)
           atomicOr(J.err, 2);
       }
+    };
+#if SEG_PIPE
+    // the next batch's rows are in flight while this batch's runs are read-modify-written (rows and out
+    // are different buffers; a run that closes in a batch never reappears in a later one)
+    float4 xa[SEG_U], xb[SEG_U];
+    load(xa, 0);
+    for (int h0 = 0; h0 < cnt; h0 += 2 * SEG_U) {
+      if (h0 + SEG_U < cnt) load(xb, h0 + SEG_U);
+      process(xa, h0);
+      if (h0 + SEG_U >= cnt) break;
+      if (h0 + 2 * SEG_U < cnt) load(xa, h0 + 2 * SEG_U);
+      process(xb, h0 + SEG_U);
     }
+#else
+    for (int h0 = 0; h0 < cnt; h0 += SEG_U) {
+      float4 x[SEG_U];
+      load(x, h0);
+      process(x, h0);
+    }
+#endif
   }
 }
 

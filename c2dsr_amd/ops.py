@@ -461,6 +461,7 @@ class GCNFn(Function):
 _side_streams = {}
 _PLAN_SIDE = __import__('os').environ.get('C2DSR_PLAN_SIDE', '1') == '1'
 PLAN_SRC = {}  # plan buffer data_ptr -> data_ptr of the index tensor it sorts (roofline accounting)
+ROW_COUNT = {}  # compact gradient part data_ptr -> its rows (roofline accounting of c2dsr_embed_bwd_planned_rows)
 
 
 def side_stream(device):
@@ -609,6 +610,9 @@ class EmbedFn(Function):
             ws_bytes = lib.raw('c2dsr_embed_bwd_planned_workspace')(n, d)
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=(G if G is not None else gP).device)
             if parts is not None:  # the two compact row sources, read through their maps
+                if len(ROW_COUNT) > 256:
+                    ROW_COUNT.clear()
+                ROW_COUNT[parts[0].data_ptr()], ROW_COUNT[parts[2].data_ptr()] = parts[0].shape[0], parts[2].shape[0]
                 lib('c2dsr_embed_bwd_planned_rows', sp, pp, n, d, *parts, ctx.keys[0], ctx.keys[1], float(ctx.p),
                     int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], ws, ws_bytes,
                     stream())
