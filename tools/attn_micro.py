@@ -25,6 +25,7 @@ def timeit(fn, reps=20):
 
 def main():
     B, L, d, H = 2048, 50, 256, 1
+    pdrop = float(os.environ.get('ATTN_P', '0.2'))
     pad = 100782
     rng = np.random.default_rng(1)
     lens = rng.integers(6, L + 1, size=B)
@@ -61,8 +62,8 @@ def main():
     do_r = torch.randn(nq, d, device=dev)
     dq = torch.empty(nq, d, device=dev, dtype=torch.bfloat16)
     dkv = torch.empty(nk, 2 * d, device=dev, dtype=torch.bfloat16)
-    fr = lambda: lib('c2dsr_attn_fwd_rows', q, kv, sd, pad, qi, qo, ki, ko, B, L, d, H, 1, 2, 0.2, 0, o_r, P, s)  # noqa
-    gr = lambda: lib('c2dsr_attn_bwd_rows', q, kv, sd, pad, qi, qo, ki, ko, B, L, d, H, 1, 2, 0.2, 0, P, do_r,  # noqa
+    fr = lambda: lib('c2dsr_attn_fwd_rows', q, kv, sd, pad, qi, qo, ki, ko, B, L, d, H, 1, 2, pdrop, 0, o_r, P, s)  # noqa
+    gr = lambda: lib('c2dsr_attn_bwd_rows', q, kv, sd, pad, qi, qo, ki, ko, B, L, d, H, 1, 2, pdrop, 0, P, do_r,  # noqa
                      dq, dkv, 1, s)
     tfr = timeit(fr)
     tbr = timeit(gr)

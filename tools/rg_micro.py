@@ -40,6 +40,22 @@ def epilogue_costs():
         print(f'{lib_}: epilogue {name:14s} M {M}: {t:6.1f} us', flush=True)
 
 
+def wg_costs():
+    """The weight-gradient product (c2dsr_wgemm: split partials + fixed-order sum) at the encoder's shapes."""
+    from c2dsr_amd.ops import wgemm
+    dev = torch.device('cuda')
+    lib_ = os.path.basename(os.environ.get("C2DSR_LIB", "default"))
+    for T, N, b16 in ((38000, 256, False), (57000, 256, False), (38000, 256, True), (57000, 512, True)):
+        dY = torch.randn(T, N, device=dev)
+        if b16:
+            dY = dY.to(torch.bfloat16)
+        X = torch.randn(T, 256, device=dev)
+        dW = torch.zeros(N, 256, device=dev)
+        db = torch.zeros(N, device=dev)
+        t = timeit(lambda: wgemm(dY, X, dW, T=T, N=N, D=256, db=db))
+        print(f'{lib_}: wgemm T {T} N {N} {"bf16" if b16 else "fp32"} dY: {t:6.1f} us', flush=True)
+
+
 def main():
     dev = torch.device('cuda')
     K = 256
@@ -57,5 +73,7 @@ def main():
 if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'epi':
         epilogue_costs()
+    elif len(sys.argv) > 1 and sys.argv[1] == 'wg':
+        wg_costs()
     else:
         main()
