@@ -321,10 +321,26 @@ __device__ __forceinline__ bf16x8 tr32(const char* img, int rr0, int kb0, int la
 
 // YB16: dY is bf16 in HBM (the attention backward's dqkv): 8-byte loads, no conversion; the bias
 // column sums add the same bf16 values.
+// Segments (c2dsr_wgemm_multi): the row sets of several products into the same dW (one weight used by several
+// encoder passes) walked as one virtual row range; segment k occupies virtual rows [vbeg[k], vbeg[k+1]) (its
+// T[k] rows padded to a multiple of 32, so no 32-row chunk straddles two segments or a split end).
+constexpr int WG_MAXSEG = 4;
+struct WSeg {
+  const void* dY[WG_MAXSEG];
+  const float* X[WG_MAXSEG];
+  int ldy[WG_MAXSEG], ldx[WG_MAXSEG], T[WG_MAXSEG];
+  int vbeg[WG_MAXSEG + 1];
+  int nseg;
+};
+template <typename V>
+__device__ __forceinline__ V wg_pick(const V (&a)[WG_MAXSEG], int k) {  // uniform k: no dynamic indexing
+  return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
+}
+
 template <bool YB16>
-__global__ __launch_bounds__(256) void wg_kernel(int T, int N, const void* __restrict__ dY, long ldy,
-                                                 const float* __restrict__ X, long ldx, float* __restrict__ part,
+__global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restrict__ part,
                                                  float* __restrict__ part_b, int NTL, int rows_per_split) {
+  const int T = sg.vbeg[WG_MAXSEG];  // virtual rows (entries past nseg repeat the total)
   __shared__ __attribute__((aligned(16))) float4 red_b[8][32];
   __shared__ __attribute__((aligned(16))) char yimg[2][32 * 128 * 2];
   __shared__ __attribute__((aligned(16))) char ximg[2][32 * 256 * 2];
@@ -340,15 +356,20 @@ __global__ __launch_bounds__(256) void wg_kernel(int T, int N, const void* __res
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n_base = nt * 128;
   constexpr int YEB = YB16 ? 2 : 4;
-  const auto ysrc = rsrc_bytes(dY, (long)t_end * ldy * YEB);  // rows past the split's end read 0
-  const auto xsrc = rsrc_bytes(X, (long)t_end * ldx * 4);
   const int lrow = threadIdx.x >> 6;  // 0..3
-  const int ldyb = (int)ldy * YEB, ldxb = (int)ldx * 4;
   // chunk c: thread t loads dY rows lrow + 4u (u < 8) → 1 float4 (cols 4·(lane&31) of the 128) per
-  // half-wave pair... simpler: dY chunk 32×128 floats = 1024 float4 = 4 per thread, X 2048 = 8 per thread
+  // half-wave pair... simpler: dY chunk 32×128 floats = 1024 float4 = 4 per thread, X 2048 = 8 per thread.
+  // The chunk's segment (uniform): rows past its T read 0 through the descriptors.
 #define WG_LOAD(c, PY, PX)                                                                                    \
   {                                                                                                           \
-    const int t0_ = t_beg + min(c, nchunk - 1) * 32;                                                          \
+    const int tv_ = t_beg + min(c, nchunk - 1) * 32;                                                          \
+    int k_ = 0;                                                                                               \
+    _Pragma("unroll") for (int kk = 1; kk < WG_MAXSEG; ++kk) k_ = (kk < sg.nseg && tv_ >= sg.vbeg[kk]) ? kk : k_; \
+    const int t0_ = tv_ - (k_ == 0 ? sg.vbeg[0] : k_ == 1 ? sg.vbeg[1] : k_ == 2 ? sg.vbeg[2] : sg.vbeg[3]);  \
+    const int ly_ = wg_pick(sg.ldy, k_), lx_ = wg_pick(sg.ldx, k_), tk_ = wg_pick(sg.T, k_);                 \
+    const int ldyb = ly_ * YEB, ldxb = lx_ * 4;                                                               \
+    const auto ysrc = rsrc_bytes(wg_pick(sg.dY, k_), (long)tk_ * ly_ * YEB);                                  \
+    const auto xsrc = rsrc_bytes(wg_pick(sg.X, k_), (long)tk_ * lx_ * 4);                                     \
     _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
       const int q_ = threadIdx.x + 256 * u; /* 0..1023: row q_>>5, float4 q_&31 */                           \
       const int yo_ = (t0_ + (q_ >> 5)) * ldyb + (n_base + 4 * (q_ & 31)) * YEB;                              \
@@ -640,9 +661,11 @@ C2_API int c2dsr_wgemm_supported(int T, int N, int D) {
   return T > 0 && D == 256 && N % 128 == 0 && N <= 32 * 128 && (long)T * N * 4 < (1L << 31) && (long)T * D * 4 < (1L << 31);
 }
 C2_API size_t c2dsr_wgemm_workspace(int N) { return (size_t)wg_splits(N) * N * 257 * 4; }
-static int wgemm_impl(int T, int N, int D, const void* dY, bool yb16, int ldy, const float* X, int ldx, float beta,
-                      float* dW, float* db, void* part, void* stream) {
-  if (!c2dsr_wgemm_supported(T, N, D) || ldy % 4 || ldx % 4) return (int)hipErrorInvalidValue;
+static int wgemm_segs(const WSeg& sg, int N, int D, bool yb16, float beta, float* dW, float* db, void* part,
+                      void* stream) {
+  const int T = sg.vbeg[WG_MAXSEG];
+  if (T == 0) return 0;
+  if (!c2dsr_wgemm_supported(T, N, D)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int NTL = N / 128;
   const int splits = wg_splits(N);
@@ -652,14 +675,52 @@ static int wgemm_impl(int T, int N, int D, const void* dY, bool yb16, int ldy, c
   const long n = (long)N * 256;
   float* part_b = db ? (float*)part + (long)splits * n : nullptr;
   if (yb16)
-    wg_kernel<true><<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, part_b, NTL, rows);
+    wg_kernel<true><<<blocks, 256, 0, s>>>(N, sg, (float*)part, part_b, NTL, rows);
   else
-    wg_kernel<false><<<blocks, 256, 0, s>>>(T, N, dY, ldy, X, ldx, (float*)part, part_b, NTL, rows);
+    wg_kernel<false><<<blocks, 256, 0, s>>>(N, sg, (float*)part, part_b, NTL, rows);
   const long blocks_a = c2::ceil_div(n / 4 * 8, 256), blocks_b = db ? c2::ceil_div((long)N / 4 * 8, 256) : 0;
   sum_parts_kernel2<<<blocks_a + blocks_b, 256, 0, s>>>((const float*)part, n, dW, part_b, N, db, splits, beta,
                                                         blocks_a);
   C2_CHECK_LAUNCH();
   return 0;
+}
+
+static int wgemm_impl(int T, int N, int D, const void* dY, bool yb16, int ldy, const float* X, int ldx, float beta,
+                      float* dW, float* db, void* part, void* stream) {
+  if (!c2dsr_wgemm_supported(T, N, D) || ldy % 4 || ldx % 4) return (int)hipErrorInvalidValue;
+  WSeg sg{};
+  sg.nseg = 1;
+  sg.dY[0] = dY;
+  sg.X[0] = X;
+  sg.ldy[0] = ldy;
+  sg.ldx[0] = ldx;
+  sg.T[0] = T;
+  sg.vbeg[0] = 0;
+  for (int k = 1; k <= WG_MAXSEG; ++k) sg.vbeg[k] = c2::ceil_div(T, 32) * 32;
+  return wgemm_segs(sg, N, D, yb16, beta, dW, db, part, stream);
+}
+
+// dW[N, D] = beta·dW + Σ_k dY_kᵀ·X_k (and db = beta·db + Σ_k Σ_t dY_k[t]) over up to 4 row sets in ONE product
+// (the weight of a module that several encoder passes used): seg = HOST array of nseg records of five int64
+// (dY, ldy, X, ldx, T); dY fp32 (yb16 = 0) or bf16 (1); the same deterministic split partials as c2dsr_wgemm
+C2_API int c2dsr_wgemm_multi(const int64_t* seg, int nseg, int N, int D, int yb16, float beta, float* dW, float* db,
+                             void* part, void* stream) {
+  if (nseg < 1 || nseg > WG_MAXSEG) return (int)hipErrorInvalidValue;
+  WSeg sg{};
+  sg.nseg = nseg;
+  sg.vbeg[0] = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const int64_t* r = seg + 5 * k;
+    sg.dY[k] = (const void*)(intptr_t)r[0];
+    sg.ldy[k] = (int)r[1];
+    sg.X[k] = (const float*)(intptr_t)r[2];
+    sg.ldx[k] = (int)r[3];
+    sg.T[k] = (int)r[4];
+    if (sg.T[k] < 0 || sg.ldy[k] % 4 || sg.ldx[k] % 4) return (int)hipErrorInvalidValue;
+    sg.vbeg[k + 1] = sg.vbeg[k] + c2::ceil_div(sg.T[k], 32) * 32;
+  }
+  for (int k = nseg + 1; k <= WG_MAXSEG; ++k) sg.vbeg[k] = sg.vbeg[nseg];
+  return wgemm_segs(sg, N, D, yb16 != 0, beta, dW, db, part, stream);
 }
 
 C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,

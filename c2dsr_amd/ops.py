@@ -159,9 +159,51 @@ def wgemm_ok(T, N, D):
     return bool(lib.raw('c2dsr_wgemm_supported')(T, N, D))
 
 
+class WGradBatch:
+    """The projection weight-gradient products of one training backward, deferred and grouped per weight: a
+    SelfAttention module that several encoder passes used (attn_share: the share pass and both negative
+    passes) gets ONE c2dsr_wgemm_multi product over all its passes' rows instead of one per pass (one set of
+    split partials and one fixed-order sum instead of three).  Flushed when the last embedding backward
+    (``lookups`` of them) finishes — before the data-parallel hook issues the dense range — or by the
+    trainer after the backward."""
+
+    def __init__(self, lookups):
+        self.groups = {}
+        self.lookups_left = lookups
+
+    def add(self, dY, X, dW, db, T, N, D):
+        key = (dW.data_ptr(), N, D, dY.dtype, None if db is None else db.data_ptr())
+        g = self.groups.setdefault(key, [dW, db, []])
+        g[2].append((dY, X, T))
+
+    def lookup_done(self):
+        self.lookups_left -= 1
+        if self.lookups_left == 0:
+            self.flush()
+
+    def flush(self):
+        s = stream()
+        for (_, N, D, dt, _), (dW, db, segs) in self.groups.items():
+            ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
+            for i in range(0, len(segs), 4):
+                chunk = segs[i:i + 4]
+                desc = np.asarray([v for dY, X, T in chunk for v in (dY.data_ptr(), N, X.data_ptr(), D, T)],
+                                  dtype=np.int64)
+                lib('c2dsr_wgemm_multi', desc.ctypes.data, len(chunk), N, D, int(dt == torch.bfloat16), 1.0, dW,
+                    db, ws, s)
+        self.groups = {}
+
+
+WBATCH = None  # the active WGradBatch (Trainer.train_batch, bf16 mode), else None
+
+
 def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None):
     """dW[N, D] = beta·dW + dYᵀ·X over T rows and (db given) db[N] = beta·db + Σ_t dY[t]
-    (c2dsr_wgemm, deterministic split-t partials)."""
+    (c2dsr_wgemm, deterministic split-t partials).  With a WGradBatch active (and beta = 1) the product is
+    deferred into it."""
+    if WBATCH is not None and beta == 1.0 and dY.is_contiguous() and X.is_contiguous():
+        WBATCH.add(dY, X, dW, db, T, N, D)
+        return
     ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
     name = 'c2dsr_wgemm_b16y' if dY.dtype == torch.bfloat16 else 'c2dsr_wgemm'
     lib(name, T, N, D, dY, N, X, D, float(beta), dW, db, ws, stream())
@@ -631,6 +673,8 @@ class EmbedFn(Function):
             lib('c2dsr_embed_bwd', seq, pos, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.row_base) * L,
                 float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes, stream())
         ctx.plans = None
+        if WBATCH is not None:  # the last lookup: the deferred weight-gradient products run now
+            WBATCH.lookup_done()
         if ctx.sink is not None:
             notify_lookup(ctx.sink.state)
         tok_grad = torch.empty((), device=seq.device)  # value never read (GCNFn.backward reads the sink)

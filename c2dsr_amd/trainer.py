@@ -90,6 +90,8 @@ class Trainer(object):
         self.compact_rows = os.environ.get('C2DSR_ROW_COMPACT', '1') == '1'
         # last-layer attention on the read rows / padding keys only (ops.RowsQKVAttnFn)
         self.rows_attn = os.environ.get('C2DSR_ROWS_ATTN', '1') == '1'
+        # projection weight gradients grouped per weight across passes (ops.WGradBatch)
+        self.batch_wgrad = os.environ.get('C2DSR_BATCH_WGRAD', '1') == '1'
         self.lambda_loss = args.lambda_loss
         self.dp_split = True  # slice each global batch across data-parallel ranks
 
@@ -259,15 +261,27 @@ class Trainer(object):
             m.state.grad_hook = DPComm(m.flat, self.comm_plan, 5, tables, zero=self.zero)
             meta.on_head_grads = m.state.grad_hook.head_done  # issued as the loss head's backward returns
             try:
-                loss.backward()
+                self._backward(loss)
             finally:
                 hook, m.state.grad_hook = m.state.grad_hook, None
             hook.finish()
             meta.finish_values()
         else:
-            loss.backward()
+            self._backward(loss)
         self.optimizer.step()
         return loss, loss_rec, loss_mi
+
+    def _backward(self, loss):
+        """loss.backward() with the projections' weight-gradient products grouped per weight (ops.WGradBatch,
+        bf16 mode: flushed by the last embedding backward, or here)."""
+        batch = ops.WGradBatch(5) if self.batch_wgrad and self.model.precision == ops.BF16 else None
+        ops.WBATCH = batch
+        try:
+            loss.backward()
+        finally:
+            ops.WBATCH = None
+        if batch is not None:
+            batch.flush()
 
     # ------------------------------------------------------------------ evaluation
     def eval_ranks(self, batch):

@@ -319,6 +319,11 @@ int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, i
 /* ... with dY in bf16 (the bias sums add the bf16 values) */
 int c2dsr_wgemm_b16y(int T, int N, int D, const void* dY, int ldy, const float* X, int ldx, float beta, float* dW,
                      float* db, void* part, void* stream);
+/* c2dsr_wgemm over up to 4 row sets in one product into the same dW (a weight several encoder passes used;
+ * its gradient products deferred to the end of the backward, ops.WGradBatch): seg = HOST array of nseg
+ * records of five int64 (dY, ldy, X, ldx, T); yb16: dY bf16 */
+int c2dsr_wgemm_multi(const int64_t* seg, int nseg, int N, int D, int yb16, float beta, float* dW, float* db,
+                      void* part, void* stream);
 /* y = bf16(x), x fp32 [R][Cc] with row stride ldx; trans: y is [Cc][R] (weight copies for rgemm). */
 int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream);
 /* c2dsr_to_bf16 over up to 64 matrices in one launch (the projection weights' bf16 images after an optimizer

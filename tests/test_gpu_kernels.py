@@ -982,3 +982,33 @@ def test_add_ln2_equals_two_layernorms(rows, d, p, mapped):
     assert torch.equal(xs2, xs)
     for u, v in [(y2, y), (da2, da), (db2, db)] + list(zip(gf, gr)):
         assert rel(u, v) < 1e-6
+
+
+@pytest.mark.parametrize('b16', [False, True])
+def test_wgemm_multi_segments(b16):
+    """c2dsr_wgemm_multi (one weight-gradient product over the row sets of several passes, ops.WGradBatch)
+    against float64 Σ_k dY_kᵀ·X_k of the bf16-rounded operands, segments of ragged lengths (not multiples of
+    32), with the bias column sums; deterministic."""
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(11 + b16)
+    N, D = 512, 256
+    Ts = (1000, 33, 4097)
+    dYs = [torch.randn(T, N, generator=g) for T in Ts]
+    Xs = [torch.randn(T, D, generator=g) for T in Ts]
+    dYd = [y.to(DEV).to(torch.bfloat16) if b16 else y.to(DEV) for y in dYs]
+    Xd = [x.to(DEV) for x in Xs]
+    ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=DEV)
+    desc = np.asarray([v for y, x, T in zip(dYd, Xd, Ts) for v in (y.data_ptr(), N, x.data_ptr(), D, T)],
+                      dtype=np.int64)
+    outs = []
+    for _ in range(2):
+        dW = torch.full((N, D), 0.5, device=DEV)
+        db = torch.full((N,), 0.25, device=DEV)
+        lib('c2dsr_wgemm_multi', desc.ctypes.data, len(Ts), N, D, int(b16), 1.0, dW, db, ws, stream())
+        outs.append((dW, db))
+    torch.cuda.synchronize()
+    r = lambda t: t.to(torch.bfloat16).double()  # noqa: E731  (the MFMA operands)
+    refW = 0.5 + sum(r(y).T @ r(x) for y, x in zip(dYs, Xs))
+    refb = 0.25 + sum((r(y) if b16 else y.double()).sum(0) for y in dYs)
+    assert rel(outs[0][0], refW) < 2e-3 and rel(outs[0][1], refb) < 1e-5
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
