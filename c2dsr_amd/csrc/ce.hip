@@ -224,14 +224,17 @@ __global__ __launch_bounds__(256) void ce_rows_kernel(const float* __restrict__ 
   if (t >= 0 && t < n)
     for (int k = lane; k < D; k += 64) dot += H[r * D + k] * W[t * D + k];
   dot = c2::wave_sum(dot);
+  // the splits' partials one per lane (loads in parallel), combined by wave reductions (fixed order)
+  float pm = -INFINITY, ps = 0.f;
+  for (int s = lane; s < n_split; s += 64) {
+    const float m = part_m[(long)s * M + r], z = part_s[(long)s * M + r];
+    const float mx = fmaxf(pm, m);
+    ps = (pm == -INFINITY ? 0.f : ps * exp2f(pm - mx)) + (m == -INFINITY ? 0.f : z * exp2f(m - mx));
+    pm = mx;
+  }
+  const float mm = c2::wave_max(pm);
+  const float ss = c2::wave_sum(pm == -INFINITY ? 0.f : ps * exp2f(pm - mm));
   if (lane == 0) {
-    float mm = -INFINITY;
-    for (int s = 0; s < n_split; ++s) mm = fmaxf(mm, part_m[(long)s * M + r]);
-    float ss = 0.f;
-    for (int s = 0; s < n_split; ++s) {
-      const float m = part_m[(long)s * M + r];
-      if (m != -INFINITY) ss += part_s[(long)s * M + r] * exp2f(m - mm);
-    }
     const float lse_items = (mm + log2f(ss)) / LOG2E;
     const float pl = padlogit[r];
     const float hi = fmaxf(lse_items, pl);
