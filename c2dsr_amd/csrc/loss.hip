@@ -373,18 +373,23 @@ __global__ __launch_bounds__(1024) void mi_loss_kernel(const float* __restrict__
       ds[k * B + b] = (sig - y) / Bn;
     }
   }
-  float tot = 0.f;
+  // fixed-order reduction: wave trees, then the wave sums in wave order (one barrier)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
   for (int k = 0; k < 4; ++k) {
-    red[threadIdx.x] = acc[k];
-    __syncthreads();
-    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    tot += red[0] / Bn;
-    __syncthreads();
+    const float v = c2::wave_sum(acc[k]);
+    if (lane == 0) red[k * 16 + w] = v;
   }
-  if (threadIdx.x == 0) *loss_mi = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int k = 0; k < 4; ++k) {
+      float t = 0.f;
+      for (int q = 0; q < nw; ++q) t += red[k * 16 + q];
+      tot += t / Bn;
+    }
+    *loss_mi = tot;
+  }
 }
 
 // Hcat = [hs_r ; hs_r + hx_r], Hpad = [hs_r ; hx_r] (rows (b, L-R+k)), tcat = [t_share_r ; t_spec_r]

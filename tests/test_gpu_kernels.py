@@ -837,8 +837,10 @@ def test_attention_rows_equals_full_layout(B, L, d, H, p, q_frac):
     g = torch.empty_like(qkv)
     lib('c2dsr_attn_bwd', qkv, sd, pad, B, L, d, H, 5, 6, p, 2, P, dout, g, s)
     qL, kL = torch.from_numpy(qi).long().to(DEV), torch.from_numpy(ki).long().to(DEV)
-    q = qkv[qL, :d].contiguous()
-    kv = qkv[kL, d:].contiguous()
+    # compact q / kv whose storage ENDS at the last row (a read past the last sequence's rows would leave the
+    # allocation: the round-1 attention fault's shape, for the row-subset kernels)
+    q = _tail_of_segment(qkv[qL, :d].contiguous().cpu())
+    kv = _tail_of_segment(qkv[kL, d:].contiguous().cpu())
     out_r = torch.empty(len(qi), d, device=DEV)
     lib('c2dsr_attn_fwd_rows', q, kv, sd, pad, rs.idx, rs.off, ks.idx, ks.off, B, L, d, H, 5, 6, p, 2, out_r, Pr, s)
     dq = torch.full((len(qi), d), 7.0, device=DEV)
