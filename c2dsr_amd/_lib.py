@@ -56,12 +56,14 @@ class HipLibError(RuntimeError):
 
 
 DEBUG_SYNC = os.environ.get('C2DSR_DEBUG_SYNC', '0') == '1'
+_FAST = os.environ.get('C2DSR_LIB_FAST', '1') == '1'
 
 
 class _Lib:
     def __init__(self):
         self._lib = None
         self._sigs = None
+        self._fns = {}  # name -> bound ctypes function (argtypes set)
         self.time_names = set()  # entry points bracketed by HIP events (bench.py roofline)
         self.timed = {}
         self.time_meta = {}  # name -> fn(args) evaluated at launch; its value is appended to the record
@@ -86,13 +88,16 @@ class _Lib:
         return sorted(self._sigs)
 
     def __call__(self, name: str, *args):
-        lib = self.load()
-        conv = []
-        for a in args:
-            if isinstance(a, torch.Tensor):
-                conv.append(a.data_ptr())
-            else:
-                conv.append(a)
+        fn = self._fns.get(name)
+        if fn is None:
+            fn = self._fns[name] = getattr(self.load(), name)
+        lib = self._lib
+        conv = [a.data_ptr() if isinstance(a, torch.Tensor) else a for a in args]
+        if _FAST and not DEBUG_SYNC and name not in self.time_names:  # the common path: one ctypes call
+            rc = fn(*conv)
+            if rc != 0:
+                raise HipLibError(f'{name} failed with hipError {rc}')
+            return rc
         if name in self.time_names:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -118,7 +123,10 @@ class _Lib:
         return rc
 
     def raw(self, name: str):
-        return getattr(self.load(), name)
+        fn = self._fns.get(name)
+        if fn is None:
+            fn = self._fns[name] = getattr(self.load(), name)
+        return fn
 
 
 lib = _Lib()
