@@ -19,7 +19,7 @@ import torch
 from torch.autograd import Function
 
 from ._lib import lib, stream
-from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm
+from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rgemm, rgemm_ok, weight_bf16, wgemm, wgemm_ok
 
 
 _NCU = None
@@ -101,8 +101,11 @@ class LossHeadFn(Function):
         # ---- bilinear: s = x1ᵀ W x2 (+b)  via  U = X2·Wᵀ, s = rowdot(x1, U) ----
         Ua = torch.empty(2 * B, d, **f32)
         Ub = torch.empty(2 * B, d, **f32)
-        gemm(X2a, m.Da_w, Ua, M=2 * B, N=d, K=d, transB=1, precision=FP32)
-        gemm(X2b, m.Db_w, Ub, M=2 * B, N=d, K=d, transB=1, precision=FP32)
+        for X2, Wd, U in ((X2a, m.Da_w, Ua), (X2b, m.Db_w, Ub)):
+            if m.precision == BF16 and rgemm_ok(2 * B, d, d):  # bf16 mode: the row-streaming MFMA GEMM
+                rgemm(X2, weight_bf16(Wd.view(d, d)), U, M=2 * B, N=d, K=d)
+            else:
+                gemm(X2, Wd, U, M=2 * B, N=d, K=d, transB=1, precision=FP32)
         S = torch.empty(4, B, **f32)
         lib('c2dsr_rowdot', Phx, d, Ua, d, B, d, m.Da_b, S[0], 1, s)
         lib('c2dsr_rowdot', Phx, d, Ua[B:], d, B, d, m.Da_b, S[1], 1, s)
@@ -256,9 +259,15 @@ class LossHeadFn(Function):
             lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
             lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
             dX2 = torch.empty(2 * B, d, **f32)
-            gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
+            b16 = m.precision == BF16 and rgemm_ok(2 * B, d, d) and wgemm_ok(2 * B, d, d)
+            if b16:
+                rgemm(dU, weight_bf16(Wd.view(d, d), trans=True), dX2, M=2 * B, N=d, K=d)
+            else:
+                gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
             gWd = _grad_target(Wd)
-            if gWd is not None:
+            if gWd is not None and b16:  # not deferred: the head range is reduced as this backward returns
+                wgemm(dU, X2, gWd.view(d, d), T=2 * B, N=d, D=d, defer=False)
+            elif gWd is not None:
                 gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
             gbd = _grad_target(bd)
             if gbd is not None:

@@ -197,11 +197,11 @@ class WGradBatch:
 WBATCH = None  # the active WGradBatch (Trainer.train_batch, bf16 mode), else None
 
 
-def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None):
+def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None, defer=True):
     """dW[N, D] = beta·dW + dYᵀ·X over T rows and (db given) db[N] = beta·db + Σ_t dY[t]
     (c2dsr_wgemm, deterministic split-t partials).  With a WGradBatch active (and beta = 1) the product is
     deferred into it."""
-    if WBATCH is not None and beta == 1.0 and dY.is_contiguous() and X.is_contiguous():
+    if defer and WBATCH is not None and beta == 1.0 and dY.is_contiguous() and X.is_contiguous():
         WBATCH.add(dY, X, dW, db, T, N, D)
         return
     ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
