@@ -315,15 +315,34 @@ __global__ __launch_bounds__(256) void ln2_bwd_kernel(const float* __restrict__ 
     wF4[q] = c < d ? *(const float4*)(wF + c) : c2::f4(0.f);
   }
   const long stride = (long)gridDim.x * GROUPS;
-  for (long r = (long)blockIdx.x * GROUPS + g; r < rows; r += stride) {
-    const float m2 = st[r], r2 = st[rows + r], mF = st[2l * rows + r], rF = st[3l * rows + r];
+  constexpr int RB = 2;  // rows per step per lane group: both rows' loads issued before the reductions
+  for (long r0 = (long)blockIdx.x * GROUPS + g; r0 < rows; r0 += RB * stride) {
+    float4 xin[RB][NC], din[RB][NC];
+    float stv[RB][4];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const long rk = r0 + k * stride;
+      const bool ok = rk < rows;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stv[k][j] = ok ? st[j * (long)rows + rk] : 0.f;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) {
+        const int c = (lane + q * LPR) * 4;
+        const bool in = ok && c < d;
+        xin[k][q] = in ? *(const float4*)(x + rk * d + c) : c2::f4(0.f);
+        din[k][q] = in ? *(const float4*)(dy + rk * d + c) : c2::f4(0.f);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+    const long r = r0 + k * stride;
+    if (r >= rows) break;  // uniform over the group
+    const float m2 = stv[k][0], r2 = stv[k][1], mF = stv[k][2], rF = stv[k][3];
     float4 xh2[NC], xhF[NC], gv[NC], dv[NC];
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
-      const int c = (lane + q * LPR) * 4;
-      const bool in = c < d;
-      const float4 xv = in ? *(const float4*)(x + r * d + c) : c2::f4(0.f);
-      dv[q] = in ? *(const float4*)(dy + r * d + c) : c2::f4(0.f);
+      const float4 xv = xin[k][q];
+      dv[q] = din[k][q];
       xh2[q] = make_float4((xv.x - m2) * r2, (xv.y - m2) * r2, (xv.z - m2) * r2, (xv.w - m2) * r2);
       // x2 exactly as the forward computed it: (x - m2)·r2·w2 + b2
       const float4 x2 = make_float4((xv.x - m2) * r2 * w24[q].x + b24[q].x, (xv.y - m2) * r2 * w24[q].y + b24[q].y,
@@ -367,6 +386,7 @@ __global__ __launch_bounds__(256) void ln2_bwd_kernel(const float* __restrict__ 
         if (drop.active()) o = o * drop.mul4((uint64_t)(idx_base + (rowmap ? rowmap[r] : r)) * d + c);
         *(float4*)(db_out + r * d + c) = o;
       }
+    }
     }
   }
   // block reduce of the per-group partials → part[block][4][d]
