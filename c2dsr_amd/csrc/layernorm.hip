@@ -469,7 +469,10 @@ int lpr_for(int d) {
   return l;
 }
 
-constexpr int LN_BWD_BLOCKS = 2048;  // 8 waves per SIMD at d=256 (grid-stride over rows)
+#ifndef LN_BWD_BLOCKS_CFG
+#define LN_BWD_BLOCKS_CFG 1024
+#endif
+constexpr int LN_BWD_BLOCKS = LN_BWD_BLOCKS_CFG;  // grid-stride over rows; 1024: half the partials of 2048 (LN bwd + reduce 88 -> 77 us per pass)
 
 }  // namespace
 
