@@ -98,6 +98,10 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work
   }
 }
 
+#ifndef COMBINE_U
+#define COMBINE_U 16
+#endif
+
 // split[s] = {row, slot_begin, slot_end}: sum the row's pieces in order, then the epilogue.
 template <int LPR, bool MASK_OUT>
 __global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ split, int n_split, int d, Epi ep,
@@ -111,7 +115,16 @@ __global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ s
   for (int c = lane * 4; c < d; c += LPR * 4) {
     float4 acc = c2::f4(0.f);
     int k = sp.y;
-    for (; k + 8 <= sp.z; k += 8) {  // eight pieces' loads in flight, added in piece order
+    // A hub row's combine is a latency chain (up to ~200 pieces at bench sizes): COMBINE_U pieces' loads in
+    // flight per round trip, then eight, added in piece order either way.
+    for (; k + COMBINE_U <= sp.z; k += COMBINE_U) {
+      float4 v[COMBINE_U];
+#pragma unroll
+      for (int u = 0; u < COMBINE_U; ++u) v[u] = *(const float4*)(part + (long)(k + u) * d + c);
+#pragma unroll
+      for (int u = 0; u < COMBINE_U; ++u) acc = acc + v[u];
+    }
+    for (; k + 8 <= sp.z; k += 8) {
       float4 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = *(const float4*)(part + (long)(k + u) * d + c);
