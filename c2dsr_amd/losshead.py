@@ -247,50 +247,14 @@ class LossHeadFn(Function):
         s = stream()
         f32 = dict(device=dev, dtype=torch.float32)
         gscale = gloss.contiguous().reshape(1)
-        # ---- discriminators ----
-        Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi
-        lib('c2dsr_scale_ds', dS, 4 * B, gscale, float(1.0 - m.lam), s)
-        dP = {}
-        for (x1, X2, U, Wd, bd, k) in ((Phx, X2a, Ua, m.Da_w, m.Da_b, 0), (Phy, X2b, Ub, m.Db_w, m.Db_b, 2)):
-            dx1 = torch.empty(B, d, **f32)
-            lib('c2dsr_rowscale', U, dS[k], B * d, d, dx1, 0, s)
-            lib('c2dsr_rowscale', U[B:], dS[k + 1], B * d, d, dx1, 1, s)
-            dU = torch.empty(2 * B, d, **f32)
-            lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
-            lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
-            dX2 = torch.empty(2 * B, d, **f32)
-            b16 = m.precision == BF16 and rgemm_ok(2 * B, d, d) and wgemm_ok(2 * B, d, d)
-            if b16:
-                rgemm(dU, weight_bf16(Wd.view(d, d), trans=True), dX2, M=2 * B, N=d, K=d)
-            else:
-                gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
-            gWd = _grad_target(Wd)
-            if gWd is not None and b16:  # not deferred: the head range is reduced as this backward returns
-                wgemm(dU, X2, gWd.view(d, d), T=2 * B, N=d, D=d, defer=False)
-            elif gWd is not None:
-                gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
-            gbd = _grad_target(bd)
-            if gbd is not None:
-                colsum(dS[k], 2 * B, 1, 1, gbd)
-            dP[k] = (dx1, dX2)
-        (dPhx, dX2a), (dPhy, dX2b) = dP[0], dP[2]
-        wa, wb = ctx.w
-        # the pooling backward WRITES the five encoder-output gradients (no zero fill); the classifier
-        # heads below add their last-R-position parts
-        # (row-subset outputs get row-subset gradients: pooling writes their rows, heads add through the maps)
-        dh_share, dhx, dhy, dh_na, dh_nb = [torch.empty(sh, **f32) for sh in ctx.hshapes]
-        rsets = ctx.rsets
-        sub = [(r.idx, r.n) if r is not None else (None, 0) for r in rsets]
-        mp = [r.inv if r is not None else None for r in rsets]
-        lib('c2dsr_pool2_bwd', dPhx, wa, None, None, B, L, d, *sub[1], 0, dhx, s)
-        lib('c2dsr_pool2_bwd', dPhy, wb, None, None, B, L, d, *sub[2], 0, dhy, s)
-        lib('c2dsr_pool2_bwd', dX2a, wb, dX2b, wa, B, L, d, *sub[0], 0, dh_share, s)
-        lib('c2dsr_pool2_bwd', dX2a[B:], wa, None, None, B, L, d, *sub[3], 0, dh_na, s)
-        lib('c2dsr_pool2_bwd', dX2b[B:], wb, None, None, B, L, d, *sub[4], 0, dh_nb, s)
         # ---- classifier heads ----
+        # (first: their CE kernels are the long ones, so the host's bookkeeping for the discriminators and the
+        # pooling below runs while they execute; the heads' input gradients are added after the pooling writes)
+        scat = []
+        rsets = ctx.rsets
+        mp = [r.inv if r is not None else None for r in rsets]
         gwpad, gbpad = _grad_target(m.wpad), _grad_target(m.bpad)
-        for k, ((Hcat, Hpad, tcat, logits, lse, rows, W, bias, n), coef, hdom_grad) in enumerate(
-                zip(ctx.heads, ctx.coefs, (dhx, dhy))):
+        for k, ((Hcat, Hpad, tcat, logits, lse, rows, W, bias, n), coef) in enumerate(zip(ctx.heads, ctx.coefs)):
             M2 = 2 * BR
             dHcat = torch.empty(M2, d, **f32)
             gW, gb = _grad_target(W), _grad_target(bias)
@@ -350,9 +314,49 @@ class LossHeadFn(Function):
                 lib('c2dsr_wcolsum', Hpad, M2, d, d, pad_col, pad_ld, 1.0, 1.0, gwpad, ws, s)
             if gbpad is not None:
                 colsum(pad_col, M2, 1, pad_ld, gbpad)
+            scat.append((dHcat, pad_col, pad_ld, k))
+        # ---- discriminators ----
+        Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi
+        lib('c2dsr_scale_ds', dS, 4 * B, gscale, float(1.0 - m.lam), s)
+        dP = {}
+        for (x1, X2, U, Wd, bd, k) in ((Phx, X2a, Ua, m.Da_w, m.Da_b, 0), (Phy, X2b, Ub, m.Db_w, m.Db_b, 2)):
+            dx1 = torch.empty(B, d, **f32)
+            lib('c2dsr_rowscale', U, dS[k], B * d, d, dx1, 0, s)
+            lib('c2dsr_rowscale', U[B:], dS[k + 1], B * d, d, dx1, 1, s)
+            dU = torch.empty(2 * B, d, **f32)
+            lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
+            lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
+            dX2 = torch.empty(2 * B, d, **f32)
+            b16 = m.precision == BF16 and rgemm_ok(2 * B, d, d) and wgemm_ok(2 * B, d, d)
+            if b16:
+                rgemm(dU, weight_bf16(Wd.view(d, d), trans=True), dX2, M=2 * B, N=d, K=d)
+            else:
+                gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
+            gWd = _grad_target(Wd)
+            if gWd is not None and b16:  # not deferred: the head range is reduced as this backward returns
+                wgemm(dU, X2, gWd.view(d, d), T=2 * B, N=d, D=d, defer=False)
+            elif gWd is not None:
+                gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
+            gbd = _grad_target(bd)
+            if gbd is not None:
+                colsum(dS[k], 2 * B, 1, 1, gbd)
+            dP[k] = (dx1, dX2)
+        (dPhx, dX2a), (dPhy, dX2b) = dP[0], dP[2]
+        wa, wb = ctx.w
+        # the pooling backward WRITES the five encoder-output gradients (no zero fill); the classifier
+        # heads below add their last-R-position parts
+        # (row-subset outputs get row-subset gradients: pooling writes their rows, heads add through the maps)
+        dh_share, dhx, dhy, dh_na, dh_nb = [torch.empty(sh, **f32) for sh in ctx.hshapes]
+        sub = [(r.idx, r.n) if r is not None else (None, 0) for r in rsets]
+        lib('c2dsr_pool2_bwd', dPhx, wa, None, None, B, L, d, *sub[1], 0, dhx, s)
+        lib('c2dsr_pool2_bwd', dPhy, wb, None, None, B, L, d, *sub[2], 0, dhy, s)
+        lib('c2dsr_pool2_bwd', dX2a, wb, dX2b, wa, B, L, d, *sub[0], 0, dh_share, s)
+        lib('c2dsr_pool2_bwd', dX2a[B:], wa, None, None, B, L, d, *sub[3], 0, dh_na, s)
+        lib('c2dsr_pool2_bwd', dX2b[B:], wb, None, None, B, L, d, *sub[4], 0, dh_nb, s)
+        for dHcat, pad_col, pad_ld, k in scat:
             # classifier_pad's input gradient (pad column ⊗ wpad) is folded into the scatter
-            lib('c2dsr_rec_scatter', dHcat, pad_col, pad_ld, m.wpad, B, L, d, R, dh_share, mp[0], hdom_grad, mp[1 + k],
-                s)
+            lib('c2dsr_rec_scatter', dHcat, pad_col, pad_ld, m.wpad, B, L, d, R, dh_share, mp[0], (dhx, dhy)[k],
+                mp[1 + k], s)
         # the saved buffers (bf16 images, logits / lse, plans) are released with the backward even if a
         # caller keeps the graph alive (e.g. an undetached loss accumulator)
         if m.on_head_grads is not None:  # the classifier / discriminator gradients are final: their

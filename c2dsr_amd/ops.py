@@ -519,19 +519,46 @@ class IndexPlan:
     side stream as soon as the forward sees the indices, so the sort runs under the forward kernels;
     ``get()`` orders the current stream after it and returns the plan buffer."""
 
-    def __init__(self, idx, n_keys):
-        n = idx.numel()
-        nb = int(lib.raw('c2dsr_index_plan_bytes')(n))
-        self.buf = torch.empty(nb, dtype=torch.uint8, device=idx.device)
-        PLAN_SRC[self.buf.data_ptr()] = idx.data_ptr()
-        side = side_stream(idx.device) if _PLAN_SIDE else torch.cuda.current_stream(idx.device)
-        side.wait_stream(torch.cuda.current_stream(idx.device))  # idx and buf are ready
-        lib('c2dsr_index_plan', idx, n, int(n_keys), self.buf, nb, side.cuda_stream)
+    def __init__(self, idx, n_keys, _batch=None):
+        if _batch is not None:  # a slice of IndexPlan.many's buffer (launched there)
+            self.buf, self.ev = _batch
+            return
+        nb = int(lib.raw('c2dsr_index_plan_bytes')(idx.numel()))
+        buf = torch.empty(nb, dtype=torch.uint8, device=idx.device)
+        self.buf, self.ev = IndexPlan._launch([(idx, n_keys)], [buf], [nb], buf)[0]
         if _CHECK_PLANS:
             self.idx, self.n_keys = idx, int(n_keys)
-        self.buf.record_stream(side)
-        self.ev = torch.cuda.Event()
-        self.ev.record(side)
+
+    @staticmethod
+    def _launch(pairs, bufs, sizes, whole):
+        dev = whole.device
+        side = side_stream(dev) if _PLAN_SIDE else torch.cuda.current_stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))  # the indices and the buffer are ready
+        for (idx, n_keys), buf, nb in zip(pairs, bufs, sizes):
+            PLAN_SRC[buf.data_ptr()] = idx.data_ptr()
+            lib('c2dsr_index_plan', idx, idx.numel(), int(n_keys), buf, nb, side.cuda_stream)
+        whole.record_stream(side)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        return [(buf, ev) for buf in bufs]
+
+    @staticmethod
+    def many(pairs):
+        """Plans of several (idx, n_keys) in one buffer, one stream hand-off and one event (the host cost of
+        a plan is mostly its Python bookkeeping: one training step builds eight)."""
+        sizes = [int(lib.raw('c2dsr_index_plan_bytes')(idx.numel())) for idx, _ in pairs]
+        whole = torch.empty(sum(sizes), dtype=torch.uint8, device=pairs[0][0].device)  # sizes are 256-aligned
+        bufs, o = [], 0
+        for nb in sizes:
+            bufs.append(whole[o:o + nb])
+            o += nb
+        out = []
+        for (idx, n_keys), be in zip(pairs, IndexPlan._launch(pairs, bufs, sizes, whole)):
+            pl = IndexPlan(None, None, _batch=be)
+            if _CHECK_PLANS:
+                pl.idx, pl.n_keys = idx, int(n_keys)
+            out.append(pl)
+        return out
 
     def get(self):
         torch.cuda.current_stream(self.buf.device).wait_event(self.ev)
@@ -601,6 +628,25 @@ def index_plan(state, idx, n_keys):
             cache.clear()
         pl = cache[key] = IndexPlan(idx, n_keys)
     return pl
+
+
+def index_plans(state, pairs):
+    """index_plan of every (idx, n_keys) of ``pairs`` (those not cached yet built by one IndexPlan.many)."""
+    cache = getattr(state, 'plans', None) if state is not None else None
+    if cache is None:
+        return IndexPlan.many(pairs)
+    if cache and next(iter(cache))[0] != state.step:
+        cache.clear()
+    todo, keys = [], []
+    for idx, n_keys in pairs:
+        key = (state.step, idx.data_ptr(), idx.numel(), int(n_keys))
+        if key not in cache and key not in keys:
+            todo.append((idx, n_keys))
+            keys.append(key)
+    if todo:
+        for key, pl in zip(keys, IndexPlan.many(todo)):
+            cache[key] = pl
+    return [cache[(state.step, idx.data_ptr(), idx.numel(), int(n_keys))] for idx, n_keys in pairs]
 
 
 # ----------------------------------------------------------------------------- embedding fuse (K2)

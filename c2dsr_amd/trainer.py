@@ -235,9 +235,9 @@ class Trainer(object):
         if m.training:
             # the embedding backward's sort plans of every pass, enqueued on the side stream now (while the GCN
             # forward runs) rather than from inside each pass's forward
-            for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b), (neg_a, pos), (neg_b, pos)):
-                ops.index_plan(m.state, sq, m.n_item)
-                ops.index_plan(m.state, ps, m.attn_share.len_max)
+            ops.index_plans(m.state, [pr for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b),
+                                                         (neg_a, pos), (neg_b, pos))
+                                       for pr in ((sq, m.n_item), (ps, m.attn_share.len_max))])
         m.state.need, m.state.pad_rows, m.state.compact_out = need, pads, bool(need)
         try:
             h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
