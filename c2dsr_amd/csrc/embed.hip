@@ -157,7 +157,10 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
 // the chunks' head/tail slots.  A "split" is a run that continues past the end of its first
 // chunk: out[key] += tail[c] + head[c+1] + ... + head[last], summed in chunk order (pass B).  The
 // split list depends on the indices only, so it is part of the plan (off the critical path).
-constexpr int SEG_CH = 32;
+#ifndef SEG_CH_CFG
+#define SEG_CH_CFG 32
+#endif
+constexpr int SEG_CH = SEG_CH_CFG;
 constexpr int PL_T = 256;         // plan kernels: threads per block
 constexpr int PL_E = 4;           // entries per thread
 constexpr int PL_B = PL_T * PL_E;  // entries per block

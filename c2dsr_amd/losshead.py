@@ -57,6 +57,12 @@ class LossMeta:
         del self.__dict__['self']
         self.pending = None
         self.on_head_grads = None  # data parallel: called when the backward has written the head gradients
+        self.after_first_ce = None  # host work to enqueue once the first long CE kernel is queued (or at the end)
+
+    def run_after_first_ce(self):
+        f, self.after_first_ce = self.after_first_ce, None
+        if f is not None:
+            f()
 
     def finish_values(self):
         """Data parallel: wait for the loss values' sums and recompute (loss, loss_rec, loss_mi) from them
@@ -192,6 +198,7 @@ class LossHeadFn(Function):
                     lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tc, Hc, W, bias,
                         lse_c, lse2, rows_c, s)
                     u = (Up, pm, ns)
+                    m.run_after_first_ce()
                 elif Mv:
                     ns = split_count(Mv, 256)
                     pm = torch.empty(ns, Mv, **f32)
@@ -235,6 +242,7 @@ class LossHeadFn(Function):
         loss, loss_rec, loss_mi_o = out3[0], out3[1], out3[2]
         ctx.mark_non_differentiable(loss_rec, loss_mi_o)
         ctx.set_materialize_grads(False)  # no zero scalars for the two reported losses
+        m.run_after_first_ce()
         return loss, loss_rec, loss_mi_o
 
     @staticmethod

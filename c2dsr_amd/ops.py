@@ -667,9 +667,10 @@ class EmbedFn(Function):
         ctx.link = link
         ctx.plans = None
         if any(ctx.needs_input_grad[:3]) and (P.requires_grad or sink is not None):  # forward runs under no_grad
-            state = sink.state if sink is not None else None
-            ctx.plans = (index_plan(state, seq, E.shape[0]) if sink is not None else None,
-                         index_plan(state, pos, P.shape[0]) if P.requires_grad else None)
+            # the sort plans are looked up (or built) when the backward needs them: a trainer enqueues the step's
+            # plans where the stream has long kernels queued (trainer.train_batch), not between these launches
+            ctx.plans = (sink.state if sink is not None else None, sink is not None, E.shape[0], P.requires_grad,
+                         P.shape[0])
         return x
 
     @staticmethod
@@ -678,6 +679,10 @@ class EmbedFn(Function):
         B, L = seq.shape
         d = gx.shape[-1]
         n = B * L
+        if ctx.plans is not None:
+            state, on_seq, n_seq, on_pos, n_pos = ctx.plans
+            ctx.plans = (index_plan(state, seq, n_seq) if on_seq else None,
+                         index_plan(state, pos, n_pos) if on_pos else None)
         parts = ctx.link.take() if ctx.link is not None else None  # gx is a placeholder then (RowsGrad)
         G = ctx.sink.buf() if ctx.sink is not None else None
         gP = _grad_target(ctx.P)

@@ -232,12 +232,15 @@ class Trainer(object):
         self.dp_counts = None
         need, pads, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b,
                                           (seq_share, seq_a, seq_b, neg_a, neg_b))
+        plans = None
         if m.training:
-            # the embedding backward's sort plans of every pass, enqueued on the side stream now (while the GCN
-            # forward runs) rather than from inside each pass's forward
-            ops.index_plans(m.state, [pr for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b),
-                                                         (neg_a, pos), (neg_b, pos))
-                                       for pr in ((sq, m.n_item), (ps, m.attn_share.len_max))])
+            # the embedding backward's sort plans of every pass (side stream), enqueued by the loss head right
+            # after its first long CE launch: ~110 small launches the host issues while the device is busy,
+            # instead of ahead of the encoder passes, whose first kernels would wait behind them
+            st = m.state
+            pairs = [pr for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b), (neg_a, pos), (neg_b, pos))
+                     for pr in ((sq, m.n_item), (ps, m.attn_share.len_max))]
+            plans = lambda: ops.index_plans(st, pairs)  # noqa: E731
         m.state.need, m.state.pad_rows, m.state.compact_out = need, pads, bool(need)
         try:
             h_share, hx, hy = m(seq_share, seq_a, seq_b, pos, pos_a, pos_b)
@@ -247,6 +250,7 @@ class Trainer(object):
             m.state.need, m.state.pad_rows, m.state.compact_out = {}, {}, False
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
         meta.ce_pre = ce_pre
+        meta.after_first_ce = plans
         if self.dp_counts is not None:
             meta.counts = self.dp_counts
             meta.reduce_async = lambda t: dist.all_reduce(t, async_op=True)  # noqa: E731
