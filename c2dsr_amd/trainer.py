@@ -10,6 +10,7 @@ the reference (zero_grad only at the start of run_epoch, Q3).
 """
 from __future__ import annotations
 
+import gc
 import os
 import time
 from os.path import join
@@ -27,6 +28,8 @@ from .losshead import LossHeadFn, LossMeta
 from .metrics import RankMetrics
 from .models.C2DSR import C2DSR
 from .optim import FlatAdamW
+
+_GC_STEP = os.environ.get('C2DSR_GC_STEP', '1') == '1'
 
 
 def dp_rows(B_full, rank, world, dp_split=True, global_rows=None):
@@ -223,7 +226,18 @@ class Trainer(object):
     def train_batch(self, batch, *, global_rows=None):
         """trainer.py:91-160.  ``batch``: 14 int64 [B, L] tensors (host or device).  Under data
         parallelism each rank trains its slice of the global batch (or, with ``dp_split=False``, its
-        own batch; ``global_rows`` then gives the global batch size)."""
+        own batch; ``global_rows`` then gives the global batch size).
+        Python's cyclic collector is paused while the step is enqueued (a collection in the middle of the
+        launch sequence leaves the device idle); it runs after the optimizer launch, under that kernel."""
+        if not _GC_STEP or not gc.isenabled():
+            return self._train_batch(batch, global_rows=global_rows)
+        gc.disable()
+        try:
+            return self._train_batch(batch, global_rows=global_rows)
+        finally:
+            gc.enable()
+
+    def _train_batch(self, batch, *, global_rows=None):
         lo, hi, row_offset, B_global = dp_rows(batch[0].shape[0], self.rank, self.world, self.dp_split, global_rows)
         (seq_share, seq_a, seq_b, pos, pos_a, pos_b, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, neg_a,
          neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
