@@ -76,13 +76,14 @@ class KernelTimer:
     logits GEMMs (c2dsr_gemm calls of > 1e11 FLOP)."""
 
     NAMES_BF16 = ('c2dsr_ce_fused_fwd_u', 'c2dsr_ce_fused_fwd', 'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
+    NAMES_X3 = ('c2dsr_ce3_fused_fwd_u', 'c2dsr_ce3_fused_dw')
     # credited products per launch: fwd_u = the lse logits + the softmax·W part of dH (online, one sweep)
-    CREDIT = {'c2dsr_ce_fused_fwd_u': 2}
+    CREDIT = {'c2dsr_ce_fused_fwd_u': 2, 'c2dsr_ce3_fused_fwd_u': 2}
 
     def __init__(self, precision):
         from c2dsr_amd._lib import lib
         self.lib = lib
-        self.names = self.NAMES_BF16 if precision == 'bf16' else ('c2dsr_gemm',)
+        self.names = {'bf16': self.NAMES_BF16, 'fp32': self.NAMES_X3}.get(precision, ('c2dsr_gemm',))
 
     def start(self):
         self.lib.timed.clear()
@@ -375,7 +376,7 @@ def main():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', default='mb', choices=list(CONFIGS) + ['c5'])
-    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32', 'fp32_exact'])
     ap.add_argument('--batch', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=20.0)

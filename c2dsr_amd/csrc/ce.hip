@@ -1219,6 +1219,17 @@ C2_API int c2dsr_ce_fused_fwd_u(const void* Hb, const void* Wb, const float* bia
   return 0;
 }
 
+// per row: lse over the splits' (max, sum) partials and the pad column, target logit, loss (see ce_rows_kernel)
+C2_API int c2dsr_ce_rows(const float* part_m, const float* part_s, int n_split, int M, const float* padlogit,
+                         const int64_t* tgt, int n, const float* H, const float* W, const float* bias, int D,
+                         float* lse, float* lse2, float* loss_row, void* stream) {
+  if (M == 0) return 0;
+  ce_rows_kernel<<<c2::ceil_div(M, 4), 256, 0, (hipStream_t)stream>>>(part_m, part_s, n_split, M, padlogit, tgt, n, H,
+                                                                     W, bias, D, lse, lse2, loss_row);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
 C2_API int c2dsr_ce_dh_from_u(const float* Up, const float* part_m, int ns, int M, int D, const float* lse2,
                               const int* t32, const float* rw, const float* W, int n, float* dH, void* stream) {
   if (M == 0) return 0;

@@ -74,11 +74,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_bytes(const void* base, l
 // AB16: A is bf16 in HBM (the attention backward's dqkv, c2dsr_rgemm_aux_b16a): the same [32][256] chunk
 // lands as 8-byte loads and is staged without conversion — half the bytes of the fp32 stream, identical
 // products (the fp32 path rounds A to bf16 the same way, RNE).
-template <int KCH, int CT, bool EPI, int AUX = AUX_NONE, bool AB16 = false>
+// X3 (fp32 mode, c2dsr_rgemm_x3): split-bf16 operands — B is the image [N][2K] = hi ‖ lo (ldb = 2K) held in
+// registers as two fragment sets, each A chunk is staged as hi = RNE(a) and lo = RNE(a − hi) in two LDS
+// images, and every k-step runs three MFMAs (a_hi·b_hi + a_lo·b_hi + a_hi·b_lo; see ce3.hip for the error
+// bound: ≈3·2^-17 relative per product term, fp32 accumulation).
+template <int KCH, int CT, bool EPI, int AUX = AUX_NONE, bool AB16 = false, bool X3 = false>
 __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void* __restrict__ A, long lda,
                                                  const bf16* __restrict__ B, long ldb, float* C,
                                                  long ldc, Epi2 ep, int G) {
-  __shared__ __attribute__((aligned(16))) char aimg[2][32 * 256 * 2];
+  static_assert(!(AB16 && X3), "split operands take fp32 A");
+  constexpr int AIMG = 32 * 256 * 2;  // bytes of one [32][256] bf16 image (X3: lo image right after hi)
+  __shared__ __attribute__((aligned(16))) char aimg[2][(X3 ? 2 : 1) * AIMG];
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int nslots = gridDim.x >> 3;
   const int nwalk = nslots / G;
@@ -92,19 +98,26 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
   const int ncol0 = g * (128 * CT) + w * (32 * CT);  // this wave's first column
   // ---- B fragments → registers (once): lane (j = l&31, kh) holds B[col j][16ks + 8kh .. +7]
   bf16x8 bq[CT][KCH * 16];
+  bf16x8 bl[X3 ? CT : 1][X3 ? KCH * 16 : 1];  // X3: the lo fragments
   float bcol[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     const int col = min(ncol0 + ct * 32 + (lane & 31), N - 1);
 #pragma unroll
-    for (int ks = 0; ks < KCH * 16; ++ks) bq[ct][ks] = *(const bf16x8*)(B + (long)col * ldb + ks * 16 + 8 * (lane >> 5));
+    for (int ks = 0; ks < KCH * 16; ++ks) {
+      bq[ct][ks] = *(const bf16x8*)(B + (long)col * ldb + ks * 16 + 8 * (lane >> 5));
+      if constexpr (X3) bl[ct][ks] = *(const bf16x8*)(B + (long)col * ldb + K + ks * 16 + 8 * (lane >> 5));
+    }
     bcol[ct] = ep.bias ? ep.bias[col] : 0.f;
   }
   // land every loop-invariant register operand here, where the compiler sees the wait
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
 #pragma unroll
-    for (int ks = 0; ks < KCH * 16; ++ks) pin(bq[ct][ks]);
+    for (int ks = 0; ks < KCH * 16; ++ks) {
+      pin(bq[ct][ks]);
+      if constexpr (X3) pin(bl[ct][ks]);
+    }
     pin(bcol[ct]);
   }
   vm_drain();
@@ -178,6 +191,12 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
         v_[0] = (bf16)P[u].x; v_[1] = (bf16)P[u].y; v_[2] = (bf16)P[u].z; v_[3] = (bf16)P[u].w;                \
       }                                                                                                        \
       *(bf16x4*)((im) + aoff(lrow + 4 * u, 4 * lane)) = v_;                                                   \
+      if constexpr (X3) {                                                                                      \
+        bf16x4 l_;                                                                                             \
+        l_[0] = (bf16)(P[u].x - (float)v_[0]); l_[1] = (bf16)(P[u].y - (float)v_[1]);                          \
+        l_[2] = (bf16)(P[u].z - (float)v_[2]); l_[3] = (bf16)(P[u].w - (float)v_[3]);                          \
+        *(bf16x4*)((im) + AIMG + aoff(lrow + 4 * u, 4 * lane)) = l_;                                           \
+      }                                                                                                        \
     }                                                                                                          \
   }
   f32x16 acc[CT];
@@ -195,6 +214,13 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
       const bf16x8 af_ = *(const bf16x8*)(im_ + aoff(lane & 31, ks * 16 + 8 * (lane >> 5)));                   \
       _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) acc[ct] =                                              \
           __builtin_amdgcn_mfma_f32_32x32x16_bf16(af_, bq[ct][(KC) * 16 + ks], acc[ct], 0, 0, 0);              \
+      if constexpr (X3) {                                                                                      \
+        const bf16x8 al_ = *(const bf16x8*)(im_ + AIMG + aoff(lane & 31, ks * 16 + 8 * (lane >> 5)));          \
+        _Pragma("unroll") for (int ct = 0; ct < CT; ++ct) {                                                    \
+          acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al_, bq[ct][(KC) * 16 + ks], acc[ct], 0, 0, 0);    \
+          acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af_, bl[ct][(KC) * 16 + ks], acc[ct], 0, 0, 0);    \
+        }                                                                                                      \
+      }                                                                                                        \
     }                                                                                                          \
     if constexpr ((KC) == KCH - 1) epilogue(min((c) / KCH, ntile - 1), (c) / KCH < ntile);                    \
     RG_STAGE(S, aimg[((c) + 1) & 1])                                                                           \
@@ -337,13 +363,17 @@ __device__ __forceinline__ V wg_pick(const V (&a)[WG_MAXSEG], int k) {  // unifo
   return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3];
 }
 
-template <bool YB16>
+// X3 (fp32 mode, c2dsr_wgemm_x3): both chunks staged as split-bf16 hi and lo images, three MFMAs per step
+// (y_hi·x_hi + y_lo·x_hi + y_hi·x_lo, fp32 accumulation; the bias column sums stay exact fp32).
+template <bool YB16, bool X3 = false>
 __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restrict__ part,
                                                  float* __restrict__ part_b, int NTL, int rows_per_split) {
+  static_assert(!(YB16 && X3), "split operands take fp32 dY");
   const int T = sg.vbeg[WG_MAXSEG];  // virtual rows (entries past nseg repeat the total)
+  constexpr int YIMG = 32 * 128 * 2, XIMG = 32 * 256 * 2;  // bytes per image (X3: lo image after hi)
   __shared__ __attribute__((aligned(16))) float4 red_b[8][32];
-  __shared__ __attribute__((aligned(16))) char yimg[2][32 * 128 * 2];
-  __shared__ __attribute__((aligned(16))) char ximg[2][32 * 256 * 2];
+  __shared__ __attribute__((aligned(16))) char yimg[2][(X3 ? 2 : 1) * YIMG];
+  __shared__ __attribute__((aligned(16))) char ximg[2][(X3 ? 2 : 1) * XIMG];
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int nslots = gridDim.x >> 3;
   const int per_x = nslots / NTL;  // splits per XCD
@@ -386,11 +416,18 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
                                              xsrc, (t0_ + lrow + 4 * u) * ldxb + 16 * lane, 0, 0));           \
     }                                                                                                         \
   }
-#define WG_PUT(im, row, col, v4)                                                                              \
+#define WG_PUT(im, LOFF, row, col, v4)                                                                        \
   {                                                                                                           \
     bf16x4 b_;                                                                                                \
     b_[0] = (bf16)(v4).x; b_[1] = (bf16)(v4).y; b_[2] = (bf16)(v4).z; b_[3] = (bf16)(v4).w;                   \
-    *(bf16x4*)((im) + ((col) >> 7) * (32 * 256) + swz(row, ((col) & 127) >> 3) + 2 * ((col) & 7)) = b_;       \
+    const int o_ = ((col) >> 7) * (32 * 256) + swz(row, ((col) & 127) >> 3) + 2 * ((col) & 7);               \
+    *(bf16x4*)((im) + o_) = b_;                                                                               \
+    if constexpr (X3) {                                                                                       \
+      bf16x4 l_;                                                                                              \
+      l_[0] = (bf16)((v4).x - (float)b_[0]); l_[1] = (bf16)((v4).y - (float)b_[1]);                           \
+      l_[2] = (bf16)((v4).z - (float)b_[2]); l_[3] = (bf16)((v4).w - (float)b_[3]);                           \
+      *(bf16x4*)((im) + (LOFF) + o_) = l_;                                                                    \
+    }                                                                                                         \
   }
 // staging chunk cc also adds its dY rows into the column sums (the bias gradient): this thread
 // always holds columns n_base + 4·(tid & 31) of rows (tid >> 5) + 8u; clamped re-loads past the
@@ -400,13 +437,13 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
     const float on_ = (cc) < nchunk ? 1.f : 0.f;                                                              \
     _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
       const int q_ = threadIdx.x + 256 * u;                                                                   \
-      WG_PUT(yimg[b], q_ >> 5, 4 * (q_ & 31), PY[u])                                                          \
+      WG_PUT(yimg[b], YIMG, q_ >> 5, 4 * (q_ & 31), PY[u])                                                    \
       csum.x = fmaf(on_, PY[u].x, csum.x);                                                                    \
       csum.y = fmaf(on_, PY[u].y, csum.y);                                                                    \
       csum.z = fmaf(on_, PY[u].z, csum.z);                                                                    \
       csum.w = fmaf(on_, PY[u].w, csum.w);                                                                    \
     }                                                                                                         \
-    _Pragma("unroll") for (int u = 0; u < 8; ++u) WG_PUT(ximg[b], lrow + 4 * u, 4 * lane, PX[u])              \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) WG_PUT(ximg[b], XIMG, lrow + 4 * u, 4 * lane, PX[u])        \
   }
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
   f32x16 acc[2][4];
@@ -428,6 +465,15 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
       _Pragma("unroll") for (int b = 0; b < 4; ++b) fb_[b] = tr32(xi_, 16 * kst, wi + 32 * b, lane);          \
       _Pragma("unroll") for (int a = 0; a < 2; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) acc[a][b] = \
           __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_[a], fb_[b], acc[a][b], 0, 0, 0);                        \
+      if constexpr (X3) {                                                                                     \
+        bf16x8 fal_[2], fbl_[4];                                                                              \
+        _Pragma("unroll") for (int a = 0; a < 2; ++a) fal_[a] = tr32(yi_ + YIMG, 16 * kst, wn + 32 * a, lane); \
+        _Pragma("unroll") for (int b = 0; b < 4; ++b) fbl_[b] = tr32(xi_ + XIMG, 16 * kst, wi + 32 * b, lane); \
+        _Pragma("unroll") for (int a = 0; a < 2; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) {        \
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fal_[a], fb_[b], acc[a][b], 0, 0, 0);           \
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_[a], fbl_[b], acc[a][b], 0, 0, 0);           \
+        }                                                                                                     \
+      }                                                                                                       \
     }                                                                                                         \
     WG_STAGE(SY, SX, ((c) + 1) & 1, (c) + 1)                                                                  \
     __syncthreads();                                                                                          \
@@ -549,8 +595,9 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
 static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, const void* B, int ldb, float* C,
                       int ldc, float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1,
                       float p, int64_t row_base, const int* rowmap, int aux_mode, const float* aux,
-                      const int* auxmap, float aux_scale, void* stream) {
+                      const int* auxmap, float aux_scale, void* stream, bool x3 = false) {
   if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
+  if (x3 && (ab16 || (K != 256 && K != 512) || ldb < 2 * K)) return (int)hipErrorInvalidValue;
   if (ab16 && (epilogue || aux_mode == AUX_MASK || (K != 768 && aux_mode == AUX_ACC_MAP) ||
                (K == 512 && aux_mode != AUX_NONE)))
     return (int)hipErrorInvalidValue;
@@ -567,10 +614,10 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
     if (ncu <= 0) ncu = 256;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int CT = K == 256 ? 2 : 1;
+  const int CT = K == 256 && !x3 ? 2 : 1;
   const int G = c2::ceil_div(N, 128 * CT);
   // persistent grid: exactly the workgroups that are resident at once (occupancy of the variant)
-  static int per_cu[21] = {0};
+  static int per_cu[31] = {0};
   auto launch = [&](void (*kern)(int, int, int, const void*, long, const bf16*, long, float*, long, Epi2, int),
                     int slot) -> int {
     if (!per_cu[slot]) {
@@ -585,7 +632,20 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
   };
   int rc;
   const bool e = epilogue == 1;
-  if (ab16 && K == 256) {  // the row-subset attention's bf16 dq (+ the parked LN gradient)
+  if (x3) {  // split-bf16 operands (fp32 mode): one 32-column tile per wave (hi + lo fragments in registers)
+    const bool k1 = K == 256;
+    if (aux_mode == AUX_ACC)
+      rc = k1 ? launch(rg_kernel<1, 1, false, AUX_ACC, false, true>, 21) : launch(rg_kernel<2, 1, false, AUX_ACC, false, true>, 22);
+    else if (aux_mode == AUX_ACC_MAP)
+      rc = k1 ? launch(rg_kernel<1, 1, false, AUX_ACC_MAP, false, true>, 23)
+              : launch(rg_kernel<2, 1, false, AUX_ACC_MAP, false, true>, 24);
+    else if (aux_mode == AUX_MASK)
+      rc = k1 ? launch(rg_kernel<1, 1, false, AUX_MASK, false, true>, 25) : launch(rg_kernel<2, 1, false, AUX_MASK, false, true>, 26);
+    else if (e)
+      rc = k1 ? launch(rg_kernel<1, 1, true, AUX_NONE, false, true>, 27) : launch(rg_kernel<2, 1, true, AUX_NONE, false, true>, 28);
+    else
+      rc = k1 ? launch(rg_kernel<1, 1, false, AUX_NONE, false, true>, 29) : launch(rg_kernel<2, 1, false, AUX_NONE, false, true>, 30);
+  } else if (ab16 && K == 256) {  // the row-subset attention's bf16 dq (+ the parked LN gradient)
     rc = aux_mode == AUX_ACC ? launch(rg_kernel<1, 2, false, AUX_ACC, true>, 18)
                              : launch(rg_kernel<1, 2, false, AUX_NONE, true>, 19);
   } else if (ab16 && K == 512) {  // ... and its bf16 dkv
@@ -637,6 +697,18 @@ C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const v
                     aux_mode, aux, auxmap, aux_scale, stream);
 }
 
+// fp32 mode: split-bf16 products (B = the split image [N][2K] = hi ‖ lo, ldb >= 2K; K = 256 or 512)
+C2_API int c2dsr_rgemm_x3_supported(int M, int N, int K) {
+  return c2dsr_rgemm_supported(M, N, K) && (K == 256 || K == 512);
+}
+C2_API int c2dsr_rgemm_x3(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                          float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                          int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
+                          float aux_scale, void* stream) {
+  return rgemm_impl(M, N, K, A, false, lda, B, ldb, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, rowmap,
+                    aux_mode, aux, auxmap, aux_scale, stream, true);
+}
+
 // the same with A bf16 (K = 768, no epilogue, aux modes 0 / 1 / 3)
 C2_API int c2dsr_rgemm_aux_b16a(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
                                 float alpha, float beta, const float* bias, int aux_mode, const float* aux,
@@ -662,7 +734,7 @@ C2_API int c2dsr_wgemm_supported(int T, int N, int D) {
 }
 C2_API size_t c2dsr_wgemm_workspace(int N) { return (size_t)wg_splits(N) * N * 257 * 4; }
 static int wgemm_segs(const WSeg& sg, int N, int D, bool yb16, float beta, float* dW, float* db, void* part,
-                      void* stream) {
+                      void* stream, bool x3 = false) {
   const int T = sg.vbeg[WG_MAXSEG];
   if (T == 0) return 0;
   if (!c2dsr_wgemm_supported(T, N, D)) return (int)hipErrorInvalidValue;
@@ -674,7 +746,10 @@ static int wgemm_segs(const WSeg& sg, int N, int D, bool yb16, float beta, float
   const int blocks = splits * NTL;  // = 8 XCDs x (splits/8) x NTL
   const long n = (long)N * 256;
   float* part_b = db ? (float*)part + (long)splits * n : nullptr;
-  if (yb16)
+  if (x3 && yb16) return (int)hipErrorInvalidValue;
+  if (x3)
+    wg_kernel<false, true><<<blocks, 256, 0, s>>>(N, sg, (float*)part, part_b, NTL, rows);
+  else if (yb16)
     wg_kernel<true><<<blocks, 256, 0, s>>>(N, sg, (float*)part, part_b, NTL, rows);
   else
     wg_kernel<false><<<blocks, 256, 0, s>>>(N, sg, (float*)part, part_b, NTL, rows);
@@ -686,7 +761,7 @@ static int wgemm_segs(const WSeg& sg, int N, int D, bool yb16, float beta, float
 }
 
 static int wgemm_impl(int T, int N, int D, const void* dY, bool yb16, int ldy, const float* X, int ldx, float beta,
-                      float* dW, float* db, void* part, void* stream) {
+                      float* dW, float* db, void* part, void* stream, bool x3 = false) {
   if (!c2dsr_wgemm_supported(T, N, D) || ldy % 4 || ldx % 4) return (int)hipErrorInvalidValue;
   WSeg sg{};
   sg.nseg = 1;
@@ -697,14 +772,14 @@ static int wgemm_impl(int T, int N, int D, const void* dY, bool yb16, int ldy, c
   sg.T[0] = T;
   sg.vbeg[0] = 0;
   for (int k = 1; k <= WG_MAXSEG; ++k) sg.vbeg[k] = c2::ceil_div(T, 32) * 32;
-  return wgemm_segs(sg, N, D, yb16, beta, dW, db, part, stream);
+  return wgemm_segs(sg, N, D, yb16, beta, dW, db, part, stream, x3);
 }
 
 // dW[N, D] = beta·dW + Σ_k dY_kᵀ·X_k (and db = beta·db + Σ_k Σ_t dY_k[t]) over up to 4 row sets in ONE product
 // (the weight of a module that several encoder passes used): seg = HOST array of nseg records of five int64
 // (dY, ldy, X, ldx, T); dY fp32 (yb16 = 0) or bf16 (1); the same deterministic split partials as c2dsr_wgemm
-C2_API int c2dsr_wgemm_multi(const int64_t* seg, int nseg, int N, int D, int yb16, float beta, float* dW, float* db,
-                             void* part, void* stream) {
+static int wgemm_multi_impl(const int64_t* seg, int nseg, int N, int D, int yb16, float beta, float* dW, float* db,
+                            void* part, void* stream, bool x3) {
   if (nseg < 1 || nseg > WG_MAXSEG) return (int)hipErrorInvalidValue;
   WSeg sg{};
   sg.nseg = nseg;
@@ -720,7 +795,20 @@ C2_API int c2dsr_wgemm_multi(const int64_t* seg, int nseg, int N, int D, int yb1
     sg.vbeg[k + 1] = sg.vbeg[k] + c2::ceil_div(sg.T[k], 32) * 32;
   }
   for (int k = nseg + 1; k <= WG_MAXSEG; ++k) sg.vbeg[k] = sg.vbeg[nseg];
-  return wgemm_segs(sg, N, D, yb16 != 0, beta, dW, db, part, stream);
+  return wgemm_segs(sg, N, D, yb16 != 0, beta, dW, db, part, stream, x3);
+}
+C2_API int c2dsr_wgemm_multi(const int64_t* seg, int nseg, int N, int D, int yb16, float beta, float* dW, float* db,
+                             void* part, void* stream) {
+  return wgemm_multi_impl(seg, nseg, N, D, yb16, beta, dW, db, part, stream, false);
+}
+// fp32 mode: split-bf16 products (dY fp32)
+C2_API int c2dsr_wgemm_x3_multi(const int64_t* seg, int nseg, int N, int D, float beta, float* dW, float* db,
+                                void* part, void* stream) {
+  return wgemm_multi_impl(seg, nseg, N, D, 0, beta, dW, db, part, stream, true);
+}
+C2_API int c2dsr_wgemm_x3(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
+                          float* db, void* part, void* stream) {
+  return wgemm_impl(T, N, D, dY, false, ldy, X, ldx, beta, dW, db, part, stream, true);
 }
 
 C2_API int c2dsr_wgemm(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
@@ -745,6 +833,8 @@ struct MultiBf16 {
 };
 // every matrix of the list in one launch: block b converts 256 elements of the matrix whose block range holds
 // it (block-uniform lookup: scalar reads of the argument block)
+// SPLIT: y = hi ‖ lo (row r of y: [hi(row) | lo(row)], width 2·C, or transposed [C][2R])
+template <bool SPLIT = false>
 __global__ __launch_bounds__(256) void to_bf16_multi_kernel(MultiBf16 m) {
   const int b = blockIdx.x;
   int lo = 0, hi = m.count - 1;
@@ -756,17 +846,26 @@ __global__ __launch_bounds__(256) void to_bf16_multi_kernel(MultiBf16 m) {
   const int Cc = m.C[lo], R = m.R[lo];
   if (e >= (long)R * Cc) return;
   const int r = (int)(e / Cc), c = (int)(e % Cc);
-  const bf16 v = (bf16)m.x[lo][(long)r * m.ld[lo] + c];
-  if (m.tr[lo])
+  const float x = m.x[lo][(long)r * m.ld[lo] + c];
+  const bf16 v = (bf16)x;
+  if constexpr (SPLIT) {
+    const bf16 l = (bf16)(x - (float)v);
+    const int RR = m.tr[lo] ? Cc : R, CC = m.tr[lo] ? R : Cc;  // output rows / columns
+    const int orow = m.tr[lo] ? c : r, ocol = m.tr[lo] ? r : c;
+    (void)RR;
+    m.y[lo][(long)orow * 2 * CC + ocol] = v;
+    m.y[lo][(long)orow * 2 * CC + CC + ocol] = l;
+  } else if (m.tr[lo]) {
     m.y[lo][(long)c * R + r] = v;
-  else
+  } else {
     m.y[lo][e] = v;
+  }
 }
 }  // namespace
 
 // c2dsr_to_bf16 over a list of matrices in one launch: desc = HOST array of count (<= 64) records of six
 // int64 (x, y, R, Cc, ldx, trans) with the meaning of c2dsr_to_bf16's arguments
-C2_API int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream) {
+static int to_bf16_multi_impl(const int64_t* desc, int count, void* stream, bool split) {
   if (count < 0 || count > MULTI_MAX) return (int)hipErrorInvalidValue;
   if (count == 0) return 0;
   MultiBf16 m;
@@ -785,9 +884,19 @@ C2_API int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream) {
   }
   if (m.bstart[count] == 0) return 0;
   for (int k = count + 1; k <= MULTI_MAX; ++k) m.bstart[k] = m.bstart[count];
-  to_bf16_multi_kernel<<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
+  if (split)
+    to_bf16_multi_kernel<true><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
+  else
+    to_bf16_multi_kernel<false><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
   C2_CHECK_LAUNCH();
   return 0;
+}
+C2_API int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream) {
+  return to_bf16_multi_impl(desc, count, stream, false);
+}
+// the split-bf16 images (y = [R][2·Cc] hi ‖ lo, or [Cc][2·R] transposed) of a list of matrices in one launch
+C2_API int c2dsr_to_split_bf16_multi(const int64_t* desc, int count, void* stream) {
+  return to_bf16_multi_impl(desc, count, stream, true);
 }
 
 C2_API int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream) {

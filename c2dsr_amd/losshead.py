@@ -19,7 +19,7 @@ import torch
 from torch.autograd import Function
 
 from ._lib import lib, stream
-from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rgemm, rgemm_ok, weight_bf16, wgemm, wgemm_ok
+from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rg_kind, rgemm, weight_img, wg_kind, wgemm
 
 
 _NCU = None
@@ -45,6 +45,16 @@ def split_count(rows, tile, max_split=16, per_cu=1):
         if best_t is None or t < best_t - 1e-12:
             best, best_t = s, t
     return best
+
+
+def ce_kind(precision, d):
+    """Fused classifier-head kernels for this precision and width: 'b16' (ce.hip, bf16 operands), 'x3'
+    (ce3.hip, split-bf16 operands: the fp32 mode), or None (materialised fp32 logits + exact fp32 GEMMs)."""
+    if precision == BF16 and bool(lib.raw('c2dsr_ce_supported')(d)):
+        return 'b16'
+    if precision == FP32 and bool(lib.raw('c2dsr_ce3_supported')(d)):
+        return 'x3'
+    return None
 
 
 class LossMeta:
@@ -108,8 +118,9 @@ class LossHeadFn(Function):
         Ua = torch.empty(2 * B, d, **f32)
         Ub = torch.empty(2 * B, d, **f32)
         for X2, Wd, U in ((X2a, m.Da_w, Ua), (X2b, m.Db_w, Ub)):
-            if m.precision == BF16 and rgemm_ok(2 * B, d, d):  # bf16 mode: the row-streaming MFMA GEMM
-                rgemm(X2, weight_bf16(Wd.view(d, d)), U, M=2 * B, N=d, K=d)
+            kind = rg_kind(m.precision, 2 * B, d, d)
+            if kind:  # the row-streaming MFMA GEMM (bf16 or split-bf16 operands)
+                rgemm(X2, weight_img(Wd.view(d, d), kind), U, M=2 * B, N=d, K=d, x3=kind == 'x3')
             else:
                 gemm(X2, Wd, U, M=2 * B, N=d, K=d, transB=1, precision=FP32)
         S = torch.empty(4, B, **f32)
@@ -122,8 +133,10 @@ class LossHeadFn(Function):
         dS = torch.empty(4, B, **f32)
         lib('c2dsr_mi_loss', S, B, Bg, vec[8:], dS, s)
         # ---- classifier heads ----
-        fused = m.precision == BF16 and bool(lib.raw('c2dsr_ce_supported')(d))
-        ctx.fused = fused
+        kind = ce_kind(m.precision, d)
+        fused = kind is not None
+        x3 = kind == 'x3'  # fp32 mode: split-bf16 operands [rows][2d] = hi ‖ lo, three MFMAs per product
+        ctx.fused, ctx.x3 = fused, x3
         heads = []
         specs = ((hx, m.Wa, m.ba, m.gt_share_a, m.gt_a, m.n_a), (hy, m.Wb, m.bb, m.gt_share_b, m.gt_b, m.n_b))
         M2 = 2 * BR
@@ -168,16 +181,23 @@ class LossHeadFn(Function):
                 n_pad = -(-n // 128) * 128 + 64  # + a 64-value tail: tiles near n DMA 64 constants
                 Hc = torch.empty(Mv, d, **f32)
                 lib('c2dsr_gather_rows', Hcat, d, idx, Mv, d, Hc, s)
-                Hb = torch.empty(M_pad, d, device=dev, dtype=torch.bfloat16)  # whole 64-row H tiles (dW sweep)
-                if M_pad > Mv:
-                    Hb[Mv:].zero_()
-                n64 = -(-n // 64) * 64  # whole 64-row W tiles for the LDS-DMA (zero rows past n)
-                Wb = torch.empty(n64, d, device=dev, dtype=torch.bfloat16)
-                if n64 > n:
-                    Wb[n:].zero_()
-                if Mv:
-                    lib('c2dsr_f32_to_bf16', Hc, Hc.numel(), Hb, s)
-                lib('c2dsr_f32_to_bf16', W, W.numel(), Wb, s)
+                if x3:  # hi ‖ lo images, zero rows past the end (whole 32-row tiles)
+                    Hb = torch.empty(M_pad, 2 * d, device=dev, dtype=torch.bfloat16)
+                    lib('c2dsr_f32_split_bf16', Hc, Mv, d, M_pad, Hb, s)
+                    n32 = -(-n // 32) * 32
+                    Wb = torch.empty(n32, 2 * d, device=dev, dtype=torch.bfloat16)
+                    lib('c2dsr_f32_split_bf16', W, n, d, n32, Wb, s)
+                else:
+                    Hb = torch.empty(M_pad, d, device=dev, dtype=torch.bfloat16)  # whole 64-row H tiles (dW sweep)
+                    if M_pad > Mv:
+                        Hb[Mv:].zero_()
+                    n64 = -(-n // 64) * 64  # whole 64-row W tiles for the LDS-DMA (zero rows past n)
+                    Wb = torch.empty(n64, d, device=dev, dtype=torch.bfloat16)
+                    if n64 > n:
+                        Wb[n:].zero_()
+                    if Mv:
+                        lib('c2dsr_f32_to_bf16', Hc, Hc.numel(), Hb, s)
+                    lib('c2dsr_f32_to_bf16', W, W.numel(), Wb, s)
                 bias2 = torch.empty(n_pad, **f32)
                 lib('c2dsr_ce_bias2', bias, n, n_pad, bias2, s)
                 padlogit = torch.empty(M2, **f32)
@@ -188,15 +208,15 @@ class LossHeadFn(Function):
                 rows_c = torch.empty(max(Mv, 1), **f32)
                 lse2 = torch.empty(M_pad, **f32)
                 u = None
-                if Mv and any(ctx.needs_input_grad[:5]):
+                if Mv and (x3 or any(ctx.needs_input_grad[:5])):
                     # forward + the softmax part of the input gradient in one sweep (online lse, flash
                     # style): the backward runs no dH sweep
                     ns = split_count(Mv, 128)
                     pm = torch.empty(ns, Mv, **f32)
                     ps = torch.empty(ns, Mv, **f32)
                     Up = torch.empty(ns, Mv, d, **f32)
-                    lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tc, Hc, W, bias,
-                        lse_c, lse2, rows_c, s)
+                    lib('c2dsr_ce3_fused_fwd_u' if x3 else 'c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm,
+                        ps, Up, padc, tc, Hc, W, bias, lse_c, lse2, rows_c, s)
                     u = (Up, pm, ns)
                     m.run_after_first_ce()
                 elif Mv:
@@ -272,7 +292,7 @@ class LossHeadFn(Function):
                 rw = torch.empty(M_pad, **f32)
                 t32 = torch.empty(M_pad, device=dev, dtype=torch.int32)
                 dpad_c = torch.empty(max(Mv, 1), **f32)
-                crow = torch.empty(M_pad, **f32)
+                crow = torch.empty(M_pad + (64 if ctx.x3 else 0), **f32)  # x3: the dW sweep's row-constant DMA
                 dHc = torch.empty(max(Mv, 1), d, **f32)
                 if Mv:
                     # compact rows keep their order: the first Mv0 are the shared-sequence rows (coef[0])
@@ -290,7 +310,8 @@ class LossHeadFn(Function):
                     nr = split_count(n, 128)
                     dWp = torch.empty(nr, n, d, **f32)
                     dbp = torch.empty(nr, n, **f32)
-                    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)
+                    lib('c2dsr_ce3_fused_dw' if ctx.x3 else 'c2dsr_ce_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow,
+                        dWp, dbp, s)
                     if gW is not None:
                         lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
                     if gb is not None:
@@ -335,14 +356,15 @@ class LossHeadFn(Function):
             lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
             lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
             dX2 = torch.empty(2 * B, d, **f32)
-            b16 = m.precision == BF16 and rgemm_ok(2 * B, d, d) and wgemm_ok(2 * B, d, d)
+            kind = rg_kind(m.precision, 2 * B, d, d)
+            b16 = kind is not None and wg_kind(m.precision, 2 * B, d, d) is not None
             if b16:
-                rgemm(dU, weight_bf16(Wd.view(d, d), trans=True), dX2, M=2 * B, N=d, K=d)
+                rgemm(dU, weight_img(Wd.view(d, d), kind, trans=True), dX2, M=2 * B, N=d, K=d, x3=kind == 'x3')
             else:
                 gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
             gWd = _grad_target(Wd)
             if gWd is not None and b16:  # not deferred: the head range is reduced as this backward returns
-                wgemm(dU, X2, gWd.view(d, d), T=2 * B, N=d, D=d, defer=False)
+                wgemm(dU, X2, gWd.view(d, d), T=2 * B, N=d, D=d, defer=False, x3=kind == 'x3')
             elif gWd is not None:
                 gemm(dU, X2, gWd, M=d, N=d, K=2 * B, transA=1, beta=1.0, precision=FP32)
             gbd = _grad_target(bd)

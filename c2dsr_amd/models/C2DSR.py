@@ -108,7 +108,9 @@ class C2DSR(nn.Module):
 
     # ------------------------------------------------------------------ setup
     def set_precision(self, precision):
-        pr = ops.BF16 if precision in ('bf16', ops.BF16) else ops.FP32
+        pr = {'bf16': ops.BF16, 'fp32': ops.FP32, 'fp32_exact': ops.FP32_EXACT}.get(precision, precision)
+        if pr not in (ops.FP32, ops.BF16, ops.FP32_EXACT):
+            raise ValueError(f'precision {precision!r}: expected fp32, bf16 or fp32_exact')
         self.precision = pr
         for a in (self.attn_share, self.attn_a, self.attn_b):
             a.precision = pr

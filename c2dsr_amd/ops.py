@@ -14,7 +14,10 @@ from torch.autograd import Function
 from ._lib import HipLibError, lib, stream, require_device
 from .dp import notify_lookup, notify_rows, notify_table, row_cuts
 
-FP32, BF16 = 0, 1
+# precision modes: FP32 = the reference's precision (fp32 results; products on split-bf16 MFMAs where a kernel
+# exists — ce3.hip —, exact fp32-input MFMA elsewhere), BF16 = bf16 operands with fp32 accumulation,
+# FP32_EXACT = exact fp32-input MFMA for every product (materialised logits; the A/B check of FP32)
+FP32, BF16, FP32_EXACT = 0, 1, 2
 
 
 def _grad_target(param):
@@ -62,6 +65,23 @@ def rgemm_ok(M, N, K):
     return bool(lib.raw('c2dsr_rgemm_supported')(M, N, K))
 
 
+def rg_kind(precision, M, N, K):
+    """The row-streaming projection kernel (csrc/rgemm.hip) for this precision and shape: 'b16' (bf16
+    operands), 'x3' (split-bf16 operands: the fp32 mode) or None (the tiled GEMM, exact fp32 MFMA)."""
+    if precision == BF16 and rgemm_ok(M, N, K):
+        return 'b16'
+    if precision == FP32 and bool(lib.raw('c2dsr_rgemm_x3_supported')(M, N, K)):
+        return 'x3'
+    return None
+
+
+def wg_kind(precision, T, N, D):
+    """The weight-gradient kernel (c2dsr_wgemm / _x3) for this precision and shape, like rg_kind."""
+    if precision in (BF16, FP32) and wgemm_ok(T, N, D):
+        return 'b16' if precision == BF16 else 'x3'
+    return None
+
+
 def to_bf16(X, trans=False):
     """bf16 copy of a 2-D fp32 matrix (transposed if asked)."""
     R, Cc = X.shape
@@ -92,28 +112,31 @@ class _WeightImages:
             self._refresh_known()
 
     def _refresh_known(self):
-        recs, done = [], []
-        for key, (W, y) in self.known.items():
-            R, Cc = W.shape
-            recs += [W.data_ptr(), y.data_ptr(), R, Cc, W.stride(0), int(key[2])]
-            done.append((key, W, y))
+        for split, fn in ((False, 'c2dsr_to_bf16_multi'), (True, 'c2dsr_to_split_bf16_multi')):
+            recs, done = [], []
+            for key, (W, y) in self.known.items():
+                if key[3] != split:
+                    continue
+                R, Cc = W.shape
+                recs += [W.data_ptr(), y.data_ptr(), R, Cc, W.stride(0), int(key[2])]
+                done.append((key, W, y))
+            for i in range(0, len(done), 64):
+                chunk = done[i:i + 64]
+                desc = np.asarray(recs[6 * i:6 * (i + len(chunk))], dtype=np.int64)
+                lib(fn, desc.ctypes.data, len(chunk), stream())
+            for key, W, y in done:
+                self.cache[key] = ((self.epoch, W._version), y, W)
         self.known = {}
-        for i in range(0, len(done), 64):
-            chunk = done[i:i + 64]
-            desc = np.asarray(recs[6 * i:6 * (i + len(chunk))], dtype=np.int64)
-            lib('c2dsr_to_bf16_multi', desc.ctypes.data, len(chunk), stream())
-        for key, W, y in done:
-            self.cache[key] = ((self.epoch, W._version), y, W)
 
-    def get(self, W, trans):
-        key = (W.data_ptr(), tuple(W.shape), bool(trans))
+    def get(self, W, trans, split=False):
+        key = (W.data_ptr(), tuple(W.shape), bool(trans), bool(split))
         tag = (self.epoch, W._version)
         if key not in self.cache and key in self.known:
             self._refresh_known()
         hit = self.cache.get(key)
         if hit is not None and hit[0] == tag:
             return hit[1]
-        y = to_bf16(W, trans)
+        y = to_split_bf16(W, trans) if split else to_bf16(W, trans)
         self.cache[key] = (tag, y, W)
         return y
 
@@ -125,13 +148,29 @@ def weight_bf16(W, trans=False):
     return WEIGHTS.get(W.detach(), trans)
 
 
+def weight_img(W, kind, trans=False):
+    """The operand image of a projection weight for a rg_kind / wg_kind kernel: bf16 [R][C] ('b16') or the
+    split image [R][2C] = hi ‖ lo ('x3'); transposed ([C][…]) if asked."""
+    return WEIGHTS.get(W.detach(), trans, split=kind == 'x3')
+
+
+def to_split_bf16(X, trans=False):
+    """Split-bf16 image of a 2-D fp32 matrix: [R][2C] with row = hi ‖ lo ([C][2R] if transposed)."""
+    R, Cc = X.shape
+    y = torch.empty((Cc, 2 * R) if trans else (R, 2 * Cc), device=X.device, dtype=torch.bfloat16)
+    desc = np.asarray([X.data_ptr(), y.data_ptr(), R, Cc, X.stride(0), int(trans)], dtype=np.int64)
+    lib('c2dsr_to_split_bf16_multi', desc.ctypes.data, 1, stream())
+    return y
+
+
 AUX_ACC, AUX_MASK, AUX_ACC_MAP = 1, 2, 3
 
 
 def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, aux_mode=0, aux=None, aux_scale=0.0,
-          rowmap=None, auxmap=None):
+          rowmap=None, auxmap=None, x3=False):
     """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm); aux_mode
-    AUX_ACC: C += aux (aux may be C itself), AUX_MASK: C = aux > 0 ? C·aux_scale : 0 (c2dsr_rgemm_aux)."""
+    AUX_ACC: C += aux (aux may be C itself), AUX_MASK: C = aux > 0 ? C·aux_scale : 0 (c2dsr_rgemm_aux).
+    x3: Bb is the split image [N, 2K] and the products run on split-bf16 operands (c2dsr_rgemm_x3)."""
     k0 = k1 = 0
     p = 0.0
     row_base = 0
@@ -141,7 +180,10 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
         (k0, k1), p, row_base = relu_drop[:3]
         if len(relu_drop) > 3:
             rowmap = relu_drop[3]
-    if A.dtype == torch.bfloat16:  # the attention backward's bf16 dqkv (in_proj dX; c2dsr_rgemm_aux_b16a)
+    if x3:
+        lib('c2dsr_rgemm_x3', M, N, K, A, K, Bb, 2 * K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
+            int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
+    elif A.dtype == torch.bfloat16:  # the attention backward's bf16 dqkv (in_proj dX; c2dsr_rgemm_aux_b16a)
         if epi or aux_mode == AUX_MASK:
             raise HipLibError('rgemm: bf16 A supports no epilogue / mask mode')
         lib('c2dsr_rgemm_aux_b16a', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, int(aux_mode), aux,
@@ -171,8 +213,8 @@ class WGradBatch:
         self.groups = {}
         self.lookups_left = lookups
 
-    def add(self, dY, X, dW, db, T, N, D):
-        key = (dW.data_ptr(), N, D, dY.dtype, None if db is None else db.data_ptr())
+    def add(self, dY, X, dW, db, T, N, D, x3=False):
+        key = (dW.data_ptr(), N, D, dY.dtype, None if db is None else db.data_ptr(), x3)
         g = self.groups.setdefault(key, [dW, db, []])
         g[2].append((dY, X, T))
 
@@ -183,29 +225,35 @@ class WGradBatch:
 
     def flush(self):
         s = stream()
-        for (_, N, D, dt, _), (dW, db, segs) in self.groups.items():
+        for (_, N, D, dt, _, x3), (dW, db, segs) in self.groups.items():
             ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
             for i in range(0, len(segs), 4):
                 chunk = segs[i:i + 4]
                 desc = np.asarray([v for dY, X, T in chunk for v in (dY.data_ptr(), N, X.data_ptr(), D, T)],
                                   dtype=np.int64)
-                lib('c2dsr_wgemm_multi', desc.ctypes.data, len(chunk), N, D, int(dt == torch.bfloat16), 1.0, dW,
-                    db, ws, s)
+                if x3:
+                    lib('c2dsr_wgemm_x3_multi', desc.ctypes.data, len(chunk), N, D, 1.0, dW, db, ws, s)
+                else:
+                    lib('c2dsr_wgemm_multi', desc.ctypes.data, len(chunk), N, D, int(dt == torch.bfloat16), 1.0, dW,
+                        db, ws, s)
         self.groups = {}
 
 
-WBATCH = None  # the active WGradBatch (Trainer.train_batch, bf16 mode), else None
+WBATCH = None  # the active WGradBatch (Trainer.train_batch, bf16 / fp32 mode), else None
 
 
-def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None, defer=True):
+def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None, defer=True, x3=False):
     """dW[N, D] = beta·dW + dYᵀ·X over T rows and (db given) db[N] = beta·db + Σ_t dY[t]
-    (c2dsr_wgemm, deterministic split-t partials).  With a WGradBatch active (and beta = 1) the product is
-    deferred into it."""
+    (c2dsr_wgemm, deterministic split-t partials; x3: split-bf16 products, c2dsr_wgemm_x3).  With a
+    WGradBatch active (and beta = 1) the product is deferred into it."""
     if defer and WBATCH is not None and beta == 1.0 and dY.is_contiguous() and X.is_contiguous():
-        WBATCH.add(dY, X, dW, db, T, N, D)
+        WBATCH.add(dY, X, dW, db, T, N, D, x3)
         return
     ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
-    name = 'c2dsr_wgemm_b16y' if dY.dtype == torch.bfloat16 else 'c2dsr_wgemm'
+    if x3:
+        name = 'c2dsr_wgemm_x3'
+    else:
+        name = 'c2dsr_wgemm_b16y' if dY.dtype == torch.bfloat16 else 'c2dsr_wgemm'
     lib(name, T, N, D, dY, N, X, D, float(beta), dW, db, ws, stream())
 
 
@@ -243,8 +291,9 @@ class LinearFn(Function):
         N, K = W.shape
         M = x.numel() // K
         y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
-        if precision == BF16 and rgemm_ok(M, N, K):
-            rgemm(x, weight_bf16(W), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
+        kind = rg_kind(precision, M, N, K)
+        if kind:
+            rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop, x3=kind == 'x3')
         else:
             gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)
         ctx.save_for_backward(x, W, y if relu_drop is not None else None)
@@ -274,7 +323,10 @@ def linear_backward(ctx, x, W, y, dy, need_dx):
         dy = d2
     dx = None
     if need_dx:
-        fused = ctx.precision == BF16 and rgemm_ok(M, K, N)
+        kind = rg_kind(ctx.precision, M, K, N)
+        fused = kind is not None
+        x3 = kind == 'x3'
+        Wt = weight_img(W, kind, trans=True) if fused else None
         park = ctx.res.grad if ctx.res is not None else None
         if ctx.res is not None:
             ctx.res.grad = None
@@ -285,19 +337,17 @@ def linear_backward(ctx, x, W, y, dy, need_dx):
             park, sub = full, False
         if sub:  # dx = dy·W + the parked rows, read through the row map
             dx = torch.empty_like(x)
-            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park,
-                  auxmap=ctx.res.inv)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park, auxmap=ctx.res.inv, x3=x3)
         elif fused and park is not None:  # dx = parked LN gradient + dy·W, in place
             dx = park
-            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx, x3=x3)
         elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here
             dx = torch.empty_like(x)
-            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x,
-                  aux_scale=1.0 / (1.0 - ctx.ff.p))
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x, aux_scale=1.0 / (1.0 - ctx.ff.p), x3=x3)
             ctx.ff.premasked = True
         elif fused:
             dx = torch.empty_like(x)
-            rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, x3=x3)
         elif park is not None:
             dx = park
             gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0, precision=ctx.precision)
@@ -306,8 +356,9 @@ def linear_backward(ctx, x, W, y, dy, need_dx):
             gemm(dy, W, dx, M=M, N=K, K=N, precision=ctx.precision)
     gW = _grad_target(W)
     gb = _grad_target(ctx.b)
-    if gW is not None and ctx.precision == BF16 and wgemm_ok(M, N, K):
-        wgemm(dy, x, gW, T=M, N=N, D=K, db=gb)  # bias gradient from the same dY chunks
+    wk = wg_kind(ctx.precision, M, N, K) if dy.dtype == torch.float32 or ctx.precision == BF16 else None
+    if gW is not None and wk:
+        wgemm(dy, x, gW, T=M, N=N, D=K, db=gb, x3=wk == 'x3')  # bias gradient from the same dY chunks
         gb = None
     elif gW is not None:
         gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=ctx.precision)
@@ -822,8 +873,9 @@ class QKVAttnFn(Function):
         N, K = W.shape
         M = x.numel() // K
         qkv = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
-        if precision == BF16 and rgemm_ok(M, N, K):
-            rgemm(x, weight_bf16(W), qkv, M=M, N=N, K=K, bias=b)
+        kind = rg_kind(precision, M, N, K)
+        if kind:
+            rgemm(x, weight_img(W, kind), qkv, M=M, N=N, K=K, bias=b, x3=kind == 'x3')
         else:
             gemm(x, W, qkv, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
         B, L, d3 = qkv.shape
@@ -872,8 +924,9 @@ def _proj(x, W, b, y, precision):
     M = x.shape[0]
     if M == 0:
         return y
-    if precision == BF16 and rgemm_ok(M, N, K):
-        rgemm(x, weight_bf16(W), y, M=M, N=N, K=K, bias=b)
+    kind = rg_kind(precision, M, N, K)
+    if kind:
+        rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, x3=kind == 'x3')
     else:
         gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
     return y
@@ -886,13 +939,15 @@ def _proj_backward(x, W, dy, dx, acc, gW, gb, precision):
     M = x.shape[0]
     if M == 0:
         return
-    if precision == BF16 and rgemm_ok(M, K, N):
-        rgemm(dy, weight_bf16(W, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC if acc else 0,
-              aux=dx if acc else None)
+    kind = rg_kind(precision, M, K, N)
+    if kind:
+        rgemm(dy, weight_img(W, kind, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC if acc else 0,
+              aux=dx if acc else None, x3=kind == 'x3')
     else:
         gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0 if acc else 0.0, precision=precision)
-    if gW is not None and precision == BF16 and wgemm_ok(M, N, K):
-        wgemm(dy, x, gW, T=M, N=N, D=K, db=gb)
+    wk = wg_kind(precision, M, N, K)
+    if gW is not None and wk:
+        wgemm(dy, x, gW, T=M, N=N, D=K, db=gb, x3=wk == 'x3')
     else:
         if gW is not None:
             gemm(dy, x, gW, M=N, N=K, K=M, transA=1, lda=N, ldb=K, beta=1.0, precision=precision)

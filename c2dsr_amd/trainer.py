@@ -24,7 +24,7 @@ from . import ops
 from ._lib import lib, stream
 from .dp import CommPlan, DPComm, Zero1
 from .graph import make_graph
-from .losshead import LossHeadFn, LossMeta
+from .losshead import LossHeadFn, LossMeta, ce_kind
 from .metrics import RankMetrics
 from .models.C2DSR import C2DSR
 from .optim import FlatAdamW
@@ -182,7 +182,7 @@ class Trainer(object):
                 pad_sets = (pidx, pinv, poff)
                 counts.append(pcnt)
         ce = None
-        if m.precision == ops.BF16 and bool(lib.raw('c2dsr_ce_supported')(self.d_latent)):
+        if ce_kind(m.precision, self.d_latent) is not None:
             M2 = 2 * B * R
             ce = []
             for ts, tx, n_items in ((gt_share_a, gt_a, self.n_item_a), (gt_share_b, gt_b, self.n_item_b)):
@@ -292,7 +292,8 @@ class Trainer(object):
     def _backward(self, loss):
         """loss.backward() with the projections' weight-gradient products grouped per weight (ops.WGradBatch,
         bf16 mode: flushed by the last embedding backward, or here)."""
-        batch = ops.WGradBatch(5) if self.batch_wgrad and self.model.precision == ops.BF16 else None
+        batch = (ops.WGradBatch(5) if self.batch_wgrad and self.model.precision in (ops.BF16, ops.FP32)
+                 else None)
         ops.WBATCH = batch
         try:
             loss.backward()

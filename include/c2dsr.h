@@ -266,6 +266,25 @@ int c2dsr_ce_onehot_dw_planned(const void* plan, int M, int n, const float* H, i
                                float* gb, void* workspace, size_t ws_bytes, void* stream);
 int c2dsr_ce_onehot_dw(const int64_t* tgt, int M, int n, const float* H, int D, const float* rw, float* gW, float* gb,
                        void* workspace, size_t ws_bytes, void* stream);
+/* per row: lse over the splits' (max, sum) partials and the pad column, lse2 = lse·log2e, the fp32 target
+ * logit and loss_row (the row step of c2dsr_ce_fused_fwd / _fwd_u / c2dsr_ce3_fused_fwd_u) */
+int c2dsr_ce_rows(const float* part_m, const float* part_s, int n_split, int M, const float* padlogit,
+                  const int64_t* tgt, int n, const float* H, const float* W, const float* bias, int D, float* lse,
+                  float* lse2, float* loss_row, void* stream);
+
+/* K5 at the reference's precision (fp32 training mode; csrc/ce3.hip).  Same contract as
+ * c2dsr_ce_fused_fwd_u / c2dsr_ce_fused_dw (trainer.py:131-154), but the operands are split-bf16 images
+ * [rows][2·D] = hi ‖ lo (x = hi + lo to 2^-17 relative; c2dsr_f32_split_bf16) and every product runs as
+ * three bf16 MFMAs (hi·hi + lo·hi + hi·lo) with fp32 accumulation.  Hx holds ⌈M/32⌉·32 rows and Wx
+ * ⌈n/32⌉·32 rows (zero rows past the end); bias2 as for ce.hip; crow holds ⌈M/64⌉·64 + 64 values. */
+int c2dsr_ce3_supported(int D);
+int c2dsr_f32_split_bf16(const float* x, long rows, int D, long rows_out, void* out, void* stream);
+int c2dsr_ce3_fused_fwd_u(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_split,
+                          float* part_m, float* part_s, float* Up, const float* padlogit, const int64_t* tgt,
+                          const float* H, const float* W, const float* bias, float* lse, float* lse2, float* loss_row,
+                          void* stream);
+int c2dsr_ce3_fused_dw(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_rsplit,
+                       const float* crow, float* dWp, float* dbp, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
 int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */
@@ -307,6 +326,21 @@ int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const void* B,
 int c2dsr_rgemm_aux_b16a(int M, int N, int K, const void* A, int lda, const void* B, int ldb, float* C, int ldc,
                          float alpha, float beta, const float* bias, int aux_mode, const float* aux, const int* auxmap,
                          void* stream);
+/* fp32 mode (split-bf16 products, three bf16 MFMAs per k-step, fp32 accumulation — see csrc/ce3.hip): the
+ * same contract as c2dsr_rgemm_aux with B the split image [N][2K] = hi ‖ lo (ldb >= 2K), K = 256 or 512 */
+int c2dsr_rgemm_x3_supported(int M, int N, int K);
+int c2dsr_rgemm_x3(int M, int N, int K, const float* A, int lda, const void* B, int ldb, float* C, int ldc,
+                   float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                   int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
+                   float aux_scale, void* stream);
+/* ... and the weight-gradient products (c2dsr_wgemm / _multi contract, dY fp32) */
+int c2dsr_wgemm_x3(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
+                   float* db, void* part, void* stream);
+int c2dsr_wgemm_x3_multi(const int64_t* seg, int nseg, int N, int D, float beta, float* dW, float* db, void* part,
+                         void* stream);
+/* split-bf16 images of a list of matrices (c2dsr_to_bf16_multi's descriptors): y = [R][2·Cc] (row = hi ‖ lo),
+ * or [Cc][2·R] when trans */
+int c2dsr_to_split_bf16_multi(const int64_t* desc, int count, void* stream);
 /* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
  * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
  * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS

@@ -1,0 +1,246 @@
+"""K5 at reference precision (csrc/ce3.hip): the fused classifier head + cross-entropy on split-bf16
+operands (hi + lo, three bf16 MFMAs per product, fp32 accumulation) against a float64 computation of the
+same op on the SAME fp32 operands (no rounding of the inputs): the fp32 training mode's tolerance.
+
+Reference semantics: trainer.py:131-154 (logits = h·Wᵀ + b ‖ pad column, cross_entropy with
+ignore_index = n) — forward lse / per-row loss, dH = rw·(softmax − onehot)·W, dW = Σ_r rw·(softmax −
+onehot)ᵀ·H, db likewise."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _run(H, W, b, pl, t, coef, lam, ns, nr, BR):
+    """The fp32-mode head exactly as losshead.py drives it (x3 kernels)."""
+    from c2dsr_amd._lib import lib, stream
+    s = stream()
+    d = lambda x: x.to(DEV)  # noqa: E731
+    M, D = H.shape
+    n = W.shape[0]
+    M_pad = max(64, -(-M // 64) * 64)
+    n32 = -(-n // 32) * 32
+    Hx = torch.empty(M_pad, 2 * D, dtype=torch.bfloat16, device=DEV)
+    Wx = torch.empty(n32, 2 * D, dtype=torch.bfloat16, device=DEV)
+    lib('c2dsr_f32_split_bf16', d(H), M, D, M_pad, Hx, s)
+    lib('c2dsr_f32_split_bf16', d(W), n, D, n32, Wx, s)
+    n_pad = -(-n // 128) * 128 + 64
+    bias2 = torch.empty(n_pad, device=DEV)
+    lib('c2dsr_ce_bias2', d(b), n, n_pad, bias2, s)
+    pm, ps = torch.empty(ns, M, device=DEV), torch.empty(ns, M, device=DEV)
+    Up = torch.empty(ns, M, D, device=DEV)
+    lse, rows = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    lse2 = torch.empty(M_pad, device=DEV)
+    lib('c2dsr_ce3_fused_fwd_u', Hx, Wx, bias2, M, n, D, ns, pm, ps, Up, d(pl), d(t), d(H), d(W), d(b), lse, lse2,
+        rows, s)
+    rw, dpad = torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)
+    t32 = torch.empty(M_pad, device=DEV, dtype=torch.int32)
+    crow = torch.empty(M_pad + 64, device=DEV)
+    gs = torch.tensor([1.0])
+    lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, t32, lse2, crow, dpad, s)
+    dH = torch.empty(M, D, device=DEV)
+    lib('c2dsr_ce_dh_from_u', Up, pm, ns, M, D, lse2, t32, rw, d(W), n, dH, s)
+    gW = torch.zeros(n, D, device=DEV)
+    gb = torch.zeros(n, device=DEV)
+    dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
+    lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, M, n, D, nr, crow, dWp, dbp, s)
+    lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
+    lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
+    wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M, n, D))
+    ws = torch.empty(wsb, device=DEV, dtype=torch.uint8)
+    lib('c2dsr_ce_onehot_dw', d(t), M, n, d(H), D, rw, gW, gb, ws, wsb, s)
+    torch.cuda.synchronize()
+    return lse, rows, dH, gW, gb, dpad, Up
+
+
+def _ref(H, W, b, pl, t, coef, lam, BR):
+    M = H.shape[0]
+    n = W.shape[0]
+    lg = torch.cat([H.double() @ W.double().T + b.double(), pl.double()[:, None]], 1)
+    lse = torch.logsumexp(lg, 1)
+    valid = t != n
+    rows = torch.where(valid, lse - lg.gather(1, t[:, None])[:, 0], torch.zeros(M, dtype=torch.float64))
+    w_r = torch.where(valid, lam * coef[(torch.arange(M) >= BR).long()].double(), torch.zeros(M, dtype=torch.float64))
+    P = torch.softmax(lg, 1)
+    oh = torch.zeros_like(P)
+    oh[torch.arange(M), t] = 1.0
+    dl = (P - oh) * w_r[:, None]
+    return lse, rows, dl[:, :n] @ W.double(), dl[:, :n].T @ H.double(), dl[:, :n].sum(0), dl[:, n]
+
+
+# fp32-mode tolerances: split-bf16 products carry ≈3·2^-17 relative error per term (see ce3.hip), so a
+# logit over d = 256 terms is off by ~1e-5 of Σ|h·w| (fp32: ~1e-6); north_star's bound is 1e-4 relative.
+# lse within 1e-5 relative, per-row losses and every gradient within 5e-5 of their max-abs.
+TOL_LSE, TOL = 1e-5, 5e-5
+
+
+@pytest.mark.parametrize('M,n,D,ns,nr', [(300, 700, 256, 3, 2), (1000, 2100, 128, 4, 3), (64, 65, 256, 1, 1),
+                                         (777, 4099, 256, 7, 5), (33, 31, 256, 2, 3)])
+def test_ce3_matches_float64(M, n, D, ns, nr):
+    g = torch.Generator().manual_seed(M + n + D)
+    H = torch.randn(M, D, generator=g) * 0.5
+    W = torch.randn(n, D, generator=g) * 0.5
+    b = torch.randn(n, generator=g) * 0.1
+    pl = torch.randn(M, generator=g)
+    t = torch.randint(0, n + 1, (M,), generator=g)
+    t[:5] = n  # ignored rows
+    coef, lam, BR = torch.tensor([0.37, 1.9]), 0.7, M // 2
+    lse, rows, dH, gW, gb, dpad, _ = _run(H, W, b, pl, t, coef, lam, ns, nr, BR)
+    lse_r, rows_r, dH_r, gW_r, gb_r, dpad_r = _ref(H, W, b, pl, t, coef, lam, BR)
+    err = dict(lse=rel(lse, lse_r), rows=rel(rows, rows_r), dpad=rel(dpad, dpad_r), dH=rel(dH, dH_r),
+               gW=rel(gW, gW_r), gb=rel(gb, gb_r))
+    print('ce3 errors', {k: f'{v:.2e}' for k, v in err.items()})
+    assert err.pop('lse') < TOL_LSE
+    assert all(v < TOL for v in err.values()), err
+
+
+@pytest.mark.parametrize('M,n,D,ns', [(200, 1500, 256, 2), (333, 3000, 128, 5)])
+def test_ce3_online_rescale(M, n, D, ns):
+    """Row max rising and falling across column tiles (bias ramp of 60 nats): the lazy rescale fires at
+    different tiles for different rows of one wave.  The logits reach |h·w| ≈ 20 here, and the softmax's
+    relative error is the logit's ABSOLUTE error (≈ 4e-6·|h·w| for split-bf16 products), so the weight
+    gradient is held to north_star's 1e-4 instead of TOL."""
+    g = torch.Generator().manual_seed(M * 7 + n)
+    H = torch.randn(M, D, generator=g) * 0.3
+    H[1::2, :8] = -H[1::2, :8].abs() - 1.0
+    H[0::2, :8] = H[0::2, :8].abs() + 1.0
+    W = torch.randn(n, D, generator=g) * 0.2
+    W[:, :8] = torch.linspace(-2.0, 2.0, n)[:, None]
+    b = torch.linspace(0.0, 60.0, n) * (torch.rand(n, generator=g) > 0.5)
+    pl = torch.randn(M, generator=g)
+    t = torch.randint(0, n, (M,), generator=g)
+    coef, lam, BR = torch.tensor([0.5, 1.5]), 0.7, M // 2
+    lse, rows, dH, gW, gb, _, Up = _run(H, W, b, pl, t, coef, lam, ns, 2, BR)
+    lse_r, rows_r, dH_r, gW_r, gb_r, _ = _ref(H, W, b, pl, t, coef, lam, BR)
+    assert torch.isfinite(Up).all()
+    err = dict(lse=rel(lse, lse_r), rows=rel(rows, rows_r), dH=rel(dH, dH_r), gW=rel(gW, gW_r), gb=rel(gb, gb_r))
+    print('ce3 rescale errors', {k: f'{v:.2e}' for k, v in err.items()})
+    assert err.pop('lse') < TOL_LSE
+    assert all(v < 1e-4 for v in err.values()), err
+
+
+def test_split_bf16_is_exact_to_2e17():
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(70, 256, generator=g) * torch.logspace(-3, 3, 256)
+    out = torch.full((96, 512), 7.0, dtype=torch.bfloat16, device=DEV)
+    lib('c2dsr_f32_split_bf16', x.to(DEV), 70, 256, 96, out, stream())
+    torch.cuda.synchronize()
+    o = out.float().cpu()
+    hi, lo = o[:70, :256], o[:70, 256:]
+    assert torch.equal(hi, x.to(torch.bfloat16).float())
+    assert float(((hi.double() + lo.double() - x.double()).abs() / x.double().abs()).max()) <= 2 ** -17
+    assert torch.equal(o[70:], torch.zeros(26, 512))
+
+
+# ---------------------------------------------------------------- fp32-mode projections (csrc/rgemm.hip, X3)
+@pytest.mark.parametrize('M,N,K', [(1000, 768, 256), (129, 256, 256), (77, 320, 512), (32 * 37 + 5, 256, 512)])
+def test_rgemm_x3_matches_float64(M, N, K):
+    """Split-bf16 row-streaming GEMM on unrounded fp32 operands vs float64: plain, bias + alpha, and every aux
+    epilogue (in-place accumulate, drop(relu)-backward mask, mapped accumulate) at the fp32-mode tolerance."""
+    from c2dsr_amd.ops import AUX_ACC, AUX_ACC_MAP, AUX_MASK, rgemm, to_split_bf16
+    g = torch.Generator().manual_seed(M + N + K)
+    A, W, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+    Wx = to_split_bf16(W.to(DEV))
+    prod = A.double() @ W.double().T
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), Wx, C, M=M, N=N, K=K, alpha=0.5, bias=b.to(DEV), x3=True)
+    assert rel(C, 0.5 * prod + b.double()) < TOL
+    Wt = torch.randn(K, N, generator=g)  # transposed image (the dx = dy·W product)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), to_split_bf16(Wt.to(DEV), trans=True), C, M=M, N=N, K=K, x3=True)
+    assert rel(C, A.double() @ Wt.double()) < TOL
+    C0 = torch.randn(M, N, generator=g)
+    C = C0.to(DEV)
+    rgemm(A.to(DEV), Wx, C, M=M, N=N, K=K, aux_mode=AUX_ACC, aux=C, x3=True)
+    assert rel(C, prod + C0.double()) < TOL
+    src = torch.randn(M, N, generator=g)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), Wx, C, M=M, N=N, K=K, aux_mode=AUX_MASK, aux=src.to(DEV), aux_scale=1.25, x3=True)
+    assert rel(C, torch.where(src.double() > 0, prod * 1.25, torch.zeros_like(prod))) < TOL
+    keep = torch.nonzero(torch.rand(M, generator=g) < 0.6).reshape(-1)
+    inv = torch.full((M,), -1, dtype=torch.int32)
+    inv[keep] = torch.arange(keep.numel(), dtype=torch.int32)
+    park = torch.randn(keep.numel(), N, generator=g)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), Wx, C, M=M, N=N, K=K, aux_mode=AUX_ACC_MAP, aux=park.to(DEV), auxmap=inv.to(DEV), x3=True)
+    full = torch.zeros(M, N, dtype=torch.float64)
+    full[keep] = park.double()
+    assert rel(C, prod + full) < TOL
+
+
+def test_rgemm_x3_relu_dropout_epilogue():
+    from c2dsr_amd.ops import rgemm, to_split_bf16
+    from oracle.c2dsr_oracle import keep_mask
+    import numpy as np
+    M, N, K, p = 333, 256, 256, 0.3
+    g = torch.Generator().manual_seed(3)
+    A, W, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+    keys = (123456, 987654)
+    C = torch.empty(M, N, device=DEV)
+    rgemm(A.to(DEV), to_split_bf16(W.to(DEV)), C, M=M, N=N, K=K, bias=b.to(DEV), relu_drop=(keys, p, 1000), x3=True)
+    idx = (np.arange(M)[:, None] + 1000) * N + np.arange(N)[None, :]
+    mk = torch.from_numpy(keep_mask(idx, keys, p).astype(np.float32)).double() / (1 - p)
+    ref = torch.relu(A.double() @ W.double().T + b.double()) * mk
+    assert rel(C, ref) < TOL
+
+
+@pytest.mark.parametrize('T,N', [(1000, 256), (4097, 768), (31, 128)])
+def test_wgemm_x3_matches_float64(T, N):
+    """Split-bf16 weight gradient dW = beta·dW + dYᵀ·X (+ exact fp32 bias sums) vs float64; deterministic;
+    the multi-segment form (ops.WGradBatch) on ragged segments."""
+    import numpy as np
+    from c2dsr_amd._lib import lib, stream
+    from c2dsr_amd.ops import wgemm
+    D = 256
+    g = torch.Generator().manual_seed(T + N)
+    dY, X, W0 = torch.randn(T, N, generator=g), torch.randn(T, D, generator=g), torch.randn(N, D, generator=g)
+    dW = W0.to(DEV)
+    db = torch.full((N,), 3.0, device=DEV)
+    wgemm(dY.to(DEV), X.to(DEV), dW, T=T, N=N, D=D, beta=1.0, db=db, x3=True)
+    assert rel(dW, W0.double() + dY.double().T @ X.double()) < TOL
+    assert rel(db, 3.0 + dY.double().sum(0)) < 1e-6
+    dW2 = W0.to(DEV)
+    wgemm(dY.to(DEV), X.to(DEV), dW2, T=T, N=N, D=D, beta=1.0, db=torch.full((N,), 3.0, device=DEV), x3=True)
+    assert torch.equal(dW, dW2)
+    Ts = (T, 33)
+    dYs = [dY, torch.randn(33, N, generator=g)]
+    Xs = [X, torch.randn(33, D, generator=g)]
+    dYd, Xd = [y.to(DEV) for y in dYs], [x.to(DEV) for x in Xs]
+    ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=DEV)
+    desc = np.asarray([v for y, x, t in zip(dYd, Xd, Ts) for v in (y.data_ptr(), N, x.data_ptr(), D, t)],
+                      dtype=np.int64)
+    dWm = torch.full((N, D), 0.5, device=DEV)
+    lib('c2dsr_wgemm_x3_multi', desc.ctypes.data, 2, N, D, 1.0, dWm, None, ws, stream())
+    torch.cuda.synchronize()
+    assert rel(dWm, 0.5 + sum(y.double().T @ x.double() for y, x in zip(dYs, Xs))) < TOL
+
+
+def test_split_weight_images_multi():
+    """c2dsr_to_split_bf16_multi (the optimizer-step refresh of the fp32 mode's weight images): both
+    orientations equal the single conversions."""
+    import numpy as np
+    from c2dsr_amd._lib import lib, stream
+    from c2dsr_amd.ops import to_split_bf16
+    g = torch.Generator().manual_seed(9)
+    Ws = [torch.randn(768, 256, generator=g).to(DEV), torch.randn(256, 256, generator=g).to(DEV)]
+    outs, recs = [], []
+    for W, tr in ((Ws[0], 0), (Ws[0], 1), (Ws[1], 1)):
+        R, C = W.shape
+        y = torch.empty((C, 2 * R) if tr else (R, 2 * C), device=DEV, dtype=torch.bfloat16)
+        outs.append((y, to_split_bf16(W, bool(tr))))
+        recs += [W.data_ptr(), y.data_ptr(), R, C, W.stride(0), tr]
+    desc = np.asarray(recs, dtype=np.int64)
+    lib('c2dsr_to_split_bf16_multi', desc.ctypes.data, 3, stream())
+    torch.cuda.synchronize()
+    for y, ref in outs:
+        assert torch.equal(y, ref)
+    hi, lo = outs[1][1][:, :768].float(), outs[1][1][:, 768:].float()
+    assert float((hi + lo - Ws[0].T).abs().max() / Ws[0].abs().max()) < 2 ** -16
