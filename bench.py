@@ -5,8 +5,11 @@ A step = convolve_graph() + train_batch() (HIP forward, fused loss head, backwar
 RCCL gradient all-reduce when N>1, fused AdamW-amsgrad) over one batch of synthetic
 two-domain sequences already resident in HBM.  Workload (N=1 line): Movie-Book item
 counts (36,845 + 63,937; BASELINE configs[2]), d=256, L=50, B=2048 per GPU, R=10,
-dropout 0.2, bf16 MFMA compute / fp32 storage.  Weak scaling: every rank trains its
-own batch of B, `value` = total sequences/s over all ranks.
+dropout 0.2, at the reference's precision (fp32 results: every product on split-bf16
+MFMAs with fp32 accumulation, parity 1e-4 vs the fp32 oracle).  Extra lines: the bf16
+performance mode on the same workload, BASELINE configs[1] (Food-Kitchen sizes, bf16)
+and configs[4] (C5 kernel roofline run).  Weak scaling: every rank trains its own batch
+of B, `value` = total sequences/s over all ranks.
 
 Launch:  python bench.py [--gpus N --steps K --warmup W]
          N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -37,7 +40,10 @@ CONFIGS = {
     'tiny': dict(n_a=2000, n_b=3000, d=64, L=20, B=256, label='tiny smoke workload'),
 }
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
-PEAK_FP32_TFLOPS = 157.3
+PEAK_FP32_TFLOPS = 157.3    # fp32-input MFMA (v_mfma_f32_32x32x2_f32, the exact-fp32 path)
+# fp32 mode: each fp32-accurate product runs as three bf16 MFMAs (hi·hi + lo·hi + hi·lo, csrc/ce3.hip), so
+# the matrix cores deliver at most a third of the bf16 peak in credited fp32 flops
+PEAK_X3_TFLOPS = PEAK_BF16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
 
 
@@ -211,19 +217,19 @@ def k5_traffic(precision):
     summarised by tools/pmc_traffic.py into profiles/k5_traffic.json.  PMC counters cannot be read
     from inside this process, so the committed measurement of the same code is reported (null if
     absent or for another precision)."""
-    path = os.path.join(ROOT, 'profiles', 'k5_traffic.json')
-    if precision != 'bf16' or not os.path.exists(path):
+    path = os.path.join(ROOT, 'profiles', {'bf16': 'k5_traffic.json', 'fp32': 'k5_traffic_fp32.json'}.get(precision, '-'))
+    if not os.path.exists(path):
         return None, None, None
     with open(path) as f:
         t = json.load(f)
     return t.get('bytes_per_launch_triple'), t.get('source'), t.get('mfma_busy')
 
 
-def hbm_traffic():
+def hbm_traffic(precision):
     """K1 + K2 HBM bytes per step (all their launches) from the same PMC passes (profiles/hbm_traffic.json,
     tools/pmc_traffic.py): measured DRAM traffic below the algorithmic bytes means the MALL / L2 served
     part of the gathers (re-read table rows)."""
-    path = os.path.join(ROOT, 'profiles', 'hbm_traffic.json')
+    path = os.path.join(ROOT, 'profiles', 'hbm_traffic.json' if precision == 'bf16' else 'hbm_traffic_fp32.json')
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -231,15 +237,21 @@ def hbm_traffic():
     return t.get('bytes_per_step'), t.get('source')
 
 
-def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
+def cpu_threads():
+    """The host threads the CPU baseline uses: the box's CPU share for one GPU (OMP_NUM_THREADS, 16 on the
+    GPU box; os.cpu_count() there reports the whole machine, whose other cores belong to other jobs)."""
+    share = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or 16
+    return max(1, min(os.cpu_count() or 1, share))
+
+
+def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0, min_steps=1):
     """The oracle (CPU fp32 restatement, oracle/c2dsr_oracle.py) on a bounded sample of the same
     workload at the configuration's own batch: same item tables, d, L,
-    B; one untimed warm-up step, then timed steps until ``budget_s`` is spent (at least one)."""
+    B; one untimed warm-up step, then timed steps until ``budget_s`` is spent and at least ``min_steps``."""
     sys.path.insert(0, ROOT)
     from oracle import c2dsr_oracle as O
     from c2dsr_amd.models.C2DSR import C2DSR
-    threads = os.cpu_count() or 1
-    threads = min(threads, 16)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     args = make_args(cfg, torch.device('cpu'), 'fp32')
     torch.manual_seed(0)
@@ -264,16 +276,17 @@ def cpu_baseline(cfg, rows, gs, gp, budget_s=20.0):
             el += time.time() - t0
             done += Bs
             log(f'[bench] cpu baseline step {steps}: {time.time() - t0:.1f}s')
-            if el > budget_s:
+            if el > budget_s and done // Bs >= min_steps:
                 break
         steps += 1
     return dict(value=round(done / el, 3), unit='train sequences/sec', cores=threads, kind='port',
                 sample=f'oracle (torch-CPU fp32 restatement) train step, {cfg["label"]}, d={cfg["d"]}, '
-                       f'L={cfg["L"]}, batch {Bs} (the GPU line\'s batch), 1 warm-up + {done // Bs} timed steps, '
-                       'dropout 0.2')
+                       f'L={cfg["L"]}, batch {Bs}, 1 warm-up + {done // Bs} timed steps '
+                       f'(budget {budget_s:.0f} s, at least {min_steps}), dropout 0.2, {threads} host threads '
+                       '(the box\'s CPU share for one GPU)')
 
 
-def run_c5(opt, world, rank, device):
+def run_c5(opt, world, rank, device, emit=True):
     """BASELINE configs[4] / SURVEY.md §8(d) C5 as a kernel roofline run: synthetic two-domain
     10M + 10M items, d=512, L=100, B=8192 global (8192/N per GPU, weak per-GPU work at N=8: 1024),
     graph from 2M sequences.  A full replicated model is infeasible (164 GB of fp32 parameters before
@@ -324,7 +337,7 @@ def run_c5(opt, world, rank, device):
 
     def step():
         state.step += 1
-        H, tok, sink = gcn(E, dg)
+        H, tok, sink = gcn.propagate(E, dg)
         xs = []
         for k, (seq, pos) in enumerate(passes):
             keys = state.keys(DK.site_enc(k, 0, DK.K_INPUT))
@@ -356,6 +369,7 @@ def run_c5(opt, world, rank, device):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     roof = ht.summary(opt.steps)
+    out = None
     if rank == 0:
         out = {'metric': 'C5 HBM roofline: K1 GCN SpMM + K2 embedding gather (fwd+bwd), algorithmic GB/s',
                'value': round(roof['achieved'] * world, 1), 'unit': 'GB/s (all ranks)', 'n_gpus': world,
@@ -367,7 +381,9 @@ def run_c5(opt, world, rank, device):
                           'graph_sequences': opt.c5_seqs, 'graph_nnz': g.nnz, 'dropout': p,
                           'parallelism': f'dp{world}'},
                'roofline': roof, 'cpu_baseline': None}
-        print(json.dumps(out), flush=True)
+        if emit:
+            print(json.dumps(out), flush=True)
+    return out
 
 
 def main():
@@ -376,13 +392,14 @@ def main():
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', default='mb', choices=list(CONFIGS) + ['c5'])
-    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32', 'fp32_exact'])
+    ap.add_argument('--precision', default='fp32', choices=['bf16', 'fp32', 'fp32_exact'])
     ap.add_argument('--batch', type=int, default=0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--c5-seqs', type=int, default=2_000_000)
     ap.add_argument('--no-extra', dest='extra', action='store_false',
-                    help='skip the extra lines (MB fp32 mode, FK bf16) of the default N=1 run')
+                    help='skip the extra lines (MB bf16 mode, FK bf16, C5) of the default N=1 run')
+    ap.add_argument('--no-c5', dest='c5_extra', action='store_false', help='skip the C5 extra line')
     ap.add_argument('--zero1', action='store_true',
                     help='N>1: ZeRO-1 (reduce-scatter, 1/p AdamW, all-gather; c2dsr_amd/dp.py) for the main line')
     ap.add_argument('--dp-split', action='store_true',
@@ -435,17 +452,27 @@ def main():
                 extra['ee_c4_split'] = brief(r3)
     if rank == 0:
         if world == 1 and opt.extra and opt.config == 'mb' and not opt.batch:
-            # driver-visible lines of the other single-GPU configurations: the fp32 parity
-            # mode on the same workload, and BASELINE configs[1] (Food-Kitchen sizes, B=1024, bf16)
-            extra['mb_fp32'] = brief(run_train(opt, cfg, 'mb', 'fp32', wl, world, rank, device))
+            # driver-visible lines of the other single-GPU configurations: the other precision mode on the same
+            # workload, and BASELINE configs[1] (Food-Kitchen sizes, B=1024, bf16 as BASELINE names it)
+            other = 'bf16' if opt.precision != 'bf16' else 'fp32'
+            extra[f'mb_{other}'] = brief(run_train(opt, cfg, 'mb', other, wl, world, rank, device))
             torch.cuda.empty_cache()
             fk = dict(CONFIGS['fk'])
             wfk = workload(fk, 'fk')
             extra['fk_bf16'] = brief(run_train(opt, fk, 'fk', 'bf16', wfk, world, rank, device))
             del wfk
+            torch.cuda.empty_cache()
+            if opt.c5_extra:  # BASELINE configs[4]: the K1 + K2 HBM roofline run at 10M + 10M items, d = 512
+                extra['c5_hbm'] = run_c5(opt, world, rank, device, emit=False)
+                torch.cuda.empty_cache()
         cpu = None
         if world == 1 and not opt.no_cpu_baseline:
             cpu = cpu_baseline(cfg, *wl, opt.cpu_budget)
+            if opt.config == 'mb' and opt.extra:
+                # the same restatement at configs[0] (C1: Food-Kitchen item counts, d=64, L=15,
+                # B=128 — the reference's own CPU-runnable case) for at least five timed steps
+                c1 = dict(n_a=29207, n_b=34886, d=64, L=15, B=128, label='Food-Kitchen sizes (synthetic), C1')
+                cpu['extra'] = {'c1_fk_d64': cpu_baseline(c1, *workload(c1, 'c1'), budget_s=5.0, min_steps=5)}
         res['cpu_baseline'] = cpu
         if extra:
             res['extra_lines'] = extra
@@ -537,27 +564,35 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     ms = el / opt.steps * 1e3
     value = B_global * opt.steps / el
     del tr, batches
-    peak = PEAK_BF16_TFLOPS if precision == 'bf16' else PEAK_FP32_TFLOPS
+    peak = {'bf16': PEAK_BF16_TFLOPS, 'fp32': PEAK_X3_TFLOPS}.get(precision, PEAK_FP32_TFLOPS)
     roof = None
     if ks is not None:
         traffic, tsrc, busy = k5_traffic(precision) if name == 'mb' else (None, None, None)
         roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
                     frac=round(ks['tflops'] / peak, 4), traffic=traffic, traffic_source=tsrc,
-                    kernel=('K5 fused classifier head + CE: ce_fwdu_kernel (lse + dH, online) + ce_dw_kernel '
-                            '(bf16 MFMA); credited 2·M·n·d per product (fwd_u 2, dw 1)'
-                            if precision == 'bf16' else 'gemm_kernel (K5 materialised logits GEMMs)'),
+                    kernel={'bf16': 'K5 fused classifier head + CE: ce_fwdu_kernel (lse + dH, online) + ce_dw_kernel '
+                                    '(bf16 MFMA); credited 2·M·n·d per product (fwd_u 2, dw 1)',
+                            'fp32': 'K5 fused classifier head + CE at fp32 accuracy: ce3_kernel<256,0> (lse + dH, '
+                                    'online) + ce3_kernel<256,1> (dW), split-bf16 operands, 3 bf16 MFMAs per '
+                                    'product; credited 2·Mv·n·d per fp32 product over the Mv valid rows (fwd_u 2, '
+                                    'dw 1); peak = bf16 dense peak / 3'}.get(
+                        precision, 'gemm_kernel (K5 materialised logits GEMMs, fp32-input MFMA)'),
                     ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'],
                     mfma_busy=busy, mfma_busy_note='SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles of the K5 launches '
                     '(same PMC run as traffic; counts the recomputed logits tiles that frac does not credit)')
-    if hb is not None and name == 'mb' and precision == 'bf16':
-        hb['traffic'], hb['traffic_source'] = hbm_traffic()
+    if hb is not None and name == 'mb' and precision in ('bf16', 'fp32'):
+        hb['traffic'], hb['traffic_source'] = hbm_traffic(precision)
         hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
     par = f'dp{world}' + ('-split' if dp_split and world > 1 else '') + ('-zero1' if zero1 and world > 1 else '')
     return {'metric': 'train sequences/sec at d=256, seq_len=50, |items|~100k',
             'value': round(value, 2), 'unit': 'train sequences/sec', 'n_gpus': world, 'steps': opt.steps,
             'warmup': opt.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
             'scaling': 'strong' if dp_split and world > 1 else 'weak',
-            'vs_baseline': None, 'dtype': precision, 'data': 'synthetic (Zipf two-domain sequences)',
+            'vs_baseline': None, 'dtype': {'fp32': 'f32', 'bf16': 'bf16', 'fp32_exact': 'f32'}[precision],
+            'precision_mode': {'fp32': 'fp32 results, split-bf16 x3 MFMA products (reference parity 1e-4)',
+                               'bf16': 'bf16 MFMA operands, fp32 accumulate and storage',
+                               'fp32_exact': 'fp32-input MFMA for every product'}[precision],
+            'data': 'synthetic (Zipf two-domain sequences)',
             'config': {'workload': f'{name}: {cfg["label"]}', 'n_item_a': cfg['n_a'], 'n_item_b': cfg['n_b'],
                        'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B_local, 'global_batch': B_global,
                        'train_sequences': int(n_rows), 'len_rec': 10, 'dropout': 0.2, 'parallelism': par},

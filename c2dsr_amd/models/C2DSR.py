@@ -145,9 +145,9 @@ class C2DSR(nn.Module):
         if self.training:
             self.new_step()
         g_share, g_spec = self.graphs()
-        hs, ts, ss = self.gnn_share(self.embed_i.weight, g_share)
-        ha, ta, sa = self.gnn_a(self.embed_i_a.weight, g_spec)
-        hb, tb, sb = self.gnn_b(self.embed_i_b.weight, g_spec)
+        hs, ts, ss = self.gnn_share.propagate(self.embed_i.weight, g_share)
+        ha, ta, sa = self.gnn_a.propagate(self.embed_i_a.weight, g_spec)
+        hb, tb, sb = self.gnn_b.propagate(self.embed_i_b.weight, g_spec)
         self.hi_share, self.hi_a, self.hi_b = hs, ha, hb
         self._tok, self._sink = (ts, ta, tb), (ss, sa, sb)
 

@@ -16,6 +16,7 @@ import torch.nn as nn
 
 from .. import dropout as DK
 from .. import ops
+from ..graph import DeviceGraph
 
 
 class MultiheadAttentionParams(nn.Module):
@@ -176,11 +177,18 @@ class SelfAttention(nn.Module):
         return ops.AddLNFn.apply(x, None, nm.weight, nm.bias, 0.0, (0, 0), 0, nm.eps)
 
     def forward(self, seq, seq_enc, pos, pass_id=None):
-        """encoders.py:29-33 on a caller-provided seq_enc (the fused path is ``forward_items``)."""
+        """encoders.py:29-33 on a caller-provided seq_enc [B, L, d] (the training step's fused path is
+        ``forward_items``): ``seq_enc += pos_emb(pos)`` mutates the caller's tensor in place as the reference
+        does (Q20), then dropout and the encoder stack."""
         if pass_id is None:
             pass_id = DK.PASS_SHARE
+        if not seq_enc.is_contiguous():
+            raise ValueError('SelfAttention.forward: seq_enc must be contiguous (it is updated in place)')
         p, k = self._drop(pass_id, 0, DK.K_INPUT)
-        x = ops.PosDropFn.apply(seq_enc.contiguous(), self.pos_emb.weight, pos, p, k, self.state.row_offset)
+        L = seq_enc.shape[1]
+        x = ops.PosAddFn.apply(seq_enc, self.pos_emb.weight, pos)
+        if p > 0.0:
+            x = ops.DropFn.apply(x, p, k, self.state.row_offset * L)
         return self.encode(x, seq, pass_id)
 
     def forward_items(self, seq, pos, H, tok, E, sink, pass_id):
@@ -202,12 +210,36 @@ class GCN(nn.Module):
         self.state = StepState()
         self.table = 0
         self.pad_row = args.idx_pad
+        self._graph_cache = None
 
-    def forward(self, h, adj, sink=None):
-        """h: [N, d] table, adj: c2dsr_amd.graph.DeviceGraph.  Returns (H, token)."""
+    def _keys(self):
         p = self.dropout_gnn if self.training else 0.0
-        keys = [self.state.keys(DK.site_gcn(self.table, k)) if p > 0 else (0, 0) for k in range(self.n_gnn)]
+        return p, [self.state.keys(DK.site_gcn(self.table, k)) if p > 0 else (0, 0) for k in range(self.n_gnn)]
+
+    def _device_graph(self, adj, device):
+        """adj as the reference passes it (the torch sparse COO of utils/graph.make_graph), a CSRGraph or a
+        DeviceGraph → the DeviceGraph the SpMM runs on (converted once per adjacency object)."""
+        if isinstance(adj, DeviceGraph):
+            return adj
+        hit = self._graph_cache
+        if hit is not None and hit[0] is adj and hit[1].rowptr.device == device:
+            return hit[1]
+        from .C2DSR import _as_csr
+        dg = DeviceGraph(_as_csr(adj, adj.shape[0]), device)
+        self._graph_cache = (adj, dg)
+        return dg
+
+    def forward(self, h, adj):
+        """encoders.py:42-48: h [N, d], adj [N, N] (torch sparse COO as make_graph returns it) → H [N, d] =
+        mean(h, A·drop(h), …), differentiable w.r.t. h (ops.GCNPropFn)."""
+        p, keys = self._keys()
+        return ops.GCNPropFn.apply(h, self._device_graph(adj, h.device), self.n_gnn, p, keys)
+
+    def propagate(self, h, adj, sink=None):
+        """The training step's fused form (C2DSR.convolve_graph): h [N, d], adj a DeviceGraph → (H, token,
+        sink); H's gradient arrives through the sink, filled by the embedding lookups of H (ops.GCNFn)."""
+        p, keys = self._keys()
         if sink is None:
             sink = ops.GradSink(h.shape[0], h.shape[1], h.device, self.state)
-        H, tok = ops.GCNFn.apply(h, adj, self.n_gnn, p, keys, self.pad_row, sink)
+        H, tok = ops.GCNFn.apply(h, self._device_graph(adj, h.device), self.n_gnn, p, keys, self.pad_row, sink)
         return H, tok, sink

@@ -550,6 +550,44 @@ class GCNFn(Function):
         return (None if direct else gE), None, None, None, None, None, None
 
 
+class GCNPropFn(Function):
+    """``GCN.forward(h, adj)`` at the module API (models/encoders.py:42-48): H = mean(E, A·drop(E), …) as an
+    ordinary differentiable op — the gradient of any use of H flows back to E through Aᵀ (same kernels and
+    dropout masks as GCNFn, whose fused form serves the training step's embedding lookups instead)."""
+
+    @staticmethod
+    def forward(ctx, E, graph, n_gnn, p, keys):
+        require_device(E)
+        out = torch.empty_like(E)
+        inv = 1.0 / (n_gnn + 1)
+        if n_gnn == 0:
+            out.copy_(E)
+        h_prev = E
+        for k in range(n_gnn):
+            h_k = None if k == n_gnn - 1 else torch.empty_like(E)
+            spmm(graph, False, h_prev, keys[k], p, 0, inv, E if k == 0 else None, inv, 0.0, -1,
+                 0.0 if k == 0 else 1.0, out, h_k)
+            h_prev = h_k
+        ctx.graph, ctx.n_gnn, ctx.p, ctx.keys = graph, n_gnn, p, keys
+        return out
+
+    @staticmethod
+    def backward(ctx, gH):
+        G = gH.contiguous()
+        n = ctx.n_gnn
+        if n == 0:
+            return G, None, None, None, None
+        inv = 1.0 / (n + 1)
+        X, alpha = G, inv
+        for k in range(n, 1, -1):  # T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k
+            T = torch.empty_like(G)
+            spmm(ctx.graph, True, X, ctx.keys[k - 1], ctx.p, 1, alpha, G, inv, 0.0, -1, 0.0, T)
+            X, alpha = T, 1.0
+        gE = torch.empty_like(G)
+        spmm(ctx.graph, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 0.0, -1, 0.0, gE)
+        return gE, None, None, None, None
+
+
 # ----------------------------------------------------------------------------- index plans
 _side_streams = {}
 _PLAN_SIDE = __import__('os').environ.get('C2DSR_PLAN_SIDE', '1') == '1'
@@ -830,6 +868,64 @@ class PosDropFn(Function):
         lib('c2dsr_embed_bwd', pos, pos, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.row_base) * L,
             1.0, None, 0, gP, ctx.P.shape[0], gxin, ws, ws_bytes, stream())
         return gxin, gP_ret, None, None, None, None
+
+
+class PosAddFn(Function):
+    """``seq_enc += self.pos_emb(pos)`` IN PLACE (encoders.py:30, Q20): the caller's tensor is mutated as the
+    reference's in-place add mutates it (c2dsr_embed_fwd with Xin = X), and autograd sees an in-place op
+    (mark_dirty): the gradient of the mutated tensor flows to the original values and, summed by position,
+    to the position table."""
+
+    @staticmethod
+    def forward(ctx, xin, P, pos):
+        require_device(xin)
+        B, L, d = xin.shape
+        lib('c2dsr_embed_fwd', pos, pos, B * L, d, None, None, xin, P, 1.0, 0, 0, 0.0, 0, xin, stream())
+        ctx.mark_dirty(xin)
+        ctx.save_for_backward(pos)
+        ctx.P = P
+        return xin
+
+    @staticmethod
+    def backward(ctx, gx):
+        (pos,) = ctx.saved_tensors
+        gx = gx.contiguous()
+        B, L = pos.shape
+        d = gx.shape[-1]
+        n = B * L
+        gP = _grad_target(ctx.P)
+        gP_ret = None
+        if gP is None and ctx.needs_input_grad[1]:
+            gP_ret = torch.zeros_like(ctx.P)
+            gP = gP_ret
+        if gP is None:
+            return gx, None, None
+        gxin = torch.empty_like(gx)
+        ws_bytes = lib.raw('c2dsr_embed_bwd_workspace')(n, d)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gx.device)
+        lib('c2dsr_embed_bwd', pos, pos, n, d, gx, 0, 0, 0.0, 0, 1.0, None, 0, gP, ctx.P.shape[0], gxin, ws, ws_bytes,
+            stream())
+        return gxin, gP_ret, None
+
+
+class DropFn(Function):
+    """y = dropout(x) with the stateless hash masks (encoders.py:31), index (row_base + row)·d + col."""
+
+    @staticmethod
+    def forward(ctx, x, p, keys, row_base):
+        y = torch.empty_like(x)
+        lib('c2dsr_add_dropout', None, x.contiguous(), x.numel(), x.shape[-1], keys[0], keys[1], float(p),
+            int(row_base), y, stream())
+        ctx.p, ctx.keys, ctx.row_base = p, keys, row_base
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        lib('c2dsr_add_dropout', None, dy, dy.numel(), dy.shape[-1], ctx.keys[0], ctx.keys[1], float(ctx.p),
+            int(ctx.row_base), dx, stream())
+        return dx, None, None, None
 
 
 # ----------------------------------------------------------------------------- attention

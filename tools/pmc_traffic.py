@@ -2,7 +2,9 @@
 FETCH_SIZE (KB) doubled per the gfx950 correction (MI355X_MICROARCH.md §HBM), WRITE_SIZE (KB) as is.
 Also the K1 + K2 kernels (GCN SpMM, embedding gather / segment sums) per step → hbm_traffic.json next to
 the K5 file (the PMC run is bench.py --steps 2 --warmup 1: 3 steps).
-usage: python tools/pmc_traffic.py gpurun_out/TAG [profiles/k5_traffic.json]"""
+usage: python tools/pmc_traffic.py gpurun_out/TAG [profiles/k5_traffic_fp32.json] [fp32|bf16]
+(the precision of the profiled bench line selects the K5 kernels: fp32 mode = ce3.hip, bf16 = ce.hip; the K1+K2
+file is written next to the K5 file as hbm_traffic[_fp32].json)"""
 import csv
 import json
 import re
@@ -12,8 +14,10 @@ from collections import defaultdict
 
 pre = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else None
-# the kernels the two timed K5 entry points launch per head (c2dsr_ce_fused_fwd_u: fwdu + rows; _dw: dw)
-K5 = ('ce_fwdu_kernel', 'ce_rows_kernel', 'ce_dw_kernel')
+prec = sys.argv[3] if len(sys.argv) > 3 else 'fp32'
+# the kernels the two timed K5 entry points launch per head (fwd_u: sweep + rows; dw: sweep)
+K5 = (('ce_fwdu_kernel', 'ce_rows_kernel', 'ce_dw_kernel') if prec == 'bf16' else
+      ('ce3_kernel<256, 0>', 'ce_rows_kernel', 'ce3_kernel<256, 1>'))
 K12 = ('spmm_kernel', 'combine_kernel', 'embed_fwd_kernel', 'seg_chunk_kernel', 'seg_split1_kernel',
        'seg_split2_kernel')
 PMC_STEPS = 3
@@ -26,7 +30,7 @@ def per_kernel(path, counter, names=K5):
             continue
         name = re.sub(r'\(anonymous namespace\)::', '', r['Kernel_Name'])
         for k in names:
-            if re.search(r'\b' + k + r'\b', name):
+            if (k in name) if '<' in k else re.search(r'\b' + k + r'\b', name):
                 vals[k].append(float(r['Counter_Value']) * 1e3)  # KB -> B
     return vals
 
@@ -48,7 +52,7 @@ try:
     busy, cyc = 0.0, 0.0
     for r in csv.DictReader(open(f'{pre}_sq/run_counter_collection.csv')):
         name = re.sub(r'\(anonymous namespace\)::', '', r['Kernel_Name'])
-        if not any(re.search(r'\b' + k + r'\b', name) for k in K5):
+        if not any((k in name) if '<' in k else re.search(r'\b' + k + r'\b', name) for k in K5):
             continue
         if r['Counter_Name'] == 'SQ_VALU_MFMA_BUSY_CYCLES':
             busy += float(r['Counter_Value'])
@@ -79,4 +83,5 @@ if out:
     import os
     json.dump(dict(bytes_per_step=tot2, per_kernel=rows2,
                    source=f'rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE passes, {pre.split("/")[-1]}, rev {rev}'),
-              open(os.path.join(os.path.dirname(out), 'hbm_traffic.json'), 'w'), indent=1)
+              open(os.path.join(os.path.dirname(out), 'hbm_traffic.json' if prec == 'bf16' else 'hbm_traffic_fp32.json'),
+                   'w'), indent=1)
