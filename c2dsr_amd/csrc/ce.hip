@@ -29,37 +29,8 @@
 #ifndef CE_FWDU_DT
 #define CE_FWDU_DT 3
 #endif
-#ifndef CE_FWDU_KBFAST
-#define CE_FWDU_KBFAST 0
-#endif
 #ifndef CE_DW_DS
 #define CE_DW_DS 3
-#endif
-#ifndef CE_S_B2B
-#define CE_S_B2B 0
-#endif
-// experiment switches of the fwd_u kernel (wrong results; timing only): no exp, no W-tile DMA in the
-// loop, 1/8 of the U MFMAs, no per-tile barrier
-#ifndef CE_X_NOEXP
-#define CE_X_NOEXP 0
-#endif
-#ifndef CE_X_NODMA
-#define CE_X_NODMA 0
-#endif
-#ifndef CE_X_NOU
-#define CE_X_NOU 0
-#endif
-#ifndef CE_X_NOBAR
-#define CE_X_NOBAR 0
-#endif
-#ifndef CE_X_NOMAX
-#define CE_X_NOMAX 0
-#endif
-#ifndef CE_X_NOLDS
-#define CE_X_NOLDS 0
-#endif
-#ifndef CE_X_TAU
-#define CE_X_TAU 8.f
 #endif
 #ifndef CE_DW_DT
 #define CE_DW_DT 3
@@ -434,15 +405,9 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
       }(std::make_integer_sequence<int, KS>{});
       // ---- dHᵀ[k][r] += Σ_c W[c][k] P'ᵀ[c][r], q = (kb, cb, st)
       bf16x8 tf[DT + 2];
-      // U step q: output k-block U_KB(q), column quarter U_J(q) (16 columns: block U_J >> 1, half U_J & 1);
-      // CE_FWDU_KBFAST cycles the 8 accumulators fastest (no back-to-back MFMAs on one accumulator)
-#if CE_FWDU_KBFAST
-#define U_KB(q) ((q) % KB)
-#define U_J(q) ((q) / KB)
-#else
+      // U step q: output k-block U_KB(q), column quarter U_J(q) (16 columns: block U_J >> 1, half U_J & 1)
 #define U_KB(q) ((q) >> 2)
 #define U_J(q) ((q) & 3)
-#endif
       [&]<int... P>(std::integer_sequence<int, P...>) {
         ((tf[P] = tr_frag_c<TILE, U_J(P) * 16, U_KB(P) * 32, 0>(oH)), ...);
       }(std::make_integer_sequence<int, DT>{});
@@ -455,14 +420,9 @@ __global__ __launch_bounds__(256, 1) void ce_dh_kernel(const bf16* __restrict__ 
                 constexpr int q1 = q + DT;
                 tf[q1 % (DT + 2)] = tr_frag_c<TILE, U_J(q1) * 16, U_KB(q1) * 32, 0>(oH);
               }
-#if CE_X_NOU
-              if constexpr (q % 8 == 0)
-#endif
               dacc[U_KB(q)] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[U_J(q) >> 1][U_J(q) & 1],
                                                                      dacc[U_KB(q)], 0, 0, 0);
-#if !CE_X_NODMA
               if constexpr (q % 4 == 1 && q / 4 < NDMA) dma16_s<q == 1>(nsrc, dvoff[q / 4], ddst[q / 4] + nbuf);
-#endif
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -513,7 +473,7 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
   constexpr int IMG = TILE * D * 2;
   constexpr int NDMA = (TILE / 4) * (D / 128) / 4;
   constexpr int NB = 4;
-  constexpr float TAU = CE_X_TAU;
+  constexpr float TAU = 8.f;  // lazy-max threshold (p ≤ 2^TAU)
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
   __shared__ __attribute__((aligned(16))) float b2s[NB][4][TILE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -612,9 +572,7 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
       const int cn = min(c_beg + (t + 3) * TILE, c_last);
       const bf16* nsrc = Wb + (long)cn * D;
       const unsigned nbuf = ((t + 3) % NB) * IMG;
-#if !CE_X_NODMA
       dma4(bias2 + cn + lane, b2s[(t + 3) % NB][w]);
-#endif
       // lazy rescale: the row's max moved up by more than TAU (always on the first tile)
       {
         const bool need = mnext > mrow + TAU;
@@ -645,46 +603,6 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
       // ---- S(t+1) ∥ epilogue(t)
       f32x16 sn[2];
       bf16x8 x[2][2];
-#if CE_S_B2B
-      // the two accumulator chains one after the other (unit u: block u / KS, k-step u % KS): each MFMA
-      // accumulates onto the one just issued, which the matrix core forwards; interleaving the chains
-      // (distance 2) waits for the write-back of every result instead
-      bf16x8 fb[DS + 2];
-      [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((fb[P] = row_frag_c<TILE, (P / KS) * 32, P % KS, 0>(oS)), ...);
-      }(std::make_integer_sequence<int, DS>{});
-      __builtin_amdgcn_sched_barrier(0);
-      [&]<int... K>(std::integer_sequence<int, K...>) {
-        (
-            [&] {
-              constexpr int u = K;
-              constexpr int cb = u / KS, ks = u % KS;
-              if constexpr (u + DS < 2 * KS) {
-                constexpr int u1 = u + DS;
-                fb[u1 % (DS + 2)] = row_frag_c<TILE, (u1 / KS) * 32, u1 % KS, 0>(oS);
-              }
-              if constexpr (ks == 0)
-                sn[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[u % (DS + 2)], hf[0], f32x16{}, 0, 0, 0);
-              else
-                sn[cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[u % (DS + 2)], hf[ks], sn[cb], 0, 0, 0);
-              constexpr int ce = u & 1, ke = u >> 1;  // epilogue unit: block ce, elements ke·EPK ..
-#pragma unroll
-              for (int e = 0; e < EPK; ++e) {
-                const int i = ke * EPK + e;
-#if CE_X_NOEXP
-                const float pv = sc[ce][i] - msub;
-#else
-                const float pv = ex2(sc[ce][i] - msub);
-#endif
-                sc[ce][i] = pv;
-                zrow += pv;
-              }
-              if constexpr ((ke * EPK + EPK) % 8 == 0) x[ce][(ke * EPK) / 8] = acc_frag(sc[ce], (ke * EPK) / 8);
-              __builtin_amdgcn_sched_barrier(0);
-            }(),
-            ...);
-      }(std::make_integer_sequence<int, 2 * KS>{});
-#else
       bf16x8 fa[DS + 2][2];
       [&]<int... P>(std::integer_sequence<int, P...>) {
         ((fa[P][0] = row_frag_c<TILE, 0, P, 0>(oS), fa[P][1] = row_frag_c<TILE, 32, P, 0>(oS)), ...);
@@ -694,17 +612,10 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
         (
             [&] {
               constexpr int ks = K;
-#if !CE_X_NOLDS
               if constexpr (ks + DS < KS) {
                 fa[(ks + DS) % (DS + 2)][0] = row_frag_c<TILE, 0, ks + DS, 0>(oS);
                 fa[(ks + DS) % (DS + 2)][1] = row_frag_c<TILE, 32, ks + DS, 0>(oS);
               }
-#else
-              if constexpr (ks + DS < KS) {
-                fa[(ks + DS) % (DS + 2)][0] = fa[0][0];
-                fa[(ks + DS) % (DS + 2)][1] = fa[0][1];
-              }
-#endif
               if constexpr (ks == 0) {
                 sn[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][0], hf[0], f32x16{}, 0, 0, 0);
                 sn[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][1], hf[0], f32x16{}, 0, 0, 0);
@@ -717,11 +628,7 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
 #pragma unroll
                 for (int e = 0; e < EPK; ++e) {
                   const int i = ks * EPK + e;
-#if CE_X_NOEXP
-                  const float pv = sc[cb][i] - msub;
-#else
                   const float pv = ex2(sc[cb][i] - msub);
-#endif
                   sc[cb][i] = pv;
                   zrow += pv;
                 }
@@ -734,21 +641,14 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
             }(),
             ...);
       }(std::make_integer_sequence<int, KS>{});
-#endif
       // ---- Uᵀ[k][r] += Σ_c W[c][k] Pᵀ[c][r]  ∥  v = S(t+1)·log2e + b2 and its max
       f32x4 b4n[2][4];
       bias4(bs, b4n);
       float tm = -INFINITY;
       bf16x8 tf[DT + 2];
-      // U step q: output k-block U_KB(q), column quarter U_J(q) (16 columns: block U_J >> 1, half U_J & 1);
-      // CE_FWDU_KBFAST cycles the 8 accumulators fastest (no back-to-back MFMAs on one accumulator)
-#if CE_FWDU_KBFAST
-#define U_KB(q) ((q) % KB)
-#define U_J(q) ((q) / KB)
-#else
+      // U step q: output k-block U_KB(q), column quarter U_J(q) (16 columns: block U_J >> 1, half U_J & 1)
 #define U_KB(q) ((q) >> 2)
 #define U_J(q) ((q) & 3)
-#endif
       [&]<int... P>(std::integer_sequence<int, P...>) {
         ((tf[P] = tr_frag_c<TILE, U_J(P) * 16, U_KB(P) * 32, 0>(oH)), ...);
       }(std::make_integer_sequence<int, DT>{});
@@ -761,15 +661,9 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
                 constexpr int q1 = q + DT;
                 tf[q1 % (DT + 2)] = tr_frag_c<TILE, U_J(q1) * 16, U_KB(q1) * 32, 0>(oH);
               }
-#if CE_X_NOU
-              if constexpr (q % 8 == 0)
-#endif
               dacc[U_KB(q)] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[q % (DT + 2)], x[U_J(q) >> 1][U_J(q) & 1],
                                                                      dacc[U_KB(q)], 0, 0, 0);
-#if !CE_X_NODMA
               if constexpr (q % 4 == 1 && q / 4 < NDMA) dma16_s<q == 1>(nsrc, dvoff[q / 4], ddst[q / 4] + nbuf);
-#endif
-#if !CE_X_NOMAX
 #pragma unroll
               for (int e = 0; e < MPK; ++e) {
                 const int el = q * MPK + e;
@@ -778,7 +672,6 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
                 sn[cb][i] = v;
                 tm = fmaxf(tm, v);
               }
-#endif
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -788,14 +681,8 @@ __global__ __launch_bounds__(256, 1) void ce_fwdu_kernel(const bf16* __restrict_
       mnext = fmaxf(tm, __shfl_xor(tm, 32, 64));
       sc[0] = sn[0];
       sc[1] = sn[1];
-#if CE_X_NODMA
-      dma_wait();
-#else
       dma_wait_keep<NDMA + 1>();
-#endif
-#if !CE_X_NOBAR
       __syncthreads();
-#endif
     }
   }
   const float ztot = zrow + __shfl_xor(zrow, 32, 64);

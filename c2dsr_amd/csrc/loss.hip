@@ -548,25 +548,6 @@ __global__ __launch_bounds__(64) void loss_partials_final_kernel(const float* __
   if (threadIdx.x < 8) vec[k] = t;
 }
 
-// per-device scratch for the stage-1 partials (grown on demand, never freed)
-float* partials_scratch(size_t floats) {
-  static float* buf[64] = {nullptr};
-  static size_t cap[64] = {0};
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev < 0 || dev >= 64) return nullptr;
-  if (cap[dev] < floats) {
-    if (buf[dev]) {
-      (void)hipDeviceSynchronize();
-      (void)hipFree(buf[dev]);
-    }
-    buf[dev] = nullptr;
-    cap[dev] = 0;
-    if (hipMalloc((void**)&buf[dev], floats * sizeof(float)) != hipSuccess) return nullptr;
-    cap[dev] = floats;
-  }
-  return buf[dev];
-}
 
 // scalar combination (trainer.py:143-156) from the (globally reduced) vec[0..8]
 // (vec[8] = loss_mi).  out3 = (loss, loss_rec, loss_mi); coefA/coefB = per-row
@@ -759,12 +740,13 @@ C2_API int c2dsr_outer_add(const float* a, long sa, const float* v, int M, int d
   C2_CHECK_LAUNCH();
   return 0;
 }
+// the stage-1 partials of c2dsr_loss_partials (floats), allocated by the caller on the launch stream
+C2_API size_t c2dsr_loss_partials_workspace(int BR) { return (size_t)c2::ceil_div(2 * BR, 256) * 8; }
 C2_API int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, const float* rowsB, const int64_t* tB,
-                               int n_b, int BR, float* vec, void* stream) {
+                               int n_b, int BR, float* vec, float* part, void* stream) {
   const int nblk = c2::ceil_div(2 * BR, 256);
   if (nblk == 0) return (int)hipMemsetAsync(vec, 0, 8 * sizeof(float), (hipStream_t)stream);
-  float* part = partials_scratch((size_t)nblk * 8);
-  if (!part) return (int)hipErrorOutOfMemory;
+  if (!part) return (int)hipErrorInvalidValue;
   loss_partials_kernel<<<nblk, 256, 0, (hipStream_t)stream>>>(rowsA, tA, n_a, rowsB, tB, n_b, BR, part);
   loss_partials_final_kernel<<<1, 64, 0, (hipStream_t)stream>>>(part, nblk, vec);
   C2_CHECK_LAUNCH();

@@ -60,8 +60,18 @@ class FlatStore:
                     self.fresh[o:o + n].add_(p.grad.reshape(-1))
                 p.grad = self.fresh[o:o + n].view(p.shape)
 
+    def release_accum(self):
+        """ZeRO-1 keeps the epoch accumulation for this rank's shard only (optim.FlatAdamW): the full-size
+        buffer is freed and grad_total is unavailable."""
+        if self.direct:
+            raise RuntimeError('the direct store has no separate accumulator')
+        self.accum = None
+
     def grad_total(self, name):
         """Accumulated gradient (epoch accumulator + this step's) of one parameter."""
+        if self.accum is None:
+            raise RuntimeError('ZeRO-1: the accumulated gradient is sharded across ranks (FlatAdamW.accum holds '
+                               'this rank\'s shard); grad_total is unavailable')
         for nm, p, o, n in self.entries:
             if nm == name:
                 if self.direct:

@@ -241,7 +241,8 @@ class LossHeadFn(Function):
         coefA = torch.empty(2, **f32)
         coefB = torch.empty(2, **f32)
         (_, _, tA, _, _, rA, _, _, _), (_, _, tB, _, _, rB, _, _, _) = heads
-        lib('c2dsr_loss_partials', rA, tA, m.n_a, rB, tB, m.n_b, BR, vec, s)
+        lpw = torch.empty(max(1, int(lib.raw('c2dsr_loss_partials_workspace')(BR))), **f32)
+        lib('c2dsr_loss_partials', rA, tA, m.n_a, rB, tB, m.n_b, BR, vec, lpw, s)
         cnt = None
         if m.counts is not None:
             # data parallel: the global valid-target counts (the only global values the gradient needs)
@@ -249,7 +250,9 @@ class LossHeadFn(Function):
             # asynchronously and finalized after the backward (LossMeta.finish_values)
             cnt, work = m.counts
             work.wait()
-            m.pending = (m.reduce_async(vec), vec, cnt, Bg * R, out3)
+            # the collective works on its own copy: the loss finalised below (and returned) reads vec now
+            vred = vec.clone()
+            m.pending = (m.reduce_async(vred), vred, cnt, Bg * R, out3)
         elif m.allreduce is not None:  # data parallel without pre-reduced counts: reduce everything now
             m.allreduce(vec)
         lib('c2dsr_loss_finalize', vec, cnt, Bg * R, float(m.lam), out3, coefA, coefB, s)

@@ -292,6 +292,12 @@ class LinearFn(Function):
         M = x.numel() // K
         y = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
         kind = rg_kind(precision, M, N, K)
+        if kind == 'x3' and relu_drop is not None:
+            # the ReLU producer (linear1): its sign decisions select which gradient terms exist, so a
+            # pre-activation within the split product's rounding (~1e-5 relative) of zero would flip a whole
+            # dy·x term of the weight gradient (tools/fp32_diag.py: 2e-3 vs 1.6e-5 with this product exact) —
+            # it runs on the exact fp32-input MFMA GEMM
+            kind = None
         if kind:
             rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop, x3=kind == 'x3')
         else:

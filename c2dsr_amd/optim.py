@@ -28,7 +28,11 @@ class FlatAdamW(torch.optim.Optimizer):
         self.m = torch.zeros(n, device=dev)
         self.v = torch.zeros(n, device=dev)
         self.vmax = torch.zeros(n, device=dev)
-        self.accum = flat.accum if zero is None else torch.zeros(n, device=dev)
+        if zero is None:
+            self.accum = flat.accum
+        else:
+            self.accum = torch.zeros(n, device=dev)
+            flat.release_accum()  # the shard above replaces it (1/p of the state, not 1 + 1/p)
         self.n_steps = 0
         self.accumulate = True  # grads accumulate until zero_grad (Q3)
 

@@ -64,11 +64,26 @@ def load_lists(path: str):
         return _check_lists(_Restricted(f, allow_tensors=False).load(), path)
 
 
-def save_lists(path: str, data) -> None:
-    """dataloader.py:28-29."""
+def _writer_rank() -> bool:
+    """Data parallel: one writer (rank 0) — every rank builds the same lists, concurrent truncating writes of
+    one path would race (the reference is single-process)."""
+    import torch.distributed as dist
+    return not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+
+
+def _dump_atomic(path: str, obj) -> None:
+    """pickle to a temporary file beside ``path`` and rename it over ``path``: a reader never sees a torn file."""
     os.makedirs(os.path.dirname(path) or '.', exist_ok=True)
-    with open(path, 'wb') as f:
-        pickle.dump(data, f)
+    tmp = f'{path}.tmp{os.getpid()}'
+    with open(tmp, 'wb') as f:
+        pickle.dump(obj, f)
+    os.replace(tmp, path)
+
+
+def save_lists(path: str, data) -> None:
+    """dataloader.py:28-29 (rank 0 only under data parallelism; atomic replace)."""
+    if _writer_rank():
+        _dump_atomic(path, data)
 
 
 def _to_sparse(g):
@@ -78,10 +93,10 @@ def _to_sparse(g):
 
 
 def save_graph(path: str, g_share, g_spec) -> None:
-    """utils/graph.py:101-103: the two normalised adjacencies as torch sparse COO tensors."""
-    os.makedirs(os.path.dirname(path) or '.', exist_ok=True)
-    with open(path, 'wb') as f:
-        pickle.dump((_to_sparse(g_share), _to_sparse(g_spec)), f)
+    """utils/graph.py:101-103: the two normalised adjacencies as torch sparse COO tensors (rank 0 only under
+    data parallelism; atomic replace)."""
+    if _writer_rank():
+        _dump_atomic(path, (_to_sparse(g_share), _to_sparse(g_spec)))
 
 
 def load_graph(path: str):

@@ -204,8 +204,10 @@ class Trainer(object):
                 t = torch.empty(2 * B * R, device=dev, dtype=torch.int64)
                 lib('c2dsr_rec_targets', ts, tx, B, L, R, t, s)
                 tg.append(t)
-            cvec = torch.empty(9, device=dev, dtype=torch.float32)
-            lib('c2dsr_loss_partials', None, tg[0], self.n_item_a, None, tg[1], self.n_item_b, B * R, cvec, s)
+            cvec = torch.zeros(9, device=dev, dtype=torch.float32)  # [8] (loss_mi) is not written here
+            lpw = torch.empty(max(1, int(lib.raw('c2dsr_loss_partials_workspace')(B * R))), device=dev,
+                              dtype=torch.float32)
+            lib('c2dsr_loss_partials', None, tg[0], self.n_item_a, None, tg[1], self.n_item_b, B * R, cvec, lpw, s)
             self.dp_counts = (cvec, dist.all_reduce(cvec, async_op=True))
         if not counts:
             return {}, {}, None

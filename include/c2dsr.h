@@ -210,7 +210,9 @@ int c2dsr_outer_add(const float* a, long sa, const float* v, int M, int d, float
 /* vec[0..7] = per-head CE sums and valid counts of this rank's rows (all-reduced under DP); rowsA/rowsB
  * may be NULL (counts only: data parallel reduces the counts ahead of the forward) */
 int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, const float* rowsB, const int64_t* tB, int n_b,
-                        int BR, float* vec, void* stream);
+                        int BR, float* vec, float* workspace, void* stream);
+/* floats of c2dsr_loss_partials' workspace (per-block partials; the caller allocates it on the launch stream) */
+size_t c2dsr_loss_partials_workspace(int BR);
 /* out3 = (loss, loss_rec, loss_mi) from vec[0..8]; coefA/B = per-row grad weights; cnt (nullable) supplies
  * the valid counts cnt[4..7] instead of vec[4..7] */
 int c2dsr_loss_finalize(const float* vec, const float* cnt, int BR_global, float lam, float* out3, float* coefA,
