@@ -30,6 +30,14 @@
 
 #include <utility>
 
+// tuning knobs (tools/ce3_micro.py; the defaults are the shipped configuration)
+#ifndef CE3_DS
+#define CE3_DS 2
+#endif
+#ifndef CE3_DT
+#define CE3_DT 2
+#endif
+
 namespace {
 
 using namespace c2img;
@@ -56,7 +64,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
   constexpr int IMG = T3 * D2 * 2;                 // bytes per image
   constexpr int NDMA = (T3 / 4) * (D2 / 128) / 4;  // LDS-DMA wave-instructions per wave per tile
   constexpr int NB = 4;                            // images: S(t+1), second product(t), t+2 landed, t+3 landing
-  constexpr int DS = 2, DT = 2;                    // LDS fragment prefetch depth (steps ahead)
+  constexpr int DS = CE3_DS, DT = CE3_DT;          // LDS fragment prefetch depth (steps ahead)
   constexpr int EPK = 16 / KS;                     // epilogue elements per S k-step
   constexpr int MPK = 16 / NQ;                     // prep elements per second-product step
   constexpr float TAU = 8.f;                       // lazy-max threshold (p ≤ 2^TAU)

@@ -1,0 +1,115 @@
+"""BASELINE configs[4] (C5) on the GPU at its shape: 10M + 10M items (a 20,000,001-row table), d = 512,
+L = 100 — the two HBM-bound kernels of the bench's C5 roofline line (bench.py run_c5) checked on a table of
+the full size, through the product's autograd functions: the GCN forward (models/encoders.py:42-48,
+H = (E + A·E)/2) and its backward through Aᵀ (K1), the five embedding gathers (models/C2DSR.py:65-71 +
+encoders.py:30, K2) and their deterministic segment-sum backward into the table (direct lookups, pad row
+excluded) and into the GCN output (then through Aᵀ).  Every full-size output is compared on sampled rows
+against fp64 host computations from the same inputs (a float64 restatement of the same op — the oracle of
+this property test); dropout 0.  ~170 GB of device memory."""
+import math
+import random
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_c5_gcn_and_embedding_at_20m_rows():
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import ops, synth
+    from c2dsr_amd.models.encoders import GCN, StepState
+    n_a = n_b = 10_000_000
+    d, L, B = 512, 100, 256
+    N = n_a + n_b + 1
+    pad = N - 1
+    items, off = synth.make_flat_sequences(200_000, n_a, n_b, L, seed=1)
+    seq_id = np.repeat(np.arange(off.size - 1, dtype=np.int64), np.diff(off))
+    same = seq_id[1:] == seq_id[:-1]
+    g = GR.normalized_csr(np.stack([items[:-1][same], items[1:][same]], 1), N)
+    seqs = [items[off[i]:off[i + 1]].tolist() for i in range(2 * B)]
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, n_a, n_b, L))
+    assert rows[0].shape[0] >= B
+    hb = [r[:B] for r in rows]
+    dg = GR.DeviceGraph(g, DEV)
+    b = [torch.from_numpy(r.copy()).to(DEV) for r in hb]
+    pass_idx = [(0, 3), (1, 4), (2, 5), (12, 3), (13, 3)]  # (seq, pos) of the five passes
+    torch.manual_seed(0)
+    E = torch.nn.Parameter(torch.empty(N, d, device=DEV).normal_(0.0, 0.1))
+    E.grad = torch.zeros_like(E)
+    P = torch.nn.Parameter(torch.empty(L, d, device=DEV).normal_(0.0, 0.1))
+    P.grad = torch.zeros_like(P)
+    state = StepState(seed=1)
+    state.step = 1
+    gcn = GCN(SimpleNamespace(dropout_gnn=0.0, n_gnn=1, idx_pad=pad))
+    gcn.state = state
+    H, tok, sink = gcn.propagate(E, dg)
+    scale = math.sqrt(d)
+    xs = [ops.EmbedFn.apply(tok, E, P, b[s], b[p], H, scale, 0.0, (0, 0), 0, sink, pad) for s, p in pass_idx]
+    gx = torch.empty(B, L, d, device=DEV).normal_(0.0, 1.0)
+    # forward checks before the backward (the table is unchanged by it; H is consumed by nothing else)
+    rng = np.random.default_rng(0)
+    r, c, v = g.coo()
+    batch_items = np.unique(np.concatenate([hb[s].reshape(-1) for s, _ in pass_idx]))
+    batch_items = batch_items[batch_items != pad]
+    has_out = np.flatnonzero(np.diff(g.rowptr) > 0)
+    h_rows = np.unique(np.concatenate([rng.choice(batch_items, 300, replace=False), rng.choice(has_out, 300)]))
+    sel = np.isin(r, h_rows)
+    need = np.unique(np.concatenate([h_rows, c[sel]]))
+    Eh = dict(zip(need.tolist(), E.detach()[torch.from_numpy(need).to(DEV)].double().cpu().numpy()))
+    Hg = H[torch.from_numpy(h_rows).to(DEV)].double().cpu().numpy()
+    ref = np.stack([Eh[i] for i in h_rows.tolist()])
+    acc = np.zeros_like(ref)
+    pos_of = {i: k for k, i in enumerate(h_rows.tolist())}
+    for rr, cc, vv in zip(r[sel], c[sel], v[sel]):
+        acc[pos_of[int(rr)]] += float(vv) * Eh[int(cc)]
+    assert rel(Hg, (ref + acc) / 2) < 1e-5, 'GCN forward (sampled rows)'
+    Ph = P.detach().double().cpu().numpy()
+    for k, (s, p) in enumerate(pass_idx):
+        rr = rng.choice(B * L, 400, replace=False)
+        it = hb[s].reshape(-1)[rr]
+        ps = hb[p].reshape(-1)[rr]
+        Hi = H[torch.from_numpy(it).to(DEV)].double().cpu().numpy()
+        Ei = E.detach()[torch.from_numpy(it).to(DEV)].double().cpu().numpy()
+        got = xs[k].detach().reshape(B * L, d)[torch.from_numpy(rr).to(DEV)].double().cpu().numpy()
+        assert rel(got, (Hi + Ei) * scale + Ph[ps]) < 1e-5, f'embedding forward, pass {k}'
+    torch.autograd.backward(xs, [gx] * len(xs))
+    torch.cuda.synchronize()
+    # host fp64: S_i = Σ over passes and rows with seq = i of gx (per distinct item of the batch)
+    G = gx.double().cpu().numpy().reshape(B * L, d)
+    uniq = np.unique(np.concatenate([hb[s].reshape(-1) for s, _ in pass_idx]))
+    S = np.zeros((uniq.size, d))
+    Pref = np.zeros((L, d))
+    for s, p in pass_idx:
+        np.add.at(S, np.searchsorted(uniq, hb[s].reshape(-1)), G)
+        np.add.at(Pref, hb[p].reshape(-1), G)
+    assert rel(P.grad.double().cpu().numpy(), Pref) < 1e-5, 'position-table gradient'
+    # E.grad[i] = √d·S_i (direct lookups, i != pad) + (√d·S_i + Σ_j A[j, i]·√d·S_j) / 2 (the lookups of H)
+    gt = g.transpose()
+    has_in = np.flatnonzero(np.diff(gt.rowptr) > 0)
+    e_rows = np.unique(np.concatenate([rng.choice(batch_items, 300, replace=False), rng.choice(has_in, 300),
+                                       [pad]]))
+    Sd = {int(i): S[k] * scale for k, i in enumerate(uniq.tolist())}
+    zero = np.zeros(d)
+    want = []
+    for i in e_rows.tolist():
+        t = Sd.get(i, zero).copy()
+        for e in range(gt.rowptr[i], gt.rowptr[i + 1]):
+            t += float(gt.val[e]) * Sd.get(int(gt.col[e]), zero)
+        w = t / 2
+        if i != pad:
+            w = w + Sd.get(i, zero)
+        want.append(w)
+    got = E.grad[torch.from_numpy(e_rows).to(DEV)].double().cpu().numpy()
+    assert rel(got, np.stack(want)) < 1e-5, 'table gradient (direct lookups + GCN backward through A^T)'

@@ -277,6 +277,45 @@ def test_fp32_step_d256_matches_oracle():
 FULL = {'C3_mb': (36845, 63937, 2048), 'C2_fk': (29207, 34886, 1024)}
 
 
+def loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, tol_loss, tol_grad):
+    """The fused loss head of the HIP step (classifier heads + CE, discriminators) against the oracle's loss
+    head (torch fp32 on the device) evaluated on the HIP encoder outputs of the same step: the three losses
+    (relative tol_loss) and the head parameters' gradients (tol_grad of max-abs).  P: the parameters before
+    the step; box: capture(tr) of the step."""
+    from c2dsr_amd import dropout as DK
+    from oracle import c2dsr_oracle as O
+    L, d = c['len_max'], c['d_latent']
+
+    def full(key, got):
+        # a row-subset output holds only the rows the loss reads; the others do not enter the loss
+        pid = {'h_share': DK.PASS_SHARE, 'hx': DK.PASS_A, 'hy': DK.PASS_B, 'neg0': DK.PASS_NEG0,
+               'neg1': DK.PASS_NEG0 + 1}[key]
+        idx = box['need'].get(pid)
+        if idx is None:
+            return got.reshape(B, L, d).float()
+        out = torch.zeros(B * L, d, device=DEV)
+        out[idx.to(DEV)] = got.reshape(-1, d)
+        return out.reshape(B, L, d)
+
+    hs = [full(k, v).requires_grad_(False) for k, v in (('h_share', box['h_share']), ('hx', box['hx']),
+                                                         ('hy', box['hy']), ('neg0', box['neg'][0]),
+                                                         ('neg1', box['neg'][1]))]
+    names = ['classifier_a.weight', 'classifier_a.bias', 'classifier_b.weight', 'classifier_b.bias',
+             'classifier_pad.weight', 'classifier_pad.bias', 'D_a.weight', 'D_b.weight']
+    for n in names:
+        P[n].requires_grad_(True)
+    cfg = dict(n_item_a=c['n_a'], n_item_b=c['n_b'], len_rec=c['len_rec'], lambda_loss=0.7)
+    bd = tuple(x.to(DEV) for x in b)
+    out = O.loss_head(P, *hs, bd, cfg)
+    grads = torch.autograd.grad(out['loss'], [P[n] for n in names])
+    for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
+        e = abs(float(v.detach()) - float(out[k])) / abs(float(out[k]))
+        assert e < tol_loss, (k, float(v), float(out[k]), e)
+    for n, g in zip(names, grads):
+        e = rel(box['grads'][n], g)
+        assert e < tol_grad, (n, e)
+
+
 @pytest.mark.parametrize('cfg', ['C3_mb', 'C2_fk'])
 @pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
 def test_bf16_full_size_loss_head_vs_fp32(compact, cfg):
@@ -314,36 +353,7 @@ def test_bf16_full_size_loss_head_vs_fp32(compact, cfg):
     assert all(math.isfinite(float(v.detach())) for v in (loss, loss_rec, loss_mi))
     assert bool(box['need']) == compact
 
-    L, d = c['len_max'], c['d_latent']
-
-    def full(key, got):
-        # a row-subset output holds only the rows the loss reads; the others do not enter the loss
-        pid = {'h_share': DK.PASS_SHARE, 'hx': DK.PASS_A, 'hy': DK.PASS_B, 'neg0': DK.PASS_NEG0,
-               'neg1': DK.PASS_NEG0 + 1}[key]
-        idx = box['need'].get(pid)
-        if idx is None:
-            return got.reshape(B, L, d).float()
-        out = torch.zeros(B * L, d, device=DEV)
-        out[idx.to(DEV)] = got.reshape(-1, d)
-        return out.reshape(B, L, d)
-
-    hs = [full(k, v).requires_grad_(False) for k, v in (('h_share', box['h_share']), ('hx', box['hx']),
-                                                         ('hy', box['hy']), ('neg0', box['neg'][0]),
-                                                         ('neg1', box['neg'][1]))]
-    names = ['classifier_a.weight', 'classifier_a.bias', 'classifier_b.weight', 'classifier_b.bias',
-             'classifier_pad.weight', 'classifier_pad.bias', 'D_a.weight', 'D_b.weight']
-    for n in names:
-        P[n].requires_grad_(True)
-    cfg = dict(n_item_a=c['n_a'], n_item_b=c['n_b'], len_rec=c['len_rec'], lambda_loss=0.7)
-    bd = tuple(x.to(DEV) for x in b)
-    out = O.loss_head(P, *hs, bd, cfg)
-    grads = torch.autograd.grad(out['loss'], [P[n] for n in names])
-    for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
-        e = abs(float(v.detach()) - float(out[k])) / abs(float(out[k]))
-        assert e < 2e-3, (k, float(v), float(out[k]), e)
-    for n, g in zip(names, grads):
-        e = rel(box['grads'][n], g)
-        assert e < BF16_GRAD, (n, e)
+    loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, 2e-3, BF16_GRAD)
 
 
 def test_c1_food_kitchen_shape_fp32_vs_oracle():
@@ -469,30 +479,31 @@ C4 = dict(n_a=8367, n_b=11404, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_
           norm_first=False, d_bias=False, shared_item_embed=False)
 
 
-def _c4_case(precision):
+def _c4_case(precision, B):
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
     from c2dsr_amd import synth
     import random
     c = C4
-    seqs = synth.make_sequences(600, c['n_a'], c['n_b'], c['len_max'], seed=5, n_min=6)
+    seqs = synth.make_sequences(max(600, 2 * B + 400), c['n_a'], c['n_b'], c['len_max'], seed=5, n_min=6)
     random.seed(3407)
     rows = DL.to_arrays(DL.preprocess_train(seqs, c['n_a'], c['n_b'], c['len_max']))
+    assert rows[0].shape[0] >= B
     gs, gp = GR.preprocess_graph(seqs, c['n_a'], c['n_a'] + c['n_b'] + 1)
     args = make_args(c, dropout=0.2, precision=precision, seed=11)
-    args.batch_size = 256
+    args.batch_size = B
     torch.manual_seed(0)
     tr = build_trainer(args, gs, gp)
-    return tr, tuple(torch.from_numpy(r[:256].copy()) for r in rows)
+    return tr, tuple(torch.from_numpy(r[:B].copy()) for r in rows)
 
 
-def _c4_worker(rank, world, port, precision, out_dir):
+def _c4_worker(rank, world, port, precision, B, out_dir):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        tr, b = _c4_case(precision)
+        tr, b = _c4_case(precision, B)
         assert tr.world == world and tr.dp_split
         tr.model.train()
         tr.optimizer.zero_grad()
@@ -508,26 +519,33 @@ def _c4_worker(rank, world, port, precision, out_dir):
 
 
 @pytest.mark.parametrize('precision', ['fp32', 'bf16'])
-def test_c4_ee_shape_dp_split_world2_equals_single_device(tmp_path, precision):
-    """BASELINE configs[3] (C4) shape: Entertainment-Education item counts, d=256, L=50, one global batch
-    split over two data-parallel ranks (dp_split, rows [r·B/2, (r+1)·B/2), global-count normalisation, the
-    gradient exchange of c2dsr_amd/dp.py; two ranks on cuda:0 over gloo) against the same global batch on
-    one device: the loss and every gradient agree to the summation-order level."""
+def test_c4_ee_b4096_dp_split_world2_equals_single_device(tmp_path, precision):
+    """BASELINE configs[3] (C4) at its workload: Entertainment-Education item counts, d=256, L=50, the global
+    batch B=4096 split over two data-parallel ranks (dp_split, rows [r·B/2, (r+1)·B/2), global-count
+    normalisation, the gradient exchange of c2dsr_amd/dp.py; two ranks on cuda:0 over gloo) against the same
+    global batch on one device — the loss and every gradient agree to the summation-order level — and the
+    single device's loss head against the oracle's loss head on its encoder outputs (fp32: 1e-4)."""
     import socket
     import torch.multiprocessing as mp
+    B = 4096
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
         port = s.getsockname()[1]
-    mp.spawn(_c4_worker, args=(2, port, precision, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_c4_worker, args=(2, port, precision, B, str(tmp_path)), nprocs=2, join=True)
     got = np.load(tmp_path / 'c4.npz')
-    tr, b = _c4_case(precision)
+    tr, b = _c4_case(precision, B)
+    P = {n: p.detach().clone() for n, p in tr.model.named_parameters()}
     tr.model.train()
     tr.optimizer.zero_grad()
     box = capture(tr)
     tr.model.convolve_graph()
-    loss, _, _ = tr.train_batch(b)
+    loss, loss_rec, loss_mi = tr.train_batch(b)
     torch.cuda.synchronize()
     assert abs(float(got['loss']) - float(loss)) <= 1e-5 * abs(float(loss))
     tol = 1e-4 if precision == 'fp32' else 2e-3
     for n, g in box['grads'].items():
         assert rel(got[f'g/{n}'], g) < tol, n
+    if precision == 'fp32':
+        loss_head_vs_oracle(tr, box, b, C4, B, loss, loss_rec, loss_mi, P, TOL, TOL)
+    else:
+        loss_head_vs_oracle(tr, box, b, C4, B, loss, loss_rec, loss_mi, P, 2e-3, BF16_GRAD)

@@ -375,14 +375,100 @@ def gen_fk(ref):
     print(f'[fk] trainlike={arr.shape} eval={len(ev)} nnz={out["share_nnz"]}/{out["specific_nnz"]}')
 
 
+FK_EPOCHS = 2
+
+
+def gen_fk_trajectory(ref):
+    """north_star's metric reproduction on Food-Kitchen: main.py's loop (main.py:88-148)
+    through the reference's own Trainer on the FK stand-in — the only FK interaction files present are
+    data/raw/Food-Kitchen/val.txt and test_new.txt (train_new.txt is a missing blob), so
+    train := val.txt and val := test := test_new.txt — at BASELINE configs[0] (C1: d=64, L=15 as main.py
+    forces for FK, B=128, R=10, 999 sampled negatives), dropout 0, num_workers 0, FK_EPOCHS epochs.
+    Writes tests/golden/fk_raw.npz (the four raw input files as bytes) and traj_fk.npz: per-step losses,
+    per-epoch train losses, the shuffled batch order, val/test ranks, cal_metrics and cal_score."""
+    ref_dl, ref_model, ref_trainer, ref_graph, ref_metrics = ref
+    src = os.path.join(REF, 'data/raw/Food-Kitchen')
+    tmp = tempfile.mkdtemp(prefix='c2dsr_fktraj_')
+    path_raw = os.path.join(tmp, 'raw')
+    path_data = os.path.join(tmp, 'data')
+    os.makedirs(path_raw)
+    os.makedirs(path_data)
+    files = {'train_new.txt': 'val.txt', 'val_new.txt': 'test_new.txt', 'test_new.txt': 'test_new.txt',
+             'items_a.txt': 'items_a.txt', 'items_b.txt': 'items_b.txt'}
+    raw = {}
+    for dst, f in files.items():
+        data = open(os.path.join(src, f), 'rb').read()
+        open(os.path.join(path_raw, dst), 'wb').write(data)
+        raw[f] = np.frombuffer(data, dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, 'fk_raw.npz'), **{k.replace('.', '_'): v for k, v in raw.items()})
+    cfg = dict(n_a=29207, n_b=34886, len_max=15, len_rec=10, d_latent=64, n_gnn=1, n_attn=1, n_head=1,
+               norm_first=False, d_bias=False, shared_item_embed=False)
+    args = make_args(cfg, path_raw, path_data)
+    args.dataset = 'Food-Kitchen'
+    args.batch_size = 128
+    args.batch_size_eval = 2048
+    args.n_neg_sample = 999
+    bench = [0.1124, 0.0865, 0.0574, 0.0416]  # utils/constant.py:14
+    random.seed(3407)
+    torch.manual_seed(3407)
+    np.random.seed(3407)
+    noter = _Noter()
+    tr = ref_trainer.Trainer(args, noter)
+    sched = torch.optim.lr_scheduler.StepLR(tr.optimizer, step_size=args.lr_step, gamma=args.lr_gamma)
+    out = {'n_epoch': np.int64(FK_EPOCHS)}
+    steps = []
+    tb_orig = tr.train_batch
+
+    def tb(batch):
+        r = tb_orig(batch)
+        steps.append([float(x) for x in r])
+        return r
+
+    tr.train_batch = tb
+    loader = tr.trainloader
+
+    class _Rec:
+        def __init__(self, order):
+            self.order = order
+            self.dataset = loader.dataset
+
+        def __iter__(self):
+            for b in loader:
+                self.order.append(b[0].numpy().copy())
+                yield b
+
+    for e in range(FK_EPOCHS):
+        order = []
+        tr.trainloader = _Rec(order)
+        va, vb = tr.run_epoch()
+        sched.step()
+        ta, tb_ = tr.run_test()
+        out[f'e{e}/order_seq_share'] = np.concatenate(order)
+        out[f'e{e}/loss'] = np.asarray(noter.train[-1], dtype=np.float64)
+        out[f'e{e}/step_losses'] = np.asarray(steps, dtype=np.float64)
+        steps.clear()
+        for k, v in (('val_a', va), ('val_b', vb), ('test_a', ta), ('test_b', tb_)):
+            out[f'e{e}/{k}'] = np.asarray(v, dtype=np.int64)
+            out[f'e{e}/{k}_metrics'] = np.asarray(ref_metrics.cal_metrics(v), dtype=np.float64)
+        out[f'e{e}/val_score'] = np.asarray(ref_metrics.cal_score(va, vb, bench), dtype=np.float64)
+        out[f'e{e}/test_score'] = np.asarray(ref_metrics.cal_score(ta, tb_, bench), dtype=np.float64)
+        print(f'[fk traj] epoch {e}: loss {out[f"e{e}/loss"]} test score {out[f"e{e}/test_score"]}', flush=True)
+    np.savez_compressed(os.path.join(OUT, 'traj_fk.npz'), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--only', default='')
     ap.add_argument('--traj', action='store_true', help='only the epoch trajectories')
+    ap.add_argument('--fk-traj', action='store_true', help='only the Food-Kitchen metric trajectory')
     opt = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
     ref = ref_import()
+    if opt.fk_traj:
+        torch.set_num_threads(8)
+        gen_fk_trajectory(ref)
+        return
     if opt.traj:
         for name in ('base', 'var'):
             gen_trajectory(name, CONFIGS[name], ref)
