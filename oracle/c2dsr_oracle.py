@@ -23,6 +23,14 @@ Reference semantics restated (file:line in /root/reference):
   * evaluate_batch      trainer.py:162-181        (rank vs sampled negatives, ties not counted)
   * cal_metrics/score   utils/metrics.py:4-31     (HR/MRR/NDCG@{5,20}, improvement over benchmark)
 
+bf16 emulation (``cfg['bf16']``; the checker of the HIP path's bf16 mode, not a restatement of the
+reference): every product the bf16 mode runs on bf16 MFMA operands rounds the same operands at the same
+points — the projections (rgemm / wgemm: bf16(x)·bf16(W)ᵀ forward, bf16(dy)·bf16(W) and bf16(dy)ᵀ·bf16(x)
+backward, fp32 accumulate, bias sums fp32), the bilinear U = bf16(X2)·bf16(W)ᵀ, and the classifier heads
+(ce.hip: logits over bf16(H)·bf16(W)ᵀ, the target and pad logits exact fp32, the softmax parts of dH / dW
+over bf16 operands and bf16(softmax·w), the one-hot parts exact).  Attention, LayerNorm, embedding and GCN
+stay fp32 in both.
+
 Dropout: the reference draws torch-CPU masks that no GPU RNG can reproduce, so
 parity against the reference uses p = 0.  For p > 0 the GPU kernels use a
 counter-based hash mask; :func:`keep_mask` restates that hash so the oracle
@@ -105,6 +113,68 @@ class Dropper:
         return torch.from_numpy(keep.reshape(shape).astype(np.float32) / np.float32(1.0 - p))
 
 
+# ----------------------------------------------------------------------------- bf16 emulation
+def _b(x):
+    """round to bf16 (RNE) and back"""
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+class B16Linear(torch.autograd.Function):
+    """x·Wᵀ on bf16-rounded operands with fp32 accumulation, and the backward products on bf16-rounded
+    operands too (the bf16 mode's rg / wg kernels, csrc/rgemm.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, W):
+        ctx.save_for_backward(x, W)
+        return _b(x) @ _b(W).T
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        gb = _b(g)
+        N, K = W.shape
+        return gb @ _b(W), gb.reshape(-1, N).T @ _b(x).reshape(-1, K)
+
+
+def linear(x, W, b, cfg):
+    """nn.Linear: plain fp32, or the bf16 mode's products (cfg['bf16'])."""
+    y = B16Linear.apply(x, W) if cfg.get('bf16') else x @ W.T
+    return y + b if b is not None else y
+
+
+class B16CERows(torch.autograd.Function):
+    """Per-row cross-entropy terms of one stacked head in the bf16 mode (csrc/ce.hip): lse over the logits
+    bf16(H)·bf16(W)ᵀ + b and the fp32 pad logit, minus the target logit taken in fp32 (0 on ignored rows).
+    Backward with row weights g: dH = bf16(softmax·g)[:, :n]·bf16(W) − g·W[t], dW = bf16(softmax·g)ᵀ·bf16(H)
+    − Σ g·H (one-hot parts exact), db and the pad logit's gradient from the fp32 softmax."""
+
+    @staticmethod
+    def forward(ctx, H, W, b, pl, t, ignore):
+        n = W.shape[0]
+        full = torch.cat([_b(H) @ _b(W).T + b, pl[:, None]], 1)
+        lse = torch.logsumexp(full, 1)
+        valid = t != ignore
+        tc = torch.clamp(t, max=n - 1)
+        s_t = torch.where(t < n, (H * W[tc]).sum(-1) + b[tc], pl)
+        ctx.save_for_backward(H, W, torch.softmax(full, 1), t, valid)
+        return torch.where(valid, lse - s_t, torch.zeros_like(lse))
+
+    @staticmethod
+    def backward(ctx, g):
+        H, W, Pm, t, valid = ctx.saved_tensors
+        n = W.shape[0]
+        rw = torch.where(valid, g, torch.zeros_like(g))
+        Ps = Pm * rw[:, None]
+        on = valid & (t < n)
+        tc = torch.clamp(t, max=n - 1)
+        oh = torch.zeros(H.shape[0], n, dtype=H.dtype, device=H.device)
+        oh[on, tc[on]] = rw[on]
+        dH = _b(Ps[:, :n]) @ _b(W) - oh @ W
+        dW = _b(Ps[:, :n]).T @ _b(H) - oh.T @ H
+        db = Ps[:, :n].sum(0) - oh.sum(0)
+        return dH, dW, db, Ps[:, n], None, None
+
+
 # ----------------------------------------------------------------------------- model pieces
 def spmm_coo(row: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n: int, h: torch.Tensor) -> torch.Tensor:
     out = torch.zeros(n, h.shape[1], dtype=h.dtype)
@@ -131,12 +201,13 @@ def layer_norm(x, w, b, eps=1e-8):
     return (x - mu) / torch.sqrt(var + eps) * w + b
 
 
-def attention(x, P, pre, seq, idx_pad, n_head, p, dropper, pass_id, layer):
+def attention(x, P, pre, seq, idx_pad, n_head, p, dropper, pass_id, layer, cfg=None):
     """nn.MultiheadAttention → F.multi_head_attention_forward → SDPA (math), with the
     causal float mask + inverted bool kpm merged additively (functional.py mask merge)."""
+    cfg = cfg or {}
     B, L, d = x.shape
     dh = d // n_head
-    qkv = x @ P[pre + 'self_attn.in_proj_weight'].T + P[pre + 'self_attn.in_proj_bias']
+    qkv = linear(x, P[pre + 'self_attn.in_proj_weight'], P[pre + 'self_attn.in_proj_bias'], cfg)
     q, k, v = qkv.split(d, dim=-1)
     q = q.reshape(B, L, n_head, dh).transpose(1, 2)
     k = k.reshape(B, L, n_head, dh).transpose(1, 2)
@@ -153,18 +224,19 @@ def attention(x, P, pre, seq, idx_pad, n_head, p, dropper, pass_id, layer):
     if m is not None:
         a = a * m
     o = (a @ v).transpose(1, 2).reshape(B, L, d)
-    out = o @ P[pre + 'self_attn.out_proj.weight'].T + P[pre + 'self_attn.out_proj.bias']
+    out = linear(o, P[pre + 'self_attn.out_proj.weight'], P[pre + 'self_attn.out_proj.bias'], cfg)
     m = dropper.mask((B, L, d), site_enc(pass_id, layer, 2), p, row_dim_prod=L * d)
     return out * m if m is not None else out
 
 
-def feed_forward(x, P, pre, p, dropper, pass_id, layer):
+def feed_forward(x, P, pre, p, dropper, pass_id, layer, cfg=None):
+    cfg = cfg or {}
     B, L, d = x.shape
-    f = torch.relu(x @ P[pre + 'linear1.weight'].T + P[pre + 'linear1.bias'])
+    f = torch.relu(linear(x, P[pre + 'linear1.weight'], P[pre + 'linear1.bias'], cfg))
     m = dropper.mask(tuple(f.shape), site_enc(pass_id, layer, 3), p, row_dim_prod=L * f.shape[-1])
     if m is not None:
         f = f * m
-    out = f @ P[pre + 'linear2.weight'].T + P[pre + 'linear2.bias']
+    out = linear(f, P[pre + 'linear2.weight'], P[pre + 'linear2.bias'], cfg)
     m = dropper.mask((B, L, d), site_enc(pass_id, layer, 4), p, row_dim_prod=L * d)
     return out * m if m is not None else out
 
@@ -181,13 +253,14 @@ def self_attention(P, mod, seq, x, pos, cfg, dropper, pass_id):
         pre = f'{mod}.encoder.layers.{l}.'
         if cfg['norm_first']:
             x = x + attention(layer_norm(x, P[pre + 'norm1.weight'], P[pre + 'norm1.bias']), P, pre, seq,
-                              cfg['idx_pad'], cfg['n_head'], p, dropper, pass_id, l)
+                              cfg['idx_pad'], cfg['n_head'], p, dropper, pass_id, l, cfg)
             x = x + feed_forward(layer_norm(x, P[pre + 'norm2.weight'], P[pre + 'norm2.bias']), P, pre, p,
-                                 dropper, pass_id, l)
+                                 dropper, pass_id, l, cfg)
         else:
-            x = layer_norm(x + attention(x, P, pre, seq, cfg['idx_pad'], cfg['n_head'], p, dropper, pass_id, l),
+            x = layer_norm(x + attention(x, P, pre, seq, cfg['idx_pad'], cfg['n_head'], p, dropper, pass_id, l,
+                                         cfg),
                            P[pre + 'norm1.weight'], P[pre + 'norm1.bias'])
-            x = layer_norm(x + feed_forward(x, P, pre, p, dropper, pass_id, l),
+            x = layer_norm(x + feed_forward(x, P, pre, p, dropper, pass_id, l, cfg),
                            P[pre + 'norm2.weight'], P[pre + 'norm2.bias'])
     return layer_norm(x, P[mod + '.encoder.norm.weight'], P[mod + '.encoder.norm.bias'])
 
@@ -217,8 +290,11 @@ def encode(P, H, ename, mod, seq, pos, cfg, dropper, pass_id):
     return self_attention(P, mod, seq, x, pos, cfg, dropper, pass_id)
 
 
-def bilinear(x1, x2, W, b):
-    out = torch.einsum('bi,oij,bj->bo', x1, W, x2)
+def bilinear(x1, x2, W, b, cfg=None):
+    if cfg is not None and cfg.get('bf16'):  # U = bf16(x2)·bf16(W)ᵀ (rgemm), s = x1·U in fp32
+        out = (x1 * B16Linear.apply(x2, W[0])).sum(-1, keepdim=True)
+    else:
+        out = torch.einsum('bi,oij,bj->bo', x1, W, x2)
     return out + b if b is not None else out
 
 
@@ -229,6 +305,8 @@ def bce_logits(s, y, denom=None):
 
 def cross_entropy(logits, tgt, ignore, denom=None):
     valid = tgt != ignore
+    if hasattr(logits, 'rows'):  # bf16 emulation: per-row terms from B16CERows
+        return logits.rows.sum() / (valid.sum() if denom is None else denom)
     lse = torch.logsumexp(logits, -1)
     t = torch.where(valid, tgt, torch.zeros_like(tgt))
     picked = logits.gather(1, t[:, None])[:, 0]
@@ -281,10 +359,10 @@ def loss_head(P, h_share, hx, hy, h_neg_a, h_neg_b, batch, cfg, counts=None):
     hy_mean = (hy * wb).sum(1)
     Da_b = P.get('D_a.bias')
     Db_b = P.get('D_b.bias')
-    sim_a_pos = bilinear(hx_mean, (h_share * wb).sum(1), P['D_a.weight'], Da_b)
-    sim_a_neg = bilinear(hx_mean, (h_neg_a * wa).sum(1), P['D_a.weight'], Da_b)
-    sim_b_pos = bilinear(hy_mean, (h_share * wa).sum(1), P['D_b.weight'], Db_b)
-    sim_b_neg = bilinear(hy_mean, (h_neg_b * wb).sum(1), P['D_b.weight'], Db_b)
+    sim_a_pos = bilinear(hx_mean, (h_share * wb).sum(1), P['D_a.weight'], Da_b, cfg)
+    sim_a_neg = bilinear(hx_mean, (h_neg_a * wa).sum(1), P['D_a.weight'], Da_b, cfg)
+    sim_b_pos = bilinear(hy_mean, (h_share * wa).sum(1), P['D_b.weight'], Db_b, cfg)
+    sim_b_neg = bilinear(hy_mean, (h_neg_b * wb).sum(1), P['D_b.weight'], Db_b, cfg)
     out['sim_a'] = torch.stack([sim_a_pos, sim_a_neg])
     out['sim_b'] = torch.stack([sim_b_pos, sim_b_neg])
     one = torch.ones(B, 1, device=hx.device)
@@ -295,18 +373,32 @@ def loss_head(P, h_share, hx, hy, h_neg_a, h_neg_b, batch, cfg, counts=None):
 
     hs_r, ha_r, hb_r = h_share[:, -R:], hx[:, -R:], hy[:, -R:]
 
-    def head(h, W, bias, hpad):
-        lg = h @ W.T + bias
-        pad = hpad @ P['classifier_pad.weight'].T + P['classifier_pad.bias']
-        return torch.cat([lg, pad], -1)
-
     Wa, ba, Wb, bb = P['classifier_a.weight'], P['classifier_a.bias'], P['classifier_b.weight'], P['classifier_b.bias']
-    s_sa = head(hs_r, Wa, ba, hs_r).reshape(-1, n_a + 1)
-    s_sb = head(hs_r, Wb, bb, hs_r).reshape(-1, n_b + 1)
-    s_a = head(hs_r + ha_r, Wa, ba, ha_r).reshape(-1, n_a + 1)
-    s_b = head(hs_r + hb_r, Wb, bb, hb_r).reshape(-1, n_b + 1)
     t_sa, t_sb = gt_sa[:, -R:].reshape(-1), gt_sb[:, -R:].reshape(-1)
     t_a, t_b = gt_a[:, -R:].reshape(-1), gt_b[:, -R:].reshape(-1)
+
+    def pad_logit(hpad):
+        return hpad @ P['classifier_pad.weight'].T + P['classifier_pad.bias']
+
+    if cfg.get('bf16'):  # the fused bf16 heads (csrc/ce.hip): per-row terms, means taken below
+        d = h_share.shape[-1]
+
+        class _Rows:
+            def __init__(self, h, W, bias, hpad, t, ignore):
+                self.rows = B16CERows.apply(h.reshape(-1, d), W, bias, pad_logit(hpad).reshape(-1), t, ignore)
+
+        s_sa = _Rows(hs_r, Wa, ba, hs_r, t_sa, n_a)
+        s_sb = _Rows(hs_r, Wb, bb, hs_r, t_sb, n_b)
+        s_a = _Rows(hs_r + ha_r, Wa, ba, ha_r, t_a, n_a)
+        s_b = _Rows(hs_r + hb_r, Wb, bb, hb_r, t_b, n_b)
+    else:
+        def head(h, W, bias, hpad):
+            return torch.cat([h @ W.T + bias, pad_logit(hpad)], -1)
+
+        s_sa = head(hs_r, Wa, ba, hs_r).reshape(-1, n_a + 1)
+        s_sb = head(hs_r, Wb, bb, hs_r).reshape(-1, n_b + 1)
+        s_a = head(hs_r + ha_r, Wa, ba, ha_r).reshape(-1, n_a + 1)
+        s_b = head(hs_r + hb_r, Wb, bb, hb_r).reshape(-1, n_b + 1)
     if counts is None:
         l_sa = cross_entropy(s_sa, t_sa, n_a)
         l_sb = cross_entropy(s_sb, t_sb, n_b)

@@ -375,6 +375,86 @@ def gen_fk(ref):
     print(f'[fk] trainlike={arr.shape} eval={len(ev)} nnz={out["share_nnz"]}/{out["specific_nnz"]}')
 
 
+D256 = dict(n_a=300, n_b=400, len_max=50, len_rec=10, d_latent=256, n_train=40, n_eval=8,
+            n_gnn=1, n_attn=1, n_head=1, norm_first=False, d_bias=False, shared_item_embed=False)
+
+
+def sample_idx(n):
+    """the elements of a flattened tensor a d=256 fixture keeps (≤ ~4k, evenly strided)"""
+    return np.arange(0, n, max(1, n // 4096), dtype=np.int64)
+
+
+def gen_d256(ref):
+    """The benchmarked shape (d=256, L=50, R=10) pinned by the reference itself at small
+    item counts: one train_batch (dropout 0) of the reference Trainer on a synthetic raw set.  The model's
+    initial parameters are not stored — torch.manual_seed(1234) before C2DSR(...) reproduces them bit for
+    bit in c2dsr_amd (checked for the d=16 configs, tests/test_model_surface.py) — and the large tensors are
+    kept on an even sample of their elements (sample_idx) with their full max-abs, so the fixture stays small.
+    Writes tests/golden/model_d256.npz (+ the processed train lists and the graph COO)."""
+    ref_dl, ref_model, ref_trainer, ref_graph, ref_metrics = ref
+    cfg = D256
+    tmp = tempfile.mkdtemp(prefix='c2dsr_fx_d256_')
+    path_raw = os.path.join(tmp, 'raw')
+    path_data = os.path.join(tmp, 'data')
+    os.makedirs(path_data)
+    synth.make_dataset(path_raw, cfg['n_a'], cfg['n_b'], cfg['len_max'], cfg['n_train'], cfg['n_eval'],
+                       seed=17, ties=True, n_min=20)
+    args = make_args(cfg, path_raw, path_data)
+    random.seed(3407)
+    torch.manual_seed(3407)
+    np.random.seed(3407)
+    ds_tr = ref_dl.CDSRDataset(args, 'train')
+    out = lists_to_arrays(ds_tr.data, 'train')
+    adj_s, adj_p = ref_graph.preprocess_graph(args, os.path.join(path_raw, 'train_new.txt'))
+    for k, adj in (('share', adj_s), ('specific', adj_p)):
+        idx = adj._indices().numpy()
+        out[f'{k}_row'] = idx[0].astype(np.int64)
+        out[f'{k}_col'] = idx[1].astype(np.int64)
+        out[f'{k}_val'] = adj._values().numpy().astype(np.float32)
+    torch.manual_seed(1234)
+    model = ref_model.C2DSR(args, adj_s, adj_p)
+    tr = ref_trainer.Trainer.__new__(ref_trainer.Trainer)
+    tr.model = model
+    tr.optimizer = torch.optim.AdamW(filter(lambda x: x.requires_grad, model.parameters()), lr=args.lr,
+                                     weight_decay=args.l2, amsgrad=True)
+    tr.device, tr.d_latent, tr.n_item_a, tr.n_item_b = args.device, args.d_latent, args.n_item_a, args.n_item_b
+    tr.len_rec, tr.lambda_loss = args.len_rec, args.lambda_loss
+    tr.label_pos = torch.ones(args.batch_size, 1)
+    tr.label_neg = torch.zeros(args.batch_size, 1)
+    cap = {}
+    hooks = [getattr(model, nm).register_forward_hook(
+        (lambda nm: lambda mod, inp, o: cap.setdefault(nm, []).append(o.detach().numpy().copy()))(nm))
+        for nm in ('gnn_share', 'gnn_a', 'gnn_b', 'attn_share', 'attn_a', 'attn_b')]
+    snap = {}
+    real_step = tr.optimizer.step
+
+    def step_wrapper(*a, **kw):
+        snap.update({n: p.grad.detach().numpy().copy() for n, p in model.named_parameters() if p.grad is not None})
+        return real_step(*a, **kw)
+
+    tr.optimizer.step = step_wrapper
+    tensors = [torch.LongTensor(np.stack([np.asarray(r[j]) for r in ds_tr.data])) for j in range(14)]
+    model.train()
+    tr.optimizer.zero_grad()
+    model.convolve_graph()
+    loss, loss_rec, loss_mi = tr.train_batch(tuple(t[:BATCH] for t in tensors))
+    for h in hooks:
+        h.remove()
+    out.update({'s0/loss': np.float64(loss.item()), 's0/loss_rec': np.float64(loss_rec.item()),
+                's0/loss_mi': np.float64(loss_mi.item()), 'batch_n': np.int64(BATCH)})
+    named = {'hi_share': cap['gnn_share'][0], 'hi_a': cap['gnn_a'][0], 'hi_b': cap['gnn_b'][0],
+             'h_share': cap['attn_share'][0], 'h_neg_a': cap['attn_share'][1], 'h_neg_b': cap['attn_share'][2],
+             'hx': cap['attn_a'][0], 'hy': cap['attn_b'][0]}
+    named.update({f'grad/{n}': g for n, g in snap.items()})
+    for k, v in named.items():
+        flat = v.reshape(-1).astype(np.float32)
+        out[f's0/{k}'] = flat[sample_idx(flat.size)]
+        out[f's0/{k}:maxabs'] = np.float64(np.abs(flat).max())
+        out[f's0/{k}:numel'] = np.int64(flat.size)
+    np.savez_compressed(os.path.join(OUT, 'model_d256.npz'), **out)
+    print(f'[d256] train={len(ds_tr.data)} loss={loss.item():.6f} tensors={len(named)}')
+
+
 FK_EPOCHS = 2
 
 
@@ -461,10 +541,14 @@ def main():
     ap.add_argument('--only', default='')
     ap.add_argument('--traj', action='store_true', help='only the epoch trajectories')
     ap.add_argument('--fk-traj', action='store_true', help='only the Food-Kitchen metric trajectory')
+    ap.add_argument('--d256', action='store_true', help='only the d=256 / L=50 / R=10 golden step')
     opt = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
     ref = ref_import()
+    if opt.d256:
+        gen_d256(ref)
+        return
     if opt.fk_traj:
         torch.set_num_threads(8)
         gen_fk_trajectory(ref)
