@@ -269,8 +269,10 @@ def test_bf16_step_d256_matches_oracle(compact):
 # bf16 mode vs the oracle's bf16 EMULATION (oracle/c2dsr_oracle.py: the same operands rounded at the same
 # points): what remains is fp32 accumulation order and the one rounding point the fused CE places differently
 # (the unnormalised softmax of the online dH sweep), so the composition is held to 5e-3 of each gradient's
-# max-abs (instead of 7e-2 against plain fp32), outputs and losses to 1e-3, post-step parameters to 5e-3.
-B16E_OUT, B16E_GRAD, B16E_PARAM = 1e-3, 5e-3, 5e-3
+# max-abs (instead of 7e-2 against plain fp32), outputs and losses to 1e-3.  Post-step parameters keep the
+# bf16 test's 2e-2: AdamW's first steps move every element by ≈ lr·sign(g), and the query/key rows of in_proj
+# carry rounding-level gradients (Q1: every query sees only PAD keys), whose signs neither side pins.
+B16E_OUT, B16E_GRAD, B16E_PARAM = 1e-3, 5e-3, 2e-2
 
 
 @pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
