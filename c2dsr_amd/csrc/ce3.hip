@@ -52,6 +52,17 @@ __device__ __forceinline__ bf16x8 lo_frag(const f32x16& a, int s, const bf16x8& 
   return r;
 }
 
+// the two half-waves hold the two halves of a row's columns: combine them with one v_permlane32_swap (no LDS
+// round trip): swap(x, x) returns (lower half broadcast, upper half broadcast)
+__device__ __forceinline__ float half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs, const bf16* __restrict__ Xw,
                                                      const float* __restrict__ svec, const float* __restrict__ wvec,
@@ -172,7 +183,19 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
         sc[i] = v;
         tm = fmaxf(tm, v);
       }
-      if constexpr (MODE == 0) mnext = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      if constexpr (MODE == 0) mnext = half_max(tm);
+    }
+    // fragment rings carried across the phase boundaries: the first DS row fragments of the next S phase are
+    // read during the last steps of the second product, the first DT transposed fragments of the second
+    // product during the last S steps — no LDS-latency bubble at either boundary
+    bf16x8 fa[DS + 2][2];
+    bf16x8 tf[DT + 2][2];
+    {
+      ImgOffsets oS;
+      offs_rows(1 % NB, oS);  // S(1) reads tile 1 (landed in the prologue)
+      [&]<int... P>(std::integer_sequence<int, P...>) {
+        ((fa[P][0] = row_frag_c<T3, 0, P, 0>(oS), fa[P][1] = row_frag_c<T3, 0, KS + P, 0>(oS)), ...);
+      }(std::make_integer_sequence<int, DS>{});
     }
     for (int t = 0; t < ntiles; ++t) {
       const int bh = t % NB, bs = (t + 1) % NB;
@@ -198,14 +221,10 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       ImgOffsets oS, oH;
       offs_rows(bs, oS);
       offs_tr(bh, oH);
-      // ---- S(t+1) ∥ epilogue(t): p = 2^(v − msub), packed into the hi / lo B fragments
+      // ---- S(t+1) ∥ epilogue(t): p = 2^(v − msub), packed into the hi / lo B fragments; the last DT steps
+      //      read the second product's first transposed fragments (tile t)
       f32x16 sn;
       bf16x8 xh[2], xl[2];
-      bf16x8 fa[DS + 2][2];
-      [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((fa[P][0] = row_frag_c<T3, 0, P, 0>(oS), fa[P][1] = row_frag_c<T3, 0, KS + P, 0>(oS)), ...);
-      }(std::make_integer_sequence<int, DS>{});
-      __builtin_amdgcn_sched_barrier(0);
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
@@ -213,6 +232,12 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
               if constexpr (ks + DS < KS) {
                 fa[(ks + DS) % (DS + 2)][0] = row_frag_c<T3, 0, ks + DS, 0>(oS);
                 fa[(ks + DS) % (DS + 2)][1] = row_frag_c<T3, 0, KS + ks + DS, 0>(oS);
+              } else {
+                constexpr int q1 = ks + DS - KS;  // 0 .. DS-1 → the second product's fragments q1 < DT
+                if constexpr (q1 < DT) {
+                  tf[q1][0] = tr_frag_c<T3, (q1 & 1) * 16, (q1 >> 1) * 32, 0>(oH);
+                  tf[q1][1] = tr_frag_c<T3, (q1 & 1) * 16, D + (q1 >> 1) * 32, 0>(oH);
+                }
               }
               const bf16x8& ah = fa[ks % (DS + 2)][0];
               const bf16x8& al = fa[ks % (DS + 2)][1];
@@ -238,18 +263,18 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
             }(),
             ...);
       }(std::make_integer_sequence<int, KS>{});
-      // ---- second product (t) ∥ prep of S(t+1) ∥ DMA of tile t+3:
+      // ---- tile t+2 (issued during the previous second product) has landed for every wave, and every wave
+      //      is past its reads of buffer (t+3) % NB (the previous second product): publish / reuse
+      dma_wait();
+      __syncthreads();
+      // ---- second product (t) ∥ prep of S(t+1) ∥ DMA of tile t+3; the last DS steps read the first row
+      //      fragments of S(t+2) (tile t+2, landed above)
       //      Oᵀ[k][s] += Σ_{c in tile} X_w[c][k]·P[c][s],  q = (kb = q >> 1, half st = q & 1)
+      ImgOffsets oN;
+      offs_rows((t + 2) % NB, oN);
       f32x4 c4n[4];
       wconst(bs, c4n);
       float tm = -INFINITY;
-      bf16x8 tf[DT + 2][2];
-      [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((tf[P][0] = tr_frag_c<T3, (P & 1) * 16, (P >> 1) * 32, 0>(oH),
-          tf[P][1] = tr_frag_c<T3, (P & 1) * 16, D + (P >> 1) * 32, 0>(oH)),
-         ...);
-      }(std::make_integer_sequence<int, DT>{});
-      __builtin_amdgcn_sched_barrier(0);
       [&]<int... Q>(std::integer_sequence<int, Q...>) {
         (
             [&] {
@@ -259,6 +284,12 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
                 constexpr int q1 = q + DT;
                 tf[q1 % (DT + 2)][0] = tr_frag_c<T3, (q1 & 1) * 16, (q1 >> 1) * 32, 0>(oH);
                 tf[q1 % (DT + 2)][1] = tr_frag_c<T3, (q1 & 1) * 16, D + (q1 >> 1) * 32, 0>(oH);
+              } else {
+                constexpr int k1 = q + DT - NQ;  // S(t+2)'s fragments k1 < DS
+                if constexpr (k1 < DS) {
+                  fa[k1][0] = row_frag_c<T3, 0, k1, 0>(oN);
+                  fa[k1][1] = row_frag_c<T3, 0, KS + k1, 0>(oN);
+                }
               }
               const bf16x8& th = tf[q % (DT + 2)][0];
               const bf16x8& tl = tf[q % (DT + 2)][1];
@@ -278,13 +309,11 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
             }(),
             ...);
       }(std::make_integer_sequence<int, NQ>{});
-      if constexpr (MODE == 0) mnext = fmaxf(tm, __shfl_xor(tm, 32, 64));
+      if constexpr (MODE == 0) mnext = half_max(tm);
       sc = sn;
-      dma_wait_keep<NDMA + 1>();  // tile t+2 has landed; tile t+3 (pieces + row constants) may be in flight
-      __syncthreads();
     }
   }
-  const float ztot = zrow + __shfl_xor(zrow, 32, 64);
+  const float ztot = half_sum(zrow);
   if (s < n_s) {
     if (lane < 32) {
       if constexpr (MODE == 0) part_m[(long)blockIdx.y * n_s + s] = mrow;
