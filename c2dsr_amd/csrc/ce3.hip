@@ -21,11 +21,16 @@
 //   MODE 1 (dW): stationary = W rows (lane ↔ column c), swept = H rows r:
 //     S = H·W_cᵀ, E = 2^(S·log2e + cr_r + b2_c) (cr = log2 rw − lse2), db += E, dWᵀ += Hᵀ·E
 //     → dbp [split][n], dWp [split][n][D]
-// Per 32-row tile and wave (32 stationary rows): 48 MFMAs for S, 48 for the second product; the swept
-// image (32 rows × 2D bf16 = 32 KiB at D = 256) streams through four LDS buffers by saddr LDS-DMA
-// (tile t+3 issued during the second product of tile t), read row-wise (ds_read_b128) for S and
-// transposed (ds_read_b64_tr_b16) for the second product, whose B operand is S's accumulator itself
-// (P split into hi/lo in registers).  The epilogue of S(t) runs in the MFMA shadow of S(t+1).
+// v_mfma_f32_16x16x32_bf16 throughout: on this chip the 16x16x32 shape holds a ≈14 % higher clock under
+// full matrix load than 32x32x16 at equal cycles per flop (tools/peak/mfma_peak.hip: 2147 vs 1887 TFLOP/s
+// sustained; measured here 2.2 vs 1.84 GHz inside this kernel).  Per wave: 32 stationary rows as two
+// 16-row blocks sb (lane ↔ row 16sb + l%16), their hi / lo k-slices (128 registers) pinned to AGPRs as
+// MFMA B operands; per 32-row swept tile: 96 MFMAs for S, 96 for the second product, whose accumulator
+// (Uᵀ / dWᵀ, 128 registers) is also AGPR-resident.  The swept image (32 rows × 2D bf16 = 32 KiB at
+// D = 256) streams through four LDS buffers by saddr LDS-DMA (tile t+3 issued during the second product
+// of tile t), read row-wise (ds_read_b128) for S and transposed (ds_read_b64_tr_b16) for the second
+// product, whose B operand is S's accumulator itself (P split into hi/lo in registers).  The epilogue
+// of S(t) runs in the MFMA shadow of S(t+1).
 #include "img.h"
 
 #include <utility>
@@ -44,14 +49,6 @@ using namespace c2img;
 
 constexpr int T3 = 32;  // swept rows per LDS tile
 
-// lo part of a B-operand fragment: element j = a[8s+j] − hi[j], rounded
-__device__ __forceinline__ bf16x8 lo_frag(const f32x16& a, int s, const bf16x8& hi) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (bf16)(a[8 * s + j] - (float)hi[j]);
-  return r;
-}
-
 // the two half-waves hold the two halves of a row's columns: combine them with one v_permlane32_swap (no LDS
 // round trip): swap(x, x) returns (lower half broadcast, upper half broadcast)
 __device__ __forceinline__ float half_max(float x) {
@@ -63,41 +60,93 @@ __device__ __forceinline__ float half_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// ---------------------------------------------------------------- fragment layout
+// Swept tiles of 32 rows as two 16-row blocks cb.  Sᵀ block
+// (cb, sb): lane holds swept rows 16cb + 4g + i (g = lane/16, i < 4) of stationary row 16sb + l%16, so a
+// lane's 8 values of one sb ARE the B operand of the second product with the reduction index permuted
+// k = 8g + j ↔ swept row (j < 4 ? 4g + j : 16 + 4g + j − 4); the A operand (Xwᵀ, rows = columns e of
+// the image) is read transposed in the same order: two ds_read_b64_tr_b16, rows 4g.. and 16 + 4g...
+// Image swizzle: 16-byte chunk ch of row r at r·256 + 16·(ch ^ sw(r)), sw(r) = ((r&3)<<2) | h((r>>2)&3),
+// h = [0,2,3,1]: conflict-free for the row reads (each LDS cycle's 16 lanes = 16 distinct rows mixing
+// two adjacent k-groups) and the transposed reads (8 rows × 2 chunks per 32-lane half).
+__device__ __forceinline__ int swq(int row) { return ((row & 3) << 2) | ((0x78 >> (2 * ((row >> 2) & 3))) & 3); }
+__device__ __forceinline__ float quad_max(float x) {  // over lanes l, l^16, l^32, l^48
+  x = half_max(x);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float quad_sum(float x) {
+  x = half_sum(x);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// One split product step as ONE asm statement (three MFMAs on one accumulator; separate statements get
+// an s_nop between dependent MFMAs from the hazard pass):  acc (+)= a_hi·b_hi + a_lo·b_hi + a_hi·b_lo.
+// S product: the stationary b_hi / b_lo pinned to AGPRs (128 registers that would otherwise be re-staged
+// into VGPRs every tile), acc in VGPRs (read by the VALU only after s_nop padding).
+__device__ __forceinline__ void split3_s0(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                          const bf16x8& bl) {
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, 0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
+      : "=&v"(acc)
+      : "v"(ah), "v"(al), "a"(bh), "a"(bl));
+}
+__device__ __forceinline__ void split3_s(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                         const bf16x8& bl) {
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
+      : "+v"(acc)
+      : "v"(ah), "v"(al), "a"(bh), "a"(bl));
+}
+// second product: the long-lived accumulator pinned to AGPRs (the compiler otherwise stages it through
+// VGPRs around the rescale branch); VALU readers of acc run after mfma_drain(); the B operand's VALU
+// writes are a phase behind.  acc += a_hi·b_hi + a_hi·b_lo + a_lo·b_hi
+__device__ __forceinline__ void split3_u(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                         const bf16x8& bl) {
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0"
+      : "+a"(acc)
+      : "v"(ah), "v"(al), "v"(bh), "v"(bl));
+}
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs, const bf16* __restrict__ Xw,
-                                                     const float* __restrict__ svec, const float* __restrict__ wvec,
-                                                     int n_s, int n_w, int per_split, float* __restrict__ part_m,
-                                                     float* __restrict__ part_s, float* __restrict__ outp) {
-  constexpr int KS = D / 16;                       // k-steps of a product
-  constexpr int KB = D / 32;                       // 32-wide output k-blocks of the second product
-  constexpr int NQ = 2 * KB;                       // second-product steps: (k-block, 16-row half of the tile)
+                                                      const float* __restrict__ svec, const float* __restrict__ wvec,
+                                                      int n_s, int n_w, int per_split, float* __restrict__ part_m,
+                                                      float* __restrict__ part_s, float* __restrict__ outp) {
+  constexpr int KS = D / 32;                       // k-steps of the S product
+  constexpr int NSS = 2 * KS;                      // S-phase steps: (ks, cb)
+  constexpr int NE = D / 16;                       // second-product steps: 16-column e-blocks
   constexpr int D2 = 2 * D;                        // hi ‖ lo
   constexpr int IMG = T3 * D2 * 2;                 // bytes per image
+  constexpr int HT = T3 * 256;                     // bytes per 128-column half-tile
   constexpr int NDMA = (T3 / 4) * (D2 / 128) / 4;  // LDS-DMA wave-instructions per wave per tile
-  constexpr int NB = 4;                            // images: S(t+1), second product(t), t+2 landed, t+3 landing
-  constexpr int DS = CE3_DS, DT = CE3_DT;          // LDS fragment prefetch depth (steps ahead)
-  constexpr int EPK = 16 / KS;                     // epilogue elements per S k-step
-  constexpr int MPK = 16 / NQ;                     // prep elements per second-product step
-  constexpr float TAU = 8.f;                       // lazy-max threshold (p ≤ 2^TAU)
-  static_assert(KS * EPK == 16 && NQ * MPK == 16 && NQ % NDMA == 0, "tile / wave split");
-  constexpr int QD = NQ / NDMA;                    // second-product steps per DMA piece
+  constexpr int NB = 4;
+  constexpr int DS = CE3_DS, DT = CE3_DT;
+  constexpr int EPK = 16 / NSS;                    // epilogue elements per S step
+  constexpr int MPK = 16 / NE;                     // prep elements per second-product step
+  constexpr float TAU = 8.f;
+  static_assert(NSS * EPK == 16 && NE * MPK == 16 && NE % NDMA == 0 && EPK <= 8, "tile / wave split");
+  constexpr int QD = NE / NDMA;
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
-  __shared__ __attribute__((aligned(16))) float wv[NB][4][64];  // [buffer][wave]: the tile's per-row constants
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int s = blockIdx.x * 128 + w * 32 + (lane & 31);
-  const int sc_ = min(s, n_s - 1);
+  __shared__ __attribute__((aligned(16))) float wv[NB][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
+  const int s0 = blockIdx.x * 128 + w * 32 + l16;  // stationary rows s0 (sb 0), s0 + 16 (sb 1)
   const int w_beg = blockIdx.y * per_split;
   const int w_end = min(n_w, w_beg + per_split);
   const int ntiles = w_end > w_beg ? (w_end - w_beg + T3 - 1) / T3 : 0;
-  f32x16 dacc[KB];
+  f32x4 dacc[NE][2];
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dacc[kb][i] = 0.f;
-  float mrow = -INFINITY, zrow = 0.f;  // MODE 0: running max (log2 domain) and sum; MODE 1: zrow = db
+  for (int e = 0; e < NE; ++e) dacc[e][0] = dacc[e][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrow[2] = {-INFINITY, -INFINITY}, zrow[2] = {0.f, 0.f};
   if (ntiles > 0) {
     const int w_last = w_beg + (ntiles - 1) * T3;
-    const ImgOffsets o0 = img_offsets(lane);
     const int ib = (int)lds_addr(img[0]);
     unsigned dvoff[NDMA], ddst[NDMA];
 #pragma unroll
@@ -106,11 +155,11 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       constexpr int GROUPS = T3 / 4;
       const int half = q / GROUPS, rg = q % GROUPS;
       const int row = rg * 4 + (lane >> 4);
-      const int lch = (lane & 15) ^ swz_f(row);
+      const int lch = (lane & 15) ^ swq(row);
       dvoff[i] = (unsigned)((row * D2 + half * 128 + lch * 8) * 2);
-      ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * (T3 * 256) + rg * 1024));
+      ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * HT + rg * 1024));
     }
-    auto dma = [&](int tt) {  // tile tt (clamped to the last) → buffer tt % NB
+    auto dma = [&](int tt) {
       const int r0 = min(w_beg + tt * T3, w_last);
       const int buf = tt % NB;
       const bf16* base = Xw + (long)r0 * D2;
@@ -118,83 +167,123 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + buf * IMG);
       dma4(wvec + r0 + lane, wv[buf][w]);
     };
-    bf16x8 fh[KS], fl[KS];  // the lane's stationary row: hi and lo k-slices (B operands)
+    // per-lane image offsets: row fragments (row l16 of block cb, k-chunk 4c + g) and transposed
+    // fragments (rows 4g + (l16>>2) and +16, columns 16v + 4(lane&3)..)
+    int roff0[4], toff0[8];
+    {
+      const int fr = swq(l16);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      fh[ks] = *(const bf16x8*)(Xs + (long)sc_ * D2 + ks * 16 + 8 * (lane >> 5));
-      fl[ks] = *(const bf16x8*)(Xs + (long)sc_ * D2 + D + ks * 16 + 8 * (lane >> 5));
+      for (int c = 0; c < 4; ++c) roff0[c] = l16 * 256 + 16 * ((4 * c + g) ^ fr);
+      const int trow = 4 * g + (l16 >> 2), p = lane & 3, ft = swq(trow);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) toff0[v] = trow * 256 + 16 * ((2 * v + (p >> 1)) ^ ft) + 8 * (p & 1);
     }
-    const float b2s = MODE == 1 ? svec[s] : 0.f;  // MODE 1: the lane column's bias·log2e (-inf past n)
+    bf16x8 fh[2][KS], fl[2][KS];
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const long sr = min(s0 + 16 * sb, n_s - 1);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        fh[sb][ks] = *(const bf16x8*)(Xs + sr * D2 + ks * 32 + 8 * g);
+        fl[sb][ks] = *(const bf16x8*)(Xs + sr * D2 + D + ks * 32 + 8 * g);
+      }
+    }
+    float b2s[2] = {0.f, 0.f};
+    if constexpr (MODE == 1) {
+      b2s[0] = svec[s0];
+      b2s[1] = svec[s0 + 16];
+    }
     dma(0);
     dma(1);
     dma(2);
     vm_drain();
     dma_wait();
     __syncthreads();
-    auto offs_rows = [&](int b, ImgOffsets& o) {
-      const int add = ib + b * IMG;
+    struct Offs {
+      int r[4];
+      int t[8];
+    };
+    auto offs_rows = [&](int b, Offs& o) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) o.roff[c] = o0.roff[c] + add;
+      for (int c = 0; c < 4; ++c) o.r[c] = roff0[c] + ib + b * IMG;
     };
-    auto offs_tr = [&](int b, ImgOffsets& o) {
-      const int add = ib + b * IMG;
+    auto offs_tr = [&](int b, Offs& o) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        o.troff[v][0] = o0.troff[v][0] + add;
-        o.troff[v][1] = o0.troff[v][1] + add;
-      }
+      for (int v = 0; v < 8; ++v) o.t[v] = toff0[v] + ib + b * IMG;
     };
-    // the per-swept-row constants of this lane's 16 accumulator rows (row creg(i, lane) = (i&3) + 8(i>>2) + 4h)
-    auto wconst = [&](int b, f32x4 (&c4)[4]) {
-      const int bo = (int)lds_addr(wv[b][w]) + 16 * (lane >> 5);
-      [&]<int... J>(std::integer_sequence<int, J...>) {
-        ((c4[J] = lds_ld<f32x4, 32 * J>(bo)), ...);
-      }(std::make_integer_sequence<int, 4>{});
+    // row fragment of image column block kx (32 columns; hi: ks, lo: KS + ks) and swept-row block CB
+    auto rfrag = [&]<int KX, int CB>(const Offs& o) {
+      return lds_ld128<(KX >> 2) * HT + CB * 16 * 256 + 16 * 0>(o.r[KX & 3]);
     };
-    // ---- S(0) and its prep (not overlapped)
-    f32x16 sc;
+    // transposed fragment of image columns 16·EX .. +15 (hi: EX, lo: D/16 + EX)
+    auto tfrag = [&]<int EX>(const Offs& o) {
+      constexpr int IMM = (EX >> 3) * HT;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (lds_bf16x4*)(size_t)(lds_base(o.t[EX & 7]) + IMM));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (lds_bf16x4*)(size_t)(lds_base(o.t[EX & 7]) + IMM + 16 * 256));
+      bf16x8 v;
+      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+      v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+      return v;
+    };
+    // the per-swept-row constants of this lane's rows 16cb + 4g + i
+    auto wconst = [&](int b, f32x4 (&c4)[2]) {
+      const int bo = (int)lds_addr(wv[b][w]) + 16 * g;
+      c4[0] = lds_ld<f32x4, 0>(bo);
+      c4[1] = lds_ld<f32x4, 64>(bo);
+    };
+    // S-phase step k (0 .. NSS-1) ↔ (ks = k >> 1, cb = k & 1); epilogue element i (0..15) ↔
+    // (sb = i >> 3, cb = (i >> 2) & 1, r = i & 3) = accumulator (cb·2 + sb)[r]
+    f32x4 sc[4];
     {
-      ImgOffsets oS;
+      Offs oS;
       offs_rows(0, oS);
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
-              constexpr int ks = K;
-              const bf16x8 ah = row_frag_c<T3, 0, ks, 0>(oS);
-              const bf16x8 al = row_frag_c<T3, 0, KS + ks, 0>(oS);
-              if constexpr (ks == 0)
-                sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, fh[0], f32x16{}, 0, 0, 0);
-              else
-                sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, fh[ks], sc, 0, 0, 0);
-              sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, fh[ks], sc, 0, 0, 0);
-              sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, fl[ks], sc, 0, 0, 0);
+              constexpr int ks = K >> 1, cb = K & 1;
+              const bf16x8 ah = rfrag.template operator()<ks, cb>(oS);
+              const bf16x8 al = rfrag.template operator()<KS + ks, cb>(oS);
+#pragma unroll
+              for (int sb = 0; sb < 2; ++sb) {
+                if constexpr (ks == 0)
+                  split3_s0(sc[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
+                else
+                  split3_s(sc[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
+              }
             }(),
             ...);
-      }(std::make_integer_sequence<int, KS>{});
+      }(std::make_integer_sequence<int, NSS>{});
     }
-    float mnext = -INFINITY;
+    mfma_drain();
+    float mnext[2] = {-INFINITY, -INFINITY};
     {
-      f32x4 c4[4];
+      f32x4 c4[2];
       wconst(0, c4);
-      float tm = -INFINITY;
+      float tm[2] = {-INFINITY, -INFINITY};
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float v = fmaf(sc[i], LOG2E, ((const float*)&c4[i >> 2])[i & 3]) + b2s;
-        sc[i] = v;
-        tm = fmaxf(tm, v);
+        const int sb = i >> 3, cb = (i >> 2) & 1, r = i & 3;
+        float v = fmaf(sc[cb * 2 + sb][r], LOG2E, c4[cb][r]);
+        if constexpr (MODE == 1) v += b2s[sb];
+        sc[cb * 2 + sb][r] = v;
+        tm[sb] = fmaxf(tm[sb], v);
       }
-      if constexpr (MODE == 0) mnext = half_max(tm);
+      if constexpr (MODE == 0) {
+        mnext[0] = quad_max(tm[0]);
+        mnext[1] = quad_max(tm[1]);
+      }
     }
-    // fragment rings carried across the phase boundaries: the first DS row fragments of the next S phase are
-    // read during the last steps of the second product, the first DT transposed fragments of the second
-    // product during the last S steps — no LDS-latency bubble at either boundary
     bf16x8 fa[DS + 2][2];
     bf16x8 tf[DT + 2][2];
     {
-      ImgOffsets oS;
-      offs_rows(1 % NB, oS);  // S(1) reads tile 1 (landed in the prologue)
+      Offs oS;
+      offs_rows(1 % NB, oS);
       [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((fa[P][0] = row_frag_c<T3, 0, P, 0>(oS), fa[P][1] = row_frag_c<T3, 0, KS + P, 0>(oS)), ...);
+        ((fa[P][0] = rfrag.template operator()<(P >> 1), (P & 1)>(oS),
+          fa[P][1] = rfrag.template operator()<(KS + (P >> 1)), (P & 1)>(oS)),
+         ...);
       }(std::make_integer_sequence<int, DS>{});
     }
     for (int t = 0; t < ntiles; ++t) {
@@ -203,127 +292,150 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       const bf16* nsrc = Xw + (long)rn * D2;
       const unsigned nbuf = ((t + 3) % NB) * IMG;
       dma4(wvec + rn + lane, wv[(t + 3) % NB][w]);
-      float msub = 0.f;
+      float msub[2] = {0.f, 0.f};
       if constexpr (MODE == 0) {
-        // lazy rescale: the row's max moved up by more than TAU (always on the first tile with a finite max)
-        const bool need = mnext > mrow + TAU;
-        if (__builtin_amdgcn_ballot_w64(need)) {
-          const float f = need ? ex2(mrow - mnext) : 1.f;  // mrow = -inf → 0
 #pragma unroll
-          for (int kb = 0; kb < KB; ++kb)
+        for (int sb = 0; sb < 2; ++sb) {
+          const bool need = mnext[sb] > mrow[sb] + TAU;
+          if (__builtin_amdgcn_ballot_w64(need)) [[unlikely]] {
+            const float f = need ? ex2(mrow[sb] - mnext[sb]) : 1.f;
+            mfma_drain();
 #pragma unroll
-            for (int i = 0; i < 16; ++i) dacc[kb][i] *= f;
-          zrow *= f;
-          mrow = need ? mnext : mrow;
+            for (int e = 0; e < NE; ++e) {
+              // (re)defined here, so the copies to VGPRs for the multiply cannot be hoisted above the branch
+              asm volatile("" : "+a"(dacc[e][sb]) : "v"(f));
+              dacc[e][sb] *= f;
+              asm volatile("" : "+a"(dacc[e][sb]));  // back to AGPRs inside the branch
+            }
+            zrow[sb] *= f;
+            mrow[sb] = need ? mnext[sb] : mrow[sb];
+          }
+          // keep the accumulators in AGPRs across the branch (else they are staged through VGPRs every tile)
+#pragma unroll
+          for (int e = 0; e < NE; ++e) asm volatile("" : "+a"(dacc[e][sb]));
+          msub[sb] = mrow[sb] == -INFINITY ? 0.f : mrow[sb];
         }
-        msub = mrow == -INFINITY ? 0.f : mrow;  // all of S(t) is -inf then: p = 0
       }
-      ImgOffsets oS, oH;
+      Offs oS, oH;
       offs_rows(bs, oS);
       offs_tr(bh, oH);
-      // ---- S(t+1) ∥ epilogue(t): p = 2^(v − msub), packed into the hi / lo B fragments; the last DT steps
-      //      read the second product's first transposed fragments (tile t)
-      f32x16 sn;
+      // ---- S(t+1) ∥ epilogue(t)
+      f32x4 sn[4];
       bf16x8 xh[2], xl[2];
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
-              constexpr int ks = K;
-              if constexpr (ks + DS < KS) {
-                fa[(ks + DS) % (DS + 2)][0] = row_frag_c<T3, 0, ks + DS, 0>(oS);
-                fa[(ks + DS) % (DS + 2)][1] = row_frag_c<T3, 0, KS + ks + DS, 0>(oS);
+              constexpr int k = K, ks = k >> 1, cb = k & 1;
+              if constexpr (k + DS < NSS) {
+                constexpr int k1 = k + DS;
+                fa[k1 % (DS + 2)][0] = rfrag.template operator()<(k1 >> 1), (k1 & 1)>(oS);
+                fa[k1 % (DS + 2)][1] = rfrag.template operator()<(KS + (k1 >> 1)), (k1 & 1)>(oS);
               } else {
-                constexpr int q1 = ks + DS - KS;  // 0 .. DS-1 → the second product's fragments q1 < DT
+                constexpr int q1 = k + DS - NSS;
                 if constexpr (q1 < DT) {
-                  tf[q1][0] = tr_frag_c<T3, (q1 & 1) * 16, (q1 >> 1) * 32, 0>(oH);
-                  tf[q1][1] = tr_frag_c<T3, (q1 & 1) * 16, D + (q1 >> 1) * 32, 0>(oH);
+                  tf[q1][0] = tfrag.template operator()<q1>(oH);
+                  tf[q1][1] = tfrag.template operator()<NE + q1>(oH);
                 }
               }
-              const bf16x8& ah = fa[ks % (DS + 2)][0];
-              const bf16x8& al = fa[ks % (DS + 2)][1];
-              if constexpr (ks == 0)
-                sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, fh[0], f32x16{}, 0, 0, 0);
-              else
-                sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, fh[ks], sn, 0, 0, 0);
-              sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, fh[ks], sn, 0, 0, 0);
-              sn = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, fl[ks], sn, 0, 0, 0);
+              const bf16x8& ah = fa[k % (DS + 2)][0];
+              const bf16x8& al = fa[k % (DS + 2)][1];
+#pragma unroll
+              for (int sb = 0; sb < 2; ++sb) {
+                if constexpr (ks == 0)
+                  split3_s0(sn[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
+                else
+                  split3_s(sn[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
+              }
 #pragma unroll
               for (int e = 0; e < EPK; ++e) {
-                const int i = ks * EPK + e;
-                const float pv = ex2(sc[i] - msub);
-                sc[i] = pv;
-                zrow += pv;
+                constexpr int i0 = k * EPK;
+                const int i = i0 + e, sb = i >> 3, cb2 = (i >> 2) & 1, r = i & 3;
+                const float pv = ex2(sc[cb2 * 2 + sb][r] - msub[sb]);
+                sc[cb2 * 2 + sb][r] = pv;
+                zrow[sb] += pv;
               }
-              if constexpr ((ks * EPK + EPK) % 8 == 0) {
-                constexpr int st = (ks * EPK) / 8;
-                xh[st] = acc_frag(sc, st);
-                xl[st] = lo_frag(sc, st, xh[st]);
+              if constexpr ((k * EPK + EPK) % 8 == 0) {
+                constexpr int sb = (k * EPK) / 8;
+                bf16x8 h, l;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  const float x = sc[(j >> 2) * 2 + sb][j & 3];
+                  h[j] = (bf16)x;
+                  l[j] = (bf16)(x - (float)h[j]);
+                }
+                xh[sb] = h;
+                xl[sb] = l;
               }
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
-      }(std::make_integer_sequence<int, KS>{});
-      // ---- tile t+2 (issued during the previous second product) has landed for every wave, and every wave
-      //      is past its reads of buffer (t+3) % NB (the previous second product): publish / reuse
+      }(std::make_integer_sequence<int, NSS>{});
+      asm volatile("s_nop 7" ::: "memory");  // S(t+1)'s last results before the prep's VALU reads
       dma_wait();
       __syncthreads();
-      // ---- second product (t) ∥ prep of S(t+1) ∥ DMA of tile t+3; the last DS steps read the first row
-      //      fragments of S(t+2) (tile t+2, landed above)
-      //      Oᵀ[k][s] += Σ_{c in tile} X_w[c][k]·P[c][s],  q = (kb = q >> 1, half st = q & 1)
-      ImgOffsets oN;
+      // ---- second product (t) ∥ prep of S(t+1) ∥ DMA of tile t+3
+      Offs oN;
       offs_rows((t + 2) % NB, oN);
-      f32x4 c4n[4];
+      f32x4 c4n[2];
       wconst(bs, c4n);
-      float tm = -INFINITY;
+      float tm[2] = {-INFINITY, -INFINITY};
       [&]<int... Q>(std::integer_sequence<int, Q...>) {
         (
             [&] {
               constexpr int q = Q;
-              constexpr int kb = q >> 1, st = q & 1;
-              if constexpr (q + DT < NQ) {
+              if constexpr (q + DT < NE) {
                 constexpr int q1 = q + DT;
-                tf[q1 % (DT + 2)][0] = tr_frag_c<T3, (q1 & 1) * 16, (q1 >> 1) * 32, 0>(oH);
-                tf[q1 % (DT + 2)][1] = tr_frag_c<T3, (q1 & 1) * 16, D + (q1 >> 1) * 32, 0>(oH);
+                tf[q1 % (DT + 2)][0] = tfrag.template operator()<q1>(oH);
+                tf[q1 % (DT + 2)][1] = tfrag.template operator()<NE + q1>(oH);
               } else {
-                constexpr int k1 = q + DT - NQ;  // S(t+2)'s fragments k1 < DS
+                constexpr int k1 = q + DT - NE;
                 if constexpr (k1 < DS) {
-                  fa[k1][0] = row_frag_c<T3, 0, k1, 0>(oN);
-                  fa[k1][1] = row_frag_c<T3, 0, KS + k1, 0>(oN);
+                  fa[k1][0] = rfrag.template operator()<(k1 >> 1), (k1 & 1)>(oN);
+                  fa[k1][1] = rfrag.template operator()<(KS + (k1 >> 1)), (k1 & 1)>(oN);
                 }
               }
               const bf16x8& th = tf[q % (DT + 2)][0];
               const bf16x8& tl = tf[q % (DT + 2)][1];
-              dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, xh[st], dacc[kb], 0, 0, 0);
-              dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, xl[st], dacc[kb], 0, 0, 0);
-              dacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, xh[st], dacc[kb], 0, 0, 0);
-              if constexpr (q % QD == QD - 1)
-                dma16_s<q == QD - 1>(nsrc, dvoff[q / QD], ddst[q / QD] + nbuf);
+#pragma unroll
+              for (int sb = 0; sb < 2; ++sb) {
+                split3_u(dacc[q][sb], th, tl, xh[sb], xl[sb]);
+              }
+              if constexpr (q % QD == QD - 1) dma16_s<q == QD - 1>(nsrc, dvoff[q / QD], ddst[q / QD] + nbuf);
 #pragma unroll
               for (int e = 0; e < MPK; ++e) {
-                const int i = q * MPK + e;
-                const float v = fmaf(sn[i], LOG2E, ((const float*)&c4n[i >> 2])[i & 3]) + b2s;
-                sn[i] = v;
-                tm = fmaxf(tm, v);
+                constexpr int i0 = q * MPK;
+                const int i = i0 + e, sb = i >> 3, cb = (i >> 2) & 1, r = i & 3;
+                float v = fmaf(sn[cb * 2 + sb][r], LOG2E, c4n[cb][r]);
+                if constexpr (MODE == 1) v += b2s[sb];
+                sn[cb * 2 + sb][r] = v;
+                tm[sb] = fmaxf(tm[sb], v);
               }
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
-      }(std::make_integer_sequence<int, NQ>{});
-      if constexpr (MODE == 0) mnext = half_max(tm);
-      sc = sn;
+      }(std::make_integer_sequence<int, NE>{});
+      if constexpr (MODE == 0) {
+        mnext[0] = quad_max(tm[0]);
+        mnext[1] = quad_max(tm[1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[i] = sn[i];
     }
   }
-  const float ztot = half_sum(zrow);
-  if (s < n_s) {
-    if (lane < 32) {
-      if constexpr (MODE == 0) part_m[(long)blockIdx.y * n_s + s] = mrow;
-      part_s[(long)blockIdx.y * n_s + s] = ztot;
+  mfma_drain();
+#pragma unroll
+  for (int sb = 0; sb < 2; ++sb) {
+    const float ztot = quad_sum(zrow[sb]);
+    const int s = s0 + 16 * sb;
+    if (s < n_s) {
+      if (g == 0) {
+        if constexpr (MODE == 0) part_m[(long)blockIdx.y * n_s + s] = mrow[sb];
+        part_s[(long)blockIdx.y * n_s + s] = ztot;
+      }
+      float* out = outp + ((long)blockIdx.y * n_s + s) * D + 4 * g;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
     }
-    float* out = outp + ((long)blockIdx.y * n_s + s) * D;
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) out[kb * 32 + creg(i, lane)] = dacc[kb][i];
   }
 }
 
@@ -360,10 +472,10 @@ int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec
   dim3 grid(c2::ceil_div(n_s, 128), nsplit);
   if (D == 128)
     ce3_kernel<128, MODE><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm, ps,
-                                                out);
+                                                 out);
   else if (D == 256)
     ce3_kernel<256, MODE><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm, ps,
-                                                out);
+                                                 out);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
