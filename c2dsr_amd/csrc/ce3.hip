@@ -66,10 +66,7 @@ __device__ __forceinline__ float half_sum(float x) {
 // lane's 8 values of one sb ARE the B operand of the second product with the reduction index permuted
 // k = 8g + j ↔ swept row (j < 4 ? 4g + j : 16 + 4g + j − 4); the A operand (Xwᵀ, rows = columns e of
 // the image) is read transposed in the same order: two ds_read_b64_tr_b16, rows 4g.. and 16 + 4g...
-// Image swizzle: 16-byte chunk ch of row r at r·256 + 16·(ch ^ sw(r)), sw(r) = ((r&3)<<2) | h((r>>2)&3),
-// h = [0,2,3,1]: conflict-free for the row reads (each LDS cycle's 16 lanes = 16 distinct rows mixing
-// two adjacent k-groups) and the transposed reads (8 rows × 2 chunks per 32-lane half).
-__device__ __forceinline__ int swq(int row) { return ((row & 3) << 2) | ((0x78 >> (2 * ((row >> 2) & 3))) & 3); }
+// Image swizzle: img.h swz16.
 __device__ __forceinline__ float quad_max(float x) {  // over lanes l, l^16, l^32, l^48
   x = half_max(x);
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -155,7 +152,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       constexpr int GROUPS = T3 / 4;
       const int half = q / GROUPS, rg = q % GROUPS;
       const int row = rg * 4 + (lane >> 4);
-      const int lch = (lane & 15) ^ swq(row);
+      const int lch = (lane & 15) ^ swz16(row);
       dvoff[i] = (unsigned)((row * D2 + half * 128 + lch * 8) * 2);
       ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * HT + rg * 1024));
     }
@@ -171,10 +168,10 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
     // fragments (rows 4g + (l16>>2) and +16, columns 16v + 4(lane&3)..)
     int roff0[4], toff0[8];
     {
-      const int fr = swq(l16);
+      const int fr = swz16(l16);
 #pragma unroll
       for (int c = 0; c < 4; ++c) roff0[c] = l16 * 256 + 16 * ((4 * c + g) ^ fr);
-      const int trow = 4 * g + (l16 >> 2), p = lane & 3, ft = swq(trow);
+      const int trow = 4 * g + (l16 >> 2), p = lane & 3, ft = swz16(trow);
 #pragma unroll
       for (int v = 0; v < 8; ++v) toff0[v] = trow * 256 + 16 * ((2 * v + (p >> 1)) ^ ft) + 8 * (p & 1);
     }

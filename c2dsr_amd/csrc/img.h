@@ -284,6 +284,13 @@ __device__ __forceinline__ void dma_vec64(const void* __restrict__ src, void* ds
   if ((threadIdx.x >> 6) == wv) dma4((const char*)src + 4 * (threadIdx.x & 63), dst);
 }
 
+// XOR swizzle of the 16-byte chunks of a 256-byte image row for the 16x16x32 operand layouts (ce3.hip,
+// rgemm.hip rg3): chunk ch of row r sits at r·256 + 16·(ch ^ swz16(r)), swz16(r) = ((r&3)<<2) | h((r>>2)&3),
+// h = [0,2,3,1] — conflict-free for row fragments (lane ↔ row l%16, chunk 4c + l/16: each LDS cycle's 16 lanes
+// are 16 distinct rows of two adjacent chunk groups) and for transposed fragments (rows 4g + (l%16)/4, two
+// chunks per 16-column block).
+__device__ __forceinline__ int swz16(int row) { return ((row & 3) << 2) | ((0x78 >> (2 * ((row >> 2) & 3))) & 3); }
+
 __device__ __forceinline__ int creg(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 
 // raw v_exp_f32 (2^x; no denormal range handling — results below 2^-126 flush to 0)

@@ -320,6 +320,227 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
 }
 
 // ---------------------------------------------------------------------------------------------
+// rg3: the split-bf16 (fp32 mode) row-streaming GEMM on v_mfma_f32_16x16x32_bf16, computed transposed:
+// Cᵀ tile = B·Aᵀ, so a lane's accumulator holds 4 CONSECUTIVE columns of one output row (float4 stores,
+// a float4 epilogue: bias, relu·dropout pairs, aux) instead of 16 rows of one column (16 scalar stores per
+// lane per tile: the old epilogue was store-issue-bound).  B (the split weight image, hi ‖ lo) is the MFMA
+// A operand, pinned to AGPRs for the launch: 64 columns × K = 256 (or 32 × 512) hi + lo = 256 registers per
+// lane; the workgroup covers 256 / KCH columns, so at N = 256 / K = 256 every A row is read from HBM once
+// and converted once.  A streams as before: [32][256] fp32 chunks loaded two ahead in registers, split into
+// hi / lo images (img.h swz16 layout; the conversion of chunk c+1 interleaved with chunk c's MFMAs), read as
+// the MFMA B operand (lane ↔ row l%16, k 8·(l/16)..).  Per 32-row chunk and wave: 2 row blocks × NCB column
+// blocks × 8 k-steps × 3 MFMAs (a_hi·b_hi + a_hi·b_lo + a_lo·b_hi).
+// Rows past M read 0 and are not stored (buffer descriptors); N % 4 == 0, ldc % 4 == 0.
+__device__ __forceinline__ void x3_0(f32x4& acc, const bf16x8& wh, const bf16x8& wl, const bf16x8& ah,
+                                     const bf16x8& al) {
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, 0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
+      : "=&v"(acc)
+      : "a"(wh), "a"(wl), "v"(ah), "v"(al));
+}
+__device__ __forceinline__ void x3_acc(f32x4& acc, const bf16x8& wh, const bf16x8& wl, const bf16x8& ah,
+                                       const bf16x8& al) {
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
+      : "+v"(acc)
+      : "a"(wh), "a"(wl), "v"(ah), "v"(al));
+}
+
+template <int KCH, bool EPI, int AUX>
+__global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* __restrict__ A, long lda,
+                                                     const bf16* __restrict__ B, long ldb, float* C, long ldc, Epi2 ep,
+                                                     int G) {
+  constexpr int K = 256 * KCH;
+  constexpr int NCB = 4 / KCH;      // 16-column blocks per wave
+  constexpr int CW = 16 * NCB;      // columns per wave
+  constexpr int WGC = 4 * CW;       // columns per workgroup
+  constexpr int IMGB = 32 * 256 * 2;  // bytes of one [32][256] bf16 image
+  constexpr int NST = 16;           // MFMA steps per chunk: (k-step ks, row block rb)
+  __shared__ __attribute__((aligned(16))) char aimg[2][2 * IMGB];  // [buffer][hi | lo]
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nslots = gridDim.x >> 3;
+  const int nwalk = nslots / G;
+  const int gcol = slot % G, walker = slot / G;
+  if (walker >= nwalk) return;  // uniform
+  const int RT = (M + 31) >> 5;
+  const int rt0 = xcd + 8 * walker, rts = 8 * nwalk;
+  const int ntile = rt0 < RT ? (RT - 1 - rt0) / rts + 1 : 0;
+  if (ntile == 0) return;  // uniform
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
+  const int ncol0 = gcol * WGC + w * CW;
+  bf16x8 wh[NCB][8 * KCH], wl[NCB][8 * KCH];  // the weight columns' hi / lo fragments (AGPRs)
+  f32x4 bias4[NCB];
+  const auto asrc = rsrc_bytes(A, (long)M * lda * 4);   // rows >= M read 0
+  const auto csrc = rsrc_bytes(C, (long)M * ldc * 4);   // stores to rows >= M are dropped
+  const auto xsrc = rsrc_bytes(AUX != AUX_NONE ? ep.aux : C, (long)M * ldc * 4);  // rows >= M read 0
+  // per-lane image offsets: row l16 (+16 rb), chunk 4c + g of the 128-column half-tile
+  int roff[4];
+  {
+    const int sw = swz16(l16);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) roff[c] = (int)lds_addr(aimg[0]) + l16 * 256 + 16 * ((4 * c + g) ^ sw);
+  }
+  // staging: thread t converts the float4 of row lrow + 4u (u < 8), columns 4·lane .. +3 of a chunk
+  const int lrow = threadIdx.x >> 6;
+  int soff[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int row = lrow + 4 * u, k = 4 * lane;
+    soff[u] = (int)lds_addr(aimg[0]) + (k >> 7) * (32 * 256) + row * 256 + 16 * (((k & 127) >> 3) ^ swz16(row)) +
+              2 * (k & 7);
+  }
+  const int ldab = (int)lda * 4;
+  auto load = [&](int c, float4 (&P)[8]) {
+    const int tile = min(c / KCH, ntile - 1), kc = c % KCH;
+    const int vo = ((rt0 + tile * rts) * 32 + lrow) * ldab + (kc * 256 + 4 * lane) * 4;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      P[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc, vo + u * 4 * ldab, 0, 0));
+  };
+  typedef __attribute__((address_space(3))) bf16x4 lds4;
+  auto stage1 = [&](const float4& v, int u, int buf) {
+    bf16x4 h, l;
+    h[0] = (bf16)v.x; h[1] = (bf16)v.y; h[2] = (bf16)v.z; h[3] = (bf16)v.w;
+    l[0] = (bf16)(v.x - (float)h[0]); l[1] = (bf16)(v.y - (float)h[1]);
+    l[2] = (bf16)(v.z - (float)h[2]); l[3] = (bf16)(v.w - (float)h[3]);
+    *(lds4*)(size_t)lds_base(soff[u] + buf * 2 * IMGB) = h;
+    *(lds4*)(size_t)lds_base(soff[u] + buf * 2 * IMGB + IMGB) = l;
+  };
+  // aux / row maps of the current tile (loaded at its first chunk, used by its epilogue)
+  f32x4 aux4[AUX != AUX_NONE ? 2 : 1][AUX != AUX_NONE ? NCB : 1];
+  int amap[2], dmap[2];
+  auto tile_rows = [&](int tile, int rb) { return (rt0 + tile * rts) * 32 + 16 * rb + l16; };
+  auto pre_tile = [&](int tile) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int row = tile_rows(tile, rb);
+      if constexpr (AUX == AUX_ACC_MAP) amap[rb] = row < M ? ep.auxmap[row] : -1;
+      if constexpr (EPI) dmap[rb] = ep.rowmap ? ep.rowmap[min(row, M - 1)] : row;
+    }
+    if constexpr (AUX != AUX_NONE) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int row = tile_rows(tile, rb);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const int col = ncol0 + 16 * cb + 4 * g;
+          int off;
+          if constexpr (AUX == AUX_ACC_MAP)
+            off = (col < N && amap[rb] >= 0) ? (amap[rb] * (int)ldc + col) * 4 : 0x7ffffff0;
+          else
+            off = col < N ? (row * (int)ldc + col) * 4 : 0x7ffffff0;
+          aux4[rb][cb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xsrc, off, 0, 0));
+        }
+      }
+    }
+  };
+  f32x4 acc[2][NCB];
+  auto epilogue = [&](int tile, bool live) {
+    mfma_drain();
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int row = tile_rows(tile, rb);
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const int col = ncol0 + 16 * cb + 4 * g;
+        f32x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = fmaf(ep.alpha, acc[rb][cb][i], bias4[cb][i]);
+        if constexpr (EPI) {
+          const float4 dm = ep.drop.mul4((uint64_t)(ep.row_base + dmap[rb]) * N + col);
+          v[0] = fmaxf(v[0], 0.f) * dm.x;
+          v[1] = fmaxf(v[1], 0.f) * dm.y;
+          v[2] = fmaxf(v[2], 0.f) * dm.z;
+          v[3] = fmaxf(v[3], 0.f) * dm.w;
+        }
+        if constexpr (AUX == AUX_ACC || AUX == AUX_ACC_MAP) v += aux4[rb][cb];
+        if constexpr (AUX == AUX_MASK) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = aux4[rb][cb][i] > 0.f ? v[i] * ep.aux_scale : 0.f;
+        }
+        const int off = (col < N && live) ? (row * (int)ldc + col) * 4 : 0x7ffffff0;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), csrc, off, 0, 0);
+      }
+    }
+  };
+  float4 Pa[8], Pb[8];
+  load(0, Pa);
+  load(1, Pb);
+  // the weight fragments are fetched (L2) while the first two A chunks are in flight (HBM)
+  // B (split image) fragments → AGPRs: column ncol0 + 16cb + l16, k = 32ks + 8g
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const long col = min(ncol0 + 16 * cb + l16, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 8 * KCH; ++ks) {
+      wh[cb][ks] = *(const bf16x8*)(B + col * ldb + ks * 32 + 8 * g);
+      wl[cb][ks] = *(const bf16x8*)(B + col * ldb + K + ks * 32 + 8 * g);
+    }
+    const int c4 = min(ncol0 + 16 * cb + 4 * g, N - 4);
+    bias4[cb] = ep.bias ? *(const f32x4*)(ep.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  vm_drain();
+#pragma unroll
+  for (int u = 0; u < 8; ++u) stage1(Pa[u], u, 0);
+  pre_tile(0);
+  __syncthreads();
+  // chunk c (k-chunk KC): MFMAs on image c&1 ∥ split of chunk c+1 (registers S) into image (c+1)&1; R is
+  // refilled with chunk c+2 first
+  auto step = [&]<int KC>(int c, float4 (&R)[8], float4 (&S)[8]) {
+    load(c + 2, R);
+    const int buf = c & 1, nb = (c + 1) & 1;
+    const int tile = c / KCH;
+    bf16x8 fr[4][2];
+    auto rd = [&]<int ST>() {
+      constexpr int ks = ST >> 1, rb = ST & 1;
+      constexpr int IMM = (ks >> 2) * (32 * 256) + rb * 16 * 256;
+      fr[ST & 3][0] = lds_ld128<IMM>(roff[ks & 3] + buf * 2 * IMGB);
+      fr[ST & 3][1] = lds_ld128<IMM + IMGB>(roff[ks & 3] + buf * 2 * IMGB);
+    };
+    rd.template operator()<0>();
+    rd.template operator()<1>();
+    [&]<int... SS>(std::integer_sequence<int, SS...>) {
+      (
+          [&] {
+            constexpr int st = SS, ks = st >> 1, rb = st & 1;
+            if constexpr (st + 2 < NST) rd.template operator()<st + 2>();
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+              if constexpr (KC == 0 && ks == 0)
+                x3_0(acc[rb][cb], wh[cb][KC * 8 + ks], wl[cb][KC * 8 + ks], fr[st & 3][0], fr[st & 3][1]);
+              else
+                x3_acc(acc[rb][cb], wh[cb][KC * 8 + ks], wl[cb][KC * 8 + ks], fr[st & 3][0], fr[st & 3][1]);
+            }
+            if constexpr (st % 2 == 1) stage1(S[st >> 1], st >> 1, nb);
+            __builtin_amdgcn_sched_barrier(0);
+          }(),
+          ...);
+    }(std::make_integer_sequence<int, NST>{});
+    if constexpr (KC == KCH - 1) {
+      epilogue(min(tile, ntile - 1), tile < ntile);
+      pre_tile(min(tile + 1, ntile - 1));
+    }
+    __syncthreads();
+  };
+  const int nchunk = ntile * KCH;
+  const int npair = (nchunk + 1) >> 1;
+  for (int i = 0; i < npair; ++i) {
+    const int c0 = 2 * i;
+    if constexpr (KCH == 1) {
+      step.template operator()<0>(c0, Pa, Pb);
+      step.template operator()<0>(c0 + 1, Pb, Pa);
+    } else {
+      step.template operator()<0>(c0, Pa, Pb);
+      step.template operator()<1>(c0 + 1, Pb, Pa);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // wg: dW[N, 256] partials = Σ_{t in split} dY[t, N]ᵀ·X[t, 256], both operands t-major (fp32).
 // Workgroup = 4 waves = a 128-row slice of N × all 256 columns (wave: 64 × 128, 2×4 MFMA tiles);
 // 32-row chunks of dY (32×128) and X (32×256) are converted to bf16 into LDS images and both
@@ -617,7 +838,7 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
   const int CT = K == 256 && !x3 ? 2 : 1;
   const int G = c2::ceil_div(N, 128 * CT);
   // persistent grid: exactly the workgroups that are resident at once (occupancy of the variant)
-  static int per_cu[31] = {0};
+  static int per_cu[48] = {0};
   auto launch = [&](void (*kern)(int, int, int, const void*, long, const bf16*, long, float*, long, Epi2, int),
                     int slot) -> int {
     if (!per_cu[slot]) {
@@ -632,7 +853,35 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
   };
   int rc;
   const bool e = epilogue == 1;
-  if (x3) {  // split-bf16 operands (fp32 mode): one 32-column tile per wave (hi + lo fragments in registers)
+  if (x3 && N % 4 == 0 && ldc % 4 == 0) {  // split-bf16 operands (fp32 mode): rg3 (16x16x32, transposed tiles)
+    const int G3 = c2::ceil_div(N, K == 256 ? 256 : 128);
+    auto launch3 = [&](void (*kern)(int, int, const float*, long, const bf16*, long, float*, long, Epi2, int),
+                       int slot) -> int {
+      if (!per_cu[slot]) {
+        int n = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kern, 256, 0);
+        per_cu[slot] = n > 0 ? n : 1;
+      }
+      const int blocks = (ncu * per_cu[slot] / 8) * 8;
+      if (blocks / 8 < G3) return (int)hipErrorInvalidValue;
+      kern<<<blocks, 256, 0, s>>>(M, N, (const float*)A, lda, (const bf16*)B, ldb, C, ldc, ep, G3);
+      return 0;
+    };
+    const bool k1 = K == 256;
+#define RG3(E, X) (k1 ? launch3(rg3_kernel<1, E, X>, 31 + 2 * (X) + (E ? 8 : 0)) \
+                      : launch3(rg3_kernel<2, E, X>, 32 + 2 * (X) + (E ? 8 : 0)))
+    if (e && aux_mode == AUX_NONE)
+      rc = RG3(true, AUX_NONE);
+    else if (aux_mode == AUX_ACC)
+      rc = RG3(false, AUX_ACC);
+    else if (aux_mode == AUX_ACC_MAP)
+      rc = RG3(false, AUX_ACC_MAP);
+    else if (aux_mode == AUX_MASK)
+      rc = RG3(false, AUX_MASK);
+    else
+      rc = RG3(false, AUX_NONE);
+#undef RG3
+  } else if (x3) {  // split-bf16 operands, N or ldc not a multiple of 4: one 32-column tile per wave
     const bool k1 = K == 256;
     if (aux_mode == AUX_ACC)
       rc = k1 ? launch(rg_kernel<1, 1, false, AUX_ACC, false, true>, 21) : launch(rg_kernel<2, 1, false, AUX_ACC, false, true>, 22);

@@ -1,13 +1,13 @@
 """Micro-benchmark of the K3 row-streaming projection GEMM (c2dsr_rgemm) at the encoder's shapes: time vs M
 for K = 256 (N = 256, 512) and the achieved HBM rate of its A read + C write (HIP events).
-usage: python tools/rg_micro.py"""
+usage: python tools/rg_micro.py [epi | wg | x3]"""
 import os
 import sys
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from c2dsr_amd.ops import rgemm, to_bf16  # noqa: E402
+from c2dsr_amd.ops import rgemm, to_bf16, to_split_bf16  # noqa: E402
 
 
 def timeit(fn, reps=30):
@@ -56,17 +56,18 @@ def wg_costs():
         print(f'{lib_}: wgemm T {T} N {N} {"bf16" if b16 else "fp32"} dY: {t:6.1f} us', flush=True)
 
 
-def main():
+def main(x3=False):
     dev = torch.device('cuda')
     K = 256
     for N in (256, 512):
-        Wb = to_bf16(torch.randn(N, K, device=dev))
+        W = torch.randn(N, K, device=dev)
+        Wb = to_split_bf16(W) if x3 else to_bf16(W)
         for M in (8192, 20000, 38000, 57000, 102400):
             A = torch.randn(M, K, device=dev)
             C = torch.empty(M, N, device=dev)
-            t = timeit(lambda: rgemm(A, Wb, C, M=M, N=N, K=K))
+            t = timeit(lambda: rgemm(A, Wb, C, M=M, N=N, K=K, x3=x3))
             gb = 4.0 * M * (K + N) / t / 1e3
-            print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: N {N} M {M:6d}: {t:6.1f} us '
+            print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: {"x3" if x3 else "b16"} N {N} M {M:6d}: {t:6.1f} us '
                   f'{gb:6.0f} GB/s', flush=True)
 
 
@@ -75,5 +76,7 @@ if __name__ == '__main__':
         epilogue_costs()
     elif len(sys.argv) > 1 and sys.argv[1] == 'wg':
         wg_costs()
+    elif len(sys.argv) > 1 and sys.argv[1] == 'x3':
+        main(x3=True)
     else:
         main()
