@@ -140,7 +140,7 @@ class HbmTimer:
       Sort passes and pad-row segments are overhead, not credited."""
 
     NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_bwd', 'c2dsr_embed_bwd_planned',
-             'c2dsr_embed_bwd_planned_rows')
+             'c2dsr_embed_bwd_planned_rows', 'c2dsr_gcn_spmm_b16', 'c2dsr_embed_fwd_b16', 'c2dsr_embed_bwd_planned_b16')
 
     def __init__(self, n_rows_table, nnz_by_col_ptr, uniq_by_seq_ptr):
         from c2dsr_amd._lib import lib
@@ -156,24 +156,30 @@ class HbmTimer:
         self.lib.time_names.update(self.NAMES)
         # a planned backward's first argument is the seq plan: resolve it to the index tensor at launch
         self.lib.time_meta['c2dsr_embed_bwd_planned'] = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0]), 0)
+        self.lib.time_meta['c2dsr_embed_bwd_planned_b16'] = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0]), 0)
         self.lib.time_meta['c2dsr_embed_bwd_planned_rows'] = lambda a: (
             self.uniq.get(ops.PLAN_SRC.get(a[0]), 0), ops.ROW_COUNT.get(a[4], 0) + ops.ROW_COUNT.get(a[6], 0))
 
     def stop(self):
         self.lib.time_names.difference_update(self.NAMES)
         self.lib.time_meta.pop('c2dsr_embed_bwd_planned', None)
+        self.lib.time_meta.pop('c2dsr_embed_bwd_planned_b16', None)
         self.lib.time_meta.pop('c2dsr_embed_bwd_planned_rows', None)
 
     def launch_bytes(self, name, a):
-        if name == 'c2dsr_gcn_spmm':
-            d, E, N = a[7], self.nnz[a[5]], self.N
+        if name in ('c2dsr_gcn_spmm', 'c2dsr_gcn_spmm_b16'):  # table bytes per element: 4, or 2 (bf16 tables)
+            d, E, N, tb = a[7], self.nnz[a[5]], self.N, (2 if name.endswith('_b16') else 4)
             rows = 1 + (a[14] is not None) + (a[18] != 0.0) + (a[20] is not None)
-            return 4 * d * E + 8 * E + 4 * (N + 1) + 4 * d * N * rows
+            return tb * d * E + 8 * E + 4 * (N + 1) + tb * d * N * rows
         if name == 'c2dsr_embed_fwd':
             n, d = a[2], a[3]
             reads = (a[4] is not None) + (a[5] is not None) + (a[6] is not None)
             return n * (16 + 4 * d * reads + 4 * d)
         n, d = a[2], a[3]
+        if name == 'c2dsr_embed_fwd_b16':  # (seq, pos, n, d, H, E, P, ..., X): two bf16 table rows, fp32 X
+            return n * (16 + 2 * 2 * d + 4 * d)
+        if name == 'c2dsr_embed_bwd_planned_b16':  # read dX (fp32); bf16 read-modify-write per distinct item
+            return n * (16 + 4 * d) + 4 * d * a[-1]
         if name == 'c2dsr_embed_bwd_planned_rows':  # (.., n, d, gXa, inv_a, gXb, inv_b, ..) + (uniq, rows of parts)
             uniq, part_rows = a[-1]
             return n * (16 + 8) + 4 * d * part_rows + 8 * d * uniq
@@ -294,8 +300,10 @@ def run_c5(opt, world, rank, device, emit=True):
     optimizer state, ~13 TB of logits), so a step is the HBM-bound part of the training step on the
     shared table: K1 GCN forward (A·drop(E), mean) + the five K2 embedding gathers (share, a, b, neg_a,
     neg_b index sets) forward + their deterministic backward + the K1 GCN backward through Aᵀ into
-    E.grad, all on the product's autograd functions (ops.GCNFn / ops.EmbedFn).  Value = algorithmic
-    GB/s of those kernels (HbmTimer); each rank works on its own batch (no exchange)."""
+    E.grad.  The line's value is on bf16 [N, d] tables (E, H, the lookup gradient and E.grad,
+    4 × 20.5 GB; the *_b16 kernels, fp32 arithmetic); ``fp32_tables`` is the same step on fp32 tables through the
+    product's autograd functions (ops.GCNFn / ops.EmbedFn).  Value = algorithmic GB/s of those kernels
+    (HbmTimer); each rank works on its own batch (no exchange)."""
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
     from c2dsr_amd import ops, synth
@@ -324,52 +332,90 @@ def run_c5(opt, world, rank, device, emit=True):
     dg = GR.DeviceGraph(g, device)
     b = [torch.from_numpy(r[:B].copy()).to(device) for r in rows]
     passes = [(b[0], b[3]), (b[1], b[4]), (b[2], b[5]), (b[12], b[3]), (b[13], b[3])]
-    torch.manual_seed(0)
-    E = torch.nn.Parameter(torch.empty(N, d, device=device).normal_(0.0, 0.1))
-    E.grad = torch.zeros_like(E)
-    P = torch.nn.Parameter(torch.empty(L, d, device=device).normal_(0.0, 0.1))
-    P.grad = torch.zeros_like(P)
-    gx = torch.empty(B, L, d, device=device).normal_(0.0, 1e-3)
-    args = SimpleNamespace(dropout_gnn=0.2, n_gnn=1, idx_pad=N - 1)
-    state = StepState(seed=3407)
-    gcn = GCN(args)
-    gcn.state = state
-    p = 0.2
-
-    def step():
-        state.step += 1
-        H, tok, sink = gcn.propagate(E, dg)
-        xs = []
-        for k, (seq, pos) in enumerate(passes):
-            keys = state.keys(DK.site_enc(k, 0, DK.K_INPUT))
-            xs.append(ops.EmbedFn.apply(tok, E, P, seq, pos, H, math.sqrt(d), p, keys, rank * B, sink, N - 1))
-        torch.autograd.backward(xs, [gx] * len(xs))
-
     nnz = {}
     for t in (False, True):
         col = dg.plan(t)[5]
         nnz[col.data_ptr()] = col.numel()
     uniq = {seq.data_ptr(): int(np.unique(rows[j][:B]).size) for j, (seq, _) in zip((0, 1, 2, 12, 13), passes)}
-    ht = HbmTimer(N, nnz, uniq)
-    for _ in range(opt.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    ht.start()
-    t0 = time.perf_counter()
-    for _ in range(opt.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    ht.stop()
-    if world > 1:
-        t = torch.tensor([el], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t)
-    roof = ht.summary(opt.steps)
+    p = 0.2
+
+    def measure(b16):
+        torch.manual_seed(0)
+        gx = torch.empty(B, L, d, device=device).normal_(0.0, 1e-3)
+        args = SimpleNamespace(dropout_gnn=p, n_gnn=1, idx_pad=N - 1)
+        state = StepState(seed=3407)
+        gcn = GCN(args)
+        gcn.state = state
+        if b16:  # E, H, the lookup gradient G and E.grad as bf16 [N, d] tables (4 × 20.5 GB), fp32 arithmetic
+            from c2dsr_amd._lib import lib, stream
+            E = torch.empty(N, d, device=device, dtype=torch.bfloat16).normal_(0.0, 0.1)
+            H, G, gE = torch.empty_like(E), torch.empty_like(E), torch.zeros_like(E)
+            P = torch.empty(L, d, device=device).normal_(0.0, 0.1)
+            gP = torch.zeros_like(P)
+            x = torch.empty(B, L, d, device=device)
+            ws_bytes = int(lib.raw('c2dsr_embed_bwd_planned_workspace')(B * L, d))
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+        else:
+            E = torch.nn.Parameter(torch.empty(N, d, device=device).normal_(0.0, 0.1))
+            E.grad = torch.zeros_like(E)
+            P = torch.nn.Parameter(torch.empty(L, d, device=device).normal_(0.0, 0.1))
+            P.grad = torch.zeros_like(P)
+
+        def step_fp32():  # the product's autograd functions (ops.GCNFn / ops.EmbedFn)
+            state.step += 1
+            H, tok, sink = gcn.propagate(E, dg)
+            xs = []
+            for k, (seq, pos) in enumerate(passes):
+                keys = state.keys(DK.site_enc(k, 0, DK.K_INPUT))
+                xs.append(ops.EmbedFn.apply(tok, E, P, seq, pos, H, math.sqrt(d), p, keys, rank * B, sink, N - 1))
+            torch.autograd.backward(xs, [gx] * len(xs))
+
+        def step_b16():
+            # the same kernels on bf16 tables (the fused GCN / embedding autograd functions' launches, by hand):
+            # H = (E + A·drop(E))/2; five gathers; G = Σ segment sums of the five passes; E.grad += (drop(AᵀG) +
+            # G)/2 + [i != pad]·G (ops.GCNFn.backward with n_gnn = 1)
+            state.step += 1
+            pg, gkeys = gcn._keys()
+            ops.spmm(dg, False, E, gkeys[0], pg, 0, 0.5, E, 0.5, 0.0, -1, 0.0, H)
+            plans = ops.index_plans(state, [(seq, N) for seq, _ in passes] + [(pos, L) for _, pos in passes])
+            ekeys = [state.keys(DK.site_enc(k, 0, DK.K_INPUT)) for k in range(len(passes))]
+            for k, (seq, pos) in enumerate(passes):  # forward (x is consumed by nothing else here)
+                lib('c2dsr_embed_fwd_b16', seq, pos, B * L, d, H, E, P, math.sqrt(d), ekeys[k][0], ekeys[k][1], p,
+                    rank * B * L, x, stream())
+            G.zero_()
+            for k, (seq, pos) in enumerate(passes):
+                lib('c2dsr_embed_bwd_planned_b16', plans[k].get(), plans[len(passes) + k].get(), B * L, d, gx,
+                    ekeys[k][0], ekeys[k][1], p, rank * B * L, math.sqrt(d), G, N, gP, L, ws, ws_bytes, stream())
+            ops.spmm(dg, True, G, gkeys[0], pg, 1, 0.5, G, 0.5, 1.0, N - 1, 1.0, gE)
+
+        step = step_b16 if b16 else step_fp32
+        ht = HbmTimer(N, nnz, uniq)
+        for _ in range(opt.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ht.start()
+        t0 = time.perf_counter()
+        for _ in range(opt.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        ht.stop()
+        if world > 1:
+            t = torch.tensor([el], device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        return ht.summary(opt.steps), el
+
+    modes = ['bf16', 'fp32'] if opt.c5_tables == 'both' else [opt.c5_tables]
+    res = {}
+    for m in modes:
+        res[m] = measure(m == 'bf16')
+        torch.cuda.empty_cache()
+    roof, el = res[modes[0]]
     out = None
     if rank == 0:
         out = {'metric': 'C5 HBM roofline: K1 GCN SpMM + K2 embedding gather (fwd+bwd), algorithmic GB/s',
@@ -378,10 +424,15 @@ def run_c5(opt, world, rank, device, emit=True):
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
                'data': 'synthetic (Zipf two-domain sequences, vectorised generator)',
                'config': {'workload': 'c5: synthetic 10M+10M items, d=512, L=100 (BASELINE configs[4])',
+                          'tables': modes[0],
                           'n_item': N, 'd': d, 'seq_len': L, 'batch_per_gpu': B, 'global_batch': B * world,
                           'graph_sequences': opt.c5_seqs, 'graph_nnz': g.nnz, 'dropout': p,
                           'parallelism': f'dp{world}'},
                'roofline': roof, 'cpu_baseline': None}
+        for m in modes[1:]:  # the other table storage on the same graph and batch
+            r2, el2 = res[m]
+            out[f'{m}_tables'] = {'value': round(r2['achieved'] * world, 1),
+                                  'ms_per_step': round(el2 / opt.steps * 1e3, 3), 'roofline': r2}
         if emit:
             print(json.dumps(out), flush=True)
     return out
@@ -398,6 +449,9 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-budget', type=float, default=20.0)
     ap.add_argument('--c5-seqs', type=int, default=2_000_000)
+    ap.add_argument('--c5-tables', default='both', choices=['bf16', 'fp32', 'both'],
+                    help='C5 [N, d] table storage (SURVEY.md §8(d): bf16 tables, the line\'s value; fp32 = the '
+                         'product\'s autograd path; both: bf16 line + fp32_tables sub-object on the same graph)')
     ap.add_argument('--no-extra', dest='extra', action='store_false',
                     help='skip the extra lines (MB bf16 mode, FK bf16, C5) of the default N=1 run')
     ap.add_argument('--no-c5', dest='c5_extra', action='store_false', help='skip the C5 extra line')

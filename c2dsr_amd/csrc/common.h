@@ -78,6 +78,46 @@ __device__ __forceinline__ float4 fma4(float s, float4 a, float4 c) {
   return make_float4(fmaf(s, a.x, c.x), fmaf(s, a.y, c.y), fmaf(s, a.z, c.z), fmaf(s, a.w, c.w));
 }
 
+// 4 consecutive elements of an embedding-table row stored as fp32 (float4 access) or bf16 (8-byte access,
+// RNE on store): the C5 roofline run keeps its [N, d] tables in bf16; arithmetic is fp32
+typedef __bf16 tbf16;
+typedef tbf16 tbf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ float4 ld4(const tbf16* p) {
+  const tbf16x4 v = *(const tbf16x4*)p;
+  return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+__device__ __forceinline__ void st4(float* p, float4 v) { *(float4*)p = v; }
+__device__ __forceinline__ void st4(tbf16* p, float4 v) {
+  tbf16x4 r;
+  r[0] = (tbf16)v.x; r[1] = (tbf16)v.y; r[2] = (tbf16)v.z; r[3] = (tbf16)v.w;
+  *(tbf16x4*)p = r;
+}
+
+// A lane's slice of a table row per step, as fp32 arithmetic: 16 bytes = VW elements (4 fp32 or 8 bf16) → VW/4
+// float4 (a 32-byte bf16 slice — two rows per wave — measured 20 % slower in the C5 SpMM)
+template <typename T>
+constexpr int VW = 16 / (int)sizeof(T);
+template <typename T>
+struct RowV {
+  float4 v[VW<T> / 4];
+};
+__device__ __forceinline__ RowV<float> ldv(const float* p) { return RowV<float>{{*(const float4*)p}}; }
+__device__ __forceinline__ RowV<tbf16> ldv(const tbf16* p) {
+  typedef tbf16 tbf16x8 __attribute__((ext_vector_type(8)));
+  const tbf16x8 x = *(const tbf16x8*)p;
+  return RowV<tbf16>{{make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]),
+                      make_float4((float)x[4], (float)x[5], (float)x[6], (float)x[7])}};
+}
+__device__ __forceinline__ void stv(float* p, const RowV<float>& r) { *(float4*)p = r.v[0]; }
+__device__ __forceinline__ void stv(tbf16* p, const RowV<tbf16>& r) {
+  typedef tbf16 tbf16x8 __attribute__((ext_vector_type(8)));
+  tbf16x8 x;
+  x[0] = (tbf16)r.v[0].x; x[1] = (tbf16)r.v[0].y; x[2] = (tbf16)r.v[0].z; x[3] = (tbf16)r.v[0].w;
+  x[4] = (tbf16)r.v[1].x; x[5] = (tbf16)r.v[1].y; x[6] = (tbf16)r.v[1].z; x[7] = (tbf16)r.v[1].w;
+  *(tbf16x8*)p = x;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

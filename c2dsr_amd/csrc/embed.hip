@@ -14,10 +14,10 @@
 namespace {
 
 // ------------------------------------------------------------------ forward gather
-template <int LPR, bool GATHER>
+template <int LPR, bool GATHER, typename T = float>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ seq, const int64_t* __restrict__ pos,
-                                                        int n_rows, int d, const float* __restrict__ H,
-                                                        const float* __restrict__ E, const float* __restrict__ Xin,
+                                                        int n_rows, int d, const T* __restrict__ H,
+                                                        const T* __restrict__ E, const float* __restrict__ Xin,
                                                         const float* __restrict__ P, float scale, c2::Drop drop,
                                                         int64_t idx_base, float* __restrict__ X) {
   constexpr int GROUPS = 256 / LPR;
@@ -31,8 +31,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   for (int c = lane * 4; c < d; c += LPR * 4) {
     float4 a;
     if (GATHER) {
-      const float4 h = *(const float4*)(H + s * d + c);
-      const float4 e = *(const float4*)(E + s * d + c);
+      const float4 h = c2::ld4(H + s * d + c);
+      const float4 e = c2::ld4(E + s * d + c);
       a = scale * (h + e);
     } else {
       a = *(const float4*)(Xin + r * d + c);
@@ -74,33 +74,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint32_t* __r
   hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan of m counters, single workgroup of 1024 threads
-__global__ __launch_bounds__(1024) void rs_scan_kernel(uint32_t* __restrict__ hist, int m) {
-  __shared__ uint32_t part[1024];
-  const int t = threadIdx.x;
-  const int per = (m + 1023) / 1024;
-  const int lo = min(m, t * per), hi = min(m, lo + per);
-  uint32_t s = 0;
-  for (int i = lo; i < hi; ++i) s += hist[i];
-  part[t] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    uint32_t v = t >= o ? part[t - o] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - s;
-  for (int i = lo; i < hi; ++i) {
-    uint32_t c = hist[i];
-    hist[i] = run;
-    run += c;
-  }
-}
-
 __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* __restrict__ kin,
                                                                const uint32_t* __restrict__ vin, int n, int shift,
-                                                               int nblocks, const uint32_t* __restrict__ offs,
+                                                               int nblocks, const uint32_t* __restrict__ offs,  // digit histograms [256][nblocks]
                                                                uint32_t* __restrict__ kout,
                                                                uint32_t* __restrict__ vout) {
   __shared__ uint32_t wcnt[4][256];
@@ -110,7 +86,28 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   for (int q = 0; q < 4; ++q) wcnt[q][t] = 0;
   run[t] = 0;
-  gbase[t] = offs[t * nblocks + blockIdx.x];
+  {
+    // this block's first destination of digit t = (entries of smaller digits) + (digit-t entries of earlier
+    // blocks): read off the digit histograms of all blocks here instead of a separate single-workgroup scan
+    const uint32_t* ht = offs + (long)t * nblocks;
+    uint32_t pre = 0, tot = 0;
+    for (int b = 0; b < nblocks; ++b) {
+      const uint32_t c = ht[b];
+      pre += b < (int)blockIdx.x ? c : 0u;
+      tot += c;
+    }
+    // exclusive scan of tot over the 256 digits (four waves: in-wave shuffles, then the wave totals)
+    uint32_t inc = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) woff[0][w] = inc;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int k = 0; k < w; ++k) base += woff[0][k];
+    gbase[t] = base + inc - tot + pre;
+  }
   __syncthreads();
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int base = blockIdx.x * RS_TILE;
@@ -190,31 +187,6 @@ __global__ __launch_bounds__(PL_T) void plan_count_kernel(const uint32_t* __rest
   }
 }
 
-// exclusive scan of the block counts (single workgroup); total → counts[1]
-__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ cnt, int nb, int* __restrict__ counts) {
-  __shared__ uint32_t part[1024];
-  const int t = threadIdx.x;
-  const int per = (nb + 1023) / 1024;
-  const int lo = min(nb, t * per), hi = min(nb, lo + per);
-  uint32_t s0 = 0;
-  for (int i = lo; i < hi; ++i) s0 += cnt[i];
-  part[t] = s0;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t v0 = t >= o ? part[t - o] : 0;
-    __syncthreads();
-    part[t] += v0;
-    __syncthreads();
-  }
-  uint32_t r0 = part[t] - s0;
-  for (int i = lo; i < hi; ++i) {
-    const uint32_t c0 = cnt[i];
-    cnt[i] = r0;
-    r0 += c0;
-  }
-  if (t == 1023) counts[1] = (int)part[1023];
-}
-
 // exclusive block-wide prefix of one u32 per thread (PL_T threads)
 __device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -232,9 +204,21 @@ __device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t* red) {
 }
 
 // writes splits[j] = {key, first chunk, chunks spanned, 0} in entry order
+// The block's first output slot is the sum of the earlier blocks' counts (plan_count_kernel), read here
+// (≤ a few hundred u32 from L2) instead of a separate scan launch; the last block writes the total → counts[1].
 __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restrict__ K, int n,
-                                                         const uint32_t* __restrict__ cnt, int4* __restrict__ splits) {
+                                                         const uint32_t* __restrict__ cnt, int4* __restrict__ splits,
+                                                         int* __restrict__ counts) {
   __shared__ uint32_t red[PL_T / 64];
+  uint32_t before = 0;
+  for (int b = threadIdx.x; b < (int)blockIdx.x; b += PL_T) before += cnt[b];
+  for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = before;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int k = 0; k < PL_T / 64; ++k) base += red[k];
+  __syncthreads();
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) counts[1] = (int)(base + cnt[blockIdx.x]);
   // thread t owns entries [base + t·PL_E, base + (t+1)·PL_E): contiguous, so the order is kept
   const int i0 = blockIdx.x * PL_B + threadIdx.x * PL_E;
   uint32_t fs = 0;
@@ -242,7 +226,7 @@ __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restr
     const int i = i0 + j;
     if (i < n) fs |= (uint32_t)split_start(K, n, i) << j;
   }
-  uint32_t os = cnt[blockIdx.x] + block_prefix(__popc(fs), red);
+  uint32_t os = base + block_prefix(__popc(fs), red);
   for (int j = 0; j < PL_E; ++j) {
     if (fs >> j & 1) {
       const int i = i0 + j;
@@ -313,6 +297,7 @@ struct SegJob {
   int n, n_out, skip_key, nblocks;
   RowSrc src;
   float *out, *ph, *pt, *slot2;
+  c2::tbf16* out16;  // non-null: the output table is bf16 (then out is null; the C5 roofline run)
 };
 
 // pass A: one lane group per chunk of SEG_CH sorted entries.  The block stages its keys and row
@@ -398,12 +383,19 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
       }
       float4 prev[SEG_U];
 #pragma unroll
-      for (int u = 0; u < SEG_U; ++u)
-        prev[u] = kind[u] == 1 ? *(const float4*)(J.out + (long)sk[o + h0 + u + 1] * d + c) : c2::f4(0.f);
+      for (int u = 0; u < SEG_U; ++u) {
+        const long off = (long)sk[o + h0 + u + 1] * d + c;
+        prev[u] = kind[u] != 1 ? c2::f4(0.f) : (J.out16 ? c2::ld4(J.out16 + off) : *(const float4*)(J.out + off));
+      }
 #pragma unroll
       for (int u = 0; u < SEG_U; ++u) {
-        if (kind[u] == 1)
-          *(float4*)(J.out + (long)sk[o + h0 + u + 1] * d + c) = prev[u] + x[u];
+        if (kind[u] == 1) {
+          const long off = (long)sk[o + h0 + u + 1] * d + c;
+          if (J.out16)
+            c2::st4(J.out16 + off, prev[u] + x[u]);
+          else
+            *(float4*)(J.out + off) = prev[u] + x[u];
+        }
         else if (kind[u] == 2)
           *(float4*)(J.ph + chunk * d + c) = x[u];
         else if (kind[u] == 3)
@@ -445,11 +437,13 @@ struct SplitView {
   float* out;
   const float *ph, *pt;
   float* slot2;
+  c2::tbf16* out16;
   __device__ __forceinline__ SplitView(const SegJob& j0, const SegJob& j1, bool y)
       : splits(y ? j1.splits : j0.splits), subs(y ? j1.subs : j0.subs), suboff(y ? j1.suboff : j0.suboff),
         counts(y ? j1.counts : j0.counts), err(y ? j1.err : j0.err), n(y ? j1.n : j0.n),
         n_out(y ? j1.n_out : j0.n_out), skip_key(y ? j1.skip_key : j0.skip_key), d(y ? j1.src.d : j0.src.d),
-        out(y ? j1.out : j0.out), ph(y ? j1.ph : j0.ph), pt(y ? j1.pt : j0.pt), slot2(y ? j1.slot2 : j0.slot2) {}
+        out(y ? j1.out : j0.out), ph(y ? j1.ph : j0.ph), pt(y ? j1.pt : j0.pt), slot2(y ? j1.slot2 : j0.slot2),
+        out16(y ? j1.out16 : j0.out16) {}
   __device__ __forceinline__ int nchunks() const { return (n + SEG_CH - 1) / SEG_CH; }
   __device__ __forceinline__ int max_sub() const { return nchunks() + 2 + n / (SEG_CH * SUBP); }
 };
@@ -529,11 +523,14 @@ __global__ __launch_bounds__(256) void seg_split2_kernel(SegJob j0, SegJob j1) {
       continue;
     }
     if (key == J.skip_key) continue;
-    float* o = J.out + (long)key * d;
+    const long o = (long)key * d;
     for (int c = lane * 4; c < d; c += LPR * 4) {
-      float4 t = *(const float4*)(o + c);
+      float4 t = J.out16 ? c2::ld4(J.out16 + o + c) : *(const float4*)(J.out + o + c);
       for (int k = b0; k < b1; ++k) t = t + *(const float4*)(J.slot2 + (long)k * d + c);
-      *(float4*)(o + c) = t;
+      if (J.out16)
+        c2::st4(J.out16 + o + c, t);
+      else
+        *(float4*)(J.out + o + c) = t;
     }
   }
 }
@@ -657,7 +654,6 @@ int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t
   prep_keys_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(idx, n, ki, vi);
   for (int shift = 0; shift < bits; shift += 8) {
     rs_hist_kernel<<<w.nblocks, RS_THREADS, 0, s>>>(ki, n, shift, w.nblocks, w.hist);
-    rs_scan_kernel<<<1, 1024, 0, s>>>(w.hist, 256 * w.nblocks);
     rs_scatter_kernel<<<w.nblocks, RS_THREADS, 0, s>>>(ki, vi, n, shift, w.nblocks, w.hist, ko, vo);
     uint32_t* t = ki; ki = ko; ko = t;
     t = vi; vi = vo; vo = t;
@@ -668,8 +664,7 @@ int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t
   }
   const int pb = c2::ceil_div(n, PL_B);
   plan_count_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt);
-  plan_scan_kernel<<<1, 1024, 0, s>>>(w.bcnt, pb, w.counts);
-  plan_emit_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt, w.splits);
+  plan_emit_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt, w.splits, w.counts);
   plan_subs_kernel<<<1, 1024, 0, s>>>(w.splits, w.counts, w.suboff, w.subs, w.counts + 3);
   C2_CHECK_LAUNCH();
   return 0;
@@ -717,6 +712,7 @@ SegJob seg_job(const Plan& p, int n, int n_out, const RowSrc& src, float* out, c
   j.nblocks = 0;
   j.src = src;
   j.out = out;
+  j.out16 = nullptr;
   j.ph = (float*)ws;
   j.pt = (float*)(ws + seg_slot_bytes(n, src.d));
   j.slot2 = (float*)(ws + 2 * seg_slot_bytes(n, src.d));
@@ -797,19 +793,22 @@ C2_API size_t c2dsr_plan_err_offset(int n) {
 static int embed_bwd_planned_impl(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
                                   const int* map1, const float* gX2, const int* map2, uint32_t k0, uint32_t k1,
                                   float p, int64_t idx_base, float scale, float* G, int n_items, float* gP, int n_pos,
-                                  float* gXin, void* workspace, size_t ws_bytes, void* stream) {
+                                  float* gXin, void* workspace, size_t ws_bytes, void* stream,
+                                  c2::tbf16* G16 = nullptr) {
   if (d % 4) return (int)hipErrorInvalidValue;
   if (n_rows == 0) return 0;
-  if (ws_bytes < c2dsr_embed_bwd_planned_workspace(n_rows, d) || (G && !seq_plan) || (gP && !pos_plan))
+  if (ws_bytes < c2dsr_embed_bwd_planned_workspace(n_rows, d) || ((G || G16) && !seq_plan) || (gP && !pos_plan))
     return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   c2::Drop dr = c2::make_drop(k0, k1, p);
   char* ws = (char*)workspace;
   SegJob jobs[2];
   int nj = 0;
-  if (G)
-    jobs[nj++] = seg_job(plan_view(seq_plan, n_rows), n_rows, n_items,
-                         RowSrc{gX, d, dr, idx_base, scale, nullptr, map1, map2, gX2}, G, ws, -1);
+  if (G || G16) {
+    jobs[nj] = seg_job(plan_view(seq_plan, n_rows), n_rows, n_items,
+                       RowSrc{gX, d, dr, idx_base, scale, nullptr, map1, map2, gX2}, G, ws, -1);
+    jobs[nj++].out16 = G16;
+  }
   if (gP)
     jobs[nj++] = seg_job(plan_view(pos_plan, n_rows), n_rows, n_pos,
                          RowSrc{gX, d, dr, idx_base, 1.0f, nullptr, map1, map2, gX2}, gP,
@@ -829,6 +828,40 @@ C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, i
                                    void* stream) {
   return embed_bwd_planned_impl(seq_plan, pos_plan, n_rows, d, gX, nullptr, nullptr, nullptr, k0, k1, p, idx_base,
                                 scale, G, n_items, gP, n_pos, gXin, workspace, ws_bytes, stream);
+}
+
+// bf16 item tables (the C5 roofline run): the gather reads bf16 H / E rows, the item segment
+// sums read-modify-write a bf16 G (fp32 sums, RNE store); P, X, gX, gP stay fp32
+C2_API int c2dsr_embed_fwd_b16(const int64_t* seq, const int64_t* pos, int n_rows, int d, const void* H, const void* E,
+                               const float* P, float scale, uint32_t k0, uint32_t k1, float p, int64_t idx_base,
+                               float* X, void* stream) {
+  if (d % 4 || n_rows <= 0 || !H || !E) return n_rows == 0 ? 0 : (int)hipErrorInvalidValue;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  hipStream_t s = (hipStream_t)stream;
+  const int lpr = lpr_for(d);
+  dim3 grid(c2::ceil_div(n_rows, 256 / lpr));
+  const c2::tbf16 *Hb = (const c2::tbf16*)H, *Eb = (const c2::tbf16*)E;
+#define C2_EMB(L) \
+  embed_fwd_kernel<L, true, c2::tbf16><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, Hb, Eb, nullptr, P, scale, dr, idx_base, X);
+  switch (lpr) {
+    case 64: C2_EMB(64) break;
+    case 32: C2_EMB(32) break;
+    case 16: C2_EMB(16) break;
+    case 8: C2_EMB(8) break;
+    default: C2_EMB(4) break;
+  }
+#undef C2_EMB
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_embed_bwd_planned_b16(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
+                                       uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, void* G,
+                                       int n_items, float* gP, int n_pos, void* workspace, size_t ws_bytes,
+                                       void* stream) {
+  if (!G) return (int)hipErrorInvalidValue;
+  return embed_bwd_planned_impl(seq_plan, pos_plan, n_rows, d, gX, nullptr, nullptr, nullptr, k0, k1, p, idx_base,
+                                scale, nullptr, n_items, gP, n_pos, nullptr, workspace, ws_bytes, stream,
+                                (c2::tbf16*)G);
 }
 
 // the same with gX given as two compact row sources: row r = (inv_a[r] >= 0 ? gXa[inv_a[r]] : 0)

@@ -13,44 +13,57 @@
 // static "work" list built once per graph, c2dsr_amd/graph.py); a piece of an
 // unsplit row runs the full epilogue, pieces of split rows write raw partial sums
 // to a scratch slab that a second pass adds up in piece order (deterministic).
-// One work item per group of LPR lanes, float4 per lane (d <= 4*LPR per pass).
+// One work item per group of LPR lanes, 4 elements per lane (d <= 4*LPR per pass).  Tables (X, Z, Y, Y2) are
+// fp32, or bf16 for the C5 roofline run (c2dsr_gcn_spmm_b16: SURVEY.md §8(d); fp32 arithmetic, RNE stores).
 #include "common.h"
 
 namespace {
 
+template <typename T>
 struct Epi {
   float alpha;
-  const float* Z;
+  const T* Z;
   float beta, delta;
   int pad_row;
   float gamma;
-  float* Y;
-  float* Y2;
+  T* Y;
+  T* Y2;
   c2::Drop drop;
 };
 
-template <bool MASK_OUT>
-__device__ __forceinline__ void epilogue(float4 acc, long row, int c, int d, const Epi& ep) {
+template <bool MASK_OUT, typename T>
+__device__ __forceinline__ void epilogue(c2::RowV<T> acc, long row, int c, int d, const Epi<T>& ep) {
+  constexpr int NH = c2::VW<T> / 4;
   if (MASK_OUT && ep.drop.active()) {
-    const uint64_t b = (uint64_t)row * d + c;
-    acc = acc * ep.drop.mul4(b);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc.v[h] = acc.v[h] * ep.drop.mul4((uint64_t)row * d + c + 4 * h);
   }
-  if (ep.Y2) *(float4*)(ep.Y2 + row * d + c) = acc;
-  float4 y = ep.alpha * acc;
+  if (ep.Y2) c2::stv(ep.Y2 + row * d + c, acc);
+  c2::RowV<T> y;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) y.v[h] = ep.alpha * acc.v[h];
   if (ep.Z) {
     const float zc = ep.beta + (row != ep.pad_row ? ep.delta : 0.f);
-    y = c2::fma4(zc, *(const float4*)(ep.Z + row * d + c), y);
+    const c2::RowV<T> z = c2::ldv(ep.Z + row * d + c);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) y.v[h] = c2::fma4(zc, z.v[h], y.v[h]);
   }
-  if (ep.gamma != 0.f) y = c2::fma4(ep.gamma, *(const float4*)(ep.Y + row * d + c), y);
-  *(float4*)(ep.Y + row * d + c) = y;
+  if (ep.gamma != 0.f) {
+    const c2::RowV<T> o = c2::ldv(ep.Y + row * d + c);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) y.v[h] = c2::fma4(ep.gamma, o.v[h], y.v[h]);
+  }
+  c2::stv(ep.Y + row * d + c, y);
 }
 
 // work[w] = {row, e_begin, e_end, slot}; slot < 0: whole row (epilogue), else partial slab index.
-template <int LPR, bool MASK_OUT>
+// A lane handles 16 bytes of a table row per step (4 fp32 or 8 bf16 elements).
+template <int LPR, bool MASK_OUT, typename T>
 __global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work, int n_work,
                                                    const int* __restrict__ col, const float* __restrict__ val, int d,
-                                                   const float* __restrict__ X, Epi ep, float* __restrict__ part) {
+                                                   const T* __restrict__ X, Epi<T> ep, float* __restrict__ part) {
   constexpr int GROUPS = 256 / LPR;
+  constexpr int V = c2::VW<T>, NH = V / 4;
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
   const long w = (long)blockIdx.x * GROUPS + g;
@@ -59,42 +72,51 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work
   const long row = wk.x;
   const int e0 = wk.y, e1 = wk.z, slot = wk.w;
   const c2::Drop& drop = ep.drop;
-  for (int c = lane * 4; c < d; c += LPR * 4) {
-    float4 acc = c2::f4(0.f);
+  for (int c = lane * V; c < d; c += LPR * V) {
+    c2::RowV<T> acc;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc.v[h] = c2::f4(0.f);
     int e = e0;
-    for (; e + 3 < e1; e += 4) {
-      const int j0 = col[e], j1 = col[e + 1], j2 = col[e + 2], j3 = col[e + 3];
-      const float v0 = val[e], v1 = val[e + 1], v2 = val[e + 2], v3 = val[e + 3];
-      float4 x0 = *(const float4*)(X + (long)j0 * d + c);
-      float4 x1 = *(const float4*)(X + (long)j1 * d + c);
-      float4 x2 = *(const float4*)(X + (long)j2 * d + c);
-      float4 x3 = *(const float4*)(X + (long)j3 * d + c);
-      if (!MASK_OUT && drop.active()) {
-        const uint64_t b0 = (uint64_t)j0 * d + c, b1 = (uint64_t)j1 * d + c;
-        const uint64_t b2 = (uint64_t)j2 * d + c, b3 = (uint64_t)j3 * d + c;
-        x0 = x0 * drop.mul4(b0);
-        x1 = x1 * drop.mul4(b1);
-        x2 = x2 * drop.mul4(b2);
-        x3 = x3 * drop.mul4(b3);
+    // UE rows in flight per lane group (most rows of a Zipf item graph have one or two edges: deeper batches only
+    // push edges into the one-at-a-time tail)
+    constexpr int UE = 4;
+    for (; e + UE - 1 < e1; e += UE) {
+      int j[UE];
+      float vv[UE];
+#pragma unroll
+      for (int u = 0; u < UE; ++u) {
+        j[u] = col[e + u];
+        vv[u] = val[e + u];
       }
-      acc = c2::fma4(v0, x0, acc);
-      acc = c2::fma4(v1, x1, acc);
-      acc = c2::fma4(v2, x2, acc);
-      acc = c2::fma4(v3, x3, acc);
+      c2::RowV<T> x[UE];
+#pragma unroll
+      for (int u = 0; u < UE; ++u) x[u] = c2::ldv(X + (long)j[u] * d + c);
+      if (!MASK_OUT && drop.active()) {
+#pragma unroll
+        for (int u = 0; u < UE; ++u)
+#pragma unroll
+          for (int h = 0; h < NH; ++h) x[u].v[h] = x[u].v[h] * drop.mul4((uint64_t)j[u] * d + c + 4 * h);
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int u = 0; u < UE; ++u) acc.v[h] = c2::fma4(vv[u], x[u].v[h], acc.v[h]);
     }
     for (; e < e1; ++e) {
       const int j = col[e];
-      float4 x = *(const float4*)(X + (long)j * d + c);
-      if (!MASK_OUT && drop.active()) {
-        const uint64_t b = (uint64_t)j * d + c;
-        x = x * drop.mul4(b);
+      c2::RowV<T> x = c2::ldv(X + (long)j * d + c);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        if (!MASK_OUT && drop.active()) x.v[h] = x.v[h] * drop.mul4((uint64_t)j * d + c + 4 * h);
+        acc.v[h] = c2::fma4(val[e], x.v[h], acc.v[h]);
       }
-      acc = c2::fma4(val[e], x, acc);
     }
-    if (slot >= 0)
-      *(float4*)(part + (long)slot * d + c) = acc;
-    else
+    if (slot >= 0) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) *(float4*)(part + (long)slot * d + c + 4 * h) = acc.v[h];
+    } else {
       epilogue<MASK_OUT>(acc, row, c, d, ep);
+    }
   }
 }
 
@@ -103,49 +125,56 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work
 #endif
 
 // split[s] = {row, slot_begin, slot_end}: sum the row's pieces in order, then the epilogue.
-template <int LPR, bool MASK_OUT>
-__global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ split, int n_split, int d, Epi ep,
+template <int LPR, bool MASK_OUT, typename T>
+__global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ split, int n_split, int d, Epi<T> ep,
                                                       const float* __restrict__ part) {
   constexpr int GROUPS = 256 / LPR;
+  constexpr int V = c2::VW<T>, NH = V / 4;
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
   const long s = (long)blockIdx.x * GROUPS + g;
   if (s >= n_split) return;
   const int4 sp = split[s];
-  for (int c = lane * 4; c < d; c += LPR * 4) {
-    float4 acc = c2::f4(0.f);
-    int k = sp.y;
-    // A hub row's combine is a latency chain (up to ~200 pieces at bench sizes): COMBINE_U pieces' loads in
-    // flight per round trip, then eight, added in piece order either way.
-    for (; k + COMBINE_U <= sp.z; k += COMBINE_U) {
-      float4 v[COMBINE_U];
+  for (int c0 = lane * V; c0 < d; c0 += LPR * V) {
+    c2::RowV<T> res;
 #pragma unroll
-      for (int u = 0; u < COMBINE_U; ++u) v[u] = *(const float4*)(part + (long)(k + u) * d + c);
+    for (int h = 0; h < NH; ++h) {
+      const int c = c0 + 4 * h;
+      float4 acc = c2::f4(0.f);
+      int k = sp.y;
+      // A hub row's combine is a latency chain (up to ~200 pieces at bench sizes): COMBINE_U pieces' loads in
+      // flight per round trip, then eight, added in piece order either way.
+      for (; k + COMBINE_U <= sp.z; k += COMBINE_U) {
+        float4 v[COMBINE_U];
 #pragma unroll
-      for (int u = 0; u < COMBINE_U; ++u) acc = acc + v[u];
+        for (int u = 0; u < COMBINE_U; ++u) v[u] = *(const float4*)(part + (long)(k + u) * d + c);
+#pragma unroll
+        for (int u = 0; u < COMBINE_U; ++u) acc = acc + v[u];
+      }
+      for (; k + 8 <= sp.z; k += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = *(const float4*)(part + (long)(k + u) * d + c);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + v[u];
+      }
+      for (; k < sp.z; ++k) acc = acc + *(const float4*)(part + (long)k * d + c);
+      res.v[h] = acc;
     }
-    for (; k + 8 <= sp.z; k += 8) {
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *(const float4*)(part + (long)(k + u) * d + c);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = acc + v[u];
-    }
-    for (; k < sp.z; ++k) acc = acc + *(const float4*)(part + (long)k * d + c);
-    epilogue<MASK_OUT>(acc, sp.x, c, d, ep);
+    epilogue<MASK_OUT>(res, sp.x, c0, d, ep);
   }
 }
 
 int lpr_for(int d) { return d / 4 >= 64 ? 64 : (d / 4 >= 32 ? 32 : (d / 4 >= 16 ? 16 : (d / 4 >= 8 ? 8 : 4))); }
 
-template <bool MASK_OUT>
+template <bool MASK_OUT, typename T>
 int launch(const int4* work, int n_work, const int4* split, int n_split, const int* col, const float* val, int d,
-           const float* X, const Epi& ep, float* part, hipStream_t s) {
-  const int lpr = lpr_for(d);
+           const T* X, const Epi<T>& ep, float* part, hipStream_t s) {
+  const int lpr = lpr_for(d * 4 / c2::VW<T>);  // lanes per row: VW elements each
   const int groups = 256 / lpr;
 #define C2_SPMM(L)                                                                                              \
-  spmm_kernel<L, MASK_OUT><<<c2::ceil_div(n_work, groups), 256, 0, s>>>(work, n_work, col, val, d, X, ep, part); \
-  if (n_split > 0) combine_kernel<L, MASK_OUT><<<c2::ceil_div(n_split, groups), 256, 0, s>>>(split, n_split, d, ep, part);
+  spmm_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_work, groups), 256, 0, s>>>(work, n_work, col, val, d, X, ep, part); \
+  if (n_split > 0) combine_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_split, groups), 256, 0, s>>>(split, n_split, d, ep, part);
   switch (lpr) {
     case 64: C2_SPMM(64) break;
     case 32: C2_SPMM(32) break;
@@ -160,15 +189,33 @@ int launch(const int4* work, int n_work, const int4* split, int n_split, const i
 
 }  // namespace
 
-C2_API int c2dsr_gcn_spmm(const int* work, int n_work, const int* split, int n_split, float* part, const int* col,
-                          const float* val, int d, const float* X, uint32_t k0, uint32_t k1, float p,
-                          int mask_on_output, float alpha, const float* Z, float beta, float delta, int pad_row,
-                          float gamma, float* Y, float* Y2, void* stream) {
-  if (d % 4) return (int)hipErrorInvalidValue;
+template <typename T>
+int gcn_spmm(const int* work, int n_work, const int* split, int n_split, float* part, const int* col, const float* val,
+             int d, const T* X, uint32_t k0, uint32_t k1, float p, int mask_on_output, float alpha, const T* Z,
+             float beta, float delta, int pad_row, float gamma, T* Y, T* Y2, void* stream) {
+  if (d % c2::VW<T>) return (int)hipErrorInvalidValue;
   if (n_work == 0) return 0;
-  Epi ep{alpha, Z, beta, delta, pad_row, gamma, Y, Y2, c2::make_drop(k0, k1, p)};
+  Epi<T> ep{alpha, Z, beta, delta, pad_row, gamma, Y, Y2, c2::make_drop(k0, k1, p)};
   hipStream_t s = (hipStream_t)stream;
   if (mask_on_output)
     return launch<true>((const int4*)work, n_work, (const int4*)split, n_split, col, val, d, X, ep, part, s);
   return launch<false>((const int4*)work, n_work, (const int4*)split, n_split, col, val, d, X, ep, part, s);
+}
+
+C2_API int c2dsr_gcn_spmm(const int* work, int n_work, const int* split, int n_split, float* part, const int* col,
+                          const float* val, int d, const float* X, uint32_t k0, uint32_t k1, float p,
+                          int mask_on_output, float alpha, const float* Z, float beta, float delta, int pad_row,
+                          float gamma, float* Y, float* Y2, void* stream) {
+  return gcn_spmm<float>(work, n_work, split, n_split, part, col, val, d, X, k0, k1, p, mask_on_output, alpha, Z, beta,
+                         delta, pad_row, gamma, Y, Y2, stream);
+}
+
+// the same on bf16 tables X, Z, Y, Y2 (fp32 arithmetic and partial slab, RNE stores): the C5 roofline run
+C2_API int c2dsr_gcn_spmm_b16(const int* work, int n_work, const int* split, int n_split, float* part, const int* col,
+                              const float* val, int d, const void* X, uint32_t k0, uint32_t k1, float p,
+                              int mask_on_output, float alpha, const void* Z, float beta, float delta, int pad_row,
+                              float gamma, void* Y, void* Y2, void* stream) {
+  return gcn_spmm<c2::tbf16>(work, n_work, split, n_split, part, col, val, d, (const c2::tbf16*)X, k0, k1, p,
+                             mask_on_output, alpha, (const c2::tbf16*)Z, beta, delta, pad_row, gamma, (c2::tbf16*)Y,
+                             (c2::tbf16*)Y2, stream);
 }

@@ -491,7 +491,8 @@ def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, p
     if rows is not None:
         w0, w1, s0, s1 = graph.row_slice(transposed, *rows)
         work, n_work, split, n_split = work[w0:w1], w1 - w0, split[s0:s1], s1 - s0
-    lib('c2dsr_gcn_spmm', work, n_work, split, n_split, part, col, val, d, X, keys[0], keys[1], float(p),
+    name = 'c2dsr_gcn_spmm_b16' if X.dtype == torch.bfloat16 else 'c2dsr_gcn_spmm'  # bf16 tables: the C5 run
+    lib(name, work, n_work, split, n_split, part, col, val, d, X, keys[0], keys[1], float(p),
         int(mask_on_output), float(alpha), Z, float(beta), float(delta), int(pad_row), float(gamma), Y, Y2, stream())
     return part
 

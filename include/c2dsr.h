@@ -37,6 +37,12 @@ int c2dsr_gcn_spmm(const int* work, int n_work, const int* split, int n_split, f
                    const float* val, int d, const float* X, uint32_t k0, uint32_t k1, float p, int mask_on_output,
                    float alpha, const float* Z, float beta, float delta, int pad_row, float gamma, float* Y, float* Y2,
                    void* stream);
+/* The same on bf16 tables X, Z, Y, Y2 (fp32 arithmetic and partial slab, RNE stores): the C5 roofline run's
+ * [20M, 512] tables ("bf16 tables"). */
+int c2dsr_gcn_spmm_b16(const int* work, int n_work, const int* split, int n_split, float* part, const int* col,
+                       const float* val, int d, const void* X, uint32_t k0, uint32_t k1, float p, int mask_on_output,
+                       float alpha, const void* Z, float beta, float delta, int pad_row, float gamma, void* Y, void* Y2,
+                       void* stream);
 
 /* K2 embedding fuse.  Replaces models/C2DSR.py:65-71,81-82 + models/encoders.py:30-31:
  *   X[r] = drop((H[seq[r]] + E[seq[r]])·scale + P[pos[r]])      (Xin == NULL)
@@ -61,6 +67,14 @@ size_t c2dsr_plan_err_offset(int n);
 int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
                             uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items,
                             float* gP, int n_pos, float* gXin, void* workspace, size_t ws_bytes, void* stream);
+/* bf16 item tables (the C5 roofline run): the gather reads bf16 H / E rows; the item segment sums
+ * read-modify-write a bf16 G (fp32 sums, RNE stores).  P, X, gX and gP stay fp32. */
+int c2dsr_embed_fwd_b16(const int64_t* seq, const int64_t* pos, int n_rows, int d, const void* H, const void* E,
+                        const float* P, float scale, uint32_t k0, uint32_t k1, float p, int64_t idx_base, float* X,
+                        void* stream);
+int c2dsr_embed_bwd_planned_b16(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
+                                uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, void* G, int n_items,
+                                float* gP, int n_pos, void* workspace, size_t ws_bytes, void* stream);
 /* The same with gX given as two compact row sources (the row-subset attention layer's input gradient: query
  * rows + key rows, never combined into a full [n_rows, d] tensor): row r of gX = (inv_a[r] >= 0 ?
  * gXa[inv_a[r]] : 0) + (inv_b[r] >= 0 ? gXb[inv_b[r]] : 0). */

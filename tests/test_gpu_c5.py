@@ -24,6 +24,12 @@ def rel(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
+def rel_dev(a, b):
+    """rel() of two large device tensors, computed on the device."""
+    a, b = a.float(), b.float()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
 def test_c5_gcn_and_embedding_at_20m_rows():
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
@@ -113,3 +119,68 @@ def test_c5_gcn_and_embedding_at_20m_rows():
         want.append(w)
     got = E.grad[torch.from_numpy(e_rows).to(DEV)].double().cpu().numpy()
     assert rel(got, np.stack(want)) < 1e-5, 'table gradient (direct lookups + GCN backward through A^T)'
+
+
+def test_c5_bf16_table_kernels_match_fp32():
+    """The C5 roofline run's bf16-table kernels (c2dsr_gcn_spmm_b16, c2dsr_embed_fwd_b16,
+    c2dsr_embed_bwd_planned_b16; SURVEY.md §8(d): "bf16 tables") against the fp32 kernels on the same
+    (bf16-representable) inputs, at d = 512, L = 100 on a 2,000,001-row table: the arithmetic is fp32 in both,
+    so each bf16 result is the fp32 result rounded once (≤ 2^-8 relative) — the gather, whose inputs are the
+    same values, is bit-identical — and the five passes' segment sums into a bf16 G round once per pass."""
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import ops, synth
+    from c2dsr_amd._lib import lib, stream
+    n_a = n_b = 1_000_000
+    d, L, B = 512, 100, 128
+    N = n_a + n_b + 1
+    pad = N - 1
+    items, off = synth.make_flat_sequences(100_000, n_a, n_b, L, seed=2)
+    seq_id = np.repeat(np.arange(off.size - 1, dtype=np.int64), np.diff(off))
+    same = seq_id[1:] == seq_id[:-1]
+    g = GR.normalized_csr(np.stack([items[:-1][same], items[1:][same]], 1), N)
+    seqs = [items[off[i]:off[i + 1]].tolist() for i in range(2 * B)]
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, n_a, n_b, L))
+    b = [torch.from_numpy(r[:B].copy()).to(DEV) for r in rows]
+    dg = GR.DeviceGraph(g, DEV)
+    torch.manual_seed(0)
+    E16 = torch.empty(N, d, device=DEV, dtype=torch.bfloat16).normal_(0.0, 0.1)
+    E32 = E16.float()
+    keys, p = (11, 22), 0.2
+    H16, H32 = torch.empty_like(E16), torch.empty_like(E32)
+    ops.spmm(dg, False, E16, keys, p, 0, 0.5, E16, 0.5, 0.0, -1, 0.0, H16)
+    ops.spmm(dg, False, E32, keys, p, 0, 0.5, E32, 0.5, 0.0, -1, 0.0, H32)
+    assert rel_dev(H16, H32) < 2 ** -8, 'GCN forward on bf16 tables'
+    P = torch.empty(L, d, device=DEV).normal_(0.0, 0.1)
+    passes = [(b[0], b[3]), (b[1], b[4]), (b[2], b[5]), (b[12], b[3]), (b[13], b[3])]
+    Hr = H16.float()
+    for k, (seq, pos) in enumerate(passes):
+        x16, x32 = torch.empty(B, L, d, device=DEV), torch.empty(B, L, d, device=DEV)
+        lib('c2dsr_embed_fwd_b16', seq, pos, B * L, d, H16, E16, P, math.sqrt(d), 5, k, p, 0, x16, stream())
+        lib('c2dsr_embed_fwd', seq, pos, B * L, d, Hr, E32, None, P, math.sqrt(d), 5, k, p, 0, x32, stream())
+        assert torch.equal(x16, x32), f'gather on bf16 tables, pass {k}'
+    gx = torch.empty(B, L, d, device=DEV).normal_(0.0, 1.0)
+    G16, G32 = torch.zeros_like(E16), torch.zeros_like(E32)
+    gP16, gP32 = torch.zeros_like(P), torch.zeros_like(P)
+    ws_bytes = int(lib.raw('c2dsr_embed_bwd_planned_workspace')(B * L, d))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=DEV)
+    plans = ops.IndexPlan.many([(seq, N) for seq, _ in passes] + [(pos, L) for _, pos in passes])
+    for k in range(len(passes)):
+        sp, pp = plans[k].get(), plans[len(passes) + k].get()
+        lib('c2dsr_embed_bwd_planned_b16', sp, pp, B * L, d, gx, 5, k, p, 0, math.sqrt(d), G16, N, gP16, L, ws,
+            ws_bytes, stream())
+        lib('c2dsr_embed_bwd_planned', sp, pp, B * L, d, gx, 5, k, p, 0, math.sqrt(d), G32, N, gP32, L, None, ws,
+            ws_bytes, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(gP16, gP32), 'position sums (fp32 in both)'
+    touched = torch.unique(torch.cat([s.reshape(-1) for s, _ in passes]))
+    assert rel_dev(G16[touched], G32[touched]) < 5 * 2 ** -8, 'segment sums into a bf16 table'
+    untouched = torch.ones(N, dtype=torch.bool, device=DEV)
+    untouched[touched] = False
+    assert not G16[untouched].any()
+    gE16, gE32 = torch.zeros_like(E16), torch.zeros_like(E32)
+    Gr = G16.float()
+    ops.spmm(dg, True, G16, keys, p, 1, 0.5, G16, 0.5, 1.0, pad, 1.0, gE16)
+    ops.spmm(dg, True, Gr, keys, p, 1, 0.5, Gr, 0.5, 1.0, pad, 1.0, gE32)
+    assert rel_dev(gE16, gE32) < 2 ** -8, 'GCN backward on bf16 tables'
