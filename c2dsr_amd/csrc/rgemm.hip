@@ -467,10 +467,11 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
       }
     }
   };
-  float4 Pa[8], Pb[8];
+  float4 Pa[8], Pb[8], Pc[8];
   load(0, Pa);
   load(1, Pb);
-  // the weight fragments are fetched (L2) while the first two A chunks are in flight (HBM)
+  load(2, Pc);
+  // the weight fragments are fetched (L2) while the first A chunks are in flight (HBM)
   // B (split image) fragments → AGPRs: column ncol0 + 16cb + l16, k = 32ks + 8g
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
@@ -489,9 +490,9 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
   pre_tile(0);
   __syncthreads();
   // chunk c (k-chunk KC): MFMAs on image c&1 ∥ split of chunk c+1 (registers S) into image (c+1)&1; R is
-  // refilled with chunk c+2 first
+  // refilled with chunk c+3 first (three register sets: a staged chunk was loaded two steps earlier)
   auto step = [&]<int KC>(int c, float4 (&R)[8], float4 (&S)[8]) {
-    load(c + 2, R);
+    load(c + 3, R);
     const int buf = c & 1, nb = (c + 1) & 1;
     const int tile = c / KCH;
     bf16x8 fr[4][2];
@@ -527,16 +528,18 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
     __syncthreads();
   };
   const int nchunk = ntile * KCH;
-  const int npair = (nchunk + 1) >> 1;
-  for (int i = 0; i < npair; ++i) {
-    const int c0 = 2 * i;
-    if constexpr (KCH == 1) {
-      step.template operator()<0>(c0, Pa, Pb);
-      step.template operator()<0>(c0 + 1, Pb, Pa);
-    } else {
-      step.template operator()<0>(c0, Pa, Pb);
-      step.template operator()<1>(c0 + 1, Pb, Pa);
-    }
+  for (int c0 = 0; c0 < nchunk; c0 += 6) {  // register sets rotate with period 3, k-chunks with period KCH
+    step.template operator()<0>(c0, Pa, Pb);
+    if (c0 + 1 >= nchunk) break;
+    step.template operator()<1 % KCH>(c0 + 1, Pb, Pc);
+    if (c0 + 2 >= nchunk) break;
+    step.template operator()<0>(c0 + 2, Pc, Pa);
+    if (c0 + 3 >= nchunk) break;
+    step.template operator()<1 % KCH>(c0 + 3, Pa, Pb);
+    if (c0 + 4 >= nchunk) break;
+    step.template operator()<0>(c0 + 4, Pb, Pc);
+    if (c0 + 5 >= nchunk) break;
+    step.template operator()<1 % KCH>(c0 + 5, Pc, Pa);
   }
 }
 
@@ -572,6 +575,9 @@ __device__ __forceinline__ bf16x8 tr32(const char* img, int rr0, int kb0, int la
 // encoder passes) walked as one virtual row range; segment k occupies virtual rows [vbeg[k], vbeg[k+1]) (its
 // T[k] rows padded to a multiple of 32, so no 32-row chunk straddles two segments or a split end).
 constexpr int WG_MAXSEG = 4;
+#ifndef WG_AHEAD
+#define WG_AHEAD 2  // chunks loaded ahead (3: three register sets — spills, 2.5x slower)
+#endif
 struct WSeg {
   const void* dY[WG_MAXSEG];
   const float* X[WG_MAXSEG];
@@ -677,7 +683,7 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
   const int wn = (w >> 1) * 64, wi = (w & 1) * 128;  // this wave's 64 n-rows and 128 i-columns
 #define WG_STEP(c, RY, RX, SY, SX)                                                                            \
   {                                                                                                           \
-    WG_LOAD((c) + 2, RY, RX)                                                                                  \
+    WG_LOAD((c) + WG_AHEAD, RY, RX)                                                                           \
     const char* yi_ = yimg[(c) & 1];                                                                          \
     const char* xi_ = ximg[(c) & 1];                                                                          \
     _Pragma("unroll") for (int kst = 0; kst < 2; ++kst) {                                                     \
@@ -700,6 +706,7 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
     __syncthreads();                                                                                          \
   }
   if (nchunk > 0) {
+#if WG_AHEAD == 2
     float4 Ya[4], Xa[8], Yb[4], Xb[8];
     WG_LOAD(0, Ya, Xa)
     WG_LOAD(1, Yb, Xb)
@@ -710,6 +717,23 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
       if (c + 1 >= nchunk) break;
       WG_STEP(c + 1, Yb, Xb, Ya, Xa)
     }
+#else
+    // three register sets: chunk c+3 is loaded at step c, so the staging of chunk c+1 (end of step c) waits on a
+    // load issued two steps earlier
+    float4 Ya[4], Xa[8], Yb[4], Xb[8], Yc[4], Xc[8];
+    WG_LOAD(0, Ya, Xa)
+    WG_LOAD(1, Yb, Xb)
+    WG_LOAD(2, Yc, Xc)
+    WG_STAGE(Ya, Xa, 0, 0)
+    __syncthreads();
+    for (int c = 0; c < nchunk; c += 3) {
+      WG_STEP(c, Ya, Xa, Yb, Xb)
+      if (c + 1 >= nchunk) break;
+      WG_STEP(c + 1, Yb, Xb, Yc, Xc)
+      if (c + 2 >= nchunk) break;
+      WG_STEP(c + 2, Yc, Xc, Ya, Xa)
+    }
+#endif
   }
 #undef WG_STEP
 #undef WG_STAGE

@@ -45,15 +45,17 @@ def wg_costs():
     from c2dsr_amd.ops import wgemm
     dev = torch.device('cuda')
     lib_ = os.path.basename(os.environ.get("C2DSR_LIB", "default"))
-    for T, N, b16 in ((38000, 256, False), (57000, 256, False), (38000, 256, True), (57000, 512, True)):
+    for T, N, kind in ((38000, 256, 'fp32'), (57000, 256, 'fp32'), (38000, 256, 'bf16'), (57000, 512, 'bf16'),
+                       (38000, 256, 'x3'), (57000, 256, 'x3'), (57000, 512, 'x3')):
         dY = torch.randn(T, N, device=dev)
-        if b16:
+        if kind == 'bf16':
             dY = dY.to(torch.bfloat16)
         X = torch.randn(T, 256, device=dev)
         dW = torch.zeros(N, 256, device=dev)
         db = torch.zeros(N, device=dev)
-        t = timeit(lambda: wgemm(dY, X, dW, T=T, N=N, D=256, db=db))
-        print(f'{lib_}: wgemm T {T} N {N} {"bf16" if b16 else "fp32"} dY: {t:6.1f} us', flush=True)
+        t = timeit(lambda: wgemm(dY, X, dW, T=T, N=N, D=256, db=db, x3=kind == 'x3'))
+        gb = (T * N * (2 if kind == 'bf16' else 4) + T * 256 * 4) / t / 1e3
+        print(f'{lib_}: wgemm T {T} N {N} {kind} dY: {t:6.1f} us {gb:6.0f} GB/s', flush=True)
 
 
 def main(x3=False):
