@@ -644,35 +644,7 @@ __device__ __forceinline__ void wave_softmax(f32x16& a, f32x16& b, int ti, const
 // Q rows of stride qs (nq of them), K / V rows of stride ks (nk), O rows of stride os.  Score tiles (tj, ti):
 // t0 = (0,0), t1 = (0,1), t2 = (1,1) and, in the row-subset layout only, t3 = (1,0) (in the full layout
 // it lies above the causal diagonal; compact queries can see keys of higher index).
-// X3: the two products on split-bf16 operands (hi = RNE(x), lo = RNE(x − hi); a·b ≈ a_hi·b_hi + a_lo·b_hi +
-// a_hi·b_lo in v_mfma_f32_32x32x16_bf16, fp32 accumulation, ≈3·2^-17 relative per term — ce3.hip) instead of the
-// fp32-input MFMA (v_mfma_f32_32x32x2_f32, 64 cycles per 4 Ki flops: the wave-per-sequence attention is bound by
-// it).  Same output layouts: the 32x32 accumulator layout does not depend on the MFMA's input type, and the
-// reduction index of P·V is permuted exactly as in the fp32 form (register 8s + j of a P tile ↔ key
-// creg(8s + j, lane), V loaded per lane in that order).
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ void split8(const float* x, bf16x8_t& h, bf16x8_t& l) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    h[j] = (__bf16)x[j];
-    l[j] = (__bf16)(x[j] - (float)h[j]);
-  }
-}
-__device__ __forceinline__ void split8v(const f32x16& x, int o, bf16x8_t& h, bf16x8_t& l) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    h[j] = (__bf16)x[o + j];
-    l[j] = (__bf16)(x[o + j] - (float)h[j]);
-  }
-}
-__device__ __forceinline__ f32x16 mfma_x3(const bf16x8_t& ah, const bf16x8_t& al, const bf16x8_t& bh,
-                                          const bf16x8_t& bl, f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, c, 0, 0, 0);
-}
-
-template <int TJ, int TI, bool ROWS, bool X3 = false>
+template <int TJ, int TI, bool ROWS>
 __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, long qs, const float* __restrict__ K,
                                               const float* __restrict__ V, long ks, int nq, int dh, int nk,
                                               const WMask& mk, const c2::Drop& drop, uint64_t pbase,
@@ -682,50 +654,7 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, long 
   f32x16 t0, t1, t2, t3;
 #pragma unroll
   for (int q = 0; q < 16; ++q) t0[q] = t1[q] = t2[q] = t3[q] = 0.f;
-  if constexpr (X3) {
-    // Sᵀ tiles over k-steps of 16 dims: lane (row r of a 32-row tile, half hi) holds dims 16s + 8hi .. +7
-    const auto qsrc = rows_rsrc(Q, nq, qs, dh);
-    const auto ksrc = rows_rsrc(K, nk, ks, dh);
-    const int q0o = (r * (int)qs + 8 * hi) * 4, q1o = ((32 + r) * (int)qs + 8 * hi) * 4;
-    const int k0o = (r * (int)ks + 8 * hi) * 4, k1o = ((32 + r) * (int)ks + 8 * hi) * 4;
-    const int KST = dh >> 4;
-    auto load = [&](float (&b)[4][8], int st) {  // [k0, k1, q0, q1]
-      const int co = 64 * st;
-      const int off[4] = {k0o + co, k1o + co, q0o + co, q1o + co};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool use = i == 0 || i == 2 || (i == 1 && TJ > 1) || (i == 3 && TI > 1);
-        float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
-        if (use) {
-          u = ld_b128(i < 2 ? ksrc : qsrc, off[i], 0);
-          v = ld_b128(i < 2 ? ksrc : qsrc, off[i] + 16, 0);
-        }
-        b[i][0] = u.x; b[i][1] = u.y; b[i][2] = u.z; b[i][3] = u.w;
-        b[i][4] = v.x; b[i][5] = v.y; b[i][6] = v.z; b[i][7] = v.w;
-      }
-    };
-    auto mma = [&](const float (&b)[4][8]) {
-      bf16x8_t h[4], l[4];
-      split8(b[0], h[0], l[0]);
-      split8(b[2], h[2], l[2]);
-      if constexpr (TJ > 1) split8(b[1], h[1], l[1]);
-      if constexpr (TI > 1) split8(b[3], h[3], l[3]);
-      t0 = mfma_x3(h[0], l[0], h[2], l[2], t0);
-      if constexpr (T3) t3 = mfma_x3(h[1], l[1], h[2], l[2], t3);
-      if constexpr (TI > 1) t1 = mfma_x3(h[0], l[0], h[3], l[3], t1);
-      if constexpr (TI > 1 && TJ > 1) t2 = mfma_x3(h[1], l[1], h[3], l[3], t2);
-    };
-    float ba[4][8], bb[4][8];
-    load(ba, 0);
-#pragma unroll 1
-    for (int st = 0; st < KST; st += 2) {
-      if (st + 1 < KST) load(bb, st + 1);
-      mma(ba);
-      if (st + 1 >= KST) break;
-      if (st + 2 < KST) load(ba, st + 2);
-      mma(bb);
-    }
-  } else {
+  {
     const auto qsrc = rows_rsrc(Q, nq, qs, dh);
     const auto ksrc = rows_rsrc(K, nk, ks, dh);
     const int q0o = (r * (int)qs + 4 * hi) * 4, q1o = ((32 + r) * (int)qs + 4 * hi) * 4;
@@ -784,43 +713,17 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, long 
                        : 0.f;
     }
   };
-  // X3: the P tiles as split-bf16 A fragments, k-steps s = registers 8s .. 8s+7
-  bf16x8_t ph[4][2], pl[4][2];
-  if constexpr (X3) {
-#pragma unroll
-    for (int sidx = 0; sidx < 2; ++sidx) {
-      split8v(t0, 8 * sidx, ph[0][sidx], pl[0][sidx]);
-      if constexpr (T3) split8v(t3, 8 * sidx, ph[3][sidx], pl[3][sidx]);
-      if constexpr (TI > 1) split8v(t1, 8 * sidx, ph[1][sidx], pl[1][sidx]);
-      if constexpr (TI > 1 && TJ > 1) split8v(t2, 8 * sidx, ph[2][sidx], pl[2][sidx]);
-    }
-  }
   auto otile = [&](const float (&v)[2][16], int ct) {
     f32x16 o0, o1;
 #pragma unroll
     for (int q = 0; q < 16; ++q) o0[q] = o1[q] = 0.f;
-    if constexpr (X3) {
 #pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx) {
-        bf16x8_t vh0, vl0, vh1, vl1;
-        split8(&v[0][8 * sidx], vh0, vl0);
-        if constexpr (TJ > 1) split8(&v[1][8 * sidx], vh1, vl1);
-        o0 = mfma_x3(ph[0][sidx], pl[0][sidx], vh0, vl0, o0);
-        if constexpr (T3) o0 = mfma_x3(ph[3][sidx], pl[3][sidx], vh1, vl1, o0);
-        if constexpr (TI > 1) {
-          o1 = mfma_x3(ph[1][sidx], pl[1][sidx], vh0, vl0, o1);
-          if constexpr (TJ > 1) o1 = mfma_x3(ph[2][sidx], pl[2][sidx], vh1, vl1, o1);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        o0 = WMFMA(t0[q], v[0][q], o0, 0, 0, 0);
-        if constexpr (T3) o0 = WMFMA(t3[q], v[1][q], o0, 0, 0, 0);
-        if constexpr (TI > 1) {
-          o1 = WMFMA(t1[q], v[0][q], o1, 0, 0, 0);
-          if constexpr (TJ > 1) o1 = WMFMA(t2[q], v[1][q], o1, 0, 0, 0);
-        }
+    for (int q = 0; q < 16; ++q) {
+      o0 = WMFMA(t0[q], v[0][q], o0, 0, 0, 0);
+      if constexpr (T3) o0 = WMFMA(t3[q], v[1][q], o0, 0, 0, 0);
+      if constexpr (TI > 1) {
+        o1 = WMFMA(t1[q], v[0][q], o1, 0, 0, 0);
+        if constexpr (TJ > 1) o1 = WMFMA(t2[q], v[1][q], o1, 0, 0, 0);
       }
     }
     const int c = 32 * ct + r;
@@ -910,7 +813,6 @@ __device__ __forceinline__ WMask rows_mask(const int64_t* __restrict__ seq, int6
 #ifndef ATTN_ROWS_OCC_F
 #define ATTN_ROWS_OCC_F ATTN_ROWS_OCC
 #endif
-template <bool X3>
 __global__ __launch_bounds__(256, ATTN_ROWS_OCC_F) void attn_fwd_rows(const float* __restrict__ q, const float* __restrict__ kv,
                                                      const int64_t* __restrict__ seq, int64_t pad,
                                                      const int* __restrict__ q_idx, const int* __restrict__ q_off,
@@ -930,13 +832,13 @@ __global__ __launch_bounds__(256, ATTN_ROWS_OCC_F) void attn_fwd_rows(const floa
   float* prow = Psave + (long)bh * WAVE_PSAVE;
   const int TJ = nk > 32 ? 2 : 1, TI = nq > 32 ? 2 : 1;
   if (TI == 1 && TJ == 1)
-    fwd_wave_body<1, 1, true, X3>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
+    fwd_wave_body<1, 1, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
   else if (TI == 1)
-    fwd_wave_body<2, 1, true, X3>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
+    fwd_wave_body<2, 1, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
   else if (TJ == 1)
-    fwd_wave_body<1, 2, true, X3>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
+    fwd_wave_body<1, 2, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
   else
-    fwd_wave_body<2, 2, true, X3>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
+    fwd_wave_body<2, 2, true>(Q, d, K, K + d, 2l * d, nq, dh, nk, mk, drop, pbase, orow, d, prow);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -964,7 +866,7 @@ __device__ __forceinline__ void zero16(f32x16& a) {
 // read them as a bf16 MFMA operand anyway: c2dsr_attn_bwd_b16).  Strides: Q qs, K / V ks, dO ds, dQ dqs,
 // dK / dV dks; nkw: key rows of dK / dV to write (rows past the key tiles get zeros).  Tiles as in
 // fwd_wave_body (g3 = (1,0) in the row-subset layout only).
-template <int TJ, int TI, typename OT, bool ROWS, bool X3 = false>
+template <int TJ, int TI, typename OT, bool ROWS>
 __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long qs, const float* __restrict__ K,
                                               const float* __restrict__ V, long ks, const float* __restrict__ dO,
                                               long ds, int nq, int dh, int nk, const WMask& mk,
@@ -976,39 +878,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
   // ---- dPᵀ tiles (tj, ti): 0 = (0,0), 1 = (0,1), 2 = (1,1), 3 = (1,0)
   f32x16 g0, g1, g2, g3;
   zero16(g0); zero16(g1); zero16(g2); zero16(g3);
-  if constexpr (X3) {  // the forward's split-bf16 Sᵀ loop on (V, dO): lane holds dims 16st + 8hi .. +7
-    const auto vsrc = rows_rsrc(V, nk, ks, dh);
-    const auto osrc = rows_rsrc(dO, nq, ds, dh);
-    const int v0o = (r * (int)ks + 8 * hi) * 4, v1o = ((32 + r) * (int)ks + 8 * hi) * 4;
-    const int o0o = (r * (int)ds + 8 * hi) * 4, o1o = ((32 + r) * (int)ds + 8 * hi) * 4;
-    const int KST = dh >> 4;
-#pragma unroll 1
-    for (int st = 0; st < KST; ++st) {
-      const int co = 64 * st;
-      float b[4][8];
-      const int off[4] = {v0o + co, v1o + co, o0o + co, o1o + co};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool use = i == 0 || i == 2 || (i == 1 && TJ > 1) || (i == 3 && TI > 1);
-        float4 u = make_float4(0.f, 0.f, 0.f, 0.f), w = u;
-        if (use) {
-          u = ld_b128(i < 2 ? vsrc : osrc, off[i], 0);
-          w = ld_b128(i < 2 ? vsrc : osrc, off[i] + 16, 0);
-        }
-        b[i][0] = u.x; b[i][1] = u.y; b[i][2] = u.z; b[i][3] = u.w;
-        b[i][4] = w.x; b[i][5] = w.y; b[i][6] = w.z; b[i][7] = w.w;
-      }
-      bf16x8_t h[4], l[4];
-      split8(b[0], h[0], l[0]);
-      split8(b[2], h[2], l[2]);
-      if constexpr (TJ > 1) split8(b[1], h[1], l[1]);
-      if constexpr (TI > 1) split8(b[3], h[3], l[3]);
-      g0 = mfma_x3(h[0], l[0], h[2], l[2], g0);
-      if constexpr (T3) g3 = mfma_x3(h[1], l[1], h[2], l[2], g3);
-      if constexpr (TI > 1) g1 = mfma_x3(h[0], l[0], h[3], l[3], g1);
-      if constexpr (TI > 1 && TJ > 1) g2 = mfma_x3(h[1], l[1], h[3], l[3], g2);
-    }
-  } else {
+  {
     const auto vsrc = rows_rsrc(V, nk, ks, dh);
     const auto osrc = rows_rsrc(dO, nq, ds, dh);
     const int v0o = (r * (int)ks + 4 * hi) * 4, v1o = ((32 + r) * (int)ks + 4 * hi) * 4;
@@ -1084,16 +954,6 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
   }
   const float sc = 1.0f / sqrtf((float)dh);
   const int CT = dh >> 5;
-  bf16x8_t gh[4][2], gl[4][2];  // X3: the dS tiles as split-bf16 A fragments (registers 8s .. 8s+7)
-  if constexpr (X3) {
-#pragma unroll
-    for (int sidx = 0; sidx < 2; ++sidx) {
-      split8v(g0, 8 * sidx, gh[0][sidx], gl[0][sidx]);
-      if constexpr (T3) split8v(g3, 8 * sidx, gh[3][sidx], gl[3][sidx]);
-      if constexpr (TI > 1) split8v(g1, 8 * sidx, gh[1][sidx], gl[1][sidx]);
-      if constexpr (TI > 1 && TJ > 1) split8v(g2, 8 * sidx, gh[2][sidx], gl[2][sidx]);
-    }
-  }
   // ---- dQ = dS·K/√dh (lane = column, rows = queries)
   {
     const auto ksrc = rows_rsrc(K, nk, ks, dh);
@@ -1110,28 +970,13 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
       }
       f32x16 o0, o1;
       zero16(o0); zero16(o1);
-      if constexpr (X3) {
 #pragma unroll
-        for (int sidx = 0; sidx < 2; ++sidx) {
-          bf16x8_t kh0, kl0, kh1, kl1;
-          split8(&k0v[8 * sidx], kh0, kl0);
-          if constexpr (TJ > 1) split8(&k1v[8 * sidx], kh1, kl1);
-          o0 = mfma_x3(gh[0][sidx], gl[0][sidx], kh0, kl0, o0);
-          if constexpr (T3) o0 = mfma_x3(gh[3][sidx], gl[3][sidx], kh1, kl1, o0);
-          if constexpr (TI > 1) {
-            o1 = mfma_x3(gh[1][sidx], gl[1][sidx], kh0, kl0, o1);
-            if constexpr (TJ > 1) o1 = mfma_x3(gh[2][sidx], gl[2][sidx], kh1, kl1, o1);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          o0 = WMFMA(g0[q], k0v[q], o0, 0, 0, 0);
-          if constexpr (T3) o0 = WMFMA(g3[q], k1v[q], o0, 0, 0, 0);
-          if constexpr (TI > 1) {
-            o1 = WMFMA(g1[q], k0v[q], o1, 0, 0, 0);
-            if constexpr (TJ > 1) o1 = WMFMA(g2[q], k1v[q], o1, 0, 0, 0);
-          }
+      for (int q = 0; q < 16; ++q) {
+        o0 = WMFMA(g0[q], k0v[q], o0, 0, 0, 0);
+        if constexpr (T3) o0 = WMFMA(g3[q], k1v[q], o0, 0, 0, 0);
+        if constexpr (TI > 1) {
+          o1 = WMFMA(g1[q], k0v[q], o1, 0, 0, 0);
+          if constexpr (TJ > 1) o1 = WMFMA(g2[q], k1v[q], o1, 0, 0, 0);
         }
       }
       const int c = 32 * ct + r;
@@ -1174,27 +1019,11 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
         zero16(o);
 #pragma unroll
         for (int ti = ROWS ? 0 : tj; ti < TI; ++ti) {
-          if constexpr (X3) {
 #pragma unroll
-            for (int sidx = 0; sidx < 2; ++sidx) {
-              float av[8];
-#pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const int q = 8 * sidx + j;
-                av[j] = T[(32 * ti + (q & 3) + 8 * (q >> 2) + 4 * hi) * TLD + 32 * tj + r];
-              }
-              bf16x8_t ah, al, bh, bl;
-              split8(av, ah, al);
-              split8(ti ? &b1v[8 * sidx] : &b0v[8 * sidx], bh, bl);
-              o = mfma_x3(ah, al, bh, bl, o);
-            }
-          } else {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-              const int qi = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * hi;
-              const float a = T[qi * TLD + 32 * tj + r];
-              o = WMFMA(a, ti ? b1v[q] : b0v[q], o, 0, 0, 0);
-            }
+          for (int q = 0; q < 16; ++q) {
+            const int qi = 32 * ti + (q & 3) + 8 * (q >> 2) + 4 * hi;
+            const float a = T[qi * TLD + 32 * tj + r];
+            o = WMFMA(a, ti ? b1v[q] : b0v[q], o, 0, 0, 0);
           }
         }
 #pragma unroll
@@ -1253,7 +1082,7 @@ __global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ q
 #undef BWD_FULL
 }
 
-template <typename OT, bool X3 = false>
+template <typename OT>
 __global__ __launch_bounds__(256, ATTN_ROWS_OCC) void attn_bwd_rows(const float* __restrict__ q, const float* __restrict__ kv,
                                                      const int64_t* __restrict__ seq, int64_t pad,
                                                      const int* __restrict__ q_idx, const int* __restrict__ q_off,
@@ -1285,8 +1114,8 @@ __global__ __launch_bounds__(256, ATTN_ROWS_OCC) void attn_bwd_rows(const float*
   const float* prow = Psave + (long)bh * WAVE_PSAVE;
   const int TJ = nk > 32 ? 2 : 1, TI = nq > 32 ? 2 : 1;
 #define BWD_ROWS(TJ_, TI_)                                                                                     \
-  bwd_wave_body<TJ_, TI_, OT, true, X3>(Q, d, K, K + d, 2l * d, dO, d, nq, dh, nk, mk, drop, pbase, prow, dQ, d,  \
-                                        dK, dK + d, 2l * d, nk, tbuf[w])
+  bwd_wave_body<TJ_, TI_, OT, true>(Q, d, K, K + d, 2l * d, dO, d, nq, dh, nk, mk, drop, pbase, prow, dQ, d, dK,  \
+                                    dK + d, 2l * d, nk, tbuf[w])
   if (TI == 1 && TJ == 1)
     BWD_ROWS(1, 1);
   else if (TI == 1)
@@ -1424,20 +1253,7 @@ C2_API int c2dsr_attn_fwd_rows(const float* q, const float* kv, const int64_t* s
                                void* stream) {
   if (!c2dsr_attn_rows_supported(L, d, H)) return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
-  attn_fwd_rows<false><<<c2::ceil_div((long)B * H, 4), 256, 0, (hipStream_t)stream>>>(
-      q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, c2::make_drop(k0, k1, p), b_base, out, Psave);
-  C2_CHECK_LAUNCH();
-  return 0;
-}
-
-// the same with both products on split-bf16 operands (three bf16 MFMAs per fp32-accurate product)
-C2_API int c2dsr_attn_fwd_rows_x3(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
-                                  const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H,
-                                  uint32_t k0, uint32_t k1, float p, int64_t b_base, float* out, float* Psave,
-                                  void* stream) {
-  if (!c2dsr_attn_rows_supported(L, d, H) || (d / H) % 16) return (int)hipErrorInvalidValue;
-  if (B == 0) return 0;
-  attn_fwd_rows<true><<<c2::ceil_div((long)B * H, 4), 256, 0, (hipStream_t)stream>>>(
+  attn_fwd_rows<<<c2::ceil_div((long)B * H, 4), 256, 0, (hipStream_t)stream>>>(
       q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, c2::make_drop(k0, k1, p), b_base, out, Psave);
   C2_CHECK_LAUNCH();
   return 0;
@@ -1460,26 +1276,6 @@ C2_API int c2dsr_attn_bwd_rows(const float* q, const float* kv, const int64_t* s
   else
     attn_bwd_rows<float><<<grid, 256, 0, s>>>(q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, dr, b_base,
                                               Psave, dout, (float*)dq, (float*)dkv);
-  C2_CHECK_LAUNCH();
-  return 0;
-}
-
-// the same with the four products on split-bf16 operands (three bf16 MFMAs per fp32-accurate product)
-C2_API int c2dsr_attn_bwd_rows_x3(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
-                                  const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H,
-                                  uint32_t k0, uint32_t k1, float p, int64_t b_base, const float* Psave,
-                                  const float* dout, void* dq, void* dkv, int out_bf16, void* stream) {
-  if (!c2dsr_attn_rows_supported(L, d, H) || (d / H) % 16) return (int)hipErrorInvalidValue;
-  if (B == 0) return 0;
-  const c2::Drop dr = c2::make_drop(k0, k1, p);
-  const dim3 grid(c2::ceil_div((long)B * H, 4));
-  hipStream_t s = (hipStream_t)stream;
-  if (out_bf16)
-    attn_bwd_rows<bf16, true><<<grid, 256, 0, s>>>(q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, dr,
-                                                   b_base, Psave, dout, (bf16*)dq, (bf16*)dkv);
-  else
-    attn_bwd_rows<float, true><<<grid, 256, 0, s>>>(q, kv, seq, pad, q_idx, q_off, k_idx, k_off, B, L, d, H, dr,
-                                                    b_base, Psave, dout, (float*)dq, (float*)dkv);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -1084,9 +1084,7 @@ class RowsQKVAttnFn(Function):
         out = torch.empty(nq, d, device=x.device, dtype=torch.float32)
         P = torch.empty(int(lib.raw('c2dsr_attn_psave_floats')(B, L, d, n_head)), device=x.device,
                         dtype=torch.float32)
-        # both products on split-bf16 MFMAs (fp32-accurate, c2dsr_attn_fwd_rows_x3) except in the exact mode
-        name = 'c2dsr_attn_fwd_rows' if precision == FP32_EXACT or (d // n_head) % 16 else 'c2dsr_attn_fwd_rows_x3'
-        lib(name, q, kv, seq, int(pad), rs.idx, rs.off, ks.idx, ks.off, B, L, d, n_head, keys[0],
+        lib('c2dsr_attn_fwd_rows', q, kv, seq, int(pad), rs.idx, rs.off, ks.idx, ks.off, B, L, d, n_head, keys[0],
             keys[1], float(p), int(b_base), out, P, stream())
         ctx.save_for_backward(xc, xk, W, q, kv, seq, P)
         ctx.b, ctx.pad, ctx.n_head, ctx.p, ctx.keys, ctx.b_base = b, pad, n_head, p, keys, b_base
@@ -1105,9 +1103,7 @@ class RowsQKVAttnFn(Function):
         gt = torch.bfloat16 if b16 else torch.float32
         dq = torch.empty(nq, d, device=q.device, dtype=gt)
         dkv = torch.empty(nk, 2 * d, device=q.device, dtype=gt)
-        name = ('c2dsr_attn_bwd_rows' if ctx.precision == FP32_EXACT or (d // ctx.n_head) % 16
-                else 'c2dsr_attn_bwd_rows_x3')  # split-bf16 products, as the forward
-        lib(name, q, kv, seq, int(ctx.pad), rs.idx, rs.off, ks.idx, ks.off, B, L, d, ctx.n_head,
+        lib('c2dsr_attn_bwd_rows', q, kv, seq, int(ctx.pad), rs.idx, rs.off, ks.idx, ks.off, B, L, d, ctx.n_head,
             ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.b_base), P, dout.contiguous(), dq, dkv, int(b16), s)
         park = None
         if ctx.res is not None:

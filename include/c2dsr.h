@@ -132,20 +132,10 @@ int c2dsr_attn_rows_supported(int L, int d, int H);
 int c2dsr_attn_fwd_rows(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
                         const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H, uint32_t k0,
                         uint32_t k1, float p, int64_t b_base, float* out, float* Psave, void* stream);
-/* The same with both products (QKᵀ, P·V) on split-bf16 operands: three bf16 MFMAs per fp32-accurate product
- * (≈3·2^-17 relative per term, fp32 accumulation; the fp32-input MFMA bounds the plain form). */
-int c2dsr_attn_fwd_rows_x3(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
-                           const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H, uint32_t k0,
-                           uint32_t k1, float p, int64_t b_base, float* out, float* Psave, void* stream);
 int c2dsr_attn_bwd_rows(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
                         const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H, uint32_t k0,
                         uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout, void* dq,
                         void* dkv, int out_bf16, void* stream);
-/* The same with the four products (dPᵀ, dQ, dV, dK) on split-bf16 operands. */
-int c2dsr_attn_bwd_rows_x3(const float* q, const float* kv, const int64_t* seq, int64_t pad, const int* q_idx,
-                           const int* q_off, const int* k_idx, const int* k_off, int B, int L, int d, int H, uint32_t k0,
-                           uint32_t k1, float p, int64_t b_base, const float* Psave, const float* dout, void* dq,
-                           void* dkv, int out_bf16, void* stream);
 
 /* Residual + dropout + LayerNorm (TransformerEncoderLayer norm1/norm2, encoder.norm; eps 1e-8). */
 int c2dsr_add_ln_fwd(const float* a, const float* b, int rows, int d, uint32_t k0, uint32_t k1, float p,

@@ -858,20 +858,6 @@ def test_attention_rows_equals_full_layout(B, L, d, H, p, q_frac):
     assert torch.equal(dq16, dq.to(torch.bfloat16)) and torch.equal(dkv16, dkv.to(torch.bfloat16))
     # rows with no admissible key (no padding at or before them) are exactly 0 in both
     assert torch.equal(out_r[out[qL].abs().amax(1) == 0], torch.zeros_like(out_r[out[qL].abs().amax(1) == 0]))
-    # the split-bf16 form (c2dsr_attn_fwd_rows_x3, the fp32 mode's): output and saved probabilities within the
-    # x3 product error (≈3·2^-17 relative per term) of the exact fp32-MFMA kernel
-    out_x, Px = torch.empty_like(out_r), Pr.clone()  # (entries of tiles never computed stay as they are)
-    lib('c2dsr_attn_fwd_rows_x3', q, kv, sd, pad, rs.idx, rs.off, ks.idx, ks.off, B, L, d, H, 5, 6, p, 2, out_x, Px,
-        s)
-    torch.cuda.synchronize()
-    assert rel(out_x, out_r) < 2e-5
-    assert (Px - Pr).abs().max().item() < 2e-5
-    dqx = torch.full((len(qi), d), 7.0, device=DEV)
-    dkvx = torch.full((len(ki), 2 * d), 7.0, device=DEV)
-    lib('c2dsr_attn_bwd_rows_x3', q, kv, sd, pad, rs.idx, rs.off, ks.idx, ks.off, B, L, d, H, 5, 6, p, 2, Pr, dout_c,
-        dqx, dkvx, 0, s)
-    torch.cuda.synchronize()
-    assert rel(dqx, dq) < 5e-5 and rel(dkvx, dkv) < 5e-5
 
 
 @pytest.mark.parametrize('K,aux', [(256, 0), (256, 1), (512, 0)])
