@@ -134,8 +134,13 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
   __shared__ __attribute__((aligned(16))) float wv[NB][4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
-  const int s0 = blockIdx.x * 128 + w * 32 + l16;  // stationary rows s0 (sb 0), s0 + 16 (sb 1)
-  const int w_beg = blockIdx.y * per_split;
+  // XCD-aware work map: block b runs on XCD b % 8; the (split, row block) pairs, split-major, are dealt to the XCDs in
+  // contiguous ranges, so each split's swept slice streams through the L2 of one or two XCDs instead of all eight
+  const int nrb = (n_s + 127) >> 7, nb = (int)gridDim.x;
+  const int pidx = nb % 8 == 0 ? (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int split = pidx / nrb, rblk = pidx % nrb;
+  const int s0 = rblk * 128 + w * 32 + l16;  // stationary rows s0 (sb 0), s0 + 16 (sb 1)
+  const int w_beg = split * per_split;
   const int w_end = min(n_w, w_beg + per_split);
   const int ntiles = w_end > w_beg ? (w_end - w_beg + T3 - 1) / T3 : 0;
   f32x4 dacc[NE][2];
@@ -426,10 +431,10 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
     const int s = s0 + 16 * sb;
     if (s < n_s) {
       if (g == 0) {
-        if constexpr (MODE == 0) part_m[(long)blockIdx.y * n_s + s] = mrow[sb];
-        part_s[(long)blockIdx.y * n_s + s] = ztot;
+        if constexpr (MODE == 0) part_m[(long)split * n_s + s] = mrow[sb];
+        part_s[(long)split * n_s + s] = ztot;
       }
-      float* out = outp + ((long)blockIdx.y * n_s + s) * D + 4 * g;
+      float* out = outp + ((long)split * n_s + s) * D + 4 * g;
 #pragma unroll
       for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
     }
@@ -466,7 +471,7 @@ template <int MODE>
 int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec, int n_s, int n_w, int D, int nsplit,
             float* pm, float* ps, float* out, hipStream_t st) {
   const int per = per_split3(n_w, nsplit);
-  dim3 grid(c2::ceil_div(n_s, 128), nsplit);
+  const dim3 grid(c2::ceil_div(n_s, 128) * nsplit);  // (row block, split) pairs: ce3_kernel's XCD-aware map
   if (D == 128)
     ce3_kernel<128, MODE><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm, ps,
                                                  out);
