@@ -74,17 +74,18 @@ def make_args(cfg, device, precision, dropout=0.2, zero1=False):
 
 class KernelTimer:
     """HIP-event timing (on the stream the kernels are launched on, inside the timed region) of the
-    dominant op, K5 — the fused classifier head + cross-entropy — in bf16 mode: c2dsr_ce_fused_fwd_u
-    (online log-sum-exp AND the softmax·W part of dH in one sweep) and c2dsr_ce_fused_dw (the older
-    split c2dsr_ce_fused_fwd / _dh pair when selected).  Credited FLOPs: 2·M·n·d per
-    product — forward logits, dH, dW (fwd_u carries two) — the logits tile the dW kernel recomputes is
-    overhead and not credited.  fp32 mode: the materialised
-    logits GEMMs (c2dsr_gemm calls of > 1e11 FLOP)."""
+    dominant op, K5 — the fused classifier head + cross-entropy — in bf16 mode: c2dsr_ce3b_fused_fwd_u
+    (online log-sum-exp AND the softmax·W part of dH in one sweep) and c2dsr_ce3b_fused_dw (ce.hip's
+    c2dsr_ce_fused_* pair for other widths, the older split _fwd / _dh pair when selected).  Credited
+    FLOPs: 2·M·n·d per product — forward logits, dH, dW (fwd_u carries two) — the
+    logits tile the dW kernel recomputes is overhead and not credited.  fp32 mode: the split-bf16 pair
+    c2dsr_ce3_fused_fwd_u / _dw."""
 
-    NAMES_BF16 = ('c2dsr_ce_fused_fwd_u', 'c2dsr_ce_fused_fwd', 'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
+    NAMES_BF16 = ('c2dsr_ce3b_fused_fwd_u', 'c2dsr_ce3b_fused_dw', 'c2dsr_ce_fused_fwd_u', 'c2dsr_ce_fused_fwd',
+                  'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
     NAMES_X3 = ('c2dsr_ce3_fused_fwd_u', 'c2dsr_ce3_fused_dw')
     # credited products per launch: fwd_u = the lse logits + the softmax·W part of dH (online, one sweep)
-    CREDIT = {'c2dsr_ce_fused_fwd_u': 2, 'c2dsr_ce3_fused_fwd_u': 2}
+    CREDIT = {'c2dsr_ce_fused_fwd_u': 2, 'c2dsr_ce3_fused_fwd_u': 2, 'c2dsr_ce3b_fused_fwd_u': 2}
 
     def __init__(self, precision):
         from c2dsr_amd._lib import lib
@@ -626,8 +627,9 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
         traffic, tsrc, busy = k5_traffic(precision) if name == 'mb' else (None, None, None)
         roof = dict(bound='mfma', achieved=round(ks['tflops'], 2), peak=peak, unit='TFLOP/s',
                     frac=round(ks['tflops'] / peak, 4), traffic=traffic, traffic_source=tsrc,
-                    kernel={'bf16': 'K5 fused classifier head + CE: ce_fwdu_kernel (lse + dH, online) + ce_dw_kernel '
-                                    '(bf16 MFMA); credited 2·M·n·d per product (fwd_u 2, dw 1)',
+                    kernel={'bf16': 'K5 fused classifier head + CE: ce3_kernel<256,0,bf16> (lse + dH, online) + '
+                                    'ce3_kernel<256,1,bf16> (dW), one bf16 MFMA per product; credited 2·Mv·n·d per '
+                                    'product over the Mv valid rows (fwd_u 2, dw 1)',
                             'fp32': 'K5 fused classifier head + CE at fp32 accuracy: ce3_kernel<256,0> (lse + dH, '
                                     'online) + ce3_kernel<256,1> (dW), split-bf16 operands, 3 bf16 MFMAs per '
                                     'product; credited 2·Mv·n·d per fp32 product over the Mv valid rows (fwd_u 2, '

@@ -42,6 +42,24 @@
 #ifndef CE3_DT
 #define CE3_DT 2
 #endif
+#ifndef CE3B_DS  // the plain-bf16 instantiation (one MFMA per fragment: the reads run further ahead)
+#define CE3B_DS 2
+#endif
+#ifndef CE3B_DT
+#define CE3B_DT 2
+#endif
+#ifndef CE3_ILV
+#define CE3_ILV 1
+#endif
+#ifndef CE3B_ILV
+#define CE3B_ILV 1
+#endif
+#ifndef CE3_DQ
+#define CE3_DQ 2
+#endif
+#ifndef CE3B_DQ
+#define CE3B_DQ 4
+#endif
 
 namespace {
 
@@ -112,25 +130,50 @@ __device__ __forceinline__ void split3_u(f32x4& acc, const bf16x8& ah, const bf1
       : "v"(ah), "v"(al), "v"(bh), "v"(bl));
 }
 
-template <int D, int MODE>
+// plain-bf16 products (the bf16 training mode): one MFMA, stationary operand in AGPRs / accumulator in AGPRs
+__device__ __forceinline__ void mf1_s0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
+}
+__device__ __forceinline__ void mf1_s(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
+}
+__device__ __forceinline__ void mf1_u(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// swept rows per LDS tile: 32 for split images (2D columns), 64 for plain bf16 (D columns) — 32 KiB at D = 256
+template <bool SPLIT>
+constexpr int tile_rows() { return SPLIT ? 32 : 64; }
+
+template <int D, int MODE, bool SPLIT>
 __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs, const bf16* __restrict__ Xw,
                                                       const float* __restrict__ svec, const float* __restrict__ wvec,
                                                       int n_s, int n_w, int per_split, float* __restrict__ part_m,
                                                       float* __restrict__ part_s, float* __restrict__ outp) {
+  constexpr int T3 = tile_rows<SPLIT>();
+  constexpr int CB = T3 / 16;                      // 16-row swept blocks per tile
+  constexpr int UK = T3 / 32;                      // 32-row k-steps of the second product per e-block
   constexpr int KS = D / 32;                       // k-steps of the S product
-  constexpr int NSS = 2 * KS;                      // S-phase steps: (ks, cb)
-  constexpr int NE = D / 16;                       // second-product steps: 16-column e-blocks
-  constexpr int D2 = 2 * D;                        // hi ‖ lo
+  constexpr int NSS = KS * CB;                     // S-phase steps: (ks, cb)
+  constexpr int NE = D / 16;                       // 16-column e-blocks of the second product
+  constexpr int NUS = NE * UK;                     // second-product steps: (u, e-block)
+  constexpr int D2 = SPLIT ? 2 * D : D;            // image columns (hi ‖ lo, or bf16)
   constexpr int IMG = T3 * D2 * 2;                 // bytes per image
   constexpr int HT = T3 * 256;                     // bytes per 128-column half-tile
   constexpr int NDMA = (T3 / 4) * (D2 / 128) / 4;  // LDS-DMA wave-instructions per wave per tile
   constexpr int NB = 4;
-  constexpr int DS = CE3_DS, DT = CE3_DT;
-  constexpr int EPK = 16 / NSS;                    // epilogue elements per S step
-  constexpr int MPK = 16 / NE;                     // prep elements per second-product step
+  constexpr int DS = SPLIT ? CE3_DS : CE3B_DS, DT = SPLIT ? CE3_DT : CE3B_DT;
+  constexpr int NEL = 8 * CB;                      // S values per lane per tile (2 stationary blocks × CB)
+  constexpr int EPK = NEL / NSS;                   // epilogue elements per S step
+  constexpr int MPK = NEL / NUS;                   // prep elements per second-product step
   constexpr float TAU = 8.f;
-  static_assert(NSS * EPK == 16 && NE * MPK == 16 && NE % NDMA == 0 && EPK <= 8, "tile / wave split");
-  constexpr int QD = NE / NDMA;
+  static_assert(NSS * EPK == NEL && NUS * MPK == NEL && EPK <= 8 && 8 % EPK == 0 && DS <= NUS && DT <= NSS,
+                "tile / wave split");
+  // one LDS-DMA wave-instruction of tile t+3 every DQ second-product steps, from the first (DQ = 1: the whole
+  // tile at the start of the phase, the longest time to land before the barrier that publishes it)
+  constexpr int DQ = SPLIT ? CE3_DQ : CE3B_DQ;
+  constexpr bool ILV = SPLIT ? CE3_ILV : CE3B_ILV;
+  static_assert(DQ >= 1 && DQ * NDMA <= NUS, "DMA spacing");
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
   __shared__ __attribute__((aligned(16))) float wv[NB][4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
@@ -187,7 +230,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         fh[sb][ks] = *(const bf16x8*)(Xs + sr * D2 + ks * 32 + 8 * g);
-        fl[sb][ks] = *(const bf16x8*)(Xs + sr * D2 + D + ks * 32 + 8 * g);
+        if constexpr (SPLIT) fl[sb][ks] = *(const bf16x8*)(Xs + sr * D2 + D + ks * 32 + 8 * g);
       }
     }
     float b2s[2] = {0.f, 0.f};
@@ -213,13 +256,13 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
 #pragma unroll
       for (int v = 0; v < 8; ++v) o.t[v] = toff0[v] + ib + b * IMG;
     };
-    // row fragment of image column block kx (32 columns; hi: ks, lo: KS + ks) and swept-row block CB
-    auto rfrag = [&]<int KX, int CB>(const Offs& o) {
-      return lds_ld128<(KX >> 2) * HT + CB * 16 * 256 + 16 * 0>(o.r[KX & 3]);
+    // row fragment of image column block kx (32 columns; hi: ks, lo: KS + ks) and swept-row block C
+    auto rfrag = [&]<int KX, int C>(const Offs& o) {
+      return lds_ld128<(KX >> 2) * HT + C * 16 * 256>(o.r[KX & 3]);
     };
-    // transposed fragment of image columns 16·EX .. +15 (hi: EX, lo: D/16 + EX)
-    auto tfrag = [&]<int EX>(const Offs& o) {
-      constexpr int IMM = (EX >> 3) * HT;
+    // transposed fragment of image columns 16·EX .. +15 (hi: EX, lo: D/16 + EX), swept rows 32U ..
+    auto tfrag = [&]<int EX, int U>(const Offs& o) {
+      constexpr int IMM = (EX >> 3) * HT + U * 32 * 256;
       const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
           (lds_bf16x4*)(size_t)(lds_base(o.t[EX & 7]) + IMM));
       const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
@@ -229,31 +272,49 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
       return v;
     };
-    // the per-swept-row constants of this lane's rows 16cb + 4g + i
-    auto wconst = [&](int b, f32x4 (&c4)[2]) {
-      const int bo = (int)lds_addr(wv[b][w]) + 16 * g;
-      c4[0] = lds_ld<f32x4, 0>(bo);
-      c4[1] = lds_ld<f32x4, 64>(bo);
+    // S-phase step k ↔ (ks = k / CB, cb = k % CB); second-product step k ↔ (u = k / NE, e-block k % NE)
+    auto s_frags = [&]<int K>(const Offs& o, bf16x8(&f)[2]) {
+      f[0] = rfrag.template operator()<K / CB, K % CB>(o);
+      if constexpr (SPLIT) f[1] = rfrag.template operator()<KS + K / CB, K % CB>(o);
     };
-    // S-phase step k (0 .. NSS-1) ↔ (ks = k >> 1, cb = k & 1); epilogue element i (0..15) ↔
-    // (sb = i >> 3, cb = (i >> 2) & 1, r = i & 3) = accumulator (cb·2 + sb)[r]
-    f32x4 sc[4];
+    auto u_frags = [&]<int K>(const Offs& o, bf16x8(&f)[2]) {
+      f[0] = tfrag.template operator()<K % NE, K / NE>(o);
+      if constexpr (SPLIT) f[1] = tfrag.template operator()<NE + K % NE, K / NE>(o);
+    };
+    auto s_prod = [&]<int KSI>(f32x4& acc, const bf16x8(&a)[2], int sb) {
+      if constexpr (SPLIT) {
+        if constexpr (KSI == 0)
+          split3_s0(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
+        else
+          split3_s(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
+      } else {
+        if constexpr (KSI == 0)
+          mf1_s0(acc, a[0], fh[sb][KSI]);
+        else
+          mf1_s(acc, a[0], fh[sb][KSI]);
+      }
+    };
+    // the per-swept-row constants of this lane's rows 16cb + 4g + i
+    auto wconst = [&](int b, f32x4(&c4)[CB]) {
+      const int bo = (int)lds_addr(wv[b][w]) + 16 * g;
+      [&]<int... C>(std::integer_sequence<int, C...>) {
+        ((c4[C] = lds_ld<f32x4, 64 * C>(bo)), ...);
+      }(std::make_integer_sequence<int, CB>{});
+    };
+    // epilogue element i (0 .. NEL-1) ↔ (sb = i / 4CB, cb = (i / 4) % CB, r = i % 4) = accumulator (cb·2 + sb)[r];
+    // the second product's B fragment (u, sb) packs elements of cb = 2u, 2u + 1 (8-element chunk sb·UK + u)
+    f32x4 sc[2 * CB];
     {
       Offs oS;
       offs_rows(0, oS);
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
-              constexpr int ks = K >> 1, cb = K & 1;
-              const bf16x8 ah = rfrag.template operator()<ks, cb>(oS);
-              const bf16x8 al = rfrag.template operator()<KS + ks, cb>(oS);
+              constexpr int cb = K % CB;
+              bf16x8 a[2];
+              s_frags.template operator()<K>(oS, a);
 #pragma unroll
-              for (int sb = 0; sb < 2; ++sb) {
-                if constexpr (ks == 0)
-                  split3_s0(sc[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
-                else
-                  split3_s(sc[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
-              }
+              for (int sb = 0; sb < 2; ++sb) s_prod.template operator()<K / CB>(sc[cb * 2 + sb], a, sb);
             }(),
             ...);
       }(std::make_integer_sequence<int, NSS>{});
@@ -261,12 +322,12 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
     mfma_drain();
     float mnext[2] = {-INFINITY, -INFINITY};
     {
-      f32x4 c4[2];
+      f32x4 c4[CB];
       wconst(0, c4);
       float tm[2] = {-INFINITY, -INFINITY};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int sb = i >> 3, cb = (i >> 2) & 1, r = i & 3;
+      for (int i = 0; i < NEL; ++i) {
+        const int sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
         float v = fmaf(sc[cb * 2 + sb][r], LOG2E, c4[cb][r]);
         if constexpr (MODE == 1) v += b2s[sb];
         sc[cb * 2 + sb][r] = v;
@@ -283,9 +344,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       Offs oS;
       offs_rows(1 % NB, oS);
       [&]<int... P>(std::integer_sequence<int, P...>) {
-        ((fa[P][0] = rfrag.template operator()<(P >> 1), (P & 1)>(oS),
-          fa[P][1] = rfrag.template operator()<(KS + (P >> 1)), (P & 1)>(oS)),
-         ...);
+        (s_frags.template operator()<P>(oS, fa[P]), ...);
       }(std::make_integer_sequence<int, DS>{});
     }
     for (int t = 0; t < ntiles; ++t) {
@@ -322,51 +381,43 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       offs_rows(bs, oS);
       offs_tr(bh, oH);
       // ---- S(t+1) ∥ epilogue(t)
-      f32x4 sn[4];
-      bf16x8 xh[2], xl[2];
+      f32x4 sn[2 * CB];
+      bf16x8 xh[UK][2], xl[UK][2];
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
-              constexpr int k = K, ks = k >> 1, cb = k & 1;
-              if constexpr (k + DS < NSS) {
-                constexpr int k1 = k + DS;
-                fa[k1 % (DS + 2)][0] = rfrag.template operator()<(k1 >> 1), (k1 & 1)>(oS);
-                fa[k1 % (DS + 2)][1] = rfrag.template operator()<(KS + (k1 >> 1)), (k1 & 1)>(oS);
-              } else {
-                constexpr int q1 = k + DS - NSS;
-                if constexpr (q1 < DT) {
-                  tf[q1][0] = tfrag.template operator()<q1>(oH);
-                  tf[q1][1] = tfrag.template operator()<NE + q1>(oH);
-                }
-              }
-              const bf16x8& ah = fa[k % (DS + 2)][0];
-              const bf16x8& al = fa[k % (DS + 2)][1];
-#pragma unroll
-              for (int sb = 0; sb < 2; ++sb) {
-                if constexpr (ks == 0)
-                  split3_s0(sn[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
-                else
-                  split3_s(sn[cb * 2 + sb], ah, al, fh[sb][ks], fl[sb][ks]);
-              }
+              constexpr int k = K, cb = k % CB;
+              // the two rings run DS / DT steps ahead, each across the phase boundary
+              if constexpr (k + DS < NSS) s_frags.template operator()<k + DS>(oS, fa[(k + DS) % (DS + 2)]);
+              if constexpr (k + DT >= NSS) u_frags.template operator()<k + DT - NSS>(oH, tf[k + DT - NSS]);
+              // ILV: the step's VALU work between its two stationary blocks' products (each MFMA's shadow
+              // covers half of it; in-order issue otherwise stalls it behind the second MFMA)
+              s_prod.template operator()<k / CB>(sn[cb * 2], fa[k % (DS + 2)], 0);
+              if constexpr (ILV) __builtin_amdgcn_sched_barrier(0);
+              else s_prod.template operator()<k / CB>(sn[cb * 2 + 1], fa[k % (DS + 2)], 1);
 #pragma unroll
               for (int e = 0; e < EPK; ++e) {
                 constexpr int i0 = k * EPK;
-                const int i = i0 + e, sb = i >> 3, cb2 = (i >> 2) & 1, r = i & 3;
+                const int i = i0 + e, sb = i / (4 * CB), cb2 = (i >> 2) % CB, r = i & 3;
                 const float pv = ex2(sc[cb2 * 2 + sb][r] - msub[sb]);
                 sc[cb2 * 2 + sb][r] = pv;
                 zrow[sb] += pv;
               }
               if constexpr ((k * EPK + EPK) % 8 == 0) {
-                constexpr int sb = (k * EPK) / 8;
+                constexpr int c = (k * EPK) / 8, sb = c / UK, u = c % UK;
                 bf16x8 h, l;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                  const float x = sc[(j >> 2) * 2 + sb][j & 3];
+                  const float x = sc[(2 * u + (j >> 2)) * 2 + sb][j & 3];
                   h[j] = (bf16)x;
-                  l[j] = (bf16)(x - (float)h[j]);
+                  if constexpr (SPLIT) l[j] = (bf16)(x - (float)h[j]);
                 }
-                xh[sb] = h;
-                xl[sb] = l;
+                xh[u][sb] = h;
+                if constexpr (SPLIT) xl[u][sb] = l;
+              }
+              if constexpr (ILV) {
+                __builtin_amdgcn_sched_barrier(0);
+                s_prod.template operator()<k / CB>(sn[cb * 2 + 1], fa[k % (DS + 2)], 1);
               }
               __builtin_amdgcn_sched_barrier(0);
             }(),
@@ -378,50 +429,50 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       // ---- second product (t) ∥ prep of S(t+1) ∥ DMA of tile t+3
       Offs oN;
       offs_rows((t + 2) % NB, oN);
-      f32x4 c4n[2];
+      f32x4 c4n[CB];
       wconst(bs, c4n);
       float tm[2] = {-INFINITY, -INFINITY};
       [&]<int... Q>(std::integer_sequence<int, Q...>) {
         (
             [&] {
-              constexpr int q = Q;
-              if constexpr (q + DT < NE) {
-                constexpr int q1 = q + DT;
-                tf[q1 % (DT + 2)][0] = tfrag.template operator()<q1>(oH);
-                tf[q1 % (DT + 2)][1] = tfrag.template operator()<NE + q1>(oH);
-              } else {
-                constexpr int k1 = q + DT - NE;
-                if constexpr (k1 < DS) {
-                  fa[k1][0] = rfrag.template operator()<(k1 >> 1), (k1 & 1)>(oN);
-                  fa[k1][1] = rfrag.template operator()<(KS + (k1 >> 1)), (k1 & 1)>(oN);
-                }
-              }
-              const bf16x8& th = tf[q % (DT + 2)][0];
-              const bf16x8& tl = tf[q % (DT + 2)][1];
-#pragma unroll
-              for (int sb = 0; sb < 2; ++sb) {
-                split3_u(dacc[q][sb], th, tl, xh[sb], xl[sb]);
-              }
-              if constexpr (q % QD == QD - 1) dma16_s<q == QD - 1>(nsrc, dvoff[q / QD], ddst[q / QD] + nbuf);
+              constexpr int k = Q, q = k % NE, u = k / NE;
+              if constexpr (k + DT < NUS) u_frags.template operator()<k + DT>(oH, tf[(k + DT) % (DT + 2)]);
+              if constexpr (k + DS >= NUS) s_frags.template operator()<k + DS - NUS>(oN, fa[k + DS - NUS]);
+              const bf16x8(&tq)[2] = tf[k % (DT + 2)];
+              auto u_prod = [&](int sb) {
+                if constexpr (SPLIT)
+                  split3_u(dacc[q][sb], tq[0], tq[1], xh[u][sb], xl[u][sb]);
+                else
+                  mf1_u(dacc[q][sb], tq[0], xh[u][sb]);
+              };
+              u_prod(0);
+              if constexpr (ILV) __builtin_amdgcn_sched_barrier(0);
+              else u_prod(1);
+              if constexpr (k % DQ == DQ - 1 && k / DQ < NDMA)
+                dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
 #pragma unroll
               for (int e = 0; e < MPK; ++e) {
-                constexpr int i0 = q * MPK;
-                const int i = i0 + e, sb = i >> 3, cb = (i >> 2) & 1, r = i & 3;
+                constexpr int i0 = k * MPK;
+                const int i = i0 + e, sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
                 float v = fmaf(sn[cb * 2 + sb][r], LOG2E, c4n[cb][r]);
                 if constexpr (MODE == 1) v += b2s[sb];
                 sn[cb * 2 + sb][r] = v;
                 tm[sb] = fmaxf(tm[sb], v);
               }
+              if constexpr (ILV) {
+                __builtin_amdgcn_sched_barrier(0);
+                u_prod(1);
+              }
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
-      }(std::make_integer_sequence<int, NE>{});
+      }(std::make_integer_sequence<int, NUS>{});
       if constexpr (MODE == 0) {
         mnext[0] = quad_max(tm[0]);
         mnext[1] = quad_max(tm[1]);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sc[i] = sn[i];
+      for (int i = 0; i < 2 * CB; ++i) sc[i] = sn[i];
     }
   }
   mfma_drain();
@@ -462,22 +513,22 @@ __global__ void split_bf16_kernel(const float* __restrict__ x, long rows, int D,
   *(bf16x4*)(out + r * 2 * D + D + k) = l;
 }
 
-int per_split3(int total, int nsplit) {
-  const int tiles = c2::ceil_div(total, T3);
-  return c2::ceil_div(tiles, nsplit) * T3;
+int per_split3(int total, int nsplit, int t3) {
+  const int tiles = c2::ceil_div(total, t3);
+  return c2::ceil_div(tiles, nsplit) * t3;
 }
 
-template <int MODE>
+template <int MODE, bool SPLIT>
 int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec, int n_s, int n_w, int D, int nsplit,
             float* pm, float* ps, float* out, hipStream_t st) {
-  const int per = per_split3(n_w, nsplit);
+  const int per = per_split3(n_w, nsplit, tile_rows<SPLIT>());
   const dim3 grid(c2::ceil_div(n_s, 128) * nsplit);  // (row block, split) pairs: ce3_kernel's XCD-aware map
   if (D == 128)
-    ce3_kernel<128, MODE><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm, ps,
-                                                 out);
+    ce3_kernel<128, MODE, SPLIT><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm,
+                                                        ps, out);
   else if (D == 256)
-    ce3_kernel<256, MODE><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm, ps,
-                                                 out);
+    ce3_kernel<256, MODE, SPLIT><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm,
+                                                        ps, out);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
@@ -506,7 +557,7 @@ C2_API int c2dsr_ce3_fused_fwd_u(const void* Hx, const void* Wx, const float* bi
                                  const float* H, const float* W, const float* bias, float* lse, float* lse2,
                                  float* loss_row, void* stream) {
   if (M == 0) return 0;
-  const int e = launch3<0>(Hx, Wx, nullptr, bias2, M, n, D, n_split, part_m, part_s, Up, (hipStream_t)stream);
+  const int e = launch3<0, true>(Hx, Wx, nullptr, bias2, M, n, D, n_split, part_m, part_s, Up, (hipStream_t)stream);
   if (e) return e;
   return c2dsr_ce_rows(part_m, part_s, n_split, M, padlogit, tgt, n, H, W, bias, D, lse, lse2, loss_row, stream);
 }
@@ -514,5 +565,24 @@ C2_API int c2dsr_ce3_fused_fwd_u(const void* Hx, const void* Wx, const float* bi
 C2_API int c2dsr_ce3_fused_dw(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_rsplit,
                               const float* crow, float* dWp, float* dbp, void* stream) {
   if (n == 0) return 0;
-  return launch3<1>(Wx, Hx, bias2, crow, n, M, D, n_rsplit, nullptr, dbp, dWp, (hipStream_t)stream);
+  return launch3<1, true>(Wx, Hx, bias2, crow, n, M, D, n_rsplit, nullptr, dbp, dWp, (hipStream_t)stream);
+}
+
+// The same pair on plain bf16 images [rows][D] (the bf16 mode; drop-in for ce.hip's c2dsr_ce_fused_fwd_u /
+// c2dsr_ce_fused_dw, same arguments and outputs): 64-row swept tiles, one MFMA per product.  Images hold whole
+// 64-row tiles (zero rows past the end); crow carries a 64-value tail.
+C2_API int c2dsr_ce3b_fused_fwd_u(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
+                                  float* part_m, float* part_s, float* Up, const float* padlogit, const int64_t* tgt,
+                                  const float* H, const float* W, const float* bias, float* lse, float* lse2,
+                                  float* loss_row, void* stream) {
+  if (M == 0) return 0;
+  const int e = launch3<0, false>(Hb, Wb, nullptr, bias2, M, n, D, n_split, part_m, part_s, Up, (hipStream_t)stream);
+  if (e) return e;
+  return c2dsr_ce_rows(part_m, part_s, n_split, M, padlogit, tgt, n, H, W, bias, D, lse, lse2, loss_row, stream);
+}
+
+C2_API int c2dsr_ce3b_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
+                               const float* crow, float* dWp, float* dbp, void* stream) {
+  if (n == 0) return 0;
+  return launch3<1, false>(Wb, Hb, bias2, crow, n, M, D, n_rsplit, nullptr, dbp, dWp, (hipStream_t)stream);
 }

@@ -57,6 +57,14 @@ def ce_kind(precision, d):
     return None
 
 
+def ce_entry(x3, d, role):
+    """The fused head's sweep kernels: split-bf16 images → ce3.hip (x3); bf16 images → ce3.hip's plain-bf16
+    instantiation where it covers d (128, 256), else ce.hip's pair (same arguments and outputs)."""
+    if x3:
+        return 'c2dsr_ce3_fused_' + role
+    return ('c2dsr_ce3b_fused_' if bool(lib.raw('c2dsr_ce3_supported')(d)) else 'c2dsr_ce_fused_') + role
+
+
 class LossMeta:
     def __init__(self, *, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, n_a, n_b, R, lam, Wa, ba, Wb, bb, wpad,
                  bpad, Da_w, Da_b, Db_w, Db_b, precision=FP32, B_global=None, allreduce=None, ce_pre=None,
@@ -215,8 +223,8 @@ class LossHeadFn(Function):
                     pm = torch.empty(ns, Mv, **f32)
                     ps = torch.empty(ns, Mv, **f32)
                     Up = torch.empty(ns, Mv, d, **f32)
-                    lib('c2dsr_ce3_fused_fwd_u' if x3 else 'c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm,
-                        ps, Up, padc, tc, Hc, W, bias, lse_c, lse2, rows_c, s)
+                    lib(ce_entry(x3, d, 'fwd_u'), Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tc, Hc, W, bias, lse_c,
+                        lse2, rows_c, s)
                     u = (Up, pm, ns)
                     m.run_after_first_ce()
                 elif Mv:
@@ -295,7 +303,7 @@ class LossHeadFn(Function):
                 rw = torch.empty(M_pad, **f32)
                 t32 = torch.empty(M_pad, device=dev, dtype=torch.int32)
                 dpad_c = torch.empty(max(Mv, 1), **f32)
-                crow = torch.empty(M_pad + (64 if ctx.x3 else 0), **f32)  # x3: the dW sweep's row-constant DMA
+                crow = torch.empty(M_pad + 64, **f32)  # + the tail the dW sweep's row-constant DMA reads
                 dHc = torch.empty(max(Mv, 1), d, **f32)
                 if Mv:
                     # compact rows keep their order: the first Mv0 are the shared-sequence rows (coef[0])
@@ -313,8 +321,7 @@ class LossHeadFn(Function):
                     nr = split_count(n, 128)
                     dWp = torch.empty(nr, n, d, **f32)
                     dbp = torch.empty(nr, n, **f32)
-                    lib('c2dsr_ce3_fused_dw' if ctx.x3 else 'c2dsr_ce_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow,
-                        dWp, dbp, s)
+                    lib(ce_entry(ctx.x3, d, 'dw'), Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)
                     if gW is not None:
                         lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
                     if gb is not None:

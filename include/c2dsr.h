@@ -301,6 +301,16 @@ int c2dsr_ce3_fused_fwd_u(const void* Hx, const void* Wx, const float* bias2, in
                           void* stream);
 int c2dsr_ce3_fused_dw(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_rsplit,
                        const float* crow, float* dWp, float* dbp, void* stream);
+/* The bf16 mode's pair on ce3.hip's plain-bf16 instantiation (one MFMA per product, 64-row swept tiles; D = 128
+ * or 256, c2dsr_ce3_supported): drop-in for c2dsr_ce_fused_fwd_u / c2dsr_ce_fused_dw — same arguments, same
+ * outputs (trainer.py:131-154).  Hb holds ⌈M/64⌉·64 rows and Wb ⌈n/64⌉·64 rows (zero rows past the end); crow
+ * holds ⌈M/64⌉·64 + 64 values. */
+int c2dsr_ce3b_fused_fwd_u(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_split,
+                           float* part_m, float* part_s, float* Up, const float* padlogit, const int64_t* tgt,
+                           const float* H, const float* W, const float* bias, float* lse, float* lse2,
+                           float* loss_row, void* stream);
+int c2dsr_ce3b_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
+                        const float* crow, float* dWp, float* dbp, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
 int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */

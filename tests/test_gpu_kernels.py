@@ -349,10 +349,17 @@ def _bf16(t):
     return t.to(torch.bfloat16).to(torch.float32)
 
 
-@pytest.mark.parametrize('M,n,D', [(300, 700, 256), (1000, 2100, 128), (64, 65, 256)])
-def test_fused_linear_ce_vs_reference(M, n, D):
+# the bf16-mode fwd_u / dw pair: ce.hip (32x32x16, 64-row stationary blocks) and ce3.hip's plain-bf16
+# instantiation (16x16x32, the kernel the bf16 mode runs for D = 128 / 256) — same arguments, same outputs
+CE_B16 = {'ce': ('c2dsr_ce_fused_fwd_u', 'c2dsr_ce_fused_dw'), 'ce3b': ('c2dsr_ce3b_fused_fwd_u', 'c2dsr_ce3b_fused_dw')}
+
+
+@pytest.mark.parametrize('kern', sorted(CE_B16))
+@pytest.mark.parametrize('M,n,D', [(300, 700, 256), (1000, 2100, 128), (64, 65, 256), (777, 4099, 256), (33, 31, 128)])
+def test_fused_linear_ce_vs_reference(M, n, D, kern):
     """K5 fused head (bf16 MFMA) vs a float64 CPU computation of the same op on the same bf16-rounded
     operands: lse rel 2e-5; gradients (P' rounded to bf16 for the 2nd product) rel 1e-2 of max."""
+    fwd_u, fdw = CE_B16[kern]
     from c2dsr_amd._lib import lib, stream
     g = torch.Generator().manual_seed(M + n)
     H = _bf16(torch.randn(M, D, generator=g) * 0.5)
@@ -390,7 +397,7 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     assert rel(rows, rows_r) < 1e-4
     rw, dpad = torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)
     t32 = torch.empty(M_pad, device=DEV, dtype=torch.int32)
-    crow = torch.empty(M_pad, device=DEV)
+    crow = torch.empty(M_pad + 64, device=DEV)
     lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, t32, lse2, crow, dpad, s)
     w_r = torch.where(valid, lam * coef[(torch.arange(M) >= BR).long()].double(), torch.zeros(M, dtype=torch.float64))
     P = torch.softmax(lg, 1)
@@ -408,8 +415,7 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     Up = torch.empty(ns, M, D, device=DEV)
     lse_u, rows_u = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
     lse2_u = torch.empty(M_pad, device=DEV)
-    lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, M, n, D, ns, pm2, ps2, Up, d(pl), d(t), d(H), d(W), d(b), lse_u,
-        lse2_u, rows_u, s)
+    lib(fwd_u, Hb, Wb, bias2, M, n, D, ns, pm2, ps2, Up, d(pl), d(t), d(H), d(W), d(b), lse_u, lse2_u, rows_u, s)
     assert rel(lse_u, lse_r) < 2e-5
     assert rel(rows_u, rows_r) < 1e-4
     dHu = torch.empty(M, D, device=DEV)
@@ -418,7 +424,7 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     gW = torch.ones(n, D, device=DEV)
     gb = torch.ones(n, device=DEV)
     dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
-    lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, M, n, D, nr, crow, dWp, dbp, s)
+    lib(fdw, Hb, Wb, bias2, M, n, D, nr, crow, dWp, dbp, s)
     lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
     lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M, n, D))
@@ -436,8 +442,9 @@ def test_fused_linear_ce_vs_reference(M, n, D):
     assert torch.equal(gW0, gW) and torch.equal(gb0, gb)
 
 
+@pytest.mark.parametrize('kern', sorted(CE_B16))
 @pytest.mark.parametrize('M,n,D,ns', [(200, 1500, 256, 2), (333, 3000, 128, 5), (130, 900, 256, 1)])
-def test_fused_ce_online_rescale(M, n, D, ns):
+def test_fused_ce_online_rescale(M, n, D, ns, kern):
     """c2dsr_ce_fused_fwd_u when the row max keeps rising across column tiles (bias ramp of 60 nats and
     a column-dependent scale: the lazy rescale fires many times, at different tiles for different rows
     of one wave) and when it falls (reversed ramp on half of the rows via their H sign): lse vs float64,
@@ -468,15 +475,14 @@ def test_fused_ce_online_rescale(M, n, D, ns):
     Up = torch.empty(ns, M, D, device=DEV)
     lse, rows = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
     lse2 = torch.empty(M_pad, device=DEV)
-    lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, M, n, D, ns, pm, ps, Up, d(pl), d(t), d(H), d(W), d(b), lse, lse2,
-        rows, s)
+    lib(CE_B16[kern][0], Hb, Wb, bias2, M, n, D, ns, pm, ps, Up, d(pl), d(t), d(H), d(W), d(b), lse, lse2, rows, s)
     lg = torch.cat([H.double() @ W.double().T + b.double(), pl.double()[:, None]], 1)
     lse_r = torch.logsumexp(lg, 1)
     assert rel(lse, lse_r) < 2e-5
     coef, gs, lam = torch.tensor([0.5, 1.5]), torch.tensor([1.0]), 0.7
     rw, dpad = torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)
     t32 = torch.empty(M_pad, device=DEV, dtype=torch.int32)
-    crow = torch.empty(M_pad, device=DEV)
+    crow = torch.empty(M_pad + 64, device=DEV)
     lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), M // 2, d(gs), lam, d(pl), lse, rw, t32, lse2, crow,
         dpad, s)
     dH = torch.empty(M, D, device=DEV)

@@ -1,7 +1,8 @@
 """Micro-benchmark of the K5 kernels at the bench's shapes: c2dsr_ce_fused_fwd_u (online lse + the softmax
 part of dH) and c2dsr_ce_fused_dw, one head of the MB config (n = 63,937 items, Mv ≈ 18.9k valid stacked rows,
 d = 256), HIP-event timed.  Compare kernel variants by pointing C2DSR_LIB at a variant library
-(tools/ce_variants.sh builds them with the ce.hip tuning knobs).
+(tools/ce_variants.sh builds them with the ce.hip tuning knobs).  Times both bf16 pairs: ce.hip's and ce3.hip's
+plain-bf16 instantiation (c2dsr_ce3b_*).
 usage: python tools/ce_micro.py [Mv] [n]"""
 import os
 import sys
@@ -50,23 +51,25 @@ def main():
     ns = split_count(Mv, 128)
     pm, ps = torch.empty(ns, Mv, **f32), torch.empty(ns, Mv, **f32)
     Up = torch.empty(ns, Mv, d, **f32)
-    fwd = lambda: lib('c2dsr_ce_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tgt, H, W, bias,  # noqa
-                      lse, lse2, rows, s)
-    t_f = timeit(fwd)
-    rw, crow, dpad = torch.empty(Mp, **f32), torch.empty(Mp, **f32), torch.empty(Mp, **f32)
+    rw, crow, dpad = torch.empty(Mp, **f32), torch.empty(Mp + 64, **f32), torch.empty(Mp, **f32)
     t32 = torch.empty(Mp, device=dev, dtype=torch.int32)
     coef = torch.tensor([1.0 / Mv, 1.0 / Mv], **f32)
     gscale = torch.ones(1, **f32)
-    lib('c2dsr_ce_row_weights', tgt, Mv, Mp, n, coef, Mv // 2, gscale, 0.7, padc, lse, rw, t32, lse2, crow, dpad, s)
     nr = split_count(n, 128)
     dWp, dbp = torch.empty(nr, n, d, **f32), torch.empty(nr, n, **f32)
-    dw = lambda: lib('c2dsr_ce_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
-    t_w = timeit(dw)
     fl = 2.0 * Mv * n * d
-    print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: fwd_u {t_f:.1f} us '
-          f'({2 * fl / t_f / 1e6:.0f} TFLOP/s credited, ns {ns}), dw {t_w:.1f} us ({fl / t_w / 1e6:.0f} credited, '
-          f'{2 * fl / t_w / 1e6:.0f} computed, nr {nr}); '
-          f'checksum {float(lse.sum()):.4f} {float(dWp.sum()):.4f}', flush=True)
+    for pre in ('c2dsr_ce_fused_', 'c2dsr_ce3b_fused_'):
+        fwd = lambda: lib(pre + 'fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tgt, H, W, bias,  # noqa
+                          lse, lse2, rows, s)
+        t_f = timeit(fwd)
+        lib('c2dsr_ce_row_weights', tgt, Mv, Mp, n, coef, Mv // 2, gscale, 0.7, padc, lse, rw, t32, lse2, crow, dpad,
+            s)
+        dw = lambda: lib(pre + 'dw', Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
+        t_w = timeit(dw)
+        print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))} {pre[6:-7]}: fwd_u {t_f:.1f} us '
+              f'({2 * fl / t_f / 1e6:.0f} TFLOP/s credited, ns {ns}), dw {t_w:.1f} us ({fl / t_w / 1e6:.0f} credited, '
+              f'{2 * fl / t_w / 1e6:.0f} computed, nr {nr}); '
+              f'checksum {float(lse.sum()):.4f} {float(dWp.sum()):.4f}', flush=True)
 
 
 if __name__ == '__main__':
