@@ -65,6 +65,22 @@ namespace {
 
 using namespace c2img;
 
+#ifdef CE3_STAMP  // diagnostic build only: per-phase cycle sums of the tile loop (tools/ce3_micro.py prints them)
+__device__ unsigned long long ce3_stamp_acc[8];
+#define STAMP(i)                                                   \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    const unsigned now_ = (unsigned)__builtin_amdgcn_s_memtime();  \
+    st_acc[i] += now_ - st_prev;                                   \
+    st_prev = now_;                                                \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
 constexpr int T3 = 32;  // swept rows per LDS tile
 
 // the two half-waves hold the two halves of a row's columns: combine them with one v_permlane32_swap (no LDS
@@ -347,7 +363,11 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
         (s_frags.template operator()<P>(oS, fa[P]), ...);
       }(std::make_integer_sequence<int, DS>{});
     }
+#ifdef CE3_STAMP
+    unsigned st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = (unsigned)__builtin_amdgcn_s_memtime();
+#endif
     for (int t = 0; t < ntiles; ++t) {
+      STAMP(5);
       const int bh = t % NB, bs = (t + 1) % NB;
       const int rn = min(w_beg + (t + 3) * T3, w_last);
       const bf16* nsrc = Xw + (long)rn * D2;
@@ -377,6 +397,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
           msub[sb] = mrow[sb] == -INFINITY ? 0.f : mrow[sb];
         }
       }
+      STAMP(0);
       Offs oS, oH;
       offs_rows(bs, oS);
       offs_tr(bh, oH);
@@ -423,9 +444,12 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
             }(),
             ...);
       }(std::make_integer_sequence<int, NSS>{});
+      STAMP(1);
       asm volatile("s_nop 7" ::: "memory");  // S(t+1)'s last results before the prep's VALU reads
       dma_wait();
+      STAMP(2);
       __syncthreads();
+      STAMP(3);
       // ---- second product (t) ∥ prep of S(t+1) ∥ DMA of tile t+3
       Offs oN;
       offs_rows((t + 2) % NB, oN);
@@ -473,7 +497,14 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       }
 #pragma unroll
       for (int i = 0; i < 2 * CB; ++i) sc[i] = sn[i];
+      STAMP(4);
     }
+#ifdef CE3_STAMP
+    if (lane == 0) {
+      for (int i = 0; i < 6; ++i) atomicAdd(&ce3_stamp_acc[i], (unsigned long long)st_acc[i]);
+      atomicAdd(&ce3_stamp_acc[6], (unsigned long long)ntiles);
+    }
+#endif
   }
   mfma_drain();
 #pragma unroll
@@ -586,3 +617,14 @@ C2_API int c2dsr_ce3b_fused_dw(const void* Hb, const void* Wb, const float* bias
   if (n == 0) return 0;
   return launch3<1, false>(Wb, Hb, bias2, crow, n, M, D, n_rsplit, nullptr, dbp, dWp, (hipStream_t)stream);
 }
+
+#ifdef CE3_STAMP
+C2_API int c2dsr_ce3_stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(ce3_stamp_acc), sizeof(ce3_stamp_acc));
+  if (e == hipSuccess && reset) {
+    static const unsigned long long z[8] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(ce3_stamp_acc), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif

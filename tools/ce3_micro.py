@@ -69,7 +69,27 @@ def main():
           f'{6 * fl / t_f / 1e6:.0f} executed, ns {ns}); dw {t_w:.1f} us ({fl / t_w / 1e6:.0f} credited, '
           f'{6 * fl / t_w / 1e6:.0f} executed, nr {nr}); checksum {float(lse.sum()):.4f} {float(dWp.sum()):.4f}',
           flush=True)
+    print_stamps([('fwd_u', fwd), ('dw', dw)])
 
+
+def print_stamps(fns):
+    """Diagnostic build (-DCE3_STAMP): cycles per tile per wave of the ce3 tile loop's phases."""
+    try:
+        fn = lib.raw('c2dsr_ce3_stamps')
+    except AttributeError:
+        return
+    import ctypes
+    buf = (ctypes.c_ulonglong * 8)()
+    ph = ('rescale/pre', 'S+epi', 'nop+dmawait', 'barrier', 'U+prep', 'loop-top')
+    for name, f in fns:
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        f()
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        tiles = max(1, buf[6])
+        print(f'  stamps {name}: ' + ', '.join(f'{p} {buf[i] / tiles:.0f}' for i, p in enumerate(ph))
+              + f' (cycles per tile per wave, {tiles} wave-tiles)', flush=True)
 
 if __name__ == '__main__':
     main()

@@ -70,6 +70,9 @@ def main():
               f'({2 * fl / t_f / 1e6:.0f} TFLOP/s credited, ns {ns}), dw {t_w:.1f} us ({fl / t_w / 1e6:.0f} credited, '
               f'{2 * fl / t_w / 1e6:.0f} computed, nr {nr}); '
               f'checksum {float(lse.sum()):.4f} {float(dWp.sum()):.4f}', flush=True)
+        if 'ce3b' in pre:
+            from ce3_micro import print_stamps
+            print_stamps([('fwd_u', fwd), ('dw', dw)])
 
 
 if __name__ == '__main__':
