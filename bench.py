@@ -529,6 +529,9 @@ def main():
                 # B=128 — the reference's own CPU-runnable case) for at least five timed steps
                 c1 = dict(n_a=29207, n_b=34886, d=64, L=15, B=128, label='Food-Kitchen sizes (synthetic), C1')
                 cpu['extra'] = {'c1_fk_d64': cpu_baseline(c1, *workload(c1, 'c1'), budget_s=5.0, min_steps=5)}
+                # and at configs[1] (C2: Food-Kitchen sizes, d=256, L=50, B=1024; one timed step ≈ 20 s)
+                fk = dict(CONFIGS['fk'])
+                cpu['extra']['c2_fk_d256'] = cpu_baseline(fk, *workload(fk, 'fk'), budget_s=10.0, min_steps=1)
         res['cpu_baseline'] = cpu
         if extra:
             res['extra_lines'] = extra

@@ -15,21 +15,7 @@
 
 typedef __bf16 bf16;
 
-// experiment switch (wrong results; timing only): ATTN_X_NOMFMA replaces the wave kernels' fp32 MFMAs by
-// one FMA into the accumulator, to measure how much of their time the matrix products take
-#ifndef ATTN_X_NOMFMA
-#define ATTN_X_NOMFMA 0
-#endif
-#if ATTN_X_NOMFMA
-template <typename V>
-__device__ __forceinline__ V wmfma_fake(float a, float b, V c) {
-  c[0] = fmaf(a, b, c[0]);
-  return c;
-}
-#define WMFMA(a, b, c, x, y, z) wmfma_fake((a), (b), (c))
-#else
 #define WMFMA(a, b, c, x, y, z) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), (x), (y), (z))
-#endif
 
 #include <cstdlib>
 
