@@ -63,13 +63,13 @@ def make_workload(cfg, n_seqs, seed=1):
     return rows, gs, gp
 
 
-def make_args(cfg, device, precision, dropout=0.2, zero1=False):
+def make_args(cfg, device, precision, dropout=0.2, zero1=False, gnn_shard=False):
     n = cfg['n_a'] + cfg['n_b'] + 1
     return SimpleNamespace(d_latent=cfg['d'], n_item=n, n_item_a=cfg['n_a'], n_item_b=cfg['n_b'], idx_pad=n - 1,
                            shared_item_embed=False, d_bias=False, n_gnn=1, dropout_gnn=dropout, n_attn=1, n_head=1,
                            dropout_attn=dropout, norm_first=False, len_max=cfg['L'], len_rec=10, lambda_loss=0.7,
                            lr=1e-3, l2=5e-4, lr_step=10, lr_gamma=0.5, batch_size=cfg['B'], device=device,
-                           precision=precision, seed=3407, zero1=zero1)
+                           precision=precision, seed=3407, zero1=zero1, gnn_shard=gnn_shard)
 
 
 class KernelTimer:
@@ -170,6 +170,9 @@ class HbmTimer:
     def launch_bytes(self, name, a):
         if name in ('c2dsr_gcn_spmm', 'c2dsr_gcn_spmm_b16'):  # table bytes per element: 4, or 2 (bf16 tables)
             d, E, N, tb = a[7], self.nnz[a[5]], self.N, (2 if name.endswith('_b16') else 4)
+            from c2dsr_amd import ops
+            if a[0] in ops.SPMM_SLICE:  # a row slice (chunked backward, row-sharded forward): its rows and edges
+                N, E = ops.SPMM_SLICE[a[0]]
             rows = 1 + (a[14] is not None) + (a[18] != 0.0) + (a[20] is not None)
             return tb * d * E + 8 * E + 4 * (N + 1) + tb * d * N * rows
         if name == 'c2dsr_embed_fwd':
@@ -458,6 +461,9 @@ def main():
     ap.add_argument('--no-c5', dest='c5_extra', action='store_false', help='skip the C5 extra line')
     ap.add_argument('--zero1', action='store_true',
                     help='N>1: ZeRO-1 (reduce-scatter, 1/p AdamW, all-gather; c2dsr_amd/dp.py) for the main line')
+    ap.add_argument('--gnn-shard', action='store_true',
+                    help='N>1: row-sharded GCN propagation (each rank propagates N/p rows, all-gather; ops.RowShard) '
+                         'for the main line')
     ap.add_argument('--dp-split', action='store_true',
                     help='strong scaling: every rank trains its slice of the same global batch (BASELINE '
                          'configs[3], e.g. --config ee --batch 4096)')
@@ -498,6 +504,11 @@ def main():
         r2 = run_train(opt, cfg, opt.config, opt.precision, wl, world, rank, device, zero1=alt)
         if rank == 0:
             extra['dp_zero1' if alt else 'dp_allreduce'] = brief(r2)
+        # the other GCN propagation of the N>1 path: row-sharded + all-gather, or replicated
+        torch.cuda.empty_cache()
+        r4 = run_train(opt, cfg, opt.config, opt.precision, wl, world, rank, device, gnn_shard=not opt.gnn_shard)
+        if rank == 0:
+            extra['dp_gnn_replicated' if opt.gnn_shard else 'dp_gnn_shard'] = brief(r4)
         if opt.config == 'mb' and not opt.batch:
             # BASELINE configs[3] (C4): Entertainment-Education sizes, B=4096 global split over the ranks
             # (strong scaling), the same exchange as the main line
@@ -559,7 +570,7 @@ def brief(r):
     return out
 
 
-def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp_split=None):
+def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp_split=None, gnn_shard=None):
     """W untimed + K timed training steps of one configuration; returns the bench line (rank 0)."""
     rows, gs, gp = wl
     B = cfg['B']
@@ -568,7 +579,8 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     from c2dsr_amd.trainer import Trainer
     zero1 = opt.zero1 if zero1 is None else zero1
     dp_split = opt.dp_split if dp_split is None else dp_split
-    args = make_args(cfg, device, precision, zero1=zero1 and world > 1)
+    gnn_shard = opt.gnn_shard if gnn_shard is None else gnn_shard
+    args = make_args(cfg, device, precision, zero1=zero1 and world > 1, gnn_shard=gnn_shard and world > 1)
     torch.manual_seed(3407)
     tr = Trainer(args, None, data=(None, None, None), graphs=(gs, gp))
     tr.dp_split = dp_split

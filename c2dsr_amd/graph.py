@@ -155,6 +155,7 @@ class DeviceGraph:
         self.work_t, self.split_t, self.n_work_t, self.n_split_t, self.n_slots_t = (to(wt), to(st), len(wt), len(st),
                                                                                     nslot_t)
         self.host = g
+        self._rowptr_t_host = t.rowptr
         self._row_keys = {False: (w[:, 0], s[:, 0]), True: (wt[:, 0], st[:, 0])}  # host copies, sorted by row
 
     def row_slice(self, transposed: bool, r0: int, r1: int):
@@ -163,6 +164,9 @@ class DeviceGraph:
         w0, w1 = np.searchsorted(wr, [r0, r1])
         s0, s1 = np.searchsorted(sr, [r0, r1])
         return int(w0), int(w1), int(s0), int(s1)
+
+    def host_rowptr(self, transposed: bool):
+        return self._rowptr_t_host if transposed else self.host.rowptr
 
     def plan(self, transposed: bool):
         if transposed:

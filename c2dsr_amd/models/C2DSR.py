@@ -8,8 +8,11 @@ embeddings (K2) and run the sequence encoders.  Each training call of
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from .. import dropout as DK
@@ -93,7 +96,11 @@ class C2DSR(nn.Module):
         nn.init.xavier_uniform_(self.D_a.weight)
         nn.init.xavier_uniform_(self.D_b.weight)
 
-        self.hi_share, self.hi_a, self.hi_b = None, None, None
+        self._hi = (None, None, None)
+        # row-sharded GCN propagation over the data-parallel ranks (ops.RowShard): args.gnn_shard
+        # or C2DSR_GNN_SHARD=1, effective when torch.distributed runs more than one rank
+        self.gnn_shard = bool(getattr(args, 'gnn_shard', False)) or os.environ.get('C2DSR_GNN_SHARD', '0') == '1'
+        self.row_shard = None
         self._tok = (None, None, None)
         self._sink = (None, None, None)
         self.state = StepState(seed=int(getattr(args, 'seed', 0)))
@@ -135,6 +142,23 @@ class C2DSR(nn.Module):
             self._dev_graphs = (DeviceGraph(self.adj_share, dev), DeviceGraph(self.adj_specific, dev))
         return self._dev_graphs
 
+    def _shard(self):
+        if not self.gnn_shard or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() < 2:
+            return None
+        if self.row_shard is None:
+            self.row_shard = ops.RowShard(dist.get_rank(), dist.get_world_size())
+        return self.row_shard
+
+    def _tables(self):
+        if self.row_shard is not None:
+            self.row_shard.wait()  # the all-gathers of the propagated tables (issued by convolve_graph)
+        return self._hi
+
+    # the GCN outputs of the last convolve_graph() (C2DSR.py:60-62)
+    hi_share = property(lambda self: self._tables()[0])
+    hi_a = property(lambda self: self._tables()[1])
+    hi_b = property(lambda self: self._tables()[2])
+
     def new_step(self):
         self.state.step += 1
         self.state.next_share_pass = DK.PASS_NEG0
@@ -145,10 +169,11 @@ class C2DSR(nn.Module):
         if self.training:
             self.new_step()
         g_share, g_spec = self.graphs()
-        hs, ts, ss = self.gnn_share.propagate(self.embed_i.weight, g_share)
-        ha, ta, sa = self.gnn_a.propagate(self.embed_i_a.weight, g_spec)
-        hb, tb, sb = self.gnn_b.propagate(self.embed_i_b.weight, g_spec)
-        self.hi_share, self.hi_a, self.hi_b = hs, ha, hb
+        sh = self._shard()
+        hs, ts, ss = self.gnn_share.propagate(self.embed_i.weight, g_share, shard=sh)
+        ha, ta, sa = self.gnn_a.propagate(self.embed_i_a.weight, g_spec, shard=sh)
+        hb, tb, sb = self.gnn_b.propagate(self.embed_i_b.weight, g_spec, shard=sh)
+        self._hi = (hs, ha, hb)
         self._tok, self._sink = (ts, ta, tb), (ss, sa, sb)
 
     def forward(self, seq_share, seq_a, seq_b, pos_share, pos_a, pos_b):

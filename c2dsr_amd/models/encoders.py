@@ -235,11 +235,13 @@ class GCN(nn.Module):
         p, keys = self._keys()
         return ops.GCNPropFn.apply(h, self._device_graph(adj, h.device), self.n_gnn, p, keys)
 
-    def propagate(self, h, adj, sink=None):
+    def propagate(self, h, adj, sink=None, shard=None):
         """The training step's fused form (C2DSR.convolve_graph): h [N, d], adj a DeviceGraph → (H, token,
-        sink); H's gradient arrives through the sink, filled by the embedding lookups of H (ops.GCNFn)."""
+        sink); H's gradient arrives through the sink, filled by the embedding lookups of H (ops.GCNFn).
+        ``shard``: an ops.RowShard — this rank propagates its block of rows and the blocks are all-gathered."""
         p, keys = self._keys()
         if sink is None:
             sink = ops.GradSink(h.shape[0], h.shape[1], h.device, self.state)
-        H, tok = ops.GCNFn.apply(h, self._device_graph(adj, h.device), self.n_gnn, p, keys, self.pad_row, sink)
+        H, tok = ops.GCNFn.apply(h, self._device_graph(adj, h.device), self.n_gnn, p, keys, self.pad_row, sink,
+                                 shard)
         return H, tok, sink

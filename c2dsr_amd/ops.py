@@ -479,6 +479,41 @@ class GradSink:
         return self.G
 
 
+class RowShard:
+    """Row-sharded GCN propagation over ``world`` data-parallel ranks: rank r owns rows
+    [r·c, (r+1)·c) of every propagated table, c = ⌈N/world⌉; tables are allocated with world·c rows (the tail
+    beyond N is never written or read) so the blocks all-gather in place."""
+
+    def __init__(self, rank, world, gather=None):
+        from .dp import all_gather
+        self.rank, self.world = rank, world
+        self._gather = gather or all_gather
+        self.pending = []
+
+    def block(self, n):
+        return (n + self.world - 1) // self.world
+
+    def rows(self, n):
+        c = self.block(n)
+        return min(n, self.rank * c), min(n, (self.rank + 1) * c)
+
+    def buffer(self, like):
+        n, d = like.shape
+        return torch.empty(self.block(n) * self.world, d, device=like.device, dtype=like.dtype)
+
+    def gather(self, full):
+        c = full.shape[0] // self.world
+        return self._gather(full, full[self.rank * c:(self.rank + 1) * c])
+
+    def wait(self):
+        for w in self.pending:
+            w.wait()
+        self.pending = []
+
+
+SPMM_SLICE = {}  # work-list pointer of a row-slice SpMM launch -> (rows, edges) (roofline accounting)
+
+
 def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, pad_row, gamma, Y, Y2=None,
          rows=None, part=None):
     """Y = alpha·P + (beta + [i != pad]·delta)·Z + gamma·Y with P = A·drop(X) (or drop(Aᵀ·X)); see c2dsr_gcn_spmm.
@@ -491,6 +526,9 @@ def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, p
     if rows is not None:
         w0, w1, s0, s1 = graph.row_slice(transposed, *rows)
         work, n_work, split, n_split = work[w0:w1], w1 - w0, split[s0:s1], s1 - s0
+        if w1 > w0:  # roofline accounting of a row-slice launch (bench.py HbmTimer): its rows and edges
+            rp = graph.host_rowptr(transposed)
+            SPMM_SLICE[work.data_ptr()] = (rows[1] - rows[0], int(rp[rows[1]]) - int(rp[rows[0]]))
     name = 'c2dsr_gcn_spmm_b16' if X.dtype == torch.bfloat16 else 'c2dsr_gcn_spmm'  # bf16 tables: the C5 run
     lib(name, work, n_work, split, n_split, part, col, val, d, X, keys[0], keys[1], float(p),
         int(mask_on_output), float(alpha), Z, float(beta), float(delta), int(pad_row), float(gamma), Y, Y2, stream())
@@ -500,21 +538,41 @@ def spmm(graph, transposed, X, keys, p, mask_on_output, alpha, Z, beta, delta, p
 class GCNFn(Function):
     """H = mean(E, A·drop(E), A·drop(A·drop(E)), ...)  (models/encoders.py:42-48).
     Outputs (H, token): H is non-differentiable; the scalar token carries the
-    dependency of every lookup of H back to this node."""
+    dependency of every lookup of H back to this node.
+
+    ``shard`` = a RowShard (data parallel): this rank propagates only its block of rows of
+    every round (the SpMM's row slice: the same work items, so the same bits) and the blocks are all-gathered —
+    synchronously for an intermediate round (the next round reads every row), asynchronously for H, whose
+    handle ``shard.pending`` is waited on before H is first read (C2DSR.forward).  The backward is unchanged:
+    each rank runs Aᵀ over its own lookup gradient and the flat-gradient exchange sums the ranks (dp.py)."""
 
     @staticmethod
-    def forward(ctx, E, graph, n_gnn, p, keys, pad_row, sink):
+    def forward(ctx, E, graph, n_gnn, p, keys, pad_row, sink, shard=None):
         require_device(E)
-        out = torch.empty_like(E)
         inv = 1.0 / (n_gnn + 1)
+        rows = None
+        if shard is not None and n_gnn > 0:
+            out_full = shard.buffer(E)
+            out = out_full[:E.shape[0]]
+            rows = shard.rows(E.shape[0])
+        else:
+            out = torch.empty_like(E)
         if n_gnn == 0:  # H = E
             spmm(graph, False, E, (0, 0), 0.0, 0, 0.0, E, 1.0, 0.0, -1, 0.0, out)
         h_prev = E
         for k in range(n_gnn):
-            h_k = None if k == n_gnn - 1 else torch.empty_like(E)
+            last = k == n_gnn - 1
+            h_full = None
+            if not last:
+                h_full = shard.buffer(E) if rows is not None else torch.empty_like(E)
+            h_k = None if last else h_full[:E.shape[0]]
             spmm(graph, False, h_prev, keys[k], p, 0, inv, E if k == 0 else None, inv, 0.0, -1,
-                 0.0 if k == 0 else 1.0, out, h_k)
+                 0.0 if k == 0 else 1.0, out, h_k, rows=rows)
+            if rows is not None and not last:
+                shard.gather(h_full).wait()  # the next round gathers rows of every block
             h_prev = h_k
+        if rows is not None:
+            shard.pending.append(shard.gather(out_full))
         ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
         ctx.E = E
         ctx.mark_non_differentiable(out)
@@ -528,7 +586,7 @@ class GCNFn(Function):
         E = ctx.E
         if G is None:
             notify_table(ctx.sink.state, E)
-            return (None,) * 7
+            return (None,) * 8
         g = ctx.graph
         n = ctx.n_gnn
         inv = 1.0 / (n + 1)
@@ -554,7 +612,7 @@ class GCNFn(Function):
         ctx.sink.G = None
         if direct:
             notify_table(ctx.sink.state, E)  # E.grad final: its all-reduce runs under the next GCN backward
-        return (None if direct else gE), None, None, None, None, None, None
+        return (None if direct else gE), None, None, None, None, None, None, None
 
 
 class GCNPropFn(Function):

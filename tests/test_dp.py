@@ -242,3 +242,49 @@ def _bucket_worker(rank, world, port, out_dir):
 def test_allreduce_ranges_world2_equal_full_allreduce(tmp_path):
     mp.spawn(_bucket_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert float(np.load(tmp_path / 'err.npy')[0]) == 0.0
+
+
+@pytest.mark.parametrize('world', [2, 3, 8])
+@pytest.mark.parametrize('n', [1, 7, 101, 100783])
+def test_row_shard_blocks_tile_the_table(world, n):
+    """ops.RowShard (row-sharded GCN propagation): the ranks' row blocks tile [0, n) in rank
+    order, every block (but a tail one) has ⌈n/world⌉ rows, and the padded buffer splits into world equal parts."""
+    from c2dsr_amd.ops import RowShard
+    pos = 0
+    for r in range(world):
+        sh = RowShard(r, world, gather=lambda out, inp: _Done())
+        r0, r1 = sh.rows(n)
+        assert r0 == pos and r1 >= r0
+        assert r1 - r0 == sh.block(n) or r1 == n
+        pos = r1
+        buf = sh.buffer(torch.empty(n, 4))
+        assert buf.shape == (sh.block(n) * world, 4) and buf.shape[0] >= n
+    assert pos == n
+
+
+def _shard_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from c2dsr_amd.ops import RowShard
+        sh = RowShard(rank, world)
+        n, d = 37, 8
+        full = sh.buffer(torch.empty(n, d))
+        full.fill_(-1.0)
+        r0, r1 = sh.rows(n)
+        ref = torch.arange(n * d, dtype=torch.float32).view(n, d)
+        full[r0:r1] = ref[r0:r1]  # this rank's block only
+        sh.pending.append(sh.gather(full))
+        sh.wait()
+        torch.save(full[:n].clone(), os.path.join(out_dir, f'g{rank}.pt'))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_shard_gather_world3(tmp_path):
+    """The blocks written by each rank are all-gathered in place into every rank's full table (gloo, 3 ranks)."""
+    port = _free_port()
+    mp.spawn(_shard_worker, args=(3, port, str(tmp_path)), nprocs=3, join=True)
+    ref = torch.arange(37 * 8, dtype=torch.float32).view(37, 8)
+    for r in range(3):
+        assert torch.equal(torch.load(tmp_path / f'g{r}.pt', weights_only=True), ref)

@@ -492,6 +492,52 @@ def test_zero1_world2_equals_replicated_and_reference(tmp_path, name):
             assert rel(got, want) < 1e-3, n
 
 
+def _shard_gpu_worker(rank, world, port, name, shard, out_dir):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), C2DSR_GNN_SHARD='1' if shard else '0')
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        gs, gp = golden_graphs(name)
+        tr = build_trainer(make_args(G.CONFIGS[name], dropout=0.2), gs, gp, G.init_params(name))
+        tr.model.train()
+        tr.optimizer.zero_grad()
+        m = G.load(f'model_{name}.npz')
+        hs = {}
+        for s in range(int(m['n_steps'])):
+            tr.model.convolve_graph()
+            if s == 0:
+                assert (tr.model.row_shard is not None) == shard
+                hs = {k: getattr(tr.model, k).detach().cpu().numpy() for k in ('hi_share', 'hi_a', 'hi_b')}
+            tr.train_batch(G.batch(name, int(m[f's{s}/batch_lo']), int(m[f's{s}/batch_n'])))
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, f'p{rank}_{int(shard)}.npz'),
+                 **{n: p.detach().cpu().numpy() for n, p in tr.model.named_parameters()},
+                 **{f'H/{k}': v for k, v in hs.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('name', ['base', 'var'])
+def test_row_sharded_gcn_world2_equals_replicated(tmp_path, name):
+    """Row-sharded GCN propagation (ops.RowShard, SURVEY.md §8 f3: each rank propagates its block of rows of
+    every round and the blocks are all-gathered; 'var' has n_gnn = 2, so an intermediate round is gathered
+    too) vs the replicated propagation, two ranks on cuda:0 over gloo with dropout 0.2 over all golden steps:
+    the propagated tables of the first step and the final parameters are bit-equal on both ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    for shard in (False, True):
+        with socket.socket() as s:
+            s.bind(('127.0.0.1', 0))
+            port = s.getsockname()[1]
+        mp.spawn(_shard_gpu_worker, args=(2, port, name, shard, str(tmp_path)), nprocs=2, join=True)
+    ref = np.load(tmp_path / 'p0_0.npz')
+    for f in ('p1_0.npz', 'p0_1.npz', 'p1_1.npz'):
+        got = np.load(tmp_path / f)
+        for n in ref.files:
+            np.testing.assert_array_equal(got[n], ref[n], err_msg=f'{f} {n}')
+
+
 C4 = dict(n_a=8367, n_b=11404, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
           norm_first=False, d_bias=False, shared_item_embed=False)
 
