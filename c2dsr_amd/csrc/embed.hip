@@ -154,8 +154,10 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
 // the chunks' head/tail slots.  A "split" is a run that continues past the end of its first
 // chunk: out[key] += tail[c] + head[c+1] + ... + head[last], summed in chunk order (pass B).  The
 // split list depends on the indices only, so it is part of the plan (off the critical path).
+// Chunk length (tools/embed_micro.py, MB embedding backward, items + positions in one launch): 32 → 61.7 µs,
+// 16 → 54.0 µs (twice the waves, each half as long), 8 → 64.3, 64 → 70.2 (the split passes grow below 16).
 #ifndef SEG_CH_CFG
-#define SEG_CH_CFG 32
+#define SEG_CH_CFG 16
 #endif
 constexpr int SEG_CH = SEG_CH_CFG;
 constexpr int PL_T = 256;         // plan kernels: threads per block

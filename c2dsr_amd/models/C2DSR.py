@@ -150,6 +150,7 @@ class C2DSR(nn.Module):
         return self.row_shard
 
     def _tables(self):
+        self.launch_graph()
         if self.row_shard is not None:
             self.row_shard.wait()  # the all-gathers of the propagated tables (issued by convolve_graph)
         return self._hi
@@ -165,19 +166,39 @@ class C2DSR(nn.Module):
 
     # ------------------------------------------------------------------ reference API
     def convolve_graph(self):
-        """C2DSR.py:59-62."""
+        """C2DSR.py:59-62.  The three propagations are enqueued by ``launch_graph``: at the first read of a table
+        (hi_* / forward), or earlier by the trainer — right after its index work, so that work (and the host
+        read of its counts) is queued ahead of the GCN kernels instead of behind them (trainer._train_batch)."""
         if self.training:
             self.new_step()
+        self._graph_pending = (torch.is_grad_enabled(), self.training)  # the modes of the call, kept for the launch
+
+    def launch_graph(self):
+        pending = getattr(self, '_graph_pending', None)
+        if not pending:
+            return
+        self._graph_pending = None
+        grad, train = pending
         g_share, g_spec = self.graphs()
         sh = self._shard()
-        hs, ts, ss = self.gnn_share.propagate(self.embed_i.weight, g_share, shard=sh)
-        ha, ta, sa = self.gnn_a.propagate(self.embed_i_a.weight, g_spec, shard=sh)
-        hb, tb, sb = self.gnn_b.propagate(self.embed_i_b.weight, g_spec, shard=sh)
+        mods = (self.gnn_share, self.gnn_a, self.gnn_b)
+        modes = [g.training for g in mods]
+        for g in mods:
+            g.training = train
+        try:
+            with torch.set_grad_enabled(grad):
+                hs, ts, ss = self.gnn_share.propagate(self.embed_i.weight, g_share, shard=sh)
+                ha, ta, sa = self.gnn_a.propagate(self.embed_i_a.weight, g_spec, shard=sh)
+                hb, tb, sb = self.gnn_b.propagate(self.embed_i_b.weight, g_spec, shard=sh)
+        finally:
+            for g, t in zip(mods, modes):
+                g.training = t
         self._hi = (hs, ha, hb)
         self._tok, self._sink = (ts, ta, tb), (ss, sa, sb)
 
     def forward(self, seq_share, seq_a, seq_b, pos_share, pos_a, pos_b):
         """C2DSR.py:64-77 → (h_share, hx, hy), each [B, L, d]."""
+        self.launch_graph()
         (ts, ta, tb), (ss, sa, sb) = self._tok, self._sink
         h_share = self.attn_share.forward_items(seq_share, pos_share, self.hi_share, ts, self.embed_i.weight, ss,
                                                 DK.PASS_SHARE)
@@ -187,6 +208,7 @@ class C2DSR(nn.Module):
 
     def forward_share(self, seq, pos):
         """C2DSR.py:79-85 (shared table + attn_share only)."""
+        self.launch_graph()
         pass_id = self.state.next_share_pass
         self.state.next_share_pass += 1
         return self.attn_share.forward_items(seq, pos, self.hi_share, self._tok[0], self.embed_i.weight,

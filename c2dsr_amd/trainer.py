@@ -248,6 +248,9 @@ class Trainer(object):
         self.dp_counts = None
         need, pads, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b,
                                           (seq_share, seq_a, seq_b, neg_a, neg_b))
+        # the GCN forwards of convolve_graph() are enqueued now, behind the index work and its count copy: the host
+        # reads those counts while the device still has the propagations to run (no idle gap at the read)
+        m.launch_graph()
         plans = None
         if m.training:
             # the embedding backward's sort plans of every pass (side stream), enqueued by the loss head right

@@ -507,8 +507,8 @@ def _shard_gpu_worker(rank, world, port, name, shard, out_dir):
         for s in range(int(m['n_steps'])):
             tr.model.convolve_graph()
             if s == 0:
-                assert (tr.model.row_shard is not None) == shard
                 hs = {k: getattr(tr.model, k).detach().cpu().numpy() for k in ('hi_share', 'hi_a', 'hi_b')}
+                assert (tr.model.row_shard is not None) == shard
             tr.train_batch(G.batch(name, int(m[f's{s}/batch_lo']), int(m[f's{s}/batch_n'])))
         torch.cuda.synchronize()
         np.savez(os.path.join(out_dir, f'p{rank}_{int(shard)}.npz'),
