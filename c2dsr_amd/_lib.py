@@ -56,7 +56,6 @@ class HipLibError(RuntimeError):
 
 
 DEBUG_SYNC = os.environ.get('C2DSR_DEBUG_SYNC', '0') == '1'
-_FAST = os.environ.get('C2DSR_LIB_FAST', '1') == '1'
 
 
 class _Lib:
@@ -93,7 +92,7 @@ class _Lib:
             fn = self._fns[name] = getattr(self.load(), name)
         lib = self._lib
         conv = [a.data_ptr() if isinstance(a, torch.Tensor) else a for a in args]
-        if _FAST and not DEBUG_SYNC and name not in self.time_names:  # the common path: one ctypes call
+        if not DEBUG_SYNC and name not in self.time_names:  # the common path: one ctypes call
             rc = fn(*conv)
             if rc != 0:
                 raise HipLibError(f'{name} failed with hipError {rc}')

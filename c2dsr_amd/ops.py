@@ -655,7 +655,6 @@ class GCNPropFn(Function):
 
 # ----------------------------------------------------------------------------- index plans
 _side_streams = {}
-_PLAN_SIDE = __import__('os').environ.get('C2DSR_PLAN_SIDE', '1') == '1'
 PLAN_SRC = {}  # plan buffer data_ptr -> data_ptr of the index tensor it sorts (roofline accounting)
 ROW_COUNT = {}  # compact gradient part data_ptr -> its rows (roofline accounting of c2dsr_embed_bwd_planned_rows)
 
@@ -686,7 +685,7 @@ class IndexPlan:
     @staticmethod
     def _launch(pairs, bufs, sizes, whole):
         dev = whole.device
-        side = side_stream(dev) if _PLAN_SIDE else torch.cuda.current_stream(dev)
+        side = side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))  # the indices and the buffer are ready
         for (idx, n_keys), buf, nb in zip(pairs, bufs, sizes):
             PLAN_SRC[buf.data_ptr()] = idx.data_ptr()
@@ -1058,7 +1057,7 @@ class QKVAttnFn(Function):
         d = d3 // 3
         M = B * L
         s = stream()
-        b16 = (ctx.precision == BF16 and _B16_DQKV and bool(lib.raw('c2dsr_attn_bwd_b16_supported')(L, d, ctx.n_head))
+        b16 = (ctx.precision == BF16 and bool(lib.raw('c2dsr_attn_bwd_b16_supported')(L, d, ctx.n_head))
                and rgemm_ok(M, d, d3) and wgemm_ok(M, d3, d))
         args = (qkv, seq, int(ctx.pad), B, L, d, ctx.n_head, ctx.keys[0], ctx.keys[1], float(ctx.p), int(ctx.b_base), P,
                 dout.contiguous())
@@ -1072,7 +1071,6 @@ class QKVAttnFn(Function):
         return (dx,) + (None,) * 10
 
 
-_B16_DQKV = __import__('os').environ.get('C2DSR_B16_DQKV', '1') == '1'
 
 
 def attn_rows_ok(L, d, n_head):
@@ -1156,7 +1154,7 @@ class RowsQKVAttnFn(Function):
         rs, ks = ctx.rs, ctx.ks
         nq, nk = q.shape[0], kv.shape[0]
         s = stream()
-        b16 = (ctx.precision == BF16 and _B16_DQKV and rgemm_ok(max(nq, 1), d, d) and rgemm_ok(max(nk, 1), d, 2 * d)
+        b16 = (ctx.precision == BF16 and rgemm_ok(max(nq, 1), d, d) and rgemm_ok(max(nk, 1), d, 2 * d)
                and wgemm_ok(max(nq, 1), d, d) and wgemm_ok(max(nk, 1), 2 * d, d))
         gt = torch.bfloat16 if b16 else torch.float32
         dq = torch.empty(nq, d, device=q.device, dtype=gt)

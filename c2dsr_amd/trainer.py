@@ -29,7 +29,6 @@ from .metrics import RankMetrics
 from .models.C2DSR import C2DSR
 from .optim import FlatAdamW
 
-_GC_STEP = os.environ.get('C2DSR_GC_STEP', '1') == '1'
 
 
 def dp_rows(B_full, rank, world, dp_split=True, global_rows=None):
@@ -90,11 +89,12 @@ class Trainer(object):
         self.n_item_a = args.n_item_a
         self.n_item_b = args.n_item_b
         self.len_rec = args.len_rec
-        self.compact_rows = os.environ.get('C2DSR_ROW_COMPACT', '1') == '1'
+        # the last encoder layer's row-wise part on the rows the loss reads (tests compare both layouts)
+        self.compact_rows = True
         # last-layer attention on the read rows / padding keys only (ops.RowsQKVAttnFn)
-        self.rows_attn = os.environ.get('C2DSR_ROWS_ATTN', '1') == '1'
+        self.rows_attn = True
         # projection weight gradients grouped per weight across passes (ops.WGradBatch)
-        self.batch_wgrad = os.environ.get('C2DSR_BATCH_WGRAD', '1') == '1'
+        self.batch_wgrad = True
         self.lambda_loss = args.lambda_loss
         self.dp_split = True  # slice each global batch across data-parallel ranks
 
@@ -231,7 +231,7 @@ class Trainer(object):
         own batch; ``global_rows`` then gives the global batch size).
         Python's cyclic collector is paused while the step is enqueued (a collection in the middle of the
         launch sequence leaves the device idle); it runs after the optimizer launch, under that kernel."""
-        if not _GC_STEP or not gc.isenabled():
+        if not gc.isenabled():
             return self._train_batch(batch, global_rows=global_rows)
         gc.disable()
         try:
