@@ -118,6 +118,32 @@ __device__ __forceinline__ void stv(tbf16* p, const RowV<tbf16>& r) {
   *(tbf16x8*)p = x;
 }
 
+// non-temporal forms (streamed rows touched once per launch: they should not evict re-read rows from L2 / MALL)
+typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ RowV<float> ldv_nt(const float* p) {
+  const nt_f32x4 v = __builtin_nontemporal_load((const nt_f32x4*)p);
+  return RowV<float>{{make_float4(v[0], v[1], v[2], v[3])}};
+}
+__device__ __forceinline__ RowV<tbf16> ldv_nt(const tbf16* p) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  typedef tbf16 tbf16x8 __attribute__((ext_vector_type(8)));
+  const tbf16x8 x = __builtin_bit_cast(tbf16x8, __builtin_nontemporal_load((const s16x8*)p));
+  return RowV<tbf16>{{make_float4((float)x[0], (float)x[1], (float)x[2], (float)x[3]),
+                      make_float4((float)x[4], (float)x[5], (float)x[6], (float)x[7])}};
+}
+__device__ __forceinline__ void stv_nt(float* p, const RowV<float>& r) {
+  const nt_f32x4 v = {r.v[0].x, r.v[0].y, r.v[0].z, r.v[0].w};
+  __builtin_nontemporal_store(v, (nt_f32x4*)p);
+}
+__device__ __forceinline__ void stv_nt(tbf16* p, const RowV<tbf16>& r) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  typedef tbf16 tbf16x8 __attribute__((ext_vector_type(8)));
+  tbf16x8 x;
+  x[0] = (tbf16)r.v[0].x; x[1] = (tbf16)r.v[0].y; x[2] = (tbf16)r.v[0].z; x[3] = (tbf16)r.v[0].w;
+  x[4] = (tbf16)r.v[1].x; x[5] = (tbf16)r.v[1].y; x[6] = (tbf16)r.v[1].z; x[7] = (tbf16)r.v[1].w;
+  __builtin_nontemporal_store(__builtin_bit_cast(s16x8, x), (s16x8*)p);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -17,7 +17,24 @@
 // fp32, or bf16 for the C5 roofline run (c2dsr_gcn_spmm_b16: SURVEY.md §8(d); fp32 arithmetic, RNE stores).
 #include "common.h"
 
+// GCN_NT 1: the epilogue's row streams (Z, the accumulated Y, the Y / Y2 stores) bypass the caches' normal
+// retention, leaving L2 / MALL to the gathered rows X[col] (Zipf-popular rows are re-read)
+#ifndef GCN_NT
+#define GCN_NT 1
+#endif
+
 namespace {
+
+template <typename T>
+__device__ __forceinline__ c2::RowV<T> ld_stream(const T* p) {
+  if constexpr (GCN_NT) return c2::ldv_nt(p);
+  else return c2::ldv(p);
+}
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, const c2::RowV<T>& r) {
+  if constexpr (GCN_NT) c2::stv_nt(p, r);
+  else c2::stv(p, r);
+}
 
 template <typename T>
 struct Epi {
@@ -38,22 +55,22 @@ __device__ __forceinline__ void epilogue(c2::RowV<T> acc, long row, int c, int d
 #pragma unroll
     for (int h = 0; h < NH; ++h) acc.v[h] = acc.v[h] * ep.drop.mul4((uint64_t)row * d + c + 4 * h);
   }
-  if (ep.Y2) c2::stv(ep.Y2 + row * d + c, acc);
+  if (ep.Y2) st_stream(ep.Y2 + row * d + c, acc);
   c2::RowV<T> y;
 #pragma unroll
   for (int h = 0; h < NH; ++h) y.v[h] = ep.alpha * acc.v[h];
   if (ep.Z) {
     const float zc = ep.beta + (row != ep.pad_row ? ep.delta : 0.f);
-    const c2::RowV<T> z = c2::ldv(ep.Z + row * d + c);
+    const c2::RowV<T> z = ld_stream(ep.Z + row * d + c);
 #pragma unroll
     for (int h = 0; h < NH; ++h) y.v[h] = c2::fma4(zc, z.v[h], y.v[h]);
   }
   if (ep.gamma != 0.f) {
-    const c2::RowV<T> o = c2::ldv(ep.Y + row * d + c);
+    const c2::RowV<T> o = ld_stream(ep.Y + row * d + c);
 #pragma unroll
     for (int h = 0; h < NH; ++h) y.v[h] = c2::fma4(ep.gamma, o.v[h], y.v[h]);
   }
-  c2::stv(ep.Y + row * d + c, y);
+  st_stream(ep.Y + row * d + c, y);
 }
 
 // work[w] = {row, e_begin, e_end, slot}; slot < 0: whole row (epilogue), else partial slab index.
