@@ -433,6 +433,13 @@ def run_c5(opt, world, rank, device, emit=True):
                           'graph_sequences': opt.c5_seqs, 'graph_nnz': g.nnz, 'dropout': p,
                           'parallelism': f'dp{world}'},
                'roofline': roof, 'cpu_baseline': None}
+        tpath = os.path.join(ROOT, 'profiles', 'c5_traffic.json')
+        if modes[0] == 'bf16' and os.path.exists(tpath):  # PMC DRAM bytes of the same step (tools/pmc_traffic.py c5)
+            with open(tpath) as f:
+                t = json.load(f)
+            roof['traffic'] = t.get('bytes_per_step')
+            roof['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
+            roof['traffic_source'] = t.get('source')
         for m in modes[1:]:  # the other table storage on the same graph and batch
             r2, el2 = res[m]
             out[f'{m}_tables'] = {'value': round(r2['achieved'] * world, 1),

@@ -3,6 +3,8 @@ FETCH_SIZE (KB) doubled per the gfx950 correction (MI355X_MICROARCH.md §HBM), W
 Also the K1 + K2 kernels (GCN SpMM, embedding gather / segment sums) per step → hbm_traffic.json next to
 the K5 file (the PMC run is bench.py --steps 2 --warmup 1: 3 steps).
 usage: python tools/pmc_traffic.py gpurun_out/TAG [profiles/k5_traffic_fp32.json] [fp32|bf16]
+       python tools/pmc_traffic.py gpurun_out/TAG profiles/c5_traffic.json c5   (the C5 line: bench.py --config c5
+       --c5-tables bf16 --steps 2 --warmup 1; K1 + K2 only, written to the given file)
 (the precision of the profiled bench line selects the K5 kernels: fp32 mode = ce3.hip, bf16 = ce.hip; the K1+K2
 file is written next to the K5 file as hbm_traffic[_fp32].json)"""
 import csv
@@ -30,11 +32,14 @@ def per_kernel(path, counter, names=K5):
             continue
         name = re.sub(r'\(anonymous namespace\)::', '', r['Kernel_Name'])
         for k in names:
-            if (k in name) if '<' in k else re.search(r'\b' + k + r'\b', name):
+            # (names of the bf16-table instantiations stay mangled: a plain substring test there)
+            if (k in name) if ('<' in k or name.startswith('_Z')) else re.search(r'\b' + k + r'\b', name):
                 vals[k].append(float(r['Counter_Value']) * 1e3)  # KB -> B
     return vals
 
 
+if prec == 'c5':
+    K5 = ()
 fe = per_kernel(f'{pre}_fetch/run_counter_collection.csv', 'FETCH_SIZE')
 wr = per_kernel(f'{pre}_write/run_counter_collection.csv', 'WRITE_SIZE')
 rows = {}
@@ -62,7 +67,8 @@ try:
     print(f'K5 MFMA busy: {mfma_busy}')
 except FileNotFoundError:
     pass
-if out:
+rev = subprocess.run(['git', 'rev-parse', '--short', 'HEAD'], capture_output=True, text=True).stdout.strip()
+if out and prec != 'c5':
     rev = subprocess.run(['git', 'rev-parse', '--short', 'HEAD'], capture_output=True, text=True).stdout.strip()
     json.dump(dict(bytes_per_launch_triple=tot, per_kernel=rows, mfma_busy=mfma_busy,
                    source=f'rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE passes, {pre.split("/")[-1]}, rev {rev}'),
@@ -83,5 +89,6 @@ if out:
     import os
     json.dump(dict(bytes_per_step=tot2, per_kernel=rows2,
                    source=f'rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE passes, {pre.split("/")[-1]}, rev {rev}'),
-              open(os.path.join(os.path.dirname(out), 'hbm_traffic.json' if prec == 'bf16' else 'hbm_traffic_fp32.json'),
+              open(out if prec == 'c5' else
+                   os.path.join(os.path.dirname(out), 'hbm_traffic.json' if prec == 'bf16' else 'hbm_traffic_fp32.json'),
                    'w'), indent=1)
