@@ -17,6 +17,8 @@
 // fp32, or bf16 for the C5 roofline run (c2dsr_gcn_spmm_b16: SURVEY.md §8(d); fp32 arithmetic, RNE stores).
 #include "common.h"
 
+#include <type_traits>
+
 // GCN_NT 1: the epilogue's row streams (Z, the accumulated Y, the Y / Y2 stores) bypass the caches' normal
 // retention, leaving L2 / MALL to the gathered rows X[col] (Zipf-popular rows are re-read)
 #ifndef GCN_NT
@@ -137,6 +139,84 @@ __global__ __launch_bounds__(256) void spmm_kernel(const int4* __restrict__ work
   }
 }
 
+// The same with NC 16-byte slices of the row per lane, loaded together (d == LPR·VW·NC): every edge's whole row
+// is in flight at once instead of one slice per pass over the edges — and with LPR = 32 two work items share a
+// wave.  Same accumulation order per element as spmm_kernel (edges in order).
+template <int LPR, int NC, bool MASK_OUT, typename T>
+__global__ __launch_bounds__(256) void spmm_nc_kernel(const int4* __restrict__ work, int n_work,
+                                                      const int* __restrict__ col, const float* __restrict__ val,
+                                                      int d, const T* __restrict__ X, Epi<T> ep,
+                                                      float* __restrict__ part) {
+  constexpr int GROUPS = 256 / LPR;
+  constexpr int V = c2::VW<T>, NH = V / 4;
+  constexpr int UE = NC >= 2 ? 2 : 4;  // row slices in flight per lane: UE·NC
+  const int g = threadIdx.x / LPR;
+  const int lane = threadIdx.x % LPR;
+  const long w = (long)blockIdx.x * GROUPS + g;
+  if (w >= n_work) return;
+  const int4 wk = work[w];
+  const long row = wk.x;
+  const int e0 = wk.y, e1 = wk.z, slot = wk.w;
+  const c2::Drop& drop = ep.drop;
+  c2::RowV<T> acc[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc[k].v[h] = c2::f4(0.f);
+  auto cof = [&](int k) { return lane * V + k * LPR * V; };
+  int e = e0;
+  for (; e + UE - 1 < e1; e += UE) {
+    int j[UE];
+    float vv[UE];
+#pragma unroll
+    for (int u = 0; u < UE; ++u) {
+      j[u] = col[e + u];
+      vv[u] = val[e + u];
+    }
+    c2::RowV<T> x[UE][NC];
+#pragma unroll
+    for (int u = 0; u < UE; ++u)
+#pragma unroll
+      for (int k = 0; k < NC; ++k) x[u][k] = c2::ldv(X + (long)j[u] * d + cof(k));
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      if (!MASK_OUT && drop.active()) {
+#pragma unroll
+        for (int u = 0; u < UE; ++u)
+#pragma unroll
+          for (int h = 0; h < NH; ++h) x[u][k].v[h] = x[u][k].v[h] * drop.mul4((uint64_t)j[u] * d + cof(k) + 4 * h);
+      }
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int u = 0; u < UE; ++u) acc[k].v[h] = c2::fma4(vv[u], x[u][k].v[h], acc[k].v[h]);
+    }
+  }
+  for (; e < e1; ++e) {
+    const int j = col[e];
+    const float v = val[e];
+    c2::RowV<T> x[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) x[k] = c2::ldv(X + (long)j * d + cof(k));
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        if (!MASK_OUT && drop.active()) x[k].v[h] = x[k].v[h] * drop.mul4((uint64_t)j * d + cof(k) + 4 * h);
+        acc[k].v[h] = c2::fma4(v, x[k].v[h], acc[k].v[h]);
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    if (slot >= 0) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) *(float4*)(part + (long)slot * d + cof(k) + 4 * h) = acc[k].v[h];
+    } else {
+      epilogue<MASK_OUT>(acc[k], row, cof(k), d, ep);
+    }
+  }
+}
+
 #ifndef COMBINE_U
 #define COMBINE_U 16
 #endif
@@ -189,6 +269,21 @@ int launch(const int4* work, int n_work, const int4* split, int n_split, const i
            const T* X, const Epi<T>& ep, float* part, hipStream_t s) {
   const int lpr = lpr_for(d * 4 / c2::VW<T>);  // lanes per row: VW elements each
   const int groups = 256 / lpr;
+#ifndef SPMM_NC
+#define SPMM_NC 1
+#endif
+  // fp32 rows of d = 512: both 16-byte slices of a lane loaded per edge in one pass over the edges (C5 fp32 tables
+  // 6838 → 6894 GB/s).  bf16 rows stay one slice per lane, one work item per wave: two work items per wave (32
+  // lanes × 2 slices) measured 15.6 → 16.4 ms per launch at C5
+  if (SPMM_NC && d == 512 && std::is_same_v<T, float>) {
+    constexpr int L = 64;
+    spmm_nc_kernel<L, 2, MASK_OUT, T><<<c2::ceil_div(n_work, 256 / L), 256, 0, s>>>(work, n_work, col, val, d, X, ep,
+                                                                                  part);
+    if (n_split > 0)
+      combine_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_split, 256 / L), 256, 0, s>>>(split, n_split, d, ep, part);
+    C2_CHECK_LAUNCH();
+    return 0;
+  }
 #define C2_SPMM(L)                                                                                              \
   spmm_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_work, groups), 256, 0, s>>>(work, n_work, col, val, d, X, ep, part); \
   if (n_split > 0) combine_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_split, groups), 256, 0, s>>>(split, n_split, d, ep, part);
