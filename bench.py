@@ -663,7 +663,8 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     if hb is not None and name == 'mb' and precision in ('bf16', 'fp32'):
         hb['traffic'], hb['traffic_source'] = hbm_traffic(precision)
         hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
-    par = f'dp{world}' + ('-split' if dp_split and world > 1 else '') + ('-zero1' if zero1 and world > 1 else '')
+    par = (f'dp{world}' + ('-split' if dp_split and world > 1 else '') + ('-zero1' if zero1 and world > 1 else '')
+           + ('-gnnshard' if gnn_shard and world > 1 else ''))
     return {'metric': 'train sequences/sec at d=256, seq_len=50, |items|~100k',
             'value': round(value, 2), 'unit': 'train sequences/sec', 'n_gpus': world, 'steps': opt.steps,
             'warmup': opt.warmup, 'ms_per_step': round(ms, 3), 'higher_is_better': True,
