@@ -64,11 +64,19 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint32_t* __r
                                                             int nblocks, uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[256];
   h[threadIdx.x] = 0;
-  __syncthreads();
+  // every round's key loaded up front (one memory round trip per block instead of one per round)
+  uint32_t k[RS_ROUNDS];
   const int base = blockIdx.x * RS_TILE;
+#pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
-    int i = base + r * RS_THREADS + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    const int i = base + r * RS_THREADS + threadIdx.x;
+    k[r] = i < n ? keys[i] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int i = base + r * RS_THREADS + threadIdx.x;
+    if (i < n) atomicAdd(&h[(k[r] >> shift) & 255u], 1u);
   }
   __syncthreads();
   hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
@@ -84,6 +92,16 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
   __shared__ uint32_t run[256];
   __shared__ uint32_t gbase[256];
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int base = blockIdx.x * RS_TILE;
+  // every round's key and row loaded up front: their latency overlaps the offset computation below instead of
+  // opening each of the RS_ROUNDS rounds
+  uint32_t kr[RS_ROUNDS], vr[RS_ROUNDS];
+#pragma unroll
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int i = base + r * RS_THREADS + t;
+    kr[r] = i < n ? kin[i] : 0u;
+    vr[r] = i < n ? vin[i] : 0u;
+  }
   for (int q = 0; q < 4; ++q) wcnt[q][t] = 0;
   run[t] = 0;
   {
@@ -91,6 +109,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
     // blocks): read off the digit histograms of all blocks here instead of a separate single-workgroup scan
     const uint32_t* ht = offs + (long)t * nblocks;
     uint32_t pre = 0, tot = 0;
+#pragma unroll 8
     for (int b = 0; b < nblocks; ++b) {
       const uint32_t c = ht[b];
       pre += b < (int)blockIdx.x ? c : 0u;
@@ -110,16 +129,12 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
   }
   __syncthreads();
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int base = blockIdx.x * RS_TILE;
+#pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const int i = base + r * RS_THREADS + t;
     const bool act = i < n;
-    uint32_t key = 0, val = 0, dg = 0;
-    if (act) {
-      key = kin[i];
-      val = vin[i];
-      dg = (key >> shift) & 255u;
-    }
+    const uint32_t key = kr[r], val = vr[r];
+    const uint32_t dg = act ? (key >> shift) & 255u : 0u;
     uint64_t peers = __ballot(act);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -154,8 +169,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
 // the chunks' head/tail slots.  A "split" is a run that continues past the end of its first
 // chunk: out[key] += tail[c] + head[c+1] + ... + head[last], summed in chunk order (pass B).  The
 // split list depends on the indices only, so it is part of the plan (off the critical path).
-// Chunk length (tools/embed_micro.py, MB embedding backward, items + positions in one launch): 32 → 61.7 µs,
-// 16 → 54.0 µs (twice the waves, each half as long), 8 → 64.3, 64 → 70.2 (the split passes grow below 16).
+// Chunk length (tools/embed_micro.py, MB embedding backward, items + positions in one launch): 16 entries with 2
+// rows in flight (SEG_U below) 54.0 µs against 61.7 at 32 / 4 — twice the waves, each half as long; 8 → 64.3,
+// 64 → 70.2 (the split passes grow below 16).
 #ifndef SEG_CH_CFG
 #define SEG_CH_CFG 16
 #endif
@@ -245,11 +261,11 @@ __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restr
 }
 
 // ------------------------------------------------------------------ segment sums
-// rows in flight per lane group: 4 (occupancy over batch depth — the embedding backward at the bench shapes:
-// 8 → 87 µs, 4 → 68 µs, 16 → 133 µs per pass); SEG_PIPE 1 = the next batch's rows loaded under this batch's
-// read-modify-writes (measured no better at 4)
+// rows in flight per lane group: 2 with 16-entry chunks (tools/embed_micro.py, items + positions: CH 32 / U 4 61.7 µs,
+// CH 16 / U 4 61.1, CH 16 / U 2 54.0–54.9, CH 16 / U 1 54.0, CH 8 / U 2 64.4; round 2 at CH 32: U 8 → 87 µs,
+// U 16 → 133); SEG_PIPE 1 = the next batch's rows loaded under this batch's read-modify-writes (no better at 4)
 #ifndef SEG_U_CFG
-#define SEG_U_CFG 4
+#define SEG_U_CFG 2
 #endif
 constexpr int SEG_U = SEG_U_CFG;  // rows in flight per lane group
 #ifndef SEG_PIPE
