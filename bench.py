@@ -207,9 +207,20 @@ class HbmTimer:
         if not per:
             return None
         ach = tb / (tms * 1e-3) / 1e9
+        # north_star names "embedding-gather + GNN-SpMM": the same accounting over those kernels alone (the forward
+        # gathers and both SpMM directions), next to the whole K1 + K2 figure that also carries the backward's
+        # deterministic segment sums
+        gs = [n for n in per if 'spmm' in n or 'embed_fwd' in n]
+        gb = sum(per[n]['bytes_per_launch'] * per[n]['launches'] for n in gs)
+        gms = sum(per[n]['avg_ms'] * per[n]['launches'] for n in gs)
+        gather_spmm = None
+        if gms > 0:
+            ga = gb / (gms * 1e-3) / 1e9
+            gather_spmm = dict(achieved=round(ga, 1), frac=round(ga / PEAK_HBM_GBS, 4), kernels=gs)
         return dict(bound='hbm', achieved=round(ach, 1), peak=PEAK_HBM_GBS, unit='GB/s', frac=round(ach / PEAK_HBM_GBS, 4),
                     traffic=None, kernel='K1 c2dsr_gcn_spmm (fwd+bwd) + K2 c2dsr_embed_fwd/bwd; algorithmic bytes '
-                    '(bench.py HbmTimer)', ms_per_step=round(tms / steps, 4), per_kernel=per)
+                    '(bench.py HbmTimer)', ms_per_step=round(tms / steps, 4), per_kernel=per,
+                    gather_spmm=gather_spmm)
 
 
 def uniq_counts(batches, host):
@@ -573,7 +584,8 @@ def brief(r):
     out = {k: r[k] for k in keep}
     for k in ('roofline', 'roofline_hbm'):
         if r.get(k):
-            out[k] = {kk: r[k][kk] for kk in ('bound', 'achieved', 'peak', 'unit', 'frac', 'ms_per_step')}
+            out[k] = {kk: r[k][kk] for kk in ('bound', 'achieved', 'peak', 'unit', 'frac', 'ms_per_step', 'gather_spmm')
+                      if kk in r[k]}
     return out
 
 
