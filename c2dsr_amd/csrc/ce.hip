@@ -710,11 +710,19 @@ __global__ void ce_dh_from_u_kernel(const float* __restrict__ Up, const float* _
   const int r = (int)(i / D), k = (int)(i % D);
   const float l2 = lse2[r];
   float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int s = 0; s < ns; ++s) {
-    const float m = pm[(long)s * M + r];
-    if (m == -INFINITY) continue;
-    t = c2::fma4(exp2f(m - l2), *(const float4*)(Up + ((long)s * M) * D + i), t);
-  }
+  // every split's running max, then every split's slab loaded before the first add (one round trip each instead
+  // of ns dependent pairs); added in split order as before.  ns <= DHU_MAX (losshead.split_count caps it at 16).
+  constexpr int DHU_MAX = 16;
+  float mm[DHU_MAX];
+#pragma unroll
+  for (int s = 0; s < DHU_MAX; ++s) mm[s] = s < ns ? pm[(long)s * M + r] : -INFINITY;
+  float4 u[DHU_MAX];
+#pragma unroll
+  for (int s = 0; s < DHU_MAX; ++s)
+    u[s] = mm[s] != -INFINITY ? *(const float4*)(Up + ((long)s * M) * D + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < DHU_MAX; ++s)
+    if (mm[s] != -INFINITY) t = c2::fma4(exp2f(mm[s] - l2), u[s], t);
   const float w = rw[r];
   const int tg = t32[r];
   if (tg >= 0 && tg < n) t = c2::fma4(-1.f, *(const float4*)(W + (long)tg * D + k), t);
@@ -1120,7 +1128,7 @@ C2_API int c2dsr_ce_rows(const float* part_m, const float* part_s, int n_split, 
 C2_API int c2dsr_ce_dh_from_u(const float* Up, const float* part_m, int ns, int M, int D, const float* lse2,
                               const int* t32, const float* rw, const float* W, int n, float* dH, void* stream) {
   if (M == 0) return 0;
-  if (D % 4) return (int)hipErrorInvalidValue;
+  if (D % 4 || ns < 1 || ns > 16) return (int)hipErrorInvalidValue;  // the kernel holds at most 16 splits
   ce_dh_from_u_kernel<<<c2::ceil_div((long)M * D / 4, 256), 256, 0, (hipStream_t)stream>>>(Up, part_m, ns, M, D, lse2,
                                                                                           t32, rw, W, n, dH);
   C2_CHECK_LAUNCH();
