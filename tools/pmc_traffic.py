@@ -5,7 +5,8 @@ the K5 file (the PMC run is bench.py --steps 2 --warmup 1: 3 steps).
 usage: python tools/pmc_traffic.py gpurun_out/TAG [profiles/k5_traffic_fp32.json] [fp32|bf16]
        python tools/pmc_traffic.py gpurun_out/TAG profiles/c5_traffic.json c5   (the C5 line: bench.py --config c5
        --c5-tables bf16 --steps 2 --warmup 1; K1 + K2 only, written to the given file)
-(the precision of the profiled bench line selects the K5 kernels: fp32 mode = ce3.hip, bf16 = ce.hip; the K1+K2
+(the precision of the profiled bench line selects the K5 kernels: ce3.hip's split (fp32 mode) or plain-bf16
+instantiation; the K1+K2
 file is written next to the K5 file as hbm_traffic[_fp32].json)"""
 import csv
 import json
@@ -18,8 +19,9 @@ pre = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else None
 prec = sys.argv[3] if len(sys.argv) > 3 else 'fp32'
 # the kernels the two timed K5 entry points launch per head (fwd_u: sweep + rows; dw: sweep)
-K5 = (('ce_fwdu_kernel', 'ce_rows_kernel', 'ce_dw_kernel') if prec == 'bf16' else
-      ('ce3_kernel<256, 0>', 'ce_rows_kernel', 'ce3_kernel<256, 1>'))
+# (ce3_kernel<D, MODE, SPLIT>: SPLIT = true in the fp32 mode, false for the plain-bf16 instantiation)
+K5 = (('ce3_kernel<256, 0, false>', 'ce_rows_kernel', 'ce3_kernel<256, 1, false>') if prec == 'bf16' else
+      ('ce3_kernel<256, 0, true>', 'ce_rows_kernel', 'ce3_kernel<256, 1, true>'))
 K12 = ('spmm_kernel', 'combine_kernel', 'embed_fwd_kernel', 'seg_chunk_kernel', 'seg_split1_kernel',
        'seg_split2_kernel')
 PMC_STEPS = 3
