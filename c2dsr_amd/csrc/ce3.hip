@@ -165,7 +165,8 @@ template <int D, int MODE, bool SPLIT>
 __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs, const bf16* __restrict__ Xw,
                                                       const float* __restrict__ svec, const float* __restrict__ wvec,
                                                       int n_s, int n_w, int per_split, float* __restrict__ part_m,
-                                                      float* __restrict__ part_s, float* __restrict__ outp) {
+                                                      float* __restrict__ part_s, float* __restrict__ outp,
+                                                      int accum) {
   constexpr int T3 = tile_rows<SPLIT>();
   constexpr int CB = T3 / 16;                      // 16-row swept blocks per tile
   constexpr int UK = T3 / 32;                      // 32-row k-steps of the second product per e-block
@@ -514,11 +515,17 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
     if (s < n_s) {
       if (g == 0) {
         if constexpr (MODE == 0) part_m[(long)split * n_s + s] = mrow[sb];
-        part_s[(long)split * n_s + s] = ztot;
+        // accum (MODE 1, one split: this workgroup owns its columns): add onto the epoch-long gradient directly
+        part_s[(long)split * n_s + s] = accum ? part_s[s] + ztot : ztot;
       }
       float* out = outp + ((long)split * n_s + s) * D + 4 * g;
+      if (accum) {
 #pragma unroll
-      for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
+        for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = *(const f32x4*)(out + 16 * e) + dacc[e][sb];
+      } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
+      }
     }
   }
 }
@@ -552,14 +559,18 @@ int per_split3(int total, int nsplit, int t3) {
 template <int MODE, bool SPLIT>
 int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec, int n_s, int n_w, int D, int nsplit,
             float* pm, float* ps, float* out, hipStream_t st) {
+  // MODE 1 with nsplit == 0: one split, accumulated straight onto out / ps (the gradient buffers)
+  const int accum = MODE == 1 && nsplit == 0;
+  if (accum) nsplit = 1;
+  if (nsplit < 1) return (int)hipErrorInvalidValue;
   const int per = per_split3(n_w, nsplit, tile_rows<SPLIT>());
   const dim3 grid(c2::ceil_div(n_s, 128) * nsplit);  // (row block, split) pairs: ce3_kernel's XCD-aware map
   if (D == 128)
     ce3_kernel<128, MODE, SPLIT><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm,
-                                                        ps, out);
+                                                        ps, out, accum);
   else if (D == 256)
     ce3_kernel<256, MODE, SPLIT><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm,
-                                                        ps, out);
+                                                        ps, out, accum);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();

@@ -319,14 +319,19 @@ class LossHeadFn(Function):
                         lib('c2dsr_ce_dh_combine', dHp, ns, Mv, d, t32, rw, W, n, dHc, s)
                         del dHp
                     nr = split_count(n, 128)
-                    dWp = torch.empty(nr, n, d, **f32)
-                    dbp = torch.empty(nr, n, **f32)
-                    lib(ce_entry(ctx.x3, d, 'dw'), Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)
-                    if gW is not None:
-                        lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
-                    if gb is not None:
-                        lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
-                    del dWp, dbp
+                    entry = ce_entry(ctx.x3, d, 'dw')
+                    if nr == 1 and gW is not None and gb is not None and entry.startswith('c2dsr_ce3'):
+                        # one split: the sweep adds onto the gradients itself (n_rsplit = 0; no partials / sum)
+                        lib(entry, Hb, Wb, bias2, Mv, n, d, 0, crow, gW, gb, s)
+                    else:
+                        dWp = torch.empty(nr, n, d, **f32)
+                        dbp = torch.empty(nr, n, **f32)
+                        lib(entry, Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)
+                        if gW is not None:
+                            lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
+                        if gb is not None:
+                            lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
+                        del dWp, dbp
                     if (gW is not None or gb is not None) and tplan is not None:
                         wsb = int(lib.raw('c2dsr_ce_onehot_planned_workspace')(Mv, n, d))
                         ws = torch.empty(wsb, device=dev, dtype=torch.uint8)

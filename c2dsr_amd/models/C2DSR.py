@@ -97,6 +97,11 @@ class C2DSR(nn.Module):
         nn.init.xavier_uniform_(self.D_b.weight)
 
         self._hi = (None, None, None)
+        # deferred propagation (convolve_graph → first read) only for a model driven by c2dsr_amd.Trainer, whose
+        # step reads the tables right after its index work; a model used on its own propagates at the call, as
+        # the reference does (C2DSR.py:59-62)
+        self.defer_graph = False
+        self._graph_versions = None
         # row-sharded GCN propagation over the data-parallel ranks (ops.RowShard): args.gnn_shard
         # or C2DSR_GNN_SHARD=1, effective when torch.distributed runs more than one rank
         self.gnn_shard = bool(getattr(args, 'gnn_shard', False)) or os.environ.get('C2DSR_GNN_SHARD', '0') == '1'
@@ -166,17 +171,29 @@ class C2DSR(nn.Module):
 
     # ------------------------------------------------------------------ reference API
     def convolve_graph(self):
-        """C2DSR.py:59-62.  The three propagations are enqueued by ``launch_graph``: at the first read of a table
-        (hi_* / forward), or earlier by the trainer — right after its index work, so that work (and the host
-        read of its counts) is queued ahead of the GCN kernels instead of behind them (trainer._train_batch)."""
+        """C2DSR.py:59-62.  The three propagations are enqueued by ``launch_graph``: at the call, or — for a model
+        driven by c2dsr_amd.Trainer (``defer_graph``) — at the first read of a table (hi_* / forward) or earlier by
+        the trainer, right after its index work, so that work (and the host read of its counts) is queued ahead of
+        the GCN kernels instead of behind them (trainer._train_batch).  A deferred launch refuses item-embedding
+        weights modified in place since the call (optimizer step, load_state_dict, manual edits)."""
         if self.training:
             self.new_step()
         self._graph_pending = (torch.is_grad_enabled(), self.training)  # the modes of the call, kept for the launch
+        self._graph_versions = self._table_versions()
+        if not self.defer_graph:
+            self.launch_graph()
+
+    def _table_versions(self):
+        return tuple(w._version for w in (self.embed_i.weight, self.embed_i_a.weight, self.embed_i_b.weight))
 
     def launch_graph(self):
         pending = getattr(self, '_graph_pending', None)
         if not pending:
             return
+        if self._table_versions() != self._graph_versions:
+            # the tables would be built from weights the reference's convolve_graph() never saw
+            raise RuntimeError('item-embedding weights were modified between convolve_graph() and the first read '
+                               'of its tables (deferred propagation, C2DSR.defer_graph); call convolve_graph() again')
         self._graph_pending = None
         grad, train = pending
         g_share, g_spec = self.graphs()

@@ -181,6 +181,9 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
         if len(relu_drop) > 3:
             rowmap = relu_drop[3]
     if x3:
+        if A.dtype != torch.float32 or Bb.dtype != torch.bfloat16 or Bb.shape[-1] != 2 * K:
+            raise TypeError(f'rgemm x3: A must be fp32 and Bb a split image [N, 2K] (got A {A.dtype}, Bb {Bb.dtype} '
+                            f'{tuple(Bb.shape)})')
         lib('c2dsr_rgemm_x3', M, N, K, A, K, Bb, 2 * K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
             int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
     elif A.dtype == torch.bfloat16:  # the attention backward's bf16 dqkv (in_proj dX; c2dsr_rgemm_aux_b16a)
@@ -246,6 +249,8 @@ def wgemm(dY, X, dW, *, T, N, D, beta=1.0, db=None, defer=True, x3=False):
     """dW[N, D] = beta·dW + dYᵀ·X over T rows and (db given) db[N] = beta·db + Σ_t dY[t]
     (c2dsr_wgemm, deterministic split-t partials; x3: split-bf16 products, c2dsr_wgemm_x3).  With a
     WGradBatch active (and beta = 1) the product is deferred into it."""
+    if x3 and (dY.dtype != torch.float32 or X.dtype != torch.float32):
+        raise TypeError(f'wgemm x3: fp32 operands only (got dY {dY.dtype}, X {X.dtype})')
     if defer and WBATCH is not None and beta == 1.0 and dY.is_contiguous() and X.is_contiguous():
         WBATCH.add(dY, X, dW, db, T, N, D, x3)
         return

@@ -97,6 +97,7 @@ class Trainer(object):
         self.batch_wgrad = True
         self.lambda_loss = args.lambda_loss
         self.dp_split = True  # slice each global batch across data-parallel ranks
+        self.model.defer_graph = True  # convolve_graph() → launch behind the step's index work (_train_batch)
 
     # ------------------------------------------------------------------ training
     def run_epoch(self):

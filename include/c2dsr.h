@@ -292,7 +292,9 @@ int c2dsr_ce_rows(const float* part_m, const float* part_s, int n_split, int M, 
  * c2dsr_ce_fused_fwd_u / c2dsr_ce_fused_dw (trainer.py:131-154), but the operands are split-bf16 images
  * [rows][2·D] = hi ‖ lo (x = hi + lo to 2^-17 relative; c2dsr_f32_split_bf16) and every product runs as
  * three bf16 MFMAs (hi·hi + lo·hi + hi·lo) with fp32 accumulation.  Hx holds ⌈M/32⌉·32 rows and Wx
- * ⌈n/32⌉·32 rows (zero rows past the end); bias2 as for ce.hip; crow holds ⌈M/64⌉·64 + 64 values. */
+ * ⌈n/32⌉·32 rows (zero rows past the end); bias2 as for ce.hip; crow holds ⌈M/64⌉·64 + 64 values.
+ * dw with n_rsplit == 0 (also c2dsr_ce3b_fused_dw): one split whose workgroups own their columns, added straight
+ * onto dWp [n][D] / dbp [n] (the parameters' epoch-long gradients, trainer.py:42 — no partials, no sum). */
 int c2dsr_ce3_supported(int D);
 int c2dsr_f32_split_bf16(const float* x, long rows, int D, long rows_out, void* out, void* stream);
 int c2dsr_ce3_fused_fwd_u(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_split,

@@ -18,7 +18,7 @@ def rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-def _run(H, W, b, pl, t, coef, lam, ns, nr, BR):
+def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None):
     """The fp32-mode head exactly as losshead.py drives it (x3 kernels)."""
     from c2dsr_amd._lib import lib, stream
     s = stream()
@@ -47,12 +47,15 @@ def _run(H, W, b, pl, t, coef, lam, ns, nr, BR):
     lib('c2dsr_ce_row_weights', d(t), M, M_pad, n, d(coef), BR, d(gs), lam, d(pl), lse, rw, t32, lse2, crow, dpad, s)
     dH = torch.empty(M, D, device=DEV)
     lib('c2dsr_ce_dh_from_u', Up, pm, ns, M, D, lse2, t32, rw, d(W), n, dH, s)
-    gW = torch.zeros(n, D, device=DEV)
-    gb = torch.zeros(n, device=DEV)
-    dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
-    lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, M, n, D, nr, crow, dWp, dbp, s)
-    lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
-    lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
+    gW = torch.zeros(n, D, device=DEV) if g0 is None else g0[0].clone().to(DEV)
+    gb = torch.zeros(n, device=DEV) if g0 is None else g0[1].clone().to(DEV)
+    if nr == 0:  # one split added straight onto the gradients
+        lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, M, n, D, 0, crow, gW, gb, s)
+    else:
+        dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
+        lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, M, n, D, nr, crow, dWp, dbp, s)
+        lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
+        lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M, n, D))
     ws = torch.empty(wsb, device=DEV, dtype=torch.uint8)
     lib('c2dsr_ce_onehot_dw', d(t), M, n, d(H), D, rw, gW, gb, ws, wsb, s)
@@ -124,6 +127,24 @@ def test_ce3_online_rescale(M, n, D, ns):
     print('ce3 rescale errors', {k: f'{v:.2e}' for k, v in err.items()})
     assert err.pop('lse') < TOL_LSE
     assert all(v < 1e-4 for v in err.values()), err
+
+
+def test_ce3_dw_accumulates_onto_gradient():
+    """n_rsplit = 0 (one split, losshead.py when split_count(n) == 1): the dW / db sweep adds onto the existing
+    gradient buffers (the epoch-long accumulation, Q3) and equals the partial + sum path bit for bit."""
+    M, n, D = 500, 2100, 256
+    g = torch.Generator().manual_seed(99)
+    H = torch.randn(M, D, generator=g) * 0.5
+    W = torch.randn(n, D, generator=g) * 0.5
+    b = torch.randn(n, generator=g) * 0.1
+    pl = torch.randn(M, generator=g)
+    t = torch.randint(0, n + 1, (M,), generator=g)
+    coef = torch.tensor([0.37, 1.9])
+    g0 = (torch.randn(n, D, generator=g), torch.randn(n, generator=g))
+    r1 = _run(H, W, b, pl, t, coef, 0.7, 3, 0, M // 2, g0=g0)
+    r2 = _run(H, W, b, pl, t, coef, 0.7, 3, 1, M // 2, g0=g0)
+    assert torch.equal(r1[3], r2[3]) and torch.equal(r1[4], r2[4])
+    assert not torch.equal(r1[3].cpu(), g0[0])
 
 
 def test_split_bf16_is_exact_to_2e17():
@@ -244,3 +265,60 @@ def test_split_weight_images_multi():
         assert torch.equal(y, ref)
     hi, lo = outs[1][1][:, :768].float(), outs[1][1][:, 768:].float()
     assert float((hi + lo - Ws[0].T).abs().max() / Ws[0].abs().max()) < 2 ** -16
+
+
+def _ref_chunked(H, W, b, pl, t, coef, lam, BR, chunk=2048):
+    """_ref in float64 on the device, in row chunks (the MB head-b logits are 9.7 GB in float64)."""
+    H, W, b, pl, t = (x.to(DEV) for x in (H, W, b, pl, t))
+    Hd, Wd, bd = H.double(), W.double(), b.double()
+    M, n = H.shape[0], W.shape[0]
+    lse = torch.empty(M, dtype=torch.float64, device=DEV)
+    rows = torch.empty(M, dtype=torch.float64, device=DEV)
+    dH = torch.empty(M, H.shape[1], dtype=torch.float64, device=DEV)
+    gW = torch.zeros(n, H.shape[1], dtype=torch.float64, device=DEV)
+    gb = torch.zeros(n, dtype=torch.float64, device=DEV)
+    dpad = torch.empty(M, dtype=torch.float64, device=DEV)
+    cf = coef.double().to(DEV)
+    for r0 in range(0, M, chunk):
+        r1 = min(M, r0 + chunk)
+        lg = torch.cat([Hd[r0:r1] @ Wd.T + bd, pl[r0:r1].double()[:, None]], 1)
+        ls = torch.logsumexp(lg, 1)
+        tt = t[r0:r1]
+        valid = tt != n
+        lse[r0:r1] = ls
+        rows[r0:r1] = torch.where(valid, ls - lg.gather(1, tt[:, None])[:, 0], torch.zeros_like(ls))
+        w_r = torch.where(valid, lam * cf[(torch.arange(r0, r1, device=DEV) >= BR).long()], torch.zeros_like(ls))
+        dl = torch.exp(lg - ls[:, None])
+        dl[torch.arange(r1 - r0, device=DEV), tt] -= 1.0
+        dl *= w_r[:, None]
+        dH[r0:r1] = dl[:, :n] @ Wd
+        gW += dl[:, :n].T @ Hd[r0:r1]
+        gb += dl[:, :n].sum(0)
+        dpad[r0:r1] = dl[:, n]
+        del lg, dl
+    return lse, rows, dH, gW, gb, dpad
+
+
+def test_ce3_mb_head_b_shape_matches_float64():
+    """K5 at the headline's own shape: Movie-Book head b — Mv = 18,944 valid stacked rows,
+    n = 63,937 columns, d = 256 — with the split counts losshead.py derives for it (split_count over 128-row /
+    128-column tiles) and the XCD block map over ~2,000 column tiles, against float64 on the same fp32
+    operands: full lse and per-row losses, the whole dH, dW and db.  Operand scales as in training: H like a
+    LayerNorm output (unit normal), W / b like the classifier's nn.Linear init (U(±1/√d))."""
+    from c2dsr_amd.losshead import split_count
+    M, n, D = 18944, 63937, 256
+    g = torch.Generator().manual_seed(2048)
+    H = torch.randn(M, D, generator=g)
+    W = (torch.rand(n, D, generator=g) * 2 - 1) / 16
+    b = (torch.rand(n, generator=g) * 2 - 1) / 16
+    pl = torch.randn(M, generator=g) * 0.3
+    t = torch.randint(0, n, (M,), generator=g)
+    coef, lam, BR = torch.tensor([0.45, 1.0]), 0.7, 9100
+    ns, nr = split_count(M, 128), split_count(n, 128)
+    lse, rows, dH, gW, gb, dpad, _ = _run(H, W, b, pl, t, coef, lam, ns, nr, BR)
+    ref = _ref_chunked(H, W, b, pl, t, coef, lam, BR)
+    err = {k: rel(x, r) for k, x, r in zip(('lse', 'rows', 'dH', 'gW', 'gb', 'dpad'), (lse, rows, dH, gW, gb, dpad),
+                                           ref)}
+    print(f'ce3 MB head b (ns={ns}, nr={nr}) errors', {k: f'{v:.2e}' for k, v in err.items()})
+    assert err.pop('lse') < TOL_LSE
+    assert all(v < TOL for v in err.values()), err

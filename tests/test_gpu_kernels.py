@@ -62,7 +62,10 @@ def test_gemm_relu_dropout_epilogue():
     assert rel(C, ref) < 1e-5
 
 
-@pytest.mark.parametrize('d,n_gnn,p', [(16, 1, 0.0), (64, 1, 0.25), (256, 2, 0.2), (12, 1, 0.0)])
+# d = 512 runs the fp32 one-pass-over-the-edges SpMM (spmm_nc_kernel, both 16-byte slices per lane; the C5 width):
+# its dropout element index and split-row (hub) combine are checked here against the oracle
+@pytest.mark.parametrize('d,n_gnn,p', [(16, 1, 0.0), (64, 1, 0.25), (256, 2, 0.2), (12, 1, 0.0), (512, 1, 0.2),
+                                       (512, 2, 0.3)])
 def test_gcn_fwd_bwd_vs_oracle(d, n_gnn, p):
     from c2dsr_amd import ops
     from c2dsr_amd.graph import DeviceGraph, normalized_csr

@@ -53,12 +53,18 @@ def capture(tr):
         box['need'] = {pid: rs.idx[:rs.n].long().cpu() for pid, rs in m.state.need.items()}
         out = orig_fwd(*a)
         box['h_share'], box['hx'], box['hy'] = [o.detach().clone() for o in out]
+        for key, o in zip(('h_share', 'hx', 'hy'), out):  # the loss head's gradient w.r.t. each output
+            if o.requires_grad:
+                o.register_hook(lambda g, key=key: box.setdefault('dh', {}).__setitem__(key, g.detach().clone()))
         box['hi_share'], box['hi_a'], box['hi_b'] = m.hi_share.clone(), m.hi_a.clone(), m.hi_b.clone()
         return out
 
     def fsh(seq, pos):
         out = orig_share(seq, pos)
+        key = f"neg{len(box.get('neg', []))}"
         box.setdefault('neg', []).append(out.detach().clone())
+        if out.requires_grad:
+            out.register_hook(lambda g, key=key: box.setdefault('dh', {}).__setitem__(key, g.detach().clone()))
         return out
 
     def step():
@@ -294,7 +300,7 @@ def test_fp32_step_d256_matches_oracle():
 FULL = {'C3_mb': (36845, 63937, 2048), 'C2_fk': (29207, 34886, 1024)}
 
 
-def loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, tol_loss, tol_grad):
+def loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, tol_loss, tol_grad, tol_dh=None):
     """The fused loss head of the HIP step (classifier heads + CE, discriminators) against the oracle's loss
     head (torch fp32 on the device) evaluated on the HIP encoder outputs of the same step: the three losses
     (relative tol_loss) and the head parameters' gradients (tol_grad of max-abs).  P: the parameters before
@@ -314,9 +320,9 @@ def loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, tol_loss, 
         out[idx.to(DEV)] = got.reshape(-1, d)
         return out.reshape(B, L, d)
 
-    hs = [full(k, v).requires_grad_(False) for k, v in (('h_share', box['h_share']), ('hx', box['hx']),
-                                                         ('hy', box['hy']), ('neg0', box['neg'][0]),
-                                                         ('neg1', box['neg'][1]))]
+    keys = ('h_share', 'hx', 'hy', 'neg0', 'neg1')
+    hs = [full(k, v).requires_grad_(tol_dh is not None)
+          for k, v in zip(keys, (box['h_share'], box['hx'], box['hy'], box['neg'][0], box['neg'][1]))]
     names = ['classifier_a.weight', 'classifier_a.bias', 'classifier_b.weight', 'classifier_b.bias',
              'classifier_pad.weight', 'classifier_pad.bias', 'D_a.weight', 'D_b.weight']
     for n in names:
@@ -324,13 +330,32 @@ def loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, tol_loss, 
     cfg = dict(n_item_a=c['n_a'], n_item_b=c['n_b'], len_rec=c['len_rec'], lambda_loss=0.7)
     bd = tuple(x.to(DEV) for x in b)
     out = O.loss_head(P, *hs, bd, cfg)
-    grads = torch.autograd.grad(out['loss'], [P[n] for n in names])
+    wrt = [P[n] for n in names] + (hs if tol_dh is not None else [])
+    grads = torch.autograd.grad(out['loss'], wrt)
+    worst = {}
     for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
         e = abs(float(v.detach()) - float(out[k])) / abs(float(out[k]))
+        worst[k] = e
         assert e < tol_loss, (k, float(v), float(out[k]), e)
     for n, g in zip(names, grads):
         e = rel(box['grads'][n], g)
+        worst[n] = e
         assert e < tol_grad, (n, e)
+    if tol_dh is not None:
+        # the input gradient of the loss head (K5's dH, the pooling / discriminator backward) on every row the
+        # loss reads, against the oracle's gradient w.r.t. the same encoder outputs
+        for k, g in zip(keys, grads[len(names):]):
+            got = box['dh'][k]
+            pid = {'h_share': DK.PASS_SHARE, 'hx': DK.PASS_A, 'hy': DK.PASS_B, 'neg0': DK.PASS_NEG0,
+                   'neg1': DK.PASS_NEG0 + 1}[k]
+            idx = box['need'].get(pid)
+            ref = g.reshape(-1, d)
+            if idx is not None and got.reshape(-1, d).shape[0] == idx.numel():
+                ref = ref[idx.to(DEV)]
+            e = rel(got.reshape(-1, d), ref)
+            worst['d' + k] = e
+            assert e < tol_dh, ('d' + k, e)
+    return worst
 
 
 @pytest.mark.parametrize('cfg', ['C3_mb', 'C2_fk'])
@@ -341,11 +366,16 @@ def test_bf16_full_size_loss_head_vs_fp32(compact, cfg):
     the discriminators agree with the fp32 materialised loss head (the oracle's loss_head, run with torch on
     the device) evaluated on the HIP encoder outputs of the same step — the losses and the classifier /
     discriminator gradients (VERDICT r01 #1)."""
+    tr, box, b, c, B, loss, loss_rec, loss_mi, P = _full_case(cfg, 'bf16', compact)
+    loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, 2e-3, BF16_GRAD)
+
+
+def _full_case(cfg, precision, compact):
+    """One step of the benchmarked configuration (FULL[cfg]: d=256, L=50, R=10, dropout 0.2) in the given
+    precision mode; returns what loss_head_vs_oracle needs."""
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
     from c2dsr_amd import synth
-    from c2dsr_amd import dropout as DK
-    from oracle import c2dsr_oracle as O
     import random
     n_a, n_b, B = FULL[cfg]
     c = dict(n_a=n_a, n_b=n_b, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
@@ -354,7 +384,7 @@ def test_bf16_full_size_loss_head_vs_fp32(compact, cfg):
     random.seed(3407)
     rows = DL.to_arrays(DL.preprocess_train(seqs, c['n_a'], c['n_b'], c['len_max']))
     gs, gp = GR.preprocess_graph(seqs, c['n_a'], c['n_a'] + c['n_b'] + 1)
-    args = make_args(c, dropout=0.2, precision='bf16', seed=3407)
+    args = make_args(c, dropout=0.2, precision=precision, seed=3407)
     args.batch_size = B
     torch.manual_seed(0)
     tr = build_trainer(args, gs, gp)
@@ -369,8 +399,22 @@ def test_bf16_full_size_loss_head_vs_fp32(compact, cfg):
     torch.cuda.synchronize()
     assert all(math.isfinite(float(v.detach())) for v in (loss, loss_rec, loss_mi))
     assert bool(box['need']) == compact
+    return tr, box, b, c, B, loss, loss_rec, loss_mi, P
 
-    loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, 2e-3, BF16_GRAD)
+
+@pytest.mark.parametrize('cfg', ['C3_mb', 'C2_fk'])
+@pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
+def test_fp32_full_size_loss_head_vs_oracle(compact, cfg):
+    """The HEADLINE mode at the headline size: the fp32 mode (split-bf16 fused CE =
+    ce3_kernel at the bench's shapes — Mv ≈ 19k valid rows, n = 63,937 / 36,845 columns, the bench's split counts
+    and XCD block map —, the x3 bilinear products) at C3 (Movie-Book item counts, B=2048) and C2 (Food-Kitchen,
+    B=1024), dropout 0.2, against the oracle's fp32 loss head (torch on the device, materialised logits) on the
+    HIP encoder outputs of the same step: the three losses at 1e-4 relative, every classifier / discriminator
+    gradient and the loss head's gradient w.r.t. the five encoder outputs (K5's dH included) at 1e-4 of
+    max-abs (north_star's tolerance)."""
+    tr, box, b, c, B, loss, loss_rec, loss_mi, P = _full_case(cfg, 'fp32', compact)
+    worst = loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, TOL, TOL, tol_dh=TOL)
+    print(f'fp32 {cfg} worst:', {k: f'{v:.1e}' for k, v in sorted(worst.items(), key=lambda x: -x[1])[:6]})
 
 
 def test_c1_food_kitchen_shape_fp32_vs_oracle():
@@ -667,3 +711,133 @@ def test_d256_step_matches_reference(compact):
     for n_, g in box['grads'].items():
         worst[n_] = check(f'grad/{n_}', g)
     print('d256 vs reference, worst:', {k: f'{v:.1e}' for k, v in sorted(worst.items(), key=lambda x: -x[1])[:6]})
+
+
+def _sha(arrs):
+    import hashlib
+    h = hashlib.sha256()
+    for a in arrs:
+        a = np.ascontiguousarray(a)
+        h.update(str(a.dtype).encode() + str(a.shape).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
+def test_c2_step_matches_reference(compact):
+    """BASELINE configs[1] (C2) pinned by the REFERENCE at its full shape: one train_batch
+    of the reference Trainer at Food-Kitchen item counts (29,207 + 34,886), d=256, L=50, R=10, B=1024, dropout 0
+    (tests/golden/model_c2.npz, tools/gen_fixtures.py --c2) against the fp32 mode — the split-bf16 fused CE over
+    ~10k valid rows × 34,887 / 29,208 columns, the x3 projections, the row-subset last layer when compact.  The
+    batch and graphs are rebuilt here through c2dsr_amd and must hash to the reference's processed forms.
+    Losses at 1e-4 relative; the GCN tables, encoder outputs and every parameter gradient on an even sample of
+    their elements (plus a sample of the nonzero elements of the sparse table gradients), relative to the full
+    tensor's max-abs, at 1e-4."""
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import synth
+    import random
+    z = G.load('model_c2.npz')
+    B = int(z['batch_n'])
+    c = dict(n_a=29207, n_b=34886, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
+             norm_first=False, d_bias=False, shared_item_embed=False)
+    seqs = synth.make_sequences(int(z['n_users']), c['n_a'], c['n_b'], c['len_max'], seed=1, n_min=6)
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, c['n_a'], c['n_b'], c['len_max']))
+    assert rows[0].shape[0] == int(z['n_train'])
+    lists = [np.ascontiguousarray(r[:B], dtype=np.int64) for r in rows]
+    assert _sha(lists) == str(z['batch_sha256'])
+    gr = GR.preprocess_graph(seqs, c['n_a'], c['n_a'] + c['n_b'] + 1)
+    for k, g in zip(('share', 'specific'), gr):
+        r = np.repeat(np.arange(g.n, dtype=np.int64), np.diff(g.rowptr.astype(np.int64)))
+        assert int(g.nnz) == int(z[f'{k}_nnz'])
+        assert _sha([r, g.col.astype(np.int64), g.val.astype(np.float32)]) == str(z[f'{k}_sha256']), k
+    args = make_args(c)
+    args.batch_size = B
+    torch.manual_seed(1234)
+    tr = build_trainer(args, *gr)
+    tr.compact_rows = compact
+    b = tuple(torch.from_numpy(x) for x in lists)
+    tr.model.train()
+    tr.optimizer.zero_grad()
+    box = capture(tr)
+    tr.model.convolve_graph()
+    loss, loss_rec, loss_mi = tr.train_batch(b)
+    torch.cuda.synchronize()
+    for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
+        assert abs(float(v) - float(z[f's0/{k}'])) <= TOL * abs(float(z[f's0/{k}'])), k
+
+    def check(key, full):
+        flat = full.detach().reshape(-1).cpu().double().numpy()
+        assert flat.size == int(z[f's0/{key}:numel']), key
+        idx = np.arange(0, flat.size, max(1, flat.size // 4096))
+        e = float(np.abs(flat[idx] - z[f's0/{key}']).max() / z[f's0/{key}:maxabs'])
+        if f's0/{key}:nz_idx' in z:
+            e = max(e, float(np.abs(flat[z[f's0/{key}:nz_idx']] - z[f's0/{key}:nz_val']).max()
+                             / z[f's0/{key}:maxabs']))
+        assert e < TOL, (key, e)
+        return e
+
+    worst = {}
+    for k in ('hi_share', 'hi_a', 'hi_b'):
+        worst[k] = check(k, box[k])
+    if not compact:
+        for k, got in (('h_share', box['h_share']), ('hx', box['hx']), ('hy', box['hy']),
+                       ('h_neg_a', box['neg'][0]), ('h_neg_b', box['neg'][1])):
+            worst[k] = check(k, got)
+    for n_, g in box['grads'].items():
+        worst[n_] = check(f'grad/{n_}', g)
+    print('C2 vs reference, worst:', {k: f'{v:.1e}' for k, v in sorted(worst.items(), key=lambda x: -x[1])[:6]})
+
+
+def test_row_shard_readers_wait_for_gather():
+    """Every reader of the row-sharded propagated tables goes through the gather's wait(): rank 0
+    of a simulated world of 2 gets an injected gather that POISONS the other rank's block (NaN) when issued and
+    fills it with the correct rows only inside wait().  A step (dropout 0.2) must then equal the replicated
+    run bit for bit — a read before the wait would carry NaN into the loss and every gradient."""
+    from c2dsr_amd.ops import RowShard
+    name = 'base'
+    gs, gp = golden_graphs(name)
+    b = G.batch(name, 0, G.BATCH)
+
+    def run(shard_gather):
+        tr = build_trainer(make_args(G.CONFIGS[name], dropout=0.2), gs, gp, G.init_params(name))
+        if shard_gather is not None:
+            tr.model.gnn_shard = True
+            tr.model.row_shard = RowShard(0, 2, gather=shard_gather)
+            tr.model._shard = lambda: tr.model.row_shard
+        tr.model.train()
+        tr.optimizer.zero_grad()
+        box = capture(tr)
+        tr.model.convolve_graph()
+        loss, _, _ = tr.train_batch(b)
+        torch.cuda.synchronize()
+        return tr, box, float(loss)
+
+    tr_a, box_a, loss_a = run(None)
+    ref_tables = [box_a[k] for k in ('hi_share', 'hi_a', 'hi_b')]
+    issued, waited = [], []
+
+    class Handle:
+        def __init__(self, full, src, c):
+            self.full, self.src, self.c = full, src, c
+
+        def wait(self):
+            n = self.src.shape[0]
+            self.full[self.c:n].copy_(self.src[self.c:n])
+            waited.append(self)
+
+    def gather(full, mine):
+        c = mine.shape[0]
+        full[c:].fill_(float('nan'))  # the other rank's block: poison until wait()
+        h = Handle(full, ref_tables[len(issued)], c)
+        issued.append(h)
+        return h
+
+    tr_b, box_b, loss_b = run(gather)
+    assert len(issued) == 3 and len(waited) == 3
+    assert loss_b == loss_a
+    for n, g in box_a['grads'].items():
+        assert torch.equal(box_b['grads'][n], g), n
+    for (n, p), (_, q) in zip(tr_a.model.named_parameters(), tr_b.model.named_parameters()):
+        assert torch.equal(p, q), n

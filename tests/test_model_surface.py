@@ -63,6 +63,7 @@ def test_convolve_graph_defers_the_propagation_to_first_use():
 
     for g in (model.gnn_share, model.gnn_a, model.gnn_b):
         g.propagate = stub(g)
+    model.defer_graph = True  # as c2dsr_amd.Trainer sets it
     model.train()
     step0 = model.state.step
     model.convolve_graph()
@@ -79,3 +80,31 @@ def test_convolve_graph_defers_the_propagation_to_first_use():
     model.launch_graph()
     assert calls[3:] == [(0, False, False), (1, False, False), (2, False, False)]
     assert model.state.step == step0 + 1  # eval calls open no dropout step
+
+
+def test_convolve_graph_is_eager_unless_trainer_driven_and_guards_weight_edits():
+    """a model used on its own propagates at convolve_graph() like the reference; a deferred
+    (trainer-driven) launch refuses item-embedding weights edited in place between the call and the first read."""
+    import pytest
+    from c2dsr_amd.models.C2DSR import C2DSR
+    args = make_args(G.CONFIGS['base'])
+    args.device = torch.device('cpu')
+    gs, gp = golden_graphs('base')
+    model = C2DSR(args, gs, gp)
+    calls = []
+    for g in (model.gnn_share, model.gnn_a, model.gnn_b):
+        g.propagate = (lambda gnn: lambda h, adj, sink=None, shard=None: (calls.append(gnn.table), (h.clone(), None,
+                                                                                                   None))[1])(g)
+    model.train()
+    model.convolve_graph()
+    assert calls == [0, 1, 2]  # eager
+    assert torch.equal(model.hi_a, model.embed_i_a.weight)
+    model.defer_graph = True
+    model.convolve_graph()
+    assert calls == [0, 1, 2]
+    with torch.no_grad():
+        model.embed_i_a.weight.add_(1.0)  # e.g. an optimizer step between the call and the first read
+    with pytest.raises(RuntimeError, match='modified between convolve_graph'):
+        model.hi_a
+    model.convolve_graph()  # a new call sees the new weights
+    assert torch.equal(model.hi_a, model.embed_i_a.weight) and calls == [0, 1, 2, 0, 1, 2]

@@ -93,3 +93,32 @@ def test_oracle_metrics_match_reference():
     np.testing.assert_allclose(O.cal_metrics(ra), m['metrics_a'], rtol=1e-14)
     np.testing.assert_allclose(O.cal_score(ra, rb, [0.1124, 0.0865, 0.0574, 0.0416]), m['score_fk'], rtol=1e-14)
     np.testing.assert_allclose(O.cal_score(ra, rb, [0.0647, 0.0476, 0.0284, 0.0217]), m['score_mb'], rtol=1e-14)
+
+
+def test_c2_fixture_inputs_rebuild():
+    """model_c2.npz (the reference's C2-shape step) stores no inputs: the batch and graphs are rebuilt from the
+    synthetic generator through the bit-exact data path and must hash to the reference's processed forms."""
+    import hashlib
+    import random
+    from c2dsr_amd import dataloader as DL
+    from c2dsr_amd import graph as GR
+    from c2dsr_amd import synth
+
+    def sha(arrs):
+        h = hashlib.sha256()
+        for a in arrs:
+            a = np.ascontiguousarray(a)
+            h.update(str(a.dtype).encode() + str(a.shape).encode())
+            h.update(a.tobytes())
+        return h.hexdigest()
+
+    z = G.load('model_c2.npz')
+    B = int(z['batch_n'])
+    seqs = synth.make_sequences(int(z['n_users']), 29207, 34886, 50, seed=1, n_min=6)
+    random.seed(3407)
+    rows = DL.to_arrays(DL.preprocess_train(seqs, 29207, 34886, 50))
+    assert rows[0].shape[0] == int(z['n_train'])
+    assert sha([np.ascontiguousarray(r[:B], dtype=np.int64) for r in rows]) == str(z['batch_sha256'])
+    for k, g in zip(('share', 'specific'), GR.preprocess_graph(seqs, 29207, 29207 + 34886 + 1)):
+        r = np.repeat(np.arange(g.n, dtype=np.int64), np.diff(g.rowptr.astype(np.int64)))
+        assert sha([r, g.col.astype(np.int64), g.val.astype(np.float32)]) == str(z[f'{k}_sha256']), k

@@ -455,6 +455,101 @@ def gen_d256(ref):
     print(f'[d256] train={len(ds_tr.data)} loss={loss.item():.6f} tensors={len(named)}')
 
 
+# BASELINE configs[1] (C2) at its own shape: Food-Kitchen item counts, d=256, L=50, R=10, B=1024 (VERDICT r03
+# next #1).  The inputs are NOT stored: they are the synthetic sequences the full-size GPU tests build
+# (synth.make_sequences(2·B, seed=1, n_min=6)), written in the raw format for the reference to process; the fixture
+# pins their processed form by sha256 so a test that rebuilds them through c2dsr_amd proves it fed the same batch.
+C2 = dict(n_a=29207, n_b=34886, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
+          norm_first=False, d_bias=False, shared_item_embed=False)
+C2_BATCH = 1024
+
+
+def _sha(arrs):
+    h = hashlib.sha256()
+    for a in arrs:
+        a = np.ascontiguousarray(a)
+        h.update(str(a.dtype).encode() + str(a.shape).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def gen_c2(ref):
+    """One reference train_batch (dropout 0) at C2's full shape, stored like model_d256.npz (an even sample of
+    every tensor's elements with the full max-abs) plus, for the sparse embedding-table gradients, a sample of
+    their nonzero elements.  Writes tests/golden/model_c2.npz."""
+    ref_dl, ref_model, ref_trainer, ref_graph, ref_metrics = ref
+    cfg, B = C2, C2_BATCH
+    tmp = tempfile.mkdtemp(prefix='c2dsr_fx_c2_')
+    path_raw = os.path.join(tmp, 'raw')
+    path_data = os.path.join(tmp, 'data')
+    os.makedirs(path_data)
+    seqs = synth.make_sequences(2 * B, cfg['n_a'], cfg['n_b'], cfg['len_max'], seed=1, n_min=6)
+    synth.write_items(path_raw, cfg['n_a'], cfg['n_b'])
+    synth.write_raw(path_raw, 'train', seqs, ties=False)
+    args = make_args(cfg, path_raw, path_data)
+    args.batch_size = B
+    random.seed(3407)
+    torch.manual_seed(3407)
+    np.random.seed(3407)
+    ds_tr = ref_dl.CDSRDataset(args, 'train')
+    lists = [np.asarray([r[j] for r in ds_tr.data[:B]], dtype=np.int64) for j in range(14)]
+    out = {'batch_n': np.int64(B), 'n_users': np.int64(2 * B), 'n_train': np.int64(len(ds_tr.data)),
+           'batch_sha256': np.str_(_sha(lists))}
+    adj_s, adj_p = ref_graph.preprocess_graph(args, os.path.join(path_raw, 'train_new.txt'))
+    for k, adj in (('share', adj_s), ('specific', adj_p)):
+        a = adj.coalesce()
+        idx = a.indices().numpy()
+        out[f'{k}_sha256'] = np.str_(_sha([idx[0].astype(np.int64), idx[1].astype(np.int64),
+                                           a.values().numpy().astype(np.float32)]))
+        out[f'{k}_nnz'] = np.int64(idx.shape[1])
+    torch.manual_seed(1234)
+    model = ref_model.C2DSR(args, adj_s, adj_p)
+    tr = ref_trainer.Trainer.__new__(ref_trainer.Trainer)
+    tr.model = model
+    tr.optimizer = torch.optim.AdamW(filter(lambda x: x.requires_grad, model.parameters()), lr=args.lr,
+                                     weight_decay=args.l2, amsgrad=True)
+    tr.device, tr.d_latent, tr.n_item_a, tr.n_item_b = args.device, args.d_latent, args.n_item_a, args.n_item_b
+    tr.len_rec, tr.lambda_loss = args.len_rec, args.lambda_loss
+    tr.label_pos = torch.ones(B, 1)
+    tr.label_neg = torch.zeros(B, 1)
+    cap = {}
+    hooks = [getattr(model, nm).register_forward_hook(
+        (lambda nm: lambda mod, inp, o: cap.setdefault(nm, []).append(o.detach().numpy().copy()))(nm))
+        for nm in ('gnn_share', 'gnn_a', 'gnn_b', 'attn_share', 'attn_a', 'attn_b')]
+    snap = {}
+    real_step = tr.optimizer.step
+
+    def step_wrapper(*a, **kw):
+        snap.update({n: p.grad.detach().numpy().copy() for n, p in model.named_parameters() if p.grad is not None})
+        return real_step(*a, **kw)
+
+    tr.optimizer.step = step_wrapper
+    model.train()
+    tr.optimizer.zero_grad()
+    model.convolve_graph()
+    loss, loss_rec, loss_mi = tr.train_batch(tuple(torch.from_numpy(x) for x in lists))
+    for h in hooks:
+        h.remove()
+    out.update({'s0/loss': np.float64(loss.item()), 's0/loss_rec': np.float64(loss_rec.item()),
+                's0/loss_mi': np.float64(loss_mi.item())})
+    named = {'hi_share': cap['gnn_share'][0], 'hi_a': cap['gnn_a'][0], 'hi_b': cap['gnn_b'][0],
+             'h_share': cap['attn_share'][0], 'h_neg_a': cap['attn_share'][1], 'h_neg_b': cap['attn_share'][2],
+             'hx': cap['attn_a'][0], 'hy': cap['attn_b'][0]}
+    named.update({f'grad/{n}': g for n, g in snap.items()})
+    for k, v in named.items():
+        flat = v.reshape(-1).astype(np.float32)
+        out[f's0/{k}'] = flat[sample_idx(flat.size)]
+        out[f's0/{k}:maxabs'] = np.float64(np.abs(flat).max())
+        out[f's0/{k}:numel'] = np.int64(flat.size)
+        nz = np.flatnonzero(flat)
+        if k.startswith('grad/') and nz.size < flat.size // 2:  # sparse (embedding tables): sample the nonzeros
+            sel = nz[sample_idx(nz.size)]
+            out[f's0/{k}:nz_idx'] = sel.astype(np.int64)
+            out[f's0/{k}:nz_val'] = flat[sel]
+    np.savez_compressed(os.path.join(OUT, 'model_c2.npz'), **out)
+    print(f'[c2] train={len(ds_tr.data)} loss={loss.item():.6f} tensors={len(named)}')
+
+
 FK_EPOCHS = 2
 
 
@@ -542,12 +637,17 @@ def main():
     ap.add_argument('--traj', action='store_true', help='only the epoch trajectories')
     ap.add_argument('--fk-traj', action='store_true', help='only the Food-Kitchen metric trajectory')
     ap.add_argument('--d256', action='store_true', help='only the d=256 / L=50 / R=10 golden step')
+    ap.add_argument('--c2', action='store_true', help='only the C2-shape (FK items, d=256, L=50, B=1024) golden step')
     opt = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
     ref = ref_import()
     if opt.d256:
         gen_d256(ref)
+        return
+    if opt.c2:
+        torch.set_num_threads(8)
+        gen_c2(ref)
         return
     if opt.fk_traj:
         torch.set_num_threads(8)
