@@ -623,12 +623,14 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     tr.optimizer.zero_grad()
     B_global = B * world if not dp_split else B
 
-    def step(b):
+    def step(i):
+        # host[i]: the batch's host copy (the data pipeline's own arrays) — the step's launch sizes are counted
+        # from it, so no count is read back from the device inside a step
         tr.model.convolve_graph()
-        return tr.train_batch(b, global_rows=B_global)
+        return tr.train_batch(batches[i], global_rows=B_global, host=host[i])
 
     for i in range(opt.warmup):
-        step(batches[i])
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -638,7 +640,7 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     t0 = time.perf_counter()
     last = None
     for i in range(opt.steps):
-        last = step(batches[opt.warmup + i])
+        last = step(opt.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

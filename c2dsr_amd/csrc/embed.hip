@@ -271,6 +271,9 @@ constexpr int SEG_U = SEG_U_CFG;  // rows in flight per lane group
 #ifndef SEG_PIPE
 #define SEG_PIPE 0
 #endif
+#ifndef SEG_PREF
+#define SEG_PREF 0
+#endif
 constexpr int SUBP = 128;  // pieces per level-1 block of a split
 
 struct RowSrc {
@@ -422,7 +425,66 @@ __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
           atomicOr(J.err, 2);
       }
     };
-#if SEG_PIPE
+#if SEG_PREF
+    // the out rows a batch read-modify-writes are known from the staged keys alone (each key's row is written by
+    // exactly one run close in the launch: a run cut by a chunk edge goes to the head / tail slots instead), so
+    // they are loaded together with the batch's gradient rows: one memory round trip per batch, not two
+    for (int h0 = 0; h0 < cnt; h0 += SEG_U) {
+      int kind[SEG_U];  // as in process(): 0 nothing closes / 1 out[key] += / 2 head / 3 tail / 4 bad key
+      bool closes[SEG_U];
+#pragma unroll
+      for (int u = 0; u < SEG_U; ++u) {
+        const int q = h0 + u;
+        kind[u] = 0;
+        closes[u] = q < cnt && (q == cnt - 1 || sk[o + q + 2] != sk[o + q + 1]);
+        if (closes[u]) {
+          const uint32_t key = sk[o + q + 1];
+          if (first && cont_head)
+            kind[u] = 2;
+          else if (q == cnt - 1 && cont_tail)
+            kind[u] = 3;
+          else if (key >= (uint32_t)J.n_out)
+            kind[u] = 4;
+          else if ((int)key != J.skip_key)
+            kind[u] = 1;
+          first = false;
+        }
+      }
+      float4 x[SEG_U], prev[SEG_U];
+      load(x, h0);
+#pragma unroll
+      for (int u = 0; u < SEG_U; ++u) {
+        const long off = (long)sk[o + h0 + u + 1] * d + c;
+        prev[u] = kind[u] != 1 ? c2::f4(0.f) : (J.out16 ? c2::ld4(J.out16 + off) : *(const float4*)(J.out + off));
+      }
+#pragma unroll
+      for (int u = 0; u < SEG_U; ++u) {
+        if (h0 + u < cnt) {
+          acc = acc + x[u];
+          if (closes[u]) {
+            x[u] = acc;
+            acc = c2::f4(0.f);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SEG_U; ++u) {
+        if (kind[u] == 1) {
+          const long off = (long)sk[o + h0 + u + 1] * d + c;
+          if (J.out16)
+            c2::st4(J.out16 + off, prev[u] + x[u]);
+          else
+            *(float4*)(J.out + off) = prev[u] + x[u];
+        } else if (kind[u] == 2)
+          *(float4*)(J.ph + chunk * d + c) = x[u];
+        else if (kind[u] == 3)
+          *(float4*)(J.pt + chunk * d + c) = x[u];
+        else if (kind[u] == 4 && lane == 0)
+          atomicOr(J.err, 2);
+      }
+    }
+    (void)process;
+#elif SEG_PIPE
     // the next batch's rows are in flight while this batch's runs are read-modify-written (rows and out
     // are different buffers; a run that closes in a batch never reappears in a later one)
     float4 xa[SEG_U], xb[SEG_U];

@@ -390,17 +390,24 @@ class HostCounts:
     on first use: the host blocks only if the device has not got that far yet, so the stream never
     drains the way an immediate ``.tolist()`` would make it."""
 
-    def __init__(self, dev_counts):
-        self.host = torch.empty(dev_counts.numel(), dtype=torch.int32, pin_memory=True)
-        self.host.copy_(dev_counts, non_blocking=True)
-        self.ev = torch.cuda.Event()
-        self.ev.record()
-        self.vals = None
+    def __init__(self, dev_counts, known=None, check=False):
+        """known: the same counts computed on the host from the batch's host copy (Trainer.host_counts) — then
+        nothing is copied and nothing ever waits on the device; check: also copy the device counts and compare
+        them with ``known`` at the first read (C2DSR_CHECK_COUNTS=1; raises on a mismatch)."""
+        self.known = None if known is None else [int(v) for v in known]
+        self.vals = self.known if not check else None
+        if self.vals is None:
+            self.host = torch.empty(dev_counts.numel(), dtype=torch.int32, pin_memory=True)
+            self.host.copy_(dev_counts, non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record()
 
     def __getitem__(self, i):
         if self.vals is None:
             self.ev.synchronize()
             self.vals = self.host.tolist()
+            if self.known is not None and self.known != self.vals:
+                raise RuntimeError(f'host-computed counts {self.known} != device counts {self.vals}')
         return self.vals[i]
 
 

@@ -15,6 +15,7 @@ import os
 import time
 from os.path import join
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -98,6 +99,10 @@ class Trainer(object):
         self.lambda_loss = args.lambda_loss
         self.dp_split = True  # slice each global batch across data-parallel ranks
         self.model.defer_graph = True  # convolve_graph() → launch behind the step's index work (_train_batch)
+        # the launch-sizing counts of a step from the batch's host copy (no device read in the step); the device's
+        # own counts are checked against them with C2DSR_CHECK_COUNTS=1
+        self.host_counts_ok = True
+        self.check_counts = os.environ.get('C2DSR_CHECK_COUNTS', '0') == '1'
 
     # ------------------------------------------------------------------ training
     def run_epoch(self):
@@ -145,7 +150,30 @@ class Trainer(object):
     PASS_ROWS = ((DK.PASS_SHARE, 1 | 2 | 4), (DK.PASS_A, 1 | 4), (DK.PASS_B, 2 | 4), (DK.PASS_NEG0, 1),
                  (DK.PASS_NEG0 + 1, 2))
 
-    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b, seqs=None):
+    def host_counts(self, hb, *, need, pads, ce):
+        """The counts ``prepare``'s device kernels produce, from the host copy ``hb`` of the (rank's slice of
+        the) batch (numpy arrays in batch order): the five passes' need-set sizes (c2dsr_need_rows: rows
+        with a nonzero a / b pooling weight or among the last R positions, per pass code), their padding-row
+        counts (c2dsr_pad_rows: seq == idx_pad), and per classifier head the valid targets among the last R
+        positions of the shared and the specific sequences (c2dsr_compact_valid: target != n_items).  Pure
+        integer counting, so equal to the device's by construction (checked under C2DSR_CHECK_COUNTS=1)."""
+        (seq_share, seq_a, seq_b, _, _, _, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, neg_a, neg_b) = hb
+        B, L = gm_a.shape
+        R = self.len_rec
+        out = []
+        if need:
+            have = ((gm_a != 0).astype(np.uint8) | ((gm_b != 0).astype(np.uint8) << 1) |
+                    (np.arange(L) >= L - R).astype(np.uint8)[None, :] << 2)
+            out += [int(np.count_nonzero(have & bits)) for _, bits in self.PASS_ROWS]
+        if pads:
+            pad = int(self.model.attn_share.idx_pad)
+            out += [int(np.count_nonzero(x == pad)) for x in (seq_share, seq_a, seq_b, neg_a, neg_b)]
+        if ce:
+            for ts, tx, n in ((gt_share_a, gt_a, self.n_item_a), (gt_share_b, gt_b, self.n_item_b)):
+                out += [int(np.count_nonzero(ts[:, L - R:] != n)), int(np.count_nonzero(tx[:, L - R:] != n))]
+        return out
+
+    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b, seqs=None, host=None):
         """Index work the step sizes its launches by, enqueued ahead of the forward with one deferred host
         read of all its counts (ops.HostCounts; nothing waits until the first count is needed):
           * RowSets of the five encoder passes (c2dsr_need_rows), so the last encoder layer runs its
@@ -212,7 +240,10 @@ class Trainer(object):
             self.dp_counts = (cvec, dist.all_reduce(cvec, async_op=True))
         if not counts:
             return {}, {}, None
-        hc = ops.HostCounts(torch.cat(counts))
+        known = None
+        if host is not None and self.host_counts_ok:
+            known = self.host_counts(host, need=need_sets is not None, pads=pad_sets is not None, ce=ce is not None)
+        hc = ops.HostCounts(torch.cat(counts), known=known, check=self.check_counts)
         need, pads = {}, {}
         base = 0
         for sets, out in ((need_sets, need), (pad_sets, pads)):
@@ -226,31 +257,38 @@ class Trainer(object):
             ce_pre = [c + ((hc, base + 2 * k),) for k, c in enumerate(ce)]
         return need, pads, ce_pre
 
-    def train_batch(self, batch, *, global_rows=None):
+    def train_batch(self, batch, *, global_rows=None, host=None):
         """trainer.py:91-160.  ``batch``: 14 int64 [B, L] tensors (host or device).  Under data
         parallelism each rank trains its slice of the global batch (or, with ``dp_split=False``, its
-        own batch; ``global_rows`` then gives the global batch size).
+        own batch; ``global_rows`` then gives the global batch size).  ``host``: the same 14 arrays on the
+        host when ``batch`` is already on the device (a batch of host tensors is its own host copy): the
+        step's launch sizes are counted from it, so the host never waits on the device inside a step.
         Python's cyclic collector is paused while the step is enqueued (a collection in the middle of the
         launch sequence leaves the device idle); it runs after the optimizer launch, under that kernel."""
         if not gc.isenabled():
-            return self._train_batch(batch, global_rows=global_rows)
+            return self._train_batch(batch, global_rows=global_rows, host=host)
         gc.disable()
         try:
-            return self._train_batch(batch, global_rows=global_rows)
+            return self._train_batch(batch, global_rows=global_rows, host=host)
         finally:
             gc.enable()
 
-    def _train_batch(self, batch, *, global_rows=None):
+    def _train_batch(self, batch, *, global_rows=None, host=None):
         lo, hi, row_offset, B_global = dp_rows(batch[0].shape[0], self.rank, self.world, self.dp_split, global_rows)
+        if host is None and all(isinstance(x, torch.Tensor) and x.device.type == 'cpu' for x in batch):
+            host = batch
+        hb = None
+        if host is not None:
+            hb = tuple(np.asarray(x[lo:hi]) for x in host)
         (seq_share, seq_a, seq_b, pos, pos_a, pos_b, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, neg_a,
          neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
         m = self.model
         m.state.row_offset = row_offset
         self.dp_counts = None
         need, pads, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b,
-                                          (seq_share, seq_a, seq_b, neg_a, neg_b))
-        # the GCN forwards of convolve_graph() are enqueued now, behind the index work and its count copy: the host
-        # reads those counts while the device still has the propagations to run (no idle gap at the read)
+                                          (seq_share, seq_a, seq_b, neg_a, neg_b), host=hb)
+        # the GCN forwards of convolve_graph() are enqueued now, behind the index work (and its count copy when the
+        # counts are not known on the host: the host then reads them while the device runs the propagations)
         m.launch_graph()
         plans = None
         if m.training:

@@ -389,6 +389,7 @@ def _full_case(cfg, precision, compact):
     torch.manual_seed(0)
     tr = build_trainer(args, gs, gp)
     tr.compact_rows = compact
+    tr.check_counts = True  # the host-counted launch sizes (a host batch) must equal the device's counts
     P = {n: p.detach().clone() for n, p in tr.model.named_parameters()}
     tr.model.train()
     tr.optimizer.zero_grad()
@@ -841,3 +842,30 @@ def test_row_shard_readers_wait_for_gather():
         assert torch.equal(box_b['grads'][n], g), n
     for (n, p), (_, q) in zip(tr_a.model.named_parameters(), tr_b.model.named_parameters()):
         assert torch.equal(p, q), n
+
+
+@pytest.mark.parametrize('name', list(G.CONFIGS))
+def test_host_counts_equal_device_counts(name):
+    """The step's launch sizes counted on the host (Trainer.host_counts: need sets, padding rows, valid targets)
+    equal the device kernels' counts, and a device-resident batch with its host copy trains bit-identically to
+    the same batch counted on the device (no host read in the step otherwise)."""
+    m = G.load(f'model_{name}.npz')
+    c = G.CONFIGS[name]
+    b = G.batch(name, int(m['s0/batch_lo']), int(m['s0/batch_n']))
+    outs = []
+    for mode in ('device', 'host'):
+        args = make_args(c, dropout=0.2)
+        gs, gp = golden_graphs(name)
+        tr = build_trainer(args, gs, gp, G.init_params(name))
+        tr.check_counts = mode == 'host'
+        tr.host_counts_ok = mode == 'host'
+        tr.model.train()
+        tr.optimizer.zero_grad()
+        bd = tuple(x.to(DEV) for x in b)
+        tr.model.convolve_graph()
+        loss, loss_rec, loss_mi = tr.train_batch(bd, host=b if mode == 'host' else None)
+        torch.cuda.synchronize()
+        outs.append((float(loss.detach()), float(loss_rec), float(loss_mi),
+                     torch.cat([p.detach().reshape(-1) for p in tr.model.parameters()]).cpu()))
+    assert outs[0][:3] == outs[1][:3]
+    assert torch.equal(outs[0][3], outs[1][3])
