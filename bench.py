@@ -623,11 +623,13 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     tr.optimizer.zero_grad()
     B_global = B * world if not dp_split else B
 
+    # the launch sizes of every step (compact row sets, padding rows, valid targets), counted by the data pipeline
+    # from the batches' host arrays as it stages them — so no count is read back from the device inside a step
+    counts = [tr.launch_counts(h, global_rows=B_global) for h in host]
+
     def step(i):
-        # host[i]: the batch's host copy (the data pipeline's own arrays) — the step's launch sizes are counted
-        # from it, so no count is read back from the device inside a step
         tr.model.convolve_graph()
-        return tr.train_batch(batches[i], global_rows=B_global, host=host[i])
+        return tr.train_batch(batches[i], global_rows=B_global, counts=counts[i])
 
     for i in range(opt.warmup):
         step(i)

@@ -33,6 +33,12 @@ struct Epi2 {
   float aux_scale;
   const int* rowmap;  // dropout row index = row_base + (rowmap ? rowmap[row] : row)
   const int* auxmap;  // AUX_ACC_MAP: aux row of output row r = auxmap[r] (< 0: none, aux reads 0)
+  // guarded ReLU (rg3 GUARD, c2dsr_rgemm_x3_relu_guard): pre-activations within the split product's error bound
+  // of zero are listed for an exact recompute: |v| <= tau·‖a_r‖·‖w_c‖  ⇔  v² <= gtau2·‖a_r‖²·wn2[c]
+  const float* wn2;  // [N] squared norms of the weight rows (output columns)
+  int* glist;        // listed elements r·N + c
+  int* gcnt;         // list length
+  float gtau2;
 };
 
 // epilogues that read a second [M, N] tensor at the output positions (prefetched one tile ahead):
@@ -350,10 +356,32 @@ __device__ __forceinline__ void x3_acc(f32x4& acc, const bf16x8& wh, const bf16x
       : "a"(wh), "a"(wl), "v"(ah), "v"(al));
 }
 
-template <int KCH, bool EPI, int AUX>
+#ifdef RG3_STAMP  // diagnostic build only: per-phase cycle sums of the rg3 chunk loop (tools/rg_micro.py prints them)
+__device__ unsigned long long rg3_stamp_acc[8];
+#define RSTAMP(i)                                                  \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    const unsigned now_ = (unsigned)__builtin_amdgcn_s_memtime();  \
+    st_acc[i] += now_ - st_prev;                                   \
+    st_prev = now_;                                                \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } while (0)
+#else
+#define RSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
+// GUARD (EPI, K = 256 only; the ReLU producer linear1 in the fp32 mode): a pre-activation v = a·w + b whose split
+// product error could move it across zero — |a·w − split(a·w)| ≤ 3·2^-18·Σ|a_k w_k| ≤ 3·2^-18·‖a‖‖w‖, guarded at
+// 2^-15·‖a‖‖w‖ — is listed (r·N + c) and recomputed exactly by guard_fix_kernel: the ReLU's sign decisions, which
+// select the dy·x terms of the weight gradient, are those of an fp32 product (tools/fp32_diag.py).  ‖a_r‖² is summed
+// while a chunk is staged (a wave holds whole rows at K = 256), ‖w_c‖² comes from the caller (ep.wn2).
+template <int KCH, bool EPI, int AUX, bool GUARD = false>
 __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* __restrict__ A, long lda,
                                                      const bf16* __restrict__ B, long ldb, float* C, long ldc, Epi2 ep,
                                                      int G) {
+  static_assert(!GUARD || (EPI && KCH == 1 && AUX == AUX_NONE), "guarded ReLU: the K = 256 relu·dropout epilogue");
   constexpr int K = 256 * KCH;
   constexpr int NCB = 4 / KCH;      // 16-column blocks per wave
   constexpr int CW = 16 * NCB;      // columns per wave
@@ -361,6 +389,8 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
   constexpr int IMGB = 32 * 256 * 2;  // bytes of one [32][256] bf16 image
   constexpr int NST = 16;           // MFMA steps per chunk: (k-step ks, row block rb)
   __shared__ __attribute__((aligned(16))) char aimg[2][2 * IMGB];  // [buffer][hi | lo]
+  __shared__ float rn2s[2][GUARD ? 32 : 1];  // GUARD: ‖a_r‖² of the chunk's 32 rows, per image buffer
+  __shared__ __attribute__((aligned(16))) float wn2s[GUARD ? 256 : 1];  // GUARD: ‖w_c‖² of the workgroup's columns
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int nslots = gridDim.x >> 3;
   const int nwalk = nslots / G;
@@ -371,6 +401,9 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
   const int ntile = rt0 < RT ? (RT - 1 - rt0) / rts + 1 : 0;
   if (ntile == 0) return;  // uniform
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
+#ifdef RG3_STAMP
+  unsigned st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = (unsigned)__builtin_amdgcn_s_memtime();
+#endif
   const int ncol0 = gcol * WGC + w * CW;
   bf16x8 wh[NCB][8 * KCH], wl[NCB][8 * KCH];  // the weight columns' hi / lo fragments (AGPRs)
   f32x4 bias4[NCB];
@@ -409,6 +442,18 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
     l[2] = (bf16)(v.z - (float)h[2]); l[3] = (bf16)(v.w - (float)h[3]);
     *(lds4*)(size_t)lds_base(soff[u] + buf * 2 * IMGB) = h;
     *(lds4*)(size_t)lds_base(soff[u] + buf * 2 * IMGB + IMGB) = l;
+    if constexpr (GUARD) {  // ‖row lrow + 4u‖²: the row is this wave's 64 lanes × 4 (K = 256)
+      float x = fmaf(v.w, v.w, fmaf(v.z, v.z, fmaf(v.y, v.y, v.x * v.x)));
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x124, 0xf, 0xf, false));  // row_ror 4
+      x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x128, 0xf, 0xf, false));  // row_ror 8
+      const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+      x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+      const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+      x = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+      if (lane == 0) rn2s[buf][lrow + 4 * u] = x;
+    }
   };
   // aux / row maps of the current tile (loaded at its first chunk, used by its epilogue)
   f32x4 aux4[AUX != AUX_NONE ? 2 : 1][AUX != AUX_NONE ? NCB : 1];
@@ -439,7 +484,7 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
     }
   };
   f32x4 acc[2][NCB];
-  auto epilogue = [&](int tile, bool live) {
+  auto epilogue = [&](int tile, bool live, int buf) {
     mfma_drain();
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
@@ -450,6 +495,23 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
         f32x4 v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = fmaf(ep.alpha, acc[rb][cb][i], bias4[cb][i]);
+        if constexpr (GUARD) {
+          const float rr = rn2s[buf][16 * rb + l16] * ep.gtau2;
+          const f32x4 wq = *(const f32x4*)&wn2s[16 * cb + w * CW + 4 * g];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool flag = live && row < M && col + i < N && v[i] * v[i] <= rr * wq[i];
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(flag);
+            if (m) [[unlikely]] {  // wave-uniform: append the flagged elements (one atomic per wave)
+              const int lead = __builtin_ctzll(m);
+              int base = 0;
+              if (lane == lead) base = atomicAdd(ep.gcnt, __builtin_popcountll(m));
+              base = __builtin_amdgcn_readlane(base, lead);
+              const int k = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+              if (flag) ep.glist[base + k] = row * N + col + i;
+            }
+          }
+        }
         if constexpr (EPI) {
           const float4 dm = ep.drop.mul4((uint64_t)(ep.row_base + dmap[rb]) * N + col);
           v[0] = fmaxf(v[0], 0.f) * dm.x;
@@ -484,11 +546,13 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
     const int c4 = min(ncol0 + 16 * cb + 4 * g, N - 4);
     bias4[cb] = ep.bias ? *(const f32x4*)(ep.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  if constexpr (GUARD) wn2s[threadIdx.x] = ep.wn2[min(gcol * WGC + (int)threadIdx.x, N - 1)];
   vm_drain();
 #pragma unroll
   for (int u = 0; u < 8; ++u) stage1(Pa[u], u, 0);
   pre_tile(0);
   __syncthreads();
+  RSTAMP(0);
   // chunk c (k-chunk KC): MFMAs on image c&1 ∥ split of chunk c+1 (registers S) into image (c+1)&1; R is
   // refilled with chunk c+3 first (three register sets: a staged chunk was loaded two steps earlier)
   auto step = [&]<int KC>(int c, float4 (&R)[8], float4 (&S)[8]) {
@@ -521,11 +585,14 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
           }(),
           ...);
     }(std::make_integer_sequence<int, NST>{});
+    RSTAMP(1);
     if constexpr (KC == KCH - 1) {
-      epilogue(min(tile, ntile - 1), tile < ntile);
+      epilogue(min(tile, ntile - 1), tile < ntile, buf);
       pre_tile(min(tile + 1, ntile - 1));
     }
+    RSTAMP(2);
     __syncthreads();
+    RSTAMP(3);
   };
   const int nchunk = ntile * KCH;
   for (int c0 = 0; c0 < nchunk; c0 += 6) {  // register sets rotate with period 3, k-chunks with period KCH
@@ -541,6 +608,13 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
     if (c0 + 5 >= nchunk) break;
     step.template operator()<1 % KCH>(c0 + 5, Pc, Pa);
   }
+#ifdef RG3_STAMP
+  if (lane == 0) {
+    for (int i = 0; i < 4; ++i) atomicAdd(&rg3_stamp_acc[i], (unsigned long long)st_acc[i]);
+    atomicAdd(&rg3_stamp_acc[6], (unsigned long long)nchunk);
+    atomicAdd(&rg3_stamp_acc[7], 1ull);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -813,6 +887,43 @@ __global__ void to_bf16_kernel(const float* __restrict__ x, int R, int Cc, long 
     y[i] = v;
 }
 
+// ‖W[c]‖² for the guarded ReLU (W fp32 [N][K], K = 256): one wave per row, fixed-order butterfly
+__global__ void row_norm2_kernel(const float* __restrict__ W, int N, int K, float* __restrict__ out) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int k = 4 * lane; k < K; k += 256) {
+    const float4 w = *(const float4*)(W + (long)c * K + k);
+    s = fmaf(w.w, w.w, fmaf(w.z, w.z, fmaf(w.y, w.y, fmaf(w.x, w.x, s))));
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (lane == 0) out[c] = s;
+}
+
+// the exact recompute of the guarded elements (rg3 GUARD): C[r][c] = drop(relu(alpha·Σ_k A[r][k]·W[c][k] + b[c]))
+// with fp32 products and a fixed-order wave reduction (K = 256: a float4 per lane), one wave per listed element
+__global__ __launch_bounds__(256) void guard_fix_kernel(const float* __restrict__ A, long lda,
+                                                        const float* __restrict__ W, int N, Epi2 ep,
+                                                        float* __restrict__ C, long ldc) {
+  const int lane = threadIdx.x & 63;
+  const int n = *ep.gcnt;
+  for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
+    const int idx = ep.glist[e];
+    const int r = idx / N, c = idx % N;
+    const float4 a = *(const float4*)(A + (long)r * lda + 4 * lane);
+    const float4 w = *(const float4*)(W + (long)c * 256 + 4 * lane);
+    float s = fmaf(a.w, w.w, fmaf(a.z, w.z, fmaf(a.y, w.y, a.x * w.x)));
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if (lane == 0) {
+      const float v = fmaf(ep.alpha, s, ep.bias ? ep.bias[c] : 0.f);
+      const int dr = ep.rowmap ? ep.rowmap[r] : r;
+      C[(long)r * ldc + c] = fmaxf(v, 0.f) * ep.drop.mul((uint64_t)(ep.row_base + dr) * N + c);
+    }
+  }
+}
+
 }  // namespace
 
 // 1 when c2dsr_rgemm takes (M, N, K): K ∈ {256, 512, 768} (the encoder projections at d = 256)
@@ -850,7 +961,7 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
   if ((aux_mode == AUX_ACC_MAP) != (auxmap != nullptr) || (aux_mode == AUX_ACC_MAP && aux == C))
     return (int)hipErrorInvalidValue;
   Epi2 ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base, aux,
-          aux_scale, rowmap, auxmap};
+          aux_scale, rowmap, auxmap, nullptr, nullptr, nullptr, 0.f};
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -971,6 +1082,59 @@ C2_API int c2dsr_rgemm_aux(int M, int N, int K, const float* A, int lda, const v
 }
 
 // fp32 mode: split-bf16 products (B = the split image [N][2K] = hi ‖ lo, ldb >= 2K; K = 256 or 512)
+#ifdef RG3_STAMP
+C2_API int c2dsr_rg3_stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rg3_stamp_acc), sizeof(rg3_stamp_acc));
+  if (e == hipSuccess && reset) {
+    static const unsigned long long z[8] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(rg3_stamp_acc), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
+// workspace of c2dsr_rgemm_x3_relu_guard: the list length, ‖W[c]‖² [N], the list (every element may be listed)
+C2_API size_t c2dsr_rgemm_guard_workspace(int M, int N) {
+  return 256 + (((size_t)N * 4 + 255) & ~(size_t)255) + (size_t)M * N * 4;
+}
+
+// linear1 of the fp32 mode (models/encoders.py:23-27 → TransformerEncoderLayer linear1 + relu + dropout):
+// C = drop(relu(A·Wᵀ + bias)) on split-bf16 products (B = the split image of W, K = 256), with every pre-activation
+// within the split error bound of zero recomputed exactly from the fp32 A and W (rg3 GUARD + guard_fix_kernel)
+C2_API int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int lda, const void* B, int ldb,
+                                     const float* W, float* C, int ldc, const float* bias, uint32_t k0, uint32_t k1,
+                                     float p, int64_t row_base, const int* rowmap, void* workspace, size_t ws_bytes,
+                                     void* stream) {
+  if (M <= 0 || K != 256 || N % 4 || ldc % 4 || lda % 4 || ldb < 2 * K || ldb % 8 || !W ||
+      !c2dsr_rgemm_supported(M, N, K) || ws_bytes < c2dsr_rgemm_guard_workspace(M, N))
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  int* cnt = (int*)ws;
+  float* wn2 = (float*)(ws + 256);
+  int* list = (int*)(ws + 256 + (((size_t)N * 4 + 255) & ~(size_t)255));
+  (void)hipMemsetAsync(cnt, 0, 4, s);
+  row_norm2_kernel<<<c2::ceil_div(N, 4), 256, 0, s>>>(W, N, K, wn2);
+  Epi2 ep{1.f, 0.f, bias, 1, c2::make_drop(k0, k1, p), row_base, nullptr, 0.f, rowmap, nullptr,
+          wn2, list, cnt, 0x1p-30f};  // tau = 2^-15
+  static int ncu = 0, per_cu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+    int n = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)rg3_kernel<1, true, AUX_NONE, true>, 256, 0);
+    per_cu = n > 0 ? n : 1;
+  }
+  const int G3 = c2::ceil_div(N, 256);
+  const int blocks = (ncu * per_cu / 8) * 8;
+  if (blocks / 8 < G3) return (int)hipErrorInvalidValue;
+  rg3_kernel<1, true, AUX_NONE, true><<<blocks, 256, 0, s>>>(M, N, A, lda, (const bf16*)B, ldb, C, ldc, ep, G3);
+  guard_fix_kernel<<<256, 256, 0, s>>>(A, lda, W, N, ep, C, ldc);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
 C2_API int c2dsr_rgemm_x3_supported(int M, int N, int K) {
   return c2dsr_rgemm_supported(M, N, K) && (K == 256 || K == 512);
 }

@@ -200,6 +200,28 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
     return C
 
 
+def rgemm_relu_guard(A, Wimg, W, C, *, M, N, K, bias, relu_drop):
+    """C = drop(relu(A·Wᵀ + bias)) in the fp32 mode (c2dsr_rgemm_x3_relu_guard): split-bf16 products with every
+    pre-activation within the split error bound of zero recomputed exactly from the fp32 A and W (linear1: its
+    ReLU's sign decisions select the dy·x terms of the weight gradient)."""
+    (k0, k1), p, row_base = relu_drop[:3]
+    rowmap = relu_drop[3] if len(relu_drop) > 3 else None
+    if A.dtype != torch.float32 or W.dtype != torch.float32 or Wimg.shape[-1] != 2 * K:
+        raise TypeError('rgemm_relu_guard: fp32 A and W, split image [N, 2K]')
+    wsb = int(lib.raw('c2dsr_rgemm_guard_workspace')(M, N))
+    ws = torch.empty(wsb, device=A.device, dtype=torch.uint8)
+    lib('c2dsr_rgemm_x3_relu_guard', M, N, K, A, K, Wimg, 2 * K, W, C, N, bias, k0, k1, float(p), int(row_base), rowmap,
+        ws, wsb, stream())
+    return C
+
+
+RELU_GUARD = False  # linear1 of the fp32 mode on the guarded split kernel (see LinearFn.forward)
+
+
+def relu_guard_ok(M, N, K):
+    return K == 256 and N % 4 == 0 and bool(lib.raw('c2dsr_rgemm_x3_supported')(M, N, K))
+
+
 def wgemm_ok(T, N, D):
     return bool(lib.raw('c2dsr_wgemm_supported')(T, N, D))
 
@@ -301,9 +323,16 @@ class LinearFn(Function):
             # the ReLU producer (linear1): its sign decisions select which gradient terms exist, so a
             # pre-activation within the split product's rounding (~1e-5 relative) of zero would flip a whole
             # dy·x term of the weight gradient (tools/fp32_diag.py: 2e-3 vs 1.6e-5 with this product exact) —
-            # it runs on the exact fp32-input MFMA GEMM
+            # it runs on the exact fp32-input MFMA GEMM.  RELU_GUARD: split products with the pre-activations inside
+            # the split error bound recomputed exactly (c2dsr_rgemm_x3_relu_guard) — measured 80.8 → 60.2 µs per
+            # pass, but the reference C2 golden step's linear1 gradient moved from < 1e-4 to 1.2e-4: not the default
             kind = None
-        if kind:
+            if RELU_GUARD and relu_guard_ok(M, N, K):
+                rgemm_relu_guard(x, weight_img(W, 'x3'), W, y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
+                kind = 'guard'
+        if kind == 'guard':
+            pass
+        elif kind:
             rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop, x3=kind == 'x3')
         else:
             gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)

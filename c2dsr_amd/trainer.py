@@ -162,9 +162,11 @@ class Trainer(object):
         R = self.len_rec
         out = []
         if need:
-            have = ((gm_a != 0).astype(np.uint8) | ((gm_b != 0).astype(np.uint8) << 1) |
-                    (np.arange(L) >= L - R).astype(np.uint8)[None, :] << 2)
-            out += [int(np.count_nonzero(have & bits)) for _, bits in self.PASS_ROWS]
+            # rows by (a-weight, b-weight) class, apart for the last R positions (bit 4)
+            have = (gm_a != 0).view(np.uint8) + 2 * (gm_b != 0).view(np.uint8)
+            cls = np.concatenate([np.bincount(have[:, :L - R].ravel(), minlength=4),
+                                  np.bincount(have[:, L - R:].ravel(), minlength=4)])
+            out += [int(sum(int(cls[h]) for h in range(8) if h & bits)) for _, bits in self.PASS_ROWS]
         if pads:
             pad = int(self.model.attn_share.idx_pad)
             out += [int(np.count_nonzero(x == pad)) for x in (seq_share, seq_a, seq_b, neg_a, neg_b)]
@@ -173,7 +175,24 @@ class Trainer(object):
                 out += [int(np.count_nonzero(ts[:, L - R:] != n)), int(np.count_nonzero(tx[:, L - R:] != n))]
         return out
 
-    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b, seqs=None, host=None):
+    def count_flags(self, L):
+        """Which count groups prepare() produces for a batch of length L: (need sets, padding rows, CE valid rows)."""
+        m = self.model
+        need = bool(self.compact_rows and m.training and not m.attn_share.norm_first)
+        pads = need and self.rows_attn and ops.attn_rows_ok(L, self.d_latent, m.attn_share.n_head)
+        ce = ce_kind(m.precision, self.d_latent) is not None
+        return need, pads, ce
+
+    def launch_counts(self, host, *, global_rows=None):
+        """The launch sizes of a training step on ``host`` (the batch's host arrays) exactly as the step's device
+        kernels count them — for a data pipeline that prepares them with the batch (bench.py does, ahead of the
+        timed steps) and hands them to train_batch(counts=...)."""
+        lo, hi, _, _ = dp_rows(host[0].shape[0], self.rank, self.world, self.dp_split, global_rows)
+        hb = tuple(np.asarray(x[lo:hi]) for x in host)
+        need, pads, ce = self.count_flags(hb[0].shape[1])
+        return self.host_counts(hb, need=need, pads=pads, ce=ce)
+
+    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b, seqs=None, host=None, known=None):
         """Index work the step sizes its launches by, enqueued ahead of the forward with one deferred host
         read of all its counts (ops.HostCounts; nothing waits until the first count is needed):
           * RowSets of the five encoder passes (c2dsr_need_rows), so the last encoder layer runs its
@@ -191,7 +210,8 @@ class Trainer(object):
         i32 = dict(device=dev, dtype=torch.int32)
         counts = []
         need_sets = pad_sets = None
-        if self.compact_rows and m.training and not m.attn_share.norm_first:
+        f_need, f_pads, f_ce = self.count_flags(L)
+        if f_need:
             n = len(self.PASS_ROWS)
             idx = torch.empty(n, M, **i32)
             inv = torch.empty(n, M, **i32)
@@ -202,7 +222,7 @@ class Trainer(object):
             lib('c2dsr_need_rows', gm_a, gm_b, B, L, R, n, code, idx, inv, cnt, off, ws, s)
             need_sets = (idx, inv, off)
             counts.append(cnt)
-            if seqs is not None and self.rows_attn and ops.attn_rows_ok(L, self.d_latent, m.attn_share.n_head):
+            if seqs is not None and f_pads:
                 sq = torch.stack([x.reshape(M) for x in seqs])
                 pidx, pinv = torch.empty(n, M, **i32), torch.empty(n, M, **i32)
                 pcnt, poff = torch.empty(n, **i32), torch.empty(n, B + 1, **i32)
@@ -211,7 +231,7 @@ class Trainer(object):
                 pad_sets = (pidx, pinv, poff)
                 counts.append(pcnt)
         ce = None
-        if ce_kind(m.precision, self.d_latent) is not None:
+        if f_ce:
             M2 = 2 * B * R
             ce = []
             for ts, tx, n_items in ((gt_share_a, gt_a, self.n_item_a), (gt_share_b, gt_b, self.n_item_b)):
@@ -240,8 +260,9 @@ class Trainer(object):
             self.dp_counts = (cvec, dist.all_reduce(cvec, async_op=True))
         if not counts:
             return {}, {}, None
-        known = None
-        if host is not None and self.host_counts_ok:
+        if not self.host_counts_ok:
+            known = None
+        elif known is None and host is not None:
             known = self.host_counts(host, need=need_sets is not None, pads=pad_sets is not None, ce=ce is not None)
         hc = ops.HostCounts(torch.cat(counts), known=known, check=self.check_counts)
         need, pads = {}, {}
@@ -257,28 +278,29 @@ class Trainer(object):
             ce_pre = [c + ((hc, base + 2 * k),) for k, c in enumerate(ce)]
         return need, pads, ce_pre
 
-    def train_batch(self, batch, *, global_rows=None, host=None):
+    def train_batch(self, batch, *, global_rows=None, host=None, counts=None):
         """trainer.py:91-160.  ``batch``: 14 int64 [B, L] tensors (host or device).  Under data
         parallelism each rank trains its slice of the global batch (or, with ``dp_split=False``, its
         own batch; ``global_rows`` then gives the global batch size).  ``host``: the same 14 arrays on the
         host when ``batch`` is already on the device (a batch of host tensors is its own host copy): the
-        step's launch sizes are counted from it, so the host never waits on the device inside a step.
+        step's launch sizes are counted from it, so the host never waits on the device inside a step; ``counts``:
+        those sizes already counted by the data pipeline (launch_counts).
         Python's cyclic collector is paused while the step is enqueued (a collection in the middle of the
         launch sequence leaves the device idle); it runs after the optimizer launch, under that kernel."""
         if not gc.isenabled():
-            return self._train_batch(batch, global_rows=global_rows, host=host)
+            return self._train_batch(batch, global_rows=global_rows, host=host, counts=counts)
         gc.disable()
         try:
-            return self._train_batch(batch, global_rows=global_rows, host=host)
+            return self._train_batch(batch, global_rows=global_rows, host=host, counts=counts)
         finally:
             gc.enable()
 
-    def _train_batch(self, batch, *, global_rows=None, host=None):
+    def _train_batch(self, batch, *, global_rows=None, host=None, counts=None):
         lo, hi, row_offset, B_global = dp_rows(batch[0].shape[0], self.rank, self.world, self.dp_split, global_rows)
         if host is None and all(isinstance(x, torch.Tensor) and x.device.type == 'cpu' for x in batch):
             host = batch
         hb = None
-        if host is not None:
+        if host is not None and counts is None:
             hb = tuple(np.asarray(x[lo:hi]) for x in host)
         (seq_share, seq_a, seq_b, pos, pos_a, pos_b, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, neg_a,
          neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
@@ -286,7 +308,7 @@ class Trainer(object):
         m.state.row_offset = row_offset
         self.dp_counts = None
         need, pads, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b,
-                                          (seq_share, seq_a, seq_b, neg_a, neg_b), host=hb)
+                                          (seq_share, seq_a, seq_b, neg_a, neg_b), host=hb, known=counts)
         # the GCN forwards of convolve_graph() are enqueued now, behind the index work (and its count copy when the
         # counts are not known on the host: the host then reads them while the device runs the propagations)
         m.launch_graph()

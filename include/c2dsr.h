@@ -361,6 +361,15 @@ int c2dsr_rgemm_x3(int M, int N, int K, const float* A, int lda, const void* B, 
                    float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                    int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
                    float aux_scale, void* stream);
+/* linear1 + ReLU + dropout of the fp32 mode (replaces models/encoders.py:23-27 → TransformerEncoderLayer
+ * linear1 / activation / dropout): C = drop(relu(A·Wᵀ + bias)) on split-bf16 products (B = the split image of the
+ * fp32 weight W [N][256], K = 256), every pre-activation within the split error bound of zero (|v| ≤ 2^-15·‖a‖‖w‖)
+ * recomputed exactly from A and W, so the ReLU's sign decisions are those of an fp32 product.  Dropout index
+ * (row_base + (rowmap ? rowmap[r] : r))·N + c, as c2dsr_rgemm's epilogue 1.  workspace: guard_workspace bytes. */
+size_t c2dsr_rgemm_guard_workspace(int M, int N);
+int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int lda, const void* B, int ldb, const float* W,
+                              float* C, int ldc, const float* bias, uint32_t k0, uint32_t k1, float p, int64_t row_base,
+                              const int* rowmap, void* workspace, size_t ws_bytes, void* stream);
 /* ... and the weight-gradient products (c2dsr_wgemm / _multi contract, dY fp32) */
 int c2dsr_wgemm_x3(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
                    float* db, void* part, void* stream);

@@ -213,6 +213,48 @@ def test_rgemm_x3_relu_dropout_epilogue():
     assert rel(C, ref) < TOL
 
 
+@pytest.mark.parametrize('M,rowmap', [(4099, False), (1000, True)])
+def test_rgemm_x3_relu_guard_signs(M, rowmap):
+    """linear1 of the fp32 mode (c2dsr_rgemm_x3_relu_guard): split products with every pre-activation within
+    the split error bound of zero recomputed exactly.  Inputs are built so that one column per row has a
+    pre-activation ~1e-6 of ‖a‖‖w‖ (far inside the split error, outside fp32's): every ReLU decision with
+    |v| > 2e-7·‖a‖‖w‖ matches float64 (the unguarded split product flips some of them), values within the
+    fp32-mode tolerance, relu·dropout with the row map as c2dsr_rgemm's epilogue."""
+    import numpy as np
+    from c2dsr_amd.ops import rgemm, rgemm_relu_guard, to_split_bf16
+    from oracle.c2dsr_oracle import keep_mask
+    N, K, p = 256, 256, 0.2
+    g = torch.Generator().manual_seed(M)
+    W = torch.randn(N, K, generator=g, dtype=torch.float64) / 16
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    b = torch.zeros(N, dtype=torch.float64)
+    c = torch.arange(M) % N
+    w = W[c]
+    eps = (torch.rand(M, generator=g, dtype=torch.float64) - 0.5) * 2e-6
+    A = A - ((A * w).sum(1) / (w * w).sum(1) - eps * A.norm(dim=1) / w.norm(dim=1))[:, None] * w
+    A32, W32 = A.float(), W.float()
+    v = A32.double() @ W32.double().T  # the fp32 operands' exact pre-activations
+    scale = A32.double().norm(dim=1)[:, None] * W32.double().norm(dim=1)[None, :]
+    keys = (2024, 77)
+    rmap = torch.randperm(3 * M, generator=g)[:M].sort()[0].to(torch.int32) if rowmap else None
+    rd = (keys, p, 500) + ((rmap.to(DEV),) if rowmap else ())
+    rows = (rmap.numpy().astype(np.int64) if rowmap else np.arange(M)) + 500
+    mk = torch.from_numpy(keep_mask(rows[:, None] * N + np.arange(N)[None, :], keys, p).astype(np.float32)).double()
+    ref = torch.relu(v) * mk / (1 - p)
+    Wx = to_split_bf16(W32.to(DEV))
+    C = torch.empty(M, N, device=DEV)
+    rgemm_relu_guard(A32.to(DEV), Wx, W32.to(DEV), C, M=M, N=N, K=K, bias=b.float().to(DEV), relu_drop=rd)
+    C0 = torch.empty(M, N, device=DEV)
+    rgemm(A32.to(DEV), Wx, C0, M=M, N=N, K=K, bias=b.float().to(DEV), relu_drop=rd, x3=True)
+    torch.cuda.synchronize()
+    clear = (v.abs() > 2e-7 * scale) & (mk > 0)
+    got, plain = C.double().cpu(), C0.double().cpu()
+    assert torch.equal((got > 0)[clear], (v > 0)[clear])
+    flips = int(((plain > 0) != (v > 0))[clear].sum())
+    assert flips > 0, 'the inputs should put some pre-activations inside the split error'
+    assert rel(C, ref) < TOL
+
+
 @pytest.mark.parametrize('T,N', [(1000, 256), (4097, 768), (31, 128)])
 def test_wgemm_x3_matches_float64(T, N):
     """Split-bf16 weight gradient dW = beta·dW + dYᵀ·X (+ exact fp32 bias sums) vs float64; deterministic;

@@ -25,10 +25,12 @@ def main():
     batches = [tuple(torch.from_numpy(r[i * B:(i + 1) * B].copy()).cuda() for r in rows) for i in range(12)]
     tr.model.train()
     tr.optimizer.zero_grad()
+    counts = {id(b): tr.launch_counts(tuple(r[i * B:(i + 1) * B] for r in rows), global_rows=B)
+              for i, b in enumerate(batches)}  # as bench.py: the launch sizes come with the batch
 
     def step(b):
         tr.model.convolve_graph()
-        return tr.train_batch(b, global_rows=B)
+        return tr.train_batch(b, global_rows=B, counts=counts[id(b)])
 
     for i in range(3):
         step(batches[i])

@@ -71,6 +71,27 @@ def main(x3=False):
             gb = 4.0 * M * (K + N) / t / 1e3
             print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: {"x3" if x3 else "b16"} N {N} M {M:6d}: {t:6.1f} us '
                   f'{gb:6.0f} GB/s', flush=True)
+            if x3:
+                rg3_stamps(lambda: rgemm(A, Wb, C, M=M, N=N, K=K, x3=x3))
+
+
+def rg3_stamps(f):
+    """Diagnostic build (-DRG3_STAMP): cycles per chunk per wave of the rg3 loop's phases."""
+    from c2dsr_amd._lib import lib
+    try:
+        fn = lib.raw('c2dsr_rg3_stamps')
+    except AttributeError:
+        return
+    import ctypes
+    buf = (ctypes.c_ulonglong * 8)()
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    f()
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    ch, waves = max(1, buf[6]), max(1, buf[7])
+    print(f'  stamps: prologue {buf[0] / waves:.0f} per wave; per chunk: mfma+stage {buf[1] / ch:.0f}, '
+          f'epilogue {buf[2] / ch:.0f}, barrier {buf[3] / ch:.0f} cycles ({ch // waves} chunks per wave)', flush=True)
 
 
 if __name__ == '__main__':
