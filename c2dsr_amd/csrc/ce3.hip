@@ -49,7 +49,7 @@
 #define CE3B_DT 2
 #endif
 #ifndef CE3_ILV
-#define CE3_ILV 1
+#define CE3_ILV (CE3_BI ? 0 : 1)
 #endif
 #ifndef CE3B_ILV
 #define CE3B_ILV 1
@@ -111,6 +111,41 @@ __device__ __forceinline__ float quad_sum(float x) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+#ifndef CE3_BI
+#define CE3_BI 0
+#endif
+#ifndef CE3_VN
+#define CE3_VN 3
+#endif
+#if CE3_BI
+// CE3_BI: the split products as compiler-visible MFMAs (exact hazard padding, so the scheduler can place the
+// step's LDS reads and VALU work between dependent MFMAs, sched_group_barrier pattern in the tile loop)
+#define MF(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
+__device__ __forceinline__ void split3_s0(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                          const bf16x8& bl) {
+  acc = MF(ah, bh, (f32x4{0.f, 0.f, 0.f, 0.f}));
+  acc = MF(al, bh, acc);
+  acc = MF(ah, bl, acc);
+}
+__device__ __forceinline__ void split3_s(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                         const bf16x8& bl) {
+  acc = MF(ah, bh, acc);
+  acc = MF(al, bh, acc);
+  acc = MF(ah, bl, acc);
+}
+__device__ __forceinline__ void split3_u(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                         const bf16x8& bl) {
+  acc = MF(ah, bh, acc);
+  acc = MF(ah, bl, acc);
+  acc = MF(al, bh, acc);
+}
+__device__ __forceinline__ void mf1_s0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  acc = MF(a, b, (f32x4{0.f, 0.f, 0.f, 0.f}));
+}
+__device__ __forceinline__ void mf1_s(f32x4& acc, const bf16x8& a, const bf16x8& b) { acc = MF(a, b, acc); }
+__device__ __forceinline__ void mf1_u(f32x4& acc, const bf16x8& a, const bf16x8& b) { acc = MF(a, b, acc); }
+#undef MF
+#else
 // One split product step as ONE asm statement (three MFMAs on one accumulator; separate statements get
 // an s_nop between dependent MFMAs from the hazard pass):  acc (+)= a_hi·b_hi + a_lo·b_hi + a_hi·b_lo.
 // S product: the stationary b_hi / b_lo pinned to AGPRs (128 registers that would otherwise be re-staged
@@ -155,6 +190,18 @@ __device__ __forceinline__ void mf1_s(f32x4& acc, const bf16x8& a, const bf16x8&
 }
 __device__ __forceinline__ void mf1_u(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+#endif
+// scheduling hint for one tile-loop step (CE3_BI): per MFMA, one LDS read and up to VN VALU instructions
+template <int NMF, int VN>
+__device__ __forceinline__ void step_pattern() {
+#if CE3_BI
+  [&]<int... I>(std::integer_sequence<int, I...>) {
+    ((__builtin_amdgcn_sched_group_barrier(0x008, 1, 0), __builtin_amdgcn_sched_group_barrier(0x100, 1, 0),
+      __builtin_amdgcn_sched_group_barrier(0x002, VN, 0), (void)I),
+     ...);
+  }(std::make_integer_sequence<int, NMF>{});
+#endif
 }
 
 // swept rows per LDS tile: 32 for split images (2D columns), 64 for plain bf16 (D columns) — 32 KiB at D = 256
@@ -441,6 +488,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
                 __builtin_amdgcn_sched_barrier(0);
                 s_prod.template operator()<k / CB>(sn[cb * 2 + 1], fa[k % (DS + 2)], 1);
               }
+              step_pattern<SPLIT ? 6 : 2, CE3_VN>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -488,6 +536,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
                 __builtin_amdgcn_sched_barrier(0);
                 u_prod(1);
               }
+              step_pattern<SPLIT ? 6 : 2, CE3_VN>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);

@@ -1,7 +1,9 @@
 // PyTorch-ROCm extension of the gfx950 kernel library (north_star: "exposed through a PyTorch-ROCm C++/HIP
 // extension"): TORCH_LIBRARY(c2dsr, m) registers every C-ABI entry point of include/c2dsr.h as a
-// schema op (torch.ops.c2dsr.*, generated: torch_ops_gen.inc) plus the fused launch sequences of the training
-// step's stages (one dispatcher call instead of one host call per kernel; c2dsr_amd/ops.py, losshead.py use them).
+// schema op (torch.ops.c2dsr.<name without the c2dsr_ prefix>, generated from the header: torch_ops_gen.inc), with
+// tensor arguments checked for device and dtype.  The training step's Python host side (c2dsr_amd/ops.py,
+// losshead.py) binds the same library through ctypes (c2dsr_amd/_lib.py); these ops are the interface for
+// TorchScript / C++ callers, and tests/test_gpu_torch_ops.py holds them bit-equal to the ctypes path.
 // Every op enqueues on the current HIP stream and raises (RuntimeError) on a bad argument or a hipError.
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
