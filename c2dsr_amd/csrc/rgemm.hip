@@ -650,7 +650,13 @@ __device__ __forceinline__ bf16x8 tr32(const char* img, int rr0, int kb0, int la
 // T[k] rows padded to a multiple of 32, so no 32-row chunk straddles two segments or a split end).
 constexpr int WG_MAXSEG = 4;
 #ifndef WG_AHEAD
-#define WG_AHEAD 2  // chunks loaded ahead (3: three register sets — spills, 2.5x slower)
+#define WG_AHEAD 2  // chunks loaded ahead (3: three register sets — spills at 4 waves, 2.5x slower)
+#endif
+#ifndef WG_NW_X3
+#define WG_NW_X3 4  // waves per workgroup of the split-bf16 weight gradient
+#endif
+#ifndef WG_AH_X3
+#define WG_AH_X3 WG_AHEAD
 #endif
 struct WSeg {
   const void* dY[WG_MAXSEG];
@@ -666,13 +672,21 @@ __device__ __forceinline__ V wg_pick(const V (&a)[WG_MAXSEG], int k) {  // unifo
 
 // X3 (fp32 mode, c2dsr_wgemm_x3): both chunks staged as split-bf16 hi and lo images, three MFMAs per step
 // (y_hi·x_hi + y_lo·x_hi + y_hi·x_lo, fp32 accumulation; the bias column sums stay exact fp32).
-template <bool YB16, bool X3 = false>
-__global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restrict__ part,
-                                                 float* __restrict__ part_b, int NTL, int rows_per_split) {
+// NW: waves per workgroup — 4 (wave tile 64 n × 128 i) or 8 (32 n × 128 i: two waves per SIMD, so one wave's
+// staging and barrier waits run under the other's MFMAs); AH: chunks loaded ahead in registers (2 or 3).  The
+// accumulation order of every output element is the same for all (NW, AH).
+template <bool YB16, bool X3 = false, int NW = 4, int AH = WG_AHEAD>
+__global__ __launch_bounds__(64 * NW) void wg_kernel(int N, WSeg sg, float* __restrict__ part,
+                                                     float* __restrict__ part_b, int NTL, int rows_per_split) {
   static_assert(!(YB16 && X3), "split operands take fp32 dY");
+  static_assert((NW == 4 || NW == 8) && (AH == 2 || AH == 3), "wg shape");
+  constexpr int NT = 64 * NW;       // threads
+  constexpr int NYU = 1024 / NT;    // dY float4 per thread per chunk (32 rows × 128 columns)
+  constexpr int NXU = 2048 / NT;    // X float4 per thread per chunk (32 rows × 256 columns)
+  constexpr int NA = 8 / NW;        // 32-row n tiles per wave
   const int T = sg.vbeg[WG_MAXSEG];  // virtual rows (entries past nseg repeat the total)
   constexpr int YIMG = 32 * 128 * 2, XIMG = 32 * 256 * 2;  // bytes per image (X3: lo image after hi)
-  __shared__ __attribute__((aligned(16))) float4 red_b[8][32];
+  __shared__ __attribute__((aligned(16))) float4 red_b[NT / 32][32];
   __shared__ __attribute__((aligned(16))) char yimg[2][(X3 ? 2 : 1) * YIMG];
   __shared__ __attribute__((aligned(16))) char ximg[2][(X3 ? 2 : 1) * XIMG];
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -687,7 +701,7 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n_base = nt * 128;
   constexpr int YEB = YB16 ? 2 : 4;
-  const int lrow = threadIdx.x >> 6;  // 0..3
+  const int lrow = threadIdx.x >> 6;  // 0..NW-1
   // chunk c: thread t loads dY rows lrow + 4u (u < 8) → 1 float4 (cols 4·(lane&31) of the 128) per
   // half-wave pair... simpler: dY chunk 32×128 floats = 1024 float4 = 4 per thread, X 2048 = 8 per thread.
   // The chunk's segment (uniform): rows past its T read 0 through the descriptors.
@@ -701,8 +715,8 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
     const int ldyb = ly_ * YEB, ldxb = lx_ * 4;                                                               \
     const auto ysrc = rsrc_bytes(wg_pick(sg.dY, k_), (long)tk_ * ly_ * YEB);                                  \
     const auto xsrc = rsrc_bytes(wg_pick(sg.X, k_), (long)tk_ * lx_ * 4);                                     \
-    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
-      const int q_ = threadIdx.x + 256 * u; /* 0..1023: row q_>>5, float4 q_&31 */                           \
+    _Pragma("unroll") for (int u = 0; u < NYU; ++u) {                                                         \
+      const int q_ = threadIdx.x + NT * u; /* 0..1023: row q_>>5, float4 q_&31 */                            \
       const int yo_ = (t0_ + (q_ >> 5)) * ldyb + (n_base + 4 * (q_ & 31)) * YEB;                              \
       if constexpr (YB16) {                                                                                   \
         const auto h_ = __builtin_amdgcn_raw_buffer_load_b64(ysrc, yo_, 0, 0);                                \
@@ -712,9 +726,9 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
         PY[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ysrc, yo_, 0, 0));           \
       }                                                                                                       \
     }                                                                                                         \
-    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                                           \
+    _Pragma("unroll") for (int u = 0; u < NXU; ++u) {                                                         \
       PX[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(                              \
-                                             xsrc, (t0_ + lrow + 4 * u) * ldxb + 16 * lane, 0, 0));           \
+                                             xsrc, (t0_ + lrow + NW * u) * ldxb + 16 * lane, 0, 0));          \
     }                                                                                                         \
   }
 #define WG_PUT(im, LOFF, row, col, v4)                                                                        \
@@ -736,41 +750,41 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
 #define WG_STAGE(PY, PX, b, cc)                                                                               \
   {                                                                                                           \
     const float on_ = (cc) < nchunk ? 1.f : 0.f;                                                              \
-    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                           \
-      const int q_ = threadIdx.x + 256 * u;                                                                   \
+    _Pragma("unroll") for (int u = 0; u < NYU; ++u) {                                                         \
+      const int q_ = threadIdx.x + NT * u;                                                                    \
       WG_PUT(yimg[b], YIMG, q_ >> 5, 4 * (q_ & 31), PY[u])                                                    \
       csum.x = fmaf(on_, PY[u].x, csum.x);                                                                    \
       csum.y = fmaf(on_, PY[u].y, csum.y);                                                                    \
       csum.z = fmaf(on_, PY[u].z, csum.z);                                                                    \
       csum.w = fmaf(on_, PY[u].w, csum.w);                                                                    \
     }                                                                                                         \
-    _Pragma("unroll") for (int u = 0; u < 8; ++u) WG_PUT(ximg[b], XIMG, lrow + 4 * u, 4 * lane, PX[u])        \
+    _Pragma("unroll") for (int u = 0; u < NXU; ++u) WG_PUT(ximg[b], XIMG, lrow + NW * u, 4 * lane, PX[u])     \
   }
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
-  f32x16 acc[2][4];
+  f32x16 acc[NA][4];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.f;
-  const int wn = (w >> 1) * 64, wi = (w & 1) * 128;  // this wave's 64 n-rows and 128 i-columns
+  const int wn = (w >> 1) * 32 * NA, wi = (w & 1) * 128;  // this wave's 32·NA n-rows and 128 i-columns
 #define WG_STEP(c, RY, RX, SY, SX)                                                                            \
   {                                                                                                           \
-    WG_LOAD((c) + WG_AHEAD, RY, RX)                                                                           \
+    WG_LOAD((c) + AH, RY, RX)                                                                                 \
     const char* yi_ = yimg[(c) & 1];                                                                          \
     const char* xi_ = ximg[(c) & 1];                                                                          \
     _Pragma("unroll") for (int kst = 0; kst < 2; ++kst) {                                                     \
-      bf16x8 fa_[2], fb_[4];                                                                                  \
-      _Pragma("unroll") for (int a = 0; a < 2; ++a) fa_[a] = tr32(yi_, 16 * kst, wn + 32 * a, lane);          \
+      bf16x8 fa_[NA], fb_[4];                                                                                 \
+      _Pragma("unroll") for (int a = 0; a < NA; ++a) fa_[a] = tr32(yi_, 16 * kst, wn + 32 * a, lane);         \
       _Pragma("unroll") for (int b = 0; b < 4; ++b) fb_[b] = tr32(xi_, 16 * kst, wi + 32 * b, lane);          \
-      _Pragma("unroll") for (int a = 0; a < 2; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) acc[a][b] = \
+      _Pragma("unroll") for (int a = 0; a < NA; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) acc[a][b] = \
           __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_[a], fb_[b], acc[a][b], 0, 0, 0);                        \
       if constexpr (X3) {                                                                                     \
-        bf16x8 fal_[2], fbl_[4];                                                                              \
-        _Pragma("unroll") for (int a = 0; a < 2; ++a) fal_[a] = tr32(yi_ + YIMG, 16 * kst, wn + 32 * a, lane); \
+        bf16x8 fal_[NA], fbl_[4];                                                                             \
+        _Pragma("unroll") for (int a = 0; a < NA; ++a) fal_[a] = tr32(yi_ + YIMG, 16 * kst, wn + 32 * a, lane); \
         _Pragma("unroll") for (int b = 0; b < 4; ++b) fbl_[b] = tr32(xi_ + XIMG, 16 * kst, wi + 32 * b, lane); \
-        _Pragma("unroll") for (int a = 0; a < 2; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) {        \
+        _Pragma("unroll") for (int a = 0; a < NA; ++a) _Pragma("unroll") for (int b = 0; b < 4; ++b) {       \
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fal_[a], fb_[b], acc[a][b], 0, 0, 0);           \
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa_[a], fbl_[b], acc[a][b], 0, 0, 0);           \
         }                                                                                                     \
@@ -780,8 +794,8 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
     __syncthreads();                                                                                          \
   }
   if (nchunk > 0) {
-#if WG_AHEAD == 2
-    float4 Ya[4], Xa[8], Yb[4], Xb[8];
+    if constexpr (AH == 2) {
+    float4 Ya[NYU], Xa[NXU], Yb[NYU], Xb[NXU];
     WG_LOAD(0, Ya, Xa)
     WG_LOAD(1, Yb, Xb)
     WG_STAGE(Ya, Xa, 0, 0)
@@ -791,10 +805,10 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
       if (c + 1 >= nchunk) break;
       WG_STEP(c + 1, Yb, Xb, Ya, Xa)
     }
-#else
+    } else {
     // three register sets: chunk c+3 is loaded at step c, so the staging of chunk c+1 (end of step c) waits on a
     // load issued two steps earlier
-    float4 Ya[4], Xa[8], Yb[4], Xb[8], Yc[4], Xc[8];
+    float4 Ya[NYU], Xa[NXU], Yb[NYU], Xb[NXU], Yc[NYU], Xc[NXU];
     WG_LOAD(0, Ya, Xa)
     WG_LOAD(1, Yb, Xb)
     WG_LOAD(2, Yc, Xc)
@@ -807,20 +821,20 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
       if (c + 2 >= nchunk) break;
       WG_STEP(c + 2, Yc, Xc, Ya, Xa)
     }
-#endif
+    }
   }
 #undef WG_STEP
 #undef WG_STAGE
 #undef WG_PUT
 #undef WG_LOAD
-  // column sums: the 8 threads of a column group (tid >> 5 = 0..7) combined in a fixed order
+  // column sums: the NT/32 threads of a column group (tid >> 5) combined in a fixed order
   if (part_b) {
     red_b[threadIdx.x >> 5][threadIdx.x & 31] = csum;
     __syncthreads();
     if (threadIdx.x < 32) {
       float4 t = red_b[0][threadIdx.x];
 #pragma unroll
-      for (int j = 1; j < 8; ++j) t = make_float4(t.x + red_b[j][threadIdx.x].x, t.y + red_b[j][threadIdx.x].y,
+      for (int j = 1; j < NT / 32; ++j) t = make_float4(t.x + red_b[j][threadIdx.x].x, t.y + red_b[j][threadIdx.x].y,
                                                   t.z + red_b[j][threadIdx.x].z, t.w + red_b[j][threadIdx.x].w);
       const int n0 = n_base + 4 * threadIdx.x;
       if (n0 < N) *(float4*)(part_b + (long)split * N + n0) = t;
@@ -829,7 +843,7 @@ __global__ __launch_bounds__(256) void wg_kernel(int N, WSeg sg, float* __restri
   // D[n][i]: lane holds (row n = wn + 32a + creg(r), col i = wi + 32b + (lane&31))
   float* out = part + (long)split * N * 256;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < NA; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b)
 #pragma unroll
@@ -1185,7 +1199,8 @@ static int wgemm_segs(const WSeg& sg, int N, int D, bool yb16, float beta, float
   float* part_b = db ? (float*)part + (long)splits * n : nullptr;
   if (x3 && yb16) return (int)hipErrorInvalidValue;
   if (x3)
-    wg_kernel<false, true><<<blocks, 256, 0, s>>>(N, sg, (float*)part, part_b, NTL, rows);
+    wg_kernel<false, true, WG_NW_X3, WG_AH_X3><<<blocks, 64 * WG_NW_X3, 0, s>>>(N, sg, (float*)part, part_b, NTL,
+                                                                                rows);
   else if (yb16)
     wg_kernel<true><<<blocks, 256, 0, s>>>(N, sg, (float*)part, part_b, NTL, rows);
   else
