@@ -628,16 +628,23 @@ __global__ __launch_bounds__(256) void seg_split2_kernel(SegJob j0, SegJob j1) {
 // staged keys) are in flight per wave.
 constexpr int FE = 256;  // plan entries per workgroup (a multiple of SEG_CH)
 constexpr int FU = 32;   // entries per batch
-static_assert(FE % SEG_CH == 0, "fused chunk geometry");
+static_assert(FE % SEG_CH == 0 && FU <= 64 && (FU & (FU - 1)) == 0, "fused chunk geometry");
+
+// buffer descriptor over [base, base + bytes) (out-of-range offsets load 0 and store nothing: branch-free reads of
+// optional rows); inputs made wave-uniform so the buffer ops need no waterfall loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fused_rsrc(const void* base, long bytes) {
+  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL));
+  const uint64_t p = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
+}
 
 template <bool MAPPED, bool OUT16>
 __global__ __launch_bounds__(256) void seg_fused_kernel(SegJob J, const int64_t* __restrict__ pos, int n_pos,
-                                                        float* __restrict__ ppart) {
-  extern __shared__ float bins[];  // [n_pos][256]
+                                                        long rows_a, long rows_b, float* __restrict__ ppart) {
+  extern __shared__ float bins[];  // [n_pos + 1][256] (row n_pos: the sink of rows without a valid position)
   __shared__ uint32_t sk[FE + 2];  // sk[e + 1] = K[e0 + e]; the neighbours at 0 and FE + 1
-  __shared__ uint32_t sv[FE];
-  __shared__ int sm[2][MAPPED ? FE : 1];
-  __shared__ int sp[FE];
+  __shared__ int sa[FE], sb[FE], sp[FE], sq[FE], sr[FE];  // per entry: source rows (-1: absent), bin, close, row
   const int n = J.n, d = J.src.d;
   const long e0 = (long)blockIdx.x * FE;
   const int cnt = (int)min((long)FE, (long)n - e0);
@@ -645,91 +652,102 @@ __global__ __launch_bounds__(256) void seg_fused_kernel(SegJob J, const int64_t*
     const long gi = e0 - 1 + e;
     sk[e] = (gi >= 0 && gi < n) ? J.K[gi] : 0xffffffffu;
   }
-  for (int e = threadIdx.x; e < FE; e += 256) {
-    const long gi = e0 + e;
-    const uint32_t rv = gi < n ? min(J.V[gi], (uint32_t)(n - 1)) : 0u;
-    sv[e] = rv;
-    if constexpr (MAPPED) {
-      sm[0][e] = J.src.map1[rv];
-      sm[1][e] = J.src.map2[rv];
+  __syncthreads();
+  // per-entry constants, once per workgroup: the row sources, the position bin (n_pos: the sink of an invalid
+  // position), and how the item run closes there — seg_chunk_kernel's rules per 16-entry chunk, encoded as
+  // kind << 28 | (the out row for kind 1, the 16-entry chunk for the head / tail slots)
+  for (int i = threadIdx.x; i < FE; i += 256) {
+    const long e = e0 + i;
+    int a = -1, b = -1, bin = n_pos, kq = 0, r = 0;
+    if (i < cnt) {
+      r = (int)min(J.V[e], (uint32_t)(n - 1));
+      if constexpr (MAPPED) {
+        a = J.src.map1[r];
+        b = J.src.map2[r];
+      } else {
+        a = r;
+      }
+      const int64_t pq = pos[r];
+      if (pq >= 0 && pq < n_pos) bin = (int)pq;
+      else atomicOr(J.err, 16);
+      const long s16 = e & ~(long)(SEG_CH - 1), end16 = min(s16 + SEG_CH, (long)n);
+      const int ls = (int)(s16 - e0), le = (int)(end16 - e0);
+      const uint32_t key = sk[i + 1];
+      if (e == end16 - 1 || sk[i + 2] != key) {
+        const bool cont_head = s16 > 0 && sk[ls + 1] == sk[ls];
+        const bool first = key == sk[ls + 1];
+        const bool cont_tail = end16 < n && sk[le + 1] == sk[le];
+        const int kind = (first && cont_head) ? 2 : (e == end16 - 1 && cont_tail) ? 3 : key >= (uint32_t)J.n_out ? 4
+                       : (int)key != J.skip_key ? 1 : 5;
+        kq = (kind << 28) | (kind == 1 ? (int)key : (int)(e / SEG_CH));
+      }
     }
-    const int64_t pq = gi < n ? pos[rv] : 0;
-    const bool ok = pq >= 0 && pq < n_pos;
-    sp[e] = ok ? (int)pq : -1;
-    if (gi < n && !ok) atomicOr(J.err, 16);
+    sa[i] = a;
+    sb[i] = b;
+    sp[i] = bin;
+    sq[i] = kq;
+    sr[i] = r;
   }
-  for (int i = threadIdx.x; i < n_pos * 256; i += 256) bins[i] = 0.f;
+  for (int i = threadIdx.x; i < (n_pos + 1) * 256; i += 256) bins[i] = 0.f;
   __syncthreads();
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int col = blockIdx.y * 256 + 64 * w + lane;
   if (col < d) {  // wave-uniform (d % 64 == 0)
     const RowSrc& src = J.src;
+    const auto ra = fused_rsrc(src.gX, rows_a * d * 4);
+    const auto rb = fused_rsrc(MAPPED ? src.gX2 : src.gX, rows_b * d * 4);
+    const auto ro = fused_rsrc(OUT16 ? (const void*)J.out16 : (const void*)J.out, (long)J.n_out * d * (OUT16 ? 2 : 4));
+    const int cb = col * 4;
     float* bcol = bins + 64 * w + lane;
     float acc = 0.f;
     for (int h0 = 0; h0 < cnt; h0 += FU) {
       float xa[FU], xb[FU], pv[FU];
-      int kind[FU];  // 0 nothing closes, 1 out[key] +=, 2 head slot, 3 tail slot, 4 bad key, 5 closes (skipped key)
+      // the batch's per-entry constants: lane u reads entry h0 + u's (one LDS round trip), each is then broadcast
+      // to the wave by readlane (scalar)
+      const int li = min(h0 + (lane & (FU - 1)), cnt - 1);
+      const int va = sa[li], vb = sb[li], vp = sp[li], vq = sq[li], vr = sr[li];
 #pragma unroll
-      for (int u = 0; u < FU; ++u) {
-        const int i = h0 + u;
-        xa[u] = xb[u] = 0.f;
-        if (i < cnt) {
-          if constexpr (MAPPED) {
-            const int a = sm[0][i], b = sm[1][i];
-            if (a >= 0) xa[u] = src.gX[(long)a * d + col];
-            if (b >= 0) xb[u] = src.gX2[(long)b * d + col];
-          } else {
-            xa[u] = src.gX[(long)sv[i] * d + col];
-          }
+      for (int u = 0; u < FU; ++u) {  // every load issued before any is used; absent rows read 0 (no traffic)
+        const int a = __builtin_amdgcn_readlane(va, u);
+        xa[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, a >= 0 ? a * d * 4 + cb : 0x7ffffff0, 0, 0));
+        if constexpr (MAPPED) {
+          const int b = __builtin_amdgcn_readlane(vb, u);
+          xb[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, b >= 0 ? b * d * 4 + cb : 0x7ffffff0, 0, 0));
+        }
+        const int kq = __builtin_amdgcn_readlane(vq, u);
+        const int ooff = (kq >> 28) == 1 && h0 + u < cnt ? (kq & 0x0fffffff) * d * (OUT16 ? 2 : 4) + col * (OUT16 ? 2 : 4)
+                                                         : 0x7ffffff0;
+        if constexpr (OUT16) {
+          const unsigned short h = __builtin_amdgcn_raw_buffer_load_b16(ro, ooff, 0, 0);
+          pv[u] = (float)__builtin_bit_cast(c2::tbf16, h);
+        } else {
+          pv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ro, ooff, 0, 0));
         }
       }
 #pragma unroll
       for (int u = 0; u < FU; ++u) {
         const int i = h0 + u;
-        const long e = e0 + i;
-        kind[u] = 0;
-        pv[u] = 0.f;
-        if (i < cnt) {
-          const long s16 = e & ~(long)(SEG_CH - 1), end16 = min(s16 + SEG_CH, (long)n);
-          const int ls = (int)(s16 - e0), le = (int)(end16 - e0);
-          const uint32_t key = sk[i + 1];
-          if (e == end16 - 1 || sk[i + 2] != key) {
-            const bool cont_head = s16 > 0 && sk[ls + 1] == sk[ls];
-            const bool first = key == sk[ls + 1];
-            const bool cont_tail = end16 < n && sk[le + 1] == sk[le];
-            kind[u] = (first && cont_head) ? 2 : (e == end16 - 1 && cont_tail) ? 3 : key >= (uint32_t)J.n_out ? 4
-                    : (int)key != J.skip_key ? 1 : 5;
-            if (kind[u] == 1) {
-              const long off = (long)key * d + col;
-              pv[u] = OUT16 ? (float)J.out16[off] : J.out[off];
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < FU; ++u) {
-        const int i = h0 + u;
-        if (i < cnt) {
-          const uint32_t r = sv[i];
+        if (i < cnt) {  // uniform
           float v = xa[u];
           if constexpr (MAPPED) {
-            if (sm[1][i] >= 0) v = v + xb[u];
+            if (__builtin_amdgcn_readlane(vb, u) >= 0) v = v + xb[u];
           }
-          if (src.drop.active()) v = v * src.drop.mul((uint64_t)(src.idx_base + r) * d + col);
-          const int pq = sp[i];
-          if (pq >= 0 && (!MAPPED || sm[0][i] >= 0 || sm[1][i] >= 0)) atomicAdd(bcol + pq * 256, v);
+          if (src.drop.active())
+            v = v * src.drop.mul((uint64_t)(src.idx_base + __builtin_amdgcn_readlane(vr, u)) * d + col);
+          atomicAdd(bcol + __builtin_amdgcn_readlane(vp, u) * 256, v);
           acc = acc + src.scale * v;
-          if (kind[u]) {
-            const long gq = (e0 + i) / SEG_CH;
-            if (kind[u] == 1) {
-              const long off = (long)sk[i + 1] * d + col;
-              if constexpr (OUT16) J.out16[off] = (c2::tbf16)(pv[u] + acc);
-              else J.out[off] = pv[u] + acc;
-            } else if (kind[u] == 2) {
-              J.ph[gq * d + col] = acc;
-            } else if (kind[u] == 3) {
-              J.pt[gq * d + col] = acc;
-            } else if (kind[u] == 4 && lane == 0) {
+          const int kq = __builtin_amdgcn_readlane(vq, u);
+          const int kind = kq >> 28;
+          if (kind) {
+            const long slot = (long)(kq & 0x0fffffff) * d + col;
+            if (kind == 1) {
+              if constexpr (OUT16) J.out16[slot] = (c2::tbf16)(pv[u] + acc);
+              else J.out[slot] = pv[u] + acc;
+            } else if (kind == 2) {
+              J.ph[slot] = acc;
+            } else if (kind == 3) {
+              J.pt[slot] = acc;
+            } else if (kind == 4 && lane == 0) {
               atomicOr(J.err, 2);
             }
             acc = 0.f;
@@ -1046,19 +1064,24 @@ static int embed_bwd_planned_impl(const void* seq_plan, const void* pos_plan, in
 // ---- fused form: item sums over the item plan + position sums from the same row reads (seg_fused_kernel)
 extern "C" int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 
-C2_API int c2dsr_embed_bwd_fused_supported(int d, int n_pos) { return d % 64 == 0 && n_pos > 0 && n_pos <= 56; }
+C2_API int c2dsr_embed_bwd_fused_supported(int n_rows, int d, int n_items, int n_pos) {
+  return d % 64 == 0 && n_pos > 0 && n_pos <= 56 && (long)n_items * d * 4 < (1L << 31) &&
+         (long)n_rows * d * 4 < (1L << 31);
+}
 
 C2_API size_t c2dsr_embed_bwd_fused_workspace(int n_rows, int d, int n_pos) {
   return seg_ws_bytes(n_rows, d) + align256((size_t)c2::ceil_div(n_rows, FE) * n_pos * d * 4);
 }
 
 C2_API int c2dsr_embed_bwd_fused(const void* seq_plan, const int64_t* pos, int n_rows, int d, const float* gXa,
-                                 const int* inv_a, const float* gXb, const int* inv_b, uint32_t k0, uint32_t k1, float p,
-                                 int64_t idx_base, float scale, float* G, int n_items, float* gP, int n_pos,
-                                 void* workspace, size_t ws_bytes, void* stream) {
+                                 int rows_a, const int* inv_a, const float* gXb, int rows_b, const int* inv_b, uint32_t k0,
+                                 uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items, float* gP,
+                                 int n_pos, void* workspace, size_t ws_bytes, void* stream) {
   if (n_rows == 0) return 0;
   const bool mapped = inv_a != nullptr;
-  if (!c2dsr_embed_bwd_fused_supported(d, n_pos) || !seq_plan || !pos || !G || !gP || !gXa ||
+  if (!mapped) rows_a = rows_b = n_rows;
+  if (!c2dsr_embed_bwd_fused_supported(n_rows, d, n_items, n_pos) || !seq_plan || !pos || !G || !gP || !gXa ||
+      (long)rows_a * d * 4 >= (1L << 31) || (long)rows_b * d * 4 >= (1L << 31) ||
       mapped != (inv_b != nullptr) || mapped != (gXb != nullptr) ||
       ws_bytes < c2dsr_embed_bwd_fused_workspace(n_rows, d, n_pos))
     return (int)hipErrorInvalidValue;
@@ -1070,11 +1093,11 @@ C2_API int c2dsr_embed_bwd_fused(const void* seq_plan, const int64_t* pos, int n
   float* ppart = (float*)(ws + seg_ws_bytes(n_rows, d));
   const int nch = c2::ceil_div(n_rows, FE);
   const dim3 grid(nch, c2::ceil_div(d, 256));
-  const size_t shm = (size_t)n_pos * 256 * 4;
+  const size_t shm = (size_t)(n_pos + 1) * 256 * 4;
   if (mapped)
-    seg_fused_kernel<true, false><<<grid, 256, shm, s>>>(j, pos, n_pos, ppart);
+    seg_fused_kernel<true, false><<<grid, 256, shm, s>>>(j, pos, n_pos, rows_a, rows_b, ppart);
   else
-    seg_fused_kernel<false, false><<<grid, 256, shm, s>>>(j, pos, n_pos, ppart);
+    seg_fused_kernel<false, false><<<grid, 256, shm, s>>>(j, pos, n_pos, rows_a, rows_b, ppart);
   switch (lpr_for(d)) {
     case 64: seg_pass_b<64>(j, s); break;
     case 32: seg_pass_b<32>(j, s); break;

@@ -190,13 +190,13 @@ def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
         assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
         # the one-read form (c2dsr_embed_bwd_fused: item sums over the item plan, position sums from the same row
         # reads): item sums bit-identical to the planned form, position sums to float64 at 1e-5, reproducible
-        assert lib.raw('c2dsr_embed_bwd_fused_supported')(d, L)
+        assert lib.raw('c2dsr_embed_bwd_fused_supported')(n_rows, d, n_items, L)
         fb = lib.raw('c2dsr_embed_bwd_fused_workspace')(n_rows, d, L)
         fws = torch.empty(fb, dtype=torch.uint8, device=DEV)
         fused = []
         for rows in (False, True, True):
             G4, gP4 = torch.zeros(n_items, d, device=DEV), torch.zeros(L, d, device=DEV)
-            src = (ga, ia, gb, ib) if rows else (gfull, None, None, None)
+            src = (ga, ga.shape[0], ia, gb, gb.shape[0], ib) if rows else (gfull, n_rows, None, None, n_rows, None)
             lib('c2dsr_embed_bwd_fused', sp.get(), pd, n_rows, d, *src, keys[0], keys[1], p, 77, scale, G4, n_items,
                 gP4, L, fws, fb, stream())
             fused.append((G4, gP4))

@@ -55,8 +55,8 @@ def main():
 
     fb = int(lib.raw('c2dsr_embed_bwd_fused_workspace')(n_rows, d, L))
     fws = torch.empty(fb, dtype=torch.uint8, device=dev)
-    t_f = timeit(lambda: lib('c2dsr_embed_bwd_fused', spb, pd, n_rows, d, gX, None, None, None, 0, 0, 0.0, 0, 1.0, G,
-                             N, gP, L, fws, fb, s))
+    t_f = timeit(lambda: lib('c2dsr_embed_bwd_fused', spb, pd, n_rows, d, gX, n_rows, None, None, n_rows, None, 0, 0,
+                             0.0, 0, 1.0, G, N, gP, L, fws, fb, s))
     t_g = timeit(lambda: run(G, None))
     t_p = timeit(lambda: run(None, gP))
     t_b = timeit(lambda: run(G, gP))

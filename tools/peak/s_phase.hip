@@ -27,7 +27,9 @@ __device__ __forceinline__ void one(f32x4& acc, const bf16x8& a, const bf16x8& b
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
 }
 
-template <bool R, bool V, bool C, bool I>
+#define MFB(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
+// PD: prefetch distance of the reads (steps); BI: compiler-visible MFMAs, one read / VALU group per MFMA gap
+template <bool R, bool V, bool C, bool I, int PD = 2, bool BI = false>
 __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigned long long* cyc) {
   __shared__ __attribute__((aligned(16))) char img[65536];
   const int lane = threadIdx.x & 63;
@@ -45,9 +47,9 @@ __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigne
   }
   f32x4 s0 = {}, s1 = {}, s2 = {}, s3 = {}, s4 = {}, s5 = {};
   float z = 0.f, sc = 0.1f * lane, m = 0.5f;
-  bf16x8 fr[4][2];
+  bf16x8 fr[8][2];
   const int base = (lane * 16) & 0x3ff0;
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < 8; ++k) {
     fr[k][0] = ah;
     fr[k][1] = al;
   }
@@ -57,12 +59,30 @@ __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigne
     for (int k = 0; k < 16; ++k) {
       if constexpr (R) {
         const int o = (k * 2048 + (it & 7) * 4096) & 0x7fff;  // varies with it: not hoisted
-        fr[(k + 2) & 3][0] = *(const bf16x8*)(img + base + o);
-        fr[(k + 2) & 3][1] = *(const bf16x8*)(img + base + o + 32768);
+        fr[(k + PD) & 7][0] = *(const bf16x8*)(img + base + o);
+        fr[(k + PD) & 7][1] = *(const bf16x8*)(img + base + o + 32768);
       }
-      const bf16x8& a = fr[k & 3][0];
-      const bf16x8& b = fr[k & 3][1];
-      if constexpr (I) {
+      const bf16x8& a = fr[k & 7][0];
+      const bf16x8& b = fr[k & 7][1];
+      if constexpr (BI) {
+        s0 = MFB(a, bh0, s0);
+        s0 = MFB(b, bh0, s0);
+        s0 = MFB(a, bl0, s0);
+        if constexpr (V) {
+          const float p = __builtin_amdgcn_exp2f(sc - m);
+          sc = p * 0.999f;
+          z += p;
+        }
+        s1 = MFB(a, bh1, s1);
+        s1 = MFB(b, bh1, s1);
+        s1 = MFB(a, bl1, s1);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+      } else if constexpr (I) {
         one(s0, a, bh0);
         one(s1, b, bh0);
         one(s2, a, bl0);
@@ -104,15 +124,15 @@ __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigne
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <bool R, bool V, bool C, bool I>
+template <bool R, bool V, bool C, bool I, int PD = 2, bool BI = false>
 void run(const char* name, int iters, float* out, unsigned long long* cyc, int ncu) {
-  s_phase<R, V, C, I><<<ncu, 256>>>(iters, out, cyc);
+  s_phase<R, V, C, I, PD, BI><<<ncu, 256>>>(iters, out, cyc);
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  s_phase<R, V, C, I><<<ncu, 256>>>(iters, out, cyc);
+  s_phase<R, V, C, I, PD, BI><<<ncu, 256>>>(iters, out, cyc);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0.f;
@@ -143,5 +163,10 @@ int main(int argc, char** argv) {
   run<true, true, false, false>("+reads+valu", iters, out, cyc, ncu);
   run<true, true, true, false>("+reads+valu+burst", iters, out, cyc, ncu);
   run<false, false, true, false>("+burst", iters, out, cyc, ncu);
+  run<true, false, false, false, 4>("+reads pd4", iters, out, cyc, ncu);
+  run<true, true, false, false, 4>("+reads+valu pd4", iters, out, cyc, ncu);
+  run<true, false, false, false, 2, true>("BI +reads", iters, out, cyc, ncu);
+  run<true, true, false, false, 2, true>("BI +reads+valu", iters, out, cyc, ncu);
+  run<true, true, false, false, 4, true>("BI +reads+valu pd4", iters, out, cyc, ncu);
   return 0;
 }
