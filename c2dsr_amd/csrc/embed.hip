@@ -615,154 +615,6 @@ __global__ __launch_bounds__(256) void seg_split2_kernel(SegJob j0, SegJob j1) {
   }
 }
 
-// ------------------------------------------------------------------ fused item + position sums (one read per row)
-// The embedding backward's two segment sums from ONE read of each gradient row: the item sums walk
-// the item plan exactly as seg_chunk_kernel does — the same 16-entry chunk geometry, the same run closes into
-// out[key] / head / tail slots, the same per-element arithmetic, so pass B (seg_split1/2) completes them unchanged and
-// the item table gradient is bit-identical to the two-job form — while every row read also goes into per-workgroup
-// position bins in LDS (ds_add_f32: each (bin, column) belongs to one lane of one wave, whose LDS operations retire
-// in issue order, so the sums have a fixed order).  A workgroup takes FE consecutive plan entries and a 256-column
-// slice of the rows (wave w: columns 64w + lane, one float per lane, one entry per wave instruction: 256-byte
-// coalesced row slices); its bins [n_pos][256] go to ppart[chunk][n_pos][d], summed over the chunks in order by
-// c2dsr_sum_parts.  FU entries' row slices (and the out values their run closes read-modify-write, known from the
-// staged keys) are in flight per wave.
-constexpr int FE = 256;  // plan entries per workgroup (a multiple of SEG_CH)
-constexpr int FU = 32;   // entries per batch
-static_assert(FE % SEG_CH == 0 && FU <= 64 && (FU & (FU - 1)) == 0, "fused chunk geometry");
-
-// buffer descriptor over [base, base + bytes) (out-of-range offsets load 0 and store nothing: branch-free reads of
-// optional rows); inputs made wave-uniform so the buffer ops need no waterfall loop
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t fused_rsrc(const void* base, long bytes) {
-  const int nb = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL));
-  const uint64_t p = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, nb, 0x00020000);
-}
-
-template <bool MAPPED, bool OUT16>
-__global__ __launch_bounds__(256) void seg_fused_kernel(SegJob J, const int64_t* __restrict__ pos, int n_pos,
-                                                        long rows_a, long rows_b, float* __restrict__ ppart) {
-  extern __shared__ float bins[];  // [n_pos + 1][256] (row n_pos: the sink of rows without a valid position)
-  __shared__ uint32_t sk[FE + 2];  // sk[e + 1] = K[e0 + e]; the neighbours at 0 and FE + 1
-  __shared__ int sa[FE], sb[FE], sp[FE], sq[FE], sr[FE];  // per entry: source rows (-1: absent), bin, close, row
-  const int n = J.n, d = J.src.d;
-  const long e0 = (long)blockIdx.x * FE;
-  const int cnt = (int)min((long)FE, (long)n - e0);
-  for (int e = threadIdx.x; e < FE + 2; e += 256) {
-    const long gi = e0 - 1 + e;
-    sk[e] = (gi >= 0 && gi < n) ? J.K[gi] : 0xffffffffu;
-  }
-  __syncthreads();
-  // per-entry constants, once per workgroup: the row sources, the position bin (n_pos: the sink of an invalid
-  // position), and how the item run closes there — seg_chunk_kernel's rules per 16-entry chunk, encoded as
-  // kind << 28 | (the out row for kind 1, the 16-entry chunk for the head / tail slots)
-  for (int i = threadIdx.x; i < FE; i += 256) {
-    const long e = e0 + i;
-    int a = -1, b = -1, bin = n_pos, kq = 0, r = 0;
-    if (i < cnt) {
-      r = (int)min(J.V[e], (uint32_t)(n - 1));
-      if constexpr (MAPPED) {
-        a = J.src.map1[r];
-        b = J.src.map2[r];
-      } else {
-        a = r;
-      }
-      const int64_t pq = pos[r];
-      if (pq >= 0 && pq < n_pos) bin = (int)pq;
-      else atomicOr(J.err, 16);
-      const long s16 = e & ~(long)(SEG_CH - 1), end16 = min(s16 + SEG_CH, (long)n);
-      const int ls = (int)(s16 - e0), le = (int)(end16 - e0);
-      const uint32_t key = sk[i + 1];
-      if (e == end16 - 1 || sk[i + 2] != key) {
-        const bool cont_head = s16 > 0 && sk[ls + 1] == sk[ls];
-        const bool first = key == sk[ls + 1];
-        const bool cont_tail = end16 < n && sk[le + 1] == sk[le];
-        const int kind = (first && cont_head) ? 2 : (e == end16 - 1 && cont_tail) ? 3 : key >= (uint32_t)J.n_out ? 4
-                       : (int)key != J.skip_key ? 1 : 5;
-        kq = (kind << 28) | (kind == 1 ? (int)key : (int)(e / SEG_CH));
-      }
-    }
-    sa[i] = a;
-    sb[i] = b;
-    sp[i] = bin;
-    sq[i] = kq;
-    sr[i] = r;
-  }
-  for (int i = threadIdx.x; i < (n_pos + 1) * 256; i += 256) bins[i] = 0.f;
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int col = blockIdx.y * 256 + 64 * w + lane;
-  if (col < d) {  // wave-uniform (d % 64 == 0)
-    const RowSrc& src = J.src;
-    const auto ra = fused_rsrc(src.gX, rows_a * d * 4);
-    const auto rb = fused_rsrc(MAPPED ? src.gX2 : src.gX, rows_b * d * 4);
-    const auto ro = fused_rsrc(OUT16 ? (const void*)J.out16 : (const void*)J.out, (long)J.n_out * d * (OUT16 ? 2 : 4));
-    const int cb = col * 4;
-    float* bcol = bins + 64 * w + lane;
-    float acc = 0.f;
-    for (int h0 = 0; h0 < cnt; h0 += FU) {
-      float xa[FU], xb[FU], pv[FU];
-      // the batch's per-entry constants: lane u reads entry h0 + u's (one LDS round trip), each is then broadcast
-      // to the wave by readlane (scalar)
-      const int li = min(h0 + (lane & (FU - 1)), cnt - 1);
-      const int va = sa[li], vb = sb[li], vp = sp[li], vq = sq[li], vr = sr[li];
-#pragma unroll
-      for (int u = 0; u < FU; ++u) {  // every load issued before any is used; absent rows read 0 (no traffic)
-        const int a = __builtin_amdgcn_readlane(va, u);
-        xa[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra, a >= 0 ? a * d * 4 + cb : 0x7ffffff0, 0, 0));
-        if constexpr (MAPPED) {
-          const int b = __builtin_amdgcn_readlane(vb, u);
-          xb[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, b >= 0 ? b * d * 4 + cb : 0x7ffffff0, 0, 0));
-        }
-        const int kq = __builtin_amdgcn_readlane(vq, u);
-        const int ooff = (kq >> 28) == 1 && h0 + u < cnt ? (kq & 0x0fffffff) * d * (OUT16 ? 2 : 4) + col * (OUT16 ? 2 : 4)
-                                                         : 0x7ffffff0;
-        if constexpr (OUT16) {
-          const unsigned short h = __builtin_amdgcn_raw_buffer_load_b16(ro, ooff, 0, 0);
-          pv[u] = (float)__builtin_bit_cast(c2::tbf16, h);
-        } else {
-          pv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ro, ooff, 0, 0));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < FU; ++u) {
-        const int i = h0 + u;
-        if (i < cnt) {  // uniform
-          float v = xa[u];
-          if constexpr (MAPPED) {
-            if (__builtin_amdgcn_readlane(vb, u) >= 0) v = v + xb[u];
-          }
-          if (src.drop.active())
-            v = v * src.drop.mul((uint64_t)(src.idx_base + __builtin_amdgcn_readlane(vr, u)) * d + col);
-          atomicAdd(bcol + __builtin_amdgcn_readlane(vp, u) * 256, v);
-          acc = acc + src.scale * v;
-          const int kq = __builtin_amdgcn_readlane(vq, u);
-          const int kind = kq >> 28;
-          if (kind) {
-            const long slot = (long)(kq & 0x0fffffff) * d + col;
-            if (kind == 1) {
-              if constexpr (OUT16) J.out16[slot] = (c2::tbf16)(pv[u] + acc);
-              else J.out[slot] = pv[u] + acc;
-            } else if (kind == 2) {
-              J.ph[slot] = acc;
-            } else if (kind == 3) {
-              J.pt[slot] = acc;
-            } else if (kind == 4 && lane == 0) {
-              atomicOr(J.err, 2);
-            }
-            acc = 0.f;
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < n_pos * 256; i += 256) {
-    const int c = blockIdx.y * 256 + (i & 255);
-    if (c < d) ppart[((long)blockIdx.x * n_pos + (i >> 8)) * d + c] = bins[i];
-  }
-}
-
 // plan: sub-ranges of every split.  One workgroup: per-thread runs of splits, block scan of their
 // sub counts → suboff[nsplit + 1], subs[total] = (split, first piece), counts[2] = total; the
 // error word starts at 0.
@@ -947,17 +799,6 @@ SegJob seg_job(const Plan& p, int n, int n_out, const RowSrc& src, float* out, c
   return j;
 }
 
-// pass B of one job (the item sums after seg_fused_kernel)
-template <int LPR>
-void seg_pass_b(const SegJob& j, hipStream_t s) {
-  constexpr int GROUPS = 256 / LPR;
-  if (j.n <= SEG_CH) return;
-  dim3 g1(std::max(1, std::min(max_subs(j.n), 2 * num_cus())), 1);
-  seg_split1_kernel<LPR><<<g1, 1024, (size_t)(1024 / LPR) * j.src.d * 4, s>>>(j, j);
-  dim3 g2(std::max(1, std::min(c2::ceil_div(c2::ceil_div(j.n, SEG_CH), GROUPS), 2 * num_cus())), 1);
-  seg_split2_kernel<LPR><<<g2, 256, 0, s>>>(j, j);
-}
-
 // one or two jobs of the same row width in one launch per pass
 void seg_dispatch(const SegJob& j0, const SegJob* j1, hipStream_t s) {
   const SegJob& b = j1 ? *j1 : j0;
@@ -1059,52 +900,6 @@ static int embed_bwd_planned_impl(const void* seq_plan, const void* pos_plan, in
   }
   C2_CHECK_LAUNCH();
   return 0;
-}
-
-// ---- fused form: item sums over the item plan + position sums from the same row reads (seg_fused_kernel)
-extern "C" int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
-
-C2_API int c2dsr_embed_bwd_fused_supported(int n_rows, int d, int n_items, int n_pos) {
-  return d % 64 == 0 && n_pos > 0 && n_pos <= 56 && (long)n_items * d * 4 < (1L << 31) &&
-         (long)n_rows * d * 4 < (1L << 31);
-}
-
-C2_API size_t c2dsr_embed_bwd_fused_workspace(int n_rows, int d, int n_pos) {
-  return seg_ws_bytes(n_rows, d) + align256((size_t)c2::ceil_div(n_rows, FE) * n_pos * d * 4);
-}
-
-C2_API int c2dsr_embed_bwd_fused(const void* seq_plan, const int64_t* pos, int n_rows, int d, const float* gXa,
-                                 int rows_a, const int* inv_a, const float* gXb, int rows_b, const int* inv_b, uint32_t k0,
-                                 uint32_t k1, float p, int64_t idx_base, float scale, float* G, int n_items, float* gP,
-                                 int n_pos, void* workspace, size_t ws_bytes, void* stream) {
-  if (n_rows == 0) return 0;
-  const bool mapped = inv_a != nullptr;
-  if (!mapped) rows_a = rows_b = n_rows;
-  if (!c2dsr_embed_bwd_fused_supported(n_rows, d, n_items, n_pos) || !seq_plan || !pos || !G || !gP || !gXa ||
-      (long)rows_a * d * 4 >= (1L << 31) || (long)rows_b * d * 4 >= (1L << 31) ||
-      mapped != (inv_b != nullptr) || mapped != (gXb != nullptr) ||
-      ws_bytes < c2dsr_embed_bwd_fused_workspace(n_rows, d, n_pos))
-    return (int)hipErrorInvalidValue;
-  hipStream_t s = (hipStream_t)stream;
-  char* ws = (char*)workspace;
-  const SegJob j = seg_job(plan_view(seq_plan, n_rows), n_rows, n_items,
-                           RowSrc{gXa, d, c2::make_drop(k0, k1, p), idx_base, scale, nullptr, inv_a, inv_b, gXb}, G, ws,
-                           -1);
-  float* ppart = (float*)(ws + seg_ws_bytes(n_rows, d));
-  const int nch = c2::ceil_div(n_rows, FE);
-  const dim3 grid(nch, c2::ceil_div(d, 256));
-  const size_t shm = (size_t)(n_pos + 1) * 256 * 4;
-  if (mapped)
-    seg_fused_kernel<true, false><<<grid, 256, shm, s>>>(j, pos, n_pos, rows_a, rows_b, ppart);
-  else
-    seg_fused_kernel<false, false><<<grid, 256, shm, s>>>(j, pos, n_pos, rows_a, rows_b, ppart);
-  switch (lpr_for(d)) {
-    case 64: seg_pass_b<64>(j, s); break;
-    case 32: seg_pass_b<32>(j, s); break;
-    default: seg_pass_b<16>(j, s); break;
-  }
-  C2_CHECK_LAUNCH();
-  return c2dsr_sum_parts(ppart, nch, (long)n_pos * d, 1.0f, gP, stream);
 }
 
 C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,

@@ -356,6 +356,9 @@ __device__ __forceinline__ void x3_acc(f32x4& acc, const bf16x8& wh, const bf16x
       : "a"(wh), "a"(wl), "v"(ah), "v"(al));
 }
 
+#ifndef RG3_NW
+#define RG3_NW 4  // waves per workgroup of the split-bf16 row-streaming GEMM
+#endif
 #ifdef RG3_STAMP  // diagnostic build only: per-phase cycle sums of the rg3 chunk loop (tools/rg_micro.py prints them)
 __device__ unsigned long long rg3_stamp_acc[8];
 #define RSTAMP(i)                                                  \
@@ -377,15 +380,22 @@ __device__ unsigned long long rg3_stamp_acc[8];
 // 2^-15·‖a‖‖w‖ — is listed (r·N + c) and recomputed exactly by guard_fix_kernel: the ReLU's sign decisions, which
 // select the dy·x terms of the weight gradient, are those of an fp32 product (tools/fp32_diag.py).  ‖a_r‖² is summed
 // while a chunk is staged (a wave holds whole rows at K = 256), ‖w_c‖² comes from the caller (ep.wn2).
-template <int KCH, bool EPI, int AUX, bool GUARD = false>
-__global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* __restrict__ A, long lda,
-                                                     const bf16* __restrict__ B, long ldb, float* C, long ldc, Epi2 ep,
-                                                     int G) {
-  static_assert(!GUARD || (EPI && KCH == 1 && AUX == AUX_NONE), "guarded ReLU: the K = 256 relu·dropout epilogue");
+// NW: waves per workgroup — 4 (one per SIMD, 64 columns × K hi + lo = 256 AGPRs each) or 8 (two per SIMD, half the
+// columns each: one wave's staging / epilogue / barrier waits run under the other's MFMAs).  The workgroup covers the
+// same 256 / KCH columns either way; every output element's accumulation order is the same.
+template <int KCH, bool EPI, int AUX, bool GUARD = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const float* __restrict__ A, long lda,
+                                                         const bf16* __restrict__ B, long ldb, float* C, long ldc,
+                                                         Epi2 ep, int G) {
+  static_assert(!GUARD || (EPI && KCH == 1 && AUX == AUX_NONE && NW == 4),
+                "guarded ReLU: the K = 256 relu·dropout epilogue, 4 waves");
+  static_assert(NW == 4 || NW == 8, "rg3 waves");
   constexpr int K = 256 * KCH;
-  constexpr int NCB = 4 / KCH;      // 16-column blocks per wave
+  constexpr int NCB = 16 / NW / KCH;  // 16-column blocks per wave
   constexpr int CW = 16 * NCB;      // columns per wave
-  constexpr int WGC = 4 * CW;       // columns per workgroup
+  constexpr int WGC = NW * CW;      // columns per workgroup
+  constexpr int SPU = 32 / NW;      // rows of a chunk each thread stages (float4 per thread per chunk)
+  constexpr int RA = NW == 4 ? 3 : 2;  // chunks loaded ahead (register sets): 3 at one wave per SIMD, 2 at two
   constexpr int IMGB = 32 * 256 * 2;  // bytes of one [32][256] bf16 image
   constexpr int NST = 16;           // MFMA steps per chunk: (k-step ks, row block rb)
   __shared__ __attribute__((aligned(16))) char aimg[2][2 * IMGB];  // [buffer][hi | lo]
@@ -417,22 +427,22 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
 #pragma unroll
     for (int c = 0; c < 4; ++c) roff[c] = (int)lds_addr(aimg[0]) + l16 * 256 + 16 * ((4 * c + g) ^ sw);
   }
-  // staging: thread t converts the float4 of row lrow + 4u (u < 8), columns 4·lane .. +3 of a chunk
+  // staging: thread t converts the float4 of row lrow + NW·u (u < SPU), columns 4·lane .. +3 of a chunk
   const int lrow = threadIdx.x >> 6;
-  int soff[8];
+  int soff[SPU];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int row = lrow + 4 * u, k = 4 * lane;
+  for (int u = 0; u < SPU; ++u) {
+    const int row = lrow + NW * u, k = 4 * lane;
     soff[u] = (int)lds_addr(aimg[0]) + (k >> 7) * (32 * 256) + row * 256 + 16 * (((k & 127) >> 3) ^ swz16(row)) +
               2 * (k & 7);
   }
   const int ldab = (int)lda * 4;
-  auto load = [&](int c, float4 (&P)[8]) {
+  auto load = [&](int c, float4 (&P)[SPU]) {
     const int tile = min(c / KCH, ntile - 1), kc = c % KCH;
     const int vo = ((rt0 + tile * rts) * 32 + lrow) * ldab + (kc * 256 + 4 * lane) * 4;
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      P[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc, vo + u * 4 * ldab, 0, 0));
+    for (int u = 0; u < SPU; ++u)
+      P[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(asrc, vo + u * NW * ldab, 0, 0));
   };
   typedef __attribute__((address_space(3))) bf16x4 lds4;
   auto stage1 = [&](const float4& v, int u, int buf) {
@@ -452,7 +462,7 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
       x = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
       const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
       x = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
-      if (lane == 0) rn2s[buf][lrow + 4 * u] = x;
+      if (lane == 0) rn2s[buf][lrow + NW * u] = x;
     }
   };
   // aux / row maps of the current tile (loaded at its first chunk, used by its epilogue)
@@ -529,10 +539,10 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
       }
     }
   };
-  float4 Pa[8], Pb[8], Pc[8];
+  float4 Pa[SPU], Pb[SPU], Pc[RA == 3 ? SPU : 1];
   load(0, Pa);
   load(1, Pb);
-  load(2, Pc);
+  if constexpr (RA == 3) load(2, Pc);
   // the weight fragments are fetched (L2) while the first A chunks are in flight (HBM)
   // B (split image) fragments → AGPRs: column ncol0 + 16cb + l16, k = 32ks + 8g
 #pragma unroll
@@ -549,14 +559,14 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
   if constexpr (GUARD) wn2s[threadIdx.x] = ep.wn2[min(gcol * WGC + (int)threadIdx.x, N - 1)];
   vm_drain();
 #pragma unroll
-  for (int u = 0; u < 8; ++u) stage1(Pa[u], u, 0);
+  for (int u = 0; u < SPU; ++u) stage1(Pa[u], u, 0);
   pre_tile(0);
   __syncthreads();
   RSTAMP(0);
   // chunk c (k-chunk KC): MFMAs on image c&1 ∥ split of chunk c+1 (registers S) into image (c+1)&1; R is
   // refilled with chunk c+3 first (three register sets: a staged chunk was loaded two steps earlier)
-  auto step = [&]<int KC>(int c, float4 (&R)[8], float4 (&S)[8]) {
-    load(c + 3, R);
+  auto step = [&]<int KC>(int c, float4 (&R)[SPU], float4 (&S)[SPU]) {
+    load(c + RA, R);
     const int buf = c & 1, nb = (c + 1) & 1;
     const int tile = c / KCH;
     bf16x8 fr[4][2];
@@ -580,7 +590,7 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
               else
                 x3_acc(acc[rb][cb], wh[cb][KC * 8 + ks], wl[cb][KC * 8 + ks], fr[st & 3][0], fr[st & 3][1]);
             }
-            if constexpr (st % 2 == 1) stage1(S[st >> 1], st >> 1, nb);
+            if constexpr (st % (NST / SPU) == NST / SPU - 1) stage1(S[st / (NST / SPU)], st / (NST / SPU), nb);
             __builtin_amdgcn_sched_barrier(0);
           }(),
           ...);
@@ -595,6 +605,13 @@ __global__ __launch_bounds__(256, 1) void rg3_kernel(int M, int N, const float* 
     RSTAMP(3);
   };
   const int nchunk = ntile * KCH;
+  if constexpr (RA == 2) {
+    for (int c0 = 0; c0 < nchunk; c0 += 2) {  // register sets and k-chunks both rotate with period 2
+      step.template operator()<0>(c0, Pa, Pb);
+      if (c0 + 1 >= nchunk) break;
+      step.template operator()<1 % KCH>(c0 + 1, Pb, Pa);
+    }
+  } else
   for (int c0 = 0; c0 < nchunk; c0 += 6) {  // register sets rotate with period 3, k-chunks with period KCH
     step.template operator()<0>(c0, Pa, Pb);
     if (c0 + 1 >= nchunk) break;
@@ -1008,17 +1025,17 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
                        int slot) -> int {
       if (!per_cu[slot]) {
         int n = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kern, 256, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kern, 64 * RG3_NW, 0);
         per_cu[slot] = n > 0 ? n : 1;
       }
       const int blocks = (ncu * per_cu[slot] / 8) * 8;
       if (blocks / 8 < G3) return (int)hipErrorInvalidValue;
-      kern<<<blocks, 256, 0, s>>>(M, N, (const float*)A, lda, (const bf16*)B, ldb, C, ldc, ep, G3);
+      kern<<<blocks, 64 * RG3_NW, 0, s>>>(M, N, (const float*)A, lda, (const bf16*)B, ldb, C, ldc, ep, G3);
       return 0;
     };
     const bool k1 = K == 256;
-#define RG3(E, X) (k1 ? launch3(rg3_kernel<1, E, X>, 31 + 2 * (X) + (E ? 8 : 0)) \
-                      : launch3(rg3_kernel<2, E, X>, 32 + 2 * (X) + (E ? 8 : 0)))
+#define RG3(E, X) (k1 ? launch3(rg3_kernel<1, E, X, false, RG3_NW>, 31 + 2 * (X) + (E ? 8 : 0)) \
+                      : launch3(rg3_kernel<2, E, X, false, RG3_NW>, 32 + 2 * (X) + (E ? 8 : 0)))
     if (e && aux_mode == AUX_NONE)
       rc = RG3(true, AUX_NONE);
     else if (aux_mode == AUX_ACC)

@@ -844,16 +844,6 @@ def index_plans(state, pairs):
 
 
 # ----------------------------------------------------------------------------- embedding fuse (K2)
-EMBED_FUSED = False  # item and position sums from one read of each gradient row (c2dsr_embed_bwd_fused)
-
-
-def embed_fused_ok(n_rows, d, n_items, n_pos):
-    """The embedding backward's one-read form applies (row width a multiple of 64, n_pos position bins in LDS);
-    its position sums need no position plan."""
-    return EMBED_FUSED and bool(lib.raw('c2dsr_embed_bwd_fused_supported')(int(n_rows), int(d), int(n_items),
-                                                                           int(n_pos)))
-
-
 class EmbedFn(Function):
     """x = drop((H[seq] + E[seq])·√d + P[pos])  (models/C2DSR.py:65-71 + encoders.py:30-31)."""
 
@@ -889,29 +879,11 @@ class EmbedFn(Function):
         if gP is None and ctx.needs_input_grad[2]:
             gP_ret = torch.zeros_like(ctx.P)
             gP = gP_ret
-        fused = (G is not None and gP is not None and ctx.plans is not None
-                 and embed_fused_ok(n, d, ctx.n_items, ctx.P.shape[0]))
         if ctx.plans is not None:
             state, on_seq, n_seq, on_pos, n_pos = ctx.plans
             ctx.plans = (index_plan(state, seq, n_seq) if on_seq else None,
-                         index_plan(state, pos, n_pos) if on_pos and not fused else None)
+                         index_plan(state, pos, n_pos) if on_pos else None)
         parts = ctx.link.take() if ctx.link is not None else None  # gx is a placeholder then (RowsGrad)
-        if fused and ctx.plans[0] is not None:  # one read of each gradient row for both sums
-            sp = ctx.plans[0].get()
-            ws_bytes = int(lib.raw('c2dsr_embed_bwd_fused_workspace')(n, d, ctx.P.shape[0]))
-            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=G.device)
-            if parts is not None:
-                if len(ROW_COUNT) > 256:
-                    ROW_COUNT.clear()
-                ROW_COUNT[parts[0].data_ptr()], ROW_COUNT[parts[2].data_ptr()] = parts[0].shape[0], parts[2].shape[0]
-                src = (parts[0], parts[0].shape[0], parts[1], parts[2], parts[2].shape[0], parts[3])
-            else:
-                src = (gx.contiguous(), n, None, None, n, None)
-            lib('c2dsr_embed_bwd_fused', sp, pos, n, d, *src, ctx.keys[0], ctx.keys[1], float(ctx.p),
-                int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], ws, ws_bytes, stream())
-            if _CHECK_PLANS or _CHECK_ERR:
-                _check_err(sp, int(lib.raw('c2dsr_plan_err_offset')(n)), 'c2dsr_embed_bwd_fused')
-            return EmbedFn._done(ctx, seq, gP_ret)
         planned = (ctx.plans is not None and (G is None or ctx.plans[0] is not None)
                    and (gP is None or ctx.plans[1] is not None))
         if parts is not None and not planned:

@@ -318,10 +318,8 @@ class Trainer(object):
             # after its first long CE launch: ~110 small launches the host issues while the device is busy,
             # instead of ahead of the encoder passes, whose first kernels would wait behind them
             st = m.state
-            # (the one-read embedding backward needs no position plans: ops.embed_fused_ok)
-            with_pos = not ops.embed_fused_ok(B * L, self.d_latent, m.n_item, m.attn_share.len_max)
             pairs = [pr for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b), (neg_a, pos), (neg_b, pos))
-                     for pr in ((sq, m.n_item),) + (((ps, m.attn_share.len_max),) if with_pos else ())]
+                     for pr in ((sq, m.n_item), (ps, m.attn_share.len_max))]
             plans = lambda: ops.index_plans(st, pairs)  # noqa: E731
         m.state.need, m.state.pad_rows, m.state.compact_out = need, pads, bool(need)
         try:

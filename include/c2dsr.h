@@ -82,18 +82,6 @@ int c2dsr_embed_bwd_planned_rows(const void* seq_plan, const void* pos_plan, int
                                  const int* inv_a, const float* gXb, const int* inv_b, uint32_t k0, uint32_t k1,
                                  float p, int64_t idx_base, float scale, float* G, int n_items, float* gP, int n_pos,
                                  void* workspace, size_t ws_bytes, void* stream);
-/* The same sums from ONE read of each gradient row (replaces models/C2DSR.py:65-71 / encoders.py:30 embedding
- * backward, like c2dsr_embed_bwd_planned): the item sums over the item plan (bit-identical to the planned form),
- * the position sums gP[pos[r]] += drop(row r) from the same reads (pos: the [n_rows] int64 position indices, no
- * position plan; fixed summation order).  Rows as c2dsr_embed_bwd_planned (gXb / inv_a / inv_b null) or as the
- * two compact sources of c2dsr_embed_bwd_planned_rows (rows_a / rows_b: their row counts).  d % 64 == 0, n_pos <= 56
- * (c2dsr_embed_bwd_fused_supported). */
-int c2dsr_embed_bwd_fused_supported(int n_rows, int d, int n_items, int n_pos);
-size_t c2dsr_embed_bwd_fused_workspace(int n_rows, int d, int n_pos);
-int c2dsr_embed_bwd_fused(const void* seq_plan, const int64_t* pos, int n_rows, int d, const float* gXa, int rows_a,
-                          const int* inv_a, const float* gXb, int rows_b, const int* inv_b, uint32_t k0, uint32_t k1,
-                          float p, int64_t idx_base, float scale, float* G, int n_items, float* gP, int n_pos,
-                          void* workspace, size_t ws_bytes, void* stream);
 /* Deterministic (radix-sort + ordered segment sum) backward of the above
  * (replaces embedding_dense_backward):  G[seq[r]] += scale·drop(gX[r]);
  * gP[pos[r]] += drop(gX[r]);  gXin[r] = drop(gX[r]).  Null outputs are skipped. */

@@ -188,24 +188,6 @@ def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
                     n_items, gP3, L, None, ws, ws_b, stream())
             res.append((G3, gP3))
         assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
-        # the one-read form (c2dsr_embed_bwd_fused: item sums over the item plan, position sums from the same row
-        # reads): item sums bit-identical to the planned form, position sums to float64 at 1e-5, reproducible
-        assert lib.raw('c2dsr_embed_bwd_fused_supported')(n_rows, d, n_items, L)
-        fb = lib.raw('c2dsr_embed_bwd_fused_workspace')(n_rows, d, L)
-        fws = torch.empty(fb, dtype=torch.uint8, device=DEV)
-        fused = []
-        for rows in (False, True, True):
-            G4, gP4 = torch.zeros(n_items, d, device=DEV), torch.zeros(L, d, device=DEV)
-            src = (ga, ga.shape[0], ia, gb, gb.shape[0], ib) if rows else (gfull, n_rows, None, None, n_rows, None)
-            lib('c2dsr_embed_bwd_fused', sp.get(), pd, n_rows, d, *src, keys[0], keys[1], p, 77, scale, G4, n_items,
-                gP4, L, fws, fb, stream())
-            fused.append((G4, gP4))
-        assert torch.equal(fused[0][0], res[0][0]) and torch.equal(fused[1][0], res[0][0])
-        gf = gfull.cpu() * mk
-        Pr2 = torch.zeros(L, d, dtype=torch.float64).index_add_(0, torch.from_numpy(pos), gf.double())
-        assert rel(fused[0][1], Pr2) < 1e-5 and rel(fused[1][1], Pr2) < 1e-5
-        assert torch.equal(fused[1][1], fused[2][1]) and torch.equal(fused[1][0], fused[2][0])
-        assert int(sp.get()[off:off + 4].view(torch.int32).item()) == 0
 
 
 def _tail_of_segment(t):

@@ -53,10 +53,6 @@ def main():
         lib('c2dsr_embed_bwd_planned', spb if g is not None else None, ppb if p is not None else None, n_rows, d, gX,
             0, 0, 0.0, 0, 1.0, g, N, p, L, None, ws, wsb, s)
 
-    fb = int(lib.raw('c2dsr_embed_bwd_fused_workspace')(n_rows, d, L))
-    fws = torch.empty(fb, dtype=torch.uint8, device=dev)
-    t_f = timeit(lambda: lib('c2dsr_embed_bwd_fused', spb, pd, n_rows, d, gX, n_rows, None, None, n_rows, None, 0, 0,
-                             0.0, 0, 1.0, G, N, gP, L, fws, fb, s))
     t_g = timeit(lambda: run(G, None))
     t_p = timeit(lambda: run(None, gP))
     t_b = timeit(lambda: run(G, gP))
@@ -65,8 +61,7 @@ def main():
     t_plan = timeit(lambda: lib('c2dsr_index_plan', sd, n_rows, N, buf, pb, s))
     byt = n_rows * (16 + 4 * d) + 8 * d * uniq
     print(f'rows {n_rows} uniq {uniq}: G-only {t_g:.1f} us, gP-only {t_p:.1f} us, both {t_b:.1f} us '
-          f'({byt / (t_b * 1e-6) / 1e9:.0f} GB/s credited), fused one-read {t_f:.1f} us '
-          f'({byt / (t_f * 1e-6) / 1e9:.0f} GB/s credited), seq plan build {t_plan:.1f} us', flush=True)
+          f'({byt / (t_b * 1e-6) / 1e9:.0f} GB/s credited), seq plan build {t_plan:.1f} us', flush=True)
 
 
 if __name__ == '__main__':
