@@ -357,7 +357,7 @@ __device__ __forceinline__ void x3_acc(f32x4& acc, const bf16x8& wh, const bf16x
 }
 
 #ifndef RG3_NW
-#define RG3_NW 4  // waves per workgroup of the split-bf16 row-streaming GEMM
+#define RG3_NW 8  // waves per workgroup of the split-bf16 row-streaming GEMM (8: 2 per SIMD, measured 5-13% over 4 at N=256)
 #endif
 #ifdef RG3_STAMP  // diagnostic build only: per-phase cycle sums of the rg3 chunk loop (tools/rg_micro.py prints them)
 __device__ unsigned long long rg3_stamp_acc[8];
