@@ -54,6 +54,12 @@
 #ifndef CE3B_ILV
 #define CE3B_ILV 1
 #endif
+#ifndef CE3_NW  // waves per workgroup (4: one per SIMD; 8: two per SIMD, one stationary block each)
+#define CE3_NW 4
+#endif
+#ifndef CE3B_NW
+#define CE3B_NW 4
+#endif
 #ifndef CE3_DQ
 #define CE3_DQ 2
 #endif
@@ -208,8 +214,11 @@ __device__ __forceinline__ void step_pattern() {
 template <bool SPLIT>
 constexpr int tile_rows() { return SPLIT ? 32 : 64; }
 
-template <int D, int MODE, bool SPLIT>
-__global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs, const bf16* __restrict__ Xw,
+// NW: waves per workgroup — 4 (one per SIMD, two 16-row stationary blocks each) or 8 (two per SIMD, one block each:
+// half the registers, so one wave's LDS waits, epilogue VALU and barrier run under its partner's MFMAs).  The
+// workgroup covers the same 128 stationary rows either way and every accumulation order is the same.
+template <int D, int MODE, bool SPLIT, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict__ Xs, const bf16* __restrict__ Xw,
                                                       const float* __restrict__ svec, const float* __restrict__ wvec,
                                                       int n_s, int n_w, int per_split, float* __restrict__ part_m,
                                                       float* __restrict__ part_s, float* __restrict__ outp,
@@ -224,43 +233,47 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
   constexpr int D2 = SPLIT ? 2 * D : D;            // image columns (hi ‖ lo, or bf16)
   constexpr int IMG = T3 * D2 * 2;                 // bytes per image
   constexpr int HT = T3 * 256;                     // bytes per 128-column half-tile
-  constexpr int NDMA = (T3 / 4) * (D2 / 128) / 4;  // LDS-DMA wave-instructions per wave per tile
+  constexpr int SBW = 8 / NW;                      // 16-row stationary blocks per wave
+  constexpr int NDMA = (T3 / 4) * (D2 / 128) / NW;  // LDS-DMA wave-instructions per wave per tile
   constexpr int NB = 4;
   constexpr int DS = SPLIT ? CE3_DS : CE3B_DS, DT = SPLIT ? CE3_DT : CE3B_DT;
-  constexpr int NEL = 8 * CB;                      // S values per lane per tile (2 stationary blocks × CB)
-  constexpr int EPK = NEL / NSS;                   // epilogue elements per S step
-  constexpr int MPK = NEL / NUS;                   // prep elements per second-product step
+  constexpr int NEL = 4 * SBW * CB;                // S values per lane per tile (SBW stationary blocks × CB)
   constexpr float TAU = 8.f;
-  static_assert(NSS * EPK == NEL && NUS * MPK == NEL && EPK <= 8 && 8 % EPK == 0 && DS <= NUS && DT <= NSS,
-                "tile / wave split");
+  static_assert((NW == 4 || NW == 8) && NDMA * NW == (T3 / 4) * (D2 / 128) && NEL % 8 == 0 && DS <= NUS &&
+                    DT <= NSS, "tile / wave split");
   // one LDS-DMA wave-instruction of tile t+3 every DQ second-product steps, from the first (DQ = 1: the whole
   // tile at the start of the phase, the longest time to land before the barrier that publishes it)
   constexpr int DQ = SPLIT ? CE3_DQ : CE3B_DQ;
   constexpr bool ILV = SPLIT ? CE3_ILV : CE3B_ILV;
   static_assert(DQ >= 1 && DQ * NDMA <= NUS, "DMA spacing");
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
-  __shared__ __attribute__((aligned(16))) float wv[NB][4][64];
+  __shared__ __attribute__((aligned(16))) float wv[NB][NW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
   // XCD-aware work map: block b runs on XCD b % 8; the (split, row block) pairs, split-major, are dealt to the XCDs in
   // contiguous ranges, so each split's swept slice streams through the L2 of one or two XCDs instead of all eight
   const int nrb = (n_s + 127) >> 7, nb = (int)gridDim.x;
   const int pidx = nb % 8 == 0 ? (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   const int split = pidx / nrb, rblk = pidx % nrb;
-  const int s0 = rblk * 128 + w * 32 + l16;  // stationary rows s0 (sb 0), s0 + 16 (sb 1)
+  const int s0 = rblk * 128 + w * 16 * SBW + l16;  // stationary rows s0 + 16·sb, sb < SBW
   const int w_beg = split * per_split;
   const int w_end = min(n_w, w_beg + per_split);
   const int ntiles = w_end > w_beg ? (w_end - w_beg + T3 - 1) / T3 : 0;
-  f32x4 dacc[NE][2];
+  f32x4 dacc[NE][SBW];
+  float mrow[SBW], zrow[SBW];
 #pragma unroll
-  for (int e = 0; e < NE; ++e) dacc[e][0] = dacc[e][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float mrow[2] = {-INFINITY, -INFINITY}, zrow[2] = {0.f, 0.f};
+  for (int sb = 0; sb < SBW; ++sb) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) dacc[e][sb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mrow[sb] = -INFINITY;
+    zrow[sb] = 0.f;
+  }
   if (ntiles > 0) {
     const int w_last = w_beg + (ntiles - 1) * T3;
     const int ib = (int)lds_addr(img[0]);
     unsigned dvoff[NDMA], ddst[NDMA];
 #pragma unroll
     for (int i = 0; i < NDMA; ++i) {
-      const int q = w + 4 * i;
+      const int q = w + NW * i;
       constexpr int GROUPS = T3 / 4;
       const int half = q / GROUPS, rg = q % GROUPS;
       const int row = rg * 4 + (lane >> 4);
@@ -287,9 +300,9 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
 #pragma unroll
       for (int v = 0; v < 8; ++v) toff0[v] = trow * 256 + 16 * ((2 * v + (p >> 1)) ^ ft) + 8 * (p & 1);
     }
-    bf16x8 fh[2][KS], fl[2][KS];
+    bf16x8 fh[SBW][KS], fl[SBW][KS];
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
+    for (int sb = 0; sb < SBW; ++sb) {
       const long sr = min(s0 + 16 * sb, n_s - 1);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -297,11 +310,9 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
         if constexpr (SPLIT) fl[sb][ks] = *(const bf16x8*)(Xs + sr * D2 + D + ks * 32 + 8 * g);
       }
     }
-    float b2s[2] = {0.f, 0.f};
-    if constexpr (MODE == 1) {
-      b2s[0] = svec[s0];
-      b2s[1] = svec[s0 + 16];
-    }
+    float b2s[SBW];
+#pragma unroll
+    for (int sb = 0; sb < SBW; ++sb) b2s[sb] = MODE == 1 ? svec[s0 + 16 * sb] : 0.f;
     dma(0);
     dma(1);
     dma(2);
@@ -365,9 +376,10 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
         ((c4[C] = lds_ld<f32x4, 64 * C>(bo)), ...);
       }(std::make_integer_sequence<int, CB>{});
     };
-    // epilogue element i (0 .. NEL-1) ↔ (sb = i / 4CB, cb = (i / 4) % CB, r = i % 4) = accumulator (cb·2 + sb)[r];
-    // the second product's B fragment (u, sb) packs elements of cb = 2u, 2u + 1 (8-element chunk sb·UK + u)
-    f32x4 sc[2 * CB];
+    // epilogue element i (0 .. NEL-1) ↔ (sb = i / 4CB, cb = (i / 4) % CB, r = i % 4) = accumulator (cb·SBW + sb)[r];
+    // the second product's B fragment (u, sb) packs elements of cb = 2u, 2u + 1 (8-element chunk sb·UK + u).
+    // Step k of a phase with NST steps handles elements [⌈k·NEL/NST⌉, ⌈(k+1)·NEL/NST⌉)
+    f32x4 sc[SBW * CB];
     {
       Offs oS;
       offs_rows(0, oS);
@@ -378,28 +390,30 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
               bf16x8 a[2];
               s_frags.template operator()<K>(oS, a);
 #pragma unroll
-              for (int sb = 0; sb < 2; ++sb) s_prod.template operator()<K / CB>(sc[cb * 2 + sb], a, sb);
+              for (int sb = 0; sb < SBW; ++sb) s_prod.template operator()<K / CB>(sc[cb * SBW + sb], a, sb);
             }(),
             ...);
       }(std::make_integer_sequence<int, NSS>{});
     }
     mfma_drain();
-    float mnext[2] = {-INFINITY, -INFINITY};
+    float mnext[SBW];
     {
       f32x4 c4[CB];
       wconst(0, c4);
-      float tm[2] = {-INFINITY, -INFINITY};
+      float tm[SBW];
+#pragma unroll
+      for (int sb = 0; sb < SBW; ++sb) tm[sb] = mnext[sb] = -INFINITY;
 #pragma unroll
       for (int i = 0; i < NEL; ++i) {
         const int sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
-        float v = fmaf(sc[cb * 2 + sb][r], LOG2E, c4[cb][r]);
+        float v = fmaf(sc[cb * SBW + sb][r], LOG2E, c4[cb][r]);
         if constexpr (MODE == 1) v += b2s[sb];
-        sc[cb * 2 + sb][r] = v;
+        sc[cb * SBW + sb][r] = v;
         tm[sb] = fmaxf(tm[sb], v);
       }
       if constexpr (MODE == 0) {
-        mnext[0] = quad_max(tm[0]);
-        mnext[1] = quad_max(tm[1]);
+#pragma unroll
+        for (int sb = 0; sb < SBW; ++sb) mnext[sb] = quad_max(tm[sb]);
       }
     }
     bf16x8 fa[DS + 2][2];
@@ -421,10 +435,12 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       const bf16* nsrc = Xw + (long)rn * D2;
       const unsigned nbuf = ((t + 3) % NB) * IMG;
       dma4(wvec + rn + lane, wv[(t + 3) % NB][w]);
-      float msub[2] = {0.f, 0.f};
+      float msub[SBW];
+#pragma unroll
+      for (int sb = 0; sb < SBW; ++sb) msub[sb] = 0.f;
       if constexpr (MODE == 0) {
 #pragma unroll
-        for (int sb = 0; sb < 2; ++sb) {
+        for (int sb = 0; sb < SBW; ++sb) {
           const bool need = mnext[sb] > mrow[sb] + TAU;
           if (__builtin_amdgcn_ballot_w64(need)) [[unlikely]] {
             const float f = need ? ex2(mrow[sb] - mnext[sb]) : 1.f;
@@ -450,8 +466,8 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       offs_rows(bs, oS);
       offs_tr(bh, oH);
       // ---- S(t+1) ∥ epilogue(t)
-      f32x4 sn[2 * CB];
-      bf16x8 xh[UK][2], xl[UK][2];
+      f32x4 sn[SBW * CB];
+      bf16x8 xh[UK][SBW], xl[UK][SBW];
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
@@ -461,34 +477,34 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
               if constexpr (k + DT >= NSS) u_frags.template operator()<k + DT - NSS>(oH, tf[k + DT - NSS]);
               // ILV: the step's VALU work between its two stationary blocks' products (each MFMA's shadow
               // covers half of it; in-order issue otherwise stalls it behind the second MFMA)
-              s_prod.template operator()<k / CB>(sn[cb * 2], fa[k % (DS + 2)], 0);
-              if constexpr (ILV) __builtin_amdgcn_sched_barrier(0);
-              else s_prod.template operator()<k / CB>(sn[cb * 2 + 1], fa[k % (DS + 2)], 1);
+              s_prod.template operator()<k / CB>(sn[cb * SBW], fa[k % (DS + 2)], 0);
+              if constexpr (ILV || SBW == 1) __builtin_amdgcn_sched_barrier(0);
+              else s_prod.template operator()<k / CB>(sn[cb * SBW + 1], fa[k % (DS + 2)], 1);
+              constexpr int ib = (k * NEL + NSS - 1) / NSS, ie = ((k + 1) * NEL + NSS - 1) / NSS;
 #pragma unroll
-              for (int e = 0; e < EPK; ++e) {
-                constexpr int i0 = k * EPK;
-                const int i = i0 + e, sb = i / (4 * CB), cb2 = (i >> 2) % CB, r = i & 3;
-                const float pv = ex2(sc[cb2 * 2 + sb][r] - msub[sb]);
-                sc[cb2 * 2 + sb][r] = pv;
+              for (int i = ib; i < ie; ++i) {
+                const int sb = i / (4 * CB), cb2 = (i >> 2) % CB, r = i & 3;
+                const float pv = ex2(sc[cb2 * SBW + sb][r] - msub[sb]);
+                sc[cb2 * SBW + sb][r] = pv;
                 zrow[sb] += pv;
               }
-              if constexpr ((k * EPK + EPK) % 8 == 0) {
-                constexpr int c = (k * EPK) / 8, sb = c / UK, u = c % UK;
+              if constexpr (ie > ib && ie % 8 == 0) {
+                constexpr int c = ie / 8 - 1, sb = c / UK, u = c % UK;
                 bf16x8 h, l;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                  const float x = sc[(2 * u + (j >> 2)) * 2 + sb][j & 3];
+                  const float x = sc[(2 * u + (j >> 2)) * SBW + sb][j & 3];
                   h[j] = (bf16)x;
                   if constexpr (SPLIT) l[j] = (bf16)(x - (float)h[j]);
                 }
                 xh[u][sb] = h;
                 if constexpr (SPLIT) xl[u][sb] = l;
               }
-              if constexpr (ILV) {
+              if constexpr (ILV && SBW == 2) {
                 __builtin_amdgcn_sched_barrier(0);
-                s_prod.template operator()<k / CB>(sn[cb * 2 + 1], fa[k % (DS + 2)], 1);
+                s_prod.template operator()<k / CB>(sn[cb * SBW + 1], fa[k % (DS + 2)], 1);
               }
-              step_pattern<SPLIT ? 6 : 2, CE3_VN>();
+              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -504,7 +520,9 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
       offs_rows((t + 2) % NB, oN);
       f32x4 c4n[CB];
       wconst(bs, c4n);
-      float tm[2] = {-INFINITY, -INFINITY};
+      float tm[SBW];
+#pragma unroll
+      for (int sb = 0; sb < SBW; ++sb) tm[sb] = -INFINITY;
       [&]<int... Q>(std::integer_sequence<int, Q...>) {
         (
             [&] {
@@ -519,34 +537,34 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
                   mf1_u(dacc[q][sb], tq[0], xh[u][sb]);
               };
               u_prod(0);
-              if constexpr (ILV) __builtin_amdgcn_sched_barrier(0);
+              if constexpr (ILV || SBW == 1) __builtin_amdgcn_sched_barrier(0);
               else u_prod(1);
               if constexpr (k % DQ == DQ - 1 && k / DQ < NDMA)
                 dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
+              constexpr int ib = (k * NEL + NUS - 1) / NUS, ie = ((k + 1) * NEL + NUS - 1) / NUS;
 #pragma unroll
-              for (int e = 0; e < MPK; ++e) {
-                constexpr int i0 = k * MPK;
-                const int i = i0 + e, sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
-                float v = fmaf(sn[cb * 2 + sb][r], LOG2E, c4n[cb][r]);
+              for (int i = ib; i < ie; ++i) {
+                const int sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
+                float v = fmaf(sn[cb * SBW + sb][r], LOG2E, c4n[cb][r]);
                 if constexpr (MODE == 1) v += b2s[sb];
-                sn[cb * 2 + sb][r] = v;
+                sn[cb * SBW + sb][r] = v;
                 tm[sb] = fmaxf(tm[sb], v);
               }
-              if constexpr (ILV) {
+              if constexpr (ILV && SBW == 2) {
                 __builtin_amdgcn_sched_barrier(0);
                 u_prod(1);
               }
-              step_pattern<SPLIT ? 6 : 2, CE3_VN>();
+              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
       }(std::make_integer_sequence<int, NUS>{});
       if constexpr (MODE == 0) {
-        mnext[0] = quad_max(tm[0]);
-        mnext[1] = quad_max(tm[1]);
+#pragma unroll
+        for (int sb = 0; sb < SBW; ++sb) mnext[sb] = quad_max(tm[sb]);
       }
 #pragma unroll
-      for (int i = 0; i < 2 * CB; ++i) sc[i] = sn[i];
+      for (int i = 0; i < SBW * CB; ++i) sc[i] = sn[i];
       STAMP(4);
     }
 #ifdef CE3_STAMP
@@ -558,7 +576,7 @@ __global__ __launch_bounds__(256, 1) void ce3_kernel(const bf16* __restrict__ Xs
   }
   mfma_drain();
 #pragma unroll
-  for (int sb = 0; sb < 2; ++sb) {
+  for (int sb = 0; sb < SBW; ++sb) {
     const float ztot = quad_sum(zrow[sb]);
     const int s = s0 + 16 * sb;
     if (s < n_s) {
@@ -614,12 +632,13 @@ int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec
   if (nsplit < 1) return (int)hipErrorInvalidValue;
   const int per = per_split3(n_w, nsplit, tile_rows<SPLIT>());
   const dim3 grid(c2::ceil_div(n_s, 128) * nsplit);  // (row block, split) pairs: ce3_kernel's XCD-aware map
+  constexpr int NW = SPLIT ? CE3_NW : CE3B_NW;
   if (D == 128)
-    ce3_kernel<128, MODE, SPLIT><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm,
-                                                        ps, out, accum);
+    ce3_kernel<128, MODE, SPLIT, NW><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w,
+                                                                per, pm, ps, out, accum);
   else if (D == 256)
-    ce3_kernel<256, MODE, SPLIT><<<grid, 256, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w, per, pm,
-                                                        ps, out, accum);
+    ce3_kernel<256, MODE, SPLIT, NW><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w,
+                                                                per, pm, ps, out, accum);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
