@@ -60,6 +60,9 @@
 #ifndef CE3B_NW
 #define CE3B_NW 4
 #endif
+#ifndef CE3_PRIO
+#define CE3_PRIO 0
+#endif
 #ifndef CE3_DQ
 #define CE3_DQ 2
 #endif
@@ -428,6 +431,10 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
 #ifdef CE3_STAMP
     unsigned st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = (unsigned)__builtin_amdgcn_s_memtime();
 #endif
+    // CE3_PRIO (8 waves): static priority for the second-dispatched half, the arbitration loser of each SIMD pair
+    if constexpr (NW == 8 && CE3_PRIO) {
+      if (w >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     for (int t = 0; t < ntiles; ++t) {
       STAMP(5);
       const int bh = t % NB, bs = (t + 1) % NB;
@@ -510,6 +517,16 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
             ...);
       }(std::make_integer_sequence<int, NSS>{});
       STAMP(1);
+      // the second product's B fragments are redefined here: their VALU conversions cannot sink past this point
+      // to just before an asm MFMA that reads them (no hazard padding is inserted for asm operands)
+#pragma unroll
+      for (int u = 0; u < UK; ++u) {
+#pragma unroll
+        for (int sb = 0; sb < SBW; ++sb) {
+          asm volatile("" : "+v"(xh[u][sb]));
+          if constexpr (SPLIT) asm volatile("" : "+v"(xl[u][sb]));
+        }
+      }
       asm volatile("s_nop 7" ::: "memory");  // S(t+1)'s last results before the prep's VALU reads
       dma_wait();
       STAMP(2);
