@@ -550,8 +550,12 @@ __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const flo
     const long col = min(ncol0 + 16 * cb + l16, N - 1);
 #pragma unroll
     for (int ks = 0; ks < 8 * KCH; ++ks) {
+#ifdef RG3_X_NOW  // timing experiment only (wrong results): no weight fetch, the prologue's cost without it
+      wh[cb][ks] = wl[cb][ks] = bf16x8{} + (bf16)(0.001f * (col + ks));
+#else
       wh[cb][ks] = *(const bf16x8*)(B + col * ldb + ks * 32 + 8 * g);
       wl[cb][ks] = *(const bf16x8*)(B + col * ldb + K + ks * 32 + 8 * g);
+#endif
     }
     const int c4 = min(ncol0 + 16 * cb + 4 * g, N - 4);
     bias4[cb] = ep.bias ? *(const f32x4*)(ep.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};

@@ -15,3 +15,8 @@ for v in base ce8; do L=c2dsr_amd/libc2dsr_hip.so; [ $v != base ] && L=variants/
   C2DSR_LIB=$L timeout -s KILL 90 rocprofv3 --pmc $P -d gpurun_out/exp9_$v -o run --output-format csv -- python3 tools/ce3_micro.py > gpurun_out/exp9_$v.log 2>&1 || { echo "pmc $v failed" >> $O; cat $O; exit 1; }
   python tools/pmc_kernels.py gpurun_out/exp9_$v ce3_kernel >> $O 2>&1; done
 cat $O
+O2=gpurun_out/exp9b.log
+: > $O2
+for v in base rgnow; do L=c2dsr_amd/libc2dsr_hip.so; [ $v != base ] && L=variants/lib_$v.so; echo "== $v" >> $O2
+  C2DSR_LIB=$L timeout -k 10 150 python -u tools/rg_micro.py x3 2>&1 | grep -v amdgpu.ids >> $O2 || exit 1; done
+cat $O2
