@@ -48,9 +48,6 @@
 #ifndef CE3B_DT
 #define CE3B_DT 2
 #endif
-#ifndef CE3_ILV
-#define CE3_ILV (CE3_BI ? 0 : 1)
-#endif
 #ifndef CE3B_ILV
 #define CE3B_ILV 1
 #endif
@@ -120,75 +117,77 @@ __device__ __forceinline__ float quad_sum(float x) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-#ifndef CE3_BI
+#ifndef CE3_BI  // compiler-visible MFMAs in both roles (CE3_BI0: MODE 0 only, CE3_BI1: MODE 1 only)
 #define CE3_BI 0
 #endif
-#ifndef CE3_VN
-#define CE3_VN 3
+#ifndef CE3_BI0
+#define CE3_BI0 CE3_BI
 #endif
-#if CE3_BI
-// CE3_BI: the split products as compiler-visible MFMAs (exact hazard padding, so the scheduler can place the
-// step's LDS reads and VALU work between dependent MFMAs, sched_group_barrier pattern in the tile loop)
+#ifndef CE3_BI1
+#define CE3_BI1 CE3_BI
+#endif
+#ifndef CE3_VN
+#define CE3_VN 5
+#endif
+// Two forms of one split product step, acc (+)= a_hi·b_hi + a_lo·b_hi + a_hi·b_lo, chosen per kernel role:
+//  * asm: ONE asm statement for the three MFMAs on one accumulator (separate statements get an s_nop between
+//    dependent MFMAs from the hazard pass).  S product: the stationary b_hi / b_lo pinned to AGPRs (128 registers
+//    that would otherwise be re-staged into VGPRs every tile), acc in VGPRs (read by the VALU only after s_nop
+//    padding).  Second product: the long-lived accumulator pinned to AGPRs (the compiler otherwise stages it
+//    through VGPRs around the rescale branch); VALU readers of acc run after mfma_drain().
+//  * builtin (BI): compiler-visible MFMAs (exact hazard padding), so the scheduler places the step's LDS reads and
+//    VALU work between dependent MFMAs (sched_group_barrier pattern in the tile loop, step_pattern).
 #define MF(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
+template <bool BI>
 __device__ __forceinline__ void split3_s0(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
                                           const bf16x8& bl) {
-  acc = MF(ah, bh, (f32x4{0.f, 0.f, 0.f, 0.f}));
-  acc = MF(al, bh, acc);
-  acc = MF(ah, bl, acc);
+  if constexpr (BI) {
+    acc = MF(ah, bh, (f32x4{0.f, 0.f, 0.f, 0.f}));
+    acc = MF(al, bh, acc);
+    acc = MF(ah, bl, acc);
+  } else {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, 0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
+        : "=&v"(acc)
+        : "v"(ah), "v"(al), "a"(bh), "a"(bl));
+  }
 }
+template <bool BI>
 __device__ __forceinline__ void split3_s(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
                                          const bf16x8& bl) {
-  acc = MF(ah, bh, acc);
-  acc = MF(al, bh, acc);
-  acc = MF(ah, bl, acc);
+  if constexpr (BI) {
+    acc = MF(ah, bh, acc);
+    acc = MF(al, bh, acc);
+    acc = MF(ah, bl, acc);
+  } else {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
+        : "+v"(acc)
+        : "v"(ah), "v"(al), "a"(bh), "a"(bl));
+  }
 }
+// second product: acc += a_hi·b_hi + a_hi·b_lo + a_lo·b_hi
+template <bool BI>
 __device__ __forceinline__ void split3_u(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
                                          const bf16x8& bl) {
-  acc = MF(ah, bh, acc);
-  acc = MF(ah, bl, acc);
-  acc = MF(al, bh, acc);
+  if constexpr (BI) {
+    acc = MF(ah, bh, acc);
+    acc = MF(ah, bl, acc);
+    acc = MF(al, bh, acc);
+  } else {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0"
+        : "+a"(acc)
+        : "v"(ah), "v"(al), "v"(bh), "v"(bl));
+  }
 }
-__device__ __forceinline__ void mf1_s0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  acc = MF(a, b, (f32x4{0.f, 0.f, 0.f, 0.f}));
-}
-__device__ __forceinline__ void mf1_s(f32x4& acc, const bf16x8& a, const bf16x8& b) { acc = MF(a, b, acc); }
-__device__ __forceinline__ void mf1_u(f32x4& acc, const bf16x8& a, const bf16x8& b) { acc = MF(a, b, acc); }
 #undef MF
-#else
-// One split product step as ONE asm statement (three MFMAs on one accumulator; separate statements get
-// an s_nop between dependent MFMAs from the hazard pass):  acc (+)= a_hi·b_hi + a_lo·b_hi + a_hi·b_lo.
-// S product: the stationary b_hi / b_lo pinned to AGPRs (128 registers that would otherwise be re-staged
-// into VGPRs every tile), acc in VGPRs (read by the VALU only after s_nop padding).
-__device__ __forceinline__ void split3_s0(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
-                                          const bf16x8& bl) {
-  asm volatile(
-      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, 0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
-      : "=&v"(acc)
-      : "v"(ah), "v"(al), "a"(bh), "a"(bl));
-}
-__device__ __forceinline__ void split3_s(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
-                                         const bf16x8& bl) {
-  asm volatile(
-      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
-      : "+v"(acc)
-      : "v"(ah), "v"(al), "a"(bh), "a"(bl));
-}
-// second product: the long-lived accumulator pinned to AGPRs (the compiler otherwise stages it through
-// VGPRs around the rescale branch); VALU readers of acc run after mfma_drain(); the B operand's VALU
-// writes are a phase behind.  acc += a_hi·b_hi + a_hi·b_lo + a_lo·b_hi
-__device__ __forceinline__ void split3_u(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
-                                         const bf16x8& bl) {
-  asm volatile(
-      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0\n\t"
-      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0"
-      : "+a"(acc)
-      : "v"(ah), "v"(al), "v"(bh), "v"(bl));
-}
 
 // plain-bf16 products (the bf16 training mode): one MFMA, stationary operand in AGPRs / accumulator in AGPRs
 __device__ __forceinline__ void mf1_s0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
@@ -200,17 +199,16 @@ __device__ __forceinline__ void mf1_s(f32x4& acc, const bf16x8& a, const bf16x8&
 __device__ __forceinline__ void mf1_u(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
-#endif
-// scheduling hint for one tile-loop step (CE3_BI): per MFMA, one LDS read and up to VN VALU instructions
-template <int NMF, int VN>
+// scheduling hint for one tile-loop step of the builtin form: per MFMA, one LDS read and up to VN VALU instructions
+template <int NMF, int VN, bool BI>
 __device__ __forceinline__ void step_pattern() {
-#if CE3_BI
-  [&]<int... I>(std::integer_sequence<int, I...>) {
-    ((__builtin_amdgcn_sched_group_barrier(0x008, 1, 0), __builtin_amdgcn_sched_group_barrier(0x100, 1, 0),
-      __builtin_amdgcn_sched_group_barrier(0x002, VN, 0), (void)I),
-     ...);
-  }(std::make_integer_sequence<int, NMF>{});
-#endif
+  if constexpr (BI) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      ((__builtin_amdgcn_sched_group_barrier(0x008, 1, 0), __builtin_amdgcn_sched_group_barrier(0x100, 1, 0),
+        __builtin_amdgcn_sched_group_barrier(0x002, VN, 0), (void)I),
+       ...);
+    }(std::make_integer_sequence<int, NMF>{});
+  }
 }
 
 // swept rows per LDS tile: 32 for split images (2D columns), 64 for plain bf16 (D columns) — 32 KiB at D = 256
@@ -247,7 +245,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   // one LDS-DMA wave-instruction of tile t+3 every DQ second-product steps, from the first (DQ = 1: the whole
   // tile at the start of the phase, the longest time to land before the barrier that publishes it)
   constexpr int DQ = SPLIT ? CE3_DQ : CE3B_DQ;
-  constexpr bool ILV = SPLIT ? CE3_ILV : CE3B_ILV;
+  constexpr bool BI = SPLIT && (MODE == 0 ? CE3_BI0 : CE3_BI1);  // builtin MFMA form for this role
+  // ILV (asm form): the step's VALU work between its stationary blocks' products; the builtin form is scheduled
+  constexpr bool ILV = SPLIT ? !BI : CE3B_ILV;
   static_assert(DQ >= 1 && DQ * NDMA <= NUS, "DMA spacing");
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
   __shared__ __attribute__((aligned(16))) float wv[NB][NW][64];
@@ -362,9 +362,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     auto s_prod = [&]<int KSI>(f32x4& acc, const bf16x8(&a)[2], int sb) {
       if constexpr (SPLIT) {
         if constexpr (KSI == 0)
-          split3_s0(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
+          split3_s0<BI>(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
         else
-          split3_s(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
+          split3_s<BI>(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
       } else {
         if constexpr (KSI == 0)
           mf1_s0(acc, a[0], fh[sb][KSI]);
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 __builtin_amdgcn_sched_barrier(0);
                 s_prod.template operator()<k / CB>(sn[cb * SBW + 1], fa[k % (DS + 2)], 1);
               }
-              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN>();
+              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BI>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
               const bf16x8(&tq)[2] = tf[k % (DT + 2)];
               auto u_prod = [&](int sb) {
                 if constexpr (SPLIT)
-                  split3_u(dacc[q][sb], tq[0], tq[1], xh[u][sb], xl[u][sb]);
+                  split3_u<BI>(dacc[q][sb], tq[0], tq[1], xh[u][sb], xl[u][sb]);
                 else
                   mf1_u(dacc[q][sb], tq[0], xh[u][sb]);
               };
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 __builtin_amdgcn_sched_barrier(0);
                 u_prod(1);
               }
-              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN>();
+              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BI>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
