@@ -337,6 +337,14 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
 // the MFMA B operand (lane ↔ row l%16, k 8·(l/16)..).  Per 32-row chunk and wave: 2 row blocks × NCB column
 // blocks × 8 k-steps × 3 MFMAs (a_hi·b_hi + a_hi·b_lo + a_lo·b_hi).
 // Rows past M read 0 and are not stored (buffer descriptors); N % 4 == 0, ldc % 4 == 0.
+// Fragment order of a split weight image (c2dsr_to_split_bf16_frag_multi → c2dsr_rgemm_x3f): the values one rg3
+// wave loads for (16-column block cb, k-step ks, hi / lo) are one contiguous 1 KiB piece — lane g·16 + l16 holds
+// column 16cb + l16, k = 32ks + 8g .. +7 — so each weight load is one coalesced 1 KiB read instead of 16 row
+// segments of 64 B.  Piece (cb, ks, hl) = cb·(2K/32) + 2ks + hl.
+__host__ __device__ __forceinline__ long split_frag_index(int col, int k, int hl, int K) {
+  const long piece = (long)(col >> 4) * (K / 16) + 2 * (k >> 5) + hl;
+  return (piece * 64 + ((k >> 3) & 3) * 16 + (col & 15)) * 8 + (k & 7);
+}
 __device__ __forceinline__ void x3_0(f32x4& acc, const bf16x8& wh, const bf16x8& wl, const bf16x8& ah,
                                      const bf16x8& al) {
   asm volatile(
@@ -553,8 +561,14 @@ __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const flo
 #ifdef RG3_X_NOW  // timing experiment only (wrong results): no weight fetch, the prologue's cost without it
       wh[cb][ks] = wl[cb][ks] = bf16x8{} + (bf16)(0.001f * (col + ks));
 #else
-      wh[cb][ks] = *(const bf16x8*)(B + col * ldb + ks * 32 + 8 * g);
-      wl[cb][ks] = *(const bf16x8*)(B + col * ldb + K + ks * 32 + 8 * g);
+      if (ldb == 0) {  // fragment-ordered image (split_frag_index): one coalesced 1 KiB piece per load
+        const long f = ((long)(min(ncol0 + 16 * cb, N - 1) >> 4) * (K / 16) + 2 * ks) * 64 + lane;
+        wh[cb][ks] = *(const bf16x8*)(B + f * 8);
+        wl[cb][ks] = *(const bf16x8*)(B + (f + 64) * 8);
+      } else {
+        wh[cb][ks] = *(const bf16x8*)(B + col * ldb + ks * 32 + 8 * g);
+        wl[cb][ks] = *(const bf16x8*)(B + col * ldb + K + ks * 32 + 8 * g);
+      }
 #endif
     }
     const int c4 = min(ncol0 + 16 * cb + 4 * g, N - 4);
@@ -986,9 +1000,10 @@ C2_API int c2dsr_rgemm(int M, int N, int K, const float* A, int lda, const void*
 static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, const void* B, int ldb, float* C,
                       int ldc, float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1,
                       float p, int64_t row_base, const int* rowmap, int aux_mode, const float* aux,
-                      const int* auxmap, float aux_scale, void* stream, bool x3 = false) {
+                      const int* auxmap, float aux_scale, void* stream, bool x3 = false, bool frag = false) {
   if (!c2dsr_rgemm_supported(M, N, K) || lda % 4 || ldb % 8 || beta != 0.f) return (int)hipErrorInvalidValue;
-  if (x3 && (ab16 || (K != 256 && K != 512) || ldb < 2 * K)) return (int)hipErrorInvalidValue;
+  if (x3 && (ab16 || (K != 256 && K != 512) || (frag ? ldb != 0 || N % 4 || ldc % 4 : ldb < 2 * K)))
+    return (int)hipErrorInvalidValue;
   if (ab16 && (epilogue || aux_mode == AUX_MASK || (K != 768 && aux_mode == AUX_ACC_MAP) ||
                (K == 512 && aux_mode != AUX_NONE)))
     return (int)hipErrorInvalidValue;
@@ -1177,8 +1192,16 @@ C2_API int c2dsr_rgemm_x3(int M, int N, int K, const float* A, int lda, const vo
                           float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
                           float aux_scale, void* stream) {
+  if (ldb == 0) return (int)hipErrorInvalidValue;  // 0 selects the fragment-ordered image (c2dsr_rgemm_x3f)
   return rgemm_impl(M, N, K, A, false, lda, B, ldb, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, rowmap,
                     aux_mode, aux, auxmap, aux_scale, stream, true);
+}
+C2_API int c2dsr_rgemm_x3f(int M, int N, int K, const float* A, int lda, const void* B, float* C, int ldc, float alpha,
+                           float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
+                           int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
+                           float aux_scale, void* stream) {
+  return rgemm_impl(M, N, K, A, false, lda, B, 0, C, ldc, alpha, beta, bias, epilogue, k0, k1, p, row_base, rowmap,
+                    aux_mode, aux, auxmap, aux_scale, stream, true, true);
 }
 
 // the same with A bf16 (K = 768, no epilogue, aux modes 0 / 1 / 3)
@@ -1307,7 +1330,8 @@ struct MultiBf16 {
 // every matrix of the list in one launch: block b converts 256 elements of the matrix whose block range holds
 // it (block-uniform lookup: scalar reads of the argument block)
 // SPLIT: y = hi ‖ lo (row r of y: [hi(row) | lo(row)], width 2·C, or transposed [C][2R])
-template <bool SPLIT = false>
+// FRAG (SPLIT only): the same values in rg3's fragment order (split_frag_index)
+template <bool SPLIT = false, bool FRAG = false>
 __global__ __launch_bounds__(256) void to_bf16_multi_kernel(MultiBf16 m) {
   const int b = blockIdx.x;
   int lo = 0, hi = m.count - 1;
@@ -1326,8 +1350,13 @@ __global__ __launch_bounds__(256) void to_bf16_multi_kernel(MultiBf16 m) {
     const int RR = m.tr[lo] ? Cc : R, CC = m.tr[lo] ? R : Cc;  // output rows / columns
     const int orow = m.tr[lo] ? c : r, ocol = m.tr[lo] ? r : c;
     (void)RR;
-    m.y[lo][(long)orow * 2 * CC + ocol] = v;
-    m.y[lo][(long)orow * 2 * CC + CC + ocol] = l;
+    if constexpr (FRAG) {
+      m.y[lo][split_frag_index(orow, ocol, 0, CC)] = v;
+      m.y[lo][split_frag_index(orow, ocol, 1, CC)] = l;
+    } else {
+      m.y[lo][(long)orow * 2 * CC + ocol] = v;
+      m.y[lo][(long)orow * 2 * CC + CC + ocol] = l;
+    }
   } else if (m.tr[lo]) {
     m.y[lo][(long)c * R + r] = v;
   } else {
@@ -1338,7 +1367,7 @@ __global__ __launch_bounds__(256) void to_bf16_multi_kernel(MultiBf16 m) {
 
 // c2dsr_to_bf16 over a list of matrices in one launch: desc = HOST array of count (<= 64) records of six
 // int64 (x, y, R, Cc, ldx, trans) with the meaning of c2dsr_to_bf16's arguments
-static int to_bf16_multi_impl(const int64_t* desc, int count, void* stream, bool split) {
+static int to_bf16_multi_impl(const int64_t* desc, int count, void* stream, bool split, bool frag = false) {
   if (count < 0 || count > MULTI_MAX) return (int)hipErrorInvalidValue;
   if (count == 0) return 0;
   MultiBf16 m;
@@ -1357,7 +1386,11 @@ static int to_bf16_multi_impl(const int64_t* desc, int count, void* stream, bool
   }
   if (m.bstart[count] == 0) return 0;
   for (int k = count + 1; k <= MULTI_MAX; ++k) m.bstart[k] = m.bstart[count];
-  if (split)
+  if (frag) {
+    for (int k = 0; k < count; ++k)  // rg3's fragment order: K (the image's reduction width) 256 or 512
+      if ((m.tr[k] ? m.R[k] : m.C[k]) % 256 || (m.tr[k] ? m.R[k] : m.C[k]) > 512) return (int)hipErrorInvalidValue;
+    to_bf16_multi_kernel<true, true><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
+  } else if (split)
     to_bf16_multi_kernel<true><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
   else
     to_bf16_multi_kernel<false><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
@@ -1370,6 +1403,11 @@ C2_API int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream) {
 // the split-bf16 images (y = [R][2·Cc] hi ‖ lo, or [Cc][2·R] transposed) of a list of matrices in one launch
 C2_API int c2dsr_to_split_bf16_multi(const int64_t* desc, int count, void* stream) {
   return to_bf16_multi_impl(desc, count, stream, true);
+}
+// the same values in rg3's fragment order (c2dsr_rgemm_x3f's B): ⌈N'/16⌉·16 × 2K' bf16 per matrix, N' / K' = the
+// output rows / columns (Cc / R when transposed); rows past N' are not written
+C2_API int c2dsr_to_split_bf16_frag_multi(const int64_t* desc, int count, void* stream) {
+  return to_bf16_multi_impl(desc, count, stream, true, true);
 }
 
 C2_API int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream) {

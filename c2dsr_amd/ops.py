@@ -112,10 +112,11 @@ class _WeightImages:
             self._refresh_known()
 
     def _refresh_known(self):
-        for split, fn in ((False, 'c2dsr_to_bf16_multi'), (True, 'c2dsr_to_split_bf16_multi')):
+        for layout, fn in ((None, 'c2dsr_to_bf16_multi'), ('split', 'c2dsr_to_split_bf16_multi'),
+                           ('frag', 'c2dsr_to_split_bf16_frag_multi')):
             recs, done = [], []
             for key, (W, y) in self.known.items():
-                if key[3] != split:
+                if key[3] != layout:
                     continue
                 R, Cc = W.shape
                 recs += [W.data_ptr(), y.data_ptr(), R, Cc, W.stride(0), int(key[2])]
@@ -128,15 +129,16 @@ class _WeightImages:
                 self.cache[key] = ((self.epoch, W._version), y, W)
         self.known = {}
 
-    def get(self, W, trans, split=False):
-        key = (W.data_ptr(), tuple(W.shape), bool(trans), bool(split))
+    def get(self, W, trans, layout=None):
+        """layout None: bf16 image; 'split': split image hi ‖ lo; 'frag': the split image in rg3's fragment order."""
+        key = (W.data_ptr(), tuple(W.shape), bool(trans), layout)
         tag = (self.epoch, W._version)
         if key not in self.cache and key in self.known:
             self._refresh_known()
         hit = self.cache.get(key)
         if hit is not None and hit[0] == tag:
             return hit[1]
-        y = to_split_bf16(W, trans) if split else to_bf16(W, trans)
+        y = to_bf16(W, trans) if layout is None else to_split_bf16(W, trans, frag=layout == 'frag')
         self.cache[key] = (tag, y, W)
         return y
 
@@ -149,17 +151,24 @@ def weight_bf16(W, trans=False):
 
 
 def weight_img(W, kind, trans=False):
-    """The operand image of a projection weight for a rg_kind / wg_kind kernel: bf16 [R][C] ('b16') or the
-    split image [R][2C] = hi ‖ lo ('x3'); transposed ([C][…]) if asked."""
-    return WEIGHTS.get(W.detach(), trans, split=kind == 'x3')
+    """The operand image of a projection weight for a rg_kind kernel: bf16 [R][C] ('b16'), the split image in the
+    row-streaming kernel's fragment order ('x3': rgemm(..., x3=True, frag=True)) or as rows [R][2C] = hi ‖ lo
+    ('x3row'); transposed ([C][…]) if asked."""
+    layout = {'b16': None, 'x3': 'frag', 'x3row': 'split'}[kind]
+    return WEIGHTS.get(W.detach(), trans, layout=layout)
 
 
-def to_split_bf16(X, trans=False):
-    """Split-bf16 image of a 2-D fp32 matrix: [R][2C] with row = hi ‖ lo ([C][2R] if transposed)."""
+def to_split_bf16(X, trans=False, frag=False):
+    """Split-bf16 image of a 2-D fp32 matrix: [R][2C] with row = hi ‖ lo ([C][2R] if transposed); frag: the same
+    values in c2dsr_rgemm_x3f's fragment order, rows padded to a multiple of 16 (zero)."""
     R, Cc = X.shape
-    y = torch.empty((Cc, 2 * R) if trans else (R, 2 * Cc), device=X.device, dtype=torch.bfloat16)
+    rows, cols = (Cc, R) if trans else (R, Cc)
+    if frag:
+        y = torch.zeros(-(-rows // 16) * 16, 2 * cols, device=X.device, dtype=torch.bfloat16)
+    else:
+        y = torch.empty(rows, 2 * cols, device=X.device, dtype=torch.bfloat16)
     desc = np.asarray([X.data_ptr(), y.data_ptr(), R, Cc, X.stride(0), int(trans)], dtype=np.int64)
-    lib('c2dsr_to_split_bf16_multi', desc.ctypes.data, 1, stream())
+    lib('c2dsr_to_split_bf16_frag_multi' if frag else 'c2dsr_to_split_bf16_multi', desc.ctypes.data, 1, stream())
     return y
 
 
@@ -167,10 +176,11 @@ AUX_ACC, AUX_MASK, AUX_ACC_MAP = 1, 2, 3
 
 
 def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, aux_mode=0, aux=None, aux_scale=0.0,
-          rowmap=None, auxmap=None, x3=False):
+          rowmap=None, auxmap=None, x3=False, frag=False):
     """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm); aux_mode
     AUX_ACC: C += aux (aux may be C itself), AUX_MASK: C = aux > 0 ? C·aux_scale : 0 (c2dsr_rgemm_aux).
-    x3: Bb is the split image [N, 2K] and the products run on split-bf16 operands (c2dsr_rgemm_x3)."""
+    x3: Bb is the split image [N, 2K] and the products run on split-bf16 operands (c2dsr_rgemm_x3); frag: Bb is
+    that image in fragment order (to_split_bf16(..., frag=True), c2dsr_rgemm_x3f)."""
     k0 = k1 = 0
     p = 0.0
     row_base = 0
@@ -184,8 +194,12 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
         if A.dtype != torch.float32 or Bb.dtype != torch.bfloat16 or Bb.shape[-1] != 2 * K:
             raise TypeError(f'rgemm x3: A must be fp32 and Bb a split image [N, 2K] (got A {A.dtype}, Bb {Bb.dtype} '
                             f'{tuple(Bb.shape)})')
-        lib('c2dsr_rgemm_x3', M, N, K, A, K, Bb, 2 * K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
-            int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
+        if frag:
+            lib('c2dsr_rgemm_x3f', M, N, K, A, K, Bb, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
+                int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
+        else:
+            lib('c2dsr_rgemm_x3', M, N, K, A, K, Bb, 2 * K, C, N, float(alpha), float(beta), bias, epi, k0, k1,
+                float(p), int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
     elif A.dtype == torch.bfloat16:  # the attention backward's bf16 dqkv (in_proj dX; c2dsr_rgemm_aux_b16a)
         if epi or aux_mode == AUX_MASK:
             raise HipLibError('rgemm: bf16 A supports no epilogue / mask mode')
@@ -328,12 +342,13 @@ class LinearFn(Function):
             # pass, but the reference C2 golden step's linear1 gradient moved from < 1e-4 to 1.2e-4: not the default
             kind = None
             if RELU_GUARD and relu_guard_ok(M, N, K):
-                rgemm_relu_guard(x, weight_img(W, 'x3'), W, y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
+                rgemm_relu_guard(x, weight_img(W, 'x3row'), W, y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
                 kind = 'guard'
         if kind == 'guard':
             pass
         elif kind:
-            rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop, x3=kind == 'x3')
+            rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop, x3=kind == 'x3',
+                  frag=kind == 'x3')
         else:
             gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)
         ctx.save_for_backward(x, W, y if relu_drop is not None else None)
@@ -377,17 +392,17 @@ def linear_backward(ctx, x, W, y, dy, need_dx):
             park, sub = full, False
         if sub:  # dx = dy·W + the parked rows, read through the row map
             dx = torch.empty_like(x)
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park, auxmap=ctx.res.inv, x3=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park, auxmap=ctx.res.inv, x3=x3, frag=x3)
         elif fused and park is not None:  # dx = parked LN gradient + dy·W, in place
             dx = park
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx, x3=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx, x3=x3, frag=x3)
         elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here
             dx = torch.empty_like(x)
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x, aux_scale=1.0 / (1.0 - ctx.ff.p), x3=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x, aux_scale=1.0 / (1.0 - ctx.ff.p), x3=x3, frag=x3)
             ctx.ff.premasked = True
         elif fused:
             dx = torch.empty_like(x)
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, x3=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, x3=x3, frag=x3)
         elif park is not None:
             dx = park
             gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0, precision=ctx.precision)
@@ -1080,7 +1095,7 @@ class QKVAttnFn(Function):
         qkv = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
         kind = rg_kind(precision, M, N, K)
         if kind:
-            rgemm(x, weight_img(W, kind), qkv, M=M, N=N, K=K, bias=b, x3=kind == 'x3')
+            rgemm(x, weight_img(W, kind), qkv, M=M, N=N, K=K, bias=b, x3=kind == 'x3', frag=kind == 'x3')
         else:
             gemm(x, W, qkv, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
         B, L, d3 = qkv.shape
@@ -1130,7 +1145,7 @@ def _proj(x, W, b, y, precision):
         return y
     kind = rg_kind(precision, M, N, K)
     if kind:
-        rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, x3=kind == 'x3')
+        rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, x3=kind == 'x3', frag=kind == 'x3')
     else:
         gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
     return y
@@ -1146,7 +1161,7 @@ def _proj_backward(x, W, dy, dx, acc, gW, gb, precision):
     kind = rg_kind(precision, M, K, N)
     if kind:
         rgemm(dy, weight_img(W, kind, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC if acc else 0,
-              aux=dx if acc else None, x3=kind == 'x3')
+              aux=dx if acc else None, x3=kind == 'x3', frag=kind == 'x3')
     else:
         gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0 if acc else 0.0, precision=precision)
     wk = wg_kind(precision, M, N, K)

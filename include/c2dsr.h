@@ -361,6 +361,12 @@ int c2dsr_rgemm_x3(int M, int N, int K, const float* A, int lda, const void* B, 
                    float alpha, float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p,
                    int64_t row_base, const int* rowmap, int aux_mode, const float* aux, const int* auxmap,
                    float aux_scale, void* stream);
+/* the same with B the fragment-ordered split image (c2dsr_to_split_bf16_frag_multi; no ldb): each weight load of the
+ * kernel is one coalesced 1 KiB read; N % 4 == 0, ldc % 4 == 0.  Bit-identical to c2dsr_rgemm_x3 on the same W. */
+int c2dsr_rgemm_x3f(int M, int N, int K, const float* A, int lda, const void* B, float* C, int ldc, float alpha,
+                    float beta, const float* bias, int epilogue, uint32_t k0, uint32_t k1, float p, int64_t row_base,
+                    const int* rowmap, int aux_mode, const float* aux, const int* auxmap, float aux_scale,
+                    void* stream);
 /* linear1 + ReLU + dropout of the fp32 mode (replaces models/encoders.py:23-27 → TransformerEncoderLayer
  * linear1 / activation / dropout): C = drop(relu(A·Wᵀ + bias)) on split-bf16 products (B = the split image of the
  * fp32 weight W [N][256], K = 256), every pre-activation within the split error bound of zero (|v| ≤ 2^-15·‖a‖‖w‖)
@@ -378,6 +384,10 @@ int c2dsr_wgemm_x3_multi(const int64_t* seg, int nseg, int N, int D, float beta,
 /* split-bf16 images of a list of matrices (c2dsr_to_bf16_multi's descriptors): y = [R][2·Cc] (row = hi ‖ lo),
  * or [Cc][2·R] when trans */
 int c2dsr_to_split_bf16_multi(const int64_t* desc, int count, void* stream);
+/* the same values in c2dsr_rgemm_x3f's fragment order: ⌈N'/16⌉·16 rows × 2K' bf16 per matrix (N' × K' = the image's
+ * rows × columns: R × Cc, or Cc × R when trans; K' = 256 or 512); element (n, k) hi / lo (hl = 0 / 1) at
+ * ((⌊n/16⌋·(K'/16) + 2⌊k/32⌋ + hl)·64 + (⌊k/8⌋ mod 4)·16 + n mod 16)·8 + k mod 8; rows past N' are not written */
+int c2dsr_to_split_bf16_frag_multi(const int64_t* desc, int count, void* stream);
 /* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
  * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
  * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS

@@ -309,6 +309,45 @@ def test_split_weight_images_multi():
     assert float((hi + lo - Ws[0].T).abs().max() / Ws[0].abs().max()) < 2 ** -16
 
 
+def frag_index(n, k, hl, K):
+    """c2dsr_to_split_bf16_frag_multi's element position (include/c2dsr.h), restated."""
+    return (((n // 16) * (K // 16) + 2 * (k // 32) + hl) * 64 + ((k // 8) % 4) * 16 + n % 16) * 8 + k % 8
+
+
+@pytest.mark.parametrize('N,K,tr', [(256, 256, 0), (768, 256, 0), (256, 512, 1), (200, 256, 0)])
+def test_rgemm_x3_fragment_image(N, K, tr):
+    """The fragment-ordered split image (c2dsr_to_split_bf16_frag_multi) is the row image's values at the header's
+    positions, and c2dsr_rgemm_x3f on it is bit-identical to c2dsr_rgemm_x3 on the row image in every epilogue mode
+    (the weight loads differ, the MFMA operands do not)."""
+    from c2dsr_amd.ops import AUX_ACC, AUX_MASK, rgemm, to_split_bf16
+    g = torch.Generator().manual_seed(N + K + tr)
+    W = torch.randn(K, N, generator=g) if tr else torch.randn(N, K, generator=g)
+    row = to_split_bf16(W.to(DEV), bool(tr)).cpu()
+    frag = to_split_bf16(W.to(DEV), bool(tr), frag=True).cpu()
+    assert frag.shape == (-(-N // 16) * 16, 2 * K)
+    n, k = torch.meshgrid(torch.arange(N), torch.arange(K), indexing='ij')
+    flat = frag.reshape(-1)
+    for hl in (0, 1):
+        assert torch.equal(flat[frag_index(n, k, hl, K)], row[:, hl * K:(hl + 1) * K])
+    M = 1000 + 37
+    A = torch.randn(M, K, generator=g).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    aux = torch.randn(M, N, generator=g).to(DEV)
+    for kw in (dict(bias=b), dict(bias=b, relu_drop=((5, 6), 0.2, 100)), dict(aux_mode=AUX_MASK, aux=aux, aux_scale=2.0)):
+        outs = []
+        for fr, img in ((False, row.to(DEV)), (True, frag.to(DEV))):
+            C = torch.empty(M, N, device=DEV)
+            rgemm(A, img, C, M=M, N=N, K=K, x3=True, frag=fr, **kw)
+            outs.append(C)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+    C0, C1 = aux.clone(), aux.clone()
+    rgemm(A, row.to(DEV), C0, M=M, N=N, K=K, aux_mode=AUX_ACC, aux=C0, x3=True)
+    rgemm(A, frag.to(DEV), C1, M=M, N=N, K=K, aux_mode=AUX_ACC, aux=C1, x3=True, frag=True)
+    torch.cuda.synchronize()
+    assert torch.equal(C0, C1)
+
+
 def _ref_chunked(H, W, b, pl, t, coef, lam, BR, chunk=2048):
     """_ref in float64 on the device, in row chunks (the MB head-b logits are 9.7 GB in float64)."""
     H, W, b, pl, t = (x.to(DEV) for x in (H, W, b, pl, t))

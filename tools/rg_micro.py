@@ -63,16 +63,19 @@ def main(x3=False):
     K = 256
     for N in (256, 512):
         W = torch.randn(N, K, device=dev)
-        Wb = to_split_bf16(W) if x3 else to_bf16(W)
+        # x3: the row image (c2dsr_rgemm_x3) and the fragment-ordered image the fp32 step uses (c2dsr_rgemm_x3f)
+        forms = ((('x3', False, to_split_bf16(W)), ('x3f', True, to_split_bf16(W, frag=True))) if x3 else
+                 (('b16', False, to_bf16(W)),))
         for M in (8192, 20000, 38000, 57000, 102400):
             A = torch.randn(M, K, device=dev)
             C = torch.empty(M, N, device=dev)
-            t = timeit(lambda: rgemm(A, Wb, C, M=M, N=N, K=K, x3=x3))
-            gb = 4.0 * M * (K + N) / t / 1e3
-            print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: {"x3" if x3 else "b16"} N {N} M {M:6d}: {t:6.1f} us '
-                  f'{gb:6.0f} GB/s', flush=True)
-            if x3:
-                rg3_stamps(lambda: rgemm(A, Wb, C, M=M, N=N, K=K, x3=x3))
+            for name, fr, Wb in forms:
+                t = timeit(lambda: rgemm(A, Wb, C, M=M, N=N, K=K, x3=x3, frag=fr))
+                gb = 4.0 * M * (K + N) / t / 1e3
+                print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: {name} N {N} M {M:6d}: '
+                      f'{t:6.1f} us {gb:6.0f} GB/s', flush=True)
+                if x3:
+                    rg3_stamps(lambda: rgemm(A, Wb, C, M=M, N=N, K=K, x3=x3, frag=fr))
 
 
 def rg3_stamps(f):
