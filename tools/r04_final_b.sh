@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-4 evidence, part b: FETCH / WRITE / SQ PMC passes of the main line, kernel stats + FETCH / WRITE passes of
+# the C5 line (bf16 tables).   usage: bash tools/r04_final_b.sh TAG
+set -o pipefail
+TAG=${1:-r04z}
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+A="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extra"
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o run --output-format csv -- python3 $A > gpurun_out/${TAG}_fetch.log 2>&1 &&
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o run --output-format csv -- python3 $A > gpurun_out/${TAG}_write.log 2>&1 &&
+timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAIT_INST_LDS SQ_BUSY_CYCLES -d gpurun_out/${TAG}_sq -o run --output-format csv -- python3 $A > gpurun_out/${TAG}_sq.log 2>&1 || { echo "pmc failed"; exit 1; }
+C="bench.py --config c5 --c5-tables bf16 --steps 2 --warmup 1"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}c5_prof -o run --output-format csv -- python3 $C > gpurun_out/${TAG}c5_prof.log 2>&1 &&
+python tools/prof_summary.py gpurun_out/${TAG}c5_prof 3 20 > gpurun_out/${TAG}c5_summary.txt 2>&1 &&
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}c5_fetch -o run --output-format csv -- python3 $C > gpurun_out/${TAG}c5_fetch.log 2>&1 &&
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}c5_write -o run --output-format csv -- python3 $C > gpurun_out/${TAG}c5_write.log 2>&1 || { echo "c5 passes failed"; exit 1; }
+echo "part b done"
