@@ -19,9 +19,10 @@ pre = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else None
 prec = sys.argv[3] if len(sys.argv) > 3 else 'fp32'
 # the kernels the two timed K5 entry points launch per head (fwd_u: sweep + rows; dw: sweep)
-# (ce3_kernel<D, MODE, SPLIT>: SPLIT = true in the fp32 mode, false for the plain-bf16 instantiation)
-K5 = (('ce3_kernel<256, 0, false>', 'ce_rows_kernel', 'ce3_kernel<256, 1, false>') if prec == 'bf16' else
-      ('ce3_kernel<256, 0, true>', 'ce_rows_kernel', 'ce3_kernel<256, 1, true>'))
+# (ce3_kernel<D, MODE, SPLIT, NW>: SPLIT = true in the fp32 mode, false for the plain-bf16 instantiation; matched
+# without the trailing arguments)
+K5 = (('ce3_kernel<256, 0, false', 'ce_rows_kernel', 'ce3_kernel<256, 1, false') if prec == 'bf16' else
+      ('ce3_kernel<256, 0, true', 'ce_rows_kernel', 'ce3_kernel<256, 1, true'))
 K12 = ('spmm_kernel', 'combine_kernel', 'embed_fwd_kernel', 'seg_chunk_kernel', 'seg_split1_kernel',
        'seg_split2_kernel')
 PMC_STEPS = 3
