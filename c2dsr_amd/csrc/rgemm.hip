@@ -33,11 +33,10 @@ struct Epi2 {
   float aux_scale;
   const int* rowmap;  // dropout row index = row_base + (rowmap ? rowmap[row] : row)
   const int* auxmap;  // AUX_ACC_MAP: aux row of output row r = auxmap[r] (< 0: none, aux reads 0)
-  // guarded ReLU (rg3 GUARD, c2dsr_rgemm_x3_relu_guard): pre-activations within the split product's error bound
-  // of zero are listed for an exact recompute: |v| <= tau·‖a_r‖·‖w_c‖  ⇔  v² <= gtau2·‖a_r‖²·wn2[c]
-  const float* wn2;  // [N] squared norms of the weight rows (output columns)
-  int* glist;        // listed elements r·N + c
-  int* gcnt;         // list length
+  // guarded ReLU (rg3 GUARD, c2dsr_rgemm_x3_relu_guard): a pre-activation within the split product's error bound
+  // of zero is flagged for an exact recompute: |v| <= tau·‖a_r‖·‖w_c‖  ⇔  v² <= gtau2·‖a_r‖²·wn2[c]
+  const float* wn2;      // [N] squared norms of the weight rows (output columns)
+  unsigned char* gflag;  // [M][N/4]: bit e of byte (r, q) ↔ element (r, 4q + e) (zero on entry; the fix clears)
   float gtau2;
 };
 
@@ -364,6 +363,9 @@ __device__ __forceinline__ void x3_acc(f32x4& acc, const bf16x8& wh, const bf16x
       : "a"(wh), "a"(wl), "v"(ah), "v"(al));
 }
 
+#ifndef RG3_GUARD_NW  // waves per workgroup of the guarded instance (at 4 its unrolled three-set loop spills 39 registers, at 8 five)
+#define RG3_GUARD_NW 8
+#endif
 #ifndef RG3_NW
 #define RG3_NW 8  // waves per workgroup of the split-bf16 row-streaming GEMM (8: 2 per SIMD, measured 5-13% over 4 at N=256)
 #endif
@@ -395,8 +397,7 @@ template <int KCH, bool EPI, int AUX, bool GUARD = false, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const float* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, float* C, long ldc,
                                                          Epi2 ep, int G) {
-  static_assert(!GUARD || (EPI && KCH == 1 && AUX == AUX_NONE && NW == 4),
-                "guarded ReLU: the K = 256 relu·dropout epilogue, 4 waves");
+  static_assert(!GUARD || (EPI && KCH == 1 && AUX == AUX_NONE), "guarded ReLU: the K = 256 relu·dropout epilogue");
   static_assert(NW == 4 || NW == 8, "rg3 waves");
   constexpr int K = 256 * KCH;
   constexpr int NCB = 16 / NW / KCH;  // 16-column blocks per wave
@@ -427,6 +428,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const flo
   f32x4 bias4[NCB];
   const auto asrc = rsrc_bytes(A, (long)M * lda * 4);   // rows >= M read 0
   const auto csrc = rsrc_bytes(C, (long)M * ldc * 4);   // stores to rows >= M are dropped
+  const auto fsrc = rsrc_bytes(GUARD ? (void*)ep.gflag : (void*)C, GUARD ? (long)M * (N >> 2) : 0);
   const auto xsrc = rsrc_bytes(AUX != AUX_NONE ? ep.aux : C, (long)M * ldc * 4);  // rows >= M read 0
   // per-lane image offsets: row l16 (+16 rb), chunk 4c + g of the 128-column half-tile
   int roff[4];
@@ -504,6 +506,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const flo
   f32x4 acc[2][NCB];
   auto epilogue = [&](int tile, bool live, int buf) {
     mfma_drain();
+    unsigned gmask = 0;  // GUARD: bit (rb·NCB + cb)·4 + i ↔ element (rb, cb, i) of this lane needs the exact product
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       const int row = tile_rows(tile, rb);
@@ -517,18 +520,8 @@ __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const flo
           const float rr = rn2s[buf][16 * rb + l16] * ep.gtau2;
           const f32x4 wq = *(const f32x4*)&wn2s[16 * cb + w * CW + 4 * g];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const bool flag = live && row < M && col + i < N && v[i] * v[i] <= rr * wq[i];
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(flag);
-            if (m) [[unlikely]] {  // wave-uniform: append the flagged elements (one atomic per wave)
-              const int lead = __builtin_ctzll(m);
-              int base = 0;
-              if (lane == lead) base = atomicAdd(ep.gcnt, __builtin_popcountll(m));
-              base = __builtin_amdgcn_readlane(base, lead);
-              const int k = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
-              if (flag) ep.glist[base + k] = row * N + col + i;
-            }
-          }
+          for (int i = 0; i < 4; ++i)
+            gmask |= (unsigned)(live && row < M && col + i < N && v[i] * v[i] <= rr * wq[i]) << ((rb * NCB + cb) * 4 + i);
         }
         if constexpr (EPI) {
           const float4 dm = ep.drop.mul4((uint64_t)(ep.row_base + dmap[rb]) * N + col);
@@ -544,6 +537,19 @@ __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const flo
         }
         const int off = (col < N && live) ? (row * (int)ldc + col) * 4 : 0x7ffffff0;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), csrc, off, 0, 0);
+      }
+    }
+    if constexpr (GUARD) {
+      // the lane's 4-column groups with a guarded element: one flag byte each (a group belongs to one lane),
+      // branch-free — unflagged groups store out of range
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const unsigned f = (gmask >> ((rb * NCB + cb) * 4)) & 0xfu;
+          const int off = f ? tile_rows(tile, rb) * (N >> 2) + ((ncol0 + 16 * cb + 4 * g) >> 2) : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b8((unsigned char)f, fsrc, off, 0, 0);
+        }
       }
     }
   };
@@ -574,7 +580,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rg3_kernel(int M, int N, const flo
     const int c4 = min(ncol0 + 16 * cb + 4 * g, N - 4);
     bias4[cb] = ep.bias ? *(const f32x4*)(ep.bias + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  if constexpr (GUARD) wn2s[threadIdx.x] = ep.wn2[min(gcol * WGC + (int)threadIdx.x, N - 1)];
+  if constexpr (GUARD) {
+    if ((int)threadIdx.x < WGC) wn2s[threadIdx.x] = ep.wn2[min(gcol * WGC + (int)threadIdx.x, N - 1)];
+  }
   vm_drain();
 #pragma unroll
   for (int u = 0; u < SPU; ++u) stage1(Pa[u], u, 0);
@@ -950,26 +958,43 @@ __global__ void row_norm2_kernel(const float* __restrict__ W, int N, int K, floa
   if (lane == 0) out[c] = s;
 }
 
-// the exact recompute of the guarded elements (rg3 GUARD): C[r][c] = drop(relu(alpha·Σ_k A[r][k]·W[c][k] + b[c]))
-// with fp32 products and a fixed-order wave reduction (K = 256: a float4 per lane), one wave per listed element
+// the exact recompute of the flagged elements (rg3 GUARD): C[r][c] = drop(relu(alpha·Σ_k A[r][k]·W[c][k] + b[c])),
+// each dot product one fp32 FMA chain in k order — the order of a k-sequential fp32 GEMM, so a pre-activation within
+// fp32 rounding of zero gets that GEMM's sign (tools/linear1_emu.py: a float64-exact product misses the reference's C2
+// step by 1.2e-4 on linear1's weight gradient through one such tie; this order matches it).  One wave per 64 flag bytes
+// (a byte = a 4-column group of one row); per flagged byte the wave stages the row of A and the 4 weight rows in LDS
+// with coalesced loads and lanes 0..3 run the chains of the group's 4 columns from there.  The flags are cleared.
 __global__ __launch_bounds__(256) void guard_fix_kernel(const float* __restrict__ A, long lda,
-                                                        const float* __restrict__ W, int N, Epi2 ep,
+                                                        const float* __restrict__ W, int M, int N, Epi2 ep,
                                                         float* __restrict__ C, long ldc) {
-  const int lane = threadIdx.x & 63;
-  const int n = *ep.gcnt;
-  for (int e = blockIdx.x * 4 + (threadIdx.x >> 6); e < n; e += gridDim.x * 4) {
-    const int idx = ep.glist[e];
-    const int r = idx / N, c = idx % N;
-    const float4 a = *(const float4*)(A + (long)r * lda + 4 * lane);
-    const float4 w = *(const float4*)(W + (long)c * 256 + 4 * lane);
-    float s = fmaf(a.w, w.w, fmaf(a.z, w.z, fmaf(a.y, w.y, a.x * w.x)));
+  __shared__ float4 st[4][5][64];  // per wave: A row, 4 weight rows (K = 256)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nq = N >> 2;
+  const long fi = (long)blockIdx.x * 256 + threadIdx.x;
+  const bool in = fi < (long)M * nq;
+  const unsigned f = in ? ep.gflag[fi] : 0u;
+  if (f) ep.gflag[fi] = 0;
+  for (unsigned long long m = __builtin_amdgcn_ballot_w64(f != 0); m; m &= m - 1) {  // wave-uniform
+    const int src = __builtin_ctzll(m);
+    const long fl = fi - lane + src;
+    const unsigned fs = (unsigned)__builtin_amdgcn_readlane((int)f, src);
+    const int r = (int)(fl / nq), c0 = (int)(fl % nq) * 4;
+    st[wv][0][lane] = *(const float4*)(A + (long)r * lda + 4 * lane);
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-    if (lane == 0) {
-      const float v = fmaf(ep.alpha, s, ep.bias ? ep.bias[c] : 0.f);
-      const int dr = ep.rowmap ? ep.rowmap[r] : r;
+    for (int e = 0; e < 4; ++e) st[wv][1 + e][lane] = *(const float4*)(W + (long)(c0 + e) * 256 + 4 * lane);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS stores have landed
+    if (lane < 4 && ((fs >> lane) & 1u)) {
+      float sum = 0.f;
+#pragma unroll 16
+      for (int k = 0; k < 64; ++k) {
+        const float4 a = st[wv][0][k], w = st[wv][1 + lane][k];
+        sum = fmaf(a.w, w.w, fmaf(a.z, w.z, fmaf(a.y, w.y, fmaf(a.x, w.x, sum))));
+      }
+      const int c = c0 + lane, dr = ep.rowmap ? ep.rowmap[r] : r;
+      const float v = fmaf(ep.alpha, sum, ep.bias ? ep.bias[c] : 0.f);
       C[(long)r * ldc + c] = fmaxf(v, 0.f) * ep.drop.mul((uint64_t)(ep.row_base + dr) * N + c);
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1011,7 +1036,7 @@ static int rgemm_impl(int M, int N, int K, const void* A, bool ab16, int lda, co
   if ((aux_mode == AUX_ACC_MAP) != (auxmap != nullptr) || (aux_mode == AUX_ACC_MAP && aux == C))
     return (int)hipErrorInvalidValue;
   Epi2 ep{alpha, beta, bias, epilogue == 1, c2::make_drop(k0, k1, epilogue == 1 ? p : 0.f), row_base, aux,
-          aux_scale, rowmap, auxmap, nullptr, nullptr, nullptr, 0.f};
+          aux_scale, rowmap, auxmap, nullptr, nullptr, 0.f};
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -1142,30 +1167,31 @@ C2_API int c2dsr_rg3_stamps(unsigned long long* out, int reset) {
   return (int)e;
 }
 #endif
-// workspace of c2dsr_rgemm_x3_relu_guard: the list length, ‖W[c]‖² [N], the list (every element may be listed)
+// workspace of c2dsr_rgemm_x3_relu_guard: ‖W[c]‖² [N], then the element flags [M][N/4] (zero on entry; every call
+// leaves them zero again, so a workspace zeroed once serves all later calls of the same or smaller M·N)
 C2_API size_t c2dsr_rgemm_guard_workspace(int M, int N) {
-  return 256 + (((size_t)N * 4 + 255) & ~(size_t)255) + (size_t)M * N * 4;
+  return (((size_t)N * 4 + 255) & ~(size_t)255) + (((size_t)M * (N / 4) + 15) & ~(size_t)15);
 }
 
 // linear1 of the fp32 mode (models/encoders.py:23-27 → TransformerEncoderLayer linear1 + relu + dropout):
-// C = drop(relu(A·Wᵀ + bias)) on split-bf16 products (B = the split image of W, K = 256), with every pre-activation
-// within the split error bound of zero recomputed exactly from the fp32 A and W (rg3 GUARD + guard_fix_kernel)
+// C = drop(relu(A·Wᵀ + bias)) on split-bf16 products (B = the split image of W, K = 256), every pre-activation within
+// the split error bound of zero recomputed exactly from the fp32 A and W in k order (rg3 GUARD flags it,
+// guard_fix_kernel recomputes and clears)
 C2_API int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int lda, const void* B, int ldb,
                                      const float* W, float* C, int ldc, const float* bias, uint32_t k0, uint32_t k1,
                                      float p, int64_t row_base, const int* rowmap, void* workspace, size_t ws_bytes,
                                      void* stream) {
-  if (M <= 0 || K != 256 || N % 4 || ldc % 4 || lda % 4 || ldb < 2 * K || ldb % 8 || !W ||
+  // ldb == 0: B is the fragment-ordered split image (c2dsr_to_split_bf16_frag_multi)
+  if (M <= 0 || K != 256 || N % 4 || ldc % 4 || lda % 4 || (ldb != 0 && ldb < 2 * K) || ldb % 8 || !W ||
       !c2dsr_rgemm_supported(M, N, K) || ws_bytes < c2dsr_rgemm_guard_workspace(M, N))
     return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  int* cnt = (int*)ws;
-  float* wn2 = (float*)(ws + 256);
-  int* list = (int*)(ws + 256 + (((size_t)N * 4 + 255) & ~(size_t)255));
-  (void)hipMemsetAsync(cnt, 0, 4, s);
+  float* wn2 = (float*)ws;
+  unsigned char* flags = (unsigned char*)(ws + (((size_t)N * 4 + 255) & ~(size_t)255));
   row_norm2_kernel<<<c2::ceil_div(N, 4), 256, 0, s>>>(W, N, K, wn2);
   Epi2 ep{1.f, 0.f, bias, 1, c2::make_drop(k0, k1, p), row_base, nullptr, 0.f, rowmap, nullptr,
-          wn2, list, cnt, 0x1p-30f};  // tau = 2^-15
+          wn2, flags, 0x1p-30f};  // tau = 2^-15
   static int ncu = 0, per_cu = 0;
   if (!ncu) {
     int dev = 0;
@@ -1173,14 +1199,16 @@ C2_API int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int ld
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu <= 0) ncu = 256;
     int n = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)rg3_kernel<1, true, AUX_NONE, true>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)rg3_kernel<1, true, AUX_NONE, true, RG3_GUARD_NW>,
+                                                       64 * RG3_GUARD_NW, 0);
     per_cu = n > 0 ? n : 1;
   }
   const int G3 = c2::ceil_div(N, 256);
   const int blocks = (ncu * per_cu / 8) * 8;
   if (blocks / 8 < G3) return (int)hipErrorInvalidValue;
-  rg3_kernel<1, true, AUX_NONE, true><<<blocks, 256, 0, s>>>(M, N, A, lda, (const bf16*)B, ldb, C, ldc, ep, G3);
-  guard_fix_kernel<<<256, 256, 0, s>>>(A, lda, W, N, ep, C, ldc);
+  rg3_kernel<1, true, AUX_NONE, true, RG3_GUARD_NW><<<blocks, 64 * RG3_GUARD_NW, 0, s>>>(M, N, A, lda, (const bf16*)B,
+                                                                                         ldb, C, ldc, ep, G3);
+  guard_fix_kernel<<<c2::ceil_div((long)M * (N / 4), 256), 256, 0, s>>>(A, lda, W, M, N, ep, C, ldc);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -214,22 +214,27 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
     return C
 
 
-def rgemm_relu_guard(A, Wimg, W, C, *, M, N, K, bias, relu_drop):
+_GUARD_WS = {}  # device -> the guarded producer's workspace (c2dsr_rgemm_guard_workspace)
+
+
+def rgemm_relu_guard(A, Wimg, W, C, *, M, N, K, bias, relu_drop, frag=False):
     """C = drop(relu(A·Wᵀ + bias)) in the fp32 mode (c2dsr_rgemm_x3_relu_guard): split-bf16 products with every
     pre-activation within the split error bound of zero recomputed exactly from the fp32 A and W (linear1: its
-    ReLU's sign decisions select the dy·x terms of the weight gradient)."""
+    ReLU's sign decisions select the dy·x terms of the weight gradient).  frag: Wimg is the fragment-ordered image."""
     (k0, k1), p, row_base = relu_drop[:3]
     rowmap = relu_drop[3] if len(relu_drop) > 3 else None
     if A.dtype != torch.float32 or W.dtype != torch.float32 or Wimg.shape[-1] != 2 * K:
         raise TypeError('rgemm_relu_guard: fp32 A and W, split image [N, 2K]')
     wsb = int(lib.raw('c2dsr_rgemm_guard_workspace')(M, N))
-    ws = torch.empty(wsb, device=A.device, dtype=torch.uint8)
-    lib('c2dsr_rgemm_x3_relu_guard', M, N, K, A, K, Wimg, 2 * K, W, C, N, bias, k0, k1, float(p), int(row_base), rowmap,
-        ws, wsb, stream())
+    ws = _GUARD_WS.get(A.device)
+    if ws is None or ws.numel() < wsb:  # zeroed once: every call leaves its block flags cleared
+        ws = _GUARD_WS[A.device] = torch.zeros(max(wsb, 1 << 20), device=A.device, dtype=torch.uint8)
+    lib('c2dsr_rgemm_x3_relu_guard', M, N, K, A, K, Wimg, 0 if frag else 2 * K, W, C, N, bias, k0, k1, float(p),
+        int(row_base), rowmap, ws, ws.numel(), stream())
     return C
 
 
-RELU_GUARD = False  # linear1 of the fp32 mode on the guarded split kernel (see LinearFn.forward)
+RELU_GUARD = True  # linear1 of the fp32 mode on the guarded split kernel (see LinearFn.forward)
 
 
 def relu_guard_ok(M, N, K):
@@ -336,13 +341,15 @@ class LinearFn(Function):
         if kind == 'x3' and relu_drop is not None:
             # the ReLU producer (linear1): its sign decisions select which gradient terms exist, so a
             # pre-activation within the split product's rounding (~1e-5 relative) of zero would flip a whole
-            # dy·x term of the weight gradient (tools/fp32_diag.py: 2e-3 vs 1.6e-5 with this product exact) —
-            # it runs on the exact fp32-input MFMA GEMM.  RELU_GUARD: split products with the pre-activations inside
-            # the split error bound recomputed exactly (c2dsr_rgemm_x3_relu_guard) — measured 80.8 → 60.2 µs per
-            # pass, but the reference C2 golden step's linear1 gradient moved from < 1e-4 to 1.2e-4: not the default
+            # dy·x term of the weight gradient (tools/fp32_diag.py: 2e-3 vs 1.6e-5 with this product exact).
+            # RELU_GUARD (default): split products, every pre-activation inside the split error bound recomputed as
+            # a k-ordered fp32 FMA chain (c2dsr_rgemm_x3_relu_guard; the order decides the reference C2 step's
+            # ties: a float64-exact product misses it by 1.2e-4, tools/linear1_emu.py) — 105 → 60 µs at 57k rows;
+            # otherwise the exact fp32-input MFMA GEMM
             kind = None
             if RELU_GUARD and relu_guard_ok(M, N, K):
-                rgemm_relu_guard(x, weight_img(W, 'x3row'), W, y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop)
+                rgemm_relu_guard(x, weight_img(W, 'x3'), W, y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop,
+                                 frag=True)
                 kind = 'guard'
         if kind == 'guard':
             pass

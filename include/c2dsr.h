@@ -369,9 +369,11 @@ int c2dsr_rgemm_x3f(int M, int N, int K, const float* A, int lda, const void* B,
                     void* stream);
 /* linear1 + ReLU + dropout of the fp32 mode (replaces models/encoders.py:23-27 → TransformerEncoderLayer
  * linear1 / activation / dropout): C = drop(relu(A·Wᵀ + bias)) on split-bf16 products (B = the split image of the
- * fp32 weight W [N][256], K = 256), every pre-activation within the split error bound of zero (|v| ≤ 2^-15·‖a‖‖w‖)
- * recomputed exactly from A and W, so the ReLU's sign decisions are those of an fp32 product.  Dropout index
- * (row_base + (rowmap ? rowmap[r] : r))·N + c, as c2dsr_rgemm's epilogue 1.  workspace: guard_workspace bytes. */
+ * fp32 weight W [N][256], ldb >= 2K, or its fragment-ordered image, ldb = 0; K = 256, N % 4 == 0), every
+ * pre-activation within the split error bound of zero (|v| ≤ 2^-15·‖a‖‖w‖) recomputed from A and W as one fp32 FMA
+ * chain in k order, so the ReLU's sign decisions are those of a k-sequential fp32 product.  Dropout index
+ * (row_base + (rowmap ? rowmap[r] : r))·N + c, as c2dsr_rgemm's epilogue 1.  workspace: guard_workspace bytes,
+ * zero-filled before its first use (each call leaves it reusable: the flags are cleared as they are consumed). */
 size_t c2dsr_rgemm_guard_workspace(int M, int N);
 int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int lda, const void* B, int ldb, const float* W,
                               float* C, int ldc, const float* bias, uint32_t k0, uint32_t k1, float p, int64_t row_base,

@@ -213,7 +213,7 @@ def test_rgemm_x3_relu_dropout_epilogue():
     assert rel(C, ref) < TOL
 
 
-@pytest.mark.parametrize('M,rowmap', [(4099, False), (1000, True)])
+@pytest.mark.parametrize('M,rowmap', [(4099, False), (1000, True), (57000, False), (40000, True)])
 def test_rgemm_x3_relu_guard_signs(M, rowmap):
     """linear1 of the fp32 mode (c2dsr_rgemm_x3_relu_guard): split products with every pre-activation within
     the split error bound of zero recomputed exactly.  Inputs are built so that one column per row has a
@@ -246,7 +246,11 @@ def test_rgemm_x3_relu_guard_signs(M, rowmap):
     rgemm_relu_guard(A32.to(DEV), Wx, W32.to(DEV), C, M=M, N=N, K=K, bias=b.float().to(DEV), relu_drop=rd)
     C0 = torch.empty(M, N, device=DEV)
     rgemm(A32.to(DEV), Wx, C0, M=M, N=N, K=K, bias=b.float().to(DEV), relu_drop=rd, x3=True)
+    Cf = torch.empty(M, N, device=DEV)  # the fragment-ordered image the training step uses: bit-identical
+    rgemm_relu_guard(A32.to(DEV), to_split_bf16(W32.to(DEV), frag=True), W32.to(DEV), Cf, M=M, N=N, K=K,
+                     bias=b.float().to(DEV), relu_drop=rd, frag=True)
     torch.cuda.synchronize()
+    assert torch.equal(C, Cf)
     clear = (v.abs() > 2e-7 * scale) & (mk > 0)
     got, plain = C.double().cpu(), C0.double().cpu()
     assert torch.equal((got > 0)[clear], (v > 0)[clear])

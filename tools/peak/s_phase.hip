@@ -23,13 +23,22 @@ __device__ __forceinline__ void tri(f32x4& acc, const bf16x8& ah, const bf16x8& 
       : "+v"(acc)
       : "v"(ah), "v"(al), "a"(bh), "a"(bl));
 }
+__device__ __forceinline__ void tri_a(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& bh,
+                                      const bf16x8& bl) {  // accumulator in AGPRs (VGPR ports free for VALU / DS)
+  asm volatile(
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_bf16 %0, %1, %4, %0"
+      : "+a"(acc)
+      : "v"(ah), "v"(al), "a"(bh), "a"(bl));
+}
 __device__ __forceinline__ void one(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
 }
 
 #define MFB(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
 // PD: prefetch distance of the reads (steps); BI: compiler-visible MFMAs, one read / VALU group per MFMA gap
-template <bool R, bool V, bool C, bool I, int PD = 2, bool BI = false>
+template <bool R, bool V, bool C, bool I, int PD = 2, bool BI = false, bool ACCA = false>
 __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigned long long* cyc) {
   __shared__ __attribute__((aligned(16))) char img[65536];
   const int lane = threadIdx.x & 63;
@@ -90,7 +99,7 @@ __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigne
         one(s4, b, bh1);
         one(s5, a, bl1);
       } else {
-        tri(s0, a, b, bh0, bl0);
+        if constexpr (ACCA) tri_a(s0, a, b, bh0, bl0); else tri(s0, a, b, bh0, bl0);
         if constexpr (V) {
           __builtin_amdgcn_sched_barrier(0);
           const float p = __builtin_amdgcn_exp2f(sc - m);
@@ -112,7 +121,7 @@ __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigne
             __builtin_amdgcn_sched_barrier(0);
           }
         }
-        tri(s1, a, b, bh1, bl1);
+        if constexpr (ACCA) tri_a(s1, a, b, bh1, bl1); else tri(s1, a, b, bh1, bl1);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -124,15 +133,15 @@ __global__ __launch_bounds__(256, 1) void s_phase(int iters, float* out, unsigne
   if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <bool R, bool V, bool C, bool I, int PD = 2, bool BI = false>
+template <bool R, bool V, bool C, bool I, int PD = 2, bool BI = false, bool ACCA = false>
 void run(const char* name, int iters, float* out, unsigned long long* cyc, int ncu) {
-  s_phase<R, V, C, I, PD, BI><<<ncu, 256>>>(iters, out, cyc);
+  s_phase<R, V, C, I, PD, BI, ACCA><<<ncu, 256>>>(iters, out, cyc);
   hipDeviceSynchronize();
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   hipEventRecord(e0);
-  s_phase<R, V, C, I, PD, BI><<<ncu, 256>>>(iters, out, cyc);
+  s_phase<R, V, C, I, PD, BI, ACCA><<<ncu, 256>>>(iters, out, cyc);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0.f;
@@ -168,5 +177,9 @@ int main(int argc, char** argv) {
   run<true, false, false, false, 2, true>("BI +reads", iters, out, cyc, ncu);
   run<true, true, false, false, 2, true>("BI +reads+valu", iters, out, cyc, ncu);
   run<true, true, false, false, 4, true>("BI +reads+valu pd4", iters, out, cyc, ncu);
+  run<true, false, false, false, 2, false, true>("accA +reads", iters, out, cyc, ncu);
+  run<false, true, false, false, 2, false, true>("accA +valu", iters, out, cyc, ncu);
+  run<true, true, false, false, 2, false, true>("accA +reads+valu", iters, out, cyc, ncu);
+  run<true, true, true, false, 2, false, true>("accA +reads+valu+burst", iters, out, cyc, ncu);
   return 0;
 }
