@@ -126,6 +126,18 @@ __device__ __forceinline__ float quad_sum(float x) {
 #ifndef CE3_BI1
 #define CE3_BI1 CE3_BI
 #endif
+#ifndef CE3_BIS0  // the S phase only (MODE 0 / MODE 1), and the second-product phase only
+#define CE3_BIS0 0
+#endif
+#ifndef CE3_BIS1
+#define CE3_BIS1 0
+#endif
+#ifndef CE3_BIU0  // default: the second product on builtin MFMAs (fwd_u 2676 → 2590 µs, dw −1 % at MB head-b shapes)
+#define CE3_BIU0 1
+#endif
+#ifndef CE3_BIU1
+#define CE3_BIU1 1
+#endif
 #ifndef CE3_VN
 #define CE3_VN 5
 #endif
@@ -245,9 +257,11 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   // one LDS-DMA wave-instruction of tile t+3 every DQ second-product steps, from the first (DQ = 1: the whole
   // tile at the start of the phase, the longest time to land before the barrier that publishes it)
   constexpr int DQ = SPLIT ? CE3_DQ : CE3B_DQ;
-  constexpr bool BI = SPLIT && (MODE == 0 ? CE3_BI0 : CE3_BI1);  // builtin MFMA form for this role
-  // ILV (asm form): the step's VALU work between its stationary blocks' products; the builtin form is scheduled
-  constexpr bool ILV = SPLIT ? !BI : CE3B_ILV;
+  // builtin MFMA form per role and phase (S: the first product, U: the second); ILV (asm form): the step's VALU work
+  // between its stationary blocks' products — the builtin form is scheduled by step_pattern instead
+  constexpr bool BIS = SPLIT && (MODE == 0 ? CE3_BI0 || CE3_BIS0 : CE3_BI1 || CE3_BIS1);
+  constexpr bool BIU = SPLIT && (MODE == 0 ? CE3_BI0 || CE3_BIU0 : CE3_BI1 || CE3_BIU1);
+  constexpr bool ILVS = SPLIT ? !BIS : CE3B_ILV, ILVU = SPLIT ? !BIU : CE3B_ILV;
   static_assert(DQ >= 1 && DQ * NDMA <= NUS, "DMA spacing");
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
   __shared__ __attribute__((aligned(16))) float wv[NB][NW][64];
@@ -362,9 +376,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     auto s_prod = [&]<int KSI>(f32x4& acc, const bf16x8(&a)[2], int sb) {
       if constexpr (SPLIT) {
         if constexpr (KSI == 0)
-          split3_s0<BI>(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
+          split3_s0<BIS>(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
         else
-          split3_s<BI>(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
+          split3_s<BIS>(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
       } else {
         if constexpr (KSI == 0)
           mf1_s0(acc, a[0], fh[sb][KSI]);
@@ -485,7 +499,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
               // ILV: the step's VALU work between its two stationary blocks' products (each MFMA's shadow
               // covers half of it; in-order issue otherwise stalls it behind the second MFMA)
               s_prod.template operator()<k / CB>(sn[cb * SBW], fa[k % (DS + 2)], 0);
-              if constexpr (ILV || SBW == 1) __builtin_amdgcn_sched_barrier(0);
+              if constexpr (ILVS || SBW == 1) __builtin_amdgcn_sched_barrier(0);
               else s_prod.template operator()<k / CB>(sn[cb * SBW + 1], fa[k % (DS + 2)], 1);
               constexpr int ib = (k * NEL + NSS - 1) / NSS, ie = ((k + 1) * NEL + NSS - 1) / NSS;
 #pragma unroll
@@ -507,11 +521,11 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 xh[u][sb] = h;
                 if constexpr (SPLIT) xl[u][sb] = l;
               }
-              if constexpr (ILV && SBW == 2) {
+              if constexpr (ILVS && SBW == 2) {
                 __builtin_amdgcn_sched_barrier(0);
                 s_prod.template operator()<k / CB>(sn[cb * SBW + 1], fa[k % (DS + 2)], 1);
               }
-              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BI>();
+              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BIS>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
@@ -549,12 +563,12 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
               const bf16x8(&tq)[2] = tf[k % (DT + 2)];
               auto u_prod = [&](int sb) {
                 if constexpr (SPLIT)
-                  split3_u<BI>(dacc[q][sb], tq[0], tq[1], xh[u][sb], xl[u][sb]);
+                  split3_u<BIU>(dacc[q][sb], tq[0], tq[1], xh[u][sb], xl[u][sb]);
                 else
                   mf1_u(dacc[q][sb], tq[0], xh[u][sb]);
               };
               u_prod(0);
-              if constexpr (ILV || SBW == 1) __builtin_amdgcn_sched_barrier(0);
+              if constexpr (ILVU || SBW == 1) __builtin_amdgcn_sched_barrier(0);
               else u_prod(1);
               if constexpr (k % DQ == DQ - 1 && k / DQ < NDMA)
                 dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
@@ -567,11 +581,11 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 sn[cb * SBW + sb][r] = v;
                 tm[sb] = fmaxf(tm[sb], v);
               }
-              if constexpr (ILV && SBW == 2) {
+              if constexpr (ILVU && SBW == 2) {
                 __builtin_amdgcn_sched_barrier(0);
                 u_prod(1);
               }
-              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BI>();
+              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BIU>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
