@@ -962,8 +962,9 @@ __global__ void row_norm2_kernel(const float* __restrict__ W, int N, int K, floa
 // each dot product one fp32 FMA chain in k order — the order of a k-sequential fp32 GEMM, so a pre-activation within
 // fp32 rounding of zero gets that GEMM's sign (tools/linear1_emu.py: a float64-exact product misses the reference's C2
 // step by 1.2e-4 on linear1's weight gradient through one such tie; this order matches it).  One wave per 64 flag bytes
-// (a byte = a 4-column group of one row); per flagged byte the wave stages the row of A and the 4 weight rows in LDS
-// with coalesced loads and lanes 0..3 run the chains of the group's 4 columns from there.  The flags are cleared.
+// (a byte = a 4-column group of one row: flagged bytes are rare, so each wave sees one at most, usually); per flagged
+// byte the wave stages the row of A and the 4 weight rows in LDS with coalesced loads and lanes 0..3 run the chains of
+// the group's 4 columns from there.  The flags are cleared.
 __global__ __launch_bounds__(256) void guard_fix_kernel(const float* __restrict__ A, long lda,
                                                         const float* __restrict__ W, int M, int N, Epi2 ep,
                                                         float* __restrict__ C, long ldc) {
@@ -1178,9 +1179,9 @@ C2_API size_t c2dsr_rgemm_guard_workspace(int M, int N) {
 // the split error bound of zero recomputed exactly from the fp32 A and W in k order (rg3 GUARD flags it,
 // guard_fix_kernel recomputes and clears)
 C2_API int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int lda, const void* B, int ldb,
-                                     const float* W, float* C, int ldc, const float* bias, uint32_t k0, uint32_t k1,
-                                     float p, int64_t row_base, const int* rowmap, void* workspace, size_t ws_bytes,
-                                     void* stream) {
+                                     const float* W, const float* wn2_in, float* C, int ldc, const float* bias,
+                                     uint32_t k0, uint32_t k1, float p, int64_t row_base, const int* rowmap,
+                                     void* workspace, size_t ws_bytes, void* stream) {
   // ldb == 0: B is the fragment-ordered split image (c2dsr_to_split_bf16_frag_multi)
   if (M <= 0 || K != 256 || N % 4 || ldc % 4 || lda % 4 || (ldb != 0 && ldb < 2 * K) || ldb % 8 || !W ||
       !c2dsr_rgemm_supported(M, N, K) || ws_bytes < c2dsr_rgemm_guard_workspace(M, N))
@@ -1189,9 +1190,9 @@ C2_API int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int ld
   char* ws = (char*)workspace;
   float* wn2 = (float*)ws;
   unsigned char* flags = (unsigned char*)(ws + (((size_t)N * 4 + 255) & ~(size_t)255));
-  row_norm2_kernel<<<c2::ceil_div(N, 4), 256, 0, s>>>(W, N, K, wn2);
+  if (!wn2_in) row_norm2_kernel<<<c2::ceil_div(N, 4), 256, 0, s>>>(W, N, K, wn2);
   Epi2 ep{1.f, 0.f, bias, 1, c2::make_drop(k0, k1, p), row_base, nullptr, 0.f, rowmap, nullptr,
-          wn2, flags, 0x1p-30f};  // tau = 2^-15
+          wn2_in ? wn2_in : wn2, flags, 0x1p-30f};  // tau = 2^-15
   static int ncu = 0, per_cu = 0;
   if (!ncu) {
     int dev = 0;

@@ -127,10 +127,15 @@ class _WeightImages:
                 lib(fn, desc.ctypes.data, len(chunk), stream())
             for key, W, y in done:
                 self.cache[key] = ((self.epoch, W._version), y, W)
+        for key, (W, y) in self.known.items():
+            if key[3] == 'norm2':
+                torch.sum(W * W, 1, out=y)
+                self.cache[key] = ((self.epoch, W._version), y, W)
         self.known = {}
 
     def get(self, W, trans, layout=None):
-        """layout None: bf16 image; 'split': split image hi ‖ lo; 'frag': the split image in rg3's fragment order."""
+        """layout None: bf16 image; 'split': split image hi ‖ lo; 'frag': the split image in rg3's fragment order;
+        'norm2': the squared row norms ‖W[r]‖² (the guarded linear1's threshold)."""
         key = (W.data_ptr(), tuple(W.shape), bool(trans), layout)
         tag = (self.epoch, W._version)
         if key not in self.cache and key in self.known:
@@ -138,7 +143,10 @@ class _WeightImages:
         hit = self.cache.get(key)
         if hit is not None and hit[0] == tag:
             return hit[1]
-        y = to_bf16(W, trans) if layout is None else to_split_bf16(W, trans, frag=layout == 'frag')
+        if layout == 'norm2':  # ‖W[r]‖² [R] (torch's fixed-order reduction)
+            y = (W * W).sum(1)
+        else:
+            y = to_bf16(W, trans) if layout is None else to_split_bf16(W, trans, frag=layout == 'frag')
         self.cache[key] = (tag, y, W)
         return y
 
@@ -217,10 +225,11 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
 _GUARD_WS = {}  # device -> the guarded producer's workspace (c2dsr_rgemm_guard_workspace)
 
 
-def rgemm_relu_guard(A, Wimg, W, C, *, M, N, K, bias, relu_drop, frag=False):
+def rgemm_relu_guard(A, Wimg, W, C, *, M, N, K, bias, relu_drop, frag=False, wn2=None):
     """C = drop(relu(A·Wᵀ + bias)) in the fp32 mode (c2dsr_rgemm_x3_relu_guard): split-bf16 products with every
     pre-activation within the split error bound of zero recomputed exactly from the fp32 A and W (linear1: its
-    ReLU's sign decisions select the dy·x terms of the weight gradient).  frag: Wimg is the fragment-ordered image."""
+    ReLU's sign decisions select the dy·x terms of the weight gradient).  frag: Wimg is the fragment-ordered image;
+    wn2: ‖W[c]‖² [N] kept per weight update (weight_norm2), else computed in the call."""
     (k0, k1), p, row_base = relu_drop[:3]
     rowmap = relu_drop[3] if len(relu_drop) > 3 else None
     if A.dtype != torch.float32 or W.dtype != torch.float32 or Wimg.shape[-1] != 2 * K:
@@ -229,7 +238,7 @@ def rgemm_relu_guard(A, Wimg, W, C, *, M, N, K, bias, relu_drop, frag=False):
     ws = _GUARD_WS.get(A.device)
     if ws is None or ws.numel() < wsb:  # zeroed once: every call leaves its block flags cleared
         ws = _GUARD_WS[A.device] = torch.zeros(max(wsb, 1 << 20), device=A.device, dtype=torch.uint8)
-    lib('c2dsr_rgemm_x3_relu_guard', M, N, K, A, K, Wimg, 0 if frag else 2 * K, W, C, N, bias, k0, k1, float(p),
+    lib('c2dsr_rgemm_x3_relu_guard', M, N, K, A, K, Wimg, 0 if frag else 2 * K, W, wn2, C, N, bias, k0, k1, float(p),
         int(row_base), rowmap, ws, ws.numel(), stream())
     return C
 
@@ -349,7 +358,7 @@ class LinearFn(Function):
             kind = None
             if RELU_GUARD and relu_guard_ok(M, N, K):
                 rgemm_relu_guard(x, weight_img(W, 'x3'), W, y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop,
-                                 frag=True)
+                                 frag=True, wn2=WEIGHTS.get(W.detach(), False, layout='norm2'))
                 kind = 'guard'
         if kind == 'guard':
             pass

@@ -373,11 +373,12 @@ int c2dsr_rgemm_x3f(int M, int N, int K, const float* A, int lda, const void* B,
  * pre-activation within the split error bound of zero (|v| ≤ 2^-15·‖a‖‖w‖) recomputed from A and W as one fp32 FMA
  * chain in k order, so the ReLU's sign decisions are those of a k-sequential fp32 product.  Dropout index
  * (row_base + (rowmap ? rowmap[r] : r))·N + c, as c2dsr_rgemm's epilogue 1.  workspace: guard_workspace bytes,
- * zero-filled before its first use (each call leaves it reusable: the flags are cleared as they are consumed). */
+ * zero-filled before its first use (each call leaves it reusable: the flags are cleared as they are consumed).
+ * wn2: the squared row norms ‖W[c]‖² [N] if the caller keeps them per weight update, or null (computed here). */
 size_t c2dsr_rgemm_guard_workspace(int M, int N);
 int c2dsr_rgemm_x3_relu_guard(int M, int N, int K, const float* A, int lda, const void* B, int ldb, const float* W,
-                              float* C, int ldc, const float* bias, uint32_t k0, uint32_t k1, float p, int64_t row_base,
-                              const int* rowmap, void* workspace, size_t ws_bytes, void* stream);
+                              const float* wn2, float* C, int ldc, const float* bias, uint32_t k0, uint32_t k1, float p,
+                              int64_t row_base, const int* rowmap, void* workspace, size_t ws_bytes, void* stream);
 /* ... and the weight-gradient products (c2dsr_wgemm / _multi contract, dY fp32) */
 int c2dsr_wgemm_x3(int T, int N, int D, const float* dY, int ldy, const float* X, int ldx, float beta, float* dW,
                    float* db, void* part, void* stream);
