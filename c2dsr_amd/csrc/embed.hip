@@ -739,8 +739,8 @@ int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t
     t = vi; vi = vo; vo = t;
   }
   if (ki != w.k0) {  // (not taken: the start pair makes the last pass land in k0 / v0)
-    hipMemcpyAsync(w.k0, ki, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
-    hipMemcpyAsync(w.v0, vi, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(w.k0, ki, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+    (void)hipMemcpyAsync(w.v0, vi, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
   }
   const int pb = c2::ceil_div(n, PL_B);
   plan_count_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt);
@@ -754,8 +754,8 @@ int g_ncu = 0;
 int num_cus() {
   if (!g_ncu) {
     int dev = 0, v = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
     g_ncu = v > 0 ? v : 256;
   }
   return g_ncu;
@@ -1002,7 +1002,7 @@ C2_API int c2dsr_ce_onehot_dw_planned(const void* plan, int M, int n, const floa
   }
   if (gb) {
     float* T = (float*)(seg + seg_ws_bytes(M, D));
-    hipMemsetAsync(T, 0, (size_t)n * 16, s);
+    (void)hipMemsetAsync(T, 0, (size_t)n * 16, s);
     const SegJob j = seg_job(p, M, n + 1, RowSrc{nullptr, 4, nodrop, 0, -1.f, rw}, T, seg, n);
     seg_dispatch(j, nullptr, s);
     col0_add_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(T, n, gb);
