@@ -110,7 +110,10 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
     const int col = min(ncol0 + ct * 32 + (lane & 31), N - 1);
 #pragma unroll
     for (int ks = 0; ks < KCH * 16; ++ks) {
-      bq[ct][ks] = *(const bf16x8*)(B + (long)col * ldb + ks * 16 + 8 * (lane >> 5));
+      if (!X3 && ldb == 0)  // fragment-ordered bf16 image (b16_frag_index): one coalesced 1 KiB piece per load
+        bq[ct][ks] = *(const bf16x8*)(B + (((long)(min(ncol0 + ct * 32, N - 1) >> 5) * (K / 16) + ks) * 64 + lane) * 8);
+      else
+        bq[ct][ks] = *(const bf16x8*)(B + (long)col * ldb + ks * 16 + 8 * (lane >> 5));
       if constexpr (X3) bl[ct][ks] = *(const bf16x8*)(B + (long)col * ldb + K + ks * 16 + 8 * (lane >> 5));
     }
     bcol[ct] = ep.bias ? ep.bias[col] : 0.f;
@@ -343,6 +346,12 @@ __global__ __launch_bounds__(256) void rg_kernel(int M, int N, int K, const void
 __host__ __device__ __forceinline__ long split_frag_index(int col, int k, int hl, int K) {
   const long piece = (long)(col >> 4) * (K / 16) + 2 * (k >> 5) + hl;
   return (piece * 64 + ((k >> 3) & 3) * 16 + (col & 15)) * 8 + (k & 7);
+}
+// The same for a bf16 weight image and rg_kernel (the bf16 mode: 32x32 fragments, lane (j = l % 32, kh = l / 32)
+// holds column 32ct + j, k = 16ks + 8kh .. +7): piece (32-column block, k-step of 16) = one 1 KiB wave load.
+__host__ __device__ __forceinline__ long b16_frag_index(int col, int k, int K) {
+  const long piece = (long)(col >> 5) * (K / 16) + (k >> 4);
+  return (piece * 64 + ((k >> 3) & 1) * 32 + (col & 31)) * 8 + (k & 7);
 }
 __device__ __forceinline__ void x3_0(f32x4& acc, const bf16x8& wh, const bf16x8& wl, const bf16x8& ah,
                                      const bf16x8& al) {
@@ -1386,6 +1395,9 @@ __global__ __launch_bounds__(256) void to_bf16_multi_kernel(MultiBf16 m) {
       m.y[lo][(long)orow * 2 * CC + ocol] = v;
       m.y[lo][(long)orow * 2 * CC + CC + ocol] = l;
     }
+  } else if constexpr (FRAG) {  // rg_kernel's fragment order (b16_frag_index)
+    const int CC = m.tr[lo] ? R : Cc;
+    m.y[lo][b16_frag_index(m.tr[lo] ? c : r, m.tr[lo] ? r : c, CC)] = v;
   } else if (m.tr[lo]) {
     m.y[lo][(long)c * R + r] = v;
   } else {
@@ -1415,10 +1427,14 @@ static int to_bf16_multi_impl(const int64_t* desc, int count, void* stream, bool
   }
   if (m.bstart[count] == 0) return 0;
   for (int k = count + 1; k <= MULTI_MAX; ++k) m.bstart[k] = m.bstart[count];
-  if (frag) {
+  if (frag && split) {
     for (int k = 0; k < count; ++k)  // rg3's fragment order: K (the image's reduction width) 256 or 512
       if ((m.tr[k] ? m.R[k] : m.C[k]) % 256 || (m.tr[k] ? m.R[k] : m.C[k]) > 512) return (int)hipErrorInvalidValue;
     to_bf16_multi_kernel<true, true><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
+  } else if (frag) {
+    for (int k = 0; k < count; ++k)  // rg_kernel's fragment order: K 256, 512 or 768
+      if ((m.tr[k] ? m.R[k] : m.C[k]) % 256 || (m.tr[k] ? m.R[k] : m.C[k]) > 768) return (int)hipErrorInvalidValue;
+    to_bf16_multi_kernel<false, true><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
   } else if (split)
     to_bf16_multi_kernel<true><<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
   else
@@ -1432,6 +1448,10 @@ C2_API int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream) {
 // the split-bf16 images (y = [R][2·Cc] hi ‖ lo, or [Cc][2·R] transposed) of a list of matrices in one launch
 C2_API int c2dsr_to_split_bf16_multi(const int64_t* desc, int count, void* stream) {
   return to_bf16_multi_impl(desc, count, stream, true);
+}
+// bf16 images in rg_kernel's fragment order (c2dsr_rgemm* with ldb = 0): ⌈N'/32⌉·32 × K' bf16 per matrix
+C2_API int c2dsr_to_bf16_frag_multi(const int64_t* desc, int count, void* stream) {
+  return to_bf16_multi_impl(desc, count, stream, false, true);
 }
 // the same values in rg3's fragment order (c2dsr_rgemm_x3f's B): ⌈N'/16⌉·16 × 2K' bf16 per matrix, N' / K' = the
 // output rows / columns (Cc / R when transposed); rows past N' are not written

@@ -129,7 +129,7 @@ class LossHeadFn(Function):
             kind = rg_kind(m.precision, 2 * B, d, d)
             if kind:  # the row-streaming MFMA GEMM (bf16 or split-bf16 operands)
                 rgemm(X2, weight_img(Wd.view(d, d), kind), U, M=2 * B, N=d, K=d, x3=kind == 'x3',
-                      frag=kind == 'x3')
+                      frag=True)
             else:
                 gemm(X2, Wd, U, M=2 * B, N=d, K=d, transB=1, precision=FP32)
         S = torch.empty(4, B, **f32)
@@ -376,7 +376,7 @@ class LossHeadFn(Function):
             b16 = kind is not None and wg_kind(m.precision, 2 * B, d, d) is not None
             if b16:
                 rgemm(dU, weight_img(Wd.view(d, d), kind, trans=True), dX2, M=2 * B, N=d, K=d, x3=kind == 'x3',
-                      frag=kind == 'x3')
+                      frag=True)
             else:
                 gemm(dU, Wd, dX2, M=2 * B, N=d, K=d, precision=FP32)
             gWd = _grad_target(Wd)

@@ -113,7 +113,7 @@ class _WeightImages:
 
     def _refresh_known(self):
         for layout, fn in ((None, 'c2dsr_to_bf16_multi'), ('split', 'c2dsr_to_split_bf16_multi'),
-                           ('frag', 'c2dsr_to_split_bf16_frag_multi')):
+                           ('frag', 'c2dsr_to_split_bf16_frag_multi'), ('b16frag', 'c2dsr_to_bf16_frag_multi')):
             recs, done = [], []
             for key, (W, y) in self.known.items():
                 if key[3] != layout:
@@ -134,8 +134,9 @@ class _WeightImages:
         self.known = {}
 
     def get(self, W, trans, layout=None):
-        """layout None: bf16 image; 'split': split image hi ‖ lo; 'frag': the split image in rg3's fragment order;
-        'norm2': the squared row norms ‖W[r]‖² (the guarded linear1's threshold)."""
+        """layout None: bf16 image; 'b16frag': the bf16 image in rg_kernel's fragment order; 'split': split image
+        hi ‖ lo; 'frag': the split image in rg3's fragment order; 'norm2': the squared row norms ‖W[r]‖² (the guarded
+        linear1's threshold)."""
         key = (W.data_ptr(), tuple(W.shape), bool(trans), layout)
         tag = (self.epoch, W._version)
         if key not in self.cache and key in self.known:
@@ -145,6 +146,12 @@ class _WeightImages:
             return hit[1]
         if layout == 'norm2':  # ‖W[r]‖² [R] (torch's fixed-order reduction)
             y = (W * W).sum(1)
+        elif layout == 'b16frag':
+            R, Cc = W.shape
+            rows, cols = (Cc, R) if trans else (R, Cc)
+            y = torch.zeros(-(-rows // 32) * 32, cols, device=W.device, dtype=torch.bfloat16)
+            desc = np.asarray([W.data_ptr(), y.data_ptr(), R, Cc, W.stride(0), int(trans)], dtype=np.int64)
+            lib('c2dsr_to_bf16_frag_multi', desc.ctypes.data, 1, stream())
         else:
             y = to_bf16(W, trans) if layout is None else to_split_bf16(W, trans, frag=layout == 'frag')
         self.cache[key] = (tag, y, W)
@@ -159,10 +166,10 @@ def weight_bf16(W, trans=False):
 
 
 def weight_img(W, kind, trans=False):
-    """The operand image of a projection weight for a rg_kind kernel: bf16 [R][C] ('b16'), the split image in the
-    row-streaming kernel's fragment order ('x3': rgemm(..., x3=True, frag=True)) or as rows [R][2C] = hi ‖ lo
-    ('x3row'); transposed ([C][…]) if asked."""
-    layout = {'b16': None, 'x3': 'frag', 'x3row': 'split'}[kind]
+    """The operand image of a projection weight for a rg_kind kernel, in the row-streaming kernels' fragment order
+    (rgemm(..., frag=True)): bf16 ('b16') or split hi ‖ lo ('x3'); or the split image as rows [R][2C] ('x3row');
+    transposed ([C][…]) if asked."""
+    layout = {'b16': 'b16frag', 'x3': 'frag', 'x3row': 'split'}[kind]
     return WEIGHTS.get(W.detach(), trans, layout=layout)
 
 
@@ -188,7 +195,7 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
     """C = alpha·A·Bbᵀ + beta·C + bias with A fp32 [M, K], Bb bf16 [N, K] (c2dsr_rgemm); aux_mode
     AUX_ACC: C += aux (aux may be C itself), AUX_MASK: C = aux > 0 ? C·aux_scale : 0 (c2dsr_rgemm_aux).
     x3: Bb is the split image [N, 2K] and the products run on split-bf16 operands (c2dsr_rgemm_x3); frag: Bb is
-    that image in fragment order (to_split_bf16(..., frag=True), c2dsr_rgemm_x3f)."""
+    the (bf16 or split) image in the kernel's fragment order (weight_img; c2dsr_rgemm_x3f, or ldb = 0)."""
     k0 = k1 = 0
     p = 0.0
     row_base = 0
@@ -211,14 +218,14 @@ def rgemm(A, Bb, C, *, M, N, K, alpha=1.0, beta=0.0, bias=None, relu_drop=None, 
     elif A.dtype == torch.bfloat16:  # the attention backward's bf16 dqkv (in_proj dX; c2dsr_rgemm_aux_b16a)
         if epi or aux_mode == AUX_MASK:
             raise HipLibError('rgemm: bf16 A supports no epilogue / mask mode')
-        lib('c2dsr_rgemm_aux_b16a', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, int(aux_mode), aux,
-            auxmap, stream())
+        lib('c2dsr_rgemm_aux_b16a', M, N, K, A, K, Bb, 0 if frag else K, C, N, float(alpha), float(beta), bias,
+            int(aux_mode), aux, auxmap, stream())
     elif aux_mode:
-        lib('c2dsr_rgemm_aux', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
-            int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
+        lib('c2dsr_rgemm_aux', M, N, K, A, K, Bb, 0 if frag else K, C, N, float(alpha), float(beta), bias, epi, k0, k1,
+            float(p), int(row_base), rowmap, int(aux_mode), aux, auxmap, float(aux_scale), stream())
     else:
-        lib('c2dsr_rgemm', M, N, K, A, K, Bb, K, C, N, float(alpha), float(beta), bias, epi, k0, k1, float(p),
-            int(row_base), rowmap, stream())
+        lib('c2dsr_rgemm', M, N, K, A, K, Bb, 0 if frag else K, C, N, float(alpha), float(beta), bias, epi, k0, k1,
+            float(p), int(row_base), rowmap, stream())
     return C
 
 
@@ -364,7 +371,7 @@ class LinearFn(Function):
             pass
         elif kind:
             rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, relu_drop=relu_drop, x3=kind == 'x3',
-                  frag=kind == 'x3')
+                  frag=True)
         else:
             gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, relu_drop=relu_drop, precision=precision)
         ctx.save_for_backward(x, W, y if relu_drop is not None else None)
@@ -408,17 +415,18 @@ def linear_backward(ctx, x, W, y, dy, need_dx):
             park, sub = full, False
         if sub:  # dx = dy·W + the parked rows, read through the row map
             dx = torch.empty_like(x)
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park, auxmap=ctx.res.inv, x3=x3, frag=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC_MAP, aux=park, auxmap=ctx.res.inv, x3=x3, frag=True)
         elif fused and park is not None:  # dx = parked LN gradient + dy·W, in place
             dx = park
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx, x3=x3, frag=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_ACC, aux=dx, x3=x3, frag=True)
         elif fused and ctx.ff is not None and ctx.ff_role == 'out':  # linear1's drop(relu) backward here
             dx = torch.empty_like(x)
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x, aux_scale=1.0 / (1.0 - ctx.ff.p), x3=x3, frag=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, aux_mode=AUX_MASK, aux=x, aux_scale=1.0 / (1.0 - ctx.ff.p), x3=x3,
+                  frag=True)
             ctx.ff.premasked = True
         elif fused:
             dx = torch.empty_like(x)
-            rgemm(dy, Wt, dx, M=M, N=K, K=N, x3=x3, frag=x3)
+            rgemm(dy, Wt, dx, M=M, N=K, K=N, x3=x3, frag=True)
         elif park is not None:
             dx = park
             gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0, precision=ctx.precision)
@@ -1111,7 +1119,7 @@ class QKVAttnFn(Function):
         qkv = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
         kind = rg_kind(precision, M, N, K)
         if kind:
-            rgemm(x, weight_img(W, kind), qkv, M=M, N=N, K=K, bias=b, x3=kind == 'x3', frag=kind == 'x3')
+            rgemm(x, weight_img(W, kind), qkv, M=M, N=N, K=K, bias=b, x3=kind == 'x3', frag=True)
         else:
             gemm(x, W, qkv, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
         B, L, d3 = qkv.shape
@@ -1161,7 +1169,7 @@ def _proj(x, W, b, y, precision):
         return y
     kind = rg_kind(precision, M, N, K)
     if kind:
-        rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, x3=kind == 'x3', frag=kind == 'x3')
+        rgemm(x, weight_img(W, kind), y, M=M, N=N, K=K, bias=b, x3=kind == 'x3', frag=True)
     else:
         gemm(x, W, y, M=M, N=N, K=K, transB=1, bias=b, precision=precision)
     return y
@@ -1177,7 +1185,7 @@ def _proj_backward(x, W, dy, dx, acc, gW, gb, precision):
     kind = rg_kind(precision, M, K, N)
     if kind:
         rgemm(dy, weight_img(W, kind, trans=True), dx, M=M, N=K, K=N, aux_mode=AUX_ACC if acc else 0,
-              aux=dx if acc else None, x3=kind == 'x3', frag=kind == 'x3')
+              aux=dx if acc else None, x3=kind == 'x3', frag=True)
     else:
         gemm(dy, W, dx, M=M, N=K, K=N, beta=1.0 if acc else 0.0, precision=precision)
     wk = wg_kind(precision, M, N, K)

@@ -391,6 +391,11 @@ int c2dsr_to_split_bf16_multi(const int64_t* desc, int count, void* stream);
  * rows × columns: R × Cc, or Cc × R when trans; K' = 256 or 512); element (n, k) hi / lo (hl = 0 / 1) at
  * ((⌊n/16⌋·(K'/16) + 2⌊k/32⌋ + hl)·64 + (⌊k/8⌋ mod 4)·16 + n mod 16)·8 + k mod 8; rows past N' are not written */
 int c2dsr_to_split_bf16_frag_multi(const int64_t* desc, int count, void* stream);
+/* bf16 images (c2dsr_to_bf16_multi's descriptors) in the bf16-mode kernel's fragment order: ⌈N'/32⌉·32 rows × K'
+ * (K' = 256, 512 or 768); element (n, k) at ((⌊n/32⌋·(K'/16) + ⌊k/16⌋)·64 + (⌊k/8⌋ mod 2)·32 + n mod 32)·8 + k mod 8.
+ * c2dsr_rgemm / c2dsr_rgemm_aux / c2dsr_rgemm_aux_b16a take such an image as B with ldb = 0 (every weight load one
+ * coalesced 1 KiB read; results identical to the row image's). */
+int c2dsr_to_bf16_frag_multi(const int64_t* desc, int count, void* stream);
 /* K3 projection weight/bias gradients (csrc/rgemm.hip): dW[N][256] = beta·dW + Σ_t dY[t][N]ᵀ·X[t][256]
  * (the mm of the linear backward, N % 128 == 0) and, if db is non-null, db[N] = beta·db + Σ_t dY[t][N]
  * (fp32 column sums of the same dY chunks; replaces c2dsr_colsum there); bf16 MFMA with transposed LDS

@@ -352,6 +352,55 @@ def test_rgemm_x3_fragment_image(N, K, tr):
     assert torch.equal(C0, C1)
 
 
+def b16_frag_index(n, k, K):
+    """c2dsr_to_bf16_frag_multi's element position (include/c2dsr.h), restated."""
+    return (((n // 32) * (K // 16) + k // 16) * 64 + ((k // 8) % 2) * 32 + n % 32) * 8 + k % 8
+
+
+@pytest.mark.parametrize('N,K,tr', [(256, 256, 0), (768, 256, 0), (256, 768, 1), (200, 512, 0)])
+def test_rgemm_b16_fragment_image(N, K, tr):
+    """The bf16 mode's weight image in fragment order (c2dsr_to_bf16_frag_multi, ops.weight_img 'b16') holds the
+    row image's values at the header's positions, and the bf16 row-streaming kernel on it (ldb = 0) is bit-identical
+    to the row image's in every epilogue mode, also with bf16 A (c2dsr_rgemm_aux_b16a, K = 768)."""
+    import numpy as np
+    from c2dsr_amd._lib import lib, stream
+    from c2dsr_amd.ops import AUX_ACC, AUX_MASK, rgemm, to_bf16
+    g = torch.Generator().manual_seed(N * 3 + K + tr)
+    W = (torch.randn(K, N, generator=g) if tr else torch.randn(N, K, generator=g)).to(DEV)
+    row = to_bf16(W, bool(tr))
+    R, C = W.shape
+    frag = torch.zeros(-(-N // 32) * 32, K, device=DEV, dtype=torch.bfloat16)
+    desc = np.asarray([W.data_ptr(), frag.data_ptr(), R, C, W.stride(0), tr], dtype=np.int64)
+    lib('c2dsr_to_bf16_frag_multi', desc.ctypes.data, 1, stream())
+    torch.cuda.synchronize()
+    n, k = torch.meshgrid(torch.arange(N), torch.arange(K), indexing='ij')
+    assert torch.equal(frag.cpu().reshape(-1)[b16_frag_index(n, k, K)], row.cpu())
+    M = 1000 + 37
+    A = torch.randn(M, K, generator=g).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    aux = torch.randn(M, N, generator=g).to(DEV)
+    modes = [dict(bias=b), dict(aux_mode=AUX_ACC, aux=aux)]
+    if K == 256:
+        modes += [dict(bias=b, relu_drop=((5, 6), 0.2, 100)), dict(aux_mode=AUX_MASK, aux=aux, aux_scale=2.0)]
+    for kw in modes:
+        outs = []
+        for fr, img in ((False, row), (True, frag)):
+            Cm = torch.empty(M, N, device=DEV)
+            rgemm(A, img, Cm, M=M, N=N, K=K, frag=fr, **kw)
+            outs.append(Cm)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+    if K == 768:  # bf16 A (the attention backward's dqkv)
+        Ab = A.to(torch.bfloat16)
+        outs = []
+        for fr, img in ((False, row), (True, frag)):
+            Cm = torch.empty(M, N, device=DEV)
+            rgemm(Ab, img, Cm, M=M, N=N, K=K, frag=fr)
+            outs.append(Cm)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1])
+
+
 def _ref_chunked(H, W, b, pl, t, coef, lam, BR, chunk=2048):
     """_ref in float64 on the device, in row chunks (the MB head-b logits are 9.7 GB in float64)."""
     H, W, b, pl, t = (x.to(DEV) for x in (H, W, b, pl, t))

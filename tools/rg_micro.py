@@ -7,7 +7,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from c2dsr_amd.ops import rgemm, to_bf16, to_split_bf16  # noqa: E402
+from c2dsr_amd.ops import rgemm, to_bf16, to_split_bf16, weight_img  # noqa: E402
 
 
 def timeit(fn, reps=30):
@@ -65,7 +65,7 @@ def main(x3=False):
         W = torch.randn(N, K, device=dev)
         # x3: the row image (c2dsr_rgemm_x3) and the fragment-ordered image the fp32 step uses (c2dsr_rgemm_x3f)
         forms = ((('x3', False, to_split_bf16(W)), ('x3f', True, to_split_bf16(W, frag=True))) if x3 else
-                 (('b16', False, to_bf16(W)),))
+                 (('b16', False, to_bf16(W)), ('b16f', True, weight_img(W, 'b16'))))
         for M in (8192, 20000, 38000, 57000, 102400):
             A = torch.randn(M, K, device=dev)
             C = torch.empty(M, N, device=dev)
