@@ -226,6 +226,92 @@ __global__ __launch_bounds__(256) void spmm_nc_kernel(const int4* __restrict__ w
   }
 }
 
+// One-pass rows (d == LPR·VW: the C5 bf16 width) with ITEMS consecutive work items per lane group: every item's
+// header and its first two edges' (col, val) are loaded up front, so per item only the row gathers and the epilogue
+// streams remain on the dependent-latency chain (work → col → X in spmm_kernel).  Same per-element accumulation
+// order (edges in order, one fma each), so bit-identical to spmm_kernel.
+template <int LPR, int ITEMS, bool MASK_OUT, typename T>
+__global__ __launch_bounds__(256) void spmm_pf_kernel(const int4* __restrict__ work, int n_work,
+                                                      const int* __restrict__ col, const float* __restrict__ val,
+                                                      int d, const T* __restrict__ X, Epi<T> ep,
+                                                      float* __restrict__ part) {
+  constexpr int GROUPS = 256 / LPR;
+  constexpr int V = c2::VW<T>, NH = V / 4;
+  const int g = threadIdx.x / LPR;
+  const int c = (threadIdx.x % LPR) * V;
+  const long w0 = ((long)blockIdx.x * GROUPS + g) * ITEMS;
+  if (w0 >= n_work) return;
+  const c2::Drop& drop = ep.drop;
+  int4 wk[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) wk[i] = w0 + i < n_work ? work[w0 + i] : make_int4(0, 0, 0, -2);
+  int j0[ITEMS], j1[ITEMS];
+  float v0[ITEMS], v1[ITEMS];
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e0 = wk[i].y, e1 = wk[i].z;
+    j0[i] = e0 < e1 ? col[e0] : 0;
+    v0[i] = e0 < e1 ? val[e0] : 0.f;
+    j1[i] = e0 + 1 < e1 ? col[e0 + 1] : 0;
+    v1[i] = e0 + 1 < e1 ? val[e0 + 1] : 0.f;
+  }
+  auto mask = [&](c2::RowV<T>& x, int j) {
+    if (!MASK_OUT && drop.active()) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) x.v[h] = x.v[h] * drop.mul4((uint64_t)j * d + c + 4 * h);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < ITEMS; ++i) {
+    const int e0 = wk[i].y, e1 = wk[i].z, slot = wk[i].w;
+    if (slot == -2) break;
+    c2::RowV<T> acc;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc.v[h] = c2::f4(0.f);
+    if (e0 + 1 < e1) {
+      c2::RowV<T> x0 = c2::ldv(X + (long)j0[i] * d + c), x1 = c2::ldv(X + (long)j1[i] * d + c);
+      mask(x0, j0[i]);
+      mask(x1, j1[i]);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        acc.v[h] = c2::fma4(v0[i], x0.v[h], acc.v[h]);
+        acc.v[h] = c2::fma4(v1[i], x1.v[h], acc.v[h]);
+      }
+    } else if (e0 < e1) {
+      c2::RowV<T> x0 = c2::ldv(X + (long)j0[i] * d + c);
+      mask(x0, j0[i]);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) acc.v[h] = c2::fma4(v0[i], x0.v[h], acc.v[h]);
+    }
+    int e = e0 + 2;
+    for (; e + 1 < e1; e += 2) {
+      const int ja = col[e], jb = col[e + 1];
+      const float va = val[e], vb = val[e + 1];
+      c2::RowV<T> xa = c2::ldv(X + (long)ja * d + c), xb = c2::ldv(X + (long)jb * d + c);
+      mask(xa, ja);
+      mask(xb, jb);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        acc.v[h] = c2::fma4(va, xa.v[h], acc.v[h]);
+        acc.v[h] = c2::fma4(vb, xb.v[h], acc.v[h]);
+      }
+    }
+    for (; e < e1; ++e) {
+      const int j = col[e];
+      c2::RowV<T> x = c2::ldv(X + (long)j * d + c);
+      mask(x, j);
+#pragma unroll
+      for (int h = 0; h < NH; ++h) acc.v[h] = c2::fma4(val[e], x.v[h], acc.v[h]);
+    }
+    if (slot >= 0) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) *(float4*)(part + (long)slot * d + c + 4 * h) = acc.v[h];
+    } else {
+      epilogue<MASK_OUT>(acc, wk[i].x, c, d, ep);
+    }
+  }
+}
+
 #ifndef COMBINE_U
 #define COMBINE_U 16
 #endif
@@ -293,7 +379,22 @@ int launch(const int4* work, int n_work, const int4* split, int n_split, const i
     C2_CHECK_LAUNCH();
     return 0;
   }
-#define C2_SPMM(L)                                                                                              \
+#ifndef GCN_PF_B16
+#define GCN_PF_B16 2
+#endif
+  // bf16 rows of d = 512 (C5): GCN_PF_B16 work items per wave with their headers and first edges loaded up front
+  // (C5 bf16-table line 5350 → 5652 GB/s at 2, 5071 at 4; outputs bit-identical: profiles/r04_exp28_gcn_pf.txt)
+  if constexpr (GCN_PF_B16 > 1 && std::is_same_v<T, c2::tbf16>) {
+    if (d == 64 * c2::VW<T>) {
+      spmm_pf_kernel<64, GCN_PF_B16, MASK_OUT, T><<<c2::ceil_div(n_work, 4 * GCN_PF_B16), 256, 0, s>>>(
+          work, n_work, col, val, d, X, ep, part);
+      if (n_split > 0)
+        combine_kernel<64, MASK_OUT, T><<<c2::ceil_div(n_split, 4), 256, 0, s>>>(split, n_split, d, ep, part);
+      C2_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+#define C2_SPMM(L)                                                                                       \
   spmm_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_work, groups), 256, 0, s>>>(work, n_work, col, val, d, X, ep, part); \
   if (n_split > 0) combine_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_split, groups), 256, 0, s>>>(split, n_split, d, ep, part);
   switch (lpr) {
