@@ -394,6 +394,21 @@ int launch(const int4* work, int n_work, const int4* split, int n_split, const i
       return 0;
     }
   }
+#ifndef GCN_PF_F32
+#define GCN_PF_F32 1
+#endif
+  // the same for fp32 rows of d = 256 (the bench's Movie-Book width): measured and not kept — MB fwd 100.7 → 117.0 µs
+  // at 2, 152 µs at 4; bwd 61.8 → 79.6 / 108 µs (profiles/r04_exp29_gcn_pf_f32.txt)
+  if constexpr (GCN_PF_F32 > 1 && std::is_same_v<T, float>) {
+    if (d == 64 * c2::VW<T>) {
+      spmm_pf_kernel<64, GCN_PF_F32, MASK_OUT, T><<<c2::ceil_div(n_work, 4 * GCN_PF_F32), 256, 0, s>>>(
+          work, n_work, col, val, d, X, ep, part);
+      if (n_split > 0)
+        combine_kernel<64, MASK_OUT, T><<<c2::ceil_div(n_split, 4), 256, 0, s>>>(split, n_split, d, ep, part);
+      C2_CHECK_LAUNCH();
+      return 0;
+    }
+  }
 #define C2_SPMM(L)                                                                                       \
   spmm_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_work, groups), 256, 0, s>>>(work, n_work, col, val, d, X, ep, part); \
   if (n_split > 0) combine_kernel<L, MASK_OUT, T><<<c2::ceil_div(n_split, groups), 256, 0, s>>>(split, n_split, d, ep, part);

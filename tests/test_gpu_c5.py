@@ -152,6 +152,9 @@ def test_c5_bf16_table_kernels_match_fp32():
     ops.spmm(dg, False, E16, keys, p, 0, 0.5, E16, 0.5, 0.0, -1, 0.0, H16)
     ops.spmm(dg, False, E32, keys, p, 0, 0.5, E32, 0.5, 0.0, -1, 0.0, H32)
     assert rel_dev(H16, H32) < 2 ** -8, 'GCN forward on bf16 tables'
+    # same fp32 arithmetic in the same edge order (spmm_pf_kernel on bf16 rows, spmm_nc_kernel on fp32 rows), one
+    # RNE rounding at the store: bit-equal to the fp32 result rounded to bf16
+    assert torch.equal(H16, H32.to(torch.bfloat16)), 'GCN forward on bf16 tables = fp32 forward rounded once'
     P = torch.empty(L, d, device=DEV).normal_(0.0, 0.1)
     passes = [(b[0], b[3]), (b[1], b[4]), (b[2], b[5]), (b[12], b[3]), (b[13], b[3])]
     Hr = H16.float()
@@ -184,3 +187,4 @@ def test_c5_bf16_table_kernels_match_fp32():
     ops.spmm(dg, True, G16, keys, p, 1, 0.5, G16, 0.5, 1.0, pad, 1.0, gE16)
     ops.spmm(dg, True, Gr, keys, p, 1, 0.5, Gr, 0.5, 1.0, pad, 1.0, gE32)
     assert rel_dev(gE16, gE32) < 2 ** -8, 'GCN backward on bf16 tables'
+    assert torch.equal(gE16, gE32.to(torch.bfloat16)), 'GCN backward on bf16 tables = fp32 backward rounded once'
