@@ -315,6 +315,9 @@ __global__ __launch_bounds__(256) void spmm_pf_kernel(const int4* __restrict__ w
 #ifndef COMBINE_U
 #define COMBINE_U 16
 #endif
+#ifndef COMBINE_HI
+#define COMBINE_HI 1
+#endif
 
 // split[s] = {row, slot_begin, slot_end}: sum the row's pieces in order, then the epilogue.
 template <int LPR, bool MASK_OUT, typename T>
@@ -329,6 +332,39 @@ __global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ s
   const int4 sp = split[s];
   for (int c0 = lane * V; c0 < d; c0 += LPR * V) {
     c2::RowV<T> res;
+#if COMBINE_HI
+    // all NH float4 slices of the lane's piece rows in flight together (bf16 rows: 2 per piece), each slice still
+    // summed in piece order (bit-identical; C5 bf16-table line 5708 → 5807 GB/s, COMBINE_U 32: 5524;
+    // profiles/r04_exp30_combine.txt)
+#pragma unroll
+    for (int h = 0; h < NH; ++h) res.v[h] = c2::f4(0.f);
+    int k = sp.y;
+    for (; k + COMBINE_U <= sp.z; k += COMBINE_U) {
+      float4 v[COMBINE_U][NH];
+#pragma unroll
+      for (int u = 0; u < COMBINE_U; ++u)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) v[u][h] = *(const float4*)(part + (long)(k + u) * d + c0 + 4 * h);
+#pragma unroll
+      for (int u = 0; u < COMBINE_U; ++u)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) res.v[h] = res.v[h] + v[u][h];
+    }
+    for (; k + 8 <= sp.z; k += 8) {
+      float4 v[8][NH];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) v[u][h] = *(const float4*)(part + (long)(k + u) * d + c0 + 4 * h);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int h = 0; h < NH; ++h) res.v[h] = res.v[h] + v[u][h];
+    }
+    for (; k < sp.z; ++k)
+#pragma unroll
+      for (int h = 0; h < NH; ++h) res.v[h] = res.v[h] + *(const float4*)(part + (long)k * d + c0 + 4 * h);
+#else
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int c = c0 + 4 * h;
@@ -353,6 +389,7 @@ __global__ __launch_bounds__(256) void combine_kernel(const int4* __restrict__ s
       for (; k < sp.z; ++k) acc = acc + *(const float4*)(part + (long)k * d + c);
       res.v[h] = acc;
     }
+#endif
     epilogue<MASK_OUT>(res, sp.x, c0, d, ep);
   }
 }
