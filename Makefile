@@ -6,7 +6,11 @@ OBJ := $(patsubst c2dsr_amd/csrc/%.hip,build/%.o,$(SRC))
 HDR := $(wildcard c2dsr_amd/csrc/*.h) include/c2dsr.h
 FLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++20 -Iinclude -Wno-unused-result
 
-all: c2dsr_amd/libc2dsr_hip.so c2dsr_amd/libc2dsr_prep.so c2dsr_amd/libc2dsr_torch.so
+all: kernels torch
+
+# the kernel library and the host pipeline need no torch; `make kernels` builds them alone
+kernels: c2dsr_amd/libc2dsr_hip.so c2dsr_amd/libc2dsr_prep.so
+torch: c2dsr_amd/libc2dsr_torch.so
 
 build/%.o: c2dsr_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
@@ -20,8 +24,10 @@ c2dsr_amd/libc2dsr_prep.so: c2dsr_amd/csrc_host/prep.cpp include/c2dsr_prep.h
 	g++ -O3 -fPIC -shared -std=c++17 -Wall -Iinclude $< -o $@
 
 # PyTorch-ROCm extension: TORCH_LIBRARY(c2dsr) over the C ABI (host C++, links the kernel library by rpath)
-TORCH_DIR := $(shell python3 -c 'import os, torch; print(os.path.dirname(torch.__file__))')
-TORCH_FLAGS := -O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI=1 \
+# (recursively expanded: torch is queried only when the torch target is built, never by `make clean` / `kernels`)
+TORCH_DIR ?= $(shell python3 -c 'import os, torch; print(os.path.dirname(torch.__file__))')
+TORCH_ABI ?= $(shell python3 -c 'import torch; print(int(torch.compiled_with_cxx11_abi()))')
+TORCH_FLAGS = -O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI=$(TORCH_ABI) \
 	-Iinclude -I$(TORCH_DIR)/include -I$(TORCH_DIR)/include/torch/csrc/api/include -I/opt/rocm/include
 
 c2dsr_amd/csrc_torch/torch_ops_gen.inc: include/c2dsr.h tools/gen_torch_ops.py
@@ -34,4 +40,4 @@ c2dsr_amd/libc2dsr_torch.so: c2dsr_amd/csrc_torch/torch_ops.cpp c2dsr_amd/csrc_t
 clean:
 	rm -rf build c2dsr_amd/libc2dsr_hip.so c2dsr_amd/libc2dsr_prep.so c2dsr_amd/libc2dsr_torch.so
 
-.PHONY: all clean
+.PHONY: all clean kernels torch

@@ -132,6 +132,8 @@ lib = _Lib()
 
 
 def stream() -> int:
+    if not torch.cuda.is_available():
+        raise HipLibError('c2dsr_amd kernels need a HIP device (no CPU fallback)')
     return torch.cuda.current_stream().cuda_stream
 
 

@@ -726,7 +726,9 @@ __device__ __forceinline__ V wg_pick(const V (&a)[WG_MAXSEG], int k) {  // unifo
 // (y_hi·x_hi + y_lo·x_hi + y_hi·x_lo, fp32 accumulation; the bias column sums stay exact fp32).
 // NW: waves per workgroup — 4 (wave tile 64 n × 128 i) or 8 (32 n × 128 i: two waves per SIMD, so one wave's
 // staging and barrier waits run under the other's MFMAs); AH: chunks loaded ahead in registers (2 or 3).  The
-// accumulation order of every output element is the same for all (NW, AH).
+// accumulation order of every dW element is the same for all (NW, AH); the bias column sums (db) are not: each
+// thread's partial covers NYU rows and red_b combines NT/32 partials, so db's bits depend on NW (deterministic for
+// a given NW).
 template <bool YB16, bool X3 = false, int NW = 4, int AH = WG_AHEAD>
 __global__ __launch_bounds__(64 * NW) void wg_kernel(int N, WSeg sg, float* __restrict__ part,
                                                      float* __restrict__ part_b, int NTL, int rows_per_split) {

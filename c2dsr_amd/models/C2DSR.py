@@ -184,7 +184,9 @@ class C2DSR(nn.Module):
             self.launch_graph()
 
     def _table_versions(self):
-        return tuple(w._version for w in (self.embed_i.weight, self.embed_i_a.weight, self.embed_i_b.weight))
+        # torch in-place ops bump _version; the fused optimizer writes through a kernel and bumps WEIGHTS.epoch
+        return (ops.WEIGHTS.epoch,) + tuple(w._version for w in (self.embed_i.weight, self.embed_i_a.weight,
+                                                                  self.embed_i_b.weight))
 
     def launch_graph(self):
         pending = getattr(self, '_graph_pending', None)

@@ -463,6 +463,9 @@ class HostCounts:
         nothing is copied and nothing ever waits on the device; check: also copy the device counts and compare
         them with ``known`` at the first read (C2DSR_CHECK_COUNTS=1; raises on a mismatch)."""
         self.known = None if known is None else [int(v) for v in known]
+        if self.known is not None and len(self.known) != dev_counts.numel():
+            # counts prepared under other count_flags (model mode, seqs=None, …) would be read from wrong slots
+            raise ValueError(f'{len(self.known)} host-prepared counts for {dev_counts.numel()} device count slots')
         self.vals = self.known if not check else None
         if self.vals is None:
             self.host = torch.empty(dev_counts.numel(), dtype=torch.int32, pin_memory=True)

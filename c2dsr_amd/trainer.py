@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import gc
 import os
+import sys
 import time
 from os.path import join
 
@@ -53,10 +54,52 @@ def dp_info():
     return 0, 1
 
 
+def init_data_parallel(args):
+    """Data parallelism under an UNCHANGED main.py launched by torchrun (BASELINE north_star).
+
+    main.py builds ``args.device = cuda:<--cuda>`` for every process (reference main.py:72-75) and constructs
+    ``Trainer(args, noter)`` (main.py:102) without touching torch.distributed.  When the launcher's environment
+    says WORLD_SIZE > 1 and no process group exists yet, this runs before the trainer's first device call:
+      * the rank's device is ``cuda:LOCAL_RANK`` (``args.device`` is overwritten — main.py's value is the same
+        device on every rank), ``torch.cuda.set_device`` makes it current;
+      * the process group is RCCL (``'nccl'``, bound to that device) when the node has a device per local rank;
+        on a node with fewer devices than local ranks (the one-GPU rehearsal) ranks share devices round-robin
+        and the group is gloo, since RCCL refuses two ranks on one device; ``--cuda cpu`` gives gloo on the host
+        (the product path then stops at its first kernel: there is no CPU fallback).
+    ``C2DSR_DP_BACKEND`` overrides the backend.  Returns (rank, world) — (0, 1) outside a launcher; a process
+    group the caller initialised itself is used as it is."""
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world <= 1 or not dist.is_available() or dist.is_initialized():
+        return dp_info()
+    rank = int(os.environ['RANK'])
+    local = int(os.environ.get('LOCAL_RANK', rank))
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
+    backend = os.environ.get('C2DSR_DP_BACKEND')
+    dev = torch.device(getattr(args, 'device', 'cpu'))
+    kw = {}
+    if dev.type == 'cuda':
+        n_dev = torch.cuda.device_count()  # counts devices without initialising the runtime
+        if n_dev < 1:
+            raise RuntimeError('data parallel on cuda: no visible device')
+        dev = torch.device('cuda', local % n_dev)
+        backend = backend or ('nccl' if n_dev >= local_world else 'gloo')
+        torch.cuda.set_device(dev)
+        if backend == 'nccl':
+            kw['device_id'] = dev
+    else:
+        backend = backend or 'gloo'
+    args.device = dev
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    print(f'[c2dsr] data parallel: rank {rank}/{world} on {dev} ({backend})', file=sys.stderr, flush=True)
+    return rank, world
+
+
 class Trainer(object):
     def __init__(self, args, noter=None, *, data=None, graphs=None):
         """``data`` = (trainloader, valloader, testloader) and ``graphs`` = (adj_share, adj_specific)
-        may be given to skip reading ``args.path_raw`` (tests, benchmarks)."""
+        may be given to skip reading ``args.path_raw`` (tests, benchmarks).  Under torchrun the process group
+        and the rank's device are set up here (init_data_parallel), so main.py needs no change."""
+        init_data_parallel(args)
         if data is None:
             data = get_dataloader(args)
         self.trainloader, self.valloader, self.testloader = data

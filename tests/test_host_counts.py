@@ -53,3 +53,14 @@ def test_host_counts_match_kernel_predicates():
     # subsets keep the device order: need sets, then padding rows, then (Mv0, Mv1) per head
     assert Trainer.host_counts(fake, tuple(arrs), need=False, pads=False, ce=True) == got[10:]
     assert Trainer.host_counts(fake, tuple(arrs), need=True, pads=False, ce=False) == got[:5]
+
+
+def test_host_counts_refuse_a_length_mismatch():
+    """counts prepared under other flags than the step's would be read from the wrong slots."""
+    import pytest
+    import torch
+    from c2dsr_amd.ops import HostCounts
+    hc = HostCounts(torch.zeros(4, dtype=torch.int32), known=[1, 2, 3, 4])
+    assert [hc[i] for i in range(4)] == [1, 2, 3, 4]
+    with pytest.raises(ValueError, match='host-prepared counts'):
+        HostCounts(torch.zeros(14, dtype=torch.int32), known=[1, 2, 3, 4])

@@ -108,3 +108,12 @@ def test_convolve_graph_is_eager_unless_trainer_driven_and_guards_weight_edits()
         model.hi_a
     model.convolve_graph()  # a new call sees the new weights
     assert torch.equal(model.hi_a, model.embed_i_a.weight) and calls == [0, 1, 2, 0, 1, 2]
+    # the fused optimizer writes the weights through a kernel (no _version bump) and bumps
+    # ops.WEIGHTS.epoch instead — a step between the call and the first read is refused as well
+    from c2dsr_amd import ops
+    model.convolve_graph()
+    ops.WEIGHTS.epoch += 1  # what FlatAdamW.step() → WEIGHTS.bump() does after its kernel
+    with pytest.raises(RuntimeError, match='modified between convolve_graph'):
+        model.hi_b
+    model.convolve_graph()
+    assert torch.equal(model.hi_b, model.embed_i_b.weight)

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 evidence at the benched revision (every step under its own limit, chained):
+# Round evidence at the benched revision (every step under its own limit, chained):
 #   smoke, the default bench line, rocprofv3 kernel stats of the main line (+ idle gaps), FETCH / WRITE / SQ PMC passes
 #   of the main line, kernel stats + FETCH / WRITE passes of the C5 line (bf16 tables), the GPU suite.
-#   usage: bash tools/r04_final.sh TAG        (outputs under gpurun_out/TAG_*)
+#   usage: bash tools/evidence.sh TAG        (outputs under gpurun_out/TAG_*)
 set -o pipefail
-TAG=${1:-r04z}
+TAG=${1:-r05z}
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 timeout -k 10 200 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -30 gpurun_out/${TAG}_smoke.log; exit 1; }

@@ -473,13 +473,19 @@ def _sha(arrs):
     return h.hexdigest()
 
 
-def gen_c2(ref):
-    """One reference train_batch (dropout 0) at C2's full shape, stored like model_d256.npz (an even sample of
-    every tensor's elements with the full max-abs) plus, for the sparse embedding-table gradients, a sample of
-    their nonzero elements.  Writes tests/golden/model_c2.npz."""
+# BASELINE configs[2] (C3) at Movie-Book item counts: 36,845 + 63,937 items, d=256, L=50,
+# R=10; B=1024 — the reference's CPU step at B=2048 materialises ~33 GB of logits / log-softmax / their gradients
+# per step on top of the model, more than this container's 64 GB leaves room for.  Same synthetic generator as C2.
+C3 = dict(C2, n_a=36845, n_b=63937)
+C3_BATCH = 1024
+
+
+def gen_c2(ref, cfg=C2, B=C2_BATCH, tag='c2'):
+    """One reference train_batch (dropout 0) at C2's (or, tag 'c3', C3's) full shape, stored like model_d256.npz
+    (an even sample of every tensor's elements with the full max-abs) plus, for the sparse embedding-table
+    gradients, a sample of their nonzero elements.  Writes tests/golden/model_<tag>.npz."""
     ref_dl, ref_model, ref_trainer, ref_graph, ref_metrics = ref
-    cfg, B = C2, C2_BATCH
-    tmp = tempfile.mkdtemp(prefix='c2dsr_fx_c2_')
+    tmp = tempfile.mkdtemp(prefix=f'c2dsr_fx_{tag}_')
     path_raw = os.path.join(tmp, 'raw')
     path_data = os.path.join(tmp, 'data')
     os.makedirs(path_data)
@@ -546,8 +552,8 @@ def gen_c2(ref):
             sel = nz[sample_idx(nz.size)]
             out[f's0/{k}:nz_idx'] = sel.astype(np.int64)
             out[f's0/{k}:nz_val'] = flat[sel]
-    np.savez_compressed(os.path.join(OUT, 'model_c2.npz'), **out)
-    print(f'[c2] train={len(ds_tr.data)} loss={loss.item():.6f} tensors={len(named)}')
+    np.savez_compressed(os.path.join(OUT, f'model_{tag}.npz'), **out)
+    print(f'[{tag}] train={len(ds_tr.data)} loss={loss.item():.6f} tensors={len(named)}')
 
 
 FK_EPOCHS = 2
@@ -638,6 +644,7 @@ def main():
     ap.add_argument('--fk-traj', action='store_true', help='only the Food-Kitchen metric trajectory')
     ap.add_argument('--d256', action='store_true', help='only the d=256 / L=50 / R=10 golden step')
     ap.add_argument('--c2', action='store_true', help='only the C2-shape (FK items, d=256, L=50, B=1024) golden step')
+    ap.add_argument('--c3', action='store_true', help='only the C3-shape (MB items, d=256, L=50, B=1024) golden step')
     opt = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     torch.set_num_threads(4)
@@ -648,6 +655,10 @@ def main():
     if opt.c2:
         torch.set_num_threads(8)
         gen_c2(ref)
+        return
+    if opt.c3:
+        torch.set_num_threads(8)
+        gen_c2(ref, C3, C3_BATCH, 'c3')
         return
     if opt.fk_traj:
         torch.set_num_threads(8)
