@@ -724,6 +724,9 @@ def _sha(arrs):
     return h.hexdigest()
 
 
+REF_STEPS = {'c2': (29207, 34886), 'c3': (36845, 63937)}
+
+
 @pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
 def test_c2_step_matches_reference(compact):
     """BASELINE configs[1] (C2) pinned by the REFERENCE at its full shape: one train_batch
@@ -734,13 +737,28 @@ def test_c2_step_matches_reference(compact):
     Losses at 1e-4 relative; the GCN tables, encoder outputs and every parameter gradient on an even sample of
     their elements (plus a sample of the nonzero elements of the sparse table gradients), relative to the full
     tensor's max-abs, at 1e-4."""
+    _ref_step_check('c2', compact)
+
+
+@pytest.mark.parametrize('compact', [True, False], ids=['compact', 'full'])
+def test_c3_step_matches_reference(compact):
+    """BASELINE configs[2] (C3, the bench workload's item counts) pinned by the REFERENCE: one
+    train_batch of the reference Trainer at Movie-Book item counts (36,845 + 63,937), d=256, L=50, R=10, B=1024,
+    dropout 0 (tests/golden/model_c3.npz, tools/gen_fixtures.py --c3; B=1024 is the largest batch whose reference
+    CPU step fits this container's memory) — the 63,938-column CE, the MB-size GCN tables, embedding and encoder
+    gradients through the reference's own train_batch — checked exactly as the C2 step."""
+    _ref_step_check('c3', compact)
+
+
+def _ref_step_check(tag, compact):
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
     from c2dsr_amd import synth
     import random
-    z = G.load('model_c2.npz')
+    z = G.load(f'model_{tag}.npz')
     B = int(z['batch_n'])
-    c = dict(n_a=29207, n_b=34886, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
+    n_a, n_b = REF_STEPS[tag]
+    c = dict(n_a=n_a, n_b=n_b, len_max=50, len_rec=10, d_latent=256, n_gnn=1, n_attn=1, n_head=1,
              norm_first=False, d_bias=False, shared_item_embed=False)
     seqs = synth.make_sequences(int(z['n_users']), c['n_a'], c['n_b'], c['len_max'], seed=1, n_min=6)
     random.seed(3407)
@@ -788,7 +806,7 @@ def test_c2_step_matches_reference(compact):
             worst[k] = check(k, got)
     for n_, g in box['grads'].items():
         worst[n_] = check(f'grad/{n_}', g)
-    print('C2 vs reference, worst:', {k: f'{v:.1e}' for k, v in sorted(worst.items(), key=lambda x: -x[1])[:6]})
+    print(f'{tag} vs reference, worst:', {k: f'{v:.1e}' for k, v in sorted(worst.items(), key=lambda x: -x[1])[:6]})
 
 
 def test_row_shard_readers_wait_for_gather():
