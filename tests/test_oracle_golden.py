@@ -95,9 +95,11 @@ def test_oracle_metrics_match_reference():
     np.testing.assert_allclose(O.cal_score(ra, rb, [0.0647, 0.0476, 0.0284, 0.0217]), m['score_mb'], rtol=1e-14)
 
 
-def test_c2_fixture_inputs_rebuild():
-    """model_c2.npz (the reference's C2-shape step) stores no inputs: the batch and graphs are rebuilt from the
-    synthetic generator through the bit-exact data path and must hash to the reference's processed forms."""
+@pytest.mark.parametrize('tag,n_a,n_b', [('c2', 29207, 34886), ('c3', 36845, 63937)])
+def test_c2_fixture_inputs_rebuild(tag, n_a, n_b):
+    """model_c2.npz / model_c3.npz (the reference's C2- / C3-shape steps) store no inputs: the batch and graphs are
+    rebuilt from the synthetic generator through the bit-exact data path and must hash to the reference's
+    processed forms."""
     import hashlib
     import random
     from c2dsr_amd import dataloader as DL
@@ -112,13 +114,13 @@ def test_c2_fixture_inputs_rebuild():
             h.update(a.tobytes())
         return h.hexdigest()
 
-    z = G.load('model_c2.npz')
+    z = G.load(f'model_{tag}.npz')
     B = int(z['batch_n'])
-    seqs = synth.make_sequences(int(z['n_users']), 29207, 34886, 50, seed=1, n_min=6)
+    seqs = synth.make_sequences(int(z['n_users']), n_a, n_b, 50, seed=1, n_min=6)
     random.seed(3407)
-    rows = DL.to_arrays(DL.preprocess_train(seqs, 29207, 34886, 50))
+    rows = DL.to_arrays(DL.preprocess_train(seqs, n_a, n_b, 50))
     assert rows[0].shape[0] == int(z['n_train'])
     assert sha([np.ascontiguousarray(r[:B], dtype=np.int64) for r in rows]) == str(z['batch_sha256'])
-    for k, g in zip(('share', 'specific'), GR.preprocess_graph(seqs, 29207, 29207 + 34886 + 1)):
+    for k, g in zip(('share', 'specific'), GR.preprocess_graph(seqs, n_a, n_a + n_b + 1)):
         r = np.repeat(np.arange(g.n, dtype=np.int64), np.diff(g.rowptr.astype(np.int64)))
         assert sha([r, g.col.astype(np.int64), g.val.astype(np.float32)]) == str(z[f'{k}_sha256']), k
