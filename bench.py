@@ -259,6 +259,51 @@ def hbm_traffic(precision):
     return t.get('bytes_per_step'), t.get('source')
 
 
+# the GPU kernels behind each timed C-ABI entry point (PMC counters are per GPU kernel; the embedding backward's
+# segment sums are the ROLE 0 instantiations — tools/pmc_traffic.py)
+SEG0 = ('seg_chunk_kernel<64, 0>', 'seg_split1_kernel<64, 0>', 'seg_split2_kernel<64, 0>')
+DRAM_KERNELS = {'c2dsr_gcn_spmm': ('spmm_kernel', 'spmm_pf_kernel', 'combine_kernel'),
+                'c2dsr_gcn_spmm_b16': ('spmm_kernel', 'spmm_pf_kernel', 'combine_kernel'),
+                'c2dsr_embed_fwd': ('embed_fwd_kernel',), 'c2dsr_embed_fwd_b16': ('embed_fwd_kernel',),
+                'c2dsr_embed_bwd_planned': SEG0, 'c2dsr_embed_bwd_planned_rows': SEG0, 'c2dsr_embed_bwd_planned_b16': SEG0}
+
+
+def add_dram(roof, path, steps):
+    """DRAM-side fractions beside the algorithmic ones: the PMC bytes per step of the same
+    kernels (profiles/*traffic*.json: rocprofv3 FETCH_SIZE ×2 + WRITE_SIZE passes, tools/pmc_traffic.py) over the
+    kernels' time measured here.  Algorithmic bytes credit every gathered row, so a Zipf-popular row served from
+    L2 / MALL counts each time it is read; the DRAM figure counts what left HBM.  An entry point whose kernels the
+    PMC file does not cover gets no DRAM figure."""
+    if roof is None or not os.path.exists(path):
+        return
+    with open(path) as f:
+        t = json.load(f)
+    pk = t.get('per_kernel', {})
+    tot_b, tot_ms = 0.0, 0.0
+    for name, rec in roof['per_kernel'].items():
+        ks = [k for k in DRAM_KERNELS.get(name, ()) if k in pk]
+        if not ks:
+            continue
+        by = sum(pk[k]['bytes'] for k in ks)  # per step
+        ms = rec['avg_ms'] * rec['launches'] / steps
+        rec['dram_gbs'] = round(by / (ms * 1e-3) / 1e9, 1)
+        rec['dram_frac'] = round(rec['dram_gbs'] / PEAK_HBM_GBS, 4)
+        tot_b += by
+        tot_ms += ms
+    gs = roof.get('gather_spmm')
+    if gs:
+        recs = [roof['per_kernel'][n] for n in gs['kernels'] if 'dram_gbs' in roof['per_kernel'][n]]
+        if recs:
+            b = sum(r['dram_gbs'] * r['avg_ms'] * r['launches'] for r in recs)
+            gs['dram_achieved'] = round(b / sum(r['avg_ms'] * r['launches'] for r in recs), 1)
+            gs['dram_frac'] = round(gs['dram_achieved'] / PEAK_HBM_GBS, 4)
+    if tot_ms > 0:
+        roof['dram_achieved'] = round(tot_b / (tot_ms * 1e-3) / 1e9, 1)
+        roof['dram_frac'] = round(roof['dram_achieved'] / PEAK_HBM_GBS, 4)
+        roof['dram_source'] = (f'{t.get("source")} ({os.path.basename(path)}): PMC DRAM bytes per step / kernel '
+                               'time here; achieved / frac stay algorithmic (SURVEY §8(d))')
+
+
 def cpu_threads():
     """The host threads the CPU baseline uses: the box's CPU share for one GPU (OMP_NUM_THREADS, 16 on the
     GPU box; os.cpu_count() there reports the whole machine, whose other cores belong to other jobs)."""
@@ -451,6 +496,7 @@ def run_c5(opt, world, rank, device, emit=True):
             roof['traffic'] = t.get('bytes_per_step')
             roof['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
             roof['traffic_source'] = t.get('source')
+            add_dram(roof, tpath, opt.steps)
         for m in modes[1:]:  # the other table storage on the same graph and batch
             r2, el2 = res[m]
             out[f'{m}_tables'] = {'value': round(r2['achieved'] * world, 1),
@@ -580,12 +626,12 @@ def workload(cfg, name):
 
 
 def brief(r):
-    keep = ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'loss', 'n_gpus')
+    keep = ('value', 'unit', 'ms_per_step', 'dtype', 'config', 'loss', 'n_gpus', 'host_prep')
     out = {k: r[k] for k in keep}
     for k in ('roofline', 'roofline_hbm'):
         if r.get(k):
-            out[k] = {kk: r[k][kk] for kk in ('bound', 'achieved', 'peak', 'unit', 'frac', 'ms_per_step', 'gather_spmm')
-                      if kk in r[k]}
+            out[k] = {kk: r[k][kk] for kk in ('bound', 'achieved', 'peak', 'unit', 'frac', 'ms_per_step', 'gather_spmm',
+                                              'dram_achieved', 'dram_frac') if kk in r[k]}
     return out
 
 
@@ -625,7 +671,9 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
 
     # the launch sizes of every step (compact row sets, padding rows, valid targets), counted by the data pipeline
     # from the batches' host arrays as it stages them — so no count is read back from the device inside a step
+    t_cnt = time.perf_counter()
     counts = [tr.launch_counts(h, global_rows=B_global) for h in host]
+    host_counts_ms = (time.perf_counter() - t_cnt) * 1e3 / max(1, len(host))
 
     def step(i):
         tr.model.convolve_graph()
@@ -679,6 +727,8 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     if hb is not None and name == 'mb' and precision in ('bf16', 'fp32'):
         hb['traffic'], hb['traffic_source'] = hbm_traffic(precision)
         hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'
+        add_dram(hb, os.path.join(ROOT, 'profiles', 'hbm_traffic.json' if precision == 'bf16'
+                                  else 'hbm_traffic_fp32.json'), opt.steps)
     par = (f'dp{world}' + ('-split' if dp_split and world > 1 else '') + ('-zero1' if zero1 and world > 1 else '')
            + ('-gnnshard' if gnn_shard and world > 1 else ''))
     return {'metric': 'train sequences/sec at d=256, seq_len=50, |items|~100k',
@@ -694,6 +744,10 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
                        'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B_local, 'global_batch': B_global,
                        'train_sequences': int(n_rows), 'len_rec': 10, 'dropout': 0.2, 'parallelism': par},
             'loss': round(loss, 5) if math.isfinite(loss) else None,
+            'host_prep': {'launch_counts_ms_per_step': round(host_counts_ms, 3),
+                          'note': 'host data prep, outside the timed region (SURVEY §8(d)): the step\'s launch sizes '
+                                  'counted from the batch\'s host copy by the data pipeline (Trainer.launch_counts); '
+                                  'batches are staged in HBM before timing'},
             'roofline': roof, 'roofline_hbm': hb}
 
 

@@ -329,7 +329,9 @@ struct SegJob {
 // first run goes to its head slot when it continues the previous chunk, the last run to the tail
 // slot when it continues into the next (pass B adds those up).  Keys outside [0, n_out) are never
 // followed (err is set; checked by the host in debug runs).
-template <int LPR>
+// ROLE only names the instantiation (0: embedding backward, 1: classifier one-hot dW) so PMC passes can tell the
+// two callers' launches apart (tools/pmc_traffic.py); the code is the same
+template <int LPR, int ROLE = 0>
 __global__ __launch_bounds__(256) void seg_chunk_kernel(SegJob j0, SegJob j1) {
   constexpr int GROUPS = 256 / LPR;
   constexpr int ENT = GROUPS * SEG_CH;
@@ -534,7 +536,7 @@ struct SplitView {
 // sums added in group order → slot2[sub].  Level 2: one lane group per split adds its level-1
 // sums in sub order to out[key].  Fixed orders → deterministic; a padding run of thousands of
 // pieces is spread over many blocks.
-template <int LPR>
+template <int LPR, int ROLE = 0>
 __global__ __launch_bounds__(1024) void seg_split1_kernel(SegJob j0, SegJob j1) {
   constexpr int GROUPS = 1024 / LPR;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [GROUPS][d]
@@ -584,7 +586,7 @@ __global__ __launch_bounds__(1024) void seg_split1_kernel(SegJob j0, SegJob j1) 
   }
 }
 
-template <int LPR>
+template <int LPR, int ROLE = 0>
 __global__ __launch_bounds__(256) void seg_split2_kernel(SegJob j0, SegJob j1) {
   constexpr int GROUPS = 256 / LPR;
   const SplitView J(j0, j1, blockIdx.y != 0);
@@ -761,18 +763,18 @@ int num_cus() {
   return g_ncu;
 }
 
-template <int LPR>
+template <int LPR, int ROLE>
 void seg_launch(SegJob j0, SegJob j1, int njobs, hipStream_t s) {
   constexpr int GROUPS = 256 / LPR;
   j0.nblocks = c2::ceil_div(c2::ceil_div(j0.n, SEG_CH), GROUPS);  // one lane group per chunk
   j1.nblocks = njobs > 1 ? c2::ceil_div(c2::ceil_div(j1.n, SEG_CH), GROUPS) : 0;
-  seg_chunk_kernel<LPR><<<j0.nblocks + j1.nblocks, 256, 0, s>>>(j0, j1);
+  seg_chunk_kernel<LPR, ROLE><<<j0.nblocks + j1.nblocks, 256, 0, s>>>(j0, j1);
   const int nmax = std::max(j0.n, njobs > 1 ? j1.n : 0);
   if (nmax > SEG_CH) {
     dim3 g1(std::max(1, std::min(max_subs(nmax), 2 * num_cus())), njobs);
-    seg_split1_kernel<LPR><<<g1, 1024, (size_t)(1024 / LPR) * j0.src.d * 4, s>>>(j0, j1);
+    seg_split1_kernel<LPR, ROLE><<<g1, 1024, (size_t)(1024 / LPR) * j0.src.d * 4, s>>>(j0, j1);
     dim3 g2(std::max(1, std::min(c2::ceil_div(c2::ceil_div(nmax, SEG_CH), GROUPS), 2 * num_cus())), njobs);
-    seg_split2_kernel<LPR><<<g2, 256, 0, s>>>(j0, j1);
+    seg_split2_kernel<LPR, ROLE><<<g2, 256, 0, s>>>(j0, j1);
   }
 }
 
@@ -800,15 +802,16 @@ SegJob seg_job(const Plan& p, int n, int n_out, const RowSrc& src, float* out, c
 }
 
 // one or two jobs of the same row width in one launch per pass
+template <int ROLE = 0>
 void seg_dispatch(const SegJob& j0, const SegJob* j1, hipStream_t s) {
   const SegJob& b = j1 ? *j1 : j0;
   const int nj = j1 ? 2 : 1;
   switch (lpr_for(j0.src.d)) {
-    case 64: seg_launch<64>(j0, b, nj, s); break;
-    case 32: seg_launch<32>(j0, b, nj, s); break;
-    case 16: seg_launch<16>(j0, b, nj, s); break;
-    case 8: seg_launch<8>(j0, b, nj, s); break;
-    default: seg_launch<4>(j0, b, nj, s); break;
+    case 64: seg_launch<64, ROLE>(j0, b, nj, s); break;
+    case 32: seg_launch<32, ROLE>(j0, b, nj, s); break;
+    case 16: seg_launch<16, ROLE>(j0, b, nj, s); break;
+    case 8: seg_launch<8, ROLE>(j0, b, nj, s); break;
+    default: seg_launch<4, ROLE>(j0, b, nj, s); break;
   }
 }
 
@@ -998,13 +1001,13 @@ C2_API int c2dsr_ce_onehot_dw_planned(const void* plan, int M, int n, const floa
   const c2::Drop nodrop = c2::make_drop(0, 0, 0.f);
   if (gW) {
     const SegJob j = seg_job(p, M, n + 1, RowSrc{H, D, nodrop, 0, -1.f, rw}, gW, seg, n);
-    seg_dispatch(j, nullptr, s);
+    seg_dispatch<1>(j, nullptr, s);
   }
   if (gb) {
     float* T = (float*)(seg + seg_ws_bytes(M, D));
     (void)hipMemsetAsync(T, 0, (size_t)n * 16, s);
     const SegJob j = seg_job(p, M, n + 1, RowSrc{nullptr, 4, nodrop, 0, -1.f, rw}, T, seg, n);
-    seg_dispatch(j, nullptr, s);
+    seg_dispatch<1>(j, nullptr, s);
     col0_add_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(T, n, gb);
   }
   C2_CHECK_LAUNCH();
