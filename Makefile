@@ -33,9 +33,16 @@ TORCH_FLAGS = -O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIB
 c2dsr_amd/csrc_torch/torch_ops_gen.inc: include/c2dsr.h tools/gen_torch_ops.py
 	python3 tools/gen_torch_ops.py $@
 
-c2dsr_amd/libc2dsr_torch.so: c2dsr_amd/csrc_torch/torch_ops.cpp c2dsr_amd/csrc_torch/torch_ops_gen.inc c2dsr_amd/libc2dsr_hip.so
-	g++ $(TORCH_FLAGS) -shared $< -o $@ -Lc2dsr_amd -lc2dsr_hip -Wl,-rpath,'$$ORIGIN' \
-		-L$(TORCH_DIR)/lib -ltorch -ltorch_cpu -lc10 -lc10_hip -ltorch_hip -Wl,-rpath,$(TORCH_DIR)/lib
+TORCH_SRC := $(wildcard c2dsr_amd/csrc_torch/*.cpp)
+TORCH_OBJ := $(patsubst c2dsr_amd/csrc_torch/%.cpp,build/torch_%.o,$(TORCH_SRC))
+
+build/torch_%.o: c2dsr_amd/csrc_torch/%.cpp c2dsr_amd/csrc_torch/c2t.h c2dsr_amd/csrc_torch/torch_ops_gen.inc include/c2dsr.h
+	@mkdir -p build
+	g++ $(TORCH_FLAGS) -c $< -o $@
+
+c2dsr_amd/libc2dsr_torch.so: $(TORCH_OBJ) c2dsr_amd/libc2dsr_hip.so
+	g++ -shared $(TORCH_OBJ) -o $@ -Lc2dsr_amd -lc2dsr_hip -Wl,-rpath,'$$ORIGIN' \
+		-L$(TORCH_DIR)/lib -ltorch -ltorch_cpu -lc10 -lc10_hip -ltorch_hip -lamdhip64 -Wl,-rpath,$(TORCH_DIR)/lib
 
 clean:
 	rm -rf build c2dsr_amd/libc2dsr_hip.so c2dsr_amd/libc2dsr_prep.so c2dsr_amd/libc2dsr_torch.so

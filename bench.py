@@ -88,31 +88,21 @@ class KernelTimer:
     CREDIT = {'c2dsr_ce_fused_fwd_u': 2, 'c2dsr_ce3_fused_fwd_u': 2, 'c2dsr_ce3b_fused_fwd_u': 2}
 
     def __init__(self, precision):
-        from c2dsr_amd._lib import lib
-        self.lib = lib
         self.names = {'bf16': self.NAMES_BF16, 'fp32': self.NAMES_X3}.get(precision, ('c2dsr_gemm',))
 
-    def start(self):
-        self.lib.timed.clear()
-        self.lib.time_names.update(self.names)
-
-    def stop(self):
-        self.lib.time_names.difference_update(self.names)
-
-    def summary(self):
-        torch.cuda.synchronize()
+    def summary(self, recs):
         per = {}
         ms_all, fl_all = 0.0, 0.0
         for name in self.names:
             ms, fl = [], []
-            for e0, e1, a in self.lib.timed.get(name, []):
+            for t, a in recs.get(name, []):
                 if name == 'c2dsr_gemm':
                     f = 2.0 * a[2] * a[3] * a[4]
                     if f < 1e11:  # only the classifier-head GEMMs
                         continue
                 else:  # (Hb, Wb, bias2, M, n, D, ...)
                     f = 2.0 * a[3] * a[4] * a[5] * self.CREDIT.get(name, 1)
-                ms.append(e0.elapsed_time(e1))
+                ms.append(t)
                 fl.append(f)
             if ms:
                 per[name] = dict(launches=len(ms), avg_ms=round(sum(ms) / len(ms), 4),
@@ -144,42 +134,33 @@ class HbmTimer:
              'c2dsr_embed_bwd_planned_rows', 'c2dsr_gcn_spmm_b16', 'c2dsr_embed_fwd_b16', 'c2dsr_embed_bwd_planned_b16')
 
     def __init__(self, n_rows_table, nnz_by_col_ptr, uniq_by_seq_ptr):
-        from c2dsr_amd._lib import lib
-        self.lib = lib
         self.N = n_rows_table
         self.nnz = nnz_by_col_ptr
         self.uniq = uniq_by_seq_ptr
+        self.names = self.NAMES
 
-    def start(self):
+    def meta_fns(self):
+        """Host-side accounting evaluated at each call: a planned backward's first argument is the seq plan —
+        resolved to its index tensor's distinct-item count; the two-source form adds the rows of its two parts."""
         from c2dsr_amd import ops
-        for n in self.NAMES:
-            self.lib.timed.pop(n, None)
-        self.lib.time_names.update(self.NAMES)
-        # a planned backward's first argument is the seq plan: resolve it to the index tensor at launch
-        self.lib.time_meta['c2dsr_embed_bwd_planned'] = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0]), 0)
-        self.lib.time_meta['c2dsr_embed_bwd_planned_b16'] = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0]), 0)
-        self.lib.time_meta['c2dsr_embed_bwd_planned_rows'] = lambda a: (
-            self.uniq.get(ops.PLAN_SRC.get(a[0]), 0), ops.ROW_COUNT.get(a[4], 0) + ops.ROW_COUNT.get(a[6], 0))
-
-    def stop(self):
-        self.lib.time_names.difference_update(self.NAMES)
-        self.lib.time_meta.pop('c2dsr_embed_bwd_planned', None)
-        self.lib.time_meta.pop('c2dsr_embed_bwd_planned_b16', None)
-        self.lib.time_meta.pop('c2dsr_embed_bwd_planned_rows', None)
+        uniq = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0].data_ptr()), 0)  # noqa: E731
+        return {'c2dsr_embed_bwd_planned': uniq, 'c2dsr_embed_bwd_planned_b16': uniq,
+                'c2dsr_embed_bwd_planned_rows': lambda a: (uniq(a), a[4].shape[0] + a[6].shape[0])}
 
     def launch_bytes(self, name, a):
+        """a: the call's arguments as numbers (pointers as addresses, null 0) + the meta_fns value"""
         if name in ('c2dsr_gcn_spmm', 'c2dsr_gcn_spmm_b16'):  # table bytes per element: 4, or 2 (bf16 tables)
-            d, E, N, tb = a[7], self.nnz[a[5]], self.N, (2 if name.endswith('_b16') else 4)
+            d, E, N, tb = int(a[7]), self.nnz[int(a[5])], self.N, (2 if name.endswith('_b16') else 4)
             from c2dsr_amd import ops
-            if a[0] in ops.SPMM_SLICE:  # a row slice (chunked backward, row-sharded forward): its rows and edges
-                N, E = ops.SPMM_SLICE[a[0]]
-            rows = 1 + (a[14] is not None) + (a[18] != 0.0) + (a[20] is not None)
+            if int(a[0]) in ops.SPMM_SLICE:  # a row slice (chunked backward, row-sharded forward): its rows and edges
+                N, E = ops.SPMM_SLICE[int(a[0])]
+            rows = 1 + (a[14] != 0) + (a[18] != 0.0) + (a[20] != 0)
             return tb * d * E + 8 * E + 4 * (N + 1) + tb * d * N * rows
         if name == 'c2dsr_embed_fwd':
-            n, d = a[2], a[3]
-            reads = (a[4] is not None) + (a[5] is not None) + (a[6] is not None)
+            n, d = int(a[2]), int(a[3])
+            reads = (a[4] != 0) + (a[5] != 0) + (a[6] != 0)
             return n * (16 + 4 * d * reads + 4 * d)
-        n, d = a[2], a[3]
+        n, d = int(a[2]), int(a[3])
         if name == 'c2dsr_embed_fwd_b16':  # (seq, pos, n, d, H, E, P, ..., X): two bf16 table rows, fp32 X
             return n * (16 + 2 * 2 * d + 4 * d)
         if name == 'c2dsr_embed_bwd_planned_b16':  # read dX (fp32); bf16 read-modify-write per distinct item
@@ -188,18 +169,17 @@ class HbmTimer:
             uniq, part_rows = a[-1]
             return n * (16 + 8) + 4 * d * part_rows + 8 * d * uniq
         if name == 'c2dsr_embed_bwd_planned':  # (seq_plan, pos_plan, n, d, gX, .., G, n_items, gP, n_pos, gXin, ..)
-            return n * (16 + 4 * d + (4 * d if a[14] is not None else 0)) + 8 * d * a[-1]
-        return n * (16 + 4 * d + (4 * d if a[14] is not None else 0)) + 8 * d * self.uniq.get(a[0], 0)
+            return n * (16 + 4 * d + (4 * d if a[14] != 0 else 0)) + 8 * d * a[-1]
+        return n * (16 + 4 * d + (4 * d if a[14] != 0 else 0)) + 8 * d * self.uniq.get(int(a[0]), 0)
 
-    def summary(self, steps):
-        torch.cuda.synchronize()
+    def summary(self, recs, steps):
         per, tb, tms = {}, 0.0, 0.0
         for name in self.NAMES:
-            rec = self.lib.timed.get(name, [])
+            rec = recs.get(name, [])
             if not rec:
                 continue
-            ms = sum(e0.elapsed_time(e1) for e0, e1, _ in rec)
-            by = sum(self.launch_bytes(name, a) for _, _, a in rec)
+            ms = sum(t for t, _ in rec)
+            by = sum(self.launch_bytes(name, a) for _, a in rec)
             per[name] = dict(launches=len(rec), avg_ms=round(ms / len(rec), 4), gbs=round(by / (ms * 1e-3) / 1e9, 1),
                              bytes_per_launch=int(by / len(rec)))
             tb += by
@@ -221,6 +201,26 @@ class HbmTimer:
                     traffic=None, kernel='K1 c2dsr_gcn_spmm (fwd+bwd) + K2 c2dsr_embed_fwd/bwd; algorithmic bytes '
                     '(bench.py HbmTimer)', ms_per_step=round(tms / steps, 4), per_kernel=per,
                     gather_spmm=gather_spmm)
+
+
+def timing_begin(*timers):
+    """Bracket the timers' entry points with HIP events from here on (c2dsr::timing_set)."""
+    from c2dsr_amd._lib import lib
+    lib.time_meta = {}
+    for t in timers:
+        if hasattr(t, 'meta_fns'):
+            lib.time_meta.update(t.meta_fns())
+    lib.timing_start(sorted({n for t in timers for n in t.names}))
+
+
+def timing_end():
+    """Stop timing; the records of every bracketed call since timing_begin (name -> [(ms, args)])."""
+    from c2dsr_amd._lib import lib
+    torch.cuda.synchronize()
+    recs = lib.timing_take()
+    lib.timing_start([])
+    lib.time_meta = {}
+    return recs
 
 
 def uniq_counts(batches, host):
@@ -455,7 +455,7 @@ def run_c5(opt, world, rank, device, emit=True):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        ht.start()
+        timing_begin(ht)
         t0 = time.perf_counter()
         for _ in range(opt.steps):
             step()
@@ -463,12 +463,12 @@ def run_c5(opt, world, rank, device, emit=True):
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
-        ht.stop()
+        recs = timing_end()
         if world > 1:
             t = torch.tensor([el], device=device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t)
-        return ht.summary(opt.steps), el
+        return ht.summary(recs, opt.steps), el
 
     modes = ['bf16', 'fp32'] if opt.c5_tables == 'both' else [opt.c5_tables]
     res = {}
@@ -684,8 +684,7 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.start()
-    htimer.start()
+    timing_begin(timer, htimer)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = None
@@ -695,15 +694,14 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    timer.stop()
-    htimer.stop()
+    recs = timing_end()
     if world > 1:
         t = torch.tensor([el], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
     loss = float(last[0].detach())
-    ks = timer.summary()
-    hb = htimer.summary(opt.steps)
+    ks = timer.summary(recs)
+    hb = htimer.summary(recs, opt.steps)
     ms = el / opt.steps * 1e3
     value = B_global * opt.steps / el
     del tr, batches

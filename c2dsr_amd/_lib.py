@@ -1,53 +1,42 @@
-"""ctypes binding of the gfx950 kernel library (``libc2dsr_hip.so``, C ABI in
-``include/c2dsr.h``).
+"""Binding of the gfx950 kernel library (``libc2dsr_hip.so``, C ABI in ``include/c2dsr.h``) through its PyTorch
+operator library ``libc2dsr_torch.so`` (c2dsr_amd/csrc_torch/):
 
-The argument types are read from the header itself, so the binding and the
-declared ABI cannot drift apart.  Tensors are passed as raw device pointers
-(``Tensor.data_ptr()``) and the stream as ``torch.cuda.current_stream().cuda_stream``.
+* ``torch.ops.c2dsr`` — the stage operators the training step runs on (Tensor in / Tensor out, sizes derived from
+  the tensors and checked; stage_ops.cpp), reached as ``stage_ops()``;
+* ``torch.ops.c2dsr_raw`` — one schema op per C-ABI entry point (pointers as tensors, the ABI's int sizes), reached
+  as ``lib(name, *args)`` for the remaining per-kernel calls and ``lib.raw(name)`` for the size / support queries.
 
-There is deliberately no fallback: if the library (or a GPU) is missing, calls
-raise, so nothing silently runs on some other path.
+Every call enqueues on torch's current HIP stream: the ``stream()`` argument the call sites pass (taken from that
+same current stream; the side-stream index plans switch streams with ``torch.cuda.stream``) is dropped.  There is deliberately no fallback: if the libraries (or a GPU) are
+missing, calls raise, so nothing silently runs on some other path.
 """
 from __future__ import annotations
 
-import ctypes
 import os
 import re
 
-import torch  # noqa: F401  (load torch's HIP runtime first: same soname libamdhip64.so.7)
+import numpy as np
+import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('C2DSR_LIB') or os.path.join(_HERE, 'libc2dsr_hip.so')
+TORCH_LIB_PATH = os.environ.get('C2DSR_TORCH_LIB') or os.path.join(_HERE, 'libc2dsr_torch.so')
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'c2dsr.h')
-
-_CTYPES = {
-    'int': ctypes.c_int,
-    'long': ctypes.c_long,
-    'float': ctypes.c_float,
-    'uint32_t': ctypes.c_uint32,
-    'int64_t': ctypes.c_int64,
-    'size_t': ctypes.c_size_t,
-}
 
 
 def parse_header(path: str = HEADER) -> dict:
-    """name -> (restype, [argtypes]) for every ``c2dsr_*`` declaration."""
+    """name -> (return type, [(param name, is_pointer)]) for every ``c2dsr_*`` declaration."""
     text = open(path).read()
     text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
     out = {}
     for m in re.finditer(r'\b(int|size_t)\s+(c2dsr_\w+)\s*\(([^)]*)\)\s*;', text):
         ret, name, args = m.group(1), m.group(2), m.group(3)
-        types = []
+        params = []
         for a in args.split(','):
-            a = a.strip()
-            if not a:
-                continue
-            if '*' in a:
-                types.append(ctypes.c_void_p)
-            else:
-                base = a.replace('const ', '').split()[0]
-                types.append(_CTYPES[base])
-        out[name] = (_CTYPES[ret], types)
+            a = ' '.join(a.split())
+            if a:
+                params.append((a.replace('*', ' ').split()[-1], '*' in a))
+        out[name] = (ret, params)
     return out
 
 
@@ -55,83 +44,97 @@ class HipLibError(RuntimeError):
     pass
 
 
-DEBUG_SYNC = os.environ.get('C2DSR_DEBUG_SYNC', '0') == '1'
+_ops = {}
+
+
+def _load_ops():
+    """torch.ops.c2dsr / c2dsr_raw, loading libc2dsr_torch.so (and through it libc2dsr_hip.so) once."""
+    if not _ops:
+        for p in (LIB_PATH, TORCH_LIB_PATH):
+            if not os.path.exists(p):
+                raise HipLibError(f'{p} not built (run `make` or __graft_entry__.build())')
+        torch.ops.load_library(TORCH_LIB_PATH)
+        _ops['stage'], _ops['raw'] = torch.ops.c2dsr, torch.ops.c2dsr_raw
+    return _ops
+
+
+def stage_ops():
+    """torch.ops.c2dsr (the stage operators; stage_ops.cpp)."""
+    return _load_ops()['stage']
 
 
 class _Lib:
     def __init__(self):
-        self._lib = None
         self._sigs = None
-        self._fns = {}  # name -> bound ctypes function (argtypes set)
-        self.time_names = set()  # entry points bracketed by HIP events (bench.py roofline)
-        self.timed = {}
-        self.time_meta = {}  # name -> fn(args) evaluated at launch; its value is appended to the record
+        self._fns = {}  # name -> (raw op, has trailing stream param)
+        self.time_meta = {}  # name -> fn(call args): a value appended to that call's timing record (bench accounting)
+        self._extra = {}
 
     def load(self):
-        if self._lib is not None:
-            return self._lib
-        if not os.path.exists(LIB_PATH):
-            raise HipLibError(f'{LIB_PATH} not built (run `make` or __graft_entry__.build())')
-        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-        sigs = parse_header()
-        for name, (res, args) in sigs.items():
-            f = getattr(lib, name)
-            f.restype = res
-            f.argtypes = args
-        self._lib, self._sigs = lib, sigs
-        return lib
+        """Load the operator libraries (import check of __graft_entry__.build()); returns the raw op namespace."""
+        if self._sigs is None:
+            self._sigs = parse_header()
+        return _load_ops()['raw']
 
     @property
     def symbols(self) -> list:
         self.load()
         return sorted(self._sigs)
 
+    def _fn(self, name):
+        f = self._fns.get(name)
+        if f is None:
+            raw = self.load()
+            ret, params = self._sigs[name]
+            has_stream = bool(params) and params[-1] == ('stream', True)
+            f = self._fns[name] = (getattr(raw, name[len('c2dsr_'):]), has_stream)
+        return f
+
     def __call__(self, name: str, *args):
-        fn = self._fns.get(name)
-        if fn is None:
-            fn = self._fns[name] = getattr(self.load(), name)
-        lib = self._lib
-        conv = [a.data_ptr() if isinstance(a, torch.Tensor) else a for a in args]
-        if not DEBUG_SYNC and name not in self.time_names:  # the common path: one ctypes call
-            rc = fn(*conv)
-            if rc != 0:
-                raise HipLibError(f'{name} failed with hipError {rc}')
-            return rc
-        if name in self.time_names:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            rc = getattr(lib, name)(*conv)
-            e1.record()
-            meta = self.time_meta.get(name)
-            rec = conv + [meta(conv)] if meta is not None else conv
-            self.timed.setdefault(name, []).append((e0, e1, rec))
-        elif DEBUG_SYNC:  # C2DSR_DEBUG_SYNC=1: attribute an asynchronous device fault to its entry point
-            try:
-                torch.cuda.synchronize()
-            except Exception as e:  # noqa: BLE001
-                raise HipLibError(f'device fault before {name} (after the previous entry point)') from e
-            rc = getattr(lib, name)(*conv)
-            try:
-                torch.cuda.synchronize()
-            except Exception as e:  # noqa: BLE001
-                raise HipLibError(f'device fault in {name} (args {conv})') from e
-        else:
-            rc = getattr(lib, name)(*conv)
-        if rc != 0:
-            raise HipLibError(f'{name} failed with hipError {rc}')
-        return rc
+        """One entry point on torch's current stream; tensors (or None) for pointers, numpy arrays for the host
+        descriptor arrays, ints / floats for scalars.  Raises HipLibError on a failed launch."""
+        op, has_stream = self._fn(name)
+        if self.time_meta and name in self.time_meta:
+            self._extra.setdefault(name, []).append(self.time_meta[name](args))
+        if has_stream:
+            args = args[:-1]  # the call sites' stream() argument: the op uses torch's current stream itself
+        args = [torch.from_numpy(a) if type(a) is np.ndarray else a for a in args]
+        try:
+            return op(*args)
+        except RuntimeError as e:
+            raise HipLibError(str(e)) from None
 
     def raw(self, name: str):
-        fn = self._fns.get(name)
-        if fn is None:
-            fn = self._fns[name] = getattr(self.load(), name)
-        return fn
+        """The op of a query entry point (no stream: ``*_supported``, workspace sizes), called with its ints."""
+        return self._fn(name)[0]
+
+    # ---- in-process event timing of chosen entry points (bench.py): records (ms, args as numbers + extras)
+    def timing_start(self, names):
+        """Bracket every later call of these entry points (made anywhere: here or inside a stage operator) with HIP
+        events on its launch stream; an empty list stops."""
+        self._extra = {}
+        stage_ops().timing_set(sorted(names))
+
+    def timing_take(self) -> dict:
+        """name -> [(ms, [the call's arguments as numbers (pointers as addresses, null 0), extras...])] in launch
+        order; a time_meta value of the call (host-side calls only) is appended last."""
+        names, ms, meta, lens = stage_ops().timing_take()
+        out, o = {}, 0
+        for n, t, k in zip(names, ms, lens):
+            out.setdefault(n, []).append((t, list(meta[o:o + k])))
+            o += k
+        for n, vals in self._extra.items():
+            for rec, v in zip(out.get(n, []), vals):
+                rec[1].append(v)
+        self._extra = {}
+        return out
 
 
 lib = _Lib()
 
 
 def stream() -> int:
+    """The current HIP stream (the kernels' launch stream; raises without a device: no CPU fallback)."""
     if not torch.cuda.is_available():
         raise HipLibError('c2dsr_amd kernels need a HIP device (no CPU fallback)')
     return torch.cuda.current_stream().cuda_stream

@@ -1,0 +1,91 @@
+// Host-side helpers shared by the PyTorch operator layer (libc2dsr_torch.so): tensor checks, the current HIP
+// stream, and `launch`, through which every call into the kernel library (include/c2dsr.h) goes — it turns a
+// nonzero hipError_t into a RuntimeError naming the entry point, and optionally (a) brackets the call with HIP
+// events for bench.py's in-process kernel timing (timing_set / timing_take) and (b) synchronises around it to pin
+// an asynchronous fault on its entry point (C2DSR_DEBUG_SYNC=1).
+#pragma once
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstdint>
+#include <optional>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "c2dsr.h"
+
+namespace c2t {
+
+inline void* stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
+
+inline void* ptr(const std::optional<at::Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
+inline void* ptr(const at::Tensor& t) { return t.defined() ? t.data_ptr() : nullptr; }
+
+// device / dtype check of a pointer argument (a host descriptor array must be a CPU tensor)
+inline void check(const char* op, const char* arg, const std::optional<at::Tensor>& t, bool host,
+                  std::optional<at::ScalarType> dt) {
+  if (!t.has_value() || !t->defined()) return;
+  if (host) {
+    TORCH_CHECK(t->device().is_cpu(), "c2dsr::", op, ": ", arg, " is a host array (CPU tensor expected)");
+  } else {
+    TORCH_CHECK(t->is_cuda(), "c2dsr::", op, ": ", arg, " must be on the HIP device (no CPU fallback)");
+  }
+  if (dt.has_value()) {
+    const auto s = t->scalar_type();
+    const bool ok = s == *dt || (*dt == at::kInt && s == at::kUInt32);
+    TORCH_CHECK(ok, "c2dsr::", op, ": ", arg, " has dtype ", s, ", expected ", *dt);
+  }
+}
+
+// ---- timing / debug registry (defined in torch_ops.cpp)
+struct Rec {
+  std::string name;
+  hipEvent_t e0, e1;
+  std::vector<double> meta;
+};
+bool timed(const char* name);  // cheap when no name is registered
+void record(const char* name, hipEvent_t e0, hipEvent_t e1, std::vector<double>&& meta);
+bool debug_sync();
+void sync_check(const char* name, const char* where);
+
+template <class T>
+inline double as_meta(T v) {
+  if constexpr (std::is_pointer_v<T>)
+    return (double)(uintptr_t)v;
+  else
+    return (double)v;
+}
+
+// one call into the kernel library: F returns 0 or a hipError_t; `extra` values are appended to the timing record
+// (bench.py's accounting: e.g. the compact row counts of a fused stage)
+template <class F, class... A>
+inline int64_t launch_x(const char* name, std::initializer_list<double> extra, F fn, A... a) {
+  const bool dbg = debug_sync();
+  if (dbg) sync_check(name, "before");
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  const bool tm = timed(name);
+  if (tm) {
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, (hipStream_t)stream());
+  }
+  const int rc = fn(a...);
+  if (tm) {
+    (void)hipEventRecord(e1, (hipStream_t)stream());
+    std::vector<double> meta{as_meta(a)...};
+    meta.insert(meta.end(), extra.begin(), extra.end());
+    record(name, e0, e1, std::move(meta));
+  }
+  if (dbg) sync_check(name, "in");
+  TORCH_CHECK(rc == 0, name, " failed with hipError ", rc);
+  return rc;
+}
+template <class F, class... A>
+inline int64_t launch(const char* name, F fn, A... a) {
+  return launch_x(name, {}, fn, a...);
+}
+
+}  // namespace c2t

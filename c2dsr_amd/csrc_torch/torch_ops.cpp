@@ -1,51 +1,103 @@
 // PyTorch-ROCm extension of the gfx950 kernel library (north_star: "exposed through a PyTorch-ROCm C++/HIP
-// extension"): TORCH_LIBRARY(c2dsr, m) registers every C-ABI entry point of include/c2dsr.h as a
-// schema op (torch.ops.c2dsr.<name without the c2dsr_ prefix>, generated from the header: torch_ops_gen.inc), with
-// tensor arguments checked for device and dtype.  The training step's Python host side (c2dsr_amd/ops.py,
-// losshead.py) binds the same library through ctypes (c2dsr_amd/_lib.py); these ops are the interface for
-// TorchScript / C++ callers, and tests/test_gpu_torch_ops.py holds them bit-equal to the ctypes path.
-// Every op enqueues on the current HIP stream and raises (RuntimeError) on a bad argument or a hipError.
-#include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
+// extension").  Two operator namespaces:
+//   * c2dsr_raw:: — every C-ABI entry point of include/c2dsr.h as a schema op (generated from the header:
+//     torch_ops_gen.inc): pointers as tensors (written ones annotated Tensor(a!)), checked for device and dtype,
+//     sizes as the ABI's ints.  The host side's remaining per-kernel calls (c2dsr_amd/_lib.py `lib`) go here.
+//   * c2dsr:: — the stage operators the training step runs on (stage_ops.cpp: Tensor in / Tensor out, every size
+//     derived from the tensors and every extent checked), plus the timing hooks below.
+// Every op enqueues on the current HIP stream and raises RuntimeError on a bad argument or a hipError.
 #include <torch/library.h>
 
-#include <optional>
+#include <cstdlib>
+#include <mutex>
+#include <set>
+#include <tuple>
 
-#include "c2dsr.h"
+#include "c2t.h"
 
-namespace c2dsr_torch {
+namespace c2t {
 
-inline void* stream() { return (void*)c10::hip::getCurrentHIPStream().stream(); }
+// ---- event timing of chosen entry points (bench.py: the K5 / K1 / K2 launches inside the timed region)
+static std::atomic<bool> g_any{false};
+static std::mutex g_mu;
+static std::set<std::string> g_names;
+static std::vector<Rec> g_recs;
 
-inline void* ptr(const std::optional<at::Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr() : nullptr; }
-
-inline void check(const char* op, const char* arg, const std::optional<at::Tensor>& t, bool host,
-                  std::optional<at::ScalarType> dt) {
-  if (!t.has_value() || !t->defined()) return;
-  if (host) {
-    TORCH_CHECK(t->device().is_cpu(), "c2dsr::", op, ": ", arg, " is a host array (CPU tensor expected)");
-  } else {
-    TORCH_CHECK(t->is_cuda(), "c2dsr::", op, ": ", arg, " must be on the HIP device (no CPU fallback)");
-  }
-  if (dt.has_value()) {
-    const auto s = t->scalar_type();
-    const bool ok = s == *dt || (*dt == at::kInt && s == at::kUInt32);
-    TORCH_CHECK(ok, "c2dsr::", op, ": ", arg, " has dtype ", s, ", expected ", *dt);
-  }
+bool timed(const char* name) {
+  if (!g_any.load(std::memory_order_relaxed)) return false;
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_names.count(name) != 0;
 }
 
-}  // namespace c2dsr_torch
+void record(const char* name, hipEvent_t e0, hipEvent_t e1, std::vector<double>&& meta) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_recs.push_back(Rec{name, e0, e1, std::move(meta)});
+}
+
+bool debug_sync() {
+  static const bool on = [] {
+    const char* v = std::getenv("C2DSR_DEBUG_SYNC");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
+void sync_check(const char* name, const char* where) {
+  const hipError_t e = hipStreamSynchronize((hipStream_t)stream());
+  TORCH_CHECK(e == hipSuccess, "device fault ", where, " ", name, " (hipError ", (int)e, ")");
+}
+
+}  // namespace c2t
 
 #include "torch_ops_gen.inc"
 
-TORCH_LIBRARY(c2dsr, m) {
-  C2DSR_GENERATED_DEFS(m)
-  m.def("generated_count() -> int");
+// names of the entry points to bracket with events (empty: off); earlier records are dropped
+static void op_timing_set(const std::vector<std::string>& names) {
+  std::lock_guard<std::mutex> lk(c2t::g_mu);
+  c2t::g_names = std::set<std::string>(names.begin(), names.end());
+  for (auto& r : c2t::g_recs) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
+  c2t::g_recs.clear();
+  c2t::g_any.store(!c2t::g_names.empty());
+}
+
+// the records since timing_set, in launch order: (names, ms, meta values, meta lengths); synchronises on the events
+static std::tuple<std::vector<std::string>, std::vector<double>, std::vector<double>, std::vector<int64_t>>
+op_timing_take() {
+  std::lock_guard<std::mutex> lk(c2t::g_mu);
+  std::vector<std::string> names;
+  std::vector<double> ms, meta;
+  std::vector<int64_t> lens;
+  for (auto& r : c2t::g_recs) {
+    float t = 0.f;
+    (void)hipEventSynchronize(r.e1);
+    (void)hipEventElapsedTime(&t, r.e0, r.e1);
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+    names.push_back(r.name);
+    ms.push_back(t);
+    meta.insert(meta.end(), r.meta.begin(), r.meta.end());
+    lens.push_back((int64_t)r.meta.size());
+  }
+  c2t::g_recs.clear();
+  return {names, ms, meta, lens};
 }
 
 static int64_t op_generated_count() { return C2DSR_GENERATED_COUNT; }
 
-TORCH_LIBRARY_IMPL(c2dsr, CompositeExplicitAutograd, m) {
+TORCH_LIBRARY(c2dsr_raw, m) {
+  C2DSR_GENERATED_DEFS(m)
+  m.def("generated_count() -> int");
+}
+
+TORCH_LIBRARY_IMPL(c2dsr_raw, CompositeExplicitAutograd, m) {
   C2DSR_GENERATED_IMPLS(m)
   m.impl("generated_count", &op_generated_count);
+}
+
+TORCH_LIBRARY_FRAGMENT(c2dsr, m) {
+  m.def("timing_set(str[] names) -> ()", &op_timing_set);
+  m.def("timing_take() -> (str[], float[], float[], int[])", &op_timing_take);
 }

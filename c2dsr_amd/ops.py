@@ -124,7 +124,7 @@ class _WeightImages:
             for i in range(0, len(done), 64):
                 chunk = done[i:i + 64]
                 desc = np.asarray(recs[6 * i:6 * (i + len(chunk))], dtype=np.int64)
-                lib(fn, desc.ctypes.data, len(chunk), stream())
+                lib(fn, desc, len(chunk), stream())
             for key, W, y in done:
                 self.cache[key] = ((self.epoch, W._version), y, W)
         for key, (W, y) in self.known.items():
@@ -151,7 +151,7 @@ class _WeightImages:
             rows, cols = (Cc, R) if trans else (R, Cc)
             y = torch.zeros(-(-rows // 32) * 32, cols, device=W.device, dtype=torch.bfloat16)
             desc = np.asarray([W.data_ptr(), y.data_ptr(), R, Cc, W.stride(0), int(trans)], dtype=np.int64)
-            lib('c2dsr_to_bf16_frag_multi', desc.ctypes.data, 1, stream())
+            lib('c2dsr_to_bf16_frag_multi', desc, 1, stream())
         else:
             y = to_bf16(W, trans) if layout is None else to_split_bf16(W, trans, frag=layout == 'frag')
         self.cache[key] = (tag, y, W)
@@ -183,7 +183,7 @@ def to_split_bf16(X, trans=False, frag=False):
     else:
         y = torch.empty(rows, 2 * cols, device=X.device, dtype=torch.bfloat16)
     desc = np.asarray([X.data_ptr(), y.data_ptr(), R, Cc, X.stride(0), int(trans)], dtype=np.int64)
-    lib('c2dsr_to_split_bf16_frag_multi' if frag else 'c2dsr_to_split_bf16_multi', desc.ctypes.data, 1, stream())
+    lib('c2dsr_to_split_bf16_frag_multi' if frag else 'c2dsr_to_split_bf16_multi', desc, 1, stream())
     return y
 
 
@@ -292,9 +292,9 @@ class WGradBatch:
                 desc = np.asarray([v for dY, X, T in chunk for v in (dY.data_ptr(), N, X.data_ptr(), D, T)],
                                   dtype=np.int64)
                 if x3:
-                    lib('c2dsr_wgemm_x3_multi', desc.ctypes.data, len(chunk), N, D, 1.0, dW, db, ws, s)
+                    lib('c2dsr_wgemm_x3_multi', desc, len(chunk), N, D, 1.0, dW, db, ws, s)
                 else:
-                    lib('c2dsr_wgemm_multi', desc.ctypes.data, len(chunk), N, D, int(dt == torch.bfloat16), 1.0, dW,
+                    lib('c2dsr_wgemm_multi', desc, len(chunk), N, D, int(dt == torch.bfloat16), 1.0, dW,
                         db, ws, s)
         self.groups = {}
 
@@ -770,9 +770,10 @@ class IndexPlan:
         dev = whole.device
         side = side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))  # the indices and the buffer are ready
-        for (idx, n_keys), buf, nb in zip(pairs, bufs, sizes):
-            PLAN_SRC[buf.data_ptr()] = idx.data_ptr()
-            lib('c2dsr_index_plan', idx, idx.numel(), int(n_keys), buf, nb, side.cuda_stream)
+        with torch.cuda.stream(side):
+            for (idx, n_keys), buf, nb in zip(pairs, bufs, sizes):
+                PLAN_SRC[buf.data_ptr()] = idx.data_ptr()
+                lib('c2dsr_index_plan', idx, idx.numel(), int(n_keys), buf, nb, side.cuda_stream)
         whole.record_stream(side)
         ev = torch.cuda.Event()
         ev.record(side)

@@ -294,7 +294,7 @@ def test_wgemm_x3_matches_float64(T, N):
     desc = np.asarray([v for y, x, t in zip(dYd, Xd, Ts) for v in (y.data_ptr(), N, x.data_ptr(), D, t)],
                       dtype=np.int64)
     dWm = torch.full((N, D), 0.5, device=DEV)
-    lib('c2dsr_wgemm_x3_multi', desc.ctypes.data, 2, N, D, 1.0, dWm, None, ws, stream())
+    lib('c2dsr_wgemm_x3_multi', desc, 2, N, D, 1.0, dWm, None, ws, stream())
     torch.cuda.synchronize()
     assert rel(dWm, 0.5 + sum(y.double().T @ x.double() for y, x in zip(dYs, Xs))) < TOL
 
@@ -314,7 +314,7 @@ def test_split_weight_images_multi():
         outs.append((y, to_split_bf16(W, bool(tr))))
         recs += [W.data_ptr(), y.data_ptr(), R, C, W.stride(0), tr]
     desc = np.asarray(recs, dtype=np.int64)
-    lib('c2dsr_to_split_bf16_multi', desc.ctypes.data, 3, stream())
+    lib('c2dsr_to_split_bf16_multi', desc, 3, stream())
     torch.cuda.synchronize()
     for y, ref in outs:
         assert torch.equal(y, ref)
@@ -380,7 +380,7 @@ def test_rgemm_b16_fragment_image(N, K, tr):
     R, C = W.shape
     frag = torch.zeros(-(-N // 32) * 32, K, device=DEV, dtype=torch.bfloat16)
     desc = np.asarray([W.data_ptr(), frag.data_ptr(), R, C, W.stride(0), tr], dtype=np.int64)
-    lib('c2dsr_to_bf16_frag_multi', desc.ctypes.data, 1, stream())
+    lib('c2dsr_to_bf16_frag_multi', desc, 1, stream())
     torch.cuda.synchronize()
     n, k = torch.meshgrid(torch.arange(N), torch.arange(K), indexing='ij')
     assert torch.equal(frag.cpu().reshape(-1)[b16_frag_index(n, k, K)], row.cpu())

@@ -166,9 +166,10 @@ def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
     # gX given as two compact row sources (the row-subset attention layer, d >= 64): the same sums as on the
     # combined rows
     if d < 64:  # not supported there: refused
-        assert lib.raw('c2dsr_embed_bwd_planned_rows')(sp.get().data_ptr(), None, n_rows, d, None, None, None, None,
-                                                       0, 0, 0.0, 0, 1.0, None, n_items, None, L, None, 0,
-                                                       None) != 0
+        from c2dsr_amd._lib import HipLibError
+        with pytest.raises(HipLibError, match='hipError 1'):
+            lib('c2dsr_embed_bwd_planned_rows', sp.get(), None, n_rows, d, None, None, None, None, 0, 0, 0.0, 0, 1.0,
+                None, n_items, None, L, None, 0, stream())
     else:
         ma, mb = rng.random(n_rows) < 0.4, rng.random(n_rows) < 0.6
         inv_a, inv_b = np.full(n_rows, -1, np.int32), np.full(n_rows, -1, np.int32)
@@ -907,7 +908,7 @@ def test_to_bf16_multi_equals_single():
         outs.append(y)
         recs += [X.data_ptr(), y.data_ptr(), R, C, X.stride(0), tr]
     desc = np.asarray(recs, dtype=np.int64)
-    lib('c2dsr_to_bf16_multi', desc.ctypes.data, len(mats), stream())
+    lib('c2dsr_to_bf16_multi', desc, len(mats), stream())
     torch.cuda.synchronize()
     for (X, tr), y in zip(mats, outs):
         if X.numel():
@@ -1015,7 +1016,7 @@ def test_wgemm_multi_segments(b16):
     for _ in range(2):
         dW = torch.full((N, D), 0.5, device=DEV)
         db = torch.full((N,), 0.25, device=DEV)
-        lib('c2dsr_wgemm_multi', desc.ctypes.data, len(Ts), N, D, int(b16), 1.0, dW, db, ws, stream())
+        lib('c2dsr_wgemm_multi', desc, len(Ts), N, D, int(b16), 1.0, dW, db, ws, stream())
         outs.append((dW, db))
     torch.cuda.synchronize()
     r = lambda t: t.to(torch.bfloat16).double()  # noqa: E731  (the MFMA operands)

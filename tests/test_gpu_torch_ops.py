@@ -1,6 +1,8 @@
-"""The TORCH_LIBRARY(c2dsr) ops (c2dsr_amd/libc2dsr_torch.so) run the same kernels as the ctypes binding the
-training step uses: a GCN SpMM round with dropout, the embedding gather and a split-bf16 projection, each called
-both ways on the same inputs — bit-identical outputs."""
+"""The operator library (c2dsr_amd/libc2dsr_torch.so: c2dsr_raw:: and the stage ops the training step uses) runs the
+same kernels as a direct ctypes call of the C ABI (the binding INTEGRATION.md §3 shows a maintainer would add): a GCN
+SpMM round with dropout, the embedding gather and a split-bf16 projection, each called both ways on the same inputs
+— bit-identical outputs."""
+import ctypes
 import os
 
 import numpy as np
@@ -20,11 +22,34 @@ def _ext():
     yield
 
 
+_CT = {'int': ctypes.c_int, 'long': ctypes.c_long, 'float': ctypes.c_float, 'uint32_t': ctypes.c_uint32,
+       'int64_t': ctypes.c_int64, 'size_t': ctypes.c_size_t}
+
+
+def _cabi(name):
+    """c2dsr_<name> of libc2dsr_hip.so through ctypes, argument types from include/c2dsr.h; tensors → data_ptr,
+    the current stream appended."""
+    import re
+    from c2dsr_amd._lib import HEADER, LIB_PATH
+    text = re.sub(r'/\*.*?\*/', '', open(HEADER).read(), flags=re.S)
+    m = re.search(r'\bint\s+c2dsr_' + name + r'\s*\(([^)]*)\)\s*;', text)
+    types = []
+    for a in m.group(1).split(','):
+        a = a.strip()
+        types.append(ctypes.c_void_p if '*' in a else _CT[a.replace('const ', '').split()[0]])
+    f = getattr(ctypes.CDLL(LIB_PATH), 'c2dsr_' + name)
+    f.restype, f.argtypes = ctypes.c_int, types
+
+    def call(*args):
+        conv = [a.data_ptr() if isinstance(a, torch.Tensor) else a for a in args]
+        assert f(*conv, torch.cuda.current_stream().cuda_stream) == 0
+    return call
+
+
 def test_torch_ops_equal_ctypes_path():
-    from c2dsr_amd._lib import lib, stream
     from c2dsr_amd.graph import CSRGraph, DeviceGraph
     from c2dsr_amd.ops import rgemm, to_split_bf16
-    T = torch.ops.c2dsr
+    T = torch.ops.c2dsr_raw
     g = torch.Generator().manual_seed(11)
     # GCN SpMM (one propagation round: mask on the gathered rows, mean epilogue) over a Zipf-ish graph
     n, d = 3000, 256
@@ -42,7 +67,7 @@ def test_torch_ops_equal_ctypes_path():
         Y = torch.empty(n, d, device=DEV)
         args = (work, n_work, split, n_split, part, col, v, d, X, 7, 9, 0.2, 0, 0.5, X, 0.5, 0.0, -1, 0.0, Y, None)
         if way == 'ctypes':
-            lib('c2dsr_gcn_spmm', *args, stream())
+            _cabi('gcn_spmm')(*args)
         else:
             T.gcn_spmm(*args)
         outs.append(Y)
@@ -58,7 +83,7 @@ def test_torch_ops_equal_ctypes_path():
         Xo = torch.empty(B * L, d, device=DEV)
         args = (seq, pos, B * L, d, X, X, None, P, 16.0, 3, 4, 0.2, 0, Xo)
         if way == 'ctypes':
-            lib('c2dsr_embed_fwd', *args, stream())
+            _cabi('embed_fwd')(*args)
         else:
             T.embed_fwd(*args)
         outs.append(Xo)
@@ -70,6 +95,6 @@ def test_torch_ops_equal_ctypes_path():
     Wx = to_split_bf16(W)
     C0 = rgemm(A, Wx, torch.empty(M, N, device=DEV), M=M, N=N, K=K, bias=b, x3=True)
     C1 = torch.empty(M, N, device=DEV)
-    T.rgemm_x3(M, N, K, A, K, Wx, 2 * K, C1, N, 1.0, 0.0, b, 0, 0, 0, 0.0, 0, None, 0, None, None, 0.0)
+    _cabi('rgemm_x3')(M, N, K, A, K, Wx, 2 * K, C1, N, 1.0, 0.0, b, 0, 0, 0, 0.0, 0, None, 0, None, None, 0.0)
     torch.cuda.synchronize()
     assert torch.equal(C0, C1)
