@@ -140,12 +140,11 @@ class HbmTimer:
         self.names = self.NAMES
 
     def meta_fns(self):
-        """Host-side accounting evaluated at each call: a planned backward's first argument is the seq plan —
-        resolved to its index tensor's distinct-item count; the two-source form adds the rows of its two parts."""
+        """Host-side accounting evaluated at each host-side call (the C5 bf16-table backward, bench-driven): its
+        first argument is the seq plan — resolved to the index tensor it sorts.  The stage operators append the
+        same (and the compact parts' row count) to their own records."""
         from c2dsr_amd import ops
-        uniq = lambda a: self.uniq.get(ops.PLAN_SRC.get(a[0].data_ptr()), 0)  # noqa: E731
-        return {'c2dsr_embed_bwd_planned': uniq, 'c2dsr_embed_bwd_planned_b16': uniq,
-                'c2dsr_embed_bwd_planned_rows': lambda a: (uniq(a), a[4].shape[0] + a[6].shape[0])}
+        return {'c2dsr_embed_bwd_planned_b16': lambda a: float(ops.PLAN_SRC.get(a[0].data_ptr(), 0))}
 
     def launch_bytes(self, name, a):
         """a: the call's arguments as numbers (pointers as addresses, null 0) + the meta_fns value"""
@@ -163,13 +162,13 @@ class HbmTimer:
         n, d = int(a[2]), int(a[3])
         if name == 'c2dsr_embed_fwd_b16':  # (seq, pos, n, d, H, E, P, ..., X): two bf16 table rows, fp32 X
             return n * (16 + 2 * 2 * d + 4 * d)
+        # planned backwards: the last meta value is the index tensor the seq plan sorts (its distinct items)
         if name == 'c2dsr_embed_bwd_planned_b16':  # read dX (fp32); bf16 read-modify-write per distinct item
-            return n * (16 + 4 * d) + 4 * d * a[-1]
-        if name == 'c2dsr_embed_bwd_planned_rows':  # (.., n, d, gXa, inv_a, gXb, inv_b, ..) + (uniq, rows of parts)
-            uniq, part_rows = a[-1]
-            return n * (16 + 8) + 4 * d * part_rows + 8 * d * uniq
+            return n * (16 + 4 * d) + 4 * d * self.uniq.get(int(a[-1]), 0)
+        if name == 'c2dsr_embed_bwd_planned_rows':  # (.., n, d, gXa, inv_a, gXb, inv_b, ..) + (rows of parts, seq)
+            return n * (16 + 8) + 4 * d * a[-2] + 8 * d * self.uniq.get(int(a[-1]), 0)
         if name == 'c2dsr_embed_bwd_planned':  # (seq_plan, pos_plan, n, d, gX, .., G, n_items, gP, n_pos, gXin, ..)
-            return n * (16 + 4 * d + (4 * d if a[14] != 0 else 0)) + 8 * d * a[-1]
+            return n * (16 + 4 * d + (4 * d if a[14] != 0 else 0)) + 8 * d * self.uniq.get(int(a[-1]), 0)
         return n * (16 + 4 * d + (4 * d if a[14] != 0 else 0)) + 8 * d * self.uniq.get(int(a[0]), 0)
 
     def summary(self, recs, steps):

@@ -62,7 +62,7 @@ inline double as_meta(T v) {
 // one call into the kernel library: F returns 0 or a hipError_t; `extra` values are appended to the timing record
 // (bench.py's accounting: e.g. the compact row counts of a fused stage)
 template <class F, class... A>
-inline int64_t launch_x(const char* name, std::initializer_list<double> extra, F fn, A... a) {
+inline int64_t launch_x(const char* name, const std::vector<double>& extra, F fn, A... a) {
   const bool dbg = debug_sync();
   if (dbg) sync_check(name, "before");
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -85,7 +85,7 @@ inline int64_t launch_x(const char* name, std::initializer_list<double> extra, F
 }
 template <class F, class... A>
 inline int64_t launch(const char* name, F fn, A... a) {
-  return launch_x(name, {}, fn, a...);
+  return launch_x(name, std::vector<double>{}, fn, a...);
 }
 
 }  // namespace c2t

@@ -194,6 +194,17 @@ class SelfAttention(nn.Module):
     def forward_items(self, seq, pos, H, tok, E, sink, pass_id):
         """Fused C2DSR.py:65-71 + encoders.py:29-33: gather (H[seq]+E[seq])·√d + P[pos], dropout, encoder."""
         p, k = self._drop(pass_id, 0, DK.K_INPUT)
+        if self.training and not self.norm_first and self.n_attn == 1:
+            # the training step's fast path: the whole pass as one stage operator each way (ops.EncoderPassFn)
+            rs, ks = self.state.need.get(pass_id), self.state.pad_rows.get(pass_id)
+            B, L = seq.shape
+            if rs is not None and ks is not None and ops.fused_pass_ok(self.precision, B, L, self.d, self.n_head):
+                keys = [k] + [self._drop(pass_id, 0, kind)[1]
+                              for kind in (DK.K_ATTN, DK.K_SA, DK.K_FF_MID, DK.K_FF_OUT)]
+                outc = ops.EncoderPassFn.apply(tok, E, self.pos_emb.weight, seq, pos, H, self, self.encoder.norm, rs,
+                                               ks, keys, p, self.state.row_offset, self.precision, sink,
+                                               math.sqrt(self.d))
+                return outc if self.state.compact_out else ops.ExpandRowsFn.apply(outc, rs, (B, L, self.d))
         link = ops.RowsGrad() if self.training else None
         x = ops.EmbedFn.apply(tok, E, self.pos_emb.weight, seq, pos, H, math.sqrt(self.d), p, k,
                               self.state.row_offset, sink, self.idx_pad, link)

@@ -11,13 +11,18 @@ import numpy as np
 import torch
 from torch.autograd import Function
 
-from ._lib import HipLibError, lib, stream, require_device
+from ._lib import HipLibError, lib, stream, require_device, stage_ops
 from .dp import notify_lookup, notify_rows, notify_table, row_cuts
 
 # precision modes: FP32 = the reference's precision (fp32 results; products on split-bf16 MFMAs where a kernel
 # exists — ce3.hip —, exact fp32-input MFMA elsewhere), BF16 = bf16 operands with fp32 accumulation,
 # FP32_EXACT = exact fp32-input MFMA for every product (materialised logits; the A/B check of FP32)
 FP32, BF16, FP32_EXACT = 0, 1, 2
+
+
+def flat_keys(keys):
+    """[(k0, k1), …] → [k0, k1, …] (the stage operators' int[] keys)"""
+    return [int(v) for k in keys for v in k]
 
 
 def _grad_target(param):
@@ -634,12 +639,17 @@ class GCNFn(Function):
         require_device(E)
         inv = 1.0 / (n_gnn + 1)
         rows = None
-        if shard is not None and n_gnn > 0:
-            out_full = shard.buffer(E)
-            out = out_full[:E.shape[0]]
-            rows = shard.rows(E.shape[0])
-        else:
-            out = torch.empty_like(E)
+        if shard is None or n_gnn == 0:  # the whole table: one stage operator (all rounds)
+            work, _, split, _, n_slots, col, val = graph.plan(False)
+            out = stage_ops().gcn_propagate(E, work, split, col, val, n_slots, n_gnn, float(p), flat_keys(keys))
+            ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
+            ctx.E = E
+            ctx.mark_non_differentiable(out)
+            ctx.set_materialize_grads(False)
+            return out, torch.empty((), device=E.device)
+        out_full = shard.buffer(E)
+        out = out_full[:E.shape[0]]
+        rows = shard.rows(E.shape[0])
         if n_gnn == 0:  # H = E
             spmm(graph, False, E, (0, 0), 0.0, 0, 0.0, E, 1.0, 0.0, -1, 0.0, out)
         h_prev = E
@@ -672,26 +682,27 @@ class GCNFn(Function):
             return (None,) * 8
         g = ctx.graph
         n = ctx.n_gnn
-        inv = 1.0 / (n + 1)
         direct = E.grad is not None
         gE = E.grad if direct else torch.zeros_like(E)
-        if n == 0:  # H = E: gE += G (all rows) + direct lookup (rows != pad)
-            spmm(g, True, G, (0, 0), 0.0, 1, 0.0, G, 1.0, 1.0, ctx.pad_row, 1.0, gE)
-        else:
-            X, alpha = G, inv
-            for k in range(n, 1, -1):  # T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k
-                T = torch.empty_like(E)
-                spmm(g, True, X, ctx.keys[k - 1], ctx.p, 1, alpha, G, inv, 0.0, -1, 0.0, T)
-                X, alpha = T, 1.0
-            cuts = row_cuts(ctx.sink.state, E) if direct else None
-            if cuts is None:
-                spmm(g, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 1.0, ctx.pad_row, 1.0, gE)
-            else:  # this table's gradient is final chunk by chunk: its collectives start per chunk (dp.py)
-                part = None
-                for r0, r1 in cuts:
-                    part = spmm(g, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 1.0, ctx.pad_row, 1.0, gE,
-                                rows=(r0, r1), part=part)
-                    notify_rows(ctx.sink.state, E, r0, r1)
+        T = stage_ops()
+        work, _, split, _, n_slots, col, val = g.plan(True)
+        p = float(ctx.p)
+        # gE += drop(Aᵀ T_1)/… + G/(n+1) + [i != pad]·G  (rounds before the last: T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k)
+        X = T.gcn_backward_rounds(G, work, split, col, val, n_slots, n, p, flat_keys(ctx.keys)) if n > 1 else G
+        k0, k1 = ctx.keys[0] if n > 0 else (0, 0)
+        cuts = row_cuts(ctx.sink.state, E) if direct and n > 0 else None
+        if cuts is None:
+            T.gcn_backward_final(X, G, gE, work, split, col, val, n_slots, n, p, k0, k1, ctx.pad_row, 1.0, 1.0)
+        else:  # this table's gradient is final chunk by chunk: its collectives start per chunk (dp.py)
+            part = torch.empty(max(n_slots, 1), G.shape[1], device=G.device, dtype=torch.float32)
+            for r0, r1 in cuts:
+                w0, w1, s0, s1 = g.row_slice(True, r0, r1)
+                if w1 > w0:  # roofline accounting of a row-slice launch (bench.py HbmTimer): its rows and edges
+                    rp = g.host_rowptr(True)
+                    SPMM_SLICE[work[w0:w1].data_ptr()] = (r1 - r0, int(rp[r1]) - int(rp[r0]))
+                T.gcn_backward_final(X, G, gE, work[w0:w1], split[s0:s1], col, val, n_slots, n, p, k0, k1,
+                                     ctx.pad_row, 1.0, 1.0, part)
+                notify_rows(ctx.sink.state, E, r0, r1)
         ctx.sink.G = None
         if direct:
             notify_table(ctx.sink.state, E)  # E.grad final: its all-reduce runs under the next GCN backward
@@ -706,16 +717,9 @@ class GCNPropFn(Function):
     @staticmethod
     def forward(ctx, E, graph, n_gnn, p, keys):
         require_device(E)
-        out = torch.empty_like(E)
-        inv = 1.0 / (n_gnn + 1)
-        if n_gnn == 0:
-            out.copy_(E)
-        h_prev = E
-        for k in range(n_gnn):
-            h_k = None if k == n_gnn - 1 else torch.empty_like(E)
-            spmm(graph, False, h_prev, keys[k], p, 0, inv, E if k == 0 else None, inv, 0.0, -1,
-                 0.0 if k == 0 else 1.0, out, h_k)
-            h_prev = h_k
+        work, _, split, _, n_slots, col, val = graph.plan(False)
+        out = stage_ops().gcn_propagate(E.contiguous(), work, split, col, val, n_slots, n_gnn, float(p),
+                                        flat_keys(keys))
         ctx.graph, ctx.n_gnn, ctx.p, ctx.keys = graph, n_gnn, p, keys
         return out
 
@@ -725,21 +729,19 @@ class GCNPropFn(Function):
         n = ctx.n_gnn
         if n == 0:
             return G, None, None, None, None
-        inv = 1.0 / (n + 1)
-        X, alpha = G, inv
-        for k in range(n, 1, -1):  # T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k
-            T = torch.empty_like(G)
-            spmm(ctx.graph, True, X, ctx.keys[k - 1], ctx.p, 1, alpha, G, inv, 0.0, -1, 0.0, T)
-            X, alpha = T, 1.0
-        gE = torch.empty_like(G)
-        spmm(ctx.graph, True, X, ctx.keys[0], ctx.p, 1, alpha, G, inv, 0.0, -1, 0.0, gE)
+        T = stage_ops()
+        work, _, split, _, n_slots, col, val = ctx.graph.plan(True)
+        p = float(ctx.p)
+        X = T.gcn_backward_rounds(G, work, split, col, val, n_slots, n, p, flat_keys(ctx.keys)) if n > 1 else G
+        gE = torch.empty_like(G)  # the pure gradient: no lookup term, nothing accumulated
+        T.gcn_backward_final(X, G, gE, work, split, col, val, n_slots, n, p, ctx.keys[0][0], ctx.keys[0][1], -1, 0.0,
+                             0.0)
         return gE, None, None, None, None
 
 
 # ----------------------------------------------------------------------------- index plans
 _side_streams = {}
 PLAN_SRC = {}  # plan buffer data_ptr -> data_ptr of the index tensor it sorts (roofline accounting)
-ROW_COUNT = {}  # compact gradient part data_ptr -> its rows (roofline accounting of c2dsr_embed_bwd_planned_rows)
 
 
 def side_stream(device):
@@ -770,10 +772,10 @@ class IndexPlan:
         dev = whole.device
         side = side_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))  # the indices and the buffer are ready
-        with torch.cuda.stream(side):
-            for (idx, n_keys), buf, nb in zip(pairs, bufs, sizes):
-                PLAN_SRC[buf.data_ptr()] = idx.data_ptr()
-                lib('c2dsr_index_plan', idx, idx.numel(), int(n_keys), buf, nb, side.cuda_stream)
+        for (idx, _), buf in zip(pairs, bufs):
+            PLAN_SRC[buf.data_ptr()] = idx.data_ptr()
+        with torch.cuda.stream(side):  # one stage operator for all the plans, on the side stream
+            stage_ops().index_plans([idx for idx, _ in pairs], [int(k) for _, k in pairs], whole)
         whole.record_stream(side)
         ev = torch.cuda.Event()
         ev.record(side)
@@ -895,9 +897,7 @@ class EmbedFn(Function):
         require_device(E)
         B, L = seq.shape
         d = E.shape[1]
-        x = torch.empty(B, L, d, device=E.device, dtype=torch.float32)
-        lib('c2dsr_embed_fwd', seq, pos, B * L, d, H, E, None, P, float(scale), keys[0], keys[1], float(p),
-            int(row_base) * L, x, stream())
+        x = stage_ops().embed_fuse(seq, pos, H, E, None, P, float(scale), float(p), keys[0], keys[1], int(row_base))
         ctx.save_for_backward(seq, pos)
         ctx.scale, ctx.p, ctx.keys, ctx.row_base, ctx.sink, ctx.n_items = scale, p, keys, row_base, sink, E.shape[0]
         ctx.P = P
@@ -937,19 +937,15 @@ class EmbedFn(Function):
         if planned:
             sp = ctx.plans[0].get() if G is not None else None
             pp = ctx.plans[1].get() if gP is not None else None
-            ws_bytes = lib.raw('c2dsr_embed_bwd_planned_workspace')(n, d)
-            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=(G if G is not None else gP).device)
+            # (bench accounting: the rows of the two compact parts, and the index tensor the seq plan sorts)
             if parts is not None:  # the two compact row sources, read through their maps
-                if len(ROW_COUNT) > 256:
-                    ROW_COUNT.clear()
-                ROW_COUNT[parts[0].data_ptr()], ROW_COUNT[parts[2].data_ptr()] = parts[0].shape[0], parts[2].shape[0]
-                lib('c2dsr_embed_bwd_planned_rows', sp, pp, n, d, *parts, ctx.keys[0], ctx.keys[1], float(ctx.p),
-                    int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], ws, ws_bytes,
-                    stream())
+                stage_ops().embed_fuse_backward(sp, pp, n, d, None, *parts, float(ctx.p), ctx.keys[0], ctx.keys[1],
+                                                int(ctx.row_base) * L, float(ctx.scale), G, gP,
+                                                [float(parts[0].shape[0] + parts[2].shape[0]), float(seq.data_ptr())])
             else:
-                lib('c2dsr_embed_bwd_planned', sp, pp, n, d, gx, ctx.keys[0], ctx.keys[1], float(ctx.p),
-                    int(ctx.row_base) * L, float(ctx.scale), G, ctx.n_items, gP, ctx.P.shape[0], None, ws, ws_bytes,
-                    stream())
+                stage_ops().embed_fuse_backward(sp, pp, n, d, gx, None, None, None, None, float(ctx.p), ctx.keys[0],
+                                                ctx.keys[1], int(ctx.row_base) * L, float(ctx.scale), G, gP,
+                                                [0.0, float(seq.data_ptr())])
             if _CHECK_PLANS or _CHECK_ERR:
                 off = int(lib.raw('c2dsr_plan_err_offset')(n))
                 for pl in (sp, pp):
@@ -971,6 +967,108 @@ class EmbedFn(Function):
             notify_lookup(ctx.sink.state)
         tok_grad = torch.empty((), device=seq.device)  # value never read (GCNFn.backward reads the sink)
         return tok_grad, None, gP_ret, None, None, None, None, None, None, None, None, None, None
+
+
+FUSED_PASS = True  # the training step's encoder passes as one stage operator each way (EncoderPassFn)
+
+
+def fused_pass_ok(precision, B, L, d, n_head):
+    """The fused pass covers the step's fast path — d = 256, the row-subset attention, the split-bf16 (fp32 mode, linear1
+    guarded) or bf16 projection kernels; any other shape or precision runs op by op (EmbedFn → RowsQKVAttnFn → …)."""
+    if not FUSED_PASS or d != 256 or precision not in (FP32, BF16) or not attn_rows_ok(L, d, n_head):
+        return False
+    M = B * L  # the compact row counts are at most B·L (the support checks bound sizes from above)
+    kind = 'x3' if precision == FP32 else 'b16'
+    ok = all(rg_kind(precision, M, n, k) == kind for n, k in ((d, d), (2 * d, d), (d, 2 * d)))
+    ok = ok and all(wg_kind(precision, M, n, d) == kind for n in (d, 2 * d))
+    return ok and (precision == BF16 or (RELU_GUARD and relu_guard_ok(M, d, d)))
+
+
+class EncoderPassFn(Function):
+    """One training pass (models/C2DSR.py:64-85 → encoders.py:29-33, TransformerEncoder with one post-norm layer + the
+    final LayerNorm) as ONE stage operator each way: c2dsr::encoder_pass / encoder_pass_backward
+    (csrc_torch/encoder_ops.cpp).  The same kernels in the same order as the op-by-op path EmbedFn → RowsQKVAttnFn →
+    LinearFn → AddLNFn → LinearFn ×2 → AddLN2Fn (bit-identical results): the embedding fuse, Q at the rows the loss
+    reads (rs) and K / V at the padding rows (ks), the row-wise rest of the layer on the rs rows.  Returns the [n, d]
+    output rows (the loss head reads them through rs.inv).  Backward: the weight-gradient operands go to the step's
+    WGradBatch (grouped per weight across passes) and the input gradient, in its two compact parts, straight into
+    the embedding's deterministic segment sums (G: the GCN output's gradient sink; the position table)."""
+
+    @staticmethod
+    def forward(ctx, tok, E, P, seq, pos, H, att, nm, rs, ks, keys, p, row_off, precision, sink, scale):
+        require_device(E)
+        lay = att.encoder.layers[0]
+        at = lay.self_attn
+        d = E.shape[1]
+        kind = 'x3' if precision == FP32 else 'b16'
+        w = [at.in_proj_weight, at.in_proj_bias, at.out_proj.weight, at.out_proj.bias, lay.linear1.weight,
+             lay.linear1.bias, lay.linear2.weight, lay.linear2.bias, lay.norm1.weight, lay.norm1.bias, lay.norm2.weight,
+             lay.norm2.bias, nm.weight, nm.bias]
+        wd = [t.detach() for t in w]
+        Wq, Wkv = wd[0][:d], wd[0][d:]
+        img = [weight_img(Wq, kind), weight_img(Wkv, kind), weight_img(wd[2], kind), weight_img(wd[4], kind),
+               weight_img(wd[6], kind)]
+        gws = None
+        if precision == FP32:
+            img.append(WEIGHTS.get(wd[4], False, layout='norm2'))
+            nq = rs.n
+            wsb = int(lib.raw('c2dsr_rgemm_guard_workspace')(max(nq, 1), d))
+            gws = _GUARD_WS.get(E.device)
+            if gws is None or gws.numel() < wsb:  # zeroed once: every call leaves its flags cleared
+                gws = _GUARD_WS[E.device] = torch.zeros(max(wsb, 1 << 20), device=E.device, dtype=torch.uint8)
+        else:
+            img.append(torch.empty(0, device=E.device))
+        rsi, ksi = rs.idx[:rs.n], ks.idx[:ks.n]
+        outs = stage_ops().encoder_pass(seq, pos, H, E, P, float(scale), wd, img, rsi, rs.off, ksi, ks.off,
+                                        int(att.idx_pad), int(att.n_head), float(p), flat_keys(keys),
+                                        [float(lay.norm1.eps), float(lay.norm2.eps), float(nm.eps)], int(row_off),
+                                        0 if precision == FP32 else 1, gws)
+        ctx.saved = outs[1:]
+        ctx.args = (seq, pos, w, wd, rs, ks, rsi, ksi, keys, p, row_off, precision, att, scale)
+        ctx.sink, ctx.P, ctx.n_items = sink, P, E.shape[0]
+        return outs[0]
+
+    @staticmethod
+    def backward(ctx, gout):
+        seq, pos, w, wd, rs, ks, rsi, ksi, keys, p, row_off, precision, att, scale = ctx.args
+        d = wd[2].shape[0]
+        kind = 'x3' if precision == FP32 else 'b16'
+        imgT = [weight_img(wd[0][:d], kind, True), weight_img(wd[0][d:], kind, True), weight_img(wd[2], kind, True),
+                weight_img(wd[4], kind, True), weight_img(wd[6], kind, True)]
+        sink = ctx.sink
+        G = sink.buf() if sink is not None else None
+        gP = _grad_target(ctx.P)
+        gP_ret = None
+        if gP is None and ctx.needs_input_grad[2]:
+            gP_ret = gP = torch.zeros_like(ctx.P)
+        state = sink.state if sink is not None else None
+        sp = index_plan(state, seq, ctx.n_items).get() if G is not None else None
+        pp = index_plan(state, pos, ctx.P.shape[0]).get() if gP is not None else None
+        lng = []
+        for t in w[8:]:
+            g = _grad_target(t)
+            lng.append(g if g is not None else torch.zeros_like(t))  # a frozen LayerNorm parameter: scratch
+        pairs = stage_ops().encoder_pass_backward(gout.contiguous(), ctx.saved, seq, wd, imgT, rsi, rs.inv, rs.off, ksi,
+                                                  ks.inv, ks.off, int(att.idx_pad), int(att.n_head), float(p),
+                                                  flat_keys(keys), int(row_off), 0 if precision == FP32 else 1, lng,
+                                                  sp, pp, float(scale), G, gP)
+        ctx.saved = None
+        # weight / bias gradients of linear2, linear1, out_proj, in_proj (q rows, k/v rows) — the op-by-op path's order
+        gWin, gbin = _grad_target(w[0]), _grad_target(w[1])
+        targets = [(_grad_target(w[6]), _grad_target(w[7])), (_grad_target(w[4]), _grad_target(w[5])),
+                   (_grad_target(w[2]), _grad_target(w[3])),
+                   (None if gWin is None else gWin[:d], None if gbin is None else gbin[:d]),
+                   (None if gWin is None else gWin[d:], None if gbin is None else gbin[d:])]
+        for (gW, gb), dY, X in zip(targets, pairs[0::2], pairs[1::2]):
+            if gW is None or X.shape[0] == 0:
+                continue
+            wgemm(dY, X, gW, T=X.shape[0], N=gW.shape[0], D=X.shape[1], db=gb, x3=precision == FP32)
+        if WBATCH is not None:  # this pass's lookup is done (the last one flushes the deferred products)
+            WBATCH.lookup_done()
+        if sink is not None:
+            notify_lookup(sink.state)
+        tok_grad = torch.empty((), device=gout.device)
+        return (tok_grad, None, gP_ret) + (None,) * 13
 
 
 class RowsGrad:

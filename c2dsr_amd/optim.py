@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import lib, stream
+from ._lib import stage_ops
 from .flat import FlatStore
 
 
@@ -51,14 +51,14 @@ class FlatAdamW(torch.optim.Optimizer):
         if self.zero is None:
             # direct store (one device): fresh is accum — read only, 36 B/param; without epoch accumulation
             # the same buffer is this step's gradient and is cleared
-            lib('c2dsr_adamw', f.param, f.fresh, self.accum if self.accumulate else None, self.m, self.v, self.vmax,
-                f.numel, *hyper, stream())
+            stage_ops().adamw_step(f.param, f.fresh, self.accum if self.accumulate else None, self.m, self.v,
+                                   self.vmax, *hyper)
         else:
             z = self.zero
             for _, _, olo, ohi, off in z.parts:
                 n, sl = ohi - olo, slice(off, off + ohi - olo)
-                lib('c2dsr_adamw', f.param[olo:ohi], z.gshard[sl], self.accum[sl] if self.accumulate else None,
-                    self.m[sl], self.v[sl], self.vmax[sl], n, *hyper, stream())
+                stage_ops().adamw_step(f.param[olo:ohi], z.gshard[sl], self.accum[sl] if self.accumulate else None,
+                                       self.m[sl], self.v[sl], self.vmax[sl], *hyper)
             f.fresh.zero_()  # the next backward accumulates into it
             for w in z.gather():
                 w.wait()

@@ -1,0 +1,85 @@
+"""The c2dsr:: stage operators derive their sizes from the tensors and check every extent before any launch
+(VERDICT r04 next #2): an undersized or mis-shaped tensor raises RuntimeError — checked here on
+the host, where the checks run before the device check (a well-shaped host tensor is refused as not on the device)."""
+import os
+
+import pytest
+import torch
+
+EXT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'c2dsr_amd', 'libc2dsr_torch.so')
+
+
+@pytest.fixture(scope='module')
+def T():
+    torch.ops.load_library(EXT)
+    return torch.ops.c2dsr
+
+
+def test_embed_fuse_checks(T):
+    B, L, d, N = 4, 6, 8, 10
+    seq, pos = torch.zeros(B, L, dtype=torch.long), torch.zeros(B, L, dtype=torch.long)
+    H, E, P = torch.zeros(N, d), torch.zeros(N, d), torch.zeros(L, d)
+    with pytest.raises(RuntimeError, match='pos has shape'):
+        T.embed_fuse(seq, pos[:, :5].contiguous(), H, E, None, P, 1.0, 0.0, 0, 0, 0)
+    with pytest.raises(RuntimeError, match='E has shape'):
+        T.embed_fuse(seq, pos, H, E[:7], None, P, 1.0, 0.0, 0, 0, 0)
+    with pytest.raises(RuntimeError, match='out has shape'):  # an undersized output
+        T.embed_fuse(seq, pos, H, E, None, P, 1.0, 0.0, 0, 0, 0, torch.zeros(B, L - 1, d))
+    with pytest.raises(RuntimeError, match='must be on the HIP device'):
+        T.embed_fuse(seq, pos, H, E, None, P, 1.0, 0.0, 0, 0, 0)
+
+
+def test_embed_fuse_backward_checks(T):
+    n, d = 24, 64
+    plan = torch.zeros(16, dtype=torch.uint8)
+    with pytest.raises(RuntimeError, match='seq_plan holds'):  # an undersized plan buffer
+        T.embed_fuse_backward(plan, None, n, d, torch.zeros(n, d), None, None, None, None, 0.0, 0, 0, 0, 1.0,
+                              torch.zeros(10, d), None)
+    with pytest.raises(RuntimeError, match='inv_a has shape'):
+        T.embed_fuse_backward(None, None, n, d, None, torch.zeros(5, d), torch.zeros(n - 1, dtype=torch.int32),
+                              torch.zeros(5, d), torch.zeros(n, dtype=torch.int32), 0.0, 0, 0, 0, 1.0, None, None)
+
+
+def test_gcn_checks(T):
+    N, d = 10, 8
+    E = torch.zeros(N, d)
+    work, split = torch.zeros(12, 4, dtype=torch.int32), torch.zeros(0, 4, dtype=torch.int32)
+    col, val = torch.zeros(30, dtype=torch.int32), torch.zeros(29)
+    with pytest.raises(RuntimeError, match='val has shape'):
+        T.gcn_propagate(E, work, split, col, val, 0, 1, 0.0, [0, 0])
+    with pytest.raises(RuntimeError, match='work has shape'):
+        T.gcn_propagate(E, torch.zeros(12, 3, dtype=torch.int32), split, col, torch.zeros(30), 0, 1, 0.0, [0, 0])
+    with pytest.raises(RuntimeError, match='keys must hold'):
+        T.gcn_propagate(E, work, split, col, torch.zeros(30), 0, 2, 0.0, [0, 0])
+    with pytest.raises(RuntimeError, match='gE has shape'):
+        T.gcn_backward_final(E, E, torch.zeros(N - 1, d), work, split, col, torch.zeros(30), 0, 1, 0.0, 0, 0, -1, 1.0,
+                             1.0)
+
+
+def test_encoder_pass_checks(T):
+    B, L, d, N = 2, 50, 256, 20
+    seq, pos = torch.zeros(B, L, dtype=torch.long), torch.zeros(B, L, dtype=torch.long)
+    H, E, P = torch.zeros(N, d), torch.zeros(N, d), torch.zeros(L, d)
+    w = [torch.zeros(3 * d, d), torch.zeros(3 * d)] + [torch.zeros(d, d), torch.zeros(d)] * 3 + [torch.zeros(d)] * 6
+    img = [torch.zeros(16, 2 * d, dtype=torch.bfloat16)] * 5 + [torch.zeros(d)]
+    rs_idx, ks_idx = torch.zeros(7, dtype=torch.int32), torch.zeros(5, dtype=torch.int32)
+    off = torch.zeros(B + 1, dtype=torch.int32)
+    args = (seq, pos, H, E, P, 16.0)
+    tail = (N - 1, 1, 0.2, [0] * 10, [1e-8] * 3, 0, 0, torch.zeros(1 << 20, dtype=torch.uint8))
+    with pytest.raises(RuntimeError, match='rs_off has shape'):  # the per-sequence offsets are B + 1 long
+        T.encoder_pass(*args, w, img, rs_idx, off[:B], ks_idx, off, *tail)
+    with pytest.raises(RuntimeError, match='in_proj_weight has shape'):
+        T.encoder_pass(*args, [torch.zeros(2 * d, d)] + w[1:], img, rs_idx, off, ks_idx, off, *tail)
+    with pytest.raises(RuntimeError, match='image too small'):  # an undersized weight image
+        T.encoder_pass(*args, w, img, rs_idx, off, ks_idx, off, *tail)
+    with pytest.raises(RuntimeError, match='14 weight tensors'):
+        T.encoder_pass(*args, w[:-1], img, rs_idx, off, ks_idx, off, *tail)
+
+
+def test_adamw_checks(T):
+    n = 40
+    p, g, m, v, vm = (torch.zeros(n) for _ in range(5))
+    with pytest.raises(RuntimeError, match='state has shape'):
+        T.adamw_step(p, g, None, torch.zeros(n - 4), v, vm, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1)
+    with pytest.raises(RuntimeError, match='must be on the HIP device'):
+        T.adamw_step(p, g, None, m, v, vm, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1)
