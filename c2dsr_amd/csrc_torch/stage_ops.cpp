@@ -312,7 +312,8 @@ void adamw_step(const Tensor& param, const Tensor& fresh, const OptT& accum, con
 
 }  // namespace
 
-void register_encoder_ops(torch::Library& m);  // encoder_ops.cpp
+void register_encoder_ops(torch::Library& m);   // encoder_ops.cpp
+void register_losshead_ops(torch::Library& m);  // losshead_ops.cpp
 
 TORCH_LIBRARY_FRAGMENT(c2dsr, m) {
   m.def("gcn_propagate(Tensor E, Tensor work, Tensor split, Tensor col, Tensor val, int n_slots, int n_gnn, float p, "
@@ -331,6 +332,7 @@ TORCH_LIBRARY_FRAGMENT(c2dsr, m) {
   m.def("adamw_step(Tensor(a!) param, Tensor(b!) fresh, Tensor(c!)? accum, Tensor(d!) m, Tensor(e!) v, "
         "Tensor(f!) vmax, float lr, float wd, float b1, float b2, float eps, int step) -> ()");
   register_encoder_ops(m);
+  register_losshead_ops(m);
 }
 
 TORCH_LIBRARY_IMPL(c2dsr, CompositeExplicitAutograd, m) {

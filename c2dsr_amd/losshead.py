@@ -18,8 +18,10 @@ from __future__ import annotations
 import torch
 from torch.autograd import Function
 
-from ._lib import lib, stream
+from ._lib import lib, stage_ops, stream
 from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rg_kind, rgemm, weight_img, wg_kind, wgemm
+
+FUSED_HEAD = True  # the training step's loss head on the c2dsr:: stage operators (csrc_torch/losshead_ops.cpp)
 
 
 _NCU = None
@@ -94,11 +96,29 @@ class LossMeta:
         lib('c2dsr_loss_finalize', vec, cnt, BR_global, float(self.lam), out3, scratch[:2], scratch[2:], stream())
 
 
+def fused_head_mode(m, B, d, training):
+    """0 / 1 (split-bf16 / bf16 operands) when the loss head runs on the stage operators: a training step with its
+    targets compacted ahead (Trainer.prepare), the ce3.hip sweep kernels at this width and the projection kernels
+    for the discriminators; None: op by op."""
+    kind = ce_kind(m.precision, d)
+    if not (FUSED_HEAD and training and m.ce_pre is not None and kind is not None
+            and bool(lib.raw('c2dsr_ce3_supported')(d))):
+        return None
+    want = 'x3' if kind == 'x3' else 'b16'
+    if rg_kind(m.precision, 2 * B, d, d) != want or wg_kind(m.precision, 2 * B, d, d) != want:
+        return None
+    return 0 if kind == 'x3' else 1
+
+
 class LossHeadFn(Function):
     @staticmethod
     def forward(ctx, h_share, hx, hy, h_neg_a, h_neg_b, m: LossMeta):
         B, L = m.gm_a.shape  # (encoder outputs may hold a row subset: [n, d])
         d = h_share.shape[-1]
+        mode = fused_head_mode(m, B, d, any(ctx.needs_input_grad[:5]))
+        if mode is not None:
+            return LossHeadFn._forward_stage(ctx, (h_share, hx, hy, h_neg_a, h_neg_b), m, mode)
+        ctx.stage = None
         R = m.R
         BR = B * R
         dev = h_share.device
@@ -278,7 +298,84 @@ class LossHeadFn(Function):
         return loss, loss_rec, loss_mi_o
 
     @staticmethod
+    def _forward_stage(ctx, hs, m, mode):
+        """The forward on the stage operators: loss_disc_forward, ce_head_forward per head (the host work queued after
+        the first head's long sweep: m.after_first_ce), loss_partials, loss_finalize (and the data-parallel
+        reductions between them, as in the op-by-op path)."""
+        T = stage_ops()
+        B, L = m.gm_a.shape
+        d = hs[0].shape[-1]
+        R = m.R
+        BR = B * R
+        kind = 'x3' if mode == 0 else 'b16'
+        rsets = tuple(m.row_sets) if m.row_sets is not None else (None,) * 5
+        mp = [r.inv if r is not None else None for r in rsets]
+        Bg = m.B_global if m.B_global is not None else B
+        vec = torch.empty(9, device=hs[0].device, dtype=torch.float32)  # [CE sums ×4, counts ×4, loss_mi]
+        D = [m.Da_w, m.Da_b, m.Db_w, m.Db_b]
+        Dimg = [weight_img(m.Da_w.view(d, d), kind), weight_img(m.Db_w.view(d, d), kind)]
+        disc = T.loss_disc_forward(list(hs), mp, m.gm_a, m.gm_b, D, Dimg, mode, Bg, vec)
+        heads = []
+        specs = ((hs[1], m.Wa, m.ba, m.n_a), (hs[2], m.Wb, m.bb, m.n_b))
+        for k, (hdom, W, bias, n) in enumerate(specs):
+            tcat, idx, inv, tc, (hc, slot) = m.ce_pre[k]
+            Mv0, Mv1 = int(hc[slot]), int(hc[slot + 1])
+            Mv = Mv0 + Mv1
+            out = T.ce_head_forward(hs[0], mp[0], hdom, mp[1 + k], B, L, R, W, bias, m.wpad, m.bpad, idx, inv, tc,
+                                    Mv0, Mv1, split_count(Mv, 128), mode)
+            if k == 0:
+                m.run_after_first_ce()
+            # target sort for the one-hot part of dW/db, on the side stream under the rest of the step
+            tplan = IndexPlan(tc[:Mv], n + 1) if Mv and W.requires_grad else None
+            heads.append((out[0], tcat, out[1:], inv, tc, Mv0, Mv1, tplan, W, bias, n))
+        T.loss_partials(heads[0][0], heads[0][1], m.n_a, heads[1][0], heads[1][1], m.n_b, BR, vec)
+        cnt = None
+        if m.counts is not None:  # data parallel: global counts reduced ahead; the values' sums reduced async
+            cnt, work = m.counts
+            work.wait()
+            vred = vec.clone()
+            m.pending = (m.reduce_async(vred), vred, cnt, Bg * R, torch.empty(3, device=vec.device))
+        elif m.allreduce is not None:
+            m.allreduce(vec)
+        out3, coefA, coefB = T.loss_finalize(vec, cnt, Bg * R, float(m.lam))
+        if m.pending is not None:  # finish_values rewrites the returned losses in place
+            m.pending = m.pending[:4] + (out3,)
+        ctx.stage = (mode, kind, disc, [h[2:] for h in heads], (coefA, coefB), rsets, mp, (B, L, d))
+        ctx.m = m
+        loss, loss_rec, loss_mi_o = out3[0], out3[1], out3[2]
+        ctx.mark_non_differentiable(loss_rec, loss_mi_o)
+        ctx.set_materialize_grads(False)
+        m.run_after_first_ce()
+        return loss, loss_rec, loss_mi_o
+
+    @staticmethod
+    def _backward_stage(ctx, gloss):
+        """ce_head_backward per head, then loss_disc_backward (discriminators, poolings, the heads' dH scatter)."""
+        T = stage_ops()
+        m = ctx.m
+        mode, kind, disc, heads, coefs, rsets, mp, (B, L, d) = ctx.stage
+        gscale = gloss.contiguous().reshape(1)
+        gwpad, gbpad = _grad_target(m.wpad), _grad_target(m.bpad)
+        hd = []
+        for (saved, inv, tc, Mv0, Mv1, tplan, W, bias, n), coef in zip(heads, coefs):
+            gW, gb = _grad_target(W), _grad_target(bias)
+            hd += T.ce_head_backward(saved, W, inv, tc, Mv0, Mv1, coef, gscale, float(m.lam), gW, gb, gwpad, gbpad,
+                                     tplan.get() if tplan is not None else None, split_count(n, 128), mode)
+        imgT = [weight_img(m.Da_w.view(d, d), kind, trans=True), weight_img(m.Db_w.view(d, d), kind, trans=True)]
+        gD = [_grad_target(t) for t in (m.Da_w, m.Da_b, m.Db_w, m.Db_b)]
+        sub = [r.idx[:r.n] if r is not None else None for r in rsets]
+        dh = T.loss_disc_backward(disc, gscale, float(m.lam), [m.Da_w, m.Da_b, m.Db_w, m.Db_b], imgT, gD, hd, m.wpad,
+                                  sub, mp, L, m.R, mode)
+        if m.on_head_grads is not None:  # the classifier / discriminator gradients are final: their
+            m.on_head_grads()                # collectives run under the encoder backwards (dp.py)
+            m.on_head_grads = None
+        ctx.m = ctx.stage = None
+        return tuple(dh) + (None,)
+
+    @staticmethod
     def backward(ctx, gloss, _g1, _g2):
+        if ctx.stage is not None:
+            return LossHeadFn._backward_stage(ctx, gloss)
         m = ctx.m
         B, L, d = ctx.shape
         R = m.R

@@ -2,7 +2,7 @@
 gcn_backward_*, embed_fuse*, index_plans, adamw_step; csrc_torch/) against the op-by-op path they replace (the same
 kernels launched one by one from c2dsr_amd/ops.py): two training steps at the benchmarked shape (d = 256, L = 50,
 R = 10) with dropout 0.2, in both precision modes — the losses, every gradient and the updated parameters are
-bit-identical.  Also: the number of operator calls a step makes."""
+bit-identical.  Also: the fused pass and loss head are the ones taken."""
 import numpy as np
 import pytest
 import torch
@@ -28,8 +28,8 @@ def _case(precision):
 
 
 def _run(precision, fused, rows, gs, gp, B=96):
-    from c2dsr_amd import ops
-    ops.FUSED_PASS = fused
+    from c2dsr_amd import losshead, ops
+    ops.FUSED_PASS = losshead.FUSED_HEAD = fused
     try:
         args = make_args(C, dropout=0.2, precision=precision, seed=5)
         args.batch_size = B
@@ -47,7 +47,7 @@ def _run(precision, fused, rows, gs, gp, B=96):
         params = {n: p.detach().cpu().clone() for n, p in tr.model.named_parameters()}
         return out, params
     finally:
-        ops.FUSED_PASS = True
+        ops.FUSED_PASS = losshead.FUSED_HEAD = True
 
 
 @pytest.mark.parametrize('precision', ['fp32', 'bf16'])
@@ -63,11 +63,9 @@ def test_fused_pass_equals_op_by_op_path(precision):
         assert torch.equal(pa[n], pb[n]), n
 
 
-def test_fused_pass_is_taken_and_step_op_count():
-    """The fused pass runs (its operator is called once per pass each way) and a training step makes a few dozen
-    operator calls, not one per kernel: counted with the operator library's event-timing hook."""
-    from c2dsr_amd import ops
-    from c2dsr_amd._lib import lib
+def test_fused_pass_and_head_are_taken():
+    """The fused pass runs (once per pass each way) and the loss head takes the stage operators."""
+    from c2dsr_amd import losshead, ops
     rows, gs, gp = _case('fp32')
     args = make_args(C, dropout=0.2, precision='fp32', seed=5)
     args.batch_size = 96
@@ -75,8 +73,13 @@ def test_fused_pass_is_taken_and_step_op_count():
     tr = build_trainer(args, gs, gp)
     tr.model.train()
     tr.optimizer.zero_grad()
-    calls = {'fwd': 0, 'bwd': 0}
+    calls = {'fwd': 0, 'bwd': 0, 'head': 0}
     f0, b0 = ops.EncoderPassFn.forward, ops.EncoderPassFn.backward
+    h0 = losshead.LossHeadFn._backward_stage
+
+    def head(*a):
+        calls['head'] += 1
+        return h0(*a)
 
     def fwd(*a):
         calls['fwd'] += 1
@@ -86,11 +89,12 @@ def test_fused_pass_is_taken_and_step_op_count():
         calls['bwd'] += 1
         return b0(*a)
     ops.EncoderPassFn.forward, ops.EncoderPassFn.backward = staticmethod(fwd), staticmethod(bwd)
+    losshead.LossHeadFn._backward_stage = staticmethod(head)
     try:
         tr.model.convolve_graph()
         tr.train_batch(tuple(torch.from_numpy(r[:96].copy()) for r in rows))
         torch.cuda.synchronize()
     finally:
         ops.EncoderPassFn.forward, ops.EncoderPassFn.backward = staticmethod(f0), staticmethod(b0)
-    assert calls == {'fwd': 5, 'bwd': 5}
-    del lib
+        losshead.LossHeadFn._backward_stage = staticmethod(h0)
+    assert calls == {'fwd': 5, 'bwd': 5, 'head': 1}
