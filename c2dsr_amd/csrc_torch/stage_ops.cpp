@@ -314,6 +314,7 @@ void adamw_step(const Tensor& param, const Tensor& fresh, const OptT& accum, con
 
 void register_encoder_ops(torch::Library& m);   // encoder_ops.cpp
 void register_losshead_ops(torch::Library& m);  // losshead_ops.cpp
+void register_batch_ops(torch::Library& m);     // batch_ops.cpp
 
 TORCH_LIBRARY_FRAGMENT(c2dsr, m) {
   m.def("gcn_propagate(Tensor E, Tensor work, Tensor split, Tensor col, Tensor val, int n_slots, int n_gnn, float p, "
@@ -333,6 +334,7 @@ TORCH_LIBRARY_FRAGMENT(c2dsr, m) {
         "Tensor(f!) vmax, float lr, float wd, float b1, float b2, float eps, int step) -> ()");
   register_encoder_ops(m);
   register_losshead_ops(m);
+  register_batch_ops(m);
 }
 
 TORCH_LIBRARY_IMPL(c2dsr, CompositeExplicitAutograd, m) {

@@ -116,22 +116,15 @@ class _WeightImages:
         if self.known:
             self._refresh_known()
 
+    LAYOUT = {None: 0, 'split': 1, 'frag': 2, 'b16frag': 3}  # c2dsr::weight_images' layout codes
+
     def _refresh_known(self):
-        for layout, fn in ((None, 'c2dsr_to_bf16_multi'), ('split', 'c2dsr_to_split_bf16_multi'),
-                           ('frag', 'c2dsr_to_split_bf16_frag_multi'), ('b16frag', 'c2dsr_to_bf16_frag_multi')):
-            recs, done = [], []
-            for key, (W, y) in self.known.items():
-                if key[3] != layout:
-                    continue
-                R, Cc = W.shape
-                recs += [W.data_ptr(), y.data_ptr(), R, Cc, W.stride(0), int(key[2])]
-                done.append((key, W, y))
-            for i in range(0, len(done), 64):
-                chunk = done[i:i + 64]
-                desc = np.asarray(recs[6 * i:6 * (i + len(chunk))], dtype=np.int64)
-                lib(fn, desc, len(chunk), stream())
-            for key, W, y in done:
-                self.cache[key] = ((self.epoch, W._version), y, W)
+        done = [(key, W, y) for key, (W, y) in self.known.items() if key[3] in self.LAYOUT]
+        if done:  # one stage operator: a multi-matrix launch per layout
+            stage_ops().weight_images([W for _, W, _ in done], [y for _, _, y in done], [int(k[2]) for k, _, _ in done],
+                                      [self.LAYOUT[k[3]] for k, _, _ in done])
+        for key, W, y in done:
+            self.cache[key] = ((self.epoch, W._version), y, W)
         for key, (W, y) in self.known.items():
             if key[3] == 'norm2':
                 torch.sum(W * W, 1, out=y)
@@ -289,18 +282,19 @@ class WGradBatch:
             self.flush()
 
     def flush(self):
-        s = stream()
-        for (_, N, D, dt, _, x3), (dW, db, segs) in self.groups.items():
-            ws = torch.empty(lib.raw('c2dsr_wgemm_workspace')(N), dtype=torch.uint8, device=dW.device)
-            for i in range(0, len(segs), 4):
-                chunk = segs[i:i + 4]
-                desc = np.asarray([v for dY, X, T in chunk for v in (dY.data_ptr(), N, X.data_ptr(), D, T)],
-                                  dtype=np.int64)
-                if x3:
-                    lib('c2dsr_wgemm_x3_multi', desc, len(chunk), N, D, 1.0, dW, db, ws, s)
-                else:
-                    lib('c2dsr_wgemm_multi', desc, len(chunk), N, D, int(dt == torch.bfloat16), 1.0, dW,
-                        db, ws, s)
+        """All groups' products in one stage operator (c2dsr::wgrad_groups: per group, four segments per product)."""
+        if not self.groups:
+            return
+        dYs, Xs, gid, dWs, dbs, x3s = [], [], [], [], [], []
+        for g, ((_, N, D, dt, _, x3), (dW, db, segs)) in enumerate(self.groups.items()):
+            for dY, X, T in segs:
+                dYs.append(dY.reshape(-1, N)[:T])
+                Xs.append(X.reshape(-1, D)[:T])
+                gid.append(g)
+            dWs.append(dW.view(N, D))
+            dbs.append(db)
+            x3s.append(int(x3))
+        stage_ops().wgrad_groups(dYs, Xs, gid, dWs, dbs, x3s)
         self.groups = {}
 
 

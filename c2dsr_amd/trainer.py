@@ -23,7 +23,7 @@ import torch.distributed as dist
 from .dataloader import get_dataloader
 from . import dropout as DK
 from . import ops
-from ._lib import lib, stream
+from ._lib import lib, stage_ops, stream
 from .dp import CommPlan, DPComm, Zero1
 from .graph import make_graph
 from .losshead import LossHeadFn, LossMeta, ce_kind
@@ -249,43 +249,33 @@ class Trainer(object):
         B, L = gm_a.shape
         M, R = B * L, self.len_rec
         dev = gm_a.device
-        s = stream()
-        i32 = dict(device=dev, dtype=torch.int32)
         counts = []
         need_sets = pad_sets = None
         f_need, f_pads, f_ce = self.count_flags(L)
+        n = len(self.PASS_ROWS)
+        code = sum(bits << (3 * q) for q, (_, bits) in enumerate(self.PASS_ROWS))
+        # one stage operator for all of it (c2dsr::step_prepare)
+        heads = ((gt_share_a, gt_a, self.n_item_a), (gt_share_b, gt_b, self.n_item_b)) if f_ce else ()
+        out = stage_ops().step_prepare(gm_a, gm_b, R, n, code,
+                                       list(seqs) if (f_need and seqs is not None and f_pads) else [],
+                                       int(m.attn_share.idx_pad), [t for h in heads for t in h[:2]],
+                                       [h[2] for h in heads], bool(f_need))
+        o = 0
         if f_need:
-            n = len(self.PASS_ROWS)
-            idx = torch.empty(n, M, **i32)
-            inv = torch.empty(n, M, **i32)
-            cnt = torch.empty(n, **i32)
-            off = torch.empty(n, B + 1, **i32)
-            ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, **i32)
-            code = sum(bits << (3 * q) for q, (_, bits) in enumerate(self.PASS_ROWS))
-            lib('c2dsr_need_rows', gm_a, gm_b, B, L, R, n, code, idx, inv, cnt, off, ws, s)
+            idx, inv, cnt, off = out[0:4]
             need_sets = (idx, inv, off)
             counts.append(cnt)
+            o = 4
             if seqs is not None and f_pads:
-                sq = torch.stack([x.reshape(M) for x in seqs])
-                pidx, pinv = torch.empty(n, M, **i32), torch.empty(n, M, **i32)
-                pcnt, poff = torch.empty(n, **i32), torch.empty(n, B + 1, **i32)
-                pws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, n) // 4 + 1, **i32)
-                lib('c2dsr_pad_rows', sq, int(m.attn_share.idx_pad), B, L, n, pidx, pinv, pcnt, poff, pws, s)
+                pidx, pinv, pcnt, poff = out[4:8]
                 pad_sets = (pidx, pinv, poff)
                 counts.append(pcnt)
+                o = 8
         ce = None
         if f_ce:
-            M2 = 2 * B * R
             ce = []
-            for ts, tx, n_items in ((gt_share_a, gt_a, self.n_item_a), (gt_share_b, gt_b, self.n_item_b)):
-                tcat = torch.empty(M2, device=dev, dtype=torch.int64)
-                lib('c2dsr_rec_targets', ts, tx, B, L, R, tcat, s)
-                idx_c = torch.empty(M2, **i32)
-                inv_c = torch.empty(M2, **i32)
-                tc = torch.empty(M2, device=dev, dtype=torch.int64)
-                cnt = torch.empty(2, **i32)
-                ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M2, 1) // 4 + 1, **i32)
-                lib('c2dsr_compact_valid', tcat, M2, B * R, n_items, idx_c, inv_c, tc, cnt, ws, s)
+            for k in range(2):
+                tcat, idx_c, inv_c, tc, cnt = out[o + 5 * k:o + 5 * k + 5]
                 ce.append((tcat, idx_c, inv_c, tc))
                 counts.append(cnt)
         if self.world > 1:
