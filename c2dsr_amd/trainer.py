@@ -245,6 +245,7 @@ class Trainer(object):
             (c2dsr_rec_targets) and their valid-row compaction (c2dsr_compact_valid) for the fused CE.
         Returns (need: {pass_id: RowSet}, pads: {pass_id: RowSet},
                  ce_pre: [(tcat, idx, inv, tc, (HostCounts, slot)), ...] or None)."""
+        ops.require_device(gm_a)  # (no CPU fallback: refused here, before any operator checks shapes)
         m = self.model
         B, L = gm_a.shape
         M, R = B * L, self.len_rec
