@@ -280,6 +280,7 @@ class Trainer(object):
                 ce.append((tcat, idx_c, inv_c, tc))
                 counts.append(cnt)
         if self.world > 1:
+            s = stream()
             # the global valid-target counts — all the gradient's normalisation needs (trainer.py:143-156,
             # SURVEY.md §8(e)) — reduced ahead of the forward, overlapped with it
             tg = [c[0] for c in ce] if ce is not None else []
