@@ -130,7 +130,7 @@ class HbmTimer:
       4·d per row of each part (n_q + n_k rows read), plus the 8·d per distinct item.
       Sort passes and pad-row segments are overhead, not credited."""
 
-    NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_bwd', 'c2dsr_embed_bwd_planned',
+    NAMES = ('c2dsr_gcn_spmm', 'c2dsr_embed_fwd', 'c2dsr_embed_fwd_rows', 'c2dsr_embed_bwd', 'c2dsr_embed_bwd_planned',
              'c2dsr_embed_bwd_planned_rows', 'c2dsr_gcn_spmm_b16', 'c2dsr_embed_fwd_b16', 'c2dsr_embed_bwd_planned_b16')
 
     def __init__(self, n_rows_table, nnz_by_col_ptr, uniq_by_seq_ptr):
@@ -159,6 +159,9 @@ class HbmTimer:
             n, d = int(a[2]), int(a[3])
             reads = (a[4] != 0) + (a[5] != 0) + (a[6] != 0)
             return n * (16 + 4 * d * reads + 4 * d)
+        if name == 'c2dsr_embed_fwd_rows':  # (seq, pos, n_rows, d, H, E, P, .., q_idx, nq, k_idx, nk, X): rows made
+            k, d = int(a[13]) + int(a[15]), int(a[3])
+            return k * (16 + 4 + 2 * 4 * d + 4 * d)
         n, d = int(a[2]), int(a[3])
         if name == 'c2dsr_embed_fwd_b16':  # (seq, pos, n, d, H, E, P, ..., X): two bf16 table rows, fp32 X
             return n * (16 + 2 * 2 * d + 4 * d)
@@ -264,6 +267,7 @@ SEG0 = ('seg_chunk_kernel<64, 0>', 'seg_split1_kernel<64, 0>', 'seg_split2_kerne
 DRAM_KERNELS = {'c2dsr_gcn_spmm': ('spmm_kernel', 'spmm_pf_kernel', 'combine_kernel'),
                 'c2dsr_gcn_spmm_b16': ('spmm_kernel', 'spmm_pf_kernel', 'combine_kernel'),
                 'c2dsr_embed_fwd': ('embed_fwd_kernel',), 'c2dsr_embed_fwd_b16': ('embed_fwd_kernel',),
+                'c2dsr_embed_fwd_rows': ('embed_fwd_rows_kernel',),
                 'c2dsr_embed_bwd_planned': SEG0, 'c2dsr_embed_bwd_planned_rows': SEG0, 'c2dsr_embed_bwd_planned_b16': SEG0}
 
 

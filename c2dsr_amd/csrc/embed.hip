@@ -46,6 +46,37 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   }
 }
 
+// the same, computing only chosen rows: output row k is input row qi[k] (k < nq) or ki[k - nq] (the row-subset
+// encoder layer's query rows and key rows, written side by side: the [B·L, d] embedding is never stored)
+template <int LPR>
+__global__ __launch_bounds__(256) void embed_fwd_rows_kernel(const int64_t* __restrict__ seq,
+                                                             const int64_t* __restrict__ pos, int n_rows, int d,
+                                                             const float* __restrict__ H, const float* __restrict__ E,
+                                                             const float* __restrict__ P, float scale, c2::Drop drop,
+                                                             int64_t idx_base, const int* __restrict__ qi, int nq,
+                                                             const int* __restrict__ ki, int nk,
+                                                             float* __restrict__ X) {
+  constexpr int GROUPS = 256 / LPR;
+  const int g = threadIdx.x / LPR;
+  const int lane = threadIdx.x % LPR;
+  const long k = (long)blockIdx.x * GROUPS + g;
+  if (k >= nq + nk) return;
+  const long r = min(max(k < nq ? qi[k] : ki[k - nq], 0), n_rows - 1);
+  const long p = pos[r], s = seq[r];
+  for (int c = lane * 4; c < d; c += LPR * 4) {
+    // (the statements of embed_fwd_kernel's gather path: the same rounding)
+    const float4 h = c2::ld4(H + s * d + c);
+    const float4 e = c2::ld4(E + s * d + c);
+    const float4 a = scale * (h + e);
+    float4 x = a + *(const float4*)(P + p * d + c);
+    if (drop.active()) {
+      const uint64_t b = (uint64_t)(idx_base + r) * d + c;
+      x = x * drop.mul4(b);
+    }
+    *(float4*)(X + k * d + c) = x;
+  }
+}
+
 // ------------------------------------------------------------------ radix sort (stable LSD)
 constexpr int RS_THREADS = 256;
 constexpr int RS_ROUNDS = 8;
@@ -831,6 +862,31 @@ C2_API int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, i
     embed_fwd_kernel<L, true><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, Xin, P, scale, dr, idx_base, X);     \
   else                                                                                                             \
     embed_fwd_kernel<L, false><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, Xin, P, scale, dr, idx_base, X);
+  switch (lpr) {
+    case 64: C2_EMB(64) break;
+    case 32: C2_EMB(32) break;
+    case 16: C2_EMB(16) break;
+    case 8: C2_EMB(8) break;
+    default: C2_EMB(4) break;
+  }
+#undef C2_EMB
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
+C2_API int c2dsr_embed_fwd_rows(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H,
+                                const float* E, const float* P, float scale, uint32_t k0, uint32_t k1, float p,
+                                int64_t idx_base, const int* q_idx, int nq, const int* k_idx, int nk, float* X,
+                                void* stream) {
+  if (d % 4 || nq < 0 || nk < 0 || !H || !E || !P) return (int)hipErrorInvalidValue;
+  if (nq + nk == 0 || n_rows <= 0) return 0;
+  c2::Drop dr = c2::make_drop(k0, k1, p);
+  hipStream_t s = (hipStream_t)stream;
+  const int lpr = lpr_for(d);
+  dim3 grid(c2::ceil_div(nq + nk, 256 / lpr));
+#define C2_EMB(L)                                                                                                    \
+  embed_fwd_rows_kernel<L><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, P, scale, dr, idx_base, q_idx, nq, k_idx, \
+                                                nk, X);
   switch (lpr) {
     case 64: C2_EMB(64) break;
     case 32: C2_EMB(32) break;

@@ -7,9 +7,10 @@
 // Everything after the attention is row-wise and the loss reads only the rows `rs` (pooled positions, last R
 // positions; trainer.py:101-154), and a query attends only to padding keys (Q1: inverted key-padding mask), so:
 // Q is projected for the rs rows, K / V for the padding rows `ks` only, and the rest of the layer runs on the rs
-// rows (dropout indices through the row map: the masks are the full-size run's).  The kernels and their order
-// are exactly those of the host side's op-by-op path (c2dsr_amd/ops.py: EmbedFn → RowsQKVAttnFn → LinearFn →
-// AddLNFn → LinearFn ×2 → AddLN2Fn), so the results are bit-identical to it.
+// rows (dropout indices through the row map: the masks are the full-size run's).  The embedding is computed at
+// those rows only (c2dsr_embed_fwd_rows: query rows and key rows side by side, the [B·L, d] tensor is never
+// stored); the rest are the kernels of the host side's op-by-op path in its order (c2dsr_amd/ops.py: EmbedFn →
+// RowsQKVAttnFn → LinearFn → AddLNFn → LinearFn ×2 → AddLN2Fn), so the results are bit-identical to it.
 //
 // precision 0: fp32 results, split-bf16 ×3 products (csrc/rgemm.hip rg3, linear1 guarded); 1: bf16 operands.
 #include <torch/library.h>
@@ -161,21 +162,12 @@ std::vector<Tensor> encoder_pass(const Tensor& seq, const Tensor& pos, const Ten
   on_device({}, img);
   const auto f32 = H.options();
   const int64_t rb_rows = row_off * L;
-  // K2: X = drop((H[seq] + E[seq])·√d + P[pos])
-  Tensor X = at::empty({B, L, d}, f32);
-  if (M)
-    c2t::launch("c2dsr_embed_fwd", &c2dsr_embed_fwd, seq.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), (int)M, (int)d,
-                F(H), F(E), (const float*)nullptr, F(P), (float)scale, ps.k0(K_INPUT), ps.k1(K_INPUT), p, rb_rows,
-                F(X), S());
-  // the rows: queries xc (the loss's rows), keys xk (the padding rows)
-  Tensor xc = at::empty({nq, d}, f32), xk = at::empty({nk, d}, f32);
-  if (nq)
-    c2t::launch("c2dsr_gather_rows", &c2dsr_gather_rows, F(X), (long)d, rs_idx.data_ptr<int>(), (int)nq, (int)d,
-                F(xc), S());
-  if (nk)
-    c2t::launch("c2dsr_gather_rows", &c2dsr_gather_rows, F(X), (long)d, ks_idx.data_ptr<int>(), (int)nk, (int)d,
-                F(xk), S());
-  X.reset();
+  // K2 on the rows the layer reads: xc = X[rs], xk = X[ks] with X = drop((H[seq] + E[seq])·√d + P[pos]) (never stored)
+  Tensor xck = at::empty({nq + nk, d}, f32);
+  c2t::launch("c2dsr_embed_fwd_rows", &c2dsr_embed_fwd_rows, seq.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), (int)M,
+              (int)d, F(H), F(E), F(P), (float)scale, ps.k0(K_INPUT), ps.k1(K_INPUT), p, rb_rows,
+              rs_idx.data_ptr<int>(), (int)nq, ks_idx.data_ptr<int>(), (int)nk, F(xck), S());
+  Tensor xc = xck.narrow(0, 0, nq), xk = xck.narrow(0, nq, nk);
   const float* bin = F(w[B_IN]);
   Tensor q = at::empty({nq, d}, f32), kv = at::empty({nk, 2 * d}, f32);
   proj(ps, nq, d, d, xc, img[0], q, bin, 0, 0, 0, 0.f, 0, nullptr, 0, nullptr, 0.f);

@@ -51,6 +51,13 @@ int c2dsr_gcn_spmm_b16(const int* work, int n_work, const int* split, int n_spli
 int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H, const float* E,
                     const float* Xin, const float* P, float scale, uint32_t k0, uint32_t k1, float p,
                     int64_t idx_base, float* X, void* stream);
+/* The gather form on chosen rows only (the row-subset encoder layer of a training pass, c2dsr::encoder_pass): output
+ * row k = the row above for input row q_idx[k] (k < nq) or k_idx[k - nq] (its query rows, then its padding-key rows),
+ * dropout index (idx_base + input row)·d + c; X [nq + nk, d] — the [n_rows, d] embedding is never stored.
+ * Replaces the same sites as c2dsr_embed_fwd (models/C2DSR.py:65-71, encoders.py:30-31). */
+int c2dsr_embed_fwd_rows(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H, const float* E,
+                         const float* P, float scale, uint32_t k0, uint32_t k1, float p, int64_t idx_base,
+                         const int* q_idx, int nq, const int* k_idx, int nk, float* X, void* stream);
 size_t c2dsr_embed_bwd_workspace(int n_rows, int d);
 /* Sort plan of an index array (stable LSD radix sort; depends on the indices only, so it is built
  * on a side stream under the forward pass): plan = [keys u32 n | rows u32 n | scratch], keys

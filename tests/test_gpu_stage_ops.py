@@ -98,3 +98,53 @@ def test_fused_pass_and_head_are_taken():
         ops.EncoderPassFn.forward, ops.EncoderPassFn.backward = staticmethod(f0), staticmethod(b0)
         losshead.LossHeadFn._backward_stage = staticmethod(h0)
     assert calls == {'fwd': 5, 'bwd': 5, 'head': 1}
+
+
+class _Count:
+    """Counts the calls made through an operator namespace (torch.ops.c2dsr / c2dsr_raw)."""
+
+    def __init__(self, ns, tally, tag):
+        self._ns, self._tally, self._tag = ns, tally, tag
+
+    def __getattr__(self, name):
+        op = getattr(self._ns, name)
+
+        def call(*a, **k):
+            self._tally[f'{self._tag}::{name}'] = self._tally.get(f'{self._tag}::{name}', 0) + 1
+            return op(*a, **k)
+        return call
+
+
+def test_step_operator_calls():
+    """a training step issues a few dozen operator calls (c2dsr:: stage operators plus the
+    c2dsr_raw entry points still called one by one), not one call per kernel."""
+    from c2dsr_amd import _lib
+    rows, gs, gp = _case('fp32')
+    args = make_args(C, dropout=0.2, precision='fp32', seed=5)
+    args.batch_size = 96
+    torch.manual_seed(1234)
+    tr = build_trainer(args, gs, gp)
+    tr.model.train()
+    tr.optimizer.zero_grad()
+    b = [tuple(torch.from_numpy(r[s * 96:(s + 1) * 96].copy()) for r in rows) for s in range(2)]
+    tr.model.convolve_graph()
+    tr.train_batch(b[0])  # warm-up: weight images made, plans cached
+    torch.cuda.synchronize()
+    tally = {}
+    ops = _lib._load_ops()
+    saved = dict(ops)
+    ops['stage'], ops['raw'] = _Count(saved['stage'], tally, 'c2dsr'), _Count(saved['raw'], tally, 'c2dsr_raw')
+    _lib.lib._fns.clear()
+    try:
+        tr.model.convolve_graph()
+        tr.train_batch(b[1])
+        torch.cuda.synchronize()
+    finally:
+        ops.update(saved)
+        _lib.lib._fns.clear()
+    raw = {k: v for k, v in tally.items() if k.startswith('c2dsr_raw::') and not k.endswith(('_workspace', '_bytes',
+                                                                                               '_supported'))}
+    n = sum(tally[k] for k in tally if k.startswith('c2dsr::')) + sum(raw.values())
+    print('operator calls per step:', n, sorted(tally.items()))
+    assert tally.get('c2dsr::encoder_pass') == 5 and tally.get('c2dsr::encoder_pass_backward') == 5
+    assert n <= 48, (n, tally)
