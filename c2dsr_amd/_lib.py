@@ -19,8 +19,11 @@ import numpy as np
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get('C2DSR_LIB') or os.path.join(_HERE, 'libc2dsr_hip.so')
-TORCH_LIB_PATH = os.environ.get('C2DSR_TORCH_LIB') or os.path.join(_HERE, 'libc2dsr_torch.so')
+# C2DSR_LIB_DIR: a directory holding a variant build of both libraries (tools/lib_variant.sh; the operator library
+# loads the kernel library next to it)
+_DIR = os.environ.get('C2DSR_LIB_DIR') or _HERE
+LIB_PATH = os.path.join(_DIR, 'libc2dsr_hip.so')
+TORCH_LIB_PATH = os.path.join(_DIR, 'libc2dsr_torch.so')
 HEADER = os.path.join(os.path.dirname(_HERE), 'include', 'c2dsr.h')
 
 

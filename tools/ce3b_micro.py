@@ -1,0 +1,60 @@
+"""Micro-benchmark of the bf16-mode K5 kernels (csrc/ce3.hip plain-bf16 instantiation: c2dsr_ce3b_fused_fwd_u / _dw)
+at one classifier head, HIP-event timed.  Credited flops 2·Mv·n·d per product (fwd_u: logits + U; dw: dW).
+usage: python tools/ce3b_micro.py [Mv] [n]     (defaults: the FK config's head b, B = 1024: Mv 9472, n 34,886)"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from c2dsr_amd._lib import lib, stream  # noqa: E402
+from c2dsr_amd.losshead import split_count  # noqa: E402
+from tools.ce3_micro import timeit  # noqa: E402
+
+
+def main():
+    Mv = int(sys.argv[1]) if len(sys.argv) > 1 else 9472
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 34886
+    d = 256
+    dev = torch.device('cuda')
+    torch.manual_seed(0)
+    f32 = dict(device=dev, dtype=torch.float32)
+    s = stream()
+    H = torch.randn(Mv, d, **f32) * 0.5
+    W = torch.randn(n, d, **f32) * 0.05
+    bias = torch.randn(n, **f32) * 0.1
+    Mp, n_pad, n64 = -(-Mv // 64) * 64, -(-n // 128) * 128 + 64, -(-n // 64) * 64
+    Hb = torch.zeros(Mp, d, device=dev, dtype=torch.bfloat16)
+    Wb = torch.zeros(n64, d, device=dev, dtype=torch.bfloat16)
+    lib('c2dsr_f32_to_bf16', H, H.numel(), Hb, s)
+    lib('c2dsr_f32_to_bf16', W, W.numel(), Wb, s)
+    bias2 = torch.empty(n_pad, **f32)
+    lib('c2dsr_ce_bias2', bias, n, n_pad, bias2, s)
+    tgt = torch.randint(0, n, (Mv,), device=dev)
+    padc = torch.randn(Mv, **f32)
+    lse, lse2, rows = torch.empty(Mv, **f32), torch.empty(Mp, **f32), torch.empty(Mv, **f32)
+    ns = split_count(Mv, 128)
+    pm, ps = torch.empty(ns, Mv, **f32), torch.empty(ns, Mv, **f32)
+    Up = torch.empty(ns, Mv, d, **f32)
+    fwd = lambda: lib('c2dsr_ce3b_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tgt, H, W, bias,  # noqa
+                      lse, lse2, rows, s)
+    t_f = timeit(fwd)
+    rw, dpad = torch.empty(Mp, **f32), torch.empty(Mp, **f32)
+    crow = torch.empty(Mp + 64, **f32)
+    t32 = torch.empty(Mp, device=dev, dtype=torch.int32)
+    coef = torch.tensor([1.0 / Mv, 1.0 / Mv], **f32)
+    gscale = torch.ones(1, **f32)
+    lib('c2dsr_ce_row_weights', tgt, Mv, Mp, n, coef, Mv // 2, gscale, 0.7, padc, lse, rw, t32, lse2, crow, dpad, s)
+    nr = split_count(n, 128)
+    dWp, dbp = torch.empty(nr, n, d, **f32), torch.empty(nr, n, **f32)
+    dw = lambda: lib('c2dsr_ce3b_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
+    t_w = timeit(dw)
+    fl = 2.0 * Mv * n * d
+    print(f'ce3b Mv={Mv} n={n}: fwd_u {t_f:.1f} us ({2 * fl / t_f / 1e6:.0f} TFLOP/s, ns {ns}); dw {t_w:.1f} us '
+          f'({2 * fl / t_w / 1e6:.0f} executed, {fl / t_w / 1e6:.0f} credited, nr {nr}); both {3 * fl / (t_f + t_w) / 1e6:.0f} '
+          f'credited = {3 * fl / (t_f + t_w) / 1e6 / 2500:.3f} of 2.5 PF; checksum {float(lse.sum()):.4f} '
+          f'{float(dWp.sum()):.4f}', flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -1,6 +1,6 @@
 """Bit-identity probe for K1 variants on bf16 tables at d = 512 (the C5 width): forward (mask on the gathered
 rows) and backward (Aᵀ, mask on the output rows) on a 400,001-row synthetic item graph with split hub rows;
-prints a digest of both outputs and the per-launch time.  Run once per library (C2DSR_LIB=...) and compare."""
+prints a digest of both outputs and the per-launch time.  Run once per library (C2DSR_LIB_DIR=...) and compare."""
 import hashlib
 import os
 import sys
