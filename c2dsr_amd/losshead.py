@@ -49,6 +49,26 @@ def split_count(rows, tile, max_split=16, per_cu=1):
     return best
 
 
+def dw_split_count(n, Mv, x3, d=256, max_split=16):
+    """Row splits of the dW sweep (ce3.hip MODE 1: 128 stationary W rows per workgroup; the Mv swept rows in 32-row
+    tiles on split images, 64-row tiles on bf16 ones): the count minimising rounds × (tiles per workgroup + a
+    workgroup's fixed cost) + the partial slabs' combine, in tile-times fitted to split sweeps on the box
+    (tools/ce3_micro.py / ce3b_micro.py: a tile 1.87 / 1.47 µs, a workgroup's fixed cost ≈ 16 / 9 tiles, a partial
+    slab of n·d fp32 written and summed ≈ 7.5 µs at 36.8k × 256).  One split accumulates straight into the gradient.
+    (split_count alone picked 15 splits for the Food-Kitchen heads: 543 µs of sweep + sum where 3-4 take 379.)"""
+    tiles = max(1, -(-n // 128))
+    sweep = max(1, -(-Mv // (32 if x3 else 64)))
+    t_tile, wg = (1.87, 16.0) if x3 else (1.47, 9.0)
+    slab = 7.5 * (n * d) / (36845 * 256) / t_tile
+    slots = _ncu()
+    best, best_t = 1, None
+    for s in range(1, max_split + 1):
+        t = -(-tiles * s // slots) * (-(-sweep // s) + wg) + (s * slab if s > 1 else 0.0)
+        if best_t is None or t < best_t - 1e-9:
+            best, best_t = s, t
+    return best
+
+
 def ce_kind(precision, d):
     """Fused classifier-head kernels for this precision and width: 'b16' (ce.hip, bf16 operands), 'x3'
     (ce3.hip, split-bf16 operands: the fp32 mode), or None (materialised fp32 logits + exact fp32 GEMMs)."""
@@ -360,7 +380,8 @@ class LossHeadFn(Function):
         for (saved, inv, tc, Mv0, Mv1, tplan, W, bias, n), coef in zip(heads, coefs):
             gW, gb = _grad_target(W), _grad_target(bias)
             hd += T.ce_head_backward(saved, W, inv, tc, Mv0, Mv1, coef, gscale, float(m.lam), gW, gb, gwpad, gbpad,
-                                     tplan.get() if tplan is not None else None, split_count(n, 128), mode)
+                                     tplan.get() if tplan is not None else None,
+                                     dw_split_count(n, Mv0 + Mv1, mode == 0, d), mode)
         imgT = [weight_img(m.Da_w.view(d, d), kind, trans=True), weight_img(m.Db_w.view(d, d), kind, trans=True)]
         gD = [_grad_target(t) for t in (m.Da_w, m.Da_b, m.Db_w, m.Db_b)]
         sub = [r.idx[:r.n] if r is not None else None for r in rsets]
@@ -416,7 +437,7 @@ class LossHeadFn(Function):
                         lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, Mv, n, d, ns, crow, dHp, s)
                         lib('c2dsr_ce_dh_combine', dHp, ns, Mv, d, t32, rw, W, n, dHc, s)
                         del dHp
-                    nr = split_count(n, 128)
+                    nr = dw_split_count(n, Mv, ctx.x3, d) if d == 256 else split_count(n, 128)
                     entry = ce_entry(ctx.x3, d, 'dw')
                     if nr == 1 and gW is not None and gb is not None and entry.startswith('c2dsr_ce3'):
                         # one split: the sweep adds onto the gradients itself (n_rsplit = 0; no partials / sum)

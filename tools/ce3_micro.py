@@ -48,7 +48,7 @@ def main():
     tgt = torch.randint(0, n, (Mv,), device=dev)
     padc = torch.randn(Mv, **f32)
     lse, lse2, rows = torch.empty(Mv, **f32), torch.empty(Mp, **f32), torch.empty(Mv, **f32)
-    ns = int(sys.argv[3]) if len(sys.argv) > 3 else split_count(Mv, 128)
+    ns = int(sys.argv[3]) if len(sys.argv) > 3 and int(sys.argv[3]) else split_count(Mv, 128)
     pm, ps = torch.empty(ns, Mv, **f32), torch.empty(ns, Mv, **f32)
     Up = torch.empty(ns, Mv, d, **f32)
     fwd = lambda: lib('c2dsr_ce3_fused_fwd_u', Hx, Wx, bias2, Mv, n, d, ns, pm, ps, Up, padc, tgt, H, W, bias,  # noqa
@@ -60,14 +60,15 @@ def main():
     coef = torch.tensor([1.0 / Mv, 1.0 / Mv], **f32)
     gscale = torch.ones(1, **f32)
     lib('c2dsr_ce_row_weights', tgt, Mv, Mp, n, coef, Mv // 2, gscale, 0.7, padc, lse, rw, t32, lse2, crow, dpad, s)
-    nr = int(sys.argv[4]) if len(sys.argv) > 4 else split_count(n, 128)
+    nr = int(sys.argv[4]) if len(sys.argv) > 4 and int(sys.argv[4]) else split_count(n, 128)
     dWp, dbp = torch.empty(nr, n, d, **f32), torch.empty(nr, n, **f32)
     dw = lambda: lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
     t_w = timeit(dw)
+    t_s = timeit(lambda: lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, W, s)) if nr > 1 else 0.0
     fl = 2.0 * Mv * n * d
     print(f'ce3 Mv={Mv} n={n}: split {t_split:.1f} us; fwd_u {t_f:.1f} us ({2 * fl / t_f / 1e6:.0f} TFLOP/s credited, '
           f'{6 * fl / t_f / 1e6:.0f} executed, ns {ns}); dw {t_w:.1f} us ({fl / t_w / 1e6:.0f} credited, '
-          f'{6 * fl / t_w / 1e6:.0f} executed, nr {nr}); checksum {float(lse.sum()):.4f} {float(dWp.sum()):.4f}',
+          f'{6 * fl / t_w / 1e6:.0f} executed, nr {nr}, sum {t_s:.1f} us); checksum {float(lse.sum()):.4f} {float(dWp.sum()):.4f}',
           flush=True)
     print_stamps([('fwd_u', fwd), ('dw', dw)])
 

@@ -1,6 +1,7 @@
 """Micro-benchmark of the bf16-mode K5 kernels (csrc/ce3.hip plain-bf16 instantiation: c2dsr_ce3b_fused_fwd_u / _dw)
 at one classifier head, HIP-event timed.  Credited flops 2·Mv·n·d per product (fwd_u: logits + U; dw: dW).
-usage: python tools/ce3b_micro.py [Mv] [n]     (defaults: the FK config's head b, B = 1024: Mv 9472, n 34,886)"""
+usage: python tools/ce3b_micro.py [Mv] [n] [split_fwd] [split_dw]   (defaults: the FK config's head b, B = 1024: Mv 9472,
+       n 34,886; splits: losshead.split_count)"""
 import os
 import sys
 
@@ -33,7 +34,7 @@ def main():
     tgt = torch.randint(0, n, (Mv,), device=dev)
     padc = torch.randn(Mv, **f32)
     lse, lse2, rows = torch.empty(Mv, **f32), torch.empty(Mp, **f32), torch.empty(Mv, **f32)
-    ns = split_count(Mv, 128)
+    ns = int(sys.argv[3]) if len(sys.argv) > 3 and int(sys.argv[3]) else split_count(Mv, 128)
     pm, ps = torch.empty(ns, Mv, **f32), torch.empty(ns, Mv, **f32)
     Up = torch.empty(ns, Mv, d, **f32)
     fwd = lambda: lib('c2dsr_ce3b_fused_fwd_u', Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tgt, H, W, bias,  # noqa
@@ -45,13 +46,14 @@ def main():
     coef = torch.tensor([1.0 / Mv, 1.0 / Mv], **f32)
     gscale = torch.ones(1, **f32)
     lib('c2dsr_ce_row_weights', tgt, Mv, Mp, n, coef, Mv // 2, gscale, 0.7, padc, lse, rw, t32, lse2, crow, dpad, s)
-    nr = split_count(n, 128)
+    nr = int(sys.argv[4]) if len(sys.argv) > 4 and int(sys.argv[4]) else split_count(n, 128)
     dWp, dbp = torch.empty(nr, n, d, **f32), torch.empty(nr, n, **f32)
     dw = lambda: lib('c2dsr_ce3b_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
     t_w = timeit(dw)
+    t_s = timeit(lambda: lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, W, s)) if nr > 1 else 0.0
     fl = 2.0 * Mv * n * d
     print(f'ce3b Mv={Mv} n={n}: fwd_u {t_f:.1f} us ({2 * fl / t_f / 1e6:.0f} TFLOP/s, ns {ns}); dw {t_w:.1f} us '
-          f'({2 * fl / t_w / 1e6:.0f} executed, {fl / t_w / 1e6:.0f} credited, nr {nr}); both {3 * fl / (t_f + t_w) / 1e6:.0f} '
+          f'({2 * fl / t_w / 1e6:.0f} executed, {fl / t_w / 1e6:.0f} credited, nr {nr}, sum {t_s:.1f} us); both {3 * fl / (t_f + t_w) / 1e6:.0f} '
           f'credited = {3 * fl / (t_f + t_w) / 1e6 / 2500:.3f} of 2.5 PF; checksum {float(lse.sum()):.4f} '
           f'{float(dWp.sum()):.4f}', flush=True)
 
