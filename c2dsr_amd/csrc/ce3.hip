@@ -141,6 +141,9 @@ __device__ __forceinline__ float quad_sum(float x) {
 #ifndef CE3_VN
 #define CE3_VN 5
 #endif
+#ifndef CE3_P1  // the second product with the probabilities as one bf16 term (2 MFMAs instead of 3; measured option)
+#define CE3_P1 0
+#endif
 // Two forms of one split product step, acc (+)= a_hi·b_hi + a_lo·b_hi + a_hi·b_lo, chosen per kernel role:
 //  * asm: ONE asm statement for the three MFMAs on one accumulator (separate statements get an s_nop between
 //    dependent MFMAs from the hazard pass).  S product: the stationary b_hi / b_lo pinned to AGPRs (128 registers
@@ -197,6 +200,21 @@ __device__ __forceinline__ void split3_u(f32x4& acc, const bf16x8& ah, const bf1
         "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0"
         : "+a"(acc)
         : "v"(ah), "v"(al), "v"(bh), "v"(bl));
+  }
+}
+// second product with the B operand (the probabilities) as ONE bf16 term (CE3_P1, measured option, not the default):
+// acc += a_hi·b + a_lo·b
+template <bool BI>
+__device__ __forceinline__ void split2_u(f32x4& acc, const bf16x8& ah, const bf16x8& al, const bf16x8& b) {
+  if constexpr (BI) {
+    acc = MF(ah, b, acc);
+    acc = MF(al, b, acc);
+  } else {
+    asm volatile(
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0"
+        : "+a"(acc)
+        : "v"(ah), "v"(al), "v"(b));
   }
 }
 #undef MF
@@ -516,10 +534,10 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 for (int j = 0; j < 8; ++j) {
                   const float x = sc[(2 * u + (j >> 2)) * SBW + sb][j & 3];
                   h[j] = (bf16)x;
-                  if constexpr (SPLIT) l[j] = (bf16)(x - (float)h[j]);
+                  if constexpr (SPLIT && !CE3_P1) l[j] = (bf16)(x - (float)h[j]);
                 }
                 xh[u][sb] = h;
-                if constexpr (SPLIT) xl[u][sb] = l;
+                if constexpr (SPLIT && !CE3_P1) xl[u][sb] = l;
               }
               if constexpr (ILVS && SBW == 2) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
 #pragma unroll
         for (int sb = 0; sb < SBW; ++sb) {
           asm volatile("" : "+v"(xh[u][sb]));
-          if constexpr (SPLIT) asm volatile("" : "+v"(xl[u][sb]));
+          if constexpr (SPLIT && !CE3_P1) asm volatile("" : "+v"(xl[u][sb]));
         }
       }
       asm volatile("s_nop 7" ::: "memory");  // S(t+1)'s last results before the prep's VALU reads
@@ -562,7 +580,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
               if constexpr (k + DS >= NUS) s_frags.template operator()<k + DS - NUS>(oN, fa[k + DS - NUS]);
               const bf16x8(&tq)[2] = tf[k % (DT + 2)];
               auto u_prod = [&](int sb) {
-                if constexpr (SPLIT)
+                if constexpr (SPLIT && CE3_P1)
+                  split2_u<BIU>(dacc[q][sb], tq[0], tq[1], xh[u][sb]);
+                else if constexpr (SPLIT)
                   split3_u<BIU>(dacc[q][sb], tq[0], tq[1], xh[u][sb], xl[u][sb]);
                 else
                   mf1_u(dacc[q][sb], tq[0], xh[u][sb]);
@@ -585,7 +605,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 __builtin_amdgcn_sched_barrier(0);
                 u_prod(1);
               }
-              step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BIU>();
+              step_pattern<SPLIT ? (CE3_P1 ? 2 : 3) * SBW : SBW, CE3_VN, BIU>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
