@@ -75,11 +75,12 @@ def main():
 
 def print_stamps(fns):
     """Diagnostic build (-DCE3_STAMP): cycles per tile per wave of the ce3 tile loop's phases."""
-    try:
-        fn = lib.raw('c2dsr_ce3_stamps')
-    except AttributeError:
-        return
     import ctypes
+    from c2dsr_amd import _lib
+    so = ctypes.CDLL(os.path.join(_lib._DIR, 'libc2dsr_hip.so'))  # the stamp entry exists in the diagnostic build only
+    if not hasattr(so, 'c2dsr_ce3_stamps'):
+        return
+    fn = so.c2dsr_ce3_stamps
     buf = (ctypes.c_ulonglong * 8)()
     ph = ('rescale/pre', 'S+epi', 'nop+dmawait', 'barrier', 'U+prep', 'loop-top')
     for name, f in fns:

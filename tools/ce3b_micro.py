@@ -10,7 +10,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from c2dsr_amd._lib import lib, stream  # noqa: E402
 from c2dsr_amd.losshead import split_count  # noqa: E402
-from tools.ce3_micro import timeit  # noqa: E402
+from tools.ce3_micro import print_stamps, timeit  # noqa: E402
 
 
 def main():
@@ -56,6 +56,7 @@ def main():
           f'({2 * fl / t_w / 1e6:.0f} executed, {fl / t_w / 1e6:.0f} credited, nr {nr}, sum {t_s:.1f} us); both {3 * fl / (t_f + t_w) / 1e6:.0f} '
           f'credited = {3 * fl / (t_f + t_w) / 1e6 / 2500:.3f} of 2.5 PF; checksum {float(lse.sum()):.4f} '
           f'{float(dWp.sum()):.4f}', flush=True)
+    print_stamps([('fwd_u', fwd), ('dw', dw)])
 
 
 if __name__ == '__main__':

@@ -63,6 +63,30 @@ def main():
     print(f'rows {n_rows} uniq {uniq}: G-only {t_g:.1f} us, gP-only {t_p:.1f} us, both {t_b:.1f} us '
           f'({byt / (t_b * 1e-6) / 1e9:.0f} GB/s credited), seq plan build {t_plan:.1f} us', flush=True)
 
+    # the fused pass's form (c2dsr_embed_bwd_planned_rows): the gradient as two compact parts — the rows the loss reads
+    # (here: every non-padding row with probability 0.6) and the padding rows (the keys of the inverted mask)
+    nonpad = pos.reshape(-1) != 0
+    q_rows = np.flatnonzero(nonpad & (rng.random(n_rows) < 0.6))
+    k_rows = np.flatnonzero(~nonpad)
+    inv_a = np.full(n_rows, -1, dtype=np.int32)
+    inv_b = np.full(n_rows, -1, dtype=np.int32)
+    inv_a[q_rows] = np.arange(q_rows.size, dtype=np.int32)
+    inv_b[k_rows] = np.arange(k_rows.size, dtype=np.int32)
+    gXa = torch.randn(q_rows.size, d, device=dev)
+    gXb = torch.randn(k_rows.size, d, device=dev)
+    ia, ib = torch.from_numpy(inv_a).to(dev), torch.from_numpy(inv_b).to(dev)
+
+    def run_rows(g, p):
+        lib('c2dsr_embed_bwd_planned_rows', spb if g is not None else None, ppb if p is not None else None, n_rows, d,
+            gXa, ia, gXb, ib, 0, 0, 0.0, 0, 1.0, g, N, p, L, ws, wsb, s)
+
+    r_g = timeit(lambda: run_rows(G, None))
+    r_p = timeit(lambda: run_rows(None, gP))
+    r_b = timeit(lambda: run_rows(G, gP))
+    print(f'two-part rows (q {q_rows.size}, k {k_rows.size}): G-only {r_g:.1f} us, gP-only {r_p:.1f} us, both {r_b:.1f} us '
+          f'({byt / (r_b * 1e-6) / 1e9:.0f} GB/s credited); checksum {float(G.sum()):.4e} {float(gP.sum()):.4e}',
+          flush=True)
+
 
 if __name__ == '__main__':
     main()
