@@ -16,11 +16,6 @@
 typedef __bf16 bf16;
 
 #define WMFMA(a, b, c, x, y, z) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), (x), (y), (z))
-// wave-per-sequence kernels: the next 32-column tile's row loads issued before this tile's MFMAs (V in the forward's
-// O product, K in dQ, dO / Q in dV / dK)
-#ifndef ATTN_PF
-#define ATTN_PF 0
-#endif
 
 #include <cstdlib>
 
@@ -726,26 +721,12 @@ __device__ __forceinline__ void fwd_wave_body(const float* __restrict__ Q, long 
     }
   };
   const int CT = dh >> 5;
-#if ATTN_PF
-  // the next column tile's V loads in flight under this tile's MFMAs
-  float va[2][16], vb[2][16];
-  vload(va, 0);
-#pragma unroll 1
-  for (int ct = 0; ct < CT; ct += 2) {
-    if (ct + 1 < CT) vload(vb, ct + 1);
-    otile(va, ct);
-    if (ct + 1 >= CT) break;
-    if (ct + 2 < CT) vload(va, ct + 2);
-    otile(vb, ct + 1);
-  }
-#else
 #pragma unroll 1
   for (int ct = 0; ct < CT; ++ct) {
     float va[2][16];
     vload(va, ct);
     otile(va, ct);
   }
-#endif
 }
 
 // the wave's sequence in the full layout: padding bits and key extent (one past the last padding key)
@@ -962,19 +943,17 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
   // ---- dQ = dS·K/√dh (lane = column, rows = queries)
   {
     const auto ksrc = rows_rsrc(K, nk, ks, dh);
-    auto kload = [&](float (&kv)[2][16], int ct) {
+#pragma unroll 1
+    for (int ct = 0; ct < CT; ++ct) {
+      float k0v[16], k1v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int key = (q & 3) + 8 * (q >> 2) + 4 * hi;
-        kv[0][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrc, (key * (int)ks + 32 * ct + r) * 4, 0, 0));
-        kv[1][q] = TJ > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                ksrc, ((32 + key) * (int)ks + 32 * ct + r) * 4, 0, 0))
-                          : 0.f;
+        k0v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrc, (key * (int)ks + 32 * ct + r) * 4, 0, 0));
+        k1v[q] = TJ > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                              ksrc, ((32 + key) * (int)ks + 32 * ct + r) * 4, 0, 0))
+                        : 0.f;
       }
-    };
-    auto dqtile = [&](const float (&kv)[2][16], int ct) {
-      const float(&k0v)[16] = kv[0];
-      const float(&k1v)[16] = kv[1];
       f32x16 o0, o1;
       zero16(o0); zero16(o1);
 #pragma unroll
@@ -993,26 +972,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
         if (i0 < nq) dQ[(long)i0 * dqs + c] = (OT)(sc * o0[q]);
         if (TI > 1 && i1 < nq) dQ[(long)i1 * dqs + c] = (OT)(sc * o1[q]);
       }
-    };
-#if ATTN_PF
-    float ka[2][16], kb[2][16];
-    kload(ka, 0);
-#pragma unroll 1
-    for (int ct = 0; ct < CT; ct += 2) {
-      if (ct + 1 < CT) kload(kb, ct + 1);
-      dqtile(ka, ct);
-      if (ct + 1 >= CT) break;
-      if (ct + 2 < CT) kload(ka, ct + 2);
-      dqtile(kb, ct + 1);
     }
-#else
-#pragma unroll 1
-    for (int ct = 0; ct < CT; ++ct) {
-      float ka[2][16];
-      kload(ka, ct);
-      dqtile(ka, ct);
-    }
-#endif
   }
   // ---- dV = Pdᵀ·dO, dK = dSᵀ·Q/√dh: transpose through this wave's LDS tile T[i][j] (stride 65)
   constexpr int TLD = 65;
@@ -1027,20 +987,17 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
   };
   auto keys_out = [&](const float* __restrict__ Src, long ss, float scale, OT* __restrict__ Dst) {
     const auto src = rows_rsrc(Src, nq, ss, dh);
-    // Src rows (queries) of register q: (q&3) + 8(q>>2) + 4hi (+32)
-    auto bload = [&](float (&bv)[2][16], int ct) {
+#pragma unroll 1
+    for (int ct = 0; ct < CT; ++ct) {
+      float b0v[16], b1v[16];  // Src rows (queries) of register q: (q&3) + 8(q>>2) + 4hi (+32)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int qi = (q & 3) + 8 * (q >> 2) + 4 * hi;
-        bv[0][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(src, (qi * (int)ss + 32 * ct + r) * 4, 0, 0));
-        bv[1][q] = TI > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                src, ((32 + qi) * (int)ss + 32 * ct + r) * 4, 0, 0))
-                          : 0.f;
+        b0v[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(src, (qi * (int)ss + 32 * ct + r) * 4, 0, 0));
+        b1v[q] = TI > 1 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                              src, ((32 + qi) * (int)ss + 32 * ct + r) * 4, 0, 0))
+                        : 0.f;
       }
-    };
-    auto ktile = [&](const float (&bv)[2][16], int ct) {
-      const float(&b0v)[16] = bv[0];
-      const float(&b1v)[16] = bv[1];
       const int c = 32 * ct + r;
 #pragma unroll
       for (int tj = 0; tj < TJ; ++tj) {
@@ -1062,26 +1019,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
         }
       }
       for (int j = 32 * TJ + hi; j < nkw; j += 2) Dst[(long)j * dks + c] = (OT)0.f;  // keys past the tiles
-    };
-#if ATTN_PF
-    float ba[2][16], bb[2][16];
-    bload(ba, 0);
-#pragma unroll 1
-    for (int ct = 0; ct < CT; ct += 2) {
-      if (ct + 1 < CT) bload(bb, ct + 1);
-      ktile(ba, ct);
-      if (ct + 1 >= CT) break;
-      if (ct + 2 < CT) bload(ba, ct + 2);
-      ktile(bb, ct + 1);
     }
-#else
-#pragma unroll 1
-    for (int ct = 0; ct < CT; ++ct) {
-      float ba[2][16];
-      bload(ba, ct);
-      ktile(ba, ct);
-    }
-#endif
   };
   // T starts as garbage: every entry the products read ([0, 32·TI) x [0, 32·TJ)) is written first
   put(p0, p3, T3, 0);
