@@ -253,7 +253,8 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                                                       const float* __restrict__ svec, const float* __restrict__ wvec,
                                                       int n_s, int n_w, int per_split, float* __restrict__ part_m,
                                                       float* __restrict__ part_s, float* __restrict__ outp,
-                                                      int accum) {
+                                                      int accum, int sk_nwg, float* __restrict__ slot_w,
+                                                      float* __restrict__ slot_b) {
   constexpr int T3 = tile_rows<SPLIT>();
   constexpr int CB = T3 / 16;                      // 16-row swept blocks per tile
   constexpr int UK = T3 / 32;                      // 32-row k-steps of the second product per e-block
@@ -287,11 +288,34 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   // XCD-aware work map: block b runs on XCD b % 8; the (split, row block) pairs, split-major, are dealt to the XCDs in
   // contiguous ranges, so each split's swept slice streams through the L2 of one or two XCDs instead of all eight
   const int nrb = (n_s + 127) >> 7, nb = (int)gridDim.x;
-  const int pidx = nb % 8 == 0 ? (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
-  const int split = pidx / nrb, rblk = pidx % nrb;
+  // stream-K (MODE 1, sk_nwg workgroups, one per CU): the (row block, swept tile) units in row-block-major order are
+  // dealt to the workgroups in equal contiguous ranges, one launch round with no partial last round; a workgroup walks
+  // its range as segments (≤ one per row block it touches).  A row block swept whole by one workgroup is added onto the
+  // gradient directly; a split one leaves a partial in its workgroup's slot 0 (its first segment) or 1 (its last),
+  // summed in workgroup order by ce3_sk_combine_kernel.
+  const long skT = (n_w + T3 - 1) / T3, skU = (long)nrb * skT;
+  long sk_u = sk_nwg ? (long)blockIdx.x * skU / sk_nwg : 0;
+  const long sk_u1 = sk_nwg ? ((long)blockIdx.x + 1) * skU / sk_nwg : 0;
+  for (int seg = 0;; ++seg) {
+  int split, rblk, w_beg, w_end, slot = -1;
+  if (sk_nwg) {
+    if (sk_u >= sk_u1) break;  // uniform over the workgroup
+    rblk = (int)(sk_u / skT);
+    const long t0 = sk_u % skT, t1 = min(skT, t0 + (sk_u1 - sk_u));
+    split = 0;
+    w_beg = (int)(t0 * T3);
+    w_end = min(n_w, (int)(t1 * T3));
+    if (t0 != 0 || t1 != skT) slot = seg == 0 ? 0 : 1;
+    sk_u += t1 - t0;
+  } else {
+    if (seg) break;
+    const int pidx = nb % 8 == 0 ? (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    split = pidx / nrb;
+    rblk = pidx % nrb;
+    w_beg = split * per_split;
+    w_end = min(n_w, w_beg + per_split);
+  }
   const int s0 = rblk * 128 + w * 16 * SBW + l16;  // stationary rows s0 + 16·sb, sb < SBW
-  const int w_beg = split * per_split;
-  const int w_end = min(n_w, w_beg + per_split);
   const int ntiles = w_end > w_beg ? (w_end - w_beg + T3 - 1) / T3 : 0;
   f32x4 dacc[NE][SBW];
   float mrow[SBW], zrow[SBW];
@@ -630,20 +654,74 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   for (int sb = 0; sb < SBW; ++sb) {
     const float ztot = quad_sum(zrow[sb]);
     const int s = s0 + 16 * sb;
-    if (s < n_s) {
+    if (s < n_s && slot >= 0) {  // stream-K partial of a split row block
+      const long so = (long)(2 * blockIdx.x + slot) * 128 + (s - rblk * 128);
+      if (g == 0) slot_b[so] = ztot;
+      float* out = slot_w + so * D + 4 * g;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
+    } else if (s < n_s) {
+      const bool acc = accum || sk_nwg;
       if (g == 0) {
         if constexpr (MODE == 0) part_m[(long)split * n_s + s] = mrow[sb];
-        // accum (MODE 1, one split: this workgroup owns its columns): add onto the epoch-long gradient directly
-        part_s[(long)split * n_s + s] = accum ? part_s[s] + ztot : ztot;
+        // accum (MODE 1, one split or a whole stream-K row block: this workgroup owns its columns): add onto the
+        // epoch-long gradient directly
+        part_s[(long)split * n_s + s] = acc ? part_s[s] + ztot : ztot;
       }
       float* out = outp + ((long)split * n_s + s) * D + 4 * g;
-      if (accum) {
+      if (acc) {
 #pragma unroll
         for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = *(const f32x4*)(out + 16 * e) + dacc[e][sb];
       } else {
 #pragma unroll
         for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
       }
+    }
+  }
+  if (sk_nwg) {  // the next segment's prologue refills the LDS images: every wave past this one's reads and DMAs
+    vm_drain();
+    __syncthreads();
+  }
+  }  // segments
+}
+
+// stream-K partials of the split row blocks (ce3_kernel MODE 1): gW[rb] += Σ_w slot(w, rb), w ascending over the
+// workgroups whose unit ranges overlap row block rb (a block swept whole by one workgroup was written directly).
+// One block per row block; thread → (row, float4 column).
+__device__ __forceinline__ int sk_wg_of(long u, long U, int nwg) {
+  int w = (int)((u * nwg) / U);
+  while (w + 1 < nwg && ((long)(w + 1) * U) / nwg <= u) ++w;
+  while (w > 0 && ((long)w * U) / nwg > u) --w;
+  return w;
+}
+__global__ __launch_bounds__(256) void ce3_sk_combine_kernel(const float* __restrict__ slot_w,
+                                                             const float* __restrict__ slot_b, int n, int D, long T,
+                                                             int nwg, float* __restrict__ gW, float* __restrict__ gb) {
+  const int rb = blockIdx.x;
+  const long U = (long)((n + 127) >> 7) * T;
+  const long ub = (long)rb * T, ue = ub + T - 1;
+  const int wa = sk_wg_of(ub, U, nwg), wz = sk_wg_of(ue, U, nwg);
+  if (wa == wz) return;  // uniform
+  const int C4 = D / 4;
+  for (int i = threadIdx.x; i < 128 * (C4 + 1); i += 256) {
+    const int r = i / (C4 + 1), c = i % (C4 + 1);  // c == C4: the bias column
+    const long row = (long)rb * 128 + r;
+    if (row >= n) continue;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    float b = 0.f;
+    for (int w = wa; w <= wz; ++w) {
+      const long wu0 = ((long)w * U) / nwg;
+      if (wu0 == ((long)(w + 1) * U) / nwg) continue;  // an empty range (fewer units than workgroups)
+      const int sl = wu0 >= ub ? 0 : 1;
+      const long so = (long)(2 * w + sl) * 128 + r;
+      if (c < C4) a = a + *(const float4*)(slot_w + so * D + 4 * c);
+      else b += slot_b[so];
+    }
+    if (c < C4) {
+      float4* o = (float4*)(gW + row * D + 4 * c);
+      *o = *o + a;
+    } else {
+      gb[row] += b;
     }
   }
 }
@@ -674,26 +752,59 @@ int per_split3(int total, int nsplit, int t3) {
   return c2::ceil_div(tiles, nsplit) * t3;
 }
 
+int g_ncu3 = 0;
+int num_cus3() {
+  if (!g_ncu3) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+    g_ncu3 = v > 0 ? v : 256;
+  }
+  return g_ncu3;
+}
+
+// stream-K slots: two [128][D] fp32 partials (+ two [128] bias partials) per workgroup
+size_t sk_slot_floats(int nwg, int D) { return (size_t)2 * nwg * 128 * D; }
+size_t sk_ws_bytes(int nwg, int D) { return (sk_slot_floats(nwg, D) + (size_t)2 * nwg * 128) * 4; }
+
 template <int MODE, bool SPLIT>
 int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec, int n_s, int n_w, int D, int nsplit,
-            float* pm, float* ps, float* out, hipStream_t st) {
-  // MODE 1 with nsplit == 0: one split, accumulated straight onto out / ps (the gradient buffers)
+            float* pm, float* ps, float* out, hipStream_t st, int sk_nwg = 0, float* slot_w = nullptr,
+            float* slot_b = nullptr) {
+  // MODE 1 with nsplit == 0: one split, accumulated straight onto out / ps (the gradient buffers); sk_nwg > 0:
+  // stream-K over sk_nwg workgroups (MODE 1; whole row blocks accumulated, partials into the slots)
   const int accum = MODE == 1 && nsplit == 0;
   if (accum) nsplit = 1;
-  if (nsplit < 1) return (int)hipErrorInvalidValue;
+  if (nsplit < 1 || (sk_nwg && (MODE != 1 || !slot_w || !slot_b))) return (int)hipErrorInvalidValue;
   const int per = per_split3(n_w, nsplit, tile_rows<SPLIT>());
-  const dim3 grid(c2::ceil_div(n_s, 128) * nsplit);  // (row block, split) pairs: ce3_kernel's XCD-aware map
+  // (row block, split) pairs: ce3_kernel's XCD-aware map; stream-K: one workgroup per CU
+  const dim3 grid(sk_nwg ? sk_nwg : c2::ceil_div(n_s, 128) * nsplit);
   constexpr int NW = SPLIT ? CE3_NW : CE3B_NW;
   if (D == 128)
     ce3_kernel<128, MODE, SPLIT, NW><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w,
-                                                                per, pm, ps, out, accum);
+                                                                per, pm, ps, out, accum, sk_nwg, slot_w, slot_b);
   else if (D == 256)
     ce3_kernel<256, MODE, SPLIT, NW><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w,
-                                                                per, pm, ps, out, accum);
+                                                                per, pm, ps, out, accum, sk_nwg, slot_w, slot_b);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
+  if (sk_nwg) {
+    const long T = (n_w + tile_rows<SPLIT>() - 1) / tile_rows<SPLIT>();
+    ce3_sk_combine_kernel<<<c2::ceil_div(n_s, 128), 256, 0, st>>>(slot_w, slot_b, n_s, D, T, sk_nwg, out, ps);
+    C2_CHECK_LAUNCH();
+  }
   return 0;
+}
+
+template <bool SPLIT>
+int dw_sk(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, const float* crow, float* gW,
+          float* gb, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (n == 0) return 0;
+  const int nwg = num_cus3();
+  if (!gW || !gb || !ws || ws_bytes < sk_ws_bytes(nwg, D)) return (int)hipErrorInvalidValue;
+  float* sw = (float*)ws;
+  return launch3<1, SPLIT>(Wx, Hx, bias2, crow, n, M, D, 1, nullptr, gb, gW, st, nwg, sw, sw + sk_slot_floats(nwg, D));
 }
 
 }  // namespace
@@ -729,6 +840,13 @@ C2_API int c2dsr_ce3_fused_dw(const void* Hx, const void* Wx, const float* bias2
   return launch3<1, true>(Wx, Hx, bias2, crow, n, M, D, n_rsplit, nullptr, dbp, dWp, (hipStream_t)stream);
 }
 
+C2_API size_t c2dsr_ce3_dw_sk_workspace(int D) { return sk_ws_bytes(num_cus3(), D); }
+
+C2_API int c2dsr_ce3_fused_dw_sk(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D,
+                                 const float* crow, float* gW, float* gb, void* ws, size_t ws_bytes, void* stream) {
+  return dw_sk<true>(Hx, Wx, bias2, M, n, D, crow, gW, gb, ws, ws_bytes, (hipStream_t)stream);
+}
+
 // The same pair on plain bf16 images [rows][D] (the bf16 mode; drop-in for ce.hip's c2dsr_ce_fused_fwd_u /
 // c2dsr_ce_fused_dw, same arguments and outputs): 64-row swept tiles, one MFMA per product.  Images hold whole
 // 64-row tiles (zero rows past the end); crow carries a 64-value tail.
@@ -746,6 +864,11 @@ C2_API int c2dsr_ce3b_fused_dw(const void* Hb, const void* Wb, const float* bias
                                const float* crow, float* dWp, float* dbp, void* stream) {
   if (n == 0) return 0;
   return launch3<1, false>(Wb, Hb, bias2, crow, n, M, D, n_rsplit, nullptr, dbp, dWp, (hipStream_t)stream);
+}
+
+C2_API int c2dsr_ce3b_fused_dw_sk(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D,
+                                  const float* crow, float* gW, float* gb, void* ws, size_t ws_bytes, void* stream) {
+  return dw_sk<false>(Hb, Wb, bias2, M, n, D, crow, gW, gb, ws, ws_bytes, (hipStream_t)stream);
 }
 
 #ifdef CE3_STAMP

@@ -298,7 +298,8 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
   if (has(tplan))
     TORCH_CHECK(tplan->scalar_type() == at::kByte && (size_t)tplan->nbytes() >= c2dsr_index_plan_bytes((int)Mv),
                 "c2dsr::ce_head_backward: target plan too small");
-  TORCH_CHECK(n_rsplit >= 1 && n_rsplit <= 64 && (mode == 0 || mode == 1), "c2dsr::ce_head_backward: splits / mode");
+  // n_rsplit 0: the stream-K sweep (c2dsr_ce3_fused_dw_sk; needs both gradients)
+  TORCH_CHECK(n_rsplit >= 0 && n_rsplit <= 64 && (mode == 0 || mode == 1), "c2dsr::ce_head_backward: splits / mode");
   on_device(op, {&W, &Hpad, &inv, &tc, &Hc, &padc, &lse_c, &lse2, &Up, &pm, &bias2, &Hb, &Wb, &coef, &gscale});
   on_device(op, {gW, gb, gwpad, gbpad, tplan});
   const auto f32 = W.options();
@@ -322,9 +323,20 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
                     (const void*)Wb.data_ptr(), (const float*)F(bias2), (int)Mv, (int)n, (int)d, nr,
                     (const float*)F(crow), dWp, dbp, S());
     };
-    if (n_rsplit == 1 && has(gW) && has(gb)) {
+    if (n_rsplit == 0 && has(gW) && has(gb)) {  // stream-K: whole row blocks added directly, split ones combined
+      Tensor ws = at::empty({(int64_t)c2dsr_ce3_dw_sk_workspace((int)d)}, f32.dtype(at::kByte));
+      if (mode == 0)
+        c2t::launch("c2dsr_ce3_fused_dw_sk", &c2dsr_ce3_fused_dw_sk, (const void*)Hb.data_ptr(),
+                    (const void*)Wb.data_ptr(), (const float*)F(bias2), (int)Mv, (int)n, (int)d, (const float*)F(crow),
+                    F(*gW), F(*gb), ws.data_ptr(), (size_t)ws.nbytes(), S());
+      else
+        c2t::launch("c2dsr_ce3b_fused_dw_sk", &c2dsr_ce3b_fused_dw_sk, (const void*)Hb.data_ptr(),
+                    (const void*)Wb.data_ptr(), (const float*)F(bias2), (int)Mv, (int)n, (int)d, (const float*)F(crow),
+                    F(*gW), F(*gb), ws.data_ptr(), (size_t)ws.nbytes(), S());
+    } else if (n_rsplit <= 1 && has(gW) && has(gb)) {
       dw(0, F(*gW), F(*gb));  // one split: the sweep adds onto the gradients itself (no partials / sum)
     } else {
+      n_rsplit = std::max<int64_t>(n_rsplit, 1);
       Tensor dWp = at::empty({n_rsplit, n, d}, f32), dbp = at::empty({n_rsplit, n}, f32);
       dw((int)n_rsplit, F(dWp), F(dbp));
       if (has(gW))

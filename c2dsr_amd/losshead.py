@@ -49,24 +49,50 @@ def split_count(rows, tile, max_split=16, per_cu=1):
     return best
 
 
-def dw_split_count(n, Mv, x3, d=256, max_split=16):
-    """Row splits of the dW sweep (ce3.hip MODE 1: 128 stationary W rows per workgroup; the Mv swept rows in 32-row
-    tiles on split images, 64-row tiles on bf16 ones): the count minimising rounds × (tiles per workgroup + a
-    workgroup's fixed cost) + the partial slabs' combine, in tile-times fitted to split sweeps on the box
+def _dw_costs(n, Mv, x3, d=256, max_split=16):
+    """Fitted cost (in swept-tile times) of the dW sweep (ce3.hip MODE 1: 128 stationary W rows per workgroup; the Mv
+    swept rows in 32-row tiles on split images, 64-row tiles on bf16 ones) for each row-split count s — rounds ×
+    (tiles per workgroup + a workgroup's fixed cost) + the partial slabs' combine — and for the stream-K sweep —
+    (units per workgroup + fixed cost per segment) × a locality factor (its workgroups start at different swept
+    tiles, so they share fewer of them in L2) + its combine.  Fitted to split / stream-K sweeps on the box
     (tools/ce3_micro.py / ce3b_micro.py: a tile 1.87 / 1.47 µs, a workgroup's fixed cost ≈ 16 / 9 tiles, a partial
-    slab of n·d fp32 written and summed ≈ 7.5 µs at 36.8k × 256).  One split accumulates straight into the gradient.
-    (split_count alone picked 15 splits for the Food-Kitchen heads: 543 µs of sweep + sum where 3-4 take 379.)"""
+    slab of n·d fp32 written and summed ≈ 7.5 µs at 36.8k × 256, stream-K locality 1.15 / 1.35)."""
     tiles = max(1, -(-n // 128))
     sweep = max(1, -(-Mv // (32 if x3 else 64)))
-    t_tile, wg = (1.87, 16.0) if x3 else (1.47, 9.0)
+    t_tile, wg, sk_loc = (1.87, 16.0, 1.15) if x3 else (1.47, 9.0, 1.35)
     slab = 7.5 * (n * d) / (36845 * 256) / t_tile
     slots = _ncu()
-    best, best_t = 1, None
+    split = {}
     for s in range(1, max_split + 1):
-        t = -(-tiles * s // slots) * (-(-sweep // s) + wg) + (s * slab if s > 1 else 0.0)
-        if best_t is None or t < best_t - 1e-9:
-            best, best_t = s, t
-    return best
+        split[s] = -(-tiles * s // slots) * (-(-sweep // s) + wg) + (s * slab if s > 1 else 0.0)
+    per = tiles * sweep / slots
+    sk = sk_loc * (per + wg * (1.0 + per / sweep)) + 10.0 / t_tile
+    return split, sk
+
+
+def dw_split_count(n, Mv, x3, d=256, max_split=16):
+    """Row splits of the dW sweep: the count of least fitted cost (_dw_costs), the smaller count on ties.  One split
+    accumulates straight into the gradient.  (split_count alone picked 15 splits for the Food-Kitchen heads: 543 µs
+    of sweep + sum where 3-4 take 379.)"""
+    split, _ = _dw_costs(n, Mv, x3, d, max_split)
+    best = min(split.values())
+    return min(s for s in split if split[s] <= best + 1e-9)
+
+
+DW_SK = True  # the dW sweep as stream-K (c2dsr_ce3*_fused_dw_sk) where its fitted cost is lower
+
+
+def dw_plan(n, Mv, x3, d, both_grads=True):
+    """The dW sweep's split argument: 0 = stream-K (one workgroup per CU over equal ranges of (W row block, swept
+    tile) units; needs both gradients and ce3.hip's kernels) when _dw_costs rates it below the best row-split
+    count — Movie-Book head a (288 row blocks: 1.1 rounds of 256 CUs) 2236 → 1496 µs — else dw_split_count
+    (d = 256: the fitted shapes; other widths keep split_count)."""
+    if d == 256:
+        split, sk = _dw_costs(n, Mv, x3, d)
+        if DW_SK and both_grads and sk < min(split.values()):
+            return 0
+        return dw_split_count(n, Mv, x3, d)
+    return split_count(n, 128)
 
 
 def ce_kind(precision, d):
@@ -381,7 +407,7 @@ class LossHeadFn(Function):
             gW, gb = _grad_target(W), _grad_target(bias)
             hd += T.ce_head_backward(saved, W, inv, tc, Mv0, Mv1, coef, gscale, float(m.lam), gW, gb, gwpad, gbpad,
                                      tplan.get() if tplan is not None else None,
-                                     dw_split_count(n, Mv0 + Mv1, mode == 0, d), mode)
+                                     dw_plan(n, Mv0 + Mv1, mode == 0, d, gW is not None and gb is not None), mode)
         imgT = [weight_img(m.Da_w.view(d, d), kind, trans=True), weight_img(m.Db_w.view(d, d), kind, trans=True)]
         gD = [_grad_target(t) for t in (m.Da_w, m.Da_b, m.Db_w, m.Db_b)]
         sub = [r.idx[:r.n] if r is not None else None for r in rsets]
@@ -437,9 +463,15 @@ class LossHeadFn(Function):
                         lib('c2dsr_ce_fused_dh', Hb, Wb, bias2, Mv, n, d, ns, crow, dHp, s)
                         lib('c2dsr_ce_dh_combine', dHp, ns, Mv, d, t32, rw, W, n, dHc, s)
                         del dHp
-                    nr = dw_split_count(n, Mv, ctx.x3, d) if d == 256 else split_count(n, 128)
                     entry = ce_entry(ctx.x3, d, 'dw')
-                    if nr == 1 and gW is not None and gb is not None and entry.startswith('c2dsr_ce3'):
+                    both = gW is not None and gb is not None and entry.startswith('c2dsr_ce3')
+                    nr = dw_plan(n, Mv, ctx.x3, d, both)
+                    if nr == 0:  # stream-K: whole row blocks added onto the gradients, split ones combined in order
+                        wsb = int(lib.raw('c2dsr_ce3_dw_sk_workspace')(d))
+                        ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+                        lib(entry + '_sk', Hb, Wb, bias2, Mv, n, d, crow, gW, gb, ws, wsb, s)
+                        del ws
+                    elif nr == 1 and both:
                         # one split: the sweep adds onto the gradients itself (n_rsplit = 0; no partials / sum)
                         lib(entry, Hb, Wb, bias2, Mv, n, d, 0, crow, gW, gb, s)
                     else:

@@ -320,6 +320,16 @@ int c2dsr_ce3b_fused_fwd_u(const void* Hb, const void* Wb, const float* bias2, i
                            float* loss_row, void* stream);
 int c2dsr_ce3b_fused_dw(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, int n_rsplit,
                         const float* crow, float* dWp, float* dbp, void* stream);
+/* The dW sweep as stream-K (trainer.py:131-154, the classifier's weight / bias gradients): the (128-row W block,
+ * swept H tile) units are dealt to one workgroup per CU in equal contiguous ranges — one launch round, no partial
+ * last round, one prologue per workgroup segment.  Row blocks swept whole by one workgroup are added straight onto
+ * gW [n][D] / gb [n]; split ones leave partials in ws that a combine pass adds in workgroup order (deterministic).
+ * ws: c2dsr_ce3_dw_sk_workspace(D) bytes.  Operands as c2dsr_ce3_fused_dw (split images) / c2dsr_ce3b_fused_dw. */
+size_t c2dsr_ce3_dw_sk_workspace(int D);
+int c2dsr_ce3_fused_dw_sk(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, const float* crow,
+                          float* gW, float* gb, void* ws, size_t ws_bytes, void* stream);
+int c2dsr_ce3b_fused_dw_sk(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, const float* crow,
+                           float* gW, float* gb, void* ws, size_t ws_bytes, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
 int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */

@@ -58,7 +58,11 @@ def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None, b16=False):
     lib('c2dsr_ce_dh_from_u', Up, pm, ns, M, D, lse2, t32, rw, d(W), n, dH, s)
     gW = torch.zeros(n, D, device=DEV) if g0 is None else g0[0].clone().to(DEV)
     gb = torch.zeros(n, device=DEV) if g0 is None else g0[1].clone().to(DEV)
-    if nr == 0:  # one split added straight onto the gradients
+    if nr == -1:  # stream-K sweep (whole row blocks added directly, split ones combined in workgroup order)
+        wsb = int(lib.raw('c2dsr_ce3_dw_sk_workspace')(D))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+        lib(pre + 'dw_sk', Hx, Wx, bias2, M, n, D, crow, gW, gb, ws, wsb, s)
+    elif nr == 0:  # one split added straight onto the gradients
         lib(pre + 'dw', Hx, Wx, bias2, M, n, D, 0, crow, gW, gb, s)
     else:
         dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
@@ -94,7 +98,8 @@ TOL_LSE, TOL = 1e-5, 5e-5
 
 
 @pytest.mark.parametrize('M,n,D,ns,nr', [(300, 700, 256, 3, 2), (1000, 2100, 128, 4, 3), (64, 65, 256, 1, 1),
-                                         (777, 4099, 256, 7, 5), (33, 31, 256, 2, 3)])
+                                         (777, 4099, 256, 7, 5), (33, 31, 256, 2, 3), (300, 700, 256, 3, -1),
+                                         (1000, 2100, 128, 4, -1), (2500, 40000, 256, 5, -1), (33, 31, 256, 2, -1)])
 def test_ce3_matches_float64(M, n, D, ns, nr):
     g = torch.Generator().manual_seed(M + n + D)
     H = torch.randn(M, D, generator=g) * 0.5
@@ -442,6 +447,14 @@ def _ref_chunked(H, W, b, pl, t, coef, lam, BR, chunk=2048):
     return lse, rows, dH, gW, gb, dpad
 
 
+def _shipped_dw(n, M, x3, D):
+    """The dW sweep the loss head runs at this shape (losshead.dw_plan) in _run's convention: -1 stream-K, 0 one
+    split added onto the gradients, k > 1 row splits summed."""
+    from c2dsr_amd.losshead import dw_plan
+    p = dw_plan(n, M, x3, D)
+    return -1 if p == 0 else (0 if p == 1 else p)
+
+
 def test_ce3_mb_head_b_shape_matches_float64():
     """K5 at the headline's own shape: Movie-Book head b — Mv = 18,944 valid stacked rows,
     n = 63,937 columns, d = 256 — with the split counts losshead.py derives for it (split_count over 128-row /
@@ -450,6 +463,7 @@ def test_ce3_mb_head_b_shape_matches_float64():
     LayerNorm output (unit normal), W / b like the classifier's nn.Linear init (U(±1/√d))."""
     from c2dsr_amd.losshead import split_count
     M, n, D = 18944, 63937, 256
+    nr = _shipped_dw(n, M, True, D)
     g = torch.Generator().manual_seed(2048)
     H = torch.randn(M, D, generator=g)
     W = (torch.rand(n, D, generator=g) * 2 - 1) / 16
@@ -457,7 +471,7 @@ def test_ce3_mb_head_b_shape_matches_float64():
     pl = torch.randn(M, generator=g) * 0.3
     t = torch.randint(0, n, (M,), generator=g)
     coef, lam, BR = torch.tensor([0.45, 1.0]), 0.7, 9100
-    ns, nr = split_count(M, 128), split_count(n, 128)
+    ns = split_count(M, 128)
     lse, rows, dH, gW, gb, dpad, _ = _run(H, W, b, pl, t, coef, lam, ns, nr, BR)
     ref = _ref_chunked(H, W, b, pl, t, coef, lam, BR)
     err = {k: rel(x, r) for k, x, r in zip(('lse', 'rows', 'dH', 'gW', 'gb', 'dpad'), (lse, rows, dH, gW, gb, dpad),
@@ -476,6 +490,7 @@ def test_ce3b_mb_head_b_shape_matches_float64():
     bf16 comparison's 7e-2 is dominated by the bf16 encoder, not K5)."""
     from c2dsr_amd.losshead import split_count
     M, n, D = 18944, 63937, 256
+    nr = _shipped_dw(n, M, False, D)
     g = torch.Generator().manual_seed(4096)
     H = torch.randn(M, D, generator=g).bfloat16().float()
     W = ((torch.rand(n, D, generator=g) * 2 - 1) / 16).bfloat16().float()
@@ -483,7 +498,7 @@ def test_ce3b_mb_head_b_shape_matches_float64():
     pl = torch.randn(M, generator=g) * 0.3
     t = torch.randint(0, n, (M,), generator=g)
     coef, lam, BR = torch.tensor([0.45, 1.0]), 0.7, 9100
-    ns, nr = split_count(M, 128), split_count(n, 128)
+    ns = split_count(M, 128)
     lse, rows, dH, gW, gb, dpad, _ = _run(H, W, b, pl, t, coef, lam, ns, nr, BR, b16=True)
     ref = _ref_chunked(H, W, b, pl, t, coef, lam, BR)
     err = {k: rel(x, r) for k, x, r in zip(('lse', 'rows', 'dH', 'gW', 'gb', 'dpad'), (lse, rows, dH, gW, gb, dpad),

@@ -61,10 +61,18 @@ def main():
     gscale = torch.ones(1, **f32)
     lib('c2dsr_ce_row_weights', tgt, Mv, Mp, n, coef, Mv // 2, gscale, 0.7, padc, lse, rw, t32, lse2, crow, dpad, s)
     nr = int(sys.argv[4]) if len(sys.argv) > 4 and int(sys.argv[4]) else split_count(n, 128)
-    dWp, dbp = torch.empty(nr, n, d, **f32), torch.empty(nr, n, **f32)
-    dw = lambda: lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
+    if nr == -1:  # stream-K (c2dsr_ce3*_fused_dw_sk) onto gradient buffers
+        wsb = int(lib.raw('c2dsr_ce3_dw_sk_workspace')(d))
+        sk_ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+        dWp, dbp = torch.zeros(1, n, d, **f32), torch.zeros(1, n, **f32)
+    else:
+        dWp, dbp = torch.empty(max(nr, 1), n, d, **f32), torch.empty(max(nr, 1), n, **f32)
+    if nr == -1:
+        dw = lambda: lib('c2dsr_ce3_fused_dw_sk', Hx, Wx, bias2, Mv, n, d, crow, dWp[0], dbp[0], sk_ws, wsb, s)  # noqa: E731
+    else:
+        dw = lambda: lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
     t_w = timeit(dw)
-    t_s = timeit(lambda: lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, W, s)) if nr > 1 else 0.0
+    t_s = timeit(lambda: lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, W, s)) if nr > 1 else 0.0  # (stream-K: the combine runs inside dw)
     fl = 2.0 * Mv * n * d
     print(f'ce3 Mv={Mv} n={n}: split {t_split:.1f} us; fwd_u {t_f:.1f} us ({2 * fl / t_f / 1e6:.0f} TFLOP/s credited, '
           f'{6 * fl / t_f / 1e6:.0f} executed, ns {ns}); dw {t_w:.1f} us ({fl / t_w / 1e6:.0f} credited, '
