@@ -298,8 +298,9 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
   if (has(tplan))
     TORCH_CHECK(tplan->scalar_type() == at::kByte && (size_t)tplan->nbytes() >= c2dsr_index_plan_bytes((int)Mv),
                 "c2dsr::ce_head_backward: target plan too small");
-  // n_rsplit 0: the stream-K sweep (c2dsr_ce3_fused_dw_sk; needs both gradients)
-  TORCH_CHECK(n_rsplit >= 0 && n_rsplit <= 64 && (mode == 0 || mode == 1), "c2dsr::ce_head_backward: splits / mode");
+  // n_rsplit 0: the stream-K sweep (c2dsr_ce3_fused_dw_sk); −k: whole rounds unsplit, the remainder k ways (both need
+  // both gradients; losshead.dw_plan)
+  TORCH_CHECK(n_rsplit >= -64 && n_rsplit <= 64 && (mode == 0 || mode == 1), "c2dsr::ce_head_backward: splits / mode");
   on_device(op, {&W, &Hpad, &inv, &tc, &Hc, &padc, &lse_c, &lse2, &Up, &pm, &bias2, &Hb, &Wb, &coef, &gscale});
   on_device(op, {gW, gb, gwpad, gbpad, tplan});
   const auto f32 = W.options();
@@ -314,15 +315,18 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
     c2t::launch("c2dsr_ce_dh_from_u", &c2dsr_ce_dh_from_u, (const float*)F(Up), (const float*)F(pm), (int)ns, (int)Mv,
                 (int)d, (const float*)F(lse2), (const int*)t32.data_ptr<int>(), (const float*)F(rw),
                 (const float*)F(W), (int)n, F(dHc), S());
-    auto dw = [&](int nr, float* dWp, float* dbp) {
+    // the sweep over W rows [off, off + rows) (the stationary operand: image rows, bias2, outputs offset alike)
+    auto dw_rows = [&](int nr, float* dWp, float* dbp, int64_t off, int64_t rows) {
+      const void* wimg = (const void*)((const at::BFloat16*)Wb.data_ptr() + off * (mode == 0 ? 2 : 1) * d);
+      const float* b2 = (const float*)F(bias2) + off;
       if (mode == 0)
-        c2t::launch("c2dsr_ce3_fused_dw", &c2dsr_ce3_fused_dw, (const void*)Hb.data_ptr(), (const void*)Wb.data_ptr(),
-                    (const float*)F(bias2), (int)Mv, (int)n, (int)d, nr, (const float*)F(crow), dWp, dbp, S());
+        c2t::launch("c2dsr_ce3_fused_dw", &c2dsr_ce3_fused_dw, (const void*)Hb.data_ptr(), wimg, b2, (int)Mv,
+                    (int)rows, (int)d, nr, (const float*)F(crow), dWp, dbp, S());
       else
-        c2t::launch("c2dsr_ce3b_fused_dw", &c2dsr_ce3b_fused_dw, (const void*)Hb.data_ptr(),
-                    (const void*)Wb.data_ptr(), (const float*)F(bias2), (int)Mv, (int)n, (int)d, nr,
-                    (const float*)F(crow), dWp, dbp, S());
+        c2t::launch("c2dsr_ce3b_fused_dw", &c2dsr_ce3b_fused_dw, (const void*)Hb.data_ptr(), wimg, b2, (int)Mv,
+                    (int)rows, (int)d, nr, (const float*)F(crow), dWp, dbp, S());
     };
+    auto dw = [&](int nr, float* dWp, float* dbp) { dw_rows(nr, dWp, dbp, 0, n); };
     if (n_rsplit == 0 && has(gW) && has(gb)) {  // stream-K: whole row blocks added directly, split ones combined
       Tensor ws = at::empty({(int64_t)c2dsr_ce3_dw_sk_workspace((int)d)}, f32.dtype(at::kByte));
       if (mode == 0)
@@ -333,6 +337,20 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
         c2t::launch("c2dsr_ce3b_fused_dw_sk", &c2dsr_ce3b_fused_dw_sk, (const void*)Hb.data_ptr(),
                     (const void*)Wb.data_ptr(), (const float*)F(bias2), (int)Mv, (int)n, (int)d, (const float*)F(crow),
                     F(*gW), F(*gb), ws.data_ptr(), (size_t)ws.nbytes(), S());
+    } else if (n_rsplit < 0 && has(gW) && has(gb)) {
+      // whole rounds of unsplit row blocks onto the gradients, then the last partial round's row blocks −n_rsplit ways
+      int dev = 0, ncu = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      const int64_t full = ncu > 0 ? (n + 127) / 128 / ncu * ncu * 128 : 0, rem = n - full, k = -n_rsplit;
+      TORCH_CHECK(full > 0 && rem > 0, "c2dsr::ce_head_backward: a remainder split needs whole rounds and a remainder");
+      dw_rows(0, F(*gW), F(*gb), 0, full);
+      Tensor dWp = at::empty({k, rem, d}, f32), dbp = at::empty({k, rem}, f32);
+      dw_rows((int)k, F(dWp), F(dbp), full, rem);
+      c2t::launch("c2dsr_sum_parts", &c2dsr_sum_parts, (const float*)F(dWp), (int)k, (long)(rem * d), 1.f,
+                  F(*gW) + full * d, S());
+      c2t::launch("c2dsr_sum_parts", &c2dsr_sum_parts, (const float*)F(dbp), (int)k, (long)rem, 1.f, F(*gb) + full,
+                  S());
     } else if (n_rsplit <= 1 && has(gW) && has(gb)) {
       dw(0, F(*gW), F(*gb));  // one split: the sweep adds onto the gradients itself (no partials / sum)
     } else {

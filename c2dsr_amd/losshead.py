@@ -83,16 +83,37 @@ DW_SK = True  # the dW sweep as stream-K (c2dsr_ce3*_fused_dw_sk) where its fitt
 
 
 def dw_plan(n, Mv, x3, d, both_grads=True):
-    """The dW sweep's split argument: 0 = stream-K (one workgroup per CU over equal ranges of (W row block, swept
-    tile) units; needs both gradients and ce3.hip's kernels) when _dw_costs rates it below the best row-split
-    count — Movie-Book head a (288 row blocks: 1.1 rounds of 256 CUs) 2236 → 1496 µs — else dw_split_count
-    (d = 256: the fitted shapes; other widths keep split_count)."""
-    if d == 256:
-        split, sk = _dw_costs(n, Mv, x3, d)
-        if DW_SK and both_grads and sk < min(split.values()):
-            return 0
-        return dw_split_count(n, Mv, x3, d)
-    return split_count(n, 128)
+    """The dW sweep's plan as the loss head's split argument (ce_head_backward's n_rsplit), the least fitted cost of
+      k ≥ 1  row splits (dw_split_count; k = 1: one split added onto the gradients),
+      0      stream-K (one workgroup per CU over equal ranges of (W row block, swept tile) units),
+      −k     whole rounds of unsplit row blocks, then the last partial round's row blocks in k splits: the first
+             ⌊blocks / CUs⌋·CUs row blocks added onto the gradients by one launch, the rest split k ways by a second —
+             Movie-Book head a (288 row blocks on 256 CUs) and the Food-Kitchen heads (273) have a 32- / 17-block
+             remainder that one undivided round would leave 7/8 of the chip idle for.
+    Stream-K and the remainder split need both gradients and ce3.hip's kernels (d = 256: the fitted shapes; other
+    widths keep split_count)."""
+    if d != 256:
+        return split_count(n, 128)
+    split, sk = _dw_costs(n, Mv, x3, d)
+    best_k = dw_split_count(n, Mv, x3, d)
+    plan, cost = best_k, split[best_k]
+    if not (DW_SK and both_grads):
+        return plan
+    if sk < cost:
+        plan, cost = 0, sk
+    slots = _ncu()
+    blocks = -(-n // 128)
+    full = blocks // slots * slots
+    if full and full < blocks:
+        rem = n - full * 128
+        rsplit, _ = _dw_costs(rem, Mv, x3, d)
+        k = dw_split_count(rem, Mv, x3, d)
+        sweep = max(1, -(-Mv // (32 if x3 else 64)))
+        t_wg = 16.0 if x3 else 9.0
+        hyb = full // slots * (sweep + t_wg) + rsplit[k]
+        if k > 1 and hyb < cost:
+            plan, cost = -k, hyb
+    return plan
 
 
 def ce_kind(precision, d):
@@ -471,6 +492,17 @@ class LossHeadFn(Function):
                         ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
                         lib(entry + '_sk', Hb, Wb, bias2, Mv, n, d, crow, gW, gb, ws, wsb, s)
                         del ws
+                    elif nr < 0:  # whole rounds unsplit onto the gradients, the remainder row blocks −nr ways
+                        full = -(-n // 128) // _ncu() * _ncu() * 128
+                        rem, k = n - full, -nr
+                        ic = (2 if ctx.x3 else 1) * d
+                        lib(entry, Hb, Wb, bias2, Mv, full, d, 0, crow, gW, gb, s)
+                        dWp = torch.empty(k, rem, d, **f32)
+                        dbp = torch.empty(k, rem, **f32)
+                        lib(entry, Hb, Wb.view(-1)[full * ic:], bias2[full:], Mv, rem, d, k, crow, dWp, dbp, s)
+                        lib('c2dsr_sum_parts', dWp, k, rem * d, 1.0, gW.view(-1)[full * d:], s)
+                        lib('c2dsr_sum_parts', dbp, k, rem, 1.0, gb[full:], s)
+                        del dWp, dbp
                     elif nr == 1 and both:
                         # one split: the sweep adds onto the gradients itself (n_rsplit = 0; no partials / sum)
                         lib(entry, Hb, Wb, bias2, Mv, n, d, 0, crow, gW, gb, s)

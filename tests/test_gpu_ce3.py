@@ -58,7 +58,17 @@ def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None, b16=False):
     lib('c2dsr_ce_dh_from_u', Up, pm, ns, M, D, lse2, t32, rw, d(W), n, dH, s)
     gW = torch.zeros(n, D, device=DEV) if g0 is None else g0[0].clone().to(DEV)
     gb = torch.zeros(n, device=DEV) if g0 is None else g0[1].clone().to(DEV)
-    if nr == -1:  # stream-K sweep (whole row blocks added directly, split ones combined in workgroup order)
+    if nr <= -2:  # whole rounds of row blocks added directly, the remainder's row blocks split -nr ways and summed
+        from c2dsr_amd.losshead import _ncu
+        full = -(-n // 128) // _ncu() * _ncu() * 128
+        rem, k = n - full, -nr
+        ic = Wx.shape[1]
+        lib(pre + 'dw', Hx, Wx, bias2, M, full, D, 0, crow, gW, gb, s)
+        dWp, dbp = torch.empty(k, rem, D, device=DEV), torch.empty(k, rem, device=DEV)
+        lib(pre + 'dw', Hx, Wx.view(-1)[full * ic:], bias2[full:], M, rem, D, k, crow, dWp, dbp, s)
+        lib('c2dsr_sum_parts', dWp, k, rem * D, 1.0, gW.view(-1)[full * D:], s)
+        lib('c2dsr_sum_parts', dbp, k, rem, 1.0, gb[full:], s)
+    elif nr == -1:  # stream-K sweep (whole row blocks added directly, split ones combined in workgroup order)
         wsb = int(lib.raw('c2dsr_ce3_dw_sk_workspace')(D))
         ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
         lib(pre + 'dw_sk', Hx, Wx, bias2, M, n, D, crow, gW, gb, ws, wsb, s)
@@ -99,7 +109,8 @@ TOL_LSE, TOL = 1e-5, 5e-5
 
 @pytest.mark.parametrize('M,n,D,ns,nr', [(300, 700, 256, 3, 2), (1000, 2100, 128, 4, 3), (64, 65, 256, 1, 1),
                                          (777, 4099, 256, 7, 5), (33, 31, 256, 2, 3), (300, 700, 256, 3, -1),
-                                         (1000, 2100, 128, 4, -1), (2500, 40000, 256, 5, -1), (33, 31, 256, 2, -1)])
+                                         (1000, 2100, 128, 4, -1), (2500, 40000, 256, 5, -1), (33, 31, 256, 2, -1),
+                                         (700, 36845, 256, 3, -8)])
 def test_ce3_matches_float64(M, n, D, ns, nr):
     g = torch.Generator().manual_seed(M + n + D)
     H = torch.randn(M, D, generator=g) * 0.5
@@ -452,7 +463,7 @@ def _shipped_dw(n, M, x3, D):
     split added onto the gradients, k > 1 row splits summed."""
     from c2dsr_amd.losshead import dw_plan
     p = dw_plan(n, M, x3, D)
-    return -1 if p == 0 else (0 if p == 1 else p)
+    return -1 if p == 0 else (0 if p == 1 else p)  # (p < 0: the remainder split, the same convention)
 
 
 def test_ce3_mb_head_b_shape_matches_float64():
