@@ -744,6 +744,8 @@ __global__ __launch_bounds__(256) void attn_fwd_wave(const float* __restrict__ q
                                                      int64_t pad, int B, int L, int d, int H, c2::Drop drop,
                                                      int64_t b_base, float* __restrict__ out,
                                                      float* __restrict__ Psave) {
+  // (the wave index stays a vector value here: as a scalar the full-layout kernels measured slower — fwd 117 → 127 µs,
+  // bwd 238 → 335 µs at the bench shape — while attn_fwd_rows gains)
   const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bh >= B * H) return;  // uniform over the wave
   const int b = bh / H, h = bh % H, dh = d / H;
@@ -805,7 +807,9 @@ __global__ __launch_bounds__(256, ATTN_ROWS_OCC_F) void attn_fwd_rows(const floa
                                                      const int* __restrict__ k_idx, const int* __restrict__ k_off,
                                                      int B, int L, int d, int H, c2::Drop drop, int64_t b_base,
                                                      float* __restrict__ out, float* __restrict__ Psave) {
-  const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // the wave index as a scalar: everything derived from it (sequence, row ranges, buffer descriptors) stays uniform,
+  // so each buffer load takes its descriptor from SGPRs instead of a readfirstlane waterfall loop
+  const int bh = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (bh >= B * H) return;  // uniform over the wave
   const int b = bh / H, h = bh % H, dh = d / H;
   int q0, nq, k0, nk;
@@ -1043,7 +1047,7 @@ __global__ __launch_bounds__(256) void attn_bwd_wave(const float* __restrict__ q
                                                      int64_t b_base, const float* __restrict__ Psave,
                                                      const float* __restrict__ dout, OT* __restrict__ dqkv) {
   __shared__ float tbuf[4][64 * 65];
-  const int w = threadIdx.x >> 6;
+  const int w = threadIdx.x >> 6;  // (vector, as in attn_fwd_wave)
   const int bh = blockIdx.x * 4 + w;
   if (bh >= B * H) return;  // uniform over the wave (no block-level barriers below)
   const int b = bh / H, h = bh % H, dh = d / H;
@@ -1077,6 +1081,9 @@ __global__ __launch_bounds__(256, ATTN_ROWS_OCC) void attn_bwd_rows(const float*
                                                      const float* __restrict__ Psave, const float* __restrict__ dout,
                                                      OT* __restrict__ dq, OT* __restrict__ dkv) {
   __shared__ float tbuf[4][64 * 65];
+  // (a vector wave index here: as a scalar — no descriptor waterfall loops — this kernel measured faster on one-tile
+  // sequences, 129 → 109 µs in tools/attn_micro.py, but slower in the step, 148 → 218 µs, whose a / b passes have many
+  // two-key-tile sequences; scalar descriptor bases alone, the same: micro 109 µs, step −2 %)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int bh = blockIdx.x * 4 + w;
   if (bh >= B * H) return;  // uniform over the wave (no block-level barriers below)
