@@ -13,6 +13,8 @@
 // modes bit-identical here while staying far off the critical path.
 #include "common.h"
 
+#include <type_traits>
+
 typedef __bf16 bf16;
 
 #define WMFMA(a, b, c, x, y, z) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), (x), (y), (z))
@@ -1081,10 +1083,11 @@ __global__ __launch_bounds__(256, ATTN_ROWS_OCC) void attn_bwd_rows(const float*
                                                      const float* __restrict__ Psave, const float* __restrict__ dout,
                                                      OT* __restrict__ dq, OT* __restrict__ dkv) {
   __shared__ float tbuf[4][64 * 65];
-  // (a vector wave index here: as a scalar — no descriptor waterfall loops — this kernel measured faster on one-tile
-  // sequences, 129 → 109 µs in tools/attn_micro.py, but slower in the step, 148 → 218 µs, whose a / b passes have many
-  // two-key-tile sequences; scalar descriptor bases alone, the same: micro 109 µs, step −2 %)
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // The wave index as a scalar (uniform descriptors, no waterfall loops, as attn_fwd_rows) for the bf16-output
+  // instantiation only: 130 → 109 µs (tools/attn_micro.py); the fp32-output one (the fp32 mode) measured slower that
+  // way, 138 → 191 µs (and 148 → 218 µs in the step), with or without its two-tile path split out as a call.
+  const int w = std::is_same_v<OT, float> ? (int)(threadIdx.x >> 6) : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
   const int bh = blockIdx.x * 4 + w;
   if (bh >= B * H) return;  // uniform over the wave (no block-level barriers below)
   const int b = bh / H, h = bh % H, dh = d / H;

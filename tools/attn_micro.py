@@ -67,9 +67,38 @@ def main():
                      dq, dkv, 1, s)
     tfr = timeit(fr)
     tbr = timeit(gr)
+    # the fp32 mode's backward (fp32 dq / dkv: attn_bwd_rows<float>)
+    dq32 = torch.empty(nq, d, device=dev)
+    dkv32 = torch.empty(nk, 2 * d, device=dev)
+    gr32 = lambda: lib('c2dsr_attn_bwd_rows', q, kv, sd, pad, qi, qo, ki, ko, B, L, d, H, 1, 2, pdrop, 0, P, do_r,  # noqa
+                       dq32, dkv32, 0, s)
+    tbr32 = timeit(gr32)
     print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: attn fwd {tf:.1f} us, bwd {tb:.1f} us; '
-          f'rows (nq {nq / B:.1f}, nk {nk / B:.1f} per seq) fwd {tfr:.1f} us, bwd {tbr:.1f} us; '
-          f'checksum {float(o_r.double().sum()):.6e} {float(dkv.double().sum()):.6e}', flush=True)
+          f'rows (nq {nq / B:.1f}, nk {nk / B:.1f} per seq) fwd {tfr:.1f} us, bwd {tbr:.1f} us (bf16 out) '
+          f'{tbr32:.1f} us (fp32 out); checksum {float(o_r.double().sum()):.6e} {float(dkv.double().sum()):.6e}',
+          flush=True)
+    # a domain pass's shape (the a / b sequences: most positions are the other domain's, i.e. padding keys)
+    lens2 = rng.integers(2, 26, size=B)
+    seq2 = np.full((B, L), pad, dtype=np.int64)
+    for b in range(B):
+        pos2 = np.sort(rng.choice(L, size=lens2[b], replace=False))
+        seq2[b, pos2] = rng.integers(0, pad, size=lens2[b])
+    sd2 = torch.from_numpy(seq2).to(dev)
+    need2 = (rng.random((B, L)) < 0.2) | (seq2 != pad)
+    need2[:, -10:] = True
+    qi2, qo2, nq2 = rowset(need2 & (rng.random((B, L)) < 0.55))
+    ki2, ko2, nk2 = rowset(seq2 == pad)
+    q2 = torch.randn(nq2, d, device=dev)
+    kv2 = torch.randn(nk2, 2 * d, device=dev)
+    o2 = torch.empty(nq2, d, device=dev)
+    do2 = torch.randn(nq2, d, device=dev)
+    dq2 = torch.empty(nq2, d, device=dev)
+    dkv2 = torch.empty(nk2, 2 * d, device=dev)
+    f2 = lambda: lib('c2dsr_attn_fwd_rows', q2, kv2, sd2, pad, qi2, qo2, ki2, ko2, B, L, d, H, 1, 2, pdrop, 0, o2, P, s)  # noqa
+    g2 = lambda: lib('c2dsr_attn_bwd_rows', q2, kv2, sd2, pad, qi2, qo2, ki2, ko2, B, L, d, H, 1, 2, pdrop, 0, P, do2,  # noqa
+                     dq2, dkv2, 0, s)
+    print(f'  domain-pass shape (nq {nq2 / B:.1f}, nk {nk2 / B:.1f} per seq): fwd {timeit(f2):.1f} us, '
+          f'bwd {timeit(g2):.1f} us (fp32 out)', flush=True)
 
 
 if __name__ == '__main__':
