@@ -246,7 +246,7 @@ def k5_traffic(precision):
         return None, None, None
     with open(path) as f:
         t = json.load(f)
-    return t.get('bytes_per_launch_triple'), t.get('source'), t.get('mfma_busy')
+    return t.get('bytes_per_head', t.get('bytes_per_launch_triple')), t.get('source'), t.get('mfma_busy')
 
 
 def hbm_traffic(precision):

@@ -47,13 +47,16 @@ if prec == 'c5':
 fe = per_kernel(f'{pre}_fetch/run_counter_collection.csv', 'FETCH_SIZE')
 wr = per_kernel(f'{pre}_write/run_counter_collection.csv', 'WRITE_SIZE')
 rows = {}
+# per HEAD: a head's dW sweep can take two launches (whole rounds + the split remainder, losshead.dw_plan), so every
+# kernel's bytes are divided by the number of heads profiled (= the fwd_u sweep launches), not by its own launches
+heads = max(1, len(fe[K5[0]])) if K5 else 1
 for k in K5:
-    f = 2 * sum(fe[k]) / max(1, len(fe[k]))
-    w = sum(wr[k]) / max(1, len(wr[k]))
+    f = 2 * sum(fe[k]) / heads
+    w = sum(wr[k]) / heads
     rows[k] = dict(launches=len(fe[k]), fetch_bytes=round(f), write_bytes=round(w), bytes=round(f + w))
-    print(f'{k:16} launches {len(fe[k]):3d}  fetch {f / 1e6:9.1f} MB  write {w / 1e6:8.1f} MB')
+    print(f'{k:16} launches {len(fe[k]):3d}  per head: fetch {f / 1e6:9.1f} MB  write {w / 1e6:8.1f} MB')
 tot = sum(r['bytes'] for r in rows.values())
-print(f'K5 per head (fwd_u + rows + dw launches): {tot / 1e6:.1f} MB')
+print(f'K5 per head (fwd_u + rows + dw launches, {heads} heads): {tot / 1e6:.1f} MB')
 # MFMA-busy fraction of the K5 kernels from the SQ pass (SQ_VALU_MFMA_BUSY_CYCLES over the 1024 SIMDs'
 # cycles, GRBM_GUI_ACTIVE summed over the 8 XCDs), summed over their launches
 mfma_busy = None
@@ -74,7 +77,7 @@ except FileNotFoundError:
 rev = subprocess.run(['git', 'rev-parse', '--short', 'HEAD'], capture_output=True, text=True).stdout.strip()
 if out and prec != 'c5':
     rev = subprocess.run(['git', 'rev-parse', '--short', 'HEAD'], capture_output=True, text=True).stdout.strip()
-    json.dump(dict(bytes_per_launch_triple=tot, per_kernel=rows, mfma_busy=mfma_busy,
+    json.dump(dict(bytes_per_head=tot, bytes_per_launch_triple=tot, per_kernel=rows, mfma_busy=mfma_busy,
                    source=f'rocprofv3 --pmc FETCH_SIZE (x2) / WRITE_SIZE passes, {pre.split("/")[-1]}, rev {rev}'),
               open(out, 'w'), indent=1)
 
