@@ -81,9 +81,11 @@ class KernelTimer:
     logits tile the dW kernel recomputes is overhead and not credited.  fp32 mode: the split-bf16 pair
     c2dsr_ce3_fused_fwd_u / _dw."""
 
-    NAMES_BF16 = ('c2dsr_ce3b_fused_fwd_u', 'c2dsr_ce3b_fused_dw', 'c2dsr_ce_fused_fwd_u', 'c2dsr_ce_fused_fwd',
-                  'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
-    NAMES_X3 = ('c2dsr_ce3_fused_fwd_u', 'c2dsr_ce3_fused_dw')
+    NAMES_BF16 = ('c2dsr_ce3b_fused_fwd_u', 'c2dsr_ce3b_fused_dw', 'c2dsr_ce3b_fused_dw_sk', 'c2dsr_ce_fused_fwd_u',
+                  'c2dsr_ce_fused_fwd', 'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
+    # (the dW sweep's forms, losshead.dw_plan: row splits, whole rounds + a split remainder — two launches of _dw —,
+    # or stream-K, _dw_sk, whose launch includes its partial combine)
+    NAMES_X3 = ('c2dsr_ce3_fused_fwd_u', 'c2dsr_ce3_fused_dw', 'c2dsr_ce3_fused_dw_sk')
     # credited products per launch: fwd_u = the lse logits + the softmax·W part of dH (online, one sweep)
     CREDIT = {'c2dsr_ce_fused_fwd_u': 2, 'c2dsr_ce3_fused_fwd_u': 2, 'c2dsr_ce3b_fused_fwd_u': 2}
 
