@@ -411,6 +411,59 @@ __global__ void rec_gather_kernel(const float* __restrict__ hs, const int* __res
   Hpad[(BR + r) * d + c] = x;
 }
 
+// The classifier head's operand rows in one pass: Hpad = [hs_r ; hx_r] over the 2BR stacked rows and, for the Mv valid
+// rows (idx: compact → stacked row), Hc = Hcat[idx] (Hcat = [hs_r ; hs_r + hx_r]) and its MFMA image — split
+// hi ‖ lo [M_pad][2d] (split) or bf16 [M_pad][d], rows Mv..M_pad zero.  The values of rec_gather → gather_rows →
+// split_bf16 / to_bf16 (same additions, same RNE conversions) without the [2BR, d] Hcat round trip.  4 columns per
+// thread: threads [0, BR·d/4) write Hpad, the rest the M_pad compact rows.
+__global__ void rec_gather_c_kernel(const float* __restrict__ hs, const int* __restrict__ hs_map,
+                                    const float* __restrict__ hx, const int* __restrict__ hx_map, int B, int L, int d,
+                                    int R, const int* __restrict__ idx, int Mv, int M_pad, int split,
+                                    float* __restrict__ Hpad, float* __restrict__ Hc, c2::tbf16* __restrict__ img) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int d4 = d >> 2;
+  const long BR = (long)B * R;
+  auto rows = [&](long r, float4& a, float4& x, int c) {  // the (b, L-R+k) rows of hs and hx for stacked row r < BR
+    const long b = r / R, l = L - R + r % R, bl = b * L + l;
+    a = *(const float4*)(hs + (hs_map ? hs_map[bl] : bl) * d + c);
+    x = *(const float4*)(hx + (hx_map ? hx_map[bl] : bl) * d + c);
+  };
+  if (i < BR * d4) {
+    const long r = i / d4;
+    const int c = 4 * (int)(i % d4);
+    float4 a, x;
+    rows(r, a, x, c);
+    *(float4*)(Hpad + r * d + c) = a;
+    *(float4*)(Hpad + (BR + r) * d + c) = x;
+    return;
+  }
+  const long j = i - BR * d4;
+  if (j >= (long)M_pad * d4) return;
+  const long m = j / d4;
+  const int c = 4 * (int)(j % d4);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (m < Mv) {
+    const long rr = idx[m];
+    float4 a, x;
+    rows(rr % BR, a, x, c);
+    v = rr < BR ? a : make_float4(a.x + x.x, a.y + x.y, a.z + x.z, a.w + x.w);
+    *(float4*)(Hc + m * d + c) = v;
+  }
+  c2::tbf16 h[4] = {(c2::tbf16)v.x, (c2::tbf16)v.y, (c2::tbf16)v.z, (c2::tbf16)v.w};
+  if (split) {
+    c2::tbf16 lo[4] = {(c2::tbf16)(v.x - (float)h[0]), (c2::tbf16)(v.y - (float)h[1]), (c2::tbf16)(v.z - (float)h[2]),
+                       (c2::tbf16)(v.w - (float)h[3])};
+    c2::tbf16* o = img + m * 2 * d + c;
+    for (int k = 0; k < 4; ++k) {
+      o[k] = h[k];
+      o[d + k] = lo[k];
+    }
+  } else {
+    c2::tbf16* o = img + m * d + c;
+    for (int k = 0; k < 4; ++k) o[k] = h[k];
+  }
+}
+
 __global__ void rec_targets_kernel(const int64_t* __restrict__ ts, const int64_t* __restrict__ tx, int B, int L, int R,
                                    int64_t* __restrict__ tcat) {
   const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -699,6 +752,17 @@ C2_API int c2dsr_rec_gather(const float* hs, const int* hs_map, const float* hx,
   if (n == 0) return 0;
   rec_gather_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(hs, hs_map, hx, hx_map, B, L, d, R, Hcat,
                                                                            Hpad);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_rec_gather_compact(const float* hs, const int* hs_map, const float* hx, const int* hx_map, int B, int L,
+                                     int d, int R, const int* idx, int Mv, int M_pad, int split, float* Hpad, float* Hc,
+                                     void* img, void* stream) {
+  if (d % 4 || Mv < 0 || M_pad < Mv || (Mv && (!idx || !Hc)) || !img) return (int)hipErrorInvalidValue;
+  const long n = ((long)B * R + M_pad) * (d / 4);
+  if (n == 0) return 0;
+  rec_gather_c_kernel<<<c2::ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(hs, hs_map, hx, hx_map, B, L, d, R, idx, Mv,
+                                                                             M_pad, split, Hpad, Hc, (c2::tbf16*)img);
   C2_CHECK_LAUNCH();
   return 0;
 }

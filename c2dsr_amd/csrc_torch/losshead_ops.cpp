@@ -167,34 +167,24 @@ std::vector<Tensor> ce_head_forward(const Tensor& hs, const OptT& hs_map, const 
   on_device(op, {&hs, &hd, &W, &bias, &wpad, &bpad, &idx, &inv, &tc});
   on_device(op, {hs_map, hd_map});
   const auto f32 = W.options();
-  Tensor Hcat = at::empty({M2, d}, f32), Hpad = at::empty({M2, d}, f32);
-  c2t::launch("c2dsr_rec_gather", &c2dsr_rec_gather, (const float*)F(hs), IO(hs_map), (const float*)F(hd), IO(hd_map),
-              (int)B, (int)L, (int)d, (int)R, F(Hcat), F(Hpad), S());
   const int64_t M_pad = std::max<int64_t>(64, ceil_to(Mv, 64)), n_pad = ceil_to(n, 128) + 64;
-  Tensor Hc = at::empty({Mv, d}, f32);
-  if (Mv)
-    c2t::launch("c2dsr_gather_rows", &c2dsr_gather_rows, (const float*)F(Hcat), (long)d, idx.data_ptr<int>(), (int)Mv,
-                (int)d, F(Hc), S());
-  Hcat.reset();
-  Tensor Hb, Wb;
   const auto b16 = f32.dtype(at::kBFloat16);
+  // Hpad, the valid rows Hc and their MFMA image (hi ‖ lo for the fp32 mode's split products, bf16 otherwise; zero
+  // rows past Mv: whole tiles) in one pass over the gathered rows
+  Tensor Hpad = at::empty({M2, d}, f32), Hc = at::empty({Mv, d}, f32);
+  Tensor Hb = at::empty({M_pad, (mode == 0 ? 2 : 1) * d}, b16), Wb;
+  c2t::launch("c2dsr_rec_gather_compact", &c2dsr_rec_gather_compact, (const float*)F(hs), IO(hs_map),
+              (const float*)F(hd), IO(hd_map), (int)B, (int)L, (int)d, (int)R, (const int*)idx.data_ptr<int>(), (int)Mv,
+              (int)M_pad, (int)(mode == 0), F(Hpad), Mv ? F(Hc) : nullptr, (void*)Hb.data_ptr(), S());
   if (mode == 0) {  // hi ‖ lo images, zero rows past the end (whole 32-row tiles)
-    Hb = at::empty({M_pad, 2 * d}, b16);
-    c2t::launch("c2dsr_f32_split_bf16", &c2dsr_f32_split_bf16, (const float*)F(Hc), (long)Mv, (int)d, (long)M_pad,
-                (void*)Hb.data_ptr(), S());
     const int64_t n32 = ceil_to(n, 32);
     Wb = at::empty({n32, 2 * d}, b16);
     c2t::launch("c2dsr_f32_split_bf16", &c2dsr_f32_split_bf16, (const float*)F(W), (long)n, (int)d, (long)n32,
                 (void*)Wb.data_ptr(), S());
   } else {  // whole 64-row tiles, zero rows past the end
-    Hb = at::empty({M_pad, d}, b16);
-    if (M_pad > Mv) Hb.narrow(0, Mv, M_pad - Mv).zero_();
     const int64_t n64 = ceil_to(n, 64);
     Wb = at::empty({n64, d}, b16);
     if (n64 > n) Wb.narrow(0, n, n64 - n).zero_();
-    if (Mv)
-      c2t::launch("c2dsr_f32_to_bf16", &c2dsr_f32_to_bf16, (const float*)F(Hc), (long)Hc.numel(), (void*)Hb.data_ptr(),
-                  S());
     c2t::launch("c2dsr_f32_to_bf16", &c2dsr_f32_to_bf16, (const float*)F(W), (long)W.numel(), (void*)Wb.data_ptr(), S());
   }
   Tensor bias2 = at::empty({n_pad}, f32);

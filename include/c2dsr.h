@@ -217,6 +217,12 @@ int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int 
 int c2dsr_mi_loss(const float* s, int B, int B_norm, float* loss_mi, float* ds, void* stream);
 int c2dsr_rec_gather(const float* hs, const int* hs_map, const float* hx, const int* hx_map, int B, int L, int d,
                      int R, float* Hcat, float* Hpad, void* stream);
+/* The head's operand rows in one pass (trainer.py:122-131): Hpad as c2dsr_rec_gather, and for the Mv valid rows
+ * (idx: compact → stacked row of [hs_r ; hs_r + hx_r]) Hc [Mv][d] and its MFMA image img — split hi ‖ lo [M_pad][2d]
+ * (split = 1, as c2dsr_f32_split_bf16) or bf16 [M_pad][d] — rows Mv..M_pad zero.  d % 4 == 0. */
+int c2dsr_rec_gather_compact(const float* hs, const int* hs_map, const float* hx, const int* hx_map, int B, int L,
+                             int d, int R, const int* idx, int Mv, int M_pad, int split, float* Hpad, float* Hc,
+                             void* img, void* stream);
 int c2dsr_rec_targets(const int64_t* ts, const int64_t* tx, int B, int L, int R, int64_t* tcat, void* stream);
 /* dhs[b,l] += dHcat[r] + dHcat[BR+r] + pad[r·pad_ld]·wpad;  dhx[b,l] += dHcat[BR+r] + pad[(BR+r)·pad_ld]·wpad
  * for the last R positions (r = b·R + l - (L-R)); pad = the pad column of the stacked dlogits (classifier_pad,
