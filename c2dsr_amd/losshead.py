@@ -49,6 +49,29 @@ def split_count(rows, tile, max_split=16, per_cu=1):
     return best
 
 
+FWD_PLAN = True  # the fp32 mode's forward split count from fwd_split_count's fitted cost (else split_count)
+
+
+def fwd_split_count(Mv, n, x3, d=256, max_split=16):
+    """Column splits of the forward sweep (ce3.hip MODE 0: 128 stationary H rows per workgroup, the n columns in
+    32-row tiles split s ways), fp32 mode at d = 256: the least fitted cost rounds × (tiles per workgroup + a
+    workgroup's fixed cost ≈ 4 tiles) + the U slabs' combine (c2dsr_ce_dh_from_u reads s slabs of Mv·d fp32, ≈ 2.1
+    tile-times each at Mv = 18,944), the smaller count on ties.  Fitted to fwd sweeps on the box (tools/ce3_micro.py,
+    s = 3 … 16): Movie-Book head a (n = 36,845) 5 splits — 1614 µs against 1626 at 12, with 7 fewer 19 MB slabs to
+    write and combine —, head b (63,937) 12.  Other modes / widths: split_count (whole rounds)."""
+    if not (FWD_PLAN and x3 and d == 256):
+        return split_count(Mv, 128, max_split)
+    blocks = max(1, -(-Mv // 128))
+    tiles = max(1, -(-n // 32))
+    slots = _ncu()
+    best, best_c = 1, None
+    for s in range(1, max_split + 1):
+        c = -(-blocks * s // slots) * (-(-tiles // s) + 4.0) + 2.1 * s * Mv / 18944
+        if best_c is None or c < best_c - 1e-9:
+            best, best_c = s, c
+    return best
+
+
 def _dw_costs(n, Mv, x3, d=256, max_split=16):
     """Fitted cost (in swept-tile times) of the dW sweep (ce3.hip MODE 1: 128 stationary W rows per workgroup; the Mv
     swept rows in 32-row tiles on split images, 64-row tiles on bf16 ones) for each row-split count s — rounds ×
@@ -307,7 +330,7 @@ class LossHeadFn(Function):
                 if Mv and (x3 or any(ctx.needs_input_grad[:5])):
                     # forward + the softmax part of the input gradient in one sweep (online lse, flash
                     # style): the backward runs no dH sweep
-                    ns = split_count(Mv, 128)
+                    ns = fwd_split_count(Mv, n, x3, d)
                     pm = torch.empty(ns, Mv, **f32)
                     ps = torch.empty(ns, Mv, **f32)
                     Up = torch.empty(ns, Mv, d, **f32)
@@ -389,7 +412,7 @@ class LossHeadFn(Function):
             Mv0, Mv1 = int(hc[slot]), int(hc[slot + 1])
             Mv = Mv0 + Mv1
             out = T.ce_head_forward(hs[0], mp[0], hdom, mp[1 + k], B, L, R, W, bias, m.wpad, m.bpad, idx, inv, tc,
-                                    Mv0, Mv1, split_count(Mv, 128), mode)
+                                    Mv0, Mv1, fwd_split_count(Mv, n, mode == 0, d), mode)
             if k == 0:
                 m.run_after_first_ce()
             # target sort for the one-hot part of dW/db, on the side stream under the rest of the step

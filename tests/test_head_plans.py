@@ -51,3 +51,15 @@ def test_fwd_split_count_whole_rounds():
     # 148 row blocks (MB head, Mv = 18,944): 12 splits = 1776 workgroups, 6.94 rounds of 256
     assert L.split_count(18944, 128) == 12
     assert L.split_count(64, 128) >= 1
+
+
+def test_fwd_split_count_fitted():
+    # fp32 mode at the MB heads (Mv = 18,944): head a 5 splits (fewer U slabs at equal sweep time), head b 12
+    assert L.fwd_split_count(18944, 36845, True) == 5
+    assert L.fwd_split_count(18944, 63937, True) == 12
+    # the bf16 mode and other widths keep split_count
+    assert L.fwd_split_count(18944, 36845, False) == L.split_count(18944, 128)
+    assert L.fwd_split_count(18944, 36845, True, d=128) == L.split_count(18944, 128)
+    for Mv in (1, 64, 9472, 40960):
+        for n in (31, 36845, 63937):
+            assert 1 <= L.fwd_split_count(Mv, n, True) <= 16
