@@ -49,24 +49,27 @@ def split_count(rows, tile, max_split=16, per_cu=1):
     return best
 
 
-FWD_PLAN = True  # the fp32 mode's forward split count from fwd_split_count's fitted cost (else split_count)
+FWD_PLAN = True  # the forward split count from fwd_split_count's fitted cost (else split_count's whole-round fill)
 
 
 def fwd_split_count(Mv, n, x3, d=256, max_split=16):
     """Column splits of the forward sweep (ce3.hip MODE 0: 128 stationary H rows per workgroup, the n columns in
-    32-row tiles split s ways), fp32 mode at d = 256: the least fitted cost rounds × (tiles per workgroup + a
-    workgroup's fixed cost ≈ 4 tiles) + the U slabs' combine (c2dsr_ce_dh_from_u reads s slabs of Mv·d fp32, ≈ 2.1
-    tile-times each at Mv = 18,944), the smaller count on ties.  Fitted to fwd sweeps on the box (tools/ce3_micro.py,
-    s = 3 … 16): Movie-Book head a (n = 36,845) 5 splits — 1614 µs against 1626 at 12, with 7 fewer 19 MB slabs to
-    write and combine —, head b (63,937) 12.  Other modes / widths: split_count (whole rounds)."""
-    if not (FWD_PLAN and x3 and d == 256):
+    32-row tiles on split images, 64-row tiles on bf16 ones, split s ways) at d = 256: the least fitted cost
+    rounds × (tiles per workgroup + a workgroup's fixed cost) + the U slabs' combine (c2dsr_ce_dh_from_u reads s slabs
+    of Mv·d fp32), the smaller count on ties.  Fitted to fwd sweeps on the box (tools/ce3_micro.py / ce3b_micro.py,
+    s = 3 … 16; fixed cost ≈ 4 / 5 tiles, a slab ≈ 2.1 / 2.7 tile-times at Mv = 18,944): fp32 Movie-Book head a
+    (n = 36,845) 5 splits — 1614 µs against 1626 at 12, with 7 fewer 19 MB slabs —, head b (63,937) 12; bf16 5 for
+    both (758 / 1239 µs against 793 / 1257 at 12), Food-Kitchen (Mv ≈ 9.5k) 3 (382 µs against 386 at 10, with 7
+    fewer slabs).  Other widths: split_count (whole rounds)."""
+    if not (FWD_PLAN and d == 256):
         return split_count(Mv, 128, max_split)
+    rows, wg, slab = (32, 4.0, 2.1) if x3 else (64, 5.0, 2.7)
     blocks = max(1, -(-Mv // 128))
-    tiles = max(1, -(-n // 32))
+    tiles = max(1, -(-n // rows))
     slots = _ncu()
     best, best_c = 1, None
     for s in range(1, max_split + 1):
-        c = -(-blocks * s // slots) * (-(-tiles // s) + 4.0) + 2.1 * s * Mv / 18944
+        c = -(-blocks * s // slots) * (-(-tiles // s) + wg) + slab * s * Mv / 18944
         if best_c is None or c < best_c - 1e-9:
             best, best_c = s, c
     return best
@@ -330,7 +333,8 @@ class LossHeadFn(Function):
                 if Mv and (x3 or any(ctx.needs_input_grad[:5])):
                     # forward + the softmax part of the input gradient in one sweep (online lse, flash
                     # style): the backward runs no dH sweep
-                    ns = fwd_split_count(Mv, n, x3, d)
+                    ns = fwd_split_count(Mv, n, x3, d) if ce_entry(x3, d, 'fwd_u').startswith('c2dsr_ce3') \
+                        else split_count(Mv, 128)
                     pm = torch.empty(ns, Mv, **f32)
                     ps = torch.empty(ns, Mv, **f32)
                     Up = torch.empty(ns, Mv, d, **f32)

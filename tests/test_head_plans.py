@@ -57,8 +57,9 @@ def test_fwd_split_count_fitted():
     # fp32 mode at the MB heads (Mv = 18,944): head a 5 splits (fewer U slabs at equal sweep time), head b 12
     assert L.fwd_split_count(18944, 36845, True) == 5
     assert L.fwd_split_count(18944, 63937, True) == 12
-    # the bf16 mode and other widths keep split_count
-    assert L.fwd_split_count(18944, 36845, False) == L.split_count(18944, 128)
+    # bf16 (64-row tiles): 5 at the MB heads, 3 at the Food-Kitchen heads; other widths keep split_count
+    assert L.fwd_split_count(18944, 36845, False) == 5 and L.fwd_split_count(18944, 63937, False) == 5
+    assert L.fwd_split_count(9472, 34886, False) == 3
     assert L.fwd_split_count(18944, 36845, True, d=128) == L.split_count(18944, 128)
     for Mv in (1, 64, 9472, 40960):
         for n in (31, 36845, 63937):
