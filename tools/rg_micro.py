@@ -80,12 +80,12 @@ def main(x3=False):
 
 def rg3_stamps(f):
     """Diagnostic build (-DRG3_STAMP): cycles per chunk per wave of the rg3 loop's phases."""
-    from c2dsr_amd._lib import lib
-    try:
-        fn = lib.raw('c2dsr_rg3_stamps')
-    except AttributeError:
-        return
     import ctypes
+    from c2dsr_amd import _lib
+    so = ctypes.CDLL(os.path.join(_lib._DIR, 'libc2dsr_hip.so'))  # the stamp entry exists in the diagnostic build only
+    if not hasattr(so, 'c2dsr_rg3_stamps'):
+        return
+    fn = so.c2dsr_rg3_stamps
     buf = (ctypes.c_ulonglong * 8)()
     torch.cuda.synchronize()
     fn(buf, 1)
