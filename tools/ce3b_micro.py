@@ -53,7 +53,19 @@ def main():
         dWp, dbp = torch.zeros(1, n, d, **f32), torch.zeros(1, n, **f32)
     else:
         dWp, dbp = torch.empty(max(nr, 1), n, d, **f32), torch.empty(max(nr, 1), n, **f32)
-    if nr == -1:
+    if nr <= -2:  # whole rounds of row blocks unsplit, the remainder split -nr ways (losshead.dw_plan's third form)
+        from c2dsr_amd.losshead import _ncu
+        full = -(-n // 128) // _ncu() * _ncu() * 128
+        rem, k = n - full, -nr
+        gW, gb = torch.zeros(n, d, **f32), torch.zeros(n, **f32)
+        rWp, rbp = torch.empty(k, rem, d, **f32), torch.empty(k, rem, **f32)
+
+        def dw():
+            lib('c2dsr_ce3b_fused_dw', Hb, Wb, bias2, Mv, full, d, 0, crow, gW, gb, s)
+            lib('c2dsr_ce3b_fused_dw', Hb, Wb.view(-1)[full * d:], bias2[full:], Mv, rem, d, k, crow, rWp, rbp, s)
+            lib('c2dsr_sum_parts', rWp, k, rem * d, 1.0, gW.view(-1)[full * d:], s)
+            lib('c2dsr_sum_parts', rbp, k, rem, 1.0, gb[full:], s)
+    elif nr == -1:
         dw = lambda: lib('c2dsr_ce3b_fused_dw_sk', Hb, Wb, bias2, Mv, n, d, crow, dWp[0], dbp[0], sk_ws, wsb, s)  # noqa: E731
     else:
         dw = lambda: lib('c2dsr_ce3b_fused_dw', Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)  # noqa: E731
