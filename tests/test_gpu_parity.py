@@ -130,7 +130,7 @@ def test_train_steps_match_reference(name, compact):
         if not compact:
             assert not box['need']
         for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
-            assert abs(float(v) - float(m[f's{s}/{k}'])) <= TOL * abs(float(m[f's{s}/{k}'])), (s, k)
+            assert abs(float(v.detach()) - float(m[f's{s}/{k}'])) <= TOL * abs(float(m[f's{s}/{k}'])), (s, k)
         for n, gv in box['grads'].items():
             assert rel(gv, m[f's{s}/grad/{n}']) < TOL, (s, n)
         # continue from the reference's post-step parameters (AdamW turns rounding noise in
