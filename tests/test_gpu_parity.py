@@ -334,9 +334,10 @@ def loss_head_vs_oracle(tr, box, b, c, B, loss, loss_rec, loss_mi, P, tol_loss, 
     grads = torch.autograd.grad(out['loss'], wrt)
     worst = {}
     for k, v in (('loss', loss), ('loss_rec', loss_rec), ('loss_mi', loss_mi)):
-        e = abs(float(v.detach()) - float(out[k])) / abs(float(out[k]))
+        r = float(out[k].detach())
+        e = abs(float(v.detach()) - r) / abs(r)
         worst[k] = e
-        assert e < tol_loss, (k, float(v), float(out[k]), e)
+        assert e < tol_loss, (k, float(v.detach()), r, e)
     for n, g in zip(names, grads):
         e = rel(box['grads'][n], g)
         worst[n] = e
