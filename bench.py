@@ -446,7 +446,7 @@ def run_c5(opt, world, rank, device, emit=True):
             ekeys = [state.keys(DK.site_enc(k, 0, DK.K_INPUT)) for k in range(len(passes))]
             for k, (seq, pos) in enumerate(passes):  # forward (x is consumed by nothing else here)
                 lib('c2dsr_embed_fwd_b16', seq, pos, B * L, d, H, E, P, math.sqrt(d), ekeys[k][0], ekeys[k][1], p,
-                    rank * B * L, x, stream())
+                    rank * B * L, x, N, L, None, stream())
             G.zero_()
             for k, (seq, pos) in enumerate(passes):
                 lib('c2dsr_embed_bwd_planned_b16', plans[k].get(), plans[len(passes) + k].get(), B * L, d, gx,
@@ -528,6 +528,7 @@ def main():
     ap.add_argument('--no-extra', dest='extra', action='store_false',
                     help='skip the extra lines (MB bf16 mode, FK bf16, C5) of the default N=1 run')
     ap.add_argument('--no-c5', dest='c5_extra', action='store_false', help='skip the C5 extra line')
+    ap.add_argument('--no-c4', dest='c4_extra', action='store_false', help='skip the C4 strong-scaling model line')
     ap.add_argument('--zero1', action='store_true',
                     help='N>1: ZeRO-1 (reduce-scatter, 1/p AdamW, all-gather; c2dsr_amd/dp.py) for the main line')
     ap.add_argument('--gnn-shard', action='store_true',
@@ -598,6 +599,9 @@ def main():
             extra['fk_bf16'] = brief(run_train(opt, fk, 'fk', 'bf16', wfk, world, rank, device))
             del wfk
             torch.cuda.empty_cache()
+            if opt.c4_extra:  # BASELINE configs[3]: the strong-scaling model of C4 from two one-GPU points
+                extra['c4_strong'] = c4_strong(opt, rank, device)
+                torch.cuda.empty_cache()
             if opt.c5_extra:  # BASELINE configs[4]: the K1 + K2 HBM roofline run at 10M + 10M items, d = 512
                 extra['c5_hbm'] = run_c5(opt, world, rank, device, emit=False)
                 torch.cuda.empty_cache()
@@ -618,6 +622,49 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+XGMI_BUSBW_GBS = (300.0, 600.0)  # assumed RCCL all-reduce bus bandwidth on 8 × MI355X (conservative, optimistic)
+
+
+def c4_strong(opt, rank, device):
+    """BASELINE configs[3] (C4: Entertainment-Education sizes, B = 4096 global over 8 GPUs, strong scaling) modelled
+    from two one-GPU runs (T(p) = F + V/p, target ≥ 6× at p = 8):
+      T(4096) = F + V and T(512) = F + V/8  ⇒  V = 8/7·(T(4096) − T(512)),  F = T(4096) − V,
+    F = the per-step work that does not shrink with the per-GPU batch (GCN propagation fwd + bwd over the whole item
+    graph, AdamW over all parameters, launch overheads), V = the batch-proportional part.  At p = 8 each rank also
+    all-reduces the flat fp32 gradient (4·n_params bytes; ring: 2·7/8 of it per GPU) — issued range by range inside
+    the backward (c2dsr_amd/dp.py), so only the last table chunk is exposed; the projection charges the WHOLE
+    all-reduce as exposed (upper bound on T(8)) and, separately, the last chunk only."""
+    ee = CONFIGS['ee']
+    pts = {}
+    for B in (4096, 512):
+        c = dict(ee, B=B)
+        wl = workload(c, 'ee')
+        pts[B] = run_train(opt, c, 'ee', opt.precision, wl, 1, rank, device)
+        del wl
+        torch.cuda.empty_cache()
+    t8, t1 = pts[512]['ms_per_step'], pts[4096]['ms_per_step']
+    V = 8.0 / 7.0 * (t1 - t8)
+    F = t1 - V
+    n_params = pts[4096]['n_params']
+    wire = 2 * 7 / 8 * 4 * n_params  # bytes per GPU of a ring all-reduce over 8 ranks
+    n_item = ee['n_a'] + ee['n_b'] + 1
+    last_chunk = 4 * n_item * ee['d'] / 4  # one of the 4 row chunks of the last item table (dp.TABLE_CHUNKS)
+    proj = {}
+    for bw in XGMI_BUSBW_GBS:
+        ar = wire / (bw * 1e9) * 1e3
+        ex = 2 * 7 / 8 * last_chunk / (bw * 1e9) * 1e3
+        proj[f'busbw_{int(bw)}GBs'] = dict(allreduce_ms=round(ar, 3), exposed_tail_ms=round(ex, 4),
+                                           T8_ms_all_exposed=round(F + V / 8 + ar, 3),
+                                           speedup_all_exposed=round(t1 / (F + V / 8 + ar), 2),
+                                           T8_ms_tail_exposed=round(F + V / 8 + ex, 3),
+                                           speedup_tail_exposed=round(t1 / (F + V / 8 + ex), 2))
+    return dict(b4096=brief(pts[4096]), b512=brief(pts[512]), F_ms=round(F, 3), V_ms=round(V, 3),
+                F_over_V=round(F / V, 4) if V > 0 else None, n_params=n_params, grad_bytes=4 * n_params,
+                projection_p8=proj, ideal_speedup_p8=round(t1 / (F + V / 8), 2),
+                note='one-GPU measurements; T(p) = F + V/p (SURVEY §8(e)); all-reduce at an assumed xGMI bus '
+                     'bandwidth (no 8-GPU node here)')
 
 
 def workload(cfg, name):
@@ -709,6 +756,7 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
     hb = htimer.summary(recs, opt.steps)
     ms = el / opt.steps * 1e3
     value = B_global * opt.steps / el
+    n_params = int(tr.model.flat.numel)
     del tr, batches
     peak = {'bf16': PEAK_BF16_TFLOPS, 'fp32': PEAK_X3_TFLOPS}.get(precision, PEAK_FP32_TFLOPS)
     roof = None
@@ -746,7 +794,7 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
             'config': {'workload': f'{name}: {cfg["label"]}', 'n_item_a': cfg['n_a'], 'n_item_b': cfg['n_b'],
                        'd': cfg['d'], 'seq_len': cfg['L'], 'batch_per_gpu': B_local, 'global_batch': B_global,
                        'train_sequences': int(n_rows), 'len_rec': 10, 'dropout': 0.2, 'parallelism': par},
-            'loss': round(loss, 5) if math.isfinite(loss) else None,
+            'loss': round(loss, 5) if math.isfinite(loss) else None, 'n_params': n_params,
             'host_prep': {'launch_counts_ms_per_step': round(host_counts_ms, 3),
                           'note': 'host data prep, outside the timed region (SURVEY §8(d)): the step\'s launch sizes '
                                   'counted from the batch\'s host copy by the data pipeline (Trainer.launch_counts); '

@@ -6,8 +6,9 @@ operator library ``libc2dsr_torch.so`` (c2dsr_amd/csrc_torch/):
 * ``torch.ops.c2dsr_raw`` — one schema op per C-ABI entry point (pointers as tensors, the ABI's int sizes), reached
   as ``lib(name, *args)`` for the remaining per-kernel calls and ``lib.raw(name)`` for the size / support queries.
 
-Every call enqueues on torch's current HIP stream: the ``stream()`` argument the call sites pass (taken from that
-same current stream; the side-stream index plans switch streams with ``torch.cuda.stream``) is dropped.  There is deliberately no fallback: if the libraries (or a GPU) are
+Every call enqueues on torch's current HIP stream: the ``stream()`` argument the call sites pass must be that same
+current stream (checked: a call naming another stream raises instead of being reordered; the side-stream index plans
+switch streams with ``torch.cuda.stream``).  There is deliberately no fallback: if the libraries (or a GPU) are
 missing, calls raise, so nothing silently runs on some other path.
 """
 from __future__ import annotations
@@ -100,7 +101,12 @@ class _Lib:
         if self.time_meta and name in self.time_meta:
             self._extra.setdefault(name, []).append(self.time_meta[name](args))
         if has_stream:
-            args = args[:-1]  # the call sites' stream() argument: the op uses torch's current stream itself
+            # the call sites' stream() argument: the op launches on torch's current stream itself, so a call naming
+            # any other stream would be silently reordered — refused instead
+            s = args[-1]
+            if s is not None and s != torch.cuda.current_stream().cuda_stream:
+                raise HipLibError(f'{name}: stream argument {s:#x} is not the current stream (use torch.cuda.stream)')
+            args = args[:-1]
         args = [torch.from_numpy(a) if type(a) is np.ndarray else a for a in args]
         try:
             return op(*args)
@@ -141,6 +147,13 @@ def stream() -> int:
     if not torch.cuda.is_available():
         raise HipLibError('c2dsr_amd kernels need a HIP device (no CPU fallback)')
     return torch.cuda.current_stream().cuda_stream
+
+
+def error_word() -> torch.Tensor:
+    """The current device's index error word (int32 [4], aliased; word 0 holds the C2DSR_IDX_ERR_* bits of
+    include/c2dsr.h): every range-checked lookup of a training step ORs into it, AdamW changes nothing while it is
+    nonzero, and the trainer reads it at its host sync (Trainer.check_index_errors)."""
+    return stage_ops().error_word()
 
 
 def require_device(t: torch.Tensor):

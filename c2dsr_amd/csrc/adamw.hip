@@ -40,7 +40,11 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, floa
                                                     float4* __restrict__ accum, float4* __restrict__ m,
                                                     float4* __restrict__ v, float4* __restrict__ vmax, long n4,
                                                     float lr, float wd_factor, float b1, float b2, float eps,
-                                                    float step_size, float inv_bc2_sqrt) {
+                                                    float step_size, float inv_bc2_sqrt,
+                                                    const int* __restrict__ err) {
+  // a step whose indices were out of range changes nothing (the reference raises before optimizer.step(),
+  // trainer.py:97-158); the host raises IndexError at its next sync
+  if (err && *err) return;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 g = ld_s(fresh + i);
     if constexpr (!KEEP) {
@@ -77,7 +81,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float4* __restrict__ p, floa
 // All buffers fp32 [n], n % 4 == 0, 16-byte aligned.  accum may be null (no epoch accumulation);
 // accum == fresh: the gradient buffer is the epoch accumulation itself (read only).
 C2_API int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,
-                       float b1, float b2, float eps, int step, void* stream) {
+                       float b1, float b2, float eps, int step, const int* err, void* stream) {
   if (n % 4) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   const double bc1 = 1.0 - pow((double)b1, (double)step);
@@ -96,11 +100,11 @@ C2_API int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v,
   if (accum && accum == fresh)
     adamw_kernel<true><<<blocks, 256, 0, (hipStream_t)stream>>>((float4*)p, (float4*)fresh, nullptr, (float4*)m,
                                                                 (float4*)v, (float4*)vmax, n4, lr, 1.f - lr * wd, b1,
-                                                                b2, eps, step_size, inv_bc2_sqrt);
+                                                                b2, eps, step_size, inv_bc2_sqrt, err);
   else
     adamw_kernel<false><<<blocks, 256, 0, (hipStream_t)stream>>>((float4*)p, (float4*)fresh, (float4*)accum,
                                                                  (float4*)m, (float4*)v, (float4*)vmax, n4, lr,
-                                                                 1.f - lr * wd, b1, b2, eps, step_size, inv_bc2_sqrt);
+                                                                 1.f - lr * wd, b1, b2, eps, step_size, inv_bc2_sqrt, err);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -4,6 +4,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include "c2dsr.h"  // the C ABI: every C2_API definition is checked against its declaration
+
 #define C2_API extern "C" __attribute__((visibility("default")))
 
 #define C2_CHECK_LAUNCH()                         \

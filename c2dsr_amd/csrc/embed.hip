@@ -14,20 +14,32 @@
 namespace {
 
 // ------------------------------------------------------------------ forward gather
+// Index range checks of the lookups (F.embedding / nn.Embedding raise IndexError for an index outside [0, N),
+// models/C2DSR.py:65-67,81, encoders.py:30): a bad item index sets IDX_ERR_ITEM, a bad position IDX_ERR_POS in the
+// caller's error word (host reads it at its next sync and raises), and the row read is row 0 instead — no load
+// ever leaves the tables.
+__device__ __forceinline__ long checked_index(int64_t v, int n, int bit, int* err) {
+  if (v >= 0 && v < n) return (long)v;
+  if (err) atomicOr(err, bit);
+  return 0;
+}
+
 template <int LPR, bool GATHER, typename T = float>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ seq, const int64_t* __restrict__ pos,
                                                         int n_rows, int d, const T* __restrict__ H,
                                                         const T* __restrict__ E, const float* __restrict__ Xin,
                                                         const float* __restrict__ P, float scale, c2::Drop drop,
-                                                        int64_t idx_base, float* __restrict__ X) {
+                                                        int64_t idx_base, float* __restrict__ X, int n_items,
+                                                        int n_pos, int* __restrict__ err) {
   constexpr int GROUPS = 256 / LPR;
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
   const long r = (long)blockIdx.x * GROUPS + g;
   if (r >= n_rows) return;
-  const long p = pos[r];
+  const bool flag = lane == 0;
+  const long p = checked_index(pos[r], n_pos, C2DSR_IDX_ERR_POS, flag ? err : nullptr);
   long s = 0;
-  if (GATHER) s = seq[r];
+  if (GATHER) s = checked_index(seq[r], n_items, C2DSR_IDX_ERR_ITEM, flag ? err : nullptr);
   for (int c = lane * 4; c < d; c += LPR * 4) {
     float4 a;
     if (GATHER) {
@@ -55,14 +67,17 @@ __global__ __launch_bounds__(256) void embed_fwd_rows_kernel(const int64_t* __re
                                                              const float* __restrict__ P, float scale, c2::Drop drop,
                                                              int64_t idx_base, const int* __restrict__ qi, int nq,
                                                              const int* __restrict__ ki, int nk,
-                                                             float* __restrict__ X) {
+                                                             float* __restrict__ X, int n_items, int n_pos,
+                                                             int* __restrict__ err) {
   constexpr int GROUPS = 256 / LPR;
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
   const long k = (long)blockIdx.x * GROUPS + g;
   if (k >= nq + nk) return;
   const long r = min(max(k < nq ? qi[k] : ki[k - nq], 0), n_rows - 1);
-  const long p = pos[r], s = seq[r];
+  int* const e = lane == 0 ? err : nullptr;
+  const long p = checked_index(pos[r], n_pos, C2DSR_IDX_ERR_POS, e);
+  const long s = checked_index(seq[r], n_items, C2DSR_IDX_ERR_ITEM, e);
   for (int c = lane * 4; c < d; c += LPR * 4) {
     // (the statements of embed_fwd_kernel's gather path: the same rounding)
     const float4 h = c2::ld4(H + s * d + c);
@@ -82,11 +97,16 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ROUNDS = 8;
 constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;
 
-__global__ void prep_keys_kernel(const int64_t* __restrict__ idx, int n, uint32_t* __restrict__ keys,
-                                 uint32_t* __restrict__ vals) {
+// an index outside [0, n_keys) becomes the key n_keys (sorted after every valid key; the segment sums never follow
+// a key >= n_out) and sets `bit` in the caller's error word: a bad index never reaches a gradient read-modify-write
+__global__ void prep_keys_kernel(const int64_t* __restrict__ idx, int n, int n_keys, int bit, uint32_t* __restrict__ keys,
+                                 uint32_t* __restrict__ vals, int* __restrict__ err) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
-    keys[i] = (uint32_t)idx[i];
+    const int64_t v = idx[i];
+    const bool ok = v >= 0 && v < n_keys;
+    if (!ok && err) atomicOr(err, bit);
+    keys[i] = ok ? (uint32_t)v : (uint32_t)n_keys;
     vals[i] = (uint32_t)i;
   }
 }
@@ -210,6 +230,7 @@ constexpr int SEG_CH = SEG_CH_CFG;
 constexpr int PL_T = 256;         // plan kernels: threads per block
 constexpr int PL_E = 4;           // entries per thread
 constexpr int PL_B = PL_T * PL_E;  // entries per block
+constexpr int SUBP = 128;          // pieces per level-1 block of a split (pass B)
 
 __device__ __forceinline__ bool split_start(const uint32_t* K, int n, int i) {
   if (!(i == 0 || K[i] != K[i - 1])) return false;
@@ -217,22 +238,48 @@ __device__ __forceinline__ bool split_start(const uint32_t* K, int n, int i) {
   return ce < n && K[ce] == K[i];
 }
 
-// per block: number of splits starting among its PL_B entries → cnt[b]
+// chunks spanned by the run that starts at entry i (keys are sorted: binary search for its end)
+__device__ __forceinline__ int split_span(const uint32_t* K, int n, int i) {
+  const uint32_t key = K[i];
+  int lo = i, hi = n;  // first entry with a larger key
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (K[mid] <= key) lo = mid + 1; else hi = mid;
+  }
+  return (lo - 1) / SEG_CH - i / SEG_CH + 1;
+}
+
+__device__ __forceinline__ uint32_t n_subs(int span) { return (uint32_t)((span + SUBP - 1) / SUBP); }
+
+// per block: the splits starting among its PL_B entries and their SUBP-piece sub-ranges → cnt[b], cnt[nb + b]
 __global__ __launch_bounds__(PL_T) void plan_count_kernel(const uint32_t* __restrict__ K, int n,
                                                           uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t red[PL_T / 64];
-  uint32_t q = 0;
+  __shared__ uint32_t red[2][PL_T / 64];
+  uint32_t q = 0, u = 0;
   for (int j = 0; j < PL_E; ++j) {
     const int i = blockIdx.x * PL_B + j * PL_T + threadIdx.x;
-    if (i < n) q += split_start(K, n, i);
+    if (i < n && split_start(K, n, i)) {
+      ++q;
+      u += n_subs(split_span(K, n, i));
+    }
   }
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  for (int o = 32; o > 0; o >>= 1) {
+    q += __shfl_xor(q, o, 64);
+    u += __shfl_xor(u, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = q;
+    red[1][threadIdx.x >> 6] = u;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < PL_T / 64; ++w) t += red[w];
+    uint32_t t = 0, v = 0;
+    for (int w = 0; w < PL_T / 64; ++w) {
+      t += red[0][w];
+      v += red[1][w];
+    }
     cnt[blockIdx.x] = t;
+    cnt[gridDim.x + blockIdx.x] = v;
   }
 }
 
@@ -252,42 +299,67 @@ __device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t* red) {
   return base + inc - v;
 }
 
-// writes splits[j] = {key, first chunk, chunks spanned, 0} in entry order
-// The block's first output slot is the sum of the earlier blocks' counts (plan_count_kernel), read here
-// (≤ a few hundred u32 from L2) instead of a separate scan launch; the last block writes the total → counts[1].
+// writes splits[j] = {key, first chunk, chunks spanned, 0} in entry order, and — the work a single-workgroup
+// launch (plan_subs) used to do after it — every split's SUBP-piece sub-ranges: suboff[j] = its first sub,
+// subs[suboff[j] + y] = (j, y·SUBP), suboff[splits] = counts[2] = the sub total; counts[1] = the split total, and the
+// plan's error word (counts[3]) starts at 0.  A block's first output slots are the sums of the earlier blocks'
+// counts (plan_count_kernel), read here (≤ a few hundred u32 from L2) instead of a separate scan launch.
 __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restrict__ K, int n,
                                                          const uint32_t* __restrict__ cnt, int4* __restrict__ splits,
+                                                         int* __restrict__ suboff, int2* __restrict__ subs,
                                                          int* __restrict__ counts) {
-  __shared__ uint32_t red[PL_T / 64];
-  uint32_t before = 0;
-  for (int b = threadIdx.x; b < (int)blockIdx.x; b += PL_T) before += cnt[b];
-  for (int o = 32; o > 0; o >>= 1) before += __shfl_xor(before, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = before;
+  __shared__ uint32_t red[2][PL_T / 64];
+  uint32_t bs = 0, bu = 0;
+  for (int b = threadIdx.x; b < (int)blockIdx.x; b += PL_T) {
+    bs += cnt[b];
+    bu += cnt[gridDim.x + b];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    bs += __shfl_xor(bs, o, 64);
+    bu += __shfl_xor(bu, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = bs;
+    red[1][threadIdx.x >> 6] = bu;
+  }
   __syncthreads();
-  uint32_t base = 0;
-  for (int k = 0; k < PL_T / 64; ++k) base += red[k];
+  uint32_t base_s = 0, base_u = 0;
+  for (int k = 0; k < PL_T / 64; ++k) {
+    base_s += red[0][k];
+    base_u += red[1][k];
+  }
   __syncthreads();
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) counts[1] = (int)(base + cnt[blockIdx.x]);
-  // thread t owns entries [base + t·PL_E, base + (t+1)·PL_E): contiguous, so the order is kept
+  // thread t owns entries [i0, i0 + PL_E): contiguous, so the order is kept
   const int i0 = blockIdx.x * PL_B + threadIdx.x * PL_E;
-  uint32_t fs = 0;
+  uint32_t fs = 0, nu = 0;
+  int span[PL_E];
   for (int j = 0; j < PL_E; ++j) {
     const int i = i0 + j;
-    if (i < n) fs |= (uint32_t)split_start(K, n, i) << j;
+    span[j] = 0;
+    if (i < n && split_start(K, n, i)) {
+      fs |= 1u << j;
+      span[j] = split_span(K, n, i);
+      nu += n_subs(span[j]);
+    }
   }
-  uint32_t os = base + block_prefix(__popc(fs), red);
+  uint32_t os = base_s + block_prefix(__popc(fs), red[0]);
+  uint32_t ou = base_u + block_prefix(nu, red[1]);
   for (int j = 0; j < PL_E; ++j) {
     if (fs >> j & 1) {
       const int i = i0 + j;
-      const uint32_t key = K[i];
-      int lo = i, hi = n;  // first entry with a larger key (keys are sorted)
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (K[mid] <= key) lo = mid + 1; else hi = mid;
-      }
-      const int c = i / SEG_CH, last = (lo - 1) / SEG_CH;
-      splits[os++] = make_int4((int)key, c, last - c + 1, 0);
+      splits[os] = make_int4((int)K[i], i / SEG_CH, span[j], 0);
+      suboff[os] = (int)ou;
+      const uint32_t k = n_subs(span[j]);
+      for (uint32_t y = 0; y < k; ++y) subs[ou + y] = make_int2((int)os, (int)(y * SUBP));
+      ++os;
+      ou += k;
     }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == PL_T - 1) {  // owns the last entries: os / ou are the totals
+    suboff[os] = (int)ou;
+    counts[1] = (int)os;
+    counts[2] = (int)ou;
+    counts[3] = 0;
   }
 }
 
@@ -305,7 +377,6 @@ constexpr int SEG_U = SEG_U_CFG;  // rows in flight per lane group
 #ifndef SEG_PREF
 #define SEG_PREF 0
 #endif
-constexpr int SUBP = 128;  // pieces per level-1 block of a split
 
 struct RowSrc {
   const float* gX;
@@ -648,41 +719,6 @@ __global__ __launch_bounds__(256) void seg_split2_kernel(SegJob j0, SegJob j1) {
   }
 }
 
-// plan: sub-ranges of every split.  One workgroup: per-thread runs of splits, block scan of their
-// sub counts → suboff[nsplit + 1], subs[total] = (split, first piece), counts[2] = total; the
-// error word starts at 0.
-__global__ __launch_bounds__(1024) void plan_subs_kernel(const int4* __restrict__ splits, int* __restrict__ counts,
-                                                         int* __restrict__ suboff, int2* __restrict__ subs,
-                                                         int* __restrict__ err) {
-  __shared__ int part[1024];
-  const int t = threadIdx.x;
-  const int ns = counts[1];
-  const int per = (ns + 1023) / 1024;
-  const int lo = min(ns, t * per), hi = min(ns, lo + per);
-  int sum = 0;
-  for (int i = lo; i < hi; ++i) sum += (splits[i].z + SUBP - 1) / SUBP;
-  part[t] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = t >= o ? part[t - o] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  int run = part[t] - sum;
-  for (int i = lo; i < hi; ++i) {
-    suboff[i] = run;
-    const int k = (splits[i].z + SUBP - 1) / SUBP;
-    for (int y = 0; y < k; ++y) subs[run + y] = make_int2(i, y * SUBP);
-    run += k;
-  }
-  if (t == 1023) {
-    suboff[ns] = part[1023];
-    counts[2] = part[1023];
-    *err = 0;
-  }
-}
-
 __global__ void drop_scale_kernel(const float* __restrict__ gX, long n4, int d, c2::Drop drop, int64_t idx_base,
                                   float* __restrict__ out) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -699,6 +735,19 @@ __global__ void drop_scale_kernel(const float* __restrict__ gX, long n4, int d, 
 __global__ void col0_add_kernel(const float* __restrict__ T, int n, float* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c < n) out[c] += T[4 * (long)c];
+}
+
+// err |= bit if any idx[r·ld + ld - cols + c] (r < rows, c < cols) lies outside [0, hi)
+__global__ __launch_bounds__(256) void index_check_kernel(const int64_t* __restrict__ idx, long rows, int ld, int cols,
+                                                          int64_t hi, int bit, int* __restrict__ err) {
+  const long n = rows * cols;
+  bool bad = false;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols;
+    const int64_t v = idx[r * ld + (ld - cols) + (i - r * cols)];
+    bad |= v < 0 || v >= hi;
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(err, bit);
 }
 
 int lpr_for(int d) { return d / 4 >= 64 ? 64 : (d / 4 >= 32 ? 32 : (d / 4 >= 16 ? 16 : (d / 4 >= 8 ? 8 : 4))); }
@@ -739,7 +788,7 @@ size_t plan_layout(int n, Plan* p, char* base) {
   char* k1 = take((size_t)n * 4);
   char* v1 = take((size_t)n * 4);
   char* hist = take((size_t)256 * nblocks * 4);
-  char* bc = take((size_t)pb * 4);
+  char* bc = take((size_t)pb * 8);  // per plan block: split count, sub count
   if (p)
     *p = Plan{(uint32_t*)k0, (uint32_t*)v0, (int4*)sp, (int*)ct, (int*)so, (int2*)sb,
               (uint32_t*)k1, (uint32_t*)v1, (uint32_t*)hist, (uint32_t*)bc, nblocks};
@@ -758,13 +807,13 @@ size_t seg_slot2_bytes(int n, int d) { return align256((size_t)max_subs(n) * d *
 size_t seg_ws_bytes(int n, int d) { return 2 * seg_slot_bytes(n, d) + seg_slot2_bytes(n, d); }
 
 // sort idx[0..n) (values < n_keys) → k0/v0 sorted (key, original row), stable; then the work lists
-int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t s) {
+int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t s, int* err = nullptr) {
   int bits = 1;
-  while ((1l << bits) < (long)n_keys) ++bits;
+  while ((1l << bits) < (long)n_keys + 1) ++bits;  // keys 0 .. n_keys (n_keys: an out-of-range index)
   // the passes alternate between the two buffer pairs: start in the pair the last pass does not write
   const bool odd = ((bits + 7) / 8) & 1;
   uint32_t *ki = odd ? w.k1 : w.k0, *vi = odd ? w.v1 : w.v0, *ko = odd ? w.k0 : w.k1, *vo = odd ? w.v0 : w.v1;
-  prep_keys_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(idx, n, ki, vi);
+  prep_keys_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(idx, n, n_keys, C2DSR_IDX_ERR_PLAN, ki, vi, err);
   for (int shift = 0; shift < bits; shift += 8) {
     rs_hist_kernel<<<w.nblocks, RS_THREADS, 0, s>>>(ki, n, shift, w.nblocks, w.hist);
     rs_scatter_kernel<<<w.nblocks, RS_THREADS, 0, s>>>(ki, vi, n, shift, w.nblocks, w.hist, ko, vo);
@@ -777,8 +826,7 @@ int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t
   }
   const int pb = c2::ceil_div(n, PL_B);
   plan_count_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt);
-  plan_emit_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt, w.splits, w.counts);
-  plan_subs_kernel<<<1, 1024, 0, s>>>(w.splits, w.counts, w.suboff, w.subs, w.counts + 3);
+  plan_emit_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt, w.splits, w.suboff, w.subs, w.counts);
   C2_CHECK_LAUNCH();
   return 0;
 }
@@ -850,8 +898,9 @@ void seg_dispatch(const SegJob& j0, const SegJob* j1, hipStream_t s) {
 
 C2_API int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H, const float* E,
                            const float* Xin, const float* P, float scale, uint32_t k0, uint32_t k1, float p,
-                           int64_t idx_base, float* X, void* stream) {
+                           int64_t idx_base, float* X, int n_items, int n_pos, int* err, void* stream) {
   if (d % 4 || n_rows <= 0) return n_rows == 0 ? 0 : (int)hipErrorInvalidValue;
+  if (n_pos <= 0 || (!Xin && n_items <= 0)) return (int)hipErrorInvalidValue;
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
   const int lpr = lpr_for(d);
@@ -859,9 +908,11 @@ C2_API int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, i
   const bool gather = Xin == nullptr;
 #define C2_EMB(L)                                                                                                  \
   if (gather)                                                                                                      \
-    embed_fwd_kernel<L, true><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, Xin, P, scale, dr, idx_base, X);     \
+    embed_fwd_kernel<L, true><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, Xin, P, scale, dr, idx_base, X,      \
+                                                   n_items, n_pos, err);                                           \
   else                                                                                                             \
-    embed_fwd_kernel<L, false><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, Xin, P, scale, dr, idx_base, X);
+    embed_fwd_kernel<L, false><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, Xin, P, scale, dr, idx_base, X,     \
+                                                    n_items, n_pos, err);
   switch (lpr) {
     case 64: C2_EMB(64) break;
     case 32: C2_EMB(32) break;
@@ -877,8 +928,8 @@ C2_API int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, i
 C2_API int c2dsr_embed_fwd_rows(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H,
                                 const float* E, const float* P, float scale, uint32_t k0, uint32_t k1, float p,
                                 int64_t idx_base, const int* q_idx, int nq, const int* k_idx, int nk, float* X,
-                                void* stream) {
-  if (d % 4 || nq < 0 || nk < 0 || !H || !E || !P) return (int)hipErrorInvalidValue;
+                                int n_items, int n_pos, int* err, void* stream) {
+  if (d % 4 || nq < 0 || nk < 0 || !H || !E || !P || n_items <= 0 || n_pos <= 0) return (int)hipErrorInvalidValue;
   if (nq + nk == 0 || n_rows <= 0) return 0;
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
@@ -886,7 +937,7 @@ C2_API int c2dsr_embed_fwd_rows(const int64_t* seq, const int64_t* pos, int n_ro
   dim3 grid(c2::ceil_div(nq + nk, 256 / lpr));
 #define C2_EMB(L)                                                                                                    \
   embed_fwd_rows_kernel<L><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, H, E, P, scale, dr, idx_base, q_idx, nq, k_idx, \
-                                                nk, X);
+                                                nk, X, n_items, n_pos, err);
   switch (lpr) {
     case 64: C2_EMB(64) break;
     case 32: C2_EMB(32) break;
@@ -899,18 +950,30 @@ C2_API int c2dsr_embed_fwd_rows(const int64_t* seq, const int64_t* pos, int n_ro
   return 0;
 }
 
+C2_API int c2dsr_index_check(const int64_t* idx, long rows, int ld, int cols, int64_t hi, int bit, int* err,
+                             void* stream) {
+  if (rows < 0 || ld <= 0 || cols < 0 || cols > ld || !err) return (int)hipErrorInvalidValue;
+  const long n = rows * cols;
+  if (n == 0) return 0;
+  const int blocks = (int)std::min<long>(c2::ceil_div(n, 256), 1024);
+  index_check_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(idx, rows, ld, cols, hi, bit, err);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
 C2_API size_t c2dsr_index_plan_bytes(int n) { return plan_layout(n, nullptr, nullptr); }
 
 // Sort plan of an index array: plan = [keys u32 n | rows u32 n | scratch], keys ascending and
 // rows ascending within equal keys (stable LSD radix sort).  Depends on the indices only, so
 // the host builds it as soon as a batch's index tensors exist (on a side stream, under the
 // forward pass) and the backward's segment sums consume it.
-C2_API int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, size_t plan_bytes, void* stream) {
-  if (n < 0 || n_keys <= 0) return (int)hipErrorInvalidValue;
+C2_API int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, size_t plan_bytes, int* err,
+                            void* stream) {
+  if (n < 0 || n_keys <= 0 || n_keys >= 0x7fffffff) return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   Plan p;
   if (plan_bytes < plan_layout(n, &p, (char*)plan)) return (int)hipErrorInvalidValue;
-  return build_plan(idx, n, n_keys, p, (hipStream_t)stream);
+  return build_plan(idx, n, n_keys, p, (hipStream_t)stream, err);
 }
 
 // two segment-sum jobs (items, positions) run side by side: two slot regions
@@ -973,15 +1036,17 @@ C2_API int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, i
 // sums read-modify-write a bf16 G (fp32 sums, RNE store); P, X, gX, gP stay fp32
 C2_API int c2dsr_embed_fwd_b16(const int64_t* seq, const int64_t* pos, int n_rows, int d, const void* H, const void* E,
                                const float* P, float scale, uint32_t k0, uint32_t k1, float p, int64_t idx_base,
-                               float* X, void* stream) {
+                               float* X, int n_items, int n_pos, int* err, void* stream) {
   if (d % 4 || n_rows <= 0 || !H || !E) return n_rows == 0 ? 0 : (int)hipErrorInvalidValue;
+  if (n_items <= 0 || n_pos <= 0) return (int)hipErrorInvalidValue;
   c2::Drop dr = c2::make_drop(k0, k1, p);
   hipStream_t s = (hipStream_t)stream;
   const int lpr = lpr_for(d);
   dim3 grid(c2::ceil_div(n_rows, 256 / lpr));
   const c2::tbf16 *Hb = (const c2::tbf16*)H, *Eb = (const c2::tbf16*)E;
 #define C2_EMB(L) \
-  embed_fwd_kernel<L, true, c2::tbf16><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, Hb, Eb, nullptr, P, scale, dr, idx_base, X);
+  embed_fwd_kernel<L, true, c2::tbf16><<<grid, 256, 0, s>>>(seq, pos, n_rows, d, Hb, Eb, nullptr, P, scale, dr, idx_base, X, \
+                                                            n_items, n_pos, err);
   switch (lpr) {
     case 64: C2_EMB(64) break;
     case 32: C2_EMB(32) break;
@@ -1031,8 +1096,8 @@ C2_API int c2dsr_embed_bwd(const int64_t* seq, const int64_t* pos, int n_rows, i
   char* pp = sp + pb;
   char* seg = pp + pb;
   int e;
-  if (G && (e = c2dsr_index_plan(seq, n_rows, n_items, sp, pb, stream))) return e;
-  if (gP && (e = c2dsr_index_plan(pos, n_rows, n_pos, pp, pb, stream))) return e;
+  if (G && (e = c2dsr_index_plan(seq, n_rows, n_items, sp, pb, nullptr, stream))) return e;
+  if (gP && (e = c2dsr_index_plan(pos, n_rows, n_pos, pp, pb, nullptr, stream))) return e;
   return c2dsr_embed_bwd_planned(G ? sp : nullptr, gP ? pp : nullptr, n_rows, d, gX, k0, k1, p, idx_base, scale, G,
                                  n_items, gP, n_pos, gXin, seg, c2dsr_embed_bwd_planned_workspace(n_rows, d), stream);
 }
@@ -1082,7 +1147,7 @@ C2_API int c2dsr_ce_onehot_dw(const int64_t* tgt, int M, int n, const float* H, 
   if (ws_bytes < c2dsr_ce_onehot_workspace(M, n, D)) return (int)hipErrorInvalidValue;
   char* plan = (char*)workspace;
   const size_t pb = align256(plan_layout(M, nullptr, nullptr));
-  int e = c2dsr_index_plan(tgt, M, n + 1, plan, pb, stream);
+  int e = c2dsr_index_plan(tgt, M, n + 1, plan, pb, nullptr, stream);
   if (e) return e;
   return c2dsr_ce_onehot_dw_planned(plan, M, n, H, D, rw, gW, gb, plan + pb, ws_bytes - pb, stream);
 }

@@ -206,8 +206,12 @@ struct ValidOp {
   int *idx, *inv;
   int64_t* tc;
   int* counts;
+  int* err;  // C2DSR_IDX_ERR_TARGET for a target outside [0, ignore] (F.cross_entropy's IndexError); not valid
   __device__ uint32_t mask(int r) const {
-    const uint32_t v = t[r] != ignore;
+    const int64_t tv = t[r];
+    const bool bad = tv < 0 || tv > ignore;
+    if (bad && err) atomicOr(err, C2DSR_IDX_ERR_TARGET);
+    const uint32_t v = tv != ignore && !bad;
     return v | ((v && r < split) ? 2u : 0u);
   }
   __device__ void put(int q, int r, uint32_t in, int k) const {
@@ -683,11 +687,11 @@ C2_API size_t c2dsr_compact_workspace(int M, int n_sets) {
   return (size_t)c2::ceil_div(M, CMP_TILE) * (size_t)(n_sets < 2 ? 2 : 8) * sizeof(int);
 }
 C2_API int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, int* idx, int* inv, int64_t* tc,
-                               int* counts, int* ws, void* stream) {
+                               int* counts, int* ws, int* err, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (M < 0) return (int)hipErrorInvalidValue;
   if (M == 0) return (int)hipMemsetAsync(counts, 0, 2 * sizeof(int), s);
-  return compact_rows(ValidOp{t, split, ignore, idx, inv, tc, counts}, M, ws, s);
+  return compact_rows(ValidOp{t, split, ignore, idx, inv, tc, counts, err}, M, ws, s);
 }
 C2_API int c2dsr_need_rows(const int64_t* gm_a, const int64_t* gm_b, int B, int L, int R, int n_sets, int bits,
                            int* idx, int* inv, int* count, int* off, int* ws, void* stream) {

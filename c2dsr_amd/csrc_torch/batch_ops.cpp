@@ -82,7 +82,7 @@ std::vector<Tensor> step_prepare(const Tensor& gm_a, const Tensor& gm_b, int64_t
     Tensor ws = at::empty({(int64_t)(c2dsr_compact_workspace((int)M2, 1) / 4 + 1)}, i32);
     c2t::launch("c2dsr_compact_valid", &c2dsr_compact_valid, (const int64_t*)tcat.data_ptr<int64_t>(), (int)M2,
                 (int)(B * R), (int)n_items[k], idx.data_ptr<int>(), inv.data_ptr<int>(), tc.data_ptr<int64_t>(),
-                cnt.data_ptr<int>(), ws.data_ptr<int>(), S());
+                cnt.data_ptr<int>(), ws.data_ptr<int>(), c2t::errp(), S());
     out.insert(out.end(), {tcat, idx, inv, tc, cnt});
   }
   return out;
@@ -195,12 +195,37 @@ void weight_images(const std::vector<Tensor>& W, const std::vector<Tensor>& Y, s
 
 }  // namespace
 
+// The range checks of a batch's index tensors (a step whose batch has no host copy: Trainer.prepare), each [B, L]
+// int64: tensor i must hold values in [0, hi[i]) in its last cols[i] columns, else bits[i] is ORed into the device's
+// index error word.  Returns word 0 copied after the checks (int32 [1]), which the step's deferred count read
+// carries to the host (ops.HostCounts raises IndexError on it) — F.embedding / F.cross_entropy raise
+// (models/C2DSR.py:65-67,81, encoders.py:30, trainer.py:143-152).
+Tensor index_check(const std::vector<Tensor>& idx, std::vector<int64_t> hi, std::vector<int64_t> cols,
+                   std::vector<int64_t> bits) {
+  const char* op = "index_check";
+  TORCH_CHECK(idx.size() == hi.size() && idx.size() == cols.size() && idx.size() == bits.size(),
+              "c2dsr::index_check: hi / cols / bits per index tensor");
+  for (size_t i = 0; i < idx.size(); ++i) {
+    want(idx[i], op, "idx", at::kLong, {-1, -1});
+    dev(idx[i], op);
+    TORCH_CHECK(cols[i] >= 0 && cols[i] <= idx[i].size(1), "c2dsr::index_check: cols outside [0, L]");
+  }
+  Tensor w = c2t::err_word();
+  for (size_t i = 0; i < idx.size(); ++i)
+    c2t::launch("c2dsr_index_check", &c2dsr_index_check, (const int64_t*)idx[i].data_ptr<int64_t>(),
+                (long)idx[i].size(0), (int)idx[i].size(1), (int)cols[i], (int64_t)hi[i], (int)bits[i], w.data_ptr<int>(),
+                S());
+  return w.narrow(0, 0, 1).clone();
+}
+
 void register_batch_ops(torch::Library& m) {
   m.def("step_prepare(Tensor gm_a, Tensor gm_b, int R, int n_sets, int code, Tensor[] seqs, int pad, Tensor[] targets, "
         "int[] n_items, bool need) -> Tensor[]");
   m.def("wgrad_groups(Tensor[] dY, Tensor[] X, int[] seg_group, Tensor(a!)[] dW, Tensor(b!)?[] db, int[] x3) -> ()");
   m.def("weight_images(Tensor[] W, Tensor(a!)[] Y, int[] trans, int[] layout) -> ()");
+  m.def("index_check(Tensor[] idx, int[] hi, int[] cols, int[] bits) -> Tensor");
   m.impl("step_prepare", c10::DispatchKey::CompositeExplicitAutograd, TORCH_FN(step_prepare));
+  m.impl("index_check", c10::DispatchKey::CompositeExplicitAutograd, TORCH_FN(index_check));
   m.impl("wgrad_groups", c10::DispatchKey::CompositeExplicitAutograd, TORCH_FN(wgrad_groups));
   m.impl("weight_images", c10::DispatchKey::CompositeExplicitAutograd, TORCH_FN(weight_images));
 }

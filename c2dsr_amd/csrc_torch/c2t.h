@@ -51,6 +51,12 @@ void record(const char* name, hipEvent_t e0, hipEvent_t e1, std::vector<double>&
 bool debug_sync();
 void sync_check(const char* name, const char* where);
 
+// The index error word of the current HIP device (int32 [4], word 0 = the C2DSR_IDX_ERR_* bits; defined in
+// torch_ops.cpp): the stage operators pass it to every kernel that range-checks indices, and to AdamW, which
+// changes nothing while it is nonzero.  The host reads it through c2dsr::error_word at its sync points.
+at::Tensor err_word();
+inline int* errp() { return err_word().data_ptr<int>(); }
+
 template <class T>
 inline double as_meta(T v) {
   if constexpr (std::is_pointer_v<T>)

@@ -166,7 +166,8 @@ std::vector<Tensor> encoder_pass(const Tensor& seq, const Tensor& pos, const Ten
   Tensor xck = at::empty({nq + nk, d}, f32);
   c2t::launch("c2dsr_embed_fwd_rows", &c2dsr_embed_fwd_rows, seq.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), (int)M,
               (int)d, F(H), F(E), F(P), (float)scale, ps.k0(K_INPUT), ps.k1(K_INPUT), p, rb_rows,
-              rs_idx.data_ptr<int>(), (int)nq, ks_idx.data_ptr<int>(), (int)nk, F(xck), S());
+              rs_idx.data_ptr<int>(), (int)nq, ks_idx.data_ptr<int>(), (int)nk, F(xck), (int)H.size(0), (int)P.size(0),
+              c2t::errp(), S());
   Tensor xc = xck.narrow(0, 0, nq), xk = xck.narrow(0, nq, nk);
   const float* bin = F(w[B_IN]);
   Tensor q = at::empty({nq, d}, f32), kv = at::empty({nk, 2 * d}, f32);

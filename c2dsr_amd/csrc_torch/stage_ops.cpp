@@ -62,8 +62,12 @@ struct Graph {
   Tensor work, split, col, val;
   int64_t n_slots;
 };
-Graph graph(const Tensor& work, const Tensor& split, const Tensor& col, const Tensor& val, int64_t n_slots,
-            const char* op) {
+// n_rows: the row count the plan was built for (DeviceGraph.n) — it must equal the table's, or the SpMM's rows and
+// column indices would walk past (or stop short of) the table
+Graph graph(const Tensor& work, const Tensor& split, const Tensor& col, const Tensor& val, int64_t n_rows,
+            int64_t n_slots, const Tensor& table, const char* op) {
+  TORCH_CHECK(table.dim() == 2 && n_rows == table.size(0), "c2dsr::", op, ": the graph has ", n_rows,
+              " rows but the table has ", table.dim() == 2 ? table.size(0) : -1);
   want(work, op, "work", at::kInt, {-1, 4});
   TORCH_CHECK(split.numel() == 0 || (split.dim() == 2 && split.size(1) == 4), "c2dsr::", op, ": split must be [n, 4]");
   if (split.numel()) want(split, op, "split", at::kInt, {-1, 4});
@@ -103,10 +107,11 @@ void check_table(const Tensor& E, const char* op, const char* name) {
 // H = mean(E, A·drop(E), A·drop(A·drop(E)), …) over n_gnn rounds (models/encoders.py:42-48); keys [2·n_gnn].
 // out (optional) receives H (e.g. the first N rows of a larger buffer); returned.
 Tensor gcn_propagate(const Tensor& E, const Tensor& work, const Tensor& split, const Tensor& col, const Tensor& val,
-                     int64_t n_slots, int64_t n_gnn, double p, std::vector<int64_t> keys, const OptT& out) {
+                     int64_t n_rows, int64_t n_slots, int64_t n_gnn, double p, std::vector<int64_t> keys,
+                     const OptT& out) {
   const char* op = "gcn_propagate";
   check_table(E, op, "E");
-  const Graph g = graph(work, split, col, val, n_slots, op);
+  const Graph g = graph(work, split, col, val, n_rows, n_slots, E, op);
   TORCH_CHECK(n_gnn >= 0 && (int64_t)keys.size() == 2 * n_gnn, "c2dsr::gcn_propagate: keys must hold 2·n_gnn values");
   Tensor H = has(out) ? *out : at::empty_like(E);
   TORCH_CHECK(H.sizes() == E.sizes() && H.scalar_type() == E.scalar_type() && H.is_contiguous(),
@@ -133,10 +138,11 @@ Tensor gcn_propagate(const Tensor& E, const Tensor& work, const Tensor& split, c
 // the rounds of the backward before the last: X = T_1 (n_gnn ≥ 2; T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k), G itself for
 // n_gnn = 1 (no launch); graph = the plan of Aᵀ
 Tensor gcn_backward_rounds(const Tensor& G, const Tensor& work, const Tensor& split, const Tensor& col,
-                           const Tensor& val, int64_t n_slots, int64_t n_gnn, double p, std::vector<int64_t> keys) {
+                           const Tensor& val, int64_t n_rows, int64_t n_slots, int64_t n_gnn, double p,
+                           std::vector<int64_t> keys) {
   const char* op = "gcn_backward_rounds";
   want(G, op, "G", at::kFloat, {-1, -1});
-  const Graph g = graph(work, split, col, val, n_slots, op);
+  const Graph g = graph(work, split, col, val, n_rows, n_slots, G, op);
   TORCH_CHECK(n_gnn >= 1 && (int64_t)keys.size() == 2 * n_gnn, "c2dsr::gcn_backward_rounds: keys must hold 2·n_gnn");
   on_device(op, {&G, &work, &split, &col, &val});
   const float inv = 1.f / (float)(n_gnn + 1);
@@ -160,13 +166,14 @@ Tensor gcn_backward_rounds(const Tensor& G, const Tensor& work, const Tensor& sp
 // the training step's form (the table's own lookups and the accumulating .grad): delta = gamma = 1; the module API's
 // GCN.forward backward (ops.GCNPropFn): delta = gamma = 0, pad_row = -1
 void gcn_backward_final(const Tensor& X, const Tensor& G, const Tensor& gE, const Tensor& work, const Tensor& split,
-                        const Tensor& col, const Tensor& val, int64_t n_slots, int64_t n_gnn, double p, int64_t k0,
+                        const Tensor& col, const Tensor& val, int64_t n_rows, int64_t n_slots, int64_t n_gnn, double p,
+                        int64_t k0,
                         int64_t k1, int64_t pad_row, double delta, double gamma, const OptT& part) {
   const char* op = "gcn_backward_final";
   want(G, op, "G", at::kFloat, {-1, -1});
   want(X, op, "X", at::kFloat, {G.size(0), G.size(1)});
   want(gE, op, "gE", at::kFloat, {G.size(0), G.size(1)});
-  const Graph g = graph(work, split, col, val, n_slots, op);
+  const Graph g = graph(work, split, col, val, n_rows, n_slots, G, op);
   TORCH_CHECK(pad_row >= -1 && pad_row < G.size(0), "c2dsr::gcn_backward_final: pad_row out of range");
   Tensor pt = has(part) ? *part : part_slab(g, G);
   TORCH_CHECK(pt.scalar_type() == at::kFloat && pt.is_contiguous() &&
@@ -214,7 +221,8 @@ Tensor embed_fuse(const Tensor& seq, const Tensor& pos, const OptT& H, const Opt
   if (B * L == 0) return X;
   c2t::launch("c2dsr_embed_fwd", &c2dsr_embed_fwd, seq.data_ptr<int64_t>(), pos.data_ptr<int64_t>(), (int)(B * L),
               (int)d, fp(H), fp(E), fp(Xin), P.data_ptr<float>(), (float)scale, (uint32_t)k0, (uint32_t)k1, (float)p,
-              (int64_t)(row_base * L), X.data_ptr<float>(), S());
+              (int64_t)(row_base * L), X.data_ptr<float>(), has(H) ? (int)H->size(0) : 0, (int)P.size(0), c2t::errp(),
+              S());
   return X;
 }
 
@@ -238,7 +246,7 @@ void index_plans(const std::vector<Tensor>& idx, std::vector<int64_t> n_keys, co
   size_t o = 0;
   for (size_t i = 0; i < idx.size(); ++i) {
     c2t::launch("c2dsr_index_plan", &c2dsr_index_plan, idx[i].data_ptr<int64_t>(), (int)idx[i].numel(),
-                (int)n_keys[i], (void*)((char*)buf.data_ptr() + o), sizes[i], S());
+                (int)n_keys[i], (void*)((char*)buf.data_ptr() + o), sizes[i], c2t::errp(), S());
     o += sizes[i];
   }
 }
@@ -307,7 +315,7 @@ void adamw_step(const Tensor& param, const Tensor& fresh, const OptT& accum, con
   on_device(op, {&accum});
   c2t::launch("c2dsr_adamw", &c2dsr_adamw, param.data_ptr<float>(), fresh.data_ptr<float>(), fpm(accum),
               m.data_ptr<float>(), v.data_ptr<float>(), vmax.data_ptr<float>(), (long)n, (float)lr, (float)wd,
-              (float)b1, (float)b2, (float)eps, (int)step, S());
+              (float)b1, (float)b2, (float)eps, (int)step, (const int*)c2t::errp(), S());
 }
 
 }  // namespace
@@ -317,12 +325,12 @@ void register_losshead_ops(torch::Library& m);  // losshead_ops.cpp
 void register_batch_ops(torch::Library& m);     // batch_ops.cpp
 
 TORCH_LIBRARY_FRAGMENT(c2dsr, m) {
-  m.def("gcn_propagate(Tensor E, Tensor work, Tensor split, Tensor col, Tensor val, int n_slots, int n_gnn, float p, "
-        "int[] keys, Tensor(a!)? out=None) -> Tensor");
-  m.def("gcn_backward_rounds(Tensor G, Tensor work, Tensor split, Tensor col, Tensor val, int n_slots, int n_gnn, "
-        "float p, int[] keys) -> Tensor");
+  m.def("gcn_propagate(Tensor E, Tensor work, Tensor split, Tensor col, Tensor val, int n_rows, int n_slots, int n_gnn, "
+        "float p, int[] keys, Tensor(a!)? out=None) -> Tensor");
+  m.def("gcn_backward_rounds(Tensor G, Tensor work, Tensor split, Tensor col, Tensor val, int n_rows, int n_slots, "
+        "int n_gnn, float p, int[] keys) -> Tensor");
   m.def("gcn_backward_final(Tensor X, Tensor G, Tensor(a!) gE, Tensor work, Tensor split, Tensor col, Tensor val, "
-        "int n_slots, int n_gnn, float p, int k0, int k1, int pad_row, float delta, float gamma, "
+        "int n_rows, int n_slots, int n_gnn, float p, int k0, int k1, int pad_row, float delta, float gamma, "
         "Tensor(b!)? part=None) -> ()");
   m.def("embed_fuse(Tensor seq, Tensor pos, Tensor? H, Tensor? E, Tensor? Xin, Tensor P, float scale, float p, int k0, "
         "int k1, int row_base, Tensor(a!)? out=None) -> Tensor");

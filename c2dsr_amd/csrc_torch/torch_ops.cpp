@@ -47,6 +47,18 @@ void sync_check(const char* name, const char* where) {
   TORCH_CHECK(e == hipSuccess, "device fault ", where, " ", name, " (hipError ", (int)e, ")");
 }
 
+static std::mutex g_err_mu;
+static std::vector<at::Tensor> g_err;  // per device index
+
+at::Tensor err_word() {
+  const int dev = (int)c10::hip::current_device();
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  if ((int)g_err.size() <= dev) g_err.resize(dev + 1);
+  if (!g_err[dev].defined())
+    g_err[dev] = at::zeros({4}, at::TensorOptions().dtype(at::kInt).device(at::Device(at::kCUDA, (int8_t)dev)));
+  return g_err[dev];
+}
+
 }  // namespace c2t
 
 #include "torch_ops_gen.inc"
@@ -87,6 +99,10 @@ op_timing_take() {
 
 static int64_t op_generated_count() { return C2DSR_GENERATED_COUNT; }
 
+// the current device's index error word itself (aliased, not a copy): the host clones it at a sync point, raises
+// IndexError when word 0 is nonzero and clears it (c2dsr_amd/trainer.py Trainer.check_index_errors)
+static at::Tensor op_error_word() { return c2t::err_word(); }
+
 TORCH_LIBRARY(c2dsr_raw, m) {
   C2DSR_GENERATED_DEFS(m)
   m.def("generated_count() -> int");
@@ -100,4 +116,5 @@ TORCH_LIBRARY_IMPL(c2dsr_raw, CompositeExplicitAutograd, m) {
 TORCH_LIBRARY_FRAGMENT(c2dsr, m) {
   m.def("timing_set(str[] names) -> ()", &op_timing_set);
   m.def("timing_take() -> (str[], float[], float[], int[])", &op_timing_take);
+  m.def("error_word() -> Tensor", &op_error_word);
 }

@@ -18,7 +18,7 @@ from __future__ import annotations
 import torch
 from torch.autograd import Function
 
-from ._lib import lib, stage_ops, stream
+from ._lib import error_word, lib, stage_ops, stream
 from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rg_kind, rgemm, weight_img, wg_kind, wgemm
 
 FUSED_HEAD = True  # the training step's loss head on the c2dsr:: stage operators (csrc_torch/losshead_ops.cpp)
@@ -285,7 +285,7 @@ class LossHeadFn(Function):
                 cnt = torch.empty(2, device=dev, dtype=torch.int32)
                 cws = torch.empty(lib.raw('c2dsr_compact_workspace')(M2, 1) // 4 + 1, device=dev,
                                   dtype=torch.int32)
-                lib('c2dsr_compact_valid', tcat, M2, BR, n, idx, inv, tc, cnt, cws, s)
+                lib('c2dsr_compact_valid', tcat, M2, BR, n, idx, inv, tc, cnt, cws, error_word(), s)
                 comp = (idx, inv, tc, cnt)
             pre.append((Hcat, Hpad, tcat, comp))
         if pre_given:  # deferred host read (ops.HostCounts), long since landed

@@ -148,7 +148,8 @@ class C2DSR(nn.Module):
         return self._dev_graphs
 
     def _shard(self):
-        if not self.gnn_shard or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() < 2:
+        from ..trainer import dp_enabled
+        if not self.gnn_shard or not dp_enabled():
             return None
         if self.row_shard is None:
             self.row_shard = ops.RowShard(dist.get_rank(), dist.get_world_size())

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 from torch.autograd import Function
 
-from ._lib import HipLibError, lib, stream, require_device, stage_ops
+from ._lib import HipLibError, error_word, lib, stream, require_device, stage_ops
 from .dp import notify_lookup, notify_rows, notify_table, row_cuts
 
 # precision modes: FP32 = the reference's precision (fp32 results; products on split-bf16 MFMAs where a kernel
@@ -452,15 +452,30 @@ def linear(x, W, b, precision=FP32, relu_drop=None, res=None, ff=None, ff_role=N
 
 
 # ----------------------------------------------------------------------------- row subsets
+# the bits of the device index error word (include/c2dsr.h C2DSR_IDX_ERR_*)
+IDX_ERR_ITEM, IDX_ERR_POS, IDX_ERR_PLAN, IDX_ERR_TARGET = 1, 2, 4, 8
+
+
+def index_error_message(bits):
+    """The IndexError text for an error word: torch's own F.embedding message plus which lookup failed."""
+    what = [n for b, n in ((IDX_ERR_ITEM, 'item index outside [0, n_item)'), (IDX_ERR_POS, 'position outside [0, len_max)'),
+                           (IDX_ERR_PLAN, 'lookup index outside its table'),
+                           (IDX_ERR_TARGET, 'target outside [0, n_item_x]')) if bits & b]
+    return 'index out of range in self (' + '; '.join(what or [f'error word {bits:#x}']) + ')'
+
+
 class HostCounts:
     """Small device int32 counts copied to pinned host memory behind the work that produces them, read
     on first use: the host blocks only if the device has not got that far yet, so the stream never
     drains the way an immediate ``.tolist()`` would make it."""
 
-    def __init__(self, dev_counts, known=None, check=False):
+    def __init__(self, dev_counts, known=None, check=False, err_slot=None):
         """known: the same counts computed on the host from the batch's host copy (Trainer.host_counts) — then
         nothing is copied and nothing ever waits on the device; check: also copy the device counts and compare
-        them with ``known`` at the first read (C2DSR_CHECK_COUNTS=1; raises on a mismatch)."""
+        them with ``known`` at the first read (C2DSR_CHECK_COUNTS=1; raises on a mismatch).  err_slot: the slot
+        holding the device's index error word after the batch's range checks (c2dsr::index_check, a batch without
+        a host copy): nonzero raises IndexError at the first read, before any backward or optimizer launch."""
+        self.err_slot = err_slot
         self.known = None if known is None else [int(v) for v in known]
         if self.known is not None and len(self.known) != dev_counts.numel():
             # counts prepared under other count_flags (model mode, seqs=None, …) would be read from wrong slots
@@ -476,6 +491,10 @@ class HostCounts:
         if self.vals is None:
             self.ev.synchronize()
             self.vals = self.host.tolist()
+            if self.err_slot is not None and self.vals[self.err_slot]:
+                bits, self.vals = self.vals[self.err_slot], None
+                error_word().zero_()
+                raise IndexError(index_error_message(bits))
             if self.known is not None and self.known != self.vals:
                 raise RuntimeError(f'host-computed counts {self.known} != device counts {self.vals}')
         return self.vals[i]
@@ -635,7 +654,8 @@ class GCNFn(Function):
         rows = None
         if shard is None or n_gnn == 0:  # the whole table: one stage operator (all rounds)
             work, _, split, _, n_slots, col, val = graph.plan(False)
-            out = stage_ops().gcn_propagate(E, work, split, col, val, n_slots, n_gnn, float(p), flat_keys(keys))
+            out = stage_ops().gcn_propagate(E, work, split, col, val, graph.n, n_slots, n_gnn, float(p),
+                                            flat_keys(keys))
             ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
             ctx.E = E
             ctx.mark_non_differentiable(out)
@@ -682,11 +702,11 @@ class GCNFn(Function):
         work, _, split, _, n_slots, col, val = g.plan(True)
         p = float(ctx.p)
         # gE += drop(Aᵀ T_1)/… + G/(n+1) + [i != pad]·G  (rounds before the last: T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k)
-        X = T.gcn_backward_rounds(G, work, split, col, val, n_slots, n, p, flat_keys(ctx.keys)) if n > 1 else G
+        X = T.gcn_backward_rounds(G, work, split, col, val, g.n, n_slots, n, p, flat_keys(ctx.keys)) if n > 1 else G
         k0, k1 = ctx.keys[0] if n > 0 else (0, 0)
         cuts = row_cuts(ctx.sink.state, E) if direct and n > 0 else None
         if cuts is None:
-            T.gcn_backward_final(X, G, gE, work, split, col, val, n_slots, n, p, k0, k1, ctx.pad_row, 1.0, 1.0)
+            T.gcn_backward_final(X, G, gE, work, split, col, val, g.n, n_slots, n, p, k0, k1, ctx.pad_row, 1.0, 1.0)
         else:  # this table's gradient is final chunk by chunk: its collectives start per chunk (dp.py)
             part = torch.empty(max(n_slots, 1), G.shape[1], device=G.device, dtype=torch.float32)
             for r0, r1 in cuts:
@@ -694,7 +714,7 @@ class GCNFn(Function):
                 if w1 > w0:  # roofline accounting of a row-slice launch (bench.py HbmTimer): its rows and edges
                     rp = g.host_rowptr(True)
                     SPMM_SLICE[work[w0:w1].data_ptr()] = (r1 - r0, int(rp[r1]) - int(rp[r0]))
-                T.gcn_backward_final(X, G, gE, work[w0:w1], split[s0:s1], col, val, n_slots, n, p, k0, k1,
+                T.gcn_backward_final(X, G, gE, work[w0:w1], split[s0:s1], col, val, g.n, n_slots, n, p, k0, k1,
                                      ctx.pad_row, 1.0, 1.0, part)
                 notify_rows(ctx.sink.state, E, r0, r1)
         ctx.sink.G = None
@@ -712,7 +732,7 @@ class GCNPropFn(Function):
     def forward(ctx, E, graph, n_gnn, p, keys):
         require_device(E)
         work, _, split, _, n_slots, col, val = graph.plan(False)
-        out = stage_ops().gcn_propagate(E.contiguous(), work, split, col, val, n_slots, n_gnn, float(p),
+        out = stage_ops().gcn_propagate(E.contiguous(), work, split, col, val, graph.n, n_slots, n_gnn, float(p),
                                         flat_keys(keys))
         ctx.graph, ctx.n_gnn, ctx.p, ctx.keys = graph, n_gnn, p, keys
         return out
@@ -726,9 +746,11 @@ class GCNPropFn(Function):
         T = stage_ops()
         work, _, split, _, n_slots, col, val = ctx.graph.plan(True)
         p = float(ctx.p)
-        X = T.gcn_backward_rounds(G, work, split, col, val, n_slots, n, p, flat_keys(ctx.keys)) if n > 1 else G
+        X = T.gcn_backward_rounds(G, work, split, col, val, ctx.graph.n, n_slots, n, p, flat_keys(ctx.keys)) \
+            if n > 1 else G
         gE = torch.empty_like(G)  # the pure gradient: no lookup term, nothing accumulated
-        T.gcn_backward_final(X, G, gE, work, split, col, val, n_slots, n, p, ctx.keys[0][0], ctx.keys[0][1], -1, 0.0,
+        T.gcn_backward_final(X, G, gE, work, split, col, val, ctx.graph.n, n_slots, n, p, ctx.keys[0][0],
+                             ctx.keys[0][1], -1, 0.0,
                              0.0)
         return gE, None, None, None, None
 
@@ -810,22 +832,24 @@ def _check_err(ws, off, name):
         raise HipLibError(f'{name}: inconsistent plan skipped on the device (error word {err:#x})')
 
 
-def _check_plan(buf, idx, n_keys, seg_ch=32):
-    """Debug (C2DSR_CHECK_PLANS=1): the plan against a host restatement (sorted keys, rows, split list)
-    before any kernel consumes it."""
+def _check_plan(buf, idx, n_keys, seg_ch=16, subp=128):
+    """Debug (C2DSR_CHECK_PLANS=1) and tests: the plan against a host restatement (sorted keys, rows, split list,
+    the splits' SUBP-piece sub-ranges; csrc/embed.hip plan_layout) before any kernel consumes it.  An index outside
+    [0, n_keys) is the key n_keys in the plan (sorted last; csrc/embed.hip prep_keys_kernel)."""
     import numpy as np
     torch.cuda.synchronize()
     b = buf.cpu().numpy()
     x = idx.reshape(-1).cpu().numpy().astype(np.int64)
     n = x.size
     a = lambda v: (v + 255) // 256 * 256  # noqa: E731
-    if n and (x.min() < 0 or x.max() >= n_keys):
-        raise HipLibError(f'index plan: keys outside [0, {n_keys}): {x.min()}..{x.max()}')
+    x = np.where((x >= 0) & (x < n_keys), x, n_keys)
     order = np.argsort(x, kind='stable')
     K = x[order]
     o_v = a(4 * n)
     o_sp = o_v + a(4 * n)
     o_ct = o_sp + a(16 * (n // seg_ch + 1))
+    o_so = o_ct + a(16)
+    o_sb = o_so + a(4 * (n // seg_ch + 2))
     cnt = b[o_ct:o_ct + 16].view(np.int32)
     errs = []
     if not np.array_equal(b[:4 * n].view(np.uint32), K.astype(np.uint32)):
@@ -839,12 +863,27 @@ def _check_plan(buf, idx, n_keys, seg_ch=32):
             if ce < n and K[ce] == K[i]:
                 end = int(np.searchsorted(K, K[i], side='right'))
                 ref.append((K[i], i // seg_ch, (end - 1) // seg_ch - i // seg_ch + 1, 0))
+    ref_so, ref_sb = [], []
+    for j, (_, _, span, _) in enumerate(ref):
+        ref_so.append(len(ref_sb))
+        ref_sb += [(j, y * subp) for y in range(-(-span // subp))]
+    ref_so.append(len(ref_sb))
     if int(cnt[1]) != len(ref):
         errs.append(f'splits {int(cnt[1])} != {len(ref)}')
     elif ref:
         got = b[o_sp:o_sp + 16 * len(ref)].view(np.int32).reshape(-1, 4)
         if not np.array_equal(got, np.array(ref, dtype=np.int32).reshape(-1, 4)):
             errs.append('split list')
+    if int(cnt[2]) != len(ref_sb):
+        errs.append(f'subs {int(cnt[2])} != {len(ref_sb)}')
+    else:
+        if not np.array_equal(b[o_so:o_so + 4 * len(ref_so)].view(np.int32), np.array(ref_so, dtype=np.int32)):
+            errs.append('sub offsets')
+        if ref_sb and not np.array_equal(b[o_sb:o_sb + 8 * len(ref_sb)].view(np.int32).reshape(-1, 2),
+                                         np.array(ref_sb, dtype=np.int32).reshape(-1, 2)):
+            errs.append('sub list')
+    if int(cnt[3]) != 0:
+        errs.append(f'error word {int(cnt[3]):#x}')
     if errs:
         raise HipLibError(f'index plan mismatch (n={n}, n_keys={n_keys}): {errs}')
 
@@ -1089,7 +1128,7 @@ class PosDropFn(Function):
         B, L, d = xin.shape
         x = torch.empty_like(xin)
         lib('c2dsr_embed_fwd', pos, pos, B * L, d, None, None, xin, P, 1.0, keys[0], keys[1], float(p),
-            int(row_base) * L, x, stream())
+            int(row_base) * L, x, 0, P.shape[0], error_word(), stream())
         ctx.save_for_backward(pos)
         ctx.p, ctx.keys, ctx.row_base, ctx.P = p, keys, row_base, P
         return x
@@ -1124,7 +1163,8 @@ class PosAddFn(Function):
     def forward(ctx, xin, P, pos):
         require_device(xin)
         B, L, d = xin.shape
-        lib('c2dsr_embed_fwd', pos, pos, B * L, d, None, None, xin, P, 1.0, 0, 0, 0.0, 0, xin, stream())
+        lib('c2dsr_embed_fwd', pos, pos, B * L, d, None, None, xin, P, 1.0, 0, 0, 0.0, 0, xin, 0, P.shape[0],
+            error_word(), stream())
         ctx.mark_dirty(xin)
         ctx.save_for_backward(pos)
         ctx.P = P

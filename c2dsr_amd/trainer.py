@@ -23,7 +23,7 @@ import torch.distributed as dist
 from .dataloader import get_dataloader
 from . import dropout as DK
 from . import ops
-from ._lib import lib, stage_ops, stream
+from ._lib import error_word, lib, stage_ops, stream
 from .dp import CommPlan, DPComm, Zero1
 from .graph import make_graph
 from .losshead import LossHeadFn, LossMeta, ce_kind
@@ -48,10 +48,37 @@ def dp_rows(B_full, rank, world, dp_split=True, global_rows=None):
     return 0, B_full, rank * B_full if world > 1 else 0, B_global
 
 
+def dp_forced():
+    """C2DSR_DP_FORCE=1: a process group of ONE rank still runs the data-parallel step (the collectives of dp.py,
+    ZeRO-1, the row-sharded GCN) — how a one-GPU box exercises RCCL itself (tests/test_gpu_rccl.py)."""
+    return os.environ.get('C2DSR_DP_FORCE', '0') == '1'
+
+
+def dp_enabled():
+    """Whether the step is data parallel: a process group with more than one rank (or one, forced)."""
+    return bool(dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or dp_forced()))
+
+
 def dp_info():
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dp_enabled():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def device_identity(dev):
+    """A string naming the physical device behind ``dev`` on this host: hostname + PCI domain:bus:device + UUID.
+    Two ranks with the same identity share one GPU, whatever their HIP_VISIBLE_DEVICES renumbering says."""
+    import socket
+    pr = torch.cuda.get_device_properties(dev)
+    pci = ':'.join(str(getattr(pr, k, '?')) for k in ('pci_domain_id', 'pci_bus_id', 'pci_device_id'))
+    return f'{socket.gethostname()}|{pci}|{getattr(pr, "uuid", "")}'
+
+
+def dp_backend(identities, rank):
+    """'nccl' (RCCL) when every rank drives its own GPU, 'gloo' when some ranks share one (RCCL refuses two
+    ranks on one device: the one-GPU rehearsal).  ``identities``: device_identity() of every rank, in rank order;
+    the rule is global, so every rank reaches the same backend."""
+    return 'gloo' if len(set(identities)) < len(identities) else 'nccl'
 
 
 def init_data_parallel(args):
@@ -62,14 +89,16 @@ def init_data_parallel(args):
     says WORLD_SIZE > 1 and no process group exists yet, this runs before the trainer's first device call:
       * the rank's device is ``cuda:LOCAL_RANK`` (``args.device`` is overwritten — main.py's value is the same
         device on every rank), ``torch.cuda.set_device`` makes it current;
-      * the process group is RCCL (``'nccl'``, bound to that device) when the node has a device per local rank;
-        on a node with fewer devices than local ranks (the one-GPU rehearsal) ranks share devices round-robin
-        and the group is gloo, since RCCL refuses two ranks on one device; ``--cuda cpu`` gives gloo on the host
-        (the product path then stops at its first kernel: there is no CPU fallback).
+      * the process group is RCCL (``'nccl'``, bound to that device) when every rank drives its own GPU, decided
+        from the ranks' physical device identities (PCI address + UUID, exchanged over the launcher's rendezvous
+        store before the group exists) — NOT from the local device count, which is 1 on a node whose launcher
+        gives each rank its own HIP_VISIBLE_DEVICES; only when ranks really share a device (the one-GPU
+        rehearsal) is the group gloo, with a warning, since RCCL refuses two ranks on one device; ``--cuda cpu``
+        gives gloo on the host (the product path then stops at its first kernel: there is no CPU fallback).
     ``C2DSR_DP_BACKEND`` overrides the backend.  Returns (rank, world) — (0, 1) outside a launcher; a process
     group the caller initialised itself is used as it is."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    if world <= 1 or not dist.is_available() or dist.is_initialized():
+    if (world <= 1 and not dp_forced()) or not dist.is_available() or dist.is_initialized():
         return dp_info()
     rank = int(os.environ['RANK'])
     local = int(os.environ.get('LOCAL_RANK', rank))
@@ -77,19 +106,29 @@ def init_data_parallel(args):
     backend = os.environ.get('C2DSR_DP_BACKEND')
     dev = torch.device(getattr(args, 'device', 'cpu'))
     kw = {}
+    # the launcher's rendezvous store (MASTER_ADDR / MASTER_PORT, or torchrun's agent store): used for the device
+    # exchange below and then handed to the process group, so there is one rendezvous
+    store, _, _ = next(dist.rendezvous('env://', rank, world))
     if dev.type == 'cuda':
         n_dev = torch.cuda.device_count()  # counts devices without initialising the runtime
         if n_dev < 1:
             raise RuntimeError('data parallel on cuda: no visible device')
         dev = torch.device('cuda', local % n_dev)
-        backend = backend or ('nccl' if n_dev >= local_world else 'gloo')
         torch.cuda.set_device(dev)
+        if backend is None:
+            store.set(f'c2dsr/device/{rank}', device_identity(dev))
+            ids = [store.get(f'c2dsr/device/{r}').decode() for r in range(world)]
+            backend = dp_backend(ids, rank)
+            if backend == 'gloo':
+                print(f'[c2dsr] WARNING: ranks share a GPU ({ids[rank]}, {n_dev} visible device(s) for '
+                      f'{local_world} local ranks): gloo with host staging instead of RCCL', file=sys.stderr,
+                      flush=True)
         if backend == 'nccl':
             kw['device_id'] = dev
     else:
         backend = backend or 'gloo'
     args.device = dev
-    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    dist.init_process_group(backend, store=store, rank=rank, world_size=world, **kw)
     print(f'[c2dsr] data parallel: rank {rank}/{world} on {dev} ({backend})', file=sys.stderr, flush=True)
     return rank, world
 
@@ -108,10 +147,11 @@ class Trainer(object):
         self.adj_share, self.adj_specific = graphs
         self.model = C2DSR(args, self.adj_share, self.adj_specific).to(args.device)
         self.rank, self.world = dp_info()
+        self.dp = dp_enabled()
         # one device: the backward accumulates straight into the epoch accumulation (no per-step buffer)
-        self.model.flatten(align=4 * self.world, direct=self.world == 1)
+        self.model.flatten(align=4 * self.world, direct=not self.dp)
         self.comm_plan, self.zero = None, None
-        if self.world > 1:
+        if self.dp:
             m = self.model
             head = [m.classifier_a.weight, m.classifier_a.bias, m.classifier_b.weight, m.classifier_b.bias,
                     m.classifier_pad.weight, m.classifier_pad.bias, m.D_a.weight, m.D_b.weight]
@@ -146,6 +186,8 @@ class Trainer(object):
         # own counts are checked against them with C2DSR_CHECK_COUNTS=1
         self.host_counts_ok = True
         self.check_counts = os.environ.get('C2DSR_CHECK_COUNTS', '0') == '1'
+        if torch.device(self.device).type == 'cuda':
+            error_word().zero_()  # a fresh trainer starts with no index error pending on its device
 
     # ------------------------------------------------------------------ training
     def run_epoch(self):
@@ -158,6 +200,7 @@ class Trainer(object):
             loss, loss_rec, loss_mi = self.train_batch(batch)
             acc += torch.stack([loss.detach(), loss_rec, loss_mi]) * batch[0].shape[0]  # one sync per epoch (f4)
         acc = (acc / max(self.n_tr, 1)).tolist()
+        self.check_index_errors()  # after the epoch's one sync: free
         if self.noter is not None:
             self.noter.log_train(acc[0], acc[1], acc[2], time.time() - t0)
         self.model.eval()
@@ -170,6 +213,58 @@ class Trainer(object):
         with torch.no_grad():
             return self._evaluate(self.testloader)
 
+    # ------------------------------------------------------------------ index errors (F.embedding / cross_entropy raise)
+    def check_batch_indices(self, hb):
+        """The reference's lookups raise IndexError on an index outside their table (F.embedding / nn.Embedding,
+        models/C2DSR.py:65-67,81, encoders.py:30; F.cross_entropy on a target outside [0, n_item_x] other than the
+        ignore index, trainer.py:143-152) before anything is updated.  With the batch's host copy ``hb`` (numpy, batch
+        order) the same check runs here, before a launch; without one, the device checks (prepare)."""
+        (seq_share, seq_a, seq_b, pos, pos_a, pos_b, gt_share_a, gt_share_b, gt_a, gt_b, _, _, neg_a, neg_b) = hb
+        m = self.model
+        R = self.len_rec
+        bits = 0
+        for x in (seq_share, seq_a, seq_b, neg_a, neg_b):
+            if x.size and (x.min() < 0 or x.max() >= m.n_item):
+                bits |= ops.IDX_ERR_ITEM
+        for x in (pos, pos_a, pos_b):
+            if x.size and (x.min() < 0 or x.max() >= m.attn_share.len_max):
+                bits |= ops.IDX_ERR_POS
+        for x, n in ((gt_share_a, self.n_item_a), (gt_a, self.n_item_a), (gt_share_b, self.n_item_b),
+                     (gt_b, self.n_item_b)):
+            t = x[:, -R:]  # the reference reads the last len_rec targets only (trainer.py:126-129)
+            if t.size and (t.min() < 0 or t.max() > n):
+                bits |= ops.IDX_ERR_TARGET
+        if bits:
+            raise IndexError(ops.index_error_message(bits))
+
+    def device_index_check(self, batch_dev):
+        """c2dsr::index_check over the step's index tensors (device batch, no host copy): returns the error word
+        copied after the checks (int32 [1]) for the step's deferred count read (ops.HostCounts err_slot)."""
+        (seq_share, seq_a, seq_b, pos, pos_a, pos_b, gt_share_a, gt_share_b, gt_a, gt_b, _, _, neg_a, neg_b) = batch_dev
+        m = self.model
+        L, R = seq_share.shape[1], self.len_rec
+        items = [seq_share, seq_a, seq_b, neg_a, neg_b]
+        poss = [pos, pos_a, pos_b]
+        tg = [(gt_share_a, self.n_item_a), (gt_a, self.n_item_a), (gt_share_b, self.n_item_b), (gt_b, self.n_item_b)]
+        idx = items + poss + [t for t, _ in tg]
+        hi = [m.n_item] * 5 + [m.attn_share.len_max] * 3 + [n + 1 for _, n in tg]
+        cols = [L] * 8 + [min(R, L)] * 4
+        bits = [ops.IDX_ERR_ITEM] * 5 + [ops.IDX_ERR_POS] * 3 + [ops.IDX_ERR_TARGET] * 4
+        return stage_ops().index_check(idx, hi, cols, bits)
+
+    def check_index_errors(self):
+        """Raise IndexError if a lookup of a step since the last check met an index outside its table (the device
+        error word of include/c2dsr.h: the kernels read row 0 instead and flag it, the segment sums skip the key,
+        and AdamW changes nothing while it is set).  run_epoch calls it at its one host sync; a caller driving
+        train_batch on device batches without a host copy calls it at its own."""
+        if torch.device(self.device).type != 'cuda':
+            return
+        w = error_word()
+        bits = int(w[0])
+        if bits:
+            w.zero_()
+            raise IndexError(ops.index_error_message(bits))
+
     def cal_mask(self, gt_mask):
         """trainer.py:85-89 (API compatibility; the fused loss head computes the weights itself)."""
         m = gt_mask.float()
@@ -179,7 +274,7 @@ class Trainer(object):
     def loss_meta(self, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global):
         m = self.model
         allreduce = None
-        if self.world > 1:
+        if self.dp:
             allreduce = lambda v: dist.all_reduce(v)  # noqa: E731
         return LossMeta(gt_share_a=gt_share_a, gt_share_b=gt_share_b, gt_a=gt_a, gt_b=gt_b, gm_a=gm_a, gm_b=gm_b,
                         n_a=self.n_item_a, n_b=self.n_item_b, R=self.len_rec, lam=self.lambda_loss,
@@ -232,10 +327,12 @@ class Trainer(object):
         timed steps) and hands them to train_batch(counts=...)."""
         lo, hi, _, _ = dp_rows(host[0].shape[0], self.rank, self.world, self.dp_split, global_rows)
         hb = tuple(np.asarray(x[lo:hi]) for x in host)
+        self.check_batch_indices(hb)  # counts handed to train_batch come with a validated batch
         need, pads, ce = self.count_flags(hb[0].shape[1])
         return self.host_counts(hb, need=need, pads=pads, ce=ce)
 
-    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b, seqs=None, host=None, known=None):
+    def prepare(self, gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b, seqs=None, host=None, known=None,
+                batch_dev=None):
         """Index work the step sizes its launches by, enqueued ahead of the forward with one deferred host
         read of all its counts (ops.HostCounts; nothing waits until the first count is needed):
           * RowSets of the five encoder passes (c2dsr_need_rows), so the last encoder layer runs its
@@ -279,7 +376,7 @@ class Trainer(object):
                 tcat, idx_c, inv_c, tc, cnt = out[o + 5 * k:o + 5 * k + 5]
                 ce.append((tcat, idx_c, inv_c, tc))
                 counts.append(cnt)
-        if self.world > 1:
+        if self.dp:
             s = stream()
             # the global valid-target counts — all the gradient's normalisation needs (trainer.py:143-156,
             # SURVEY.md §8(e)) — reduced ahead of the forward, overlapped with it
@@ -299,7 +396,13 @@ class Trainer(object):
             known = None
         elif known is None and host is not None:
             known = self.host_counts(host, need=need_sets is not None, pads=pad_sets is not None, ce=ce is not None)
-        hc = ops.HostCounts(torch.cat(counts), known=known, check=self.check_counts)
+        err_slot = None
+        if known is None and host is None and batch_dev is not None:
+            # no host copy: the batch's indices are range-checked on the device and the verdict rides on the
+            # count read the step makes anyway (raises IndexError there, before any backward / optimizer launch)
+            counts.append(self.device_index_check(batch_dev))
+            err_slot = sum(int(c.numel()) for c in counts) - 1
+        hc = ops.HostCounts(torch.cat(counts), known=known, check=self.check_counts, err_slot=err_slot)
         need, pads = {}, {}
         base = 0
         for sets, out in ((need_sets, need), (pad_sets, pads)):
@@ -337,13 +440,16 @@ class Trainer(object):
         hb = None
         if host is not None and counts is None:
             hb = tuple(np.asarray(x[lo:hi]) for x in host)
+            self.check_batch_indices(hb)  # IndexError before anything is enqueued, as the reference's lookups raise
+        dev_batch = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
         (seq_share, seq_a, seq_b, pos, pos_a, pos_b, gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, neg_a,
-         neg_b) = [x[lo:hi].to(self.device, non_blocking=True) for x in batch]
+         neg_b) = dev_batch
         m = self.model
         m.state.row_offset = row_offset
         self.dp_counts = None
         need, pads, ce_pre = self.prepare(gm_a, gm_b, gt_share_a, gt_a, gt_share_b, gt_b,
-                                          (seq_share, seq_a, seq_b, neg_a, neg_b), host=hb, known=counts)
+                                          (seq_share, seq_a, seq_b, neg_a, neg_b), host=hb, known=counts,
+                                          batch_dev=dev_batch)
         # the GCN forwards of convolve_graph() are enqueued now, behind the index work (and its count copy when the
         # counts are not known on the host: the host then reads them while the device runs the propagations)
         m.launch_graph()
@@ -372,7 +478,7 @@ class Trainer(object):
         if need:  # the five encoder outputs hold only these rows
             meta.row_sets = tuple(need[pid] for pid, _ in self.PASS_ROWS)
         loss, loss_rec, loss_mi = LossHeadFn.apply(h_share, hx, hy, h_neg_a, h_neg_b, meta)
-        if self.world > 1:
+        if self.dp:
             # the fresh gradient's collectives, each range issued as soon as the backward has made it final
             # (c2dsr_amd/dp.py): dense params under the GCN backwards, each item table per row chunk of its
             # last GCN backward; all-reduce, or reduce-scatter with ZeRO-1
@@ -429,7 +535,9 @@ class Trainer(object):
         """trainer.py:162-181: rank of the ground truth among its sampled negatives (ties not counted:
         rank = #(neg > gt) + 1), split by the domain of the last item, rows in batch order."""
         rank, flag = self.eval_ranks(batch)
-        return self._split([rank], [flag])
+        out = self._split([rank], [flag])
+        self.check_index_errors()  # the sequences' lookups (after _split's sync)
+        return out
 
     def _evaluate(self, loader):
         ranks, flags = [], []
@@ -437,7 +545,9 @@ class Trainer(object):
             rank, flag = self.eval_ranks(batch)
             ranks.append(rank)
             flags.append(flag)
-        return self._split(ranks, flags)  # one host sync per evaluation pass
+        out = self._split(ranks, flags)  # one host sync per evaluation pass
+        self.check_index_errors()  # the sequences' lookups
+        return out
 
     def evaluate_metrics(self, loader):
         """Metrics of a whole evaluation pass on the device (cal_metrics per domain, one host sync):

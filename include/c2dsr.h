@@ -6,7 +6,8 @@
  * entry point below replaces the ATen work of one reference site (cited per
  * function); the host-side mirror of the reference's module API
  * (c2dsr_amd/models/C2DSR.py, c2dsr_amd/models/encoders.py, c2dsr_amd/trainer.py)
- * binds them through ctypes (c2dsr_amd/_lib.py).  See INTEGRATION.md.
+ * reaches them through the PyTorch-ROCm operator library libc2dsr_torch.so (TORCH_LIBRARY c2dsr / c2dsr_raw,
+ * c2dsr_amd/csrc_torch/).  See INTEGRATION.md.
  *
  * Conventions: plain device pointers (fp32 unless stated, int64 index tensors as
  * the reference's LongTensors), row-major, sizes as ints; `stream` is a
@@ -47,24 +48,40 @@ int c2dsr_gcn_spmm_b16(const int* work, int n_work, const int* split, int n_spli
 /* K2 embedding fuse.  Replaces models/C2DSR.py:65-71,81-82 + models/encoders.py:30-31:
  *   X[r] = drop((H[seq[r]] + E[seq[r]])·scale + P[pos[r]])      (Xin == NULL)
  *   X[r] = drop(Xin[r] + P[pos[r]])                              (Xin != NULL: SelfAttention.forward)
- * dropout index (idx_base + r)·d + c. */
+ * dropout index (idx_base + r)·d + c.
+ * Index contract (F.embedding raises IndexError outside [0, N)): seq[r] must lie in [0, n_items) (H / E have
+ * n_items rows; unused when Xin != NULL) and pos[r] in [0, n_pos).  An index outside sets C2DSR_IDX_ERR_ITEM /
+ * C2DSR_IDX_ERR_POS in *err (atomic OR; err may be NULL) and row 0 is read instead: no load leaves the tables.
+ * The caller reads the word at its next host sync and raises (c2dsr_amd/trainer.py check_index_errors). */
+#define C2DSR_IDX_ERR_ITEM 1   /* an item index (seq / negative sequence) outside [0, n_items) */
+#define C2DSR_IDX_ERR_POS 2    /* a position outside [0, n_pos) */
+#define C2DSR_IDX_ERR_PLAN 4   /* an index-plan key outside [0, n_keys) (never followed by the segment sums) */
+#define C2DSR_IDX_ERR_TARGET 8 /* a classifier target outside [0, n_items] (n_items = ignore_index) */
 int c2dsr_embed_fwd(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H, const float* E,
                     const float* Xin, const float* P, float scale, uint32_t k0, uint32_t k1, float p,
-                    int64_t idx_base, float* X, void* stream);
+                    int64_t idx_base, float* X, int n_items, int n_pos, int* err, void* stream);
 /* The gather form on chosen rows only (the row-subset encoder layer of a training pass, c2dsr::encoder_pass): output
  * row k = the row above for input row q_idx[k] (k < nq) or k_idx[k - nq] (its query rows, then its padding-key rows),
  * dropout index (idx_base + input row)·d + c; X [nq + nk, d] — the [n_rows, d] embedding is never stored.
  * Replaces the same sites as c2dsr_embed_fwd (models/C2DSR.py:65-71, encoders.py:30-31). */
 int c2dsr_embed_fwd_rows(const int64_t* seq, const int64_t* pos, int n_rows, int d, const float* H, const float* E,
                          const float* P, float scale, uint32_t k0, uint32_t k1, float p, int64_t idx_base,
-                         const int* q_idx, int nq, const int* k_idx, int nk, float* X, void* stream);
+                         const int* q_idx, int nq, const int* k_idx, int nk, float* X, int n_items, int n_pos,
+                         int* err, void* stream);
 size_t c2dsr_embed_bwd_workspace(int n_rows, int d);
+/* Range check of a batch's index tensor on the device (a training step whose batch has no host copy; with one,
+ * the host checks it before anything is enqueued): err |= bit if any idx[r·ld + ld - cols + c] (r < rows, c < cols:
+ * the last `cols` columns of each row) lies outside [0, hi).  Reference: F.embedding / nn.Embedding / F.cross_entropy
+ * raise IndexError (models/C2DSR.py:65-67,81, encoders.py:30, trainer.py:143-152). */
+int c2dsr_index_check(const int64_t* idx, long rows, int ld, int cols, int64_t hi, int bit, int* err, void* stream);
 /* Sort plan of an index array (stable LSD radix sort; depends on the indices only, so it is built
  * on a side stream under the forward pass): plan = [keys u32 n | rows u32 n | scratch], keys
  * ascending, rows ascending within equal keys.  Replaces the sort inside embedding_dense_backward
  * (the deterministic path of F.embedding's backward, models/C2DSR.py:65). */
 size_t c2dsr_index_plan_bytes(int n);
-int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, size_t plan_bytes, void* stream);
+/* An index outside [0, n_keys) becomes the key n_keys (sorted last, never followed by a segment sum) and sets
+ * C2DSR_IDX_ERR_PLAN in *err (err may be NULL). */
+int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, size_t plan_bytes, int* err, void* stream);
 /* c2dsr_embed_bwd on prebuilt plans of seq / pos (seq_plan needed iff G, pos_plan iff gP); the item
  * and position sums share one launch of each pass.  A plan whose keys fall outside [0, n_items) /
  * [0, n_pos) or whose split lists are inconsistent is not followed: the int at
@@ -78,7 +95,7 @@ int c2dsr_embed_bwd_planned(const void* seq_plan, const void* pos_plan, int n_ro
  * read-modify-write a bf16 G (fp32 sums, RNE stores).  P, X, gX and gP stay fp32. */
 int c2dsr_embed_fwd_b16(const int64_t* seq, const int64_t* pos, int n_rows, int d, const void* H, const void* E,
                         const float* P, float scale, uint32_t k0, uint32_t k1, float p, int64_t idx_base, float* X,
-                        void* stream);
+                        int n_items, int n_pos, int* err, void* stream);
 int c2dsr_embed_bwd_planned_b16(const void* seq_plan, const void* pos_plan, int n_rows, int d, const float* gX,
                                 uint32_t k0, uint32_t k1, float p, int64_t idx_base, float scale, void* G, int n_items,
                                 float* gP, int n_pos, void* workspace, size_t ws_bytes, void* stream);
@@ -189,10 +206,11 @@ int c2dsr_pool2_bwd(const float* d1, const float* w1, const float* d2, const flo
  * Valid-row compaction of a classifier head's targets (trainer.py:131-154: rows whose target is the
  * ignore_index contribute nothing to the loss or any gradient, so the fused CE runs on the valid
  * rows only): idx[k] = k-th row with t != ignore, inv[r] = compact index or -1, tc[k] = t[idx[k]],
- * counts[0..1] = valid rows in [0, split) and [split, M). */
+ * counts[0..1] = valid rows in [0, split) and [split, M).  A target outside [0, ignore] (F.cross_entropy raises
+ * IndexError) sets C2DSR_IDX_ERR_TARGET in *err (err may be NULL) and its row is not valid. */
 size_t c2dsr_compact_workspace(int M, int n_sets);
 int c2dsr_compact_valid(const int64_t* t, int M, int split, int ignore, int* idx, int* inv, int64_t* tc, int* counts,
-                        int* ws, void* stream);
+                        int* ws, int* err, void* stream);
 /* Rows of the encoder passes the loss reads (trainer.py:101-154), n_sets <= 8 at once: set q's code is
  * (bits >> 3q) & 7 — 1 / 2 = positions with gm_a / gm_b nonzero (the pass's pooling weights), 4 = the
  * last R positions (classifier heads).  idx / inv of set q at offset q·B·L: idx[k] = k-th needed row,
@@ -343,9 +361,10 @@ int c2dsr_selftest_tr(int rr0, int kb0, short* out, void* stream);
 
 /* K6 AdamW(amsgrad) over flat buffers, folding the fresh grad into the epoch accumulator
  * (trainer.py:21-22,42,158); accum == fresh: the backward accumulated into the epoch accumulator
- * directly (one device) and it is only read. */
+ * directly (one device) and it is only read.  err (may be NULL): the step's index error word — when it is
+ * nonzero the launch changes nothing (the reference raises IndexError before its optimizer step). */
 int c2dsr_adamw(float* p, float* fresh, float* accum, float* m, float* v, float* vmax, long n, float lr, float wd,
-                float b1, float b2, float eps, int step, void* stream);
+                float b1, float b2, float eps, int step, const int* err, void* stream);
 
 
 /* K3 projections, row-streaming bf16 MFMA (csrc/rgemm.hip).  Replaces the addmm/mm of

@@ -75,3 +75,18 @@ def test_init_data_parallel_outside_a_launcher_is_a_no_op(monkeypatch):
     args = SimpleNamespace(device=torch.device('cuda:3'))
     assert init_data_parallel(args) == (0, 1)
     assert args.device == torch.device('cuda:3')  # main.py's single-process device is kept
+
+
+def test_dp_backend_from_device_identities():
+    """the backend follows the ranks' physical devices, not the local device count — a launcher
+    that gives every rank its own HIP_VISIBLE_DEVICES leaves each rank one visible device, yet each drives its own
+    GPU (RCCL); only ranks that really share a GPU fall back to gloo, and every rank reaches the same answer."""
+    from c2dsr_amd.trainer import dp_backend
+    own = [f'node0|0:{b}:0|uuid{b}' for b in (3, 4, 5, 6)]
+    assert all(dp_backend(own, r) == 'nccl' for r in range(4))
+    shared = ['node0|0:3:0|u', 'node0|0:3:0|u']
+    assert all(dp_backend(shared, r) == 'gloo' for r in range(2))
+    mixed = ['node0|0:3:0|u', 'node0|0:3:0|u', 'node0|0:4:0|v']
+    assert {dp_backend(mixed, r) for r in range(3)} == {'gloo'}
+    # the same bus number on two hosts is two GPUs
+    assert dp_backend(['a|0:3:0|u', 'b|0:3:0|u'], 0) == 'nccl'

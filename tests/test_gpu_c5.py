@@ -160,8 +160,10 @@ def test_c5_bf16_table_kernels_match_fp32():
     Hr = H16.float()
     for k, (seq, pos) in enumerate(passes):
         x16, x32 = torch.empty(B, L, d, device=DEV), torch.empty(B, L, d, device=DEV)
-        lib('c2dsr_embed_fwd_b16', seq, pos, B * L, d, H16, E16, P, math.sqrt(d), 5, k, p, 0, x16, stream())
-        lib('c2dsr_embed_fwd', seq, pos, B * L, d, Hr, E32, None, P, math.sqrt(d), 5, k, p, 0, x32, stream())
+        lib('c2dsr_embed_fwd_b16', seq, pos, B * L, d, H16, E16, P, math.sqrt(d), 5, k, p, 0, x16, N, L, None,
+            stream())
+        lib('c2dsr_embed_fwd', seq, pos, B * L, d, Hr, E32, None, P, math.sqrt(d), 5, k, p, 0, x32, N, L, None,
+            stream())
         assert torch.equal(x16, x32), f'gather on bf16 tables, pass {k}'
     gx = torch.empty(B, L, d, device=DEV).normal_(0.0, 1.0)
     G16, G32 = torch.zeros_like(E16), torch.zeros_like(E32)

@@ -116,7 +116,7 @@ def test_embed_fwd_bwd_deterministic(d, n_items, n_rows, p):
     X = torch.empty(n_rows, d, device=DEV)
     sd, pd = torch.from_numpy(seq).to(DEV), torch.from_numpy(pos).to(DEV)
     lib('c2dsr_embed_fwd', sd, pd, n_rows, d, H.to(DEV), E.to(DEV), None, P.to(DEV), scale, keys[0], keys[1], p, 77,
-        X, stream())
+        X, n_items, L, None, stream())
     idx = (np.arange(n_rows)[:, None] + 77) * d + np.arange(d)[None, :]
     mk = torch.from_numpy(keep_mask(idx, keys, p).astype(np.float32)) / (1 - p)
     ref = ((H[seq] + E[seq]) * scale + P[pos]) * mk
@@ -303,7 +303,7 @@ def test_adamw_kernel_vs_oracle():
         g = torch.randn(n)
         acc_ref += g
         fresh.copy_(g.to(DEV))
-        lib('c2dsr_adamw', pd, fresh, accum, m, v, vmax, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, step, stream())
+        lib('c2dsr_adamw', pd, fresh, accum, m, v, vmax, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, step, None, stream())
         opt.step(P, {'w': acc_ref.clone()})
         assert rel(pd, P['w']) < 1e-6
         assert float(fresh.abs().max()) == 0.0
@@ -326,7 +326,7 @@ def test_adamw_direct_accumulation_vs_oracle():
         g = torch.randn(n)
         acc_ref += g
         acc += g.to(DEV)
-        lib('c2dsr_adamw', pd, acc, acc, m, v, vmax, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, step, stream())
+        lib('c2dsr_adamw', pd, acc, acc, m, v, vmax, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, step, None, stream())
         opt.step(P, {'w': acc_ref.clone()})
         assert rel(pd, P['w']) < 1e-6
         assert rel(acc, acc_ref) < 1e-6  # read only
@@ -684,7 +684,7 @@ def test_compact_valid_targets(M):
     tc = torch.empty(M, device=DEV, dtype=torch.int64)
     cnt = torch.empty(2, device=DEV, dtype=torch.int32)
     ws = torch.empty(lib.raw('c2dsr_compact_workspace')(M, 1) // 4 + 1, device=DEV, dtype=torch.int32)
-    lib('c2dsr_compact_valid', tt, M, split, ignore, idx, inv, tc, cnt, ws, stream())
+    lib('c2dsr_compact_valid', tt, M, split, ignore, idx, inv, tc, cnt, ws, None, stream())
     want = np.nonzero(t != ignore)[0]
     n = len(want)
     assert cnt.tolist() == [int((want < split).sum()), int((want >= split).sum())]

@@ -64,3 +64,58 @@ def test_host_counts_refuse_a_length_mismatch():
     assert [hc[i] for i in range(4)] == [1, 2, 3, 4]
     with pytest.raises(ValueError, match='host-prepared counts'):
         HostCounts(torch.zeros(14, dtype=torch.int32), known=[1, 2, 3, 4])
+
+
+def _valid_batch(rng, B, L, n_item, n_a, n_b):
+    arrs = []
+    for k in range(14):
+        if k in (10, 11):
+            arrs.append((rng.random((B, L)) < 0.4).astype(np.int64))
+        elif k in (3, 4, 5):  # positions
+            arrs.append(np.tile(np.arange(L), (B, 1)).astype(np.int64))
+        elif k in (6, 8):
+            arrs.append(rng.integers(0, n_a + 1, size=(B, L)).astype(np.int64))
+        elif k in (7, 9):
+            arrs.append(rng.integers(0, n_b + 1, size=(B, L)).astype(np.int64))
+        else:
+            arrs.append(rng.integers(0, n_item, size=(B, L)).astype(np.int64))
+    return arrs
+
+
+def test_batch_index_check_raises_like_the_reference_lookups():
+    """the reference's F.embedding / nn.Embedding raise IndexError on an index outside the table
+    (models/C2DSR.py:65-67,81, encoders.py:30) and F.cross_entropy on a target outside [0, n] other than the ignore
+    index (trainer.py:143-152), before any update.  With the batch's host copy the drop-in raises the same way
+    before anything is enqueued (Trainer.check_batch_indices; the device path is tests/test_gpu_index_errors.py)."""
+    import pytest
+    rng = np.random.default_rng(3)
+    B, L, R, n_a, n_b = 8, 10, 3, 30, 40
+    n_item = n_a + n_b + 1
+    fake = SimpleNamespace(len_rec=R, n_item_a=n_a, n_item_b=n_b,
+                           model=SimpleNamespace(n_item=n_item, attn_share=SimpleNamespace(len_max=L)))
+    ok = _valid_batch(rng, B, L, n_item, n_a, n_b)
+    Trainer.check_batch_indices(fake, tuple(ok))  # in range: nothing raised
+    cases = [(0, n_item, 'item index'), (2, -1, 'item index'), (12, n_item + 5, 'item index'),  # seq_b / neg_a
+             (3, L, 'position'), (5, -1, 'position'),
+             (6, n_a + 1, 'target'), (9, -2, 'target')]
+    for k, v, what in cases:
+        bad = [a.copy() for a in ok]
+        bad[k][B // 2, L - 1] = v
+        with pytest.raises(IndexError, match=what):
+            Trainer.check_batch_indices(fake, tuple(bad))
+    # a target before the last len_rec positions is never read by the reference (trainer.py:126-129): no error
+    bad = [a.copy() for a in ok]
+    bad[6][0, 0] = n_a + 7
+    Trainer.check_batch_indices(fake, tuple(bad))
+    # the ignore index itself is a valid target
+    bad = [a.copy() for a in ok]
+    bad[8][:, -R:] = n_a
+    Trainer.check_batch_indices(fake, tuple(bad))
+
+
+def test_index_error_message_names_every_bit():
+    from c2dsr_amd.ops import index_error_message
+    m = index_error_message(1 | 2 | 4 | 8)
+    assert m.startswith('index out of range in self')
+    for w in ('item index', 'position', 'lookup index', 'target'):
+        assert w in m

@@ -46,13 +46,20 @@ def test_gcn_checks(T):
     work, split = torch.zeros(12, 4, dtype=torch.int32), torch.zeros(0, 4, dtype=torch.int32)
     col, val = torch.zeros(30, dtype=torch.int32), torch.zeros(29)
     with pytest.raises(RuntimeError, match='val has shape'):
-        T.gcn_propagate(E, work, split, col, val, 0, 1, 0.0, [0, 0])
+        T.gcn_propagate(E, work, split, col, val, N, 0, 1, 0.0, [0, 0])
     with pytest.raises(RuntimeError, match='work has shape'):
-        T.gcn_propagate(E, torch.zeros(12, 3, dtype=torch.int32), split, col, torch.zeros(30), 0, 1, 0.0, [0, 0])
+        T.gcn_propagate(E, torch.zeros(12, 3, dtype=torch.int32), split, col, torch.zeros(30), N, 0, 1, 0.0, [0, 0])
     with pytest.raises(RuntimeError, match='keys must hold'):
-        T.gcn_propagate(E, work, split, col, torch.zeros(30), 0, 2, 0.0, [0, 0])
+        T.gcn_propagate(E, work, split, col, torch.zeros(30), N, 0, 2, 0.0, [0, 0])
+    # a plan built for another table: refused before any launch
+    with pytest.raises(RuntimeError, match='the graph has 12 rows but the table has 10'):
+        T.gcn_propagate(E, work, split, col, torch.zeros(30), N + 2, 0, 1, 0.0, [0, 0])
+    with pytest.raises(RuntimeError, match='the graph has 9 rows'):
+        T.gcn_backward_rounds(E, work, split, col, torch.zeros(30), N - 1, 0, 2, 0.0, [0, 0, 0, 0])
+    with pytest.raises(RuntimeError, match='the graph has 11 rows'):
+        T.gcn_backward_final(E, E, E, work, split, col, torch.zeros(30), N + 1, 0, 1, 0.0, 0, 0, -1, 1.0, 1.0)
     with pytest.raises(RuntimeError, match='gE has shape'):
-        T.gcn_backward_final(E, E, torch.zeros(N - 1, d), work, split, col, torch.zeros(30), 0, 1, 0.0, 0, 0, -1, 1.0,
+        T.gcn_backward_final(E, E, torch.zeros(N - 1, d), work, split, col, torch.zeros(30), N, 0, 1, 0.0, 0, 0, -1, 1.0,
                              1.0)
 
 

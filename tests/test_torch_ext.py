@@ -31,7 +31,7 @@ def test_raw_op_schemas_declare_the_buffers_they_write():
     torch.ops.load_library(EXT)
     R = torch.ops.c2dsr_raw
     assert _writes(R.gcn_spmm) == {'part', 'Y', 'Y2'}
-    assert _writes(R.embed_fwd) == {'X'}
+    assert _writes(R.embed_fwd) == {'X', 'err'}  # err: the index error word (C2DSR_IDX_ERR_*)
     assert _writes(R.adamw) == {'p', 'fresh', 'accum', 'm', 'v', 'vmax'}
     assert _writes(R.rgemm_x3) == {'C'}
     assert _writes(R.ce3_fused_dw) == {'dWp', 'dbp'}

@@ -25,7 +25,7 @@ n = 105_800_000
 b = [torch.zeros(n, device='cuda') for _ in range(6)]
 p, fresh, acc, m, v, vx = b
 s = stream()
-keep = timeit(lambda: lib('c2dsr_adamw', p, acc, acc, m, v, vx, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1, s))
-fold = timeit(lambda: lib('c2dsr_adamw', p, fresh, acc, m, v, vx, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1, s))
+keep = timeit(lambda: lib('c2dsr_adamw', p, acc, acc, m, v, vx, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1, None, s))
+fold = timeit(lambda: lib('c2dsr_adamw', p, fresh, acc, m, v, vx, n, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1, None, s))
 print(f'{os.path.basename(os.environ.get("C2DSR_LIB", "default"))}: keep {keep:.1f} us ({36 * n / keep / 1e3:.0f} GB/s), '
       f'fold {fold:.1f} us ({48 * n / fold / 1e3:.0f} GB/s)', flush=True)

@@ -58,7 +58,7 @@ def main():
     t_b = timeit(lambda: run(G, gP))
     pb = int(lib.raw('c2dsr_index_plan_bytes')(n_rows))
     buf = torch.empty(pb, dtype=torch.uint8, device=dev)
-    t_plan = timeit(lambda: lib('c2dsr_index_plan', sd, n_rows, N, buf, pb, s))
+    t_plan = timeit(lambda: lib('c2dsr_index_plan', sd, n_rows, N, buf, pb, None, s))
     byt = n_rows * (16 + 4 * d) + 8 * d * uniq
     print(f'rows {n_rows} uniq {uniq}: G-only {t_g:.1f} us, gP-only {t_p:.1f} us, both {t_b:.1f} us '
           f'({byt / (t_b * 1e-6) / 1e9:.0f} GB/s credited), seq plan build {t_plan:.1f} us', flush=True)

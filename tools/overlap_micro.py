@@ -65,7 +65,7 @@ def main():
         lib('c2dsr_ce3_fused_dw', Hx, Wx, bias2, Mv, n, d, 0, crow, gW, gb, st.cuda_stream)
 
     def adam(st):
-        lib('c2dsr_adamw', p, acc, acc, m, v, vx, n_adam, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1, st.cuda_stream)
+        lib('c2dsr_adamw', p, acc, acc, m, v, vx, n_adam, 1e-3, 5e-4, 0.9, 0.999, 1e-8, 1, None, st.cuda_stream)
 
     def both():
         ev = torch.cuda.Event()
