@@ -628,6 +628,16 @@ __global__ void finalize_kernel(const float* __restrict__ vec, const float* __re
   coefB[1] = 1.f / c[7];
 }
 
+// acc[0..2] += w · (loss, loss_rec, loss_mi): the epoch's sample-weighted loss sums (trainer.py:50-52, run_epoch)
+__global__ void loss_accumulate_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                       const float* __restrict__ c, float w, float* __restrict__ acc) {
+  if (threadIdx.x == 0) {
+    acc[0] += w * a[0];
+    acc[1] += w * b[0];
+    acc[2] += w * c[0];
+  }
+}
+
 // ds[k][b] *= gscale * (1 - lam)
 __global__ void scale_ds_kernel(float* __restrict__ ds, int n, const float* __restrict__ gscale, float f) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -823,6 +833,13 @@ C2_API int c2dsr_loss_partials(const float* rowsA, const int64_t* tA, int n_a, c
 C2_API int c2dsr_loss_finalize(const float* vec, const float* cnt, int BR_global, float lam, float* out3, float* coefA,
                                float* coefB, void* stream) {
   finalize_kernel<<<1, 64, 0, (hipStream_t)stream>>>(vec, cnt, (float)BR_global, lam, out3, coefA, coefB);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_loss_accumulate(const float* loss, const float* loss_rec, const float* loss_mi, float w, float* acc3,
+                                  void* stream) {
+  if (!loss || !loss_rec || !loss_mi || !acc3) return (int)hipErrorInvalidValue;
+  loss_accumulate_kernel<<<1, 64, 0, (hipStream_t)stream>>>(loss, loss_rec, loss_mi, w, acc3);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -1461,6 +1461,58 @@ C2_API int c2dsr_to_split_bf16_frag_multi(const int64_t* desc, int count, void* 
   return to_bf16_multi_impl(desc, count, stream, true, true);
 }
 
+// ‖W[r]‖² of a list of fp32 matrices (the guarded linear1's threshold, ops.WEIGHTS 'norm2'), one launch: one wave per
+// row, lane l sums elements l, l + 64, … in order, then a fixed butterfly — deterministic.  Rows per block: 4.
+namespace {
+struct MultiNorm {
+  const float* x[MULTI_MAX];
+  float* y[MULTI_MAX];
+  int R[MULTI_MAX], C[MULTI_MAX], ld[MULTI_MAX];
+  int bstart[MULTI_MAX + 1];  // first block of each matrix
+  int count;
+};
+__global__ __launch_bounds__(256) void row_sqnorm_multi_kernel(MultiNorm m) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = m.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (m.bstart[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int r = (b - m.bstart[lo]) * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= m.R[lo]) return;
+  const float* xr = m.x[lo] + (long)r * m.ld[lo];
+  float s = 0.f;
+  for (int c = lane; c < m.C[lo]; c += 64) s = fmaf(xr[c], xr[c], s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) m.y[lo][r] = s;
+}
+}  // namespace
+
+// desc: HOST array of count (<= 64) records of six int64 (x, y, R, Cc, ldx, 0): y[r] = Σ_c x[r·ldx + c]² (fp32 [R])
+C2_API int c2dsr_row_sqnorm_multi(const int64_t* desc, int count, void* stream) {
+  if (count < 0 || count > MULTI_MAX) return (int)hipErrorInvalidValue;
+  if (count == 0) return 0;
+  MultiNorm m;
+  m.count = count;
+  m.bstart[0] = 0;
+  for (int k = 0; k < count; ++k) {
+    const int64_t* d = desc + 6 * k;
+    m.x[k] = (const float*)(intptr_t)d[0];
+    m.y[k] = (float*)(intptr_t)d[1];
+    m.R[k] = (int)d[2];
+    m.C[k] = (int)d[3];
+    m.ld[k] = (int)d[4];
+    if (m.R[k] < 0 || m.C[k] < 0 || d[5] != 0 || m.ld[k] < m.C[k]) return (int)hipErrorInvalidValue;
+    m.bstart[k + 1] = m.bstart[k] + c2::ceil_div(m.R[k], 4);
+  }
+  if (m.bstart[count] == 0) return 0;
+  for (int k = count + 1; k <= MULTI_MAX; ++k) m.bstart[k] = m.bstart[count];
+  row_sqnorm_multi_kernel<<<m.bstart[count], 256, 0, (hipStream_t)stream>>>(m);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+
 C2_API int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, void* stream) {
   const long n = (long)R * Cc;
   if (n == 0) return 0;

@@ -4,7 +4,8 @@
 //                   sets (c2dsr_need_rows), their padding rows (c2dsr_pad_rows, the attention's keys, Q1) and per
 //                   classifier head the stacked last-R targets and their valid-row compaction
 //   wgrad_groups    the projections' deferred weight-gradient products, grouped per weight (ops.WGradBatch)
-//   weight_images   the projection weights' bf16 / split-bf16 images after an optimizer step (ops._WeightImages)
+//   weight_images   the projection weights' bf16 / split-bf16 images after an optimizer step (ops._WeightImages),
+//                   and the guarded linear1's row norms ‖W1[r]‖² (layout 4)
 #include <torch/library.h>
 
 #include "c2t.h"
@@ -161,6 +162,13 @@ void weight_images(const std::vector<Tensor>& W, const std::vector<Tensor>& Y, s
   for (size_t i = 0; i < W.size(); ++i) {
     TORCH_CHECK(W[i].dim() == 2 && W[i].scalar_type() == at::kFloat && W[i].stride(1) == 1,
                 "c2dsr::weight_images: W must be fp32 [R, C] with unit column stride");
+    if (layout[i] == 4) {  // ‖W[r]‖² (fp32 [R])
+      TORCH_CHECK(!trans[i] && Y[i].scalar_type() == at::kFloat && Y[i].is_contiguous() && Y[i].numel() >= W[i].size(0),
+                  "c2dsr::weight_images: a row-norm image is fp32 [R] of an untransposed W");
+      dev(W[i], op);
+      dev(Y[i], op);
+      continue;
+    }
     TORCH_CHECK(Y[i].scalar_type() == at::kBFloat16 && Y[i].is_contiguous(), "c2dsr::weight_images: bf16 images");
     const int64_t rows = trans[i] ? W[i].size(1) : W[i].size(0), cols = trans[i] ? W[i].size(0) : W[i].size(1);
     const int64_t pad = layout[i] == 2 ? 16 : layout[i] == 3 ? 32 : 1;
@@ -171,11 +179,11 @@ void weight_images(const std::vector<Tensor>& W, const std::vector<Tensor>& Y, s
     dev(Y[i], op);
   }
   using Fn = int (*)(const int64_t*, int, void*);
-  const Fn fns[4] = {&c2dsr_to_bf16_multi, &c2dsr_to_split_bf16_multi, &c2dsr_to_split_bf16_frag_multi,
-                     &c2dsr_to_bf16_frag_multi};
-  const char* names[4] = {"c2dsr_to_bf16_multi", "c2dsr_to_split_bf16_multi", "c2dsr_to_split_bf16_frag_multi",
-                          "c2dsr_to_bf16_frag_multi"};
-  for (int lay = 0; lay < 4; ++lay) {
+  const Fn fns[5] = {&c2dsr_to_bf16_multi, &c2dsr_to_split_bf16_multi, &c2dsr_to_split_bf16_frag_multi,
+                     &c2dsr_to_bf16_frag_multi, &c2dsr_row_sqnorm_multi};
+  const char* names[5] = {"c2dsr_to_bf16_multi", "c2dsr_to_split_bf16_multi", "c2dsr_to_split_bf16_frag_multi",
+                          "c2dsr_to_bf16_frag_multi", "c2dsr_row_sqnorm_multi"};
+  for (int lay = 0; lay < 5; ++lay) {
     std::vector<int64_t> recs;
     int cnt = 0;
     auto flush = [&] {

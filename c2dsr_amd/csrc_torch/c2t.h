@@ -40,6 +40,18 @@ inline void check(const char* op, const char* arg, const std::optional<at::Tenso
   }
 }
 
+// extent check of a buffer a raw op writes (tools/raw_extents.py): the bytes from its data pointer to the end of its
+// storage must hold `need` elements of `elem` bytes (views of larger buffers are measured against their storage)
+inline void extent(const char* op, const char* arg, const std::optional<at::Tensor>& t, int64_t need, int64_t elem) {
+  if (!t.has_value() || !t->defined() || need <= 0) return;
+  const int64_t avail = (int64_t)t->storage().nbytes() - t->storage_offset() * (int64_t)t->element_size();
+  TORCH_CHECK(avail >= need * elem, "c2dsr_raw::", op, ": ", arg, " holds ", avail, " bytes, the call writes up to ",
+              need * elem, " (undersized output)");
+}
+inline int64_t span(int64_t rows, int64_t ld, int64_t cols) { return rows > 0 ? (rows - 1) * ld + cols : 0; }
+#define HAS(p) (c2t::ptr(p) != nullptr)
+#define SPAN(r, ld, c) c2t::span((int64_t)(r), (int64_t)(ld), (int64_t)(c))
+
 // ---- timing / debug registry (defined in torch_ops.cpp)
 struct Rec {
   std::string name;

@@ -116,7 +116,7 @@ class _WeightImages:
         if self.known:
             self._refresh_known()
 
-    LAYOUT = {None: 0, 'split': 1, 'frag': 2, 'b16frag': 3}  # c2dsr::weight_images' layout codes
+    LAYOUT = {None: 0, 'split': 1, 'frag': 2, 'b16frag': 3, 'norm2': 4}  # c2dsr::weight_images' layout codes
 
     def _refresh_known(self):
         done = [(key, W, y) for key, (W, y) in self.known.items() if key[3] in self.LAYOUT]
@@ -125,10 +125,6 @@ class _WeightImages:
                                       [self.LAYOUT[k[3]] for k, _, _ in done])
         for key, W, y in done:
             self.cache[key] = ((self.epoch, W._version), y, W)
-        for key, (W, y) in self.known.items():
-            if key[3] == 'norm2':
-                torch.sum(W * W, 1, out=y)
-                self.cache[key] = ((self.epoch, W._version), y, W)
         self.known = {}
 
     def get(self, W, trans, layout=None):
@@ -142,8 +138,9 @@ class _WeightImages:
         hit = self.cache.get(key)
         if hit is not None and hit[0] == tag:
             return hit[1]
-        if layout == 'norm2':  # ‖W[r]‖² [R] (torch's fixed-order reduction)
-            y = (W * W).sum(1)
+        if layout == 'norm2':  # ‖W[r]‖² [R] (c2dsr_row_sqnorm_multi: one wave per row, fixed order)
+            y = torch.empty(W.shape[0], device=W.device, dtype=torch.float32)
+            stage_ops().weight_images([W], [y], [0], [4])
         elif layout == 'b16frag':
             R, Cc = W.shape
             rows, cols = (Cc, R) if trans else (R, Cc)

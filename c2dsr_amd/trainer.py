@@ -198,7 +198,9 @@ class Trainer(object):
         for batch in self.trainloader:
             self.model.convolve_graph()
             loss, loss_rec, loss_mi = self.train_batch(batch)
-            acc += torch.stack([loss.detach(), loss_rec, loss_mi]) * batch[0].shape[0]  # one sync per epoch (f4)
+            # device-side sums, one sync per epoch (f4)
+            lib('c2dsr_loss_accumulate', loss.detach(), loss_rec.detach(), loss_mi.detach(), float(batch[0].shape[0]),
+                acc, stream())
         acc = (acc / max(self.n_tr, 1)).tolist()
         self.check_index_errors()  # after the epoch's one sync: free
         if self.noter is not None:

@@ -262,6 +262,10 @@ size_t c2dsr_loss_partials_workspace(int BR);
  * the valid counts cnt[4..7] instead of vec[4..7] */
 int c2dsr_loss_finalize(const float* vec, const float* cnt, int BR_global, float lam, float* out3, float* coefA,
                         float* coefB, void* stream);
+/* acc3[0..2] += w·(*loss, *loss_rec, *loss_mi): run_epoch's per-epoch loss sums kept on the device (one host read per
+ * epoch; reference trainer.py:50-52 accumulates loss.item()·n_batch on the host every step). */
+int c2dsr_loss_accumulate(const float* loss, const float* loss_rec, const float* loss_mi, float w, float* acc3,
+                          void* stream);
 int c2dsr_scale_ds(float* ds, int n, const float* gscale, float f, void* stream);
 int c2dsr_rowscale(const float* x, const float* s, long n, int d, float* out, int accumulate, void* stream);
 
@@ -460,6 +464,11 @@ int c2dsr_to_bf16(const float* x, int R, int Cc, int ldx, int trans, void* y, vo
 /* c2dsr_to_bf16 over up to 64 matrices in one launch (the projection weights' bf16 images after an optimizer
  * step): desc = HOST array of count records of six int64 (x, y, R, Cc, ldx, trans) */
 int c2dsr_to_bf16_multi(const int64_t* desc, int count, void* stream);
+/* Squared row norms of a list of fp32 matrices in one launch (c2dsr_to_bf16_multi's descriptors, trans = 0):
+ * y[r] = Σ_c x[r·ldx + c]² (fp32 [R]; one wave per row, fixed order) — the guarded linear1's threshold
+ * ‖W1[c]‖² (c2dsr_rgemm_x3_relu_guard's wn2), refreshed with the weight images after each optimizer step
+ * (trainer.py:158; replaces torch.sum(W * W, 1)). */
+int c2dsr_row_sqnorm_multi(const int64_t* desc, int count, void* stream);
 
 /* Evaluation (csrc/eval.hip).  Replaces trainer.py:162-181 (evaluate_batch):
  * per row i, dom = (xory[i] == 0 ? a : b), q = h_share[i,L-1] + h_dom[i, idx_last_dom[i]],

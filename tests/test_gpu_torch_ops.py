@@ -81,7 +81,7 @@ def test_torch_ops_equal_ctypes_path():
     outs = []
     for way in ('ctypes', 'torch'):
         Xo = torch.empty(B * L, d, device=DEV)
-        args = (seq, pos, B * L, d, X, X, None, P, 16.0, 3, 4, 0.2, 0, Xo)
+        args = (seq, pos, B * L, d, X, X, None, P, 16.0, 3, 4, 0.2, 0, Xo, n, L, None)
         if way == 'ctypes':
             _cabi('embed_fwd')(*args)
         else:

@@ -51,3 +51,52 @@ def test_torch_op_refuses_host_tensors():
     x = torch.zeros(4, 8)
     with pytest.raises(RuntimeError, match='must be on the HIP device'):
         torch.ops.c2dsr_raw.f32_to_bf16(x, 32, x)
+
+
+def test_raw_ops_refuse_undersized_outputs():
+    """every buffer a c2dsr_raw op writes is checked against the extent its size arguments
+    imply (tools/raw_extents.py) before the launch — an undersized output raises RuntimeError (here on CPU tensors:
+    the extent check runs before the device check)."""
+    torch.ops.load_library(EXT)
+    R = torch.ops.c2dsr_raw
+    i64 = torch.zeros(64, dtype=torch.long)
+    # embed_fwd writes X [n_rows, d]: 10 rows of 8 need 80 floats
+    with pytest.raises(RuntimeError, match='undersized output'):
+        R.embed_fwd(i64, i64, 10, 8, None, None, None, None, 1.0, 0, 0, 0.0, 0, torch.zeros(79), 5, 5, None)
+    with pytest.raises(RuntimeError, match='must be on the HIP device'):  # the right size gets past the extent check
+        R.embed_fwd(i64, i64, 10, 8, None, None, None, None, 1.0, 0, 0, 0.0, 0, torch.zeros(80), 5, 5, None)
+    # a view is measured against its storage: a narrow view of a big enough buffer passes the extent check
+    big = torch.zeros(200)
+    with pytest.raises(RuntimeError, match='must be on the HIP device'):
+        R.embed_fwd(i64, i64, 10, 8, None, None, None, None, 1.0, 0, 0, 0.0, 0, big[100:110], 5, 5, None)
+    with pytest.raises(RuntimeError, match='undersized output'):
+        R.embed_fwd(i64, i64, 10, 8, None, None, None, None, 1.0, 0, 0, 0.0, 0, big[150:], 5, 5, None)
+    # strided outputs: rgemm writes C rows with stride ldc
+    with pytest.raises(RuntimeError, match='C holds'):
+        R.rgemm(4, 16, 32, torch.zeros(128), 32, torch.zeros(1), 0, torch.zeros(3 * 20 + 15), 20, 1.0, 0.0, None, 0,
+                0, 0, 0.0, 0, None)
+    # workspaces in bytes, optional outputs only when given
+    with pytest.raises(RuntimeError, match='workspace holds'):
+        R.embed_bwd(i64, i64, 16, 4, torch.zeros(64), 0, 0, 0.0, 0, 1.0, None, 0, None, 0, None,
+                    torch.zeros(3, dtype=torch.uint8), 4)
+    with pytest.raises(RuntimeError, match='gP holds'):
+        R.embed_bwd(i64, i64, 16, 4, torch.zeros(64), 0, 0, 0.0, 0, 1.0, None, 0, torch.zeros(7), 2, None,
+                    torch.zeros(4, dtype=torch.uint8), 4)
+    with pytest.raises(RuntimeError, match='Up holds'):
+        R.ce3_fused_fwd_u(None, None, None, 100, 50, 256, 3, torch.zeros(300), torch.zeros(300),
+                          torch.zeros(3 * 100 * 256 - 1), None, None, None, None, None, torch.zeros(100),
+                          torch.zeros(100), torch.zeros(100))
+    with pytest.raises(RuntimeError, match='vmax holds'):
+        R.adamw(*[torch.zeros(16)] * 5, torch.zeros(15), 16, 1e-3, 0.0, 0.9, 0.999, 1e-8, 1, None)
+
+
+def test_every_written_raw_buffer_has_an_extent_or_a_reason():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), 'tools'))
+    import gen_torch_ops as g
+    from raw_extents import EXTENTS, UNCHECKED
+    for _, name, params in g.parse():
+        op = name[len('c2dsr_'):]
+        for pname, _, ptr, decl in params:
+            if ptr and pname != 'stream' and not decl.startswith('const ') and pname not in g.HOST_ARRAYS:
+                assert pname in EXTENTS.get(op, {}) or pname in UNCHECKED.get(op, {}), (op, pname)

@@ -1,6 +1,7 @@
 """Host-side cost of one training step at the bench workload (MB, fp32 mode): per-step enqueue time (the host
 returns before the device finishes unless it waits on a count), wall time with the device synchronised, and a
-cProfile of the Python functions that issue the launches.  usage: python tools/host_time.py [precision]"""
+cProfile of the Python functions that issue the launches.
+usage: python tools/host_time.py [precision] [config] [batch] [n_top]   (defaults: fp32 mb <config's B> 30)"""
 import cProfile
 import os
 import pstats
@@ -15,8 +16,12 @@ import bench  # noqa: E402
 
 def main():
     precision = sys.argv[1] if len(sys.argv) > 1 else 'fp32'
-    cfg = dict(bench.CONFIGS['mb'])
-    rows, gs, gp = bench.workload(cfg, 'mb')
+    name = sys.argv[2] if len(sys.argv) > 2 else 'mb'
+    cfg = dict(bench.CONFIGS[name])
+    if len(sys.argv) > 3 and int(sys.argv[3]):
+        cfg['B'] = int(sys.argv[3])
+    n_top = int(sys.argv[4]) if len(sys.argv) > 4 else 30
+    rows, gs, gp = bench.workload(cfg, name)
     from c2dsr_amd.trainer import Trainer
     args = bench.make_args(cfg, torch.device('cuda'), precision)
     torch.manual_seed(3407)
@@ -53,7 +58,7 @@ def main():
     torch.cuda.synchronize()
     pr.disable()
     st = pstats.Stats(pr)
-    st.sort_stats('tottime').print_stats(30)
+    st.sort_stats('tottime').print_stats(n_top)
 
 
 if __name__ == '__main__':
