@@ -250,13 +250,15 @@ std::vector<Tensor> loss_finalize(const Tensor& vec, const OptT& cnt, int64_t BR
 // ---------------------------------------------------------------- backward of one head
 // saved: ce_head_forward's outputs 1.. (Hpad, Hb, Wb, padc, lse2, bias2, Hc, lse_c, Up, part_m); gW / gb / gwpad /
 // gbpad: the parameters' gradients (accumulated; may be absent); tplan: the sort plan of the valid targets (the
-// one-hot part's deterministic segment sums; absent: sorted here); n_rsplit: the dW sweep's row splits.
+// one-hot part's deterministic segment sums; absent: sorted here); n_rsplit: the dW sweep's row splits
+// (losshead.dw_plan); dw_full: with n_rsplit < 0, the W rows of the whole rounds the plan costed (a multiple of 128
+// below n — passed, not re-derived here, so the sweep splits exactly as the plan that chose it).
 // Returns [dHcat [2BR, d], dpad [2BR]].
 std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Tensor& W, const Tensor& inv,
                                      const Tensor& tc, int64_t Mv0, int64_t Mv1, const Tensor& coef,
                                      const Tensor& gscale, double lam, const OptT& gW, const OptT& gb,
                                      const OptT& gwpad, const OptT& gbpad, const OptT& tplan, int64_t n_rsplit,
-                                     int64_t mode) {
+                                     int64_t mode, int64_t dw_full) {
   const char* op = "ce_head_backward";
   TORCH_CHECK(saved.size() == 10, "c2dsr::ce_head_backward: the 10 tensors ce_head_forward saved");
   const Tensor &Hpad = saved[0], &Hb = saved[1], &Wb = saved[2], &padc = saved[3], &lse2 = saved[4];
@@ -329,11 +331,9 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
                     F(*gW), F(*gb), ws.data_ptr(), (size_t)ws.nbytes(), S());
     } else if (n_rsplit < 0 && has(gW) && has(gb)) {
       // whole rounds of unsplit row blocks onto the gradients, then the last partial round's row blocks −n_rsplit ways
-      int dev = 0, ncu = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      const int64_t full = ncu > 0 ? (n + 127) / 128 / ncu * ncu * 128 : 0, rem = n - full, k = -n_rsplit;
-      TORCH_CHECK(full > 0 && rem > 0, "c2dsr::ce_head_backward: a remainder split needs whole rounds and a remainder");
+      const int64_t full = dw_full, rem = n - full, k = -n_rsplit;
+      TORCH_CHECK(full > 0 && full % 128 == 0 && rem > 0, "c2dsr::ce_head_backward: a remainder split needs dw_full = "
+                  "the whole rounds' rows (a positive multiple of 128 below n = ", n, "), got ", dw_full);
       dw_rows(0, F(*gW), F(*gb), 0, full);
       Tensor dWp = at::empty({k, rem, d}, f32), dbp = at::empty({k, rem}, f32);
       dw_rows((int)k, F(dWp), F(dbp), full, rem);
@@ -501,7 +501,7 @@ void register_losshead_ops(torch::Library& m) {
   m.def("loss_finalize(Tensor vec, Tensor? cnt, int BR_global, float lam) -> Tensor[]");
   m.def("ce_head_backward(Tensor[] saved, Tensor W, Tensor inv, Tensor tc, int Mv0, int Mv1, Tensor coef, "
         "Tensor gscale, float lam, Tensor(a!)? gW, Tensor(b!)? gb, Tensor(c!)? gwpad, Tensor(d!)? gbpad, "
-        "Tensor? tplan, int n_rsplit, int mode) -> Tensor[]");
+        "Tensor? tplan, int n_rsplit, int mode, int dw_full=0) -> Tensor[]");
   m.def("loss_disc_backward(Tensor[] fwd, Tensor gscale, float lam, Tensor?[] D, Tensor[] imgT, Tensor(a!)?[] gD, "
         "Tensor[] heads, Tensor wpad, Tensor?[] sub, Tensor?[] maps, int L, int R, int mode) -> Tensor[]");
   m.impl("loss_disc_forward", c10::DispatchKey::CompositeExplicitAutograd, TORCH_FN(loss_disc_forward));

@@ -142,6 +142,12 @@ def dw_plan(n, Mv, x3, d, both_grads=True):
     return plan
 
 
+def dw_full_rows(n):
+    """The W rows of the whole rounds of a remainder dW plan (dw_plan < 0): ⌊row blocks / CUs⌋·CUs row blocks, with
+    the CU count the plan was costed on (ce_head_backward takes it as dw_full instead of re-deriving it)."""
+    return -(-n // 128) // _ncu() * _ncu() * 128
+
+
 def ce_kind(precision, d):
     """Fused classifier-head kernels for this precision and width: 'b16' (ce.hip, bf16 operands), 'x3'
     (ce3.hip, split-bf16 operands: the fp32 mode), or None (materialised fp32 logits + exact fp32 GEMMs)."""
@@ -453,9 +459,10 @@ class LossHeadFn(Function):
         hd = []
         for (saved, inv, tc, Mv0, Mv1, tplan, W, bias, n), coef in zip(heads, coefs):
             gW, gb = _grad_target(W), _grad_target(bias)
+            nr = dw_plan(n, Mv0 + Mv1, mode == 0, d, gW is not None and gb is not None)
             hd += T.ce_head_backward(saved, W, inv, tc, Mv0, Mv1, coef, gscale, float(m.lam), gW, gb, gwpad, gbpad,
-                                     tplan.get() if tplan is not None else None,
-                                     dw_plan(n, Mv0 + Mv1, mode == 0, d, gW is not None and gb is not None), mode)
+                                     tplan.get() if tplan is not None else None, nr, mode,
+                                     dw_full_rows(n) if nr < 0 else 0)
         imgT = [weight_img(m.Da_w.view(d, d), kind, trans=True), weight_img(m.Db_w.view(d, d), kind, trans=True)]
         gD = [_grad_target(t) for t in (m.Da_w, m.Da_b, m.Db_w, m.Db_b)]
         sub = [r.idx[:r.n] if r is not None else None for r in rsets]
@@ -520,7 +527,7 @@ class LossHeadFn(Function):
                         lib(entry + '_sk', Hb, Wb, bias2, Mv, n, d, crow, gW, gb, ws, wsb, s)
                         del ws
                     elif nr < 0:  # whole rounds unsplit onto the gradients, the remainder row blocks −nr ways
-                        full = -(-n // 128) // _ncu() * _ncu() * 128
+                        full = dw_full_rows(n)
                         rem, k = n - full, -nr
                         ic = (2 if ctx.x3 else 1) * d
                         lib(entry, Hb, Wb, bias2, Mv, full, d, 0, crow, gW, gb, s)
