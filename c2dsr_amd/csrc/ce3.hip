@@ -66,6 +66,19 @@
 #ifndef CE3B_DQ
 #define CE3B_DQ 4
 #endif
+// the plain-bf16 instantiation's geometry: stationary 16-row blocks per wave and swept rows per LDS tile.  Measured in
+// round 6 (tools/ce3b_micro.py + CE3_STAMP, MB head b): 3 blocks × 32-row tiles — each LDS fragment read feeding 3
+// MFMAs instead of 2; the 3-block accumulators (192 AGPRs) and stationary fragments (96 VGPRs) fit one wave's 512
+// registers, 4 blocks would not (256 AGPRs of accumulators alone) — ran 5–35 % SLOWER than 2 × 64 (fwd_u 1282 vs
+// 1213 µs, dw 1317 vs 979 µs at one row split): per tile and wave the second product took 31 cycles per MFMA
+// (1500 / 48) against 29 (1869 / 64), the S phase 26 against 23.6, and the per-tile fixed cost (rescale, DMA wait,
+// barrier, loop top) 583 cycles now paid per 32 rows.  The default stays 2 × 64.
+#ifndef CE3B_SBW
+#define CE3B_SBW 2
+#endif
+#ifndef CE3B_T3
+#define CE3B_T3 64
+#endif
 
 namespace {
 
@@ -219,12 +232,21 @@ __device__ __forceinline__ void split2_u(f32x4& acc, const bf16x8& ah, const bf1
 }
 #undef MF
 
-// plain-bf16 products (the bf16 training mode): one MFMA, stationary operand in AGPRs / accumulator in AGPRs
+// plain-bf16 products (the bf16 training mode): one MFMA, accumulator in AGPRs; the stationary operand in AGPRs
+// (BA) or, when the accumulators leave no room there (3 stationary blocks), in VGPRs
+template <bool BA = true>
 __device__ __forceinline__ void mf1_s0(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
+  if constexpr (BA)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
 }
+template <bool BA = true>
 __device__ __forceinline__ void mf1_s(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
+  if constexpr (BA)
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
 __device__ __forceinline__ void mf1_u(f32x4& acc, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
@@ -241,9 +263,15 @@ __device__ __forceinline__ void step_pattern() {
   }
 }
 
-// swept rows per LDS tile: 32 for split images (2D columns), 64 for plain bf16 (D columns) — 32 KiB at D = 256
+// swept rows per LDS tile: 32 for split images (2D columns: 32 KiB at D = 256), CE3B_T3 for plain bf16 (D columns)
 template <bool SPLIT>
-constexpr int tile_rows() { return SPLIT ? 32 : 64; }
+constexpr int tile_rows() { return SPLIT ? 32 : CE3B_T3; }
+// 16-row stationary blocks per wave, and stationary rows per workgroup (the row block of the launch grid)
+template <bool SPLIT, int NW>
+constexpr int stat_blocks() { return SPLIT || NW != 4 ? 8 / NW : CE3B_SBW; }
+template <bool SPLIT, int NW>
+constexpr int row_block() { return 16 * NW * stat_blocks<SPLIT, NW>(); }
+constexpr int ROW_BLOCK_MAX = 16 * 4 * (CE3B_SBW > 2 ? CE3B_SBW : 2);
 
 // NW: waves per workgroup — 4 (one per SIMD, two 16-row stationary blocks each) or 8 (two per SIMD, one block each:
 // half the registers, so one wave's LDS waits, epilogue VALU and barrier run under its partner's MFMAs).  The
@@ -265,7 +293,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   constexpr int D2 = SPLIT ? 2 * D : D;            // image columns (hi ‖ lo, or bf16)
   constexpr int IMG = T3 * D2 * 2;                 // bytes per image
   constexpr int HT = T3 * 256;                     // bytes per 128-column half-tile
-  constexpr int SBW = 8 / NW;                      // 16-row stationary blocks per wave
+  constexpr int SBW = stat_blocks<SPLIT, NW>();     // 16-row stationary blocks per wave
+  constexpr int RB = row_block<SPLIT, NW>();       // stationary rows per workgroup
+  constexpr bool BA = SPLIT || SBW <= 2;           // stationary fragments in AGPRs (else VGPRs: the accumulators fill them)
   constexpr int NDMA = (T3 / 4) * (D2 / 128) / NW;  // LDS-DMA wave-instructions per wave per tile
   constexpr int NB = 4;
   constexpr int DS = SPLIT ? CE3_DS : CE3B_DS, DT = SPLIT ? CE3_DT : CE3B_DT;
@@ -287,7 +317,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
   // XCD-aware work map: block b runs on XCD b % 8; the (split, row block) pairs, split-major, are dealt to the XCDs in
   // contiguous ranges, so each split's swept slice streams through the L2 of one or two XCDs instead of all eight
-  const int nrb = (n_s + 127) >> 7, nb = (int)gridDim.x;
+  const int nrb = (n_s + RB - 1) / RB, nb = (int)gridDim.x;
   // stream-K (MODE 1, sk_nwg workgroups, one per CU): the (row block, swept tile) units in row-block-major order are
   // dealt to the workgroups in equal contiguous ranges, one launch round with no partial last round; a workgroup walks
   // its range as segments (≤ one per row block it touches).  A row block swept whole by one workgroup is added onto the
@@ -315,7 +345,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     w_beg = split * per_split;
     w_end = min(n_w, w_beg + per_split);
   }
-  const int s0 = rblk * 128 + w * 16 * SBW + l16;  // stationary rows s0 + 16·sb, sb < SBW
+  const int s0 = rblk * RB + w * 16 * SBW + l16;  // stationary rows s0 + 16·sb, sb < SBW
   const int ntiles = w_end > w_beg ? (w_end - w_beg + T3 - 1) / T3 : 0;
   f32x4 dacc[NE][SBW];
   float mrow[SBW], zrow[SBW];
@@ -371,7 +401,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     }
     float b2s[SBW];
 #pragma unroll
-    for (int sb = 0; sb < SBW; ++sb) b2s[sb] = MODE == 1 ? svec[s0 + 16 * sb] : 0.f;
+    for (int sb = 0; sb < SBW; ++sb) b2s[sb] = MODE == 1 ? svec[min(s0 + 16 * sb, n_s - 1)] : 0.f;
     dma(0);
     dma(1);
     dma(2);
@@ -423,9 +453,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
           split3_s<BIS>(acc, a[0], a[1], fh[sb][KSI], fl[sb][KSI]);
       } else {
         if constexpr (KSI == 0)
-          mf1_s0(acc, a[0], fh[sb][KSI]);
+          mf1_s0<BA>(acc, a[0], fh[sb][KSI]);
         else
-          mf1_s(acc, a[0], fh[sb][KSI]);
+          mf1_s<BA>(acc, a[0], fh[sb][KSI]);
       }
     };
     // the per-swept-row constants of this lane's rows 16cb + 4g + i
@@ -541,8 +571,12 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
               // ILV: the step's VALU work between its two stationary blocks' products (each MFMA's shadow
               // covers half of it; in-order issue otherwise stalls it behind the second MFMA)
               s_prod.template operator()<k / CB>(sn[cb * SBW], fa[k % (DS + 2)], 0);
-              if constexpr (ILVS || SBW == 1) __builtin_amdgcn_sched_barrier(0);
-              else s_prod.template operator()<k / CB>(sn[cb * SBW + 1], fa[k % (DS + 2)], 1);
+              if constexpr (ILVS || SBW == 1) {
+                __builtin_amdgcn_sched_barrier(0);
+              } else {
+#pragma unroll
+                for (int sb = 1; sb < SBW; ++sb) s_prod.template operator()<k / CB>(sn[cb * SBW + sb], fa[k % (DS + 2)], sb);
+              }
               constexpr int ib = (k * NEL + NSS - 1) / NSS, ie = ((k + 1) * NEL + NSS - 1) / NSS;
 #pragma unroll
               for (int i = ib; i < ie; ++i) {
@@ -551,21 +585,30 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 sc[cb2 * SBW + sb][r] = pv;
                 zrow[sb] += pv;
               }
-              if constexpr (ie > ib && ie % 8 == 0) {
-                constexpr int c = ie / 8 - 1, sb = c / UK, u = c % UK;
-                bf16x8 h, l;
+              // the 8-element chunks this step completes (ib < 8(c+1) <= ie: with NEL / NSS not an integer — 3
+              // stationary blocks — a step's range can straddle a chunk end)
+              [&]<int... C>(std::integer_sequence<int, C...>) {
+                (
+                    [&] {
+                      constexpr int c = C, sb = c / UK, u = c % UK;
+                      if constexpr (ib < 8 * (c + 1) && 8 * (c + 1) <= ie) {
+                        bf16x8 h, l;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                  const float x = sc[(2 * u + (j >> 2)) * SBW + sb][j & 3];
-                  h[j] = (bf16)x;
-                  if constexpr (SPLIT && !CE3_P1) l[j] = (bf16)(x - (float)h[j]);
-                }
-                xh[u][sb] = h;
-                if constexpr (SPLIT && !CE3_P1) xl[u][sb] = l;
-              }
-              if constexpr (ILVS && SBW == 2) {
+                        for (int j = 0; j < 8; ++j) {
+                          const float x = sc[(2 * u + (j >> 2)) * SBW + sb][j & 3];
+                          h[j] = (bf16)x;
+                          if constexpr (SPLIT && !CE3_P1) l[j] = (bf16)(x - (float)h[j]);
+                        }
+                        xh[u][sb] = h;
+                        if constexpr (SPLIT && !CE3_P1) xl[u][sb] = l;
+                      }
+                    }(),
+                    ...);
+              }(std::make_integer_sequence<int, NEL / 8>{});
+              if constexpr (ILVS && SBW >= 2) {
                 __builtin_amdgcn_sched_barrier(0);
-                s_prod.template operator()<k / CB>(sn[cb * SBW + 1], fa[k % (DS + 2)], 1);
+#pragma unroll
+                for (int sb = 1; sb < SBW; ++sb) s_prod.template operator()<k / CB>(sn[cb * SBW + sb], fa[k % (DS + 2)], sb);
               }
               step_pattern<SPLIT ? 3 * SBW : SBW, CE3_VN, BIS>();
               __builtin_amdgcn_sched_barrier(0);
@@ -612,8 +655,12 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                   mf1_u(dacc[q][sb], tq[0], xh[u][sb]);
               };
               u_prod(0);
-              if constexpr (ILVU || SBW == 1) __builtin_amdgcn_sched_barrier(0);
-              else u_prod(1);
+              if constexpr (ILVU || SBW == 1) {
+                __builtin_amdgcn_sched_barrier(0);
+              } else {
+#pragma unroll
+                for (int sb = 1; sb < SBW; ++sb) u_prod(sb);
+              }
               if constexpr (k % DQ == DQ - 1 && k / DQ < NDMA)
                 dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
               constexpr int ib = (k * NEL + NUS - 1) / NUS, ie = ((k + 1) * NEL + NUS - 1) / NUS;
@@ -625,9 +672,10 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 sn[cb * SBW + sb][r] = v;
                 tm[sb] = fmaxf(tm[sb], v);
               }
-              if constexpr (ILVU && SBW == 2) {
+              if constexpr (ILVU && SBW >= 2) {
                 __builtin_amdgcn_sched_barrier(0);
-                u_prod(1);
+#pragma unroll
+                for (int sb = 1; sb < SBW; ++sb) u_prod(sb);
               }
               step_pattern<SPLIT ? (CE3_P1 ? 2 : 3) * SBW : SBW, CE3_VN, BIU>();
               __builtin_amdgcn_sched_barrier(0);
@@ -655,7 +703,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     const float ztot = quad_sum(zrow[sb]);
     const int s = s0 + 16 * sb;
     if (s < n_s && slot >= 0) {  // stream-K partial of a split row block
-      const long so = (long)(2 * blockIdx.x + slot) * 128 + (s - rblk * 128);
+      const long so = (long)(2 * blockIdx.x + slot) * RB + (s - rblk * RB);
       if (g == 0) slot_b[so] = ztot;
       float* out = slot_w + so * D + 4 * g;
 #pragma unroll
@@ -696,16 +744,17 @@ __device__ __forceinline__ int sk_wg_of(long u, long U, int nwg) {
 }
 __global__ __launch_bounds__(256) void ce3_sk_combine_kernel(const float* __restrict__ slot_w,
                                                              const float* __restrict__ slot_b, int n, int D, long T,
-                                                             int nwg, float* __restrict__ gW, float* __restrict__ gb) {
+                                                             int nwg, int RB, float* __restrict__ gW,
+                                                             float* __restrict__ gb) {
   const int rb = blockIdx.x;
-  const long U = (long)((n + 127) >> 7) * T;
+  const long U = (long)((n + RB - 1) / RB) * T;
   const long ub = (long)rb * T, ue = ub + T - 1;
   const int wa = sk_wg_of(ub, U, nwg), wz = sk_wg_of(ue, U, nwg);
   if (wa == wz) return;  // uniform
   const int C4 = D / 4;
-  for (int i = threadIdx.x; i < 128 * (C4 + 1); i += 256) {
+  for (int i = threadIdx.x; i < RB * (C4 + 1); i += 256) {
     const int r = i / (C4 + 1), c = i % (C4 + 1);  // c == C4: the bias column
-    const long row = (long)rb * 128 + r;
+    const long row = (long)rb * RB + r;
     if (row >= n) continue;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     float b = 0.f;
@@ -713,7 +762,7 @@ __global__ __launch_bounds__(256) void ce3_sk_combine_kernel(const float* __rest
       const long wu0 = ((long)w * U) / nwg;
       if (wu0 == ((long)(w + 1) * U) / nwg) continue;  // an empty range (fewer units than workgroups)
       const int sl = wu0 >= ub ? 0 : 1;
-      const long so = (long)(2 * w + sl) * 128 + r;
+      const long so = (long)(2 * w + sl) * RB + r;
       if (c < C4) a = a + *(const float4*)(slot_w + so * D + 4 * c);
       else b += slot_b[so];
     }
@@ -763,9 +812,10 @@ int num_cus3() {
   return g_ncu3;
 }
 
-// stream-K slots: two [128][D] fp32 partials (+ two [128] bias partials) per workgroup
-size_t sk_slot_floats(int nwg, int D) { return (size_t)2 * nwg * 128 * D; }
-size_t sk_ws_bytes(int nwg, int D) { return (sk_slot_floats(nwg, D) + (size_t)2 * nwg * 128) * 4; }
+// stream-K slots: two [RB][D] fp32 partials (+ two [RB] bias partials) per workgroup, RB up to ROW_BLOCK_MAX (one
+// workspace size serves both instantiations)
+size_t sk_slot_floats(int nwg, int D) { return (size_t)2 * nwg * ROW_BLOCK_MAX * D; }
+size_t sk_ws_bytes(int nwg, int D) { return (sk_slot_floats(nwg, D) + (size_t)2 * nwg * ROW_BLOCK_MAX) * 4; }
 
 template <int MODE, bool SPLIT>
 int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec, int n_s, int n_w, int D, int nsplit,
@@ -778,8 +828,9 @@ int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec
   if (nsplit < 1 || (sk_nwg && (MODE != 1 || !slot_w || !slot_b))) return (int)hipErrorInvalidValue;
   const int per = per_split3(n_w, nsplit, tile_rows<SPLIT>());
   // (row block, split) pairs: ce3_kernel's XCD-aware map; stream-K: one workgroup per CU
-  const dim3 grid(sk_nwg ? sk_nwg : c2::ceil_div(n_s, 128) * nsplit);
   constexpr int NW = SPLIT ? CE3_NW : CE3B_NW;
+  constexpr int RB = row_block<SPLIT, NW>();
+  const dim3 grid(sk_nwg ? sk_nwg : c2::ceil_div(n_s, RB) * nsplit);
   if (D == 128)
     ce3_kernel<128, MODE, SPLIT, NW><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w,
                                                                 per, pm, ps, out, accum, sk_nwg, slot_w, slot_b);
@@ -791,7 +842,7 @@ int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec
   C2_CHECK_LAUNCH();
   if (sk_nwg) {
     const long T = (n_w + tile_rows<SPLIT>() - 1) / tile_rows<SPLIT>();
-    ce3_sk_combine_kernel<<<c2::ceil_div(n_s, 128), 256, 0, st>>>(slot_w, slot_b, n_s, D, T, sk_nwg, out, ps);
+    ce3_sk_combine_kernel<<<c2::ceil_div(n_s, RB), 256, 0, st>>>(slot_w, slot_b, n_s, D, T, sk_nwg, RB, out, ps);
     C2_CHECK_LAUNCH();
   }
   return 0;
@@ -814,6 +865,15 @@ extern "C" int c2dsr_ce_rows(const float* part_m, const float* part_s, int n_spl
                              float* lse, float* lse2, float* loss_row, void* stream);
 
 C2_API int c2dsr_ce3_supported(int D) { return D == 128 || D == 256; }
+
+// the sweep geometry of an instantiation (split = 1: the fp32 mode's split-bf16 kernels, 0: the bf16 mode's), for the
+// host's split plans (losshead.py): what = 0 → stationary rows per workgroup (the launch's row block), 1 → swept rows
+// per LDS tile
+C2_API int c2dsr_ce3_geometry(int split, int what) {
+  if (what == 0) return split ? row_block<true, CE3_NW>() : row_block<false, CE3B_NW>();
+  if (what == 1) return split ? tile_rows<true>() : tile_rows<false>();
+  return -1;
+}
 
 C2_API int c2dsr_f32_split_bf16(const float* x, long rows, int D, long rows_out, void* out, void* stream) {
   if (rows_out == 0) return 0;

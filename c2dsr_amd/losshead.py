@@ -35,6 +35,19 @@ def _ncu():
     return _NCU
 
 
+_GEOM = {}
+
+
+def ce3_geometry(x3):
+    """(stationary rows per workgroup, swept rows per LDS tile) of the fused-CE sweep kernels (csrc/ce3.hip
+    c2dsr_ce3_geometry, a build-time choice): fp32 mode (split-bf16, x3) 128 / 32; bf16 mode 128 / 64 (CE3B_SBW /
+    CE3B_T3: 3 stationary blocks × 32-row tiles = 192 / 32 measured slower in round 6)."""
+    if x3 not in _GEOM:
+        g = lib.raw('c2dsr_ce3_geometry')
+        _GEOM[x3] = (int(g(int(bool(x3)), 0)), int(g(int(bool(x3)), 1)))
+    return _GEOM[x3]
+
+
 def split_count(rows, tile, max_split=16, per_cu=1):
     """Work splits for a (row tiles × splits) grid of one-workgroup-per-CU kernels: the count that
     minimises the launch's makespan ⌈tiles·s / slots⌉ / s (whole rounds of workgroups; a partial
@@ -50,6 +63,8 @@ def split_count(rows, tile, max_split=16, per_cu=1):
 
 
 FWD_PLAN = True  # the forward split count from fwd_split_count's fitted cost (else split_count's whole-round fill)
+# the bf16 kernels' fitted sweep costs (tools/ce3b_micro.py on the box; units: swept-tile times unless noted)
+BF16_FIT = dict(fwd_wg=5.0, fwd_slab=2.7, dw_tile_us=1.47, dw_wg=9.0, dw_sk_loc=1.35)
 
 
 def fwd_split_count(Mv, n, x3, d=256, max_split=16):
@@ -61,10 +76,11 @@ def fwd_split_count(Mv, n, x3, d=256, max_split=16):
     (n = 36,845) 5 splits — 1614 µs against 1626 at 12, with 7 fewer 19 MB slabs —, head b (63,937) 12; bf16 5 for
     both (758 / 1239 µs against 793 / 1257 at 12), Food-Kitchen (Mv ≈ 9.5k) 3 (382 µs against 386 at 10, with 7
     fewer slabs).  Other widths: split_count (whole rounds)."""
+    rb, rows = ce3_geometry(x3)
     if not (FWD_PLAN and d == 256):
-        return split_count(Mv, 128, max_split)
-    rows, wg, slab = (32, 4.0, 2.1) if x3 else (64, 5.0, 2.7)
-    blocks = max(1, -(-Mv // 128))
+        return split_count(Mv, rb, max_split)
+    wg, slab = (4.0, 2.1) if x3 else (BF16_FIT['fwd_wg'], BF16_FIT['fwd_slab'])
+    blocks = max(1, -(-Mv // rb))
     tiles = max(1, -(-n // rows))
     slots = _ncu()
     best, best_c = 1, None
@@ -83,9 +99,10 @@ def _dw_costs(n, Mv, x3, d=256, max_split=16):
     tiles, so they share fewer of them in L2) + its combine.  Fitted to split / stream-K sweeps on the box
     (tools/ce3_micro.py / ce3b_micro.py: a tile 1.87 / 1.47 µs, a workgroup's fixed cost ≈ 16 / 9 tiles, a partial
     slab of n·d fp32 written and summed ≈ 7.5 µs at 36.8k × 256, stream-K locality 1.15 / 1.35)."""
-    tiles = max(1, -(-n // 128))
-    sweep = max(1, -(-Mv // (32 if x3 else 64)))
-    t_tile, wg, sk_loc = (1.87, 16.0, 1.15) if x3 else (1.47, 9.0, 1.35)
+    rb, rows = ce3_geometry(x3)
+    tiles = max(1, -(-n // rb))
+    sweep = max(1, -(-Mv // rows))
+    t_tile, wg, sk_loc = (1.87, 16.0, 1.15) if x3 else (BF16_FIT['dw_tile_us'], BF16_FIT['dw_wg'], BF16_FIT['dw_sk_loc'])
     slab = 7.5 * (n * d) / (36845 * 256) / t_tile
     slots = _ncu()
     split = {}
@@ -118,8 +135,9 @@ def dw_plan(n, Mv, x3, d, both_grads=True):
              remainder that one undivided round would leave 7/8 of the chip idle for.
     Stream-K and the remainder split need both gradients and ce3.hip's kernels (d = 256: the fitted shapes; other
     widths keep split_count)."""
+    rb, rows = ce3_geometry(x3)
     if d != 256:
-        return split_count(n, 128)
+        return split_count(n, rb)
     split, sk = _dw_costs(n, Mv, x3, d)
     best_k = dw_split_count(n, Mv, x3, d)
     plan, cost = best_k, split[best_k]
@@ -128,24 +146,25 @@ def dw_plan(n, Mv, x3, d, both_grads=True):
     if sk < cost:
         plan, cost = 0, sk
     slots = _ncu()
-    blocks = -(-n // 128)
+    blocks = -(-n // rb)
     full = blocks // slots * slots
     if full and full < blocks:
-        rem = n - full * 128
+        rem = n - full * rb
         rsplit, _ = _dw_costs(rem, Mv, x3, d)
         k = dw_split_count(rem, Mv, x3, d)
-        sweep = max(1, -(-Mv // (32 if x3 else 64)))
-        t_wg = 16.0 if x3 else 9.0
+        sweep = max(1, -(-Mv // rows))
+        t_wg = 16.0 if x3 else BF16_FIT['dw_wg']
         hyb = full // slots * (sweep + t_wg) + rsplit[k]
         if k > 1 and hyb < cost:
             plan, cost = -k, hyb
     return plan
 
 
-def dw_full_rows(n):
+def dw_full_rows(n, x3):
     """The W rows of the whole rounds of a remainder dW plan (dw_plan < 0): ⌊row blocks / CUs⌋·CUs row blocks, with
     the CU count the plan was costed on (ce_head_backward takes it as dw_full instead of re-deriving it)."""
-    return -(-n // 128) // _ncu() * _ncu() * 128
+    rb = ce3_geometry(x3)[0]
+    return -(-n // rb) // _ncu() * _ncu() * rb
 
 
 def ce_kind(precision, d):
@@ -462,7 +481,7 @@ class LossHeadFn(Function):
             nr = dw_plan(n, Mv0 + Mv1, mode == 0, d, gW is not None and gb is not None)
             hd += T.ce_head_backward(saved, W, inv, tc, Mv0, Mv1, coef, gscale, float(m.lam), gW, gb, gwpad, gbpad,
                                      tplan.get() if tplan is not None else None, nr, mode,
-                                     dw_full_rows(n) if nr < 0 else 0)
+                                     dw_full_rows(n, mode == 0) if nr < 0 else 0)
         imgT = [weight_img(m.Da_w.view(d, d), kind, trans=True), weight_img(m.Db_w.view(d, d), kind, trans=True)]
         gD = [_grad_target(t) for t in (m.Da_w, m.Da_b, m.Db_w, m.Db_b)]
         sub = [r.idx[:r.n] if r is not None else None for r in rsets]
@@ -527,7 +546,7 @@ class LossHeadFn(Function):
                         lib(entry + '_sk', Hb, Wb, bias2, Mv, n, d, crow, gW, gb, ws, wsb, s)
                         del ws
                     elif nr < 0:  # whole rounds unsplit onto the gradients, the remainder row blocks −nr ways
-                        full = dw_full_rows(n)
+                        full = dw_full_rows(n, ctx.x3)
                         rem, k = n - full, -nr
                         ic = (2 if ctx.x3 else 1) * d
                         lib(entry, Hb, Wb, bias2, Mv, full, d, 0, crow, gW, gb, s)

@@ -331,6 +331,10 @@ int c2dsr_ce_rows(const float* part_m, const float* part_s, int n_split, int M, 
  * dw with n_rsplit == 0 (also c2dsr_ce3b_fused_dw): one split whose workgroups own their columns, added straight
  * onto dWp [n][D] / dbp [n] (the parameters' epoch-long gradients, trainer.py:42 — no partials, no sum). */
 int c2dsr_ce3_supported(int D);
+/* The sweep geometry of the fused-CE instantiations (split = 1: fp32 mode's split-bf16 kernels, 0: bf16 mode's):
+ * what = 0 → stationary rows per workgroup (the launch grid's row block: 128 / 192), 1 → swept rows per LDS tile
+ * (32 / 32); -1 for another `what`.  The host's split plans (c2dsr_amd/losshead.py) size their grids with it. */
+int c2dsr_ce3_geometry(int split, int what);
 int c2dsr_f32_split_bf16(const float* x, long rows, int D, long rows_out, void* out, void* stream);
 int c2dsr_ce3_fused_fwd_u(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_split,
                           float* part_m, float* part_s, float* Up, const float* padlogit, const int64_t* tgt,

@@ -59,8 +59,8 @@ def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None, b16=False):
     gW = torch.zeros(n, D, device=DEV) if g0 is None else g0[0].clone().to(DEV)
     gb = torch.zeros(n, device=DEV) if g0 is None else g0[1].clone().to(DEV)
     if nr <= -2:  # whole rounds of row blocks added directly, the remainder's row blocks split -nr ways and summed
-        from c2dsr_amd.losshead import _ncu
-        full = -(-n // 128) // _ncu() * _ncu() * 128
+        from c2dsr_amd.losshead import dw_full_rows
+        full = dw_full_rows(n, not b16)  # whole rounds of the instantiation's row blocks (128 / 192 rows)
         rem, k = n - full, -nr
         ic = Wx.shape[1]
         lib(pre + 'dw', Hx, Wx, bias2, M, full, D, 0, crow, gW, gb, s)
