@@ -562,20 +562,20 @@ def main():
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    ndev = torch.cuda.device_count()
-    if world > 1 and ndev < world:
-        # rehearsal on a smaller box (e.g. two ranks on one GPU): RCCL cannot put two ranks on one
-        # device, so the collectives go through gloo; the 8-GPU node uses RCCL
-        local = local % max(ndev, 1)
+    device = torch.device('cuda', 0)
     if world > 1:
-        backend = os.environ.get('C2DSR_DIST_BACKEND') or ('nccl' if ndev >= world else 'gloo')
-        torch.cuda.set_device(local)
-        if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-        else:
-            dist.init_process_group(backend)
-    device = torch.device('cuda', local)
+        # the trainer's own set-up (c2dsr_amd.trainer.init_data_parallel): the rank's device is cuda:LOCAL_RANK (modulo
+        # the visible devices), the group RCCL when every rank drives its own GPU (device identities exchanged over
+        # the launcher's store), gloo only when ranks share one (a rehearsal on a smaller box); C2DSR_DP_BACKEND
+        # (or the older C2DSR_DIST_BACKEND) overrides
+        from types import SimpleNamespace
+        from c2dsr_amd.trainer import init_data_parallel
+        if os.environ.get('C2DSR_DIST_BACKEND') and not os.environ.get('C2DSR_DP_BACKEND'):
+            os.environ['C2DSR_DP_BACKEND'] = os.environ['C2DSR_DIST_BACKEND']
+        ns = SimpleNamespace(device=torch.device('cuda', 0))
+        rank, world = init_data_parallel(ns)
+        device = ns.device
+        log(f'[bench] rank {rank}/{world} on {device} ({dist.get_backend()})')
     if opt.config == 'c5':
         run_c5(opt, world, rank, device)
         if world > 1:
