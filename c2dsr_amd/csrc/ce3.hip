@@ -735,7 +735,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
 
 // stream-K partials of the split row blocks (ce3_kernel MODE 1): gW[rb] += Σ_w slot(w, rb), w ascending over the
 // workgroups whose unit ranges overlap row block rb (a block swept whole by one workgroup was written directly).
-// One block per row block; thread → (row, float4 column).
+// Blocks (row block, 16-row group): thread → (row, float4 column) — 16 rows per block, not the whole row block: the
+// per-element loop over the contributing workgroups is a chain of dependent adds, and one block per row block
+// (66 / 90 blocks at the Entertainment-Education heads) left the combine latency-bound at 118 µs.
 __device__ __forceinline__ int sk_wg_of(long u, long U, int nwg) {
   int w = (int)((u * nwg) / U);
   while (w + 1 < nwg && ((long)(w + 1) * U) / nwg <= u) ++w;
@@ -746,14 +748,14 @@ __global__ __launch_bounds__(256) void ce3_sk_combine_kernel(const float* __rest
                                                              const float* __restrict__ slot_b, int n, int D, long T,
                                                              int nwg, int RB, float* __restrict__ gW,
                                                              float* __restrict__ gb) {
-  const int rb = blockIdx.x;
+  const int rb = blockIdx.x, r0 = blockIdx.y * 16;
   const long U = (long)((n + RB - 1) / RB) * T;
   const long ub = (long)rb * T, ue = ub + T - 1;
   const int wa = sk_wg_of(ub, U, nwg), wz = sk_wg_of(ue, U, nwg);
   if (wa == wz) return;  // uniform
   const int C4 = D / 4;
-  for (int i = threadIdx.x; i < RB * (C4 + 1); i += 256) {
-    const int r = i / (C4 + 1), c = i % (C4 + 1);  // c == C4: the bias column
+  for (int i = threadIdx.x; i < 16 * (C4 + 1); i += 256) {
+    const int r = r0 + i / (C4 + 1), c = i % (C4 + 1);  // c == C4: the bias column
     const long row = (long)rb * RB + r;
     if (row >= n) continue;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -842,7 +844,8 @@ int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec
   C2_CHECK_LAUNCH();
   if (sk_nwg) {
     const long T = (n_w + tile_rows<SPLIT>() - 1) / tile_rows<SPLIT>();
-    ce3_sk_combine_kernel<<<c2::ceil_div(n_s, RB), 256, 0, st>>>(slot_w, slot_b, n_s, D, T, sk_nwg, RB, out, ps);
+    ce3_sk_combine_kernel<<<dim3(c2::ceil_div(n_s, RB), RB / 16), 256, 0, st>>>(slot_w, slot_b, n_s, D, T, sk_nwg, RB,
+                                                                                out, ps);
     C2_CHECK_LAUNCH();
   }
   return 0;
