@@ -10,6 +10,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <vector>
 
 namespace {
 
@@ -97,27 +98,73 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ROUNDS = 8;
 constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;
 
+// ------------------------------------------------------------------ index plans, several per launch
+// A training step builds eight plans (the item and position indices of its five lookups, positions shared); one
+// launch per pass covers all of them (jobs): the blocks of job j are [beg[j], beg[j+1]) of the launch, and a block
+// reads its job's fields through pj() (a select chain over the launch's job table: uniform, no indexed kernel-argument
+// access).  Per plan: keys prepared, one LSD pass per 8-bit digit (histogram + scatter), then the split list (count +
+// emit) — 1 + 2·passes + 2 launches for any number of plans instead of that many per plan.
+constexpr int PJ_MAX = 12;
+struct PlanJobs {
+  int nj, shift;               // jobs in this launch; the radix passes' digit shift
+  int beg[PJ_MAX + 1];         // first block of each job
+  int n[PJ_MAX], aux[PJ_MAX];  // entries; n_keys (prep) / radix blocks of the job (hist, scatter)
+  const int64_t* idx[PJ_MAX];
+  uint32_t *ki[PJ_MAX], *vi[PJ_MAX], *ko[PJ_MAX], *vo[PJ_MAX];  // prep: ki / vi; passes: in → out; plans: ki = sorted keys
+  uint32_t* hist[PJ_MAX];      // passes: digit histograms [256][radix blocks]; plans: per-block counts
+  int4* splits[PJ_MAX];
+  int* suboff[PJ_MAX];
+  int2* subs[PJ_MAX];
+  int* counts[PJ_MAX];
+};
+template <typename T>
+__device__ __forceinline__ T pj(const T (&a)[PJ_MAX], int j) {
+  T r = a[0];
+#pragma unroll
+  for (int k = 1; k < PJ_MAX; ++k) r = j == k ? a[k] : r;
+  return r;
+}
+// this block's job and its block index / block count within the job
+__device__ __forceinline__ int pj_job(const PlanJobs& P, int& lb, int& nb) {
+  int j = 0, b0 = P.beg[0], b1 = P.beg[1];  // (beg[k] = the launch's block total for k >= nj)
+#pragma unroll
+  for (int k = 1; k < PJ_MAX; ++k)
+    if (k < P.nj && (int)blockIdx.x >= P.beg[k]) {
+      j = k;
+      b0 = P.beg[k];
+      b1 = P.beg[k + 1];
+    }
+  lb = (int)blockIdx.x - b0;
+  nb = b1 - b0;
+  return j;
+}
+
 // an index outside [0, n_keys) becomes the key n_keys (sorted after every valid key; the segment sums never follow
 // a key >= n_out) and sets `bit` in the caller's error word: a bad index never reaches a gradient read-modify-write
-__global__ void prep_keys_kernel(const int64_t* __restrict__ idx, int n, int n_keys, int bit, uint32_t* __restrict__ keys,
-                                 uint32_t* __restrict__ vals, int* __restrict__ err) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void prep_keys_kernel(PlanJobs P, int bit, int* __restrict__ err) {
+  int lb, nb;
+  const int j = pj_job(P, lb, nb);
+  const int n = pj(P.n, j), n_keys = pj(P.aux, j);
+  const int i = lb * 256 + threadIdx.x;
   if (i < n) {
-    const int64_t v = idx[i];
+    const int64_t v = pj(P.idx, j)[i];
     const bool ok = v >= 0 && v < n_keys;
     if (!ok && err) atomicOr(err, bit);
-    keys[i] = ok ? (uint32_t)v : (uint32_t)n_keys;
-    vals[i] = (uint32_t)i;
+    pj(P.ki, j)[i] = ok ? (uint32_t)v : (uint32_t)n_keys;
+    pj(P.vi, j)[i] = (uint32_t)i;
   }
 }
 
-__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint32_t* __restrict__ keys, int n, int shift,
-                                                            int nblocks, uint32_t* __restrict__ hist) {
+__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(PlanJobs P) {
   __shared__ uint32_t h[256];
+  int lb, nb;
+  const int j = pj_job(P, lb, nb);
+  const uint32_t* __restrict__ keys = pj(P.ki, j);
+  const int n = pj(P.n, j), shift = P.shift;
   h[threadIdx.x] = 0;
   // every round's key loaded up front (one memory round trip per block instead of one per round)
   uint32_t k[RS_ROUNDS];
-  const int base = blockIdx.x * RS_TILE;
+  const int base = lb * RS_TILE;
 #pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const int i = base + r * RS_THREADS + threadIdx.x;
@@ -130,20 +177,24 @@ __global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint32_t* __r
     if (i < n) atomicAdd(&h[(k[r] >> shift) & 255u], 1u);
   }
   __syncthreads();
-  hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+  pj(P.hist, j)[threadIdx.x * nb + lb] = h[threadIdx.x];
 }
 
-__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* __restrict__ kin,
-                                                               const uint32_t* __restrict__ vin, int n, int shift,
-                                                               int nblocks, const uint32_t* __restrict__ offs,  // digit histograms [256][nblocks]
-                                                               uint32_t* __restrict__ kout,
-                                                               uint32_t* __restrict__ vout) {
+__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(PlanJobs P) {
   __shared__ uint32_t wcnt[4][256];
   __shared__ uint32_t woff[4][256];
   __shared__ uint32_t run[256];
   __shared__ uint32_t gbase[256];
+  int lb, nblocks;
+  const int j = pj_job(P, lb, nblocks);
+  const uint32_t* __restrict__ kin = pj(P.ki, j);
+  const uint32_t* __restrict__ vin = pj(P.vi, j);
+  uint32_t* __restrict__ kout = pj(P.ko, j);
+  uint32_t* __restrict__ vout = pj(P.vo, j);
+  const uint32_t* __restrict__ offs = pj(P.hist, j);  // digit histograms [256][nblocks]
+  const int n = pj(P.n, j), shift = P.shift;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int base = blockIdx.x * RS_TILE;
+  const int base = lb * RS_TILE;
   // every round's key and row loaded up front: their latency overlaps the offset computation below instead of
   // opening each of the RS_ROUNDS rounds
   uint32_t kr[RS_ROUNDS], vr[RS_ROUNDS];
@@ -163,7 +214,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint32_t* 
 #pragma unroll 8
     for (int b = 0; b < nblocks; ++b) {
       const uint32_t c = ht[b];
-      pre += b < (int)blockIdx.x ? c : 0u;
+      pre += b < lb ? c : 0u;
       tot += c;
     }
     // exclusive scan of tot over the 256 digits (four waves: in-wave shuffles, then the wave totals)
@@ -252,12 +303,15 @@ __device__ __forceinline__ int split_span(const uint32_t* K, int n, int i) {
 __device__ __forceinline__ uint32_t n_subs(int span) { return (uint32_t)((span + SUBP - 1) / SUBP); }
 
 // per block: the splits starting among its PL_B entries and their SUBP-piece sub-ranges → cnt[b], cnt[nb + b]
-__global__ __launch_bounds__(PL_T) void plan_count_kernel(const uint32_t* __restrict__ K, int n,
-                                                          uint32_t* __restrict__ cnt) {
+__global__ __launch_bounds__(PL_T) void plan_count_kernel(PlanJobs P) {
   __shared__ uint32_t red[2][PL_T / 64];
+  int lb, nb;
+  const int j = pj_job(P, lb, nb);
+  const uint32_t* __restrict__ K = pj(P.ki, j);
+  const int n = pj(P.n, j);
   uint32_t q = 0, u = 0;
-  for (int j = 0; j < PL_E; ++j) {
-    const int i = blockIdx.x * PL_B + j * PL_T + threadIdx.x;
+  for (int e = 0; e < PL_E; ++e) {
+    const int i = lb * PL_B + e * PL_T + threadIdx.x;
     if (i < n && split_start(K, n, i)) {
       ++q;
       u += n_subs(split_span(K, n, i));
@@ -278,8 +332,9 @@ __global__ __launch_bounds__(PL_T) void plan_count_kernel(const uint32_t* __rest
       t += red[0][w];
       v += red[1][w];
     }
-    cnt[blockIdx.x] = t;
-    cnt[gridDim.x + blockIdx.x] = v;
+    uint32_t* cnt = pj(P.hist, j);
+    cnt[lb] = t;
+    cnt[nb + lb] = v;
   }
 }
 
@@ -299,20 +354,25 @@ __device__ __forceinline__ uint32_t block_prefix(uint32_t v, uint32_t* red) {
   return base + inc - v;
 }
 
-// writes splits[j] = {key, first chunk, chunks spanned, 0} in entry order, and — the work a single-workgroup
-// launch (plan_subs) used to do after it — every split's SUBP-piece sub-ranges: suboff[j] = its first sub,
-// subs[suboff[j] + y] = (j, y·SUBP), suboff[splits] = counts[2] = the sub total; counts[1] = the split total, and the
+// writes splits[s] = {key, first chunk, chunks spanned, 0} in entry order, and — the work a single-workgroup
+// launch (plan_subs) did after it until round 6 — every split's SUBP-piece sub-ranges: suboff[s] = its first sub,
+// subs[suboff[s] + y] = (s, y·SUBP), suboff[splits] = counts[2] = the sub total; counts[1] = the split total, and the
 // plan's error word (counts[3]) starts at 0.  A block's first output slots are the sums of the earlier blocks'
 // counts (plan_count_kernel), read here (≤ a few hundred u32 from L2) instead of a separate scan launch.
-__global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restrict__ K, int n,
-                                                         const uint32_t* __restrict__ cnt, int4* __restrict__ splits,
-                                                         int* __restrict__ suboff, int2* __restrict__ subs,
-                                                         int* __restrict__ counts) {
+__global__ __launch_bounds__(PL_T) void plan_emit_kernel(PlanJobs P) {
   __shared__ uint32_t red[2][PL_T / 64];
+  int lb, nb;
+  const int j = pj_job(P, lb, nb);
+  const uint32_t* __restrict__ K = pj(P.ki, j);
+  const uint32_t* __restrict__ cnt = pj(P.hist, j);
+  int4* __restrict__ splits = pj(P.splits, j);
+  int* __restrict__ suboff = pj(P.suboff, j);
+  int2* __restrict__ subs = pj(P.subs, j);
+  const int n = pj(P.n, j);
   uint32_t bs = 0, bu = 0;
-  for (int b = threadIdx.x; b < (int)blockIdx.x; b += PL_T) {
+  for (int b = threadIdx.x; b < lb; b += PL_T) {
     bs += cnt[b];
-    bu += cnt[gridDim.x + b];
+    bu += cnt[nb + b];
   }
   for (int o = 32; o > 0; o >>= 1) {
     bs += __shfl_xor(bs, o, 64);
@@ -330,33 +390,34 @@ __global__ __launch_bounds__(PL_T) void plan_emit_kernel(const uint32_t* __restr
   }
   __syncthreads();
   // thread t owns entries [i0, i0 + PL_E): contiguous, so the order is kept
-  const int i0 = blockIdx.x * PL_B + threadIdx.x * PL_E;
+  const int i0 = lb * PL_B + threadIdx.x * PL_E;
   uint32_t fs = 0, nu = 0;
   int span[PL_E];
-  for (int j = 0; j < PL_E; ++j) {
-    const int i = i0 + j;
-    span[j] = 0;
+  for (int e = 0; e < PL_E; ++e) {
+    const int i = i0 + e;
+    span[e] = 0;
     if (i < n && split_start(K, n, i)) {
-      fs |= 1u << j;
-      span[j] = split_span(K, n, i);
-      nu += n_subs(span[j]);
+      fs |= 1u << e;
+      span[e] = split_span(K, n, i);
+      nu += n_subs(span[e]);
     }
   }
   uint32_t os = base_s + block_prefix(__popc(fs), red[0]);
   uint32_t ou = base_u + block_prefix(nu, red[1]);
-  for (int j = 0; j < PL_E; ++j) {
-    if (fs >> j & 1) {
-      const int i = i0 + j;
-      splits[os] = make_int4((int)K[i], i / SEG_CH, span[j], 0);
+  for (int e = 0; e < PL_E; ++e) {
+    if (fs >> e & 1) {
+      const int i = i0 + e;
+      splits[os] = make_int4((int)K[i], i / SEG_CH, span[e], 0);
       suboff[os] = (int)ou;
-      const uint32_t k = n_subs(span[j]);
+      const uint32_t k = n_subs(span[e]);
       for (uint32_t y = 0; y < k; ++y) subs[ou + y] = make_int2((int)os, (int)(y * SUBP));
       ++os;
       ou += k;
     }
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == PL_T - 1) {  // owns the last entries: os / ou are the totals
+  if (lb == nb - 1 && threadIdx.x == PL_T - 1) {  // owns the last entries: os / ou are the totals
     suboff[os] = (int)ou;
+    int* counts = pj(P.counts, j);
     counts[1] = (int)os;
     counts[2] = (int)ou;
     counts[3] = 0;
@@ -806,29 +867,100 @@ size_t seg_slot_bytes(int n, int d) { return align256((size_t)c2::ceil_div(n, SE
 size_t seg_slot2_bytes(int n, int d) { return align256((size_t)max_subs(n) * d * 4); }
 size_t seg_ws_bytes(int n, int d) { return 2 * seg_slot_bytes(n, d) + seg_slot2_bytes(n, d); }
 
-// sort idx[0..n) (values < n_keys) → k0/v0 sorted (key, original row), stable; then the work lists
-int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t s, int* err = nullptr) {
-  int bits = 1;
-  while ((1l << bits) < (long)n_keys + 1) ++bits;  // keys 0 .. n_keys (n_keys: an out-of-range index)
-  // the passes alternate between the two buffer pairs: start in the pair the last pass does not write
-  const bool odd = ((bits + 7) / 8) & 1;
-  uint32_t *ki = odd ? w.k1 : w.k0, *vi = odd ? w.v1 : w.v0, *ko = odd ? w.k0 : w.k1, *vo = odd ? w.v0 : w.v1;
-  prep_keys_kernel<<<c2::ceil_div(n, 256), 256, 0, s>>>(idx, n, n_keys, C2DSR_IDX_ERR_PLAN, ki, vi, err);
-  for (int shift = 0; shift < bits; shift += 8) {
-    rs_hist_kernel<<<w.nblocks, RS_THREADS, 0, s>>>(ki, n, shift, w.nblocks, w.hist);
-    rs_scatter_kernel<<<w.nblocks, RS_THREADS, 0, s>>>(ki, vi, n, shift, w.nblocks, w.hist, ko, vo);
-    uint32_t* t = ki; ki = ko; ko = t;
-    t = vi; vi = vo; vo = t;
+// sort idx[0..n) (values < n_keys) → k0/v0 sorted (key, original row), stable; then the work lists.  Several
+// plans at once: one launch per pass over all of them (PlanJobs; groups of PJ_MAX).
+struct PlanSpec {
+  const int64_t* idx;
+  int n, n_keys;
+  Plan w;
+};
+
+void build_plan_group(const PlanSpec* js, int m, hipStream_t s, int* err) {
+  uint32_t *ki[PJ_MAX], *vi[PJ_MAX], *ko[PJ_MAX], *vo[PJ_MAX];
+  int passes[PJ_MAX], max_passes = 0;
+  PlanJobs P{};
+  int b = 0;
+  for (int k = 0; k < m; ++k) {
+    const Plan& w = js[k].w;
+    int bits = 1;
+    while ((1l << bits) < (long)js[k].n_keys + 1) ++bits;  // keys 0 .. n_keys (n_keys: an out-of-range index)
+    passes[k] = (bits + 7) / 8;
+    max_passes = std::max(max_passes, passes[k]);
+    // the passes alternate between the two buffer pairs: start in the pair the last pass does not write
+    const bool odd = passes[k] & 1;
+    ki[k] = odd ? w.k1 : w.k0, vi[k] = odd ? w.v1 : w.v0, ko[k] = odd ? w.k0 : w.k1, vo[k] = odd ? w.v0 : w.v1;
+    P.beg[k] = b;
+    P.n[k] = js[k].n;
+    P.aux[k] = js[k].n_keys;
+    P.idx[k] = js[k].idx;
+    P.ki[k] = ki[k];
+    P.vi[k] = vi[k];
+    b += c2::ceil_div(js[k].n, 256);
   }
-  if (ki != w.k0) {  // (not taken: the start pair makes the last pass land in k0 / v0)
-    (void)hipMemcpyAsync(w.k0, ki, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
-    (void)hipMemcpyAsync(w.v0, vi, (size_t)n * 4, hipMemcpyDeviceToDevice, s);
+  P.nj = m;
+  for (int k = m; k <= PJ_MAX; ++k) P.beg[k] = b;
+  prep_keys_kernel<<<b, 256, 0, s>>>(P, C2DSR_IDX_ERR_PLAN, err);
+  for (int p = 0; p < max_passes; ++p) {
+    PlanJobs Q{};
+    Q.shift = 8 * p;
+    int q = 0;
+    b = 0;
+    for (int k = 0; k < m; ++k) {
+      if (passes[k] <= p) continue;
+      Q.beg[q] = b;
+      Q.n[q] = js[k].n;
+      Q.aux[q] = js[k].w.nblocks;
+      Q.ki[q] = ki[k], Q.vi[q] = vi[k], Q.ko[q] = ko[k], Q.vo[q] = vo[k];
+      Q.hist[q] = js[k].w.hist;
+      b += js[k].w.nblocks;
+      std::swap(ki[k], ko[k]);
+      std::swap(vi[k], vo[k]);
+      ++q;
+    }
+    Q.nj = q;
+    for (int k = q; k <= PJ_MAX; ++k) Q.beg[k] = b;
+    rs_hist_kernel<<<b, RS_THREADS, 0, s>>>(Q);
+    rs_scatter_kernel<<<b, RS_THREADS, 0, s>>>(Q);
   }
-  const int pb = c2::ceil_div(n, PL_B);
-  plan_count_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt);
-  plan_emit_kernel<<<pb, PL_T, 0, s>>>(w.k0, n, w.bcnt, w.splits, w.suboff, w.subs, w.counts);
+  PlanJobs C{};
+  b = 0;
+  for (int k = 0; k < m; ++k) {
+    const Plan& w = js[k].w;
+    C.beg[k] = b;
+    C.n[k] = js[k].n;
+    C.ki[k] = w.k0;  // (the start pair makes the last pass land in k0 / v0)
+    C.hist[k] = w.bcnt;
+    C.splits[k] = w.splits;
+    C.suboff[k] = w.suboff;
+    C.subs[k] = w.subs;
+    C.counts[k] = w.counts;
+    b += c2::ceil_div(js[k].n, PL_B);
+  }
+  C.nj = m;
+  for (int k = m; k <= PJ_MAX; ++k) C.beg[k] = b;
+  plan_count_kernel<<<b, PL_T, 0, s>>>(C);
+  plan_emit_kernel<<<b, PL_T, 0, s>>>(C);
+}
+
+int build_plans(const PlanSpec* js, int count, hipStream_t s, int* err) {
+  PlanSpec g[PJ_MAX];
+  int m = 0;
+  for (int k = 0; k < count; ++k) {
+    if (js[k].n == 0) continue;  // nothing to sort (no launch reads such a plan)
+    g[m++] = js[k];
+    if (m == PJ_MAX) {
+      build_plan_group(g, m, s, err);
+      m = 0;
+    }
+  }
+  if (m) build_plan_group(g, m, s, err);
   C2_CHECK_LAUNCH();
   return 0;
+}
+
+int build_plan(const int64_t* idx, int n, int n_keys, const Plan& w, hipStream_t s, int* err = nullptr) {
+  const PlanSpec j{idx, n, n_keys, w};
+  return build_plans(&j, 1, s, err);
 }
 
 int g_ncu = 0;
@@ -974,6 +1106,25 @@ C2_API int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, s
   Plan p;
   if (plan_bytes < plan_layout(n, &p, (char*)plan)) return (int)hipErrorInvalidValue;
   return build_plan(idx, n, n_keys, p, (hipStream_t)stream, err);
+}
+
+// c2dsr_index_plan over several index tensors, one launch per pass for all of them: desc = HOST array of count
+// records of five int64 (idx, n, n_keys, plan, plan_bytes)
+C2_API int c2dsr_index_plans(const int64_t* desc, int count, int* err, void* stream) {
+  if (count < 0 || (count && !desc)) return (int)hipErrorInvalidValue;
+  std::vector<PlanSpec> js;
+  js.reserve(count);
+  for (int k = 0; k < count; ++k) {
+    const int64_t* r = desc + 5 * k;
+    const int64_t n = r[1], n_keys = r[2];
+    if (n < 0 || n > 0x7fffffff || n_keys <= 0 || n_keys >= 0x7fffffff || (n && (!r[0] || !r[3])))
+      return (int)hipErrorInvalidValue;
+    PlanSpec j{(const int64_t*)(uintptr_t)r[0], (int)n, (int)n_keys, Plan{}};
+    const size_t need = plan_layout((int)n, &j.w, (char*)(uintptr_t)r[3]);
+    if (n && (r[4] < 0 || (size_t)r[4] < need)) return (int)hipErrorInvalidValue;  // (an empty job writes nothing)
+    js.push_back(j);
+  }
+  return build_plans(js.data(), count, (hipStream_t)stream, err);
 }
 
 // two segment-sum jobs (items, positions) run side by side: two slot regions

@@ -243,12 +243,14 @@ void index_plans(const std::vector<Tensor>& idx, std::vector<int64_t> n_keys, co
   bytes_at_least(buf, op, "buf", tot);
   for (const Tensor& t : idx) dev(t, op, "idx");
   dev(buf, op, "buf");
+  std::vector<int64_t> desc;  // one launch per radix pass for all the plans (c2dsr_index_plans)
   size_t o = 0;
   for (size_t i = 0; i < idx.size(); ++i) {
-    c2t::launch("c2dsr_index_plan", &c2dsr_index_plan, idx[i].data_ptr<int64_t>(), (int)idx[i].numel(),
-                (int)n_keys[i], (void*)((char*)buf.data_ptr() + o), sizes[i], c2t::errp(), S());
+    desc.insert(desc.end(), {(int64_t)(uintptr_t)idx[i].data_ptr<int64_t>(), (int64_t)idx[i].numel(), n_keys[i],
+                             (int64_t)(uintptr_t)((char*)buf.data_ptr() + o), (int64_t)sizes[i]});
     o += sizes[i];
   }
+  c2t::launch("c2dsr_index_plans", &c2dsr_index_plans, (const int64_t*)desc.data(), (int)idx.size(), c2t::errp(), S());
 }
 
 void check_plan(const OptT& plan, int64_t n, const char* op, const char* name) {

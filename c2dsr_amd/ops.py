@@ -754,6 +754,7 @@ class GCNPropFn(Function):
 
 # ----------------------------------------------------------------------------- index plans
 _side_streams = {}
+PLANS_BATCHED = True  # a step's plans in one launch per radix pass (False: one plan at a time, for A/Bs)
 PLAN_SRC = {}  # plan buffer data_ptr -> data_ptr of the index tensor it sorts (roofline accounting)
 
 
@@ -788,7 +789,11 @@ class IndexPlan:
         for (idx, _), buf in zip(pairs, bufs):
             PLAN_SRC[buf.data_ptr()] = idx.data_ptr()
         with torch.cuda.stream(side):  # one stage operator for all the plans, on the side stream
-            stage_ops().index_plans([idx for idx, _ in pairs], [int(k) for _, k in pairs], whole)
+            if PLANS_BATCHED:  # one launch per radix pass over all the plans (c2dsr_index_plans)
+                stage_ops().index_plans([idx for idx, _ in pairs], [int(k) for _, k in pairs], whole)
+            else:  # plan by plan (the round-5 form; tools/bench_ab.py c2dsr_amd.ops.PLANS_BATCHED)
+                for (idx, k), buf, nb in zip(pairs, bufs, sizes):
+                    lib('c2dsr_index_plan', idx, idx.numel(), int(k), buf, nb, error_word(), stream())
         whole.record_stream(side)
         ev = torch.cuda.Event()
         ev.record(side)

@@ -82,6 +82,10 @@ size_t c2dsr_index_plan_bytes(int n);
 /* An index outside [0, n_keys) becomes the key n_keys (sorted last, never followed by a segment sum) and sets
  * C2DSR_IDX_ERR_PLAN in *err (err may be NULL). */
 int c2dsr_index_plan(const int64_t* idx, int n, int n_keys, void* plan, size_t plan_bytes, int* err, void* stream);
+/* c2dsr_index_plan of several index tensors with one launch per pass for all of them (a training step's eight
+ * lookup plans: 9 launches instead of 60): desc = HOST array of count records of five int64 (idx, n, n_keys, plan,
+ * plan_bytes); each plan's bytes are exactly c2dsr_index_plan's.  Same error behaviour, per record. */
+int c2dsr_index_plans(const int64_t* desc, int count, int* err, void* stream);
 /* c2dsr_embed_bwd on prebuilt plans of seq / pos (seq_plan needed iff G, pos_plan iff gP); the item
  * and position sums share one launch of each pass.  A plan whose keys fall outside [0, n_items) /
  * [0, n_pos) or whose split lists are inconsistent is not followed: the int at

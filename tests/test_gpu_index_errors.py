@@ -195,3 +195,40 @@ def test_index_plan_structure(n, n_keys, hot):
     lib('c2dsr_index_plan', idx, n, n_keys, buf, pb, err, stream())
     _check_plan(buf, idx, n_keys)
     assert int(err[0]) == (4 if n > 10 else 0)
+
+
+def test_index_plans_batched_equal_single():
+    """c2dsr_index_plans (one launch per pass over all the plans, as the training step builds its eight lookup plans)
+    writes, plan by plan, exactly what c2dsr_index_plan writes for each alone: mixed key widths (1, 2 and 3 radix
+    passes in one launch set), an out-of-range index, a hot key, an empty job, more jobs than one launch group."""
+    from c2dsr_amd._lib import lib, stream
+    from c2dsr_amd.ops import _check_plan
+    rng = np.random.default_rng(7)
+    jobs = []
+    for k, (n, n_keys) in enumerate([(102_400, 36_846), (102_400, 51), (50_000, 64_000), (0, 10), (7, 3),
+                                     (30_000, 300), (20_000, 2 ** 20), (102_400, 51), (1, 5), (4096, 4096),
+                                     (9000, 100_000), (12_345, 70), (5000, 255), (5000, 256)]):
+        x = (rng.zipf(1.3, size=n) % n_keys).astype(np.int64)
+        if n > 100:
+            x[rng.random(n) < 0.3] = n_keys - 1
+            x[n // 3] = n_keys + 5 if k % 2 else -2
+        jobs.append((torch.from_numpy(x).to(DEV), n, n_keys))
+    sizes = [int(lib.raw('c2dsr_index_plan_bytes')(n)) if n else 256 for _, n, _ in jobs]
+    single = [torch.zeros(s, dtype=torch.uint8, device=DEV) for s in sizes]
+    multi = [torch.zeros(s, dtype=torch.uint8, device=DEV) for s in sizes]
+    e1 = torch.zeros(4, dtype=torch.int32, device=DEV)
+    e2 = torch.zeros(4, dtype=torch.int32, device=DEV)
+    for (idx, n, nk), buf, s in zip(jobs, single, sizes):
+        lib('c2dsr_index_plan', idx, n, nk, buf, s, e1, stream())
+    desc = torch.tensor([[idx.data_ptr(), n, nk, buf.data_ptr(), s] for (idx, n, nk), buf, s in zip(jobs, multi, sizes)],
+                        dtype=torch.int64)
+    lib('c2dsr_index_plans', desc, len(jobs), e2, stream())
+    torch.cuda.synchronize()
+    assert int(e1[0]) == int(e2[0]) == 4
+    for (idx, n, nk), a, b in zip(jobs, single, multi):
+        if n == 0:
+            continue
+        _check_plan(b, idx, nk)
+        # the bytes the consumers read (keys, rows, split list, counts, sub-ranges) are the single plan's
+        assert torch.equal(a[:8 * n], b[:8 * n]), (n, nk)
+        _check_plan(a, idx, nk)

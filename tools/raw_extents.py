@@ -19,6 +19,7 @@ EXTENTS = {
     'embed_fwd_rows': {'X': '(nq + nk) * d', 'err': '1'},
     'index_check': {'err': '1'},
     'index_plan': {'plan': 'plan_bytes', 'err': '1'},
+    'index_plans': {'err': '1'},
     'embed_bwd_planned': {'G': 'n_items * d', 'gP': 'n_pos * d', 'gXin': 'n_rows * d', 'workspace': 'ws_bytes'},
     'embed_fwd_b16': {'X': 'n_rows * d', 'err': '1'},
     'embed_bwd_planned_b16': {'G': 'n_items * d * 2', 'gP': 'n_pos * d', 'workspace': 'ws_bytes'},
