@@ -458,7 +458,8 @@ class Trainer(object):
         plans = None
         if m.training:
             # the embedding backward's sort plans of every pass (side stream), enqueued by the loss head right
-            # after its first long CE launch: ~110 small launches the host issues while the device is busy,
+            # after its first long CE launch (one launch per radix pass for all eight: c2dsr_index_plans), issued while
+            # the device is busy,
             # instead of ahead of the encoder passes, whose first kernels would wait behind them
             st = m.state
             pairs = [pr for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b), (neg_a, pos), (neg_b, pos))
