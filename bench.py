@@ -266,7 +266,7 @@ def hbm_traffic(precision):
 # the GPU kernels behind each timed C-ABI entry point (PMC counters are per GPU kernel; the embedding backward's
 # segment sums are the ROLE 0 instantiations — tools/pmc_traffic.py)
 SEG0 = ('seg_chunk_kernel<64, 0>', 'seg_split1_kernel<64, 0>', 'seg_split2_kernel<64, 0>')
-DRAM_KERNELS = {'c2dsr_gcn_spmm': ('spmm_kernel', 'spmm_pf_kernel', 'combine_kernel'),
+DRAM_KERNELS = {'c2dsr_gcn_spmm': ('spmm_kernel', 'spmm_pf_kernel', 'spmm_nc_kernel', 'combine_kernel'),
                 'c2dsr_gcn_spmm_b16': ('spmm_kernel', 'spmm_pf_kernel', 'combine_kernel'),
                 'c2dsr_embed_fwd': ('embed_fwd_kernel',), 'c2dsr_embed_fwd_b16': ('embed_fwd_kernel',),
                 'c2dsr_embed_fwd_rows': ('embed_fwd_rows_kernel',),

@@ -24,7 +24,7 @@ prec = sys.argv[3] if len(sys.argv) > 3 else 'fp32'
 K5 = (('ce3_kernel<256, 0, false', 'ce_rows_kernel', 'ce3_kernel<256, 1, false') if prec == 'bf16' else
       ('ce3_kernel<256, 0, true', 'ce_rows_kernel', 'ce3_kernel<256, 1, true'))
 # the segment sums of the embedding backward only: ROLE 0 instantiations (ROLE 1 = the classifier one-hot dW)
-K12 = ('spmm_kernel', 'spmm_pf_kernel', 'combine_kernel', 'embed_fwd_kernel', 'embed_fwd_rows_kernel', 'seg_chunk_kernel<64, 0>',
+K12 = ('spmm_kernel', 'spmm_pf_kernel', 'spmm_nc_kernel', 'combine_kernel', 'embed_fwd_kernel', 'embed_fwd_rows_kernel', 'seg_chunk_kernel<64, 0>',
        'seg_split1_kernel<64, 0>', 'seg_split2_kernel<64, 0>')
 PMC_STEPS = 3
 
