@@ -13,10 +13,12 @@ collectives run under the remaining backward kernels:
   (``EmbedFn.backward``, the tail of every encoder pass) has run and are issued then, under the three
   GCN backwards;
 * each **item table** (``embed_i``, ``embed_i_a``, ``embed_i_b``; one table when ``shared_item_embed``)
-  is final after the last GCN backward that reads it.  That backward's last SpMM runs in row chunks
-  (``GCNFn.backward`` asks ``row_cuts``) and each chunk's collective is issued as soon as the chunk is
-  written, under the chunks after it and the next table's backward — so only the last chunk of the
-  last table is exposed, not the whole table.
+  is final after the last GCN backward that reads it.  A table's GCN backward runs as soon as the last
+  lookup of its propagated table has run its backward (``ops.GradSink.lookup_done``; autograd alone would
+  run all three after every other node): table B's after pass B, table A's after pass A — their collectives
+  run under the backward of the passes after them — and the share table's after the last share pass.  Its
+  last SpMM runs in row chunks (``ops.gcn_backward`` asks ``row_cuts``) and each chunk's collective is
+  issued as soon as the chunk is written — so only the last chunk of the share table is exposed.
 
 Two modes:
   ``allreduce``  every rank ends with the summed gradient in ``fresh`` and runs the (replicated) AdamW

@@ -562,19 +562,46 @@ def gather_rows_nograd(x, rs):
 
 
 # ----------------------------------------------------------------------------- GCN (K1)
+EAGER_GCN = True  # a table's GCN backward runs as soon as its last lookup's backward has filled the sink
+
+
 class GradSink:
     """Dense gradient w.r.t. one GCN output table H, filled by every embedding lookup of H
-    (deterministic segment sums) and consumed once by the GCN backward."""
+    (deterministic segment sums) and consumed once by the GCN backward.
+
+    The GCN backward of a table needs nothing but this sink (the table's gradient E.grad is written by it alone), so
+    it runs as soon as the LAST lookup of H has run its backward (``lookup_done``, counting the lookups recorded since
+    the propagation, ``uses``) instead of where autograd would schedule GCNFn's node — after every other node, since
+    it was created first.  With data parallelism that issues each item table's collectives right after its own
+    pass (dp.py: table B's under the backward of passes A and share, table A's under the share pass), instead of all
+    three tables' at the end of the backward.  Same kernels on the same inputs: bit-identical gradients."""
 
     def __init__(self, n, d, device, state=None):
         self.n, self.d, self.device = n, d, device
         self.G = None
         self.state = state  # StepState: carries the data-parallel bucket hook (c2dsr_amd/dp.py)
+        self.uses = 0      # lookups of H recorded (with a backward to come) since the propagation
+        self.gcn = None    # (graph, n_gnn, p, keys, pad_row, E) of the propagation whose backward is pending
+        self.ran = False   # that backward already ran (eagerly): GCNFn.backward has nothing left to do
 
     def buf(self):
         if self.G is None:
             self.G = torch.zeros(self.n, self.d, device=self.device, dtype=torch.float32)
         return self.G
+
+    def propagated(self, gcn):
+        self.uses, self.gcn, self.ran = 0, gcn, False
+
+    def lookup_recorded(self):
+        self.uses += 1
+
+    def lookup_done(self):
+        """One lookup of H finished its backward; the last one runs the table's GCN backward now."""
+        self.uses -= 1
+        if self.uses == 0 and self.gcn is not None and EAGER_GCN and self.gcn[5].grad is not None:
+            args, self.gcn = self.gcn, None
+            gcn_backward(self, *args)
+            self.ran = True
 
 
 class RowShard:
@@ -655,6 +682,7 @@ class GCNFn(Function):
                                             flat_keys(keys))
             ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
             ctx.E = E
+            sink.propagated((graph, n_gnn, p, keys, pad_row, E))
             ctx.mark_non_differentiable(out)
             ctx.set_materialize_grads(False)
             return out, torch.empty((), device=E.device)
@@ -679,6 +707,7 @@ class GCNFn(Function):
             shard.pending.append(shard.gather(out_full))
         ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.sink = graph, n_gnn, p, keys, pad_row, sink
         ctx.E = E
+        sink.propagated((graph, n_gnn, p, keys, pad_row, E))
         ctx.mark_non_differentiable(out)
         ctx.set_materialize_grads(False)  # H gets no gradient: no [n, d] zeros for it
         tok = torch.empty((), device=E.device)  # value never read (the dependency is all it carries)
@@ -686,38 +715,46 @@ class GCNFn(Function):
 
     @staticmethod
     def backward(ctx, _gH, _gtok):
-        G = ctx.sink.G
-        E = ctx.E
-        if G is None:
-            notify_table(ctx.sink.state, E)
+        sink = ctx.sink
+        if sink.ran:  # run eagerly at the last lookup's backward (GradSink.lookup_done)
             return (None,) * 8
-        g = ctx.graph
-        n = ctx.n_gnn
-        direct = E.grad is not None
-        gE = E.grad if direct else torch.zeros_like(E)
-        T = stage_ops()
-        work, _, split, _, n_slots, col, val = g.plan(True)
-        p = float(ctx.p)
-        # gE += drop(Aᵀ T_1)/… + G/(n+1) + [i != pad]·G  (rounds before the last: T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k)
-        X = T.gcn_backward_rounds(G, work, split, col, val, g.n, n_slots, n, p, flat_keys(ctx.keys)) if n > 1 else G
-        k0, k1 = ctx.keys[0] if n > 0 else (0, 0)
-        cuts = row_cuts(ctx.sink.state, E) if direct and n > 0 else None
-        if cuts is None:
-            T.gcn_backward_final(X, G, gE, work, split, col, val, g.n, n_slots, n, p, k0, k1, ctx.pad_row, 1.0, 1.0)
-        else:  # this table's gradient is final chunk by chunk: its collectives start per chunk (dp.py)
-            part = torch.empty(max(n_slots, 1), G.shape[1], device=G.device, dtype=torch.float32)
-            for r0, r1 in cuts:
-                w0, w1, s0, s1 = g.row_slice(True, r0, r1)
-                if w1 > w0:  # roofline accounting of a row-slice launch (bench.py HbmTimer): its rows and edges
-                    rp = g.host_rowptr(True)
-                    SPMM_SLICE[work[w0:w1].data_ptr()] = (r1 - r0, int(rp[r1]) - int(rp[r0]))
-                T.gcn_backward_final(X, G, gE, work[w0:w1], split[s0:s1], col, val, g.n, n_slots, n, p, k0, k1,
-                                     ctx.pad_row, 1.0, 1.0, part)
-                notify_rows(ctx.sink.state, E, r0, r1)
-        ctx.sink.G = None
-        if direct:
-            notify_table(ctx.sink.state, E)  # E.grad final: its all-reduce runs under the next GCN backward
-        return (None if direct else gE), None, None, None, None, None, None, None
+        sink.gcn = None
+        gE = gcn_backward(sink, ctx.graph, ctx.n_gnn, ctx.p, ctx.keys, ctx.pad_row, ctx.E)
+        return gE, None, None, None, None, None, None, None
+
+
+def gcn_backward(sink, g, n, p, keys, pad_row, E):
+    """The GCN backward of one table from its lookup gradient (sink.G): E.grad += Aᵀ-chain(G) + the direct term
+    (in place when E.grad exists — returns None — else the gradient is returned)."""
+    G = sink.G
+    if G is None:
+        notify_table(sink.state, E)
+        return None
+    direct = E.grad is not None
+    gE = E.grad if direct else torch.zeros_like(E)
+    T = stage_ops()
+    work, _, split, _, n_slots, col, val = g.plan(True)
+    p = float(p)
+    # gE += drop(Aᵀ T_1)/… + G/(n+1) + [i != pad]·G  (rounds before the last: T_{k-1} = G/(n+1) + M_k ⊙ Aᵀ T_k)
+    X = T.gcn_backward_rounds(G, work, split, col, val, g.n, n_slots, n, p, flat_keys(keys)) if n > 1 else G
+    k0, k1 = keys[0] if n > 0 else (0, 0)
+    cuts = row_cuts(sink.state, E) if direct and n > 0 else None
+    if cuts is None:
+        T.gcn_backward_final(X, G, gE, work, split, col, val, g.n, n_slots, n, p, k0, k1, pad_row, 1.0, 1.0)
+    else:  # this table's gradient is final chunk by chunk: its collectives start per chunk (dp.py)
+        part = torch.empty(max(n_slots, 1), G.shape[1], device=G.device, dtype=torch.float32)
+        for r0, r1 in cuts:
+            w0, w1, s0, s1 = g.row_slice(True, r0, r1)
+            if w1 > w0:  # roofline accounting of a row-slice launch (bench.py HbmTimer): its rows and edges
+                rp = g.host_rowptr(True)
+                SPMM_SLICE[work[w0:w1].data_ptr()] = (r1 - r0, int(rp[r1]) - int(rp[r0]))
+            T.gcn_backward_final(X, G, gE, work[w0:w1], split[s0:s1], col, val, g.n, n_slots, n, p, k0, k1,
+                                 pad_row, 1.0, 1.0, part)
+            notify_rows(sink.state, E, r0, r1)
+    sink.G = None
+    if direct:
+        notify_table(sink.state, E)  # E.grad final: its all-reduce runs under the next GCN backward
+    return None if direct else gE
 
 
 class GCNPropFn(Function):
@@ -938,6 +975,8 @@ class EmbedFn(Function):
         ctx.P = P
         ctx.link = link
         ctx.plans = None
+        if sink is not None and any(ctx.needs_input_grad):
+            sink.lookup_recorded()
         if any(ctx.needs_input_grad[:3]) and (P.requires_grad or sink is not None):  # forward runs under no_grad
             # the sort plans are looked up (or built) when the backward needs them: a trainer enqueues the step's
             # plans where the stream has long kernels queued (trainer.train_batch), not between these launches
@@ -1000,6 +1039,7 @@ class EmbedFn(Function):
             WBATCH.lookup_done()
         if ctx.sink is not None:
             notify_lookup(ctx.sink.state)
+            ctx.sink.lookup_done()
         tok_grad = torch.empty((), device=seq.device)  # value never read (GCNFn.backward reads the sink)
         return tok_grad, None, gP_ret, None, None, None, None, None, None, None, None, None, None
 
@@ -1061,6 +1101,8 @@ class EncoderPassFn(Function):
         ctx.saved = outs[1:]
         ctx.args = (seq, pos, w, wd, rs, ks, rsi, ksi, keys, p, row_off, precision, att, scale)
         ctx.sink, ctx.P, ctx.n_items = sink, P, E.shape[0]
+        if sink is not None and any(ctx.needs_input_grad):
+            sink.lookup_recorded()
         return outs[0]
 
     @staticmethod
@@ -1102,6 +1144,7 @@ class EncoderPassFn(Function):
             WBATCH.lookup_done()
         if sink is not None:
             notify_lookup(sink.state)
+            sink.lookup_done()
         tok_grad = torch.empty((), device=gout.device)
         return (tok_grad, None, gP_ret) + (None,) * 13
 
