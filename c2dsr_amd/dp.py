@@ -193,13 +193,16 @@ class DPComm:
         self.done = [False] * len(plan.ranges)
         self.works = []
         self.issued = []  # (lo, hi) in issue order (tests)
+        self.work_of = {}  # (lo, hi) -> its collective's handle
 
     def _issue(self, lo, hi):
         i = self.plan.index[(lo, hi)]
         if not self.done[i]:
             self.done[i] = True
-            self.works.append(self.reduce(lo, hi))
+            w = self.reduce(lo, hi)
+            self.works.append(w)
             self.issued.append((lo, hi))
+            self.work_of[(lo, hi)] = w
 
     def head_done(self):
         """The loss head's backward returned: the classifier / discriminator gradients are final."""
@@ -237,14 +240,23 @@ class DPComm:
             for _, _, lo, hi in self.plan.table_chunks[k]:
                 self._issue(lo, hi)
 
-    def finish(self):
+    def finish(self, wait=True):
         """Issue whatever was not triggered (e.g. a backward that skipped a pass), then make the current
-        stream wait for every collective."""
+        stream wait for every collective — or (wait=False) leave the waits to the consumer: ``in_order()``."""
         for lo, hi in self.plan.ranges:
             self._issue(lo, hi)
-        for w in self.works:
-            w.wait()
-        self.works = []
+        if wait:
+            for w in self.works:
+                w.wait()
+            self.works, self.work_of = [], {}
+
+    def in_order(self):
+        """[(lo, hi, handle)] of every range in issue order, for a consumer that waits range by range: the
+        optimizer updates the ranges whose sums have landed while the last ones are still on the wire
+        (FlatAdamW.step)."""
+        out = [(lo, hi, self.work_of[(lo, hi)]) for lo, hi in self.issued]
+        self.works, self.work_of = [], {}
+        return out
 
 
 def notify_lookup(state):

@@ -35,6 +35,16 @@ class FlatAdamW(torch.optim.Optimizer):
             flat.release_accum()  # the shard above replaces it (1/p of the state, not 1 + 1/p)
         self.n_steps = 0
         self.accumulate = True  # grads accumulate until zero_grad (Q3)
+        # data parallel: the step's reduction ranges with their collectives' handles in issue order
+        # (DPComm.in_order); the next step() waits for each range's sum just before updating that range, so the
+        # update of the early ranges runs while the last ones are still being summed
+        self.comm = None
+
+    def sync_grads(self):
+        """Data parallel: make the current stream wait for every pending range's sum (the gradient store is then
+        final) — for a caller that reads the gradients between the backward and step()."""
+        for _, _, w in self.comm or ():
+            w.wait()
 
     def zero_grad(self, set_to_none: bool = True):
         """Reference semantics: clears the epoch accumulation (grads would be None)."""
@@ -48,16 +58,27 @@ class FlatAdamW(torch.optim.Optimizer):
         b1, b2 = g['betas']
         f = self.flat
         hyper = (float(g['lr']), float(g['weight_decay']), float(b1), float(b2), float(g['eps']), self.n_steps)
-        if self.zero is None:
+        comm, self.comm = self.comm, None
+        acc = self.accum if self.accumulate else None
+        if self.zero is None and comm is None:
             # direct store (one device): fresh is accum — read only, 36 B/param; without epoch accumulation
             # the same buffer is this step's gradient and is cleared
-            stage_ops().adamw_step(f.param, f.fresh, self.accum if self.accumulate else None, self.m, self.v,
-                                   self.vmax, *hyper)
+            stage_ops().adamw_step(f.param, f.fresh, acc, self.m, self.v, self.vmax, *hyper)
+        elif self.zero is None:  # range by range as the sums land (the update is elementwise: the same bits)
+            for lo, hi, w in comm:
+                w.wait()
+                stage_ops().adamw_step(f.param[lo:hi], f.fresh[lo:hi], None if acc is None else acc[lo:hi],
+                                       self.m[lo:hi], self.v[lo:hi], self.vmax[lo:hi], *hyper)
         else:
             z = self.zero
-            for _, _, olo, ohi, off in z.parts:
-                n, sl = ohi - olo, slice(off, off + ohi - olo)
-                stage_ops().adamw_step(f.param[olo:ohi], z.gshard[sl], self.accum[sl] if self.accumulate else None,
+            order = [(lo, hi, None) for lo, hi, _, _, _ in z.parts] if comm is None else comm
+            part = {(lo, hi): (olo, ohi, off) for lo, hi, olo, ohi, off in z.parts}
+            for lo, hi, w in order:
+                if w is not None:
+                    w.wait()
+                olo, ohi, off = part[(lo, hi)]
+                sl = slice(off, off + ohi - olo)
+                stage_ops().adamw_step(f.param[olo:ohi], z.gshard[sl], None if acc is None else acc[sl],
                                        self.m[sl], self.v[sl], self.vmax[sl], *hyper)
             f.fresh.zero_()  # the next backward accumulates into it
             for w in z.gather():

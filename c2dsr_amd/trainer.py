@@ -492,7 +492,8 @@ class Trainer(object):
                 self._backward(loss)
             finally:
                 hook, m.state.grad_hook = m.state.grad_hook, None
-            hook.finish()
+            hook.finish(wait=False)
+            self.optimizer.comm = hook.in_order()  # the optimizer waits for each range's sum just before its update
             meta.finish_values()
         else:
             self._backward(loss)

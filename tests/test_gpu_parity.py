@@ -68,6 +68,8 @@ def capture(tr):
         return out
 
     def step():
+        if hasattr(tr.optimizer, 'sync_grads'):  # data parallel: the ranges' sums land before step() updates them
+            tr.optimizer.sync_grads()
         torch.cuda.synchronize()
         box['grads'] = {n: m.flat.grad_total(n).detach().cpu().clone() for n in m.flat.names}
         return orig_step()
