@@ -800,6 +800,9 @@ __device__ __forceinline__ WMask rows_mask(const int64_t* __restrict__ seq, int6
 #ifndef ATTN_ROWS_OCC
 #define ATTN_ROWS_OCC 2
 #endif
+#ifndef ATTN_PD_EARLY
+#define ATTN_PD_EARLY 1
+#endif
 #ifndef ATTN_ROWS_OCC_F
 #define ATTN_ROWS_OCC_F ATTN_ROWS_OCC
 #endif
@@ -946,6 +949,30 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
   }
   const float sc = 1.0f / sqrtf((float)dh);
   const int CT = dh >> 5;
+  // ---- dV = Pdᵀ·dO, dK = dSᵀ·Q/√dh: transpose through this wave's LDS tile T[i][j] (stride 65)
+  constexpr int TLD = 65;
+  auto put = [&](const f32x16& a, const f32x16& b, bool two, int ti) {
+    const int i = 32 * ti + r;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int j0 = creg(q, lane);
+      T[i * TLD + j0] = a[q];
+      if (two) T[i * TLD + 32 + j0] = b[q];
+    }
+  };
+  // T starts as garbage: every entry the products read ([0, 32·TI) x [0, 32·TJ)) is written first.  Pd goes to LDS
+  // before the dQ product (ATTN_PD_EARLY, round 6): its 64 registers are dead through dQ, which then holds only dS —
+  // the row kernel's spills 294 → 115 (fp32 out) / 133 → 86 (bf16 out); rows bwd fp32 out 139.8 → 134.7 µs, domain-pass
+  // shape 158.0 → 151.0 µs (tools/attn_micro.py), main line +0.4 % (same-box A/B)
+  auto put_pd = [&] {
+    put(p0, p3, T3, 0);
+    if constexpr (TI > 1) put(p1, p2, TJ > 1, 1);
+    if constexpr (!ROWS && TJ > 1) {  // full layout: tile (tj = 1, ti = 0) is above the diagonal: zero
+#pragma unroll
+      for (int q = 0; q < 16; ++q) T[r * TLD + 32 + creg(q, lane)] = 0.f;
+    }
+  };
+  if constexpr (ATTN_PD_EARLY) put_pd();
   // ---- dQ = dS·K/√dh (lane = column, rows = queries)
   {
     const auto ksrc = rows_rsrc(K, nk, ks, dh);
@@ -980,17 +1007,6 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
       }
     }
   }
-  // ---- dV = Pdᵀ·dO, dK = dSᵀ·Q/√dh: transpose through this wave's LDS tile T[i][j] (stride 65)
-  constexpr int TLD = 65;
-  auto put = [&](const f32x16& a, const f32x16& b, bool two, int ti) {
-    const int i = 32 * ti + r;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int j0 = creg(q, lane);
-      T[i * TLD + j0] = a[q];
-      if (two) T[i * TLD + 32 + j0] = b[q];
-    }
-  };
   auto keys_out = [&](const float* __restrict__ Src, long ss, float scale, OT* __restrict__ Dst) {
     const auto src = rows_rsrc(Src, nq, ss, dh);
 #pragma unroll 1
@@ -1027,13 +1043,7 @@ __device__ __forceinline__ void bwd_wave_body(const float* __restrict__ Q, long 
       for (int j = 32 * TJ + hi; j < nkw; j += 2) Dst[(long)j * dks + c] = (OT)0.f;  // keys past the tiles
     }
   };
-  // T starts as garbage: every entry the products read ([0, 32·TI) x [0, 32·TJ)) is written first
-  put(p0, p3, T3, 0);
-  if constexpr (TI > 1) put(p1, p2, TJ > 1, 1);
-  if constexpr (!ROWS && TJ > 1) {  // full layout: tile (tj = 1, ti = 0) is above the diagonal: zero
-#pragma unroll
-    for (int q = 0; q < 16; ++q) T[r * TLD + 32 + creg(q, lane)] = 0.f;
-  }
+  if constexpr (!ATTN_PD_EARLY) put_pd();
   wave_lds_sync();
   keys_out(dO, ds, 1.0f, dV);
   wave_lds_sync();
