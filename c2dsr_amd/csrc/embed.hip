@@ -116,6 +116,7 @@ struct PlanJobs {
   int* suboff[PJ_MAX];
   int2* subs[PJ_MAX];
   int* counts[PJ_MAX];
+  int* scnt[PJ_MAX];           // plans: pass B's per-split arrival counters (zeroed here)
 };
 template <typename T>
 __device__ __forceinline__ T pj(const T (&a)[PJ_MAX], int j) {
@@ -368,6 +369,7 @@ __global__ __launch_bounds__(PL_T) void plan_emit_kernel(PlanJobs P) {
   int4* __restrict__ splits = pj(P.splits, j);
   int* __restrict__ suboff = pj(P.suboff, j);
   int2* __restrict__ subs = pj(P.subs, j);
+  int* __restrict__ scnt = pj(P.scnt, j);
   const int n = pj(P.n, j);
   uint32_t bs = 0, bu = 0;
   for (int b = threadIdx.x; b < lb; b += PL_T) {
@@ -409,6 +411,7 @@ __global__ __launch_bounds__(PL_T) void plan_emit_kernel(PlanJobs P) {
       const int i = i0 + e;
       splits[os] = make_int4((int)K[i], i / SEG_CH, span[e], 0);
       suboff[os] = (int)ou;
+      scnt[os] = 0;
       const uint32_t k = n_subs(span[e]);
       for (uint32_t y = 0; y < k; ++y) subs[ou + y] = make_int2((int)os, (int)(y * SUBP));
       ++os;
@@ -437,6 +440,9 @@ constexpr int SEG_U = SEG_U_CFG;  // rows in flight per lane group
 #endif
 #ifndef SEG_PREF
 #define SEG_PREF 0
+#endif
+#ifndef SEG_MERGE  // pass B's level 2 by each split's last-arriving level-1 block (no second launch)
+#define SEG_MERGE 1
 #endif
 
 struct RowSrc {
@@ -477,6 +483,7 @@ struct SegJob {
   const int2* subs;            // plan: (split, first piece) of every SUBP-piece sub-range
   const int* suboff;           // plan: first sub of every split
   const int* counts;           // plan: [pieces, splits, subs]
+  int* scnt;                   // plan: per-split arrival counters of pass B (zero between uses)
   int* err;                    // plan: error word (debug)
   int n, n_out, skip_key, nblocks;
   RowSrc src;
@@ -677,6 +684,7 @@ struct SplitView {
   const int2* subs;
   const int* suboff;
   const int* counts;
+  int* scnt;
   int* err;
   int n, n_out, skip_key, d;
   float* out;
@@ -685,7 +693,7 @@ struct SplitView {
   c2::tbf16* out16;
   __device__ __forceinline__ SplitView(const SegJob& j0, const SegJob& j1, bool y)
       : splits(y ? j1.splits : j0.splits), subs(y ? j1.subs : j0.subs), suboff(y ? j1.suboff : j0.suboff),
-        counts(y ? j1.counts : j0.counts), err(y ? j1.err : j0.err), n(y ? j1.n : j0.n),
+        counts(y ? j1.counts : j0.counts), scnt(y ? j1.scnt : j0.scnt), err(y ? j1.err : j0.err), n(y ? j1.n : j0.n),
         n_out(y ? j1.n_out : j0.n_out), skip_key(y ? j1.skip_key : j0.skip_key), d(y ? j1.src.d : j0.src.d),
         out(y ? j1.out : j0.out), ph(y ? j1.ph : j0.ph), pt(y ? j1.pt : j0.pt), slot2(y ? j1.slot2 : j0.slot2),
         out16(y ? j1.out16 : j0.out16) {}
@@ -696,13 +704,14 @@ struct SplitView {
 // pass B, level 1: one block per sub-range of SUBP pieces of a split (grid-stride over the plan's
 // sub list, blockIdx.y = job): the pieces (tail of the split's first chunk, heads of the following
 // ones) are dealt round-robin to the block's lane groups (eight loads in flight each), the group
-// sums added in group order → slot2[sub].  Level 2: one lane group per split adds its level-1
-// sums in sub order to out[key].  Fixed orders → deterministic; a padding run of thousands of
-// pieces is spread over many blocks.
+// sums added in group order → slot2[sub].  Level 2 (SEG_MERGE, since round 6: in the same launch, by the
+// block that finishes the split's last sub-range; else seg_split2_kernel): the split's level-1 sums in sub order
+// onto out[key].  Fixed orders → deterministic; a padding run of thousands of pieces is spread over many blocks.
 template <int LPR, int ROLE = 0>
 __global__ __launch_bounds__(1024) void seg_split1_kernel(SegJob j0, SegJob j1) {
   constexpr int GROUPS = 1024 / LPR;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [GROUPS][d]
+  __shared__ int s_last;  // (SEG_MERGE) this block finished the last sub-range of its split
   const SplitView J(j0, j1, blockIdx.y != 0);
   const int g = threadIdx.x / LPR;
   const int lane = threadIdx.x % LPR;
@@ -740,11 +749,64 @@ __global__ __launch_bounds__(1024) void seg_split1_kernel(SegJob j0, SegJob j1) 
       *(float4*)(red + g * d + c) = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
     __syncthreads();
+    // level 2 in the same launch (SEG_MERGE): out[key] += the split's level-1 sums in sub order — the order
+    // seg_split2_kernel used, so the same bits.  A split of ONE sub-range (all but the hottest keys) is finished here
+    // from the sum just computed; a longer one by its LAST sub-range to finish, through the guide's counter hand-off
+    // (MI355X_MICROARCH.md §Workgroup dispatch…, cdna_hip_programming.md §6 G16): every wave drains its slot2 stores,
+    // barrier, lane 0 releases at agent scope (then waits itself: the fence's own wait can be dropped) and takes a
+    // ticket from the plan's per-split counter; the last one acquires at agent scope before the barrier that lets its
+    // waves read the other sub-ranges' sums, and puts the counter back to 0 for the plan's next use.
+    const int key = sp.x, b0 = J.suboff[si], b1 = J.suboff[si + 1];
+    const bool bad2 = key < 0 || key >= J.n_out || b0 < 0 || b1 <= b0 || b1 > nsub;
+    const bool direct = SEG_MERGE && b1 - b0 == 1;
     for (int c = threadIdx.x * 4; c < d; c += 1024 * 4) {
       float4 t = *(const float4*)(red + c);
       for (int q = 1; q < GROUPS; ++q) t = t + *(const float4*)(red + q * d + c);
-      *(float4*)(J.slot2 + (long)j * d + c) = t;
+      if (!direct) {
+        *(float4*)(J.slot2 + (long)j * d + c) = t;
+      } else if (!bad2 && key != J.skip_key) {
+        const long o = (long)key * d;
+        const float4 u = J.out16 ? c2::ld4(J.out16 + o + c) : *(const float4*)(J.out + o + c);
+        if (J.out16)
+          c2::st4(J.out16 + o + c, u + t);
+        else
+          *(float4*)(J.out + o + c) = u + t;
+      }
     }
+    if (direct && bad2 && threadIdx.x == 0) atomicOr(J.err, 8);
+#if SEG_MERGE
+    if (!direct) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool last = !bad2 && __hip_atomic_fetch_add(J.scnt + si, 1, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) == b1 - b0 - 1;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (bad2) atomicOr(J.err, 8);
+        s_last = last;
+      }
+      __syncthreads();
+      if (s_last) {
+        if (key != J.skip_key) {
+          const long o = (long)key * d;
+          for (int c = threadIdx.x * 4; c < d; c += 1024 * 4) {
+            float4 t = J.out16 ? c2::ld4(J.out16 + o + c) : *(const float4*)(J.out + o + c);
+            for (int k = b0; k < b1; ++k) t = t + *(const float4*)(J.slot2 + (long)k * d + c);
+            if (J.out16)
+              c2::st4(J.out16 + o + c, t);
+            else
+              *(float4*)(J.out + o + c) = t;
+          }
+        }
+        if (threadIdx.x == 0) J.scnt[si] = 0;
+      }
+    }
+#endif
     __syncthreads();
   }
 }
@@ -825,6 +887,7 @@ struct Plan {
   int* suboff;
   int2* subs;
   uint32_t *k1, *v1, *hist, *bcnt;
+  int* scnt;
   int nblocks;
 };
 
@@ -850,9 +913,10 @@ size_t plan_layout(int n, Plan* p, char* base) {
   char* v1 = take((size_t)n * 4);
   char* hist = take((size_t)256 * nblocks * 4);
   char* bc = take((size_t)pb * 8);  // per plan block: split count, sub count
+  char* sc = take((size_t)(n / SEG_CH + 1) * 4);  // per split: pass B arrivals (plan_emit zeroes them)
   if (p)
     *p = Plan{(uint32_t*)k0, (uint32_t*)v0, (int4*)sp, (int*)ct, (int*)so, (int2*)sb,
-              (uint32_t*)k1, (uint32_t*)v1, (uint32_t*)hist, (uint32_t*)bc, nblocks};
+              (uint32_t*)k1, (uint32_t*)v1, (uint32_t*)hist, (uint32_t*)bc, (int*)sc, nblocks};
   return off;
 }
 
@@ -934,6 +998,7 @@ void build_plan_group(const PlanSpec* js, int m, hipStream_t s, int* err) {
     C.suboff[k] = w.suboff;
     C.subs[k] = w.subs;
     C.counts[k] = w.counts;
+    C.scnt[k] = w.scnt;
     b += c2::ceil_div(js[k].n, PL_B);
   }
   C.nj = m;
@@ -984,8 +1049,10 @@ void seg_launch(SegJob j0, SegJob j1, int njobs, hipStream_t s) {
   if (nmax > SEG_CH) {
     dim3 g1(std::max(1, std::min(max_subs(nmax), 2 * num_cus())), njobs);
     seg_split1_kernel<LPR, ROLE><<<g1, 1024, (size_t)(1024 / LPR) * j0.src.d * 4, s>>>(j0, j1);
-    dim3 g2(std::max(1, std::min(c2::ceil_div(c2::ceil_div(nmax, SEG_CH), GROUPS), 2 * num_cus())), njobs);
-    seg_split2_kernel<LPR, ROLE><<<g2, 256, 0, s>>>(j0, j1);
+    if (!SEG_MERGE) {
+      dim3 g2(std::max(1, std::min(c2::ceil_div(c2::ceil_div(nmax, SEG_CH), GROUPS), 2 * num_cus())), njobs);
+      seg_split2_kernel<LPR, ROLE><<<g2, 256, 0, s>>>(j0, j1);
+    }
   }
 }
 
@@ -998,6 +1065,7 @@ SegJob seg_job(const Plan& p, int n, int n_out, const RowSrc& src, float* out, c
   j.subs = p.subs;
   j.suboff = p.suboff;
   j.counts = p.counts;
+  j.scnt = p.scnt;
   j.err = p.counts + 3;
   j.n = n;
   j.n_out = n_out;
