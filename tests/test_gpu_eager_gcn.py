@@ -45,7 +45,7 @@ def _run(eager, name, steps=2):
         ops.EAGER_GCN = True
 
 
-@pytest.mark.parametrize('name', ['base', 'var'])
+@pytest.mark.parametrize('name', ['base', 'var', 'shared'])
 def test_eager_gcn_backward_is_bit_identical_and_early(name):
     p1, a1, l1, ev1 = _run(True, name)
     p0, a0, l0, ev0 = _run(False, name)
