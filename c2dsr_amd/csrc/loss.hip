@@ -653,7 +653,48 @@ __global__ void rowscale_kernel(const float* __restrict__ x, const float* __rest
   out[i] = accumulate ? out[i] + v : v;
 }
 
+// The two bilinear discriminators' row-scale products of the MI-loss backward (trainer.py:104-119 through D_a / D_b)
+// in ONE launch, blockIdx.y = discriminator j (replaces 4 c2dsr_rowscale launches per discriminator):
+//   dx1_j = dS[2j] ⊙ U_j[0:B] + dS[2j+1] ⊙ U_j[B:2B],  dU_j[0:B] = dS[2j] ⊙ x1_j,  dU_j[B:2B] = dS[2j+1] ⊙ x1_j
+// (dS [4][B] row scales; U_j, dU_j [2B][d]; x1_j, dx1_j [B][d]); the two products of dx1 are rounded before their sum
+__global__ void bilinear_ds_kernel(const float* __restrict__ Ua, const float* __restrict__ Ub,
+                                   const float* __restrict__ xa, const float* __restrict__ xb,
+                                   const float* __restrict__ dS, int B, int d, float* __restrict__ dxa,
+                                   float* __restrict__ dxb, float* __restrict__ dUa, float* __restrict__ dUb) {
+  const long n4 = (long)B * d / 4;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int j = blockIdx.y;
+  const float4* U = (const float4*)(j ? Ub : Ua);
+  const float4* x = (const float4*)(j ? xb : xa);
+  float4* dx = (float4*)(j ? dxb : dxa);
+  float4* dU = (float4*)(j ? dUb : dUa);
+  const int r = (int)(i * 4 / d);
+  const float s0 = dS[(long)(2 * j) * B + r], s1 = dS[(long)(2 * j + 1) * B + r];
+  const float4 u0 = U[i], u1 = U[n4 + i], xv = x[i];
+  // explicitly rounded products and sum (no fma contraction: each product is rounded as rowscale's was)
+  auto rsum = [&](float p, float q) {
+    float a = s0 * p, b = s1 * q;
+    asm volatile("" : "+v"(a), "+v"(b));  // rounded products: the sum below must not contract into an fma
+    return a + b;
+  };
+  dx[i] = make_float4(rsum(u0.x, u1.x), rsum(u0.y, u1.y), rsum(u0.z, u1.z), rsum(u0.w, u1.w));
+  dU[i] = make_float4(s0 * xv.x, s0 * xv.y, s0 * xv.z, s0 * xv.w);
+  dU[n4 + i] = make_float4(s1 * xv.x, s1 * xv.y, s1 * xv.z, s1 * xv.w);
+}
+
 }  // namespace
+
+C2_API int c2dsr_bilinear_ds(const float* Ua, const float* Ub, const float* x1a, const float* x1b, const float* dS,
+                             int B, int d, float* dx1a, float* dx1b, float* dUa, float* dUb, void* stream) {
+  if (B < 0 || d <= 0 || d % 4) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  const long n4 = (long)B * d / 4;
+  bilinear_ds_kernel<<<dim3((unsigned)c2::ceil_div(n4, 256), 2), 256, 0, (hipStream_t)stream>>>(Ua, Ub, x1a, x1b, dS, B,
+                                                                                                d, dx1a, dx1b, dUa, dUb);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
 
 C2_API int c2dsr_pool_weights(const int64_t* gm, int B, int L, float* w, void* stream) {
   if (B == 0) return 0;

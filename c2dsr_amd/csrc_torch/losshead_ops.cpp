@@ -437,21 +437,18 @@ std::vector<Tensor> loss_disc_backward(const std::vector<Tensor>& fwd, const Ten
   const Tensor* x1s[2] = {&Phx, &Phy};
   const Tensor* X2s[2] = {&X2a, &X2b};
   const Tensor* Us[2] = {&Ua, &Ub};
-  Tensor dx1[2], dX2[2];
+  Tensor dx1[2], dX2[2], dUs[2];
+  for (int j = 0; j < 2; ++j) {
+    dx1[j] = at::empty({B, d}, f32);
+    dUs[j] = at::empty({2 * B, d}, f32);
+  }
+  // both discriminators' row-scale products in one launch
+  c2t::launch("c2dsr_bilinear_ds", &c2dsr_bilinear_ds, (const float*)F(*Us[0]), (const float*)F(*Us[1]),
+              (const float*)F(*x1s[0]), (const float*)F(*x1s[1]), (const float*)F(dS), (int)B, (int)d, F(dx1[0]),
+              F(dx1[1]), F(dUs[0]), F(dUs[1]), S());
   for (int j = 0; j < 2; ++j) {
     const int k = 2 * j;
-    const float* U = F(*Us[j]);
-    const float* x1 = F(*x1s[j]);
-    dx1[j] = at::empty({B, d}, f32);
-    c2t::launch("c2dsr_rowscale", &c2dsr_rowscale, U, (const float*)(F(dS) + k * B), (long)(B * d), (int)d, F(dx1[j]),
-                0, S());
-    c2t::launch("c2dsr_rowscale", &c2dsr_rowscale, (const float*)(U + B * d), (const float*)(F(dS) + (k + 1) * B),
-                (long)(B * d), (int)d, F(dx1[j]), 1, S());
-    Tensor dU = at::empty({2 * B, d}, f32);
-    c2t::launch("c2dsr_rowscale", &c2dsr_rowscale, x1, (const float*)(F(dS) + k * B), (long)(B * d), (int)d, F(dU), 0,
-                S());
-    c2t::launch("c2dsr_rowscale", &c2dsr_rowscale, x1, (const float*)(F(dS) + (k + 1) * B), (long)(B * d), (int)d,
-                F(dU) + B * d, 0, S());
+    const Tensor& dU = dUs[j];
     dX2[j] = at::empty({2 * B, d}, f32);
     proj(mode, 2 * B, d, d, dU, imgT[j], dX2[j]);
     const OptT& gWd = gD[k];

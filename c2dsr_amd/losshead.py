@@ -599,13 +599,11 @@ class LossHeadFn(Function):
         Phx, Phy, X2a, X2b, Ua, Ub, dS = ctx.mi
         lib('c2dsr_scale_ds', dS, 4 * B, gscale, float(1.0 - m.lam), s)
         dP = {}
+        dx1s = [torch.empty(B, d, **f32) for _ in range(2)]
+        dUs = [torch.empty(2 * B, d, **f32) for _ in range(2)]
+        lib('c2dsr_bilinear_ds', Ua, Ub, Phx, Phy, dS, B, d, dx1s[0], dx1s[1], dUs[0], dUs[1], s)
         for (x1, X2, U, Wd, bd, k) in ((Phx, X2a, Ua, m.Da_w, m.Da_b, 0), (Phy, X2b, Ub, m.Db_w, m.Db_b, 2)):
-            dx1 = torch.empty(B, d, **f32)
-            lib('c2dsr_rowscale', U, dS[k], B * d, d, dx1, 0, s)
-            lib('c2dsr_rowscale', U[B:], dS[k + 1], B * d, d, dx1, 1, s)
-            dU = torch.empty(2 * B, d, **f32)
-            lib('c2dsr_rowscale', x1, dS[k], B * d, d, dU, 0, s)
-            lib('c2dsr_rowscale', x1, dS[k + 1], B * d, d, dU[B:], 0, s)
+            dx1, dU = dx1s[k // 2], dUs[k // 2]
             dX2 = torch.empty(2 * B, d, **f32)
             kind = rg_kind(m.precision, 2 * B, d, d)
             b16 = kind is not None and wg_kind(m.precision, 2 * B, d, d) is not None

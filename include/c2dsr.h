@@ -272,6 +272,12 @@ int c2dsr_loss_accumulate(const float* loss, const float* loss_rec, const float*
                           void* stream);
 int c2dsr_scale_ds(float* ds, int n, const float* gscale, float f, void* stream);
 int c2dsr_rowscale(const float* x, const float* s, long n, int d, float* out, int accumulate, void* stream);
+/* The MI-loss backward's row-scale products of both bilinear discriminators in one launch (trainer.py:104-119 through
+ * D_a / D_b; replaces eight c2dsr_rowscale calls): for j = a, b (dS [4][B]: rows 2j, 2j+1 scale the positive and
+ * negative pairs): dx1_j = dS[2j] ⊙ U_j[0:B] + dS[2j+1] ⊙ U_j[B:2B] (each product rounded, then summed),
+ * dU_j[0:B] = dS[2j] ⊙ x1_j, dU_j[B:2B] = dS[2j+1] ⊙ x1_j.  U_j, dU_j [2B][d]; x1_j, dx1_j [B][d]; d % 4 == 0. */
+int c2dsr_bilinear_ds(const float* Ua, const float* Ub, const float* x1a, const float* x1b, const float* dS, int B, int d,
+                      float* dx1a, float* dx1b, float* dUa, float* dUb, void* stream);
 
 /* K5 fused classifier head + cross-entropy (bf16 MFMA, logits never materialised; trainer.py:131-154).
  * Hb [M][D], Wb [n][D] bf16 (D = 128 or 256); bias2 = bias·log2e padded with -inf to n_pad (multiple of

@@ -1024,3 +1024,23 @@ def test_wgemm_multi_segments(b16):
     refb = 0.25 + sum((r(y) if b16 else y.double()).sum(0) for y in dYs)
     assert rel(outs[0][0], refW) < 2e-3 and rel(outs[0][1], refb) < 1e-5
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_bilinear_ds_equals_rowscale_products():
+    """c2dsr_bilinear_ds (both discriminators' row-scale products of the MI-loss backward in one launch) equals the
+    separately rounded products and their sum, bit for bit (torch elementwise ops as the reference)."""
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(5)
+    B, d = 1000, 256
+    Ua, Ub = torch.randn(2 * B, d, generator=g), torch.randn(2 * B, d, generator=g)
+    xa, xb = torch.randn(B, d, generator=g), torch.randn(B, d, generator=g)
+    dS = torch.randn(4, B, generator=g)
+    dev = [t.to(DEV) for t in (Ua, Ub, xa, xb, dS)]
+    out = [torch.empty(B, d, device=DEV), torch.empty(B, d, device=DEV), torch.empty(2 * B, d, device=DEV),
+           torch.empty(2 * B, d, device=DEV)]
+    lib('c2dsr_bilinear_ds', *dev, B, d, *out, stream())
+    torch.cuda.synchronize()
+    for j, (U, x) in enumerate(((Ua, xa), (Ub, xb))):
+        s0, s1 = dS[2 * j][:, None], dS[2 * j + 1][:, None]
+        assert torch.equal(out[j].cpu(), (s0 * U[:B]) + (s1 * U[B:]))
+        assert torch.equal(out[2 + j].cpu(), torch.cat([s0 * x, s1 * x]))

@@ -67,6 +67,7 @@ EXTENTS = {
     'loss_accumulate': {'acc3': '3'},
     'scale_ds': {'ds': 'n'},
     'rowscale': {'out': 'n'},
+    'bilinear_ds': {'dx1a': 'B * d', 'dx1b': 'B * d', 'dUa': '2 * B * d', 'dUb': '2 * B * d'},
     'f32_to_bf16': {'y': 'n * 2'},
     'ce_bias2': {'bias2': 'n_pad'},
     'ce_fused_fwd': {'part_m': 'n_split * M', 'part_s': 'n_split * M', 'lse': 'M', 'lse2': 'M', 'loss_row': 'M'},
