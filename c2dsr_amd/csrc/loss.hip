@@ -361,6 +361,25 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ x
   if (lane == 0) out[r * ldo] = s + (bias ? bias[0] : 0.f);
 }
 
+// the four discriminator scores in one launch (blockIdx.y = k): S[k][b] = x_k[b]·y_k[b] + bias_k with
+// (x, y) = (x1a, Ua[0:B]), (x1a, Ua[B:2B]), (x1b, Ub[0:B]), (x1b, Ub[B:2B]) — rowdot_kernel's sum per row, the same bits
+__global__ __launch_bounds__(256) void mi_scores_kernel(const float* __restrict__ x1a, const float* __restrict__ Ua,
+                                                        const float* __restrict__ ba, const float* __restrict__ x1b,
+                                                        const float* __restrict__ Ub, const float* __restrict__ bb,
+                                                        int B, int d, float* __restrict__ S) {
+  const int k = blockIdx.y;
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= B) return;
+  const float* x = k < 2 ? x1a : x1b;
+  const float* y = (k < 2 ? Ua : Ub) + (long)(k & 1) * B * d;
+  const float* bias = k < 2 ? ba : bb;
+  float s = 0.f;
+  for (int c = lane; c < d; c += 64) s += x[r * d + c] * y[r * d + c];
+  s = c2::wave_sum(s);
+  if (lane == 0) S[(long)k * B + r] = s + (bias ? bias[0] : 0.f);
+}
+
 // s: [4][B] = sim_a_pos, sim_a_neg, sim_b_pos, sim_b_neg (labels 1,0,1,0).
 // loss_mi = Σ_k Σ_b BCE(s_k, y_k) / Bn;  ds[k][b] = (σ(s) - y)/Bn  (Bn = global batch; = B on one device)
 __global__ __launch_bounds__(1024) void mi_loss_kernel(const float* __restrict__ s, int B, float Bn,
@@ -793,6 +812,15 @@ C2_API int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int 
                         float* out, long ldo, void* stream) {
   if (M == 0) return 0;
   rowdot_kernel<<<c2::ceil_div(M, 4), 256, 0, (hipStream_t)stream>>>(x, ldx, y, ldy, M, d, bias, out, ldo);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
+C2_API int c2dsr_mi_scores(const float* x1a, const float* Ua, const float* ba, const float* x1b, const float* Ub,
+                           const float* bb, int B, int d, float* S, void* stream) {
+  if (B < 0 || d <= 0) return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  mi_scores_kernel<<<dim3((unsigned)c2::ceil_div(B, 4), 4), 256, 0, (hipStream_t)stream>>>(x1a, Ua, ba, x1b, Ub, bb, B, d,
+                                                                                       S);
   C2_CHECK_LAUNCH();
   return 0;
 }

@@ -127,14 +127,8 @@ std::vector<Tensor> loss_disc_forward(const std::vector<Tensor>& h, const std::v
   proj(mode, 2 * B, d, d, X2a, img[0], Ua);
   proj(mode, 2 * B, d, d, X2b, img[1], Ub);
   Tensor Sc = at::empty({4, B}, f32);
-  auto rowdot = [&](const Tensor& x, const float* U, const OptT& bias, int k) {
-    c2t::launch("c2dsr_rowdot", &c2dsr_rowdot, (const float*)F(x), (long)d, U, (long)d, (int)B, (int)d, FO(bias),
-                F(Sc) + k * B, (long)1, S());
-  };
-  rowdot(Phx, F(Ua), D[1], 0);
-  rowdot(Phx, F(Ua) + B * d, D[1], 1);
-  rowdot(Phy, F(Ub), D[3], 2);
-  rowdot(Phy, F(Ub) + B * d, D[3], 3);
+  c2t::launch("c2dsr_mi_scores", &c2dsr_mi_scores, (const float*)F(Phx), (const float*)F(Ua), (const float*)FO(D[1]),
+              (const float*)F(Phy), (const float*)F(Ub), (const float*)FO(D[3]), (int)B, (int)d, F(Sc), S());
   Tensor dS = at::empty({4, B}, f32);
   c2t::launch("c2dsr_mi_loss", &c2dsr_mi_loss, (const float*)F(Sc), (int)B, (int)B_global, F(vec) + 8, F(dS), S());
   return {wa, wb, Phx, Phy, X2a, X2b, Ua, Ub, dS};

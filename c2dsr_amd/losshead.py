@@ -271,10 +271,7 @@ class LossHeadFn(Function):
             else:
                 gemm(X2, Wd, U, M=2 * B, N=d, K=d, transB=1, precision=FP32)
         S = torch.empty(4, B, **f32)
-        lib('c2dsr_rowdot', Phx, d, Ua, d, B, d, m.Da_b, S[0], 1, s)
-        lib('c2dsr_rowdot', Phx, d, Ua[B:], d, B, d, m.Da_b, S[1], 1, s)
-        lib('c2dsr_rowdot', Phy, d, Ub, d, B, d, m.Db_b, S[2], 1, s)
-        lib('c2dsr_rowdot', Phy, d, Ub[B:], d, B, d, m.Db_b, S[3], 1, s)
+        lib('c2dsr_mi_scores', Phx, Ua, m.Da_b, Phy, Ub, m.Db_b, B, d, S, s)  # the four scores, one launch
         vec = torch.empty(9, **f32)  # [CE sums ×4, counts ×4, loss_mi]
         Bg = m.B_global if m.B_global is not None else B
         dS = torch.empty(4, B, **f32)

@@ -236,6 +236,11 @@ int c2dsr_expand_rows(const float* src, const int* inv, int M, int d, float* dst
 int c2dsr_rowdot(const float* x, long ldx, const float* y, long ldy, int M, int d, const float* bias, float* out,
                  long ldo, void* stream);
 /* loss_mi = Σ_k Σ_b BCE(s_k[b], y_k)/B_norm, ds = (σ(s)-y)/B_norm; s = [sim_a_pos; sim_a_neg; sim_b_pos; sim_b_neg] */
+/* The four discriminator scores (trainer.py:104-108: D_a(h_a, h_share_b), D_a(h_a, neg_a), D_b(...), D_b(...)) in one
+ * launch: S [4][B], S[k][b] = x1_k[b]·U_k[b] + bias_k with (x1, U rows) = (x1a, Ua[0:B]), (x1a, Ua[B:2B]), (x1b, Ub[0:B]),
+ * (x1b, Ub[B:2B]) (U = X2·Wᵀ of each bilinear; bias nullable) — c2dsr_rowdot's per-row sum, the same bits. */
+int c2dsr_mi_scores(const float* x1a, const float* Ua, const float* ba, const float* x1b, const float* Ub, const float* bb,
+                    int B, int d, float* S, void* stream);
 int c2dsr_mi_loss(const float* s, int B, int B_norm, float* loss_mi, float* ds, void* stream);
 int c2dsr_rec_gather(const float* hs, const int* hs_map, const float* hx, const int* hx_map, int B, int L, int d,
                      int R, float* Hcat, float* Hpad, void* stream);

@@ -1044,3 +1044,22 @@ def test_bilinear_ds_equals_rowscale_products():
         s0, s1 = dS[2 * j][:, None], dS[2 * j + 1][:, None]
         assert torch.equal(out[j].cpu(), (s0 * U[:B]) + (s1 * U[B:]))
         assert torch.equal(out[2 + j].cpu(), torch.cat([s0 * x, s1 * x]))
+
+
+def test_mi_scores_equals_four_rowdots():
+    """c2dsr_mi_scores (the four discriminator scores in one launch) equals four c2dsr_rowdot calls bit for bit."""
+    from c2dsr_amd._lib import lib, stream
+    g = torch.Generator().manual_seed(6)
+    B, d = 777, 256
+    x1a, x1b = torch.randn(B, d, generator=g).to(DEV), torch.randn(B, d, generator=g).to(DEV)
+    Ua, Ub = torch.randn(2 * B, d, generator=g).to(DEV), torch.randn(2 * B, d, generator=g).to(DEV)
+    ba, bb = torch.randn(1, generator=g).to(DEV), None
+    S = torch.empty(4, B, device=DEV)
+    lib('c2dsr_mi_scores', x1a, Ua, ba, x1b, Ub, bb, B, d, S, stream())
+    R = torch.empty(4, B, device=DEV)
+    lib('c2dsr_rowdot', x1a, d, Ua, d, B, d, ba, R[0], 1, stream())
+    lib('c2dsr_rowdot', x1a, d, Ua[B:], d, B, d, ba, R[1], 1, stream())
+    lib('c2dsr_rowdot', x1b, d, Ub, d, B, d, bb, R[2], 1, stream())
+    lib('c2dsr_rowdot', x1b, d, Ub[B:], d, B, d, bb, R[3], 1, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(S, R)

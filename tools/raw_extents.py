@@ -54,6 +54,7 @@ EXTENTS = {
     'gather_rows': {'dst': 'n * d'},
     'expand_rows': {'dst': 'M * d'},
     'rowdot': {'out': 'SPAN(M, ldo, 1)'},
+    'mi_scores': {'S': '4 * B'},
     'mi_loss': {'loss_mi': '1', 'ds': '4 * B'},
     'rec_gather': {'Hcat': '2 * B * R * d', 'Hpad': '2 * B * R * d'},
     'rec_gather_compact': {'Hpad': '2 * B * R * d', 'Hc': 'Mv * d', 'img': 'M_pad * d * (split ? 2 : 1) * 2'},
