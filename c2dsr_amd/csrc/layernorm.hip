@@ -174,12 +174,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
   }
 }
 
-// dgw/dgb += Σ_blocks part: 64 columns x 16 block-groups per workgroup, fixed-order combine
-__global__ __launch_bounds__(1024) void reduce_parts_kernel(const float* __restrict__ part, int nblk, int d,
-                                                            float* __restrict__ dgw, float* __restrict__ dgb) {
+// dgw/dgb += Σ_blocks part: 64 columns x 16 block-groups per workgroup, fixed-order combine (bx: the workgroup's
+// column block)
+__device__ __forceinline__ void reduce_parts_body(const float* __restrict__ part, int nblk, int d,
+                                                  float* __restrict__ dgw, float* __restrict__ dgb, int bx) {
   __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int c = bx * 64 + cl;
   float s = 0.f;
   if (c < 2 * d) {
     const int which = c / d, cc = c % d;
@@ -209,6 +210,10 @@ __global__ __launch_bounds__(1024) void reduce_parts_kernel(const float* __restr
     float* o = which ? dgb : dgw;
     if (o) o[cc] += t;
   }
+}
+__global__ __launch_bounds__(1024) void reduce_parts_kernel(const float* __restrict__ part, int nblk, int d,
+                                                            float* __restrict__ dgw, float* __restrict__ dgb) {
+  reduce_parts_body(part, nblk, d, dgw, dgb, blockIdx.x);
 }
 
 // ---- Two LayerNorms back to back (the last post-norm layer's norm2 and the encoder's final norm, Q16):
@@ -409,12 +414,12 @@ __global__ __launch_bounds__(256) void ln2_bwd_kernel(const float* __restrict__ 
 }
 
 // out_k[c] += Σ_blocks part[blk][k][c] for k < 4 (null outputs skipped): as reduce_parts_kernel over 4 sets
-__global__ __launch_bounds__(1024) void reduce_parts4_kernel(const float* __restrict__ part, int nblk, int d,
-                                                             float* __restrict__ o0, float* __restrict__ o1,
-                                                             float* __restrict__ o2, float* __restrict__ o3) {
+__device__ __forceinline__ void reduce_parts4_body(const float* __restrict__ part, int nblk, int d,
+                                                   float* __restrict__ o0, float* __restrict__ o1,
+                                                   float* __restrict__ o2, float* __restrict__ o3, int bx) {
   __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int c = bx * 64 + cl;
   float s = 0.f;
   if (c < 4 * d) {
     const float* pp = part + c;
@@ -439,6 +444,23 @@ __global__ __launch_bounds__(1024) void reduce_parts4_kernel(const float* __rest
     float* o = which == 0 ? o0 : which == 1 ? o1 : which == 2 ? o2 : o3;
     if (o) o[cc] += t;
   }
+}
+__global__ __launch_bounds__(1024) void reduce_parts4_kernel(const float* __restrict__ part, int nblk, int d,
+                                                             float* __restrict__ o0, float* __restrict__ o1,
+                                                             float* __restrict__ o2, float* __restrict__ o3) {
+  reduce_parts4_body(part, nblk, d, o0, o1, o2, o3, blockIdx.x);
+}
+// both reductions of an encoder layer's two LayerNorm backwards in one launch (c2dsr_ln_reduce2): blocks
+// [0, nb4) the four sets of c2dsr_ln2_bwd's partials, the rest the two of c2dsr_ln_bwd's — each block the same sums
+__global__ __launch_bounds__(1024) void ln_reduce2_kernel(const float* __restrict__ part2, int nblk2,
+                                                          const float* __restrict__ part1, int nblk1, int d, int nb4,
+                                                          float* __restrict__ o0, float* __restrict__ o1,
+                                                          float* __restrict__ o2, float* __restrict__ o3,
+                                                          float* __restrict__ w1, float* __restrict__ b1) {
+  if ((int)blockIdx.x < nb4)
+    reduce_parts4_body(part2, nblk2, d, o0, o1, o2, o3, blockIdx.x);
+  else
+    reduce_parts_body(part1, nblk1, d, w1, b1, (int)blockIdx.x - nb4);
 }
 
 __global__ void add_drop_kernel(const float* __restrict__ a, const float* __restrict__ b, long n4, int d,
@@ -580,6 +602,24 @@ C2_API int c2dsr_add_ln2_fwd(const float* a, const float* b, int rows, int d, ui
 }
 
 C2_API size_t c2dsr_ln2_bwd_workspace(int d) { return (size_t)LN_BWD_BLOCKS * 4 * d * 4; }
+
+// partial blocks the LayerNorm backwards write for `rows` rows (both kernels: one lane group per row)
+static int ln_bwd_nblk(int rows, int d) { return std::min(c2::ceil_div(rows, 256 / lpr_for(d)), LN_BWD_BLOCKS); }
+
+// the LayerNorm parameter gradients of one encoder layer's two backwards in ONE launch: c2dsr_ln2_bwd and c2dsr_ln_bwd
+// called with null parameter-gradient outputs leave their partials in their workspaces; this adds them (rows2 / rows1:
+// the rows each backward ran on; the same fixed-order sums as their own reductions)
+C2_API int c2dsr_ln_reduce2(const void* ws2, int rows2, const void* ws1, int rows1, int d, float* dgw2, float* dgb2,
+                            float* dgwF, float* dgbF, float* dgw1, float* dgb1, void* stream) {
+  if (d % 4 || d > 1024 || rows2 < 0 || rows1 < 0) return (int)hipErrorInvalidValue;
+  const int nb4 = rows2 ? c2::ceil_div(4 * d, 64) : 0, nb2 = rows1 ? c2::ceil_div(2 * d, 64) : 0;
+  if (nb4 + nb2 == 0) return 0;
+  ln_reduce2_kernel<<<nb4 + nb2, 1024, 0, (hipStream_t)stream>>>((const float*)ws2, rows2 ? ln_bwd_nblk(rows2, d) : 0,
+                                                                  (const float*)ws1, rows1 ? ln_bwd_nblk(rows1, d) : 0,
+                                                                  d, nb4, dgw2, dgb2, dgwF, dgbF, dgw1, dgb1);
+  C2_CHECK_LAUNCH();
+  return 0;
+}
 
 // backward of c2dsr_add_ln2_fwd: dx = the gradient w.r.t. a, db_out = dx ⊙ drop mask (w.r.t. b); the four
 // LayerNorm parameter gradients accumulated (null ones skipped)

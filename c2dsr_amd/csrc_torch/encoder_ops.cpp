@@ -271,8 +271,8 @@ std::vector<Tensor> encoder_pass_backward(const Tensor& dout, const std::vector<
   Tensor ws2 = at::empty({(int64_t)c2dsr_ln2_bwd_workspace((int)d)}, f32.dtype(at::kByte));
   if (nq)
     c2t::launch("c2dsr_ln2_bwd", &c2dsr_ln2_bwd, F(xsave2), F(st), F(w[N2W]), F(w[N2B]), F(w[NFW]), F(dout), (int)nq,
-                (int)d, F(da2), F(df2), ps.k0(K_FFO), ps.k1(K_FFO), p, rb_rows, rmap, F(ln_grads[2]), F(ln_grads[3]),
-                F(ln_grads[4]), F(ln_grads[5]), ws2.data_ptr(), S());
+                (int)d, F(da2), F(df2), ps.k0(K_FFO), ps.k1(K_FFO), p, rb_rows, rmap, (float*)nullptr, (float*)nullptr,
+                (float*)nullptr, (float*)nullptr, ws2.data_ptr(), S());  // (partials only: c2dsr_ln_reduce2 below)
   // linear2's dX with linear1's drop(relu) backward in its epilogue (mask = f > 0, scale 1/(1-p))
   Tensor df = at::empty({nq, d}, f32);
   proj(ps, nq, d, d, df2, imgT[4], df, nullptr, 0, 0, 0, 0.f, 0, nullptr, 2, F(f), 1.f / (1.f - p));
@@ -284,8 +284,13 @@ std::vector<Tensor> encoder_pass_backward(const Tensor& dout, const std::vector<
   Tensor ws1 = at::empty({(int64_t)c2dsr_ln_bwd_workspace((int)d)}, f32.dtype(at::kByte));
   if (nq)
     c2t::launch("c2dsr_ln_bwd", &c2dsr_ln_bwd, F(xsave1), F(mean1), F(rstd1), F(w[N1W]), F(dx1), (int)nq, (int)d,
-                F(da1), 0, F(dsa), ps.k0(K_SA), ps.k1(K_SA), p, rb_rows, rmap, F(ln_grads[0]), F(ln_grads[1]),
+                F(da1), 0, F(dsa), ps.k0(K_SA), ps.k1(K_SA), p, rb_rows, rmap, (float*)nullptr, (float*)nullptr,
                 ws1.data_ptr(), S());
+  // both LayerNorms' parameter gradients from their partials in one launch
+  if (nq)
+    c2t::launch("c2dsr_ln_reduce2", &c2dsr_ln_reduce2, (const void*)ws2.data_ptr(), (int)nq, (const void*)ws1.data_ptr(),
+                (int)nq, (int)d, F(ln_grads[2]), F(ln_grads[3]), F(ln_grads[4]), F(ln_grads[5]), F(ln_grads[0]),
+                F(ln_grads[1]), S());
   Tensor doc = at::empty({nq, d}, f32);
   proj(ps, nq, d, d, dsa, imgT[2], doc, nullptr, 0, 0, 0, 0.f, 0, nullptr, 0, nullptr, 0.f);
   // attention on the compact rows → dq [nq, d], dkv [nk, 2d] (bf16 in bf16 mode: their only consumers are the

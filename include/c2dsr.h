@@ -187,6 +187,12 @@ int c2dsr_ln2_bwd(const float* xsave, const float* st, const float* w2, const fl
                   const float* dy, int rows, int d, float* dx, float* db_out, uint32_t k0, uint32_t k1, float p,
                   int64_t idx_base, const int* rowmap, float* dgw2, float* dgb2, float* dgwF, float* dgbF,
                   void* workspace, void* stream);
+/* The LayerNorm parameter gradients of one post-norm encoder layer's two backwards in ONE launch: c2dsr_ln2_bwd (rows2
+ * rows, workspace ws2) and c2dsr_ln_bwd (rows1, ws1) called with null parameter-gradient outputs leave their per-block
+ * partials in their workspaces; this adds them onto dgw2 / dgb2 / dgwF / dgbF and dgw1 / dgb1 (null ones skipped) in
+ * the fixed order of the two backwards' own reductions (the same bits). */
+int c2dsr_ln_reduce2(const void* ws2, int rows2, const void* ws1, int rows1, int d, float* dgw2, float* dgb2,
+                     float* dgwF, float* dgbF, float* dgw1, float* dgb1, void* stream);
 /* backward of drop(relu(.)) from its output: dx = (y > 0) ? dy/(1-p) : 0 */
 int c2dsr_relu_drop_bwd(const float* dy, const float* y, long n, float p, float* dx, void* stream);
 

@@ -38,6 +38,8 @@ EXTENTS = {
     'add_ln2_fwd': {'xsave': ROWS, 'y': ROWS, 'st': '4 * rows'},
     'ln2_bwd': {'dx': ROWS, 'db_out': ROWS, 'dgw2': 'd', 'dgb2': 'd', 'dgwF': 'd', 'dgbF': 'd',
                 'workspace': 'c2dsr_ln2_bwd_workspace((int)d)'},
+    'ln_reduce2': {'dgw2': 'HAS(dgw2) ? d : 0', 'dgb2': 'HAS(dgb2) ? d : 0', 'dgwF': 'HAS(dgwF) ? d : 0',
+                   'dgbF': 'HAS(dgbF) ? d : 0', 'dgw1': 'HAS(dgw1) ? d : 0', 'dgb1': 'HAS(dgb1) ? d : 0'},
     'relu_drop_bwd': {'dx': 'n'},
     'pool_weights': {'w': 'B * L'},
     'pool_fwd': {'out': 'B * d'},
