@@ -76,6 +76,12 @@
 #ifndef CE3B_SBW
 #define CE3B_SBW 2
 #endif
+#ifndef CE3_LGW0  // diagnostic: the forward's logits stores drained at the DMA wait (vmcnt(0))
+#define CE3_LGW0 0
+#endif
+#ifndef CE3_LGE  // the forward's logits stores in the S phase's epilogue steps (else at the end of the second product)
+#define CE3_LGE 0
+#endif
 #ifndef CE3B_T3
 #define CE3B_T3 64
 #endif
@@ -130,6 +136,19 @@ __device__ __forceinline__ float quad_sum(float x) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// global accesses by hand (saddr form: a wave-uniform base in SGPRs, a 32-bit per-lane offset, an immediate): the
+// logits store of the forward and the logits loads of ce3_dwl_kernel, which run among the tile's LDS-DMA pieces — the
+// compiler's wait-count pass does not see those (asm), so a compiler-visible load would get a wait that also drains
+// the younger DMA pieces; the loads are waited for by hand (dma_wait_keep) and their registers re-defined there
+template <int IMM>
+__device__ __forceinline__ void gst1(const void* sbase, unsigned voff, float v) {
+  asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(sbase), "n"(IMM));
+}
+template <int IMM>
+__device__ __forceinline__ void gld4(f32x4& v, const void* sbase, unsigned voff) {
+  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(v) : "v"(voff), "s"(sbase), "n"(IMM));
+}
+
 #ifndef CE3_BI  // compiler-visible MFMAs in both roles (CE3_BI0: MODE 0 only, CE3_BI1: MODE 1 only)
 #define CE3_BI 0
 #endif
@@ -276,13 +295,14 @@ constexpr int ROW_BLOCK_MAX = 16 * 4 * (CE3B_SBW > 2 ? CE3B_SBW : 2);
 // NW: waves per workgroup — 4 (one per SIMD, two 16-row stationary blocks each) or 8 (two per SIMD, one block each:
 // half the registers, so one wave's LDS waits, epilogue VALU and barrier run under its partner's MFMAs).  The
 // workgroup covers the same 128 stationary rows either way and every accumulation order is the same.
-template <int D, int MODE, bool SPLIT, int NW = 4>
+// LGS (MODE 0, split images): also store every tile's logits v = S·log2e + b2 into lg (ce3_dwl_kernel's layout, below)
+template <int D, int MODE, bool SPLIT, int NW = 4, bool LGS = false>
 __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict__ Xs, const bf16* __restrict__ Xw,
                                                       const float* __restrict__ svec, const float* __restrict__ wvec,
                                                       int n_s, int n_w, int per_split, float* __restrict__ part_m,
                                                       float* __restrict__ part_s, float* __restrict__ outp,
                                                       int accum, int sk_nwg, float* __restrict__ slot_w,
-                                                      float* __restrict__ slot_b) {
+                                                      float* __restrict__ slot_b, float* __restrict__ lg, int lg_hb) {
   constexpr int T3 = tile_rows<SPLIT>();
   constexpr int CB = T3 / 16;                      // 16-row swept blocks per tile
   constexpr int UK = T3 / 32;                      // 32-row k-steps of the second product per e-block
@@ -402,6 +422,41 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     float b2s[SBW];
 #pragma unroll
     for (int sb = 0; sb < SBW; ++sb) b2s[sb] = MODE == 1 ? svec[min(s0 + 16 * sb, n_s - 1)] : 0.f;
+    // LGS: tile tt's logits (the epilogue's v, before the running max is subtracted) into the 16 × 16 blocks
+    // [column block][row block] of lg: element (row 16sb + l16, column 16cb + 4g + r) of this wave's 32 rows.  Tile
+    // t+1's are stored at the end of the second product of tile t: at the DMA wait of the next S phase they are the
+    // youngest vector-memory operations but the loop top's row-constant DMA, and stay in flight
+    const int lg_h0 = __builtin_amdgcn_readfirstlane((rblk * RB + w * 16 * SBW) >> 4);
+    const unsigned lg_lo = (unsigned)((((l16 >> 2) * 16 + 4 * g) * 4 + (l16 & 3)) * 4);
+    constexpr bool LGW = LGS && MODE == 0 && SPLIT;
+    constexpr int NST = LGW ? NEL : 0;  // stores per tile
+    auto lg_store = [&](int tt, const f32x4(&v)[SBW * CB]) {
+      if constexpr (LGW) {
+        const int cw = (w_beg + tt * T3) >> 4;
+        [&]<int... C>(std::integer_sequence<int, C...>) {
+          (
+              [&] {
+                constexpr int cb = C / (4 * SBW), sb = (C / 4) % SBW, r = C % 4;
+                const float* base = lg + ((long)(cw + cb) * lg_hb + lg_h0) * 256;
+                gst1<sb * 1024 + r * 16>(base, lg_lo, v[cb * SBW + sb][r]);
+              }(),
+              ...);
+        }(std::make_integer_sequence<int, NST>{});
+      }
+    };
+    // CE3_LGE: each of tile t's logits stored in the epilogue step of iteration t that exponentiates it instead
+    auto lg_put = [&]<int IB, int IE>(const float* const(&lgp)[CB], const f32x4(&v)[SBW * CB]) {
+      if constexpr (LGW && CE3_LGE) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          (
+              [&] {
+                constexpr int i = IB + I, sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
+                gst1<sb * 1024 + r * 16>(lgp[cb], lg_lo, v[cb * SBW + sb][r]);
+              }(),
+              ...);
+        }(std::make_integer_sequence<int, IE - IB>{});
+      }
+    };
     dma(0);
     dma(1);
     dma(2);
@@ -505,6 +560,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
         for (int sb = 0; sb < SBW; ++sb) mnext[sb] = quad_max(tm[sb]);
       }
     }
+    if constexpr (!CE3_LGE) lg_store(0, sc);
     bf16x8 fa[DS + 2][2];
     bf16x8 tf[DT + 2][2];
     {
@@ -555,6 +611,12 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
         }
       }
       STAMP(0);
+      const float* lgp[CB];
+      if constexpr (LGW && CE3_LGE) {
+        const int cw = (w_beg + t * T3) >> 4;
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) lgp[cb] = lg + ((long)(cw + cb) * lg_hb + lg_h0) * 256;
+      }
       Offs oS, oH;
       offs_rows(bs, oS);
       offs_tr(bh, oH);
@@ -578,6 +640,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
                 for (int sb = 1; sb < SBW; ++sb) s_prod.template operator()<k / CB>(sn[cb * SBW + sb], fa[k % (DS + 2)], sb);
               }
               constexpr int ib = (k * NEL + NSS - 1) / NSS, ie = ((k + 1) * NEL + NSS - 1) / NSS;
+              lg_put.template operator()<ib, ie>(lgp, sc);
 #pragma unroll
               for (int i = ib; i < ie; ++i) {
                 const int sb = i / (4 * CB), cb2 = (i >> 2) % CB, r = i & 3;
@@ -627,7 +690,12 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
         }
       }
       asm volatile("s_nop 7" ::: "memory");  // S(t+1)'s last results before the prep's VALU reads
-      dma_wait();
+      // tile t+2's image (DMA'd during the previous second product); LGS: the logits stores that followed it and the
+      // row-constant DMA of the loop top, younger, stay in flight
+      if constexpr (LGW && !CE3_LGW0)
+        dma_wait_keep<NST + 1>();
+      else
+        dma_wait();
       STAMP(2);
       __syncthreads();
       STAMP(3);
@@ -686,6 +754,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
 #pragma unroll
         for (int sb = 0; sb < SBW; ++sb) mnext[sb] = quad_max(tm[sb]);
       }
+      if (LGW && !CE3_LGE && t + 1 < ntiles) lg_store(t + 1, sn);
 #pragma unroll
       for (int i = 0; i < SBW * CB; ++i) sc[i] = sn[i];
       STAMP(4);
@@ -716,6 +785,279 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
         // epoch-long gradient directly
         part_s[(long)split * n_s + s] = acc ? part_s[s] + ztot : ztot;
       }
+      float* out = outp + ((long)split * n_s + s) * D + 4 * g;
+      if (acc) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = *(const f32x4*)(out + 16 * e) + dacc[e][sb];
+      } else {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
+      }
+    }
+  }
+  if (sk_nwg) {  // the next segment's prologue refills the LDS images: every wave past this one's reads and DMAs
+    vm_drain();
+    __syncthreads();
+  }
+  }  // segments
+}
+
+#ifndef CE3L_X  // diagnostic builds of ce3_dwl_kernel (timing only): bit 0 no logits loads, bit 1 no per-tile H DMA
+#define CE3L_X 0
+#endif
+// ---------------------------------------------------------------- dW from the forward's logits
+// The forward (ce3_kernel MODE 0 with LGS) stores v = S·log2e + b2_c of every (row r < ⌈M/128⌉·128, column c <
+// ⌈n/32⌉·32) — the logits in log2 units, fp32 — as 16 × 16 blocks, column-block-major: block (c/16, r/16) at
+// lg + ((c/16)·HB + r/16)·256 (HB = ⌈M/128⌉·8 row blocks), element (r, c) of a block at ((r%16)/4·16 + c%16)·4 + r%4.
+// In this kernel's accumulator layout (lane ↔ column c%16 and row group (r%16)/4) a lane's four rows r%4 of a block
+// are one float4 at lane·16 bytes.  The dW sweep then needs no S product: per swept 32-row H tile
+//     E = 2^(v + cr_r)  (cr = log2 rw − lse2, −inf past M),   db += E,   dWᵀ += Hᵀ·E
+// — 96 MFMAs per tile instead of 192, the logits read once from HBM (M·n·4 bytes) instead of recomputed.  Same
+// work map, outputs and stream-K slots as ce3_kernel MODE 1.  Per wave and tile, in issue order: the logits and row
+// constants of tile t+2 (NL loads, two register sets alternating by tile parity: the loop is unrolled by two so no
+// register of a load in flight is ever copied), then — spread over the second product of tile t — the LDS-DMA pieces
+// of tile t+3's H image (NDMA).  The second product of tile t runs on the B operand built from tile t's logits during
+// tile t−1 (E, z and the hi / lo split in the MFMA shadow); tile t+1's logits (loaded at the top of tile t−1) are
+// waited for at the top of tile t with NDMA + NL younger operations left in flight, tile t+1's image at its end with
+// 2·(NL + NDMA).
+template <int D, int SBW>
+__global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict__ Xw, const float* __restrict__ lg,
+                                                         int lg_hb, int lg_cw, const float* __restrict__ crow, int n_s,
+                                                         int n_w, int per_split, float* __restrict__ part_s,
+                                                         float* __restrict__ outp, int accum, int sk_nwg,
+                                                         float* __restrict__ slot_w, float* __restrict__ slot_b) {
+  constexpr int NW = 4, T3 = 32, CB = 2, NE = D / 16, D2 = 2 * D, IMG = T3 * D2 * 2, HT = T3 * 256, NB = 4;
+  constexpr int RB = 16 * NW * SBW;
+  constexpr int NDMA = (T3 / 4) * (D2 / 128) / NW;  // LDS-DMA wave-instructions per wave per tile
+  constexpr int NL = SBW * CB + CB;                  // logits blocks + row-constant float4s per wave per tile
+  constexpr int DT = 2, DQ = NE / NDMA;
+  constexpr int NEL = 4 * SBW * CB;                  // E values per lane per tile
+  static_assert(DQ >= 1 && DQ * NDMA == NE && NEL % 8 == 0 && 2 * (NL + NDMA) < 64, "tile / wave split");
+  __shared__ __attribute__((aligned(16))) char img[NB][IMG];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
+  const int nrb = (n_s + RB - 1) / RB, nb = (int)gridDim.x;
+  const long skT = (n_w + T3 - 1) / T3, skU = (long)nrb * skT;
+  long sk_u = sk_nwg ? (long)blockIdx.x * skU / sk_nwg : 0;
+  const long sk_u1 = sk_nwg ? ((long)blockIdx.x + 1) * skU / sk_nwg : 0;
+  for (int seg = 0;; ++seg) {
+  int split, rblk, w_beg, w_end, slot = -1;
+  if (sk_nwg) {
+    if (sk_u >= sk_u1) break;  // uniform over the workgroup
+    rblk = (int)(sk_u / skT);
+    const long t0 = sk_u % skT, t1 = min(skT, t0 + (sk_u1 - sk_u));
+    split = 0;
+    w_beg = (int)(t0 * T3);
+    w_end = min(n_w, (int)(t1 * T3));
+    if (t0 != 0 || t1 != skT) slot = seg == 0 ? 0 : 1;
+    sk_u += t1 - t0;
+  } else {
+    if (seg) break;
+    const int pidx = nb % 8 == 0 ? (int)(blockIdx.x & 7) * (nb >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    split = pidx / nrb;
+    rblk = pidx % nrb;
+    w_beg = split * per_split;
+    w_end = min(n_w, w_beg + per_split);
+  }
+  const int s0 = rblk * RB + w * 16 * SBW + l16;  // stationary columns s0 + 16·sb
+  const int ntiles = w_end > w_beg ? (w_end - w_beg + T3 - 1) / T3 : 0;
+  f32x4 dacc[NE][SBW];
+  float zrow[SBW];
+#pragma unroll
+  for (int sb = 0; sb < SBW; ++sb) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) dacc[e][sb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    zrow[sb] = 0.f;
+  }
+  if (ntiles > 0) {
+    const int w_last = w_beg + (ntiles - 1) * T3;
+    const int ib = (int)lds_addr(img[0]);
+    unsigned dvoff[NDMA], ddst[NDMA];
+#pragma unroll
+    for (int i = 0; i < NDMA; ++i) {
+      const int q = w + NW * i;
+      constexpr int GROUPS = T3 / 4;
+      const int half = q / GROUPS, rg = q % GROUPS;
+      const int row = rg * 4 + (lane >> 4);
+      const int lch = (lane & 15) ^ swz16(row);
+      dvoff[i] = (unsigned)((row * D2 + half * 128 + lch * 8) * 2);
+      ddst[i] = __builtin_amdgcn_readfirstlane((unsigned)(ib + half * HT + rg * 1024));
+    }
+    int toff0[8];
+    {
+      const int trow = 4 * g + (l16 >> 2), p = lane & 3, ft = swz16(trow);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) toff0[v] = trow * 256 + 16 * ((2 * v + (p >> 1)) ^ ft) + 8 * (p & 1);
+    }
+    // this wave's logits column blocks (clamped to the written ones: columns past ⌈n/32⌉·32 only feed discarded
+    // outputs), one wave-uniform base each
+    const float* lgb[SBW];
+#pragma unroll
+    for (int sb = 0; sb < SBW; ++sb) {
+      const int c16 = __builtin_amdgcn_readfirstlane(min(((rblk * RB + w * 16 * SBW) >> 4) + sb, lg_cw - 1));
+      lgb[sb] = lg + (long)c16 * lg_hb * 256;
+    }
+    struct LSet {
+      f32x4 v[SBW][CB];  // logits: block (sb, cb), rows 16cb + 4g + i of column s0 + 16sb
+      f32x4 c[CB];       // row constants cr of rows 16cb + 4g + i
+    };
+    auto ld_logits = [&](int tt, LSet& x) {
+      if constexpr (CE3L_X & 1) {  // diagnostic: no logits traffic
+#pragma unroll
+        for (int sb = 0; sb < SBW; ++sb) x.v[sb][0] = x.v[sb][1] = f32x4{-1.f, -1.f, -1.f, -1.f};
+        x.c[0] = x.c[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        return;
+      }
+      const int r0 = min(w_beg + tt * T3, w_last);
+      const unsigned vo = (unsigned)(lane * 16 + r0 * 64), vc = (unsigned)((r0 + 4 * g) * 4);
+#pragma unroll
+      for (int sb = 0; sb < SBW; ++sb) {
+        gld4<0>(x.v[sb][0], lgb[sb], vo);
+        gld4<1024>(x.v[sb][1], lgb[sb], vo);
+      }
+      gld4<0>(x.c[0], crow, vc);
+      gld4<64>(x.c[1], crow, vc);
+    };
+    auto landed = [&](LSet& x) {  // after the wait: the set's registers are (re)defined here
+#pragma unroll
+      for (int sb = 0; sb < SBW; ++sb)
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) asm volatile("" : "+v"(x.v[sb][cb]));
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) asm volatile("" : "+v"(x.c[cb]));
+    };
+    auto dma = [&](int tt) {
+      const int r0 = min(w_beg + tt * T3, w_last);
+      const bf16* base = Xw + (long)r0 * D2;
+#pragma unroll
+      for (int i = 0; i < NDMA; ++i) dma16_s(base, dvoff[i], ddst[i] + (tt % NB) * IMG);
+    };
+    struct XSet {
+      bf16x8 h[SBW], l[SBW];  // the second product's B operand (hi / lo) per stationary block
+    };
+    // E element i (0 .. NEL-1) ↔ (sb = i / 4CB, cb = (i / 4) % CB, r = i % 4); B fragment sb packs cb = 0, 1
+    auto e_elems = [&]<int IB, int IE>(const LSet& x, float(&ev)[NEL], float zm) {
+#pragma unroll
+      for (int i = IB; i < IE; ++i) {
+        const int sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
+        const float e = ex2(x.v[sb][cb][r] + x.c[cb][r]);
+        ev[i] = e;
+        zrow[sb] = fmaf(e, zm, zrow[sb]);
+      }
+    };
+    auto pack = [&]<int SB>(const float(&ev)[NEL], XSet& xs) {
+      bf16x8 h, l;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = ev[SB * 4 * CB + j];
+        h[j] = (bf16)x;
+        l[j] = (bf16)(x - (float)h[j]);
+      }
+      xs.h[SB] = h;
+      xs.l[SB] = l;
+    };
+    auto tfrag = [&]<int EX>(int bbase) {
+      constexpr int IMM = (EX >> 3) * HT;
+      const int o = toff0[EX & 7] + bbase;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(size_t)(lds_base(o) + IMM));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(size_t)(lds_base(o) + IMM + 16 * 256));
+      bf16x8 v;
+      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+      v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+      return v;
+    };
+    LSet L[2];
+    XSet X[2];
+    ld_logits(0, L[0]);
+    dma(0);
+    ld_logits(1, L[1]);
+    dma(1);
+    dma(2);
+    vm_drain();
+    dma_wait();
+    landed(L[0]);
+    landed(L[1]);
+    __syncthreads();
+    {
+      float ev[NEL];
+      e_elems.template operator()<0, NEL>(L[0], ev, 1.f);
+      [&]<int... S>(std::integer_sequence<int, S...>) {
+        (pack.template operator()<S>(ev, X[0]), ...);
+      }(std::make_integer_sequence<int, SBW>{});
+    }
+    // tile t (parity P): loads of tile t+2 into L[P]; the second product on X[P] ∥ tile t+1's E into X[1−P] from
+    // L[1−P] ∥ the DMA of tile t+3
+    auto tile = [&]<int P>(int t) {
+      ld_logits(t + 2, L[P]);
+      dma_wait_keep<NDMA + NL>();
+      landed(L[1 - P]);
+      const int bh = ib + (t % NB) * IMG;
+      const int rn = min(w_beg + (t + 3) * T3, w_last);
+      const bf16* nsrc = Xw + (long)rn * D2;
+      const unsigned nbuf = ((t + 3) % NB) * IMG;
+      const float zm = t + 1 < ntiles ? 1.f : 0.f;  // the E of a tile past the end (clamped loads) counts nowhere
+      bf16x8 tf[DT + 2][2];
+      [&]<int... Q>(std::integer_sequence<int, Q...>) {
+        ((tf[Q][0] = tfrag.template operator()<Q>(bh), tf[Q][1] = tfrag.template operator()<NE + Q>(bh)), ...);
+      }(std::make_integer_sequence<int, DT>{});
+      float ev[NEL];
+      [&]<int... K>(std::integer_sequence<int, K...>) {
+        (
+            [&] {
+              constexpr int k = K;
+              if constexpr (k + DT < NE) {
+                tf[(k + DT) % (DT + 2)][0] = tfrag.template operator()<k + DT>(bh);
+                tf[(k + DT) % (DT + 2)][1] = tfrag.template operator()<NE + k + DT>(bh);
+              }
+              const bf16x8(&tq)[2] = tf[k % (DT + 2)];
+#pragma unroll
+              for (int sb = 0; sb < SBW; ++sb) split3_u<true>(dacc[k][sb], tq[0], tq[1], X[P].h[sb], X[P].l[sb]);
+              if constexpr (k % DQ == DQ - 1 && !(CE3L_X & 2))
+                dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
+              constexpr int i0 = (k * NEL + NE - 1) / NE, i1 = ((k + 1) * NEL + NE - 1) / NE;
+              e_elems.template operator()<i0, i1>(L[1 - P], ev, zm);
+              [&]<int... S>(std::integer_sequence<int, S...>) {
+                (
+                    [&] {
+                      if constexpr (i0 < 8 * (S + 1) && 8 * (S + 1) <= i1) pack.template operator()<S>(ev, X[1 - P]);
+                    }(),
+                    ...);
+              }(std::make_integer_sequence<int, SBW>{});
+              step_pattern<3 * SBW, CE3_VN, true>();
+              __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+      }(std::make_integer_sequence<int, NE>{});
+#pragma unroll
+      for (int sb = 0; sb < SBW; ++sb) {
+        asm volatile("" : "+v"(X[1 - P].h[sb]));
+        asm volatile("" : "+v"(X[1 - P].l[sb]));
+      }
+      dma_wait_keep<2 * (NDMA + NL)>();
+      __syncthreads();
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+      tile.template operator()<0>(t);
+      if (t + 1 < ntiles) tile.template operator()<1>(t + 1);
+    }
+    // the loads past the end (clamped) land before their registers — live until here — or the LDS are reused
+    vm_drain();
+    landed(L[0]);
+    landed(L[1]);
+  }
+  mfma_drain();
+#pragma unroll
+  for (int sb = 0; sb < SBW; ++sb) {
+    const float ztot = quad_sum(zrow[sb]);
+    const int s = s0 + 16 * sb;
+    if (s < n_s && slot >= 0) {  // stream-K partial of a split row block
+      const long so = (long)(2 * blockIdx.x + slot) * RB + (s - rblk * RB);
+      if (g == 0) slot_b[so] = ztot;
+      float* out = slot_w + so * D + 4 * g;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
+    } else if (s < n_s) {
+      const bool acc = accum || sk_nwg;
+      if (g == 0) part_s[(long)split * n_s + s] = acc ? part_s[s] + ztot : ztot;
       float* out = outp + ((long)split * n_s + s) * D + 4 * g;
       if (acc) {
 #pragma unroll
@@ -819,10 +1161,15 @@ int num_cus3() {
 size_t sk_slot_floats(int nwg, int D) { return (size_t)2 * nwg * ROW_BLOCK_MAX * D; }
 size_t sk_ws_bytes(int nwg, int D) { return (sk_slot_floats(nwg, D) + (size_t)2 * nwg * ROW_BLOCK_MAX) * 4; }
 
+// the logits layout of ce3_dwl_kernel: 16-row blocks per 16-column block (the forward's row blocks, whole), and
+// 16-column blocks written (whole 32-column tiles)
+inline int lg_row_blocks(int M) { return c2::ceil_div(M, 128) * 8; }
+inline int lg_col_blocks(int n) { return c2::ceil_div(n, 32) * 2; }
+
 template <int MODE, bool SPLIT>
 int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec, int n_s, int n_w, int D, int nsplit,
             float* pm, float* ps, float* out, hipStream_t st, int sk_nwg = 0, float* slot_w = nullptr,
-            float* slot_b = nullptr) {
+            float* slot_b = nullptr, float* lg = nullptr) {
   // MODE 1 with nsplit == 0: one split, accumulated straight onto out / ps (the gradient buffers); sk_nwg > 0:
   // stream-K over sk_nwg workgroups (MODE 1; whole row blocks accumulated, partials into the slots)
   const int accum = MODE == 1 && nsplit == 0;
@@ -833,12 +1180,24 @@ int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec
   constexpr int NW = SPLIT ? CE3_NW : CE3B_NW;
   constexpr int RB = row_block<SPLIT, NW>();
   const dim3 grid(sk_nwg ? sk_nwg : c2::ceil_div(n_s, RB) * nsplit);
-  if (D == 128)
+  const int hb = lg_row_blocks(n_s);
+  if (lg && !(MODE == 0 && SPLIT && NW == 4)) return (int)hipErrorInvalidValue;
+  if (D == 128 && lg)
+    ce3_kernel<128, MODE, SPLIT, NW, true><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s,
+                                                                      n_w, per, pm, ps, out, accum, sk_nwg, slot_w,
+                                                                      slot_b, lg, hb);
+  else if (D == 256 && lg)
+    ce3_kernel<256, MODE, SPLIT, NW, true><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s,
+                                                                      n_w, per, pm, ps, out, accum, sk_nwg, slot_w,
+                                                                      slot_b, lg, hb);
+  else if (D == 128)
     ce3_kernel<128, MODE, SPLIT, NW><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w,
-                                                                per, pm, ps, out, accum, sk_nwg, slot_w, slot_b);
+                                                                per, pm, ps, out, accum, sk_nwg, slot_w, slot_b,
+                                                                nullptr, 0);
   else if (D == 256)
     ce3_kernel<256, MODE, SPLIT, NW><<<grid, 64 * NW, 0, st>>>((const bf16*)Xs, (const bf16*)Xw, svec, wvec, n_s, n_w,
-                                                                per, pm, ps, out, accum, sk_nwg, slot_w, slot_b);
+                                                                per, pm, ps, out, accum, sk_nwg, slot_w, slot_b,
+                                                                nullptr, 0);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
@@ -846,6 +1205,40 @@ int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec
     const long T = (n_w + tile_rows<SPLIT>() - 1) / tile_rows<SPLIT>();
     ce3_sk_combine_kernel<<<dim3(c2::ceil_div(n_s, RB), RB / 16), 256, 0, st>>>(slot_w, slot_b, n_s, D, T, sk_nwg, RB,
                                                                                 out, ps);
+    C2_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// the dW sweep from stored logits (ce3_dwl_kernel): n_s = n stationary W columns, n_w = M swept H rows; nsplit as
+// launch3 (0: one split added onto out / ps), sk_nwg > 0: stream-K with its combine
+#ifndef CE3L_SBW  // stationary 16-column blocks per wave of the dW-from-logits sweep
+#define CE3L_SBW 2
+#endif
+constexpr int DWL_SBW = CE3L_SBW;
+int launch_dwl(const void* Hx, const float* lg, int lg_hb, int lg_cw, const float* crow, int n, int M, int D,
+               int nsplit, float* ps, float* out, hipStream_t st, int sk_nwg = 0, float* slot_w = nullptr,
+               float* slot_b = nullptr) {
+  const int accum = nsplit == 0;
+  if (accum) nsplit = 1;
+  if (nsplit < 1 || !lg || lg_cw < 1 || lg_hb < c2::ceil_div(M, 16) || (sk_nwg && (!slot_w || !slot_b)))
+    return (int)hipErrorInvalidValue;
+  constexpr int RB = 64 * DWL_SBW;
+  const int per = per_split3(M, nsplit, 32);
+  const dim3 grid(sk_nwg ? sk_nwg : c2::ceil_div(n, RB) * nsplit);
+  if (D == 128)
+    ce3_dwl_kernel<128, DWL_SBW><<<grid, 256, 0, st>>>((const bf16*)Hx, lg, lg_hb, lg_cw, crow, n, M, per, ps, out,
+                                                       accum, sk_nwg, slot_w, slot_b);
+  else if (D == 256)
+    ce3_dwl_kernel<256, DWL_SBW><<<grid, 256, 0, st>>>((const bf16*)Hx, lg, lg_hb, lg_cw, crow, n, M, per, ps, out,
+                                                       accum, sk_nwg, slot_w, slot_b);
+  else
+    return (int)hipErrorInvalidValue;
+  C2_CHECK_LAUNCH();
+  if (sk_nwg) {
+    const long T = (M + 31) / 32;
+    ce3_sk_combine_kernel<<<dim3(c2::ceil_div(n, RB), RB / 16), 256, 0, st>>>(slot_w, slot_b, n, D, T, sk_nwg, RB, out,
+                                                                            ps);
     C2_CHECK_LAUNCH();
   }
   return 0;
@@ -904,6 +1297,41 @@ C2_API int c2dsr_ce3_fused_dw(const void* Hx, const void* Wx, const float* bias2
 }
 
 C2_API size_t c2dsr_ce3_dw_sk_workspace(int D) { return sk_ws_bytes(num_cus3(), D); }
+
+C2_API size_t c2dsr_ce3_logits_floats(int M, int n) {
+  return M > 0 && n > 0 ? (size_t)lg_col_blocks(n) * lg_row_blocks(M) * 256 : 0;
+}
+
+C2_API int c2dsr_ce3_fused_fwd_u_lg(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D,
+                                    int n_split, float* part_m, float* part_s, float* Up, const float* padlogit,
+                                    const int64_t* tgt, const float* H, const float* W, const float* bias, float* lse,
+                                    float* lse2, float* loss_row, float* lg, void* stream) {
+  if (M == 0) return 0;
+  if (!lg) return (int)hipErrorInvalidValue;
+  const int e = launch3<0, true>(Hx, Wx, nullptr, bias2, M, n, D, n_split, part_m, part_s, Up, (hipStream_t)stream, 0,
+                                 nullptr, nullptr, lg);
+  if (e) return e;
+  return c2dsr_ce_rows(part_m, part_s, n_split, M, padlogit, tgt, n, H, W, bias, D, lse, lse2, loss_row, stream);
+}
+
+C2_API int c2dsr_ce3_fused_dw_lg(const void* Hx, const float* lg, int M, int n_lg, int col0, int n, int D,
+                                 int n_rsplit, const float* crow, float* dWp, float* dbp, void* stream) {
+  if (n == 0) return 0;
+  if (col0 < 0 || col0 % 32 || col0 + n > n_lg) return (int)hipErrorInvalidValue;
+  const int hb = lg_row_blocks(M);
+  return launch_dwl(Hx, lg + (size_t)(col0 / 16) * hb * 256, hb, lg_col_blocks(n_lg) - col0 / 16, crow, n, M, D,
+                    n_rsplit, dbp, dWp, (hipStream_t)stream);
+}
+
+C2_API int c2dsr_ce3_fused_dw_lg_sk(const void* Hx, const float* lg, int M, int n, int D, const float* crow,
+                                    float* gW, float* gb, void* ws, size_t ws_bytes, void* stream) {
+  if (n == 0) return 0;
+  const int nwg = num_cus3();
+  if (!gW || !gb || !ws || ws_bytes < sk_ws_bytes(nwg, D)) return (int)hipErrorInvalidValue;
+  float* sw = (float*)ws;
+  return launch_dwl(Hx, lg, lg_row_blocks(M), lg_col_blocks(n), crow, n, M, D, 1, gb, gW, (hipStream_t)stream, nwg, sw,
+                    sw + sk_slot_floats(nwg, D));
+}
 
 C2_API int c2dsr_ce3_fused_dw_sk(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D,
                                  const float* crow, float* gW, float* gb, void* ws, size_t ws_bytes, void* stream) {

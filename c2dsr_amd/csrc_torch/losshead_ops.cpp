@@ -142,7 +142,8 @@ std::vector<Tensor> loss_disc_forward(const std::vector<Tensor>& h, const std::v
 std::vector<Tensor> ce_head_forward(const Tensor& hs, const OptT& hs_map, const Tensor& hd, const OptT& hd_map,
                                     int64_t B, int64_t L, int64_t R, const Tensor& W, const Tensor& bias,
                                     const Tensor& wpad, const Tensor& bpad, const Tensor& idx, const Tensor& inv,
-                                    const Tensor& tc, int64_t Mv0, int64_t Mv1, int64_t n_split, int64_t mode) {
+                                    const Tensor& tc, int64_t Mv0, int64_t Mv1, int64_t n_split, int64_t mode,
+                                    int64_t keep_logits) {
   const char* op = "ce_head_forward";
   TORCH_CHECK(W.dim() == 2, "c2dsr::ce_head_forward: W must be [n, d]");
   const int64_t n = W.size(0), d = W.size(1), M2 = 2 * B * R, Mv = Mv0 + Mv1;
@@ -193,8 +194,17 @@ std::vector<Tensor> ce_head_forward(const Tensor& hs, const OptT& hs_map, const 
                 (int)Mv, 1, F(padc), S());
   Tensor lse_c = at::empty({m1}, f32), rows_c = at::empty({m1}, f32), lse2 = at::empty({M_pad}, f32);
   Tensor pm = at::empty({n_split, Mv}, f32), psum = at::empty({n_split, Mv}, f32), Up = at::empty({n_split, Mv, d}, f32);
+  // keep_logits (fp32 mode): the forward also stores the logits for the dW sweep (c2dsr_ce3_fused_dw_lg*), which then
+  // skips recomputing them; empty otherwise
+  const bool lg_on = keep_logits && mode == 0 && Mv > 0;
+  Tensor lg = at::empty({lg_on ? (int64_t)c2dsr_ce3_logits_floats((int)Mv, (int)n) : 0}, f32);
   if (Mv) {  // forward + the softmax part of the input gradient in one sweep (online lse, flash style)
-    if (mode == 0)
+    if (lg_on)
+      c2t::launch("c2dsr_ce3_fused_fwd_u_lg", &c2dsr_ce3_fused_fwd_u_lg, (const void*)Hb.data_ptr(),
+                  (const void*)Wb.data_ptr(), (const float*)F(bias2), (int)Mv, (int)n, (int)d, (int)n_split, F(pm),
+                  F(psum), F(Up), (const float*)F(padc), tc.data_ptr<int64_t>(), (const float*)F(Hc),
+                  (const float*)F(W), (const float*)F(bias), F(lse_c), F(lse2), F(rows_c), F(lg), S());
+    else if (mode == 0)
       c2t::launch("c2dsr_ce3_fused_fwd_u", &c2dsr_ce3_fused_fwd_u, (const void*)Hb.data_ptr(), (const void*)Wb.data_ptr(),
                   (const float*)F(bias2), (int)Mv, (int)n, (int)d, (int)n_split, F(pm), F(psum), F(Up),
                   (const float*)F(padc), tc.data_ptr<int64_t>(), (const float*)F(Hc), (const float*)F(W),
@@ -208,7 +218,7 @@ std::vector<Tensor> ce_head_forward(const Tensor& hs, const OptT& hs_map, const 
   Tensor rows = at::empty({M2}, f32);
   c2t::launch("c2dsr_expand_rows", &c2dsr_expand_rows, (const float*)F(rows_c), inv.data_ptr<int>(), (int)M2, 1,
               F(rows), S());  // per-row losses, 0 on ignored rows
-  return {rows, Hpad, Hb, Wb, padc, lse2, bias2, Hc, lse_c, Up, pm};
+  return {rows, Hpad, Hb, Wb, padc, lse2, bias2, Hc, lse_c, Up, pm, lg};
 }
 
 // ---------------------------------------------------------------- loss
@@ -242,7 +252,7 @@ std::vector<Tensor> loss_finalize(const Tensor& vec, const OptT& cnt, int64_t BR
 }
 
 // ---------------------------------------------------------------- backward of one head
-// saved: ce_head_forward's outputs 1.. (Hpad, Hb, Wb, padc, lse2, bias2, Hc, lse_c, Up, part_m); gW / gb / gwpad /
+// saved: ce_head_forward's outputs 1.. (Hpad, Hb, Wb, padc, lse2, bias2, Hc, lse_c, Up, part_m, logits); gW / gb / gwpad /
 // gbpad: the parameters' gradients (accumulated; may be absent); tplan: the sort plan of the valid targets (the
 // one-hot part's deterministic segment sums; absent: sorted here); n_rsplit: the dW sweep's row splits
 // (losshead.dw_plan); dw_full: with n_rsplit < 0, the W rows of the whole rounds the plan costed (a multiple of 128
@@ -254,9 +264,10 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
                                      const OptT& gwpad, const OptT& gbpad, const OptT& tplan, int64_t n_rsplit,
                                      int64_t mode, int64_t dw_full) {
   const char* op = "ce_head_backward";
-  TORCH_CHECK(saved.size() == 10, "c2dsr::ce_head_backward: the 10 tensors ce_head_forward saved");
+  TORCH_CHECK(saved.size() == 11, "c2dsr::ce_head_backward: the 11 tensors ce_head_forward saved");
   const Tensor &Hpad = saved[0], &Hb = saved[1], &Wb = saved[2], &padc = saved[3], &lse2 = saved[4];
   const Tensor &bias2 = saved[5], &Hc = saved[6], &lse_c = saved[7], &Up = saved[8], &pm = saved[9];
+  const Tensor& lg = saved[10];
   TORCH_CHECK(W.dim() == 2 && Hpad.dim() == 2, "c2dsr::ce_head_backward: W [n, d], Hpad [2BR, d]");
   const int64_t n = W.size(0), d = W.size(1), M2 = Hpad.size(0), Mv = Mv0 + Mv1;
   const int64_t M_pad = std::max<int64_t>(64, ceil_to(Mv, 64)), m1 = std::max<int64_t>(Mv, 1);
@@ -284,10 +295,16 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
   if (has(tplan))
     TORCH_CHECK(tplan->scalar_type() == at::kByte && (size_t)tplan->nbytes() >= c2dsr_index_plan_bytes((int)Mv),
                 "c2dsr::ce_head_backward: target plan too small");
+  // stored logits (the forward's keep_logits): the dW sweeps read them instead of recomputing them
+  const bool lg_on = lg.numel() > 0;
+  if (lg_on)
+    want(lg, op, "logits", at::kFloat, {(int64_t)c2dsr_ce3_logits_floats((int)Mv, (int)n)});
+  TORCH_CHECK(!lg_on || mode == 0, "c2dsr::ce_head_backward: stored logits are the fp32 mode's");
   // n_rsplit 0: the stream-K sweep (c2dsr_ce3_fused_dw_sk); −k: whole rounds unsplit, the remainder k ways (both need
   // both gradients; losshead.dw_plan)
   TORCH_CHECK(n_rsplit >= -64 && n_rsplit <= 64 && (mode == 0 || mode == 1), "c2dsr::ce_head_backward: splits / mode");
   on_device(op, {&W, &Hpad, &inv, &tc, &Hc, &padc, &lse_c, &lse2, &Up, &pm, &bias2, &Hb, &Wb, &coef, &gscale});
+  if (lg_on) on_device(op, {&lg});
   on_device(op, {gW, gb, gwpad, gbpad, tplan});
   const auto f32 = W.options();
   Tensor rw = at::empty({M_pad}, f32), t32 = at::empty({M_pad}, f32.dtype(at::kInt));
@@ -303,6 +320,11 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
                 (const float*)F(W), (int)n, F(dHc), S());
     // the sweep over W rows [off, off + rows) (the stationary operand: image rows, bias2, outputs offset alike)
     auto dw_rows = [&](int nr, float* dWp, float* dbp, int64_t off, int64_t rows) {
+      if (lg_on) {
+        c2t::launch("c2dsr_ce3_fused_dw_lg", &c2dsr_ce3_fused_dw_lg, (const void*)Hb.data_ptr(), (const float*)F(lg),
+                    (int)Mv, (int)n, (int)off, (int)rows, (int)d, nr, (const float*)F(crow), dWp, dbp, S());
+        return;
+      }
       const void* wimg = (const void*)((const at::BFloat16*)Wb.data_ptr() + off * (mode == 0 ? 2 : 1) * d);
       const float* b2 = (const float*)F(bias2) + off;
       if (mode == 0)
@@ -315,7 +337,11 @@ std::vector<Tensor> ce_head_backward(const std::vector<Tensor>& saved, const Ten
     auto dw = [&](int nr, float* dWp, float* dbp) { dw_rows(nr, dWp, dbp, 0, n); };
     if (n_rsplit == 0 && has(gW) && has(gb)) {  // stream-K: whole row blocks added directly, split ones combined
       Tensor ws = at::empty({(int64_t)c2dsr_ce3_dw_sk_workspace((int)d)}, f32.dtype(at::kByte));
-      if (mode == 0)
+      if (lg_on)
+        c2t::launch("c2dsr_ce3_fused_dw_lg_sk", &c2dsr_ce3_fused_dw_lg_sk, (const void*)Hb.data_ptr(),
+                    (const float*)F(lg), (int)Mv, (int)n, (int)d, (const float*)F(crow), F(*gW), F(*gb), ws.data_ptr(),
+                    (size_t)ws.nbytes(), S());
+      else if (mode == 0)
         c2t::launch("c2dsr_ce3_fused_dw_sk", &c2dsr_ce3_fused_dw_sk, (const void*)Hb.data_ptr(),
                     (const void*)Wb.data_ptr(), (const float*)F(bias2), (int)Mv, (int)n, (int)d, (const float*)F(crow),
                     F(*gW), F(*gb), ws.data_ptr(), (size_t)ws.nbytes(), S());
@@ -487,7 +513,7 @@ void register_losshead_ops(torch::Library& m) {
         "int B_global, Tensor(a!) vec) -> Tensor[]");
   m.def("ce_head_forward(Tensor hs, Tensor? hs_map, Tensor hd, Tensor? hd_map, int B, int L, int R, Tensor W, "
         "Tensor bias, Tensor wpad, Tensor bpad, Tensor idx, Tensor inv, Tensor tc, int Mv0, int Mv1, int n_split, "
-        "int mode) -> Tensor[]");
+        "int mode, int keep_logits=0) -> Tensor[]");
   m.def("loss_partials(Tensor rowsA, Tensor tA, int n_a, Tensor rowsB, Tensor tB, int n_b, int BR, Tensor(a!) vec) -> ()");
   m.def("loss_finalize(Tensor vec, Tensor? cnt, int BR_global, float lam) -> Tensor[]");
   m.def("ce_head_backward(Tensor[] saved, Tensor W, Tensor inv, Tensor tc, int Mv0, int Mv1, Tensor coef, "

@@ -15,6 +15,8 @@ backward turns them into dlogits in place.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.autograd import Function
 
@@ -22,6 +24,16 @@ from ._lib import error_word, lib, stage_ops, stream
 from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rg_kind, rgemm, weight_img, wg_kind, wgemm
 
 FUSED_HEAD = True  # the training step's loss head on the c2dsr:: stage operators (csrc_torch/losshead_ops.cpp)
+# fp32 mode: the forward sweep stores the logits (Mv·n fp32 per head: 4.9 GB at the Movie-Book head b) and the dW
+# sweep reads them instead of recomputing them (c2dsr_ce3_fused_dw_lg*: one split product per tile instead of two);
+# heads whose logits would exceed CE_LOGITS_GB keep the recomputing sweep
+CE_LOGITS = os.environ.get('C2DSR_CE_LOGITS', '0') != '0'
+CE_LOGITS_GB = float(os.environ.get('C2DSR_CE_LOGITS_GB', '48'))
+
+
+def keep_logits(Mv, n, mode):
+    return int(bool(CE_LOGITS and mode == 0 and Mv > 0 and
+                    -(-Mv // 128) * 128 * -(-n // 32) * 32 * 4 <= CE_LOGITS_GB * 2 ** 30))
 
 
 _NCU = None
@@ -438,7 +450,8 @@ class LossHeadFn(Function):
             Mv0, Mv1 = int(hc[slot]), int(hc[slot + 1])
             Mv = Mv0 + Mv1
             out = T.ce_head_forward(hs[0], mp[0], hdom, mp[1 + k], B, L, R, W, bias, m.wpad, m.bpad, idx, inv, tc,
-                                    Mv0, Mv1, fwd_split_count(Mv, n, mode == 0, d), mode)
+                                    Mv0, Mv1, fwd_split_count(Mv, n, mode == 0, d), mode,
+                                    keep_logits(Mv, n, mode) if W.requires_grad else 0)
             if k == 0:
                 m.run_after_first_ce()
             # target sort for the one-hot part of dW/db, on the side stream under the rest of the step

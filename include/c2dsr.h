@@ -383,6 +383,23 @@ int c2dsr_ce3_fused_dw_sk(const void* Hx, const void* Wx, const float* bias2, in
                           float* gW, float* gb, void* ws, size_t ws_bytes, void* stream);
 int c2dsr_ce3b_fused_dw_sk(const void* Hb, const void* Wb, const float* bias2, int M, int n, int D, const float* crow,
                            float* gW, float* gb, void* ws, size_t ws_bytes, void* stream);
+/* K5's dW from stored logits (fp32 mode; trainer.py:131-154, the classifier's weight / bias gradients).  The forward
+ * c2dsr_ce3_fused_fwd_u_lg is c2dsr_ce3_fused_fwd_u that also writes every logit v = (h_r·w_c + b_c)·log2e of the
+ * rows r < ⌈M/128⌉·128 (the image's padding rows duplicate row M−1) and columns c < ⌈n/32⌉·32 (−inf past n) into lg,
+ * c2dsr_ce3_logits_floats(M, n) fp32 values: 16 × 16 blocks, column-block-major (block (c/16, r/16) at
+ * ((c/16)·⌈M/128⌉·8 + r/16)·256, element (r, c) at ((r%16)/4·16 + c%16)·4 + r%4 inside it).  The dW sweeps
+ * c2dsr_ce3_fused_dw_lg / _dw_lg_sk then compute E = 2^(v + crow_r) from the stored logits instead of recomputing
+ * them (one split product per tile instead of two), same outputs as c2dsr_ce3_fused_dw / _dw_sk: dw_lg sweeps the
+ * columns [col0, col0 + n) (col0 a multiple of 32) of the n_lg the forward wrote; n_rsplit as c2dsr_ce3_fused_dw. */
+size_t c2dsr_ce3_logits_floats(int M, int n);
+int c2dsr_ce3_fused_fwd_u_lg(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_split,
+                             float* part_m, float* part_s, float* Up, const float* padlogit, const int64_t* tgt,
+                             const float* H, const float* W, const float* bias, float* lse, float* lse2,
+                             float* loss_row, float* lg, void* stream);
+int c2dsr_ce3_fused_dw_lg(const void* Hx, const float* lg, int M, int n_lg, int col0, int n, int D, int n_rsplit,
+                          const float* crow, float* dWp, float* dbp, void* stream);
+int c2dsr_ce3_fused_dw_lg_sk(const void* Hx, const float* lg, int M, int n, int D, const float* crow, float* gW,
+                             float* gb, void* ws, size_t ws_bytes, void* stream);
 /* out[i] = beta·out[i] + Σ_s part[s·n + i]  (fixed order) */
 int c2dsr_sum_parts(const float* part, int nparts, long n, float beta, float* out, void* stream);
 /* test hook: transposed / row fragment reads of the swizzled LDS image (int16 payload) */

@@ -18,9 +18,10 @@ def rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
 
 
-def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None, b16=False):
+def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None, b16=False, lgk=False):
     """The head exactly as losshead.py drives it: the fp32 mode's x3 kernels (split-bf16 images), or with
-    b16 the bf16 mode's ce3b kernels (plain bf16 images, zero rows to whole 64-row tiles)."""
+    b16 the bf16 mode's ce3b kernels (plain bf16 images, zero rows to whole 64-row tiles); lgk: the fp32 mode with
+    the logits stored by the forward and the dW sweeps reading them (c2dsr_ce3_fused_fwd_u_lg / _dw_lg*)."""
     from c2dsr_amd._lib import lib, stream
     s = stream()
     d = lambda x: x.to(DEV)  # noqa: E731
@@ -47,8 +48,17 @@ def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None, b16=False):
     Up = torch.empty(ns, M, D, device=DEV)
     lse, rows = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
     lse2 = torch.empty(M_pad, device=DEV)
-    lib(pre + 'fwd_u', Hx, Wx, bias2, M, n, D, ns, pm, ps, Up, d(pl), d(t), d(H), d(W), d(b), lse, lse2,
-        rows, s)
+    if lgk:
+        lg = torch.full((int(lib.raw('c2dsr_ce3_logits_floats')(M, n)),), float('nan'), device=DEV)
+        lib(pre + 'fwd_u_lg', Hx, Wx, bias2, M, n, D, ns, pm, ps, Up, d(pl), d(t), d(H), d(W), d(b), lse, lse2,
+            rows, lg, s)
+        # the dW sweeps on the stored logits, same call shapes as the recomputing ones
+        dw = lambda Hx_, Wx_, b2_, M_, n_, D_, nr_, crow_, o1, o2, s_, col0=0: lib(  # noqa: E731
+            pre + 'dw_lg', Hx_, lg, M_, n, col0, n_, D_, nr_, crow_, o1, o2, s_)
+    else:
+        lib(pre + 'fwd_u', Hx, Wx, bias2, M, n, D, ns, pm, ps, Up, d(pl), d(t), d(H), d(W), d(b), lse, lse2,
+            rows, s)
+        dw = lambda *a, col0=0: lib(pre + 'dw', *a)  # noqa: E731
     rw, dpad = torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)
     t32 = torch.empty(M_pad, device=DEV, dtype=torch.int32)
     crow = torch.empty(M_pad + 64, device=DEV)
@@ -63,20 +73,23 @@ def _run(H, W, b, pl, t, coef, lam, ns, nr, BR, g0=None, b16=False):
         full = dw_full_rows(n, not b16)  # whole rounds of the instantiation's row blocks (128 / 192 rows)
         rem, k = n - full, -nr
         ic = Wx.shape[1]
-        lib(pre + 'dw', Hx, Wx, bias2, M, full, D, 0, crow, gW, gb, s)
+        dw(Hx, Wx, bias2, M, full, D, 0, crow, gW, gb, s)
         dWp, dbp = torch.empty(k, rem, D, device=DEV), torch.empty(k, rem, device=DEV)
-        lib(pre + 'dw', Hx, Wx.view(-1)[full * ic:], bias2[full:], M, rem, D, k, crow, dWp, dbp, s)
+        dw(Hx, Wx.view(-1)[full * ic:], bias2[full:], M, rem, D, k, crow, dWp, dbp, s, col0=full)
         lib('c2dsr_sum_parts', dWp, k, rem * D, 1.0, gW.view(-1)[full * D:], s)
         lib('c2dsr_sum_parts', dbp, k, rem, 1.0, gb[full:], s)
     elif nr == -1:  # stream-K sweep (whole row blocks added directly, split ones combined in workgroup order)
         wsb = int(lib.raw('c2dsr_ce3_dw_sk_workspace')(D))
         ws = torch.empty(wsb, dtype=torch.uint8, device=DEV)
-        lib(pre + 'dw_sk', Hx, Wx, bias2, M, n, D, crow, gW, gb, ws, wsb, s)
+        if lgk:
+            lib(pre + 'dw_lg_sk', Hx, lg, M, n, D, crow, gW, gb, ws, wsb, s)
+        else:
+            lib(pre + 'dw_sk', Hx, Wx, bias2, M, n, D, crow, gW, gb, ws, wsb, s)
     elif nr == 0:  # one split added straight onto the gradients
-        lib(pre + 'dw', Hx, Wx, bias2, M, n, D, 0, crow, gW, gb, s)
+        dw(Hx, Wx, bias2, M, n, D, 0, crow, gW, gb, s)
     else:
         dWp, dbp = torch.empty(nr, n, D, device=DEV), torch.empty(nr, n, device=DEV)
-        lib(pre + 'dw', Hx, Wx, bias2, M, n, D, nr, crow, dWp, dbp, s)
+        dw(Hx, Wx, bias2, M, n, D, nr, crow, dWp, dbp, s)
         lib('c2dsr_sum_parts', dWp, nr, n * D, 1.0, gW, s)
         lib('c2dsr_sum_parts', dbp, nr, n, 1.0, gb, s)
     wsb = int(lib.raw('c2dsr_ce_onehot_workspace')(M, n, D))
@@ -111,7 +124,8 @@ TOL_LSE, TOL = 1e-5, 5e-5
                                          (777, 4099, 256, 7, 5), (33, 31, 256, 2, 3), (300, 700, 256, 3, -1),
                                          (1000, 2100, 128, 4, -1), (2500, 40000, 256, 5, -1), (33, 31, 256, 2, -1),
                                          (700, 36845, 256, 3, -8)])
-def test_ce3_matches_float64(M, n, D, ns, nr):
+@pytest.mark.parametrize('lgk', [False, True])
+def test_ce3_matches_float64(M, n, D, ns, nr, lgk):
     g = torch.Generator().manual_seed(M + n + D)
     H = torch.randn(M, D, generator=g) * 0.5
     W = torch.randn(n, D, generator=g) * 0.5
@@ -120,7 +134,7 @@ def test_ce3_matches_float64(M, n, D, ns, nr):
     t = torch.randint(0, n + 1, (M,), generator=g)
     t[:5] = n  # ignored rows
     coef, lam, BR = torch.tensor([0.37, 1.9]), 0.7, M // 2
-    lse, rows, dH, gW, gb, dpad, _ = _run(H, W, b, pl, t, coef, lam, ns, nr, BR)
+    lse, rows, dH, gW, gb, dpad, _ = _run(H, W, b, pl, t, coef, lam, ns, nr, BR, lgk=lgk)
     lse_r, rows_r, dH_r, gW_r, gb_r, dpad_r = _ref(H, W, b, pl, t, coef, lam, BR)
     err = dict(lse=rel(lse, lse_r), rows=rel(rows, rows_r), dpad=rel(dpad, dpad_r), dH=rel(dH, dH_r),
                gW=rel(gW, gW_r), gb=rel(gb, gb_r))
@@ -130,7 +144,8 @@ def test_ce3_matches_float64(M, n, D, ns, nr):
 
 
 @pytest.mark.parametrize('M,n,D,ns', [(200, 1500, 256, 2), (333, 3000, 128, 5)])
-def test_ce3_online_rescale(M, n, D, ns):
+@pytest.mark.parametrize('lgk', [False, True])
+def test_ce3_online_rescale(M, n, D, ns, lgk):
     """Row max rising and falling across column tiles (bias ramp of 60 nats): the lazy rescale fires at
     different tiles for different rows of one wave.  The logits reach |h·w| ≈ 20 here, and the softmax's
     relative error is the logit's ABSOLUTE error (≈ 4e-6·|h·w| for split-bf16 products), so the weight
@@ -145,7 +160,7 @@ def test_ce3_online_rescale(M, n, D, ns):
     pl = torch.randn(M, generator=g)
     t = torch.randint(0, n, (M,), generator=g)
     coef, lam, BR = torch.tensor([0.5, 1.5]), 0.7, M // 2
-    lse, rows, dH, gW, gb, _, Up = _run(H, W, b, pl, t, coef, lam, ns, 2, BR)
+    lse, rows, dH, gW, gb, _, Up = _run(H, W, b, pl, t, coef, lam, ns, 2, BR, lgk=lgk)
     lse_r, rows_r, dH_r, gW_r, gb_r, _ = _ref(H, W, b, pl, t, coef, lam, BR)
     assert torch.isfinite(Up).all()
     err = dict(lse=rel(lse, lse_r), rows=rel(rows, rows_r), dH=rel(dH, dH_r), gW=rel(gW, gW_r), gb=rel(gb, gb_r))
@@ -154,7 +169,8 @@ def test_ce3_online_rescale(M, n, D, ns):
     assert all(v < 1e-4 for v in err.values()), err
 
 
-def test_ce3_dw_accumulates_onto_gradient():
+@pytest.mark.parametrize('lgk', [False, True])
+def test_ce3_dw_accumulates_onto_gradient(lgk):
     """n_rsplit = 0 (one split, losshead.py when split_count(n) == 1): the dW / db sweep adds onto the existing
     gradient buffers (the epoch-long accumulation, Q3) and equals the partial + sum path bit for bit."""
     M, n, D = 500, 2100, 256
@@ -166,8 +182,8 @@ def test_ce3_dw_accumulates_onto_gradient():
     t = torch.randint(0, n + 1, (M,), generator=g)
     coef = torch.tensor([0.37, 1.9])
     g0 = (torch.randn(n, D, generator=g), torch.randn(n, generator=g))
-    r1 = _run(H, W, b, pl, t, coef, 0.7, 3, 0, M // 2, g0=g0)
-    r2 = _run(H, W, b, pl, t, coef, 0.7, 3, 1, M // 2, g0=g0)
+    r1 = _run(H, W, b, pl, t, coef, 0.7, 3, 0, M // 2, g0=g0, lgk=lgk)
+    r2 = _run(H, W, b, pl, t, coef, 0.7, 3, 1, M // 2, g0=g0, lgk=lgk)
     assert torch.equal(r1[3], r2[3]) and torch.equal(r1[4], r2[4])
     assert not torch.equal(r1[3].cpu(), g0[0])
 
@@ -518,3 +534,51 @@ def test_ce3b_mb_head_b_shape_matches_float64():
     assert err.pop('lse') < TOL_LSE
     assert err.pop('rows') < TOL
     assert all(v < 1e-4 for v in err.values()), err
+
+
+@pytest.mark.parametrize('M,n,D,ns', [(300, 700, 256, 3), (1000, 2100, 128, 4), (33, 31, 256, 2), (777, 4099, 256, 7)])
+def test_ce3_stored_logits_layout(M, n, D, ns):
+    """c2dsr_ce3_fused_fwd_u_lg's logits buffer read back through the layout include/c2dsr.h documents (16 × 16 blocks,
+    column-block-major, element (r, c) at ((r%16)/4·16 + c%16)·4 + r%4): v = (h_r·w_c + b_c)·log2e for r < M, c < n
+    (the fp32 mode's split products: within 1e-5 of max-abs), −inf for the padding columns c < ⌈n/32⌉·32, and the
+    forward's other outputs equal to the plain sweep's bit for bit."""
+    from c2dsr_amd._lib import lib, stream
+    s = stream()
+    g = torch.Generator().manual_seed(M * 3 + n)
+    H = torch.randn(M, D, generator=g) * 0.5
+    W = torch.randn(n, D, generator=g) * 0.5
+    b = torch.randn(n, generator=g) * 0.1
+    pl = torch.randn(M, generator=g)
+    t = torch.randint(0, n + 1, (M,), generator=g)
+    M_pad, n32, n_pad = max(64, -(-M // 64) * 64), -(-n // 32) * 32, -(-n // 128) * 128 + 64
+    Hx = torch.empty(M_pad, 2 * D, dtype=torch.bfloat16, device=DEV)
+    Wx = torch.empty(n32, 2 * D, dtype=torch.bfloat16, device=DEV)
+    lib('c2dsr_f32_split_bf16', H.to(DEV), M, D, M_pad, Hx, s)
+    lib('c2dsr_f32_split_bf16', W.to(DEV), n, D, n32, Wx, s)
+    bias2 = torch.empty(n_pad, device=DEV)
+    lib('c2dsr_ce_bias2', b.to(DEV), n, n_pad, bias2, s)
+    outs = []
+    for use_lg in (False, True):
+        o = [torch.empty(ns, M, device=DEV), torch.empty(ns, M, device=DEV), torch.empty(ns, M, D, device=DEV),
+             torch.empty(M, device=DEV), torch.empty(M_pad, device=DEV), torch.empty(M, device=DEV)]
+        a = (Hx, Wx, bias2, M, n, D, ns, o[0], o[1], o[2], pl.to(DEV), t.to(DEV), H.to(DEV), W.to(DEV), b.to(DEV),
+             o[3], o[4], o[5])
+        if use_lg:
+            lg = torch.full((int(lib.raw('c2dsr_ce3_logits_floats')(M, n)),), float('nan'), device=DEV)
+            lib('c2dsr_ce3_fused_fwd_u_lg', *a, lg, s)
+        else:
+            lib('c2dsr_ce3_fused_fwd_u', *a, s)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for x, y in zip(*outs):
+        assert torch.equal(x[..., :M] if x.dim() == 1 else x, y[..., :M] if y.dim() == 1 else y)
+    HB = -(-M // 128) * 8
+    CW = n32 // 16
+    blk = lg.cpu()[:CW * HB * 256].view(CW, HB, 4, 16, 4)  # [c/16][r/16][(r%16)/4][c%16][r%4]
+    full = blk.permute(1, 2, 4, 0, 3).reshape(HB * 16, CW * 16)  # [r][c]
+    ref = (H.double() @ W.double().T + b.double()) * 1.4426950408889634
+    got = full[:M, :n].double()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    print('stored logits rel err', err)
+    assert err < 1e-5
+    assert bool(torch.isneginf(full[:M, n:n32]).all())
