@@ -85,9 +85,15 @@ class KernelTimer:
                   'c2dsr_ce_fused_fwd', 'c2dsr_ce_fused_dh', 'c2dsr_ce_fused_dw')
     # (the dW sweep's forms, losshead.dw_plan: row splits, whole rounds + a split remainder — two launches of _dw —,
     # or stream-K, _dw_sk, whose launch includes its partial combine)
-    NAMES_X3 = ('c2dsr_ce3_fused_fwd_u', 'c2dsr_ce3_fused_dw', 'c2dsr_ce3_fused_dw_sk')
+    # (round 6: with the logits kept, the forward that also stores them, _fwd_u_lg, and the dW sweeps that read them,
+    # _dw_lg / _dw_lg_sk)
+    NAMES_X3 = ('c2dsr_ce3_fused_fwd_u', 'c2dsr_ce3_fused_dw', 'c2dsr_ce3_fused_dw_sk', 'c2dsr_ce3_fused_fwd_u_lg',
+                'c2dsr_ce3_fused_dw_lg', 'c2dsr_ce3_fused_dw_lg_sk')
     # credited products per launch: fwd_u = the lse logits + the softmax·W part of dH (online, one sweep)
-    CREDIT = {'c2dsr_ce_fused_fwd_u': 2, 'c2dsr_ce3_fused_fwd_u': 2, 'c2dsr_ce3b_fused_fwd_u': 2}
+    CREDIT = {'c2dsr_ce_fused_fwd_u': 2, 'c2dsr_ce3_fused_fwd_u': 2, 'c2dsr_ce3b_fused_fwd_u': 2,
+              'c2dsr_ce3_fused_fwd_u_lg': 2}
+    # positions of (M, n, D) in a launch's arguments (default: (Hx, Wx, bias2, M, n, D, ...))
+    DIMS = {'c2dsr_ce3_fused_dw_lg': (2, 5, 6), 'c2dsr_ce3_fused_dw_lg_sk': (2, 3, 4)}
 
     def __init__(self, precision):
         self.names = {'bf16': self.NAMES_BF16, 'fp32': self.NAMES_X3}.get(precision, ('c2dsr_gemm',))
@@ -103,7 +109,8 @@ class KernelTimer:
                     if f < 1e11:  # only the classifier-head GEMMs
                         continue
                 else:  # (Hb, Wb, bias2, M, n, D, ...)
-                    f = 2.0 * a[3] * a[4] * a[5] * self.CREDIT.get(name, 1)
+                    i, j, k = self.DIMS.get(name, (3, 4, 5))
+                    f = 2.0 * a[i] * a[j] * a[k] * self.CREDIT.get(name, 1)
                 ms.append(t)
                 fl.append(f)
             if ms:

@@ -80,7 +80,7 @@
 #define CE3_LGW0 0
 #endif
 #ifndef CE3_LGE  // the forward's logits stores in the S phase's epilogue steps (else at the end of the second product)
-#define CE3_LGE 0
+#define CE3_LGE 1
 #endif
 #ifndef CE3B_T3
 #define CE3B_T3 64
@@ -140,13 +140,53 @@ __device__ __forceinline__ float quad_sum(float x) {
 // logits store of the forward and the logits loads of ce3_dwl_kernel, which run among the tile's LDS-DMA pieces — the
 // compiler's wait-count pass does not see those (asm), so a compiler-visible load would get a wait that also drains
 // the younger DMA pieces; the loads are waited for by hand (dma_wait_keep) and their registers re-defined there
+// (CE3_LGNT bit 0: the stores non-temporal, bit 1: the loads — streamed once, kept out of the L2 the operand tiles
+// are shared through)
+#ifndef CE3_LGNT
+#define CE3_LGNT 1
+#endif
 template <int IMM>
 __device__ __forceinline__ void gst1(const void* sbase, unsigned voff, float v) {
-  asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(sbase), "n"(IMM));
+  if constexpr (CE3_LGNT & 1)
+    asm volatile("global_store_dword %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v), "s"(sbase), "n"(IMM));
+  else
+    asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(sbase), "n"(IMM));
+}
+#ifndef CE3_LGNOST  // diagnostic: the forward's logits transposed but not stored
+#define CE3_LGNOST 0
+#endif
+template <int IMM>
+__device__ __forceinline__ void gst4(const void* sbase, unsigned voff, const f32x4& v) {
+  if constexpr (CE3_LGNOST)
+    asm volatile("" ::"v"(voff), "v"(v), "s"(sbase));
+  else if constexpr (CE3_LGNT & 1)
+    asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3 nt" ::"v"(voff), "v"(v), "s"(sbase), "n"(IMM));
+  else
+    asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(sbase), "n"(IMM));
+}
+// 4 × 4 transpose across the lanes of a quad (lane & 3) and a lane's 4 values: out[j] of lane b = in[b] of lane j
+// (two rounds of 2 × 2 swaps, one DPP quad permutation each)
+__device__ __forceinline__ f32x4 quad_transpose(const f32x4& x) {
+  const int lane = (int)(threadIdx.x & 3);
+  f32x4 y, z;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float t = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x[r ^ 1]), 0xB1, 0xF, 0xF, false));
+    y[r] = ((r & 1) == (lane & 1)) ? x[r] : t;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float t = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y[r ^ 2]), 0x4E, 0xF, 0xF, false));
+    z[r] = ((r & 2) == (lane & 2)) ? y[r] : t;
+  }
+  return z;
 }
 template <int IMM>
 __device__ __forceinline__ void gld4(f32x4& v, const void* sbase, unsigned voff) {
-  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(v) : "v"(voff), "s"(sbase), "n"(IMM));
+  if constexpr (CE3_LGNT & 2)
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3 nt" : "=v"(v) : "v"(voff), "s"(sbase), "n"(IMM));
+  else
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(v) : "v"(voff), "s"(sbase), "n"(IMM));
 }
 
 #ifndef CE3_BI  // compiler-visible MFMAs in both roles (CE3_BI0: MODE 0 only, CE3_BI1: MODE 1 only)
@@ -444,14 +484,18 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
         }(std::make_integer_sequence<int, NST>{});
       }
     };
-    // CE3_LGE: each of tile t's logits stored in the epilogue step of iteration t that exponentiates it instead
+    // CE3_LGE: tile t's logits stored in the epilogue steps of iteration t instead, each 16 × 16 block (elements
+    // 4j .. 4j+3 of the lane, j = sb·CB + cb) in the step that exponentiates its first element: the quad's 4 × 4
+    // transpose gives each lane the block's 16-byte chunk 16·(l16/4) + 4g + l16%4 (rows 4·(l16/4) .., column 4g +
+    // l16%4), one dwordx4 store per block and wave
+    const unsigned lg_lo4 = (unsigned)((16 * (l16 >> 2) + 4 * g + (l16 & 3)) * 16);
     auto lg_put = [&]<int IB, int IE>(const float* const(&lgp)[CB], const f32x4(&v)[SBW * CB]) {
       if constexpr (LGW && CE3_LGE) {
         [&]<int... I>(std::integer_sequence<int, I...>) {
           (
               [&] {
-                constexpr int i = IB + I, sb = i / (4 * CB), cb = (i >> 2) % CB, r = i & 3;
-                gst1<sb * 1024 + r * 16>(lgp[cb], lg_lo, v[cb * SBW + sb][r]);
+                constexpr int i = IB + I, sb = i / (4 * CB), cb = (i >> 2) % CB;
+                if constexpr (i % 4 == 0) gst4<sb * 1024>(lgp[cb], lg_lo4, quad_transpose(v[cb * SBW + sb]));
               }(),
               ...);
         }(std::make_integer_sequence<int, IE - IB>{});
@@ -693,7 +737,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
       // tile t+2's image (DMA'd during the previous second product); LGS: the logits stores that followed it and the
       // row-constant DMA of the loop top, younger, stay in flight
       if constexpr (LGW && !CE3_LGW0)
-        dma_wait_keep<NST + 1>();
+        dma_wait_keep<(CE3_LGE ? NST / 4 : NST) + 1>();
       else
         dma_wait();
       STAMP(2);

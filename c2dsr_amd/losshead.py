@@ -24,9 +24,10 @@ from ._lib import error_word, lib, stage_ops, stream
 from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rg_kind, rgemm, weight_img, wg_kind, wgemm
 
 FUSED_HEAD = True  # the training step's loss head on the c2dsr:: stage operators (csrc_torch/losshead_ops.cpp)
-# fp32 mode: the forward sweep stores the logits (Mv·n fp32 per head: 4.9 GB at the Movie-Book head b) and the dW
-# sweep reads them instead of recomputing them (c2dsr_ce3_fused_dw_lg*: one split product per tile instead of two);
-# heads whose logits would exceed CE_LOGITS_GB keep the recomputing sweep
+# fp32 mode, opt-in (C2DSR_CE_LOGITS=1): the forward sweep stores the logits (Mv·n fp32 per head: 4.9 GB at the
+# Movie-Book head b) and the dW sweep reads them instead of recomputing them (c2dsr_ce3_fused_dw_lg*: one split product
+# per tile instead of two); heads whose logits would exceed CE_LOGITS_GB keep the recomputing sweep.  Measured in the
+# step (round 6): the dW sweeps −1.0 ms, the forward's 7.6 GB of stores +0.9 ms — not the default
 CE_LOGITS = os.environ.get('C2DSR_CE_LOGITS', '0') != '0'
 CE_LOGITS_GB = float(os.environ.get('C2DSR_CE_LOGITS_GB', '48'))
 
@@ -372,9 +373,14 @@ class LossHeadFn(Function):
                     pm = torch.empty(ns, Mv, **f32)
                     ps = torch.empty(ns, Mv, **f32)
                     Up = torch.empty(ns, Mv, d, **f32)
-                    lib(ce_entry(x3, d, 'fwd_u'), Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tc, Hc, W, bias, lse_c,
-                        lse2, rows_c, s)
-                    u = (Up, pm, ns)
+                    fa = (Hb, Wb, bias2, Mv, n, d, ns, pm, ps, Up, padc, tc, Hc, W, bias, lse_c, lse2, rows_c)
+                    lg = None
+                    if x3 and W.requires_grad and keep_logits(Mv, n, 0):  # the dW sweep reads the stored logits
+                        lg = torch.empty(int(lib.raw('c2dsr_ce3_logits_floats')(Mv, n)), **f32)
+                        lib('c2dsr_ce3_fused_fwd_u_lg', *fa, lg, s)
+                    else:
+                        lib(ce_entry(x3, d, 'fwd_u'), *fa, s)
+                    u = (Up, pm, ns, lg)
                     m.run_after_first_ce()
                 elif Mv:
                     ns = split_count(Mv, 256)
@@ -538,8 +544,9 @@ class LossHeadFn(Function):
                     # compact rows keep their order: the first Mv0 are the shared-sequence rows (coef[0])
                     lib('c2dsr_ce_row_weights', tc, Mv, M_pad, n, coef, Mv0, gscale, float(m.lam), padc, lse_c, rw,
                         t32, lse2, crow, dpad_c, s)
+                    lg = None
                     if u is not None:  # dH = rw·(softmax·W − W[t]) from the forward's online partials
-                        Up, pm, nsu = u
+                        Up, pm, nsu, lg = u
                         lib('c2dsr_ce_dh_from_u', Up, pm, nsu, Mv, d, lse2, t32, rw, W, n, dHc, s)
                     else:
                         ns = split_count(Mv, 128)
@@ -550,29 +557,38 @@ class LossHeadFn(Function):
                     entry = ce_entry(ctx.x3, d, 'dw')
                     both = gW is not None and gb is not None and entry.startswith('c2dsr_ce3')
                     nr = dw_plan(n, Mv, ctx.x3, d, both)
+                    ic = (2 if ctx.x3 else 1) * d
+
+                    def dw(nsplit, o1, o2, off=0, rows=n):  # the sweep over W rows [off, off + rows)
+                        if lg is not None:
+                            lib('c2dsr_ce3_fused_dw_lg', Hb, lg, Mv, n, off, rows, d, nsplit, crow, o1, o2, s)
+                        else:
+                            lib(entry, Hb, Wb.view(-1)[off * ic:], bias2[off:], Mv, rows, d, nsplit, crow, o1, o2, s)
                     if nr == 0:  # stream-K: whole row blocks added onto the gradients, split ones combined in order
                         wsb = int(lib.raw('c2dsr_ce3_dw_sk_workspace')(d))
                         ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
-                        lib(entry + '_sk', Hb, Wb, bias2, Mv, n, d, crow, gW, gb, ws, wsb, s)
+                        if lg is not None:
+                            lib('c2dsr_ce3_fused_dw_lg_sk', Hb, lg, Mv, n, d, crow, gW, gb, ws, wsb, s)
+                        else:
+                            lib(entry + '_sk', Hb, Wb, bias2, Mv, n, d, crow, gW, gb, ws, wsb, s)
                         del ws
                     elif nr < 0:  # whole rounds unsplit onto the gradients, the remainder row blocks −nr ways
                         full = dw_full_rows(n, ctx.x3)
                         rem, k = n - full, -nr
-                        ic = (2 if ctx.x3 else 1) * d
-                        lib(entry, Hb, Wb, bias2, Mv, full, d, 0, crow, gW, gb, s)
+                        dw(0, gW, gb, 0, full)
                         dWp = torch.empty(k, rem, d, **f32)
                         dbp = torch.empty(k, rem, **f32)
-                        lib(entry, Hb, Wb.view(-1)[full * ic:], bias2[full:], Mv, rem, d, k, crow, dWp, dbp, s)
+                        dw(k, dWp, dbp, full, rem)
                         lib('c2dsr_sum_parts', dWp, k, rem * d, 1.0, gW.view(-1)[full * d:], s)
                         lib('c2dsr_sum_parts', dbp, k, rem, 1.0, gb[full:], s)
                         del dWp, dbp
                     elif nr == 1 and both:
                         # one split: the sweep adds onto the gradients itself (n_rsplit = 0; no partials / sum)
-                        lib(entry, Hb, Wb, bias2, Mv, n, d, 0, crow, gW, gb, s)
+                        dw(0, gW, gb)
                     else:
                         dWp = torch.empty(nr, n, d, **f32)
                         dbp = torch.empty(nr, n, **f32)
-                        lib(entry, Hb, Wb, bias2, Mv, n, d, nr, crow, dWp, dbp, s)
+                        dw(nr, dWp, dbp)
                         if gW is not None:
                             lib('c2dsr_sum_parts', dWp, nr, n * d, 1.0, gW, s)
                         if gb is not None:
