@@ -21,14 +21,14 @@ import torch
 from torch.autograd import Function
 
 from ._lib import error_word, lib, stage_ops, stream
-from .ops import BF16, FP32, IndexPlan, _grad_target, colsum, gemm, rg_kind, rgemm, weight_img, wg_kind, wgemm
+from .ops import BF16, FP32, IndexPlan, _grad_target, index_plans, colsum, gemm, rg_kind, rgemm, weight_img, wg_kind, wgemm
 
 FUSED_HEAD = True  # the training step's loss head on the c2dsr:: stage operators (csrc_torch/losshead_ops.cpp)
 # fp32 mode, opt-in (C2DSR_CE_LOGITS=1): the forward sweep stores the logits (Mv·n fp32 per head: 4.9 GB at the
 # Movie-Book head b) and the dW sweep reads them instead of recomputing them (c2dsr_ce3_fused_dw_lg*: one split product
 # per tile instead of two); heads whose logits would exceed CE_LOGITS_GB keep the recomputing sweep.  Measured in the
 # step (round 6): the dW sweeps −1.0 ms, the forward's 7.6 GB of stores +0.9 ms — not the default
-CE_LOGITS = os.environ.get('C2DSR_CE_LOGITS', '0') != '0'
+CE_LOGITS = os.environ.get('C2DSR_CE_LOGITS', '1') != '0'
 CE_LOGITS_GB = float(os.environ.get('C2DSR_CE_LOGITS_GB', '48'))
 
 
@@ -209,6 +209,7 @@ class LossMeta:
         self.pending = None
         self.on_head_grads = None  # data parallel: called when the backward has written the head gradients
         self.after_first_ce = None  # host work to enqueue once the first long CE kernel is queued (or at the end)
+        self.plan_state = None  # the step's plan cache when its target plans were built ahead (trainer.PLANS_EARLY)
 
     def run_after_first_ce(self):
         f, self.after_first_ce = self.after_first_ce, None
@@ -460,8 +461,12 @@ class LossHeadFn(Function):
                                     keep_logits(Mv, n, mode) if W.requires_grad else 0)
             if k == 0:
                 m.run_after_first_ce()
-            # target sort for the one-hot part of dW/db, on the side stream under the rest of the step
-            tplan = IndexPlan(tc[:Mv], n + 1) if Mv and W.requires_grad else None
+            # target sort for the one-hot part of dW/db, on the side stream under the rest of the step (or built with
+            # the step's other plans ahead of the forward: trainer.PLANS_EARLY)
+            tplan = None
+            if Mv and W.requires_grad:
+                tplan = index_plans(m.plan_state, [(tc[:Mv], n + 1)])[0] if m.plan_state is not None \
+                    else IndexPlan(tc[:Mv], n + 1)
             heads.append((out[0], tcat, out[1:], inv, tc, Mv0, Mv1, tplan, W, bias, n))
         T.loss_partials(heads[0][0], heads[0][1], m.n_a, heads[1][0], heads[1][1], m.n_b, BR, vec)
         cnt = None

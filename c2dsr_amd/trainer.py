@@ -133,6 +133,11 @@ def init_data_parallel(args):
     return rank, world
 
 
+# all index plans of a step enqueued right behind the propagations in one batched launch set (else: the lookup
+# plans after the first CE sweep, each head's target plan after its forward sweep); measured, see DESIGN §8
+PLANS_EARLY = __import__('os').environ.get('C2DSR_PLANS_EARLY', '1') == '1'
+
+
 class Trainer(object):
     def __init__(self, args, noter=None, *, data=None, graphs=None):
         """``data`` = (trainloader, valloader, testloader) and ``graphs`` = (adj_share, adj_specific)
@@ -456,7 +461,21 @@ class Trainer(object):
         # counts are not known on the host: the host then reads them while the device runs the propagations)
         m.launch_graph()
         plans = None
-        if m.training:
+        early = None
+        if m.training and PLANS_EARLY and ce_pre is not None:
+            # every plan of the step — the eight lookups' and both heads' target plans — in one batched launch set on
+            # the side stream right behind the propagations, so none runs beside the loss head's long sweeps
+            st = m.state
+            pairs = [pr for sq, ps in ((seq_share, pos), (seq_a, pos_a), (seq_b, pos_b), (neg_a, pos), (neg_b, pos))
+                     for pr in ((sq, m.n_item), (ps, m.attn_share.len_max))]
+            for k, (W, n) in enumerate(((m.classifier_a.weight, self.n_item_a), (m.classifier_b.weight, self.n_item_b))):
+                tc, (hc, slot) = ce_pre[k][3], ce_pre[k][4]
+                Mv = int(hc[slot]) + int(hc[slot + 1])
+                if Mv and W.requires_grad:
+                    pairs.append((tc[:Mv], n + 1))
+            ops.index_plans(st, pairs)
+            early = st
+        elif m.training:
             # the embedding backward's sort plans of every pass (side stream), enqueued by the loss head right
             # after its first long CE launch (one launch per radix pass for all eight: c2dsr_index_plans), issued while
             # the device is busy,
@@ -475,6 +494,7 @@ class Trainer(object):
         meta = self.loss_meta(gt_share_a, gt_share_b, gt_a, gt_b, gm_a, gm_b, B_global)
         meta.ce_pre = ce_pre
         meta.after_first_ce = plans
+        meta.plan_state = early
         if self.dp_counts is not None:
             meta.counts = self.dp_counts
             meta.reduce_async = lambda t: dist.all_reduce(t, async_op=True)  # noqa: E731
