@@ -796,13 +796,15 @@ def run_train(opt, cfg, name, precision, wl, world, rank, device, zero1=None, dp
                                     'ce3_kernel<256,1,bf16> (dW), one bf16 MFMA per product; credited 2·Mv·n·d per '
                                     'product over the Mv valid rows (fwd_u 2, dw 1)',
                             'fp32': 'K5 fused classifier head + CE at fp32 accuracy: ce3_kernel<256,0> (lse + dH, '
-                                    'online) + ce3_kernel<256,1> (dW), split-bf16 operands, 3 bf16 MFMAs per '
+                                    'online; with the logits kept it also stores them) + the dW sweep — '
+                                    'ce3_dwl_kernel on the stored logits (losshead.CE_LOGITS, the default) or '
+                                    'ce3_kernel<256,1> recomputing them —, split-bf16 operands, 3 bf16 MFMAs per '
                                     'product; credited 2·Mv·n·d per fp32 product over the Mv valid rows (fwd_u 2, '
                                     'dw 1); peak = bf16 dense peak / 3'}.get(
                         precision, 'gemm_kernel (K5 materialised logits GEMMs, fp32-input MFMA)'),
                     ms_per_step=round(ks['ms'] / opt.steps, 4), per_kernel=ks['per_kernel'],
                     mfma_busy=busy, mfma_busy_note='SQ_VALU_MFMA_BUSY_CYCLES / SIMD cycles of the K5 launches '
-                    '(same PMC run as traffic; counts the recomputed logits tiles that frac does not credit)')
+                    '(same PMC run as traffic; counts any recomputed logits tiles, which frac does not credit)')
     if hb is not None and name == 'mb' and precision in ('bf16', 'fp32'):
         hb['traffic'], hb['traffic_source'] = hbm_traffic(precision)
         hb['traffic_unit'] = 'bytes per step (all K1+K2 launches); achieved/peak use algorithmic bytes'

@@ -846,6 +846,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   }  // segments
 }
 
+#ifndef CE3L_MID  // ce3_dwl_kernel: the image barrier mid-tile (see the kernel)
+#define CE3L_MID 0
+#endif
 #ifndef CE3L_X  // diagnostic builds of ce3_dwl_kernel (timing only): bit 0 no logits loads, bit 1 no per-tile H DMA
 #define CE3L_X 0
 #endif
@@ -1030,33 +1033,58 @@ __global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict_
     }
     // tile t (parity P): loads of tile t+2 into L[P]; the second product on X[P] ∥ tile t+1's E into X[1−P] from
     // L[1−P] ∥ the DMA of tile t+3
+    // CE3L_MID: the barrier that publishes tile t+1's image in the middle of tile t's second product (its DMA pieces
+    // were issued in the second half of tile t−2's), the DMA of tile t+3 in the second half (every wave is past tile
+    // t−1's reads then), and tile t+1's first fragment reads in the last steps of tile t: no barrier or exposed LDS
+    // latency between tiles
+    constexpr bool MID = CE3L_MID;
+    constexpr int DQM = (NE / 2) / NDMA;  // MID: DMA spacing over the second half
+    static_assert(!MID || (DQM >= 1 && DQM * NDMA == NE / 2 && DT <= NE / 2), "mid-tile barrier split");
+    bf16x8 tf[DT + 2][2];
+    if constexpr (MID) {
+      [&]<int... Q>(std::integer_sequence<int, Q...>) {
+        ((tf[Q][0] = tfrag.template operator()<Q>(ib), tf[Q][1] = tfrag.template operator()<NE + Q>(ib)), ...);
+      }(std::make_integer_sequence<int, DT>{});
+    }
     auto tile = [&]<int P>(int t) {
       ld_logits(t + 2, L[P]);
       dma_wait_keep<NDMA + NL>();
       landed(L[1 - P]);
-      const int bh = ib + (t % NB) * IMG;
+      const int bh = ib + (t % NB) * IMG, bh1 = ib + ((t + 1) % NB) * IMG;
       const int rn = min(w_beg + (t + 3) * T3, w_last);
       const bf16* nsrc = Xw + (long)rn * D2;
       const unsigned nbuf = ((t + 3) % NB) * IMG;
       const float zm = t + 1 < ntiles ? 1.f : 0.f;  // the E of a tile past the end (clamped loads) counts nowhere
-      bf16x8 tf[DT + 2][2];
-      [&]<int... Q>(std::integer_sequence<int, Q...>) {
-        ((tf[Q][0] = tfrag.template operator()<Q>(bh), tf[Q][1] = tfrag.template operator()<NE + Q>(bh)), ...);
-      }(std::make_integer_sequence<int, DT>{});
+      if constexpr (!MID) {
+        [&]<int... Q>(std::integer_sequence<int, Q...>) {
+          ((tf[Q][0] = tfrag.template operator()<Q>(bh), tf[Q][1] = tfrag.template operator()<NE + Q>(bh)), ...);
+        }(std::make_integer_sequence<int, DT>{});
+      }
       float ev[NEL];
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
               constexpr int k = K;
+              if constexpr (MID && k == NE / 2) {
+                dma_wait_keep<2 * NL + NDMA>();  // tile t+1's image (this wave's pieces), then every wave's
+                __syncthreads();
+              }
               if constexpr (k + DT < NE) {
                 tf[(k + DT) % (DT + 2)][0] = tfrag.template operator()<k + DT>(bh);
                 tf[(k + DT) % (DT + 2)][1] = tfrag.template operator()<NE + k + DT>(bh);
+              } else if constexpr (MID) {  // the next tile's first steps
+                tf[(k + DT) % (DT + 2)][0] = tfrag.template operator()<k + DT - NE>(bh1);
+                tf[(k + DT) % (DT + 2)][1] = tfrag.template operator()<k + DT>(bh1);
               }
               const bf16x8(&tq)[2] = tf[k % (DT + 2)];
 #pragma unroll
               for (int sb = 0; sb < SBW; ++sb) split3_u<true>(dacc[k][sb], tq[0], tq[1], X[P].h[sb], X[P].l[sb]);
-              if constexpr (k % DQ == DQ - 1 && !(CE3L_X & 2))
+              if constexpr (MID) {
+                if constexpr (k >= NE / 2 && (k - NE / 2) % DQM == DQM - 1 && !(CE3L_X & 2))
+                  dma16_s<k - NE / 2 == DQM - 1>(nsrc, dvoff[(k - NE / 2) / DQM], ddst[(k - NE / 2) / DQM] + nbuf);
+              } else if constexpr (k % DQ == DQ - 1 && !(CE3L_X & 2)) {
                 dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
+              }
               constexpr int i0 = (k * NEL + NE - 1) / NE, i1 = ((k + 1) * NEL + NE - 1) / NE;
               e_elems.template operator()<i0, i1>(L[1 - P], ev, zm);
               [&]<int... S>(std::integer_sequence<int, S...>) {
@@ -1076,8 +1104,10 @@ __global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict_
         asm volatile("" : "+v"(X[1 - P].h[sb]));
         asm volatile("" : "+v"(X[1 - P].l[sb]));
       }
-      dma_wait_keep<2 * (NDMA + NL)>();
-      __syncthreads();
+      if constexpr (!MID) {
+        dma_wait_keep<2 * (NDMA + NL)>();
+        __syncthreads();
+      }
     };
     for (int t = 0; t < ntiles; t += 2) {
       tile.template operator()<0>(t);

@@ -22,7 +22,9 @@ prec = sys.argv[3] if len(sys.argv) > 3 else 'fp32'
 # (ce3_kernel<D, MODE, SPLIT, NW>: SPLIT = true in the fp32 mode, false for the plain-bf16 instantiation; matched
 # without the trailing arguments)
 K5 = (('ce3_kernel<256, 0, false', 'ce_rows_kernel', 'ce3_kernel<256, 1, false') if prec == 'bf16' else
-      ('ce3_kernel<256, 0, true', 'ce_rows_kernel', 'ce3_kernel<256, 1, true'))
+      ('ce3_kernel<256, 0, true', 'ce_rows_kernel', 'ce3_kernel<256, 1, true', 'ce3_dwl_kernel'))
+# (fp32 mode with the logits kept, losshead.CE_LOGITS: the forward is ce3_kernel<256, 0, true, 4, true> — the same
+# prefix — and the dW sweep ce3_dwl_kernel, whose launches read the 7.6 GB of stored logits per step)
 # the segment sums of the embedding backward only: ROLE 0 instantiations (ROLE 1 = the classifier one-hot dW)
 K12 = ('spmm_kernel', 'spmm_pf_kernel', 'spmm_nc_kernel', 'combine_kernel', 'embed_fwd_kernel', 'embed_fwd_rows_kernel', 'seg_chunk_kernel<64, 0>',
        'seg_split1_kernel<64, 0>', 'seg_split2_kernel<64, 0>')
