@@ -754,6 +754,19 @@ def test_c3_step_matches_reference(compact):
     _ref_step_check('c3', compact)
 
 
+def test_c3_step_matches_reference_recomputed_dw():
+    """The C3 reference step with the classifier dW sweep RECOMPUTING the logits (losshead.CE_LOGITS off: the
+    c2dsr_ce3_fused_dw* kernels) instead of reading the ones the forward stored (the default) — both dW paths pinned
+    by the reference at the bench workload's item counts."""
+    from c2dsr_amd import losshead
+    keep = losshead.CE_LOGITS
+    losshead.CE_LOGITS = False
+    try:
+        _ref_step_check('c3', True)
+    finally:
+        losshead.CE_LOGITS = keep
+
+
 def _ref_step_check(tag, compact):
     from c2dsr_amd import dataloader as DL
     from c2dsr_amd import graph as GR
