@@ -846,8 +846,8 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   }  // segments
 }
 
-#ifndef CE3L_MID  // ce3_dwl_kernel: the image barrier mid-tile (see the kernel)
-#define CE3L_MID 0
+#ifndef CE3L_NW  // ce3_dwl_kernel at d = 256: 4 waves (one per SIMD) or 8 (two per SIMD splitting the e-blocks; measured
+#define CE3L_NW 4  // slower: MB head b 1,966 vs 1,798 µs, head a 1,108 vs 999 — the logits loads and E twice per SIMD)
 #endif
 #ifndef CE3L_X  // diagnostic builds of ce3_dwl_kernel (timing only): bit 0 no logits loads, bit 1 no per-tile H DMA
 #define CE3L_X 0
@@ -867,21 +867,26 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
 // tile t−1 (E, z and the hi / lo split in the MFMA shadow); tile t+1's logits (loaded at the top of tile t−1) are
 // waited for at the top of tile t with NDMA + NL younger operations left in flight, tile t+1's image at its end with
 // 2·(NL + NDMA).
-template <int D, int SBW>
-__global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict__ Xw, const float* __restrict__ lg,
+// NWD = 8 (D = 256): two waves per SIMD, the pair on one SIMD sharing its 32 columns and splitting the 16 e-blocks of
+// the second product (each computes the tile's E itself), so one wave's waits and VALU run under the other's MFMAs
+template <int D, int SBW, int NWD = 4>
+__global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __restrict__ Xw, const float* __restrict__ lg,
                                                          int lg_hb, int lg_cw, const float* __restrict__ crow, int n_s,
                                                          int n_w, int per_split, float* __restrict__ part_s,
                                                          float* __restrict__ outp, int accum, int sk_nwg,
                                                          float* __restrict__ slot_w, float* __restrict__ slot_b) {
-  constexpr int NW = 4, T3 = 32, CB = 2, NE = D / 16, D2 = 2 * D, IMG = T3 * D2 * 2, HT = T3 * 256, NB = 4;
-  constexpr int RB = 16 * NW * SBW;
+  constexpr int NW = NWD, T3 = 32, CB = 2, NE = D / 16, D2 = 2 * D, IMG = T3 * D2 * 2, HT = T3 * 256, NB = 4;
+  constexpr int EH = NW / 4, NES = NE / EH;          // e-block halves (waves per SIMD), e-blocks per wave = steps
+  constexpr int RB = 16 * 4 * SBW;
   constexpr int NDMA = (T3 / 4) * (D2 / 128) / NW;  // LDS-DMA wave-instructions per wave per tile
   constexpr int NL = SBW * CB + CB;                  // logits blocks + row-constant float4s per wave per tile
-  constexpr int DT = 2, DQ = NE / NDMA;
+  constexpr int DT = 2, DQ = NES / NDMA;
   constexpr int NEL = 4 * SBW * CB;                  // E values per lane per tile
-  static_assert(DQ >= 1 && DQ * NDMA == NE && NEL % 8 == 0 && 2 * (NL + NDMA) < 64, "tile / wave split");
+  static_assert((NW == 4 || (NW == 8 && NES == 8)) && DQ >= 1 && DQ * NDMA == NES && NEL % 8 == 0 &&
+                    2 * (NL + NDMA) < 64, "tile / wave split");
   __shared__ __attribute__((aligned(16))) char img[NB][IMG];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g = lane >> 4;
+  const int cw = w & 3, eh = w >> 2;  // column group, e-block half
   const int nrb = (n_s + RB - 1) / RB, nb = (int)gridDim.x;
   const long skT = (n_w + T3 - 1) / T3, skU = (long)nrb * skT;
   long sk_u = sk_nwg ? (long)blockIdx.x * skU / sk_nwg : 0;
@@ -905,19 +910,20 @@ __global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict_
     w_beg = split * per_split;
     w_end = min(n_w, w_beg + per_split);
   }
-  const int s0 = rblk * RB + w * 16 * SBW + l16;  // stationary columns s0 + 16·sb
+  const int s0 = rblk * RB + cw * 16 * SBW + l16;  // stationary columns s0 + 16·sb
   const int ntiles = w_end > w_beg ? (w_end - w_beg + T3 - 1) / T3 : 0;
-  f32x4 dacc[NE][SBW];
+  f32x4 dacc[NES][SBW];
   float zrow[SBW];
 #pragma unroll
   for (int sb = 0; sb < SBW; ++sb) {
 #pragma unroll
-    for (int e = 0; e < NE; ++e) dacc[e][sb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < NES; ++e) dacc[e][sb] = f32x4{0.f, 0.f, 0.f, 0.f};
     zrow[sb] = 0.f;
   }
   if (ntiles > 0) {
     const int w_last = w_beg + (ntiles - 1) * T3;
     const int ib = (int)lds_addr(img[0]);
+    const int ebo = eh * HT;  // this wave's e-blocks: image columns 128·eh .. (hi) and D + 128·eh .. (lo)
     unsigned dvoff[NDMA], ddst[NDMA];
 #pragma unroll
     for (int i = 0; i < NDMA; ++i) {
@@ -940,7 +946,7 @@ __global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict_
     const float* lgb[SBW];
 #pragma unroll
     for (int sb = 0; sb < SBW; ++sb) {
-      const int c16 = __builtin_amdgcn_readfirstlane(min(((rblk * RB + w * 16 * SBW) >> 4) + sb, lg_cw - 1));
+      const int c16 = __builtin_amdgcn_readfirstlane(min(((rblk * RB + cw * 16 * SBW) >> 4) + sb, lg_cw - 1));
       lgb[sb] = lg + (long)c16 * lg_hb * 256;
     }
     struct LSet {
@@ -1032,60 +1038,36 @@ __global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict_
       }(std::make_integer_sequence<int, SBW>{});
     }
     // tile t (parity P): loads of tile t+2 into L[P]; the second product on X[P] ∥ tile t+1's E into X[1−P] from
-    // L[1−P] ∥ the DMA of tile t+3
-    // CE3L_MID: the barrier that publishes tile t+1's image in the middle of tile t's second product (its DMA pieces
-    // were issued in the second half of tile t−2's), the DMA of tile t+3 in the second half (every wave is past tile
-    // t−1's reads then), and tile t+1's first fragment reads in the last steps of tile t: no barrier or exposed LDS
-    // latency between tiles
-    constexpr bool MID = CE3L_MID;
-    constexpr int DQM = (NE / 2) / NDMA;  // MID: DMA spacing over the second half
-    static_assert(!MID || (DQM >= 1 && DQM * NDMA == NE / 2 && DT <= NE / 2), "mid-tile barrier split");
+    // L[1−P] ∥ the DMA of tile t+3.  Step k: e-block eh·NES + k (image columns of the hi half at offset ebo, the lo
+    // half NE e-blocks further)
     bf16x8 tf[DT + 2][2];
-    if constexpr (MID) {
-      [&]<int... Q>(std::integer_sequence<int, Q...>) {
-        ((tf[Q][0] = tfrag.template operator()<Q>(ib), tf[Q][1] = tfrag.template operator()<NE + Q>(ib)), ...);
-      }(std::make_integer_sequence<int, DT>{});
-    }
     auto tile = [&]<int P>(int t) {
       ld_logits(t + 2, L[P]);
       dma_wait_keep<NDMA + NL>();
       landed(L[1 - P]);
-      const int bh = ib + (t % NB) * IMG, bh1 = ib + ((t + 1) % NB) * IMG;
+      const int bh = ib + (t % NB) * IMG + ebo;
       const int rn = min(w_beg + (t + 3) * T3, w_last);
       const bf16* nsrc = Xw + (long)rn * D2;
       const unsigned nbuf = ((t + 3) % NB) * IMG;
       const float zm = t + 1 < ntiles ? 1.f : 0.f;  // the E of a tile past the end (clamped loads) counts nowhere
-      if constexpr (!MID) {
-        [&]<int... Q>(std::integer_sequence<int, Q...>) {
-          ((tf[Q][0] = tfrag.template operator()<Q>(bh), tf[Q][1] = tfrag.template operator()<NE + Q>(bh)), ...);
-        }(std::make_integer_sequence<int, DT>{});
-      }
+      [&]<int... Q>(std::integer_sequence<int, Q...>) {
+        ((tf[Q][0] = tfrag.template operator()<Q>(bh), tf[Q][1] = tfrag.template operator()<NE + Q>(bh)), ...);
+      }(std::make_integer_sequence<int, DT>{});
       float ev[NEL];
       [&]<int... K>(std::integer_sequence<int, K...>) {
         (
             [&] {
               constexpr int k = K;
-              if constexpr (MID && k == NE / 2) {
-                dma_wait_keep<2 * NL + NDMA>();  // tile t+1's image (this wave's pieces), then every wave's
-                __syncthreads();
-              }
-              if constexpr (k + DT < NE) {
+              if constexpr (k + DT < NES) {
                 tf[(k + DT) % (DT + 2)][0] = tfrag.template operator()<k + DT>(bh);
                 tf[(k + DT) % (DT + 2)][1] = tfrag.template operator()<NE + k + DT>(bh);
-              } else if constexpr (MID) {  // the next tile's first steps
-                tf[(k + DT) % (DT + 2)][0] = tfrag.template operator()<k + DT - NE>(bh1);
-                tf[(k + DT) % (DT + 2)][1] = tfrag.template operator()<k + DT>(bh1);
               }
               const bf16x8(&tq)[2] = tf[k % (DT + 2)];
 #pragma unroll
               for (int sb = 0; sb < SBW; ++sb) split3_u<true>(dacc[k][sb], tq[0], tq[1], X[P].h[sb], X[P].l[sb]);
-              if constexpr (MID) {
-                if constexpr (k >= NE / 2 && (k - NE / 2) % DQM == DQM - 1 && !(CE3L_X & 2))
-                  dma16_s<k - NE / 2 == DQM - 1>(nsrc, dvoff[(k - NE / 2) / DQM], ddst[(k - NE / 2) / DQM] + nbuf);
-              } else if constexpr (k % DQ == DQ - 1 && !(CE3L_X & 2)) {
+              if constexpr (k % DQ == DQ - 1 && !(CE3L_X & 2))
                 dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
-              }
-              constexpr int i0 = (k * NEL + NE - 1) / NE, i1 = ((k + 1) * NEL + NE - 1) / NE;
+              constexpr int i0 = (k * NEL + NES - 1) / NES, i1 = ((k + 1) * NEL + NES - 1) / NES;
               e_elems.template operator()<i0, i1>(L[1 - P], ev, zm);
               [&]<int... S>(std::integer_sequence<int, S...>) {
                 (
@@ -1098,16 +1080,14 @@ __global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict_
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
-      }(std::make_integer_sequence<int, NE>{});
+      }(std::make_integer_sequence<int, NES>{});
 #pragma unroll
       for (int sb = 0; sb < SBW; ++sb) {
         asm volatile("" : "+v"(X[1 - P].h[sb]));
         asm volatile("" : "+v"(X[1 - P].l[sb]));
       }
-      if constexpr (!MID) {
-        dma_wait_keep<2 * (NDMA + NL)>();
-        __syncthreads();
-      }
+      dma_wait_keep<2 * (NDMA + NL)>();
+      __syncthreads();
     };
     for (int t = 0; t < ntiles; t += 2) {
       tile.template operator()<0>(t);
@@ -1123,22 +1103,23 @@ __global__ __launch_bounds__(256, 1) void ce3_dwl_kernel(const bf16* __restrict_
   for (int sb = 0; sb < SBW; ++sb) {
     const float ztot = quad_sum(zrow[sb]);
     const int s = s0 + 16 * sb;
+    const int eo = 16 * NES * eh;  // this wave's columns of dW
     if (s < n_s && slot >= 0) {  // stream-K partial of a split row block
       const long so = (long)(2 * blockIdx.x + slot) * RB + (s - rblk * RB);
-      if (g == 0) slot_b[so] = ztot;
-      float* out = slot_w + so * D + 4 * g;
+      if (g == 0 && eh == 0) slot_b[so] = ztot;
+      float* out = slot_w + so * D + eo + 4 * g;
 #pragma unroll
-      for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
+      for (int e = 0; e < NES; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
     } else if (s < n_s) {
       const bool acc = accum || sk_nwg;
-      if (g == 0) part_s[(long)split * n_s + s] = acc ? part_s[s] + ztot : ztot;
-      float* out = outp + ((long)split * n_s + s) * D + 4 * g;
+      if (g == 0 && eh == 0) part_s[(long)split * n_s + s] = acc ? part_s[s] + ztot : ztot;
+      float* out = outp + ((long)split * n_s + s) * D + eo + 4 * g;
       if (acc) {
 #pragma unroll
-        for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = *(const f32x4*)(out + 16 * e) + dacc[e][sb];
+        for (int e = 0; e < NES; ++e) *(f32x4*)(out + 16 * e) = *(const f32x4*)(out + 16 * e) + dacc[e][sb];
       } else {
 #pragma unroll
-        for (int e = 0; e < NE; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
+        for (int e = 0; e < NES; ++e) *(f32x4*)(out + 16 * e) = dacc[e][sb];
       }
     }
   }
@@ -1304,8 +1285,8 @@ int launch_dwl(const void* Hx, const float* lg, int lg_hb, int lg_cw, const floa
     ce3_dwl_kernel<128, DWL_SBW><<<grid, 256, 0, st>>>((const bf16*)Hx, lg, lg_hb, lg_cw, crow, n, M, per, ps, out,
                                                        accum, sk_nwg, slot_w, slot_b);
   else if (D == 256)
-    ce3_dwl_kernel<256, DWL_SBW><<<grid, 256, 0, st>>>((const bf16*)Hx, lg, lg_hb, lg_cw, crow, n, M, per, ps, out,
-                                                       accum, sk_nwg, slot_w, slot_b);
+    ce3_dwl_kernel<256, DWL_SBW, CE3L_NW><<<grid, 64 * CE3L_NW, 0, st>>>((const bf16*)Hx, lg, lg_hb, lg_cw, crow, n, M,
+                                                                         per, ps, out, accum, sk_nwg, slot_w, slot_b);
   else
     return (int)hipErrorInvalidValue;
   C2_CHECK_LAUNCH();
