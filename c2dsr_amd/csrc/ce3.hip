@@ -846,6 +846,9 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   }  // segments
 }
 
+#ifndef CE3L_PF  // ce3_dwl_kernel: tiles of logits loaded ahead (register sets; the tile loop is unrolled by it); 3
+#define CE3L_PF 2  // measured within 1.5 % of 2 (MB head b 1,808 vs 1,835 µs, head a 1,013 vs 1,022)
+#endif
 #ifndef CE3L_NW  // ce3_dwl_kernel at d = 256: 4 waves (one per SIMD) or 8 (two per SIMD splitting the e-blocks; measured
 #define CE3L_NW 4  // slower: MB head b 1,966 vs 1,798 µs, head a 1,108 vs 999 — the logits loads and E twice per SIMD)
 #endif
@@ -1018,17 +1021,20 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
       v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
       return v;
     };
-    LSet L[2];
-    XSet X[2];
+    constexpr int U = CE3L_PF;  // logits register sets = tiles loaded ahead (the loop is unrolled by U)
+    static_assert(U == 2 || U == 3, "logits prefetch depth");
+    LSet L[U];
+    XSet X[U];
     ld_logits(0, L[0]);
     dma(0);
     ld_logits(1, L[1]);
     dma(1);
+    if constexpr (U == 3) ld_logits(2, L[2]);
     dma(2);
     vm_drain();
     dma_wait();
-    landed(L[0]);
-    landed(L[1]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) landed(L[u]);
     __syncthreads();
     {
       float ev[NEL];
@@ -1037,14 +1043,15 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
         (pack.template operator()<S>(ev, X[0]), ...);
       }(std::make_integer_sequence<int, SBW>{});
     }
-    // tile t (parity P): loads of tile t+2 into L[P]; the second product on X[P] ∥ tile t+1's E into X[1−P] from
-    // L[1−P] ∥ the DMA of tile t+3.  Step k: e-block eh·NES + k (image columns of the hi half at offset ebo, the lo
+    // tile t (P = t mod U): loads of tile t+U into L[P]; the second product on X[P] ∥ tile t+1's E into X[P+1] from
+    // L[P+1] (mod U) ∥ the DMA of tile t+3.  Step k: e-block eh·NES + k (image columns of the hi half at offset ebo, the lo
     // half NE e-blocks further)
     bf16x8 tf[DT + 2][2];
     auto tile = [&]<int P>(int t) {
-      ld_logits(t + 2, L[P]);
-      dma_wait_keep<NDMA + NL>();
-      landed(L[1 - P]);
+      constexpr int PN = (P + 1) % U;
+      ld_logits(t + U, L[P]);
+      dma_wait_keep<(U - 1) * (NDMA + NL)>();
+      landed(L[PN]);
       const int bh = ib + (t % NB) * IMG + ebo;
       const int rn = min(w_beg + (t + 3) * T3, w_last);
       const bf16* nsrc = Xw + (long)rn * D2;
@@ -1068,11 +1075,11 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
               if constexpr (k % DQ == DQ - 1 && !(CE3L_X & 2))
                 dma16_s<k == DQ - 1>(nsrc, dvoff[k / DQ], ddst[k / DQ] + nbuf);
               constexpr int i0 = (k * NEL + NES - 1) / NES, i1 = ((k + 1) * NEL + NES - 1) / NES;
-              e_elems.template operator()<i0, i1>(L[1 - P], ev, zm);
+              e_elems.template operator()<i0, i1>(L[PN], ev, zm);
               [&]<int... S>(std::integer_sequence<int, S...>) {
                 (
                     [&] {
-                      if constexpr (i0 < 8 * (S + 1) && 8 * (S + 1) <= i1) pack.template operator()<S>(ev, X[1 - P]);
+                      if constexpr (i0 < 8 * (S + 1) && 8 * (S + 1) <= i1) pack.template operator()<S>(ev, X[PN]);
                     }(),
                     ...);
               }(std::make_integer_sequence<int, SBW>{});
@@ -1083,20 +1090,22 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
       }(std::make_integer_sequence<int, NES>{});
 #pragma unroll
       for (int sb = 0; sb < SBW; ++sb) {
-        asm volatile("" : "+v"(X[1 - P].h[sb]));
-        asm volatile("" : "+v"(X[1 - P].l[sb]));
+        asm volatile("" : "+v"(X[PN].h[sb]));
+        asm volatile("" : "+v"(X[PN].l[sb]));
       }
       dma_wait_keep<2 * (NDMA + NL)>();
       __syncthreads();
     };
-    for (int t = 0; t < ntiles; t += 2) {
+    for (int t = 0; t < ntiles; t += U) {
       tile.template operator()<0>(t);
       if (t + 1 < ntiles) tile.template operator()<1>(t + 1);
+      if constexpr (U == 3)
+        if (t + 2 < ntiles) tile.template operator()<2 % U>(t + 2);
     }
     // the loads past the end (clamped) land before their registers — live until here — or the LDS are reused
     vm_drain();
-    landed(L[0]);
-    landed(L[1]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) landed(L[u]);
   }
   mfma_drain();
 #pragma unroll
