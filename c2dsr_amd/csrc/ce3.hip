@@ -10,7 +10,8 @@
 // so each term of a dot product is exact to ≈3·2^-17 relative — the per-term error of an fp32 MFMA
 // chain is 2^-24, the CPU reference's accumulation-order noise at K = 256 is of order 1e-6 — at 3/16 of
 // the cost of the fp32-input MFMA (v_mfma_f32_32x32x2_f32 runs at 1/16 of the bf16 rate; gfx950 has no
-// xf32).  Logits are never materialised.
+// xf32).  Logits are never materialised over all rows; with LGS the forward stores the valid rows' logits for
+// ce3_dwl_kernel (the stored-logits dW sweep, below).
 //
 // Operands live as [rows][2·D] bf16 images "hi ‖ lo" (c2dsr_f32_split_bf16).  One kernel template, two
 // roles (the ce.hip fwd_u / dw pair with the tile height halved so the stationary hi AND lo fragments
