@@ -847,6 +847,14 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
   }  // segments
 }
 
+// ce3_dwl_kernel knobs measured at MB head b (tools/ce3_lg_micro.py, one box): fragment reads 2 / 3 / 4 steps ahead
+// 1,837 / 1,842 / 1,862 µs, the compiler's own schedule instead of the step pattern 1,857 µs — all within 1 %
+#ifndef CE3L_DT  // ce3_dwl_kernel: transposed fragment reads issued this many steps ahead
+#define CE3L_DT 2
+#endif
+#ifndef CE3L_PAT  // ce3_dwl_kernel: the sched_group_barrier step pattern (0: the compiler's own schedule)
+#define CE3L_PAT 1
+#endif
 #ifndef CE3L_PF  // ce3_dwl_kernel: tiles of logits loaded ahead (register sets; the tile loop is unrolled by it); 3
 #define CE3L_PF 2  // measured within 1.5 % of 2 (MB head b 1,808 vs 1,835 µs, head a 1,013 vs 1,022)
 #endif
@@ -884,7 +892,7 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
   constexpr int RB = 16 * 4 * SBW;
   constexpr int NDMA = (T3 / 4) * (D2 / 128) / NW;  // LDS-DMA wave-instructions per wave per tile
   constexpr int NL = SBW * CB + CB;                  // logits blocks + row-constant float4s per wave per tile
-  constexpr int DT = 2, DQ = NES / NDMA;
+  constexpr int DT = CE3L_DT, DQ = NES / NDMA;
   constexpr int NEL = 4 * SBW * CB;                  // E values per lane per tile
   static_assert((NW == 4 || (NW == 8 && NES == 8)) && DQ >= 1 && DQ * NDMA == NES && NEL % 8 == 0 &&
                     2 * (NL + NDMA) < 64, "tile / wave split");
@@ -1084,7 +1092,7 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
                     }(),
                     ...);
               }(std::make_integer_sequence<int, SBW>{});
-              step_pattern<3 * SBW, CE3_VN, true>();
+              step_pattern<3 * SBW, CE3_VN, (bool)CE3L_PAT>();
               __builtin_amdgcn_sched_barrier(0);
             }(),
             ...);
