@@ -146,6 +146,16 @@ __device__ __forceinline__ float quad_sum(float x) {
 #ifndef CE3_LGNT
 #define CE3_LGNT 1
 #endif
+// stored-logits layout: 16 × 16 blocks of 1 KiB; GRP column blocks grouped — block (c16, h16) at
+// ((c16 / GRP)·HB + h16)·GRP + c16 % GRP (GRP = 1: column-block-major; 8: a row block's 8 column blocks side by side,
+// so a forward tile's 8 row blocks × 2 column blocks fall in one 64 KiB run)
+#ifndef CE3_LGG  // measured: GRP = 8 writes at the same rate as 1 (forward 3,117 µs both, MB head b; dW within 1 %)
+#define CE3_LGG 1
+#endif
+constexpr int LGG = CE3_LGG;
+__device__ __forceinline__ long lg_blk(int c16, int h16, int hb) {
+  return ((long)(c16 / LGG) * hb + h16) * LGG + c16 % LGG;
+}
 template <int IMM>
 __device__ __forceinline__ void gst1(const void* sbase, unsigned voff, float v) {
   if constexpr (CE3_LGNT & 1)
@@ -472,14 +482,14 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     constexpr bool LGW = LGS && MODE == 0 && SPLIT;
     constexpr int NST = LGW ? NEL : 0;  // stores per tile
     auto lg_store = [&](int tt, const f32x4(&v)[SBW * CB]) {
-      if constexpr (LGW) {
+      if constexpr (LGW && !CE3_LGE) {
         const int cw = (w_beg + tt * T3) >> 4;
         [&]<int... C>(std::integer_sequence<int, C...>) {
           (
               [&] {
                 constexpr int cb = C / (4 * SBW), sb = (C / 4) % SBW, r = C % 4;
-                const float* base = lg + ((long)(cw + cb) * lg_hb + lg_h0) * 256;
-                gst1<sb * 1024 + r * 16>(base, lg_lo, v[cb * SBW + sb][r]);
+                const float* base = lg + lg_blk(cw + cb, lg_h0, lg_hb) * 256;
+                gst1<sb * 1024 * LGG + r * 16>(base, lg_lo, v[cb * SBW + sb][r]);
               }(),
               ...);
         }(std::make_integer_sequence<int, NST>{});
@@ -490,13 +500,16 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
     // transpose gives each lane the block's 16-byte chunk 16·(l16/4) + 4g + l16%4 (rows 4·(l16/4) .., column 4g +
     // l16%4), one dwordx4 store per block and wave
     const unsigned lg_lo4 = (unsigned)((16 * (l16 >> 2) + 4 * g + (l16 & 3)) * 16);
+    unsigned lg_lo4s[SBW];  // + the stationary block's row-block offset (past the immediate's range when LGG > 1)
+#pragma unroll
+    for (int sb = 0; sb < SBW; ++sb) lg_lo4s[sb] = lg_lo4 + (unsigned)(sb * LGG * 1024);
     auto lg_put = [&]<int IB, int IE>(const float* const(&lgp)[CB], const f32x4(&v)[SBW * CB]) {
       if constexpr (LGW && CE3_LGE) {
         [&]<int... I>(std::integer_sequence<int, I...>) {
           (
               [&] {
                 constexpr int i = IB + I, sb = i / (4 * CB), cb = (i >> 2) % CB;
-                if constexpr (i % 4 == 0) gst4<sb * 1024>(lgp[cb], lg_lo4, quad_transpose(v[cb * SBW + sb]));
+                if constexpr (i % 4 == 0) gst4<0>(lgp[cb], lg_lo4s[sb], quad_transpose(v[cb * SBW + sb]));
               }(),
               ...);
         }(std::make_integer_sequence<int, IE - IB>{});
@@ -660,7 +673,7 @@ __global__ __launch_bounds__(64 * NW, 1) void ce3_kernel(const bf16* __restrict_
       if constexpr (LGW && CE3_LGE) {
         const int cw = (w_beg + t * T3) >> 4;
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) lgp[cb] = lg + ((long)(cw + cb) * lg_hb + lg_h0) * 256;
+        for (int cb = 0; cb < CB; ++cb) lgp[cb] = lg + lg_blk(cw + cb, lg_h0, lg_hb) * 256;
       }
       Offs oS, oH;
       offs_rows(bs, oS);
@@ -959,7 +972,7 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
 #pragma unroll
     for (int sb = 0; sb < SBW; ++sb) {
       const int c16 = __builtin_amdgcn_readfirstlane(min(((rblk * RB + cw * 16 * SBW) >> 4) + sb, lg_cw - 1));
-      lgb[sb] = lg + (long)c16 * lg_hb * 256;
+      lgb[sb] = lg + lg_blk(c16, 0, lg_hb) * 256;
     }
     struct LSet {
       f32x4 v[SBW][CB];  // logits: block (sb, cb), rows 16cb + 4g + i of column s0 + 16sb
@@ -973,11 +986,14 @@ __global__ __launch_bounds__(64 * NWD, 1) void ce3_dwl_kernel(const bf16* __rest
         return;
       }
       const int r0 = min(w_beg + tt * T3, w_last);
-      const unsigned vo = (unsigned)(lane * 16 + r0 * 64), vc = (unsigned)((r0 + 4 * g) * 4);
+      const unsigned vo = (unsigned)(lane * 16 + r0 * 64 * LGG), vc = (unsigned)((r0 + 4 * g) * 4);
 #pragma unroll
       for (int sb = 0; sb < SBW; ++sb) {
         gld4<0>(x.v[sb][0], lgb[sb], vo);
-        gld4<1024>(x.v[sb][1], lgb[sb], vo);
+        if constexpr (LGG * 1024 < 4096)
+          gld4<LGG * 1024>(x.v[sb][1], lgb[sb], vo);
+        else
+          gld4<0>(x.v[sb][1], lgb[sb], vo + LGG * 1024);
       }
       gld4<0>(x.c[0], crow, vc);
       gld4<64>(x.c[1], crow, vc);
@@ -1237,7 +1253,7 @@ size_t sk_ws_bytes(int nwg, int D) { return (sk_slot_floats(nwg, D) + (size_t)2 
 // the logits layout of ce3_dwl_kernel: 16-row blocks per 16-column block (the forward's row blocks, whole), and
 // 16-column blocks written (whole 32-column tiles)
 inline int lg_row_blocks(int M) { return c2::ceil_div(M, 128) * 8; }
-inline int lg_col_blocks(int n) { return c2::ceil_div(n, 32) * 2; }
+inline int lg_col_blocks(int n) { return c2::ceil_div(c2::ceil_div(n, 32) * 2, LGG) * LGG; }
 
 template <int MODE, bool SPLIT>
 int launch3(const void* Xs, const void* Xw, const float* svec, const float* wvec, int n_s, int n_w, int D, int nsplit,
@@ -1371,6 +1387,8 @@ C2_API int c2dsr_ce3_fused_dw(const void* Hx, const void* Wx, const float* bias2
 
 C2_API size_t c2dsr_ce3_dw_sk_workspace(int D) { return sk_ws_bytes(num_cus3(), D); }
 
+C2_API int c2dsr_ce3_logits_group(int what) { return what == 0 ? LGG : -1; }
+
 C2_API size_t c2dsr_ce3_logits_floats(int M, int n) {
   return M > 0 && n > 0 ? (size_t)lg_col_blocks(n) * lg_row_blocks(M) * 256 : 0;
 }
@@ -1390,7 +1408,7 @@ C2_API int c2dsr_ce3_fused_fwd_u_lg(const void* Hx, const void* Wx, const float*
 C2_API int c2dsr_ce3_fused_dw_lg(const void* Hx, const float* lg, int M, int n_lg, int col0, int n, int D,
                                  int n_rsplit, const float* crow, float* dWp, float* dbp, void* stream) {
   if (n == 0) return 0;
-  if (col0 < 0 || col0 % 32 || col0 + n > n_lg) return (int)hipErrorInvalidValue;
+  if (col0 < 0 || col0 % (16 * (LGG > 2 ? LGG : 2)) || col0 + n > n_lg) return (int)hipErrorInvalidValue;
   const int hb = lg_row_blocks(M);
   return launch_dwl(Hx, lg + (size_t)(col0 / 16) * hb * 256, hb, lg_col_blocks(n_lg) - col0 / 16, crow, n, M, D,
                     n_rsplit, dbp, dWp, (hipStream_t)stream);

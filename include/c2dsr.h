@@ -392,6 +392,10 @@ int c2dsr_ce3b_fused_dw_sk(const void* Hb, const void* Wb, const float* bias2, i
  * them (one split product per tile instead of two), same outputs as c2dsr_ce3_fused_dw / _dw_sk: dw_lg sweeps the
  * columns [col0, col0 + n) (col0 a multiple of 32) of the n_lg the forward wrote; n_rsplit as c2dsr_ce3_fused_dw. */
 size_t c2dsr_ce3_logits_floats(int M, int n);
+/* the layout's column-block grouping GRP (a build-time choice, 1 or 8): block (c/16, r/16) at
+ * ((c/16 / GRP)·⌈M/128⌉·8 + r/16)·GRP + (c/16) % GRP, column blocks padded to a multiple of GRP; dw_lg's col0 then
+ * a multiple of 16·max(2, GRP); what = 0 (-1 for another `what`) */
+int c2dsr_ce3_logits_group(int what);
 int c2dsr_ce3_fused_fwd_u_lg(const void* Hx, const void* Wx, const float* bias2, int M, int n, int D, int n_split,
                              float* part_m, float* part_s, float* Up, const float* padlogit, const int64_t* tgt,
                              const float* H, const float* W, const float* bias, float* lse, float* lse2,

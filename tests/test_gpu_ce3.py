@@ -573,9 +573,12 @@ def test_ce3_stored_logits_layout(M, n, D, ns):
     for x, y in zip(*outs):
         assert torch.equal(x[..., :M] if x.dim() == 1 else x, y[..., :M] if y.dim() == 1 else y)
     HB = -(-M // 128) * 8
-    CW = n32 // 16
-    blk = lg.cpu()[:CW * HB * 256].view(CW, HB, 4, 16, 4)  # [c/16][r/16][(r%16)/4][c%16][r%4]
-    full = blk.permute(1, 2, 4, 0, 3).reshape(HB * 16, CW * 16)  # [r][c]
+    grp = int(lib.raw('c2dsr_ce3_logits_group')(0))
+    CW = -(-(n32 // 16) // grp) * grp
+    assert lg.numel() == CW * HB * 256
+    # [c/16/grp][r/16][(c/16)%grp][(r%16)/4][c%16][r%4]
+    blk = lg.cpu().view(CW // grp, HB, grp, 4, 16, 4)
+    full = blk.permute(1, 3, 5, 0, 2, 4).reshape(HB * 16, CW * 16)  # [r][c]
     ref = (H.double() @ W.double().T + b.double()) * 1.4426950408889634
     got = full[:M, :n].double()
     err = float((got - ref).abs().max() / ref.abs().max())
