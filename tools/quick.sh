@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=${1:-q}
 K=${2:-}
-shift 2 2>/dev/null
+shift $(( $# < 2 ? $# : 2 ))
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 if [ -n "$K" ]; then KA=(-k "$K"); else KA=(); fi
